@@ -1,0 +1,284 @@
+"""ctypes binding of include/kgx.h (the C ABI of libkgx.so).
+
+Everything here calls the HIP engine; there is no CPU fallback.  Loading the
+library works without a GPU (symbols only); compute entry points return
+KGX_EDEVICE when no gfx950 device is visible, and the wrappers raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from . import build as _build
+
+KGX_OK = 0
+ERRORS = {-1: "EINVAL", -2: "EIO", -3: "EFORMAT", -4: "ENOMEM", -5: "EDEVICE", -6: "ERANGE",
+          -7: "EFULL"}
+WANT_HITS, WANT_CALLS, WANT_OTU = 1, 2, 4
+HIT_IN_RUN, HIT_OTU = 1, 2
+
+HIT_DTYPE = np.dtype([("which_kmer", "<u8"), ("otu_index", "<i4"), ("avg_from_end", "<u2"),
+                      ("flags", "<u2"), ("function_index", "<i4"), ("function_wt", "<f4"),
+                      ("pos", "<u4"), ("seq", "<u4")])
+CALL_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4"), ("count", "<i4"),
+                       ("function_index", "<u4"), ("weighted_hits", "<f4")])
+OTU_DTYPE = np.dtype([("otu_index", "<i4"), ("count", "<i4")])
+SIG_DTYPE = np.dtype([("which_kmer", "<u8"), ("otu_index", "<i4"), ("avg_from_end", "<u2"),
+                      ("pad", "<u2"), ("function_index", "<i4"), ("function_wt", "<f4")])
+assert HIT_DTYPE.itemsize == 32 and CALL_DTYPE.itemsize == 20 and SIG_DTYPE.itemsize == 24
+
+
+class KgxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what}: {ERRORS.get(code, code)} ({last_error()})")
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("min_hits", ctypes.c_int32), ("max_gap", ctypes.c_int32),
+                ("order_constraint", ctypes.c_int32), ("min_weighted_hits", ctypes.c_int32)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("n_seq", ctypes.c_uint32), ("hit_offsets", ctypes.c_void_p),
+                ("hits", ctypes.c_void_p), ("call_offsets", ctypes.c_void_p),
+                ("calls", ctypes.c_void_p), ("otu_offsets", ctypes.c_void_p),
+                ("otus", ctypes.c_void_p), ("n_windows", ctypes.c_uint64)]
+
+
+class DeviceResult(ctypes.Structure):
+    _fields_ = [("n_seq", ctypes.c_uint32), ("window_base", ctypes.c_void_p),
+                ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
+                ("hits", ctypes.c_void_p), ("calls", ctypes.c_void_p)]
+
+
+_P = ctypes.c_void_p
+_U64, _U32, _I32, _INT, _SZ = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int, ctypes.c_size_t
+_CS = ctypes.c_char_p
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes), mirroring include/kgx.h
+SIGNATURES = {
+    "kgx_version": (_CS, []),
+    "kgx_last_error": (_CS, []),
+    "kgx_strerror": (_CS, [_INT]),
+    "kgx_device_count": (_INT, []),
+    "kgx_params_default": (_INT, [ctypes.POINTER(Params)]),
+    "kgx_params_parse": (_INT, [ctypes.POINTER(Params), ctypes.POINTER(_CS), ctypes.POINTER(_CS), _SZ]),
+    "kgx_image_open": (_INT, [_CS, _INT, _PP]),
+    "kgx_image_from_memory": (_INT, [_P, _U64, _INT, _PP]),
+    "kgx_image_build_synthetic": (_INT, [_U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
+    "kgx_image_close": (_INT, [_P]),
+    "kgx_image_num_sigs": (_U64, [_P]),
+    "kgx_image_device": (_INT, [_P]),
+    "kgx_image_table": (_P, [_P]),
+    "kgx_image_download": (_INT, [_P, _P, _U64]),
+    "kgx_ctx_create": (_INT, [_P, _PP]),
+    "kgx_ctx_destroy": (_INT, [_P]),
+    "kgx_ctx_stream": (_P, [_P]),
+    "kgx_ctx_set_stream": (_INT, [_P, _P]),
+    "kgx_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
+    "kgx_run_device": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U64, _U32,
+                              ctypes.POINTER(DeviceResult)]),
+    "kgx_stage_plan": (_INT, [_P, _P, _U32, _U64]),
+    "kgx_stage_probe": (_INT, [_P, _P, _P]),
+    "kgx_stage_score": (_INT, [_P, ctypes.POINTER(Params), _U32]),
+    "kgx_device_result_get": (_INT, [_P, ctypes.POINTER(DeviceResult)]),
+    "kgx_synth_queries": (_INT, [_P, _U64, _U32, _U32, _U32, _U64, _P, _P]),
+    "kgx_find_best_call": (_INT, [_P, _SZ, ctypes.POINTER(_CS), _INT, ctypes.POINTER(_I32), _P, _SZ,
+                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_INT)]),
+    "kgx_device_alloc": (_INT, [_INT, _U64, _PP]),
+    "kgx_device_free": (_INT, [_P]),
+    "kgx_memcpy_h2d": (_INT, [_P, _P, _U64]),
+    "kgx_memcpy_d2h": (_INT, [_P, _P, _U64]),
+    "kgx_ctx_synchronize": (_INT, [_P]),
+}
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/kgx.h."""
+    with open(os.path.join(_build.INCLUDE, "kgx.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(kgx_\w+)\s*\(", text)))
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libkgx.so (building it first if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_build.LIB):
+            _build.build()
+        L = ctypes.CDLL(_build.LIB)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().kgx_last_error() or b"").decode()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != KGX_OK:
+        raise KgxError(rc, what)
+
+
+def device_count() -> int:
+    return lib().kgx_device_count()
+
+
+def default_params() -> Params:
+    p = Params()
+    check(lib().kgx_params_default(ctypes.byref(p)), "kgx_params_default")
+    return p
+
+
+def parse_params(values: dict | None) -> Params:
+    """set_parameters (kguts.cc:244-268) over a query-string dict."""
+    p = Params()
+    items = list((values or {}).items())
+    names = (_CS * max(1, len(items)))(*[k.encode() for k, _ in items])
+    vals = (_CS * max(1, len(items)))(*[str(v).encode() for _, v in items])
+    check(lib().kgx_params_parse(ctypes.byref(p), names, vals, len(items)), "kgx_params_parse")
+    return p
+
+
+def _view(ptr: int | None, n: int, dtype) -> np.ndarray:
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype).copy()
+
+
+class Image:
+    """A device-resident signature image (KmerImage)."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    @classmethod
+    def open(cls, data_dir: str, device: int = 0) -> "Image":
+        h = ctypes.c_void_p()
+        check(lib().kgx_image_open(data_dir.encode(), device, ctypes.byref(h)), f"kgx_image_open({data_dir})")
+        return cls(h.value)
+
+    @classmethod
+    def from_table(cls, table: np.ndarray, device: int = 0) -> "Image":
+        table = np.ascontiguousarray(table)
+        hdr = np.array([table.nbytes // 24, 24, 1], dtype=np.int64)
+        blob = np.concatenate([hdr.view(np.uint8), table.view(np.uint8).reshape(-1)])
+        h = ctypes.c_void_p()
+        check(lib().kgx_image_from_memory(blob.ctypes.data, blob.nbytes, device, ctypes.byref(h)),
+              "kgx_image_from_memory")
+        return cls(h.value)
+
+    @classmethod
+    def synthetic(cls, n_keys: int, num_sigs: int, device: int = 0) -> tuple["Image", int]:
+        h = ctypes.c_void_p()
+        stored = ctypes.c_uint64()
+        check(lib().kgx_image_build_synthetic(n_keys, num_sigs, device, ctypes.byref(h),
+                                              ctypes.byref(stored)), "kgx_image_build_synthetic")
+        return cls(h.value), stored.value
+
+    @property
+    def num_sigs(self) -> int:
+        return lib().kgx_image_num_sigs(self.handle)
+
+    def download(self) -> np.ndarray:
+        t = np.empty(self.num_sigs, dtype=SIG_DTYPE)
+        check(lib().kgx_image_download(self.handle, t.ctypes.data, t.nbytes), "kgx_image_download")
+        return t
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_image_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class BatchResult:
+    def __init__(self, r: Result, want: int):
+        n = r.n_seq
+        self.hit_offsets = _view(r.hit_offsets, n + 1, np.uint64)
+        self.call_offsets = _view(r.call_offsets, n + 1, np.uint64)
+        self.otu_offsets = _view(r.otu_offsets, n + 1, np.uint64)
+        self.hits = _view(r.hits, int(self.hit_offsets[-1]) if n + 1 else 0, HIT_DTYPE)
+        self.calls = _view(r.calls, int(self.call_offsets[-1]), CALL_DTYPE)
+        self.otus = _view(r.otus, int(self.otu_offsets[-1]), OTU_DTYPE)
+        self.n_windows = r.n_windows
+
+
+class Context:
+    """One per host thread (like one KmerGuts per pool thread)."""
+
+    def __init__(self, image: Image):
+        self.image = image
+        h = ctypes.c_void_p()
+        check(lib().kgx_ctx_create(image.handle, ctypes.byref(h)), "kgx_ctx_create")
+        self.handle = h.value
+
+    def process_batch(self, residues, offsets, params: Params | dict | None = None,
+                      want: int = WANT_HITS | WANT_CALLS | WANT_OTU) -> BatchResult:
+        if params is None or isinstance(params, dict):
+            params = parse_params(params)
+        residues = np.ascontiguousarray(np.frombuffer(bytes(residues), np.uint8)
+                                        if isinstance(residues, (bytes, bytearray)) else residues,
+                                        dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        r = Result()
+        check(lib().kgx_process_batch(self.handle, ctypes.byref(params),
+                                      residues.ctypes.data if residues.size else None,
+                                      offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
+              "kgx_process_batch")
+        return BatchResult(r, want)
+
+    @property
+    def stream(self) -> int:
+        return lib().kgx_ctx_stream(self.handle)
+
+    def set_stream(self, stream: int | None) -> None:
+        check(lib().kgx_ctx_set_stream(self.handle, stream), "kgx_ctx_set_stream")
+
+    def synchronize(self) -> None:
+        check(lib().kgx_ctx_synchronize(self.handle), "kgx_ctx_synchronize")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def find_best_call(calls: np.ndarray, functions: list[str]):
+    """(function_index, function, score, weighted_score, score_offset|None)."""
+    calls = np.ascontiguousarray(calls, dtype=CALL_DTYPE)
+    names = (_CS * max(1, len(functions)))(*[f.encode() for f in functions])
+    fi = _I32()
+    buf = ctypes.create_string_buffer(1 << 16)
+    sc, ws, off = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+    off_set = _INT()
+    check(lib().kgx_find_best_call(calls.ctypes.data if len(calls) else None, len(calls), names,
+                                   len(functions), ctypes.byref(fi), buf, len(buf),
+                                   ctypes.byref(sc), ctypes.byref(ws), ctypes.byref(off),
+                                   ctypes.byref(off_set)), "kgx_find_best_call")
+    return fi.value, buf.value.decode(), sc.value, ws.value, (off.value if off_set.value else None)

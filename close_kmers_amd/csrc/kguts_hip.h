@@ -1,0 +1,188 @@
+/*
+ * kguts_hip.h -- C++ facade with the KmerGuts / KmerImage surface of the
+ * reference (kguts.h:146-372, kmer_image.h:25-39, fasta_parser.h:8-165),
+ * backed by the HIP engine behind include/kgx.h.
+ *
+ * Drop-in contract: the same class names, method names,
+ * argument meaning and ownership as the reference; hit_cb runs synchronously,
+ * in ascending position order, on the calling thread before process_aa_seq
+ * returns; calls / otu_stats are appended to the caller's objects.  One
+ * KmerGuts per host thread over one shared KmerImage (threadpool.cc:18-44).
+ * Differences: failures throw kgx::Error instead of exit(); and
+ * process_aa_batch() runs a whole work list (lookup_request.cc:153) in one GPU
+ * pass -- per-sequence calls work but pay a launch round trip each.
+ */
+#ifndef KGUTS_HIP_H
+#define KGUTS_HIP_H
+
+#include <cstdio>
+#include <functional>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "kgx.h"
+
+namespace kgx {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string &msg) : std::runtime_error(msg), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+typedef kgx_sig_kmer sig_kmer_t; /* kmer_image.h:17-23 */
+
+/* KmerCall, kguts.h:166-183 */
+class KmerCall {
+public:
+    unsigned int start;
+    unsigned int end;
+    int count;
+    unsigned int function_index;
+    float weighted_hits;
+
+    KmerCall() : start(0), end(0), count(0), function_index(0), weighted_hits(0.0f) {}
+    KmerCall(unsigned int s, unsigned int e, int c, unsigned int f, float w)
+        : start(s), end(e), count(c), function_index(f), weighted_hits(w) {}
+};
+
+/* KmerOtuStats, kguts.h:185-219 */
+class KmerOtuStats {
+public:
+    std::string contig_id;
+    int contig_len = 0;
+    std::map<int, int> otu_map;
+    std::vector<std::pair<int, int>> otus_by_count;
+
+    void write(FILE *fh) const;
+    /* appends otu_map to otus_by_count, then sorts by count, descending */
+    void finalize();
+};
+
+/* KmerImage (kmer_image.h:25-39): the read-only signature table, resident in
+ * the HBM of one device.  Validation as kmer_image.cc:128-147. */
+class KmerImage {
+public:
+    explicit KmerImage(const std::string &data_dir, int device = 0);
+    /* adopt an image built elsewhere (e.g. kgx_image_build_synthetic) */
+    explicit KmerImage(kgx_image *adopted);
+    ~KmerImage();
+    KmerImage(const KmerImage &) = delete;
+    KmerImage &operator=(const KmerImage &) = delete;
+
+    kgx_image *handle() const { return img_; }
+    uint64_t num_sigs() const { return kgx_image_num_sigs(img_); }
+    const std::string &data_dir() const { return data_dir_; }
+
+private:
+    kgx_image *img_ = nullptr;
+    std::string data_dir_;
+};
+
+class KmerGuts {
+public:
+    /* kguts.h:228-233 */
+    struct hit_in_sequence_t {
+        sig_kmer_t hit;
+        unsigned int offset;
+        hit_in_sequence_t(const sig_kmer_t &h, unsigned int o) : hit(h), offset(o) {}
+    };
+
+    /* one entry of a batched work list */
+    struct SeqJob {
+        std::string id;
+        std::string seq;
+        std::shared_ptr<std::vector<KmerCall>> calls;
+        std::function<void(hit_in_sequence_t)> hit_cb;
+        std::shared_ptr<KmerOtuStats> otu_stats;
+    };
+
+    /* kguts.cc:35-58: loads <dir>/function.index and <dir>/otu.index */
+    KmerGuts(const std::string &kmer_dir, std::shared_ptr<KmerImage> image);
+    ~KmerGuts();
+    KmerGuts(const KmerGuts &) = delete;
+    KmerGuts &operator=(const KmerGuts &) = delete;
+
+    /* parameters, public like the reference (kguts.h:290-293) */
+    int order_constraint;
+    int min_hits;
+    int min_weighted_hits;
+    int max_gap;
+    void set_default_parameters();
+    void set_parameters(const std::map<std::string, std::string> &params);
+
+    void process_aa_seq(const std::string &id, const std::string &seq,
+                        std::shared_ptr<std::vector<KmerCall>> calls,
+                        std::function<void(hit_in_sequence_t)> hit_cb,
+                        std::shared_ptr<KmerOtuStats> otu_stats);
+    void process_aa_seq_hits(const std::string &id, const std::string &seq,
+                             std::shared_ptr<std::vector<KmerCall>> calls,
+                             std::shared_ptr<std::vector<hit_in_sequence_t>> hits,
+                             std::shared_ptr<KmerOtuStats> otu_stats);
+    /* every job as process_aa_seq would, in order, with one GPU pass */
+    void process_aa_batch(std::vector<SeqJob> &jobs);
+
+    void find_best_call(std::vector<KmerCall> &calls, int &function_index, std::string &function,
+                        float &score, float &weighted_score, float &score_offset);
+
+    std::string format_call(const KmerCall &c);
+    std::string format_hit(const hit_in_sequence_t &h);
+    std::string format_otu_stats(const std::string &id, size_t size, KmerOtuStats &otu_stats);
+
+    const char *function_at_index(int i) const;
+    int function_count() const { return (int)functions_.size(); }
+    static void decoded_kmer(unsigned long long encodedK, char *decoded);
+    static unsigned long long encoded_aa_kmer(const char *p);
+
+    std::shared_ptr<KmerImage> image_;
+    kgx_ctx *ctx() const { return ctx_; }
+
+private:
+    kgx_ctx *ctx_ = nullptr;
+    std::vector<std::string> functions_;
+    std::vector<std::string> otus_;
+};
+
+/* FastaParser (fasta_parser.h:8-165): the framing that turns request bytes
+ * into the (id, seq) pairs fed to KmerGuts. */
+class FastaParser {
+public:
+    FastaParser();
+    void set_callback(std::function<int(const std::string &, const std::string &)> cb) { on_seq_ = cb; }
+    void set_error_callback(std::function<bool(const std::string &, int, const std::string)> cb)
+    {
+        on_error_ = cb;
+    }
+    void init_parse();
+    bool parse_char(char c);
+    void parse_complete();
+
+private:
+    enum State { START, ID, DEFLINE, DATA, ID_OR_DATA };
+    int line_number_ = 1;
+    State state_ = START;
+    std::string id_, def_, seq_;
+    std::function<int(const std::string &, const std::string &)> on_seq_;
+    std::function<bool(const std::string &, int, const std::string)> on_error_;
+    void emit();
+};
+
+/* find_best_call (kguts.cc:1008-1199) with an explicit function-name lookup */
+void best_call(const std::vector<KmerCall> &calls, const std::function<const char *(int)> &name_of,
+               int &function_index, std::string &function, float &score, float &weighted_score,
+               float &score_offset);
+
+/* load_indexed_ar (kguts.cc:544-575): "%d\t<name>\n" lines, dense and in
+ * order; returns false when the file cannot be opened or is not dense. */
+bool load_index_file(const std::string &path, std::vector<std::string> &out);
+
+}  // namespace kgx
+
+#endif

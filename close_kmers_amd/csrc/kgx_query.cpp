@@ -1,0 +1,127 @@
+/*
+ * kgx_query.cpp -- request-handler surface over the HIP engine.
+ *
+ * Prints, for every sequence of a FASTA file, what the reference's handlers
+ * print, computing everything through the KmerGuts facade (one batched GPU
+ * pass per file, like one work list of a request chunk):
+ *
+ *   query          query_request.cc:103-151 (details=0, find_best_call=0)
+ *   query_details  query_request.cc:103-151 with details=1 (HIT lines)
+ *   query_best     query_request.cc:124-135 (find_best_call=1)
+ *   add            add_request.cc:305-353 (silent=0)
+ *
+ * usage: kgx_query DATA_DIR FASTA MODE [name=value ...]   (KGX_DEVICE=n)
+ */
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "kguts_hip.h"
+
+using namespace kgx;
+
+int main(int argc, char **argv)
+{
+    if (argc < 4) {
+        std::fprintf(stderr, "usage: %s DATA_DIR FASTA MODE [name=value ...]\n", argv[0]);
+        return 2;
+    }
+    const std::string dir = argv[1], fasta = argv[2], mode = argv[3];
+    if (mode != "query" && mode != "query_details" && mode != "query_best" && mode != "add") {
+        std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
+        return 2;
+    }
+    std::map<std::string, std::string> qp;
+    for (int i = 4; i < argc; i++) {
+        std::string a = argv[i];
+        size_t eq = a.find('=');
+        if (eq != std::string::npos)
+            qp[a.substr(0, eq)] = a.substr(eq + 1);
+    }
+    const char *dev = std::getenv("KGX_DEVICE");
+    try {
+        auto image = std::make_shared<KmerImage>(dir, dev ? std::atoi(dev) : 0);
+        KmerGuts kguts(dir, image);
+        kguts.set_parameters(qp);
+
+        std::vector<KmerGuts::SeqJob> jobs;
+        FastaParser parser;
+        parser.set_callback([&jobs](const std::string &id, const std::string &seq) {
+            KmerGuts::SeqJob j;
+            j.id = id;
+            j.seq = seq;
+            jobs.push_back(std::move(j));
+            return 0;
+        });
+        std::ifstream in(fasta, std::ios::binary);
+        if (!in) {
+            std::fprintf(stderr, "cannot open %s\n", fasta.c_str());
+            return 1;
+        }
+        char ch;
+        while (in.get(ch))
+            parser.parse_char(ch);
+        parser.parse_complete();
+
+        const bool details = mode == "query_details";
+        std::vector<std::shared_ptr<std::vector<KmerGuts::hit_in_sequence_t>>> hit_lists(jobs.size());
+        for (size_t i = 0; i < jobs.size(); i++) {
+            jobs[i].calls = std::make_shared<std::vector<KmerCall>>();
+            jobs[i].otu_stats = std::make_shared<KmerOtuStats>();
+            if (details || mode == "add") {
+                auto hl = std::make_shared<std::vector<KmerGuts::hit_in_sequence_t>>();
+                hit_lists[i] = hl;
+                jobs[i].hit_cb = [hl](KmerGuts::hit_in_sequence_t h) { hl->push_back(h); };
+            }
+        }
+        kguts.process_aa_batch(jobs);
+
+        std::ostringstream os;
+        for (size_t i = 0; i < jobs.size(); i++) {
+            const std::string &id = jobs[i].id, &seq = jobs[i].seq;
+            auto &calls = *jobs[i].calls;
+            if (mode == "query_best") {
+                int fi;
+                std::string fn;
+                float score, wscore, off = 0.0f;
+                kguts.find_best_call(calls, fi, fn, score, wscore, off);
+                if (!fn.empty())
+                    os << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+            } else if (mode == "add") {
+                os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+                for (auto &c : calls)
+                    os << kguts.format_call(c);
+                os << kguts.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
+                int fi;
+                std::string fn;
+                /* uninitialised in the reference when there are no calls
+                 * (add_request.cc:334); 0 here */
+                float score, wscore, off = 0.0f;
+                kguts.find_best_call(calls, fi, fn, score, wscore, off);
+                if (fn.empty() || fn.find(" ?? ") != std::string::npos)
+                    fn = "hypothetical protein";
+                os << "BEST-CALL\t" << id << "\t" << fn << "\t" << score << "\t" << wscore << "\t"
+                   << off << "\n";
+            } else {
+                os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+                for (auto &c : calls)
+                    os << kguts.format_call(c);
+                if (details)
+                    for (auto &h : *hit_lists[i])
+                        os << kguts.format_hit(h);
+                os << kguts.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
+            }
+        }
+        const std::string s = os.str();
+        std::fwrite(s.data(), 1, s.size(), stdout);
+    } catch (const Error &e) {
+        std::fprintf(stderr, "kgx_query: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,699 @@
+/*
+ * kgx_runtime.cpp -- host side of the C ABI (include/kgx.h): image loading
+ * and replication into HBM, per-thread contexts, batch orchestration, host
+ * OTU tallies.
+ *
+ * Replaces KmerImage (kmer_image.cc:41-108) and the per-sequence loop of
+ * KmerGuts::process_aa_seq (kguts.cc:888-908) with batched HIP launches.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "kgx_internal.h"
+
+using namespace kgx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(KGX_EDEVICE, std::string(#expr ": ") + hipGetErrorString(e_));      \
+    } while (0)
+
+/* grow-only device buffer */
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap)
+            return hipSuccess;
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+bool is_gfx950(int dev)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
+
+}  // namespace
+
+struct kgx_image {
+    int device = 0;
+    uint64_t num_sigs = 0;
+    kgx_sig_kmer *d_table = nullptr;
+};
+
+struct kgx_ctx {
+    kgx_image *img = nullptr;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    /* device scratch */
+    DevBuf residues, offsets, wbase, cbase, chunk_seq, chunk_hits, hits, calls, hit_count,
+        call_count, dense_hoff, dense_coff, dense_hits, dense_calls;
+    /* current plan */
+    uint32_t n_seq = 0;
+    uint64_t n_residues = 0;
+    uint64_t max_chunks = 0;
+    const uint64_t *d_off = nullptr;
+    /* host results */
+    std::vector<uint64_t> h_hoff, h_coff, h_ooff;
+    std::vector<kgx_hit> h_hits;
+    std::vector<kgx_call> h_calls;
+    std::vector<kgx_otu> h_otus;
+    std::vector<uint32_t> h_hcount, h_ccount;
+    std::vector<char> h_res;
+};
+
+extern "C" {
+
+const char *kgx_version(void) { return "close_kmers_amd 0.1 (gfx950)"; }
+
+const char *kgx_last_error(void) { return g_last_error.c_str(); }
+
+const char *kgx_strerror(int code)
+{
+    switch (code) {
+    case KGX_OK: return "ok";
+    case KGX_EINVAL: return "invalid argument";
+    case KGX_EIO: return "i/o error";
+    case KGX_EFORMAT: return "image format mismatch";
+    case KGX_ENOMEM: return "out of memory";
+    case KGX_EDEVICE: return "device error";
+    case KGX_ERANGE: return "out of supported range";
+    case KGX_EFULL: return "hash table half full";
+    default: return "unknown error";
+    }
+}
+
+int kgx_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    int good = 0;
+    for (int d = 0; d < n; d++)
+        good += is_gfx950(d) ? 1 : 0;
+    return good;
+}
+
+int kgx_params_default(kgx_params *p)
+{
+    if (!p)
+        return fail(KGX_EINVAL, "null params");
+    /* set_default_parameters, kguts.cc:236-242 */
+    p->order_constraint = 0;
+    p->min_hits = 5;
+    p->min_weighted_hits = 0;
+    p->max_gap = 200;
+    return KGX_OK;
+}
+
+int kgx_params_parse(kgx_params *p, const char *const *names, const char *const *values, size_t n)
+{
+    if (!p || (n && (!names || !values)))
+        return fail(KGX_EINVAL, "null argument");
+    kgx_params_default(p);
+    /* set_parameters, kguts.cc:244-268: std::stoi; invalid_argument warns */
+    for (size_t i = 0; i < n; i++) {
+        int32_t *dst = nullptr;
+        std::string k = names[i] ? names[i] : "";
+        if (k == "order_constraint")
+            dst = &p->order_constraint;
+        else if (k == "min_hits")
+            dst = &p->min_hits;
+        else if (k == "min_weighted_hits")
+            dst = &p->min_weighted_hits;
+        else if (k == "max_gap")
+            dst = &p->max_gap;
+        if (!dst)
+            continue;
+        try {
+            *dst = std::stoi(values[i] ? values[i] : "");
+        } catch (const std::invalid_argument &) {
+            std::fprintf(stderr, "Warning: invalid integer '%s' passed for parameter %s\n",
+                         values[i] ? values[i] : "", k.c_str());
+        } catch (const std::out_of_range &) {
+            return fail(KGX_ERANGE, "parameter " + k + " out of int range");
+        }
+    }
+    return KGX_OK;
+}
+
+/* ---- images ------------------------------------------------------------ */
+
+static int image_alloc(int device, uint64_t num_sigs, kgx_image **out)
+{
+    if (!out)
+        return fail(KGX_EINVAL, "null output");
+    if (num_sigs == 0)
+        return fail(KGX_EFORMAT, "image with zero buckets");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(KGX_EDEVICE, "no such HIP device " + std::to_string(device));
+    if (!is_gfx950(device))
+        return fail(KGX_EDEVICE, "device " + std::to_string(device) + " is not gfx950");
+    HIP_TRY(hipSetDevice(device));
+    kgx_image *img = new kgx_image;
+    img->device = device;
+    img->num_sigs = num_sigs;
+    hipError_t e = hipMalloc(&img->d_table, num_sigs * sizeof(kgx_sig_kmer));
+    if (e != hipSuccess) {
+        delete img;
+        return fail(KGX_ENOMEM, "hipMalloc of the image table failed: " +
+                                    std::string(hipGetErrorString(e)));
+    }
+    *out = img;
+    return KGX_OK;
+}
+
+/* KmerImage::map_image_file validation, kmer_image.cc:128-147 */
+static int validate_header(const kgx_image_header &h, uint64_t file_size)
+{
+    if (file_size != sizeof(kgx_sig_kmer) * h.num_sigs + sizeof(kgx_image_header))
+        return fail(KGX_EFORMAT, "Version mismatch: file size does not match");
+    if (h.version != 1)
+        return fail(KGX_EFORMAT, "Version mismatch: file has " + std::to_string(h.version) +
+                                     " code has 1");
+    if (h.entry_size != sizeof(kgx_sig_kmer))
+        return fail(KGX_EFORMAT, "Version mismatch: entry size " + std::to_string(h.entry_size));
+    return KGX_OK;
+}
+
+int kgx_image_open(const char *dir, int device, kgx_image **out)
+{
+    if (!dir || !out)
+        return fail(KGX_EINVAL, "null argument");
+    std::string path = std::string(dir) + "/kmer.table.mem_map";
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f)
+        return fail(KGX_EIO, "open " + path + ": " + std::strerror(errno));
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0) {
+        std::fclose(f);
+        return fail(KGX_EIO, "stat " + path + " failed");
+    }
+    kgx_image_header h;
+    if (std::fread(&h, sizeof(h), 1, f) != 1) {
+        std::fclose(f);
+        return fail(KGX_EFORMAT, "Version mismatch: file size does not match");
+    }
+    int rc = validate_header(h, (uint64_t)st.st_size);
+    if (rc) {
+        std::fclose(f);
+        return rc;
+    }
+    kgx_image *img = nullptr;
+    rc = image_alloc(device, h.num_sigs, &img);
+    if (rc) {
+        std::fclose(f);
+        return rc;
+    }
+    /* stream the table through a pinned staging ring into HBM */
+    const size_t chunk = 256ull << 20;
+    void *stage[2] = {nullptr, nullptr};
+    hipStream_t s;
+    if (hipHostMalloc(&stage[0], chunk) != hipSuccess || hipHostMalloc(&stage[1], chunk) != hipSuccess ||
+        hipStreamCreate(&s) != hipSuccess) {
+        std::fclose(f);
+        kgx_image_close(img);
+        return fail(KGX_ENOMEM, "pinned staging allocation failed");
+    }
+    hipEvent_t ev[2];
+    (void)hipEventCreate(&ev[0]);
+    (void)hipEventCreate(&ev[1]);
+    uint64_t total = h.num_sigs * sizeof(kgx_sig_kmer), done = 0;
+    int buf = 0;
+    bool ok = true, used[2] = {false, false};
+    while (done < total) {
+        size_t n = (size_t)std::min<uint64_t>(chunk, total - done);
+        if (used[buf])
+            (void)hipEventSynchronize(ev[buf]);
+        if (std::fread(stage[buf], 1, n, f) != n) {
+            ok = false;
+            break;
+        }
+        if (hipMemcpyAsync(reinterpret_cast<char *>(img->d_table) + done, stage[buf], n,
+                           hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(ev[buf], s) != hipSuccess) {
+            ok = false;
+            break;
+        }
+        used[buf] = true;
+        done += n;
+        buf ^= 1;
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+    (void)hipStreamDestroy(s);
+    (void)hipHostFree(stage[0]);
+    (void)hipHostFree(stage[1]);
+    std::fclose(f);
+    if (!ok) {
+        kgx_image_close(img);
+        return fail(KGX_EIO, "short read of " + path);
+    }
+    *out = img;
+    return KGX_OK;
+}
+
+int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, kgx_image **out)
+{
+    if (!file_bytes || !out || nbytes < sizeof(kgx_image_header))
+        return fail(KGX_EINVAL, "bad image buffer");
+    kgx_image_header h;
+    std::memcpy(&h, file_bytes, sizeof(h));
+    int rc = validate_header(h, nbytes);
+    if (rc)
+        return rc;
+    kgx_image *img = nullptr;
+    rc = image_alloc(device, h.num_sigs, &img);
+    if (rc)
+        return rc;
+    hipError_t e = hipMemcpy(img->d_table, static_cast<const char *>(file_bytes) + sizeof(h),
+                             h.num_sigs * sizeof(kgx_sig_kmer), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        kgx_image_close(img);
+        return fail(KGX_EDEVICE, std::string("image upload: ") + hipGetErrorString(e));
+    }
+    *out = img;
+    return KGX_OK;
+}
+
+int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kgx_image **out,
+                              uint64_t *n_stored)
+{
+    if (2 * n_keys >= num_sigs)
+        return fail(KGX_EFULL, "Your Kmer hash is half-full (kguts.cc:213-216)");
+    kgx_image *img = nullptr;
+    int rc = image_alloc(device, num_sigs, &img);
+    if (rc)
+        return rc;
+    unsigned long long *d_count = nullptr;
+    if (hipMalloc(&d_count, sizeof(*d_count)) != hipSuccess) {
+        kgx_image_close(img);
+        return fail(KGX_ENOMEM, "counter allocation failed");
+    }
+    hipError_t e = launch_synth_image(img->d_table, num_sigs, n_keys, d_count, nullptr);
+    unsigned long long cnt = 0;
+    if (e == hipSuccess)
+        e = hipMemcpy(&cnt, d_count, sizeof(cnt), hipMemcpyDeviceToHost);
+    (void)hipFree(d_count);
+    if (e != hipSuccess) {
+        kgx_image_close(img);
+        return fail(KGX_EDEVICE, std::string("synthetic build: ") + hipGetErrorString(e));
+    }
+    if (n_stored)
+        *n_stored = cnt;
+    *out = img;
+    return KGX_OK;
+}
+
+int kgx_image_close(kgx_image *img)
+{
+    if (!img)
+        return KGX_OK;
+    if (img->d_table) {
+        (void)hipSetDevice(img->device);
+        (void)hipFree(img->d_table);
+    }
+    delete img;
+    return KGX_OK;
+}
+
+uint64_t kgx_image_num_sigs(const kgx_image *img) { return img ? img->num_sigs : 0; }
+int kgx_image_device(const kgx_image *img) { return img ? img->device : -1; }
+const void *kgx_image_table(const kgx_image *img) { return img ? img->d_table : nullptr; }
+
+int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes)
+{
+    if (!img || !dst || nbytes != img->num_sigs * sizeof(kgx_sig_kmer))
+        return fail(KGX_EINVAL, "bad download buffer");
+    HIP_TRY(hipSetDevice(img->device));
+    HIP_TRY(hipMemcpy(dst, img->d_table, nbytes, hipMemcpyDeviceToHost));
+    return KGX_OK;
+}
+
+/* ---- contexts ------------------------------------------------------------ */
+
+int kgx_ctx_create(kgx_image *img, kgx_ctx **out)
+{
+    if (!img || !out)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(img->device));
+    kgx_ctx *c = new kgx_ctx;
+    c->img = img;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(KGX_EDEVICE, std::string("stream: ") + hipGetErrorString(e));
+    }
+    c->own_stream = true;
+    *out = c;
+    return KGX_OK;
+}
+
+int kgx_ctx_destroy(kgx_ctx *c)
+{
+    if (!c)
+        return KGX_OK;
+    (void)hipSetDevice(c->img->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (DevBuf *b : {&c->residues, &c->offsets, &c->wbase, &c->cbase, &c->chunk_seq, &c->chunk_hits,
+                      &c->hits, &c->calls, &c->hit_count, &c->call_count, &c->dense_hoff,
+                      &c->dense_coff, &c->dense_hits, &c->dense_calls})
+        b->release();
+    if (c->own_stream)
+        (void)hipStreamDestroy(c->stream);
+    delete c;
+    return KGX_OK;
+}
+
+void *kgx_ctx_stream(kgx_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int kgx_ctx_set_stream(kgx_ctx *c, void *stream)
+{
+    if (!c)
+        return fail(KGX_EINVAL, "null ctx");
+    if (stream) {
+        if (c->own_stream)
+            (void)hipStreamDestroy(c->stream);
+        c->stream = (hipStream_t)stream;
+        c->own_stream = false;
+    } else if (!c->own_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return KGX_OK;
+}
+
+int kgx_ctx_synchronize(kgx_ctx *c)
+{
+    if (!c)
+        return fail(KGX_EINVAL, "null ctx");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return KGX_OK;
+}
+
+/* ---- stages ------------------------------------------------------------- */
+
+int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_residues)
+{
+    if (!c || (!d_off && n_seq))
+        return fail(KGX_EINVAL, "null argument");
+    if (n_residues > (1ull << 40))
+        return fail(KGX_ERANGE, "batch too large");
+    HIP_TRY(hipSetDevice(c->img->device));
+    /* bounds: windows <= residues; chunks <= n_seq + residues / CHUNK */
+    const uint64_t max_chunks = (uint64_t)n_seq + n_residues / CHUNK + 1;
+    const uint64_t cap_win = std::max<uint64_t>(n_residues, 1);
+    HIP_TRY(c->wbase.reserve((n_seq + 1) * sizeof(uint64_t)));
+    HIP_TRY(c->cbase.reserve((n_seq + 1) * sizeof(uint64_t)));
+    HIP_TRY(c->chunk_seq.reserve(max_chunks * sizeof(uint32_t)));
+    HIP_TRY(c->chunk_hits.reserve(max_chunks * sizeof(uint32_t)));
+    HIP_TRY(c->hits.reserve(cap_win * sizeof(kgx_hit)));
+    HIP_TRY(c->calls.reserve(cap_win * sizeof(kgx_call)));
+    HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
+    HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
+    HIP_TRY(launch_plan(d_off, n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
+                        c->chunk_seq.as<uint32_t>(), max_chunks, c->stream));
+    c->n_seq = n_seq;
+    c->n_residues = n_residues;
+    c->max_chunks = max_chunks;
+    c->d_off = d_off;
+    return KGX_OK;
+}
+
+int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
+{
+    if (!c || (!d_res && c->n_residues) || d_off != c->d_off)
+        return fail(KGX_EINVAL, "probe: residues missing or offsets differ from the plan");
+    HIP_TRY(hipSetDevice(c->img->device));
+    if (c->img->num_sigs >= (1ull << 40))
+        return fail(KGX_ERANGE, "image too large");
+    HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
+                         c->cbase.as<uint64_t>(), c->chunk_seq.as<uint32_t>(), c->n_seq,
+                         c->max_chunks, c->img->d_table, c->img->num_sigs, c->hits.as<kgx_hit>(),
+                         c->chunk_hits.as<uint32_t>(), c->stream));
+    return KGX_OK;
+}
+
+int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
+{
+    if (!c)
+        return fail(KGX_EINVAL, "null ctx");
+    kgx_params p;
+    if (params)
+        p = *params;
+    else
+        kgx_params_default(&p);
+    HIP_TRY(hipSetDevice(c->img->device));
+    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
+                         c->chunk_hits.as<uint32_t>(), c->hits.as<kgx_hit>(),
+                         c->calls.as<kgx_call>(), c->hit_count.as<uint32_t>(),
+                         c->call_count.as<uint32_t>(), p, want, c->stream));
+    return KGX_OK;
+}
+
+int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    out->n_seq = c->n_seq;
+    out->window_base = c->wbase.as<uint64_t>();
+    out->hit_count = c->hit_count.as<uint32_t>();
+    out->call_count = c->call_count.as<uint32_t>();
+    out->hits = c->hits.as<kgx_hit>();
+    out->calls = c->calls.as<kgx_call>();
+    return KGX_OK;
+}
+
+int kgx_run_device(kgx_ctx *c, const kgx_params *params, const uint8_t *d_res, const uint64_t *d_off,
+                   uint32_t n_seq, uint64_t n_residues, uint32_t want, kgx_device_result *out)
+{
+    int rc = kgx_stage_plan(c, d_off, n_seq, n_residues);
+    if (rc)
+        return rc;
+    if ((rc = kgx_stage_probe(c, d_res, d_off)))
+        return rc;
+    if ((rc = kgx_stage_score(c, params, want)))
+        return rc;
+    return out ? kgx_device_result_get(c, out) : KGX_OK;
+}
+
+/* ---- host-buffer batch ---------------------------------------------------- */
+
+int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues,
+                      const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    if (!c || !out || (!seq_offsets && n_seq))
+        return fail(KGX_EINVAL, "null argument");
+    const uint64_t r0 = n_seq ? seq_offsets[0] : 0;
+    const uint64_t n_res = n_seq ? seq_offsets[n_seq] - r0 : 0;
+    for (uint32_t s = 0; s < n_seq; s++)
+        if (seq_offsets[s + 1] < seq_offsets[s])
+            return fail(KGX_EINVAL, "seq_offsets not monotone");
+    if (n_res && !residues)
+        return fail(KGX_EINVAL, "null residues");
+    HIP_TRY(hipSetDevice(c->img->device));
+
+    /* stage residues; a sequence is cut at its first NUL (strlen bound of
+     * gather_hits, kguts.cc:792): the NUL's predecessor and everything after
+     * become 'X', which kills exactly the windows the reference never visits */
+    const char *src = residues ? residues + r0 : nullptr;
+    c->h_res.assign(src, src + n_res);
+    for (uint32_t s = 0; s < n_seq; s++) {
+        char *b = c->h_res.data() + (seq_offsets[s] - r0);
+        uint64_t len = seq_offsets[s + 1] - seq_offsets[s];
+        const void *z = len ? std::memchr(b, 0, len) : nullptr;
+        if (z) {
+            uint64_t slen = (uint64_t)((const char *)z - b);
+            for (uint64_t i = slen ? slen - 1 : 0; i < len; i++)
+                b[i] = 'X';
+        }
+    }
+    std::vector<uint64_t> off(n_seq + 1);
+    for (uint32_t s = 0; s <= n_seq; s++)
+        off[s] = n_seq ? seq_offsets[s] - r0 : 0;
+
+    HIP_TRY(c->residues.reserve(n_res + 16));
+    HIP_TRY(c->offsets.reserve((n_seq + 1) * sizeof(uint64_t)));
+    if (n_res)
+        HIP_TRY(hipMemcpyAsync(c->residues.p, c->h_res.data(), n_res, hipMemcpyHostToDevice,
+                               c->stream));
+    HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), (n_seq + 1) * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, c->stream));
+    const uint32_t dev_want = want;
+    int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq,
+                            n_res, dev_want, nullptr);
+    if (rc)
+        return rc;
+
+    /* counts -> dense CSR offsets on the host, gather on the device */
+    c->h_hcount.resize(n_seq + 1);
+    c->h_ccount.resize(n_seq + 1);
+    if (n_seq) {
+        HIP_TRY(hipMemcpyAsync(c->h_hcount.data(), c->hit_count.p, n_seq * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_ccount.data(), c->call_count.p, n_seq * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    c->h_hoff.assign(n_seq + 1, 0);
+    c->h_coff.assign(n_seq + 1, 0);
+    for (uint32_t s = 0; s < n_seq; s++) {
+        c->h_hoff[s + 1] = c->h_hoff[s] + c->h_hcount[s];
+        c->h_coff[s + 1] = c->h_coff[s] + (want_calls ? c->h_ccount[s] : 0);
+    }
+    const uint64_t nh = c->h_hoff[n_seq], nc = c->h_coff[n_seq];
+    const bool need_hits = (want & (KGX_WANT_HITS | KGX_WANT_OTU)) != 0;
+    c->h_hits.resize(need_hits ? nh : 0);
+    c->h_calls.resize(nc);
+    if ((need_hits && nh) || nc) {
+        HIP_TRY(c->dense_hoff.reserve((n_seq + 1) * sizeof(uint64_t)));
+        HIP_TRY(c->dense_coff.reserve((n_seq + 1) * sizeof(uint64_t)));
+        HIP_TRY(c->dense_hits.reserve(std::max<uint64_t>(nh, 1) * sizeof(kgx_hit)));
+        HIP_TRY(c->dense_calls.reserve(std::max<uint64_t>(nc, 1) * sizeof(kgx_call)));
+        HIP_TRY(hipMemcpyAsync(c->dense_hoff.p, c->h_hoff.data(), (n_seq + 1) * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->dense_coff.p, c->h_coff.data(), (n_seq + 1) * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_count.as<uint32_t>(),
+                              c->call_count.as<uint32_t>(), c->hits.as<kgx_hit>(),
+                              c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
+                              c->dense_coff.as<uint64_t>(),
+                              need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
+                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, c->stream));
+        if (need_hits && nh)
+            HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
+                                   hipMemcpyDeviceToHost, c->stream));
+        if (nc)
+            HIP_TRY(hipMemcpyAsync(c->h_calls.data(), c->dense_calls.p, nc * sizeof(kgx_call),
+                                   hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+
+    /* OTU tallies: KmerOtuStats::otu_map over the hits the scorer flagged,
+     * then finalize() (kguts.h:214-218: std::sort by count, descending) */
+    c->h_ooff.assign(n_seq + 1, 0);
+    c->h_otus.clear();
+    if (want & KGX_WANT_OTU) {
+        std::map<int, int> m;
+        std::vector<std::pair<int, int>> v;
+        for (uint32_t s = 0; s < n_seq; s++) {
+            m.clear();
+            for (uint64_t i = c->h_hoff[s]; i < c->h_hoff[s + 1]; i++)
+                if (c->h_hits[i].flags & KGX_HIT_OTU)
+                    m[c->h_hits[i].otu_index]++;
+            v.assign(m.begin(), m.end());
+            std::sort(v.begin(), v.end(),
+                      [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
+                          return b.second < a.second;
+                      });
+            for (auto &pr : v)
+                c->h_otus.push_back(kgx_otu{pr.first, pr.second});
+            c->h_ooff[s + 1] = c->h_otus.size();
+        }
+    }
+    uint64_t nwin = 0;
+    for (uint32_t s = 0; s < n_seq; s++)
+        nwin += windows_of(off[s + 1] - off[s]);
+
+    out->n_seq = n_seq;
+    out->hit_offsets = c->h_hoff.data();
+    out->hits = need_hits ? c->h_hits.data() : nullptr;
+    out->call_offsets = c->h_coff.data();
+    out->calls = c->h_calls.data();
+    out->otu_offsets = c->h_ooff.data();
+    out->otus = c->h_otus.data();
+    out->n_windows = nwin;
+    return KGX_OK;
+}
+
+/* ---- synthetic queries / memory helpers ----------------------------------- */
+
+int kgx_synth_queries(kgx_ctx *c, uint64_t image_n_keys, uint32_t n_seq, uint32_t length,
+                      uint32_t x_permille, uint64_t q0, uint8_t *d_res, uint64_t *d_off)
+{
+    if (!c || !d_res || !d_off)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->img->device));
+    HIP_TRY(launch_synth_queries(image_n_keys, n_seq, length, x_permille, q0, d_res, d_off,
+                                 c->stream));
+    return KGX_OK;
+}
+
+int kgx_device_alloc(int device, uint64_t nbytes, void **out)
+{
+    if (!out)
+        return fail(KGX_EINVAL, "null output");
+    HIP_TRY(hipSetDevice(device));
+    hipError_t e = hipMalloc(out, std::max<uint64_t>(nbytes, 1));
+    if (e != hipSuccess)
+        return fail(KGX_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return KGX_OK;
+}
+
+int kgx_device_free(void *p)
+{
+    if (p)
+        HIP_TRY(hipFree(p));
+    return KGX_OK;
+}
+
+int kgx_memcpy_h2d(void *dst, const void *src, uint64_t n)
+{
+    HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+    return KGX_OK;
+}
+
+int kgx_memcpy_d2h(void *dst, const void *src, uint64_t n)
+{
+    HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+    return KGX_OK;
+}
+
+}  /* extern "C" */

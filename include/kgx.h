@@ -1,0 +1,225 @@
+/*
+ * kgx.h -- C ABI of the MI355X-native close_kmers hot path:
+ *          k-mer encode -> signature-hash probe -> hit-run scoring.
+ *
+ * The reference runs this path as KmerGuts::process_aa_seq over a memory-mapped
+ * KmerImage, one KmerGuts per CPU pool thread (threadpool.cc:18-44).  This ABI
+ * replaces that per-sequence C++ call with batched entry points over plain
+ * pointers and sizes (no C++ or torch types), implemented by hand-written
+ * gfx950 HIP kernels (close_kmers_amd/csrc/).  The C++ facade in
+ * close_kmers_amd/csrc/kguts_hip.h re-exposes the KmerGuts surface on top of
+ * it; INTEGRATION.md shows the bindings.
+ *
+ * Error behaviour: every entry point returns KGX_OK (0) or a negative KGX_E*
+ * code and never exits (the reference exit()s on bad files,
+ * kmer_image.cc:88-147, kguts.cc:550-552).  kgx_last_error() returns a
+ * thread-local message for the last failure.
+ *
+ * Threading: a kgx_image is read-only after creation and may be shared by any
+ * number of contexts; a kgx_ctx is NOT thread-safe, exactly like KmerGuts
+ * (kguts.h:263-266) -- create one per host worker thread (threadpool.h:42).
+ */
+#ifndef KGX_H
+#define KGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ----------------------------------------------------- */
+#define KGX_OK 0
+#define KGX_EINVAL (-1)   /* bad argument */
+#define KGX_EIO (-2)      /* cannot open / read a file */
+#define KGX_EFORMAT (-3)  /* image size / version / entry size mismatch */
+#define KGX_ENOMEM (-4)   /* host or device allocation failed */
+#define KGX_EDEVICE (-5)  /* HIP runtime error or no gfx950 device */
+#define KGX_ERANGE (-6)   /* image or batch larger than supported */
+#define KGX_EFULL (-7)    /* image builder: table would reach half full */
+
+/* ---- what kgx_process_* computes --------------------------------------- */
+#define KGX_WANT_HITS 1u  /* hit list (what hit_cb receives, kguts.cc:814-815) */
+#define KGX_WANT_CALLS 2u /* KmerCall runs (process_set_of_hits, kguts.cc:734-781) */
+#define KGX_WANT_OTU 4u   /* OTU tallies (KmerOtuStats, kguts.h:185-219) */
+
+/* ---- on-disk / in-HBM record layouts (kmer_image.h:11-23) -------------- */
+typedef struct kgx_image_header { /* kmer_memory_image_t */
+    uint64_t num_sigs;            /* buckets */
+    uint64_t entry_size;          /* 24 */
+    int64_t version;              /* 1 (KMER_VERSION, kmer_image.h:6) */
+} kgx_image_header;
+
+typedef struct kgx_sig_kmer { /* sig_kmer_t: one 24-byte bucket */
+    uint64_t which_kmer;      /* > 20^8 means empty (kguts.cc:106-107) */
+    int32_t otu_index;
+    uint16_t avg_from_end;
+    uint16_t pad;
+    int32_t function_index;
+    float function_wt;
+} kgx_sig_kmer;
+
+/* One hit: KmerGuts::hit_in_sequence_t (kguts.h:228-233) = the bucket copy +
+ * the window offset, plus the sequence index within the batch.  32 bytes. */
+typedef struct kgx_hit {
+    uint64_t which_kmer;
+    int32_t otu_index;
+    uint16_t avg_from_end;
+    uint16_t flags; /* KGX_HIT_* (the bucket's pad bytes in the reference) */
+    int32_t function_index;
+    float function_wt;
+    uint32_t pos; /* offset of the 8-mer in the protein (pLoc, kguts.cc:803) */
+    uint32_t seq; /* index of the sequence in the batch */
+} kgx_hit;
+#define KGX_HIT_IN_RUN 1u /* appended to the run buffer (kguts.cc:845-851) */
+#define KGX_HIT_OTU 2u    /* tallied into otu_map by an emitted call (kguts.cc:760-768) */
+
+/* KmerCall (kguts.h:166-183), 20 bytes */
+typedef struct kgx_call {
+    uint32_t start;
+    uint32_t end;
+    int32_t count;
+    uint32_t function_index;
+    float weighted_hits;
+} kgx_call;
+
+/* one (otu_index, count) pair of KmerOtuStats::otus_by_count (kguts.h:214-218) */
+typedef struct kgx_otu {
+    int32_t otu_index;
+    int32_t count;
+} kgx_otu;
+
+/* KmerGuts parameters (kguts.cc:236-268); kgx_params_default() gives
+ * min_hits=5, max_gap=200, order_constraint=0, min_weighted_hits=0.
+ * min_hits <= 0 makes the reference read hits[-2] at the final flush (UB);
+ * here such a flush emits nothing. */
+typedef struct kgx_params {
+    int32_t min_hits;
+    int32_t max_gap;
+    int32_t order_constraint;
+    int32_t min_weighted_hits;
+} kgx_params;
+
+/* Host views of a batch's results (CSR by sequence).  Owned by the context
+ * and valid until the next call on it.  otus are in otus_by_count order. */
+typedef struct kgx_result {
+    uint32_t n_seq;
+    const uint64_t *hit_offsets; /* n_seq + 1 */
+    const kgx_hit *hits;
+    const uint64_t *call_offsets; /* n_seq + 1 */
+    const kgx_call *calls;
+    const uint64_t *otu_offsets; /* n_seq + 1 */
+    const kgx_otu *otus;
+    uint64_t n_windows; /* 8-mer windows probed */
+} kgx_result;
+
+/* Device-resident results of kgx_run_device (pointers into HBM).  Hits and
+ * calls of sequence s start at window_base[s]; their counts are
+ * hit_count[s] / call_count[s].  Hit records of a sequence are contiguous
+ * and in position order. */
+typedef struct kgx_device_result {
+    uint32_t n_seq;
+    const uint64_t *window_base; /* n_seq + 1: exclusive scan of max(0, len-8) */
+    const uint32_t *hit_count;   /* n_seq */
+    const uint32_t *call_count;  /* n_seq */
+    const kgx_hit *hits;         /* capacity window_base[n_seq] */
+    const kgx_call *calls;       /* capacity window_base[n_seq] */
+} kgx_device_result;
+
+typedef struct kgx_image kgx_image;
+typedef struct kgx_ctx kgx_ctx;
+
+/* ---- library ------------------------------------------------------------ */
+const char *kgx_version(void);
+const char *kgx_last_error(void);
+const char *kgx_strerror(int code);
+/* number of visible gfx950 devices (0 in a GPU-less container) */
+int kgx_device_count(void);
+int kgx_params_default(kgx_params *p);
+/* set_parameters (kguts.cc:244-268) over parallel name/value string arrays:
+ * resets to the defaults, then applies std::stoi to the four known names;
+ * an unparsable value leaves the default (the reference only warns). */
+int kgx_params_parse(kgx_params *p, const char *const *names, const char *const *values, size_t n);
+
+/* ---- images: replaces KmerImage (kmer_image.h:25-39, kmer_image.cc) ----- */
+/* Load <dir>/kmer.table.mem_map into HBM of `device`, validating size,
+ * version and entry size exactly as kmer_image.cc:128-147. */
+int kgx_image_open(const char *dir, int device, kgx_image **out);
+/* Same, from an in-memory file image (header followed by the table). */
+int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, kgx_image **out);
+/* Synthetic image built in HBM (close_kmers_amd/synth.py documents the
+ * generator): n_keys entries in num_sigs buckets, duplicates dropped (lowest
+ * entry id wins), linear probing as kguts.cc:166-171.  *n_stored receives the
+ * number of distinct keys stored. */
+int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kgx_image **out,
+                              uint64_t *n_stored);
+int kgx_image_close(kgx_image *img);
+uint64_t kgx_image_num_sigs(const kgx_image *img);
+int kgx_image_device(const kgx_image *img);
+/* device pointer to the num_sigs * 24-byte table */
+const void *kgx_image_table(const kgx_image *img);
+/* copy the table (num_sigs * 24 bytes) to host memory */
+int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes);
+
+/* ---- contexts: one per host thread, like one KmerGuts per pool thread --- */
+int kgx_ctx_create(kgx_image *img, kgx_ctx **out);
+int kgx_ctx_destroy(kgx_ctx *ctx);
+/* the HIP stream the context launches on (hipStream_t) */
+void *kgx_ctx_stream(kgx_ctx *ctx);
+/* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
+int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
+
+/* Host-buffer batch: process_aa_seq (kguts.cc:888-908) for every sequence of
+ * the batch.  residues: concatenated sequence bytes; seq_offsets[n_seq+1]
+ * delimits them.  Each sequence is cut at its first NUL byte, as
+ * gather_hits' strlen() bound does (kguts.cc:792).  Synchronous; the result
+ * views stay valid until the next call on ctx. */
+int kgx_process_batch(kgx_ctx *ctx, const kgx_params *params, const char *residues,
+                      const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                      kgx_result *out);
+
+/* Device-buffer batch: same computation on residues / offsets already in HBM
+ * (NUL-free sequences), enqueued on the context's stream without host
+ * synchronisation.  The results stay in HBM (kgx_device_result). */
+int kgx_run_device(kgx_ctx *ctx, const kgx_params *params, const uint8_t *d_residues,
+                   const uint64_t *d_seq_offsets, uint32_t n_seq, uint64_t n_residues,
+                   uint32_t want, kgx_device_result *out);
+
+/* The stages kgx_run_device enqueues, for per-kernel timing:
+ *   kgx_stage_plan   window/chunk bookkeeping (2 small kernels)
+ *   kgx_stage_probe  encode + probe: the HBM random-access kernel
+ *   kgx_stage_score  hit-run scorer (calls, OTU flags) */
+int kgx_stage_plan(kgx_ctx *ctx, const uint64_t *d_seq_offsets, uint32_t n_seq, uint64_t n_residues);
+int kgx_stage_probe(kgx_ctx *ctx, const uint8_t *d_residues, const uint64_t *d_seq_offsets);
+int kgx_stage_score(kgx_ctx *ctx, const kgx_params *params, uint32_t want);
+int kgx_device_result_get(kgx_ctx *ctx, kgx_device_result *out);
+
+/* Synthetic query batch generated in HBM (synth.py make_queries). */
+int kgx_synth_queries(kgx_ctx *ctx, uint64_t image_n_keys, uint32_t n_seq, uint32_t length,
+                      uint32_t x_permille, uint64_t q0, uint8_t *d_residues,
+                      uint64_t *d_seq_offsets);
+
+/* ---- host-side rules on results (run on the CPU, no device needed) ------ */
+/* find_best_call (kguts.cc:1008-1199) over one sequence's calls.  names /
+ * n_names is the function.index table (function_at_index, kguts.h:361-366).
+ * *function receives the called function (NUL-terminated, truncated to
+ * function_cap).  *score_offset_set is 0 when the reference leaves
+ * score_offset untouched (no calls). */
+int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const *names,
+                       int n_names, int32_t *function_index, char *function, size_t function_cap,
+                       float *score, float *weighted_score, float *score_offset,
+                       int *score_offset_set);
+
+/* Device memory helpers for callers without their own allocator. */
+int kgx_device_alloc(int device, uint64_t nbytes, void **out);
+int kgx_device_free(void *p);
+int kgx_memcpy_h2d(void *dst, const void *src, uint64_t nbytes);
+int kgx_memcpy_d2h(void *dst, const void *src, uint64_t nbytes);
+int kgx_ctx_synchronize(kgx_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KGX_H */

@@ -1,0 +1,155 @@
+/*
+ * oracle_query.cpp -- CPU oracle driver for the request-handler surface.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Reads a kmer data directory (kmer.table.mem_map,
+ * function.index, otu.index) and a FASTA file, runs the restated KmerGuts path
+ * and prints exactly what the reference handlers print for each sequence:
+ *
+ *   mode=query          query_request.cc:103-151 (details=0, find_best_call=0)
+ *   mode=query_details  query_request.cc:103-151 with details=1 (HIT lines)
+ *   mode=query_best     query_request.cc:124-135 (find_best_call=1)
+ *   mode=add            add_request.cc:305-353 (silent=0)
+ *
+ * usage: oracle_query DATA_DIR FASTA MODE [name=value ...]
+ * The name=value pairs play the role of the request's query string
+ * (krequest2.cc:112-124) and feed set_parameters (kguts.cc:244-268).
+ */
+#include "kmer_oracle.h"
+
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace oracle;
+
+/* KmerImage::map_image_file validation, kmer_image.cc:83-150 */
+static bool load_image(const std::string &dir, std::vector<SigKmer> &table, uint64_t &num_sigs)
+{
+    std::string path = dir + "/kmer.table.mem_map";
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f)
+        return false;
+    std::fseek(f, 0, SEEK_END);
+    long size = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    ImageHeader h;
+    if (std::fread(&h, sizeof(h), 1, f) != 1) {
+        std::fclose(f);
+        return false;
+    }
+    if ((uint64_t)size != sizeof(SigKmer) * h.num_sigs + sizeof(ImageHeader) || h.version != 1 ||
+        h.entry_size != sizeof(SigKmer)) {
+        std::fclose(f);
+        return false;
+    }
+    table.resize(h.num_sigs);
+    size_t got = std::fread(table.data(), sizeof(SigKmer), h.num_sigs, f);
+    std::fclose(f);
+    num_sigs = h.num_sigs;
+    return got == h.num_sigs;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 4) {
+        std::fprintf(stderr, "usage: %s DATA_DIR FASTA MODE [name=value ...]\n", argv[0]);
+        return 2;
+    }
+    std::string dir = argv[1], fasta = argv[2], mode = argv[3];
+    std::map<std::string, std::string> qp;
+    for (int i = 4; i < argc; i++) {
+        std::string a = argv[i];
+        size_t eq = a.find('=');
+        if (eq != std::string::npos)
+            qp[a.substr(0, eq)] = a.substr(eq + 1);
+    }
+    std::vector<SigKmer> table;
+    uint64_t num_sigs = 0;
+    if (!load_image(dir, table, num_sigs)) {
+        std::fprintf(stderr, "bad image in %s\n", dir.c_str());
+        return 1;
+    }
+    std::vector<std::string> functions, otus;
+    if (!load_index_file(dir + "/function.index", functions) ||
+        !load_index_file(dir + "/otu.index", otus)) {
+        std::fprintf(stderr, "missing/bad index files in %s\n", dir.c_str());
+        return 1;
+    }
+    std::ifstream in(fasta, std::ios::binary);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    auto records = parse_fasta(ss.str());
+
+    Scorer scorer(table.data(), num_sigs);
+    /* set_parameters, kguts.cc:244-268: defaults, then std::stoi per known key;
+     * std::invalid_argument only warns. */
+    scorer.params = Params();
+    {
+        std::map<std::string, int *> pm = {{"order_constraint", &scorer.params.order_constraint},
+                                           {"min_hits", &scorer.params.min_hits},
+                                           {"min_weighted_hits", &scorer.params.min_weighted_hits},
+                                           {"max_gap", &scorer.params.max_gap}};
+        for (auto &kv : qp) {
+            auto it = pm.find(kv.first);
+            if (it == pm.end())
+                continue;
+            try {
+                *it->second = std::stoi(kv.second);
+            } catch (const std::invalid_argument &) {
+                std::cerr << "Warning: invalid integer '" << kv.second << "' passed for parameter "
+                          << kv.first << "\n";
+            }
+        }
+    }
+
+    std::ostringstream os;
+    const bool details = (mode == "query_details");
+    for (auto &rec : records) {
+        const std::string &id = rec.first, &seq = rec.second;
+        std::vector<Call> calls;
+        std::vector<SeqHit> hits;
+        OtuStats stats;
+        bool want_hits = details || mode == "add";
+        scorer.process(seq.c_str(), seq.size(), &calls, want_hits ? &hits : nullptr, &stats, true);
+        if (mode == "query_best") {
+            int fi;
+            std::string fn;
+            float score, wscore, off = 0.0f;
+            find_best_call(calls, functions, fi, fn, score, wscore, off);
+            if (!fn.empty())
+                os << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+        } else if (mode == "add") {
+            os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+            for (auto &c : calls)
+                os << format_call(c, functions);
+            os << format_otu_stats(id, seq.size(), stats);
+            int fi;
+            std::string fn;
+            /* best_call_score_offset is uninitialised in the reference when
+             * there are no calls (add_request.cc:334); defined as 0 here. */
+            float score, wscore, off = 0.0f;
+            find_best_call(calls, functions, fi, fn, score, wscore, off);
+            if (fn.empty() || fn.find(" ?? ") != std::string::npos)
+                fn = "hypothetical protein";
+            os << "BEST-CALL\t" << id << "\t" << fn << "\t" << score << "\t" << wscore << "\t" << off
+               << "\n";
+        } else {
+            os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+            for (auto &c : calls)
+                os << format_call(c, functions);
+            if (details)
+                for (auto &h : hits)
+                    os << format_hit(h, functions);
+            os << format_otu_stats(id, seq.size(), stats);
+        }
+    }
+    std::fwrite(os.str().data(), 1, os.str().size(), stdout);
+    return 0;
+}

@@ -1,0 +1,320 @@
+"""Parity of the HIP path (through the C ABI / the KmerGuts facade driver)
+with the CPU oracle: bit-exact hits, calls, OTU tallies and handler text."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from close_kmers_amd import build as kbuild
+from close_kmers_amd import image_files, synth
+from helpers import GOLDEN, DesignedImage, pack, random_protein, synthetic_table
+
+pytestmark = pytest.mark.gpu
+
+HIT_FIELDS = ["which_kmer", "otu_index", "avg_from_end", "function_index", "function_wt", "pos", "seq"]
+PARAM_SETS = [(5, 200, 0, 0), (3, 200, 0, 0), (5, 50, 0, 0), (5, 200, 1, 0), (5, 200, 0, 20),
+              (2, 1000, 0, 0), (7, 10, 1, 3), (5, -1, 0, 0), (1, 200, 0, 0)]
+
+
+def eq_fields(a, b, fields=HIT_FIELDS):
+    if len(a) != len(b):
+        return False
+    for f in fields:
+        x, y = a[f], b[f]
+        if x.dtype.kind == "f":
+            x, y = x.view(np.uint32), y.view(np.uint32)
+        if not np.array_equal(x, y):
+            return False
+    return True
+
+
+def assert_same(got, want, n_seq):
+    """got: abi.BatchResult, want: oracle.BatchResult."""
+    assert np.array_equal(got.hit_offsets, want.hit_offsets)
+    for f in HIT_FIELDS:
+        wf = want.hits[f]
+        gf = got.hits[f]
+        if f == "function_wt":
+            assert np.array_equal(gf.view(np.uint32), wf.view(np.uint32)), f
+        else:
+            assert np.array_equal(gf, wf), f
+    assert np.array_equal(got.call_offsets, want.call_offsets)
+    for f in ["start", "end", "count", "function_index"]:
+        assert np.array_equal(got.calls[f], want.calls[f]), f
+    assert np.array_equal(got.calls["weighted_hits"].view(np.uint32),
+                          want.calls["weighted_hits"].view(np.uint32))
+    assert np.array_equal(got.otu_offsets, want.otu_offsets)
+    assert np.array_equal(got.otus["otu_index"], want.otus[:, 0])
+    assert np.array_equal(got.otus["count"], want.otus[:, 1])
+
+
+# ---------------------------------------------------------------------------
+# golden handler text through the C++ facade (kgx_query)
+
+def _golden_cases():
+    for ds in ("scoring", "edge", "cap"):
+        d = os.path.join(GOLDEN, ds)
+        for f in sorted(os.listdir(d)):
+            if f.startswith("expected_") and f.endswith(".txt"):
+                yield ds, f
+
+
+@pytest.mark.parametrize("ds,fname", list(_golden_cases()))
+def test_facade_text_matches_golden(gpu, ds, fname):
+    from test_oracle_golden import PARAMS, parse_case
+    mode, pname = parse_case(fname)
+    d = os.path.join(GOLDEN, ds)
+    args = [kbuild.QUERY, os.path.join(d, "data"), os.path.join(d, "input.fasta"), mode]
+    args += [f"{k}={v}" for k, v in PARAMS[pname].items()]
+    r = subprocess.run(args, capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    assert r.stdout == open(os.path.join(d, fname), "rb").read()
+
+
+# ---------------------------------------------------------------------------
+# random synthetic batches through kgx_process_batch
+
+@pytest.fixture(scope="module")
+def small_world(gpu):
+    spec, table = synthetic_table(30000)
+    img = gpu.Image.from_table(table)
+    ctx = gpu.Context(img)
+    yield spec, table, img, ctx
+    ctx.close()
+    img.close()
+
+
+@pytest.mark.parametrize("params", PARAM_SETS)
+def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params):
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 400, x_permille=5)
+    want = oracle_lib.process_batch(table, res, off, params=params)
+    got = ctx.process_batch(res, off, gpu.Params(*params))
+    assert_same(got, want, 400)
+    assert got.n_windows == want.windows
+
+
+def test_ragged_long_and_empty_sequences(small_world, oracle_lib, gpu):
+    spec, table, img, ctx = small_world
+    rng = np.random.default_rng(9)
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(spec.n_src))].reshape(spec.n_src, -1)
+    recs = []
+    for i in range(120):
+        kind = i % 6
+        if kind == 0:
+            n = int(rng.integers(0, 12))
+            s = random_protein(rng, n)
+        elif kind == 1:  # long: many planted sources back to back (multi-chunk)
+            parts = [bytes(src[int(rng.integers(0, spec.n_src))]).decode() for _ in range(int(rng.integers(2, 40)))]
+            s = "".join(parts)
+        elif kind == 2:
+            s = bytes(src[int(rng.integers(0, spec.n_src))]).decode()[: int(rng.integers(5, 300))]
+        elif kind == 3:  # ambiguity sprinkled over a planted sequence
+            s = list(bytes(src[int(rng.integers(0, spec.n_src))]).decode())
+            for p in rng.integers(0, len(s), 6):
+                s[p] = "XxB*u"[int(rng.integers(0, 5))]
+            s = "".join(s)
+        elif kind == 4:
+            s = random_protein(rng, int(rng.integers(300, 3000)))
+        else:
+            s = bytes(src[int(rng.integers(0, spec.n_src))]).decode().lower()
+        recs.append((f"s{i}", s))
+    res, off = pack(recs)
+    for params in [(5, 200, 0, 0), (3, 20, 1, 0)]:
+        want = oracle_lib.process_batch(table, res, off, params=params)
+        got = ctx.process_batch(res, off, gpu.Params(*params))
+        assert_same(got, want, len(recs))
+
+
+def test_want_flags_and_unaligned_offsets(small_world, oracle_lib, gpu):
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 64)
+    # a batch that starts mid-buffer (seq_offsets[0] != 0)
+    pad = np.frombuffer(b"QQQ", np.uint8)
+    res2 = np.concatenate([pad, res])
+    off2 = off + np.uint64(3)
+    want = oracle_lib.process_batch(table, res, off)
+    for w in (1, 2, 4, 3, 5, 6, 7):
+        got = ctx.process_batch(res2, off2, gpu.Params(5, 200, 0, 0), want=w)
+        assert np.array_equal(got.hit_offsets, want.hit_offsets)
+        if w & 1:
+            assert np.array_equal(got.hits["pos"], want.hits["pos"])
+        if w & 2:
+            assert np.array_equal(got.call_offsets, want.call_offsets)
+            assert np.array_equal(got.calls["start"], want.calls["start"])
+        else:
+            assert len(got.calls) == 0
+        if w & 4:
+            assert np.array_equal(got.otu_offsets, want.otu_offsets)
+
+
+def test_nul_byte_cuts_the_sequence(small_world, oracle_lib, gpu):
+    """gather_hits bounds the walk with strlen() (kguts.cc:792)."""
+    spec, table, img, ctx = small_world
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(4))]
+    recs = []
+    for cut in (0, 1, 7, 8, 9, 10, 50, 150, 299):
+        s = bytearray(bytes(src[cut % 4]))
+        s[cut] = 0
+        recs.append(("n", bytes(s)))
+    res, off = pack(recs)
+    want = oracle_lib.process_batch(table, res, off)
+    got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+    assert_same(got, want, len(recs))
+
+
+def test_hit_flags_reproduce_otu_tallies(small_world, gpu):
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 200)
+    got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+    for s in range(200):
+        h = got.hits[got.hit_offsets[s]:got.hit_offsets[s + 1]]
+        m = {}
+        for o in h["otu_index"][(h["flags"] & 2) != 0]:
+            m[int(o)] = m.get(int(o), 0) + 1
+        o = got.otus[got.otu_offsets[s]:got.otu_offsets[s + 1]]
+        assert dict(zip(o["otu_index"].tolist(), o["count"].tolist())) == m
+        c = got.calls[got.call_offsets[s]:got.call_offsets[s + 1]]
+        assert int(c["count"].sum()) == int(((h["flags"] & 2) != 0).sum())
+
+
+# ---------------------------------------------------------------------------
+# designed run-rule edge cases at the API level (cap, carries, order constraint)
+
+def test_hit_buffer_cap(gpu, oracle_lib):
+    d = os.path.join(GOLDEN, "cap")
+    table = image_files.read_image(os.path.join(d, "data"))
+    seq = open(os.path.join(d, "input.fasta")).read().split("\n")[1]
+    res, off = pack([("capped", seq)])
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        for params in [(5, 200, 0, 0), (5, 200, 1, 0), (2, 200, 0, 0)]:
+            want = oracle_lib.process_batch(table, res, off, params=params)
+            got = ctx.process_batch(res, off, gpu.Params(*params))
+            assert want.calls["count"].max() == 39998 or params[2]
+            assert_same(got, want, 1)
+
+
+def test_pair_switch_chains(gpu, oracle_lib):
+    """Alternating same-function pairs: every pair flushes and carries."""
+    rng = np.random.default_rng(21)
+    img = DesignedImage()
+    recs = []
+    for t in range(40):
+        s = random_protein(rng, 400)
+        p = 3
+        f = 0
+        while p < 380:
+            run = int(rng.integers(1, 7))
+            img.add_windows(s, range(p, min(p + run, 390)), f % 5, oI=int(rng.integers(-1, 3)), rng=rng)
+            p += run + int(rng.integers(0, 30))
+            f += int(rng.integers(1, 3))
+        recs.append((f"p{t}", s))
+    table = img.table()
+    res, off = pack(recs)
+    with gpu.Image.from_table(table) as im, gpu.Context(im) as ctx:
+        for params in PARAM_SETS:
+            want = oracle_lib.process_batch(table, res, off, params=params)
+            got = ctx.process_batch(res, off, gpu.Params(*params))
+            assert_same(got, want, len(recs))
+
+
+# ---------------------------------------------------------------------------
+# image loading and the device-side builders
+
+def test_image_open_validation(gpu, tmp_path):
+    L = gpu.lib()
+    h = ctypes.c_void_p()
+    assert L.kgx_image_open(str(tmp_path / "missing").encode(), 0, ctypes.byref(h)) == -2
+    t = np.zeros(3769, dtype=gpu.SIG_DTYPE)
+    t["which_kmer"] = 20 ** 8 + 1
+    d = tmp_path / "bad"
+    image_files.write_data_dir(str(d), t, ["f"], ["o"])
+    p = d / "kmer.table.mem_map"
+    raw = bytearray(p.read_bytes())
+    p.write_bytes(raw[:-1])  # size mismatch
+    assert L.kgx_image_open(str(d).encode(), 0, ctypes.byref(h)) == -3
+    raw2 = bytearray(raw)
+    raw2[16] = 2  # version 2
+    p.write_bytes(raw2)
+    assert L.kgx_image_open(str(d).encode(), 0, ctypes.byref(h)) == -3
+    p.write_bytes(raw)
+    assert L.kgx_image_open(str(d).encode(), 0, ctypes.byref(h)) == 0
+    L.kgx_image_close(h)
+
+
+def test_device_synthetic_image_equals_host_build(gpu, oracle_lib):
+    spec = synth.ImageSpec(40000)
+    img, stored = gpu.Image.synthetic(spec.n_keys, spec.num_sigs)
+    with img:
+        dev = img.download()
+    k, f, o, a, w = spec.unique_entries()
+    assert stored == len(k)
+    host = oracle_lib.build_table(spec.num_sigs, k, f, o, a, w)
+    # same multiset of buckets (placement may differ: parallel insertion)
+    occ_d = dev[dev["which_kmer"] <= 20 ** 8]
+    occ_h = host[host["which_kmer"] <= 20 ** 8]
+    assert len(occ_d) == len(occ_h)
+    sd = np.sort(occ_d, order="which_kmer")
+    sh = np.sort(occ_h, order="which_kmer")
+    for fld in ["which_kmer", "otu_index", "avg_from_end", "pad", "function_index"]:
+        assert np.array_equal(sd[fld], sh[fld]), fld
+    assert np.array_equal(sd["function_wt"].view(np.uint32), sh["function_wt"].view(np.uint32))
+    # empty buckets are zeroed like the reference writer's memset
+    emp = dev[dev["which_kmer"] > 20 ** 8]
+    assert (emp["which_kmer"] == 20 ** 8 + 1).all() and (emp["function_index"] == 0).all()
+    # lookups agree: the oracle over the device-built table == over the host table
+    res, off = synth.make_queries(spec, 300, x_permille=3)
+    a1 = oracle_lib.process_batch(dev, res, off)
+    a2 = oracle_lib.process_batch(host, res, off)
+    assert eq_fields(a1.hits, a2.hits)
+    assert eq_fields(a1.calls, a2.calls, list(a1.calls.dtype.names))
+
+
+def _dev_alloc(gpu, nbytes):
+    p = ctypes.c_void_p()
+    gpu.check(gpu.lib().kgx_device_alloc(0, nbytes, ctypes.byref(p)), "alloc")
+    return p.value
+
+
+def test_device_queries_and_run_device(gpu, oracle_lib):
+    spec, table = synthetic_table(30000)
+    n, L = 500, 300
+    L_ = gpu.lib()
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        d_res = _dev_alloc(gpu, n * L)
+        d_off = _dev_alloc(gpu, (n + 1) * 8)
+        try:
+            gpu.check(L_.kgx_synth_queries(ctx.handle, spec.n_keys, n, L, 4, 17, d_res, d_off), "synth")
+            ctx.synchronize()
+            res = np.empty(n * L, np.uint8)
+            off = np.empty(n + 1, np.uint64)
+            gpu.check(L_.kgx_memcpy_d2h(res.ctypes.data, d_res, res.nbytes), "d2h")
+            gpu.check(L_.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
+            hres, hoff = synth.make_queries(spec, n, x_permille=4, q0=17)
+            assert np.array_equal(res, hres) and np.array_equal(off, hoff)
+            out = gpu.DeviceResult()
+            p = gpu.Params(5, 200, 0, 0)
+            gpu.check(L_.kgx_run_device(ctx.handle, ctypes.byref(p), d_res, d_off, n, n * L, 7,
+                                        ctypes.byref(out)), "run_device")
+            ctx.synchronize()
+            wb = np.empty(n + 1, np.uint64)
+            hc = np.empty(n, np.uint32)
+            cc = np.empty(n, np.uint32)
+            for arr, ptr in ((wb, out.window_base), (hc, out.hit_count), (cc, out.call_count)):
+                gpu.check(L_.kgx_memcpy_d2h(arr.ctypes.data, ptr, arr.nbytes), "d2h")
+            hits = np.empty(int(wb[-1]), gpu.HIT_DTYPE)
+            calls = np.empty(int(wb[-1]), gpu.CALL_DTYPE)
+            gpu.check(L_.kgx_memcpy_d2h(hits.ctypes.data, out.hits, hits.nbytes), "d2h")
+            gpu.check(L_.kgx_memcpy_d2h(calls.ctypes.data, out.calls, calls.nbytes), "d2h")
+            want = oracle_lib.process_batch(table, hres, hoff)
+            assert np.array_equal(np.diff(want.hit_offsets), hc)
+            assert np.array_equal(np.diff(want.call_offsets), cc)
+            gh = np.concatenate([hits[wb[s]:wb[s] + hc[s]] for s in range(n)])
+            gc = np.concatenate([calls[wb[s]:wb[s] + cc[s]] for s in range(n)])
+            assert eq_fields(gh, want.hits)
+            assert eq_fields(gc, want.calls, list(want.calls.dtype.names))
+        finally:
+            L_.kgx_device_free(d_res)
+            L_.kgx_device_free(d_off)

@@ -1,0 +1,40 @@
+"""The oracle reproduces the committed golden handler text (regression of the
+checker itself; tests/golden/make_golden.py wrote these files)."""
+import os
+
+import pytest
+
+from helpers import GOLDEN
+
+
+def _cases():
+    for ds in ("scoring", "edge", "cap"):
+        d = os.path.join(GOLDEN, ds)
+        for f in sorted(os.listdir(d)):
+            if f.startswith("expected_") and f.endswith(".txt"):
+                yield ds, f
+
+
+PARAMS = {
+    "default": {}, "min_hits3": {"min_hits": "3"}, "max_gap300": {"max_gap": "300"},
+    "max_gap50": {"max_gap": "50"}, "order": {"order_constraint": "1"},
+    "min_weighted20": {"min_weighted_hits": "20"}, "min_hits2": {"min_hits": "2"},
+    "bad_int": {"min_hits": "abc", "max_gap": " 120xyz"},
+}
+
+
+def parse_case(fname):
+    stem = fname[len("expected_"):-len(".txt")]
+    for mode in ("query_details", "query_best", "query", "add"):
+        if stem.startswith(mode + "_"):
+            return mode, stem[len(mode) + 1:]
+    raise ValueError(fname)
+
+
+@pytest.mark.parametrize("ds,fname", list(_cases()))
+def test_oracle_matches_golden(oracle_lib, ds, fname):
+    mode, pname = parse_case(fname)
+    d = os.path.join(GOLDEN, ds)
+    got = oracle_lib.query_text(os.path.join(d, "data"), os.path.join(d, "input.fasta"), mode,
+                                PARAMS[pname])
+    assert got == open(os.path.join(d, fname), "rb").read()
