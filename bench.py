@@ -1,0 +1,281 @@
+"""Benchmark of the hot path: protein residues/s against a 1B-entry k-mer image.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-keys 1e9] [--n-seq 100000]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1], SURVEY §8(d) "C2"): per GPU, 100,000
+synthetic 300-aa proteins (half planted copies of image proteins with 10%
+substitutions, half uniform) against a synthetic 1,000,000,000-entry signature
+image in the reference's 24-byte bucket format (num_sigs 3,559,786,523 by the
+builder's sizing rule, 85.4 GB), built directly in HBM.  Every rank holds an
+image replica and its own query shard (weak scaling; no collective on the data
+path -- torch.distributed is used for the barrier and the max-time reduction).
+
+A step = one pass over the rank's resident batch: plan -> probe -> score
+(kgx_run_device), inputs and outputs in HBM.  The probe kernel is timed with
+HIP events on the stream it runs on; the roofline uses SURVEY §8(d)'s
+algorithmic bytes per window, (24 * P + 1), with P the mean buckets examined
+per probed window measured by the CPU oracle on the rank-0 sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
+METRIC = "protein residues/s vs 1B-entry kmer image; 1/2/4/8 MI355X"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Dist:
+    """torch.distributed (gloo, CPU tensors) for the barrier and max-reduce."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille):
+    """The oracle (bit-exact CPU restatement) over a bounded sample of rank 0's
+    batch, on this host's cores, against a host copy of the same image."""
+    import oracle
+    oracle.build(ref=False)
+    t0 = time.time()
+    table = img.download()
+    log(f"[bench] image copied to host in {time.time() - t0:.1f}s ({table.nbytes / 1e9:.1f} GB)")
+    res, off = spec_queries(spec, n_seq_sample, length, x_permille)
+    r = oracle.process_batch(table, res, off, want=7, n_threads=threads)
+    one = max(1, n_seq_sample // 16)
+    r1 = oracle.process_batch(table, res[: int(off[one])], off[: one + 1], want=7, n_threads=1)
+    del table
+    return {
+        "value": float(len(res) / r.seconds),
+        "unit": "residues/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"first {n_seq_sample} x {length}-aa queries of rank 0's batch, same image "
+                  f"(host copy), hits+calls+OTU, {threads} threads; {r.seconds:.2f} s",
+        "single_thread_value": float(int(off[one]) / r1.seconds),
+        "pbar": r.probes / max(1, r.windows),
+        "windows": int(r.windows),
+    }
+
+
+def spec_queries(spec, n, length, x_permille):
+    from close_kmers_amd import synth
+    return synth.make_queries(spec, n, length=length, x_permille=x_permille, q0=0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-keys", type=float, default=1e9)
+    ap.add_argument("--num-sigs", type=int, default=0, help="0 = builder sizing rule")
+    ap.add_argument("--n-seq", type=int, default=100000, help="sequences per GPU")
+    ap.add_argument("--length", type=int, default=300)
+    ap.add_argument("--x-permille", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=100000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
+    args = ap.parse_args()
+
+    from close_kmers_amd import abi, synth
+
+    d = Dist()
+    n_keys = int(args.n_keys)
+    spec = synth.ImageSpec(n_keys, args.num_sigs or None)
+    dev = d.local_rank
+    L = abi.lib()
+    if abi.device_count() <= dev:
+        raise SystemExit(f"rank {d.rank}: no gfx950 device {dev}")
+
+    t0 = time.time()
+    img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs, device=dev)
+    log(f"[bench] rank {d.rank}: built {stored} keys in {spec.num_sigs} buckets "
+        f"({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
+    ctx = abi.Context(img)
+    n, Ls = args.n_seq, args.length
+    n_res = n * Ls
+    d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+    abi.check(L.kgx_device_alloc(dev, n_res, ctypes.byref(d_res)), "alloc residues")
+    abi.check(L.kgx_device_alloc(dev, (n + 1) * 8, ctypes.byref(d_off)), "alloc offsets")
+    q0 = d.rank * n  # weak scaling: each rank its own shard of queries
+    abi.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, args.x_permille, q0, d_res, d_off),
+              "synth queries")
+    ctx.synchronize()
+
+    params = abi.default_params()
+    want = abi.WANT_HITS | abi.WANT_CALLS | abi.WANT_OTU
+    ev = [ctypes.c_void_p() for _ in range(4)]
+    for e in ev:
+        abi.check(L.kgx_event_create(ctypes.byref(e)), "event")
+
+    def step(timed_probe: list | None):
+        abi.check(L.kgx_stage_plan(ctx.handle, d_off, n, n_res), "plan")
+        if timed_probe is not None:
+            abi.check(L.kgx_event_record(ev[0], ctx.handle), "event")
+        abi.check(L.kgx_stage_probe(ctx.handle, d_res, d_off), "probe")
+        if timed_probe is not None:
+            abi.check(L.kgx_event_record(ev[1], ctx.handle), "event")
+        abi.check(L.kgx_stage_score(ctx.handle, ctypes.byref(params), want), "score")
+        if timed_probe is not None:
+            ms = ctypes.c_float()
+            abi.check(L.kgx_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)), "elapsed")
+            timed_probe.append(ms.value)
+
+    for _ in range(args.warmup):
+        step(None)
+    ctx.synchronize()
+
+    # probe-kernel duration (HIP events on the context's stream), untimed pass
+    probe_ms: list = []
+    for _ in range(max(3, min(args.steps, 10))):
+        step(probe_ms)
+    ctx.synchronize()
+
+    d.barrier()
+    ctx.synchronize()
+    t_start = time.perf_counter()
+    abi.check(L.kgx_event_record(ev[2], ctx.handle), "event")
+    for _ in range(args.steps):
+        step(None)
+    abi.check(L.kgx_event_record(ev[3], ctx.handle), "event")
+    ctx.synchronize()
+    d.barrier()
+    t_wall = time.perf_counter() - t_start
+    ev_ms = ctypes.c_float()
+    abi.check(L.kgx_event_elapsed_ms(ev[2], ev[3], ctypes.byref(ev_ms)), "elapsed")
+    t_max = d.max(t_wall)
+
+    # sanity: counts of the last step
+    out = abi.DeviceResult()
+    abi.check(L.kgx_device_result_get(ctx.handle, ctypes.byref(out)), "result")
+    hc = np.empty(n, np.uint32)
+    cc = np.empty(n, np.uint32)
+    abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
+    abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
+    total_hits = int(d.sum(float(hc.sum())))
+    log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
+        f"(planted mean {hc[::2].mean():.1f}, random mean {hc[1::2].mean():.2f}); "
+        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step, events {ev_ms.value / args.steps:.3f} ms/step, "
+        f"probe {np.mean(probe_ms):.3f} ms")
+
+    cpu = None
+    if d.rank == 0 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(abi, img, spec, min(args.cpu_sample, n), Ls, threads, args.x_permille)
+        log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads, "
+            f"P = {cpu['pbar']:.4f}")
+
+    for e in ev:
+        L.kgx_event_destroy(e)
+    L.kgx_device_free(d_res)
+    L.kgx_device_free(d_off)
+    ctx.close()
+    img.close()
+
+    if d.rank == 0:
+        windows_per_launch = n * max(0, Ls - 8)  # x_permille = 0: every window is probed
+        pbar = cpu["pbar"] if cpu else None
+        probe_s = float(np.mean(probe_ms)) / 1e3
+        if pbar is None:
+            # alpha = stored / num_sigs; linear probing, unsuccessful search
+            a = stored / spec.num_sigs
+            pbar = 0.5 * (1 + 1 / (1 - a) ** 2)
+        alg_bytes = windows_per_launch * (24.0 * pbar + 1.0)
+        achieved = alg_bytes / probe_s
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("n_keys") == n_keys and tj.get("n_seq") == n and tj.get("length") == Ls:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        value = d.world * n_res * args.steps / t_max
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "residues/s",
+            "n_gpus": d.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C2: {n} x {Ls}-aa synthetic proteins per GPU vs {n_keys:,}-entry "
+                            f"signature image ({spec.num_sigs:,} buckets, "
+                            f"{spec.num_sigs * 24 / 1e9:.1f} GB) resident in HBM",
+                "n_seq_per_gpu": n, "seq_len": Ls, "n_keys": n_keys, "keys_stored": stored,
+                "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
+                "hits_total": total_hits,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved / 1e9,
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK,
+                "traffic": traffic,
+                "kernel": "probe_kernel",
+                "kernel_ms": probe_s * 1e3,
+                "alg_bytes_per_launch": alg_bytes,
+                "pbar": pbar,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

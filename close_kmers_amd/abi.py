@@ -91,6 +91,10 @@ SIGNATURES = {
     "kgx_find_best_call": (_INT, [_P, _SZ, ctypes.POINTER(_CS), _INT, ctypes.POINTER(_I32), _P, _SZ,
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_INT)]),
+    "kgx_event_create": (_INT, [_PP]),
+    "kgx_event_destroy": (_INT, [_P]),
+    "kgx_event_record": (_INT, [_P, _P]),
+    "kgx_event_elapsed_ms": (_INT, [_P, _P, ctypes.POINTER(ctypes.c_float)]),
     "kgx_device_alloc": (_INT, [_INT, _U64, _PP]),
     "kgx_device_free": (_INT, [_P]),
     "kgx_memcpy_h2d": (_INT, [_P, _P, _U64]),

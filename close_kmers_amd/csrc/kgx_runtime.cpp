@@ -666,6 +666,40 @@ int kgx_synth_queries(kgx_ctx *c, uint64_t image_n_keys, uint32_t n_seq, uint32_
     return KGX_OK;
 }
 
+int kgx_event_create(void **event)
+{
+    if (!event)
+        return fail(KGX_EINVAL, "null event");
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    *event = (void *)e;
+    return KGX_OK;
+}
+
+int kgx_event_destroy(void *event)
+{
+    if (event)
+        HIP_TRY(hipEventDestroy((hipEvent_t)event));
+    return KGX_OK;
+}
+
+int kgx_event_record(void *event, kgx_ctx *c)
+{
+    if (!event || !c)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipEventRecord((hipEvent_t)event, c->stream));
+    return KGX_OK;
+}
+
+int kgx_event_elapsed_ms(void *start, void *end, float *ms)
+{
+    if (!start || !end || !ms)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipEventSynchronize((hipEvent_t)end));
+    HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
+    return KGX_OK;
+}
+
 int kgx_device_alloc(int device, uint64_t nbytes, void **out)
 {
     if (!out)

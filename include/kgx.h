@@ -111,7 +111,8 @@ typedef struct kgx_result {
     const kgx_call *calls;
     const uint64_t *otu_offsets; /* n_seq + 1 */
     const kgx_otu *otus;
-    uint64_t n_windows; /* 8-mer windows probed */
+    uint64_t n_windows; /* window positions, sum of max(0, len-8); those holding a
+                           non-standard residue are skipped, not probed */
 } kgx_result;
 
 /* Device-resident results of kgx_run_device (pointers into HBM).  Hits and
@@ -210,6 +211,14 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
                        int n_names, int32_t *function_index, char *function, size_t function_cap,
                        float *score, float *weighted_score, float *score_offset,
                        int *score_offset_set);
+
+/* ---- HIP-event timing on a context's stream ----------------------------- */
+int kgx_event_create(void **event);
+int kgx_event_destroy(void *event);
+/* record on the stream `ctx` launches on */
+int kgx_event_record(void *event, kgx_ctx *ctx);
+/* milliseconds between two recorded events (waits for `end`) */
+int kgx_event_elapsed_ms(void *start, void *end, float *ms);
 
 /* Device memory helpers for callers without their own allocator. */
 int kgx_device_alloc(int device, uint64_t nbytes, void **out);
