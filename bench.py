@@ -77,29 +77,36 @@ class Dist:
             self.pg.destroy_process_group()
 
 
-def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille):
+def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, target_s):
     """The oracle (bit-exact CPU restatement) over a bounded sample of rank 0's
-    batch, on this host's cores, against a host copy of the same image."""
+    batch, on this host's cores, against a host copy of the same image.  The
+    sample is processed repeatedly until about target_s seconds of timed work
+    (the 85 GB table does not fit any CPU cache, so repeats still miss)."""
     import oracle
     oracle.build(ref=False)
     t0 = time.time()
     table = img.download()
     log(f"[bench] image copied to host in {time.time() - t0:.1f}s ({table.nbytes / 1e9:.1f} GB)")
     res, off = spec_queries(spec, n_seq_sample, length, x_permille)
-    r = oracle.process_batch(table, res, off, want=7, n_threads=threads)
-    one = max(1, n_seq_sample // 16)
-    r1 = oracle.process_batch(table, res[: int(off[one])], off[: one + 1], want=7, n_threads=1)
+    secs, passes, probes, windows = 0.0, 0, 0, 0
+    while secs < target_s and passes < 200:
+        r = oracle.process_batch(table, res, off, want=7, n_threads=threads)
+        secs += r.seconds
+        passes += 1
+        probes, windows = r.probes, r.windows
+    r1 = oracle.process_batch(table, res, off, want=7, n_threads=1)
     del table
     return {
-        "value": float(len(res) / r.seconds),
+        "value": float(passes * len(res) / secs),
         "unit": "residues/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"first {n_seq_sample} x {length}-aa queries of rank 0's batch, same image "
-                  f"(host copy), hits+calls+OTU, {threads} threads; {r.seconds:.2f} s",
-        "single_thread_value": float(int(off[one]) / r1.seconds),
-        "pbar": r.probes / max(1, r.windows),
-        "windows": int(r.windows),
+        "sample": f"{passes} passes over the first {n_seq_sample} x {length}-aa queries of rank 0's "
+                  f"batch against a host copy of the same image (hits+calls+OTU), {threads} threads, "
+                  f"{secs:.1f} s timed",
+        "single_thread_value": float(len(res) / r1.seconds),
+        "pbar": probes / max(1, windows),
+        "windows": int(windows),
     }
 
 
@@ -120,7 +127,10 @@ def main():
     ap.add_argument("--x-permille", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=100000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-microbench", action="store_true")
+    ap.add_argument("--ab-probe", type=int, default=0, help="rounds of interleaved probe A/B")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 
@@ -178,6 +188,20 @@ def main():
         step(probe_ms)
     ctx.synchronize()
 
+    probe_ab = None
+    if args.ab_probe:
+        # interleaved A/B of the probe variants in this process (rule: one
+        # process, alternating rounds, report the distribution)
+        times = {0: [], 1: []}
+        for _ in range(args.ab_probe):
+            for v in (0, 1):
+                ctx.set_option("probe_variant", v)
+                step(times[v])
+        ctx.set_option("probe_variant", 1)
+        probe_ab = {f"variant{v}": {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
+                    for v, t in times.items()}
+        log(f"[bench] probe A/B: {probe_ab}")
+
     d.barrier()
     ctx.synchronize()
     t_start = time.perf_counter()
@@ -205,10 +229,27 @@ def main():
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step, events {ev_ms.value / args.steps:.3f} ms/step, "
         f"probe {np.mean(probe_ms):.3f} ms")
 
+    ceiling = None
+    if d.rank == 0 and not args.no_microbench:
+        ceiling = {}
+        n_reads = int(n * max(0, Ls - 8) * 1.4)
+        for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64)):
+            ms, reads = ctypes.c_float(), ctypes.c_uint64()
+            abi.check(L.kgx_microbench_random_read(ctx.handle, n_reads, mode, ctypes.byref(ms),
+                                                   ctypes.byref(reads)), "microbench")  # warm
+            abi.check(L.kgx_microbench_random_read(ctx.handle, n_reads, mode, ctypes.byref(ms),
+                                                   ctypes.byref(reads)), "microbench")
+            rate = reads.value / (ms.value / 1e3)
+            ceiling[name] = {"reads_per_s": rate, "useful_GBps": rate * useful / 1e9,
+                             "ms": ms.value, "reads": reads.value}
+            log(f"[bench] random-read {name}: {rate / 1e9:.2f} G reads/s = "
+                f"{rate * useful / 1e9:.0f} GB/s useful")
+
     cpu = None
     if d.rank == 0 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline(abi, img, spec, min(args.cpu_sample, n), Ls, threads, args.x_permille)
+        cpu = cpu_baseline(abi, img, spec, min(args.cpu_sample, n), Ls, threads, args.x_permille,
+                           args.cpu_seconds)
         log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads, "
             f"P = {cpu['pbar']:.4f}")
 
@@ -270,6 +311,10 @@ def main():
                 "kernel_ms": probe_s * 1e3,
                 "alg_bytes_per_launch": alg_bytes,
                 "pbar": pbar,
+                "random_read_ceiling": ceiling,
+                "probe_ab": probe_ab,
+                "frac_of_random_bucket_ceiling": (achieved / 1e9 / ceiling["bucket24"]["useful_GBps"]
+                                                  if ceiling else None),
             },
             "cpu_baseline": cpu,
         }

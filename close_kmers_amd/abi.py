@@ -80,6 +80,7 @@ SIGNATURES = {
     "kgx_ctx_destroy": (_INT, [_P]),
     "kgx_ctx_stream": (_P, [_P]),
     "kgx_ctx_set_stream": (_INT, [_P, _P]),
+    "kgx_ctx_set_option": (_INT, [_P, _CS, ctypes.c_int64]),
     "kgx_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
     "kgx_run_device": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U64, _U32,
                               ctypes.POINTER(DeviceResult)]),
@@ -91,6 +92,8 @@ SIGNATURES = {
     "kgx_find_best_call": (_INT, [_P, _SZ, ctypes.POINTER(_CS), _INT, ctypes.POINTER(_I32), _P, _SZ,
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_INT)]),
+    "kgx_microbench_random_read": (_INT, [_P, _U64, _INT, ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(_U64)]),
     "kgx_event_create": (_INT, [_PP]),
     "kgx_event_destroy": (_INT, [_P]),
     "kgx_event_record": (_INT, [_P, _P]),
@@ -257,6 +260,9 @@ class Context:
 
     def set_stream(self, stream: int | None) -> None:
         check(lib().kgx_ctx_set_stream(self.handle, stream), "kgx_ctx_set_stream")
+
+    def set_option(self, name: str, value: int) -> None:
+        check(lib().kgx_ctx_set_option(self.handle, name.encode(), value), f"set_option({name})")
 
     def synchronize(self) -> None:
         check(lib().kgx_ctx_synchronize(self.handle), "kgx_ctx_synchronize")

@@ -84,68 +84,131 @@ __device__ __forceinline__ void wave_lds_sync()
 
 __device__ __forceinline__ uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 
-/* One workgroup: wbase / cbase = exclusive scans of windows and chunks per
- * sequence.  Windows of a sequence of length L are positions 0 .. L-9
- * (kguts.cc:792,798: the last full window is never probed). */
-__global__ __launch_bounds__(1024) void plan_scan_kernel(const uint64_t *__restrict__ seq_off,
-                                                         uint32_t n, uint64_t *__restrict__ wbase,
-                                                         uint64_t *__restrict__ cbase)
+/*
+ * wbase / cbase = exclusive scans of windows and chunks per sequence, in two
+ * launches: plan_reduce sums each 1024-sequence tile, plan_scan adds the sums
+ * of the tiles before it, scans inside the tile and fills chunk -> sequence.
+ * Windows of a sequence of length L are positions 0 .. L-9 (kguts.cc:792,798:
+ * the last full window is never probed).
+ */
+constexpr uint32_t PLAN_PER = 4;                  /* sequences per thread */
+constexpr uint32_t PLAN_TILE = 256 * PLAN_PER;    /* sequences per workgroup */
+
+struct WinChunk {
+    uint64_t w, c;
+};
+
+__device__ __forceinline__ WinChunk thread_sums(const uint64_t *seq_off, uint32_t n, uint32_t s0)
 {
-    __shared__ uint64_t sw[1024];
-    __shared__ uint64_t sc[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (n + 1023u) / 1024u;
-    const uint32_t lo = min(n, t * per), hi = min(n, lo + per);
-    uint64_t aw = 0, ac = 0;
-    for (uint32_t s = lo; s < hi; s++) {
-        uint64_t nw = windows_of(seq_off[s + 1] - seq_off[s]);
-        aw += nw;
-        ac += (nw + CHUNK - 1) / CHUNK;
+    WinChunk a = {0, 0};
+    for (uint32_t k = 0; k < PLAN_PER; k++) {
+        const uint32_t s = s0 + k;
+        if (s < n) {
+            const uint64_t nw = windows_of(seq_off[s + 1] - seq_off[s]);
+            a.w += nw;
+            a.c += (nw + CHUNK - 1) / CHUNK;
+        }
     }
-    sw[t] = aw;
-    sc[t] = ac;
+    return a;
+}
+
+/* inclusive scan of one u64 pair over a 256-thread block */
+__device__ __forceinline__ WinChunk block_scan(WinChunk v, WinChunk *lds4, WinChunk &total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint64_t w = __shfl_up(v.w, off), c = __shfl_up(v.c, off);
+        if (lane >= off) {
+            v.w += w;
+            v.c += c;
+        }
+    }
+    if (lane == 63)
+        lds4[wave] = v;
     __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        uint64_t vw = t >= off ? sw[t - off] : 0;
-        uint64_t vc = t >= off ? sc[t - off] : 0;
-        __syncthreads();
-        sw[t] += vw;
-        sc[t] += vc;
-        __syncthreads();
+    WinChunk pre = {0, 0};
+    total = {0, 0};
+    for (uint32_t i = 0; i < 4; i++) {
+        if (i < wave) {
+            pre.w += lds4[i].w;
+            pre.c += lds4[i].c;
+        }
+        total.w += lds4[i].w;
+        total.c += lds4[i].c;
     }
-    uint64_t bw = sw[t] - aw, bc = sc[t] - ac;
-    for (uint32_t s = lo; s < hi; s++) {
-        uint64_t nw = windows_of(seq_off[s + 1] - seq_off[s]);
+    v.w += pre.w;
+    v.c += pre.c;
+    return v;
+}
+
+__global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__restrict__ seq_off,
+                                                          uint32_t n, WinChunk *__restrict__ tile_sums)
+{
+    __shared__ WinChunk lds4[4];
+    const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
+    WinChunk total;
+    block_scan(thread_sums(seq_off, n, s0), lds4, total);
+    if (threadIdx.x == 0)
+        tile_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restrict__ seq_off,
+                                                        uint32_t n,
+                                                        const WinChunk *__restrict__ tile_sums,
+                                                        uint64_t *__restrict__ wbase,
+                                                        uint64_t *__restrict__ cbase,
+                                                        uint32_t *__restrict__ chunk_seq)
+{
+    __shared__ WinChunk lds4[4];
+    __shared__ WinChunk lds_pre[4];
+    /* sum of all earlier tiles */
+    WinChunk p = {0, 0};
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 256) {
+        p.w += tile_sums[b].w;
+        p.c += tile_sums[b].c;
+    }
+    WinChunk ptot;
+    block_scan(p, lds_pre, ptot);
+    const WinChunk before = ptot;
+    __syncthreads();
+
+    const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
+    const WinChunk mine = thread_sums(seq_off, n, s0);
+    WinChunk tot;
+    const WinChunk incl = block_scan(mine, lds4, tot);
+    uint64_t bw = before.w + incl.w - mine.w, bc = before.c + incl.c - mine.c;
+    for (uint32_t k = 0; k < PLAN_PER; k++) {
+        const uint32_t s = s0 + k;
+        if (s >= n)
+            break;
+        const uint64_t nw = windows_of(seq_off[s + 1] - seq_off[s]);
+        const uint64_t nc = (nw + CHUNK - 1) / CHUNK;
         wbase[s] = bw;
         cbase[s] = bc;
+        for (uint64_t c = 0; c < nc; c++)
+            chunk_seq[bc + c] = s;
         bw += nw;
-        bc += (nw + CHUNK - 1) / CHUNK;
+        bc += nc;
     }
-    if (t == 1023) {
-        wbase[n] = sw[1023];
-        cbase[n] = sc[1023];
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) {
+        wbase[n] = before.w + tot.w;
+        cbase[n] = before.c + tot.c;
     }
 }
 
-__global__ void plan_fill_kernel(const uint64_t *__restrict__ cbase, uint32_t n,
-                                 uint32_t *__restrict__ chunk_seq)
+size_t plan_workspace_bytes(uint32_t n_seq)
 {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n)
-        return;
-    for (uint64_t c = cbase[s]; c < cbase[s + 1]; c++)
-        chunk_seq[c] = s;
+    return ((size_t)n_seq / PLAN_TILE + 1) * sizeof(WinChunk);
 }
 
 hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase, uint64_t *cbase,
-                       uint32_t *chunk_seq, uint64_t max_chunks, hipStream_t stream)
+                       uint32_t *chunk_seq, void *workspace, hipStream_t stream)
 {
-    (void)max_chunks;
-    hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, seq_off, n_seq, wbase,
-                       cbase);
-    if (n_seq)
-        hipLaunchKernelGGL(plan_fill_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream,
-                           cbase, n_seq, chunk_seq);
+    const uint32_t tiles = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
+    hipLaunchKernelGGL(plan_reduce_kernel, dim3(tiles), dim3(256), 0, stream, seq_off, n_seq,
+                       static_cast<WinChunk *>(workspace));
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(tiles), dim3(256), 0, stream, seq_off, n_seq,
+                       static_cast<const WinChunk *>(workspace), wbase, cbase, chunk_seq);
     return hipGetLastError();
 }
 
@@ -172,10 +235,15 @@ __device__ __forceinline__ uint32_t load_dword_clamped(uintptr_t a, uintptr_t lo
  * One wave = one chunk: windows [w0, w1) of sequence s.  Lane l owns windows
  * w0 + l + 64 j (j < PROBE_J), so each j-slice is 64 consecutive windows and a
  * ballot over a slice is in position order.  All PROBE_J first probes of a
- * lane are issued before any is resolved; every probe round loads the 8-byte
- * key and the 16-byte payload of its bucket together (one dependent HBM round
- * trip per bucket, the payload usually shares the key's 64-byte sector).
+ * lane are issued before any is resolved.
+ *   KEY_FIRST = false: every probe round loads the 8-byte key and the 16-byte
+ *     payload of its bucket together (two loads per bucket examined);
+ *   KEY_FIRST = true: a round loads only keys; a matching bucket's payload is
+ *     loaded in the round that finds it, overlapping the other chains (one
+ *     load per bucket + one per hit; the payload mostly shares the key's
+ *     sector, still in L2).
  */
+template <bool KEY_FIRST>
 __global__ __launch_bounds__(256) void probe_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ cbase,
@@ -237,7 +305,8 @@ __global__ __launch_bounds__(256) void probe_kernel(
         if (ok) {
             const kgx_sig_kmer *e = tab + slot[j];
             kv[j] = e->which_kmer;
-            pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+            if (!KEY_FIRST)
+                pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
         }
     }
 
@@ -251,13 +320,17 @@ __global__ __launch_bounds__(256) void probe_kernel(
                 if (kv[j] == key[j]) {
                     hit[j] = true;
                     pend[j] = false;
+                    if (KEY_FIRST)
+                        pv[j] = *reinterpret_cast<const uint4 *>(
+                            reinterpret_cast<const char *>(tab + slot[j]) + 8);
                 } else if (kv[j] > MAX_ENCODED || round + 1 >= num_sigs) {
                     pend[j] = false;
                 } else {
                     slot[j] = (slot[j] + 1 == num_sigs) ? 0 : slot[j] + 1;
                     const kgx_sig_kmer *e = tab + slot[j];
                     kv[j] = e->which_kmer;
-                    pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                    if (!KEY_FIRST)
+                        pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
                     more = true;
                 }
             }
@@ -286,14 +359,20 @@ __global__ __launch_bounds__(256) void probe_kernel(
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint64_t *cbase, const uint32_t *chunk_seq,
                         uint32_t n_seq, uint64_t max_chunks, const kgx_sig_kmer *table,
-                        uint64_t num_sigs, kgx_hit *hits, uint32_t *chunk_hits, hipStream_t stream)
+                        uint64_t num_sigs, kgx_hit *hits, uint32_t *chunk_hits, int variant,
+                        hipStream_t stream)
 {
     if (max_chunks == 0)
         return hipSuccess;
     const uint64_t blocks = (max_chunks + PROBE_WAVES - 1) / PROBE_WAVES;
-    hipLaunchKernelGGL(probe_kernel, dim3((uint32_t)blocks), dim3(64 * PROBE_WAVES), 0, stream,
-                       residues, n_residues, seq_off, wbase, cbase, chunk_seq, n_seq, table,
-                       num_sigs, mod_magic(num_sigs), hits, chunk_hits);
+    if (variant == PROBE_KEY_FIRST)
+        hipLaunchKernelGGL(probe_kernel<true>, dim3((uint32_t)blocks), dim3(64 * PROBE_WAVES), 0,
+                           stream, residues, n_residues, seq_off, wbase, cbase, chunk_seq, n_seq,
+                           table, num_sigs, mod_magic(num_sigs), hits, chunk_hits);
+    else
+        hipLaunchKernelGGL(probe_kernel<false>, dim3((uint32_t)blocks), dim3(64 * PROBE_WAVES), 0,
+                           stream, residues, n_residues, seq_off, wbase, cbase, chunk_seq, n_seq,
+                           table, num_sigs, mod_magic(num_sigs), hits, chunk_hits);
     return hipGetLastError();
 }
 
@@ -313,8 +392,10 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
  *   first/last position of buffer[0] / of the last buffered hit with fI == cur
  *   p1, p2    the last two buffered hits (gap rule, order constraint,
  *             pair switch and carry-over read only these)
- * Buffered hits are flagged KGX_HIT_IN_RUN; an emitted call's OTU tally
- * (kguts.cc:760-768) flags the buffered hits with fI == cur KGX_HIT_OTU.
+ * Buffered hits are flagged KGX_HIT_IN_RUN, and KGX_HIT_COUNTED when their
+ * function is their run's current_fI.  An emitted call records its run's hit
+ * range; one forward pass then flags the COUNTED hits inside emitted ranges
+ * KGX_HIT_OTU -- the hits the reference tallies into otu_map (kguts.cc:760-768).
  */
 struct RunTail {
     uint32_t pos, fI, idx;
@@ -322,11 +403,15 @@ struct RunTail {
     uint32_t avg;
 };
 
+constexpr int SCORE_BATCH = 8;
+constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << 16, F_CNT = KGX_HIT_COUNTED << 16,
+                   F_OTU = KGX_HIT_OTU << 16;
+
 __global__ __launch_bounds__(256) void score_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ cbase,
     const uint32_t *__restrict__ chunk_hits, kgx_hit *__restrict__ hits, kgx_call *__restrict__ calls,
-    uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count, kgx_params prm,
-    uint32_t want)
+    uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
+    kgx_params prm, uint32_t want)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_seq)
@@ -379,14 +464,9 @@ __global__ __launch_bounds__(256) void score_kernel(
                 cl.weighted_hits = wsum;
                 calls[base + ncalls] = cl;
             }
+            if (want_otu)
+                ranges[base + ncalls] = make_uint2(run_start, last_idx);
             ncalls++;
-            if (want_otu) {
-                for (uint32_t i = run_start; i <= last_idx; i++) {
-                    const uint32_t d3 = hw[8 * i + 3];
-                    if (((d3 >> 16) & KGX_HIT_IN_RUN) && hw[8 * i + 4] == cur)
-                        hw[8 * i + 3] = d3 | (KGX_HIT_OTU << 16);
-                }
-            }
         }
         if (n >= 2 && p2.fI != cur && p2.fI == p1.fI) { /* carry the pair */
             cur = p1.fI;
@@ -398,69 +478,110 @@ __global__ __launch_bounds__(256) void score_kernel(
             wsum = wsum + p1.wt;
             last_pos = p1.pos;
             last_idx = p1.idx;
+            hw[8 * p2.idx + 3] = p2.avg | F_RUN | F_CNT;
+            hw[8 * p1.idx + 3] = p1.avg | F_RUN | F_CNT;
         } else {
             n = 0;
         }
     };
 
-    for (uint32_t i = 0; i < nh; i++) {
-        const uint4 r = *reinterpret_cast<const uint4 *>(hw + 8 * i + 3); /* avg|flags, fI, wt, pos */
-        const uint32_t avg = r.x & 0xFFFFu;
-        const uint32_t fI = r.y;
-        const float wt = __uint_as_float(r.z);
-        const uint32_t pos = r.w;
+    /* hits are read SCORE_BATCH at a time, all loads issued before any is
+     * consumed: the state machine is serial, its inputs are not */
+    for (uint32_t i0 = 0; i0 < nh; i0 += SCORE_BATCH) {
+        uint4 rb[SCORE_BATCH];
+#pragma unroll
+        for (int k = 0; k < SCORE_BATCH; k++)
+            if (i0 + k < nh) /* avg|flags, fI, wt, pos */
+                rb[k] = *reinterpret_cast<const uint4 *>(hw + 8 * (i0 + k) + 3);
+#pragma unroll
+        for (int k = 0; k < SCORE_BATCH; k++) {
+            const uint32_t i = i0 + k;
+            if (i >= nh)
+                break;
+            const uint32_t avg = rb[k].x & 0xFFFFu;
+            const uint32_t fI = rb[k].y;
+            const float wt = __uint_as_float(rb[k].z);
+            const uint32_t pos = rb[k].w;
 
-        /* gap rule (kguts.cc:821-831), unsigned arithmetic */
-        if (n > 0 && p1.pos + gap < pos) {
-            if (n >= prm.min_hits)
-                flush();
-            else
-                n = 0;
-        }
-        if (n == 0) {
-            cur = fI;
-            cnt = 0;
-            wsum = 0.0f;
-            run_start = i;
-            first_pos = pos;
-        }
-        bool accept = true;
-        if (prm.order_constraint && n > 0) { /* kguts.cc:838-842 */
-            const uint32_t d = (pos - p1.pos) - (uint32_t)((int)p1.avg - (int)avg);
-            accept = (fI == p1.fI) && d <= 20u;
-        }
-        if (accept) {
-            if (n < RUN_CAP) {
-                n++;
-                hw[8 * i + 3] = avg | (KGX_HIT_IN_RUN << 16);
-                if (fI == cur) {
-                    cnt++;
-                    wsum += wt;
-                    last_pos = pos;
-                    last_idx = i;
-                }
-                p2 = p1;
-                p1 = RunTail{pos, fI, i, wt, avg};
+            /* gap rule (kguts.cc:821-831), unsigned arithmetic */
+            if (n > 0 && p1.pos + gap < pos) {
+                if (n >= prm.min_hits)
+                    flush();
+                else
+                    n = 0;
             }
-            /* pair switch (kguts.cc:852-856) */
-            if (n > 1 && cur != fI && p2.fI == p1.fI)
-                flush();
+            if (n == 0) {
+                cur = fI;
+                cnt = 0;
+                wsum = 0.0f;
+                run_start = i;
+                first_pos = pos;
+            }
+            bool accept = true;
+            if (prm.order_constraint && n > 0) { /* kguts.cc:838-842 */
+                const uint32_t d = (pos - p1.pos) - (uint32_t)((int)p1.avg - (int)avg);
+                accept = (fI == p1.fI) && d <= 20u;
+            }
+            if (accept) {
+                if (n < RUN_CAP) {
+                    n++;
+                    const bool counted = fI == cur;
+                    hw[8 * i + 3] = avg | F_RUN | (counted ? F_CNT : 0u);
+                    if (counted) {
+                        cnt++;
+                        wsum += wt;
+                        last_pos = pos;
+                        last_idx = i;
+                    }
+                    p2 = p1;
+                    p1 = RunTail{pos, fI, i, wt, avg};
+                }
+                /* pair switch (kguts.cc:852-856) */
+                if (n > 1 && cur != fI && p2.fI == p1.fI)
+                    flush();
+            }
         }
     }
     if (n >= prm.min_hits) /* kguts.cc:873-876 */
         flush();
     call_count[s] = want_calls ? ncalls : 0;
+
+    /* OTU flags: COUNTED hits inside an emitted call's range (ranges are
+     * disjoint and in order) */
+    if (want_otu && ncalls > 0) {
+        uint32_t ci = 0;
+        uint2 rg = ranges[base];
+        const uint32_t end = ranges[base + ncalls - 1].y;
+        for (uint32_t i0 = rg.x; i0 <= end; i0 += SCORE_BATCH) {
+            uint32_t fb[SCORE_BATCH];
+#pragma unroll
+            for (int k = 0; k < SCORE_BATCH; k++)
+                if (i0 + k <= end)
+                    fb[k] = hw[8 * (i0 + k) + 3];
+#pragma unroll
+            for (int k = 0; k < SCORE_BATCH; k++) {
+                const uint32_t i = i0 + k;
+                if (i > end)
+                    break;
+                while (i > rg.y) /* i <= end keeps ci < ncalls */
+                    rg = ranges[base + ++ci];
+                if (i >= rg.x && (fb[k] & F_CNT))
+                    hw[8 * i + 3] = fb[k] | F_OTU;
+            }
+        }
+    }
 }
 
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *cbase,
-                        const uint32_t *chunk_hits, kgx_hit *hits, kgx_call *calls,
+                        const uint32_t *chunk_hits, kgx_hit *hits, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
                         uint32_t want, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     hipLaunchKernelGGL(score_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
-                       cbase, chunk_hits, hits, calls, hit_count, call_count, params, want);
+                       cbase, chunk_hits, hits, calls, static_cast<uint2 *>(ranges), hit_count,
+                       call_count, params, want);
     return hipGetLastError();
 }
 
@@ -504,6 +625,71 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint32_t *
         return hipSuccess;
     hipLaunchKernelGGL(gather_kernel, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                        hit_count, call_count, hits, calls, hoff, coff, hits_out, calls_out);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* random-read ceiling of the image buffer (roofline denominator)            */
+/* ------------------------------------------------------------------------ */
+
+/* Every lane reads RR_ILP independent uniformly random buckets per round:
+ * mode 0 the whole 24-byte bucket (8-byte key + 16-byte payload, as the probe
+ * does), mode 1 the 8-byte key only, mode 2 one aligned 64-byte sector. */
+constexpr int RR_ILP = 8;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void random_read_kernel(const kgx_sig_kmer *__restrict__ t,
+                                                          uint64_t n, uint64_t magic,
+                                                          uint32_t rounds, uint64_t *sink)
+{
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t acc = 0;
+    const char *base = reinterpret_cast<const char *>(t);
+    for (uint32_t r = 0; r < rounds; r++) {
+        uint64_t idx[RR_ILP];
+#pragma unroll
+        for (int k = 0; k < RR_ILP; k++)
+            idx[k] = mod_by(mix64(tid * 977u + (uint64_t)r * RR_ILP + k) & ((1ull << 35) - 1), n, magic);
+        uint64_t kv[RR_ILP];
+        uint4 pv[RR_ILP], pw[RR_ILP], px[RR_ILP];
+#pragma unroll
+        for (int k = 0; k < RR_ILP; k++) {
+            if (MODE == 0) {
+                kv[k] = t[idx[k]].which_kmer;
+                pv[k] = *reinterpret_cast<const uint4 *>(base + idx[k] * 24 + 8);
+            } else if (MODE == 1) {
+                kv[k] = t[idx[k]].which_kmer;
+            } else {
+                const uint4 *s = reinterpret_cast<const uint4 *>(base + ((idx[k] * 24) & ~63ull));
+                pv[k] = s[0];
+                pw[k] = s[1];
+                px[k] = s[2];
+                kv[k] = *reinterpret_cast<const uint64_t *>(s + 3);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < RR_ILP; k++) {
+            acc ^= kv[k];
+            if (MODE == 0)
+                acc += pv[k].x ^ pv[k].w;
+            if (MODE == 2)
+                acc += pv[k].x ^ pw[k].y ^ px[k].z;
+        }
+    }
+    sink[tid] = acc;
+}
+
+hipError_t launch_random_read(const kgx_sig_kmer *table, uint64_t num_sigs, uint64_t threads,
+                              uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream)
+{
+    const dim3 grid((uint32_t)(threads / 256)), block(256);
+    const uint64_t m = mod_magic(num_sigs);
+    if (mode == 0)
+        hipLaunchKernelGGL(random_read_kernel<0>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
+    else if (mode == 1)
+        hipLaunchKernelGGL(random_read_kernel<1>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
+    else
+        hipLaunchKernelGGL(random_read_kernel<2>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
     return hipGetLastError();
 }
 

@@ -91,12 +91,14 @@ struct kgx_ctx {
     bool own_stream = false;
     /* device scratch */
     DevBuf residues, offsets, wbase, cbase, chunk_seq, chunk_hits, hits, calls, hit_count,
-        call_count, dense_hoff, dense_coff, dense_hits, dense_calls;
+        call_count, dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
     /* current plan */
     uint32_t n_seq = 0;
     uint64_t n_residues = 0;
     uint64_t max_chunks = 0;
     const uint64_t *d_off = nullptr;
+    /* tuning options */
+    int probe_variant = PROBE_KEY_FIRST;
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
     std::vector<kgx_hit> h_hits;
@@ -403,7 +405,7 @@ int kgx_ctx_destroy(kgx_ctx *c)
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->residues, &c->offsets, &c->wbase, &c->cbase, &c->chunk_seq, &c->chunk_hits,
                       &c->hits, &c->calls, &c->hit_count, &c->call_count, &c->dense_hoff,
-                      &c->dense_coff, &c->dense_hits, &c->dense_calls})
+                      &c->dense_coff, &c->dense_hits, &c->dense_calls, &c->plan_ws, &c->ranges})
         b->release();
     if (c->own_stream)
         (void)hipStreamDestroy(c->stream);
@@ -427,6 +429,20 @@ int kgx_ctx_set_stream(kgx_ctx *c, void *stream)
         c->own_stream = true;
     }
     return KGX_OK;
+}
+
+int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
+{
+    if (!c || !name)
+        return fail(KGX_EINVAL, "null argument");
+    const std::string n = name;
+    if (n == "probe_variant") {
+        if (value != PROBE_BUCKET && value != PROBE_KEY_FIRST)
+            return fail(KGX_EINVAL, "probe_variant must be 0 or 1");
+        c->probe_variant = (int)value;
+        return KGX_OK;
+    }
+    return fail(KGX_EINVAL, "unknown option " + n);
 }
 
 int kgx_ctx_synchronize(kgx_ctx *c)
@@ -455,10 +471,12 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->chunk_hits.reserve(max_chunks * sizeof(uint32_t)));
     HIP_TRY(c->hits.reserve(cap_win * sizeof(kgx_hit)));
     HIP_TRY(c->calls.reserve(cap_win * sizeof(kgx_call)));
+    HIP_TRY(c->ranges.reserve(cap_win * 2 * sizeof(uint32_t)));
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
+    HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
     HIP_TRY(launch_plan(d_off, n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
-                        c->chunk_seq.as<uint32_t>(), max_chunks, c->stream));
+                        c->chunk_seq.as<uint32_t>(), c->plan_ws.p, c->stream));
     c->n_seq = n_seq;
     c->n_residues = n_residues;
     c->max_chunks = max_chunks;
@@ -476,7 +494,7 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
                          c->cbase.as<uint64_t>(), c->chunk_seq.as<uint32_t>(), c->n_seq,
                          c->max_chunks, c->img->d_table, c->img->num_sigs, c->hits.as<kgx_hit>(),
-                         c->chunk_hits.as<uint32_t>(), c->stream));
+                         c->chunk_hits.as<uint32_t>(), c->probe_variant, c->stream));
     return KGX_OK;
 }
 
@@ -492,7 +510,7 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     HIP_TRY(hipSetDevice(c->img->device));
     HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
                          c->chunk_hits.as<uint32_t>(), c->hits.as<kgx_hit>(),
-                         c->calls.as<kgx_call>(), c->hit_count.as<uint32_t>(),
+                         c->calls.as<kgx_call>(), c->ranges.p, c->hit_count.as<uint32_t>(),
                          c->call_count.as<uint32_t>(), p, want, c->stream));
     return KGX_OK;
 }
@@ -663,6 +681,30 @@ int kgx_synth_queries(kgx_ctx *c, uint64_t image_n_keys, uint32_t n_seq, uint32_
     HIP_TRY(hipSetDevice(c->img->device));
     HIP_TRY(launch_synth_queries(image_n_keys, n_seq, length, x_permille, q0, d_res, d_off,
                                  c->stream));
+    return KGX_OK;
+}
+
+int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms, uint64_t *reads)
+{
+    if (!c || !ms || mode < 0 || mode > 2)
+        return fail(KGX_EINVAL, "bad argument");
+    HIP_TRY(hipSetDevice(c->img->device));
+    const uint64_t threads = 256ull * 256 * 8; /* 8 workgroups of 256 per CU */
+    const uint32_t rounds = (uint32_t)std::max<uint64_t>(1, n_reads / (threads * 8));
+    HIP_TRY(c->plan_ws.reserve(threads * sizeof(uint64_t)));
+    hipEvent_t a, b;
+    HIP_TRY(hipEventCreate(&a));
+    HIP_TRY(hipEventCreate(&b));
+    HIP_TRY(hipEventRecord(a, c->stream));
+    HIP_TRY(launch_random_read(c->img->d_table, c->img->num_sigs, threads, rounds, mode,
+                               c->plan_ws.as<uint64_t>(), c->stream));
+    HIP_TRY(hipEventRecord(b, c->stream));
+    HIP_TRY(hipEventSynchronize(b));
+    HIP_TRY(hipEventElapsedTime(ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (reads)
+        *reads = threads * rounds * 8;
     return KGX_OK;
 }
 

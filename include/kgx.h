@@ -74,6 +74,7 @@ typedef struct kgx_hit {
 } kgx_hit;
 #define KGX_HIT_IN_RUN 1u /* appended to the run buffer (kguts.cc:845-851) */
 #define KGX_HIT_OTU 2u    /* tallied into otu_map by an emitted call (kguts.cc:760-768) */
+#define KGX_HIT_COUNTED 4u /* buffered while its function was the run's current_fI */
 
 /* KmerCall (kguts.h:166-183), 20 bytes */
 typedef struct kgx_call {
@@ -168,6 +169,10 @@ int kgx_ctx_create(kgx_image *img, kgx_ctx **out);
 int kgx_ctx_destroy(kgx_ctx *ctx);
 /* the HIP stream the context launches on (hipStream_t) */
 void *kgx_ctx_stream(kgx_ctx *ctx);
+/* tuning knobs (results never change): "probe_variant" 0 = load key and
+ * payload of every bucket examined, 1 = keys first, payload of the matching
+ * bucket only (default) */
+int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
 
@@ -211,6 +216,14 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
                        int n_names, int32_t *function_index, char *function, size_t function_cap,
                        float *score, float *weighted_score, float *score_offset,
                        int *score_offset_set);
+
+/* Random-access ceiling of the context's image buffer: about n_reads
+ * uniformly random buckets read with many loads in flight.  mode 0: the
+ * whole 24-byte bucket (key + payload, the probe's access), 1: the 8-byte key
+ * only, 2: one aligned 64-byte sector.  *ms = kernel time (HIP events),
+ * *reads = buckets actually read. */
+int kgx_microbench_random_read(kgx_ctx *ctx, uint64_t n_reads, int mode, float *ms,
+                               uint64_t *reads);
 
 /* ---- HIP-event timing on a context's stream ----------------------------- */
 int kgx_event_create(void **event);

@@ -98,6 +98,19 @@ def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params):
     assert got.n_windows >= want.windows
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_probe_variants_agree(small_world, oracle_lib, gpu, variant):
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 300, x_permille=5, q0=1000)
+    want = oracle_lib.process_batch(table, res, off)
+    ctx.set_option("probe_variant", variant)
+    try:
+        got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+    finally:
+        ctx.set_option("probe_variant", 1)
+    assert_same(got, want, 300)
+
+
 def test_ragged_long_and_empty_sequences(small_world, oracle_lib, gpu):
     spec, table, img, ctx = small_world
     rng = np.random.default_rng(9)
