@@ -39,43 +39,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-class Dist:
-    """torch.distributed (gloo, CPU tensors) for the barrier and max-reduce."""
-
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.init_process_group("gloo")
-            self.pg = dist
-
-    def barrier(self):
-        if self.pg:
-            self.pg.barrier()
-
-    def max(self, x: float) -> float:
-        if not self.pg:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, x: float) -> float:
-        if not self.pg:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
-
-    def close(self):
-        if self.pg:
-            self.pg.destroy_process_group()
-
 
 def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, target_s):
     """The oracle (bit-exact CPU restatement) over a bounded sample of rank 0's
@@ -131,12 +94,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-microbench", action="store_true")
     ap.add_argument("--ab-probe", type=int, default=0, help="rounds of interleaved probe A/B")
+    ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 
-    from close_kmers_amd import abi, synth
+    from close_kmers_amd import abi, shard, synth
 
-    d = Dist()
+    d = shard.Dist()
     n_keys = int(args.n_keys)
     spec = synth.ImageSpec(n_keys, args.num_sigs or None)
     dev = d.local_rank
@@ -154,13 +118,15 @@ def main():
     d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
     abi.check(L.kgx_device_alloc(dev, n_res, ctypes.byref(d_res)), "alloc residues")
     abi.check(L.kgx_device_alloc(dev, (n + 1) * 8, ctypes.byref(d_off)), "alloc offsets")
-    q0 = d.rank * n  # weak scaling: each rank its own shard of queries
+    q0, _ = shard.weak_shard(d.rank, n)  # weak scaling: each rank its own shard
     abi.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, args.x_permille, q0, d_res, d_off),
               "synth queries")
     ctx.synchronize()
 
     params = abi.default_params()
-    want = abi.WANT_HITS | abi.WANT_CALLS | abi.WANT_OTU
+    # lookup_request.cc:166-172 (find_best_match in family mode): hits through
+    # on_hit + the calls vector, no OTU stats; --want 7 adds OTU (/add)
+    want = args.want
     ev = [ctypes.c_void_p() for _ in range(4)]
     for e in ev:
         abi.check(L.kgx_event_create(ctypes.byref(e)), "event")
@@ -278,7 +244,7 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        value = d.world * n_res * args.steps / t_max
+        value = shard.job_throughput(d.world, n_res, args.steps, t_max)
         line = {
             "metric": METRIC,
             "value": value,
@@ -299,6 +265,8 @@ def main():
                 "n_seq_per_gpu": n, "seq_len": Ls, "n_keys": n_keys, "keys_stored": stored,
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
                 "hits_total": total_hits,
+                "outputs": {3: "hits + calls (lookup_request, find_best_match)",
+                            7: "hits + calls + OTU (add_request)"}.get(want, f"want={want}"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -478,8 +478,10 @@ __global__ __launch_bounds__(256) void score_kernel(
             wsum = wsum + p1.wt;
             last_pos = p1.pos;
             last_idx = p1.idx;
-            hw[8 * p2.idx + 3] = p2.avg | F_RUN | F_CNT;
-            hw[8 * p1.idx + 3] = p1.avg | F_RUN | F_CNT;
+            if (want_otu) {
+                hw[8 * p2.idx + 3] = p2.avg | F_RUN | F_CNT;
+                hw[8 * p1.idx + 3] = p1.avg | F_RUN | F_CNT;
+            }
         } else {
             n = 0;
         }
@@ -526,7 +528,8 @@ __global__ __launch_bounds__(256) void score_kernel(
                 if (n < RUN_CAP) {
                     n++;
                     const bool counted = fI == cur;
-                    hw[8 * i + 3] = avg | F_RUN | (counted ? F_CNT : 0u);
+                    if (want_otu) /* flags only feed the OTU pass */
+                        hw[8 * i + 3] = avg | F_RUN | (counted ? F_CNT : 0u);
                     if (counted) {
                         cnt++;
                         wsum += wt;

@@ -72,6 +72,8 @@ typedef struct kgx_hit {
     uint32_t pos; /* offset of the 8-mer in the protein (pLoc, kguts.cc:803) */
     uint32_t seq; /* index of the sequence in the batch */
 } kgx_hit;
+/* hit flags are set only when KGX_WANT_OTU is requested (they feed the OTU
+ * tally); otherwise they are 0 */
 #define KGX_HIT_IN_RUN 1u /* appended to the run buffer (kguts.cc:845-851) */
 #define KGX_HIT_OTU 2u    /* tallied into otu_map by an emitted call (kguts.cc:760-768) */
 #define KGX_HIT_COUNTED 4u /* buffered while its function was the run's current_fI */

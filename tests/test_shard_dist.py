@@ -1,0 +1,86 @@
+"""The N>1 path on CPU: world_size-2 gloo ranks each process their own shard
+(no data-path collective) and the concatenation equals the one-rank result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from close_kmers_amd import shard, synth
+
+
+def test_balanced_shards_cover_and_balance():
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 2000, 997)
+    off = np.zeros(len(lens) + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    for world in (1, 2, 3, 4, 8, 16):
+        sh = shard.balanced_shards(off, world)
+        assert sh[0][0] == 0 and sh[-1][1] == len(lens)
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        res = [int(off[hi] - off[lo]) for lo, hi in sh]
+        assert max(res) - min(res) <= 2 * lens.max() + 1
+    assert shard.balanced_shards(np.zeros(1, np.uint64), 4) == [(0, 0)] * 4
+
+
+def test_weak_shard_and_throughput():
+    assert shard.weak_shard(0, 100) == (0, 100)
+    assert shard.weak_shard(3, 100) == (300, 400)
+    assert shard.job_throughput(8, 30_000_000, 20, 2.0) == 8 * 30_000_000 * 20 / 2.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import oracle
+    from helpers import synthetic_table
+    d = shard.Dist("gloo")
+    spec, table = synthetic_table(20000)
+    n = 120
+    lo, hi = shard.weak_shard(d.rank, n)
+    res, off = synth.make_queries(spec, n, q0=lo, x_permille=5)
+    r = oracle.process_batch(table, res, off)
+    d.barrier()
+    t = d.max(float(rank + 1))
+    total_hits = d.sum(float(len(r.hits)))
+    parts = d.gather_objects((lo, hi, r.hits["pos"].tolist(), r.hits["which_kmer"].tolist(),
+                              np.diff(r.call_offsets).tolist()))
+    if d.rank == 0:
+        q.put((t, total_hits, parts))
+    d.close()
+
+
+def test_two_rank_gloo_shards_equal_single_rank():
+    import torch.multiprocessing as mp
+    import oracle
+    from helpers import synthetic_table
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    t, total_hits, parts = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert t == 2.0
+    spec, table = synthetic_table(20000)
+    res, off = synth.make_queries(spec, 240, x_permille=5)
+    whole = oracle.process_batch(table, res, off)
+    assert total_hits == len(whole.hits)
+    assert [p[0] for p in parts] == [0, 120]
+    pos = sum((p[2] for p in parts), [])
+    keys = sum((p[3] for p in parts), [])
+    calls = sum((p[4] for p in parts), [])
+    assert pos == whole.hits["pos"].tolist()
+    assert keys == whole.hits["which_kmer"].tolist()
+    assert calls == np.diff(whole.call_offsets).tolist()
