@@ -93,7 +93,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-microbench", action="store_true")
-    ap.add_argument("--ab-probe", type=int, default=0, help="rounds of interleaved probe A/B")
+    ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
+    ap.add_argument("--ab-rounds", type=int, default=10)
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
@@ -155,17 +156,22 @@ def main():
     ctx.synchronize()
 
     probe_ab = None
-    if args.ab_probe:
-        # interleaved A/B of the probe variants in this process (rule: one
-        # process, alternating rounds, report the distribution)
-        times = {0: [], 1: []}
-        for _ in range(args.ab_probe):
-            for v in (0, 1):
-                ctx.set_option("probe_variant", v)
+    if args.ab:
+        # interleaved A/B of one tuning option in this process (one process,
+        # alternating rounds, report the distribution); "name=v1,v2,..."
+        name, vals = args.ab.split("=")
+        vals = [int(v) for v in vals.split(",")]
+        times = {v: [] for v in vals}
+        for _ in range(args.ab_rounds):
+            for v in vals:
+                ctx.set_option(name, v)
                 step(times[v])
+        ctx.set_option(name, vals[0])
         ctx.set_option("probe_variant", 1)
-        probe_ab = {f"variant{v}": {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
-                    for v, t in times.items()}
+        ctx.set_option("probe_j", 5)
+        probe_ab = {"option": name,
+                    **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
+                       for v, t in times.items()}}
         log(f"[bench] probe A/B: {probe_ab}")
 
     d.barrier()

@@ -50,9 +50,33 @@ class Result(ctypes.Structure):
 
 
 class DeviceResult(ctypes.Structure):
-    _fields_ = [("n_seq", ctypes.c_uint32), ("window_base", ctypes.c_void_p),
+    _fields_ = [("n_seq", ctypes.c_uint32), ("tile_windows", ctypes.c_uint32),
+                ("window_base", ctypes.c_void_p), ("hit_mask", ctypes.c_void_p),
                 ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
                 ("hits", ctypes.c_void_p), ("calls", ctypes.c_void_p)]
+
+
+def tiled_hits_per_sequence(window_base: np.ndarray, hit_mask: np.ndarray, tile_windows: int,
+                            hits: np.ndarray) -> list[np.ndarray]:
+    """Host-side walk of kgx_device_result's tiled hit layout (for tests and
+    tools): the hit records of every sequence, in position order."""
+    J = tile_windows // 64
+    pc = np.array([bin(int(x)).count("1") for x in hit_mask], dtype=np.int64)
+    out = []
+    for s in range(len(window_base) - 1):
+        gw0, gw1 = int(window_base[s]), int(window_base[s + 1])
+        parts = []
+        for g in range(gw0 >> 6, ((gw1 - 1) >> 6) + 1 if gw1 > gw0 else gw0 >> 6):
+            t = g // J
+            pre = int(pc[t * J:g].sum())
+            lo = gw0 & 63 if g == gw0 >> 6 else 0
+            hi = ((gw1 - 1) & 63) + 1 if g == (gw1 - 1) >> 6 else 64
+            full = int(hit_mask[g])
+            sel = full & (((1 << hi) - 1) & ~((1 << lo) - 1))
+            start = t * tile_windows + pre + bin(full & ((1 << lo) - 1)).count("1")
+            parts.append(hits[start:start + bin(sel).count("1")])
+        out.append(np.concatenate(parts) if parts else hits[:0])
+    return out
 
 
 _P = ctypes.c_void_p

@@ -1,0 +1,614 @@
+/*
+ * kgx_lookup.hip -- gfx950 kernels of the lookup path.
+ *
+ *   plan   : wbase = exclusive scan of windows per sequence; tile -> first
+ *            sequence map (two launches, 1,024 sequences per workgroup)
+ *   probe  : 8-mer encode + linear-probe lookup in the HBM-resident image;
+ *            one wave per tile of J*64 consecutive windows of the batch
+ *            (across sequence boundaries); J probe chains in flight per lane;
+ *            hits compacted per tile in window order with wave ballots
+ *   score  : the gather_hits / process_set_of_hits run state machine, one
+ *            lane per sequence, O(1) state (no 40,000-entry buffer)
+ *   gather : tiled hits -> dense per-sequence CSR (host-buffer path)
+ *
+ * Reference behaviour restated (kguts.cc line numbers): residue map 273-339,
+ * window set / rolling code 682-732 and 783-871, probe 585-602, run rules
+ * 734-781 and 808-876.
+ */
+#include "kgx_device.h"
+
+namespace kgx {
+
+/* ------------------------------------------------------------------------ */
+/* plan                                                                      */
+/* ------------------------------------------------------------------------ */
+
+constexpr uint32_t PLAN_PER = 4;               /* sequences per thread */
+constexpr uint32_t PLAN_TILE = 256 * PLAN_PER; /* sequences per workgroup */
+
+__device__ __forceinline__ uint64_t thread_windows(const uint64_t *seq_off, uint32_t n, uint32_t s0)
+{
+    uint64_t w = 0;
+    for (uint32_t k = 0; k < PLAN_PER; k++)
+        if (s0 + k < n)
+            w += windows_of(seq_off[s0 + k + 1] - seq_off[s0 + k]);
+    return w;
+}
+
+/* inclusive scan over a 256-thread workgroup; `total` = sum of all */
+__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *lds4, uint64_t &total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint64_t x = __shfl_up(v, off);
+        if (lane >= off)
+            v += x;
+    }
+    if (lane == 63)
+        lds4[wave] = v;
+    __syncthreads();
+    uint64_t pre = 0;
+    total = 0;
+    for (uint32_t i = 0; i < 4; i++) {
+        if (i < wave)
+            pre += lds4[i];
+        total += lds4[i];
+    }
+    return v + pre;
+}
+
+__global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__restrict__ seq_off,
+                                                          uint32_t n, uint64_t *__restrict__ sums)
+{
+    __shared__ uint64_t lds4[4];
+    uint64_t total;
+    block_scan(thread_windows(seq_off, n, blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER), lds4,
+               total);
+    if (threadIdx.x == 0)
+        sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restrict__ seq_off,
+                                                        uint32_t n, const uint64_t *__restrict__ sums,
+                                                        uint64_t *__restrict__ wbase,
+                                                        uint32_t *__restrict__ tile_seq,
+                                                        uint32_t tile_windows)
+{
+    __shared__ uint64_t lds_a[4], lds_b[4];
+    uint64_t p = 0; /* windows of all earlier workgroups */
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 256)
+        p += sums[b];
+    uint64_t before;
+    block_scan(p, lds_a, before);
+    __syncthreads();
+
+    const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
+    const uint64_t mine = thread_windows(seq_off, n, s0);
+    uint64_t tot;
+    const uint64_t incl = block_scan(mine, lds_b, tot);
+    uint64_t wb = before + incl - mine;
+    for (uint32_t k = 0; k < PLAN_PER; k++) {
+        const uint32_t s = s0 + k;
+        if (s >= n)
+            break;
+        const uint64_t we = wb + windows_of(seq_off[s + 1] - seq_off[s]);
+        wbase[s] = wb;
+        /* tiles whose first window lies in [wb, we) start inside sequence s */
+        for (uint64_t t = (wb + tile_windows - 1) / tile_windows; t * tile_windows < we; t++)
+            tile_seq[t] = s;
+        wb = we;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255)
+        wbase[n] = before + tot;
+}
+
+size_t plan_workspace_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 1) * sizeof(uint64_t); }
+
+hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase, uint32_t *tile_seq,
+                       uint32_t tile_windows, void *workspace, hipStream_t stream)
+{
+    const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
+    hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
+                       static_cast<uint64_t *>(workspace));
+    hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
+                       static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* probe                                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* 12 residue bytes from byte address `a` rounded down to 4; bytes outside
+ * [lo, hi) read as 0 (code 20) */
+__device__ __forceinline__ uint3 load_residues(uintptr_t ab, uintptr_t lo, uintptr_t hi)
+{
+    if (ab >= lo && ab + 16 <= hi) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(ab);
+        return make_uint3(v.x, v.y, v.z);
+    }
+    uint32_t d[3] = {0, 0, 0};
+    for (int b = 0; b < 12; b++)
+        if (ab + b >= lo && ab + b < hi)
+            d[b >> 2] |= (uint32_t)(*reinterpret_cast<const uint8_t *>(ab + b)) << (8 * (b & 3));
+    return make_uint3(d[0], d[1], d[2]);
+}
+
+/*
+ * One wave = one tile of J*64 windows [g0, g0 + J*64) of the batch.  Lane l
+ * owns windows g0 + 64 j + l, so slice j is 64 consecutive windows and its
+ * ballot is in window order (= (sequence, position) order).  Every lane
+ * finds its window's sequence by walking forward from the tile's first
+ * sequence, reads the 8 residues straight from the batch (one 16-byte load),
+ * maps them to codes through a 256-byte LDS table, and issues all J first
+ * probes before resolving any.
+ *   KEY_FIRST = false: each probe round loads key and payload of its bucket;
+ *   KEY_FIRST = true: rounds load keys only; the matching bucket's payload is
+ *     loaded in the round that finds it (mostly the key's sector, in L2).
+ */
+template <int J, bool KEY_FIRST>
+__global__ __launch_bounds__(256) void probe_kernel(
+    const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
+    const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
+    const kgx_sig_kmer *__restrict__ table, uint64_t num_sigs, uint64_t magic,
+    kgx_hit *__restrict__ hits, uint64_t *__restrict__ hit_mask)
+{
+    constexpr uint32_t T = 64 * J;
+    __shared__ uint8_t code_tab[256];
+    code_tab[threadIdx.x] = (uint8_t)residue_code(threadIdx.x);
+    __syncthreads();
+
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    const uint64_t W = wbase[n_seq];
+    const uint64_t tile = (uint64_t)blockIdx.x * PROBE_WAVES + wave;
+    const uint64_t g0 = tile * T;
+    if (g0 >= W)
+        return;
+
+    const uintptr_t arr_lo = reinterpret_cast<uintptr_t>(residues);
+    const uintptr_t arr_hi = arr_lo + n_residues;
+    uint32_t s = tile_seq[tile];
+    uint64_t wb_lo = wbase[s], wb_hi = wbase[s + 1], soff = seq_off[s];
+
+    uint64_t key[J], slot[J], kv[J];
+    uint4 pv[J];
+    uint32_t pos[J], sq[J];
+    bool pend[J], hit[J];
+
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint64_t gw = g0 + 64 * j + lane;
+        const bool act = gw < W;
+        while (act && gw >= wb_hi) { /* next sequence (skips window-less ones) */
+            s++;
+            wb_lo = wb_hi;
+            wb_hi = wbase[s + 1];
+            soff = seq_off[s];
+        }
+        pos[j] = (uint32_t)(gw - wb_lo);
+        sq[j] = s;
+        const uintptr_t a = arr_lo + soff + (gw - wb_lo);
+        const uintptr_t ab = a & ~(uintptr_t)3;
+        const uint32_t sh = (uint32_t)(a - ab);
+        const uint3 d = load_residues(ab, arr_lo, arr_hi);
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d.z, d.y, sh);
+        const uint32_t c0 = code_tab[lo & 0xFF], c1 = code_tab[(lo >> 8) & 0xFF],
+                       c2 = code_tab[(lo >> 16) & 0xFF], c3 = code_tab[lo >> 24];
+        const uint32_t c4 = code_tab[hi & 0xFF], c5 = code_tab[(hi >> 8) & 0xFF],
+                       c6 = code_tab[(hi >> 16) & 0xFF], c7 = code_tab[hi >> 24];
+        /* a code-20 residue anywhere kills the window (advance_past_ambig) */
+        const uint32_t cmax = max(max(max(c0, c1), max(c2, c3)), max(max(c4, c5), max(c6, c7)));
+        const bool ok = act && cmax < 20u;
+        /* big-endian base-20 Horner (encoded_kmer, kguts.cc:438-455) */
+        const uint32_t ka = ((c0 * 20 + c1) * 20 + c2) * 20 + c3;
+        const uint32_t kb = ((c4 * 20 + c5) * 20 + c6) * 20 + c7;
+        key[j] = (uint64_t)ka * 160000u + kb;
+        slot[j] = ok ? mod_by(key[j], num_sigs, magic) : 0;
+        pend[j] = ok;
+        hit[j] = false;
+        kv[j] = 0;
+        pv[j] = make_uint4(0, 0, 0, 0);
+        if (ok) {
+            const kgx_sig_kmer *e = table + slot[j];
+            kv[j] = e->which_kmer;
+            if (!KEY_FIRST)
+                pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+        }
+    }
+
+    /* linear probe rounds (lookup_hash_entry, kguts.cc:585-602); bounded by
+     * num_sigs buckets where the reference would spin forever */
+    for (uint64_t round = 0;; round++) {
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (pend[j]) {
+                if (kv[j] == key[j]) {
+                    hit[j] = true;
+                    pend[j] = false;
+                    if (KEY_FIRST)
+                        pv[j] = *reinterpret_cast<const uint4 *>(
+                            reinterpret_cast<const char *>(table + slot[j]) + 8);
+                } else if (kv[j] > MAX_ENCODED || round + 1 >= num_sigs) {
+                    pend[j] = false;
+                } else {
+                    slot[j] = (slot[j] + 1 == num_sigs) ? 0 : slot[j] + 1;
+                    const kgx_sig_kmer *e = table + slot[j];
+                    kv[j] = e->which_kmer;
+                    if (!KEY_FIRST)
+                        pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                    more = true;
+                }
+            }
+        }
+        if (!__any(more))
+            break;
+    }
+
+    /* ordered compaction of the tile's hits; one mask word per slice */
+    uint32_t count = 0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint64_t m = __ballot(hit[j]);
+        if (hit[j]) {
+            uint4 *d = reinterpret_cast<uint4 *>(hits + g0 + count + lanes_below(m));
+            d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, pv[j].y & 0xFFFFu);
+            d[1] = make_uint4(pv[j].z, pv[j].w, pos[j], sq[j]);
+        }
+        if (lane == 0 && g0 + 64 * j < W)
+            hit_mask[(g0 >> 6) + j] = m;
+        count += (uint32_t)__popcll(m);
+    }
+}
+
+template <int J>
+static void launch_probe_j(dim3 grid, hipStream_t stream, int variant, const uint8_t *residues,
+                           uint64_t n_residues, const uint64_t *seq_off, const uint64_t *wbase,
+                           const uint32_t *tile_seq, uint32_t n_seq, const kgx_sig_kmer *table,
+                           uint64_t num_sigs, kgx_hit *hits, uint64_t *hit_mask)
+{
+    if (variant == PROBE_KEY_FIRST)
+        hipLaunchKernelGGL((probe_kernel<J, true>), grid, dim3(64 * PROBE_WAVES), 0, stream,
+                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
+                           mod_magic(num_sigs), hits, hit_mask);
+    else
+        hipLaunchKernelGGL((probe_kernel<J, false>), grid, dim3(64 * PROBE_WAVES), 0, stream,
+                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
+                           mod_magic(num_sigs), hits, hit_mask);
+}
+
+hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
+                        const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
+                        uint64_t max_tiles, const kgx_sig_kmer *table, uint64_t num_sigs,
+                        kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
+                        hipStream_t stream)
+{
+    if (max_tiles == 0)
+        return hipSuccess;
+    const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+    switch (probe_j) {
+    case 2: launch_probe_j<2>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
+    case 4: launch_probe_j<4>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
+    case 5: launch_probe_j<5>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
+    case 8: launch_probe_j<8>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* hits of one sequence in the tiled layout                                  */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Calls f(storage_start, count, ordinal0) for each run of the sequence's hits
+ * (windows [gw0, gw1)): within one mask word, the sequence's hits are a
+ * contiguous stretch of its tile's compacted hits.  Returns the hit count.
+ */
+template <class F>
+__device__ __forceinline__ uint32_t for_each_run(const uint64_t *__restrict__ hit_mask,
+                                                 uint32_t tile_windows, uint64_t gw0, uint64_t gw1,
+                                                 F &&f)
+{
+    if (gw0 >= gw1)
+        return 0;
+    const uint32_t J = tile_windows / 64;
+    const uint64_t gfirst = gw0 >> 6, glast = (gw1 - 1) >> 6;
+    uint64_t tile = gfirst / J;
+    uint32_t pre = 0; /* tile's hits before word g */
+    for (uint64_t g = tile * J; g < gfirst; g++)
+        pre += (uint32_t)__popcll(hit_mask[g]);
+    uint32_t ordinal = 0;
+    for (uint64_t g = gfirst; g <= glast; g++) {
+        if (g != gfirst && g % J == 0) {
+            tile = g / J;
+            pre = 0;
+        }
+        const uint64_t full = hit_mask[g];
+        const uint32_t lo = g == gfirst ? (uint32_t)(gw0 & 63) : 0u;
+        const uint32_t hi = g == glast ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
+        const uint32_t cnt = (uint32_t)__popcll(full & bit_range(lo, hi));
+        if (cnt)
+            f(tile * tile_windows + pre + (uint32_t)__popcll(full & bit_range(0, lo)), cnt, ordinal);
+        ordinal += cnt;
+        pre += (uint32_t)__popcll(full);
+    }
+    return ordinal;
+}
+
+/* ------------------------------------------------------------------------ */
+/* score                                                                     */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * The run state machine of gather_hits (kguts.cc:808-876) and
+ * process_set_of_hits (kguts.cc:734-781), one lane per sequence.  The
+ * reference keeps up to 40000 hits in a buffer and rescans it at every flush;
+ * here the buffer is summarised by O(1) state that yields the same call:
+ *   n         number of buffered hits (capped at RUN_CAP, kguts.cc:850-851)
+ *   cur       current_fI
+ *   cnt/wsum  count and f32 sum (in append order) of buffered hits with
+ *             fI == cur -- exactly the reference's flush loop
+ *   first/last position of buffer[0] / of the last buffered hit with fI == cur
+ *   p1, p2    the last two buffered hits (gap rule, order constraint,
+ *             pair switch and carry-over read only these)
+ * With OTU output requested, buffered hits are flagged KGX_HIT_IN_RUN (and
+ * KGX_HIT_COUNTED when their function is their run's current_fI); each
+ * emitted call records its run's ordinal hit range, and a second walk flags
+ * the COUNTED hits inside emitted ranges KGX_HIT_OTU -- the hits the
+ * reference tallies into otu_map (kguts.cc:760-768).
+ */
+struct RunTail {
+    uint32_t pos, fI, idx;
+    float wt;
+    uint32_t avg;
+    uint64_t at; /* storage index */
+};
+
+constexpr int SCORE_BATCH = 8;
+constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << 16, F_CNT = KGX_HIT_COUNTED << 16,
+                   F_OTU = KGX_HIT_OTU << 16;
+
+__global__ __launch_bounds__(256) void score_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+    uint32_t tile_windows, kgx_hit *__restrict__ hits, kgx_call *__restrict__ calls,
+    uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
+    kgx_params prm, uint32_t want)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_seq)
+        return;
+    const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    if (!want_calls && !want_otu) {
+        /* process_set_of_hits returns before doing anything (kguts.cc:737) */
+        hit_count[s] = for_each_run(hit_mask, tile_windows, gw0, gw1,
+                                    [](uint64_t, uint32_t, uint32_t) {});
+        call_count[s] = 0;
+        return;
+    }
+
+    uint32_t *hw = reinterpret_cast<uint32_t *>(hits); /* 8 dwords per hit */
+    const uint64_t cbase = gw0; /* calls / ranges of s live at [gw0, ...) */
+    const uint32_t gap = (uint32_t)prm.max_gap;
+    int n = 0;
+    uint32_t cur = 0, first_pos = 0, last_pos = 0, last_idx = 0, run_start = 0;
+    int cnt = 0;
+    float wsum = 0.0f;
+    RunTail p1 = {0, 0, 0, 0.0f, 0, 0}, p2 = {0, 0, 0, 0.0f, 0, 0};
+    uint32_t ncalls = 0;
+
+    auto flush = [&]() {
+        if (n == 0)
+            return; /* min_hits <= 0 final flush: reference UB, emit nothing */
+        if (cnt >= prm.min_hits && wsum >= (float)prm.min_weighted_hits) {
+            if (want_calls) {
+                kgx_call cl;
+                cl.start = first_pos;
+                cl.end = last_pos + (KMER - 1);
+                cl.count = cnt;
+                cl.function_index = cur;
+                cl.weighted_hits = wsum;
+                calls[cbase + ncalls] = cl;
+            }
+            if (want_otu)
+                ranges[cbase + ncalls] = make_uint2(run_start, last_idx);
+            ncalls++;
+        }
+        if (n >= 2 && p2.fI != cur && p2.fI == p1.fI) { /* carry the pair */
+            cur = p1.fI;
+            n = 2;
+            run_start = p2.idx;
+            first_pos = p2.pos;
+            cnt = 2;
+            wsum = 0.0f + p2.wt;
+            wsum = wsum + p1.wt;
+            last_pos = p1.pos;
+            last_idx = p1.idx;
+            if (want_otu) {
+                hw[8 * p2.at + 3] = p2.avg | F_RUN | F_CNT;
+                hw[8 * p1.at + 3] = p1.avg | F_RUN | F_CNT;
+            }
+        } else {
+            n = 0;
+        }
+    };
+
+    auto step = [&](const uint4 &r, uint32_t i, uint64_t at) {
+        const uint32_t avg = r.x & 0xFFFFu;
+        const uint32_t fI = r.y;
+        const float wt = __uint_as_float(r.z);
+        const uint32_t pos = r.w;
+        /* gap rule (kguts.cc:821-831), unsigned arithmetic */
+        if (n > 0 && p1.pos + gap < pos) {
+            if (n >= prm.min_hits)
+                flush();
+            else
+                n = 0;
+        }
+        if (n == 0) {
+            cur = fI;
+            cnt = 0;
+            wsum = 0.0f;
+            run_start = i;
+            first_pos = pos;
+        }
+        bool accept = true;
+        if (prm.order_constraint && n > 0) { /* kguts.cc:838-842 */
+            const uint32_t d = (pos - p1.pos) - (uint32_t)((int)p1.avg - (int)avg);
+            accept = (fI == p1.fI) && d <= 20u;
+        }
+        if (accept) {
+            if (n < RUN_CAP) {
+                n++;
+                const bool counted = fI == cur;
+                if (want_otu) /* flags only feed the OTU pass */
+                    hw[8 * at + 3] = avg | F_RUN | (counted ? F_CNT : 0u);
+                if (counted) {
+                    cnt++;
+                    wsum += wt;
+                    last_pos = pos;
+                    last_idx = i;
+                }
+                p2 = p1;
+                p1 = RunTail{pos, fI, i, wt, avg, at};
+            }
+            /* pair switch (kguts.cc:852-856) */
+            if (n > 1 && cur != fI && p2.fI == p1.fI)
+                flush();
+        }
+    };
+
+    /* hits are read SCORE_BATCH at a time, all loads issued before any is
+     * consumed: the state machine is serial, its inputs are not */
+    const uint32_t nh = for_each_run(hit_mask, tile_windows, gw0, gw1,
+                                     [&](uint64_t at0, uint32_t c, uint32_t ord0) {
+        for (uint32_t b = 0; b < c; b += SCORE_BATCH) {
+            uint4 rb[SCORE_BATCH];
+#pragma unroll
+            for (int k = 0; k < SCORE_BATCH; k++)
+                if (b + k < c) /* avg|flags, fI, wt, pos */
+                    rb[k] = *reinterpret_cast<const uint4 *>(hw + 8 * (at0 + b + k) + 3);
+#pragma unroll
+            for (int k = 0; k < SCORE_BATCH; k++)
+                if (b + k < c)
+                    step(rb[k], ord0 + b + k, at0 + b + k);
+        }
+    });
+    if (n >= prm.min_hits) /* kguts.cc:873-876 */
+        flush();
+    hit_count[s] = nh;
+    call_count[s] = want_calls ? ncalls : 0;
+
+    /* OTU flags: COUNTED hits inside an emitted call's ordinal range (ranges
+     * are disjoint and in order) */
+    if (want_otu && ncalls > 0) {
+        uint32_t ci = 0;
+        uint2 rg = ranges[cbase];
+        const uint32_t end = ranges[cbase + ncalls - 1].y;
+        for_each_run(hit_mask, tile_windows, gw0, gw1, [&](uint64_t at0, uint32_t c, uint32_t ord0) {
+            for (uint32_t k = 0; k < c; k++) {
+                const uint32_t i = ord0 + k;
+                if (i > end)
+                    return;
+                while (i > rg.y) /* i <= end keeps ci < ncalls */
+                    rg = ranges[cbase + ++ci];
+                if (i >= rg.x) {
+                    const uint32_t f = hw[8 * (at0 + k) + 3];
+                    if (f & F_CNT)
+                        hw[8 * (at0 + k) + 3] = f | F_OTU;
+                }
+            }
+        });
+    }
+}
+
+hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
+                        uint32_t tile_windows, kgx_hit *hits, kgx_call *calls, void *ranges,
+                        uint32_t *hit_count, uint32_t *call_count, kgx_params params,
+                        uint32_t want, hipStream_t stream)
+{
+    if (n_seq == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(score_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
+                       hit_mask, tile_windows, hits, calls, static_cast<uint2 *>(ranges), hit_count,
+                       call_count, params, want);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* gather: tiled hits / sparse calls -> dense CSR, one wave per sequence     */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(256) void gather_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+    uint32_t tile_windows, const uint32_t *__restrict__ call_count, const kgx_hit *__restrict__ hits,
+    const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
+    const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out)
+{
+    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= n_seq)
+        return;
+    const uint32_t lane = lane_id();
+    const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
+    if (hits_out && gw0 < gw1) {
+        const uint32_t J = tile_windows / 64;
+        const uint64_t gfirst = gw0 >> 6, glast = (gw1 - 1) >> 6;
+        uint64_t done = 0; /* hits of s written so far */
+        for (uint64_t gb = gfirst; gb <= glast; gb += 64) {
+            /* lane l takes mask word gb + l: its run inside the tile */
+            const uint64_t g = gb + lane;
+            uint64_t at = 0;
+            uint32_t cnt = 0;
+            if (g <= glast) {
+                const uint64_t tile = g / J;
+                uint32_t pre = 0;
+                for (uint64_t x = tile * J; x < g; x++)
+                    pre += (uint32_t)__popcll(hit_mask[x]);
+                const uint64_t full = hit_mask[g];
+                const uint32_t lo = g == gfirst ? (uint32_t)(gw0 & 63) : 0u;
+                const uint32_t hi = g == glast ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
+                cnt = (uint32_t)__popcll(full & bit_range(lo, hi));
+                at = tile * tile_windows + pre + (uint32_t)__popcll(full & bit_range(0, lo));
+            }
+            /* exclusive prefix of cnt over the wave */
+            uint32_t incl = cnt;
+            for (uint32_t off = 1; off < 64; off <<= 1) {
+                const uint32_t x = __shfl_up(incl, off);
+                if (lane >= off)
+                    incl += x;
+            }
+            const uint64_t dst0 = hoff[s] + done + (incl - cnt);
+            const uint4 *src = reinterpret_cast<const uint4 *>(hits + at);
+            uint4 *dst = reinterpret_cast<uint4 *>(hits_out + dst0);
+            for (uint32_t i = 0; i < 2 * cnt; i++)
+                dst[i] = src[i];
+            done += __shfl(incl, 63);
+        }
+    }
+    if (calls_out) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(calls + gw0);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(calls_out + coff[s]);
+        const uint32_t n = 5 * call_count[s];
+        for (uint32_t i = lane; i < n; i += 64)
+            dst[i] = src[i];
+    }
+}
+
+hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
+                         uint32_t tile_windows, const uint32_t *call_count, const kgx_hit *hits,
+                         const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
+                         kgx_hit *hits_out, kgx_call *calls_out, hipStream_t stream)
+{
+    if (n_seq == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
+                       hit_mask, tile_windows, call_count, hits, calls, hoff, coff, hits_out,
+                       calls_out);
+    return hipGetLastError();
+}
+
+}  // namespace kgx

@@ -90,15 +90,17 @@ struct kgx_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     /* device scratch */
-    DevBuf residues, offsets, wbase, cbase, chunk_seq, chunk_hits, hits, calls, hit_count,
-        call_count, dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
+    DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
+        dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
     /* current plan */
     uint32_t n_seq = 0;
     uint64_t n_residues = 0;
-    uint64_t max_chunks = 0;
+    uint64_t max_tiles = 0;
+    uint32_t tile_windows = 64u * PROBE_J_DEFAULT;
     const uint64_t *d_off = nullptr;
     /* tuning options */
     int probe_variant = PROBE_KEY_FIRST;
+    int probe_j = PROBE_J_DEFAULT;
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
     std::vector<kgx_hit> h_hits;
@@ -403,7 +405,7 @@ int kgx_ctx_destroy(kgx_ctx *c)
         return KGX_OK;
     (void)hipSetDevice(c->img->device);
     (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->residues, &c->offsets, &c->wbase, &c->cbase, &c->chunk_seq, &c->chunk_hits,
+    for (DevBuf *b : {&c->residues, &c->offsets, &c->wbase, &c->tile_seq, &c->hit_mask,
                       &c->hits, &c->calls, &c->hit_count, &c->call_count, &c->dense_hoff,
                       &c->dense_coff, &c->dense_hits, &c->dense_calls, &c->plan_ws, &c->ranges})
         b->release();
@@ -442,6 +444,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->probe_variant = (int)value;
         return KGX_OK;
     }
+    if (n == "probe_j") {
+        if (!probe_j_supported((int)value))
+            return fail(KGX_EINVAL, "probe_j must be 2, 4, 5 or 8");
+        c->probe_j = (int)value;
+        return KGX_OK;
+    }
     return fail(KGX_EINVAL, "unknown option " + n);
 }
 
@@ -462,24 +470,25 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     if (n_residues > (1ull << 40))
         return fail(KGX_ERANGE, "batch too large");
     HIP_TRY(hipSetDevice(c->img->device));
-    /* bounds: windows <= residues; chunks <= n_seq + residues / CHUNK */
-    const uint64_t max_chunks = (uint64_t)n_seq + n_residues / CHUNK + 1;
+    /* bounds: windows <= residues, so tiles <= residues / tile + 1 */
+    const uint32_t tile_windows = 64u * (uint32_t)c->probe_j;
+    const uint64_t max_tiles = n_residues / tile_windows + 1;
     const uint64_t cap_win = std::max<uint64_t>(n_residues, 1);
     HIP_TRY(c->wbase.reserve((n_seq + 1) * sizeof(uint64_t)));
-    HIP_TRY(c->cbase.reserve((n_seq + 1) * sizeof(uint64_t)));
-    HIP_TRY(c->chunk_seq.reserve(max_chunks * sizeof(uint32_t)));
-    HIP_TRY(c->chunk_hits.reserve(max_chunks * sizeof(uint32_t)));
+    HIP_TRY(c->tile_seq.reserve(max_tiles * sizeof(uint32_t)));
+    HIP_TRY(c->hit_mask.reserve((cap_win / 64 + 2) * sizeof(uint64_t)));
     HIP_TRY(c->hits.reserve(cap_win * sizeof(kgx_hit)));
     HIP_TRY(c->calls.reserve(cap_win * sizeof(kgx_call)));
     HIP_TRY(c->ranges.reserve(cap_win * 2 * sizeof(uint32_t)));
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
-    HIP_TRY(launch_plan(d_off, n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
-                        c->chunk_seq.as<uint32_t>(), c->plan_ws.p, c->stream));
+    HIP_TRY(launch_plan(d_off, n_seq, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                        tile_windows, c->plan_ws.p, c->stream));
     c->n_seq = n_seq;
     c->n_residues = n_residues;
-    c->max_chunks = max_chunks;
+    c->max_tiles = max_tiles;
+    c->tile_windows = tile_windows;
     c->d_off = d_off;
     return KGX_OK;
 }
@@ -492,9 +501,9 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     if (c->img->num_sigs >= (1ull << 40))
         return fail(KGX_ERANGE, "image too large");
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
-                         c->cbase.as<uint64_t>(), c->chunk_seq.as<uint32_t>(), c->n_seq,
-                         c->max_chunks, c->img->d_table, c->img->num_sigs, c->hits.as<kgx_hit>(),
-                         c->chunk_hits.as<uint32_t>(), c->probe_variant, c->stream));
+                         c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->d_table,
+                         c->img->num_sigs, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
+                         (int)(c->tile_windows / 64), c->probe_variant, c->stream));
     return KGX_OK;
 }
 
@@ -508,10 +517,10 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     else
         kgx_params_default(&p);
     HIP_TRY(hipSetDevice(c->img->device));
-    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->cbase.as<uint64_t>(),
-                         c->chunk_hits.as<uint32_t>(), c->hits.as<kgx_hit>(),
-                         c->calls.as<kgx_call>(), c->ranges.p, c->hit_count.as<uint32_t>(),
-                         c->call_count.as<uint32_t>(), p, want, c->stream));
+    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(),
+                         c->tile_windows, c->hits.as<kgx_hit>(), c->calls.as<kgx_call>(),
+                         c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
+                         want, c->stream));
     return KGX_OK;
 }
 
@@ -520,7 +529,9 @@ int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
     if (!c || !out)
         return fail(KGX_EINVAL, "null argument");
     out->n_seq = c->n_seq;
+    out->tile_windows = c->tile_windows;
     out->window_base = c->wbase.as<uint64_t>();
+    out->hit_mask = c->hit_mask.as<uint64_t>();
     out->hit_count = c->hit_count.as<uint32_t>();
     out->call_count = c->call_count.as<uint32_t>();
     out->hits = c->hits.as<kgx_hit>();
@@ -619,7 +630,7 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
                                hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->dense_coff.p, c->h_coff.data(), (n_seq + 1) * sizeof(uint64_t),
                                hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_count.as<uint32_t>(),
+        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
                               c->call_count.as<uint32_t>(), c->hits.as<kgx_hit>(),
                               c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
                               c->dense_coff.as<uint64_t>(),

@@ -118,13 +118,21 @@ typedef struct kgx_result {
                            non-standard residue are skipped, not probed */
 } kgx_result;
 
-/* Device-resident results of kgx_run_device (pointers into HBM).  Hits and
- * calls of sequence s start at window_base[s]; their counts are
- * hit_count[s] / call_count[s].  Hit records of a sequence are contiguous
- * and in position order. */
+/* Device-resident results of kgx_run_device (pointers into HBM).
+ * Windows are numbered across the batch: sequence s owns global windows
+ * [window_base[s], window_base[s+1]) (position = global - window_base[s]).
+ * The probe works in tiles of tile_windows consecutive windows; tile t's hits
+ * are stored compacted in window order from hits[t * tile_windows], and bit i
+ * of hit_mask[g] is set when global window 64*g + i hit.  So the hits of a
+ * sequence are, word by word of its mask range, contiguous stretches of its
+ * tiles' hit lists (each record also carries seq and pos).  Calls of s are
+ * contiguous from calls[window_base[s]]; counts are hit_count[s] /
+ * call_count[s]. */
 typedef struct kgx_device_result {
     uint32_t n_seq;
+    uint32_t tile_windows;
     const uint64_t *window_base; /* n_seq + 1: exclusive scan of max(0, len-8) */
+    const uint64_t *hit_mask;    /* ceil(window_base[n_seq] / 64) words */
     const uint32_t *hit_count;   /* n_seq */
     const uint32_t *call_count;  /* n_seq */
     const kgx_hit *hits;         /* capacity window_base[n_seq] */
@@ -173,7 +181,8 @@ int kgx_ctx_destroy(kgx_ctx *ctx);
 void *kgx_ctx_stream(kgx_ctx *ctx);
 /* tuning knobs (results never change): "probe_variant" 0 = load key and
  * payload of every bucket examined, 1 = keys first, payload of the matching
- * bucket only (default) */
+ * bucket only (default); "probe_j" = windows per lane (2, 4, 5 or 8; a tile
+ * is 64 * probe_j windows), read at the next plan */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);

@@ -99,15 +99,23 @@ def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-def test_probe_variants_agree(small_world, oracle_lib, gpu, variant):
+@pytest.mark.parametrize("probe_j", [2, 4, 5, 8])
+def test_probe_variants_agree(small_world, oracle_lib, gpu, variant, probe_j):
     spec, table, img, ctx = small_world
+    # mixed lengths so tiles straddle many sequence boundaries
+    rng = np.random.default_rng(probe_j * 10 + variant)
     res, off = synth.make_queries(spec, 300, x_permille=5, q0=1000)
+    lens = rng.integers(0, 300, 300)
+    recs = [("q", bytes(res[int(off[i]):int(off[i]) + int(lens[i])])) for i in range(300)]
+    res, off = pack(recs)
     want = oracle_lib.process_batch(table, res, off)
     ctx.set_option("probe_variant", variant)
+    ctx.set_option("probe_j", probe_j)
     try:
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
     finally:
         ctx.set_option("probe_variant", 1)
+        ctx.set_option("probe_j", 5)
     assert_same(got, want, 300)
 
 
@@ -321,12 +329,16 @@ def test_device_queries_and_run_device(gpu, oracle_lib):
                 gpu.check(L_.kgx_memcpy_d2h(arr.ctypes.data, ptr, arr.nbytes), "d2h")
             hits = np.empty(int(wb[-1]), gpu.HIT_DTYPE)
             calls = np.empty(int(wb[-1]), gpu.CALL_DTYPE)
+            mask = np.empty((int(wb[-1]) + 63) // 64, np.uint64)
             gpu.check(L_.kgx_memcpy_d2h(hits.ctypes.data, out.hits, hits.nbytes), "d2h")
             gpu.check(L_.kgx_memcpy_d2h(calls.ctypes.data, out.calls, calls.nbytes), "d2h")
+            gpu.check(L_.kgx_memcpy_d2h(mask.ctypes.data, out.hit_mask, mask.nbytes), "d2h")
             want = oracle_lib.process_batch(table, hres, hoff)
             assert np.array_equal(np.diff(want.hit_offsets), hc)
             assert np.array_equal(np.diff(want.call_offsets), cc)
-            gh = np.concatenate([hits[wb[s]:wb[s] + hc[s]] for s in range(n)])
+            per_seq = gpu.tiled_hits_per_sequence(wb, mask, out.tile_windows, hits)
+            assert [len(x) for x in per_seq] == hc.tolist()
+            gh = np.concatenate(per_seq)
             gc = np.concatenate([calls[wb[s]:wb[s] + cc[s]] for s in range(n)])
             assert eq_fields(gh, want.hits)
             assert eq_fields(gc, want.calls, list(want.calls.dtype.names))
