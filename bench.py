@@ -168,7 +168,7 @@ def main():
                 step(times[v])
         ctx.set_option(name, vals[0])
         ctx.set_option("probe_variant", 1)
-        ctx.set_option("probe_j", 5)
+        ctx.set_option("probe_j", 4)
         probe_ab = {"option": name,
                     **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
                        for v, t in times.items()}}

@@ -32,7 +32,7 @@ constexpr int PROBE_WAVES = 4; /* waves per 256-thread workgroup */
 /* probe variants (kgx_ctx_set_option "probe_variant") */
 constexpr int PROBE_BUCKET = 0;    /* key + payload per bucket examined */
 constexpr int PROBE_KEY_FIRST = 1; /* keys only; payload for the matching bucket */
-constexpr int PROBE_J_DEFAULT = 5;
+constexpr int PROBE_J_DEFAULT = 4;
 
 /* floor((2^64-1)/n): x % n = x - umulhi(x, m)*n, corrected once (x < 2^35). */
 inline uint64_t mod_magic(uint64_t n) { return n ? (~0ULL) / n : 0; }

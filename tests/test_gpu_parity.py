@@ -115,7 +115,7 @@ def test_probe_variants_agree(small_world, oracle_lib, gpu, variant, probe_j):
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
     finally:
         ctx.set_option("probe_variant", 1)
-        ctx.set_option("probe_j", 5)
+        ctx.set_option("probe_j", 4)
     assert_same(got, want, 300)
 
 
