@@ -178,6 +178,8 @@ void KmerGuts::process_aa_batch(std::vector<SeqJob> &jobs)
                 j.otu_stats->otu_map[r.otus[i].otu_index] += r.otus[i].count;
             j.otu_stats->finalize(); /* process_aa_seq, kguts.cc:906-907 */
         }
+        if (j.on_done)
+            j.on_done();
     }
 }
 

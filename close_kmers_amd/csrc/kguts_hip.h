@@ -102,6 +102,10 @@ public:
         std::shared_ptr<std::vector<KmerCall>> calls;
         std::function<void(hit_in_sequence_t)> hit_cb;
         std::shared_ptr<KmerOtuStats> otu_stats;
+        /* runs after this job's hits / calls / OTU are delivered and before the
+         * next job's: the handler's per-sequence tail (e.g. the result block
+         * after process_aa_seq in lookup_request.cc:174-400) moves here */
+        std::function<void()> on_done;
     };
 
     /* kguts.cc:35-58: loads <dir>/function.index and <dir>/otu.index */
