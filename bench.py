@@ -12,7 +12,10 @@ image replica and its own query shard (weak scaling; no collective on the data
 path -- torch.distributed is used for the barrier and the max-time reduction).
 
 A step = one pass over the rank's resident batch: plan -> probe -> score
-(kgx_run_device), inputs and outputs in HBM.  The probe kernel is timed with
+(kgx_run_device), inputs and outputs in HBM.  Steps rotate over --pipeline
+worker contexts (own stream + buffers each, as the reference's thread pool
+keeps one KmerGuts per worker), so one batch's scoring overlaps the next
+batch's probe.  The probe kernel is timed with
 HIP events on the stream it runs on; the roofline uses SURVEY §8(d)'s
 algorithmic bytes per window, (24 * P + 1), with P the mean buckets examined
 per probed window measured by the CPU oracle on the rank-0 sample.
@@ -95,6 +98,9 @@ def main():
     ap.add_argument("--no-microbench", action="store_true")
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
+    ap.add_argument("--pipeline", type=int, default=2, help="worker contexts (streams) in flight")
+    ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
+                    help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
@@ -113,6 +119,10 @@ def main():
     img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs, device=dev)
     log(f"[bench] rank {d.rank}: built {stored} keys in {spec.num_sigs} buckets "
         f"({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
+    if args.image_layout == "aos":
+        img.set_layout(abi.Image.AOS24)
+    layout = ["AOS24", "PACKED16"][img.layout]
+    log(f"[bench] resident layout {layout}")
     ctx = abi.Context(img)
     n, Ls = args.n_seq, args.length
     n_res = n * Ls
@@ -132,22 +142,29 @@ def main():
     for e in ev:
         abi.check(L.kgx_event_create(ctypes.byref(e)), "event")
 
-    def step(timed_probe: list | None):
-        abi.check(L.kgx_stage_plan(ctx.handle, d_off, n, n_res), "plan")
+    # worker contexts: like the reference's thread pool (one KmerGuts per
+    # worker over one shared image, threadpool.cc:18-44), each has its own
+    # stream and buffers, so one worker's scoring overlaps the next worker's
+    # probe.  Every step is still a full pass over a whole batch.
+    ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
+
+    def step(timed_probe: list | None, c=ctx):
+        abi.check(L.kgx_stage_plan(c.handle, d_off, n, n_res), "plan")
         if timed_probe is not None:
-            abi.check(L.kgx_event_record(ev[0], ctx.handle), "event")
-        abi.check(L.kgx_stage_probe(ctx.handle, d_res, d_off), "probe")
+            abi.check(L.kgx_event_record(ev[0], c.handle), "event")
+        abi.check(L.kgx_stage_probe(c.handle, d_res, d_off), "probe")
         if timed_probe is not None:
-            abi.check(L.kgx_event_record(ev[1], ctx.handle), "event")
-        abi.check(L.kgx_stage_score(ctx.handle, ctypes.byref(params), want), "score")
+            abi.check(L.kgx_event_record(ev[1], c.handle), "event")
+        abi.check(L.kgx_stage_score(c.handle, ctypes.byref(params), want), "score")
         if timed_probe is not None:
             ms = ctypes.c_float()
             abi.check(L.kgx_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)), "elapsed")
             timed_probe.append(ms.value)
 
-    for _ in range(args.warmup):
-        step(None)
-    ctx.synchronize()
+    for i in range(args.warmup * len(ctxs)):
+        step(None, ctxs[i % len(ctxs)])
+    for c in ctxs:
+        c.synchronize()
 
     # probe-kernel duration (HIP events on the context's stream), untimed pass
     probe_ms: list = []
@@ -167,7 +184,7 @@ def main():
                 ctx.set_option(name, v)
                 step(times[v])
         ctx.set_option(name, vals[0])
-        ctx.set_option("probe_variant", 1)
+        ctx.set_option("probe_variant", -1)
         ctx.set_option("probe_j", 4)
         probe_ab = {"option": name,
                     **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
@@ -175,22 +192,21 @@ def main():
         log(f"[bench] probe A/B: {probe_ab}")
 
     d.barrier()
-    ctx.synchronize()
+    for c in ctxs:
+        c.synchronize()
     t_start = time.perf_counter()
-    abi.check(L.kgx_event_record(ev[2], ctx.handle), "event")
-    for _ in range(args.steps):
-        step(None)
-    abi.check(L.kgx_event_record(ev[3], ctx.handle), "event")
-    ctx.synchronize()
+    for i in range(args.steps):
+        step(None, ctxs[i % len(ctxs)])
+    for c in ctxs:
+        c.synchronize()
     d.barrier()
     t_wall = time.perf_counter() - t_start
-    ev_ms = ctypes.c_float()
-    abi.check(L.kgx_event_elapsed_ms(ev[2], ev[3], ctypes.byref(ev_ms)), "elapsed")
     t_max = d.max(t_wall)
+    last = ctxs[(args.steps - 1) % len(ctxs)]
 
     # sanity: counts of the last step
     out = abi.DeviceResult()
-    abi.check(L.kgx_device_result_get(ctx.handle, ctypes.byref(out)), "result")
+    abi.check(L.kgx_device_result_get(last.handle, ctypes.byref(out)), "result")
     hc = np.empty(n, np.uint32)
     cc = np.empty(n, np.uint32)
     abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
@@ -198,14 +214,15 @@ def main():
     total_hits = int(d.sum(float(hc.sum())))
     log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
         f"(planted mean {hc[::2].mean():.1f}, random mean {hc[1::2].mean():.2f}); "
-        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step, events {ev_ms.value / args.steps:.3f} ms/step, "
+        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts), "
         f"probe {np.mean(probe_ms):.3f} ms")
 
     ceiling = None
     if d.rank == 0 and not args.no_microbench:
         ceiling = {}
         n_reads = int(n * max(0, Ls - 8) * 1.4)
-        for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64)):
+        for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64),
+                                   (3, "rec16", 16)):
             ms, reads = ctypes.c_float(), ctypes.c_uint64()
             abi.check(L.kgx_microbench_random_read(ctx.handle, n_reads, mode, ctypes.byref(ms),
                                                    ctypes.byref(reads)), "microbench")  # warm
@@ -229,7 +246,8 @@ def main():
         L.kgx_event_destroy(e)
     L.kgx_device_free(d_res)
     L.kgx_device_free(d_off)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     img.close()
 
     if d.rank == 0:
@@ -246,7 +264,8 @@ def main():
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("n_keys") == n_keys and tj.get("n_seq") == n and tj.get("length") == Ls:
+                if (tj.get("n_keys") == n_keys and tj.get("n_seq") == n and tj.get("length") == Ls
+                        and tj.get("image_layout", "AOS24") == layout):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -270,6 +289,7 @@ def main():
                             f"{spec.num_sigs * 24 / 1e9:.1f} GB) resident in HBM",
                 "n_seq_per_gpu": n, "seq_len": Ls, "n_keys": n_keys, "keys_stored": stored,
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
+                "worker_contexts": len(ctxs),
                 "hits_total": total_hits,
                 "outputs": {3: "hits + calls (lookup_request, find_best_match)",
                             7: "hits + calls + OTU (add_request)"}.get(want, f"want={want}"),
@@ -287,8 +307,15 @@ def main():
                 "pbar": pbar,
                 "random_read_ceiling": ceiling,
                 "probe_ab": probe_ab,
-                "frac_of_random_bucket_ceiling": (achieved / 1e9 / ceiling["bucket24"]["useful_GBps"]
-                                                  if ceiling else None),
+                # SURVEY §8(d) prices a bucket at the file's 24 B; the PACKED16
+                # resident layout moves 16 B per bucket examined
+                "image_layout": layout,
+                "alg_bytes_per_launch_resident_layout": windows_per_launch * (
+                    (16.0 if layout == "PACKED16" else 24.0) * pbar + 1.0),
+                "frac_of_random_bucket_ceiling": (
+                    windows_per_launch * pbar / probe_s /
+                    ceiling["rec16" if layout == "PACKED16" else "bucket24"]["reads_per_s"]
+                    if ceiling else None),
             },
             "cpu_baseline": cpu,
         }

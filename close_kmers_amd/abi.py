@@ -99,6 +99,8 @@ SIGNATURES = {
     "kgx_image_num_sigs": (_U64, [_P]),
     "kgx_image_device": (_INT, [_P]),
     "kgx_image_table": (_P, [_P]),
+    "kgx_image_layout": (_INT, [_P]),
+    "kgx_image_set_layout": (_INT, [_P, _INT]),
     "kgx_image_download": (_INT, [_P, _P, _U64]),
     "kgx_ctx_create": (_INT, [_P, _PP]),
     "kgx_ctx_destroy": (_INT, [_P]),
@@ -224,6 +226,15 @@ class Image:
     @property
     def num_sigs(self) -> int:
         return lib().kgx_image_num_sigs(self.handle)
+
+    AOS24, PACKED16 = 0, 1
+
+    @property
+    def layout(self) -> int:
+        return lib().kgx_image_layout(self.handle)
+
+    def set_layout(self, layout: int) -> None:
+        check(lib().kgx_image_set_layout(self.handle, layout), "kgx_image_set_layout")
 
     def download(self) -> np.ndarray:
         t = np.empty(self.num_sigs, dtype=SIG_DTYPE)

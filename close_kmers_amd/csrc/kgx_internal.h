@@ -32,7 +32,69 @@ constexpr int PROBE_WAVES = 4; /* waves per 256-thread workgroup */
 /* probe variants (kgx_ctx_set_option "probe_variant") */
 constexpr int PROBE_BUCKET = 0;    /* key + payload per bucket examined */
 constexpr int PROBE_KEY_FIRST = 1; /* keys only; payload for the matching bucket */
+/* default: whole 16-B record for PACKED16, key first for AOS24 (the faster
+ * of the two on MI355X for each layout, interleaved A/B in bench.py) */
+constexpr int PROBE_AUTO = -1;
 constexpr int PROBE_J_DEFAULT = 4;
+
+/*
+ * HBM-resident bucket layouts.  The file's 24-byte bucket (kmer_image.h:11-23)
+ * straddles 64-byte sectors and needs a second dependent load for its payload;
+ * when the payload ranges allow, the image is kept as one 16-byte record per
+ * bucket at the SAME slot (so probe sequences and results are unchanged):
+ *   lo = key[0,35) | (fI+1)[35,55) | (otu+1)[0,9) at [55,64)
+ *   hi = function_wt bits[0,32) | avg_from_end[32,48) | (otu+1)[9,21) at [48,60)
+ * Keys above 20^8 (empty / stop buckets) are stored as EMPTY_KEY, which stops
+ * a probe exactly as the original does (kguts.cc:592); their payload is 0.
+ */
+struct packed_bucket {
+    uint64_t lo, hi;
+};
+constexpr uint64_t PACK_KEY_MASK = (1ull << 35) - 1;
+constexpr int64_t PACK_FI_MAX = (1ll << 20) - 2;  /* fI in [-1, PACK_FI_MAX] */
+constexpr int64_t PACK_OTU_MAX = (1ll << 21) - 2; /* otu in [-1, PACK_OTU_MAX] */
+
+__host__ __device__ inline bool packable(const kgx_sig_kmer &e)
+{
+    return e.which_kmer > MAX_ENCODED ||
+           (e.function_index >= -1 && e.function_index <= PACK_FI_MAX && e.otu_index >= -1 &&
+            e.otu_index <= PACK_OTU_MAX);
+}
+
+__host__ __device__ inline packed_bucket pack_bucket(const kgx_sig_kmer &e)
+{
+    packed_bucket b;
+    if (e.which_kmer > MAX_ENCODED) {
+        b.lo = EMPTY_KEY;
+        b.hi = 0;
+        return b;
+    }
+    uint32_t wt;
+    __builtin_memcpy(&wt, &e.function_wt, 4);
+    const uint64_t fi = (uint64_t)(e.function_index + 1), otu = (uint64_t)(e.otu_index + 1);
+    b.lo = e.which_kmer | (fi << 35) | ((otu & 0x1FFu) << 55);
+    b.hi = (uint64_t)wt | ((uint64_t)e.avg_from_end << 32) | ((otu >> 9) << 48);
+    return b;
+}
+
+__host__ __device__ inline kgx_sig_kmer unpack_bucket(const packed_bucket &b)
+{
+    kgx_sig_kmer e;
+    e.which_kmer = b.lo & PACK_KEY_MASK;
+    e.otu_index = (int32_t)(((b.lo >> 55) & 0x1FFu) | (((b.hi >> 48) & 0xFFFu) << 9)) - 1;
+    e.avg_from_end = (uint16_t)(b.hi >> 32);
+    e.pad = 0;
+    e.function_index = (int32_t)((b.lo >> 35) & 0xFFFFFu) - 1;
+    const uint32_t wt = (uint32_t)b.hi;
+    __builtin_memcpy(&e.function_wt, &wt, 4);
+    if (e.which_kmer > MAX_ENCODED) {
+        e.otu_index = 0;
+        e.avg_from_end = 0;
+        e.function_index = 0;
+        e.function_wt = 0.0f;
+    }
+    return e;
+}
 
 /* floor((2^64-1)/n): x % n = x - umulhi(x, m)*n, corrected once (x < 2^35). */
 inline uint64_t mod_magic(uint64_t n) { return n ? (~0ULL) / n : 0; }
@@ -45,9 +107,14 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase,
                        uint32_t tile_windows, void *workspace, hipStream_t stream);
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
-                        uint64_t max_tiles, const kgx_sig_kmer *table, uint64_t num_sigs,
+                        uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream);
+/* AoS -> packed; *not_packable |= 1 when some stored bucket does not fit */
+hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_t n,
+                       uint32_t *not_packable, hipStream_t stream);
+hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_t n,
+                         hipStream_t stream);
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                         uint32_t tile_windows, kgx_hit *hits, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
@@ -57,7 +124,7 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
                          hipStream_t stream);
-hipError_t launch_random_read(const kgx_sig_kmer *table, uint64_t num_sigs, uint64_t threads,
+hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
                               uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream);
 hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
                               unsigned long long *n_stored, hipStream_t stream);

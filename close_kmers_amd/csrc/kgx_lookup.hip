@@ -142,17 +142,28 @@ __device__ __forceinline__ uint3 load_residues(uintptr_t ab, uintptr_t lo, uintp
  * sequence, reads the 8 residues straight from the batch (one 16-byte load),
  * maps them to codes through a 256-byte LDS table, and issues all J first
  * probes before resolving any.
- *   KEY_FIRST = false: each probe round loads key and payload of its bucket;
- *   KEY_FIRST = true: rounds load keys only; the matching bucket's payload is
- *     loaded in the round that finds it (mostly the key's sector, in L2).
+ *   MODE_BUCKET: each probe round loads key and payload of its 24-B bucket;
+ *   MODE_KEY_FIRST: rounds load keys only; the matching bucket's payload is
+ *     loaded in the round that finds it (mostly the key's sector, in L2);
+ *   MODE_PACKED: PACKED16 images -- one aligned 16-B load per bucket gives
+ *     key and payload (never straddles a sector; 4 buckets per sector);
+ *   MODE_PACKED_KEY_FIRST: the record's low word (key, fI, otu bits) per
+ *     bucket, its high word only for the match (same sector).
  */
-template <int J, bool KEY_FIRST>
+constexpr int MODE_BUCKET = 0, MODE_KEY_FIRST = 1, MODE_PACKED = 2, MODE_PACKED_KEY_FIRST = 3;
+
+template <int J, int MODE>
 __global__ __launch_bounds__(256) void probe_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
-    const kgx_sig_kmer *__restrict__ table, uint64_t num_sigs, uint64_t magic,
+    const void *__restrict__ table_v, uint64_t num_sigs, uint64_t magic,
     kgx_hit *__restrict__ hits, uint64_t *__restrict__ hit_mask)
 {
+    constexpr bool KEY_FIRST = MODE == MODE_KEY_FIRST;
+    constexpr bool PACKED = MODE == MODE_PACKED || MODE == MODE_PACKED_KEY_FIRST;
+    const uint64_t *__restrict__ packed_w = static_cast<const uint64_t *>(table_v);
+    const kgx_sig_kmer *__restrict__ table = static_cast<const kgx_sig_kmer *>(table_v);
+    const uint4 *__restrict__ packed = static_cast<const uint4 *>(table_v);
     constexpr uint32_t T = 64 * J;
     __shared__ uint8_t code_tab[256];
     code_tab[threadIdx.x] = (uint8_t)residue_code(threadIdx.x);
@@ -211,10 +222,20 @@ __global__ __launch_bounds__(256) void probe_kernel(
         kv[j] = 0;
         pv[j] = make_uint4(0, 0, 0, 0);
         if (ok) {
-            const kgx_sig_kmer *e = table + slot[j];
-            kv[j] = e->which_kmer;
-            if (!KEY_FIRST)
-                pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+            if (MODE == MODE_PACKED) {
+                pv[j] = packed[slot[j]];
+                kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
+            } else if (MODE == MODE_PACKED_KEY_FIRST) {
+                const uint64_t lo = packed_w[2 * slot[j]];
+                pv[j].x = (uint32_t)lo;
+                pv[j].y = (uint32_t)(lo >> 32);
+                kv[j] = lo & PACK_KEY_MASK;
+            } else {
+                const kgx_sig_kmer *e = table + slot[j];
+                kv[j] = e->which_kmer;
+                if (!KEY_FIRST)
+                    pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+            }
         }
     }
 
@@ -231,14 +252,29 @@ __global__ __launch_bounds__(256) void probe_kernel(
                     if (KEY_FIRST)
                         pv[j] = *reinterpret_cast<const uint4 *>(
                             reinterpret_cast<const char *>(table + slot[j]) + 8);
+                    if (MODE == MODE_PACKED_KEY_FIRST) {
+                        const uint64_t hi = packed_w[2 * slot[j] + 1];
+                        pv[j].z = (uint32_t)hi;
+                        pv[j].w = (uint32_t)(hi >> 32);
+                    }
                 } else if (kv[j] > MAX_ENCODED || round + 1 >= num_sigs) {
                     pend[j] = false;
                 } else {
                     slot[j] = (slot[j] + 1 == num_sigs) ? 0 : slot[j] + 1;
-                    const kgx_sig_kmer *e = table + slot[j];
-                    kv[j] = e->which_kmer;
-                    if (!KEY_FIRST)
-                        pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                    if (MODE == MODE_PACKED) {
+                        pv[j] = packed[slot[j]];
+                        kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
+                    } else if (MODE == MODE_PACKED_KEY_FIRST) {
+                        const uint64_t lo = packed_w[2 * slot[j]];
+                        pv[j].x = (uint32_t)lo;
+                        pv[j].y = (uint32_t)(lo >> 32);
+                        kv[j] = lo & PACK_KEY_MASK;
+                    } else {
+                        const kgx_sig_kmer *e = table + slot[j];
+                        kv[j] = e->which_kmer;
+                        if (!KEY_FIRST)
+                            pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                    }
                     more = true;
                 }
             }
@@ -254,8 +290,16 @@ __global__ __launch_bounds__(256) void probe_kernel(
         const uint64_t m = __ballot(hit[j]);
         if (hit[j]) {
             uint4 *d = reinterpret_cast<uint4 *>(hits + g0 + count + lanes_below(m));
-            d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, pv[j].y & 0xFFFFu);
-            d[1] = make_uint4(pv[j].z, pv[j].w, pos[j], sq[j]);
+            if (PACKED) {
+                /* unpack_bucket (kgx_internal.h) of the record in pv */
+                const uint32_t otu = ((pv[j].y >> 23) & 0x1FFu) | (((pv[j].w >> 16) & 0xFFFu) << 9);
+                const uint32_t fi = (pv[j].y >> 3) & 0xFFFFFu;
+                d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), otu - 1u, pv[j].w & 0xFFFFu);
+                d[1] = make_uint4(fi - 1u, pv[j].z, pos[j], sq[j]);
+            } else {
+                d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, pv[j].y & 0xFFFFu);
+                d[1] = make_uint4(pv[j].z, pv[j].w, pos[j], sq[j]);
+            }
         }
         if (lane == 0 && g0 + 64 * j < W)
             hit_mask[(g0 >> 6) + j] = m;
@@ -264,37 +308,94 @@ __global__ __launch_bounds__(256) void probe_kernel(
 }
 
 template <int J>
-static void launch_probe_j(dim3 grid, hipStream_t stream, int variant, const uint8_t *residues,
+static void launch_probe_j(dim3 grid, hipStream_t stream, int mode, const uint8_t *residues,
                            uint64_t n_residues, const uint64_t *seq_off, const uint64_t *wbase,
-                           const uint32_t *tile_seq, uint32_t n_seq, const kgx_sig_kmer *table,
+                           const uint32_t *tile_seq, uint32_t n_seq, const void *table,
                            uint64_t num_sigs, kgx_hit *hits, uint64_t *hit_mask)
 {
-    if (variant == PROBE_KEY_FIRST)
-        hipLaunchKernelGGL((probe_kernel<J, true>), grid, dim3(64 * PROBE_WAVES), 0, stream,
+    const uint64_t magic = mod_magic(num_sigs);
+    if (mode == MODE_PACKED_KEY_FIRST)
+        hipLaunchKernelGGL((probe_kernel<J, MODE_PACKED_KEY_FIRST>), grid, dim3(64 * PROBE_WAVES), 0,
+                           stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table,
+                           num_sigs, magic, hits, hit_mask);
+    else if (mode == MODE_PACKED)
+        hipLaunchKernelGGL((probe_kernel<J, MODE_PACKED>), grid, dim3(64 * PROBE_WAVES), 0, stream,
                            residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
-                           mod_magic(num_sigs), hits, hit_mask);
+                           magic, hits, hit_mask);
+    else if (mode == MODE_KEY_FIRST)
+        hipLaunchKernelGGL((probe_kernel<J, MODE_KEY_FIRST>), grid, dim3(64 * PROBE_WAVES), 0, stream,
+                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
+                           magic, hits, hit_mask);
     else
-        hipLaunchKernelGGL((probe_kernel<J, false>), grid, dim3(64 * PROBE_WAVES), 0, stream,
+        hipLaunchKernelGGL((probe_kernel<J, MODE_BUCKET>), grid, dim3(64 * PROBE_WAVES), 0, stream,
                            residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
-                           mod_magic(num_sigs), hits, hit_mask);
+                           magic, hits, hit_mask);
 }
 
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
-                        uint64_t max_tiles, const kgx_sig_kmer *table, uint64_t num_sigs,
+                        uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream)
 {
     if (max_tiles == 0)
         return hipSuccess;
     const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+    const bool kf = variant == PROBE_AUTO ? layout != KGX_LAYOUT_PACKED16 : variant == PROBE_KEY_FIRST;
+    const int mode = layout == KGX_LAYOUT_PACKED16 ? (kf ? MODE_PACKED_KEY_FIRST : MODE_PACKED)
+                                                   : (kf ? MODE_KEY_FIRST : MODE_BUCKET);
+#define KGX_PROBE_J(JJ)                                                                              \
+    launch_probe_j<JJ>(grid, stream, mode, residues, n_residues, seq_off, wbase, tile_seq, n_seq,   \
+                       table, num_sigs, hits, hit_mask)
     switch (probe_j) {
-    case 2: launch_probe_j<2>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
-    case 4: launch_probe_j<4>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
-    case 5: launch_probe_j<5>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
-    case 8: launch_probe_j<8>(grid, stream, variant, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, hits, hit_mask); break;
+    case 2: KGX_PROBE_J(2); break;
+    case 4: KGX_PROBE_J(4); break;
+    case 5: KGX_PROBE_J(5); break;
+    case 8: KGX_PROBE_J(8); break;
     default: return hipErrorInvalidValue;
     }
+#undef KGX_PROBE_J
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* resident layout conversion                                                */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(256) void pack_kernel(const kgx_sig_kmer *__restrict__ table,
+                                                   packed_bucket *__restrict__ packed, uint64_t n,
+                                                   uint32_t *not_packable)
+{
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const kgx_sig_kmer e = table[i];
+        bad |= !packable(e);
+        packed[i] = pack_bucket(e);
+    }
+    if (__any(bad) && lane_id() == 0)
+        atomicOr(not_packable, 1u);
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const packed_bucket *__restrict__ packed,
+                                                     kgx_sig_kmer *__restrict__ out, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = unpack_bucket(packed[i]);
+}
+
+hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_t n,
+                       uint32_t *not_packable, hipStream_t stream)
+{
+    hipLaunchKernelGGL(pack_kernel, dim3(8192), dim3(256), 0, stream, table, packed, n, not_packable);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_t n,
+                         hipStream_t stream)
+{
+    hipLaunchKernelGGL(unpack_kernel, dim3(8192), dim3(256), 0, stream, packed, out, n);
     return hipGetLastError();
 }
 

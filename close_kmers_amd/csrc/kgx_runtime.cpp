@@ -82,7 +82,17 @@ uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 struct kgx_image {
     int device = 0;
     uint64_t num_sigs = 0;
-    kgx_sig_kmer *d_table = nullptr;
+    int layout = KGX_LAYOUT_AOS24;
+    kgx_sig_kmer *d_table = nullptr;   /* AOS24: the file's buckets */
+    packed_bucket *d_packed = nullptr; /* PACKED16 */
+    const void *resident() const
+    {
+        return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
+    }
+    uint64_t resident_bytes() const
+    {
+        return num_sigs * (layout == KGX_LAYOUT_PACKED16 ? sizeof(packed_bucket) : sizeof(kgx_sig_kmer));
+    }
 };
 
 struct kgx_ctx {
@@ -99,7 +109,7 @@ struct kgx_ctx {
     uint32_t tile_windows = 64u * PROBE_J_DEFAULT;
     const uint64_t *d_off = nullptr;
     /* tuning options */
-    int probe_variant = PROBE_KEY_FIRST;
+    int probe_variant = PROBE_AUTO;
     int probe_j = PROBE_J_DEFAULT;
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
@@ -212,6 +222,78 @@ static int image_alloc(int device, uint64_t num_sigs, kgx_image **out)
     return KGX_OK;
 }
 
+/* AOS24 -> PACKED16 on the device; KGX_ERANGE (image unchanged) when some
+ * stored bucket's payload does not fit the packed record */
+static int image_pack(kgx_image *img)
+{
+    if (img->layout == KGX_LAYOUT_PACKED16)
+        return KGX_OK;
+    HIP_TRY(hipSetDevice(img->device));
+    packed_bucket *p = nullptr;
+    uint32_t *flag = nullptr;
+    if (hipMalloc(&p, img->num_sigs * sizeof(packed_bucket)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(KGX_ENOMEM, "no room for the packed table");
+    }
+    uint32_t bad = 0;
+    hipError_t e = hipMalloc(&flag, sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipMemset(flag, 0, sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = launch_pack(img->d_table, p, img->num_sigs, flag, nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(&bad, flag, sizeof(bad), hipMemcpyDeviceToHost);
+    if (flag)
+        (void)hipFree(flag);
+    if (e != hipSuccess || bad) {
+        (void)hipFree(p);
+        if (e != hipSuccess)
+            return fail(KGX_EDEVICE, std::string("pack: ") + hipGetErrorString(e));
+        return fail(KGX_ERANGE, "image payloads do not fit the packed layout");
+    }
+    (void)hipFree(img->d_table);
+    img->d_table = nullptr;
+    img->d_packed = p;
+    img->layout = KGX_LAYOUT_PACKED16;
+    return KGX_OK;
+}
+
+static int image_unpack(kgx_image *img)
+{
+    if (img->layout == KGX_LAYOUT_AOS24)
+        return KGX_OK;
+    HIP_TRY(hipSetDevice(img->device));
+    kgx_sig_kmer *t = nullptr;
+    if (hipMalloc(&t, img->num_sigs * sizeof(kgx_sig_kmer)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(KGX_ENOMEM, "no room for the 24-byte table");
+    }
+    hipError_t e = launch_unpack(img->d_packed, t, img->num_sigs, nullptr);
+    if (e == hipSuccess)
+        e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(t);
+        return fail(KGX_EDEVICE, std::string("unpack: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(img->d_packed);
+    img->d_packed = nullptr;
+    img->d_table = t;
+    img->layout = KGX_LAYOUT_AOS24;
+    return KGX_OK;
+}
+
+/* images are packed at load when they fit; otherwise they stay AOS24 */
+static int image_settle(kgx_image *img, kgx_image **out)
+{
+    const int rc = image_pack(img);
+    if (rc == KGX_EDEVICE) {
+        kgx_image_close(img);
+        return rc;
+    }
+    *out = img;
+    return KGX_OK;
+}
+
 /* KmerImage::map_image_file validation, kmer_image.cc:128-147 */
 static int validate_header(const kgx_image_header &h, uint64_t file_size)
 {
@@ -299,8 +381,7 @@ int kgx_image_open(const char *dir, int device, kgx_image **out)
         kgx_image_close(img);
         return fail(KGX_EIO, "short read of " + path);
     }
-    *out = img;
-    return KGX_OK;
+    return image_settle(img, out);
 }
 
 int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, kgx_image **out)
@@ -322,8 +403,7 @@ int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, k
         kgx_image_close(img);
         return fail(KGX_EDEVICE, std::string("image upload: ") + hipGetErrorString(e));
     }
-    *out = img;
-    return KGX_OK;
+    return image_settle(img, out);
 }
 
 int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kgx_image **out,
@@ -351,18 +431,18 @@ int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kg
     }
     if (n_stored)
         *n_stored = cnt;
-    *out = img;
-    return KGX_OK;
+    return image_settle(img, out);
 }
 
 int kgx_image_close(kgx_image *img)
 {
     if (!img)
         return KGX_OK;
-    if (img->d_table) {
-        (void)hipSetDevice(img->device);
+    (void)hipSetDevice(img->device);
+    if (img->d_table)
         (void)hipFree(img->d_table);
-    }
+    if (img->d_packed)
+        (void)hipFree(img->d_packed);
     delete img;
     return KGX_OK;
 }
@@ -370,13 +450,43 @@ int kgx_image_close(kgx_image *img)
 uint64_t kgx_image_num_sigs(const kgx_image *img) { return img ? img->num_sigs : 0; }
 int kgx_image_device(const kgx_image *img) { return img ? img->device : -1; }
 const void *kgx_image_table(const kgx_image *img) { return img ? img->d_table : nullptr; }
+int kgx_image_layout(const kgx_image *img) { return img ? img->layout : -1; }
+
+int kgx_image_set_layout(kgx_image *img, int layout)
+{
+    if (!img)
+        return fail(KGX_EINVAL, "null image");
+    if (layout == KGX_LAYOUT_PACKED16)
+        return image_pack(img);
+    if (layout == KGX_LAYOUT_AOS24)
+        return image_unpack(img);
+    return fail(KGX_EINVAL, "unknown layout " + std::to_string(layout));
+}
 
 int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes)
 {
     if (!img || !dst || nbytes != img->num_sigs * sizeof(kgx_sig_kmer))
         return fail(KGX_EINVAL, "bad download buffer");
     HIP_TRY(hipSetDevice(img->device));
-    HIP_TRY(hipMemcpy(dst, img->d_table, nbytes, hipMemcpyDeviceToHost));
+    if (img->layout == KGX_LAYOUT_AOS24) {
+        HIP_TRY(hipMemcpy(dst, img->d_table, nbytes, hipMemcpyDeviceToHost));
+        return KGX_OK;
+    }
+    /* PACKED16: unpack slices on the device, then copy them out */
+    const uint64_t slice = 1ull << 24; /* buckets (384 MiB of output) */
+    kgx_sig_kmer *tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, std::min(slice, img->num_sigs) * sizeof(kgx_sig_kmer)));
+    hipError_t e = hipSuccess;
+    for (uint64_t b = 0; b < img->num_sigs && e == hipSuccess; b += slice) {
+        const uint64_t n = std::min(slice, img->num_sigs - b);
+        e = launch_unpack(img->d_packed + b, tmp, n, nullptr);
+        if (e == hipSuccess)
+            e = hipMemcpy(static_cast<kgx_sig_kmer *>(dst) + b, tmp, n * sizeof(kgx_sig_kmer),
+                          hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(tmp);
+    if (e != hipSuccess)
+        return fail(KGX_EDEVICE, std::string("download: ") + hipGetErrorString(e));
     return KGX_OK;
 }
 
@@ -439,8 +549,8 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         return fail(KGX_EINVAL, "null argument");
     const std::string n = name;
     if (n == "probe_variant") {
-        if (value != PROBE_BUCKET && value != PROBE_KEY_FIRST)
-            return fail(KGX_EINVAL, "probe_variant must be 0 or 1");
+        if (value != PROBE_AUTO && value != PROBE_BUCKET && value != PROBE_KEY_FIRST)
+            return fail(KGX_EINVAL, "probe_variant must be -1, 0 or 1");
         c->probe_variant = (int)value;
         return KGX_OK;
     }
@@ -501,8 +611,8 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     if (c->img->num_sigs >= (1ull << 40))
         return fail(KGX_ERANGE, "image too large");
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
-                         c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->d_table,
-                         c->img->num_sigs, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
+                         c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
+                         c->img->layout, c->img->num_sigs, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
                          (int)(c->tile_windows / 64), c->probe_variant, c->stream));
     return KGX_OK;
 }
@@ -697,7 +807,7 @@ int kgx_synth_queries(kgx_ctx *c, uint64_t image_n_keys, uint32_t n_seq, uint32_
 
 int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms, uint64_t *reads)
 {
-    if (!c || !ms || mode < 0 || mode > 2)
+    if (!c || !ms || mode < 0 || mode > 3)
         return fail(KGX_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(c->img->device));
     const uint64_t threads = 256ull * 256 * 8; /* 8 workgroups of 256 per CU */
@@ -707,7 +817,7 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     HIP_TRY(hipEventCreate(&a));
     HIP_TRY(hipEventCreate(&b));
     HIP_TRY(hipEventRecord(a, c->stream));
-    HIP_TRY(launch_random_read(c->img->d_table, c->img->num_sigs, threads, rounds, mode,
+    HIP_TRY(launch_random_read(c->img->resident(), c->img->resident_bytes(), threads, rounds, mode,
                                c->plan_ws.as<uint64_t>(), c->stream));
     HIP_TRY(hipEventRecord(b, c->stream));
     HIP_TRY(hipEventSynchronize(b));

@@ -16,19 +16,23 @@ namespace kgx {
 /* random-read ceiling of the image buffer (roofline denominator)            */
 /* ------------------------------------------------------------------------ */
 
-/* Every lane reads RR_ILP independent uniformly random buckets per round:
- * mode 0 the whole 24-byte bucket (8-byte key + 16-byte payload, as the probe
- * does), mode 1 the 8-byte key only, mode 2 one aligned 64-byte sector. */
+/* Every lane reads RR_ILP independent uniformly random records of the
+ * resident image buffer per round: mode 0 a whole 24-byte bucket (8-byte key
+ * + 16-byte payload, as the AOS24 probe does), mode 1 the 8-byte key of a
+ * 24-byte bucket, mode 2 one aligned 64-byte sector, mode 3 one aligned
+ * 16-byte record (as the PACKED16 probe does). */
 constexpr int RR_ILP = 8;
 
+__host__ __device__ constexpr uint64_t rr_stride(int mode) { return mode == 2 ? 64 : mode == 3 ? 16 : 24; }
+
 template <int MODE>
-__global__ __launch_bounds__(256) void random_read_kernel(const kgx_sig_kmer *__restrict__ t,
-                                                          uint64_t n, uint64_t magic,
-                                                          uint32_t rounds, uint64_t *sink)
+__global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict__ base, uint64_t n,
+                                                          uint64_t magic, uint32_t rounds,
+                                                          uint64_t *sink)
 {
+    constexpr uint64_t S = rr_stride(MODE);
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t acc = 0;
-    const char *base = reinterpret_cast<const char *>(t);
     for (uint32_t r = 0; r < rounds; r++) {
         uint64_t idx[RR_ILP];
 #pragma unroll
@@ -38,23 +42,27 @@ __global__ __launch_bounds__(256) void random_read_kernel(const kgx_sig_kmer *__
         uint4 pv[RR_ILP], pw[RR_ILP], px[RR_ILP];
 #pragma unroll
         for (int k = 0; k < RR_ILP; k++) {
+            const char *rec = base + idx[k] * S;
             if (MODE == 0) {
-                kv[k] = t[idx[k]].which_kmer;
-                pv[k] = *reinterpret_cast<const uint4 *>(base + idx[k] * 24 + 8);
+                kv[k] = *reinterpret_cast<const uint64_t *>(rec);
+                pv[k] = *reinterpret_cast<const uint4 *>(rec + 8);
             } else if (MODE == 1) {
-                kv[k] = t[idx[k]].which_kmer;
+                kv[k] = *reinterpret_cast<const uint64_t *>(rec);
+            } else if (MODE == 2) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(rec);
+                pv[k] = q[0];
+                pw[k] = q[1];
+                px[k] = q[2];
+                kv[k] = *reinterpret_cast<const uint64_t *>(q + 3);
             } else {
-                const uint4 *s = reinterpret_cast<const uint4 *>(base + ((idx[k] * 24) & ~63ull));
-                pv[k] = s[0];
-                pw[k] = s[1];
-                px[k] = s[2];
-                kv[k] = *reinterpret_cast<const uint64_t *>(s + 3);
+                pv[k] = *reinterpret_cast<const uint4 *>(rec);
+                kv[k] = pv[k].y;
             }
         }
 #pragma unroll
         for (int k = 0; k < RR_ILP; k++) {
             acc ^= kv[k];
-            if (MODE == 0)
+            if (MODE == 0 || MODE == 3)
                 acc += pv[k].x ^ pv[k].w;
             if (MODE == 2)
                 acc += pv[k].x ^ pw[k].y ^ px[k].z;
@@ -63,17 +71,19 @@ __global__ __launch_bounds__(256) void random_read_kernel(const kgx_sig_kmer *__
     sink[tid] = acc;
 }
 
-hipError_t launch_random_read(const kgx_sig_kmer *table, uint64_t num_sigs, uint64_t threads,
+hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
                               uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream)
 {
     const dim3 grid((uint32_t)(threads / 256)), block(256);
-    const uint64_t m = mod_magic(num_sigs);
-    if (mode == 0)
-        hipLaunchKernelGGL(random_read_kernel<0>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
-    else if (mode == 1)
-        hipLaunchKernelGGL(random_read_kernel<1>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
-    else
-        hipLaunchKernelGGL(random_read_kernel<2>, grid, block, 0, stream, table, num_sigs, m, rounds, sink);
+    const char *b = static_cast<const char *>(buffer);
+    const uint64_t n = bytes / rr_stride(mode), m = mod_magic(n);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(random_read_kernel<0>, grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 1: hipLaunchKernelGGL(random_read_kernel<1>, grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 2: hipLaunchKernelGGL(random_read_kernel<2>, grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 3: hipLaunchKernelGGL(random_read_kernel<3>, grid, block, 0, stream, b, n, m, rounds, sink); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -169,9 +169,22 @@ int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kg
 int kgx_image_close(kgx_image *img);
 uint64_t kgx_image_num_sigs(const kgx_image *img);
 int kgx_image_device(const kgx_image *img);
-/* device pointer to the num_sigs * 24-byte table */
+/* HBM-resident layouts.  The file format is never changed; in HBM an image
+ * is kept either as the file's 24-byte buckets (AOS24) or, when every stored
+ * bucket has function_index in [-1, 2^20-2] and otu_index in [-1, 2^21-2],
+ * as one 16-byte record per bucket at the same slot (PACKED16: one aligned
+ * load per bucket examined; 2/3 of the memory).  Lookups give identical
+ * results in both.  Images are packed at load when they fit. */
+enum { KGX_LAYOUT_AOS24 = 0, KGX_LAYOUT_PACKED16 = 1 };
+int kgx_image_layout(const kgx_image *img);
+/* convert the resident table in place; KGX_ERANGE if PACKED16 is asked for
+ * an image whose payloads do not fit (the image is left unchanged) */
+int kgx_image_set_layout(kgx_image *img, int layout);
+/* device pointer to the num_sigs * 24-byte table; NULL while PACKED16 */
 const void *kgx_image_table(const kgx_image *img);
-/* copy the table (num_sigs * 24 bytes) to host memory */
+/* copy the table as the file's num_sigs * 24-byte buckets to host memory
+ * (from PACKED16: pad fields read 0; buckets with a key above 20^8 read as
+ * {20^8+1, 0, 0, 0, 0, 0.0}) */
 int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes);
 
 /* ---- contexts: one per host thread, like one KmerGuts per pool thread --- */
@@ -180,8 +193,10 @@ int kgx_ctx_destroy(kgx_ctx *ctx);
 /* the HIP stream the context launches on (hipStream_t) */
 void *kgx_ctx_stream(kgx_ctx *ctx);
 /* tuning knobs (results never change): "probe_variant" 0 = load key and
- * payload of every bucket examined, 1 = keys first, payload of the matching
- * bucket only (default); "probe_j" = windows per lane (2, 4, 5 or 8; a tile
+ * payload of every bucket examined, 1 = keys first (the 8-byte key, or the
+ * packed record's low word), payload of the matching bucket only; -1 =
+ * the faster one for the image's layout (default: 0 for PACKED16, 1 for AOS24);
+ * "probe_j" = windows per lane (2, 4, 5 or 8; a tile
  * is 64 * probe_j windows), read at the next plan */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */

@@ -44,7 +44,7 @@ def main():
     pw, nw = mean_of(write, is_probe)
     calib = {}
     ceil = (bench.get("roofline") or {}).get("random_read_ceiling") or {}
-    for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64")):
+    for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64"), (3, "rec16")):
         b, n = mean_of(fetch, lambda k, m=mode: f"random_read_kernel<{m}>" in k)
         reads = (ceil.get(name) or {}).get("reads")
         if b is not None and reads:
@@ -52,6 +52,7 @@ def main():
     cfg = bench["config"]
     out = {
         "n_keys": cfg["n_keys"], "n_seq": cfg["n_seq_per_gpu"], "length": cfg["seq_len"],
+        "image_layout": (bench.get("roofline") or {}).get("image_layout", "AOS24"),
         "fetch_bytes_per_launch": pf, "write_bytes_per_launch": pw,
         "hbm_bytes_per_launch": (pf or 0) + (pw or 0) if pf is not None else None,
         "probe_dispatches": {"fetch": nf, "write": nw},

@@ -98,25 +98,122 @@ def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params):
     assert got.n_windows >= want.windows
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.fixture(scope="module")
+def aos_world(small_world, gpu):
+    """The same table kept in the file's 24-byte layout."""
+    spec, table, _, _ = small_world
+    img = gpu.Image.from_table(table)
+    img.set_layout(gpu.Image.AOS24)
+    ctx = gpu.Context(img)
+    yield img, ctx
+    ctx.close()
+    img.close()
+
+
+@pytest.mark.parametrize("mode", ["packed_record", "packed_key_first", "aos_bucket", "aos_key_first"])
 @pytest.mark.parametrize("probe_j", [2, 4, 5, 8])
-def test_probe_variants_agree(small_world, oracle_lib, gpu, variant, probe_j):
+def test_probe_variants_agree(small_world, aos_world, oracle_lib, gpu, mode, probe_j):
     spec, table, img, ctx = small_world
+    assert img.layout == gpu.Image.PACKED16
+    if mode.startswith("aos"):
+        img, ctx = aos_world
+        assert img.layout == gpu.Image.AOS24
     # mixed lengths so tiles straddle many sequence boundaries
-    rng = np.random.default_rng(probe_j * 10 + variant)
+    rng = np.random.default_rng(probe_j * 10 + len(mode))
     res, off = synth.make_queries(spec, 300, x_permille=5, q0=1000)
     lens = rng.integers(0, 300, 300)
     recs = [("q", bytes(res[int(off[i]):int(off[i]) + int(lens[i])])) for i in range(300)]
     res, off = pack(recs)
     want = oracle_lib.process_batch(table, res, off)
-    ctx.set_option("probe_variant", variant)
+    ctx.set_option("probe_variant", 1 if mode.endswith("key_first") else 0)
     ctx.set_option("probe_j", probe_j)
     try:
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
     finally:
-        ctx.set_option("probe_variant", 1)
+        ctx.set_option("probe_variant", -1)
         ctx.set_option("probe_j", 4)
     assert_same(got, want, 300)
+
+
+def _occupied_equal(a, b):
+    oa, ob = a[a["which_kmer"] <= 20 ** 8], b[b["which_kmer"] <= 20 ** 8]
+    assert np.array_equal(a["which_kmer"] <= 20 ** 8, b["which_kmer"] <= 20 ** 8)
+    for fld in ["which_kmer", "otu_index", "avg_from_end", "function_index"]:
+        assert np.array_equal(oa[fld], ob[fld]), fld
+    assert np.array_equal(oa["function_wt"].view(np.uint32), ob["function_wt"].view(np.uint32))
+
+
+def test_resident_layout_round_trip(small_world, gpu):
+    spec, table, img, ctx = small_world
+    assert img.layout == gpu.Image.PACKED16
+    d = img.download()
+    _occupied_equal(d, table)
+    emp = d[d["which_kmer"] > 20 ** 8]
+    assert (emp["which_kmer"] == 20 ** 8 + 1).all() and (emp["function_index"] == 0).all()
+    assert (d["pad"] == 0).all()
+    with gpu.Image.from_table(table) as im2:
+        im2.set_layout(gpu.Image.AOS24)
+        assert im2.layout == gpu.Image.AOS24
+        assert np.array_equal(im2.download().view(np.uint8), table.view(np.uint8))
+        im2.set_layout(gpu.Image.PACKED16)
+        _occupied_equal(im2.download(), table)
+
+
+@pytest.mark.parametrize("fi,otu,packs", [
+    (-1, -1, True), ((1 << 20) - 2, (1 << 21) - 2, True), (0, 0, True),
+    ((1 << 20) - 1, 0, False), (0, (1 << 21) - 1, False), (-2, 0, False), (0, -7, False),
+    (2 ** 31 - 1, 2 ** 31 - 1, False)])
+def test_payload_ranges_pick_the_layout(gpu, oracle_lib, fi, otu, packs):
+    """Boundary payloads: packed when they fit, the 24-byte layout otherwise;
+    lookups identical to the oracle either way."""
+    rng = np.random.default_rng(abs(fi) % 97 + abs(otu) % 89)
+    img = DesignedImage()
+    recs = []
+    for t in range(20):
+        s = random_protein(rng, 200)
+        img.add_windows(s, range(10, 60), fI=t % 3, oI=t % 4 - 1, rng=rng, avg=7)
+        recs.append((f"s{t}", s))
+    img.add(recs[0][1][100:108], fi, otu, 65535, -0.0)  # extreme payload, also hit
+    img.add(recs[1][1][100:108], fi, otu, 1, float("inf"))
+    table = img.table()
+    res, off = pack(recs)
+    with gpu.Image.from_table(table) as im, gpu.Context(im) as ctx:
+        assert im.layout == (gpu.Image.PACKED16 if packs else gpu.Image.AOS24)
+        _occupied_equal(im.download(), table)
+        for params in [(5, 200, 0, 0), (1, 200, 0, 0)]:
+            want = oracle_lib.process_batch(table, res, off, params=params)
+            got = ctx.process_batch(res, off, gpu.Params(*params))
+            assert_same(got, want, len(recs))
+        if not packs:
+            with pytest.raises(Exception):
+                im.set_layout(gpu.Image.PACKED16)
+            assert im.layout == gpu.Image.AOS24
+
+
+def test_stray_keys_above_max_stop_probes(gpu, oracle_lib):
+    """Any key > 20^8 ends a probe (kguts.cc:592), not just the 20^8+1 sentinel."""
+    rng = np.random.default_rng(5)
+    img = DesignedImage()
+    recs = []
+    for t in range(30):
+        s = random_protein(rng, 120)
+        img.add_windows(s, range(0, 100, 2), fI=t % 4, rng=rng)
+        recs.append((f"s{t}", s))
+    table = img.table()
+    occ = np.nonzero(table["which_kmer"] <= 20 ** 8)[0]
+    # overwrite the bucket after every 3rd occupied one with a stray stop key
+    for i in occ[::3]:
+        j = (i + 1) % len(table)
+        if table["which_kmer"][j] > 20 ** 8:
+            table["which_kmer"][j] = 20 ** 8 + 2 + int(i % 1000) * 977
+    res, off = pack(recs)
+    want = oracle_lib.process_batch(table, res, off)
+    for layout in ("packed", "aos"):
+        with gpu.Image.from_table(table) as im, gpu.Context(im) as ctx:
+            if layout == "aos":
+                im.set_layout(gpu.Image.AOS24)
+            got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+            assert_same(got, want, len(recs))
 
 
 def test_ragged_long_and_empty_sequences(small_world, oracle_lib, gpu):
