@@ -120,6 +120,17 @@ SIGNATURES = {
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_INT)]),
     "kgx_microbench_random_read": (_INT, [_P, _U64, _INT, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(_U64)]),
+    "kgx_kmap_create": (_INT, [_INT, _INT, _PP]),
+    "kgx_kmap_destroy": (_INT, [_P]),
+    "kgx_kmap_add": (_INT, [_P, _P, _P, _U64]),
+    "kgx_kmap_add_hits": (_INT, [_P, _P, _P]),
+    "kgx_kmap_num_kmers": (_U64, [_P]),
+    "kgx_kmap_num_values": (_U64, [_P]),
+    "kgx_kmap_lookup": (_INT, [_P, _P, _U64, _P, _P, _U64]),
+    "kgx_matrix_create": (_INT, [_P, _PP]),
+    "kgx_matrix_destroy": (_INT, [_P]),
+    "kgx_matrix_add_hits": (_INT, [_P, _P, _P]),
+    "kgx_matrix_pairs": (_INT, [_P, _PP, ctypes.POINTER(_U64)]),
     "kgx_event_create": (_INT, [_PP]),
     "kgx_event_destroy": (_INT, [_P]),
     "kgx_event_record": (_INT, [_P, _P]),
@@ -327,3 +338,86 @@ def find_best_call(calls: np.ndarray, functions: list[str]):
                                    ctypes.byref(sc), ctypes.byref(ws), ctypes.byref(off),
                                    ctypes.byref(off_set)), "kgx_find_best_call")
     return fi.value, buf.value.decode(), sc.value, ws.value, (off.value if off_set.value else None)
+
+
+KMAP_APPEND, KMAP_SET = 0, 1
+PAIR_DTYPE = np.dtype([("id1", np.uint32), ("id2", np.uint32), ("count", np.uint64)])
+
+
+class Kmap:
+    """Device k-mer -> id table: kmer_to_id_ (KMAP_APPEND) or kmer_to_family_id_ (KMAP_SET)."""
+
+    def __init__(self, device: int = 0, mode: int = KMAP_APPEND):
+        h = ctypes.c_void_p()
+        check(lib().kgx_kmap_create(device, mode, ctypes.byref(h)), "kgx_kmap_create")
+        self.handle = h.value
+
+    def add(self, kmers, ids) -> None:
+        k = np.ascontiguousarray(kmers, dtype=np.uint64)
+        v = np.ascontiguousarray(ids, dtype=np.uint32)
+        check(lib().kgx_kmap_add(self.handle, k.ctypes.data, v.ctypes.data, len(k)), "kgx_kmap_add")
+
+    def add_hits(self, ctx: "Context", seq_ids) -> None:
+        v = np.ascontiguousarray(seq_ids, dtype=np.uint32)
+        check(lib().kgx_kmap_add_hits(self.handle, ctx.handle, v.ctypes.data), "kgx_kmap_add_hits")
+
+    @property
+    def num_kmers(self) -> int:
+        return lib().kgx_kmap_num_kmers(self.handle)
+
+    @property
+    def num_values(self) -> int:
+        return lib().kgx_kmap_num_values(self.handle)
+
+    def lookup(self, kmers) -> tuple[np.ndarray, np.ndarray]:
+        """(offsets[n+1], ids) CSR of the lists of `kmers`."""
+        k = np.ascontiguousarray(kmers, dtype=np.uint64)
+        off = np.zeros(len(k) + 1, np.uint64)
+        check(lib().kgx_kmap_lookup(self.handle, k.ctypes.data, len(k), off.ctypes.data, None, 0),
+              "kgx_kmap_lookup")
+        ids = np.zeros(int(off[-1]), np.uint32)
+        if len(ids):
+            check(lib().kgx_kmap_lookup(self.handle, k.ctypes.data, len(k), off.ctypes.data,
+                                        ids.ctypes.data, len(ids)), "kgx_kmap_lookup")
+        return off, ids
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_kmap_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class Matrix:
+    """One /matrix request (matrix_request.cc:83-190) over a device Kmap."""
+
+    def __init__(self, kmap: Kmap):
+        self.kmap = kmap
+        h = ctypes.c_void_p()
+        check(lib().kgx_matrix_create(kmap.handle, ctypes.byref(h)), "kgx_matrix_create")
+        self.handle = h.value
+
+    def add_hits(self, ctx: "Context", seq_ids) -> None:
+        v = np.ascontiguousarray(seq_ids, dtype=np.uint32)
+        check(lib().kgx_matrix_add_hits(self.handle, ctx.handle, v.ctypes.data), "kgx_matrix_add_hits")
+
+    def pairs(self) -> np.ndarray:
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        check(lib().kgx_matrix_pairs(self.handle, ctypes.byref(p), ctypes.byref(n)), "kgx_matrix_pairs")
+        return _view(p.value, n.value, PAIR_DTYPE).copy()
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_matrix_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -1,0 +1,105 @@
+/*
+ * kgx_rt.h -- host runtime internals shared by the C ABI translation units
+ * (kgx_runtime.cpp: images, contexts, batches; kgx_tables.cpp: k-mer -> id
+ * tables and /matrix pair counting).  Not part of the public ABI.
+ */
+#ifndef KGX_RT_H
+#define KGX_RT_H
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kgx_internal.h"
+
+namespace kgx {
+
+/* sets the thread's kgx_last_error() text and returns code */
+int fail(int code, const std::string &msg);
+bool is_gfx950(int dev);
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return ::kgx::fail(KGX_EDEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+/* grow-only device buffer */
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t bytes)
+    {
+        if (bytes <= cap)
+            return hipSuccess;
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
+
+}  // namespace kgx
+
+struct kgx_image {
+    int device = 0;
+    uint64_t num_sigs = 0;
+    int layout = KGX_LAYOUT_AOS24;
+    kgx_sig_kmer *d_table = nullptr;   /* AOS24: the file's buckets */
+    kgx::packed_bucket *d_packed = nullptr; /* PACKED16 */
+    const void *resident() const
+    {
+        return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
+    }
+    uint64_t resident_bytes() const
+    {
+        return num_sigs * (layout == KGX_LAYOUT_PACKED16 ? sizeof(kgx::packed_bucket) : sizeof(kgx_sig_kmer));
+    }
+};
+
+struct kgx_ctx {
+    kgx_image *img = nullptr;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    /* device scratch */
+    kgx::DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
+        dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
+    /* current plan */
+    uint32_t n_seq = 0;
+    uint64_t n_residues = 0;
+    uint64_t max_tiles = 0;
+    uint32_t tile_windows = 64u * kgx::PROBE_J_DEFAULT;
+    const uint64_t *d_off = nullptr;
+    bool have_hits = false; /* the tiled hits of the current plan are on the device */
+    /* tuning options */
+    int probe_variant = kgx::PROBE_AUTO;
+    int probe_j = kgx::PROBE_J_DEFAULT;
+    /* host results */
+    std::vector<uint64_t> h_hoff, h_coff, h_ooff;
+    std::vector<kgx_hit> h_hits;
+    std::vector<kgx_call> h_calls;
+    std::vector<kgx_otu> h_otus;
+    std::vector<uint32_t> h_hcount, h_ccount;
+    std::vector<char> h_res;
+};
+
+#endif

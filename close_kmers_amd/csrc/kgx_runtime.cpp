@@ -18,11 +18,11 @@
 #include <sys/stat.h>
 #include <vector>
 
-#include "kgx_internal.h"
+#include "kgx_rt.h"
 
 using namespace kgx;
 
-namespace {
+namespace kgx {
 
 thread_local std::string g_last_error;
 
@@ -32,41 +32,6 @@ int fail(int code, const std::string &msg)
     return code;
 }
 
-#define HIP_TRY(expr)                                                                        \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess)                                                                \
-            return fail(KGX_EDEVICE, std::string(#expr ": ") + hipGetErrorString(e_));      \
-    } while (0)
-
-/* grow-only device buffer */
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    hipError_t reserve(size_t bytes)
-    {
-        if (bytes <= cap)
-            return hipSuccess;
-        if (p)
-            (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess)
-            cap = want;
-        return e;
-    }
-    void release()
-    {
-        if (p)
-            (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    template <class T> T *as() const { return static_cast<T *>(p); }
-};
-
 bool is_gfx950(int dev)
 {
     hipDeviceProp_t prop;
@@ -75,50 +40,7 @@ bool is_gfx950(int dev)
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
 
-uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
-
-}  // namespace
-
-struct kgx_image {
-    int device = 0;
-    uint64_t num_sigs = 0;
-    int layout = KGX_LAYOUT_AOS24;
-    kgx_sig_kmer *d_table = nullptr;   /* AOS24: the file's buckets */
-    packed_bucket *d_packed = nullptr; /* PACKED16 */
-    const void *resident() const
-    {
-        return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
-    }
-    uint64_t resident_bytes() const
-    {
-        return num_sigs * (layout == KGX_LAYOUT_PACKED16 ? sizeof(packed_bucket) : sizeof(kgx_sig_kmer));
-    }
-};
-
-struct kgx_ctx {
-    kgx_image *img = nullptr;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    /* device scratch */
-    DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
-        dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
-    /* current plan */
-    uint32_t n_seq = 0;
-    uint64_t n_residues = 0;
-    uint64_t max_tiles = 0;
-    uint32_t tile_windows = 64u * PROBE_J_DEFAULT;
-    const uint64_t *d_off = nullptr;
-    /* tuning options */
-    int probe_variant = PROBE_AUTO;
-    int probe_j = PROBE_J_DEFAULT;
-    /* host results */
-    std::vector<uint64_t> h_hoff, h_coff, h_ooff;
-    std::vector<kgx_hit> h_hits;
-    std::vector<kgx_call> h_calls;
-    std::vector<kgx_otu> h_otus;
-    std::vector<uint32_t> h_hcount, h_ccount;
-    std::vector<char> h_res;
-};
+}  // namespace kgx
 
 extern "C" {
 
@@ -600,6 +522,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     c->max_tiles = max_tiles;
     c->tile_windows = tile_windows;
     c->d_off = d_off;
+    c->have_hits = false;
     return KGX_OK;
 }
 
@@ -614,6 +537,7 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
                          c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
                          c->img->layout, c->img->num_sigs, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
                          (int)(c->tile_windows / 64), c->probe_variant, c->stream));
+    c->have_hits = true;
     return KGX_OK;
 }
 

@@ -1,0 +1,788 @@
+/*
+ * kgx_tables.hip -- k-mer -> id tables and /matrix pair counting in HBM.
+ *
+ *   kgx_kmap   : KmerPegMapping::kmer_to_id_ / kmer_to_family_id_
+ *                (kmer.h:84-127; add_mapping kmer.cc:173-210, add_fam_mapping
+ *                kmer.cc:212-256) as a CSR over sorted unique k-mers (ids in
+ *                insertion order) plus an open-addressing index k-mer -> row
+ *   kgx_matrix : MatrixRequest's matrix_proteins_ / distance_ state and its
+ *                per-hit rule (matrix_request.cc:83-95,130-163) -- a device
+ *                hash of seen ids (first request ordinal) and a device hash
+ *                of (id1, id2) -> count, read out ordered as std::map would
+ *
+ * Building a table is a stable radix sort of (k-mer, id) pairs in insertion
+ * order (hipCUB), so per-k-mer lists keep insertion order; the set flavour
+ * drops repeats of an id within a list, keeping the first.  Hits are read
+ * straight from a context's tiled device result.
+ */
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+#include "kgx_device.h"
+#include "kgx_rt.h"
+
+using namespace kgx;
+
+namespace {
+
+constexpr uint64_t EMPTY64 = ~0ull;
+constexpr uint32_t NO_ID = 0xFFFFFFFFu; /* reserved: ids must be below it */
+
+__device__ __forceinline__ uint64_t hslot(uint64_t key, uint64_t mask) { return mix64(key) & mask; }
+
+/* slot of `key`, claiming an empty one if absent; *fresh set when claimed */
+__device__ __forceinline__ uint64_t find_or_insert(uint64_t *keys, uint64_t mask, uint64_t key,
+                                                   bool &fresh)
+{
+    uint64_t h = hslot(key, mask);
+    for (;;) {
+        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long *>(keys + h),
+                                        (unsigned long long)EMPTY64, (unsigned long long)key);
+        if (prev == EMPTY64) {
+            fresh = true;
+            return h;
+        }
+        if (prev == key) {
+            fresh = false;
+            return h;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ int64_t find(const uint64_t *keys, uint64_t mask, uint64_t key)
+{
+    if (mask == 0 && keys == nullptr)
+        return -1;
+    uint64_t h = hslot(key, mask);
+    for (;;) {
+        const uint64_t k = keys[h];
+        if (k == key)
+            return (int64_t)h;
+        if (k == EMPTY64)
+            return -1;
+        h = (h + 1) & mask;
+    }
+}
+
+/* read-only view of a built table */
+struct KmapView {
+    const uint64_t *hkeys = nullptr; /* index: k-mer per slot */
+    const uint32_t *hrow = nullptr;  /* index: row per slot */
+    uint64_t hmask = 0;
+    const uint64_t *starts = nullptr; /* rows + 1 */
+    const uint32_t *vals = nullptr;
+};
+
+__device__ __forceinline__ bool kmap_row(const KmapView &m, uint64_t kmer, uint64_t &a, uint64_t &b)
+{
+    if (!m.hkeys)
+        return false;
+    const int64_t s = find(m.hkeys, m.hmask, kmer);
+    if (s < 0)
+        return false;
+    const uint32_t r = m.hrow[s];
+    a = m.starts[r];
+    b = m.starts[r + 1];
+    return true;
+}
+
+/* the tiled device result of a context (kgx_device_result) */
+struct Tiled {
+    const kgx_hit *hits;
+    const uint64_t *mask;
+    const uint64_t *wbase;
+    uint32_t n_seq;
+    uint32_t T; /* windows per tile */
+};
+
+__device__ __forceinline__ uint32_t tile_count(const Tiled &t, uint64_t tile)
+{
+    const uint64_t W = t.wbase[t.n_seq];
+    const uint32_t J = t.T / 64;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < J; j++) {
+        const uint64_t w = tile * J + j;
+        if (64 * w < W)
+            c += (uint32_t)__popcll(t.mask[w]);
+    }
+    return c;
+}
+
+/* ---------------- kernels ---------------- */
+
+__global__ void tile_counts_kernel(Tiled t, uint64_t n_tiles, uint32_t *counts)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_tiles)
+        counts[i] = tile_count(t, i);
+    else if (i == n_tiles)
+        counts[i] = 0;
+}
+
+/* dense (k-mer, id) pairs of the tiled hits, in (sequence, position) order */
+__global__ void hits_to_pairs_kernel(Tiled t, uint64_t n_tiles, const uint32_t *tile_base,
+                                     const uint32_t *seq_ids, uint64_t *kmers, uint32_t *ids)
+{
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t tile = slot / t.T;
+    const uint32_t i = (uint32_t)(slot % t.T);
+    if (tile >= n_tiles || i >= tile_base[tile + 1] - tile_base[tile])
+        return;
+    const kgx_hit &h = t.hits[tile * t.T + i];
+    const uint64_t at = tile_base[tile] + i;
+    kmers[at] = h.which_kmer;
+    ids[at] = seq_ids[h.seq];
+}
+
+__global__ void expand_rows_kernel(const uint64_t *keys, const uint64_t *starts, uint64_t n_rows,
+                                   uint64_t *out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows)
+        return;
+    for (uint64_t j = starts[r]; j < starts[r + 1]; j++)
+        out[j] = keys[r];
+}
+
+__global__ void iota_kernel(uint32_t *p, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        p[i] = (uint32_t)i;
+}
+
+__global__ void gather_u64_kernel(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        dst[i] = src[idx[i]];
+}
+
+/* (k-mer, id) order -> keep[original index] = first of its (k-mer, id) group */
+__global__ void first_of_pair_kernel(const uint64_t *k_sorted, const uint32_t *orig, const uint64_t *k1,
+                                     const uint32_t *v1, uint64_t n, uint8_t *keep)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n)
+        return;
+    const uint32_t o = orig[p];
+    bool first = true;
+    if (p > 0) {
+        const uint32_t q = orig[p - 1];
+        first = !(k1[q] == k1[o] && v1[q] == v1[o]);
+    }
+    keep[o] = first;
+    (void)k_sorted;
+}
+
+__global__ void row_heads_kernel(const uint64_t *k, uint64_t n, uint8_t *head)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        head[i] = (i == 0 || k[i] != k[i - 1]);
+}
+
+__global__ void index_insert_kernel(const uint64_t *keys, uint64_t n, uint64_t *hkeys, uint32_t *hrow,
+                                    uint64_t mask)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n)
+        return;
+    bool fresh;
+    const uint64_t s = find_or_insert(hkeys, mask, keys[r], fresh);
+    hrow[s] = (uint32_t)r;
+}
+
+__global__ void lookup_count_kernel(KmapView m, const uint64_t *kmers, uint64_t n, uint64_t *count)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    uint64_t a = 0, b = 0;
+    count[i] = kmap_row(m, kmers[i], a, b) ? b - a : 0;
+}
+
+__global__ void lookup_ids_kernel(KmapView m, const uint64_t *kmers, uint64_t n, const uint64_t *off,
+                                  uint32_t *ids)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    uint64_t a = 0, b = 0;
+    if (kmap_row(m, kmers[i], a, b))
+        for (uint64_t j = a; j < b; j++)
+            ids[off[i] + (j - a)] = m.vals[j];
+}
+
+/* --- /matrix --- */
+
+__global__ void seen_insert_kernel(const uint32_t *ids, uint32_t n, uint64_t base, uint64_t *skeys,
+                                   uint64_t *sord, uint64_t mask, unsigned long long *used)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n)
+        return;
+    bool fresh;
+    const uint64_t h = find_or_insert(skeys, mask, ids[s], fresh);
+    if (fresh)
+        atomicAdd(used, 1ull);
+    atomicMin(reinterpret_cast<unsigned long long *>(sord + h), (unsigned long long)(base + s));
+}
+
+__global__ void rehash_kernel(const uint64_t *okeys, const uint64_t *ovals, uint64_t ocap, uint64_t *nkeys,
+                              uint64_t *nvals, uint64_t nmask)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ocap || okeys[i] == EMPTY64)
+        return;
+    bool fresh;
+    const uint64_t h = find_or_insert(nkeys, nmask, okeys[i], fresh);
+    nvals[h] = ovals[i];
+}
+
+__global__ void matrix_events_kernel(Tiled t, uint64_t n_tiles, KmapView m, unsigned long long *events)
+{
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t tile = slot / t.T;
+    const uint32_t i = (uint32_t)(slot % t.T);
+    uint64_t ev = 0;
+    if (tile < n_tiles && i < tile_count(t, tile)) {
+        uint64_t a = 0, b = 0;
+        if (kmap_row(m, t.hits[tile * t.T + i].which_kmer, a, b))
+            ev = b - a;
+    }
+    /* one atomic per wave */
+    for (int o = 32; o > 0; o >>= 1)
+        ev += __shfl_xor(ev, o);
+    if (lane_id() == 0 && ev)
+        atomicAdd(events, (unsigned long long)ev);
+}
+
+__global__ void matrix_pairs_kernel(Tiled t, uint64_t n_tiles, KmapView m, const uint32_t *seq_ids,
+                                    uint64_t base, const uint64_t *skeys, const uint64_t *sord,
+                                    uint64_t smask, uint64_t *pkeys, uint64_t *pcount, uint64_t pmask,
+                                    unsigned long long *used)
+{
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t tile = slot / t.T;
+    const uint32_t i = (uint32_t)(slot % t.T);
+    if (tile >= n_tiles || i >= tile_count(t, tile))
+        return;
+    const kgx_hit &h = t.hits[tile * t.T + i];
+    uint64_t a = 0, b = 0;
+    if (!kmap_row(m, h.which_kmer, a, b))
+        return; /* matrix_request.cc:159 reports "no mapping" on stderr */
+    const uint32_t e = seq_ids[h.seq];
+    const uint64_t my_ord = base + h.seq;
+    for (uint64_t j = a; j < b; j++) {
+        const uint32_t f = m.vals[j];
+        if (f == e)
+            continue;
+        const int64_t q = find(skeys, smask, f);
+        if (q < 0 || sord[q] > my_ord)
+            continue; /* not in matrix_proteins_ yet */
+        bool fresh;
+        const uint64_t p = find_or_insert(pkeys, pmask, ((uint64_t)e << 32) | f, fresh);
+        if (fresh)
+            atomicAdd(used, 1ull);
+        atomicAdd(reinterpret_cast<unsigned long long *>(pcount + p), 1ull);
+    }
+}
+
+__global__ void compact_pairs_kernel(const uint64_t *pkeys, const uint64_t *pcount, uint64_t cap,
+                                     uint64_t *okeys, uint64_t *ocount, unsigned long long *n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap || pkeys[i] == EMPTY64)
+        return;
+    const unsigned long long at = atomicAdd(n, 1ull);
+    okeys[at] = pkeys[i];
+    ocount[at] = pcount[i];
+}
+
+inline dim3 grid_for(uint64_t n, uint32_t block = 256) { return dim3((uint32_t)((n + block - 1) / block)); }
+
+uint64_t pow2_at_least(uint64_t n)
+{
+    uint64_t c = 1024;
+    while (c < n)
+        c <<= 1;
+    return c;
+}
+
+/* hipCUB temp storage helper */
+struct CubTemp {
+    DevBuf buf;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+/* ------------------------------------------------------------------------ */
+
+struct kgx_kmap {
+    int device = 0;
+    int mode = KGX_KMAP_APPEND;
+    hipStream_t stream = nullptr;
+    uint64_t n_rows = 0, n_vals = 0, hcap = 0;
+    DevBuf keys, starts, vals, hkeys, hrow;
+    KmapView view() const
+    {
+        KmapView v;
+        if (n_rows) {
+            v.hkeys = hkeys.as<uint64_t>();
+            v.hrow = hrow.as<uint32_t>();
+            v.hmask = hcap - 1;
+            v.starts = starts.as<uint64_t>();
+            v.vals = vals.as<uint32_t>();
+        }
+        return v;
+    }
+};
+
+struct kgx_matrix {
+    kgx_kmap *map = nullptr;
+    uint64_t base = 0; /* request ordinal of the next sequence */
+    uint64_t scap = 0, sused = 0, pcap = 0, pused = 0;
+    DevBuf skeys, sord, pkeys, pcount, ids, counter, tmp_keys, tmp_count;
+    CubTemp cub;
+    std::vector<kgx_pair_count> result;
+};
+
+namespace {
+
+/* Rebuild `m` from d_k/d_v (n pairs: the old rows expanded, then the new
+ * pairs, in insertion order).  Consumes the buffers' contents. */
+int kmap_rebuild(kgx_kmap *m, DevBuf &d_k, DevBuf &d_v, uint64_t n, hipStream_t st)
+{
+    if (n == 0)
+        return KGX_OK;
+    DevBuf k1, v1, tmp;
+    HIP_TRY(k1.reserve(n * 8));
+    HIP_TRY(v1.reserve(n * 4));
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_k.as<uint64_t>(), k1.as<uint64_t>(),
+                                               d_v.as<uint32_t>(), v1.as<uint32_t>(), (int)n, 0, 64, st));
+    HIP_TRY(tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, d_k.as<uint64_t>(), k1.as<uint64_t>(),
+                                               d_v.as<uint32_t>(), v1.as<uint32_t>(), (int)n, 0, 64, st));
+    /* k1/v1: by k-mer, insertion order within a k-mer (LSD radix sort is stable) */
+    if (m->mode == KGX_KMAP_SET) {
+        /* order (k-mer, id, insertion): sort indices by id, then by k-mer */
+        DevBuf idx, v2, i2, kg, k3, i3, keep;
+        HIP_TRY(idx.reserve(n * 4));
+        HIP_TRY(v2.reserve(n * 4));
+        HIP_TRY(i2.reserve(n * 4));
+        HIP_TRY(kg.reserve(n * 8));
+        HIP_TRY(k3.reserve(n * 8));
+        HIP_TRY(i3.reserve(n * 4));
+        HIP_TRY(keep.reserve(n));
+        hipLaunchKernelGGL(iota_kernel, grid_for(n), dim3(256), 0, st, idx.as<uint32_t>(), n);
+        tb = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, v1.as<uint32_t>(), v2.as<uint32_t>(),
+                                                   idx.as<uint32_t>(), i2.as<uint32_t>(), (int)n, 0, 32, st));
+        HIP_TRY(tmp.reserve(tb));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, v1.as<uint32_t>(), v2.as<uint32_t>(),
+                                                   idx.as<uint32_t>(), i2.as<uint32_t>(), (int)n, 0, 32, st));
+        hipLaunchKernelGGL(gather_u64_kernel, grid_for(n), dim3(256), 0, st, k1.as<uint64_t>(),
+                           i2.as<uint32_t>(), n, kg.as<uint64_t>());
+        tb = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kg.as<uint64_t>(), k3.as<uint64_t>(),
+                                                   i2.as<uint32_t>(), i3.as<uint32_t>(), (int)n, 0, 64, st));
+        HIP_TRY(tmp.reserve(tb));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, kg.as<uint64_t>(), k3.as<uint64_t>(),
+                                                   i2.as<uint32_t>(), i3.as<uint32_t>(), (int)n, 0, 64, st));
+        hipLaunchKernelGGL(first_of_pair_kernel, grid_for(n), dim3(256), 0, st, k3.as<uint64_t>(),
+                           i3.as<uint32_t>(), k1.as<uint64_t>(), v1.as<uint32_t>(), n, keep.as<uint8_t>());
+        /* keep the firsts, in (k-mer, insertion) order */
+        DevBuf nsel;
+        HIP_TRY(nsel.reserve(8));
+        tb = 0;
+        HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, k1.as<uint64_t>(), keep.as<uint8_t>(),
+                                              d_k.as<uint64_t>(), nsel.as<uint64_t>(), (int)n, st));
+        HIP_TRY(tmp.reserve(tb));
+        HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, k1.as<uint64_t>(), keep.as<uint8_t>(),
+                                              d_k.as<uint64_t>(), nsel.as<uint64_t>(), (int)n, st));
+        HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, v1.as<uint32_t>(), keep.as<uint8_t>(),
+                                              d_v.as<uint32_t>(), nsel.as<uint64_t>(), (int)n, st));
+        uint64_t kept = 0;
+        HIP_TRY(hipMemcpyAsync(&kept, nsel.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n = kept;
+        std::swap(k1, d_k);
+        std::swap(v1, d_v);
+    }
+    /* rows: unique k-mers and their starts */
+    DevBuf head, nsel;
+    HIP_TRY(head.reserve(n));
+    HIP_TRY(nsel.reserve(8));
+    hipLaunchKernelGGL(row_heads_kernel, grid_for(n), dim3(256), 0, st, k1.as<uint64_t>(), n,
+                       head.as<uint8_t>());
+    HIP_TRY(m->keys.reserve(n * 8));
+    HIP_TRY(m->starts.reserve((n + 1) * 8));
+    tb = 0;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, k1.as<uint64_t>(), head.as<uint8_t>(),
+                                          m->keys.as<uint64_t>(), nsel.as<uint64_t>(), (int)n, st));
+    size_t tb2 = 0;
+    hipcub::CountingInputIterator<uint64_t> cnt(0);
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb2, cnt, head.as<uint8_t>(), m->starts.as<uint64_t>(),
+                                          nsel.as<uint64_t>(), (int)n, st));
+    HIP_TRY(tmp.reserve(std::max(tb, tb2)));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, k1.as<uint64_t>(), head.as<uint8_t>(),
+                                          m->keys.as<uint64_t>(), nsel.as<uint64_t>(), (int)n, st));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb2, cnt, head.as<uint8_t>(), m->starts.as<uint64_t>(),
+                                          nsel.as<uint64_t>(), (int)n, st));
+    uint64_t rows = 0;
+    HIP_TRY(hipMemcpyAsync(&rows, nsel.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpyAsync(m->starts.as<uint64_t>() + rows, &n, 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(m->vals.reserve(n * 4));
+    HIP_TRY(hipMemcpyAsync(m->vals.p, v1.p, n * 4, hipMemcpyDeviceToDevice, st));
+    /* index k-mer -> row */
+    const uint64_t cap = pow2_at_least(2 * rows);
+    HIP_TRY(m->hkeys.reserve(cap * 8));
+    HIP_TRY(m->hrow.reserve(cap * 4));
+    HIP_TRY(hipMemsetAsync(m->hkeys.p, 0xFF, cap * 8, st));
+    hipLaunchKernelGGL(index_insert_kernel, grid_for(rows), dim3(256), 0, st, m->keys.as<uint64_t>(), rows,
+                       m->hkeys.as<uint64_t>(), m->hrow.as<uint32_t>(), cap - 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    m->n_rows = rows;
+    m->n_vals = n;
+    m->hcap = cap;
+    return KGX_OK;
+}
+
+/* old rows expanded into d_k/d_v[0, n_vals); capacity for `extra` more */
+int kmap_expand(kgx_kmap *m, DevBuf &d_k, DevBuf &d_v, uint64_t extra, hipStream_t st)
+{
+    const uint64_t n = m->n_vals + extra;
+    HIP_TRY(d_k.reserve(std::max<uint64_t>(n, 1) * 8));
+    HIP_TRY(d_v.reserve(std::max<uint64_t>(n, 1) * 4));
+    if (m->n_rows) {
+        hipLaunchKernelGGL(expand_rows_kernel, grid_for(m->n_rows), dim3(256), 0, st, m->keys.as<uint64_t>(),
+                           m->starts.as<uint64_t>(), m->n_rows, d_k.as<uint64_t>());
+        HIP_TRY(hipMemcpyAsync(d_v.p, m->vals.p, m->n_vals * 4, hipMemcpyDeviceToDevice, st));
+    }
+    return KGX_OK;
+}
+
+Tiled tiled_of(const kgx_ctx *c)
+{
+    Tiled t;
+    t.hits = c->hits.as<kgx_hit>();
+    t.mask = c->hit_mask.as<uint64_t>();
+    t.wbase = c->wbase.as<uint64_t>();
+    t.n_seq = c->n_seq;
+    t.T = c->tile_windows;
+    return t;
+}
+
+int check_ctx_hits(kgx_ctx *c)
+{
+    if (!c || !c->img)
+        return fail(KGX_EINVAL, "null context");
+    if (!c->have_hits)
+        return fail(KGX_EINVAL, "the context has no batch with hits (want KGX_WANT_HITS)");
+    return KGX_OK;
+}
+
+int upload_ids(DevBuf &d, const uint32_t *ids, uint64_t n, hipStream_t st)
+{
+    for (uint64_t i = 0; i < n; i++)
+        if (ids[i] == NO_ID)
+            return fail(KGX_EINVAL, "id 0xFFFFFFFF is reserved");
+    HIP_TRY(d.reserve(std::max<uint64_t>(n, 1) * 4));
+    HIP_TRY(hipMemcpyAsync(d.p, ids, n * 4, hipMemcpyHostToDevice, st));
+    return KGX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kgx_kmap_create(int device, int mode, kgx_kmap **out)
+{
+    if (!out || (mode != KGX_KMAP_APPEND && mode != KGX_KMAP_SET))
+        return fail(KGX_EINVAL, "bad kmap arguments");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(KGX_EDEVICE, "no such HIP device " + std::to_string(device));
+    if (!is_gfx950(device))
+        return fail(KGX_EDEVICE, "device " + std::to_string(device) + " is not gfx950");
+    HIP_TRY(hipSetDevice(device));
+    kgx_kmap *m = new kgx_kmap;
+    m->device = device;
+    m->mode = mode;
+    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete m;
+        return fail(KGX_EDEVICE, "stream creation failed");
+    }
+    *out = m;
+    return KGX_OK;
+}
+
+int kgx_kmap_destroy(kgx_kmap *m)
+{
+    if (!m)
+        return KGX_OK;
+    (void)hipSetDevice(m->device);
+    (void)hipStreamSynchronize(m->stream);
+    for (DevBuf *b : {&m->keys, &m->starts, &m->vals, &m->hkeys, &m->hrow})
+        b->release();
+    (void)hipStreamDestroy(m->stream);
+    delete m;
+    return KGX_OK;
+}
+
+uint64_t kgx_kmap_num_kmers(const kgx_kmap *m) { return m ? m->n_rows : 0; }
+uint64_t kgx_kmap_num_values(const kgx_kmap *m) { return m ? m->n_vals : 0; }
+
+int kgx_kmap_add(kgx_kmap *m, const uint64_t *kmers, const uint32_t *ids, uint64_t n)
+{
+    if (!m || (n && (!kmers || !ids)))
+        return fail(KGX_EINVAL, "bad kmap_add arguments");
+    if (n == 0)
+        return KGX_OK;
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t st = m->stream;
+    DevBuf d_k, d_v;
+    int rc = kmap_expand(m, d_k, d_v, n, st);
+    if (rc)
+        return rc;
+    for (uint64_t i = 0; i < n; i++)
+        if (ids[i] == NO_ID)
+            return fail(KGX_EINVAL, "id 0xFFFFFFFF is reserved");
+    HIP_TRY(hipMemcpyAsync(d_k.as<uint64_t>() + m->n_vals, kmers, n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_v.as<uint32_t>() + m->n_vals, ids, n * 4, hipMemcpyHostToDevice, st));
+    return kmap_rebuild(m, d_k, d_v, m->n_vals + n, st);
+}
+
+int kgx_kmap_add_hits(kgx_kmap *m, kgx_ctx *c, const uint32_t *seq_ids)
+{
+    if (!m)
+        return fail(KGX_EINVAL, "null kmap");
+    int rc = check_ctx_hits(c);
+    if (rc)
+        return rc;
+    if (c->img->device != m->device)
+        return fail(KGX_EINVAL, "kmap and context are on different devices");
+    if (c->n_seq == 0)
+        return KGX_OK;
+    if (!seq_ids)
+        return fail(KGX_EINVAL, "null seq_ids");
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t st = c->stream;
+    DevBuf d_ids, counts, base, tmp;
+    rc = upload_ids(d_ids, seq_ids, c->n_seq, st);
+    if (rc)
+        return rc;
+    const Tiled t = tiled_of(c);
+    const uint64_t nt = c->max_tiles;
+    HIP_TRY(counts.reserve((nt + 1) * 4));
+    HIP_TRY(base.reserve((nt + 1) * 4));
+    hipLaunchKernelGGL(tile_counts_kernel, grid_for(nt + 1), dim3(256), 0, st, t, nt, counts.as<uint32_t>());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, counts.as<uint32_t>(), base.as<uint32_t>(),
+                                             (int)(nt + 1), st));
+    HIP_TRY(tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, counts.as<uint32_t>(), base.as<uint32_t>(),
+                                             (int)(nt + 1), st));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, base.as<uint32_t>() + nt, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (total == 0)
+        return KGX_OK;
+    DevBuf d_k, d_v;
+    rc = kmap_expand(m, d_k, d_v, total, st);
+    if (rc)
+        return rc;
+    hipLaunchKernelGGL(hits_to_pairs_kernel, grid_for(nt * t.T), dim3(256), 0, st, t, nt, base.as<uint32_t>(),
+                       d_ids.as<uint32_t>(), d_k.as<uint64_t>() + m->n_vals, d_v.as<uint32_t>() + m->n_vals);
+    HIP_TRY(hipGetLastError());
+    return kmap_rebuild(m, d_k, d_v, m->n_vals + total, st);
+}
+
+int kgx_kmap_lookup(kgx_kmap *m, const uint64_t *kmers, uint64_t n, uint64_t *offsets, uint32_t *ids,
+                    uint64_t ids_cap)
+{
+    if (!m || !offsets || (n && !kmers))
+        return fail(KGX_EINVAL, "bad kmap_lookup arguments");
+    offsets[0] = 0;
+    if (n == 0)
+        return KGX_OK;
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t st = m->stream;
+    DevBuf d_k, d_c;
+    HIP_TRY(d_k.reserve(n * 8));
+    HIP_TRY(d_c.reserve((n + 1) * 8));
+    HIP_TRY(hipMemcpyAsync(d_k.p, kmers, n * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lookup_count_kernel, grid_for(n), dim3(256), 0, st, m->view(), d_k.as<uint64_t>(), n,
+                       d_c.as<uint64_t>());
+    std::vector<uint64_t> cnt(n);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), d_c.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < n; i++)
+        offsets[i + 1] = offsets[i] + cnt[i];
+    if (!ids)
+        return KGX_OK;
+    if (ids_cap < offsets[n])
+        return fail(KGX_ERANGE, "ids buffer too small");
+    DevBuf d_ids;
+    HIP_TRY(d_ids.reserve(std::max<uint64_t>(offsets[n], 1) * 4));
+    HIP_TRY(hipMemcpyAsync(d_c.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lookup_ids_kernel, grid_for(n), dim3(256), 0, st, m->view(), d_k.as<uint64_t>(), n,
+                       d_c.as<uint64_t>(), d_ids.as<uint32_t>());
+    HIP_TRY(hipMemcpyAsync(ids, d_ids.p, offsets[n] * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return KGX_OK;
+}
+
+int kgx_matrix_create(kgx_kmap *map, kgx_matrix **out)
+{
+    if (!map || !out)
+        return fail(KGX_EINVAL, "bad matrix arguments");
+    kgx_matrix *x = new kgx_matrix;
+    x->map = map;
+    *out = x;
+    return KGX_OK;
+}
+
+int kgx_matrix_destroy(kgx_matrix *x)
+{
+    if (!x)
+        return KGX_OK;
+    (void)hipSetDevice(x->map->device);
+    for (DevBuf *b : {&x->skeys, &x->sord, &x->pkeys, &x->pcount, &x->ids, &x->counter, &x->tmp_keys,
+                      &x->tmp_count, &x->cub.buf})
+        b->release();
+    delete x;
+    return KGX_OK;
+}
+
+namespace {
+
+/* grow a (keys, vals) hash to hold `need` entries at load <= 1/2 */
+int grow_hash(DevBuf &keys, DevBuf &vals, uint64_t &cap, uint64_t need, uint8_t val_fill, hipStream_t st)
+{
+    if (2 * need <= cap)
+        return KGX_OK;
+    const uint64_t ncap = pow2_at_least(2 * need);
+    DevBuf nk, nv;
+    HIP_TRY(nk.reserve(ncap * 8));
+    HIP_TRY(nv.reserve(ncap * 8));
+    HIP_TRY(hipMemsetAsync(nk.p, 0xFF, ncap * 8, st));
+    HIP_TRY(hipMemsetAsync(nv.p, val_fill, ncap * 8, st));
+    if (cap)
+        hipLaunchKernelGGL(rehash_kernel, grid_for(cap), dim3(256), 0, st, keys.as<uint64_t>(),
+                           vals.as<uint64_t>(), cap, nk.as<uint64_t>(), nv.as<uint64_t>(), ncap - 1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    std::swap(keys, nk);
+    std::swap(vals, nv);
+    nk.release();
+    nv.release();
+    cap = ncap;
+    return KGX_OK;
+}
+
+}  // namespace
+
+int kgx_matrix_add_hits(kgx_matrix *x, kgx_ctx *c, const uint32_t *seq_ids)
+{
+    if (!x)
+        return fail(KGX_EINVAL, "null matrix");
+    int rc = check_ctx_hits(c);
+    if (rc)
+        return rc;
+    kgx_kmap *m = x->map;
+    if (c->img->device != m->device)
+        return fail(KGX_EINVAL, "kmap and context are on different devices");
+    const uint32_t n = c->n_seq;
+    if (n == 0)
+        return KGX_OK;
+    if (!seq_ids)
+        return fail(KGX_EINVAL, "null seq_ids");
+    HIP_TRY(hipSetDevice(m->device));
+    hipStream_t st = c->stream;
+    rc = upload_ids(x->ids, seq_ids, n, st);
+    if (rc)
+        return rc;
+    HIP_TRY(x->counter.reserve(16));
+    unsigned long long *used = x->counter.as<unsigned long long>();
+    /* matrix_proteins_: every id of the batch joins the seen set at its ordinal */
+    rc = grow_hash(x->skeys, x->sord, x->scap, x->sused + n, 0xFF, st);
+    if (rc)
+        return rc;
+    HIP_TRY(hipMemsetAsync(used, 0, 16, st));
+    hipLaunchKernelGGL(seen_insert_kernel, grid_for(n), dim3(256), 0, st, x->ids.as<uint32_t>(), n, x->base,
+                       x->skeys.as<uint64_t>(), x->sord.as<uint64_t>(), x->scap - 1, used);
+    const Tiled t = tiled_of(c);
+    const uint64_t nt = c->max_tiles;
+    const KmapView view = m->view();
+    hipLaunchKernelGGL(matrix_events_kernel, grid_for(nt * t.T), dim3(256), 0, st, t, nt, view, used + 1);
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, used, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    x->sused += h[0];
+    /* distance_: at most one new pair per event */
+    rc = grow_hash(x->pkeys, x->pcount, x->pcap, x->pused + h[1], 0, st);
+    if (rc)
+        return rc;
+    if (h[1]) {
+        HIP_TRY(hipMemsetAsync(used, 0, 8, st));
+        hipLaunchKernelGGL(matrix_pairs_kernel, grid_for(nt * t.T), dim3(256), 0, st, t, nt, view,
+                           x->ids.as<uint32_t>(), x->base, x->skeys.as<uint64_t>(), x->sord.as<uint64_t>(),
+                           x->scap - 1, x->pkeys.as<uint64_t>(), x->pcount.as<uint64_t>(), x->pcap - 1, used);
+        unsigned long long fresh = 0;
+        HIP_TRY(hipMemcpyAsync(&fresh, used, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        x->pused += fresh;
+    }
+    x->base += n;
+    return KGX_OK;
+}
+
+int kgx_matrix_pairs(kgx_matrix *x, const kgx_pair_count **pairs, uint64_t *n_pairs)
+{
+    if (!x || !pairs || !n_pairs)
+        return fail(KGX_EINVAL, "bad matrix_pairs arguments");
+    x->result.clear();
+    *pairs = nullptr;
+    *n_pairs = 0;
+    if (x->pused == 0)
+        return KGX_OK;
+    HIP_TRY(hipSetDevice(x->map->device));
+    hipStream_t st = x->map->stream;
+    const uint64_t n = x->pused;
+    DevBuf k1, c1, k2, c2;
+    HIP_TRY(k1.reserve(n * 8));
+    HIP_TRY(c1.reserve(n * 8));
+    HIP_TRY(k2.reserve(n * 8));
+    HIP_TRY(c2.reserve(n * 8));
+    HIP_TRY(x->counter.reserve(16));
+    HIP_TRY(hipMemsetAsync(x->counter.p, 0, 8, st));
+    hipLaunchKernelGGL(compact_pairs_kernel, grid_for(x->pcap), dim3(256), 0, st, x->pkeys.as<uint64_t>(),
+                       x->pcount.as<uint64_t>(), x->pcap, k1.as<uint64_t>(), c1.as<uint64_t>(),
+                       x->counter.as<unsigned long long>());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1.as<uint64_t>(), k2.as<uint64_t>(),
+                                               c1.as<uint64_t>(), c2.as<uint64_t>(), (int)n, 0, 64, st));
+    HIP_TRY(x->cub.buf.reserve(tb));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(x->cub.buf.p, tb, k1.as<uint64_t>(), k2.as<uint64_t>(),
+                                               c1.as<uint64_t>(), c2.as<uint64_t>(), (int)n, 0, 64, st));
+    std::vector<uint64_t> hk(n), hc(n);
+    HIP_TRY(hipMemcpyAsync(hk.data(), k2.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(hc.data(), c2.p, n * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    x->result.resize(n);
+    for (uint64_t i = 0; i < n; i++)
+        x->result[i] = kgx_pair_count{(uint32_t)(hk[i] >> 32), (uint32_t)hk[i], hc[i]};
+    *pairs = x->result.data();
+    *n_pairs = n;
+    return KGX_OK;
+}
+
+}  // extern "C"

@@ -244,12 +244,57 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
                        int *score_offset_set);
 
 /* Random-access ceiling of the context's image buffer: about n_reads
- * uniformly random buckets read with many loads in flight.  mode 0: the
- * whole 24-byte bucket (key + payload, the probe's access), 1: the 8-byte key
- * only, 2: one aligned 64-byte sector.  *ms = kernel time (HIP events),
+ * uniformly random records of the resident table read with many loads in
+ * flight.  mode 0: a whole 24-byte bucket (key + payload, the AOS24 probe's
+ * access), 1: the 8-byte key of a 24-byte bucket, 2: one aligned 64-byte
+ * sector, 3: one aligned 16-byte record (the PACKED16 probe's access).  *ms = kernel time (HIP events),
  * *reads = buckets actually read. */
 int kgx_microbench_random_read(kgx_ctx *ctx, uint64_t n_reads, int mode, float *ms,
                                uint64_t *reads);
+
+/* ---- k-mer -> id tables in HBM ------------------------------------------
+ * KmerPegMapping's kmer_to_id_ (kmer.h:84-127, filled by /add through
+ * add_mapping, kmer.cc:173-210: every (k-mer, id) appended, duplicates kept)
+ * and kmer_to_family_id_ (add_fam_mapping, kmer.cc:212-256: an id is added to
+ * a k-mer's list once, lists in first-insertion order).  Ids are the
+ * mapping's encoded ids (KmerPegMapping::encode_id); the id <-> name
+ * dictionaries stay with the caller. */
+typedef struct kgx_kmap kgx_kmap;
+enum { KGX_KMAP_APPEND = 0, KGX_KMAP_SET = 1 };
+int kgx_kmap_create(int device, int mode, kgx_kmap **out);
+int kgx_kmap_destroy(kgx_kmap *map);
+/* add (kmers[i], ids[i]) in order i = 0..n-1 (host arrays) */
+int kgx_kmap_add(kgx_kmap *map, const uint64_t *kmers, const uint32_t *ids, uint64_t n);
+/* add the hits of the context's last batch (want must have included HITS):
+ * for each sequence s in order, each of its hits in position order adds
+ * (hit.which_kmer, seq_ids[s]) -- the /add mapping step, add_request.cc:
+ * 164-170 / 196-206.  seq_ids: host array of the batch's n_seq ids. */
+int kgx_kmap_add_hits(kgx_kmap *map, kgx_ctx *ctx, const uint32_t *seq_ids);
+uint64_t kgx_kmap_num_kmers(const kgx_kmap *map);
+uint64_t kgx_kmap_num_values(const kgx_kmap *map);
+/* host query: offsets[n+1] (CSR over the n k-mers) and, when ids != NULL,
+ * the ids (ids_cap >= offsets[n]); unmapped k-mers have empty lists */
+int kgx_kmap_lookup(kgx_kmap *map, const uint64_t *kmers, uint64_t n, uint64_t *offsets,
+                    uint32_t *ids, uint64_t ids_cap);
+
+/* ---- /matrix pair counting (matrix_request.cc:83-190) --------------------
+ * One kgx_matrix per /matrix request (the request's matrix_proteins_ and
+ * distance_ state, matrix_request.h:25-26).  For each sequence s of a batch,
+ * in order, with id e = seq_ids[s] (e joins the request's seen set first):
+ * for every hit of s, for every id f in the hit k-mer's kmap list, if f != e
+ * and f was seen in this request, distance_[(e, f)] += 1. */
+typedef struct kgx_matrix kgx_matrix;
+typedef struct kgx_pair_count { /* one distance_ entry */
+    uint32_t id1, id2;
+    uint64_t count;
+} kgx_pair_count;
+int kgx_matrix_create(kgx_kmap *map, kgx_matrix **out);
+int kgx_matrix_destroy(kgx_matrix *mx);
+/* add the context's last batch (want must have included HITS) */
+int kgx_matrix_add_hits(kgx_matrix *mx, kgx_ctx *ctx, const uint32_t *seq_ids);
+/* all pair counts so far, ordered by (id1, id2) as std::map iterates
+ * distance_; the buffer is owned by mx and valid until the next call */
+int kgx_matrix_pairs(kgx_matrix *mx, const kgx_pair_count **pairs, uint64_t *n_pairs);
 
 /* ---- HIP-event timing on a context's stream ----------------------------- */
 int kgx_event_create(void **event);

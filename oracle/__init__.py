@@ -113,6 +113,20 @@ def lib():
         L.oracle_translate11.argtypes = [ctypes.c_char_p, ctypes.c_uint64]
         L.oracle_translate11.restype = ctypes.c_void_p
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        L.oracle_kmap_new.argtypes = [ctypes.c_int]
+        L.oracle_kmap_new.restype = vp
+        L.oracle_kmap_free.argtypes = [vp]
+        L.oracle_kmap_add.argtypes = [vp, vp, vp, u64]
+        L.oracle_kmap_lookup.argtypes = [vp, u64, vp, u64]
+        L.oracle_kmap_lookup.restype = u64
+        L.oracle_kmap_num_kmers.argtypes = [vp]
+        L.oracle_kmap_num_kmers.restype = u64
+        L.oracle_matrix_new.restype = vp
+        L.oracle_matrix_free.argtypes = [vp]
+        L.oracle_matrix_add.argtypes = [vp, vp, vp, vp, u64, vp, vp]
+        L.oracle_matrix_pairs.argtypes = [vp, vp, vp, vp, vp]
+        L.oracle_matrix_pairs.restype = u64
         _lib = L
     return _lib
 
@@ -250,3 +264,61 @@ def query_text(data_dir: str, fasta: str, mode: str, params: dict | None = None)
         build(ref=False)
     args = [QUERY_BIN, data_dir, fasta, mode] + [f"{k}={v}" for k, v in (params or {}).items()]
     return subprocess.run(args, check=True, capture_output=True).stdout
+
+
+class Kmap:
+    """KmerPegMapping kmer_to_id_ (mode 0, append) / kmer_to_family_id_ (mode 1, set)."""
+
+    def __init__(self, mode: int = 0):
+        self.h = lib().oracle_kmap_new(mode)
+
+    def add(self, kmers, ids) -> None:
+        k = np.ascontiguousarray(kmers, dtype=np.uint64)
+        v = np.ascontiguousarray(ids, dtype=np.uint32)
+        lib().oracle_kmap_add(self.h, k.ctypes.data, v.ctypes.data, len(k))
+
+    def lookup(self, kmer: int) -> np.ndarray:
+        n = lib().oracle_kmap_lookup(self.h, int(kmer), None, 0)
+        out = np.zeros(n, np.uint32)
+        if n:
+            lib().oracle_kmap_lookup(self.h, int(kmer), out.ctypes.data, n)
+        return out
+
+    @property
+    def num_kmers(self) -> int:
+        return lib().oracle_kmap_num_kmers(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_kmap_free(self.h)
+            self.h = None
+
+
+class Matrix:
+    """One /matrix request's state (matrix_request.h:25-26)."""
+
+    def __init__(self):
+        self.h = lib().oracle_matrix_new()
+
+    def add(self, kmap: Kmap, seq_ids, seq_lens, hit_off, hit_kmers) -> None:
+        ids = np.ascontiguousarray(seq_ids, dtype=np.uint32)
+        lens = np.ascontiguousarray(seq_lens, dtype=np.uint64)
+        off = np.ascontiguousarray(hit_off, dtype=np.uint64)
+        km = np.ascontiguousarray(hit_kmers, dtype=np.uint64)
+        lib().oracle_matrix_add(self.h, kmap.h, ids.ctypes.data, lens.ctypes.data, len(ids),
+                                off.ctypes.data, km.ctypes.data if len(km) else None)
+
+    def pairs(self):
+        """(id1, id2, count, score) arrays in distance_ (std::map) order."""
+        n = lib().oracle_matrix_pairs(self.h, None, None, None, None)
+        id1, id2 = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        cnt, sc = np.zeros(n, np.uint64), np.zeros(n, np.float32)
+        if n:
+            lib().oracle_matrix_pairs(self.h, id1.ctypes.data, id2.ctypes.data, cnt.ctypes.data,
+                                      sc.ctypes.data)
+        return id1, id2, cnt, sc
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_matrix_free(self.h)
+            self.h = None

@@ -1,0 +1,127 @@
+"""Parity of the device k-mer -> id tables (kmer_to_id_ / kmer_to_family_id_)
+and /matrix pair counting with the CPU oracle (oracle/handlers_oracle.cpp)."""
+import numpy as np
+import pytest
+
+from close_kmers_amd import synth
+from helpers import pack, synthetic_table
+
+pytestmark = pytest.mark.gpu
+
+
+def _lists_equal(dev_kmap, orc_kmap, kmers):
+    off, ids = dev_kmap.lookup(kmers)
+    for i, k in enumerate(kmers):
+        got = ids[int(off[i]):int(off[i + 1])]
+        want = orc_kmap.lookup(int(k))
+        assert np.array_equal(got, want), (i, int(k), got[:10], want[:10])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kmap_add_matches_oracle(gpu, oracle_lib, mode):
+    rng = np.random.default_rng(11 + mode)
+    pool = rng.integers(0, 20 ** 8, 700, dtype=np.uint64)
+    dev = gpu.Kmap(0, mode)
+    orc = oracle_lib.Kmap(mode)
+    with dev:
+        for n in (3000, 1, 2500, 0, 4000):
+            k = pool[rng.integers(0, len(pool), n)]
+            v = rng.integers(0, 60, n).astype(np.uint32)
+            dev.add(k, v)
+            orc.add(k, v)
+            assert dev.num_kmers == orc.num_kmers
+        absent = rng.integers(0, 20 ** 8, 50, dtype=np.uint64)
+        _lists_equal(dev, orc, np.concatenate([pool, absent]))
+        if mode == 1:
+            off, ids = dev.lookup(pool)
+            for i in range(len(pool)):
+                lst = ids[int(off[i]):int(off[i + 1])]
+                assert len(set(lst.tolist())) == len(lst)
+
+
+def _family_proteins(spec, rng, n_fam, per_fam, sub=0.06):
+    """Members of n_fam families: image source proteins with substitutions."""
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(n_fam))].reshape(n_fam, -1)
+    seqs = []
+    for f in range(n_fam):
+        for _ in range(per_fam):
+            s = src[f].copy()
+            m = rng.random(len(s)) < sub
+            s[m] = synth.ALPHA[rng.integers(0, 20, int(m.sum()))]
+            cut = int(rng.integers(200, len(s) + 1))
+            seqs.append(bytes(s[:cut]))
+    return seqs
+
+
+@pytest.fixture(scope="module")
+def table_world(gpu):
+    spec, table = synthetic_table(60000)
+    img = gpu.Image.from_table(table)
+    ctx = gpu.Context(img)
+    yield spec, table, img, ctx
+    ctx.close()
+    img.close()
+
+
+def _oracle_hit_kmers(oracle_lib, table, seqs):
+    res, off = pack([("s", s) for s in seqs])
+    r = oracle_lib.process_batch(table, res, off, want=1)
+    return r.hit_offsets, r.hits["which_kmer"], res, off
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kmap_add_hits_matches_oracle(table_world, gpu, oracle_lib, mode):
+    spec, table, img, ctx = table_world
+    rng = np.random.default_rng(5)
+    seqs = _family_proteins(spec, rng, 12, 5)
+    hoff, hk, res, off = _oracle_hit_kmers(oracle_lib, table, seqs)
+    ids = rng.permutation(1000)[:len(seqs)].astype(np.uint32)
+    orc = oracle_lib.Kmap(mode)
+    with gpu.Kmap(0, mode) as dev:
+        for lo, hi in ((0, 25), (25, len(seqs))):  # two /add requests
+            ctx.process_batch(res[int(off[lo]):int(off[hi])], off[lo:hi + 1] - off[lo], want=1)
+            dev.add_hits(ctx, ids[lo:hi])
+            for s in range(lo, hi):
+                k = hk[int(hoff[s]):int(hoff[s + 1])]
+                orc.add(k, np.full(len(k), ids[s], np.uint32))
+        assert dev.num_kmers == orc.num_kmers
+        _lists_equal(dev, orc, np.unique(hk))
+
+
+def test_matrix_matches_oracle(table_world, gpu, oracle_lib):
+    spec, table, img, ctx = table_world
+    rng = np.random.default_rng(9)
+    seqs = _family_proteins(spec, rng, 10, 6)
+    n = len(seqs)
+    ids = (np.arange(n) * 7 + 3).astype(np.uint32)
+    hoff, hk, res, off = _oracle_hit_kmers(oracle_lib, table, seqs)
+    lens = np.diff(off).astype(np.uint64)
+    orc_map = oracle_lib.Kmap(0)
+    with gpu.Kmap(0, 0) as dev_map:
+        # /add of the first 50 proteins
+        ctx.process_batch(res[:int(off[50])], off[:51], want=1)
+        dev_map.add_hits(ctx, ids[:50])
+        for s in range(50):
+            k = hk[int(hoff[s]):int(hoff[s + 1])]
+            orc_map.add(k, np.full(len(k), ids[s], np.uint32))
+        # /matrix over a shuffled request with repeated and never-added ids, two chunks
+        order = rng.permutation(n)
+        order = np.concatenate([order, order[:5]])
+        req_ids = ids[order].copy()
+        req_ids[3] = 999999  # an id /add never saw
+        orc_mx = oracle_lib.Matrix()
+        with gpu.Matrix(dev_map) as mx:
+            for lo, hi in ((0, 31), (31, len(order))):
+                sel = order[lo:hi]
+                r2, o2 = pack([("s", seqs[i]) for i in sel])
+                ctx.process_batch(r2, o2, want=1)
+                mx.add_hits(ctx, req_ids[lo:hi])
+                sub_off = np.concatenate([[0], np.cumsum([int(hoff[i + 1] - hoff[i]) for i in sel])])
+                sub_k = np.concatenate([hk[int(hoff[i]):int(hoff[i + 1])] for i in sel])
+                orc_mx.add(orc_map, req_ids[lo:hi], lens[sel], sub_off.astype(np.uint64), sub_k)
+            got = mx.pairs()
+        id1, id2, cnt, score = orc_mx.pairs()
+        assert len(id1) > 100
+        assert np.array_equal(got["id1"], id1)
+        assert np.array_equal(got["id2"], id2)
+        assert np.array_equal(got["count"], cnt)
