@@ -452,6 +452,110 @@ void FastaParser::parse_complete()
     seq_.clear();
 }
 
+/* ---- KmerPegMapping / MatrixRequest ------------------------------------ */
+
+void run_batch_on_device(KmerGuts &kg, const std::vector<std::string> &seqs)
+{
+    std::vector<uint64_t> off(seqs.size() + 1, 0);
+    std::string buf;
+    for (size_t i = 0; i < seqs.size(); i++) {
+        buf += seqs[i];
+        off[i + 1] = buf.size();
+    }
+    kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
+    kgx_result r;
+    int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), (uint32_t)seqs.size(), 0, &r);
+    if (rc)
+        throw_last(rc, "kgx_process_batch");
+}
+
+KmerPegMapping::KmerPegMapping(int device) : device_(device)
+{
+    int rc = kgx_kmap_create(device, KGX_KMAP_APPEND, &kmer_to_id_);
+    if (!rc)
+        rc = kgx_kmap_create(device, KGX_KMAP_SET, &kmer_to_family_id_);
+    if (rc) {
+        kgx_kmap_destroy(kmer_to_id_);
+        throw_last(rc, "kgx_kmap_create");
+    }
+}
+
+KmerPegMapping::~KmerPegMapping()
+{
+    kgx_kmap_destroy(kmer_to_id_);
+    kgx_kmap_destroy(kmer_to_family_id_);
+}
+
+KmerPegMapping::encoded_id_t KmerPegMapping::encode_id(const std::string &peg)
+{
+    auto it = peg_to_id_.find(peg);
+    if (it != peg_to_id_.end())
+        return it->second;
+    const encoded_id_t id = (encoded_id_t)id_to_peg_.size();
+    peg_to_id_[peg] = id;
+    id_to_peg_.push_back(peg);
+    return id;
+}
+
+std::string KmerPegMapping::decode_id(encoded_id_t id) const
+{
+    return id < id_to_peg_.size() ? id_to_peg_[id] : std::string();
+}
+
+void KmerPegMapping::add_batch_mappings(KmerGuts &kg, const std::vector<encoded_id_t> &ids)
+{
+    int rc = kgx_kmap_add_hits(kmer_to_id_, kg.ctx(), ids.data());
+    if (rc)
+        throw_last(rc, "kgx_kmap_add_hits");
+}
+
+void KmerPegMapping::add_batch_fam_mappings(KmerGuts &kg, const std::vector<encoded_family_id_t> &ids)
+{
+    int rc = kgx_kmap_add_hits(kmer_to_family_id_, kg.ctx(), ids.data());
+    if (rc)
+        throw_last(rc, "kgx_kmap_add_hits");
+}
+
+MatrixRequest::MatrixRequest(std::shared_ptr<KmerPegMapping> mapping) : mapping_(mapping)
+{
+    int rc = kgx_matrix_create(mapping_->kmer_to_id(), &mx_);
+    if (rc)
+        throw_last(rc, "kgx_matrix_create");
+}
+
+MatrixRequest::~MatrixRequest() { kgx_matrix_destroy(mx_); }
+
+void MatrixRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work)
+{
+    std::vector<KmerPegMapping::encoded_id_t> ids;
+    std::vector<std::string> seqs;
+    for (auto &w : work) {
+        const KmerPegMapping::encoded_id_t eid = mapping_->encode_id(w.first);
+        matrix_proteins_[eid] = w.second.size(); /* matrix_request.cc:91 */
+        ids.push_back(eid);
+        seqs.push_back(w.second);
+    }
+    run_batch_on_device(kg, seqs);
+    int rc = kgx_matrix_add_hits(mx_, kg.ctx(), ids.data());
+    if (rc)
+        throw_last(rc, "kgx_matrix_add_hits");
+}
+
+void MatrixRequest::write_results(std::ostream &os)
+{
+    const kgx_pair_count *p = nullptr;
+    uint64_t n = 0;
+    int rc = kgx_matrix_pairs(mx_, &p, &n);
+    if (rc)
+        throw_last(rc, "kgx_matrix_pairs");
+    for (uint64_t i = 0; i < n; i++) {
+        const size_t l1 = matrix_proteins_[p[i].id1], l2 = matrix_proteins_[p[i].id2];
+        const float score = (float)p[i].count / ((float)(l1 + l2));
+        os << mapping_->decode_id(p[i].id1) << "\t" << mapping_->decode_id(p[i].id2) << "\t"
+           << (unsigned long)p[i].count << "\t" << score << "\n";
+    }
+}
+
 }  // namespace kgx
 
 extern "C" int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const *names,

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <functional>
 #include <map>
+#include <ostream>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -177,6 +178,67 @@ private:
     std::function<bool(const std::string &, int, const std::string)> on_error_;
     void emit();
 };
+
+/*
+ * KmerPegMapping (kmer.h:25-157), the parts the request handlers use: the peg
+ * id dictionary (encode_id / decode_id; ids assigned from 0 in first-seen
+ * order, assign_new_peg_id kmer.h:114-121) on the host, and kmer_to_id_ /
+ * kmer_to_family_id_ as device tables (include/kgx.h kgx_kmap).
+ */
+class KmerPegMapping {
+public:
+    typedef unsigned int encoded_id_t;
+    typedef unsigned int encoded_family_id_t;
+    explicit KmerPegMapping(int device = 0);
+    ~KmerPegMapping();
+    KmerPegMapping(const KmerPegMapping &) = delete;
+    KmerPegMapping &operator=(const KmerPegMapping &) = delete;
+
+    encoded_id_t encode_id(const std::string &peg);
+    std::string decode_id(encoded_id_t id) const; /* "" when unknown, kmer.cc:288-295 */
+    /* add_mapping (kmer.cc:173-210) for every hit of kg's last batch, in
+     * order: sequence s contributes ids[s] (add_request.cc:164-170) */
+    void add_batch_mappings(KmerGuts &kg, const std::vector<encoded_id_t> &ids);
+    /* add_fam_mapping (kmer.cc:212-256) likewise, into kmer_to_family_id_ */
+    void add_batch_fam_mappings(KmerGuts &kg, const std::vector<encoded_family_id_t> &fam_ids);
+    kgx_kmap *kmer_to_id() const { return kmer_to_id_; }
+    kgx_kmap *kmer_to_family_id() const { return kmer_to_family_id_; }
+    int device() const { return device_; }
+
+private:
+    int device_;
+    std::map<std::string, encoded_id_t> peg_to_id_;
+    std::vector<std::string> id_to_peg_;
+    kgx_kmap *kmer_to_id_ = nullptr;
+    kgx_kmap *kmer_to_family_id_ = nullptr;
+};
+
+/*
+ * MatrixRequest (matrix_request.cc:83-190): one /matrix request over a
+ * mapping.  process_work() is the per-chunk worker loop (every sequence of
+ * the chunk is encoded, its length recorded and its hits counted against
+ * the proteins seen so far, in one GPU pass); write_results() prints
+ * process_results' body (matrix_request.cc:171-187).
+ */
+class MatrixRequest {
+public:
+    explicit MatrixRequest(std::shared_ptr<KmerPegMapping> mapping);
+    ~MatrixRequest();
+    MatrixRequest(const MatrixRequest &) = delete;
+    MatrixRequest &operator=(const MatrixRequest &) = delete;
+    void process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work);
+    void write_results(std::ostream &os);
+
+private:
+    std::shared_ptr<KmerPegMapping> mapping_;
+    kgx_matrix *mx_ = nullptr;
+    std::map<KmerPegMapping::encoded_id_t, size_t> matrix_proteins_;
+};
+
+/* one host-buffer batch through kg's context, device results only (no D2H):
+ * what KmerPegMapping / MatrixRequest read from (kgx_kmap_add_hits,
+ * kgx_matrix_add_hits) */
+void run_batch_on_device(KmerGuts &kg, const std::vector<std::string> &seqs);
 
 /* find_best_call (kguts.cc:1008-1199) with an explicit function-name lookup */
 void best_call(const std::vector<KmerCall> &calls, const std::function<const char *(int)> &name_of,

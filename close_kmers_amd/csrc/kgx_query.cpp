@@ -9,6 +9,8 @@
  *   query_details  query_request.cc:103-151 with details=1 (HIT lines)
  *   query_best     query_request.cc:124-135 (find_best_call=1)
  *   add            add_request.cc:305-353 (silent=0)
+ *   matrix         /add of the FASTA into an empty mapping, then one /matrix
+ *                  request over the same FASTA (matrix_request.cc:83-190)
  *
  * usage: kgx_query DATA_DIR FASTA MODE [name=value ...]   (KGX_DEVICE=n)
  */
@@ -32,7 +34,8 @@ int main(int argc, char **argv)
         return 2;
     }
     const std::string dir = argv[1], fasta = argv[2], mode = argv[3];
-    if (mode != "query" && mode != "query_details" && mode != "query_best" && mode != "add") {
+    if (mode != "query" && mode != "query_details" && mode != "query_best" && mode != "add" &&
+        mode != "matrix") {
         std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
         return 2;
     }
@@ -68,6 +71,28 @@ int main(int argc, char **argv)
             parser.parse_char(ch);
         parser.parse_complete();
 
+        if (mode == "matrix") {
+            auto mapping = std::make_shared<KmerPegMapping>(image->handle() ? kgx_image_device(image->handle()) : 0);
+            std::vector<std::string> seqs;
+            std::vector<std::pair<std::string, std::string>> work;
+            for (auto &j : jobs) {
+                seqs.push_back(j.seq);
+                work.emplace_back(j.id, j.seq);
+            }
+            /* /add (add_request.cc:164-170 / 196-206): ids encoded in order */
+            run_batch_on_device(kguts, seqs);
+            std::vector<KmerPegMapping::encoded_id_t> ids;
+            for (auto &j : jobs)
+                ids.push_back(mapping->encode_id(j.id));
+            mapping->add_batch_mappings(kguts, ids);
+            MatrixRequest mx(mapping);
+            mx.process_work(kguts, work);
+            std::ostringstream os;
+            mx.write_results(os);
+            const std::string s = os.str();
+            std::fwrite(s.data(), 1, s.size(), stdout);
+            return 0;
+        }
         const bool details = mode == "query_details";
         std::vector<std::shared_ptr<std::vector<KmerGuts::hit_in_sequence_t>>> hit_lists(jobs.size());
         for (size_t i = 0; i < jobs.size(); i++) {

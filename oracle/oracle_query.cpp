@@ -9,6 +9,9 @@
  *   mode=query_details  query_request.cc:103-151 with details=1 (HIT lines)
  *   mode=query_best     query_request.cc:124-135 (find_best_call=1)
  *   mode=add            add_request.cc:305-353 (silent=0)
+ *   mode=matrix         /add of the FASTA into an empty mapping (add_request.cc:
+ *                       164-170), then one /matrix request over the same FASTA
+ *                       (matrix_request.cc:83-190): process_results' body
  *
  * usage: oracle_query DATA_DIR FASTA MODE [name=value ...]
  * The name=value pairs play the role of the request's query string
@@ -28,6 +31,17 @@
 #include <vector>
 
 using namespace oracle;
+
+extern "C" {
+void *oracle_kmap_new(int mode);
+void oracle_kmap_free(void *p);
+void oracle_kmap_add(void *p, const uint64_t *kmers, const uint32_t *ids, uint64_t n);
+void *oracle_matrix_new(void);
+void oracle_matrix_free(void *p);
+void oracle_matrix_add(void *px, void *pk, const uint32_t *seq_ids, const uint64_t *seq_lens,
+                       uint64_t n_seq, const uint64_t *hit_off, const uint64_t *hit_kmers);
+uint64_t oracle_matrix_pairs(void *px, uint32_t *id1, uint32_t *id2, uint64_t *count, float *score);
+}
 
 /* KmerImage::map_image_file validation, kmer_image.cc:83-150 */
 static bool load_image(const std::string &dir, std::vector<SigKmer> &table, uint64_t &num_sigs)
@@ -110,6 +124,51 @@ int main(int argc, char **argv)
     }
 
     std::ostringstream os;
+    if (mode == "matrix") {
+        /* KmerPegMapping::encode_id: ids from 0 in first-seen order (kmer.h:114-121) */
+        std::map<std::string, uint32_t> peg_to_id;
+        std::vector<std::string> id_to_peg;
+        auto encode = [&](const std::string &p) {
+            auto it = peg_to_id.find(p);
+            if (it != peg_to_id.end())
+                return it->second;
+            uint32_t id = (uint32_t)id_to_peg.size();
+            peg_to_id[p] = id;
+            id_to_peg.push_back(p);
+            return id;
+        };
+        std::vector<std::vector<uint64_t>> kmers(records.size());
+        for (size_t r = 0; r < records.size(); r++) {
+            std::vector<SeqHit> hits;
+            scorer.process(records[r].second.c_str(), records[r].second.size(), nullptr, &hits, nullptr,
+                           true);
+            for (auto &h : hits)
+                kmers[r].push_back(h.hit.which_kmer);
+        }
+        void *km = oracle_kmap_new(0);
+        for (size_t r = 0; r < records.size(); r++) { /* /add */
+            std::vector<uint32_t> ids(kmers[r].size(), encode(records[r].first));
+            oracle_kmap_add(km, kmers[r].data(), ids.data(), ids.size());
+        }
+        void *mx = oracle_matrix_new();
+        for (size_t r = 0; r < records.size(); r++) { /* /matrix */
+            uint32_t id = encode(records[r].first);
+            uint64_t len = records[r].second.size(), off[2] = {0, kmers[r].size()};
+            oracle_matrix_add(mx, km, &id, &len, 1, off, kmers[r].data());
+        }
+        uint64_t n = oracle_matrix_pairs(mx, nullptr, nullptr, nullptr, nullptr);
+        std::vector<uint32_t> a(n), b(n);
+        std::vector<uint64_t> c(n);
+        std::vector<float> sc(n);
+        oracle_matrix_pairs(mx, a.data(), b.data(), c.data(), sc.data());
+        for (uint64_t i = 0; i < n; i++)
+            os << id_to_peg[a[i]] << "\t" << id_to_peg[b[i]] << "\t" << (unsigned long)c[i] << "\t" << sc[i]
+               << "\n";
+        oracle_matrix_free(mx);
+        oracle_kmap_free(km);
+        std::fwrite(os.str().data(), 1, os.str().size(), stdout);
+        return 0;
+    }
     const bool details = (mode == "query_details");
     for (auto &rec : records) {
         const std::string &id = rec.first, &seq = rec.second;

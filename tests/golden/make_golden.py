@@ -17,6 +17,9 @@ Outputs (all small):
              parameter set.
   cap/       one 40,100-residue sequence whose single run overflows the
              40,000-entry hit buffer (kguts.cc:850-851), plus expected text.
+  matrix/    protein families sharing signature k-mers (plus cross-family
+             k-mers, repeated ids and unrelated proteins): the /add-then-
+             /matrix body (matrix_request.cc:165-190) from the oracle.
 The oracle (oracle/_build/oracle_query) produces every expected_*.txt; the
 scoring case is additionally checked against the reference's own lines.
 """
@@ -236,11 +239,46 @@ def make_cap(rng) -> None:
         open(os.path.join(out, f"expected_{mode}_default.txt"), "wb").write(txt)
 
 
+def make_matrix(rng) -> None:
+    out = os.path.join(HERE, "matrix")
+    img = DesignedImage()
+    bases = [random_protein(rng, int(rng.integers(120, 200))) for _ in range(6)]
+    for f, b in enumerate(bases):
+        img.add_windows(b, range(0, len(b) - 8, 2), f, oI=f % 3 - 1, rng=rng)
+    shared = random_protein(rng, 40)  # a motif planted in several families
+    img.add_windows(shared, range(0, 32), 7, rng=rng)
+    recs = []
+    for f, b in enumerate(bases):
+        for m in range(5):
+            s = list(b)
+            for p in rng.integers(0, len(s), int(len(s) * 0.08)):
+                s[p] = "ACDEFGHIKLMNPQRSTVWY"[int(rng.integers(0, 20))]
+            s = "".join(s)
+            if f % 2 == 0 and m < 3:
+                at = int(rng.integers(0, len(s) - 40))
+                s = s[:at] + shared + s[at + 40:]
+            recs.append((f"fig|6666666.{f}.peg.{m}", s))
+    recs.append(("fig|6666666.9.peg.1", random_protein(rng, 150)))   # unrelated
+    recs.append(("fig|6666666.0.peg.1", bases[0]))                   # repeated id
+    recs.append(("fig|6666666.9.peg.2", bases[3][10:90]))            # fragment
+    order = rng.permutation(len(recs))
+    recs = [recs[i] for i in order]
+    table = img.table()
+    data = os.path.join(out, "data")
+    image_files.write_data_dir(data, table, [f"function {i}" for i in range(8)], ["o0", "o1"])
+    fasta = os.path.join(out, "input.fasta")
+    write_fasta(fasta, recs)
+    txt = oracle.query_text(data, fasta, "matrix")
+    assert txt.count(b"\n") > 50
+    open(os.path.join(out, "expected_matrix_default.txt"), "wb").write(txt)
+
+
 def main() -> None:
     oracle.build(ref=False)
     make_scoring(np.random.default_rng(2024_08_07))
     make_edge(np.random.default_rng(12345))
     make_cap(np.random.default_rng(777))
+    make_matrix(np.random.default_rng(4242))
     print("golden fixtures written under", HERE)
 
 

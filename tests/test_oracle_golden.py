@@ -8,7 +8,7 @@ from helpers import GOLDEN
 
 
 def _cases():
-    for ds in ("scoring", "edge", "cap"):
+    for ds in ("scoring", "edge", "cap", "matrix"):
         d = os.path.join(GOLDEN, ds)
         for f in sorted(os.listdir(d)):
             if f.startswith("expected_") and f.endswith(".txt"):
@@ -25,7 +25,7 @@ PARAMS = {
 
 def parse_case(fname):
     stem = fname[len("expected_"):-len(".txt")]
-    for mode in ("query_details", "query_best", "query", "add"):
+    for mode in ("query_details", "query_best", "query", "add", "matrix"):
         if stem.startswith(mode + "_"):
             return mode, stem[len(mode) + 1:]
     raise ValueError(fname)
