@@ -1,0 +1,122 @@
+"""C3 benchmark: /matrix over 10,000 proteins (BASELINE.json configs[2]).
+
+    python tools/bench_matrix.py [--n-prot 10000] [--fam-size 10] [--n-keys 1e9]
+
+Workload: n_prot synthetic proteins in families of fam_size (each family =
+one source protein of the synthetic signature image with 10% substitutions
+per member, 300 aa).  A /add request of all proteins fills kmer_to_id_
+(add_request.cc:164-170); then one /matrix request over the same proteins
+(matrix_request.cc:83-190) counts shared signature k-mers per ordered pair.
+Timed on the GPU: the /matrix request end to end from host buffers (H2D
+residues, probe + score, pair counting, ordered D2H of distance_).  The CPU
+baseline is the oracle restatement (same std::map / std::unordered_map
+containers as the reference) of the same /matrix request over the same
+hits, with the oracle's own lookups, on one host thread.  Prints one JSON
+line.  Parity: the pair list is compared with the oracle's.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def family_proteins(spec, n_prot, fam_size, rng):
+    from close_kmers_amd import synth
+    n_fam = n_prot // fam_size
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(n_fam))].reshape(n_fam, -1)
+    res = np.repeat(src, fam_size, axis=0)
+    m = rng.random(res.shape) < 0.10
+    res[m] = synth.ALPHA[rng.integers(0, 20, int(m.sum()))]
+    off = np.arange(0, res.size + 1, res.shape[1], dtype=np.uint64)
+    return res.reshape(-1).copy(), off
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-prot", type=int, default=10000)
+    ap.add_argument("--fam-size", type=int, default=10)
+    ap.add_argument("--n-keys", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from close_kmers_amd import abi, synth
+    spec = synth.ImageSpec(int(args.n_keys))
+    img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs)
+    ctx = abi.Context(img)
+    rng = np.random.default_rng(0x5EED0005)
+    res, off = family_proteins(spec, args.n_prot, args.fam_size, rng)
+    n = args.n_prot
+    ids = np.arange(n, dtype=np.uint32)
+    lens = np.diff(off)
+
+    # /add: one request over all proteins
+    kmap = abi.Kmap(0, abi.KMAP_APPEND)
+    t0 = time.perf_counter()
+    ctx.process_batch(res, off, want=0)
+    kmap.add_hits(ctx, ids)
+    t_add = time.perf_counter() - t0
+
+    def matrix_request():
+        mx = abi.Matrix(kmap)
+        ctx.process_batch(res, off, want=0)
+        mx.add_hits(ctx, ids)
+        pairs = mx.pairs()
+        mx.close()
+        return pairs
+
+    matrix_request()  # warm
+    times = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        pairs = matrix_request()
+        times.append(time.perf_counter() - t0)
+    t_mx = float(np.median(times))
+    line = {
+        "metric": "matrix_request pairwise k-mer-set counts (C3)",
+        "value": n / t_mx, "unit": "proteins/s", "ms_per_request": t_mx * 1e3,
+        "add_request_ms": t_add * 1e3, "pairs": int(len(pairs)),
+        "kmap_kmers": kmap.num_kmers, "kmap_values": kmap.num_values,
+        "config": {"n_prot": n, "fam_size": args.fam_size, "seq_len": int(lens[0]),
+                   "n_keys": spec.n_keys, "num_sigs": spec.num_sigs,
+                   "image_layout": ["AOS24", "PACKED16"][img.layout]},
+    }
+    if not args.no_cpu_baseline:
+        import oracle
+        oracle.build(ref=False)
+        table = img.download()
+        t0 = time.perf_counter()
+        r = oracle.process_batch(table, res, off, want=1, n_threads=1)
+        km = oracle.Kmap(0)
+        hk = r.hits["which_kmer"]
+        hoff = r.hit_offsets
+        km.add(hk, np.repeat(ids, np.diff(hoff).astype(np.int64)))
+        t_add_cpu = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        r = oracle.process_batch(table, res, off, want=1, n_threads=1)
+        om = oracle.Matrix()
+        om.add(km, ids, lens, r.hit_offsets, r.hits["which_kmer"])
+        id1, id2, cnt, _ = om.pairs()
+        t_cpu = time.perf_counter() - t0
+        del table
+        line["cpu_baseline"] = {"value": n / t_cpu, "unit": "proteins/s", "cores": 1, "kind": "port",
+                                "ms_per_request": t_cpu * 1e3, "add_request_ms": t_add_cpu * 1e3,
+                                "sample": "the same /matrix request (oracle lookups + std::map pair counts)"}
+        line["parity"] = bool(np.array_equal(pairs["id1"], id1) and np.array_equal(pairs["id2"], id2)
+                              and np.array_equal(pairs["count"], cnt))
+    print(json.dumps(line), flush=True)
+    kmap.close()
+    ctx.close()
+    img.close()
+
+
+if __name__ == "__main__":
+    main()
