@@ -56,6 +56,12 @@ class DeviceResult(ctypes.Structure):
                 ("hits", ctypes.c_void_p), ("calls", ctypes.c_void_p)]
 
 
+class Fragments(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_uint32), ("n_fragments", ctypes.c_uint32),
+                ("n_residues", ctypes.c_uint64), ("residues", ctypes.c_void_p),
+                ("offsets", ctypes.c_void_p), ("read", ctypes.c_void_p), ("frame", ctypes.c_void_p)]
+
+
 def tiled_hits_per_sequence(window_base: np.ndarray, hit_mask: np.ndarray, tile_windows: int,
                             hits: np.ndarray) -> list[np.ndarray]:
     """Host-side walk of kgx_device_result's tiled hit layout (for tests and
@@ -120,6 +126,12 @@ SIGNATURES = {
                                   ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_INT)]),
     "kgx_microbench_random_read": (_INT, [_P, _U64, _INT, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(_U64)]),
+    "kgx_device_batch_collect": (_INT, [_P, _U32, ctypes.POINTER(Result)]),
+    "kgx_fq_fragments": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
+    "kgx_fq_fragments_device": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
+    "kgx_fq_create": (_INT, [_P, _CS, _CS, _CS, _CS, _PP]),
+    "kgx_fq_destroy": (_INT, [_P]),
+    "kgx_fq_process": (_INT, [_P, _P, _U64, _INT, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U64)]),
     "kgx_kmap_create": (_INT, [_INT, _INT, _PP]),
     "kgx_kmap_destroy": (_INT, [_P]),
     "kgx_kmap_add": (_INT, [_P, _P, _P, _U64]),
@@ -300,6 +312,40 @@ class Context:
               "kgx_process_batch")
         return BatchResult(r, want)
 
+    def fq_fragments(self, bases, read_offsets) -> Fragments:
+        """6-frame code-11 fragments (> 10 aa) of the reads, left on the device."""
+        bases = np.ascontiguousarray(np.frombuffer(bytes(bases), np.uint8)
+                                     if isinstance(bases, (bytes, bytearray)) else bases, dtype=np.uint8)
+        off = np.ascontiguousarray(read_offsets, dtype=np.uint64)
+        f = Fragments()
+        check(lib().kgx_fq_fragments(self.handle, bases.ctypes.data if bases.size else None,
+                                     off.ctypes.data, len(off) - 1, ctypes.byref(f)), "kgx_fq_fragments")
+        return f
+
+    def fragments_to_host(self, f: Fragments) -> dict:
+        """Host copies of a kgx_fragments (tests / tools)."""
+        self.synchronize()
+        n, nr = f.n_fragments, f.n_residues
+        out = {"residues": np.zeros(nr, np.uint8), "offsets": np.zeros(n + 1, np.uint64),
+               "read": np.zeros(n, np.uint32), "frame": np.zeros(n, np.int8)}
+        for k, ptr in (("residues", f.residues), ("offsets", f.offsets), ("read", f.read),
+                       ("frame", f.frame)):
+            a = out[k]
+            if a.nbytes:
+                check(lib().kgx_memcpy_d2h(a.ctypes.data, ptr, a.nbytes), "d2h")
+        return out
+
+    def run_fragments(self, f: Fragments, params: Params | dict | None = None,
+                      want: int = WANT_HITS | WANT_CALLS) -> BatchResult:
+        """The lookup over device fragments, results collected to the host."""
+        if params is None or isinstance(params, dict):
+            params = parse_params(params)
+        check(lib().kgx_run_device(self.handle, ctypes.byref(params), f.residues, f.offsets,
+                                   f.n_fragments, f.n_residues, want, None), "kgx_run_device")
+        r = Result()
+        check(lib().kgx_device_batch_collect(self.handle, want, ctypes.byref(r)), "collect")
+        return BatchResult(r, want)
+
     @property
     def stream(self) -> int:
         return lib().kgx_ctx_stream(self.handle)
@@ -414,6 +460,34 @@ class Matrix:
     def close(self) -> None:
         if self.handle:
             lib().kgx_matrix_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class FqHandler:
+    """The fq request handler (kgx_fq_*) over an image."""
+
+    def __init__(self, image: Image, data_dir: str, genus: str = "", families: str = "", nr: str = ""):
+        h = ctypes.c_void_p()
+        check(lib().kgx_fq_create(image.handle, data_dir.encode(), genus.encode(), families.encode(),
+                                  nr.encode(), ctypes.byref(h)), "kgx_fq_create")
+        self.handle = h.value
+
+    def process(self, fastq: bytes, finished: bool = True) -> bytes:
+        t, n = ctypes.c_char_p(), ctypes.c_uint64()
+        buf = ctypes.create_string_buffer(fastq, len(fastq))
+        check(lib().kgx_fq_process(self.handle, buf, len(fastq), int(finished), ctypes.byref(t),
+                                   ctypes.byref(n)), "kgx_fq_process")
+        return ctypes.string_at(t, n.value) if n.value else b""
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_fq_destroy(self.handle)
             self.handle = None
 
     def __enter__(self):

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cctype>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <sstream>
 
@@ -58,7 +59,17 @@ KmerImage::KmerImage(kgx_image *adopted) : img_(adopted)
         throw Error(KGX_EINVAL, "KmerImage: null image");
 }
 
-KmerImage::~KmerImage() { kgx_image_close(img_); }
+KmerImage::KmerImage(kgx_image *borrowed, bool owned) : img_(borrowed), owned_(owned)
+{
+    if (!img_)
+        throw Error(KGX_EINVAL, "KmerImage: null image");
+}
+
+KmerImage::~KmerImage()
+{
+    if (owned_)
+        kgx_image_close(img_);
+}
 
 /* ---- index files ----------------------------------------------------------- */
 
@@ -556,6 +567,344 @@ void MatrixRequest::write_results(std::ostream &os)
     }
 }
 
+/* ---- family DB, FamilyMapper, FqRequest ---------------------------------- */
+
+KmerPegMapping::encoded_id_t KmerPegMapping::assign_new_peg_id(const std::string &peg)
+{
+    const encoded_id_t id = (encoded_id_t)id_to_peg_.size();
+    peg_to_id_[peg] = id;
+    id_to_peg_.push_back(peg);
+    return id;
+}
+
+static std::vector<std::string> split_tabs(const std::string &line)
+{
+    std::vector<std::string> cols; /* boost::split(cols, line, is_any_of("\t")) */
+    size_t a = 0;
+    for (;;) {
+        size_t b = line.find('\t', a);
+        cols.push_back(line.substr(a, b == std::string::npos ? std::string::npos : b - a));
+        if (b == std::string::npos)
+            return cols;
+        a = b + 1;
+    }
+}
+
+void KmerPegMapping::load_genus_map(const std::string &genus_file)
+{
+    std::ifstream gf(genus_file);
+    if (gf.fail())
+        throw Error(KGX_EIO, "Error opening gnus file " + genus_file);
+    std::string line;
+    while (std::getline(gf, line)) {
+        auto cols = split_tabs(line);
+        genus_map_[cols[0]] = cols.size() > 1 ? cols[1] : std::string();
+    }
+}
+
+void KmerPegMapping::load_families(const std::string &families_file)
+{
+    std::ifstream f(families_file);
+    if (f.fail())
+        throw Error(KGX_EIO, "Failure opening families file " + families_file);
+    const std::string zeros("00000000");
+    std::string line;
+    while (std::getline(f, line)) {
+        auto cols = split_tabs(line);
+        if (cols.size() < 9)
+            continue;
+        std::string pgf = "PGF_" + cols[0].substr(2);
+        std::string plf("PLF_");
+        unsigned long genus_id = 0;
+        auto mapped = genus_map_.find(cols[7]);
+        if (mapped == genus_map_.end()) {
+            plf += cols[7];
+        } else {
+            plf += mapped->second;
+            genus_id = std::stoul(mapped->second);
+        }
+        plf += "_";
+        plf += zeros.substr(0, 8 - cols[8].size());
+        plf += cols[8];
+        const encoded_id_t id = assign_new_peg_id(cols[3]);
+        const unsigned long seqlen = std::stoul(cols[4]);
+        auto fkey = std::make_pair(pgf, plf);
+        encoded_family_id_t fam_id;
+        auto fit = family_key_to_id_.find(fkey);
+        if (fit == family_key_to_id_.end()) {
+            fam_id = next_family_id_++;
+            family_key_to_id_[fkey] = fam_id;
+            family_data_.emplace(fam_id, family_data_t{pgf, plf, genus_id, cols[5], fam_id, seqlen, 1});
+        } else {
+            fam_id = fit->second;
+            family_data_t &d = family_data_[fam_id];
+            d.total_size += seqlen;
+            d.count++;
+        }
+        peg_to_family_.insert(std::make_pair(id, fam_id));
+    }
+}
+
+void KmerPegMapping::load_nr_families(KmerGuts &kg, const std::string &nr_fasta, size_t batch)
+{
+    std::ifstream in(nr_fasta, std::ios::binary);
+    if (!in)
+        throw Error(KGX_EIO, "cannot open " + nr_fasta);
+    std::vector<std::string> seqs;
+    std::vector<encoded_family_id_t> fams;
+    auto flush = [&]() {
+        if (seqs.empty())
+            return;
+        run_batch_on_device(kg, seqs);
+        add_batch_fam_mappings(kg, fams);
+        seqs.clear();
+        fams.clear();
+    };
+    FastaParser parser;
+    parser.set_callback([&](const std::string &id, const std::string &seq) {
+        auto fit = peg_to_family_.find(encode_id(id));
+        if (fit == peg_to_family_.end())
+            return 0; /* "NO FAM FOR id=..." (nr_loader.cc:150-156) */
+        seqs.push_back(seq);
+        fams.push_back(fit->second);
+        if (seqs.size() >= batch)
+            flush();
+        return 0;
+    });
+    char ch;
+    while (in.get(ch))
+        parser.parse_char(ch);
+    parser.parse_complete();
+    flush();
+}
+
+FamilyMapper::FamilyMapper(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping) : kg_(kg), mapping_(mapping) {}
+
+FamilyMapper::best_match_t
+FamilyMapper::find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
+                                     const uint32_t *list_ids, std::vector<KmerCall> &calls)
+{
+    seq_score_.clear(); /* ingest_protein, family_mapper.cc:48 */
+    for (auto &hl : hit_lists) { /* on_hit, family_mapper.cc:287-312 */
+        if (hl.second == 0)
+            continue;
+        const float weight = 1.0f / (float)hl.second;
+        for (uint32_t j = 0; j < hl.second; j++) {
+            sequence_accumulated_score_t &s = seq_score_[list_ids[hl.first + j]];
+            s.hit_count++;
+            s.hit_total++;
+            s.weighted_total += weight;
+        }
+    }
+    int fi;
+    std::string fn;
+    float score, wscore, off = 0.0f;
+    kg_.find_best_call(calls, fi, fn, score, wscore, off);
+    if (fn.empty() || fn.find(" ?? ") != std::string::npos)
+        fn = "hypothetical protein"; /* allow_ambiguous_functions_ = false */
+    float best_lf = 0.0f, best_gf = 0.0f;
+    std::string lf, gf;
+    std::unordered_map<std::string, float> pgf_rollup;
+    for (auto hit_ent : seq_score_) {
+        const sequence_accumulated_score_t &se = hit_ent.second;
+        if (se.hit_total < kmer_hit_threshold_)
+            continue;
+        auto fent = mapping_->family_data_.find(hit_ent.first);
+        if (fent == mapping_->family_data_.end())
+            continue;
+        const KmerPegMapping::family_data_t &fd = fent->second;
+        if (fd.function != fn)
+            continue;
+        pgf_rollup[fd.pgf] += se.weighted_total;
+        if (se.weighted_total > best_lf) {
+            best_lf = se.weighted_total;
+            lf = fd.plf;
+        }
+    }
+    for (auto pgf_ent : pgf_rollup)
+        if (pgf_ent.second > best_gf) {
+            best_gf = pgf_ent.second;
+            gf = pgf_ent.first;
+        }
+    return best_match_t{gf, best_gf, lf, best_lf, fn, score};
+}
+
+std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m)
+{
+    /* family_mapper.h:70-75 */
+    os << m.gfam_id << "\t" << m.gfam_score << "\t" << m.lfam_id << "\t" << m.lfam_score << "\t" << m.function
+       << "\t" << m.score;
+    return os;
+}
+
+FqRequest::FqRequest(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping) : kg_(kg), mapping_(mapping) {}
+
+void FqRequest::process(const std::string &block, bool finished, std::ostream &os)
+{
+    /* FastqParser::parse_char (fastq_parser.h:40-150); bad characters are
+     * reported there and skipped */
+    enum { S_START, S_ID, S_DEF, S_DATA, S_PLUS_START, S_PLUS, S_QUAL };
+    std::vector<std::pair<std::string, std::string>> reads;
+    for (char c : block) {
+        switch (state_) {
+        case S_START:
+            if (c == '@')
+                state_ = S_ID;
+            break;
+        case S_ID:
+            if (c == ' ' || c == '\t')
+                state_ = S_DEF;
+            else if (c == '\n')
+                state_ = S_DATA;
+            else
+                id_.push_back(c);
+            break;
+        case S_DEF:
+            if (c == '\n')
+                state_ = S_DATA;
+            break;
+        case S_DATA:
+            if (c == '\n')
+                state_ = S_PLUS_START;
+            else if (std::isalpha((unsigned char)c))
+                seq_.push_back(c);
+            break;
+        case S_PLUS_START:
+            if (c == '+')
+                state_ = S_PLUS;
+            break;
+        case S_PLUS:
+            if (c == '\n')
+                state_ = S_QUAL;
+            break;
+        case S_QUAL:
+            if (c == '\n') {
+                reads.emplace_back(id_, seq_);
+                id_.clear();
+                seq_.clear();
+                state_ = S_START;
+            }
+            break;
+        }
+    }
+    if (finished) { /* parse_complete, fastq_parser.cc:29-35 */
+        reads.emplace_back(id_, seq_);
+        id_.clear();
+        seq_.clear();
+    }
+    process_reads(reads, os);
+}
+
+void FqRequest::process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os)
+{
+    if (reads.empty())
+        return;
+    /* the block's reads -> fragments -> lookup, one GPU batch */
+    std::string bases;
+    std::vector<uint64_t> roff(reads.size() + 1, 0);
+    for (size_t r = 0; r < reads.size(); r++) {
+        bases += reads[r].second;
+        roff[r + 1] = bases.size();
+    }
+    kgx_ctx *ctx = kg_.ctx();
+    kgx_fragments fr;
+    int rc = kgx_fq_fragments(ctx, bases.data(), roff.data(), (uint32_t)reads.size(), &fr);
+    if (rc)
+        throw_last(rc, "kgx_fq_fragments");
+    kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
+    /* Without family lists a fragment's match depends on its calls alone,
+     * and a read without calls scores 0 in every frame: no output and no
+     * FamilyMapper state (seq_score_ stays empty).  Only then may reads
+     * without calls be skipped and hits stay on the device; with families
+     * loaded every fragment is replayed, since each one grows seq_score_ and
+     * so shapes the iteration order later reads see. */
+    const bool families = kgx_kmap_num_kmers(mapping_->kmer_to_family_id()) > 0;
+    const uint32_t want = families ? (KGX_WANT_HITS | KGX_WANT_CALLS) : KGX_WANT_CALLS;
+    rc = kgx_run_device(ctx, &p, fr.residues, fr.offsets, fr.n_fragments, fr.n_residues, want, nullptr);
+    if (rc)
+        throw_last(rc, "kgx_run_device");
+    std::vector<uint32_t> frag_read(fr.n_fragments);
+    std::vector<int8_t> frag_frame(fr.n_fragments);
+    std::vector<uint64_t> frag_off(fr.n_fragments + 1);
+    if (fr.n_fragments) {
+        kgx_ctx_synchronize(ctx);
+        kgx_memcpy_d2h(frag_read.data(), fr.read, frag_read.size() * 4);
+        kgx_memcpy_d2h(frag_frame.data(), fr.frame, frag_frame.size());
+    }
+    kgx_memcpy_d2h(frag_off.data(), fr.offsets, frag_off.size() * 8);
+    kgx_result res;
+    rc = kgx_device_batch_collect(ctx, want, &res);
+    if (rc)
+        throw_last(rc, "kgx_device_batch_collect");
+    /* kmer_to_family_id_ lists of every hit */
+    const uint64_t nh = fr.n_fragments && families ? res.hit_offsets[fr.n_fragments] : 0;
+    std::vector<uint64_t> list_off(nh + 1, 0);
+    std::vector<uint32_t> list_ids;
+    if (nh) {
+        std::vector<uint64_t> kmers(nh);
+        for (uint64_t i = 0; i < nh; i++)
+            kmers[i] = res.hits[i].which_kmer;
+        rc = kgx_kmap_lookup(mapping_->kmer_to_family_id(), kmers.data(), nh, list_off.data(), nullptr, 0);
+        if (!rc) {
+            list_ids.resize(list_off[nh]);
+            rc = kgx_kmap_lookup(mapping_->kmer_to_family_id(), kmers.data(), nh, list_off.data(),
+                                 list_ids.data(), list_ids.size());
+        }
+        if (rc)
+            throw_last(rc, "kgx_kmap_lookup");
+    }
+    /* on_parsed_seq (fq_process_request.cc:298-365), reads in order */
+    FamilyMapper mapper(kg_, mapping_);
+    std::vector<std::pair<uint64_t, uint32_t>> hit_lists;
+    std::vector<KmerCall> calls;
+    uint64_t f = 0;
+    for (uint32_t r = 0; r < (uint32_t)reads.size(); r++) {
+        const uint64_t f0 = f;
+        while (f < fr.n_fragments && frag_read[f] == r)
+            f++;
+        if (reads[r].first.empty())
+            continue;
+        if (!families && res.call_offsets[f] == res.call_offsets[f0])
+            continue; /* no calls in any frame: no output, no mapper state */
+        double best_score = 0.0;
+        int best_frame = 0;
+        std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
+        uint64_t g = f0;
+        while (g < f) {
+            const int frame = frag_frame[g];
+            double score = 0.0;
+            matches.clear();
+            for (; g < f && frag_frame[g] == frame; g++) {
+                hit_lists.clear();
+                if (families)
+                    for (uint64_t h = res.hit_offsets[g]; h < res.hit_offsets[g + 1]; h++)
+                        hit_lists.emplace_back(list_off[h], (uint32_t)(list_off[h + 1] - list_off[h]));
+                calls.clear();
+                for (uint64_t c = res.call_offsets[g]; c < res.call_offsets[g + 1]; c++)
+                    calls.emplace_back(res.calls[c].start, res.calls[c].end, res.calls[c].count,
+                                       res.calls[c].function_index, res.calls[c].weighted_hits);
+                matches.emplace_back((size_t)(frag_off[g + 1] - frag_off[g]),
+                                     mapper.find_best_family_match(hit_lists, list_ids.data(), calls));
+                score += matches.back().second.score;
+                if (score > best_score) {
+                    best_score = score;
+                    best_frame = frame;
+                    best_matches = matches;
+                }
+            }
+        }
+        if (best_score > 0.0) {
+            os << reads[r].first << "\t" << best_frame << "\t" << best_score << "\t";
+            for (size_t i = 0; i < best_matches.size(); i++) {
+                if (i)
+                    os << "\t";
+                os << best_matches[i].first << "\t" << best_matches[i].second;
+            }
+            os << std::endl;
+        }
+    }
+}
+
 }  // namespace kgx
 
 extern "C" int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const *names,
@@ -586,3 +935,72 @@ extern "C" int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const c
         *score_offset_set = n_calls > 0;
     return KGX_OK;
 }
+
+/* ---- C ABI of the fq request handler (include/kgx.h kgx_fq_*) ------------- */
+
+namespace kgx {
+int fail(int code, const std::string &msg); /* kgx_runtime.cpp: sets kgx_last_error() */
+}
+
+struct kgx_fq {
+    std::unique_ptr<kgx::KmerGuts> kg;
+    std::shared_ptr<kgx::KmerPegMapping> mapping;
+    std::unique_ptr<kgx::FqRequest> req;
+    std::string text;
+};
+
+extern "C" {
+
+int kgx_fq_create(kgx_image *img, const char *data_dir, const char *genus_file, const char *families_file,
+                  const char *nr_fasta, kgx_fq **out)
+{
+    if (!img || !data_dir || !out)
+        return kgx::fail(KGX_EINVAL, "null argument");
+    kgx_fq *q = new kgx_fq;
+    try {
+        auto image = std::make_shared<kgx::KmerImage>(img, false);
+        q->kg.reset(new kgx::KmerGuts(data_dir, image));
+        q->mapping = std::make_shared<kgx::KmerPegMapping>(kgx_image_device(img));
+        if (genus_file && *genus_file)
+            q->mapping->load_genus_map(genus_file);
+        if (families_file && *families_file)
+            q->mapping->load_families(families_file);
+        if (nr_fasta && *nr_fasta)
+            q->mapping->load_nr_families(*q->kg, nr_fasta);
+        q->req.reset(new kgx::FqRequest(*q->kg, q->mapping));
+    } catch (const kgx::Error &e) {
+        delete q;
+        return kgx::fail(e.code(), e.what());
+    } catch (const std::exception &e) {
+        delete q;
+        return kgx::fail(KGX_EINVAL, e.what());
+    }
+    *out = q;
+    return KGX_OK;
+}
+
+int kgx_fq_destroy(kgx_fq *q)
+{
+    delete q;
+    return KGX_OK;
+}
+
+int kgx_fq_process(kgx_fq *q, const char *fastq, uint64_t n, int finished, const char **text, uint64_t *text_len)
+{
+    if (!q || (n && !fastq) || !text || !text_len)
+        return kgx::fail(KGX_EINVAL, "null argument");
+    try {
+        std::ostringstream os;
+        q->req->process(std::string(fastq ? fastq : "", n), finished != 0, os);
+        q->text = os.str();
+    } catch (const kgx::Error &e) {
+        return kgx::fail(e.code(), e.what());
+    } catch (const std::exception &e) {
+        return kgx::fail(KGX_EINVAL, e.what());
+    }
+    *text = q->text.data();
+    *text_len = q->text.size();
+    return KGX_OK;
+}
+
+}  // extern "C"

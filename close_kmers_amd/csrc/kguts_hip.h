@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <functional>
 #include <map>
+#include <unordered_map>
 #include <ostream>
 #include <memory>
 #include <stdexcept>
@@ -74,6 +75,8 @@ public:
     explicit KmerImage(const std::string &data_dir, int device = 0);
     /* adopt an image built elsewhere (e.g. kgx_image_build_synthetic) */
     explicit KmerImage(kgx_image *adopted);
+    /* a borrowed image (closed by its owner, not here) */
+    KmerImage(kgx_image *borrowed, bool owned);
     ~KmerImage();
     KmerImage(const KmerImage &) = delete;
     KmerImage &operator=(const KmerImage &) = delete;
@@ -85,6 +88,7 @@ public:
 private:
     kgx_image *img_ = nullptr;
     std::string data_dir_;
+    bool owned_ = true;
 };
 
 class KmerGuts {
@@ -205,7 +209,32 @@ public:
     kgx_kmap *kmer_to_family_id() const { return kmer_to_family_id_; }
     int device() const { return device_; }
 
+    /* family data (kmer.h:58-66) */
+    struct family_data_t {
+        std::string pgf;
+        std::string plf;
+        unsigned long genus_id;
+        std::string function;
+        encoded_family_id_t family_id;
+        unsigned long total_size; /* in aa */
+        unsigned short count;
+    };
+    std::map<std::string, std::string> genus_map_;
+    std::unordered_map<encoded_family_id_t, family_data_t> family_data_;
+    std::map<std::pair<std::string, std::string>, encoded_family_id_t> family_key_to_id_;
+    std::unordered_map<encoded_id_t, encoded_family_id_t> peg_to_family_;
+    encoded_id_t assign_new_peg_id(const std::string &peg); /* kmer.h:114-121 */
+    /* kmer.cc:341-358; throws kgx::Error when the file cannot be read */
+    void load_genus_map(const std::string &genus_file);
+    /* kmer.cc:375-493 with one reader thread (families in file order) */
+    void load_families(const std::string &families_file);
+    /* NRLoader family mode (nr_loader.cc:130-176) over a protein FASTA: every
+     * hit of a protein with a family adds (k-mer, family) to
+     * kmer_to_family_id_, proteins in file order, batched on the GPU */
+    void load_nr_families(KmerGuts &kg, const std::string &nr_fasta, size_t batch = 100000);
+
 private:
+    encoded_family_id_t next_family_id_ = 0;
     int device_;
     std::map<std::string, encoded_id_t> peg_to_id_;
     std::vector<std::string> id_to_peg_;
@@ -233,6 +262,67 @@ private:
     std::shared_ptr<KmerPegMapping> mapping_;
     kgx_matrix *mx_ = nullptr;
     std::map<KmerPegMapping::encoded_id_t, size_t> matrix_proteins_;
+};
+
+/*
+ * FamilyMapper (family_mapper.cc:46-205, 287-330) in family mode with
+ * allow_ambiguous_functions_ = false, over results computed in batches: the
+ * caller supplies a fragment's hits (k-mers, in position order) with their
+ * kmer_to_family_id_ lists and its calls.  seq_score_ is one
+ * std::unordered_map kept across calls (cleared per protein), as in the
+ * reference, so iteration -- and with it tie and summation order -- matches.
+ */
+class FamilyMapper {
+public:
+    struct best_match_t {
+        std::string gfam_id;
+        float gfam_score;
+        std::string lfam_id;
+        float lfam_score;
+        std::string function;
+        float score;
+    };
+    struct sequence_accumulated_score_t {
+        unsigned int hit_count = 0;
+        unsigned int hit_total = 0;
+        float weighted_total = 0.0f;
+    };
+    FamilyMapper(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping);
+    /* hit_lists[h] = (first, count) into list_ids for hit h */
+    best_match_t find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
+                                        const uint32_t *list_ids, std::vector<KmerCall> &calls);
+    unsigned int kmer_hit_threshold_ = 3;
+
+private:
+    KmerGuts &kg_;
+    std::shared_ptr<KmerPegMapping> mapping_;
+    std::unordered_map<KmerPegMapping::encoded_id_t, sequence_accumulated_score_t> seq_score_;
+};
+std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m);
+
+/*
+ * FqProcessRequest (fq_process_request.cc:230-365): FASTQ in, per read the
+ * best frame's family matches out.  process() runs a block: the reads'
+ * 6-frame fragments, their lookup and scoring on the GPU in one batch, then
+ * on_parsed_seq's frame choice and FamilyMapper in read order on the host
+ * (one FamilyMapper per block, as process_data constructs one,
+ * fq_process_request.cc:241).
+ */
+class FqRequest {
+public:
+    FqRequest(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping);
+    /* one block of FASTQ text; `finished` = the request's last block
+     * (parse_complete).  Output lines are appended to os. */
+    void process(const std::string &fastq_block, bool finished, std::ostream &os);
+    /* reads already parsed (id, DNA) */
+    void process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os);
+
+private:
+    KmerGuts &kg_;
+    std::shared_ptr<KmerPegMapping> mapping_;
+    /* FastqParser state (fastq_parser.h:40-150) */
+    int state_ = 0;
+    std::string id_, seq_;
 };
 
 /* one host-buffer batch through kg's context, device results only (no D2H):

@@ -9,6 +9,8 @@
  *   query_details  query_request.cc:103-151 with details=1 (HIT lines)
  *   query_best     query_request.cc:124-135 (find_best_call=1)
  *   add            add_request.cc:305-353 (silent=0)
+ *   fq             the input is FASTQ: fq_process_request.cc:230-365 over
+ *                  FamilyMapper; genus=, families=, nr= load the family DB
  *   matrix         /add of the FASTA into an empty mapping, then one /matrix
  *                  request over the same FASTA (matrix_request.cc:83-190)
  *
@@ -35,7 +37,7 @@ int main(int argc, char **argv)
     }
     const std::string dir = argv[1], fasta = argv[2], mode = argv[3];
     if (mode != "query" && mode != "query_details" && mode != "query_best" && mode != "add" &&
-        mode != "matrix") {
+        mode != "matrix" && mode != "fq") {
         std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
         return 2;
     }
@@ -52,6 +54,28 @@ int main(int argc, char **argv)
         KmerGuts kguts(dir, image);
         kguts.set_parameters(qp);
 
+        if (mode == "fq") {
+            auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
+            if (!qp["genus"].empty())
+                mapping->load_genus_map(qp["genus"]);
+            if (!qp["families"].empty())
+                mapping->load_families(qp["families"]);
+            if (!qp["nr"].empty())
+                mapping->load_nr_families(kguts, qp["nr"]);
+            std::ifstream in(fasta, std::ios::binary);
+            if (!in) {
+                std::fprintf(stderr, "cannot open %s\n", fasta.c_str());
+                return 1;
+            }
+            std::stringstream ss;
+            ss << in.rdbuf();
+            FqRequest req(kguts, mapping);
+            std::ostringstream os;
+            req.process(ss.str(), true, os);
+            const std::string s = os.str();
+            std::fwrite(s.data(), 1, s.size(), stdout);
+            return 0;
+        }
         std::vector<KmerGuts::SeqJob> jobs;
         FastaParser parser;
         parser.set_callback([&jobs](const std::string &id, const std::string &seq) {
@@ -72,7 +96,7 @@ int main(int argc, char **argv)
         parser.parse_complete();
 
         if (mode == "matrix") {
-            auto mapping = std::make_shared<KmerPegMapping>(image->handle() ? kgx_image_device(image->handle()) : 0);
+            auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
             std::vector<std::string> seqs;
             std::vector<std::pair<std::string, std::string>> work;
             for (auto &j : jobs) {

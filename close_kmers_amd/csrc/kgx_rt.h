@@ -28,10 +28,25 @@ bool is_gfx950(int dev);
             return ::kgx::fail(KGX_EDEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-/* grow-only device buffer */
+/* grow-only device buffer, freed with its owner */
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), cap(o.cap)
+    {
+        o.p = nullptr;
+        o.cap = 0;
+    }
+    DevBuf &operator=(DevBuf &&o) noexcept
+    {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+        return *this;
+    }
+    ~DevBuf() { release(); }
     hipError_t reserve(size_t bytes)
     {
         if (bytes <= cap)
@@ -57,6 +72,9 @@ struct DevBuf {
 };
 
 inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
+
+int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
+                 kgx_fragments *out);
 
 }  // namespace kgx
 
@@ -90,6 +108,9 @@ struct kgx_ctx {
     uint32_t tile_windows = 64u * kgx::PROBE_J_DEFAULT;
     const uint64_t *d_off = nullptr;
     bool have_hits = false; /* the tiled hits of the current plan are on the device */
+    /* fq fragments (kgx_fq.hip) */
+    kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_nres, fq_fbase, fq_rbase, fq_tmp, fq_res, fq_off, fq_read,
+        fq_frame;
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;

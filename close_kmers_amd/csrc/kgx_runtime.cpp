@@ -628,12 +628,23 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
                                c->stream));
     HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), (n_seq + 1) * sizeof(uint64_t),
                            hipMemcpyHostToDevice, c->stream));
-    const uint32_t dev_want = want;
     int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq,
-                            n_res, dev_want, nullptr);
+                            n_res, want, nullptr);
     if (rc)
         return rc;
+    return kgx_device_batch_collect(c, want, out);
+}
 
+/* the current device batch's results -> host CSR (gather on the device, OTU
+ * tallies on the host) */
+int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    if (!c->have_hits)
+        return fail(KGX_EINVAL, "no device batch to collect");
+    HIP_TRY(hipSetDevice(c->img->device));
+    const uint32_t n_seq = c->n_seq;
     /* counts -> dense CSR offsets on the host, gather on the device */
     c->h_hcount.resize(n_seq + 1);
     c->h_ccount.resize(n_seq + 1);
@@ -702,8 +713,9 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
         }
     }
     uint64_t nwin = 0;
-    for (uint32_t s = 0; s < n_seq; s++)
-        nwin += windows_of(off[s + 1] - off[s]);
+    HIP_TRY(hipMemcpyAsync(&nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
 
     out->n_seq = n_seq;
     out->hit_offsets = c->h_hoff.data();

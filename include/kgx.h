@@ -252,6 +252,51 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
 int kgx_microbench_random_read(kgx_ctx *ctx, uint64_t n_reads, int mode, float *ms,
                                uint64_t *reads);
 
+/* The current device batch's results (after kgx_run_device or the three
+ * stages) as the host CSR kgx_process_batch returns; buffers as there. */
+int kgx_device_batch_collect(kgx_ctx *ctx, uint32_t want, kgx_result *out);
+
+/* ---- fq reads -> protein fragments (the fq handler's input side) --------
+ * For every read and frame 1, 2, 3, -1, -2, -3 (DNASequence::
+ * get_possible_proteins, dna_seq.cc:9-47): genetic code 11 translation
+ * (trans_table.cc:36-84; codons with a base outside ACGTU/acgtu give 'X'),
+ * split at '*', fragments longer than 10 residues kept
+ * (fq_process_request.cc:329-343).  The fragments form a protein batch in
+ * (read, frame, position) order, on the device, owned by ctx and valid until
+ * the next fq call: feed it to kgx_run_device. */
+typedef struct kgx_fragments {
+    uint32_t n_reads;
+    uint32_t n_fragments;
+    uint64_t n_residues;
+    const uint8_t *residues;  /* device: fragment residues, concatenated */
+    const uint64_t *offsets;  /* device: [n_fragments + 1] */
+    const uint32_t *read;     /* device: read index of each fragment */
+    const int8_t *frame;      /* device: frame of each fragment */
+} kgx_fragments;
+/* reads from host memory (bases concatenated, read_offsets[n_reads + 1]) */
+int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
+                     kgx_fragments *out);
+/* reads already in device memory */
+int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
+                            uint32_t n_reads, kgx_fragments *out);
+
+/* ---- the fq request handler (FqProcessRequest, fq_process_request.cc) ---
+ * FASTQ text in, the handler's output lines out (per read: best frame,
+ * score and the frame's family matches, fq_process_request.cc:298-365, over
+ * FamilyMapper family_mapper.cc:46-205).  data_dir holds function.index and
+ * otu.index; genus_file / families_file / nr_fasta (NULL or "" to skip) load
+ * the family DB (KmerPegMapping::load_genus_map / load_families kmer.cc:
+ * 341-493; NRLoader family mode nr_loader.cc:130-176, proteins in file
+ * order).  Blocks are processed as the reference processes request blocks
+ * (one FamilyMapper per block); `finished` marks the last block. */
+typedef struct kgx_fq kgx_fq;
+int kgx_fq_create(kgx_image *img, const char *data_dir, const char *genus_file, const char *families_file,
+                  const char *nr_fasta, kgx_fq **out);
+int kgx_fq_destroy(kgx_fq *fq);
+/* *text: output lines of the block, owned by fq, valid until the next call */
+int kgx_fq_process(kgx_fq *fq, const char *fastq, uint64_t n, int finished, const char **text,
+                   uint64_t *text_len);
+
 /* ---- k-mer -> id tables in HBM ------------------------------------------
  * KmerPegMapping's kmer_to_id_ (kmer.h:84-127, filled by /add through
  * add_mapping, kmer.cc:173-210: every (k-mer, id) appended, duplicates kept)

@@ -127,6 +127,14 @@ def lib():
         L.oracle_matrix_add.argtypes = [vp, vp, vp, vp, u64, vp, vp]
         L.oracle_matrix_pairs.argtypes = [vp, vp, vp, vp, vp]
         L.oracle_matrix_pairs.restype = u64
+        L.oracle_fq_new.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_char_p), u64, ctypes.c_char_p,
+                                    ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_fq_new.restype = vp
+        L.oracle_fq_free.argtypes = [vp]
+        L.oracle_fq_process.argtypes = [vp, ctypes.c_char_p, u64]
+        L.oracle_fq_process.restype = vp
+        L.oracle_fq_fragments.argtypes = [ctypes.c_char_p, u64]
+        L.oracle_fq_fragments.restype = vp
         _lib = L
     return _lib
 
@@ -321,4 +329,37 @@ class Matrix:
     def __del__(self):
         if getattr(self, "h", None):
             lib().oracle_matrix_free(self.h)
+            self.h = None
+
+
+def fq_fragments(dna: bytes) -> list[tuple[int, str]]:
+    """(frame, fragment) of the >10-aa fragments of a read, in the order the
+    fq handler visits them (get_possible_proteins, dna_seq.cc:9-47)."""
+    p = lib().oracle_fq_fragments(dna, len(dna))
+    text = _take_string(p).decode()
+    out = []
+    for line in text.splitlines():
+        f, s = line.split(":", 1)
+        out.append((int(f), s))
+    return out
+
+
+class FqSession:
+    """The fq handler restated (oracle/handlers_oracle.cpp) over a host table."""
+
+    def __init__(self, table: np.ndarray, functions: list[str], genus: str = "", families: str = "",
+                 nr: str = ""):
+        self.table = np.ascontiguousarray(table)  # referenced, not copied, by the session
+        names = (ctypes.c_char_p * max(1, len(functions)))(*[f.encode() for f in functions])
+        self.h = lib().oracle_fq_new(self.table.ctypes.data, len(self.table), names, len(functions),
+                                     genus.encode(), families.encode(), nr.encode())
+        if not self.h:
+            raise RuntimeError("oracle_fq_new failed")
+
+    def process(self, fastq: bytes) -> bytes:
+        return _take_string(lib().oracle_fq_process(self.h, fastq, len(fastq)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_fq_free(self.h)
             self.h = None

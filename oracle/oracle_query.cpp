@@ -9,6 +9,9 @@
  *   mode=query_details  query_request.cc:103-151 with details=1 (HIT lines)
  *   mode=query_best     query_request.cc:124-135 (find_best_call=1)
  *   mode=add            add_request.cc:305-353 (silent=0)
+ *   mode=fq             the input is FASTQ: fq_process_request.cc:298-365 over
+ *                       FamilyMapper; optional genus=, families=, nr= files
+ *                       load the family DB (kmer.cc:341-493, nr_loader.cc)
  *   mode=matrix         /add of the FASTA into an empty mapping (add_request.cc:
  *                       164-170), then one /matrix request over the same FASTA
  *                       (matrix_request.cc:83-190): process_results' body
@@ -41,6 +44,11 @@ void oracle_matrix_free(void *p);
 void oracle_matrix_add(void *px, void *pk, const uint32_t *seq_ids, const uint64_t *seq_lens,
                        uint64_t n_seq, const uint64_t *hit_off, const uint64_t *hit_kmers);
 uint64_t oracle_matrix_pairs(void *px, uint32_t *id1, uint32_t *id2, uint64_t *count, float *score);
+void *oracle_fq_new(const void *table, uint64_t num_sigs, const char *const *functions, uint64_t n_functions,
+                    const char *genus_file, const char *families_file, const char *nr_fasta);
+void oracle_fq_free(void *p);
+char *oracle_fq_process(void *p, const char *fastq, uint64_t n);
+void oracle_free(void *p);
 }
 
 /* KmerImage::map_image_file validation, kmer_image.cc:83-150 */
@@ -99,6 +107,23 @@ int main(int argc, char **argv)
     std::ifstream in(fasta, std::ios::binary);
     std::stringstream ss;
     ss << in.rdbuf();
+    if (mode == "fq") {
+        std::vector<const char *> fn;
+        for (auto &f : functions)
+            fn.push_back(f.c_str());
+        void *q = oracle_fq_new(table.data(), num_sigs, fn.data(), fn.size(), qp["genus"].c_str(),
+                                qp["families"].c_str(), qp["nr"].c_str());
+        if (!q) {
+            std::fprintf(stderr, "cannot load the family files\n");
+            return 1;
+        }
+        const std::string text = ss.str();
+        char *out = oracle_fq_process(q, text.data(), text.size());
+        std::fwrite(out, 1, std::strlen(out), stdout);
+        oracle_free(out);
+        oracle_fq_free(q);
+        return 0;
+    }
     auto records = parse_fasta(ss.str());
 
     Scorer scorer(table.data(), num_sigs);

@@ -17,6 +17,11 @@ Outputs (all small):
              parameter set.
   cap/       one 40,100-residue sequence whose single run overflows the
              40,000-entry hit buffer (kguts.cc:850-851), plus expected text.
+  fq/        FASTQ reads back-translated (code 11, both strands, stops, N,
+             lower case) from members of protein families, with a families
+             file, a genus map and the NR proteins that fill
+             kmer_to_family_id_: the fq request body (fq_process_request.cc:
+             298-365) from the oracle.
   matrix/    protein families sharing signature k-mers (plus cross-family
              k-mers, repeated ids and unrelated proteins): the /add-then-
              /matrix body (matrix_request.cc:165-190) from the oracle.
@@ -273,12 +278,93 @@ def make_matrix(rng) -> None:
     open(os.path.join(out, "expected_matrix_default.txt"), "wb").write(txt)
 
 
+CODE11 = ("FFLLSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG",
+          "TTTTTTTTTTTTTTTTCCCCCCCCCCCCCCCCAAAAAAAAAAAAAAAAGGGGGGGGGGGGGGGG",
+          "TTTTCCCCAAAAGGGGTTTTCCCCAAAAGGGGTTTTCCCCAAAAGGGGTTTTCCCCAAAAGGGG",
+          "TCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAGTCAG")
+
+
+def back_translate(prot: str, rng) -> str:
+    codons = {}
+    for i, aa in enumerate(CODE11[0]):
+        codons.setdefault(aa, []).append(CODE11[1][i] + CODE11[2][i] + CODE11[3][i])
+    return "".join(codons[a][int(rng.integers(0, len(codons[a])))] for a in prot)
+
+
+def revcomp(dna: str) -> str:
+    return dna[::-1].translate(str.maketrans("ACGTacgt", "TGCAtgca"))
+
+
+FQ_FILES = {"genus": "genus.map", "families": "families.tsv", "nr": "nr.fasta"}
+
+
+def make_fq(rng) -> None:
+    out = os.path.join(HERE, "fq")
+    data = os.path.join(out, "data")
+    img = DesignedImage()
+    n_fam = 8
+    bases = [random_protein(rng, 160) for _ in range(n_fam)]
+    fam_fn = [0, 1, 2, 2, 3, 3, 3, 4]  # families sharing a function share pgf rollups
+    for f, b in enumerate(bases):
+        img.add_windows(b, range(0, len(b) - 8), fam_fn[f], rng=rng)
+    members = []
+    for f, b in enumerate(bases):
+        for m in range(4):
+            s = list(b)
+            for p in rng.integers(0, len(s), 6):
+                s[p] = "ACDEFGHIKLMNPQRSTVWY"[int(rng.integers(0, 20))]
+            members.append((f, m, "".join(s)))
+    functions = [f"function {i}" for i in range(6)]
+    image_files.write_data_dir(data, img.table(), functions, ["o"])
+    genera = ["Escherichia", "Bacillus", "Mycoplasma"]
+    with open(os.path.join(out, "genus.map"), "w") as g:
+        g.write("Escherichia\t561\nBacillus\t1386\n")  # Mycoplasma left unmapped
+    with open(os.path.join(out, "families.tsv"), "w") as fam:
+        for f, m, s in members:
+            gf = f"GF{f // 2:08d}"              # two local families per global family
+            genus = genera[(f + m) % 3]
+            local = str(100 + f)
+            fam.write(f"{gf}\t2\t2\tfig|{1000 + f}.{m}.peg.{m}\t{len(s)}\t{functions[fam_fn[f]]}\t"
+                      f"{local}\t{genus}\t{local}\n")
+    write_fasta(os.path.join(out, "nr.fasta"),
+                [(f"fig|{1000 + f}.{m}.peg.{m}", s) for f, m, s in members] +
+                [("fig|9999.1.peg.1", bases[0])])  # no family: skipped
+    recs = []
+    for i in range(60):
+        f, m, s = members[int(rng.integers(0, len(members)))]
+        at = int(rng.integers(0, len(s) - 50))
+        prot = s[at:at + 50]
+        kind = i % 6
+        if kind == 1:  # a stop codon splits the protein
+            prot = prot[:20] + "*" + prot[21:]
+        dna = back_translate(prot, rng)
+        if kind == 2:
+            dna = revcomp(dna)
+        if kind == 3:
+            dna = "AC" + dna[:-2]  # frame 3
+        if kind == 4:
+            dna = dna.lower()
+            dna = dna[:30] + "N" + dna[31:]
+        if kind == 5:
+            dna = "".join("ACGT"[int(x)] for x in rng.integers(0, 4, 150))  # random read
+        recs.append((f"read{i}", dna))
+    recs.append(("", "ACGT" * 30))  # an empty id is skipped
+    with open(os.path.join(out, "input.fasta"), "w") as fq:  # FASTQ despite the name
+        for rid, dna in recs:
+            fq.write(f"@{rid} desc\n{dna}\n+\n{'I' * len(dna)}\n")
+    args = {k: os.path.join(out, v) for k, v in FQ_FILES.items()}
+    txt = oracle.query_text(data, os.path.join(out, "input.fasta"), "fq", args)
+    assert txt.count(b"\n") > 20
+    open(os.path.join(out, "expected_fq_default.txt"), "wb").write(txt)
+
+
 def main() -> None:
     oracle.build(ref=False)
     make_scoring(np.random.default_rng(2024_08_07))
     make_edge(np.random.default_rng(12345))
     make_cap(np.random.default_rng(777))
     make_matrix(np.random.default_rng(4242))
+    make_fq(np.random.default_rng(31337))
     print("golden fixtures written under", HERE)
 
 

@@ -1,0 +1,104 @@
+"""fq path on the GPU: 6-frame code-11 fragments vs the oracle's
+get_possible_proteins + split (dna_seq.cc:9-47), and their lookup."""
+import numpy as np
+import pytest
+
+from helpers import pack, synthetic_table
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_reads(rng, n):
+    alphabet = np.frombuffer(b"ACGTACGTACGTacgtNnUuRYKMSWBDHVX.-", np.uint8)
+    reads = []
+    for i in range(n):
+        L = int(rng.integers(0, 320)) if i % 7 else int(rng.integers(0, 12))
+        if i % 3 == 0:
+            b = alphabet[rng.integers(0, len(alphabet), L)]
+        else:
+            b = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)]
+        reads.append(bytes(b))
+    return reads
+
+
+def test_fragments_match_oracle(gpu, oracle_lib):
+    spec, table = synthetic_table(20000)
+    rng = np.random.default_rng(3)
+    reads = _random_reads(rng, 700)
+    res, off = pack([("r", r) for r in reads])
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        f = ctx.fq_fragments(res, off)
+        h = ctx.fragments_to_host(f)
+    got = {}
+    for i in range(f.n_fragments):
+        s = bytes(h["residues"][int(h["offsets"][i]):int(h["offsets"][i + 1])]).decode()
+        got.setdefault(int(h["read"][i]), []).append((int(h["frame"][i]), s))
+    assert np.all(np.diff(h["read"].astype(np.int64)) >= 0)
+    n = 0
+    for r, dna in enumerate(reads):
+        want = oracle_lib.fq_fragments(dna)
+        assert got.get(r, []) == want, r
+        n += len(want)
+    assert n == f.n_fragments and n > 500
+
+
+def test_fragment_lookup_matches_oracle(gpu, oracle_lib):
+    """Fragments fed to the lookup give the oracle's hits and calls."""
+    from close_kmers_amd import synth
+    spec, table = synthetic_table(40000)
+    rng = np.random.default_rng(4)
+    # reads that encode planted image proteins (so fragments hit), both strands
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(30))].reshape(30, -1)
+    from tests_golden_codons import back_translate, revcomp
+    reads = []
+    for i in range(200):
+        p = bytes(src[i % 30][int(rng.integers(0, 200)):][:60]).decode()
+        d = back_translate(p, rng)
+        reads.append((d if i % 2 else revcomp(d)).encode())
+    res, off = pack([("r", r) for r in reads])
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        f = ctx.fq_fragments(res, off)
+        h = ctx.fragments_to_host(f)
+        got = ctx.run_fragments(f, gpu.Params(5, 200, 0, 0), want=3)
+    want = oracle_lib.process_batch(table, h["residues"], h["offsets"], want=3)
+    assert np.array_equal(got.hit_offsets, want.hit_offsets)
+    assert np.array_equal(got.hits["which_kmer"], want.hits["which_kmer"])
+    assert np.array_equal(got.calls["start"], want.calls["start"])
+    assert np.array_equal(got.calls["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+    assert len(want.calls) > 50
+
+
+def test_fq_handler_c_abi_matches_golden(gpu, oracle_lib):
+    """kgx_fq_* (in-process handler) on the golden fq data set, in one block
+    and in three blocks split mid-record."""
+    import os
+    from close_kmers_amd import image_files
+    from helpers import GOLDEN
+    d = os.path.join(GOLDEN, "fq")
+    files = {k: os.path.join(d, v) for k, v in
+             {"genus": "genus.map", "families": "families.tsv", "nr": "nr.fasta"}.items()}
+    want = open(os.path.join(d, "expected_fq_default.txt"), "rb").read()
+    fastq = open(os.path.join(d, "input.fasta"), "rb").read()
+    table = image_files.read_image(os.path.join(d, "data"))
+    with gpu.Image.from_table(table) as img:
+        with gpu.FqHandler(img, os.path.join(d, "data"), **files) as fq:
+            assert fq.process(fastq, True) == want
+        with gpu.FqHandler(img, os.path.join(d, "data"), **files) as fq:
+            cuts = [0, len(fastq) // 3 + 7, 2 * len(fastq) // 3 + 3, len(fastq)]
+            out = b"".join(fq.process(fastq[a:b], b == len(fastq)) for a, b in zip(cuts, cuts[1:]))
+        assert out == want
+
+
+def test_fq_handler_without_families_matches_oracle(gpu, oracle_lib):
+    """No family DB: reads without calls are skipped on the host (fast path);
+    the output must still equal the oracle's."""
+    import os
+    from close_kmers_amd import image_files
+    from helpers import GOLDEN
+    d = os.path.join(GOLDEN, "fq")
+    fastq = open(os.path.join(d, "input.fasta"), "rb").read()
+    table = image_files.read_image(os.path.join(d, "data"))
+    want = oracle_lib.query_text(os.path.join(d, "data"), os.path.join(d, "input.fasta"), "fq", {})
+    assert want.count(b"\n") > 20
+    with gpu.Image.from_table(table) as img, gpu.FqHandler(img, os.path.join(d, "data")) as fq:
+        assert fq.process(fastq, True) == want

@@ -54,7 +54,7 @@ def assert_same(got, want, n_seq):
 # golden handler text through the C++ facade (kgx_query)
 
 def _golden_cases():
-    for ds in ("scoring", "edge", "cap", "matrix"):
+    for ds in ("scoring", "edge", "cap", "matrix", "fq"):
         d = os.path.join(GOLDEN, ds)
         for f in sorted(os.listdir(d)):
             if f.startswith("expected_") and f.endswith(".txt"):
@@ -63,11 +63,11 @@ def _golden_cases():
 
 @pytest.mark.parametrize("ds,fname", list(_golden_cases()))
 def test_facade_text_matches_golden(gpu, ds, fname):
-    from test_oracle_golden import PARAMS, parse_case
+    from test_oracle_golden import case_params, parse_case
     mode, pname = parse_case(fname)
     d = os.path.join(GOLDEN, ds)
     args = [kbuild.QUERY, os.path.join(d, "data"), os.path.join(d, "input.fasta"), mode]
-    args += [f"{k}={v}" for k, v in PARAMS[pname].items()]
+    args += [f"{k}={v}" for k, v in case_params(ds, pname).items()]
     r = subprocess.run(args, capture_output=True, timeout=300)
     assert r.returncode == 0, r.stderr.decode()
     assert r.stdout == open(os.path.join(d, fname), "rb").read()

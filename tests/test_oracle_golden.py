@@ -8,7 +8,7 @@ from helpers import GOLDEN
 
 
 def _cases():
-    for ds in ("scoring", "edge", "cap", "matrix"):
+    for ds in ("scoring", "edge", "cap", "matrix", "fq"):
         d = os.path.join(GOLDEN, ds)
         for f in sorted(os.listdir(d)):
             if f.startswith("expected_") and f.endswith(".txt"):
@@ -23,9 +23,20 @@ PARAMS = {
 }
 
 
+# the fq data set's family DB files (tests/golden/make_golden.py FQ_FILES)
+FQ_FILES = {"genus": "genus.map", "families": "families.tsv", "nr": "nr.fasta"}
+
+
+def case_params(ds, pname):
+    p = dict(PARAMS[pname])
+    if ds == "fq":
+        p.update({k: os.path.join(GOLDEN, ds, v) for k, v in FQ_FILES.items()})
+    return p
+
+
 def parse_case(fname):
     stem = fname[len("expected_"):-len(".txt")]
-    for mode in ("query_details", "query_best", "query", "add", "matrix"):
+    for mode in ("query_details", "query_best", "query", "add", "matrix", "fq"):
         if stem.startswith(mode + "_"):
             return mode, stem[len(mode) + 1:]
     raise ValueError(fname)
@@ -36,5 +47,5 @@ def test_oracle_matches_golden(oracle_lib, ds, fname):
     mode, pname = parse_case(fname)
     d = os.path.join(GOLDEN, ds)
     got = oracle_lib.query_text(os.path.join(d, "data"), os.path.join(d, "input.fasta"), mode,
-                                PARAMS[pname])
+                                case_params(ds, pname))
     assert got == open(os.path.join(d, fname), "rb").read()

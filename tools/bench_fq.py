@@ -1,0 +1,153 @@
+"""C4 benchmark: the fq path over 10M x 150 bp reads (BASELINE.json configs[3]).
+
+    python tools/bench_fq.py [--n-reads 10000000] [--chunk 1000000] [--n-keys 1e9]
+
+Reads: uniform ACGT, 150 bp (seed 0x5EED0004), resident in
+HBM.  Device rate (`value`): per chunk of reads, the 6-frame code-11
+translation + '*' split + >10-aa fragment extraction (kgx_fq_fragments_device)
+and the lookup + run scoring of every fragment (kgx_run_device, hits +
+calls) against the synthetic 1B-entry image -- the fq handler's GPU work.
+Handler rate (`handler`): FASTQ text of one chunk through the in-process fq
+handler (kgx_fq_process: H2D, the same GPU work, D2H, FamilyMapper and frame
+choice on the host, output text), with no family DB loaded.  CPU baseline:
+the oracle restatement of the same handler (oracle.FqSession) on a sample of
+the reads, one host thread.  Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def fastq_text(bases: np.ndarray, length: int, first: int, n: int) -> bytes:
+    lines = []
+    q = b"I" * length
+    for i in range(n):
+        r = bases[(first + i) * length:(first + i + 1) * length].tobytes()
+        lines.append(b"@r%d\n%s\n+\n%s\n" % (first + i, r, q))
+    return b"".join(lines)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-reads", type=int, default=10_000_000)
+    ap.add_argument("--length", type=int, default=150)
+    ap.add_argument("--chunk", type=int, default=1_000_000)
+    ap.add_argument("--n-keys", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--handler-reads", type=int, default=200_000)
+    ap.add_argument("--cpu-reads", type=int, default=20_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from close_kmers_amd import abi, image_files, synth
+    L = abi.lib()
+    spec = synth.ImageSpec(int(args.n_keys))
+    t0 = time.time()
+    img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs)
+    ctx = abi.Context(img)
+    n, Lr = args.n_reads, args.length
+    rng = np.random.default_rng(0x5EED0004)
+    bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
+    d_bases, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+    abi.check(L.kgx_device_alloc(0, bases.nbytes, ctypes.byref(d_bases)), "alloc")
+    abi.check(L.kgx_memcpy_h2d(d_bases, bases.ctypes.data, bases.nbytes), "h2d")
+    chunk = min(args.chunk, n)
+    off = np.arange(0, chunk * Lr + 1, Lr, dtype=np.uint64)  # the same offsets serve every chunk
+    abi.check(L.kgx_device_alloc(0, off.nbytes, ctypes.byref(d_off)), "alloc")
+    abi.check(L.kgx_memcpy_h2d(d_off, off.ctypes.data, off.nbytes), "h2d")
+    print(f"[bench_fq] image + {n} reads ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    params = abi.default_params()
+    stats = {"fragments": 0, "residues": 0, "hits": 0, "calls": 0}
+
+    def device_pass(collect_stats=False):
+        for c0 in range(0, n, chunk):
+            m = min(chunk, n - c0)
+            f = abi.Fragments()
+            abi.check(L.kgx_fq_fragments_device(ctx.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
+                      "fq_fragments")
+            dr = abi.DeviceResult()
+            abi.check(L.kgx_run_device(ctx.handle, ctypes.byref(params), f.residues, f.offsets, f.n_fragments,
+                                       f.n_residues, abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
+            if collect_stats:
+                hc = np.zeros(f.n_fragments, np.uint32)
+                cc = np.zeros(f.n_fragments, np.uint32)
+                ctx.synchronize()
+                abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, dr.hit_count, hc.nbytes), "d2h")
+                abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, dr.call_count, cc.nbytes), "d2h")
+                stats["fragments"] += f.n_fragments
+                stats["residues"] += f.n_residues
+                stats["hits"] += int(hc.sum())
+                stats["calls"] += int(cc.sum())
+        ctx.synchronize()
+
+    device_pass(collect_stats=True)
+    times = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        device_pass()
+        times.append(time.perf_counter() - t0)
+    t_dev = float(np.median(times))
+
+    # the handler end to end on FASTQ text (no family DB)
+    hn = min(args.handler_reads, n)
+    text = fastq_text(bases, Lr, 0, hn)
+    with tempfile.TemporaryDirectory() as td:
+        image_files.write_index(os.path.join(td, "function.index"), [f"function {i}" for i in range(100000)])
+        image_files.write_index(os.path.join(td, "otu.index"), ["o"])
+        with abi.FqHandler(img, td) as fq:
+            fq.process(text[:100000], True)  # warm
+            t0 = time.perf_counter()
+            out = fq.process(text, True)
+            t_h = time.perf_counter() - t0
+    line = {
+        "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
+        "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "n_keys": spec.n_keys,
+                   "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
+        "per_pass": stats,
+        "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),
+                    "note": "FASTQ text -> output text through kgx_fq_process, one block"},
+    }
+    if not args.no_cpu_baseline:
+        import oracle
+        oracle.build(ref=False)
+        table = img.download()
+        cn = min(args.cpu_reads, n)
+        sess = oracle.FqSession(table, [f"function {i}" for i in range(100000)])
+        t0 = time.perf_counter()
+        cpu_out = sess.process(fastq_text(bases, Lr, 0, cn))
+        t_cpu = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": cn / t_cpu, "unit": "reads/s", "cores": 1, "kind": "port",
+                                "sample": f"the fq handler (oracle restatement) on the first {cn} reads"}
+        line["parity_first_reads"] = bool(out.split(b"\n")[:0] == [] and
+                                          cpu_out == fastq_handler_prefix(out, cn))
+        del sess, table
+    print(json.dumps(line), flush=True)
+    L.kgx_device_free(d_bases)
+    L.kgx_device_free(d_off)
+    ctx.close()
+    img.close()
+
+
+def fastq_handler_prefix(out: bytes, n_reads: int) -> bytes:
+    """The handler's output lines for reads r0 .. r{n_reads-1}."""
+    keep = []
+    for ln in out.split(b"\n"):
+        if ln and int(ln.split(b"\t", 1)[0][1:]) < n_reads:
+            keep.append(ln + b"\n")
+    return b"".join(keep)
+
+
+if __name__ == "__main__":
+    main()
