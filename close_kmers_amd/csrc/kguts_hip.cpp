@@ -737,6 +737,198 @@ std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m)
     return os;
 }
 
+/* ---- LookupRequest ------------------------------------------------------- */
+
+static bool stoi_param(const std::map<std::string, std::string> &p, const char *k, int &out)
+{
+    /* std::stoi with only std::invalid_argument caught (lookup_request.cc:47-58) */
+    auto it = p.find(k);
+    if (it == p.end())
+        return false;
+    try {
+        out = std::stoi(it->second);
+        return true;
+    } catch (const std::invalid_argument &) {
+        return false;
+    }
+}
+
+LookupRequest::LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
+                             const std::map<std::string, std::string> &params)
+    : mapping_(mapping), family_mode_(family_mode)
+{
+    int v;
+    if (stoi_param(params, "kmer_hit_threhsold", v))
+        kmer_hit_threshold_ = (unsigned int)v;
+    if (stoi_param(params, "find_best_match", v))
+        find_best_match_ = v != 0;
+    if (stoi_param(params, "find_reps", v))
+        find_reps_ = v != 0;
+    if (stoi_param(params, "allow_ambiguous_functions", v))
+        allow_ambiguous_functions_ = v != 0;
+    auto tg_it = params.find("target_genus");
+    const std::string tg = mapping_->genus_map_[tg_it == params.end() ? std::string() : tg_it->second];
+    try {
+        if (!tg.empty())
+            target_genus_id_ = std::stoul(tg);
+    } catch (const std::invalid_argument &) {
+    }
+}
+
+void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
+                                 std::ostream &os)
+{
+    const uint32_t n = (uint32_t)work.size();
+    if (n == 0)
+        return;
+    std::string buf;
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        buf += work[i].second;
+        off[i + 1] = buf.size();
+    }
+    const bool want_calls = find_best_match_ && family_mode_;
+    kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
+    kgx_result r;
+    int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n,
+                               KGX_WANT_HITS | (want_calls ? KGX_WANT_CALLS : 0), &r);
+    if (rc)
+        throw_last(rc, "kgx_process_batch");
+    /* the on_hit lists of every hit: kmer_to_family_id_ or kmer_to_id_ */
+    kgx_kmap *map = family_mode_ ? mapping_->kmer_to_family_id() : mapping_->kmer_to_id();
+    const uint64_t nh = r.hit_offsets[n];
+    std::vector<uint64_t> loff(nh + 1, 0);
+    std::vector<uint32_t> lids;
+    if (nh && kgx_kmap_num_kmers(map)) {
+        std::vector<uint64_t> kmers(nh);
+        for (uint64_t h = 0; h < nh; h++)
+            kmers[h] = r.hits[h].which_kmer;
+        rc = kgx_kmap_lookup(map, kmers.data(), nh, loff.data(), nullptr, 0);
+        if (!rc) {
+            lids.resize(loff[nh]);
+            rc = kgx_kmap_lookup(map, kmers.data(), nh, loff.data(), lids.data(), lids.size());
+        }
+        if (rc)
+            throw_last(rc, "kgx_kmap_lookup");
+    }
+    typedef FamilyMapper::sequence_accumulated_score_t acc_t;
+    for (uint32_t s = 0; s < n; s++) {
+        const std::string &id = work[s].first;
+        seq_score_.clear();
+        for (uint64_t h = r.hit_offsets[s]; h < r.hit_offsets[s + 1]; h++) {
+            const uint64_t a = loff[h], b = loff[h + 1];
+            if (a == b)
+                continue;
+            if (family_mode_) {
+                const float weight = 1.0f / (float)(b - a);
+                for (uint64_t j = a; j < b; j++) {
+                    acc_t &e = seq_score_[lids[j]];
+                    e.hit_count++;
+                    e.hit_total++;
+                    e.weighted_total += weight;
+                }
+            } else {
+                for (uint64_t j = a; j < b; j++)
+                    seq_score_[lids[j]].hit_count++;
+            }
+        }
+        if (want_calls) {
+            std::vector<KmerCall> calls;
+            for (uint64_t c = r.call_offsets[s]; c < r.call_offsets[s + 1]; c++)
+                calls.emplace_back(r.calls[c].start, r.calls[c].end, r.calls[c].count, r.calls[c].function_index,
+                                   r.calls[c].weighted_hits);
+            int fi;
+            std::string fn, ambig;
+            float score, wscore, offs = 0.0f;
+            kg.find_best_call(calls, fi, fn, score, wscore, offs);
+            bool do_ambig = false;
+            if (fn.empty()) {
+                fn = "hypothetical protein";
+            } else {
+                const size_t where = fn.find(" ?? ");
+                if (where != std::string::npos) {
+                    if (allow_ambiguous_functions_) {
+                        ambig = fn.substr(where + 4);
+                        fn = fn.substr(0, where);
+                        do_ambig = true;
+                    } else {
+                        fn = "hypothetical protein";
+                    }
+                }
+            }
+            float lf_score = 0.0f, gf_score = 0.0f;
+            std::string lf_fam, lf_fn, gf_fam;
+            std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
+            for (auto hit_ent : seq_score_) {
+                const acc_t &se = hit_ent.second;
+                if (se.hit_total < kmer_hit_threshold_)
+                    continue;
+                auto fent = mapping_->family_data_.find(hit_ent.first);
+                if (fent == mapping_->family_data_.end())
+                    continue;
+                const KmerPegMapping::family_data_t &fd = fent->second;
+                if (do_ambig) {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else if (fd.function == ambig)
+                        pgf_rollup_ambig[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                } else {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                }
+                if (se.weighted_total > lf_score && fd.genus_id == target_genus_id_) {
+                    lf_score = se.weighted_total;
+                    lf_fam = fd.plf;
+                    lf_fn = fd.function;
+                }
+            }
+            auto *rollup = (do_ambig && lf_fn == ambig) ? &pgf_rollup_ambig : &pgf_rollup;
+            for (auto pgf_ent : *rollup)
+                if (pgf_ent.second > gf_score) {
+                    gf_score = pgf_ent.second;
+                    gf_fam = pgf_ent.first;
+                }
+            os << id << "\t" << gf_fam << "\t" << gf_score << "\t" << lf_fam << "\t" << lf_score << "\t"
+               << (do_ambig ? lf_fn : fn) << "\t" << score << "\t" << wscore << "\n";
+        } else {
+            typedef std::pair<KmerPegMapping::encoded_id_t, acc_t> data_t;
+            std::vector<data_t> vec(seq_score_.begin(), seq_score_.end());
+            std::sort(vec.begin(), vec.end(), [](const data_t &l, const data_t &rr) {
+                return l.second.weighted_total > rr.second.weighted_total;
+            });
+            os << id << "\n";
+            for (auto &it : vec) {
+                const acc_t &se = it.second;
+                if (se.hit_total < kmer_hit_threshold_)
+                    break;
+                if (family_mode_) {
+                    const KmerPegMapping::family_data_t fd = mapping_->family_data_[it.first];
+                    const float scaled = (float)se.hit_count / (float)fd.total_size;
+                    os << se.hit_count << "\t" << se.hit_total << "\t" << se.weighted_total << "\t" << fd.pgf << "\t"
+                       << fd.plf << "\t" << fd.total_size << "\t" << fd.count << "\t" << scaled << "\t"
+                       << fd.function << "\n";
+                    if (find_reps_)
+                        os << "///\n"; /* no family reps DB loaded */
+                } else {
+                    os << mapping_->decode_id(it.first) << "\t" << se.hit_count;
+                    auto fh = mapping_->peg_to_family_.find(it.first);
+                    if (fh != mapping_->peg_to_family_.end()) {
+                        const KmerPegMapping::family_data_t fd = mapping_->family_data_[fh->second];
+                        os << "\t" << fd.pgf << "\t" << fd.plf << "\t" << fd.function << "\n";
+                    } else {
+                        os << "\n";
+                    }
+                }
+            }
+            os << "//\n";
+        }
+    }
+}
+
 FqRequest::FqRequest(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping) : kg_(kg), mapping_(mapping) {}
 
 void FqRequest::process(const std::string &block, bool finished, std::ostream &os)

@@ -301,6 +301,34 @@ private:
 std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m);
 
 /*
+ * LookupRequest (lookup_request.cc): one /lookup request.  The request's
+ * query-string parameters are read as in lookup_request.cc:33-79
+ * (kmer_hit_threhsold -- sic --, find_best_match, find_reps,
+ * allow_ambiguous_functions, target_genus).  process_work() is the worker
+ * loop over a chunk (lookup_request.cc:153-400): the chunk's lookups run as
+ * one GPU batch, the per-sequence rollups (on_hit 446-482) and output run
+ * on the host in order with one seq_score_ map for the request.  No family
+ * reps DB is loaded, so find_reps prints only the "///" separators.
+ */
+class LookupRequest {
+public:
+    LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
+                  const std::map<std::string, std::string> &params);
+    void process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
+                      std::ostream &os);
+
+private:
+    std::shared_ptr<KmerPegMapping> mapping_;
+    bool family_mode_;
+    unsigned int kmer_hit_threshold_ = 3;
+    bool find_best_match_ = false;
+    bool allow_ambiguous_functions_ = false;
+    bool find_reps_ = false;
+    unsigned long target_genus_id_ = 0;
+    std::unordered_map<KmerPegMapping::encoded_id_t, FamilyMapper::sequence_accumulated_score_t> seq_score_;
+};
+
+/*
  * FqProcessRequest (fq_process_request.cc:230-365): FASTQ in, per read the
  * best frame's family matches out.  process() runs a block: the reads'
  * 6-frame fragments, their lookup and scoring on the GPU in one batch, then

@@ -11,6 +11,9 @@
  *   add            add_request.cc:305-353 (silent=0)
  *   fq             the input is FASTQ: fq_process_request.cc:230-365 over
  *                  FamilyMapper; genus=, families=, nr= load the family DB
+ *   lookup         /lookup (lookup_request.cc:153-400): family_mode=1 loads
+ *                  the family DB (genus=, families=, nr=); otherwise the FASTA
+ *                  is first /add-ed into kmer_to_id_
  *   matrix         /add of the FASTA into an empty mapping, then one /matrix
  *                  request over the same FASTA (matrix_request.cc:83-190)
  *
@@ -37,7 +40,7 @@ int main(int argc, char **argv)
     }
     const std::string dir = argv[1], fasta = argv[2], mode = argv[3];
     if (mode != "query" && mode != "query_details" && mode != "query_best" && mode != "add" &&
-        mode != "matrix" && mode != "fq") {
+        mode != "matrix" && mode != "fq" && mode != "lookup") {
         std::fprintf(stderr, "unknown mode %s\n", mode.c_str());
         return 2;
     }
@@ -95,6 +98,35 @@ int main(int argc, char **argv)
             parser.parse_char(ch);
         parser.parse_complete();
 
+        if (mode == "lookup") {
+            auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
+            if (!qp["genus"].empty())
+                mapping->load_genus_map(qp["genus"]);
+            if (!qp["families"].empty())
+                mapping->load_families(qp["families"]);
+            const bool family_mode = qp["family_mode"] == "1";
+            if (family_mode && !qp["nr"].empty())
+                mapping->load_nr_families(kguts, qp["nr"]);
+            std::vector<std::pair<std::string, std::string>> work;
+            std::vector<std::string> seqs;
+            for (auto &j : jobs) {
+                work.emplace_back(j.id, j.seq);
+                seqs.push_back(j.seq);
+            }
+            if (!family_mode) { /* /add first, ids encoded in order after the chunk */
+                run_batch_on_device(kguts, seqs);
+                std::vector<KmerPegMapping::encoded_id_t> ids;
+                for (auto &j : jobs)
+                    ids.push_back(mapping->encode_id(j.id));
+                mapping->add_batch_mappings(kguts, ids);
+            }
+            LookupRequest req(mapping, family_mode, qp);
+            std::ostringstream os;
+            req.process_work(kguts, work, os);
+            const std::string s = os.str();
+            std::fwrite(s.data(), 1, s.size(), stdout);
+            return 0;
+        }
         if (mode == "matrix") {
             auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
             std::vector<std::string> seqs;

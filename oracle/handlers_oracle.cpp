@@ -10,6 +10,8 @@
  *   oracle_matrix_* MatrixRequest (matrix_request.cc:83-95 per-sequence loop,
  *                   on_hit 130-163, process_results 165-190; state
  *                   matrix_request.h:25-26)
+ *   oracle_lookup_* LookupRequest (lookup_request.cc:33-79 parameters, 153-400
+ *                   per-sequence loop and output, on_hit 446-482)
  *   oracle_fq_*     the fq path: FastqParser (fastq_parser.h:40-150,
  *                   fastq_parser.cc), DNASequence::get_possible_proteins
  *                   (dna_seq.cc:9-47, complement dna_seq.h:28-111),
@@ -418,6 +420,185 @@ static void parse_fastq(const std::string &text,
     cb(id, seq); /* parse_complete, fastq_parser.cc:29-35 */
 }
 
+/* std::stoi on a query-string value with only invalid_argument caught
+ * (lookup_request.cc:47-58): absent or non-numeric values keep the default */
+static bool stoi_param(const std::map<std::string, std::string> &p, const std::string &k, int &out)
+{
+    auto it = p.find(k);
+    if (it == p.end())
+        return false;
+    try {
+        out = std::stoi(it->second);
+        return true;
+    } catch (const std::invalid_argument &) {
+        return false;
+    }
+}
+
+struct LookupSession {
+    FamilyDb db;
+    Kmap kmer_to_id; /* mode 0 */
+    const oracle::SigKmer *table = nullptr;
+    std::vector<std::string> functions;
+    oracle::Scorer *scorer = nullptr;
+    ~LookupSession() { delete scorer; }
+};
+
+/* one /lookup request over FASTA records (lookup_request.cc) */
+static std::string lookup_request(LookupSession &q, bool family_mode,
+                                  const std::map<std::string, std::string> &params,
+                                  const std::vector<std::pair<std::string, std::string>> &records)
+{
+    unsigned int kmer_hit_threshold = 3;
+    int v;
+    if (stoi_param(params, "kmer_hit_threhsold", v))
+        kmer_hit_threshold = (unsigned int)v;
+    bool find_best_match = false, find_reps = false, allow_ambiguous = false;
+    if (stoi_param(params, "find_best_match", v))
+        find_best_match = v != 0;
+    if (stoi_param(params, "find_reps", v))
+        find_reps = v != 0;
+    if (stoi_param(params, "allow_ambiguous_functions", v))
+        allow_ambiguous = v != 0;
+    unsigned long target_genus_id = 0;
+    {
+        auto tg_it = params.find("target_genus");
+        std::string tg = q.db.genus_map[tg_it == params.end() ? std::string() : tg_it->second];
+        try {
+            if (!tg.empty())
+                target_genus_id = std::stoul(tg);
+        } catch (const std::invalid_argument &) {
+        }
+    }
+    std::unordered_map<uint32_t, AccScore> seq_score; /* lookup_request.h:43, one per request */
+    std::ostringstream os;
+    for (auto &rec : records) {
+        const std::string &id = rec.first, &seq = rec.second;
+        seq_score.clear();
+        std::vector<oracle::Call> calls;
+        std::vector<oracle::SeqHit> hits;
+        const bool want_calls = find_best_match && family_mode;
+        q.scorer->process(seq.c_str(), seq.size(), want_calls ? &calls : nullptr, &hits, nullptr, true);
+        for (auto &h : hits) { /* on_hit, lookup_request.cc:446-482 */
+            if (family_mode) {
+                auto ki = q.db.kmer_to_family.m.find(h.hit.which_kmer);
+                if (ki == q.db.kmer_to_family.m.end())
+                    continue;
+                const float weight = 1.0f / (float)ki->second.size();
+                for (uint32_t ent : ki->second) {
+                    AccScore &s = seq_score[ent];
+                    s.hit_count++;
+                    s.hit_total++;
+                    s.weighted_total += weight;
+                }
+            } else {
+                auto ki = q.kmer_to_id.m.find(h.hit.which_kmer);
+                if (ki == q.kmer_to_id.m.end())
+                    continue;
+                for (uint32_t eid : ki->second)
+                    seq_score[eid].hit_count++;
+            }
+        }
+        if (find_best_match && family_mode) {
+            int fi;
+            std::string fn;
+            float score, wscore, off;
+            oracle::find_best_call(calls, q.functions, fi, fn, score, wscore, off);
+            std::string ambig;
+            bool do_ambig = false;
+            if (fn.empty()) {
+                fn = "hypothetical protein";
+            } else {
+                size_t where = fn.find(" ?? ");
+                if (where != std::string::npos) {
+                    if (allow_ambiguous) {
+                        ambig = fn.substr(where + 4);
+                        fn = fn.substr(0, where);
+                        do_ambig = true;
+                    } else {
+                        fn = "hypothetical protein";
+                    }
+                }
+            }
+            float lf_score = 0.0f, gf_score = 0.0f;
+            std::string lf_fam, lf_fn, gf_fam;
+            std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
+            for (auto hit_ent : seq_score) {
+                const AccScore &se = hit_ent.second;
+                if (se.hit_total < kmer_hit_threshold)
+                    continue;
+                auto fent = q.db.family_data.find(hit_ent.first);
+                if (fent == q.db.family_data.end())
+                    continue;
+                const FamilyData &fd = fent->second;
+                if (do_ambig) {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else if (fd.function == ambig)
+                        pgf_rollup_ambig[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                } else {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                }
+                if (se.weighted_total > lf_score && fd.genus_id == target_genus_id) {
+                    lf_score = se.weighted_total;
+                    lf_fam = fd.plf;
+                    lf_fn = fd.function;
+                }
+            }
+            auto *rollup = &pgf_rollup;
+            if (do_ambig && lf_fn == ambig)
+                rollup = &pgf_rollup_ambig;
+            for (auto pgf_ent : *rollup)
+                if (pgf_ent.second > gf_score) {
+                    gf_score = pgf_ent.second;
+                    gf_fam = pgf_ent.first;
+                }
+            os << id << "\t" << gf_fam << "\t" << gf_score << "\t" << lf_fam << "\t" << lf_score << "\t"
+               << (do_ambig ? lf_fn : fn) << "\t" << score << "\t" << wscore << "\n";
+        } else {
+            typedef std::pair<uint32_t, AccScore> data_t;
+            std::vector<data_t> vec;
+            for (auto it : seq_score)
+                vec.push_back(it);
+            std::sort(vec.begin(), vec.end(), [](const data_t &l, const data_t &r) {
+                return l.second.weighted_total > r.second.weighted_total;
+            });
+            os << id << "\n";
+            for (auto it : vec) {
+                const AccScore &se = it.second;
+                if (se.hit_total < kmer_hit_threshold)
+                    break;
+                if (family_mode) {
+                    const FamilyData &fd = q.db.family_data[it.first];
+                    const float scaled = (float)se.hit_count / (float)fd.total_size;
+                    os << se.hit_count << "\t" << se.hit_total << "\t" << se.weighted_total << "\t" << fd.pgf
+                       << "\t" << fd.plf << "\t" << fd.total_size << "\t" << fd.count << "\t" << scaled << "\t"
+                       << fd.function << "\n";
+                    if (find_reps)
+                        os << "///\n"; /* no family reps loaded */
+                } else {
+                    const std::string peg = it.first < q.db.id_to_peg.size() ? q.db.id_to_peg[it.first] : "";
+                    os << peg << "\t" << se.hit_count;
+                    auto fh = q.db.peg_to_family.find(it.first);
+                    if (fh != q.db.peg_to_family.end()) {
+                        const FamilyData &fd = q.db.family_data[fh->second];
+                        os << "\t" << fd.pgf << "\t" << fd.plf << "\t" << fd.function << "\n";
+                    } else {
+                        os << "\n";
+                    }
+                }
+            }
+            os << "//\n";
+        }
+    }
+    return os.str();
+}
+
 struct FqSession {
     FamilyDb db;
     const oracle::SigKmer *table = nullptr; /* the caller's, kept alive by it */
@@ -555,6 +736,72 @@ char *oracle_fq_process(void *p, const char *fastq, uint64_t n)
         fq_on_parsed_seq(id, seq, mapper, os);
     });
     const std::string s = os.str();
+    char *b = static_cast<char *>(std::malloc(s.size() + 1));
+    std::memcpy(b, s.c_str(), s.size() + 1);
+    return b;
+}
+
+/* /lookup session: table (borrowed), functions, family DB files, and an
+ * optional /add FASTA filling kmer_to_id_ first (add_request.cc:164-170) */
+void *oracle_lookup_new(const void *table, uint64_t num_sigs, const char *const *functions, uint64_t n_functions,
+                        const char *genus_file, const char *families_file, const char *nr_fasta,
+                        const char *add_fasta)
+{
+    LookupSession *q = new LookupSession;
+    q->table = static_cast<const oracle::SigKmer *>(table);
+    for (uint64_t i = 0; i < n_functions; i++)
+        q->functions.push_back(functions[i]);
+    q->scorer = new oracle::Scorer(q->table, num_sigs);
+    auto read_fasta = [](const char *path) {
+        std::ifstream in(path, std::ios::binary);
+        std::stringstream ss;
+        ss << in.rdbuf();
+        return oracle::parse_fasta(ss.str());
+    };
+    if ((genus_file && *genus_file && !load_genus_map(q->db, genus_file)) ||
+        (families_file && *families_file && !load_families(q->db, families_file))) {
+        delete q;
+        return nullptr;
+    }
+    if (nr_fasta && *nr_fasta)
+        for (auto &rec : read_fasta(nr_fasta)) {
+            auto fit = q->db.peg_to_family.find(q->db.encode_id(rec.first));
+            if (fit == q->db.peg_to_family.end())
+                continue;
+            std::vector<oracle::SeqHit> hits;
+            q->scorer->process(rec.second.c_str(), rec.second.size(), nullptr, &hits, nullptr, false);
+            for (auto &h : hits)
+                q->db.kmer_to_family.add(h.hit.which_kmer, fit->second);
+        }
+    if (add_fasta && *add_fasta) {
+        auto recs = read_fasta(add_fasta);
+        std::vector<std::vector<uint64_t>> km(recs.size());
+        for (size_t r = 0; r < recs.size(); r++) {
+            std::vector<oracle::SeqHit> hits;
+            q->scorer->process(recs[r].second.c_str(), recs[r].second.size(), nullptr, &hits, nullptr, true);
+            for (auto &h : hits)
+                km[r].push_back(h.hit.which_kmer);
+        }
+        for (size_t r = 0; r < recs.size(); r++) { /* ids encoded after the chunk (non-TBB add) */
+            uint32_t eid = q->db.encode_id(recs[r].first);
+            for (uint64_t k : km[r])
+                q->kmer_to_id.add(k, eid);
+        }
+    }
+    return q;
+}
+
+void oracle_lookup_free(void *p) { delete static_cast<LookupSession *>(p); }
+
+/* names[i] = values[i] are the request's query-string parameters */
+char *oracle_lookup_process(void *p, int family_mode, const char *const *names, const char *const *values,
+                            uint64_t n_params, const char *fasta, uint64_t n)
+{
+    LookupSession *q = static_cast<LookupSession *>(p);
+    std::map<std::string, std::string> params;
+    for (uint64_t i = 0; i < n_params; i++)
+        params[names[i]] = values[i];
+    const std::string s = lookup_request(*q, family_mode != 0, params, oracle::parse_fasta(std::string(fasta, n)));
     char *b = static_cast<char *>(std::malloc(s.size() + 1));
     std::memcpy(b, s.c_str(), s.size() + 1);
     return b;

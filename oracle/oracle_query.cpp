@@ -12,6 +12,11 @@
  *   mode=fq             the input is FASTQ: fq_process_request.cc:298-365 over
  *                       FamilyMapper; optional genus=, families=, nr= files
  *                       load the family DB (kmer.cc:341-493, nr_loader.cc)
+ *   mode=lookup         /lookup (lookup_request.cc:153-400): family_mode=1 reads
+ *                       the family DB (genus=, families=, nr=); otherwise the
+ *                       FASTA is first /add-ed into kmer_to_id_; the request
+ *                       parameters find_best_match, kmer_hit_threhsold,
+ *                       allow_ambiguous_functions, target_genus, find_reps
  *   mode=matrix         /add of the FASTA into an empty mapping (add_request.cc:
  *                       164-170), then one /matrix request over the same FASTA
  *                       (matrix_request.cc:83-190): process_results' body
@@ -49,6 +54,12 @@ void *oracle_fq_new(const void *table, uint64_t num_sigs, const char *const *fun
 void oracle_fq_free(void *p);
 char *oracle_fq_process(void *p, const char *fastq, uint64_t n);
 void oracle_free(void *p);
+void *oracle_lookup_new(const void *table, uint64_t num_sigs, const char *const *functions, uint64_t n_functions,
+                        const char *genus_file, const char *families_file, const char *nr_fasta,
+                        const char *add_fasta);
+void oracle_lookup_free(void *p);
+char *oracle_lookup_process(void *p, int family_mode, const char *const *names, const char *const *values,
+                            uint64_t n_params, const char *fasta, uint64_t n);
 }
 
 /* KmerImage::map_image_file validation, kmer_image.cc:83-150 */
@@ -122,6 +133,32 @@ int main(int argc, char **argv)
         std::fwrite(out, 1, std::strlen(out), stdout);
         oracle_free(out);
         oracle_fq_free(q);
+        return 0;
+    }
+    if (mode == "lookup") {
+        std::vector<const char *> fn;
+        for (auto &f : functions)
+            fn.push_back(f.c_str());
+        const bool family_mode = qp["family_mode"] == "1";
+        /* the NR family load runs only for a family-mode server */
+        void *q = oracle_lookup_new(table.data(), num_sigs, fn.data(), fn.size(), qp["genus"].c_str(),
+                                    qp["families"].c_str(), family_mode ? qp["nr"].c_str() : "",
+                                    family_mode ? "" : fasta.c_str());
+        if (!q) {
+            std::fprintf(stderr, "cannot load the family files\n");
+            return 1;
+        }
+        std::vector<const char *> names, values;
+        for (auto &kv : qp) {
+            names.push_back(kv.first.c_str());
+            values.push_back(kv.second.c_str());
+        }
+        const std::string text = ss.str();
+        char *out = oracle_lookup_process(q, family_mode, names.data(), values.data(), names.size(), text.data(),
+                                          text.size());
+        std::fwrite(out, 1, std::strlen(out), stdout);
+        oracle_free(out);
+        oracle_lookup_free(q);
         return 0;
     }
     auto records = parse_fasta(ss.str());

@@ -22,6 +22,10 @@ Outputs (all small):
              file, a genus map and the NR proteins that fill
              kmer_to_family_id_: the fq request body (fq_process_request.cc:
              298-365) from the oracle.
+  lookup/    /lookup (lookup_request.cc:153-482) over proteins against the fq
+             data set's image and family DB: family mode with and without
+             find_best_match (ambiguous calls, target genus, reps), and the
+             peg mode after an /add of the same proteins.
   matrix/    protein families sharing signature k-mers (plus cross-family
              k-mers, repeated ids and unrelated proteins): the /add-then-
              /matrix body (matrix_request.cc:165-190) from the oracle.
@@ -356,6 +360,45 @@ def make_fq(rng) -> None:
     txt = oracle.query_text(data, os.path.join(out, "input.fasta"), "fq", args)
     assert txt.count(b"\n") > 20
     open(os.path.join(out, "expected_fq_default.txt"), "wb").write(txt)
+    return bases, members
+
+
+LOOKUP_PARAMS = {
+    "fam_best": {"family_mode": "1", "find_best_match": "1"},
+    "fam_best_ambig": {"family_mode": "1", "find_best_match": "1", "allow_ambiguous_functions": "1"},
+    "fam_best_genus": {"family_mode": "1", "find_best_match": "1", "target_genus": "Escherichia"},
+    "fam_list": {"family_mode": "1"},
+    "fam_list_reps": {"family_mode": "1", "find_reps": "1", "kmer_hit_threhsold": "1"},
+    "peg": {},
+    "peg_all": {"kmer_hit_threhsold": "0"},
+}
+
+
+def make_lookup(rng, bases, members) -> None:
+    """/lookup over proteins, against the fq data set's image and family DB."""
+    out = os.path.join(HERE, "lookup")
+    src = os.path.join(HERE, "fq")
+    table = image_files.read_image(os.path.join(src, "data"))
+    image_files.write_data_dir(os.path.join(out, "data"), table, [f"function {i}" for i in range(6)], ["o"])
+    recs = []
+    for f, m, s in members[::3]:
+        recs.append((f"fig|{1000 + f}.{m}.peg.{m}", s))  # ids the families file knows
+    for i in range(6):
+        f, m, s = members[int(rng.integers(0, len(members)))]
+        t = list(s)
+        for p in rng.integers(0, len(t), 25):
+            t[p] = "ACDEFGHIKLMNPQRSTVWY"[int(rng.integers(0, 20))]
+        recs.append((f"query{i}", "".join(t)))
+    recs.append(("chimera", bases[2][:70] + bases[4][70:140]))  # two functions: "F1 ?? F2"
+    recs.append(("chimera2", bases[1][:80] + bases[6][80:150]))
+    recs.append(("random", random_protein(rng, 120)))
+    recs.append(("short", bases[0][:12]))
+    fasta = os.path.join(out, "input.fasta")
+    write_fasta(fasta, recs)
+    files = {k: os.path.join(src, v) for k, v in FQ_FILES.items()}
+    for pname, params in LOOKUP_PARAMS.items():
+        txt = oracle.query_text(os.path.join(out, "data"), fasta, "lookup", {**params, **files})
+        open(os.path.join(out, f"expected_lookup_{pname}.txt"), "wb").write(txt)
 
 
 def main() -> None:
@@ -364,7 +407,8 @@ def main() -> None:
     make_edge(np.random.default_rng(12345))
     make_cap(np.random.default_rng(777))
     make_matrix(np.random.default_rng(4242))
-    make_fq(np.random.default_rng(31337))
+    bases, members = make_fq(np.random.default_rng(31337))
+    make_lookup(np.random.default_rng(2718), bases, members)
     print("golden fixtures written under", HERE)
 
 

@@ -54,7 +54,7 @@ def assert_same(got, want, n_seq):
 # golden handler text through the C++ facade (kgx_query)
 
 def _golden_cases():
-    for ds in ("scoring", "edge", "cap", "matrix", "fq"):
+    for ds in ("scoring", "edge", "cap", "matrix", "fq", "lookup"):
         d = os.path.join(GOLDEN, ds)
         for f in sorted(os.listdir(d)):
             if f.startswith("expected_") and f.endswith(".txt"):
