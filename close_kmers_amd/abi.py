@@ -59,7 +59,8 @@ class DeviceResult(ctypes.Structure):
 class Fragments(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint32), ("n_fragments", ctypes.c_uint32),
                 ("n_residues", ctypes.c_uint64), ("residues", ctypes.c_void_p),
-                ("offsets", ctypes.c_void_p), ("read", ctypes.c_void_p), ("frame", ctypes.c_void_p)]
+                ("offsets", ctypes.c_void_p), ("read", ctypes.c_void_p), ("frame", ctypes.c_void_p),
+                ("frame_counts", ctypes.c_void_p)]
 
 
 def tiled_hits_per_sequence(window_base: np.ndarray, hit_mask: np.ndarray, tile_windows: int,
@@ -131,7 +132,7 @@ SIGNATURES = {
     "kgx_fq_fragments_device": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
     "kgx_fq_create": (_INT, [_P, _CS, _CS, _CS, _CS, _PP]),
     "kgx_fq_destroy": (_INT, [_P]),
-    "kgx_fq_process": (_INT, [_P, _P, _U64, _INT, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U64)]),
+    "kgx_fq_process": (_INT, [_P, _CS, _U64, _INT, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U64)]),
     "kgx_kmap_create": (_INT, [_INT, _INT, _PP]),
     "kgx_kmap_destroy": (_INT, [_P]),
     "kgx_kmap_add": (_INT, [_P, _P, _P, _U64]),
@@ -480,8 +481,8 @@ class FqHandler:
 
     def process(self, fastq: bytes, finished: bool = True) -> bytes:
         t, n = ctypes.c_char_p(), ctypes.c_uint64()
-        buf = ctypes.create_string_buffer(fastq, len(fastq))
-        check(lib().kgx_fq_process(self.handle, buf, len(fastq), int(finished), ctypes.byref(t),
+        fastq = bytes(fastq)  # passed by pointer, not copied
+        check(lib().kgx_fq_process(self.handle, fastq, len(fastq), int(finished), ctypes.byref(t),
                                    ctypes.byref(n)), "kgx_fq_process")
         return ctypes.string_at(t, n.value) if n.value else b""
 

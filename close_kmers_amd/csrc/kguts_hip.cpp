@@ -8,6 +8,10 @@
 #include "kguts_hip.h"
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cctype>
 #include <cstring>
 #include <fstream>
@@ -933,17 +937,43 @@ FqRequest::FqRequest(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping) : kg
 
 void FqRequest::process(const std::string &block, bool finished, std::ostream &os)
 {
-    /* FastqParser::parse_char (fastq_parser.h:40-150); bad characters are
-     * reported there and skipped */
+    process(block.data(), block.size(), finished, os);
+}
+
+void FqRequest::process(const char *text, size_t n, bool finished, std::ostream &os)
+{
+    /* FastqParser::parse_char (fastq_parser.h:40-150), line-at-a-time: the
+     * id runs to the first blank, sequence lines keep isalpha() characters
+     * only (others are reported there and dropped), '+' and quality lines
+     * are skipped; a record is emitted at the quality line's newline and by
+     * parse_complete() (fastq_parser.cc:29-35) */
+    static const auto alpha = [] {
+        std::array<bool, 256> t{};
+        for (int c = 'A'; c <= 'Z'; c++)
+            t[c] = t[c + 32] = true;
+        return t;
+    }();
     enum { S_START, S_ID, S_DEF, S_DATA, S_PLUS_START, S_PLUS, S_QUAL };
-    std::vector<std::pair<std::string, std::string>> reads;
-    for (char c : block) {
+    FqBlock blk;
+    blk.bases.reserve(n / 2 + seq_.size());
+    /* the current record's residues are built in place at the end of
+     * blk.bases (a record cut by the block end is carried in seq_) */
+    blk.bases += seq_;
+    seq_.clear();
+    auto emit = [&]() {
+        blk.ids.push_back(id_);
+        blk.roff.push_back(blk.bases.size());
+        id_.clear();
+    };
+    const char *p = text, *end = text + n;
+    while (p < end) {
         switch (state_) {
         case S_START:
-            if (c == '@')
+            if (*p++ == '@')
                 state_ = S_ID;
             break;
-        case S_ID:
+        case S_ID: {
+            const char c = *p++;
             if (c == ' ' || c == '\t')
                 state_ = S_DEF;
             else if (c == '\n')
@@ -951,56 +981,87 @@ void FqRequest::process(const std::string &block, bool finished, std::ostream &o
             else
                 id_.push_back(c);
             break;
+        }
         case S_DEF:
-            if (c == '\n')
-                state_ = S_DATA;
-            break;
-        case S_DATA:
-            if (c == '\n')
-                state_ = S_PLUS_START;
-            else if (std::isalpha((unsigned char)c))
-                seq_.push_back(c);
-            break;
-        case S_PLUS_START:
-            if (c == '+')
-                state_ = S_PLUS;
-            break;
         case S_PLUS:
-            if (c == '\n')
-                state_ = S_QUAL;
-            break;
-        case S_QUAL:
-            if (c == '\n') {
-                reads.emplace_back(id_, seq_);
-                id_.clear();
-                seq_.clear();
+        case S_QUAL: {
+            const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(end - p)));
+            if (!nl) {
+                p = end;
+                break;
+            }
+            p = nl + 1;
+            if (state_ == S_QUAL) {
+                emit();
                 state_ = S_START;
+            } else {
+                state_ = state_ == S_DEF ? S_DATA : S_QUAL;
             }
             break;
         }
+        case S_DATA: {
+            const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(end - p)));
+            const char *stop = nl ? nl : end;
+            const char *q = p;
+            while (q < stop && alpha[(unsigned char)*q])
+                q++;
+            blk.bases.append(p, (size_t)(q - p)); /* the all-letter prefix in one go */
+            for (p = q; p < stop; p++)
+                if (alpha[(unsigned char)*p])
+                    blk.bases.push_back(*p);
+            if (nl) {
+                p = nl + 1;
+                state_ = S_PLUS_START;
+            }
+            break;
+        }
+        case S_PLUS_START:
+            if (*p++ == '+')
+                state_ = S_PLUS;
+            break;
+        }
     }
-    if (finished) { /* parse_complete, fastq_parser.cc:29-35 */
-        reads.emplace_back(id_, seq_);
-        id_.clear();
-        seq_.clear();
+    if (finished) {
+        emit();
+    } else {
+        seq_.assign(blk.bases, blk.roff.back(), std::string::npos);
+        blk.bases.resize(blk.roff.back());
     }
-    process_reads(reads, os);
+    process_block(blk, os);
 }
 
 void FqRequest::process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os)
 {
-    if (reads.empty())
-        return;
-    /* the block's reads -> fragments -> lookup, one GPU batch */
-    std::string bases;
-    std::vector<uint64_t> roff(reads.size() + 1, 0);
-    for (size_t r = 0; r < reads.size(); r++) {
-        bases += reads[r].second;
-        roff[r + 1] = bases.size();
+    FqBlock blk;
+    for (auto &r : reads) {
+        blk.ids.push_back(r.first);
+        blk.bases += r.second;
+        blk.roff.push_back(blk.bases.size());
     }
+    process_block(blk, os);
+}
+
+void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
+{
+    const uint32_t n_reads = (uint32_t)blk.ids.size();
+    if (n_reads == 0)
+        return;
+    /* KGX_FQ_TIMING=1: per-phase wall times on stderr */
+    static const bool timing = std::getenv("KGX_FQ_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (!timing)
+            return;
+        kgx_ctx_synchronize(kg_.ctx());
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[fq] %-12s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
+    /* the block's reads -> fragments -> lookup, one GPU batch */
     kgx_ctx *ctx = kg_.ctx();
     kgx_fragments fr;
-    int rc = kgx_fq_fragments(ctx, bases.data(), roff.data(), (uint32_t)reads.size(), &fr);
+    int rc = kgx_fq_fragments(ctx, blk.bases.data(), blk.roff.data(), n_reads, &fr);
     if (rc)
         throw_last(rc, "kgx_fq_fragments");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
@@ -1015,19 +1076,16 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
     rc = kgx_run_device(ctx, &p, fr.residues, fr.offsets, fr.n_fragments, fr.n_residues, want, nullptr);
     if (rc)
         throw_last(rc, "kgx_run_device");
-    std::vector<uint32_t> frag_read(fr.n_fragments);
-    std::vector<int8_t> frag_frame(fr.n_fragments);
-    std::vector<uint64_t> frag_off(fr.n_fragments + 1);
-    if (fr.n_fragments) {
-        kgx_ctx_synchronize(ctx);
-        kgx_memcpy_d2h(frag_read.data(), fr.read, frag_read.size() * 4);
-        kgx_memcpy_d2h(frag_frame.data(), fr.frame, frag_frame.size());
-    }
-    kgx_memcpy_d2h(frag_off.data(), fr.offsets, frag_off.size() * 8);
+    mark("lookup");
+    /* fragments per (read, frame): fragment g of read r, frame slot k */
+    std::vector<uint32_t> fcount((size_t)n_reads * 6);
+    kgx_ctx_synchronize(ctx);
+    kgx_memcpy_d2h(fcount.data(), fr.frame_counts, fcount.size() * 4);
     kgx_result res;
     rc = kgx_device_batch_collect(ctx, want, &res);
     if (rc)
         throw_last(rc, "kgx_device_batch_collect");
+    mark("collect");
     /* kmer_to_family_id_ lists of every hit */
     const uint64_t nh = fr.n_fragments && families ? res.hit_offsets[fr.n_fragments] : 0;
     std::vector<uint64_t> list_off(nh + 1, 0);
@@ -1045,28 +1103,54 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
         if (rc)
             throw_last(rc, "kgx_kmap_lookup");
     }
+    /* fragment lengths (printed for matches) are needed only for reads with
+     * calls: fetch their offset slices, or all offsets when there are many */
+    std::vector<uint64_t> rfirst(n_reads + 1, 0);
+    for (uint32_t r = 0; r < n_reads; r++) {
+        uint64_t k = 0;
+        for (int f = 0; f < 6; f++)
+            k += fcount[(size_t)r * 6 + f];
+        rfirst[r + 1] = rfirst[r] + k;
+    }
+    std::vector<uint32_t> called;
+    for (uint32_t r = 0; r < n_reads; r++)
+        if (res.call_offsets[rfirst[r + 1]] != res.call_offsets[rfirst[r]])
+            called.push_back(r);
+    std::vector<uint64_t> frag_off;
+    const bool all_offsets = called.size() > 1024;
+    if (all_offsets) {
+        frag_off.resize(fr.n_fragments + 1);
+        kgx_memcpy_d2h(frag_off.data(), fr.offsets, frag_off.size() * 8);
+    }
+    std::vector<uint64_t> slice;
+    mark("family lists");
     /* on_parsed_seq (fq_process_request.cc:298-365), reads in order */
     FamilyMapper mapper(kg_, mapping_);
     std::vector<std::pair<uint64_t, uint32_t>> hit_lists;
     std::vector<KmerCall> calls;
-    uint64_t f = 0;
-    for (uint32_t r = 0; r < (uint32_t)reads.size(); r++) {
-        const uint64_t f0 = f;
-        while (f < fr.n_fragments && frag_read[f] == r)
-            f++;
-        if (reads[r].first.empty())
+    std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
+    std::vector<uint64_t> match_frag, best_frag;
+    size_t next_called = 0;
+    for (uint32_t r = 0; r < n_reads; r++) {
+        const bool has_calls = next_called < called.size() && called[next_called] == r;
+        if (has_calls)
+            next_called++;
+        if (blk.ids[r].empty())
             continue;
-        if (!families && res.call_offsets[f] == res.call_offsets[f0])
+        if (!families && !has_calls)
             continue; /* no calls in any frame: no output, no mapper state */
         double best_score = 0.0;
         int best_frame = 0;
-        std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
-        uint64_t g = f0;
-        while (g < f) {
-            const int frame = frag_frame[g];
+        best_matches.clear();
+        best_frag.clear();
+        uint64_t g = rfirst[r];
+        for (int fs = 0; fs < 6; fs++) {
+            const int frame = fs < 3 ? fs + 1 : -(fs - 2);
+            const uint64_t g_end = g + fcount[(size_t)r * 6 + fs];
             double score = 0.0;
             matches.clear();
-            for (; g < f && frag_frame[g] == frame; g++) {
+            match_frag.clear();
+            for (; g < g_end; g++) {
                 hit_lists.clear();
                 if (families)
                     for (uint64_t h = res.hit_offsets[g]; h < res.hit_offsets[g + 1]; h++)
@@ -1075,26 +1159,37 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
                 for (uint64_t c = res.call_offsets[g]; c < res.call_offsets[g + 1]; c++)
                     calls.emplace_back(res.calls[c].start, res.calls[c].end, res.calls[c].count,
                                        res.calls[c].function_index, res.calls[c].weighted_hits);
-                matches.emplace_back((size_t)(frag_off[g + 1] - frag_off[g]),
-                                     mapper.find_best_family_match(hit_lists, list_ids.data(), calls));
+                matches.emplace_back(0, mapper.find_best_family_match(hit_lists, list_ids.data(), calls));
+                match_frag.push_back(g);
                 score += matches.back().second.score;
                 if (score > best_score) {
                     best_score = score;
                     best_frame = frame;
                     best_matches = matches;
+                    best_frag = match_frag;
                 }
             }
         }
         if (best_score > 0.0) {
-            os << reads[r].first << "\t" << best_frame << "\t" << best_score << "\t";
+            /* the lengths of the printed fragments */
+            const uint64_t f0 = rfirst[r], f1 = rfirst[r + 1];
+            const uint64_t *offs = frag_off.data();
+            if (!all_offsets) {
+                slice.resize(f1 - f0 + 1);
+                kgx_memcpy_d2h(slice.data(), fr.offsets + f0, slice.size() * 8);
+                offs = slice.data() - f0;
+            }
+            os << blk.ids[r] << "\t" << best_frame << "\t" << best_score << "\t";
             for (size_t i = 0; i < best_matches.size(); i++) {
+                const uint64_t g2 = best_frag[i];
                 if (i)
                     os << "\t";
-                os << best_matches[i].first << "\t" << best_matches[i].second;
+                os << (size_t)(offs[g2 + 1] - offs[g2]) << "\t" << best_matches[i].second;
             }
             os << std::endl;
         }
     }
+    mark("host loop");
 }
 
 }  // namespace kgx
@@ -1183,7 +1278,7 @@ int kgx_fq_process(kgx_fq *q, const char *fastq, uint64_t n, int finished, const
         return kgx::fail(KGX_EINVAL, "null argument");
     try {
         std::ostringstream os;
-        q->req->process(std::string(fastq ? fastq : "", n), finished != 0, os);
+        q->req->process(fastq ? fastq : "", (size_t)n, finished != 0, os);
         q->text = os.str();
     } catch (const kgx::Error &e) {
         return kgx::fail(e.code(), e.what());

@@ -342,10 +342,17 @@ public:
     /* one block of FASTQ text; `finished` = the request's last block
      * (parse_complete).  Output lines are appended to os. */
     void process(const std::string &fastq_block, bool finished, std::ostream &os);
+    void process(const char *fastq_block, size_t n, bool finished, std::ostream &os);
     /* reads already parsed (id, DNA) */
     void process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os);
 
 private:
+    struct FqBlock { /* parsed reads: ids, bases concatenated, offsets */
+        std::vector<std::string> ids;
+        std::string bases;
+        std::vector<uint64_t> roff{0};
+    };
+    void process_block(const FqBlock &blk, std::ostream &os);
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     /* FastqParser state (fastq_parser.h:40-150) */

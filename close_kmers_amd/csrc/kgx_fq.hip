@@ -189,6 +189,7 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     out->offsets = c->fq_off.as<uint64_t>();
     out->read = c->fq_read.as<uint32_t>();
     out->frame = c->fq_frame.as<int8_t>();
+    out->frame_counts = c->fq_nfrag.as<uint32_t>();
     return KGX_OK;
 }
 

@@ -272,6 +272,7 @@ typedef struct kgx_fragments {
     const uint64_t *offsets;  /* device: [n_fragments + 1] */
     const uint32_t *read;     /* device: read index of each fragment */
     const int8_t *frame;      /* device: frame of each fragment */
+    const uint32_t *frame_counts; /* device: fragments per (read, frame), [n_reads * 6] */
 } kgx_fragments;
 /* reads from host memory (bases concatenated, read_offsets[n_reads + 1]) */
 int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
