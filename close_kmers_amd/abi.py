@@ -102,6 +102,8 @@ SIGNATURES = {
     "kgx_image_open": (_INT, [_CS, _INT, _PP]),
     "kgx_image_from_memory": (_INT, [_P, _U64, _INT, _PP]),
     "kgx_image_build_synthetic": (_INT, [_U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
+    "kgx_image_build": (_INT, [_P, _P, _P, _P, _P, _U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
+    "kgx_image_save": (_INT, [_P, _CS]),
     "kgx_image_close": (_INT, [_P]),
     "kgx_image_num_sigs": (_U64, [_P]),
     "kgx_image_device": (_INT, [_P]),
@@ -246,6 +248,24 @@ class Image:
         check(lib().kgx_image_build_synthetic(n_keys, num_sigs, device, ctypes.byref(h),
                                               ctypes.byref(stored)), "kgx_image_build_synthetic")
         return cls(h.value), stored.value
+
+    @classmethod
+    def build(cls, keys, function_index, otu_index, avg_from_end, function_wt, num_sigs: int,
+              device: int = 0) -> tuple["Image", int]:
+        """Device image build from entry arrays (insert_kmer semantics)."""
+        k = np.ascontiguousarray(keys, dtype=np.uint64)
+        f = np.ascontiguousarray(function_index, dtype=np.int32)
+        o = np.ascontiguousarray(otu_index, dtype=np.int32)
+        a = np.ascontiguousarray(avg_from_end, dtype=np.uint16)
+        w = np.ascontiguousarray(function_wt, dtype=np.float32)
+        h, stored = ctypes.c_void_p(), ctypes.c_uint64()
+        check(lib().kgx_image_build(k.ctypes.data, f.ctypes.data, o.ctypes.data, a.ctypes.data, w.ctypes.data,
+                                    len(k), num_sigs, device, ctypes.byref(h), ctypes.byref(stored)),
+              "kgx_image_build")
+        return cls(h.value), stored.value
+
+    def save(self, data_dir: str) -> None:
+        check(lib().kgx_image_save(self.handle, data_dir.encode()), "kgx_image_save")
 
     @property
     def num_sigs(self) -> int:

@@ -128,6 +128,9 @@ hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threa
                               uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream);
 hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
                               unsigned long long *n_stored, hipStream_t stream);
+hipError_t launch_entries_image(kgx_sig_kmer *table, uint64_t num_sigs, const uint64_t *keys,
+                                const int32_t *fi, const int32_t *otu, const uint16_t *avg, const float *wt,
+                                uint64_t n_entries, unsigned long long *n_stored, hipStream_t stream);
 hipError_t launch_synth_queries(uint64_t image_n_keys, uint32_t n_seq, uint32_t length,
                                 uint32_t x_permille, uint64_t q0, uint8_t *residues,
                                 uint64_t *seq_off, hipStream_t stream);

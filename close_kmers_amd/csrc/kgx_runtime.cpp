@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -356,6 +357,57 @@ int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kg
     return image_settle(img, out);
 }
 
+int kgx_image_build(const uint64_t *keys, const int32_t *function_index, const int32_t *otu_index,
+                    const uint16_t *avg_from_end, const float *function_wt, uint64_t n, uint64_t num_sigs,
+                    int device, kgx_image **out, uint64_t *n_stored)
+{
+    if (!out || (n && (!keys || !function_index || !otu_index || !avg_from_end || !function_wt)))
+        return fail(KGX_EINVAL, "null argument");
+    /* kguts.cc:209-213: every valid key counts (duplicates too) */
+    uint64_t valid = 0;
+    for (uint64_t i = 0; i < n; i++)
+        valid += keys[i] <= MAX_ENCODED;
+    if (valid >= num_sigs / 2)
+        return fail(KGX_EFULL, "Your Kmer hash is half-full (kguts.cc:209-213)");
+    kgx_image *img = nullptr;
+    int rc = image_alloc(device, num_sigs, &img);
+    if (rc)
+        return rc;
+    DevBuf d_keys, d_fi, d_otu, d_avg, d_wt, d_count;
+    hipError_t e = hipSuccess;
+    for (auto rq : {d_keys.reserve(std::max<uint64_t>(n, 1) * 8), d_fi.reserve(std::max<uint64_t>(n, 1) * 4),
+                    d_otu.reserve(std::max<uint64_t>(n, 1) * 4), d_avg.reserve(std::max<uint64_t>(n, 1) * 2),
+                    d_wt.reserve(std::max<uint64_t>(n, 1) * 4), d_count.reserve(8)})
+        if (rq != hipSuccess)
+            e = rq;
+    if (e == hipSuccess && n) {
+        e = hipMemcpy(d_keys.p, keys, n * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(d_fi.p, function_index, n * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(d_otu.p, otu_index, n * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(d_avg.p, avg_from_end, n * 2, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(d_wt.p, function_wt, n * 4, hipMemcpyHostToDevice);
+    }
+    unsigned long long cnt = 0;
+    if (e == hipSuccess)
+        e = launch_entries_image(img->d_table, num_sigs, d_keys.as<uint64_t>(), d_fi.as<int32_t>(),
+                                 d_otu.as<int32_t>(), d_avg.as<uint16_t>(), d_wt.as<float>(), n,
+                                 d_count.as<unsigned long long>(), nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(&cnt, d_count.p, 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        kgx_image_close(img);
+        return fail(e == hipErrorOutOfMemory ? KGX_ENOMEM : KGX_EDEVICE,
+                    std::string("image build: ") + hipGetErrorString(e));
+    }
+    if (n_stored)
+        *n_stored = cnt;
+    return image_settle(img, out);
+}
+
 int kgx_image_close(kgx_image *img)
 {
     if (!img)
@@ -385,31 +437,62 @@ int kgx_image_set_layout(kgx_image *img, int layout)
     return fail(KGX_EINVAL, "unknown layout " + std::to_string(layout));
 }
 
-int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes)
+/* buckets [first, first + count) in the file's format into host memory */
+static int image_read(const kgx_image *img, uint64_t first, uint64_t count, kgx_sig_kmer *dst)
 {
-    if (!img || !dst || nbytes != img->num_sigs * sizeof(kgx_sig_kmer))
-        return fail(KGX_EINVAL, "bad download buffer");
     HIP_TRY(hipSetDevice(img->device));
     if (img->layout == KGX_LAYOUT_AOS24) {
-        HIP_TRY(hipMemcpy(dst, img->d_table, nbytes, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(dst, img->d_table + first, count * sizeof(kgx_sig_kmer), hipMemcpyDeviceToHost));
         return KGX_OK;
     }
     /* PACKED16: unpack slices on the device, then copy them out */
     const uint64_t slice = 1ull << 24; /* buckets (384 MiB of output) */
     kgx_sig_kmer *tmp = nullptr;
-    HIP_TRY(hipMalloc(&tmp, std::min(slice, img->num_sigs) * sizeof(kgx_sig_kmer)));
+    HIP_TRY(hipMalloc(&tmp, std::max<uint64_t>(1, std::min(slice, count)) * sizeof(kgx_sig_kmer)));
     hipError_t e = hipSuccess;
-    for (uint64_t b = 0; b < img->num_sigs && e == hipSuccess; b += slice) {
-        const uint64_t n = std::min(slice, img->num_sigs - b);
-        e = launch_unpack(img->d_packed + b, tmp, n, nullptr);
+    for (uint64_t b = 0; b < count && e == hipSuccess; b += slice) {
+        const uint64_t m = std::min(slice, count - b);
+        e = launch_unpack(img->d_packed + first + b, tmp, m, nullptr);
         if (e == hipSuccess)
-            e = hipMemcpy(static_cast<kgx_sig_kmer *>(dst) + b, tmp, n * sizeof(kgx_sig_kmer),
-                          hipMemcpyDeviceToHost);
+            e = hipMemcpy(dst + b, tmp, m * sizeof(kgx_sig_kmer), hipMemcpyDeviceToHost);
     }
     (void)hipFree(tmp);
     if (e != hipSuccess)
         return fail(KGX_EDEVICE, std::string("download: ") + hipGetErrorString(e));
     return KGX_OK;
+}
+
+int kgx_image_download(const kgx_image *img, void *dst, uint64_t nbytes)
+{
+    if (!img || !dst || nbytes != img->num_sigs * sizeof(kgx_sig_kmer))
+        return fail(KGX_EINVAL, "bad download buffer");
+    return image_read(img, 0, img->num_sigs, static_cast<kgx_sig_kmer *>(dst));
+}
+
+int kgx_image_save(const kgx_image *img, const char *dir)
+{
+    if (!img || !dir)
+        return fail(KGX_EINVAL, "null argument");
+    const std::string path = std::string(dir) + "/kmer.table.mem_map";
+    FILE *f = std::fopen(path.c_str(), "wb");
+    if (!f)
+        return fail(KGX_EIO, "could not open " + path + " for writing: " + std::strerror(errno));
+    const kgx_image_header h{img->num_sigs, sizeof(kgx_sig_kmer), 1};
+    bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
+    const uint64_t chunk = 1ull << 25; /* buckets per write (768 MiB) */
+    std::vector<kgx_sig_kmer> buf(std::min(chunk, std::max<uint64_t>(img->num_sigs, 1)));
+    for (uint64_t b = 0; ok && b < img->num_sigs; b += chunk) {
+        const uint64_t m = std::min(chunk, img->num_sigs - b);
+        int rc = image_read(img, b, m, buf.data());
+        if (rc) {
+            std::fclose(f);
+            return rc;
+        }
+        ok = std::fwrite(buf.data(), sizeof(kgx_sig_kmer), m, f) == m;
+    }
+    if (std::fclose(f) != 0)
+        ok = false;
+    return ok ? KGX_OK : fail(KGX_EIO, "short write to " + path);
 }
 
 /* ---- contexts ------------------------------------------------------------ */

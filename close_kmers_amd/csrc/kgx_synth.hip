@@ -177,6 +177,67 @@ __global__ void synth_payload_kernel(kgx_sig_kmer *t, uint64_t n, uint64_t n_src
     }
 }
 
+/* entries given by the caller: the same CAS insert (lowest entry index owns
+ * a duplicated key, as the sequential KmerGuts::insert_kmer's earliest copy
+ * is the one a probe finds), keys above 20^8 skipped (kguts.cc:203-207) */
+__global__ void entries_insert_kernel(kgx_sig_kmer *t, uint64_t n, uint64_t magic, const uint64_t *keys,
+                                      uint64_t n_entries, unsigned long long *n_stored)
+{
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_entries;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = keys[e];
+        if (key > MAX_ENCODED)
+            continue;
+        uint64_t h = mod_by(key, n, magic);
+        for (uint64_t probes = 0; probes < n; probes++) {
+            unsigned long long *kp = reinterpret_cast<unsigned long long *>(t + h);
+            const unsigned long long old = atomicCAS(kp, (unsigned long long)EMPTY_KEY,
+                                                     (unsigned long long)key);
+            if (old == EMPTY_KEY) {
+                atomicAdd(n_stored, 1ULL);
+                break;
+            }
+            if (old == key)
+                break;
+            h = (h + 1 == n) ? 0 : h + 1;
+        }
+        atomicMin(reinterpret_cast<unsigned long long *>(t + h) + 2, (unsigned long long)e);
+    }
+}
+
+__global__ void entries_payload_kernel(kgx_sig_kmer *t, uint64_t n, const int32_t *fi, const int32_t *otu,
+                                       const uint16_t *avg, const float *wt)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t *w = reinterpret_cast<uint64_t *>(t + i);
+        if (w[0] > MAX_ENCODED) {
+            w[2] = 0;
+            continue;
+        }
+        const uint64_t e = w[2];
+        kgx_sig_kmer *k = t + i;
+        k->otu_index = otu[e];
+        k->avg_from_end = avg[e];
+        k->pad = 0;
+        k->function_index = fi[e];
+        k->function_wt = wt[e];
+    }
+}
+
+hipError_t launch_entries_image(kgx_sig_kmer *table, uint64_t num_sigs, const uint64_t *keys,
+                                const int32_t *fi, const int32_t *otu, const uint16_t *avg, const float *wt,
+                                uint64_t n_entries, unsigned long long *n_stored, hipStream_t stream)
+{
+    const dim3 grid(8192), block(256);
+    hipLaunchKernelGGL(synth_init_kernel, grid, block, 0, stream, table, num_sigs);
+    (void)hipMemsetAsync(n_stored, 0, sizeof(*n_stored), stream);
+    hipLaunchKernelGGL(entries_insert_kernel, grid, block, 0, stream, table, num_sigs, mod_magic(num_sigs), keys,
+                       n_entries, n_stored);
+    hipLaunchKernelGGL(entries_payload_kernel, grid, block, 0, stream, table, num_sigs, fi, otu, avg, wt);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
                               unsigned long long *n_stored, hipStream_t stream)
 {

@@ -166,6 +166,19 @@ int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, k
  * number of distinct keys stored. */
 int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kgx_image **out,
                               uint64_t *n_stored);
+/* An image from caller entries (host arrays, n each), in num_sigs buckets:
+ * KmerGuts::insert_kmer semantics (kguts.cc:166-228) -- keys above 20^8
+ * are skipped, KGX_EFULL when the valid entries (duplicates included) reach
+ * num_sigs / 2; of duplicated keys the lowest index is the one lookups find,
+ * as with the sequential builder.  Bucket placement may differ from a
+ * sequential build (parallel insertion); lookups are identical. */
+int kgx_image_build(const uint64_t *keys, const int32_t *function_index, const int32_t *otu_index,
+                    const uint16_t *avg_from_end, const float *function_wt, uint64_t n, uint64_t num_sigs,
+                    int device, kgx_image **out, uint64_t *n_stored);
+/* write <dir>/kmer.table.mem_map in the file format (save_kmer_hash_table,
+ * kguts.cc:194-234 with the header of kmer_image.h:25-30), loadable by
+ * KmerImage and kgx_image_open */
+int kgx_image_save(const kgx_image *img, const char *dir);
 int kgx_image_close(kgx_image *img);
 uint64_t kgx_image_num_sigs(const kgx_image *img);
 int kgx_image_device(const kgx_image *img);

@@ -442,3 +442,47 @@ def test_device_queries_and_run_device(gpu, oracle_lib):
         finally:
             L_.kgx_device_free(d_res)
             L_.kgx_device_free(d_off)
+
+
+def test_image_build_from_entries_and_save(gpu, oracle_lib, tmp_path):
+    """kgx_image_build (insert_kmer semantics: invalid keys skipped, duplicated
+    keys resolved to their first entry) and kgx_image_save (a file KmerImage
+    and kgx_image_open load): lookups equal the oracle's sequential build."""
+    from close_kmers_amd import image_files
+    rng = np.random.default_rng(17)
+    img = DesignedImage()
+    recs = []
+    for t in range(40):
+        s = random_protein(rng, 150)
+        img.add_windows(s, range(0, 120), t % 6, oI=t % 3, rng=rng)
+        recs.append((f"s{t}", s))
+    k, f, o, a, w = img.arrays()
+    # append duplicates (later entries for existing keys, other payloads) and invalid keys
+    dup = rng.integers(0, len(k), 300)
+    k2 = np.concatenate([k, k[dup], np.array([20 ** 8, 20 ** 8 + 5, 2 ** 63], np.uint64)])
+    f2 = np.concatenate([f, (f[dup] + 1) % 6, np.zeros(3, np.int32)])
+    o2 = np.concatenate([o, o[dup] + 7, np.zeros(3, np.int32)])
+    a2 = np.concatenate([a, a[dup] + 1, np.zeros(3, np.uint16)])
+    w2 = np.concatenate([w, w[dup] * 2, np.zeros(3, np.float32)])
+    num_sigs = synth.builder_num_sigs(len(k2))
+    host = oracle_lib.build_table(num_sigs, k2, f2, o2, a2, w2)  # sequential insert_kmer
+    res, off = pack(recs)
+    want = oracle_lib.process_batch(host, res, off)
+    dev, stored = gpu.Image.build(k2, f2, o2, a2, w2, num_sigs)
+    with dev:
+        assert stored == len(k)
+        with gpu.Context(dev) as ctx:
+            assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, len(recs))
+        data = str(tmp_path / "img")
+        os.makedirs(data)
+        dev.save(data)
+    table = image_files.read_image(data)
+    occ = table[table["which_kmer"] <= 20 ** 8]
+    assert len(occ) == len(k)
+    got = dict(zip(occ["which_kmer"].tolist(), occ["function_index"].tolist()))
+    assert all(got[int(kk)] == int(ff) for kk, ff in zip(k, f))  # first entry's payload
+    assert np.array_equal(oracle_lib.process_batch(table, res, off).hits["pos"], want.hits["pos"])
+    with gpu.Image.open(data) as reopened, gpu.Context(reopened) as ctx:
+        assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, len(recs))
+    with pytest.raises(Exception):
+        gpu.Image.build(k, f, o, a, w, 2 * len(k))  # half full
