@@ -96,6 +96,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-microbench", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts (streams) in flight")
@@ -217,6 +218,29 @@ def main():
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts), "
         f"probe {np.mean(probe_ms):.3f} ms")
 
+    # PCIe-inclusive rate of the host-buffer boundary (kgx_process_batch:
+    # H2D residues, plan/probe/score, gather, D2H hits + calls) -- reported
+    # beside `value`, never as it
+    host_path = None
+    if d.rank == 0 and not args.no_host_path:
+        res_h = np.empty(n_res, np.uint8)
+        off_h = np.empty(n + 1, np.uint64)
+        abi.check(L.kgx_memcpy_d2h(res_h.ctypes.data, d_res, res_h.nbytes), "d2h")
+        abi.check(L.kgx_memcpy_d2h(off_h.ctypes.data, d_off, off_h.nbytes), "d2h")
+        r = ctx.process_batch(res_h, off_h, params, want=want, copy=False)  # warm (buffer growth)
+        th = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = ctx.process_batch(res_h, off_h, params, want=want, copy=False)
+            th.append(time.perf_counter() - t0)
+        t_h = float(np.median(th))
+        host_path = {"value": n_res / t_h, "unit": "residues/s", "ms_per_batch": t_h * 1e3,
+                     "d2h_bytes": int(len(r.hits) * 32 + len(r.calls) * 20),
+                     "note": "kgx_process_batch from host buffers: H2D residues + kernels + gather + "
+                             "D2H of hits and calls into the context's pinned result buffers "
+                             "(PCIe-inclusive)"}
+        log(f"[bench] host-buffer path {n_res / t_h:.3e} residues/s ({t_h * 1e3:.1f} ms/batch)")
+
     ceiling = None
     if d.rank == 0 and not args.no_microbench:
         ceiling = {}
@@ -318,6 +342,7 @@ def main():
                     if ceiling else None),
             },
             "cpu_baseline": cpu,
+            "host_path": host_path,
         }
         print(json.dumps(line), flush=True)
     d.close()

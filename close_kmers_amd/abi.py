@@ -212,11 +212,12 @@ def parse_params(values: dict | None) -> Params:
     return p
 
 
-def _view(ptr: int | None, n: int, dtype) -> np.ndarray:
+def _view(ptr: int | None, n: int, dtype, copy: bool = True) -> np.ndarray:
     if n == 0 or not ptr:
         return np.zeros(0, dtype=dtype)
     buf = (ctypes.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
-    return np.frombuffer(buf, dtype=dtype).copy()
+    a = np.frombuffer(buf, dtype=dtype)
+    return a.copy() if copy else a
 
 
 class Image:
@@ -298,14 +299,17 @@ class Image:
 
 
 class BatchResult:
-    def __init__(self, r: Result, want: int):
+    """Host CSR results.  copy=False gives views of the context's buffers
+    (valid until its next call, as in the C ABI) instead of numpy copies."""
+
+    def __init__(self, r: Result, want: int, copy: bool = True):
         n = r.n_seq
-        self.hit_offsets = _view(r.hit_offsets, n + 1, np.uint64)
-        self.call_offsets = _view(r.call_offsets, n + 1, np.uint64)
-        self.otu_offsets = _view(r.otu_offsets, n + 1, np.uint64)
-        self.hits = _view(r.hits, int(self.hit_offsets[-1]) if n + 1 else 0, HIT_DTYPE)
-        self.calls = _view(r.calls, int(self.call_offsets[-1]), CALL_DTYPE)
-        self.otus = _view(r.otus, int(self.otu_offsets[-1]), OTU_DTYPE)
+        self.hit_offsets = _view(r.hit_offsets, n + 1, np.uint64, copy)
+        self.call_offsets = _view(r.call_offsets, n + 1, np.uint64, copy)
+        self.otu_offsets = _view(r.otu_offsets, n + 1, np.uint64, copy)
+        self.hits = _view(r.hits, int(self.hit_offsets[-1]) if n + 1 else 0, HIT_DTYPE, copy)
+        self.calls = _view(r.calls, int(self.call_offsets[-1]), CALL_DTYPE, copy)
+        self.otus = _view(r.otus, int(self.otu_offsets[-1]), OTU_DTYPE, copy)
         self.n_windows = r.n_windows
 
 
@@ -319,7 +323,7 @@ class Context:
         self.handle = h.value
 
     def process_batch(self, residues, offsets, params: Params | dict | None = None,
-                      want: int = WANT_HITS | WANT_CALLS | WANT_OTU) -> BatchResult:
+                      want: int = WANT_HITS | WANT_CALLS | WANT_OTU, copy: bool = True) -> BatchResult:
         if params is None or isinstance(params, dict):
             params = parse_params(params)
         residues = np.ascontiguousarray(np.frombuffer(bytes(residues), np.uint8)
@@ -331,7 +335,7 @@ class Context:
                                       residues.ctypes.data if residues.size else None,
                                       offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
               "kgx_process_batch")
-        return BatchResult(r, want)
+        return BatchResult(r, want, copy)
 
     def fq_fragments(self, bases, read_offsets) -> Fragments:
         """6-frame code-11 fragments (> 10 aa) of the reads, left on the device."""

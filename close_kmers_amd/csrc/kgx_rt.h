@@ -71,6 +71,46 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+/* grow-only pinned host array (hipHostMalloc): the staging and result
+ * buffers of the host-buffer path, so H2D / D2H run at DMA speed instead of
+ * through the runtime's pageable bounce buffers.  Contents are not
+ * initialised on growth. */
+template <class T> struct PinnedVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec &) = delete;
+    PinnedVec &operator=(const PinnedVec &) = delete;
+    ~PinnedVec()
+    {
+        if (p)
+            (void)hipHostFree(p);
+    }
+    hipError_t resize(size_t m)
+    {
+        if (m > cap) {
+            T *q = nullptr;
+            const size_t want = std::max<size_t>(m + m / 4, 64);
+            hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&q), want * sizeof(T), hipHostMallocDefault);
+            if (e != hipSuccess)
+                return e;
+            if (p) {
+                std::memcpy(q, p, n * sizeof(T));
+                (void)hipHostFree(p);
+            }
+            p = q;
+            cap = want;
+        }
+        n = m;
+        return hipSuccess;
+    }
+    T *data() { return p; }
+    const T *data() const { return p; }
+    size_t size() const { return n; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+};
+
 inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
@@ -116,11 +156,11 @@ struct kgx_ctx {
     int probe_j = kgx::PROBE_J_DEFAULT;
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
-    std::vector<kgx_hit> h_hits;
-    std::vector<kgx_call> h_calls;
+    kgx::PinnedVec<kgx_hit> h_hits;
+    kgx::PinnedVec<kgx_call> h_calls;
     std::vector<kgx_otu> h_otus;
-    std::vector<uint32_t> h_hcount, h_ccount;
-    std::vector<char> h_res;
+    kgx::PinnedVec<uint32_t> h_hcount, h_ccount;
+    kgx::PinnedVec<char> h_res;
 };
 
 #endif

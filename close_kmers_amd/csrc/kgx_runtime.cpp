@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +41,23 @@ bool is_gfx950(int dev)
         return false;
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
 }
+
+/* KGX_TIMING=1: phase wall times of the host-buffer path on stderr */
+struct PhaseTimer {
+    kgx_ctx *c;
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseTimer(kgx_ctx *ctx) : c(ctx), on(std::getenv("KGX_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what)
+    {
+        if (!on)
+            return;
+        (void)hipStreamSynchronize(c->stream);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[kgx] %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 }  // namespace kgx
 
@@ -684,12 +702,15 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     if (n_res && !residues)
         return fail(KGX_EINVAL, "null residues");
     HIP_TRY(hipSetDevice(c->img->device));
+    PhaseTimer tm(c);
 
     /* stage residues; a sequence is cut at its first NUL (strlen bound of
      * gather_hits, kguts.cc:792): the NUL's predecessor and everything after
      * become 'X', which kills exactly the windows the reference never visits */
     const char *src = residues ? residues + r0 : nullptr;
-    c->h_res.assign(src, src + n_res);
+    HIP_TRY(c->h_res.resize(n_res));
+    if (n_res)
+        std::memcpy(c->h_res.data(), src, n_res);
     for (uint32_t s = 0; s < n_seq; s++) {
         char *b = c->h_res.data() + (seq_offsets[s] - r0);
         uint64_t len = seq_offsets[s + 1] - seq_offsets[s];
@@ -711,11 +732,15 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
                                c->stream));
     HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), (n_seq + 1) * sizeof(uint64_t),
                            hipMemcpyHostToDevice, c->stream));
+    tm.mark("stage");
     int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq,
                             n_res, want, nullptr);
     if (rc)
         return rc;
-    return kgx_device_batch_collect(c, want, out);
+    tm.mark("device");
+    rc = kgx_device_batch_collect(c, want, out);
+    tm.mark("collect");
+    return rc;
 }
 
 /* the current device batch's results -> host CSR (gather on the device, OTU
@@ -727,10 +752,11 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     if (!c->have_hits)
         return fail(KGX_EINVAL, "no device batch to collect");
     HIP_TRY(hipSetDevice(c->img->device));
+    PhaseTimer tm(c);
     const uint32_t n_seq = c->n_seq;
     /* counts -> dense CSR offsets on the host, gather on the device */
-    c->h_hcount.resize(n_seq + 1);
-    c->h_ccount.resize(n_seq + 1);
+    HIP_TRY(c->h_hcount.resize(n_seq + 1));
+    HIP_TRY(c->h_ccount.resize(n_seq + 1));
     if (n_seq) {
         HIP_TRY(hipMemcpyAsync(c->h_hcount.data(), c->hit_count.p, n_seq * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, c->stream));
@@ -745,10 +771,11 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
         c->h_hoff[s + 1] = c->h_hoff[s] + c->h_hcount[s];
         c->h_coff[s + 1] = c->h_coff[s] + (want_calls ? c->h_ccount[s] : 0);
     }
+    tm.mark(" counts");
     const uint64_t nh = c->h_hoff[n_seq], nc = c->h_coff[n_seq];
     const bool need_hits = (want & (KGX_WANT_HITS | KGX_WANT_OTU)) != 0;
-    c->h_hits.resize(need_hits ? nh : 0);
-    c->h_calls.resize(nc);
+    HIP_TRY(c->h_hits.resize(need_hits ? nh : 0));
+    HIP_TRY(c->h_calls.resize(nc));
     if ((need_hits && nh) || nc) {
         HIP_TRY(c->dense_hoff.reserve((n_seq + 1) * sizeof(uint64_t)));
         HIP_TRY(c->dense_coff.reserve((n_seq + 1) * sizeof(uint64_t)));
@@ -773,6 +800,7 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
 
+    tm.mark(" gather+d2h");
     /* OTU tallies: KmerOtuStats::otu_map over the hits the scorer flagged,
      * then finalize() (kguts.h:214-218: std::sort by count, descending) */
     c->h_ooff.assign(n_seq + 1, 0);
