@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts (streams) in flight")
+    ap.add_argument("--filter-log2", type=int, default=0,
+                    help="presence filter of 2^N bits (0 = none), kgx_image_set_filter")
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
@@ -122,6 +124,10 @@ def main():
         f"({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
     if args.image_layout == "aos":
         img.set_layout(abi.Image.AOS24)
+    if args.filter_log2:
+        t0 = time.time()
+        img.set_filter(args.filter_log2)
+        log(f"[bench] presence filter 2^{args.filter_log2} bits built in {time.time() - t0:.2f}s")
     layout = ["AOS24", "PACKED16"][img.layout]
     log(f"[bench] resident layout {layout}")
     ctx = abi.Context(img)
@@ -187,6 +193,7 @@ def main():
         ctx.set_option(name, vals[0])
         ctx.set_option("probe_variant", -1)
         ctx.set_option("probe_j", 4)
+        ctx.set_option("probe_filter", 1)
         probe_ab = {"option": name,
                     **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
                        for v, t in times.items()}}
@@ -312,6 +319,7 @@ def main():
                             f"signature image ({spec.num_sigs:,} buckets, "
                             f"{spec.num_sigs * 24 / 1e9:.1f} GB) resident in HBM",
                 "n_seq_per_gpu": n, "seq_len": Ls, "n_keys": n_keys, "keys_stored": stored,
+                "presence_filter_bits": (1 << args.filter_log2) if args.filter_log2 else 0,
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
                 "worker_contexts": len(ctxs),
                 "hits_total": total_hits,

@@ -110,6 +110,7 @@ SIGNATURES = {
     "kgx_image_table": (_P, [_P]),
     "kgx_image_layout": (_INT, [_P]),
     "kgx_image_set_layout": (_INT, [_P, _INT]),
+    "kgx_image_set_filter": (_INT, [_P, _INT]),
     "kgx_image_download": (_INT, [_P, _P, _U64]),
     "kgx_ctx_create": (_INT, [_P, _PP]),
     "kgx_ctx_destroy": (_INT, [_P]),
@@ -264,6 +265,9 @@ class Image:
                                     len(k), num_sigs, device, ctypes.byref(h), ctypes.byref(stored)),
               "kgx_image_build")
         return cls(h.value), stored.value
+
+    def set_filter(self, log2_bits: int) -> None:
+        check(lib().kgx_image_set_filter(self.handle, log2_bits), "kgx_image_set_filter")
 
     def save(self, data_dir: str) -> None:
         check(lib().kgx_image_save(self.handle, data_dir.encode()), "kgx_image_save")

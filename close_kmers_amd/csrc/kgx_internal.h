@@ -96,6 +96,27 @@ __host__ __device__ inline kgx_sig_kmer unpack_bucket(const packed_bucket &b)
     return e;
 }
 
+/*
+ * Optional presence filter of an image: 2^log2_bits bits in 64-bit words;
+ * each stored key (<= 20^8) sets two bits of one word (a blocked Bloom
+ * filter, hash independent of the slot hash).  A key whose two bits are not
+ * both set is stored nowhere, so its probe would end at a stop bucket: the
+ * probe skips the table for it.  No false negatives, so results never change.
+ */
+__host__ __device__ inline uint64_t filter_hash(uint64_t key)
+{
+    uint64_t h = key * 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 29);
+}
+__host__ __device__ inline uint64_t filter_word(uint64_t h, uint32_t log2_words)
+{
+    return log2_words ? h >> (64 - log2_words) : 0;
+}
+__host__ __device__ inline uint64_t filter_bits(uint64_t h)
+{
+    return (1ull << (h & 63)) | (1ull << ((h >> 6) & 63));
+}
+
 /* floor((2^64-1)/n): x % n = x - umulhi(x, m)*n, corrected once (x < 2^35). */
 inline uint64_t mod_magic(uint64_t n) { return n ? (~0ULL) / n : 0; }
 
@@ -108,8 +129,12 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase,
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
+                        const uint64_t *filter, uint32_t filter_log2_words,
                         kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream);
+/* set the filter bits of every stored key of the resident table */
+hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
+                               uint32_t log2_words, hipStream_t stream);
 /* AoS -> packed; *not_packable |= 1 when some stored bucket does not fit */
 hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_t n,
                        uint32_t *not_packable, hipStream_t stream);

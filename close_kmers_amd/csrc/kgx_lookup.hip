@@ -152,11 +152,24 @@ __device__ __forceinline__ uint3 load_residues(uintptr_t ab, uintptr_t lo, uintp
  */
 constexpr int MODE_BUCKET = 0, MODE_KEY_FIRST = 1, MODE_PACKED = 2, MODE_PACKED_KEY_FIRST = 3;
 
-template <int J, int MODE>
+/* a table record; NT = non-temporal (streaming) load, so the random
+ * table traffic need not displace a cache-resident presence filter */
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT> __device__ __forceinline__ uint4 load_record(const uint4 *p)
+{
+    if (NT) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
+
+template <int J, int MODE, bool FILTER, bool NT = FILTER>
 __global__ __launch_bounds__(256) void probe_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
     const void *__restrict__ table_v, uint64_t num_sigs, uint64_t magic,
+    const uint64_t *__restrict__ filter, uint32_t filter_log2,
     kgx_hit *__restrict__ hits, uint64_t *__restrict__ hit_mask)
 {
     constexpr bool KEY_FIRST = MODE == MODE_KEY_FIRST;
@@ -216,14 +229,24 @@ __global__ __launch_bounds__(256) void probe_kernel(
         const uint32_t ka = ((c0 * 20 + c1) * 20 + c2) * 20 + c3;
         const uint32_t kb = ((c4 * 20 + c5) * 20 + c6) * 20 + c7;
         key[j] = (uint64_t)ka * 160000u + kb;
-        slot[j] = ok ? mod_by(key[j], num_sigs, magic) : 0;
         pend[j] = ok;
         hit[j] = false;
         kv[j] = 0;
         pv[j] = make_uint4(0, 0, 0, 0);
+        if (FILTER && ok) /* presence filter word (MALL-resident): issue now, test below */
+            kv[j] = filter[filter_word(filter_hash(key[j]), filter_log2)];
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (FILTER && pend[j]) {
+            const uint64_t m = filter_bits(filter_hash(key[j]));
+            pend[j] = (kv[j] & m) == m; /* else stored nowhere: a miss */
+        }
+        const bool ok = pend[j];
+        slot[j] = ok ? mod_by(key[j], num_sigs, magic) : 0;
         if (ok) {
             if (MODE == MODE_PACKED) {
-                pv[j] = packed[slot[j]];
+                pv[j] = load_record<NT>(packed + slot[j]);
                 kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
             } else if (MODE == MODE_PACKED_KEY_FIRST) {
                 const uint64_t lo = packed_w[2 * slot[j]];
@@ -262,7 +285,7 @@ __global__ __launch_bounds__(256) void probe_kernel(
                 } else {
                     slot[j] = (slot[j] + 1 == num_sigs) ? 0 : slot[j] + 1;
                     if (MODE == MODE_PACKED) {
-                        pv[j] = packed[slot[j]];
+                        pv[j] = load_record<NT>(packed + slot[j]);
                         kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
                     } else if (MODE == MODE_PACKED_KEY_FIRST) {
                         const uint64_t lo = packed_w[2 * slot[j]];
@@ -307,34 +330,48 @@ __global__ __launch_bounds__(256) void probe_kernel(
     }
 }
 
+template <int J, int MODE>
+static void launch_probe_m(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
+                           const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
+                           uint32_t n_seq, const void *table, uint64_t num_sigs, const uint64_t *filter,
+                           uint32_t filter_log2, kgx_hit *hits, uint64_t *hit_mask)
+{
+    const uint64_t magic = mod_magic(num_sigs);
+    if (filter)
+        hipLaunchKernelGGL((probe_kernel<J, MODE, true>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
+                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
+                           filter_log2, hits, hit_mask);
+    else
+        hipLaunchKernelGGL((probe_kernel<J, MODE, false>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
+                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
+                           filter_log2, hits, hit_mask);
+}
+
 template <int J>
 static void launch_probe_j(dim3 grid, hipStream_t stream, int mode, const uint8_t *residues,
                            uint64_t n_residues, const uint64_t *seq_off, const uint64_t *wbase,
                            const uint32_t *tile_seq, uint32_t n_seq, const void *table,
-                           uint64_t num_sigs, kgx_hit *hits, uint64_t *hit_mask)
+                           uint64_t num_sigs, const uint64_t *filter, uint32_t filter_log2, kgx_hit *hits,
+                           uint64_t *hit_mask)
 {
-    const uint64_t magic = mod_magic(num_sigs);
+#define KGX_PROBE_M(M)                                                                               \
+    launch_probe_m<J, M>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table,  \
+                         num_sigs, filter, filter_log2, hits, hit_mask)
     if (mode == MODE_PACKED_KEY_FIRST)
-        hipLaunchKernelGGL((probe_kernel<J, MODE_PACKED_KEY_FIRST>), grid, dim3(64 * PROBE_WAVES), 0,
-                           stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table,
-                           num_sigs, magic, hits, hit_mask);
+        KGX_PROBE_M(MODE_PACKED_KEY_FIRST);
     else if (mode == MODE_PACKED)
-        hipLaunchKernelGGL((probe_kernel<J, MODE_PACKED>), grid, dim3(64 * PROBE_WAVES), 0, stream,
-                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
-                           magic, hits, hit_mask);
+        KGX_PROBE_M(MODE_PACKED);
     else if (mode == MODE_KEY_FIRST)
-        hipLaunchKernelGGL((probe_kernel<J, MODE_KEY_FIRST>), grid, dim3(64 * PROBE_WAVES), 0, stream,
-                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
-                           magic, hits, hit_mask);
+        KGX_PROBE_M(MODE_KEY_FIRST);
     else
-        hipLaunchKernelGGL((probe_kernel<J, MODE_BUCKET>), grid, dim3(64 * PROBE_WAVES), 0, stream,
-                           residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs,
-                           magic, hits, hit_mask);
+        KGX_PROBE_M(MODE_BUCKET);
+#undef KGX_PROBE_M
 }
 
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
+                        const uint64_t *filter, uint32_t filter_log2,
                         kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream)
 {
@@ -346,7 +383,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                                                    : (kf ? MODE_KEY_FIRST : MODE_BUCKET);
 #define KGX_PROBE_J(JJ)                                                                              \
     launch_probe_j<JJ>(grid, stream, mode, residues, n_residues, seq_off, wbase, tile_seq, n_seq,   \
-                       table, num_sigs, hits, hit_mask)
+                       table, num_sigs, filter, filter_log2, hits, hit_mask)
     switch (probe_j) {
     case 2: KGX_PROBE_J(2); break;
     case 4: KGX_PROBE_J(4); break;
@@ -383,6 +420,30 @@ __global__ __launch_bounds__(256) void unpack_kernel(const packed_bucket *__rest
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x)
         out[i] = unpack_bucket(packed[i]);
+}
+
+__global__ __launch_bounds__(256) void filter_build_kernel(const void *__restrict__ table, int layout, uint64_t n,
+                                                           uint64_t *__restrict__ filter, uint32_t log2_words)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = layout == KGX_LAYOUT_PACKED16
+                                 ? static_cast<const packed_bucket *>(table)[i].lo & PACK_KEY_MASK
+                                 : static_cast<const kgx_sig_kmer *>(table)[i].which_kmer;
+        if (key > MAX_ENCODED)
+            continue;
+        const uint64_t h = filter_hash(key);
+        atomicOr(reinterpret_cast<unsigned long long *>(filter + filter_word(h, log2_words)),
+                 (unsigned long long)filter_bits(h));
+    }
+}
+
+hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
+                               uint32_t log2_words, hipStream_t stream)
+{
+    hipLaunchKernelGGL(filter_build_kernel, dim3(8192), dim3(256), 0, stream, table, layout, num_sigs, filter,
+                       log2_words);
+    return hipGetLastError();
 }
 
 hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_t n,

@@ -124,6 +124,8 @@ struct kgx_image {
     int layout = KGX_LAYOUT_AOS24;
     kgx_sig_kmer *d_table = nullptr;   /* AOS24: the file's buckets */
     kgx::packed_bucket *d_packed = nullptr; /* PACKED16 */
+    uint64_t *d_filter = nullptr;           /* presence filter (kgx_image_set_filter) */
+    uint32_t filter_log2_words = 0;
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
@@ -154,6 +156,8 @@ struct kgx_ctx {
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
+    int probe_filter = 1; /* use the image's presence filter when it has one */
+    uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
     kgx::PinnedVec<kgx_hit> h_hits;

@@ -435,6 +435,8 @@ int kgx_image_close(kgx_image *img)
         (void)hipFree(img->d_table);
     if (img->d_packed)
         (void)hipFree(img->d_packed);
+    if (img->d_filter)
+        (void)hipFree(img->d_filter);
     delete img;
     return KGX_OK;
 }
@@ -443,6 +445,32 @@ uint64_t kgx_image_num_sigs(const kgx_image *img) { return img ? img->num_sigs :
 int kgx_image_device(const kgx_image *img) { return img ? img->device : -1; }
 const void *kgx_image_table(const kgx_image *img) { return img ? img->d_table : nullptr; }
 int kgx_image_layout(const kgx_image *img) { return img ? img->layout : -1; }
+
+int kgx_image_set_filter(kgx_image *img, int log2_bits)
+{
+    if (!img || log2_bits < 0 || (log2_bits && (log2_bits < 12 || log2_bits > 40)))
+        return fail(KGX_EINVAL, "filter size: 0 (none) or 2^12 .. 2^40 bits");
+    HIP_TRY(hipSetDevice(img->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (img->d_filter)
+        (void)hipFree(img->d_filter);
+    img->d_filter = nullptr;
+    img->filter_log2_words = 0;
+    if (!log2_bits)
+        return KGX_OK;
+    const uint32_t lw = (uint32_t)log2_bits - 6;
+    const uint64_t bytes = 8ull << lw;
+    if (hipMalloc(&img->d_filter, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        img->d_filter = nullptr;
+        return fail(KGX_ENOMEM, "no room for the filter");
+    }
+    HIP_TRY(hipMemset(img->d_filter, 0, bytes));
+    HIP_TRY(launch_filter_build(img->resident(), img->layout, img->num_sigs, img->d_filter, lw, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    img->filter_log2_words = lw;
+    return KGX_OK;
+}
 
 int kgx_image_set_layout(kgx_image *img, int layout)
 {
@@ -571,6 +599,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
     if (!c || !name)
         return fail(KGX_EINVAL, "null argument");
     const std::string n = name;
+    if (n == "microbench_span") {
+        if (value < 0)
+            return fail(KGX_EINVAL, "microbench_span must be >= 0");
+        c->microbench_span = (uint64_t)value;
+        return KGX_OK;
+    }
+    if (n == "probe_filter") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "probe_filter must be 0 or 1");
+        c->probe_filter = (int)value;
+        return KGX_OK;
+    }
     if (n == "probe_variant") {
         if (value != PROBE_AUTO && value != PROBE_BUCKET && value != PROBE_KEY_FIRST)
             return fail(KGX_EINVAL, "probe_variant must be -1, 0 or 1");
@@ -636,7 +676,8 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
         return fail(KGX_ERANGE, "image too large");
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
                          c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
-                         c->img->layout, c->img->num_sigs, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
+                         c->img->layout, c->img->num_sigs,
+                         c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
                          (int)(c->tile_windows / 64), c->probe_variant, c->stream));
     c->have_hits = true;
     return KGX_OK;
@@ -864,7 +905,9 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     HIP_TRY(hipEventCreate(&a));
     HIP_TRY(hipEventCreate(&b));
     HIP_TRY(hipEventRecord(a, c->stream));
-    HIP_TRY(launch_random_read(c->img->resident(), c->img->resident_bytes(), threads, rounds, mode,
+    const uint64_t span = c->microbench_span ? std::min(c->microbench_span, c->img->resident_bytes())
+                                             : c->img->resident_bytes();
+    HIP_TRY(launch_random_read(c->img->resident(), span, threads, rounds, mode,
                                c->plan_ws.as<uint64_t>(), c->stream));
     HIP_TRY(hipEventRecord(b, c->stream));
     HIP_TRY(hipEventSynchronize(b));

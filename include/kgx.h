@@ -193,6 +193,14 @@ int kgx_image_layout(const kgx_image *img);
 /* convert the resident table in place; KGX_ERANGE if PACKED16 is asked for
  * an image whose payloads do not fit (the image is left unchanged) */
 int kgx_image_set_layout(kgx_image *img, int layout);
+/* Presence filter: 2^log2_bits bits (0 removes it), two bits per stored key
+ * in one 64-bit word (blocked Bloom filter).  A probe whose key misses the
+ * filter skips the table -- exactly the miss it would have found -- so
+ * results never change; a filter small enough to stay in the 256 MiB
+ * Infinity Cache turns most misses' DRAM reads into cache reads.  It
+ * depends on the key set only (layout changes keep it); contexts use it
+ * unless "probe_filter" is 0. */
+int kgx_image_set_filter(kgx_image *img, int log2_bits);
 /* device pointer to the num_sigs * 24-byte table; NULL while PACKED16 */
 const void *kgx_image_table(const kgx_image *img);
 /* copy the table as the file's num_sigs * 24-byte buckets to host memory
@@ -209,6 +217,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * payload of every bucket examined, 1 = keys first (the 8-byte key, or the
  * packed record's low word), payload of the matching bucket only; -1 =
  * the faster one for the image's layout (default: 0 for PACKED16, 1 for AOS24);
+ * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
+ * "microbench_span" = bytes of the table kgx_microbench_random_read covers
+ * (0 = all);
  * "probe_j" = windows per lane (2, 4, 5 or 8; a tile
  * is 64 * probe_j windows), read at the next plan */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);

@@ -488,3 +488,19 @@ def test_image_build_from_entries_and_save(gpu, oracle_lib, tmp_path):
         assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, len(recs))
     with pytest.raises(Exception):
         gpu.Image.build(k, f, o, a, w, 2 * len(k))  # half full
+
+
+@pytest.mark.parametrize("log2_bits", [12, 16, 22])
+def test_presence_filter_keeps_results(small_world, oracle_lib, gpu, log2_bits):
+    """A probe gated by the presence filter gives the unfiltered results,
+    from a tiny saturated filter (every key passes) to a sparse one."""
+    spec, table, _, _ = small_world
+    res, off = synth.make_queries(spec, 400, x_permille=5, q0=77)
+    want = oracle_lib.process_batch(table, res, off)
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        img.set_filter(log2_bits)
+        for variant in (-1, 0, 1):
+            ctx.set_option("probe_variant", variant)
+            assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, 400)
+        img.set_layout(gpu.Image.AOS24)  # the filter depends on the keys only
+        assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, 400)
