@@ -11,8 +11,10 @@
  * batch of protein sequences, in (read, frame, position) order -- the order
  * the handler visits them -- with their read index and frame.
  *
- * One thread per (read, frame); two launches (count, then emit at the
- * scanned bases).
+ * Launches: count (one thread per (read, frame): fragments and residues),
+ * scans, emit (the same threads write each fragment's offset, read, frame
+ * and first codon at the scanned bases), fill (one wave per fragment writes
+ * its residues, consecutive lanes on consecutive bytes).
  */
 #include <hipcub/hipcub.hpp>
 
@@ -101,9 +103,10 @@ __global__ void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off, 
     n_res[g] = res;
 }
 
+/* fragment records (offset, read, frame, first codon); residues by fq_fill */
 __global__ void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off, uint32_t n_reads,
-                               const uint32_t *frag_base, const uint64_t *res_base, uint8_t *out_res,
-                               uint64_t *out_off, uint32_t *out_read, int8_t *out_frame)
+                               const uint32_t *frag_base, const uint64_t *res_base, uint64_t *out_off,
+                               uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
 {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (uint64_t)n_reads * 6)
@@ -120,8 +123,7 @@ __global__ void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off, u
                 out_off[fi] = ri;
                 out_read[fi] = r;
                 out_frame[fi] = (int8_t)fr.frame;
-                for (uint64_t j = 0; j < run; j++)
-                    out_res[ri + j] = (uint8_t)fr.aa(start + j);
+                out_start[fi] = (uint32_t)start;
                 fi++;
                 ri += run;
             }
@@ -130,6 +132,23 @@ __global__ void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off, u
         } else {
             run++;
         }
+    }
+}
+
+/* one wave per fragment (grid-stride): consecutive lanes write consecutive
+ * residues, so the byte stores coalesce */
+__global__ __launch_bounds__(256) void fq_fill_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                      uint32_t n_frag, const uint64_t *off, const uint32_t *rd,
+                                                      const int8_t *frm, const uint32_t *start, uint8_t *out_res)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t f = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); f < n_frag; f += waves) {
+        const uint32_t r = rd[f];
+        const FrameReader fr{bases + read_off[r], read_off[r + 1] - read_off[r], frm[f]};
+        const uint64_t o = off[f], len = off[f + 1] - o, s = start[f];
+        for (uint64_t k = lane; k < len; k += 64)
+            out_res[o + k] = (uint8_t)fr.aa(s + k);
     }
 }
 
@@ -176,11 +195,17 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     HIP_TRY(c->fq_off.reserve(((uint64_t)nf + 1) * 8));
     HIP_TRY(c->fq_read.reserve(((uint64_t)nf + 1) * 4));
     HIP_TRY(c->fq_frame.reserve((uint64_t)nf + 1));
+    HIP_TRY(c->fq_start.reserve(((uint64_t)nf + 1) * 4));
     hipLaunchKernelGGL(fq_emit_kernel, grid_for(n_rf), dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                       c->fq_fbase.as<uint32_t>(), c->fq_rbase.as<uint64_t>(), c->fq_res.as<uint8_t>(),
-                       c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>());
+                       c->fq_fbase.as<uint32_t>(), c->fq_rbase.as<uint64_t>(), c->fq_off.as<uint64_t>(),
+                       c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>());
     hipLaunchKernelGGL(fq_close_kernel, dim3(1), dim3(1), 0, st, c->fq_fbase.as<uint32_t>(),
                        c->fq_rbase.as<uint64_t>(), n_rf, c->fq_off.as<uint64_t>());
+    if (nf)
+        hipLaunchKernelGGL(fq_fill_kernel, dim3((uint32_t)std::min<uint64_t>(((uint64_t)nf + 3) / 4, 65536)),
+                           dim3(256), 0, st, d_bases, d_read_off, nf, c->fq_off.as<uint64_t>(),
+                           c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>(),
+                           c->fq_res.as<uint8_t>());
     HIP_TRY(hipGetLastError());
     out->n_reads = n_reads;
     out->n_fragments = nf;

@@ -152,7 +152,7 @@ struct kgx_ctx {
     bool have_hits = false; /* the tiled hits of the current plan are on the device */
     /* fq fragments (kgx_fq.hip) */
     kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_nres, fq_fbase, fq_rbase, fq_tmp, fq_res, fq_off, fq_read,
-        fq_frame;
+        fq_frame, fq_start;
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
