@@ -150,7 +150,7 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
                          hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
-                              uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream);
+                              uint32_t rounds, int mode, int ilp, uint64_t *sink, hipStream_t stream);
 hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
                               unsigned long long *n_stored, hipStream_t stream);
 hipError_t launch_entries_image(kgx_sig_kmer *table, uint64_t num_sigs, const uint64_t *keys,

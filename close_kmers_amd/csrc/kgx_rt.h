@@ -158,6 +158,8 @@ struct kgx_ctx {
     int probe_j = kgx::PROBE_J_DEFAULT;
     int probe_filter = 1; /* use the image's presence filter when it has one */
     uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */
+    int microbench_ilp = 8;       /* independent reads in flight per lane */
+    int microbench_wgs = 8;       /* 256-thread workgroups per CU */
     /* host results */
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
     kgx::PinnedVec<kgx_hit> h_hits;

@@ -599,6 +599,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
     if (!c || !name)
         return fail(KGX_EINVAL, "null argument");
     const std::string n = name;
+    if (n == "microbench_ilp") {
+        if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+            return fail(KGX_EINVAL, "microbench_ilp must be 1, 2, 4, 8 or 16");
+        c->microbench_ilp = (int)value;
+        return KGX_OK;
+    }
+    if (n == "microbench_wgs") {
+        if (value < 1 || value > 32)
+            return fail(KGX_EINVAL, "microbench_wgs must be 1..32");
+        c->microbench_wgs = (int)value;
+        return KGX_OK;
+    }
     if (n == "microbench_span") {
         if (value < 0)
             return fail(KGX_EINVAL, "microbench_span must be >= 0");
@@ -898,8 +910,9 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     if (!c || !ms || mode < 0 || mode > 3)
         return fail(KGX_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(c->img->device));
-    const uint64_t threads = 256ull * 256 * 8; /* 8 workgroups of 256 per CU */
-    const uint32_t rounds = (uint32_t)std::max<uint64_t>(1, n_reads / (threads * 8));
+    const uint64_t threads = 256ull * 256 * (uint64_t)c->microbench_wgs; /* workgroups of 256 per CU */
+    const int ilp = c->microbench_ilp;
+    const uint32_t rounds = (uint32_t)std::max<uint64_t>(1, n_reads / (threads * (uint64_t)ilp));
     HIP_TRY(c->plan_ws.reserve(threads * sizeof(uint64_t)));
     hipEvent_t a, b;
     HIP_TRY(hipEventCreate(&a));
@@ -907,7 +920,7 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     HIP_TRY(hipEventRecord(a, c->stream));
     const uint64_t span = c->microbench_span ? std::min(c->microbench_span, c->img->resident_bytes())
                                              : c->img->resident_bytes();
-    HIP_TRY(launch_random_read(c->img->resident(), span, threads, rounds, mode,
+    HIP_TRY(launch_random_read(c->img->resident(), span, threads, rounds, mode, ilp,
                                c->plan_ws.as<uint64_t>(), c->stream));
     HIP_TRY(hipEventRecord(b, c->stream));
     HIP_TRY(hipEventSynchronize(b));
@@ -915,7 +928,7 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     if (reads)
-        *reads = threads * rounds * 8;
+        *reads = threads * rounds * (uint64_t)ilp;
     return KGX_OK;
 }
 

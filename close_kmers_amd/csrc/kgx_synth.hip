@@ -21,11 +21,10 @@ namespace kgx {
  * + 16-byte payload, as the AOS24 probe does), mode 1 the 8-byte key of a
  * 24-byte bucket, mode 2 one aligned 64-byte sector, mode 3 one aligned
  * 16-byte record (as the PACKED16 probe does). */
-constexpr int RR_ILP = 8;
 
 __host__ __device__ constexpr uint64_t rr_stride(int mode) { return mode == 2 ? 64 : mode == 3 ? 16 : 24; }
 
-template <int MODE>
+template <int MODE, int RR_ILP>
 __global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict__ base, uint64_t n,
                                                           uint64_t magic, uint32_t rounds,
                                                           uint64_t *sink)
@@ -71,17 +70,30 @@ __global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict
     sink[tid] = acc;
 }
 
-hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
-                              uint32_t rounds, int mode, uint64_t *sink, hipStream_t stream)
+template <int MODE>
+static void launch_rr_mode(dim3 grid, dim3 block, hipStream_t stream, const char *b, uint64_t n, uint64_t m,
+                           uint32_t rounds, int ilp, uint64_t *sink)
+{
+    switch (ilp) {
+    case 1: hipLaunchKernelGGL((random_read_kernel<MODE, 1>), grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 2: hipLaunchKernelGGL((random_read_kernel<MODE, 2>), grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 4: hipLaunchKernelGGL((random_read_kernel<MODE, 4>), grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 16: hipLaunchKernelGGL((random_read_kernel<MODE, 16>), grid, block, 0, stream, b, n, m, rounds, sink); break;
+    default: hipLaunchKernelGGL((random_read_kernel<MODE, 8>), grid, block, 0, stream, b, n, m, rounds, sink); break;
+    }
+}
+
+hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads, uint32_t rounds, int mode,
+                              int ilp, uint64_t *sink, hipStream_t stream)
 {
     const dim3 grid((uint32_t)(threads / 256)), block(256);
     const char *b = static_cast<const char *>(buffer);
     const uint64_t n = bytes / rr_stride(mode), m = mod_magic(n);
     switch (mode) {
-    case 0: hipLaunchKernelGGL(random_read_kernel<0>, grid, block, 0, stream, b, n, m, rounds, sink); break;
-    case 1: hipLaunchKernelGGL(random_read_kernel<1>, grid, block, 0, stream, b, n, m, rounds, sink); break;
-    case 2: hipLaunchKernelGGL(random_read_kernel<2>, grid, block, 0, stream, b, n, m, rounds, sink); break;
-    case 3: hipLaunchKernelGGL(random_read_kernel<3>, grid, block, 0, stream, b, n, m, rounds, sink); break;
+    case 0: launch_rr_mode<0>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
+    case 1: launch_rr_mode<1>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
+    case 2: launch_rr_mode<2>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
+    case 3: launch_rr_mode<3>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

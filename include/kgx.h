@@ -219,7 +219,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * the faster one for the image's layout (default: 0 for PACKED16, 1 for AOS24);
  * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
  * "microbench_span" = bytes of the table kgx_microbench_random_read covers
- * (0 = all);
+ * (0 = all), "microbench_ilp" (1, 2, 4, 8, 16) reads in flight per lane and
+ * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (2, 4, 5 or 8; a tile
  * is 64 * probe_j windows), read at the next plan */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
