@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box pass (run through gpurun from the repo root):
+#   bash tools/gpu_check.sh TAG [quick]
+# 1. the -m gpu test suite   2. bench.py (C2)   3. C3 /matrix   4. C4 fq
+# "quick" skips the CPU baselines.  Output in gpurun_out/TAG; every GPU step
+# has its own time limit and the script stops at the first failure.
+set -euo pipefail
+TAG=${1:-check}
+QUICK=${2:-}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$R"
+NOCPU=""
+[ "$QUICK" = "quick" ] && NOCPU="--no-cpu-baseline"
+timeout -k 10 1500 python3 -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python3 bench.py $NOCPU > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python3 tools/bench_matrix.py $NOCPU > "$OUT/bench_matrix.json" 2> "$OUT/bench_matrix.err"
+timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
+echo "[gpu_check] done" >&2
