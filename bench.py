@@ -84,8 +84,8 @@ def spec_queries(spec, n, length, x_permille):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n-keys", type=float, default=1e9)
     ap.add_argument("--num-sigs", type=int, default=0, help="0 = builder sizing rule")
     ap.add_argument("--n-seq", type=int, default=100000, help="sequences per GPU")

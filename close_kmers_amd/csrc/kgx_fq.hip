@@ -11,10 +11,9 @@
  * batch of protein sequences, in (read, frame, position) order -- the order
  * the handler visits them -- with their read index and frame.
  *
- * Launches: count (one thread per (read, frame): fragments and residues),
- * scans, emit (the same threads write each fragment's offset, read, frame
- * and first codon at the scanned bases), fill (one wave per fragment writes
- * its residues, consecutive lanes on consecutive bytes).
+ * Launches: count (one wave per read: fragments and residues per frame),
+ * scans, emit (the same waves write each fragment's offset, read, frame and
+ * first codon, and the residues, at the scanned bases).
  */
 #include <hipcub/hipcub.hpp>
 
@@ -72,60 +71,68 @@ struct FrameReader {
 
 __device__ __forceinline__ int frame_of(uint32_t f) { return f < 3 ? (int)f + 1 : -(int)(f - 2); }
 
-__global__ void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off, uint32_t n_reads,
-                                uint32_t *n_frag, uint64_t *n_res)
+/*
+ * One wave per read.  When every frame of the read has at most 64 codons
+ * (reads up to 194 bases), lane k holds codon k of the frame: the stop mask
+ * is a ballot, each lane finds its run's ends with bit scans, and kept
+ * residues / run starts are counted and placed with popcounts, so the
+ * residue stores of a frame are one contiguous, coalesced stretch.  Longer
+ * reads take the serial path: lanes 0..5 walk one frame each.
+ */
+constexpr uint32_t WAVES_PER_WG = 4;
+constexpr uint64_t SHORT_READ = 3 * 64 + 2;
+
+struct FrameFragments { /* one frame's ballot view (lane k = codon k) */
+    uint64_t kept;   /* lanes whose residue is in a fragment */
+    uint64_t starts; /* lanes that start a fragment */
+    char aa;         /* this lane's residue */
+};
+
+__device__ __forceinline__ FrameFragments frame_fragments(const FrameReader &fr, uint32_t lane)
 {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (uint64_t)n_reads * 6) {
-        if (g == (uint64_t)n_reads * 6) {
-            n_frag[g] = 0;
-            n_res[g] = 0;
-        }
-        return;
-    }
-    const uint32_t r = (uint32_t)(g / 6), f = (uint32_t)(g % 6);
-    const FrameReader fr{bases + read_off[r], read_off[r + 1] - read_off[r], frame_of(f)};
     const uint64_t nc = fr.n_codons();
-    uint32_t frags = 0;
-    uint64_t res = 0, run = 0;
-    for (uint64_t k = 0; k <= nc; k++) {
-        if (k == nc || fr.aa(k) == '*') {
-            if (run >= MIN_FRAGMENT) {
-                frags++;
-                res += run;
-            }
-            run = 0;
-        } else {
-            run++;
-        }
-    }
-    n_frag[g] = frags;
-    n_res[g] = res;
+    const bool valid = lane < nc;
+    const char aa = valid ? fr.aa(lane) : '*';
+    const uint64_t stop = __ballot(aa == '*') | (nc >= 64 ? 0ull : ~0ull << nc);
+    const uint64_t below = lane ? stop & (~0ull >> (64 - lane)) : 0ull;
+    const uint32_t run_start = below ? 64u - (uint32_t)__builtin_clzll(below) : 0u; /* after the last stop below */
+    const uint64_t at_or_above = stop >> lane;
+    const uint32_t run_end = at_or_above ? lane + (uint32_t)__builtin_ctzll(at_or_above) : 64u; /* next stop */
+    const bool in_kept_run = valid && aa != '*' && run_end - run_start >= MIN_FRAGMENT;
+    FrameFragments r;
+    r.kept = __ballot(in_kept_run);
+    r.starts = __ballot(in_kept_run && lane == run_start);
+    r.aa = aa;
+    return r;
 }
 
-/* fragment records (offset, read, frame, first codon); residues by fq_fill */
-__global__ void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off, uint32_t n_reads,
-                               const uint32_t *frag_base, const uint64_t *res_base, uint64_t *out_off,
-                               uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
+__device__ __forceinline__ uint32_t popc_below(uint64_t m, uint32_t lane)
 {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (uint64_t)n_reads * 6)
-        return;
-    const uint32_t r = (uint32_t)(g / 6), f = (uint32_t)(g % 6);
-    const FrameReader fr{bases + read_off[r], read_off[r + 1] - read_off[r], frame_of(f)};
+    return lane ? (uint32_t)__popcll(m & (~0ull >> (64 - lane))) : 0u;
+}
+
+/* serial walk of one frame: (fragments, residues); emit when out_res != null */
+__device__ void frame_serial(const FrameReader &fr, uint32_t r, uint32_t fi, uint64_t ri, uint32_t &frags,
+                             uint64_t &res, uint8_t *out_res, uint64_t *out_off, uint32_t *out_read,
+                             int8_t *out_frame, uint32_t *out_start)
+{
     const uint64_t nc = fr.n_codons();
-    uint32_t fi = frag_base[g];
-    uint64_t ri = res_base[g];
     uint64_t run = 0, start = 0;
+    frags = 0;
+    res = 0;
     for (uint64_t k = 0; k <= nc; k++) {
         if (k == nc || fr.aa(k) == '*') {
             if (run >= MIN_FRAGMENT) {
-                out_off[fi] = ri;
-                out_read[fi] = r;
-                out_frame[fi] = (int8_t)fr.frame;
-                out_start[fi] = (uint32_t)start;
-                fi++;
-                ri += run;
+                if (out_res) {
+                    out_off[fi + frags] = ri + res;
+                    out_read[fi + frags] = r;
+                    out_frame[fi + frags] = (int8_t)fr.frame;
+                    out_start[fi + frags] = (uint32_t)start;
+                    for (uint64_t j = 0; j < run; j++)
+                        out_res[ri + res + j] = (uint8_t)fr.aa(start + j);
+                }
+                frags++;
+                res += run;
             }
             run = 0;
             start = k + 1;
@@ -135,20 +142,71 @@ __global__ void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off, u
     }
 }
 
-/* one wave per fragment (grid-stride): consecutive lanes write consecutive
- * residues, so the byte stores coalesce */
-__global__ __launch_bounds__(256) void fq_fill_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                      uint32_t n_frag, const uint64_t *off, const uint32_t *rd,
-                                                      const int8_t *frm, const uint32_t *start, uint8_t *out_res)
+__global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                       uint32_t n_reads, uint32_t *n_frag, uint64_t *n_res)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t f = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); f < n_frag; f += waves) {
-        const uint32_t r = rd[f];
-        const FrameReader fr{bases + read_off[r], read_off[r + 1] - read_off[r], frm[f]};
-        const uint64_t o = off[f], len = off[f + 1] - o, s = start[f];
-        for (uint64_t k = lane; k < len; k += 64)
-            out_res[o + k] = (uint8_t)fr.aa(s + k);
+    const uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
+    if (r == n_reads && lane == 0) {
+        n_frag[r * 6] = 0;
+        n_res[r * 6] = 0;
+    }
+    if (r >= n_reads)
+        return;
+    const uint8_t *b = bases + read_off[r];
+    const uint64_t len = read_off[r + 1] - read_off[r];
+    if (len <= SHORT_READ) {
+        for (uint32_t f = 0; f < 6; f++) {
+            const FrameFragments ff = frame_fragments(FrameReader{b, len, frame_of(f)}, lane);
+            if (lane == 0) {
+                n_frag[r * 6 + f] = (uint32_t)__popcll(ff.starts);
+                n_res[r * 6 + f] = (uint64_t)__popcll(ff.kept);
+            }
+        }
+    } else if (lane < 6) {
+        uint32_t frags;
+        uint64_t res;
+        frame_serial(FrameReader{b, len, frame_of(lane)}, (uint32_t)r, 0, 0, frags, res, nullptr, nullptr, nullptr,
+                     nullptr, nullptr);
+        n_frag[r * 6 + lane] = frags;
+        n_res[r * 6 + lane] = res;
+    }
+}
+
+/* fragment records (offset, read, frame, first codon) and residues */
+__global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                      uint32_t n_reads, const uint32_t *frag_base,
+                                                      const uint64_t *res_base, uint8_t *out_res, uint64_t *out_off,
+                                                      uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
+    if (r >= n_reads)
+        return;
+    const uint8_t *b = bases + read_off[r];
+    const uint64_t len = read_off[r + 1] - read_off[r];
+    if (len <= SHORT_READ) {
+        for (uint32_t f = 0; f < 6; f++) {
+            const FrameReader fr{b, len, frame_of(f)};
+            const FrameFragments ff = frame_fragments(fr, lane);
+            const uint64_t g = r * 6 + f;
+            const uint64_t ri = res_base[g] + popc_below(ff.kept, lane);
+            if ((ff.kept >> lane) & 1)
+                out_res[ri] = (uint8_t)ff.aa;
+            if ((ff.starts >> lane) & 1) {
+                const uint64_t fi = frag_base[g] + popc_below(ff.starts, lane);
+                out_off[fi] = ri;
+                out_read[fi] = (uint32_t)r;
+                out_frame[fi] = (int8_t)fr.frame;
+                out_start[fi] = lane;
+            }
+        }
+    } else if (lane < 6) {
+        const uint64_t g = r * 6 + lane;
+        uint32_t frags;
+        uint64_t res;
+        frame_serial(FrameReader{b, len, frame_of(lane)}, (uint32_t)r, frag_base[g], res_base[g], frags, res, out_res,
+                     out_off, out_read, out_frame, out_start);
     }
 }
 
@@ -174,8 +232,14 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     HIP_TRY(c->fq_nres.reserve((n_rf + 1) * 8));
     HIP_TRY(c->fq_fbase.reserve((n_rf + 1) * 4));
     HIP_TRY(c->fq_rbase.reserve((n_rf + 1) * 8));
-    hipLaunchKernelGGL(fq_count_kernel, grid_for(n_rf + 1), dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                       c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint64_t>());
+    const dim3 wgs((uint32_t)(n_reads / WAVES_PER_WG + 1)); /* one wave per read, +1 for the scan's tail */
+    if (n_reads)
+        hipLaunchKernelGGL(fq_count_kernel, wgs, dim3(256), 0, st, d_bases, d_read_off, n_reads,
+                           c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint64_t>());
+    else {
+        HIP_TRY(hipMemsetAsync(c->fq_nfrag.p, 0, 4, st));
+        HIP_TRY(hipMemsetAsync(c->fq_nres.p, 0, 8, st));
+    }
     size_t tb1 = 0, tb2 = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
                                              (int)(n_rf + 1), st));
@@ -196,16 +260,13 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     HIP_TRY(c->fq_read.reserve(((uint64_t)nf + 1) * 4));
     HIP_TRY(c->fq_frame.reserve((uint64_t)nf + 1));
     HIP_TRY(c->fq_start.reserve(((uint64_t)nf + 1) * 4));
-    hipLaunchKernelGGL(fq_emit_kernel, grid_for(n_rf), dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                       c->fq_fbase.as<uint32_t>(), c->fq_rbase.as<uint64_t>(), c->fq_off.as<uint64_t>(),
-                       c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>());
+    if (n_reads)
+        hipLaunchKernelGGL(fq_emit_kernel, wgs, dim3(256), 0, st, d_bases, d_read_off, n_reads,
+                           c->fq_fbase.as<uint32_t>(), c->fq_rbase.as<uint64_t>(), c->fq_res.as<uint8_t>(),
+                           c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(),
+                           c->fq_start.as<uint32_t>());
     hipLaunchKernelGGL(fq_close_kernel, dim3(1), dim3(1), 0, st, c->fq_fbase.as<uint32_t>(),
                        c->fq_rbase.as<uint64_t>(), n_rf, c->fq_off.as<uint64_t>());
-    if (nf)
-        hipLaunchKernelGGL(fq_fill_kernel, dim3((uint32_t)std::min<uint64_t>(((uint64_t)nf + 3) / 4, 65536)),
-                           dim3(256), 0, st, d_bases, d_read_off, nf, c->fq_off.as<uint64_t>(),
-                           c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>(),
-                           c->fq_res.as<uint8_t>());
     HIP_TRY(hipGetLastError());
     out->n_reads = n_reads;
     out->n_fragments = nf;

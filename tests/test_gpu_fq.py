@@ -102,3 +102,24 @@ def test_fq_handler_without_families_matches_oracle(gpu, oracle_lib):
     assert want.count(b"\n") > 20
     with gpu.Image.from_table(table) as img, gpu.FqHandler(img, os.path.join(d, "data")) as fq:
         assert fq.process(fastq, True) == want
+
+
+def test_fragments_of_long_and_empty_batches(gpu, oracle_lib):
+    """Workgroups whose reads or output overflow the LDS staging take the
+    global-memory path; an empty batch yields no fragments."""
+    spec, table = synthetic_table(20000)
+    rng = np.random.default_rng(8)
+    reads = [bytes(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(n))])
+             for n in [5000, 0, 120000, 3, 900] + [150] * 60]
+    res, off = pack([("r", r) for r in reads])
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        f = ctx.fq_fragments(res, off)
+        h = ctx.fragments_to_host(f)
+        empty = ctx.fq_fragments(np.zeros(0, np.uint8), np.zeros(1, np.uint64))
+        assert empty.n_fragments == 0 and empty.n_residues == 0
+    got = {}
+    for i in range(f.n_fragments):
+        s = bytes(h["residues"][int(h["offsets"][i]):int(h["offsets"][i + 1])]).decode()
+        got.setdefault(int(h["read"][i]), []).append((int(h["frame"][i]), s))
+    for r, dna in enumerate(reads):
+        assert got.get(r, []) == oracle_lib.fq_fragments(dna), r

@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--handler-reads", type=int, default=200_000)
     ap.add_argument("--cpu-reads", type=int, default=20_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=2, help="worker contexts alternating over chunks")
     args = ap.parse_args()
 
     from close_kmers_amd import abi, image_files, synth
@@ -56,6 +57,9 @@ def main():
     t0 = time.time()
     img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs)
     ctx = abi.Context(img)
+    # worker contexts (own stream + buffers), as for bench.py: one chunk's
+    # host-side sizing sync overlaps the other context's kernels
+    ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
     n, Lr = args.n_reads, args.length
     rng = np.random.default_rng(0x5EED0004)
     bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
@@ -71,25 +75,27 @@ def main():
     stats = {"fragments": 0, "residues": 0, "hits": 0, "calls": 0}
 
     def device_pass(collect_stats=False):
-        for c0 in range(0, n, chunk):
+        for i, c0 in enumerate(range(0, n, chunk)):
+            c = ctxs[i % len(ctxs)]
             m = min(chunk, n - c0)
             f = abi.Fragments()
-            abi.check(L.kgx_fq_fragments_device(ctx.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
+            abi.check(L.kgx_fq_fragments_device(c.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
                       "fq_fragments")
             dr = abi.DeviceResult()
-            abi.check(L.kgx_run_device(ctx.handle, ctypes.byref(params), f.residues, f.offsets, f.n_fragments,
+            abi.check(L.kgx_run_device(c.handle, ctypes.byref(params), f.residues, f.offsets, f.n_fragments,
                                        f.n_residues, abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
             if collect_stats:
                 hc = np.zeros(f.n_fragments, np.uint32)
                 cc = np.zeros(f.n_fragments, np.uint32)
-                ctx.synchronize()
+                c.synchronize()
                 abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, dr.hit_count, hc.nbytes), "d2h")
                 abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, dr.call_count, cc.nbytes), "d2h")
                 stats["fragments"] += f.n_fragments
                 stats["residues"] += f.n_residues
                 stats["hits"] += int(hc.sum())
                 stats["calls"] += int(cc.sum())
-        ctx.synchronize()
+        for c in ctxs:
+            c.synchronize()
 
     device_pass(collect_stats=True)
     times = []
@@ -116,7 +122,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),
@@ -139,7 +145,8 @@ def main():
     print(json.dumps(line), flush=True)
     L.kgx_device_free(d_bases)
     L.kgx_device_free(d_off)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     img.close()
 
 
