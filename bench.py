@@ -113,7 +113,9 @@ def main():
     d = shard.Dist()
     n_keys = int(args.n_keys)
     spec = synth.ImageSpec(n_keys, args.num_sigs or None)
-    dev = d.local_rank
+    # one GPU per rank; KGX_BENCH_DEVICE pins every rank to one device (a
+    # rehearsal of the multi-rank control flow on a 1-GPU box, small images)
+    dev = int(os.environ.get("KGX_BENCH_DEVICE", d.local_rank))
     L = abi.lib()
     if abi.device_count() <= dev:
         raise SystemExit(f"rank {d.rank}: no gfx950 device {dev}")
