@@ -1079,8 +1079,8 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     mark("lookup");
     /* fragments per (read, frame): fragment g of read r, frame slot k */
     std::vector<uint32_t> fcount((size_t)n_reads * 6);
-    kgx_ctx_synchronize(ctx);
-    kgx_memcpy_d2h(fcount.data(), fr.frame_counts, fcount.size() * 4);
+    if ((rc = kgx_ctx_synchronize(ctx)) || (rc = kgx_memcpy_d2h(fcount.data(), fr.frame_counts, fcount.size() * 4)))
+        throw_last(rc, "fragment counts");
     kgx_result res;
     rc = kgx_device_batch_collect(ctx, want, &res);
     if (rc)
@@ -1120,7 +1120,8 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     const bool all_offsets = called.size() > 1024;
     if (all_offsets) {
         frag_off.resize(fr.n_fragments + 1);
-        kgx_memcpy_d2h(frag_off.data(), fr.offsets, frag_off.size() * 8);
+        if ((rc = kgx_memcpy_d2h(frag_off.data(), fr.offsets, frag_off.size() * 8)))
+            throw_last(rc, "fragment offsets");
     }
     std::vector<uint64_t> slice;
     mark("family lists");
@@ -1176,7 +1177,8 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
             const uint64_t *offs = frag_off.data();
             if (!all_offsets) {
                 slice.resize(f1 - f0 + 1);
-                kgx_memcpy_d2h(slice.data(), fr.offsets + f0, slice.size() * 8);
+                if ((rc = kgx_memcpy_d2h(slice.data(), fr.offsets + f0, slice.size() * 8)))
+                    throw_last(rc, "fragment offsets");
                 offs = slice.data() - f0;
             }
             os << blk.ids[r] << "\t" << best_frame << "\t" << best_score << "\t";
