@@ -131,6 +131,8 @@ def main():
         img.set_filter(args.filter_log2)
         log(f"[bench] presence filter 2^{args.filter_log2} bits built in {time.time() - t0:.2f}s")
     layout = ["AOS24", "PACKED16"][img.layout]
+    # the default probe (probe_variant -1): cooperative lines for PACKED16 without a filter
+    probe_kernel = "probe_line_kernel" if layout == "PACKED16" and not args.filter_log2 else "probe_kernel"
     log(f"[bench] resident layout {layout}")
     ctx = abi.Context(img)
     n, Ls = args.n_seq, args.length
@@ -185,16 +187,18 @@ def main():
     if args.ab:
         # interleaved A/B of one tuning option in this process (one process,
         # alternating rounds, report the distribution); "name=v1,v2,..."
+        # several options at once: "probe_variant,probe_j=-1:4,2:4,3:2"
         name, vals = args.ab.split("=")
-        vals = [int(v) for v in vals.split(",")]
+        names = name.split(",")
+        vals = vals.split(",")
         times = {v: [] for v in vals}
         for _ in range(args.ab_rounds):
             for v in vals:
-                ctx.set_option(name, v)
+                for nm, x in zip(names, v.split(":")):
+                    ctx.set_option(nm, int(x))
                 step(times[v])
-        ctx.set_option(name, vals[0])
         ctx.set_option("probe_variant", -1)
-        ctx.set_option("probe_j", 4)
+        ctx.set_option("probe_j", 2)
         ctx.set_option("probe_filter", 1)
         probe_ab = {"option": name,
                     **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
@@ -255,7 +259,7 @@ def main():
         ceiling = {}
         n_reads = int(n * max(0, Ls - 8) * 1.4)
         for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64),
-                                   (3, "rec16", 16)):
+                                   (3, "rec16", 16), (4, "line64", 64)):
             ms, reads = ctypes.c_float(), ctypes.c_uint64()
             abi.check(L.kgx_microbench_random_read(ctx.handle, n_reads, mode, ctypes.byref(ms),
                                                    ctypes.byref(reads)), "microbench")  # warm
@@ -335,7 +339,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic,
-                "kernel": "probe_kernel",
+                "kernel": probe_kernel,
                 "kernel_ms": probe_s * 1e3,
                 "alg_bytes_per_launch": alg_bytes,
                 "pbar": pbar,
@@ -350,6 +354,11 @@ def main():
                     windows_per_launch * pbar / probe_s /
                     ceiling["rec16" if layout == "PACKED16" else "bucket24"]["reads_per_s"]
                     if ceiling else None),
+                # the line probe reads >= 1 64-B line per window: windows/s
+                # over the cooperative random-line ceiling (a lower bound)
+                "frac_of_random_line_ceiling": (
+                    windows_per_launch / probe_s / ceiling["line64"]["reads_per_s"]
+                    if ceiling and probe_kernel == "probe_line_kernel" else None),
             },
             "cpu_baseline": cpu,
             "host_path": host_path,

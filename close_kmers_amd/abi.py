@@ -53,7 +53,21 @@ class DeviceResult(ctypes.Structure):
     _fields_ = [("n_seq", ctypes.c_uint32), ("tile_windows", ctypes.c_uint32),
                 ("window_base", ctypes.c_void_p), ("hit_mask", ctypes.c_void_p),
                 ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
-                ("hits", ctypes.c_void_p), ("calls", ctypes.c_void_p)]
+                ("hits_hot", ctypes.c_void_p), ("hits_cold", ctypes.c_void_p),
+                ("calls", ctypes.c_void_p)]
+
+
+def hits_from_planes(hot: np.ndarray, cold: np.ndarray) -> np.ndarray:
+    """kgx_hit records from kgx_device_result's two hit planes (uint32 [n, 4]
+    each): hot = {avg | flags << 16, function_index, function_wt, pos},
+    cold = {which_kmer lo, hi, otu_index, seq}."""
+    hot = np.asarray(hot, np.uint32).reshape(-1, 4)
+    cold = np.asarray(cold, np.uint32).reshape(-1, 4)
+    w = np.empty((len(hot), 8), np.uint32)
+    w[:, 0:3] = cold[:, 0:3]
+    w[:, 3:7] = hot
+    w[:, 7] = cold[:, 3]
+    return w.view(HIT_DTYPE).reshape(-1)
 
 
 class Fragments(ctypes.Structure):

@@ -25,17 +25,25 @@ constexpr int RUN_CAP = 40000 - 2;               /* MAX_HITS_PER_SEQ - 2, kguts.
  * wbase = exclusive scan of max(0, len-8)).  The probe cuts this space into
  * tiles of probe_j * 64 windows -- across sequence boundaries, so short
  * sequences pack densely -- one tile per wave.  A tile's hits are stored
- * compacted, in window order, from hits[tile * tile_windows]; bit i of
- * hit_mask[g] says whether window 64 g + i hit.
+ * compacted, in window order, from slot tile * tile_windows; bit i of
+ * hit_mask[g] says whether window 64 g + i hit.  A slot is two 16-B records
+ * in two planes of one buffer: hot = {avg | flags << 16, fI, wt bits, pos}
+ * (everything the run scorer reads) and cold = {which_kmer lo, hi, otu, seq}.
  */
 constexpr int PROBE_WAVES = 4; /* waves per 256-thread workgroup */
 /* probe variants (kgx_ctx_set_option "probe_variant") */
 constexpr int PROBE_BUCKET = 0;    /* key + payload per bucket examined */
 constexpr int PROBE_KEY_FIRST = 1; /* keys only; payload for the matching bucket */
-/* default: whole 16-B record for PACKED16, key first for AOS24 (the faster
- * of the two on MI355X for each layout, interleaved A/B in bench.py) */
+/* default: cooperative 64-B lines (PROBE_LINE) for PACKED16 without a
+ * presence filter, whole 16-B records with one; key first for AOS24 (the
+ * fastest on MI355X for each case, interleaved A/B in bench.py,
+ * profiles/r1_probe_ab.json) */
 constexpr int PROBE_AUTO = -1;
-constexpr int PROBE_J_DEFAULT = 4;
+/* PACKED16 only, no presence filter: groups of 4 (8) lanes read one aligned
+ * 64-B (128-B) table line per instruction (probe_line_kernel) */
+constexpr int PROBE_LINE = 2;
+constexpr int PROBE_LINE8 = 3;
+constexpr int PROBE_J_DEFAULT = 2;
 
 /*
  * HBM-resident bucket layouts.  The file's 24-byte bucket (kmer_image.h:11-23)
@@ -120,7 +128,7 @@ __host__ __device__ inline uint64_t filter_bits(uint64_t h)
 /* floor((2^64-1)/n): x % n = x - umulhi(x, m)*n, corrected once (x < 2^35). */
 inline uint64_t mod_magic(uint64_t n) { return n ? (~0ULL) / n : 0; }
 
-inline bool probe_j_supported(int j) { return j == 2 || j == 4 || j == 5 || j == 8; }
+inline bool probe_j_supported(int j) { return (j >= 1 && j <= 5) || j == 8; }
 
 /* launchers; all asynchronous on `stream` */
 size_t plan_workspace_bytes(uint32_t n_seq);
@@ -130,7 +138,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2_words,
-                        kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
+                        uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream);
 /* set the filter bits of every stored key of the resident table */
 hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
@@ -141,11 +149,11 @@ hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_
 hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_t n,
                          hipStream_t stream);
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                        uint32_t tile_windows, kgx_hit *hits, kgx_call *calls, void *ranges,
+                        uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
                         uint32_t want, hipStream_t stream);
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                         uint32_t tile_windows, const uint32_t *call_count, const kgx_hit *hits,
+                         uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
                          hipStream_t stream);

@@ -164,13 +164,112 @@ template <bool NT> __device__ __forceinline__ uint4 load_record(const uint4 *p)
     return *p;
 }
 
+/* the J windows g0 + 64 j + lane of a tile: their keys (big-endian base-20
+ * codes, encoded_kmer kguts.cc:438-455), whether they are valid (inside the
+ * batch, no code-20 residue: advance_past_ambig), and their (seq, pos) */
+template <int J>
+__device__ __forceinline__ void encode_tile(const uint8_t *__restrict__ residues, uint64_t n_residues,
+                                            const uint64_t *__restrict__ seq_off,
+                                            const uint64_t *__restrict__ wbase, uint32_t s,
+                                            uint64_t W, uint64_t g0, uint32_t lane,
+                                            const uint8_t *code_tab, uint64_t *key, bool *ok,
+                                            uint32_t *pos, uint32_t *sq)
+{
+    const uintptr_t arr_lo = reinterpret_cast<uintptr_t>(residues);
+    const uintptr_t arr_hi = arr_lo + n_residues;
+    uint64_t wb_lo = wbase[s], wb_hi = wbase[s + 1], soff = seq_off[s];
+    uintptr_t ab[J];
+    uint32_t sh[J];
+    uint4 v[J];
+    bool fast[J];
+    /* pass 1: each window's sequence, and one 16-byte load of its residues,
+     * issued for all J windows before any is used (a window whose 16 bytes
+     * would leave the batch is read bytewise in pass 2).  Loads under a
+     * divergent branch stay in flight past the join only when the loaded
+     * variable holds nothing older to merge with -- here and in the probes,
+     * such variables are written once per round. */
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint64_t gw = g0 + 64 * j + lane;
+        const bool act = gw < W;
+        while (act && gw >= wb_hi) { /* next sequence (skips window-less ones) */
+            s++;
+            wb_lo = wb_hi;
+            wb_hi = wbase[s + 1];
+            soff = seq_off[s];
+        }
+        pos[j] = (uint32_t)(gw - wb_lo);
+        sq[j] = s;
+        const uintptr_t a = arr_lo + soff + (gw - wb_lo);
+        ab[j] = a & ~(uintptr_t)3;
+        sh[j] = (uint32_t)(a - ab[j]);
+        ok[j] = act;
+        fast[j] = ab[j] >= arr_lo && ab[j] + 16 <= arr_hi;
+        if (fast[j])
+            v[j] = *reinterpret_cast<const uint4 *>(ab[j]);
+    }
+    /* pass 2: codes and keys */
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        uint3 d = make_uint3(v[j].x, v[j].y, v[j].z);
+        if (!fast[j])
+            d = load_residues(ab[j], arr_lo, arr_hi);
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d.y, d.x, sh[j]);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d.z, d.y, sh[j]);
+        const uint32_t c0 = code_tab[lo & 0xFF], c1 = code_tab[(lo >> 8) & 0xFF],
+                       c2 = code_tab[(lo >> 16) & 0xFF], c3 = code_tab[lo >> 24];
+        const uint32_t c4 = code_tab[hi & 0xFF], c5 = code_tab[(hi >> 8) & 0xFF],
+                       c6 = code_tab[(hi >> 16) & 0xFF], c7 = code_tab[hi >> 24];
+        /* a code-20 residue anywhere kills the window (advance_past_ambig) */
+        const uint32_t cmax = max(max(max(c0, c1), max(c2, c3)), max(max(c4, c5), max(c6, c7)));
+        ok[j] = ok[j] && cmax < 20u;
+        /* big-endian base-20 Horner (encoded_kmer, kguts.cc:438-455) */
+        const uint32_t ka = ((c0 * 20 + c1) * 20 + c2) * 20 + c3;
+        const uint32_t kb = ((c4 * 20 + c5) * 20 + c6) * 20 + c7;
+        key[j] = (uint64_t)ka * 160000u + kb;
+    }
+}
+
+/* ordered compaction of a tile's hits into the two planes; one mask word
+ * per slice.  pv = the matching PACKED16 record (PACKED) or the 16 B after
+ * the key of the matching AOS24 bucket */
+template <int J, bool PACKED>
+__device__ __forceinline__ void store_tile_hits(const bool *hit, const uint64_t *kv, const uint4 *pv,
+                                                const uint32_t *pos, const uint32_t *sq, uint64_t g0,
+                                                uint64_t W, uint32_t lane, uint4 *__restrict__ hot,
+                                                uint4 *__restrict__ cold,
+                                                uint64_t *__restrict__ hit_mask)
+{
+    uint32_t count = 0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint64_t m = __ballot(hit[j]);
+        if (hit[j]) {
+            const uint64_t at = g0 + count + lanes_below(m);
+            if (PACKED) {
+                /* unpack_bucket (kgx_internal.h) of the record in pv */
+                const uint32_t otu = ((pv[j].y >> 23) & 0x1FFu) | (((pv[j].w >> 16) & 0xFFFu) << 9);
+                const uint32_t fi = (pv[j].y >> 3) & 0xFFFFFu;
+                hot[at] = make_uint4(pv[j].w & 0xFFFFu, fi - 1u, pv[j].z, pos[j]);
+                cold[at] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), otu - 1u, sq[j]);
+            } else {
+                hot[at] = make_uint4(pv[j].y & 0xFFFFu, pv[j].z, pv[j].w, pos[j]);
+                cold[at] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, sq[j]);
+            }
+        }
+        if (lane == 0 && g0 + 64 * j < W)
+            hit_mask[(g0 >> 6) + j] = m;
+        count += (uint32_t)__popcll(m);
+    }
+}
+
 template <int J, int MODE, bool FILTER, bool NT = FILTER>
 __global__ __launch_bounds__(256) void probe_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
     const void *__restrict__ table_v, uint64_t num_sigs, uint64_t magic,
     const uint64_t *__restrict__ filter, uint32_t filter_log2,
-    kgx_hit *__restrict__ hits, uint64_t *__restrict__ hit_mask)
+    uint4 *__restrict__ hot, uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask)
 {
     constexpr bool KEY_FIRST = MODE == MODE_KEY_FIRST;
     constexpr bool PACKED = MODE == MODE_PACKED || MODE == MODE_PACKED_KEY_FIRST;
@@ -190,114 +289,195 @@ __global__ __launch_bounds__(256) void probe_kernel(
     if (g0 >= W)
         return;
 
-    const uintptr_t arr_lo = reinterpret_cast<uintptr_t>(residues);
-    const uintptr_t arr_hi = arr_lo + n_residues;
-    uint32_t s = tile_seq[tile];
-    uint64_t wb_lo = wbase[s], wb_hi = wbase[s + 1], soff = seq_off[s];
-
-    uint64_t key[J], slot[J], kv[J];
-    uint4 pv[J];
+    uint64_t key[J], slot[J], fw[J];
     uint32_t pos[J], sq[J];
     bool pend[J], hit[J];
-
+    encode_tile<J>(residues, n_residues, seq_off, wbase, tile_seq[tile], W, g0, lane, code_tab, key,
+                   pend, pos, sq);
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        const uint64_t gw = g0 + 64 * j + lane;
-        const bool act = gw < W;
-        while (act && gw >= wb_hi) { /* next sequence (skips window-less ones) */
-            s++;
-            wb_lo = wb_hi;
-            wb_hi = wbase[s + 1];
-            soff = seq_off[s];
-        }
-        pos[j] = (uint32_t)(gw - wb_lo);
-        sq[j] = s;
-        const uintptr_t a = arr_lo + soff + (gw - wb_lo);
-        const uintptr_t ab = a & ~(uintptr_t)3;
-        const uint32_t sh = (uint32_t)(a - ab);
-        const uint3 d = load_residues(ab, arr_lo, arr_hi);
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d.y, d.x, sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d.z, d.y, sh);
-        const uint32_t c0 = code_tab[lo & 0xFF], c1 = code_tab[(lo >> 8) & 0xFF],
-                       c2 = code_tab[(lo >> 16) & 0xFF], c3 = code_tab[lo >> 24];
-        const uint32_t c4 = code_tab[hi & 0xFF], c5 = code_tab[(hi >> 8) & 0xFF],
-                       c6 = code_tab[(hi >> 16) & 0xFF], c7 = code_tab[hi >> 24];
-        /* a code-20 residue anywhere kills the window (advance_past_ambig) */
-        const uint32_t cmax = max(max(max(c0, c1), max(c2, c3)), max(max(c4, c5), max(c6, c7)));
-        const bool ok = act && cmax < 20u;
-        /* big-endian base-20 Horner (encoded_kmer, kguts.cc:438-455) */
-        const uint32_t ka = ((c0 * 20 + c1) * 20 + c2) * 20 + c3;
-        const uint32_t kb = ((c4 * 20 + c5) * 20 + c6) * 20 + c7;
-        key[j] = (uint64_t)ka * 160000u + kb;
-        pend[j] = ok;
         hit[j] = false;
-        kv[j] = 0;
-        pv[j] = make_uint4(0, 0, 0, 0);
-        if (FILTER && ok) /* presence filter word (MALL-resident): issue now, test below */
-            kv[j] = filter[filter_word(filter_hash(key[j]), filter_log2)];
+        fw[j] = 0;
+        if (FILTER && pend[j]) /* presence filter word (MALL-resident): issue now, test below */
+            fw[j] = filter[filter_word(filter_hash(key[j]), filter_log2)];
     }
 #pragma unroll
     for (int j = 0; j < J; j++) {
         if (FILTER && pend[j]) {
             const uint64_t m = filter_bits(filter_hash(key[j]));
-            pend[j] = (kv[j] & m) == m; /* else stored nowhere: a miss */
+            pend[j] = (fw[j] & m) == m; /* else stored nowhere: a miss */
         }
-        const bool ok = pend[j];
-        slot[j] = ok ? mod_by(key[j], num_sigs, magic) : 0;
-        if (ok) {
-            if (MODE == MODE_PACKED) {
-                pv[j] = load_record<NT>(packed + slot[j]);
-                kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
-            } else if (MODE == MODE_PACKED_KEY_FIRST) {
-                const uint64_t lo = packed_w[2 * slot[j]];
-                pv[j].x = (uint32_t)lo;
-                pv[j].y = (uint32_t)(lo >> 32);
-                kv[j] = lo & PACK_KEY_MASK;
-            } else {
-                const kgx_sig_kmer *e = table + slot[j];
-                kv[j] = e->which_kmer;
-                if (!KEY_FIRST)
-                    pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
-            }
-        }
+        slot[j] = pend[j] ? mod_by(key[j], num_sigs, magic) : 0;
     }
+
+    uint4 rec[J]; /* the matching bucket's payload */
+#pragma unroll
+    for (int j = 0; j < J; j++)
+        rec[j] = make_uint4(0, 0, 0, 0);
 
     /* linear probe rounds (lookup_hash_entry, kguts.cc:585-602); bounded by
      * num_sigs buckets where the reference would spin forever */
     for (uint64_t round = 0;; round++) {
-        bool more = false;
+        /* bucket slot[j] of every pending window, all J in flight at once */
+        uint4 pv[J];
+        uint64_t kv[J];
 #pragma unroll
         for (int j = 0; j < J; j++) {
             if (pend[j]) {
-                if (kv[j] == key[j]) {
-                    hit[j] = true;
-                    pend[j] = false;
-                    if (KEY_FIRST)
-                        pv[j] = *reinterpret_cast<const uint4 *>(
-                            reinterpret_cast<const char *>(table + slot[j]) + 8);
-                    if (MODE == MODE_PACKED_KEY_FIRST) {
-                        const uint64_t hi = packed_w[2 * slot[j] + 1];
-                        pv[j].z = (uint32_t)hi;
-                        pv[j].w = (uint32_t)(hi >> 32);
-                    }
-                } else if (kv[j] > MAX_ENCODED || round + 1 >= num_sigs) {
-                    pend[j] = false;
+                if (MODE == MODE_PACKED) {
+                    pv[j] = load_record<NT>(packed + slot[j]);
+                } else if (MODE == MODE_PACKED_KEY_FIRST) {
+                    const uint64_t lo = packed_w[2 * slot[j]];
+                    pv[j].x = (uint32_t)lo;
+                    pv[j].y = (uint32_t)(lo >> 32);
                 } else {
-                    slot[j] = (slot[j] + 1 == num_sigs) ? 0 : slot[j] + 1;
-                    if (MODE == MODE_PACKED) {
-                        pv[j] = load_record<NT>(packed + slot[j]);
-                        kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
-                    } else if (MODE == MODE_PACKED_KEY_FIRST) {
-                        const uint64_t lo = packed_w[2 * slot[j]];
-                        pv[j].x = (uint32_t)lo;
-                        pv[j].y = (uint32_t)(lo >> 32);
-                        kv[j] = lo & PACK_KEY_MASK;
-                    } else {
-                        const kgx_sig_kmer *e = table + slot[j];
-                        kv[j] = e->which_kmer;
-                        if (!KEY_FIRST)
-                            pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                    const kgx_sig_kmer *e = table + slot[j];
+                    kv[j] = e->which_kmer;
+                    if (!KEY_FIRST)
+                        pv[j] = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(e) + 8);
+                }
+            }
+        }
+        bool more = false;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (PACKED)
+                kv[j] = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
+            /* straight-line selects: a branch here would let the compiler
+             * split the record load and re-read its payload half on a match */
+            const bool m = pend[j] && kv[j] == key[j];
+            const bool stop = kv[j] > MAX_ENCODED || round + 1 >= num_sigs;
+            if (!KEY_FIRST && MODE != MODE_PACKED_KEY_FIRST) { /* per component: a select of */
+                rec[j].x = m ? pv[j].x : rec[j].x;               /* whole uint4s goes through */
+                rec[j].y = m ? pv[j].y : rec[j].y;               /* scratch memory */
+                rec[j].z = m ? pv[j].z : rec[j].z;
+                rec[j].w = m ? pv[j].w : rec[j].w;
+            }
+            if ((KEY_FIRST || MODE == MODE_PACKED_KEY_FIRST) && m) {
+                if (KEY_FIRST)
+                    rec[j] = *reinterpret_cast<const uint4 *>(
+                        reinterpret_cast<const char *>(table + slot[j]) + 8);
+                if (MODE == MODE_PACKED_KEY_FIRST) {
+                    const uint64_t hi = packed_w[2 * slot[j] + 1];
+                    rec[j] = make_uint4(pv[j].x, pv[j].y, (uint32_t)hi, (uint32_t)(hi >> 32));
+                }
+            }
+            hit[j] = hit[j] || m;
+            pend[j] = pend[j] && !m && !stop;
+            slot[j] = pend[j] ? (slot[j] + 1 == num_sigs ? 0 : slot[j] + 1) : slot[j];
+            more = more || pend[j];
+        }
+        if (!__any(more))
+            break;
+    }
+
+    store_tile_hits<J, PACKED>(hit, key, rec, pos, sq, g0, W, lane, hot, cold, hit_mask);
+}
+
+/*
+ * Cooperative-line probe of a PACKED16 image.  The encode and the ordered
+ * compaction are probe_kernel's; the lookups are done by groups of G lanes
+ * that read one aligned G*16-byte line of the table in one instruction (lane
+ * c of the group holds bucket line + c).  A wave instruction serves 64 / G
+ * windows, and a linear-probe chain costs one line request per line it
+ * touches instead of one request per bucket: about 1.07 requests per window
+ * instead of P-bar = 1.33 (the chip's ceiling is random line requests, and
+ * 64-B lines read this way run at 45 G/s, tools/line_probe.py).
+ *
+ * Window w of the tile (w = 64 j + l, owned by lane l in slice j) is looked
+ * up by group q = w % (64 / G) in instruction i = w / (64 / G).  The group
+ * examines buckets in probe order: from the home slot to the end of its line,
+ * then whole lines, wrapping at num_sigs; the first bucket whose key matches
+ * (hit) or exceeds MAX_ENCODED (miss) ends the chain -- lookup_hash_entry,
+ * kguts.cc:585-602.  A chain that has covered the whole table without either
+ * is a miss (the reference spins forever there; probe_kernel stops after
+ * num_sigs buckets -- same answer, since every bucket has been seen).
+ * The matching lane writes the record to LDS for the window's owner.
+ */
+template <int J, int G>
+__global__ __launch_bounds__(256) void probe_line_kernel(
+    const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
+    const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
+    const uint4 *__restrict__ packed, uint64_t num_sigs, uint64_t magic, uint4 *__restrict__ hot,
+    uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask)
+{
+    constexpr uint32_t T = 64 * J;
+    constexpr uint32_t NQ = 64 / G; /* windows per instruction */
+    constexpr int NI = J * G;       /* instructions per tile */
+    __shared__ uint8_t code_tab[256];
+    __shared__ uint4 lds_rec[PROBE_WAVES][T];
+    __shared__ uint8_t lds_hit[PROBE_WAVES][T];
+    code_tab[threadIdx.x] = (uint8_t)residue_code(threadIdx.x);
+    __syncthreads();
+
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    const uint64_t W = wbase[n_seq];
+    const uint64_t tile = (uint64_t)blockIdx.x * PROBE_WAVES + wave;
+    const uint64_t g0 = tile * T;
+    if (g0 >= W)
+        return;
+
+    uint64_t key[J];
+    uint32_t pos[J], sq[J];
+    bool ok[J];
+    encode_tile<J>(residues, n_residues, seq_off, wbase, tile_seq[tile], W, g0, lane, code_tab, key, ok,
+                   pos, sq);
+    uint64_t home[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        home[j] = ok[j] ? mod_by(key[j], num_sigs, magic) : 0;
+        lds_hit[wave][64 * j + lane] = 0;
+    }
+
+    const uint32_t q = lane / G, c = lane % G;
+    uint64_t K[NI], cur[NI];
+    uint32_t live = 0; /* bit i: instruction i's chain is still open */
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        const uint32_t owner = NQ * (i % G) + q; /* slice i / G */
+        K[i] = __shfl(key[i / G], (int)owner);
+        cur[i] = __shfl(home[i / G], (int)owner);
+        live |= (uint32_t)__shfl((int)ok[i / G], (int)owner) << i;
+    }
+    /* lines a chain may visit before it has covered the whole table */
+    const uint64_t max_lines = num_sigs / G + 2;
+    for (uint64_t round = 0;; round++) {
+        /* only open chains load; d is fresh each round (no merge with an
+         * older value at the branch join, so no wait for the load there) */
+        uint4 d[NI];
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const uint64_t line = cur[i] - cur[i] % G;
+            if ((live >> i & 1u) && line + c < num_sigs)
+                d[i] = packed[line + c];
+        }
+        bool more = false;
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const bool act = live >> i & 1u;
+            const uint64_t line = cur[i] - cur[i] % G;
+            const uint64_t b = line + c;
+            const uint64_t kb = ((uint64_t)d[i].y << 32 | d[i].x) & PACK_KEY_MASK;
+            const bool valid = act && b < num_sigs && b >= cur[i];
+            const uint64_t mm = __ballot(valid && kb == K[i]);
+            const uint64_t me = __ballot(valid && kb > MAX_ENCODED);
+            const uint32_t gm = (uint32_t)(mm >> (G * q)) & ((1u << G) - 1);
+            const uint32_t ge = (uint32_t)(me >> (G * q)) & ((1u << G) - 1);
+            if (act) {
+                const uint32_t ev = gm | ge;
+                if (ev) {
+                    const uint32_t first = __builtin_ctz(ev);
+                    if (c == first && (gm >> first & 1u)) {
+                        const uint32_t w = NQ * i + q;
+                        lds_rec[wave][w] = d[i];
+                        lds_hit[wave][w] = 1;
                     }
+                    live &= ~(1u << i);
+                } else if (round + 1 >= max_lines) {
+                    live &= ~(1u << i);
+                } else {
+                    cur[i] = line + G >= num_sigs ? 0 : line + G;
                     more = true;
                 }
             }
@@ -305,58 +485,58 @@ __global__ __launch_bounds__(256) void probe_kernel(
         if (!__any(more))
             break;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    /* ordered compaction of the tile's hits; one mask word per slice */
-    uint32_t count = 0;
+    bool hit[J];
+    uint4 pv[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        const uint64_t m = __ballot(hit[j]);
-        if (hit[j]) {
-            uint4 *d = reinterpret_cast<uint4 *>(hits + g0 + count + lanes_below(m));
-            if (PACKED) {
-                /* unpack_bucket (kgx_internal.h) of the record in pv */
-                const uint32_t otu = ((pv[j].y >> 23) & 0x1FFu) | (((pv[j].w >> 16) & 0xFFFu) << 9);
-                const uint32_t fi = (pv[j].y >> 3) & 0xFFFFFu;
-                d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), otu - 1u, pv[j].w & 0xFFFFu);
-                d[1] = make_uint4(fi - 1u, pv[j].z, pos[j], sq[j]);
-            } else {
-                d[0] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, pv[j].y & 0xFFFFu);
-                d[1] = make_uint4(pv[j].z, pv[j].w, pos[j], sq[j]);
-            }
-        }
-        if (lane == 0 && g0 + 64 * j < W)
-            hit_mask[(g0 >> 6) + j] = m;
-        count += (uint32_t)__popcll(m);
+        hit[j] = lds_hit[wave][64 * j + lane] != 0;
+        pv[j] = hit[j] ? lds_rec[wave][64 * j + lane] : make_uint4(0, 0, 0, 0);
     }
+    store_tile_hits<J, true>(hit, key, pv, pos, sq, g0, W, lane, hot, cold, hit_mask);
+}
+
+template <int J, int G>
+static void launch_probe_line(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
+                              const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
+                              uint32_t n_seq, const void *table, uint64_t num_sigs, uint4 *hot, uint4 *cold,
+                              uint64_t *hit_mask)
+{
+    hipLaunchKernelGGL((probe_line_kernel<J, G>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
+                       n_residues, seq_off, wbase, tile_seq, n_seq, static_cast<const uint4 *>(table),
+                       num_sigs, mod_magic(num_sigs), hot, cold, hit_mask);
 }
 
 template <int J, int MODE>
 static void launch_probe_m(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                            const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
                            uint32_t n_seq, const void *table, uint64_t num_sigs, const uint64_t *filter,
-                           uint32_t filter_log2, kgx_hit *hits, uint64_t *hit_mask)
+                           uint32_t filter_log2, uint4 *hot, uint4 *cold, uint64_t *hit_mask)
 {
     const uint64_t magic = mod_magic(num_sigs);
     if (filter)
         hipLaunchKernelGGL((probe_kernel<J, MODE, true>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
                            n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
-                           filter_log2, hits, hit_mask);
+                           filter_log2, hot, cold, hit_mask);
     else
         hipLaunchKernelGGL((probe_kernel<J, MODE, false>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
                            n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
-                           filter_log2, hits, hit_mask);
+                           filter_log2, hot, cold, hit_mask);
 }
 
 template <int J>
 static void launch_probe_j(dim3 grid, hipStream_t stream, int mode, const uint8_t *residues,
                            uint64_t n_residues, const uint64_t *seq_off, const uint64_t *wbase,
                            const uint32_t *tile_seq, uint32_t n_seq, const void *table,
-                           uint64_t num_sigs, const uint64_t *filter, uint32_t filter_log2, kgx_hit *hits,
-                           uint64_t *hit_mask)
+                           uint64_t num_sigs, const uint64_t *filter, uint32_t filter_log2, uint4 *hot,
+                           uint4 *cold, uint64_t *hit_mask)
 {
 #define KGX_PROBE_M(M)                                                                               \
     launch_probe_m<J, M>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table,  \
-                         num_sigs, filter, filter_log2, hits, hit_mask)
+                         num_sigs, filter, filter_log2, hot, cold, hit_mask)
     if (mode == MODE_PACKED_KEY_FIRST)
         KGX_PROBE_M(MODE_PACKED_KEY_FIRST);
     else if (mode == MODE_PACKED)
@@ -372,20 +552,41 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2,
-                        kgx_hit *hits, uint64_t *hit_mask, int probe_j, int variant,
+                        uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
                         hipStream_t stream)
 {
     if (max_tiles == 0)
         return hipSuccess;
     const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+    if (variant == PROBE_AUTO && layout == KGX_LAYOUT_PACKED16 && !filter)
+        variant = PROBE_LINE;
+    if ((variant == PROBE_LINE || variant == PROBE_LINE8) && layout == KGX_LAYOUT_PACKED16 && !filter) {
+#define KGX_LINE(JJ, GG)                                                                             \
+    launch_probe_line<JJ, GG>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
+                              num_sigs, hot, cold, hit_mask);                                        \
+    return hipGetLastError()
+        const int key = probe_j * 10 + (variant == PROBE_LINE8 ? 8 : 4);
+        switch (key) {
+        case 14: KGX_LINE(1, 4);
+        case 24: KGX_LINE(2, 4);
+        case 34: KGX_LINE(3, 4);
+        case 44: KGX_LINE(4, 4);
+        case 18: KGX_LINE(1, 8);
+        case 28: KGX_LINE(2, 8);
+        default: break; /* other tile sizes: the per-bucket kernel below */
+        }
+#undef KGX_LINE
+    }
     const bool kf = variant == PROBE_AUTO ? layout != KGX_LAYOUT_PACKED16 : variant == PROBE_KEY_FIRST;
     const int mode = layout == KGX_LAYOUT_PACKED16 ? (kf ? MODE_PACKED_KEY_FIRST : MODE_PACKED)
                                                    : (kf ? MODE_KEY_FIRST : MODE_BUCKET);
 #define KGX_PROBE_J(JJ)                                                                              \
     launch_probe_j<JJ>(grid, stream, mode, residues, n_residues, seq_off, wbase, tile_seq, n_seq,   \
-                       table, num_sigs, filter, filter_log2, hits, hit_mask)
+                       table, num_sigs, filter, filter_log2, hot, cold, hit_mask)
     switch (probe_j) {
+    case 1: KGX_PROBE_J(1); break;
     case 2: KGX_PROBE_J(2); break;
+    case 3: KGX_PROBE_J(3); break;
     case 4: KGX_PROBE_J(4); break;
     case 5: KGX_PROBE_J(5); break;
     case 8: KGX_PROBE_J(8); break;
@@ -483,12 +684,15 @@ __device__ __forceinline__ uint32_t for_each_run(const uint64_t *__restrict__ hi
     for (uint64_t g = tile * J; g < gfirst; g++)
         pre += (uint32_t)__popcll(hit_mask[g]);
     uint32_t ordinal = 0;
+    uint64_t next = hit_mask[gfirst];
     for (uint64_t g = gfirst; g <= glast; g++) {
         if (g != gfirst && g % J == 0) {
             tile = g / J;
             pre = 0;
         }
-        const uint64_t full = hit_mask[g];
+        const uint64_t full = next;
+        if (g < glast)
+            next = hit_mask[g + 1]; /* in flight while f works on word g */
         const uint32_t lo = g == gfirst ? (uint32_t)(gw0 & 63) : 0u;
         const uint32_t hi = g == glast ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
         const uint32_t cnt = (uint32_t)__popcll(full & bit_range(lo, hi));
@@ -535,7 +739,7 @@ constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << 16, F_CNT = KGX_HIT_COUNTED << 16,
 
 __global__ __launch_bounds__(256) void score_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
-    uint32_t tile_windows, kgx_hit *__restrict__ hits, kgx_call *__restrict__ calls,
+    uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
     uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
     kgx_params prm, uint32_t want)
 {
@@ -553,7 +757,7 @@ __global__ __launch_bounds__(256) void score_kernel(
         return;
     }
 
-    uint32_t *hw = reinterpret_cast<uint32_t *>(hits); /* 8 dwords per hit */
+    uint32_t *hw = reinterpret_cast<uint32_t *>(hot); /* 4 dwords per hit, flags in dword 0 */
     const uint64_t cbase = gw0; /* calls / ranges of s live at [gw0, ...) */
     const uint32_t gap = (uint32_t)prm.max_gap;
     int n = 0;
@@ -591,8 +795,8 @@ __global__ __launch_bounds__(256) void score_kernel(
             last_pos = p1.pos;
             last_idx = p1.idx;
             if (want_otu) {
-                hw[8 * p2.at + 3] = p2.avg | F_RUN | F_CNT;
-                hw[8 * p1.at + 3] = p1.avg | F_RUN | F_CNT;
+                hw[4 * p2.at] = p2.avg | F_RUN | F_CNT;
+                hw[4 * p1.at] = p1.avg | F_RUN | F_CNT;
             }
         } else {
             n = 0;
@@ -628,7 +832,7 @@ __global__ __launch_bounds__(256) void score_kernel(
                 n++;
                 const bool counted = fI == cur;
                 if (want_otu) /* flags only feed the OTU pass */
-                    hw[8 * at + 3] = avg | F_RUN | (counted ? F_CNT : 0u);
+                    hw[4 * at] = avg | F_RUN | (counted ? F_CNT : 0u);
                 if (counted) {
                     cnt++;
                     wsum += wt;
@@ -644,20 +848,34 @@ __global__ __launch_bounds__(256) void score_kernel(
         }
     };
 
-    /* hits are read SCORE_BATCH at a time, all loads issued before any is
-     * consumed: the state machine is serial, its inputs are not */
+    /* hits are read SCORE_BATCH at a time and double-buffered: batch b+1's
+     * loads are in flight while batch b runs through the state machine (the
+     * machine is serial, its inputs are not) */
+    auto load_batch = [&](uint4 *rb, uint64_t at0, uint32_t b, uint32_t c) {
+#pragma unroll
+        for (int k = 0; k < SCORE_BATCH; k++)
+            if (b + k < c) /* avg|flags, fI, wt, pos */
+                rb[k] = hot[at0 + b + k];
+    };
     const uint32_t nh = for_each_run(hit_mask, tile_windows, gw0, gw1,
                                      [&](uint64_t at0, uint32_t c, uint32_t ord0) {
-        for (uint32_t b = 0; b < c; b += SCORE_BATCH) {
-            uint4 rb[SCORE_BATCH];
-#pragma unroll
-            for (int k = 0; k < SCORE_BATCH; k++)
-                if (b + k < c) /* avg|flags, fI, wt, pos */
-                    rb[k] = *reinterpret_cast<const uint4 *>(hw + 8 * (at0 + b + k) + 3);
+        uint4 ra[SCORE_BATCH], rb[SCORE_BATCH];
+        load_batch(ra, at0, 0, c);
+        for (uint32_t b = 0; b < c; b += 2 * SCORE_BATCH) {
+            if (b + SCORE_BATCH < c)
+                load_batch(rb, at0, b + SCORE_BATCH, c);
 #pragma unroll
             for (int k = 0; k < SCORE_BATCH; k++)
                 if (b + k < c)
-                    step(rb[k], ord0 + b + k, at0 + b + k);
+                    step(ra[k], ord0 + b + k, at0 + b + k);
+            if (b + SCORE_BATCH >= c)
+                break;
+            if (b + 2 * SCORE_BATCH < c)
+                load_batch(ra, at0, b + 2 * SCORE_BATCH, c);
+#pragma unroll
+            for (int k = 0; k < SCORE_BATCH; k++)
+                if (b + SCORE_BATCH + k < c)
+                    step(rb[k], ord0 + b + SCORE_BATCH + k, at0 + b + SCORE_BATCH + k);
         }
     });
     if (n >= prm.min_hits) /* kguts.cc:873-876 */
@@ -679,9 +897,9 @@ __global__ __launch_bounds__(256) void score_kernel(
                 while (i > rg.y) /* i <= end keeps ci < ncalls */
                     rg = ranges[cbase + ++ci];
                 if (i >= rg.x) {
-                    const uint32_t f = hw[8 * (at0 + k) + 3];
+                    const uint32_t f = hw[4 * (at0 + k)];
                     if (f & F_CNT)
-                        hw[8 * (at0 + k) + 3] = f | F_OTU;
+                        hw[4 * (at0 + k)] = f | F_OTU;
                 }
             }
         });
@@ -689,14 +907,14 @@ __global__ __launch_bounds__(256) void score_kernel(
 }
 
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                        uint32_t tile_windows, kgx_hit *hits, kgx_call *calls, void *ranges,
+                        uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
                         uint32_t want, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     hipLaunchKernelGGL(score_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
-                       hit_mask, tile_windows, hits, calls, static_cast<uint2 *>(ranges), hit_count,
+                       hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
                        call_count, params, want);
     return hipGetLastError();
 }
@@ -707,8 +925,8 @@ hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *h
 
 __global__ __launch_bounds__(256) void gather_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
-    uint32_t tile_windows, const uint32_t *__restrict__ call_count, const kgx_hit *__restrict__ hits,
-    const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
+    uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
+    const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
     const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out)
 {
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -744,10 +962,12 @@ __global__ __launch_bounds__(256) void gather_kernel(
                     incl += x;
             }
             const uint64_t dst0 = hoff[s] + done + (incl - cnt);
-            const uint4 *src = reinterpret_cast<const uint4 *>(hits + at);
             uint4 *dst = reinterpret_cast<uint4 *>(hits_out + dst0);
-            for (uint32_t i = 0; i < 2 * cnt; i++)
-                dst[i] = src[i];
+            for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its two planes */
+                const uint4 h = hot[at + i], c = cold[at + i];
+                dst[2 * i] = make_uint4(c.x, c.y, c.z, h.x);
+                dst[2 * i + 1] = make_uint4(h.y, h.z, h.w, c.w);
+            }
             done += __shfl(incl, 63);
         }
     }
@@ -761,14 +981,14 @@ __global__ __launch_bounds__(256) void gather_kernel(
 }
 
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                         uint32_t tile_windows, const uint32_t *call_count, const kgx_hit *hits,
+                         uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
                          kgx_hit *hits_out, kgx_call *calls_out, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     hipLaunchKernelGGL(gather_kernel, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
-                       hit_mask, tile_windows, call_count, hits, calls, hoff, coff, hits_out,
+                       hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
                        calls_out);
     return hipGetLastError();
 }

@@ -148,6 +148,7 @@ struct kgx_ctx {
     uint64_t n_residues = 0;
     uint64_t max_tiles = 0;
     uint32_t tile_windows = 64u * kgx::PROBE_J_DEFAULT;
+    uint64_t hit_slots = 0; /* slots per hit plane: cold plane at hits + hit_slots */
     const uint64_t *d_off = nullptr;
     bool have_hits = false; /* the tiled hits of the current plan are on the device */
     /* fq fragments (kgx_fq.hip) */

@@ -624,14 +624,14 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         return KGX_OK;
     }
     if (n == "probe_variant") {
-        if (value != PROBE_AUTO && value != PROBE_BUCKET && value != PROBE_KEY_FIRST)
-            return fail(KGX_EINVAL, "probe_variant must be -1, 0 or 1");
+        if (value < PROBE_AUTO || value > PROBE_LINE8)
+            return fail(KGX_EINVAL, "probe_variant must be -1, 0, 1, 2 or 3");
         c->probe_variant = (int)value;
         return KGX_OK;
     }
     if (n == "probe_j") {
         if (!probe_j_supported((int)value))
-            return fail(KGX_EINVAL, "probe_j must be 2, 4, 5 or 8");
+            return fail(KGX_EINVAL, "probe_j must be 1, 2, 3, 4, 5 or 8");
         c->probe_j = (int)value;
         return KGX_OK;
     }
@@ -662,7 +662,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->wbase.reserve((n_seq + 1) * sizeof(uint64_t)));
     HIP_TRY(c->tile_seq.reserve(max_tiles * sizeof(uint32_t)));
     HIP_TRY(c->hit_mask.reserve((cap_win / 64 + 2) * sizeof(uint64_t)));
-    HIP_TRY(c->hits.reserve(cap_win * sizeof(kgx_hit)));
+    HIP_TRY(c->hits.reserve(cap_win * 2 * sizeof(uint4))); /* hot plane, then cold plane */
     HIP_TRY(c->calls.reserve(cap_win * sizeof(kgx_call)));
     HIP_TRY(c->ranges.reserve(cap_win * 2 * sizeof(uint32_t)));
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
@@ -674,6 +674,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     c->n_residues = n_residues;
     c->max_tiles = max_tiles;
     c->tile_windows = tile_windows;
+    c->hit_slots = cap_win;
     c->d_off = d_off;
     c->have_hits = false;
     return KGX_OK;
@@ -689,7 +690,8 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
                          c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
                          c->img->layout, c->img->num_sigs,
-                         c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words, c->hits.as<kgx_hit>(), c->hit_mask.as<uint64_t>(),
+                         c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
+                         c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
                          (int)(c->tile_windows / 64), c->probe_variant, c->stream));
     c->have_hits = true;
     return KGX_OK;
@@ -706,7 +708,7 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
         kgx_params_default(&p);
     HIP_TRY(hipSetDevice(c->img->device));
     HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(),
-                         c->tile_windows, c->hits.as<kgx_hit>(), c->calls.as<kgx_call>(),
+                         c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
                          want, c->stream));
     return KGX_OK;
@@ -722,7 +724,8 @@ int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
     out->hit_mask = c->hit_mask.as<uint64_t>();
     out->hit_count = c->hit_count.as<uint32_t>();
     out->call_count = c->call_count.as<uint32_t>();
-    out->hits = c->hits.as<kgx_hit>();
+    out->hits_hot = c->hits.as<uint32_t>();
+    out->hits_cold = c->hits.as<uint32_t>() + 4 * c->hit_slots;
     out->calls = c->calls.as<kgx_call>();
     return KGX_OK;
 }
@@ -839,7 +842,8 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
         HIP_TRY(hipMemcpyAsync(c->dense_coff.p, c->h_coff.data(), (n_seq + 1) * sizeof(uint64_t),
                                hipMemcpyHostToDevice, c->stream));
         HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
-                              c->call_count.as<uint32_t>(), c->hits.as<kgx_hit>(),
+                              c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
+                              c->hits.as<uint4>() + c->hit_slots,
                               c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
                               c->dense_coff.as<uint64_t>(),
                               need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
@@ -907,7 +911,7 @@ int kgx_synth_queries(kgx_ctx *c, uint64_t image_n_keys, uint32_t n_seq, uint32_
 
 int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms, uint64_t *reads)
 {
-    if (!c || !ms || mode < 0 || mode > 3)
+    if (!c || !ms || mode < 0 || mode > 5)
         return fail(KGX_EINVAL, "bad argument");
     HIP_TRY(hipSetDevice(c->img->device));
     const uint64_t threads = 256ull * 256 * (uint64_t)c->microbench_wgs; /* workgroups of 256 per CU */
@@ -928,7 +932,7 @@ int kgx_microbench_random_read(kgx_ctx *c, uint64_t n_reads, int mode, float *ms
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     if (reads)
-        *reads = threads * rounds * (uint64_t)ilp;
+        *reads = threads * rounds * (uint64_t)ilp / (mode == 4 ? 4 : mode == 5 ? 8 : 1);
     return KGX_OK;
 }
 

@@ -20,9 +20,15 @@ namespace kgx {
  * resident image buffer per round: mode 0 a whole 24-byte bucket (8-byte key
  * + 16-byte payload, as the AOS24 probe does), mode 1 the 8-byte key of a
  * 24-byte bucket, mode 2 one aligned 64-byte sector, mode 3 one aligned
- * 16-byte record (as the PACKED16 probe does). */
+ * 16-byte record (as the PACKED16 probe does).  Modes 4 and 5 read one
+ * random aligned 64-B (128-B) line per group of 4 (8) lanes, 16 B per lane in
+ * one instruction -- the cooperative line reads of the quad probe. */
 
-__host__ __device__ constexpr uint64_t rr_stride(int mode) { return mode == 2 ? 64 : mode == 3 ? 16 : 24; }
+__host__ __device__ constexpr uint64_t rr_stride(int mode)
+{
+    return mode == 2 || mode == 4 ? 64 : mode == 5 ? 128 : mode == 3 ? 16 : 24;
+}
+__host__ __device__ constexpr uint32_t rr_group(int mode) { return mode == 4 ? 4 : mode == 5 ? 8 : 1; }
 
 template <int MODE, int RR_ILP>
 __global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict__ base, uint64_t n,
@@ -30,7 +36,9 @@ __global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict
                                                           uint64_t *sink)
 {
     constexpr uint64_t S = rr_stride(MODE);
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr uint32_t G = rr_group(MODE);
+    const uint64_t tid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint32_t part = threadIdx.x % G;
     uint64_t acc = 0;
     for (uint32_t r = 0; r < rounds; r++) {
         uint64_t idx[RR_ILP];
@@ -53,21 +61,24 @@ __global__ __launch_bounds__(256) void random_read_kernel(const char *__restrict
                 pw[k] = q[1];
                 px[k] = q[2];
                 kv[k] = *reinterpret_cast<const uint64_t *>(q + 3);
-            } else {
+            } else if (MODE == 3) {
                 pv[k] = *reinterpret_cast<const uint4 *>(rec);
+                kv[k] = pv[k].y;
+            } else {
+                pv[k] = *reinterpret_cast<const uint4 *>(rec + 16 * part);
                 kv[k] = pv[k].y;
             }
         }
 #pragma unroll
         for (int k = 0; k < RR_ILP; k++) {
             acc ^= kv[k];
-            if (MODE == 0 || MODE == 3)
+            if (MODE == 0 || MODE >= 3)
                 acc += pv[k].x ^ pv[k].w;
             if (MODE == 2)
                 acc += pv[k].x ^ pw[k].y ^ px[k].z;
         }
     }
-    sink[tid] = acc;
+    sink[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
 template <int MODE>
@@ -94,6 +105,8 @@ hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threa
     case 1: launch_rr_mode<1>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
     case 2: launch_rr_mode<2>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
     case 3: launch_rr_mode<3>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
+    case 4: launch_rr_mode<4>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
+    case 5: launch_rr_mode<5>(grid, block, stream, b, n, m, rounds, ilp, sink); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

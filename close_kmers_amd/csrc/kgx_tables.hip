@@ -90,7 +90,7 @@ __device__ __forceinline__ bool kmap_row(const KmapView &m, uint64_t kmer, uint6
 
 /* the tiled device result of a context (kgx_device_result) */
 struct Tiled {
-    const kgx_hit *hits;
+    const uint4 *cold; /* {which_kmer lo, hi, otu, seq} per slot */
     const uint64_t *mask;
     const uint64_t *wbase;
     uint32_t n_seq;
@@ -130,10 +130,10 @@ __global__ void hits_to_pairs_kernel(Tiled t, uint64_t n_tiles, const uint32_t *
     const uint32_t i = (uint32_t)(slot % t.T);
     if (tile >= n_tiles || i >= tile_base[tile + 1] - tile_base[tile])
         return;
-    const kgx_hit &h = t.hits[tile * t.T + i];
+    const uint4 h = t.cold[tile * t.T + i];
     const uint64_t at = tile_base[tile] + i;
-    kmers[at] = h.which_kmer;
-    ids[at] = seq_ids[h.seq];
+    kmers[at] = (uint64_t)h.y << 32 | h.x;
+    ids[at] = seq_ids[h.w];
 }
 
 __global__ void expand_rows_kernel(const uint64_t *keys, const uint64_t *starts, uint64_t n_rows,
@@ -250,7 +250,8 @@ __global__ void matrix_events_kernel(Tiled t, uint64_t n_tiles, KmapView m, unsi
     uint64_t ev = 0;
     if (tile < n_tiles && i < tile_count(t, tile)) {
         uint64_t a = 0, b = 0;
-        if (kmap_row(m, t.hits[tile * t.T + i].which_kmer, a, b))
+        const uint4 h = t.cold[tile * t.T + i];
+        if (kmap_row(m, (uint64_t)h.y << 32 | h.x, a, b))
             ev = b - a;
     }
     /* one atomic per wave */
@@ -270,12 +271,12 @@ __global__ void matrix_pairs_kernel(Tiled t, uint64_t n_tiles, KmapView m, const
     const uint32_t i = (uint32_t)(slot % t.T);
     if (tile >= n_tiles || i >= tile_count(t, tile))
         return;
-    const kgx_hit &h = t.hits[tile * t.T + i];
+    const uint4 h = t.cold[tile * t.T + i];
     uint64_t a = 0, b = 0;
-    if (!kmap_row(m, h.which_kmer, a, b))
+    if (!kmap_row(m, (uint64_t)h.y << 32 | h.x, a, b))
         return; /* matrix_request.cc:159 reports "no mapping" on stderr */
-    const uint32_t e = seq_ids[h.seq];
-    const uint64_t my_ord = base + h.seq;
+    const uint32_t e = seq_ids[h.w];
+    const uint64_t my_ord = base + h.w;
     for (uint64_t j = a; j < b; j++) {
         const uint32_t f = m.vals[j];
         if (f == e)
@@ -472,7 +473,7 @@ int kmap_expand(kgx_kmap *m, DevBuf &d_k, DevBuf &d_v, uint64_t extra, hipStream
 Tiled tiled_of(const kgx_ctx *c)
 {
     Tiled t;
-    t.hits = c->hits.as<kgx_hit>();
+    t.cold = c->hits.as<uint4>() + c->hit_slots;
     t.mask = c->hit_mask.as<uint64_t>();
     t.wbase = c->wbase.as<uint64_t>();
     t.n_seq = c->n_seq;

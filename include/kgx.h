@@ -122,12 +122,15 @@ typedef struct kgx_result {
  * Windows are numbered across the batch: sequence s owns global windows
  * [window_base[s], window_base[s+1]) (position = global - window_base[s]).
  * The probe works in tiles of tile_windows consecutive windows; tile t's hits
- * are stored compacted in window order from hits[t * tile_windows], and bit i
+ * are stored compacted in window order from slot t * tile_windows, and bit i
  * of hit_mask[g] is set when global window 64*g + i hit.  So the hits of a
  * sequence are, word by word of its mask range, contiguous stretches of its
- * tiles' hit lists (each record also carries seq and pos).  Calls of s are
- * contiguous from calls[window_base[s]]; counts are hit_count[s] /
- * call_count[s]. */
+ * tiles' hit lists.  A hit is two 16-byte records at the same slot, in two
+ * planes, so that the run scorer reads only what it uses:
+ *   hits_hot[i]  = {avg_from_end | flags << 16, function_index, function_wt, pos}
+ *   hits_cold[i] = {which_kmer (low, high 32 bits), otu_index, seq}
+ * Calls of s are contiguous from calls[window_base[s]]; counts are
+ * hit_count[s] / call_count[s]. */
 typedef struct kgx_device_result {
     uint32_t n_seq;
     uint32_t tile_windows;
@@ -135,7 +138,8 @@ typedef struct kgx_device_result {
     const uint64_t *hit_mask;    /* ceil(window_base[n_seq] / 64) words */
     const uint32_t *hit_count;   /* n_seq */
     const uint32_t *call_count;  /* n_seq */
-    const kgx_hit *hits;         /* capacity window_base[n_seq] */
+    const uint32_t *hits_hot;    /* 4 words per slot, capacity window_base[n_seq] slots */
+    const uint32_t *hits_cold;   /* 4 words per slot */
     const kgx_call *calls;       /* capacity window_base[n_seq] */
 } kgx_device_result;
 
@@ -216,12 +220,16 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
 /* tuning knobs (results never change): "probe_variant" 0 = load key and
  * payload of every bucket examined, 1 = keys first (the 8-byte key, or the
  * packed record's low word), payload of the matching bucket only; -1 =
- * the faster one for the image's layout (default: 0 for PACKED16, 1 for AOS24);
+ * the fastest for the image (default: 2 for PACKED16, 0 for PACKED16 with a
+ * presence filter, 1 for AOS24);
+ * 2 / 3 = PACKED16 without a presence filter: groups of 4 / 8 lanes read one
+ * aligned 64-B / 128-B table line per instruction (probe_j 1-4 / 1-2; other
+ * combinations run variant 0);
  * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
  * "microbench_span" = bytes of the table kgx_microbench_random_read covers
  * (0 = all), "microbench_ilp" (1, 2, 4, 8, 16) reads in flight per lane and
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
- * "probe_j" = windows per lane (2, 4, 5 or 8; a tile
+ * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
@@ -272,8 +280,10 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
  * uniformly random records of the resident table read with many loads in
  * flight.  mode 0: a whole 24-byte bucket (key + payload, the AOS24 probe's
  * access), 1: the 8-byte key of a 24-byte bucket, 2: one aligned 64-byte
- * sector, 3: one aligned 16-byte record (the PACKED16 probe's access).  *ms = kernel time (HIP events),
- * *reads = buckets actually read. */
+ * sector, 3: one aligned 16-byte record (the PACKED16 probe's access),
+ * 4 / 5: one aligned 64-byte / 128-byte line read cooperatively by 4 / 8
+ * lanes, 16 B each, in one instruction.  *ms = kernel time (HIP events),
+ * *reads = records (modes 0-3) or lines (modes 4-5) actually read. */
 int kgx_microbench_random_read(kgx_ctx *ctx, uint64_t n_reads, int mode, float *ms,
                                uint64_t *reads);
 

@@ -39,12 +39,12 @@ def main():
     fdir, wdir, bjson = sys.argv[1:4]
     bench = json.loads(open(bjson).read().strip().splitlines()[-1])
     fetch, write = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
-    is_probe = lambda k: "probe_kernel" in k
+    is_probe = lambda k: "probe_kernel" in k or "probe_line_kernel" in k
     pf, nf = mean_of(fetch, is_probe)
     pw, nw = mean_of(write, is_probe)
     calib = {}
     ceil = (bench.get("roofline") or {}).get("random_read_ceiling") or {}
-    for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64"), (3, "rec16")):
+    for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64"), (3, "rec16"), (4, "line64")):
         b, n = mean_of(fetch, lambda k, m=mode: f"random_read_kernel<{m}>" in k)
         reads = (ceil.get(name) or {}).get("reads")
         if b is not None and reads:

@@ -9,7 +9,8 @@ import pytest
 
 from close_kmers_amd import build as kbuild
 from close_kmers_amd import image_files, synth
-from helpers import GOLDEN, DesignedImage, pack, random_protein, synthetic_table
+from close_kmers_amd.abi import SIG_DTYPE
+from helpers import ALPHA, GOLDEN, DesignedImage, pack, random_protein, synthetic_table
 
 pytestmark = pytest.mark.gpu
 
@@ -110,8 +111,9 @@ def aos_world(small_world, gpu):
     img.close()
 
 
-@pytest.mark.parametrize("mode", ["packed_record", "packed_key_first", "aos_bucket", "aos_key_first"])
-@pytest.mark.parametrize("probe_j", [2, 4, 5, 8])
+@pytest.mark.parametrize("mode", ["packed_record", "packed_key_first", "aos_bucket", "aos_key_first",
+                                  "packed_line", "packed_line8"])
+@pytest.mark.parametrize("probe_j", [1, 2, 3, 4, 5, 8])
 def test_probe_variants_agree(small_world, aos_world, oracle_lib, gpu, mode, probe_j):
     spec, table, img, ctx = small_world
     assert img.layout == gpu.Image.PACKED16
@@ -125,13 +127,14 @@ def test_probe_variants_agree(small_world, aos_world, oracle_lib, gpu, mode, pro
     recs = [("q", bytes(res[int(off[i]):int(off[i]) + int(lens[i])])) for i in range(300)]
     res, off = pack(recs)
     want = oracle_lib.process_batch(table, res, off)
-    ctx.set_option("probe_variant", 1 if mode.endswith("key_first") else 0)
+    variant = {"packed_line": 2, "packed_line8": 3}.get(mode, 1 if mode.endswith("key_first") else 0)
+    ctx.set_option("probe_variant", variant)
     ctx.set_option("probe_j", probe_j)
     try:
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
     finally:
         ctx.set_option("probe_variant", -1)
-        ctx.set_option("probe_j", 4)
+        ctx.set_option("probe_j", 2)
     assert_same(got, want, 300)
 
 
@@ -214,6 +217,88 @@ def test_stray_keys_above_max_stop_probes(gpu, oracle_lib):
                 im.set_layout(gpu.Image.AOS24)
             got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
             assert_same(got, want, len(recs))
+
+
+def _decode(key: int) -> str:
+    out = []
+    for _ in range(8):
+        out.append(ALPHA[key % 20])
+        key //= 20
+    return "".join(reversed(out))
+
+
+def _chain_table(rng, num_sigs, n_keys, dup_every=0, stray_every=0, tail_frac=0.0):
+    """A hand-placed linear-probe table: keys inserted in order from their home
+    slot (key % num_sigs) to the first free bucket, wrapping at the end.
+    tail_frac of the keys are drawn with homes in the last 16 buckets, so
+    chains cross line boundaries and wrap; every dup_every-th key is stored a
+    second time further down its chain with another payload; every
+    stray_every-th free bucket after an occupied one gets a stray key > 20^8."""
+    table = np.zeros(num_sigs, SIG_DTYPE)
+    table["which_kmer"] = 20 ** 8 + 1
+    keys = []
+    while len(keys) < n_keys:
+        k = int(rng.integers(0, 20 ** 8))
+        if rng.random() < tail_frac:
+            k = k - k % num_sigs + num_sigs - 1 - int(rng.integers(0, 16))
+            if k >= 20 ** 8 or k < 0:
+                continue
+        keys.append(k)
+    stored = []
+    for n, k in enumerate(keys):
+        for copy in range(2 if dup_every and n % dup_every == 0 else 1):
+            h = k % num_sigs
+            for _ in range(num_sigs):
+                if table["which_kmer"][h] > 20 ** 8:
+                    break
+                h = (h + 1) % num_sigs
+            else:
+                break  # full
+            table[h] = (k, int(rng.integers(-1, 1000)), int(rng.integers(0, 300)), 0,
+                        int(rng.integers(0, 5000)), np.float32(rng.random() * 4))
+            stored.append(k)
+    if stray_every:
+        occ = np.nonzero(table["which_kmer"] <= 20 ** 8)[0]
+        for i in occ[::stray_every]:
+            j = (i + 1) % num_sigs
+            if table["which_kmer"][j] > 20 ** 8:
+                table["which_kmer"][j] = 20 ** 8 + 2 + int(i) * 31
+    return table, keys
+
+
+@pytest.mark.parametrize("shape", ["wrap", "dups_strays", "full"])
+def test_probe_chain_shapes_all_variants(gpu, oracle_lib, shape):
+    """Chains that cross 64-B / 128-B lines, wrap past the last bucket of a
+    table whose size is not a multiple of the line, meet duplicates (the
+    earliest copy wins) and stray stop keys, or never end (a full table with
+    absent keys): every probe variant gives the oracle's answer."""
+    rng = np.random.default_rng({"wrap": 1, "dups_strays": 2, "full": 3}[shape])
+    if shape == "wrap":
+        table, keys = _chain_table(rng, 1001, 800, tail_frac=0.3)
+    elif shape == "dups_strays":
+        table, keys = _chain_table(rng, 997, 500, dup_every=3, stray_every=4, tail_frac=0.2)
+    else:
+        table, keys = _chain_table(rng, 203, 300, tail_frac=0.1)
+        assert (table["which_kmer"] <= 20 ** 8).all()
+    absent = [int(x) for x in rng.integers(0, 20 ** 8, 400)]
+    pool = keys + absent
+    recs = []
+    for r in range(60):
+        pick = [pool[int(i)] for i in rng.integers(0, len(pool), 40)]
+        # runs of present k-mers (calls) separated by X, plus some overlapping windows
+        recs.append((f"q{r}", "X".join(_decode(k) for k in pick) + random_protein(rng, 30)))
+    res, off = pack(recs)
+    want = oracle_lib.process_batch(table, res, off)
+    assert int(want.hit_offsets[-1]) > 0
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        assert img.layout == gpu.Image.PACKED16
+        for variant in (-1, 0, 1, 2, 3):
+            for probe_j in (1, 2, 3, 4):
+                ctx.set_option("probe_variant", variant)
+                ctx.set_option("probe_j", probe_j)
+                got = ctx.process_batch(res, off, gpu.Params(2, 200, 0, 0))
+                assert_same(got, oracle_lib.process_batch(table, res, off, params=(2, 200, 0, 0)),
+                            len(recs))
 
 
 def test_ragged_long_and_empty_sequences(small_world, oracle_lib, gpu):
@@ -424,10 +509,13 @@ def test_device_queries_and_run_device(gpu, oracle_lib):
             cc = np.empty(n, np.uint32)
             for arr, ptr in ((wb, out.window_base), (hc, out.hit_count), (cc, out.call_count)):
                 gpu.check(L_.kgx_memcpy_d2h(arr.ctypes.data, ptr, arr.nbytes), "d2h")
-            hits = np.empty(int(wb[-1]), gpu.HIT_DTYPE)
+            hot = np.empty((int(wb[-1]), 4), np.uint32)
+            cold = np.empty((int(wb[-1]), 4), np.uint32)
             calls = np.empty(int(wb[-1]), gpu.CALL_DTYPE)
             mask = np.empty((int(wb[-1]) + 63) // 64, np.uint64)
-            gpu.check(L_.kgx_memcpy_d2h(hits.ctypes.data, out.hits, hits.nbytes), "d2h")
+            gpu.check(L_.kgx_memcpy_d2h(hot.ctypes.data, out.hits_hot, hot.nbytes), "d2h")
+            gpu.check(L_.kgx_memcpy_d2h(cold.ctypes.data, out.hits_cold, cold.nbytes), "d2h")
+            hits = gpu.hits_from_planes(hot, cold)
             gpu.check(L_.kgx_memcpy_d2h(calls.ctypes.data, out.calls, calls.nbytes), "d2h")
             gpu.check(L_.kgx_memcpy_d2h(mask.ctypes.data, out.hit_mask, mask.nbytes), "d2h")
             want = oracle_lib.process_batch(table, hres, hoff)
