@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -126,6 +127,12 @@ struct kgx_image {
     kgx::packed_bucket *d_packed = nullptr; /* PACKED16 */
     uint64_t *d_filter = nullptr;           /* presence filter (kgx_image_set_filter) */
     uint32_t filter_log2_words = 0;
+    /* probe order across the image's contexts: the probe is bound by random
+     * HBM requests, so two probes at once only share that rate; run back to
+     * back instead, each context's other kernels (plan, score, gather, fq
+     * translation) overlap the next context's probe */
+    std::mutex probe_mu;
+    hipEvent_t last_probe = nullptr; /* end of the latest probe enqueued */
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
@@ -140,6 +147,8 @@ struct kgx_ctx {
     kgx_image *img = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipEvent_t probe_done = nullptr; /* recorded after each of this context's probes */
+    int probe_serialize = 1;          /* option "probe_serialize" */
     /* device scratch */
     kgx::DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
         dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;

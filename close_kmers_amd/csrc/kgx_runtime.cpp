@@ -556,6 +556,12 @@ int kgx_ctx_create(kgx_image *img, kgx_ctx **out)
         return fail(KGX_EDEVICE, std::string("stream: ") + hipGetErrorString(e));
     }
     c->own_stream = true;
+    e = hipEventCreateWithFlags(&c->probe_done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return fail(KGX_EDEVICE, std::string("event: ") + hipGetErrorString(e));
+    }
     *out = c;
     return KGX_OK;
 }
@@ -570,6 +576,12 @@ int kgx_ctx_destroy(kgx_ctx *c)
                       &c->hits, &c->calls, &c->hit_count, &c->call_count, &c->dense_hoff,
                       &c->dense_coff, &c->dense_hits, &c->dense_calls, &c->plan_ws, &c->ranges})
         b->release();
+    {
+        std::lock_guard<std::mutex> lock(c->img->probe_mu);
+        if (c->img->last_probe == c->probe_done)
+            c->img->last_probe = nullptr;
+    }
+    (void)hipEventDestroy(c->probe_done);
     if (c->own_stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -627,6 +639,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value < PROBE_AUTO || value > PROBE_LINE8)
             return fail(KGX_EINVAL, "probe_variant must be -1, 0, 1, 2 or 3");
         c->probe_variant = (int)value;
+        return KGX_OK;
+    }
+    if (n == "probe_serialize") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "probe_serialize must be 0 or 1");
+        c->probe_serialize = (int)value;
         return KGX_OK;
     }
     if (n == "probe_j") {
@@ -687,12 +705,23 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     HIP_TRY(hipSetDevice(c->img->device));
     if (c->img->num_sigs >= (1ull << 40))
         return fail(KGX_ERANGE, "image too large");
+    kgx_image *img = c->img;
+    std::unique_lock<std::mutex> lock(img->probe_mu, std::defer_lock);
+    if (c->probe_serialize) {
+        lock.lock();
+        if (img->last_probe && img->last_probe != c->probe_done)
+            HIP_TRY(hipStreamWaitEvent(c->stream, img->last_probe, 0));
+    }
     HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
                          c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
                          c->img->layout, c->img->num_sigs,
                          c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                          c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
                          (int)(c->tile_windows / 64), c->probe_variant, c->stream));
+    if (c->probe_serialize) {
+        HIP_TRY(hipEventRecord(c->probe_done, c->stream));
+        img->last_probe = c->probe_done;
+    }
     c->have_hits = true;
     return KGX_OK;
 }

@@ -226,6 +226,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * aligned 64-B / 128-B table line per instruction (probe_j 1-4 / 1-2; other
  * combinations run variant 0);
  * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
+ * "probe_serialize" 1 (default) / 0: this context's probes wait for the
+ * image's previous probe (any context), so that probes run back to back and
+ * the other kernels of the contexts overlap them;
  * "microbench_span" = bytes of the table kgx_microbench_random_read covers
  * (0 = all), "microbench_ilp" (1, 2, 4, 8, 16) reads in flight per lane and
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
