@@ -45,7 +45,7 @@ def main():
     calib = {}
     ceil = (bench.get("roofline") or {}).get("random_read_ceiling") or {}
     for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64"), (3, "rec16"), (4, "line64")):
-        b, n = mean_of(fetch, lambda k, m=mode: f"random_read_kernel<{m}>" in k)
+        b, n = mean_of(fetch, lambda k, m=mode: f"random_read_kernel<{m}," in k)
         reads = (ceil.get(name) or {}).get("reads")
         if b is not None and reads:
             calib[name] = {"fetch_bytes_per_read": b / reads, "dispatches": n}
