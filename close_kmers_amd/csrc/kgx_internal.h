@@ -156,7 +156,9 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
-                         hipStream_t stream);
+                         uint32_t seq_base, hipStream_t stream);
+/* device stores of bytes (4-aligned) from HBM into mapped pinned host memory */
+hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
                               uint32_t rounds, int mode, int ilp, uint64_t *sink, hipStream_t stream);
 hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,

@@ -927,7 +927,8 @@ __global__ __launch_bounds__(256) void gather_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
     const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
-    const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out)
+    const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
+    uint32_t seq_base)
 {
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= n_seq)
@@ -966,7 +967,7 @@ __global__ __launch_bounds__(256) void gather_kernel(
             for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its two planes */
                 const uint4 h = hot[at + i], c = cold[at + i];
                 dst[2 * i] = make_uint4(c.x, c.y, c.z, h.x);
-                dst[2 * i + 1] = make_uint4(h.y, h.z, h.w, c.w);
+                dst[2 * i + 1] = make_uint4(h.y, h.z, h.w, c.w + seq_base);
             }
             done += __shfl(incl, 63);
         }
@@ -983,13 +984,56 @@ __global__ __launch_bounds__(256) void gather_kernel(
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
-                         kgx_hit *hits_out, kgx_call *calls_out, hipStream_t stream)
+                         kgx_hit *hits_out, kgx_call *calls_out, uint32_t seq_base, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     hipLaunchKernelGGL(gather_kernel, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                        hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                       calls_out);
+                       calls_out, seq_base);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* copy to mapped pinned host memory: the device's own stores stream the     */
+/* results over PCIe (one contiguous 1-KB run per wave instruction), so the */
+/* D2H needs no DMA-engine slot and overlaps other streams' H2D copies      */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(256) void copy16_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src,
+                                                     uint64_t n)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void copy4_kernel(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src,
+                                                    uint64_t n)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[i];
+}
+
+hipError_t launch_copy_to_host(void *dst, const void *src, uint64_t bytes, int copy_blocks, hipStream_t stream)
+{
+    if (bytes == 0)
+        return hipSuccess;
+    const bool v16 = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0) && bytes % 16 == 0;
+    if (!v16 && (((uintptr_t)dst | (uintptr_t)src | bytes) % 4 != 0))
+        return hipErrorInvalidValue;
+    const uint64_t n = v16 ? bytes / 16 : bytes / 4;
+    /* PCIe writes are posted: a few waves keep the link busy, and a full
+     * grid would starve the kernels of the other stream (latency-bound
+     * scorer, plan) that this copy is meant to run beside */
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)copy_blocks);
+    if (v16)
+        hipLaunchKernelGGL(copy16_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
+                           static_cast<const uint4 *>(src), n);
+    else
+        hipLaunchKernelGGL(copy4_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint32_t *>(dst),
+                           static_cast<const uint32_t *>(src), n);
     return hipGetLastError();
 }
 

@@ -107,6 +107,15 @@ template <class T> struct PinnedVec {
     }
     T *data() { return p; }
     const T *data() const { return p; }
+    /* the device's address of element i (pinned host memory is mapped) */
+    hipError_t device_ptr(size_t i, void **out) const
+    {
+        void *d = nullptr;
+        hipError_t e = hipHostGetDevicePointer(&d, p, 0);
+        if (e == hipSuccess)
+            *out = static_cast<char *>(d) + i * sizeof(T);
+        return e;
+    }
     size_t size() const { return n; }
     T &operator[](size_t i) { return p[i]; }
     const T &operator[](size_t i) const { return p[i]; }
@@ -177,6 +186,14 @@ struct kgx_ctx {
     std::vector<kgx_otu> h_otus;
     kgx::PinnedVec<uint32_t> h_hcount, h_ccount;
     kgx::PinnedVec<char> h_res;
+    /* host-buffer batches in chunks (option "host_chunks"): chunks alternate
+     * between this context and a twin over the same image, so one chunk's
+     * gather + D2H overlaps the next chunk's H2D + kernels */
+    int host_chunks = 3;
+    int host_copy = 1; /* chunk D2H: 0 = DMA (hipMemcpyAsync), 1 = device stores into mapped memory */
+    int host_copy_blocks = 64; /* workgroups of the store copy (option "host_copy_blocks") */
+    kgx_ctx *twin = nullptr;
+    kgx::PinnedVec<uint64_t> h_off_stage, h_dense_hoff, h_dense_coff, h_nwin;
 };
 
 #endif

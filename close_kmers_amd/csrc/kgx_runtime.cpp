@@ -571,6 +571,8 @@ int kgx_ctx_destroy(kgx_ctx *c)
     if (!c)
         return KGX_OK;
     (void)hipSetDevice(c->img->device);
+    if (c->twin)
+        kgx_ctx_destroy(c->twin);
     (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->residues, &c->offsets, &c->wbase, &c->tile_seq, &c->hit_mask,
                       &c->hits, &c->calls, &c->hit_count, &c->call_count, &c->dense_hoff,
@@ -645,6 +647,24 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "probe_serialize must be 0 or 1");
         c->probe_serialize = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_copy_blocks") {
+        if (value < 1 || value > 4096)
+            return fail(KGX_EINVAL, "host_copy_blocks must be 1..4096");
+        c->host_copy_blocks = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_copy") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_copy must be 0 or 1");
+        c->host_copy = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_chunks") {
+        if (value < 1 || value > 64)
+            return fail(KGX_EINVAL, "host_chunks must be 1..64");
+        c->host_chunks = (int)value;
         return KGX_OK;
     }
     if (n == "probe_j") {
@@ -774,6 +794,269 @@ int kgx_run_device(kgx_ctx *c, const kgx_params *params, const uint8_t *d_res, c
 
 /* ---- host-buffer batch ---------------------------------------------------- */
 
+namespace {
+
+/* a sequence is cut at its first NUL (strlen bound of gather_hits,
+ * kguts.cc:792): the NUL's predecessor and everything after become 'X', which
+ * kills exactly the windows the reference never visits */
+void cut_at_nul(char *b, uint64_t len)
+{
+    const void *z = len ? std::memchr(b, 0, len) : nullptr;
+    if (z) {
+        const uint64_t slen = (uint64_t)((const char *)z - b);
+        for (uint64_t i = slen ? slen - 1 : 0; i < len; i++)
+            b[i] = 'X';
+    }
+}
+
+/* sequences [s0, s1) of a host batch -> x's pinned staging (host work only) */
+int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1)
+{
+    const uint32_t n = s1 - s0;
+    const uint64_t r0 = n ? seq_offsets[s0] : 0;
+    const uint64_t n_res = n ? seq_offsets[s1] - r0 : 0;
+    HIP_TRY(x->h_res.resize(n_res));
+    if (n_res)
+        std::memcpy(x->h_res.data(), residues + r0, n_res);
+    /* one scan of the whole range first: NUL bytes are rare */
+    if (n_res && std::memchr(x->h_res.data(), 0, n_res))
+        for (uint32_t s = s0; s < s1; s++)
+            cut_at_nul(x->h_res.data() + (seq_offsets[s] - r0), seq_offsets[s + 1] - seq_offsets[s]);
+    HIP_TRY(x->h_off_stage.resize(n + 1));
+    for (uint32_t i = 0; i <= n; i++)
+        x->h_off_stage[i] = n ? seq_offsets[s0 + i] - r0 : 0;
+    return KGX_OK;
+}
+
+/* x's staged sequences -> HBM (async on x's stream) */
+int stage_upload(kgx_ctx *x)
+{
+    const uint64_t n_res = x->h_res.size(), n1 = x->h_off_stage.size();
+    HIP_TRY(x->residues.reserve(n_res + 16));
+    HIP_TRY(x->offsets.reserve(n1 * sizeof(uint64_t)));
+    if (n_res)
+        HIP_TRY(hipMemcpyAsync(x->residues.p, x->h_res.data(), n_res, hipMemcpyHostToDevice, x->stream));
+    HIP_TRY(hipMemcpyAsync(x->offsets.p, x->h_off_stage.data(), n1 * sizeof(uint64_t), hipMemcpyHostToDevice,
+                           x->stream));
+    return KGX_OK;
+}
+
+int stage_host_seqs(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1)
+{
+    int rc = stage_host_copy(x, residues, seq_offsets, s0, s1);
+    return rc ? rc : stage_upload(x);
+}
+
+/* one staged chunk on x: H2D, plan/probe/score, counts + window total -> host */
+int enqueue_chunk(kgx_ctx *x, const kgx_params *params, uint32_t want)
+{
+    int rc = stage_upload(x);
+    if (rc)
+        return rc;
+    const uint32_t n = (uint32_t)x->h_off_stage.size() - 1;
+    const uint64_t n_res = x->h_res.size();
+    if ((rc = kgx_run_device(x, params, x->residues.as<uint8_t>(), x->offsets.as<uint64_t>(), n, n_res, want,
+                             nullptr)))
+        return rc;
+    HIP_TRY(x->h_hcount.resize(n + 1));
+    HIP_TRY(x->h_ccount.resize(n + 1));
+    HIP_TRY(x->h_nwin.resize(1));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(x->h_hcount.data(), x->hit_count.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               x->stream));
+        HIP_TRY(hipMemcpyAsync(x->h_ccount.data(), x->call_count.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               x->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(x->h_nwin.data(), x->wbase.as<uint64_t>() + n, sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, x->stream));
+    return KGX_OK;
+}
+
+/* KmerOtuStats::otu_map over the hits the scorer flagged, then finalize()
+ * (kguts.h:214-218: std::sort by count, descending) */
+void otu_tallies(kgx_ctx *c, uint32_t n_seq, bool want_otu)
+{
+    c->h_ooff.assign(n_seq + 1, 0);
+    c->h_otus.clear();
+    if (!want_otu)
+        return;
+    std::map<int, int> m;
+    std::vector<std::pair<int, int>> v;
+    for (uint32_t s = 0; s < n_seq; s++) {
+        m.clear();
+        for (uint64_t i = c->h_hoff[s]; i < c->h_hoff[s + 1]; i++)
+            if (c->h_hits[i].flags & KGX_HIT_OTU)
+                m[c->h_hits[i].otu_index]++;
+        v.assign(m.begin(), m.end());
+        std::sort(v.begin(), v.end(),
+                  [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return b.second < a.second; });
+        for (auto &pr : v)
+            c->h_otus.push_back(kgx_otu{pr.first, pr.second});
+        c->h_ooff[s + 1] = c->h_otus.size();
+    }
+}
+
+void fill_result(kgx_ctx *c, uint32_t n_seq, bool need_hits, uint64_t nwin, kgx_result *out)
+{
+    out->n_seq = n_seq;
+    out->hit_offsets = c->h_hoff.data();
+    out->hits = need_hits ? c->h_hits.data() : nullptr;
+    out->call_offsets = c->h_coff.data();
+    out->calls = c->h_calls.data();
+    out->otu_offsets = c->h_ooff.data();
+    out->otus = c->h_otus.data();
+    out->n_windows = nwin;
+}
+
+/* The host batch in K residue-balanced chunks of whole sequences, alternating
+ * between c and its twin context: while chunk k's hits are gathered and
+ * copied to the host on one stream, chunk k+1 is staged, copied up, probed
+ * and scored on the other.  The D2H of the hit records is the bulk of the
+ * PCIe traffic, so the rest hides behind it.  Results are identical to the
+ * one-pass path (per-sequence work never spans chunks). */
+int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *residues,
+                          const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, uint32_t K,
+                          kgx_result *out)
+{
+    if (!c->twin) {
+        int rc = kgx_ctx_create(c->img, &c->twin);
+        if (rc)
+            return rc;
+    }
+    kgx_ctx *t = c->twin;
+    t->probe_variant = c->probe_variant;
+    t->probe_j = c->probe_j;
+    t->probe_filter = c->probe_filter;
+    t->probe_serialize = c->probe_serialize;
+    kgx_ctx *xs[2] = {c, t};
+
+    const uint64_t r0 = seq_offsets[0], n_res = seq_offsets[n_seq] - r0;
+    std::vector<uint32_t> cut(K + 1, 0);
+    cut[K] = n_seq;
+    for (uint32_t k = 1; k < K; k++) {
+        const uint64_t target = r0 + n_res * k / K;
+        uint32_t s = (uint32_t)(std::lower_bound(seq_offsets, seq_offsets + n_seq + 1, target) - seq_offsets);
+        cut[k] = std::min(std::max(s, cut[k - 1]), n_seq);
+    }
+    cut.erase(std::unique(cut.begin(), cut.end()), cut.end()); /* no empty chunks */
+    K = (uint32_t)cut.size() - 1;
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool need_hits = (want & (KGX_WANT_HITS | KGX_WANT_OTU)) != 0;
+    c->h_hoff.assign(n_seq + 1, 0);
+    c->h_coff.assign(n_seq + 1, 0);
+    uint64_t hbase = 0, cbase = 0, nwin = 0;
+    HIP_TRY(c->h_hits.resize(0));
+    HIP_TRY(c->h_calls.resize(0));
+
+    /* Copies of both streams share the DMA engine in submission order, so the
+     * order of submission is the schedule: chunk k+1's H2D goes in before
+     * chunk k's D2H, and chunk k+1's kernels run while that D2H streams.
+     * The host staging of chunk k+2 runs meanwhile. */
+    int rc = stage_host_copy(xs[0], residues, seq_offsets, cut[0], cut[1]);
+    if (!rc)
+        rc = enqueue_chunk(xs[0], params, want);
+    if (!rc && K > 1)
+        rc = stage_host_copy(xs[1], residues, seq_offsets, cut[1], cut[2]);
+    const bool timing = std::getenv("KGX_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    for (uint32_t k = 0; k < K && !rc; k++) {
+        kgx_ctx *x = xs[k & 1], *y = xs[(k + 1) & 1];
+        const auto t0 = now();
+        HIP_TRY(hipStreamSynchronize(x->stream)); /* chunk k's counts are on the host */
+        const auto t1 = now();
+        if (k + 1 < K && (rc = enqueue_chunk(y, params, want))) /* staged in the previous round */
+            break;
+        const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
+        HIP_TRY(x->h_dense_hoff.resize(n + 1));
+        HIP_TRY(x->h_dense_coff.resize(n + 1));
+        uint64_t nh = 0, nc = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            x->h_dense_hoff[i] = nh;
+            x->h_dense_coff[i] = nc;
+            nh += x->h_hcount[i];
+            nc += want_calls ? x->h_ccount[i] : 0;
+            c->h_hoff[s0 + i + 1] = hbase + nh;
+            c->h_coff[s0 + i + 1] = cbase + nc;
+        }
+        x->h_dense_hoff[n] = nh;
+        x->h_dense_coff[n] = nc;
+        nwin += x->h_nwin[0];
+        const uint64_t nh_all = nh; /* hit offsets count every hit; records only when wanted */
+        if (!need_hits)
+            nh = 0;
+        const uint64_t hrec = need_hits ? hbase : 0; /* where this chunk's records go */
+        if (hrec + nh > c->h_hits.cap || cbase + nc > c->h_calls.cap) {
+            /* growth moves the pinned arrays: no copy into them may be in flight */
+            HIP_TRY(hipStreamSynchronize(xs[0]->stream));
+            HIP_TRY(hipStreamSynchronize(xs[1]->stream));
+        }
+        HIP_TRY(c->h_hits.resize(hrec + nh));
+        HIP_TRY(c->h_calls.resize(cbase + nc));
+        if (nh || nc) {
+            HIP_TRY(x->dense_hoff.reserve((n + 1) * sizeof(uint64_t)));
+            HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
+            HIP_TRY(x->dense_hits.reserve(std::max<uint64_t>(nh, 1) * sizeof(kgx_hit)));
+            HIP_TRY(x->dense_calls.reserve(std::max<uint64_t>(nc, 1) * sizeof(kgx_call)));
+            HIP_TRY(hipMemcpyAsync(x->dense_hoff.p, x->h_dense_hoff.data(), (n + 1) * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, x->stream));
+            HIP_TRY(hipMemcpyAsync(x->dense_coff.p, x->h_dense_coff.data(), (n + 1) * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, x->stream));
+            HIP_TRY(launch_gather(n, x->wbase.as<uint64_t>(), x->hit_mask.as<uint64_t>(), x->tile_windows,
+                                  x->call_count.as<uint32_t>(), x->hits.as<uint4>(),
+                                  x->hits.as<uint4>() + x->hit_slots, x->calls.as<kgx_call>(),
+                                  x->dense_hoff.as<uint64_t>(), x->dense_coff.as<uint64_t>(),
+                                  nh ? x->dense_hits.as<kgx_hit>() : nullptr,
+                                  nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->stream));
+            if (c->host_copy) {
+                void *dh = nullptr, *dc = nullptr;
+                if (nh) {
+                    HIP_TRY(c->h_hits.device_ptr(hrec, &dh));
+                    HIP_TRY(launch_copy_to_host(dh, x->dense_hits.p, nh * sizeof(kgx_hit), c->host_copy_blocks, x->stream));
+                }
+                if (nc) {
+                    HIP_TRY(c->h_calls.device_ptr(cbase, &dc));
+                    HIP_TRY(launch_copy_to_host(dc, x->dense_calls.p, nc * sizeof(kgx_call), c->host_copy_blocks, x->stream));
+                }
+            } else {
+                if (nh)
+                    HIP_TRY(hipMemcpyAsync(c->h_hits.data() + hrec, x->dense_hits.p, nh * sizeof(kgx_hit),
+                                           hipMemcpyDeviceToHost, x->stream));
+                if (nc)
+                    HIP_TRY(hipMemcpyAsync(c->h_calls.data() + cbase, x->dense_calls.p, nc * sizeof(kgx_call),
+                                           hipMemcpyDeviceToHost, x->stream));
+            }
+        }
+        hbase += nh_all;
+        cbase += nc;
+        const auto t2 = now();
+        /* chunk k+2 -> x's pinned staging while the DMA engine and the device work */
+        /* (x's H2D of chunk k finished before its counts arrived; its pending
+         * D2H reads device memory only) */
+        if (k + 2 < K)
+            rc = stage_host_copy(x, residues, seq_offsets, cut[k + 2], cut[k + 3]);
+        if (timing)
+            std::fprintf(stderr, "[kgx] chunk %u: wait counts %.3f ms, enqueue %.3f ms, stage k+2 %.3f ms\n", k,
+                         ms(t0, t1), ms(t1, t2), ms(t2, now()));
+    }
+    /* drain both streams, whatever happened above */
+    const hipError_t e0 = hipStreamSynchronize(xs[0]->stream), e1 = hipStreamSynchronize(xs[1]->stream);
+    if (rc)
+        return rc;
+    HIP_TRY(e0);
+    HIP_TRY(e1);
+    /* the batch's device results are split over two contexts */
+    c->have_hits = false;
+    t->have_hits = false;
+    otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
+    fill_result(c, n_seq, need_hits, nwin, out);
+    return KGX_OK;
+}
+
+}  // namespace
+
 int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues,
                       const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out)
 {
@@ -787,39 +1070,18 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     if (n_res && !residues)
         return fail(KGX_EINVAL, "null residues");
     HIP_TRY(hipSetDevice(c->img->device));
+    /* chunks of at least 2M residues, only when there is something to copy back */
+    const uint64_t k_res = std::max<uint64_t>(1, n_res >> 21);
+    const uint32_t K = (uint32_t)std::min<uint64_t>({(uint64_t)c->host_chunks, k_res, (uint64_t)n_seq});
+    if (K >= 2 && (want & (KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU)))
+        return process_batch_chunked(c, params, residues, seq_offsets, n_seq, want, K, out);
     PhaseTimer tm(c);
-
-    /* stage residues; a sequence is cut at its first NUL (strlen bound of
-     * gather_hits, kguts.cc:792): the NUL's predecessor and everything after
-     * become 'X', which kills exactly the windows the reference never visits */
-    const char *src = residues ? residues + r0 : nullptr;
-    HIP_TRY(c->h_res.resize(n_res));
-    if (n_res)
-        std::memcpy(c->h_res.data(), src, n_res);
-    for (uint32_t s = 0; s < n_seq; s++) {
-        char *b = c->h_res.data() + (seq_offsets[s] - r0);
-        uint64_t len = seq_offsets[s + 1] - seq_offsets[s];
-        const void *z = len ? std::memchr(b, 0, len) : nullptr;
-        if (z) {
-            uint64_t slen = (uint64_t)((const char *)z - b);
-            for (uint64_t i = slen ? slen - 1 : 0; i < len; i++)
-                b[i] = 'X';
-        }
-    }
-    std::vector<uint64_t> off(n_seq + 1);
-    for (uint32_t s = 0; s <= n_seq; s++)
-        off[s] = n_seq ? seq_offsets[s] - r0 : 0;
-
-    HIP_TRY(c->residues.reserve(n_res + 16));
-    HIP_TRY(c->offsets.reserve((n_seq + 1) * sizeof(uint64_t)));
-    if (n_res)
-        HIP_TRY(hipMemcpyAsync(c->residues.p, c->h_res.data(), n_res, hipMemcpyHostToDevice,
-                               c->stream));
-    HIP_TRY(hipMemcpyAsync(c->offsets.p, off.data(), (n_seq + 1) * sizeof(uint64_t),
-                           hipMemcpyHostToDevice, c->stream));
+    int rc = stage_host_seqs(c, residues, seq_offsets, 0, n_seq);
+    if (rc)
+        return rc;
     tm.mark("stage");
-    int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq,
-                            n_res, want, nullptr);
+    rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq, n_res, want,
+                        nullptr);
     if (rc)
         return rc;
     tm.mark("device");
@@ -876,7 +1138,7 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                               c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
                               c->dense_coff.as<uint64_t>(),
                               need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
-                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, c->stream));
+                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, 0u, c->stream));
         if (need_hits && nh)
             HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
                                    hipMemcpyDeviceToHost, c->stream));
@@ -887,41 +1149,12 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     }
 
     tm.mark(" gather+d2h");
-    /* OTU tallies: KmerOtuStats::otu_map over the hits the scorer flagged,
-     * then finalize() (kguts.h:214-218: std::sort by count, descending) */
-    c->h_ooff.assign(n_seq + 1, 0);
-    c->h_otus.clear();
-    if (want & KGX_WANT_OTU) {
-        std::map<int, int> m;
-        std::vector<std::pair<int, int>> v;
-        for (uint32_t s = 0; s < n_seq; s++) {
-            m.clear();
-            for (uint64_t i = c->h_hoff[s]; i < c->h_hoff[s + 1]; i++)
-                if (c->h_hits[i].flags & KGX_HIT_OTU)
-                    m[c->h_hits[i].otu_index]++;
-            v.assign(m.begin(), m.end());
-            std::sort(v.begin(), v.end(),
-                      [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
-                          return b.second < a.second;
-                      });
-            for (auto &pr : v)
-                c->h_otus.push_back(kgx_otu{pr.first, pr.second});
-            c->h_ooff[s + 1] = c->h_otus.size();
-        }
-    }
+    otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
     uint64_t nwin = 0;
     HIP_TRY(hipMemcpyAsync(&nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-
-    out->n_seq = n_seq;
-    out->hit_offsets = c->h_hoff.data();
-    out->hits = need_hits ? c->h_hits.data() : nullptr;
-    out->call_offsets = c->h_coff.data();
-    out->calls = c->h_calls.data();
-    out->otu_offsets = c->h_ooff.data();
-    out->otus = c->h_otus.data();
-    out->n_windows = nwin;
+    fill_result(c, n_seq, need_hits, nwin, out);
     return KGX_OK;
 }
 

@@ -233,7 +233,17 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * (0 = all), "microbench_ilp" (1, 2, 4, 8, 16) reads in flight per lane and
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
- * is 64 * probe_j windows), read at the next plan */
+ * is 64 * probe_j windows), read at the next plan;
+ * "host_chunks" (1..64, default 3): kgx_process_batch splits a batch of at
+ * least 4M residues into up to this many residue-balanced chunks of whole
+ * sequences, alternating between the context and a twin context it creates
+ * on first use, so that one chunk's D2H overlaps the next chunk's H2D and
+ * kernels; "host_copy" 1 (default) / 0: a chunk's hits and calls reach the
+ * host by device stores into the mapped pinned result arrays ("host_copy_blocks"
+ * workgroups, default 64) / by DMA (hipMemcpyAsync, which shares the copy
+ * engine with the next chunk's H2D).  After a chunked batch the device results are split over the two
+ * contexts: kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch
+ * (host_chunks 1, or want 0, which never chunks) */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
@@ -242,7 +252,8 @@ int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
  * the batch.  residues: concatenated sequence bytes; seq_offsets[n_seq+1]
  * delimits them.  Each sequence is cut at its first NUL byte, as
  * gather_hits' strlen() bound does (kguts.cc:792).  Synchronous; the result
- * views stay valid until the next call on ctx. */
+ * views stay valid until the next call on ctx.  Large batches run in chunks
+ * (option "host_chunks"); the results are the same. */
 int kgx_process_batch(kgx_ctx *ctx, const kgx_params *params, const char *residues,
                       const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
                       kgx_result *out);

@@ -592,3 +592,40 @@ def test_presence_filter_keeps_results(small_world, oracle_lib, gpu, log2_bits):
             assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, 400)
         img.set_layout(gpu.Image.AOS24)  # the filter depends on the keys only
         assert_same(ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0)), want, 400)
+
+
+def test_chunked_host_batch_matches_oracle(small_world, oracle_lib, gpu):
+    """kgx_process_batch in K chunks alternating over two contexts (option
+    host_chunks) returns the same CSR as one pass and as the oracle: global
+    sequence indices, offsets continued across chunks, NUL cuts, calls/OTU."""
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 16000, x_permille=3)
+    rng = np.random.default_rng(17)
+    res = res.copy()
+    lens = np.diff(off).astype(np.int64)
+    for s in rng.choice(len(lens), 40, replace=False):  # NULs inside some sequences
+        res[int(off[s]) + int(rng.integers(0, lens[s]))] = 0
+    # a long sequence and some empties, and a batch that starts mid-buffer
+    seqs = [res[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    long_seq = np.frombuffer(random_protein(rng, 3_000_000).encode(), np.uint8)
+    empty = np.zeros(0, np.uint8)
+    seqs = seqs[:8000] + [empty, long_seq, empty] + seqs[8000:]
+    lens = np.array([0] + [len(x) for x in seqs], np.uint64)
+    off = np.cumsum(lens).astype(np.uint64) + np.uint64(2)
+    res = np.concatenate([np.frombuffer(b"MK", np.uint8)] + seqs)
+    want = oracle_lib.process_batch(table, res, off)
+    for k, hc in ((2, 1), (3, 0), (3, 1), (8, 1), (1, 1)):
+        ctx.set_option("host_chunks", k)
+        ctx.set_option("host_copy", hc)
+        got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+        assert_same(got, want, len(off) - 1)
+        assert np.array_equal(got.hits["seq"], want.hits["seq"])
+        for w in (1, 2):
+            g = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=w)
+            assert np.array_equal(g.hit_offsets, want.hit_offsets)
+            if w == 1:
+                assert eq_fields(g.hits, want.hits)
+            else:
+                assert np.array_equal(g.call_offsets, want.call_offsets)
+    ctx.set_option("host_chunks", 3)
+    ctx.set_option("host_copy", 1)
