@@ -17,7 +17,7 @@ from . import build as _build
 KGX_OK = 0
 ERRORS = {-1: "EINVAL", -2: "EIO", -3: "EFORMAT", -4: "ENOMEM", -5: "EDEVICE", -6: "ERANGE",
           -7: "EFULL"}
-WANT_HITS, WANT_CALLS, WANT_OTU = 1, 2, 4
+WANT_HITS, WANT_CALLS, WANT_OTU, WANT_BEST = 1, 2, 4, 8
 HIT_IN_RUN, HIT_OTU = 1, 2
 
 HIT_DTYPE = np.dtype([("which_kmer", "<u8"), ("otu_index", "<i4"), ("avg_from_end", "<u2"),
@@ -26,6 +26,9 @@ HIT_DTYPE = np.dtype([("which_kmer", "<u8"), ("otu_index", "<i4"), ("avg_from_en
 CALL_DTYPE = np.dtype([("start", "<u4"), ("end", "<u4"), ("count", "<i4"),
                        ("function_index", "<u4"), ("weighted_hits", "<f4")])
 OTU_DTYPE = np.dtype([("otu_index", "<i4"), ("count", "<i4")])
+# kgx_best_call: find_best_call's decision (kind 0 no calls, 1 called, 2 ambiguous pair, 3 no call)
+BEST_DTYPE = np.dtype([("kind", "<i4"), ("fi0", "<i4"), ("fi1", "<i4"), ("score", "<f4"),
+                       ("weighted_score", "<f4"), ("score_offset", "<f4")])
 SIG_DTYPE = np.dtype([("which_kmer", "<u8"), ("otu_index", "<i4"), ("avg_from_end", "<u2"),
                       ("pad", "<u2"), ("function_index", "<i4"), ("function_wt", "<f4")])
 assert HIT_DTYPE.itemsize == 32 and CALL_DTYPE.itemsize == 20 and SIG_DTYPE.itemsize == 24
@@ -46,7 +49,7 @@ class Result(ctypes.Structure):
     _fields_ = [("n_seq", ctypes.c_uint32), ("hit_offsets", ctypes.c_void_p),
                 ("hits", ctypes.c_void_p), ("call_offsets", ctypes.c_void_p),
                 ("calls", ctypes.c_void_p), ("otu_offsets", ctypes.c_void_p),
-                ("otus", ctypes.c_void_p), ("n_windows", ctypes.c_uint64)]
+                ("otus", ctypes.c_void_p), ("n_windows", ctypes.c_uint64), ("best", ctypes.c_void_p)]
 
 
 class DeviceResult(ctypes.Structure):
@@ -54,7 +57,7 @@ class DeviceResult(ctypes.Structure):
                 ("window_base", ctypes.c_void_p), ("hit_mask", ctypes.c_void_p),
                 ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
                 ("hits_hot", ctypes.c_void_p), ("hits_cold", ctypes.c_void_p),
-                ("calls", ctypes.c_void_p)]
+                ("calls", ctypes.c_void_p), ("best", ctypes.c_void_p)]
 
 
 def hits_from_planes(hot: np.ndarray, cold: np.ndarray) -> np.ndarray:
@@ -128,6 +131,7 @@ SIGNATURES = {
     "kgx_image_download": (_INT, [_P, _P, _U64]),
     "kgx_ctx_create": (_INT, [_P, _PP]),
     "kgx_ctx_destroy": (_INT, [_P]),
+    "kgx_find_best_calls": (_INT, [_P, _P, _P, _U32, _P]),
     "kgx_ctx_stream": (_P, [_P]),
     "kgx_ctx_set_stream": (_INT, [_P, _P]),
     "kgx_ctx_set_option": (_INT, [_P, _CS, ctypes.c_int64]),
@@ -329,6 +333,7 @@ class BatchResult:
         self.calls = _view(r.calls, int(self.call_offsets[-1]), CALL_DTYPE, copy)
         self.otus = _view(r.otus, int(self.otu_offsets[-1]), OTU_DTYPE, copy)
         self.n_windows = r.n_windows
+        self.best = _view(r.best, n, BEST_DTYPE, copy) if r.best else None
 
 
 class Context:
@@ -354,6 +359,16 @@ class Context:
                                       offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
               "kgx_process_batch")
         return BatchResult(r, want, copy)
+
+    def find_best_calls(self, calls: np.ndarray, call_offsets) -> np.ndarray:
+        """find_best_call of every sequence's calls, on the device."""
+        calls = np.ascontiguousarray(calls, dtype=CALL_DTYPE)
+        off = np.ascontiguousarray(call_offsets, dtype=np.uint64)
+        out = np.zeros(len(off) - 1, BEST_DTYPE)
+        check(lib().kgx_find_best_calls(self.handle, calls.ctypes.data if calls.size else None,
+                                        off.ctypes.data, len(off) - 1, out.ctypes.data),
+              "kgx_find_best_calls")
+        return out
 
     def fq_fragments(self, bases, read_offsets) -> Fragments:
         """6-frame code-11 fragments (> 10 aa) of the reads, left on the device."""

@@ -292,6 +292,32 @@ void KmerGuts::find_best_call(std::vector<KmerCall> &calls, int &function_index,
               score, weighted_score, score_offset);
 }
 
+void KmerGuts::find_best_call(const kgx_best_call &best, int &function_index, std::string &function,
+                              float &score, float &weighted_score, float &score_offset)
+{
+    best_call(best, [this](int i) { return function_at_index(i); }, function_index, function, score,
+              weighted_score, score_offset);
+}
+
+void best_call(const kgx_best_call &b, const std::function<const char *(int)> &name_of, int &function_index,
+               std::string &function, float &score, float &weighted_score, float &score_offset)
+{
+    function_index = b.kind == 1 ? b.fi0 : -1;
+    function.clear();
+    score = b.score;
+    weighted_score = b.weighted_score;
+    if (b.kind != 0)
+        score_offset = b.score_offset; /* kind 0: left as the caller had it */
+    if (b.kind == 1) {
+        function = name_of(b.fi0);
+    } else if (b.kind == 2) { /* the lexically larger name first (kguts.cc:1176-1179) */
+        std::string f1 = name_of(b.fi0), f2 = name_of(b.fi1);
+        if (f2 > f1)
+            std::swap(f1, f2);
+        function = f1 + " ?? " + f2;
+    }
+}
+
 void best_call(const std::vector<KmerCall> &calls, const std::function<const char *(int)> &name_of,
                int &function_index, std::string &function, float &score, float &weighted_score,
                float &score_offset)
@@ -794,8 +820,10 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
     const bool want_calls = find_best_match_ && family_mode_;
     kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
     kgx_result r;
+    /* find_best_call runs on the device (KGX_WANT_BEST): only its decision
+     * per sequence comes back, not the calls */
     int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n,
-                               KGX_WANT_HITS | (want_calls ? KGX_WANT_CALLS : 0), &r);
+                               KGX_WANT_HITS | (want_calls ? KGX_WANT_BEST : 0), &r);
     if (rc)
         throw_last(rc, "kgx_process_batch");
     /* the on_hit lists of every hit: kmer_to_family_id_ or kmer_to_id_ */
@@ -837,14 +865,10 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
             }
         }
         if (want_calls) {
-            std::vector<KmerCall> calls;
-            for (uint64_t c = r.call_offsets[s]; c < r.call_offsets[s + 1]; c++)
-                calls.emplace_back(r.calls[c].start, r.calls[c].end, r.calls[c].count, r.calls[c].function_index,
-                                   r.calls[c].weighted_hits);
             int fi;
             std::string fn, ambig;
             float score, wscore, offs = 0.0f;
-            kg.find_best_call(calls, fi, fn, score, wscore, offs);
+            kg.find_best_call(r.best[s], fi, fn, score, wscore, offs);
             bool do_ambig = false;
             if (fn.empty()) {
                 fn = "hypothetical protein";

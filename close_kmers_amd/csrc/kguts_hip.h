@@ -140,6 +140,9 @@ public:
 
     void find_best_call(std::vector<KmerCall> &calls, int &function_index, std::string &function,
                         float &score, float &weighted_score, float &score_offset);
+    /* the same outputs from the device's decision (KGX_WANT_BEST) */
+    void find_best_call(const kgx_best_call &best, int &function_index, std::string &function,
+                        float &score, float &weighted_score, float &score_offset);
 
     std::string format_call(const KmerCall &c);
     std::string format_hit(const hit_in_sequence_t &h);
@@ -369,6 +372,10 @@ void run_batch_on_device(KmerGuts &kg, const std::vector<std::string> &seqs);
 void best_call(const std::vector<KmerCall> &calls, const std::function<const char *(int)> &name_of,
                int &function_index, std::string &function, float &score, float &weighted_score,
                float &score_offset);
+
+/* find_best_call's outputs from a device decision (kgx_best_call) */
+void best_call(const kgx_best_call &b, const std::function<const char *(int)> &name_of, int &function_index,
+               std::string &function, float &score, float &weighted_score, float &score_offset);
 
 /* load_indexed_ar (kguts.cc:544-575): "%d\t<name>\n" lines, dense and in
  * order; returns false when the file cannot be opened or is not dense. */

@@ -157,6 +157,9 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
                          uint32_t seq_base, hipStream_t stream);
+/* find_best_call per sequence: calls[start[s] ..+ count[s]), ws same extent */
+hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64_t *start, const uint32_t *count,
+                             kgx_call *ws, kgx_best_call *out, hipStream_t stream);
 /* device stores of bytes (4-aligned) from HBM into mapped pinned host memory */
 hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,

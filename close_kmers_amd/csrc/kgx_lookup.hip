@@ -920,6 +920,157 @@ hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *h
 }
 
 /* ------------------------------------------------------------------------ */
+/* best call: find_best_call (kguts.cc:1008-1199), one lane per sequence     */
+/* ------------------------------------------------------------------------ */
+
+/* The sequence's calls are rewritten in its own stretch of the workspace
+ * (every step writes at or below the index it has read): collapse adjacent
+ * same-function calls (kguts.cc:1026-1041), join F1|F2|F1 with a weak
+ * interior (kguts.cc:1064-1084), then a stable insertion sort by function
+ * index and a run sum give the std::map<int, FuncScore> totals in key order
+ * with each float sum in the reference's order (kguts.cc:1108-1125).  The
+ * top two come from libstdc++'s partial_sort(begin, begin + 2, end) replayed
+ * step by step (__heap_select: make_heap of two, pop_heap for every later
+ * element that beats the heap top, then sort_heap), so ties and the element
+ * left at index 2 come out as in the reference. */
+__global__ __launch_bounds__(256) void best_call_kernel(uint32_t n_seq, const kgx_call *__restrict__ calls,
+                                                        const uint64_t *__restrict__ start,
+                                                        const uint32_t *__restrict__ count, kgx_call *__restrict__ ws,
+                                                        kgx_best_call *__restrict__ out)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_seq)
+        return;
+    kgx_best_call r;
+    r.kind = 0;
+    r.fi0 = -1;
+    r.fi1 = -1;
+    r.score = 0.0f;
+    r.weighted_score = 0.0f;
+    r.score_offset = 0.0f;
+    const uint32_t n = count[s];
+    if (n == 0) {
+        out[s] = r;
+        return;
+    }
+    const kgx_call *c = calls + start[s];
+    kgx_call *m = ws + start[s];
+    /* collapse */
+    uint32_t nc = 0;
+    for (uint32_t i = 0; i < n;) {
+        kgx_call cur = c[i++];
+        while (i < n && c[i].function_index == cur.function_index) {
+            cur.end = c[i].end;
+            cur.count += c[i].count;
+            cur.weighted_hits += c[i].weighted_hits;
+            i++;
+        }
+        m[nc++] = cur;
+    }
+    /* F1 | F2 | F1: interior count < 5, exterior counts >= 10 */
+    uint32_t nm = 0;
+    for (uint32_t i = 0; i < nc;) {
+        kgx_call cur = m[i++];
+        while (i + 1 < nc && m[i + 1].function_index == cur.function_index && m[i].count < 5 &&
+               cur.count + m[i + 1].count >= 10) {
+            cur.end = m[i + 1].end;
+            cur.count += m[i + 1].count;
+            cur.weighted_hits += m[i + 1].weighted_hits;
+            i += 2;
+        }
+        m[nm++] = cur;
+    }
+    /* std::map<int, FuncScore>: key order is the signed function index */
+    for (uint32_t i = 1; i < nm; i++) {
+        const kgx_call v = m[i];
+        uint32_t j = i;
+        while (j > 0 && (int32_t)m[j - 1].function_index > (int32_t)v.function_index) {
+            m[j] = m[j - 1];
+            j--;
+        }
+        m[j] = v;
+    }
+    uint32_t nr = 0;
+    for (uint32_t i = 0; i < nm;) {
+        kgx_call cur = m[i++];
+        while (i < nm && m[i].function_index == cur.function_index) {
+            cur.count += m[i].count;
+            cur.weighted_hits += m[i].weighted_hits;
+            i++;
+        }
+        m[nr++] = cur;
+    }
+    /* partial_sort(vec.begin(), vec.begin() + 2, vec.end(), weighted >) */
+    kgx_call v0 = m[0], v1 = v0, v2 = v0;
+    if (nr > 1) {
+        kgx_call h0, h1; /* the two-element heap; its top h0 is the weakest */
+        const kgx_call a0 = m[0], a1 = m[1];
+        if (a1.weighted_hits > a0.weighted_hits) {
+            h0 = a0;
+            h1 = a1;
+        } else {
+            h0 = a1;
+            h1 = a0;
+        }
+        if (nr > 2)
+            v2 = m[2];
+        for (uint32_t i = 2; i < nr; i++) {
+            const kgx_call x = m[i];
+            if (x.weighted_hits > h0.weighted_hits) { /* __pop_heap(first, middle, i) */
+                if (i == 2)
+                    v2 = h0; /* *i = *first */
+                const kgx_call t = h1;
+                if (t.weighted_hits > x.weighted_hits) {
+                    h0 = x;
+                    h1 = t;
+                } else {
+                    h0 = t;
+                    h1 = x;
+                }
+            }
+        }
+        v0 = h1; /* __sort_heap of two swaps them */
+        v1 = h0;
+    }
+    r.score_offset = nr == 1 ? (float)v0.count : (float)(v0.count - v1.count);
+    if (r.score_offset >= 5.0f) {
+        r.kind = 1;
+        r.fi0 = (int32_t)v0.function_index;
+        r.score = (float)v0.count;
+        r.weighted_score = v0.weighted_hits;
+    } else {
+        r.kind = 3;
+        if (nr >= 2) {
+            r.fi0 = (int32_t)v0.function_index;
+            r.fi1 = (int32_t)v1.function_index;
+            if (nr == 2) {
+                r.kind = 2;
+                r.score = (float)v0.count;
+            } else {
+                const float pair_offset = (float)(v1.count - v2.count);
+                if (pair_offset > 5.0f) {
+                    r.kind = 2;
+                    r.score = (float)v0.count;
+                    r.score_offset = pair_offset;
+                    r.weighted_score = v0.weighted_hits;
+                }
+            }
+        }
+    }
+    out[s] = r;
+}
+
+hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64_t *start, const uint32_t *count,
+                             kgx_call *ws, kgx_best_call *out, hipStream_t stream)
+{
+    if (n_seq == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(best_call_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, calls, start,
+                       count, ws, out);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
 /* gather: tiled hits / sparse calls -> dense CSR, one wave per sequence     */
 /* ------------------------------------------------------------------------ */
 

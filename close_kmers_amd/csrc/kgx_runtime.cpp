@@ -715,6 +715,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     c->hit_slots = cap_win;
     c->d_off = d_off;
     c->have_hits = false;
+    c->have_best = false;
     return KGX_OK;
 }
 
@@ -756,10 +757,57 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     else
         kgx_params_default(&p);
     HIP_TRY(hipSetDevice(c->img->device));
+    const bool best = (want & KGX_WANT_BEST) != 0;
     HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(),
                          c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
-                         want, c->stream));
+                         want | (best ? KGX_WANT_CALLS : 0u), c->stream));
+    c->have_best = false;
+    if (best) {
+        HIP_TRY(c->best.reserve(std::max<uint64_t>(c->n_seq, 1) * sizeof(kgx_best_call)));
+        HIP_TRY(c->best_ws.reserve(c->hit_slots * sizeof(kgx_call)));
+        HIP_TRY(launch_best_calls(c->n_seq, c->calls.as<kgx_call>(), c->wbase.as<uint64_t>(),
+                                  c->call_count.as<uint32_t>(), c->best_ws.as<kgx_call>(),
+                                  c->best.as<kgx_best_call>(), c->stream));
+        c->have_best = true;
+    }
+    return KGX_OK;
+}
+
+int kgx_find_best_calls(kgx_ctx *c, const kgx_call *calls, const uint64_t *call_offsets, uint32_t n_seq,
+                        kgx_best_call *out)
+{
+    if (!c || (n_seq && (!call_offsets || !out)))
+        return fail(KGX_EINVAL, "null argument");
+    if (n_seq == 0)
+        return KGX_OK;
+    const uint64_t c0 = call_offsets[0], n = call_offsets[n_seq] - c0;
+    if (n && !calls)
+        return fail(KGX_EINVAL, "null calls");
+    std::vector<uint64_t> start(n_seq);
+    std::vector<uint32_t> count(n_seq);
+    for (uint32_t s = 0; s < n_seq; s++) {
+        if (call_offsets[s + 1] < call_offsets[s])
+            return fail(KGX_EINVAL, "call_offsets not monotone");
+        start[s] = call_offsets[s] - c0;
+        count[s] = (uint32_t)(call_offsets[s + 1] - call_offsets[s]);
+    }
+    HIP_TRY(hipSetDevice(c->img->device));
+    HIP_TRY(c->bc_calls.reserve(std::max<uint64_t>(n, 1) * sizeof(kgx_call)));
+    HIP_TRY(c->best_ws.reserve(std::max<uint64_t>(n, 1) * sizeof(kgx_call)));
+    HIP_TRY(c->bc_start.reserve(n_seq * sizeof(uint64_t)));
+    HIP_TRY(c->bc_count.reserve(n_seq * sizeof(uint32_t)));
+    HIP_TRY(c->best.reserve(n_seq * sizeof(kgx_best_call)));
+    c->have_best = false; /* best[] now belongs to this call, not to the plan */
+    if (n)
+        HIP_TRY(hipMemcpyAsync(c->bc_calls.p, calls + c0, n * sizeof(kgx_call), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bc_start.p, start.data(), n_seq * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->bc_count.p, count.data(), n_seq * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_best_calls(n_seq, c->bc_calls.as<kgx_call>(), c->bc_start.as<uint64_t>(),
+                              c->bc_count.as<uint32_t>(), c->best_ws.as<kgx_call>(), c->best.as<kgx_best_call>(),
+                              c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->best.p, n_seq * sizeof(kgx_best_call), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return KGX_OK;
 }
 
@@ -776,6 +824,7 @@ int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
     out->hits_hot = c->hits.as<uint32_t>();
     out->hits_cold = c->hits.as<uint32_t>() + 4 * c->hit_slots;
     out->calls = c->calls.as<kgx_call>();
+    out->best = c->have_best ? c->best.as<kgx_best_call>() : nullptr;
     return KGX_OK;
 }
 
@@ -896,8 +945,9 @@ void otu_tallies(kgx_ctx *c, uint32_t n_seq, bool want_otu)
     }
 }
 
-void fill_result(kgx_ctx *c, uint32_t n_seq, bool need_hits, uint64_t nwin, kgx_result *out)
+void fill_result(kgx_ctx *c, uint32_t n_seq, bool need_hits, bool want_best, uint64_t nwin, kgx_result *out)
 {
+    out->best = want_best ? c->h_best.data() : nullptr;
     out->n_seq = n_seq;
     out->hit_offsets = c->h_hoff.data();
     out->hits = need_hits ? c->h_hits.data() : nullptr;
@@ -947,6 +997,8 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     uint64_t hbase = 0, cbase = 0, nwin = 0;
     HIP_TRY(c->h_hits.resize(0));
     HIP_TRY(c->h_calls.resize(0));
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
 
     /* Copies of both streams share the DMA engine in submission order, so the
      * order of submission is the schedule: chunk k+1's H2D goes in before
@@ -1029,6 +1081,16 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
                                            hipMemcpyDeviceToHost, x->stream));
             }
         }
+        if (want_best && n) {
+            if (c->host_copy) {
+                void *db = nullptr;
+                HIP_TRY(c->h_best.device_ptr(s0, &db));
+                HIP_TRY(launch_copy_to_host(db, x->best.p, n * sizeof(kgx_best_call), c->host_copy_blocks, x->stream));
+            } else {
+                HIP_TRY(hipMemcpyAsync(c->h_best.data() + s0, x->best.p, n * sizeof(kgx_best_call),
+                                       hipMemcpyDeviceToHost, x->stream));
+            }
+        }
         hbase += nh_all;
         cbase += nc;
         const auto t2 = now();
@@ -1051,7 +1113,7 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     c->have_hits = false;
     t->have_hits = false;
     otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
-    fill_result(c, n_seq, need_hits, nwin, out);
+    fill_result(c, n_seq, need_hits, (want & KGX_WANT_BEST) != 0, nwin, out);
     return KGX_OK;
 }
 
@@ -1073,7 +1135,7 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     /* chunks of at least 2M residues, only when there is something to copy back */
     const uint64_t k_res = std::max<uint64_t>(1, n_res >> 21);
     const uint32_t K = (uint32_t)std::min<uint64_t>({(uint64_t)c->host_chunks, k_res, (uint64_t)n_seq});
-    if (K >= 2 && (want & (KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU)))
+    if (K >= 2 && (want & (KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU | KGX_WANT_BEST)))
         return process_batch_chunked(c, params, residues, seq_offsets, n_seq, want, K, out);
     PhaseTimer tm(c);
     int rc = stage_host_seqs(c, residues, seq_offsets, 0, n_seq);
@@ -1148,13 +1210,20 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
         HIP_TRY(hipStreamSynchronize(c->stream));
     }
 
+    if ((want & KGX_WANT_BEST) && n_seq) {
+        if (!c->have_best)
+            return fail(KGX_EINVAL, "no device best calls (score with KGX_WANT_BEST)");
+        HIP_TRY(c->h_best.resize(n_seq));
+        HIP_TRY(hipMemcpyAsync(c->h_best.data(), c->best.p, n_seq * sizeof(kgx_best_call), hipMemcpyDeviceToHost,
+                               c->stream));
+    }
     tm.mark(" gather+d2h");
     otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
     uint64_t nwin = 0;
     HIP_TRY(hipMemcpyAsync(&nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    fill_result(c, n_seq, need_hits, nwin, out);
+    fill_result(c, n_seq, need_hits, (want & KGX_WANT_BEST) != 0, nwin, out);
     return KGX_OK;
 }
 

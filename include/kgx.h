@@ -43,6 +43,7 @@ extern "C" {
 #define KGX_WANT_HITS 1u  /* hit list (what hit_cb receives, kguts.cc:814-815) */
 #define KGX_WANT_CALLS 2u /* KmerCall runs (process_set_of_hits, kguts.cc:734-781) */
 #define KGX_WANT_OTU 4u   /* OTU tallies (KmerOtuStats, kguts.h:185-219) */
+#define KGX_WANT_BEST 8u  /* find_best_call per sequence, on the device (kgx_best_call) */
 
 /* ---- on-disk / in-HBM record layouts (kmer_image.h:11-23) -------------- */
 typedef struct kgx_image_header { /* kmer_memory_image_t */
@@ -87,6 +88,25 @@ typedef struct kgx_call {
     float weighted_hits;
 } kgx_call;
 
+/* What find_best_call (kguts.cc:1008-1199) decides for one sequence's calls,
+ * computed on the device.  The function names stay on the host:
+ *   kind 0  no calls: function_index -1, function "", score 0, weighted 0,
+ *           score_offset left as the caller had it (kguts.cc:1015-1018)
+ *   kind 1  called: function_index fi0, function = name(fi0)
+ *   kind 2  ambiguous pair: function_index -1, function = the lexically
+ *           larger of name(fi0), name(fi1) + " ?? " + the other
+ *   kind 3  no call: function_index -1, function "", score_offset written
+ * score / weighted_score / score_offset are the reference's values in every
+ * kind (fi0 / fi1 are the top two functions whenever there are two). */
+typedef struct kgx_best_call {
+    int32_t kind;
+    int32_t fi0;
+    int32_t fi1;
+    float score;
+    float weighted_score;
+    float score_offset;
+} kgx_best_call;
+
 /* one (otu_index, count) pair of KmerOtuStats::otus_by_count (kguts.h:214-218) */
 typedef struct kgx_otu {
     int32_t otu_index;
@@ -116,6 +136,7 @@ typedef struct kgx_result {
     const kgx_otu *otus;
     uint64_t n_windows; /* window positions, sum of max(0, len-8); those holding a
                            non-standard residue are skipped, not probed */
+    const kgx_best_call *best; /* n_seq entries with KGX_WANT_BEST, else NULL */
 } kgx_result;
 
 /* Device-resident results of kgx_run_device (pointers into HBM).
@@ -141,6 +162,7 @@ typedef struct kgx_device_result {
     const uint32_t *hits_hot;    /* 4 words per slot, capacity window_base[n_seq] slots */
     const uint32_t *hits_cold;   /* 4 words per slot */
     const kgx_call *calls;       /* capacity window_base[n_seq] */
+    const kgx_best_call *best;   /* n_seq, after a score stage with KGX_WANT_BEST, else NULL */
 } kgx_device_result;
 
 typedef struct kgx_image kgx_image;
@@ -268,7 +290,7 @@ int kgx_run_device(kgx_ctx *ctx, const kgx_params *params, const uint8_t *d_resi
 /* The stages kgx_run_device enqueues, for per-kernel timing:
  *   kgx_stage_plan   window/chunk bookkeeping (2 small kernels)
  *   kgx_stage_probe  encode + probe: the HBM random-access kernel
- *   kgx_stage_score  hit-run scorer (calls, OTU flags) */
+ *   kgx_stage_score  hit-run scorer (calls, OTU flags; find_best_call with KGX_WANT_BEST) */
 int kgx_stage_plan(kgx_ctx *ctx, const uint64_t *d_seq_offsets, uint32_t n_seq, uint64_t n_residues);
 int kgx_stage_probe(kgx_ctx *ctx, const uint8_t *d_residues, const uint64_t *d_seq_offsets);
 int kgx_stage_score(kgx_ctx *ctx, const kgx_params *params, uint32_t want);
@@ -289,6 +311,12 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
                        int n_names, int32_t *function_index, char *function, size_t function_cap,
                        float *score, float *weighted_score, float *score_offset,
                        int *score_offset_set);
+
+/* find_best_call for many sequences at once, on the context's device:
+ * sequence s owns calls[call_offsets[s] .. call_offsets[s+1]) (host arrays);
+ * out[n_seq] receives each decision (kgx_best_call).  Synchronous. */
+int kgx_find_best_calls(kgx_ctx *ctx, const kgx_call *calls, const uint64_t *call_offsets, uint32_t n_seq,
+                        kgx_best_call *out);
 
 /* Random-access ceiling of the context's image buffer: about n_reads
  * uniformly random records of the resident table read with many loads in

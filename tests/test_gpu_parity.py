@@ -614,12 +614,19 @@ def test_chunked_host_batch_matches_oracle(small_world, oracle_lib, gpu):
     off = np.cumsum(lens).astype(np.uint64) + np.uint64(2)
     res = np.concatenate([np.frombuffer(b"MK", np.uint8)] + seqs)
     want = oracle_lib.process_batch(table, res, off)
+    best_one_pass = None
     for k, hc in ((2, 1), (3, 0), (3, 1), (8, 1), (1, 1)):
         ctx.set_option("host_chunks", k)
         ctx.set_option("host_copy", hc)
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
         assert_same(got, want, len(off) - 1)
         assert np.array_equal(got.hits["seq"], want.hits["seq"])
+        gb = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=gpu.WANT_BEST | gpu.WANT_HITS)
+        if best_one_pass is None:
+            ctx.set_option("host_chunks", 1)
+            best_one_pass = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=gpu.WANT_BEST).best
+            ctx.set_option("host_chunks", k)
+        assert np.array_equal(gb.best, best_one_pass) and eq_fields(gb.hits, want.hits)
         for w in (1, 2):
             g = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=w)
             assert np.array_equal(g.hit_offsets, want.hit_offsets)
@@ -629,3 +636,87 @@ def test_chunked_host_batch_matches_oracle(small_world, oracle_lib, gpu):
                 assert np.array_equal(g.call_offsets, want.call_offsets)
     ctx.set_option("host_chunks", 3)
     ctx.set_option("host_copy", 1)
+
+
+# ---------------------------------------------------------------------------
+# find_best_call on the device (KGX_WANT_BEST, kgx_find_best_calls)
+
+def _best_as_reference(b, names):
+    """kgx_best_call -> find_best_call's (function_index, function, score,
+    weighted_score, score_offset or None), names as function_at_index."""
+    def name(i):
+        return names[i] if 0 <= i < len(names) else "INVALID_OFFSET"
+    kind = int(b["kind"])
+    fn, fi = "", -1
+    if kind == 1:
+        fi, fn = int(b["fi0"]), name(int(b["fi0"]))
+    elif kind == 2:
+        a, c = name(int(b["fi0"])), name(int(b["fi1"]))
+        if c > a:
+            a, c = c, a
+        fn = a + " ?? " + c
+    return (fi, fn, float(b["score"]), float(b["weighted_score"]),
+            None if kind == 0 else float(b["score_offset"]))
+
+
+def _same_decision(got, want):
+    f = np.float32
+    return (got[0] == want[0] and got[1] == want[1]
+            and f(got[2]).view(np.uint32) == f(want[2]).view(np.uint32)
+            and f(got[3]).view(np.uint32) == f(want[3]).view(np.uint32)
+            and (got[4] is None) == (want[4] is None)
+            and (got[4] is None or f(got[4]).view(np.uint32) == f(want[4]).view(np.uint32)))
+
+
+def test_device_best_call_on_crafted_lists(small_world, oracle_lib, gpu):
+    """Call lists built to hit every branch: collapses, F1|F2|F1 joins, weight
+    ties (partial_sort's tie order and the element left at index 2), one
+    function, ambiguous pairs with and without a clear third, unknown and
+    negative function indices, and empty lists."""
+    spec, table, img, ctx = small_world
+    rng = np.random.default_rng(23)
+    names = ["zeta kinase", "alpha protein", "Beta", "alpha protein", "", "gyrase B", "gyrase A"]
+    lists = []
+    for i in range(30000):
+        n = int(rng.integers(0, 9)) if i % 7 else int(rng.integers(0, 40))
+        fis = rng.integers(-1, 8, n) if i % 5 == 0 else rng.integers(0, 4, n)
+        cnt = rng.integers(1, 13, n)
+        wsets = [np.float32([1.0, 2.0, 3.0]), np.float32([0.1, 0.7, 1.3, 2.9]),
+                 rng.random(8).astype(np.float32) * 10]
+        wt = rng.choice(wsets[i % 3], n)
+        c = np.zeros(n, gpu.CALL_DTYPE)
+        c["start"] = np.arange(n) * 10
+        c["end"] = np.arange(n) * 10 + 7
+        c["count"] = cnt
+        c["function_index"] = fis.astype(np.int64).astype(np.uint32)
+        c["weighted_hits"] = wt
+        lists.append(c)
+    off = np.zeros(len(lists) + 1, np.uint64)
+    off[1:] = np.cumsum([len(c) for c in lists])
+    allc = np.concatenate(lists)
+    best = ctx.find_best_calls(allc, off)
+    bad = []
+    for i, c in enumerate(lists):
+        want = oracle_lib.find_best_call(c, names)
+        if not _same_decision(_best_as_reference(best[i], names), want):
+            bad.append((i, c, best[i], want))
+    assert not bad, (len(bad), bad[:3])
+    assert set(np.unique(best["kind"])) == {0, 1, 2, 3}
+
+
+def test_device_best_call_on_batches(small_world, oracle_lib, gpu):
+    spec, table, img, ctx = small_world
+    names = [f"function {i % 977}" for i in range(spec.n_src + 10)]
+    res, off = synth.make_queries(spec, 3000, x_permille=5)
+    for params in [(5, 200, 0, 0), (2, 50, 0, 0), (3, 200, 1, 0)]:
+        got = ctx.process_batch(res, off, gpu.Params(*params), want=gpu.WANT_BEST | gpu.WANT_CALLS)
+        want = oracle_lib.process_batch(table, res, off, params=params)
+        assert np.array_equal(got.call_offsets, want.call_offsets)
+        assert got.best is not None and len(got.best) == len(off) - 1
+        for s in range(len(off) - 1):
+            c = want.calls[int(want.call_offsets[s]):int(want.call_offsets[s + 1])]
+            ref = oracle_lib.find_best_call(c, names)
+            assert _same_decision(_best_as_reference(got.best[s], names), ref), s
+        # BEST alone (no calls copied back), and in chunks
+        only = ctx.process_batch(res, off, gpu.Params(*params), want=gpu.WANT_BEST)
+        assert len(only.calls) == 0 and np.array_equal(only.best, got.best)
