@@ -294,9 +294,16 @@ public:
     /* hit_lists[h] = (first, count) into list_ids for hit h */
     best_match_t find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
                                         const uint32_t *list_ids, std::vector<KmerCall> &calls);
+    /* the same with find_best_call decided on the device (KGX_WANT_BEST) */
+    best_match_t find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
+                                        const uint32_t *list_ids, const kgx_best_call &best);
     unsigned int kmer_hit_threshold_ = 3;
 
 private:
+    /* seq_score_ from the hits' family lists, then the family rollup for the
+     * called function (family_mapper.cc:46-205) */
+    best_match_t match_from(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists, const uint32_t *list_ids,
+                            std::string fn, float score);
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     std::unordered_map<KmerPegMapping::encoded_id_t, sequence_accumulated_score_t> seq_score_;
