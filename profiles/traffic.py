@@ -26,12 +26,20 @@ def per_dispatch(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            rows.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024.0)  # KiB
+            rows.setdefault(r["Kernel_Name"], []).append(
+                (int(r["Grid_Size"]), float(r["Counter_Value"]) * 1024.0))  # KiB
     return rows
 
 
-def mean_of(rows, pred):
-    vals = [v for k, vs in rows.items() if pred(k) for v in vs]
+def mean_of(rows, pred, full_grid_only=False):
+    """Mean counter value over the dispatches of the matching kernels.  With
+    full_grid_only, only the largest grid counts: bench.py's timed batch, not
+    the smaller chunks of its host-buffer leg."""
+    vals = [gv for k, vs in rows.items() if pred(k) for gv in vs]
+    if full_grid_only and vals:
+        g = max(gv[0] for gv in vals)
+        vals = [gv for gv in vals if gv[0] == g]
+    vals = [v for _, v in vals]
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
@@ -40,8 +48,8 @@ def main():
     bench = json.loads(open(bjson).read().strip().splitlines()[-1])
     fetch, write = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
     is_probe = lambda k: "probe_kernel" in k or "probe_line_kernel" in k
-    pf, nf = mean_of(fetch, is_probe)
-    pw, nw = mean_of(write, is_probe)
+    pf, nf = mean_of(fetch, is_probe, True)
+    pw, nw = mean_of(write, is_probe, True)
     calib = {}
     ceil = (bench.get("roofline") or {}).get("random_read_ceiling") or {}
     for mode, name in ((0, "bucket24"), (1, "key8"), (2, "sector64"), (3, "rec16"), (4, "line64")):
