@@ -57,7 +57,10 @@ class DeviceResult(ctypes.Structure):
                 ("window_base", ctypes.c_void_p), ("hit_mask", ctypes.c_void_p),
                 ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
                 ("hits_hot", ctypes.c_void_p), ("hits_cold", ctypes.c_void_p),
-                ("calls", ctypes.c_void_p), ("best", ctypes.c_void_p)]
+                ("calls", ctypes.c_void_p), ("best", ctypes.c_void_p), ("hit_format", ctypes.c_uint32)]
+
+
+HIT_PLANES, HIT_PACKED16 = 0, 1
 
 
 def hits_from_planes(hot: np.ndarray, cold: np.ndarray) -> np.ndarray:
@@ -80,10 +83,27 @@ class Fragments(ctypes.Structure):
                 ("frame_counts", ctypes.c_void_p)]
 
 
+def hits_from_packed(recs: np.ndarray) -> np.ndarray:
+    """kgx_hit records (pos and seq 0) from HIT_PACKED16 records (uint32
+    [n, 4]: the table's packed record, flags in bits 28-30 of word 3)."""
+    r = np.asarray(recs, np.uint32).reshape(-1, 4).astype(np.uint64)
+    lo = r[:, 0] | (r[:, 1] << np.uint64(32))
+    out = np.zeros(len(r), HIT_DTYPE)
+    out["which_kmer"] = lo & np.uint64((1 << 35) - 1)
+    out["function_index"] = (((r[:, 1] >> np.uint64(3)) & np.uint64(0xFFFFF)).astype(np.int64) - 1).astype(np.int32)
+    otu = ((r[:, 1] >> np.uint64(23)) & np.uint64(0x1FF)) | (((r[:, 3] >> np.uint64(16)) & np.uint64(0xFFF)) << np.uint64(9))
+    out["otu_index"] = (otu.astype(np.int64) - 1).astype(np.int32)
+    out["function_wt"] = r[:, 2].astype(np.uint32).view(np.float32)
+    out["avg_from_end"] = (r[:, 3] & np.uint64(0xFFFF)).astype(np.uint16)
+    out["flags"] = ((r[:, 3] >> np.uint64(28)) & np.uint64(7)).astype(np.uint16)
+    return out
+
+
 def tiled_hits_per_sequence(window_base: np.ndarray, hit_mask: np.ndarray, tile_windows: int,
-                            hits: np.ndarray) -> list[np.ndarray]:
+                            hits: np.ndarray, fill_pos: bool = False) -> list[np.ndarray]:
     """Host-side walk of kgx_device_result's tiled hit layout (for tests and
-    tools): the hit records of every sequence, in position order."""
+    tools): the hit records of every sequence, in position order.  fill_pos
+    sets pos and seq from the hits' mask bits (HIT_PACKED16 stores neither)."""
     J = tile_windows // 64
     pc = np.array([bin(int(x)).count("1") for x in hit_mask], dtype=np.int64)
     out = []
@@ -98,7 +118,12 @@ def tiled_hits_per_sequence(window_base: np.ndarray, hit_mask: np.ndarray, tile_
             full = int(hit_mask[g])
             sel = full & (((1 << hi) - 1) & ~((1 << lo) - 1))
             start = t * tile_windows + pre + bin(full & ((1 << lo) - 1)).count("1")
-            parts.append(hits[start:start + bin(sel).count("1")])
+            part = hits[start:start + bin(sel).count("1")]
+            if fill_pos:
+                part = part.copy()
+                part["pos"] = [64 * g + b - gw0 for b in range(64) if sel >> b & 1]
+                part["seq"] = s
+            parts.append(part)
         out.append(np.concatenate(parts) if parts else hits[:0])
     return out
 

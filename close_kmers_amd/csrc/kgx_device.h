@@ -60,6 +60,57 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi)
     return upto_hi & ~below_lo;
 }
 
+/* ---- hit records (kgx_internal.h: HIT_PLANES / HIT_PACKED16) ---- */
+
+/* the fields of one hit record (hot = plane 0 / the packed record,
+ * cold = plane 1, unused for PACKED16) */
+template <bool PK> struct HitFields {
+    __device__ __forceinline__ static uint32_t avg(const uint4 &h) { return PK ? (h.w & 0xFFFFu) : (h.x & 0xFFFFu); }
+    __device__ __forceinline__ static uint32_t fi(const uint4 &h) { return PK ? ((h.y >> 3) & 0xFFFFFu) - 1u : h.y; }
+    __device__ __forceinline__ static uint32_t wt(const uint4 &h) { return h.z; }
+    /* the dword that carries the flags, its flag-free value, the flag shift */
+    static constexpr int FLAG_DWORD = PK ? 3 : 0;
+    static constexpr int FLAG_SHIFT = PK ? 28 : 16;
+    __device__ __forceinline__ static uint32_t flag_base(const uint4 &h) { return PK ? (h.w & 0x0FFFFFFFu) : (h.x & 0xFFFFu); }
+    __device__ __forceinline__ static uint32_t flags(const uint4 &h) { return PK ? (h.w >> 28) & 7u : (h.x >> 16) & 0xFFFFu; }
+    __device__ __forceinline__ static uint64_t key(const uint4 &h, const uint4 &c)
+    {
+        return PK ? (((uint64_t)h.y << 32 | h.x) & PACK_KEY_MASK) : ((uint64_t)c.y << 32 | c.x);
+    }
+    __device__ __forceinline__ static uint32_t otu(const uint4 &h, const uint4 &c)
+    {
+        return PK ? (((h.y >> 23) & 0x1FFu) | (((h.w >> 16) & 0xFFFu) << 9)) - 1u : c.z;
+    }
+};
+
+/* the window (global index) of hit i of `tile`: the i-th set bit of the
+ * tile's J mask words */
+__device__ __forceinline__ uint64_t hit_window(const uint64_t *__restrict__ mask, uint64_t tile, uint32_t J,
+                                               uint32_t i)
+{
+    for (uint32_t j = 0; j < J; j++) {
+        uint64_t m = mask[tile * J + j];
+        const uint32_t pc = (uint32_t)__popcll(m);
+        if (i < pc) {
+            for (; i; i--)
+                m &= m - 1;
+            return 64 * (tile * J + j) + (uint64_t)__builtin_ctzll(m);
+        }
+        i -= pc;
+    }
+    return ~0ull; /* not reached for i < the tile's hit count */
+}
+
+/* the sequence owning global window g, walking on from the tile's first */
+__device__ __forceinline__ uint32_t window_seq(const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq,
+                                               uint64_t tile, uint64_t g)
+{
+    uint32_t s = tile_seq[tile];
+    while (wbase[s + 1] <= g)
+        s++;
+    return s;
+}
+
 }  // namespace kgx
 
 #endif

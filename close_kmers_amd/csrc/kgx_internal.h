@@ -31,6 +31,16 @@ constexpr int RUN_CAP = 40000 - 2;               /* MAX_HITS_PER_SEQ - 2, kguts.
  * (everything the run scorer reads) and cold = {which_kmer lo, hi, otu, seq}.
  */
 constexpr int PROBE_WAVES = 4; /* waves per 256-thread workgroup */
+/* Hit record formats (kgx_device_result.hit_format):
+ *   HIT_PLANES   (AOS24 images) the two planes above;
+ *   HIT_PACKED16 (PACKED16 images) one plane: the matching table record
+ *     itself (layout below), flags in bits [60,63) of hi (dword 3 bits
+ *     28-30), which the packed layout leaves 0.  Position and sequence are
+ *     not stored: they follow from the hit's window (hit_mask bit) -- half
+ *     the probe's hit-store traffic.
+ * Either way the consumers (scorer, gather, k-mer tables) take a hit's
+ * position from its mask bit. */
+constexpr uint32_t HIT_PLANES = KGX_HIT_PLANES, HIT_PACKED16 = KGX_HIT_PACKED16;
 /* probe variants (kgx_ctx_set_option "probe_variant") */
 constexpr int PROBE_BUCKET = 0;    /* key + payload per bucket examined */
 constexpr int PROBE_KEY_FIRST = 1; /* keys only; payload for the matching bucket */
@@ -151,12 +161,12 @@ hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                         uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
-                        uint32_t want, hipStream_t stream);
+                        uint32_t want, uint32_t hit_format, hipStream_t stream);
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
-                         uint32_t seq_base, hipStream_t stream);
+                         uint32_t seq_base, uint32_t hit_format, hipStream_t stream);
 /* find_best_call per sequence: calls[start[s] ..+ count[s]), ws same extent */
 hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64_t *start, const uint32_t *count,
                              kgx_call *ws, kgx_best_call *out, hipStream_t stream);

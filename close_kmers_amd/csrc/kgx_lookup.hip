@@ -230,9 +230,10 @@ __device__ __forceinline__ void encode_tile(const uint8_t *__restrict__ residues
     }
 }
 
-/* ordered compaction of a tile's hits into the two planes; one mask word
- * per slice.  pv = the matching PACKED16 record (PACKED) or the 16 B after
- * the key of the matching AOS24 bucket */
+/* ordered compaction of a tile's hits; one mask word per slice.  PACKED:
+ * pv = the matching PACKED16 record, stored as is (HIT_PACKED16); else pv =
+ * the 16 B after the key of the matching AOS24 bucket, stored as the two
+ * planes (HIT_PLANES) */
 template <int J, bool PACKED>
 __device__ __forceinline__ void store_tile_hits(const bool *hit, const uint64_t *kv, const uint4 *pv,
                                                 const uint32_t *pos, const uint32_t *sq, uint64_t g0,
@@ -247,11 +248,7 @@ __device__ __forceinline__ void store_tile_hits(const bool *hit, const uint64_t 
         if (hit[j]) {
             const uint64_t at = g0 + count + lanes_below(m);
             if (PACKED) {
-                /* unpack_bucket (kgx_internal.h) of the record in pv */
-                const uint32_t otu = ((pv[j].y >> 23) & 0x1FFu) | (((pv[j].w >> 16) & 0xFFFu) << 9);
-                const uint32_t fi = (pv[j].y >> 3) & 0xFFFFFu;
-                hot[at] = make_uint4(pv[j].w & 0xFFFFu, fi - 1u, pv[j].z, pos[j]);
-                cold[at] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), otu - 1u, sq[j]);
+                hot[at] = pv[j]; /* HIT_PACKED16: the table record itself */
             } else {
                 hot[at] = make_uint4(pv[j].y & 0xFFFFu, pv[j].z, pv[j].w, pos[j]);
                 cold[at] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, sq[j]);
@@ -695,9 +692,11 @@ __device__ __forceinline__ uint32_t for_each_run(const uint64_t *__restrict__ hi
             next = hit_mask[g + 1]; /* in flight while f works on word g */
         const uint32_t lo = g == gfirst ? (uint32_t)(gw0 & 63) : 0u;
         const uint32_t hi = g == glast ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
-        const uint32_t cnt = (uint32_t)__popcll(full & bit_range(lo, hi));
-        if (cnt)
-            f(tile * tile_windows + pre + (uint32_t)__popcll(full & bit_range(0, lo)), cnt, ordinal);
+        const uint64_t bits = full & bit_range(lo, hi);
+        const uint32_t cnt = (uint32_t)__popcll(bits);
+        if (cnt) /* the hits' positions: bit b of `bits` is position 64 g + b - gw0 */
+            f(tile * tile_windows + pre + (uint32_t)__popcll(full & bit_range(0, lo)), cnt, ordinal, bits,
+              (uint32_t)(64 * g - gw0));
         ordinal += cnt;
         pre += (uint32_t)__popcll(full);
     }
@@ -730,13 +729,13 @@ struct RunTail {
     uint32_t pos, fI, idx;
     float wt;
     uint32_t avg;
+    uint32_t fb; /* the record's flag dword without flags */
     uint64_t at; /* storage index */
 };
 
 constexpr int SCORE_BATCH = 8;
-constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << 16, F_CNT = KGX_HIT_COUNTED << 16,
-                   F_OTU = KGX_HIT_OTU << 16;
 
+template <bool PK>
 __global__ __launch_bounds__(256) void score_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
@@ -752,19 +751,23 @@ __global__ __launch_bounds__(256) void score_kernel(
     if (!want_calls && !want_otu) {
         /* process_set_of_hits returns before doing anything (kguts.cc:737) */
         hit_count[s] = for_each_run(hit_mask, tile_windows, gw0, gw1,
-                                    [](uint64_t, uint32_t, uint32_t) {});
+                                    [](uint64_t, uint32_t, uint32_t, uint64_t, uint32_t) {});
         call_count[s] = 0;
         return;
     }
 
-    uint32_t *hw = reinterpret_cast<uint32_t *>(hot); /* 4 dwords per hit, flags in dword 0 */
+    typedef HitFields<PK> HF;
+    constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << HF::FLAG_SHIFT, F_CNT = KGX_HIT_COUNTED << HF::FLAG_SHIFT,
+                       F_OTU = KGX_HIT_OTU << HF::FLAG_SHIFT;
+    constexpr int FD = HF::FLAG_DWORD;
+    uint32_t *hw = reinterpret_cast<uint32_t *>(hot); /* 4 dwords per hit, flags in dword FD */
     const uint64_t cbase = gw0; /* calls / ranges of s live at [gw0, ...) */
     const uint32_t gap = (uint32_t)prm.max_gap;
     int n = 0;
     uint32_t cur = 0, first_pos = 0, last_pos = 0, last_idx = 0, run_start = 0;
     int cnt = 0;
     float wsum = 0.0f;
-    RunTail p1 = {0, 0, 0, 0.0f, 0, 0}, p2 = {0, 0, 0, 0.0f, 0, 0};
+    RunTail p1 = {0, 0, 0, 0.0f, 0, 0, 0}, p2 = {0, 0, 0, 0.0f, 0, 0, 0};
     uint32_t ncalls = 0;
 
     auto flush = [&]() {
@@ -795,19 +798,19 @@ __global__ __launch_bounds__(256) void score_kernel(
             last_pos = p1.pos;
             last_idx = p1.idx;
             if (want_otu) {
-                hw[4 * p2.at] = p2.avg | F_RUN | F_CNT;
-                hw[4 * p1.at] = p1.avg | F_RUN | F_CNT;
+                hw[4 * p2.at + FD] = p2.fb | F_RUN | F_CNT;
+                hw[4 * p1.at + FD] = p1.fb | F_RUN | F_CNT;
             }
         } else {
             n = 0;
         }
     };
 
-    auto step = [&](const uint4 &r, uint32_t i, uint64_t at) {
-        const uint32_t avg = r.x & 0xFFFFu;
-        const uint32_t fI = r.y;
-        const float wt = __uint_as_float(r.z);
-        const uint32_t pos = r.w;
+    auto step = [&](const uint4 &r, uint32_t i, uint64_t at, uint32_t pos) {
+        const uint32_t avg = HF::avg(r);
+        const uint32_t fI = HF::fi(r);
+        const float wt = __uint_as_float(HF::wt(r));
+        const uint32_t fb = HF::flag_base(r);
         /* gap rule (kguts.cc:821-831), unsigned arithmetic */
         if (n > 0 && p1.pos + gap < pos) {
             if (n >= prm.min_hits)
@@ -832,7 +835,7 @@ __global__ __launch_bounds__(256) void score_kernel(
                 n++;
                 const bool counted = fI == cur;
                 if (want_otu) /* flags only feed the OTU pass */
-                    hw[4 * at] = avg | F_RUN | (counted ? F_CNT : 0u);
+                    hw[4 * at + FD] = fb | F_RUN | (counted ? F_CNT : 0u);
                 if (counted) {
                     cnt++;
                     wsum += wt;
@@ -840,7 +843,7 @@ __global__ __launch_bounds__(256) void score_kernel(
                     last_idx = i;
                 }
                 p2 = p1;
-                p1 = RunTail{pos, fI, i, wt, avg, at};
+                p1 = RunTail{pos, fI, i, wt, avg, fb, at};
             }
             /* pair switch (kguts.cc:852-856) */
             if (n > 1 && cur != fI && p2.fI == p1.fI)
@@ -854,11 +857,11 @@ __global__ __launch_bounds__(256) void score_kernel(
     auto load_batch = [&](uint4 *rb, uint64_t at0, uint32_t b, uint32_t c) {
 #pragma unroll
         for (int k = 0; k < SCORE_BATCH; k++)
-            if (b + k < c) /* avg|flags, fI, wt, pos */
+            if (b + k < c)
                 rb[k] = hot[at0 + b + k];
     };
     const uint32_t nh = for_each_run(hit_mask, tile_windows, gw0, gw1,
-                                     [&](uint64_t at0, uint32_t c, uint32_t ord0) {
+                                     [&](uint64_t at0, uint32_t c, uint32_t ord0, uint64_t bits, uint32_t pbase) {
         uint4 ra[SCORE_BATCH], rb[SCORE_BATCH];
         load_batch(ra, at0, 0, c);
         for (uint32_t b = 0; b < c; b += 2 * SCORE_BATCH) {
@@ -866,16 +869,21 @@ __global__ __launch_bounds__(256) void score_kernel(
                 load_batch(rb, at0, b + SCORE_BATCH, c);
 #pragma unroll
             for (int k = 0; k < SCORE_BATCH; k++)
-                if (b + k < c)
-                    step(ra[k], ord0 + b + k, at0 + b + k);
+                if (b + k < c) {
+                    step(ra[k], ord0 + b + k, at0 + b + k, pbase + (uint32_t)__builtin_ctzll(bits));
+                    bits &= bits - 1;
+                }
             if (b + SCORE_BATCH >= c)
                 break;
             if (b + 2 * SCORE_BATCH < c)
                 load_batch(ra, at0, b + 2 * SCORE_BATCH, c);
 #pragma unroll
             for (int k = 0; k < SCORE_BATCH; k++)
-                if (b + SCORE_BATCH + k < c)
-                    step(rb[k], ord0 + b + SCORE_BATCH + k, at0 + b + SCORE_BATCH + k);
+                if (b + SCORE_BATCH + k < c) {
+                    step(rb[k], ord0 + b + SCORE_BATCH + k, at0 + b + SCORE_BATCH + k,
+                         pbase + (uint32_t)__builtin_ctzll(bits));
+                    bits &= bits - 1;
+                }
         }
     });
     if (n >= prm.min_hits) /* kguts.cc:873-876 */
@@ -889,7 +897,8 @@ __global__ __launch_bounds__(256) void score_kernel(
         uint32_t ci = 0;
         uint2 rg = ranges[cbase];
         const uint32_t end = ranges[cbase + ncalls - 1].y;
-        for_each_run(hit_mask, tile_windows, gw0, gw1, [&](uint64_t at0, uint32_t c, uint32_t ord0) {
+        for_each_run(hit_mask, tile_windows, gw0, gw1,
+                     [&](uint64_t at0, uint32_t c, uint32_t ord0, uint64_t, uint32_t) {
             for (uint32_t k = 0; k < c; k++) {
                 const uint32_t i = ord0 + k;
                 if (i > end)
@@ -897,9 +906,9 @@ __global__ __launch_bounds__(256) void score_kernel(
                 while (i > rg.y) /* i <= end keeps ci < ncalls */
                     rg = ranges[cbase + ++ci];
                 if (i >= rg.x) {
-                    const uint32_t f = hw[4 * (at0 + k)];
+                    const uint32_t f = hw[4 * (at0 + k) + FD];
                     if (f & F_CNT)
-                        hw[4 * (at0 + k)] = f | F_OTU;
+                        hw[4 * (at0 + k) + FD] = f | F_OTU;
                 }
             }
         });
@@ -909,13 +918,18 @@ __global__ __launch_bounds__(256) void score_kernel(
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                         uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params,
-                        uint32_t want, hipStream_t stream)
+                        uint32_t want, uint32_t hit_format, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(score_kernel, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
-                       hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
-                       call_count, params, want);
+    if (hit_format == HIT_PACKED16)
+        hipLaunchKernelGGL(score_kernel<true>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
+                           hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
+                           call_count, params, want);
+    else
+        hipLaunchKernelGGL(score_kernel<false>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
+                           hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
+                           call_count, params, want);
     return hipGetLastError();
 }
 
@@ -1074,6 +1088,7 @@ hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64
 /* gather: tiled hits / sparse calls -> dense CSR, one wave per sequence     */
 /* ------------------------------------------------------------------------ */
 
+template <bool PK>
 __global__ __launch_bounds__(256) void gather_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
@@ -1093,7 +1108,7 @@ __global__ __launch_bounds__(256) void gather_kernel(
         for (uint64_t gb = gfirst; gb <= glast; gb += 64) {
             /* lane l takes mask word gb + l: its run inside the tile */
             const uint64_t g = gb + lane;
-            uint64_t at = 0;
+            uint64_t at = 0, bits = 0;
             uint32_t cnt = 0;
             if (g <= glast) {
                 const uint64_t tile = g / J;
@@ -1103,7 +1118,8 @@ __global__ __launch_bounds__(256) void gather_kernel(
                 const uint64_t full = hit_mask[g];
                 const uint32_t lo = g == gfirst ? (uint32_t)(gw0 & 63) : 0u;
                 const uint32_t hi = g == glast ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
-                cnt = (uint32_t)__popcll(full & bit_range(lo, hi));
+                bits = full & bit_range(lo, hi);
+                cnt = (uint32_t)__popcll(bits);
                 at = tile * tile_windows + pre + (uint32_t)__popcll(full & bit_range(0, lo));
             }
             /* exclusive prefix of cnt over the wave */
@@ -1115,10 +1131,22 @@ __global__ __launch_bounds__(256) void gather_kernel(
             }
             const uint64_t dst0 = hoff[s] + done + (incl - cnt);
             uint4 *dst = reinterpret_cast<uint4 *>(hits_out + dst0);
-            for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its two planes */
-                const uint4 h = hot[at + i], c = cold[at + i];
-                dst[2 * i] = make_uint4(c.x, c.y, c.z, h.x);
-                dst[2 * i + 1] = make_uint4(h.y, h.z, h.w, c.w + seq_base);
+            const uint32_t pbase = (uint32_t)(64 * g - gw0);
+            for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its record(s) */
+                const uint4 h = hot[at + i];
+                const uint32_t pos = pbase + (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                if (PK) {
+                    typedef HitFields<true> HF;
+                    const uint64_t k = HF::key(h, h);
+                    dst[2 * i] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), HF::otu(h, h),
+                                            HF::avg(h) | HF::flags(h) << 16);
+                    dst[2 * i + 1] = make_uint4(HF::fi(h), HF::wt(h), pos, s + seq_base);
+                } else {
+                    const uint4 c = cold[at + i];
+                    dst[2 * i] = make_uint4(c.x, c.y, c.z, h.x);
+                    dst[2 * i + 1] = make_uint4(h.y, h.z, pos, s + seq_base);
+                }
             }
             done += __shfl(incl, 63);
         }
@@ -1135,13 +1163,19 @@ __global__ __launch_bounds__(256) void gather_kernel(
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
-                         kgx_hit *hits_out, kgx_call *calls_out, uint32_t seq_base, hipStream_t stream)
+                         kgx_hit *hits_out, kgx_call *calls_out, uint32_t seq_base, uint32_t hit_format,
+                         hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(gather_kernel, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
-                       hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                       calls_out, seq_base);
+    if (hit_format == HIT_PACKED16)
+        hipLaunchKernelGGL(gather_kernel<true>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
+                           hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
+                           calls_out, seq_base);
+    else
+        hipLaunchKernelGGL(gather_kernel<false>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
+                           hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
+                           calls_out, seq_base);
     return hipGetLastError();
 }
 

@@ -169,6 +169,7 @@ struct kgx_ctx {
     uint64_t hit_slots = 0; /* slots per hit plane: cold plane at hits + hit_slots */
     const uint64_t *d_off = nullptr;
     bool have_hits = false; /* the tiled hits of the current plan are on the device */
+    uint32_t hit_format = kgx::HIT_PLANES; /* of the current plan's hits (set by the probe) */
     bool have_best = false; /* best[] holds find_best_call of the current plan */
     kgx::DevBuf best, best_ws, bc_calls, bc_start, bc_count; /* KGX_WANT_BEST / kgx_find_best_calls */
     kgx::PinnedVec<kgx_best_call> h_best;

@@ -700,7 +700,9 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->wbase.reserve((n_seq + 1) * sizeof(uint64_t)));
     HIP_TRY(c->tile_seq.reserve(max_tiles * sizeof(uint32_t)));
     HIP_TRY(c->hit_mask.reserve((cap_win / 64 + 2) * sizeof(uint64_t)));
-    HIP_TRY(c->hits.reserve(cap_win * 2 * sizeof(uint4))); /* hot plane, then cold plane */
+    /* HIT_PACKED16: one 16-B record per slot; HIT_PLANES: hot plane, then cold plane */
+    const bool packed_hits = c->img->layout == KGX_LAYOUT_PACKED16;
+    HIP_TRY(c->hits.reserve(cap_win * (packed_hits ? 1 : 2) * sizeof(uint4)));
     HIP_TRY(c->calls.reserve(cap_win * sizeof(kgx_call)));
     HIP_TRY(c->ranges.reserve(cap_win * 2 * sizeof(uint32_t)));
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
@@ -743,6 +745,8 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
         HIP_TRY(hipEventRecord(c->probe_done, c->stream));
         img->last_probe = c->probe_done;
     }
+    /* every PACKED16 probe stores the matching record itself */
+    c->hit_format = c->img->layout == KGX_LAYOUT_PACKED16 ? HIT_PACKED16 : HIT_PLANES;
     c->have_hits = true;
     return KGX_OK;
 }
@@ -761,7 +765,7 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(),
                          c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
-                         want | (best ? KGX_WANT_CALLS : 0u), c->stream));
+                         want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->stream));
     c->have_best = false;
     if (best) {
         HIP_TRY(c->best.reserve(std::max<uint64_t>(c->n_seq, 1) * sizeof(kgx_best_call)));
@@ -822,7 +826,8 @@ int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
     out->hit_count = c->hit_count.as<uint32_t>();
     out->call_count = c->call_count.as<uint32_t>();
     out->hits_hot = c->hits.as<uint32_t>();
-    out->hits_cold = c->hits.as<uint32_t>() + 4 * c->hit_slots;
+    out->hits_cold = c->hit_format == HIT_PLANES ? c->hits.as<uint32_t>() + 4 * c->hit_slots : nullptr;
+    out->hit_format = c->hit_format;
     out->calls = c->calls.as<kgx_call>();
     out->best = c->have_best ? c->best.as<kgx_best_call>() : nullptr;
     return KGX_OK;
@@ -1061,7 +1066,7 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
                                   x->hits.as<uint4>() + x->hit_slots, x->calls.as<kgx_call>(),
                                   x->dense_hoff.as<uint64_t>(), x->dense_coff.as<uint64_t>(),
                                   nh ? x->dense_hits.as<kgx_hit>() : nullptr,
-                                  nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->stream));
+                                  nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->hit_format, x->stream));
             if (c->host_copy) {
                 void *dh = nullptr, *dc = nullptr;
                 if (nh) {
@@ -1200,7 +1205,8 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                               c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
                               c->dense_coff.as<uint64_t>(),
                               need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
-                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, 0u, c->stream));
+                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, 0u, c->hit_format,
+                              c->stream));
         if (need_hits && nh)
             HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
                                    hipMemcpyDeviceToHost, c->stream));

@@ -90,12 +90,38 @@ __device__ __forceinline__ bool kmap_row(const KmapView &m, uint64_t kmer, uint6
 
 /* the tiled device result of a context (kgx_device_result) */
 struct Tiled {
-    const uint4 *cold; /* {which_kmer lo, hi, otu, seq} per slot */
+    const uint4 *hot;  /* the hit records (HIT_PACKED16) or plane 0 */
+    const uint4 *cold; /* HIT_PLANES: {which_kmer lo, hi, otu, seq} per slot */
     const uint64_t *mask;
     const uint64_t *wbase;
+    const uint32_t *tile_seq;
     uint32_t n_seq;
     uint32_t T; /* windows per tile */
+    bool packed;
 };
+
+/* k-mer and sequence of hit i of `tile` */
+__device__ __forceinline__ void hit_key_seq(const Tiled &t, uint64_t tile, uint32_t i, uint64_t &key, uint32_t &seq)
+{
+    const uint64_t slot = tile * t.T + i;
+    if (t.packed) {
+        key = HitFields<true>::key(t.hot[slot], t.hot[slot]);
+        seq = window_seq(t.wbase, t.tile_seq, tile, hit_window(t.mask, tile, t.T / 64, i));
+    } else {
+        const uint4 h = t.cold[slot];
+        key = (uint64_t)h.y << 32 | h.x;
+        seq = h.w;
+    }
+}
+
+__device__ __forceinline__ uint64_t hit_key(const Tiled &t, uint64_t tile, uint32_t i)
+{
+    const uint64_t slot = tile * t.T + i;
+    if (t.packed)
+        return HitFields<true>::key(t.hot[slot], t.hot[slot]);
+    const uint4 h = t.cold[slot];
+    return (uint64_t)h.y << 32 | h.x;
+}
 
 __device__ __forceinline__ uint32_t tile_count(const Tiled &t, uint64_t tile)
 {
@@ -130,10 +156,12 @@ __global__ void hits_to_pairs_kernel(Tiled t, uint64_t n_tiles, const uint32_t *
     const uint32_t i = (uint32_t)(slot % t.T);
     if (tile >= n_tiles || i >= tile_base[tile + 1] - tile_base[tile])
         return;
-    const uint4 h = t.cold[tile * t.T + i];
+    uint64_t key;
+    uint32_t seq;
+    hit_key_seq(t, tile, i, key, seq);
     const uint64_t at = tile_base[tile] + i;
-    kmers[at] = (uint64_t)h.y << 32 | h.x;
-    ids[at] = seq_ids[h.w];
+    kmers[at] = key;
+    ids[at] = seq_ids[seq];
 }
 
 __global__ void expand_rows_kernel(const uint64_t *keys, const uint64_t *starts, uint64_t n_rows,
@@ -250,8 +278,7 @@ __global__ void matrix_events_kernel(Tiled t, uint64_t n_tiles, KmapView m, unsi
     uint64_t ev = 0;
     if (tile < n_tiles && i < tile_count(t, tile)) {
         uint64_t a = 0, b = 0;
-        const uint4 h = t.cold[tile * t.T + i];
-        if (kmap_row(m, (uint64_t)h.y << 32 | h.x, a, b))
+        if (kmap_row(m, hit_key(t, tile, i), a, b))
             ev = b - a;
     }
     /* one atomic per wave */
@@ -271,12 +298,14 @@ __global__ void matrix_pairs_kernel(Tiled t, uint64_t n_tiles, KmapView m, const
     const uint32_t i = (uint32_t)(slot % t.T);
     if (tile >= n_tiles || i >= tile_count(t, tile))
         return;
-    const uint4 h = t.cold[tile * t.T + i];
+    uint64_t key;
+    uint32_t seq;
+    hit_key_seq(t, tile, i, key, seq);
     uint64_t a = 0, b = 0;
-    if (!kmap_row(m, (uint64_t)h.y << 32 | h.x, a, b))
+    if (!kmap_row(m, key, a, b))
         return; /* matrix_request.cc:159 reports "no mapping" on stderr */
-    const uint32_t e = seq_ids[h.w];
-    const uint64_t my_ord = base + h.w;
+    const uint32_t e = seq_ids[seq];
+    const uint64_t my_ord = base + seq;
     for (uint64_t j = a; j < b; j++) {
         const uint32_t f = m.vals[j];
         if (f == e)
@@ -473,11 +502,14 @@ int kmap_expand(kgx_kmap *m, DevBuf &d_k, DevBuf &d_v, uint64_t extra, hipStream
 Tiled tiled_of(const kgx_ctx *c)
 {
     Tiled t;
+    t.hot = c->hits.as<uint4>();
     t.cold = c->hits.as<uint4>() + c->hit_slots;
     t.mask = c->hit_mask.as<uint64_t>();
     t.wbase = c->wbase.as<uint64_t>();
+    t.tile_seq = c->tile_seq.as<uint32_t>();
     t.n_seq = c->n_seq;
     t.T = c->tile_windows;
+    t.packed = c->hit_format == HIT_PACKED16;
     return t;
 }
 

@@ -146,10 +146,15 @@ typedef struct kgx_result {
  * are stored compacted in window order from slot t * tile_windows, and bit i
  * of hit_mask[g] is set when global window 64*g + i hit.  So the hits of a
  * sequence are, word by word of its mask range, contiguous stretches of its
- * tiles' hit lists.  A hit is two 16-byte records at the same slot, in two
- * planes, so that the run scorer reads only what it uses:
- *   hits_hot[i]  = {avg_from_end | flags << 16, function_index, function_wt, pos}
- *   hits_cold[i] = {which_kmer (low, high 32 bits), otu_index, seq}
+ * tiles' hit lists, and a hit's window (hence its sequence and position)
+ * is its mask bit.  Hit records, by hit_format:
+ *   KGX_HIT_PACKED16 (PACKED16 images): one 16-byte record per slot in
+ *     hits_hot, the matching table record itself (kgx_image_set_layout's
+ *     packed layout), flags (KGX_HIT_*) in bits 28-30 of its 4th word;
+ *     hits_cold is NULL;
+ *   KGX_HIT_PLANES (AOS24 images): two 16-byte records at the same slot:
+ *     hits_hot[i]  = {avg_from_end | flags << 16, function_index, function_wt, pos}
+ *     hits_cold[i] = {which_kmer (low, high 32 bits), otu_index, seq}
  * Calls of s are contiguous from calls[window_base[s]]; counts are
  * hit_count[s] / call_count[s]. */
 typedef struct kgx_device_result {
@@ -163,7 +168,10 @@ typedef struct kgx_device_result {
     const uint32_t *hits_cold;   /* 4 words per slot */
     const kgx_call *calls;       /* capacity window_base[n_seq] */
     const kgx_best_call *best;   /* n_seq, after a score stage with KGX_WANT_BEST, else NULL */
+    uint32_t hit_format;         /* KGX_HIT_PACKED16 or KGX_HIT_PLANES */
 } kgx_device_result;
+#define KGX_HIT_PLANES 0u
+#define KGX_HIT_PACKED16 1u
 
 typedef struct kgx_image kgx_image;
 typedef struct kgx_ctx kgx_ctx;

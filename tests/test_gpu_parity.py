@@ -483,11 +483,14 @@ def _dev_alloc(gpu, nbytes):
     return p.value
 
 
-def test_device_queries_and_run_device(gpu, oracle_lib):
+@pytest.mark.parametrize("layout", ["packed", "aos"])
+def test_device_queries_and_run_device(gpu, oracle_lib, layout):
     spec, table = synthetic_table(30000)
     n, L = 500, 300
     L_ = gpu.lib()
     with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        if layout == "aos":
+            img.set_layout(gpu.Image.AOS24)
         d_res = _dev_alloc(gpu, n * L)
         d_off = _dev_alloc(gpu, (n + 1) * 8)
         try:
@@ -510,18 +513,24 @@ def test_device_queries_and_run_device(gpu, oracle_lib):
             for arr, ptr in ((wb, out.window_base), (hc, out.hit_count), (cc, out.call_count)):
                 gpu.check(L_.kgx_memcpy_d2h(arr.ctypes.data, ptr, arr.nbytes), "d2h")
             hot = np.empty((int(wb[-1]), 4), np.uint32)
-            cold = np.empty((int(wb[-1]), 4), np.uint32)
             calls = np.empty(int(wb[-1]), gpu.CALL_DTYPE)
             mask = np.empty((int(wb[-1]) + 63) // 64, np.uint64)
             gpu.check(L_.kgx_memcpy_d2h(hot.ctypes.data, out.hits_hot, hot.nbytes), "d2h")
-            gpu.check(L_.kgx_memcpy_d2h(cold.ctypes.data, out.hits_cold, cold.nbytes), "d2h")
-            hits = gpu.hits_from_planes(hot, cold)
+            packed = out.hit_format == gpu.HIT_PACKED16
+            assert packed == (img.layout == gpu.Image.PACKED16)
+            if packed:
+                assert not out.hits_cold
+                hits = gpu.hits_from_packed(hot)
+            else:
+                cold = np.empty((int(wb[-1]), 4), np.uint32)
+                gpu.check(L_.kgx_memcpy_d2h(cold.ctypes.data, out.hits_cold, cold.nbytes), "d2h")
+                hits = gpu.hits_from_planes(hot, cold)
             gpu.check(L_.kgx_memcpy_d2h(calls.ctypes.data, out.calls, calls.nbytes), "d2h")
             gpu.check(L_.kgx_memcpy_d2h(mask.ctypes.data, out.hit_mask, mask.nbytes), "d2h")
             want = oracle_lib.process_batch(table, hres, hoff)
             assert np.array_equal(np.diff(want.hit_offsets), hc)
             assert np.array_equal(np.diff(want.call_offsets), cc)
-            per_seq = gpu.tiled_hits_per_sequence(wb, mask, out.tile_windows, hits)
+            per_seq = gpu.tiled_hits_per_sequence(wb, mask, out.tile_windows, hits, fill_pos=packed)
             assert [len(x) for x in per_seq] == hc.tolist()
             gh = np.concatenate(per_seq)
             gc = np.concatenate([calls[wb[s]:wb[s] + cc[s]] for s in range(n)])

@@ -53,10 +53,15 @@ def _family_proteins(spec, rng, n_fam, per_fam, sub=0.06):
     return seqs
 
 
-@pytest.fixture(scope="module")
-def table_world(gpu):
+@pytest.fixture(scope="module", params=["packed", "aos"])
+def table_world(gpu, request):
+    """Both resident layouts: their probes store different hit records
+    (HIT_PACKED16 / HIT_PLANES), which the table kernels read."""
     spec, table = synthetic_table(60000)
     img = gpu.Image.from_table(table)
+    if request.param == "aos":
+        img.set_layout(gpu.Image.AOS24)
+    assert img.layout == (gpu.Image.AOS24 if request.param == "aos" else gpu.Image.PACKED16)
     ctx = gpu.Context(img)
     yield spec, table, img, ctx
     ctx.close()
