@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of two libkgx.so builds on one box: base (tree) vs exp/libkgx_exp.so
+# A/B of two libkgx.so builds on one box: the tree's build vs exp/libkgx_exp.so
+# (build the variant, copy it to exp/libkgx_exp.so, rebuild the tree; run through gpurun)
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/ab
