@@ -9,7 +9,9 @@ used only for the barrier and the max / sum reductions of timings and counts.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 
 import numpy as np
 
@@ -35,6 +37,22 @@ def weak_shard(rank: int, n_per_rank: int) -> tuple[int, int]:
     return rank * n_per_rank, (rank + 1) * n_per_rank
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """fd 1 -> fd 2 for the duration: gloo prints its connection report
+    ("[Gloo] Rank 0 is connected to ...") on stdout, where bench.py's one
+    JSON line must stand alone."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class Dist:
     """Rank / world from the torchrun environment; gloo for control only."""
 
@@ -45,8 +63,10 @@ class Dist:
         self.pg = None
         if self.world > 1:
             import torch.distributed as dist
-            if not dist.is_initialized():
-                dist.init_process_group(backend)
+            with _stdout_to_stderr():
+                if not dist.is_initialized():
+                    dist.init_process_group(backend)
+                dist.barrier()  # the mesh is connected (and reported) here
             self.pg = dist
 
     def barrier(self) -> None:
