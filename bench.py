@@ -62,7 +62,16 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
         probes, windows = r.probes, r.windows
     r1 = oracle.process_batch(table, res, off, want=7, n_threads=1)
     del table
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {
+        "cpu_model": cpu_model,
         "value": float(passes * len(res) / secs),
         "unit": "residues/s",
         "cores": threads,
