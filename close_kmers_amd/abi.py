@@ -57,7 +57,8 @@ class DeviceResult(ctypes.Structure):
                 ("window_base", ctypes.c_void_p), ("hit_mask", ctypes.c_void_p),
                 ("hit_count", ctypes.c_void_p), ("call_count", ctypes.c_void_p),
                 ("hits_hot", ctypes.c_void_p), ("hits_cold", ctypes.c_void_p),
-                ("calls", ctypes.c_void_p), ("best", ctypes.c_void_p), ("hit_format", ctypes.c_uint32)]
+                ("calls", ctypes.c_void_p), ("best", ctypes.c_void_p), ("hit_format", ctypes.c_uint32),
+                ("otu_count", ctypes.c_void_p), ("otus", ctypes.c_void_p)]
 
 
 HIT_PLANES, HIT_PACKED16 = 0, 1

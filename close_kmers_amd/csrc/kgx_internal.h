@@ -166,7 +166,12 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
-                         uint32_t seq_base, uint32_t hit_format, hipStream_t stream);
+                         uint32_t seq_base, uint32_t hit_format, const uint32_t *otu_count, const kgx_otu *otus,
+                         const uint64_t *otu_dense_off, kgx_otu *otus_out, hipStream_t stream);
+/* per-sequence OTU tallies in otus_by_count order at otus[window_base[s]] */
+hipError_t launch_otus(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
+                       const uint4 *hot, const uint4 *cold, int32_t *ws, kgx_otu *otus, uint32_t *otu_count,
+                       uint32_t hit_format, hipStream_t stream);
 /* find_best_call per sequence: calls[start[s] ..+ count[s]), ws same extent */
 hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64_t *start, const uint32_t *count,
                              kgx_call *ws, kgx_best_call *out, hipStream_t stream);

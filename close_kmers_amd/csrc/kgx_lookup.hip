@@ -1085,6 +1085,229 @@ hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64
 }
 
 /* ------------------------------------------------------------------------ */
+/* OTU tallies: KmerOtuStats (kguts.h:185-219), one lane per sequence         */
+/* ------------------------------------------------------------------------ */
+
+/* libstdc++'s std::sort (bits/stl_algo.h, stl_heap.h: introsort with
+ * median-of-three pivots, heapsort below the depth limit, final insertion
+ * sort, threshold 16) replayed step by step on a[0, n), so elements that
+ * compare equal end in the order the reference's std::sort leaves them.
+ * The recursion on the right part becomes an explicit stack (the parts are
+ * disjoint, so the order they are sorted in does not matter). */
+template <class T, class C>
+__device__ void lstd_push_heap(T *a, int64_t hole, int64_t top, T value, C comp)
+{
+    int64_t parent = (hole - 1) / 2;
+    while (hole > top && comp(a[parent], value)) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = value;
+}
+
+template <class T, class C>
+__device__ void lstd_adjust_heap(T *a, int64_t hole, int64_t len, T value, C comp)
+{
+    const int64_t top = hole;
+    int64_t second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (comp(a[second], a[second - 1]))
+            second--;
+        a[hole] = a[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        a[hole] = a[second - 1];
+        hole = second - 1;
+    }
+    lstd_push_heap(a, hole, top, value, comp);
+}
+
+template <class T, class C> __device__ void lstd_make_heap(T *a, int64_t len, C comp)
+{
+    if (len < 2)
+        return;
+    for (int64_t parent = (len - 2) / 2;; parent--) {
+        lstd_adjust_heap(a, parent, len, a[parent], comp);
+        if (parent == 0)
+            return;
+    }
+}
+
+/* __pop_heap(first, first + len, first + result) */
+template <class T, class C> __device__ void lstd_pop_heap(T *a, int64_t len, int64_t result, C comp)
+{
+    const T value = a[result];
+    a[result] = a[0];
+    lstd_adjust_heap(a, 0, len, value, comp);
+}
+
+/* __partial_sort(first, last, last): heap_select over the whole range, then sort_heap */
+template <class T, class C> __device__ void lstd_heap_sort(T *a, int64_t n, C comp)
+{
+    lstd_make_heap(a, n, comp);
+    for (int64_t last = n; last > 1;) {
+        --last;
+        lstd_pop_heap(a, last, last, comp);
+    }
+}
+
+template <class T> __device__ __forceinline__ void lstd_swap(T &x, T &y)
+{
+    const T t = x;
+    x = y;
+    y = t;
+}
+
+template <class T, class C> __device__ void lstd_unguarded_linear_insert(T *a, int64_t last, C comp)
+{
+    const T val = a[last];
+    int64_t next = last - 1;
+    while (comp(val, a[next])) {
+        a[last] = a[next];
+        last = next;
+        --next;
+    }
+    a[last] = val;
+}
+
+template <class T, class C> __device__ void lstd_insertion_sort(T *a, int64_t n, C comp)
+{
+    for (int64_t i = 1; i < n; i++) {
+        if (comp(a[i], a[0])) {
+            const T val = a[i];
+            for (int64_t k = i; k > 0; k--)
+                a[k] = a[k - 1];
+            a[0] = val;
+        } else {
+            lstd_unguarded_linear_insert(a, i, comp);
+        }
+    }
+}
+
+template <class T, class C> __device__ void lstd_sort(T *a, int64_t n, C comp)
+{
+    if (n <= 1)
+        return;
+    constexpr int64_t THRESH = 16;
+    struct Part {
+        int64_t first, last;
+        int depth;
+    } stack[64];
+    int sp = 0;
+    stack[sp++] = Part{0, n, 2 * (63 - __builtin_clzll((unsigned long long)n))};
+    while (sp) {
+        Part p = stack[--sp];
+        while (p.last - p.first > THRESH) {
+            if (p.depth == 0) {
+                lstd_heap_sort(a + p.first, p.last - p.first, comp);
+                break;
+            }
+            --p.depth;
+            /* __unguarded_partition_pivot */
+            const int64_t mid = p.first + (p.last - p.first) / 2;
+            T *r = a + p.first;
+            T *x = a + p.first + 1, *y = a + mid, *z = a + p.last - 1;
+            if (comp(*x, *y)) {
+                if (comp(*y, *z))
+                    lstd_swap(*r, *y);
+                else if (comp(*x, *z))
+                    lstd_swap(*r, *z);
+                else
+                    lstd_swap(*r, *x);
+            } else if (comp(*x, *z))
+                lstd_swap(*r, *x);
+            else if (comp(*y, *z))
+                lstd_swap(*r, *z);
+            else
+                lstd_swap(*r, *y);
+            int64_t lo = p.first + 1, hi = p.last;
+            const T pivot = a[p.first];
+            while (true) {
+                while (comp(a[lo], pivot))
+                    ++lo;
+                --hi;
+                while (comp(pivot, a[hi]))
+                    --hi;
+                if (!(lo < hi))
+                    break;
+                lstd_swap(a[lo], a[hi]);
+                ++lo;
+            }
+            stack[sp++] = Part{lo, p.last, p.depth}; /* __introsort_loop(cut, last) */
+            p.last = lo;
+        }
+    }
+    /* __final_insertion_sort */
+    if (n > THRESH) {
+        lstd_insertion_sort(a, THRESH, comp);
+        for (int64_t i = THRESH; i < n; i++)
+            lstd_unguarded_linear_insert(a, i, comp);
+    } else {
+        lstd_insertion_sort(a, n, comp);
+    }
+}
+
+/* otu_map[oI]++ over the hits the scorer flagged KGX_HIT_OTU (the hits
+ * process_set_of_hits tallies, kguts.cc:760-768), then finalize(): the map's
+ * pairs in key order, std::sort by count, larger first (kguts.h:214-218).
+ * Scratch: ws / otus of sequence s start at window_base[s] (a sequence has
+ * no more flagged hits than windows). */
+template <bool PK>
+__global__ __launch_bounds__(256) void otu_kernel(uint32_t n_seq, const uint64_t *__restrict__ wbase,
+                                                  const uint64_t *__restrict__ hit_mask, uint32_t tile_windows,
+                                                  const uint4 *__restrict__ hot, const uint4 *__restrict__ cold,
+                                                  int32_t *__restrict__ ws, kgx_otu *__restrict__ otus,
+                                                  uint32_t *__restrict__ otu_count)
+{
+    typedef HitFields<PK> HF;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_seq)
+        return;
+    const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
+    int32_t *v = ws + gw0;
+    int64_t n = 0;
+    for_each_run(hit_mask, tile_windows, gw0, gw1, [&](uint64_t at0, uint32_t c, uint32_t, uint64_t, uint32_t) {
+        for (uint32_t k = 0; k < c; k++) {
+            const uint4 h = hot[at0 + k];
+            if (HF::flags(h) & KGX_HIT_OTU)
+                v[n++] = (int32_t)HF::otu(h, PK ? h : cold[at0 + k]);
+        }
+    });
+    /* std::map<int, int> key order */
+    lstd_heap_sort(v, n, [](int32_t a, int32_t b) { return a < b; });
+    kgx_otu *o = otus + gw0;
+    int64_t m = 0;
+    for (int64_t i = 0; i < n;) {
+        int64_t j = i + 1;
+        while (j < n && v[j] == v[i])
+            j++;
+        o[m++] = kgx_otu{v[i], (int32_t)(j - i)};
+        i = j;
+    }
+    lstd_sort(o, m, [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; });
+    otu_count[s] = (uint32_t)m;
+}
+
+hipError_t launch_otus(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
+                       const uint4 *hot, const uint4 *cold, int32_t *ws, kgx_otu *otus, uint32_t *otu_count,
+                       uint32_t hit_format, hipStream_t stream)
+{
+    if (n_seq == 0)
+        return hipSuccess;
+    if (hit_format == HIT_PACKED16)
+        hipLaunchKernelGGL(otu_kernel<true>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase, hit_mask,
+                           tile_windows, hot, cold, ws, otus, otu_count);
+    else
+        hipLaunchKernelGGL(otu_kernel<false>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
+                           hit_mask, tile_windows, hot, cold, ws, otus, otu_count);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
 /* gather: tiled hits / sparse calls -> dense CSR, one wave per sequence     */
 /* ------------------------------------------------------------------------ */
 
@@ -1094,7 +1317,8 @@ __global__ __launch_bounds__(256) void gather_kernel(
     uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
     const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
     const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
-    uint32_t seq_base)
+    uint32_t seq_base, const uint32_t *__restrict__ otu_count, const kgx_otu *__restrict__ otus,
+    const uint64_t *__restrict__ ooff, kgx_otu *__restrict__ otus_out)
 {
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= n_seq)
@@ -1158,12 +1382,19 @@ __global__ __launch_bounds__(256) void gather_kernel(
         for (uint32_t i = lane; i < n; i += 64)
             dst[i] = src[i];
     }
+    if (otus_out) {
+        const kgx_otu *src = otus + gw0;
+        kgx_otu *dst = otus_out + ooff[s];
+        for (uint32_t i = lane; i < otu_count[s]; i += 64)
+            dst[i] = src[i];
+    }
 }
 
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
                          kgx_hit *hits_out, kgx_call *calls_out, uint32_t seq_base, uint32_t hit_format,
+                         const uint32_t *otu_count, const kgx_otu *otus, const uint64_t *ooff, kgx_otu *otus_out,
                          hipStream_t stream)
 {
     if (n_seq == 0)
@@ -1171,11 +1402,11 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
     if (hit_format == HIT_PACKED16)
         hipLaunchKernelGGL(gather_kernel<true>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                            hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                           calls_out, seq_base);
+                           calls_out, seq_base, otu_count, otus, ooff, otus_out);
     else
         hipLaunchKernelGGL(gather_kernel<false>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                            hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                           calls_out, seq_base);
+                           calls_out, seq_base, otu_count, otus, ooff, otus_out);
     return hipGetLastError();
 }
 

@@ -187,7 +187,11 @@ struct kgx_ctx {
     std::vector<uint64_t> h_hoff, h_coff, h_ooff;
     kgx::PinnedVec<kgx_hit> h_hits;
     kgx::PinnedVec<kgx_call> h_calls;
-    std::vector<kgx_otu> h_otus;
+    kgx::PinnedVec<kgx_otu> h_otus;
+    kgx::PinnedVec<uint32_t> h_ocount;
+    /* KGX_WANT_OTU: device tallies (otu_kernel) */
+    kgx::DevBuf otu_ws, otus, otu_count, dense_ooff, dense_otus;
+    bool have_otus = false;
     kgx::PinnedVec<uint32_t> h_hcount, h_ccount;
     kgx::PinnedVec<char> h_res;
     /* host-buffer batches in chunks (option "host_chunks"): chunks alternate
@@ -197,7 +201,7 @@ struct kgx_ctx {
     int host_copy = 1; /* chunk D2H: 0 = DMA (hipMemcpyAsync), 1 = device stores into mapped memory */
     int host_copy_blocks = 64; /* workgroups of the store copy (option "host_copy_blocks") */
     kgx_ctx *twin = nullptr;
-    kgx::PinnedVec<uint64_t> h_off_stage, h_dense_hoff, h_dense_coff, h_nwin;
+    kgx::PinnedVec<uint64_t> h_off_stage, h_dense_hoff, h_dense_coff, h_dense_ooff, h_nwin;
 };
 
 #endif

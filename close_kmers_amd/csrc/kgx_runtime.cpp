@@ -774,6 +774,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     c->d_off = d_off;
     c->have_hits = false;
     c->have_best = false;
+    c->have_otus = false;
     return KGX_OK;
 }
 
@@ -823,6 +824,16 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
                          want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->stream));
     c->have_best = false;
+    c->have_otus = false;
+    if (want & KGX_WANT_OTU) {
+        HIP_TRY(c->otu_ws.reserve(std::max<uint64_t>(c->hit_slots, 1) * sizeof(int32_t)));
+        HIP_TRY(c->otus.reserve(std::max<uint64_t>(c->hit_slots, 1) * sizeof(kgx_otu)));
+        HIP_TRY(c->otu_count.reserve(std::max<uint64_t>(c->n_seq, 1) * sizeof(uint32_t)));
+        HIP_TRY(launch_otus(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                            c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->otu_ws.as<int32_t>(),
+                            c->otus.as<kgx_otu>(), c->otu_count.as<uint32_t>(), c->hit_format, c->stream));
+        c->have_otus = true;
+    }
     if (best) {
         HIP_TRY(c->best.reserve(std::max<uint64_t>(c->n_seq, 1) * sizeof(kgx_best_call)));
         HIP_TRY(c->best_ws.reserve(c->hit_slots * sizeof(kgx_call)));
@@ -884,6 +895,8 @@ int kgx_device_result_get(kgx_ctx *c, kgx_device_result *out)
     out->hits_hot = c->hits.as<uint32_t>();
     out->hits_cold = c->hit_format == HIT_PLANES ? c->hits.as<uint32_t>() + 4 * c->hit_slots : nullptr;
     out->hit_format = c->hit_format;
+    out->otu_count = c->have_otus ? c->otu_count.as<uint32_t>() : nullptr;
+    out->otus = c->have_otus ? c->otus.as<kgx_otu>() : nullptr;
     out->calls = c->calls.as<kgx_call>();
     out->best = c->have_best ? c->best.as<kgx_best_call>() : nullptr;
     return KGX_OK;
@@ -970,40 +983,20 @@ int enqueue_chunk(kgx_ctx *x, const kgx_params *params, uint32_t want)
         return rc;
     HIP_TRY(x->h_hcount.resize(n + 1));
     HIP_TRY(x->h_ccount.resize(n + 1));
+    HIP_TRY(x->h_ocount.resize(n + 1));
     HIP_TRY(x->h_nwin.resize(1));
     if (n) {
         HIP_TRY(hipMemcpyAsync(x->h_hcount.data(), x->hit_count.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                x->stream));
         HIP_TRY(hipMemcpyAsync(x->h_ccount.data(), x->call_count.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                x->stream));
+        if (want & KGX_WANT_OTU)
+            HIP_TRY(hipMemcpyAsync(x->h_ocount.data(), x->otu_count.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   x->stream));
     }
     HIP_TRY(hipMemcpyAsync(x->h_nwin.data(), x->wbase.as<uint64_t>() + n, sizeof(uint64_t),
                            hipMemcpyDeviceToHost, x->stream));
     return KGX_OK;
-}
-
-/* KmerOtuStats::otu_map over the hits the scorer flagged, then finalize()
- * (kguts.h:214-218: std::sort by count, descending) */
-void otu_tallies(kgx_ctx *c, uint32_t n_seq, bool want_otu)
-{
-    c->h_ooff.assign(n_seq + 1, 0);
-    c->h_otus.clear();
-    if (!want_otu)
-        return;
-    std::map<int, int> m;
-    std::vector<std::pair<int, int>> v;
-    for (uint32_t s = 0; s < n_seq; s++) {
-        m.clear();
-        for (uint64_t i = c->h_hoff[s]; i < c->h_hoff[s + 1]; i++)
-            if (c->h_hits[i].flags & KGX_HIT_OTU)
-                m[c->h_hits[i].otu_index]++;
-        v.assign(m.begin(), m.end());
-        std::sort(v.begin(), v.end(),
-                  [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return b.second < a.second; });
-        for (auto &pr : v)
-            c->h_otus.push_back(kgx_otu{pr.first, pr.second});
-        c->h_ooff[s + 1] = c->h_otus.size();
-    }
 }
 
 void fill_result(kgx_ctx *c, uint32_t n_seq, bool need_hits, bool want_best, uint64_t nwin, kgx_result *out)
@@ -1052,14 +1045,33 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     cut.erase(std::unique(cut.begin(), cut.end()), cut.end()); /* no empty chunks */
     K = (uint32_t)cut.size() - 1;
     const bool want_calls = (want & KGX_WANT_CALLS) != 0;
-    const bool need_hits = (want & (KGX_WANT_HITS | KGX_WANT_OTU)) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    const bool need_hits = (want & KGX_WANT_HITS) != 0;
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
     c->h_hoff.assign(n_seq + 1, 0);
     c->h_coff.assign(n_seq + 1, 0);
-    uint64_t hbase = 0, cbase = 0, nwin = 0;
+    c->h_ooff.assign(n_seq + 1, 0);
+    uint64_t hbase = 0, cbase = 0, obase = 0, nwin = 0;
     HIP_TRY(c->h_hits.resize(0));
     HIP_TRY(c->h_calls.resize(0));
-    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    HIP_TRY(c->h_otus.resize(0));
     HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+
+    /* device bytes -> the pinned result array at element `at`: device stores
+     * into the mapped memory (host_copy 1) or a DMA copy */
+    auto copy_out = [&](kgx_ctx *x, auto &dst, uint64_t at, const void *src, uint64_t n) -> int {
+        if (!n)
+            return KGX_OK;
+        const uint64_t bytes = n * sizeof(dst[0]);
+        if (c->host_copy) {
+            void *d = nullptr;
+            HIP_TRY(dst.device_ptr(at, &d));
+            HIP_TRY(launch_copy_to_host(d, src, bytes, c->host_copy_blocks, x->stream));
+        } else {
+            HIP_TRY(hipMemcpyAsync(dst.data() + at, src, bytes, hipMemcpyDeviceToHost, x->stream));
+        }
+        return KGX_OK;
+    };
 
     /* Copies of both streams share the DMA engine in submission order, so the
      * order of submission is the schedule: chunk k+1's H2D goes in before
@@ -1085,75 +1097,66 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
         const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
         HIP_TRY(x->h_dense_hoff.resize(n + 1));
         HIP_TRY(x->h_dense_coff.resize(n + 1));
-        uint64_t nh = 0, nc = 0;
+        HIP_TRY(x->h_dense_ooff.resize(n + 1));
+        uint64_t nh = 0, nc = 0, no = 0;
         for (uint32_t i = 0; i < n; i++) {
             x->h_dense_hoff[i] = nh;
             x->h_dense_coff[i] = nc;
+            x->h_dense_ooff[i] = no;
             nh += x->h_hcount[i];
             nc += want_calls ? x->h_ccount[i] : 0;
+            no += want_otu ? x->h_ocount[i] : 0;
             c->h_hoff[s0 + i + 1] = hbase + nh;
             c->h_coff[s0 + i + 1] = cbase + nc;
+            c->h_ooff[s0 + i + 1] = obase + no;
         }
         x->h_dense_hoff[n] = nh;
         x->h_dense_coff[n] = nc;
+        x->h_dense_ooff[n] = no;
         nwin += x->h_nwin[0];
         const uint64_t nh_all = nh; /* hit offsets count every hit; records only when wanted */
         if (!need_hits)
             nh = 0;
         const uint64_t hrec = need_hits ? hbase : 0; /* where this chunk's records go */
-        if (hrec + nh > c->h_hits.cap || cbase + nc > c->h_calls.cap) {
+        if (hrec + nh > c->h_hits.cap || cbase + nc > c->h_calls.cap || obase + no > c->h_otus.cap) {
             /* growth moves the pinned arrays: no copy into them may be in flight */
             HIP_TRY(hipStreamSynchronize(xs[0]->stream));
             HIP_TRY(hipStreamSynchronize(xs[1]->stream));
         }
         HIP_TRY(c->h_hits.resize(hrec + nh));
         HIP_TRY(c->h_calls.resize(cbase + nc));
-        if (nh || nc) {
+        HIP_TRY(c->h_otus.resize(obase + no));
+        if (nh || nc || no) {
             HIP_TRY(x->dense_hoff.reserve((n + 1) * sizeof(uint64_t)));
             HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
+            HIP_TRY(x->dense_ooff.reserve((n + 1) * sizeof(uint64_t)));
             HIP_TRY(x->dense_hits.reserve(std::max<uint64_t>(nh, 1) * sizeof(kgx_hit)));
             HIP_TRY(x->dense_calls.reserve(std::max<uint64_t>(nc, 1) * sizeof(kgx_call)));
+            HIP_TRY(x->dense_otus.reserve(std::max<uint64_t>(no, 1) * sizeof(kgx_otu)));
             HIP_TRY(hipMemcpyAsync(x->dense_hoff.p, x->h_dense_hoff.data(), (n + 1) * sizeof(uint64_t),
                                    hipMemcpyHostToDevice, x->stream));
             HIP_TRY(hipMemcpyAsync(x->dense_coff.p, x->h_dense_coff.data(), (n + 1) * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, x->stream));
+            HIP_TRY(hipMemcpyAsync(x->dense_ooff.p, x->h_dense_ooff.data(), (n + 1) * sizeof(uint64_t),
                                    hipMemcpyHostToDevice, x->stream));
             HIP_TRY(launch_gather(n, x->wbase.as<uint64_t>(), x->hit_mask.as<uint64_t>(), x->tile_windows,
                                   x->call_count.as<uint32_t>(), x->hits.as<uint4>(),
                                   x->hits.as<uint4>() + x->hit_slots, x->calls.as<kgx_call>(),
                                   x->dense_hoff.as<uint64_t>(), x->dense_coff.as<uint64_t>(),
                                   nh ? x->dense_hits.as<kgx_hit>() : nullptr,
-                                  nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->hit_format, x->stream));
-            if (c->host_copy) {
-                void *dh = nullptr, *dc = nullptr;
-                if (nh) {
-                    HIP_TRY(c->h_hits.device_ptr(hrec, &dh));
-                    HIP_TRY(launch_copy_to_host(dh, x->dense_hits.p, nh * sizeof(kgx_hit), c->host_copy_blocks, x->stream));
-                }
-                if (nc) {
-                    HIP_TRY(c->h_calls.device_ptr(cbase, &dc));
-                    HIP_TRY(launch_copy_to_host(dc, x->dense_calls.p, nc * sizeof(kgx_call), c->host_copy_blocks, x->stream));
-                }
-            } else {
-                if (nh)
-                    HIP_TRY(hipMemcpyAsync(c->h_hits.data() + hrec, x->dense_hits.p, nh * sizeof(kgx_hit),
-                                           hipMemcpyDeviceToHost, x->stream));
-                if (nc)
-                    HIP_TRY(hipMemcpyAsync(c->h_calls.data() + cbase, x->dense_calls.p, nc * sizeof(kgx_call),
-                                           hipMemcpyDeviceToHost, x->stream));
-            }
+                                  nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->hit_format,
+                                  x->otu_count.as<uint32_t>(), x->otus.as<kgx_otu>(), x->dense_ooff.as<uint64_t>(),
+                                  no ? x->dense_otus.as<kgx_otu>() : nullptr, x->stream));
+            if ((rc = copy_out(x, c->h_hits, hrec, x->dense_hits.p, nh)) ||
+                (rc = copy_out(x, c->h_calls, cbase, x->dense_calls.p, nc)) ||
+                (rc = copy_out(x, c->h_otus, obase, x->dense_otus.p, no)))
+                break;
         }
-        if (want_best && n) {
-            if (c->host_copy) {
-                void *db = nullptr;
-                HIP_TRY(c->h_best.device_ptr(s0, &db));
-                HIP_TRY(launch_copy_to_host(db, x->best.p, n * sizeof(kgx_best_call), c->host_copy_blocks, x->stream));
-            } else {
-                HIP_TRY(hipMemcpyAsync(c->h_best.data() + s0, x->best.p, n * sizeof(kgx_best_call),
-                                       hipMemcpyDeviceToHost, x->stream));
-            }
-        }
+        if (want_best && (rc = copy_out(x, c->h_best, s0, x->best.p, n)))
+            break;
         hbase += nh_all;
         cbase += nc;
+        obase += no;
         const auto t2 = now();
         /* chunk k+2 -> x's pinned staging while the DMA engine and the device work */
         /* (x's H2D of chunk k finished before its counts arrived; its pending
@@ -1173,7 +1176,6 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     /* the batch's device results are split over two contexts */
     c->have_hits = false;
     t->have_hits = false;
-    otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
     fill_result(c, n_seq, need_hits, (want & KGX_WANT_BEST) != 0, nwin, out);
     return KGX_OK;
 }
@@ -1221,39 +1223,56 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
         return fail(KGX_EINVAL, "null argument");
     if (!c->have_hits)
         return fail(KGX_EINVAL, "no device batch to collect");
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    const bool need_hits = (want & KGX_WANT_HITS) != 0;
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    if (want_otu && !c->have_otus)
+        return fail(KGX_EINVAL, "no device OTU tallies (score with KGX_WANT_OTU)");
+    if (want_best && !c->have_best)
+        return fail(KGX_EINVAL, "no device best calls (score with KGX_WANT_BEST)");
     HIP_TRY(hipSetDevice(c->img->device));
     PhaseTimer tm(c);
     const uint32_t n_seq = c->n_seq;
     /* counts -> dense CSR offsets on the host, gather on the device */
     HIP_TRY(c->h_hcount.resize(n_seq + 1));
     HIP_TRY(c->h_ccount.resize(n_seq + 1));
+    HIP_TRY(c->h_ocount.resize(n_seq + 1));
     if (n_seq) {
         HIP_TRY(hipMemcpyAsync(c->h_hcount.data(), c->hit_count.p, n_seq * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(c->h_ccount.data(), c->call_count.p, n_seq * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, c->stream));
+        if (want_otu)
+            HIP_TRY(hipMemcpyAsync(c->h_ocount.data(), c->otu_count.p, n_seq * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
     c->h_hoff.assign(n_seq + 1, 0);
     c->h_coff.assign(n_seq + 1, 0);
+    c->h_ooff.assign(n_seq + 1, 0);
     for (uint32_t s = 0; s < n_seq; s++) {
         c->h_hoff[s + 1] = c->h_hoff[s] + c->h_hcount[s];
         c->h_coff[s + 1] = c->h_coff[s] + (want_calls ? c->h_ccount[s] : 0);
+        c->h_ooff[s + 1] = c->h_ooff[s] + (want_otu ? c->h_ocount[s] : 0);
     }
     tm.mark(" counts");
-    const uint64_t nh = c->h_hoff[n_seq], nc = c->h_coff[n_seq];
-    const bool need_hits = (want & (KGX_WANT_HITS | KGX_WANT_OTU)) != 0;
+    const uint64_t nh = c->h_hoff[n_seq], nc = c->h_coff[n_seq], no = c->h_ooff[n_seq];
     HIP_TRY(c->h_hits.resize(need_hits ? nh : 0));
     HIP_TRY(c->h_calls.resize(nc));
-    if ((need_hits && nh) || nc) {
+    HIP_TRY(c->h_otus.resize(no));
+    if ((need_hits && nh) || nc || no) {
         HIP_TRY(c->dense_hoff.reserve((n_seq + 1) * sizeof(uint64_t)));
         HIP_TRY(c->dense_coff.reserve((n_seq + 1) * sizeof(uint64_t)));
+        HIP_TRY(c->dense_ooff.reserve((n_seq + 1) * sizeof(uint64_t)));
         HIP_TRY(c->dense_hits.reserve(std::max<uint64_t>(nh, 1) * sizeof(kgx_hit)));
         HIP_TRY(c->dense_calls.reserve(std::max<uint64_t>(nc, 1) * sizeof(kgx_call)));
+        HIP_TRY(c->dense_otus.reserve(std::max<uint64_t>(no, 1) * sizeof(kgx_otu)));
         HIP_TRY(hipMemcpyAsync(c->dense_hoff.p, c->h_hoff.data(), (n_seq + 1) * sizeof(uint64_t),
                                hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->dense_coff.p, c->h_coff.data(), (n_seq + 1) * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->dense_ooff.p, c->h_ooff.data(), (n_seq + 1) * sizeof(uint64_t),
                                hipMemcpyHostToDevice, c->stream));
         HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
                               c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
@@ -1262,30 +1281,29 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                               c->dense_coff.as<uint64_t>(),
                               need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
                               want_calls ? c->dense_calls.as<kgx_call>() : nullptr, 0u, c->hit_format,
-                              c->stream));
+                              c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
+                              no ? c->dense_otus.as<kgx_otu>() : nullptr, c->stream));
         if (need_hits && nh)
             HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
                                    hipMemcpyDeviceToHost, c->stream));
         if (nc)
             HIP_TRY(hipMemcpyAsync(c->h_calls.data(), c->dense_calls.p, nc * sizeof(kgx_call),
                                    hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (no)
+            HIP_TRY(hipMemcpyAsync(c->h_otus.data(), c->dense_otus.p, no * sizeof(kgx_otu),
+                                   hipMemcpyDeviceToHost, c->stream));
     }
-
-    if ((want & KGX_WANT_BEST) && n_seq) {
-        if (!c->have_best)
-            return fail(KGX_EINVAL, "no device best calls (score with KGX_WANT_BEST)");
+    if (want_best && n_seq) {
         HIP_TRY(c->h_best.resize(n_seq));
         HIP_TRY(hipMemcpyAsync(c->h_best.data(), c->best.p, n_seq * sizeof(kgx_best_call), hipMemcpyDeviceToHost,
                                c->stream));
     }
-    tm.mark(" gather+d2h");
-    otu_tallies(c, n_seq, (want & KGX_WANT_OTU) != 0);
-    uint64_t nwin = 0;
-    HIP_TRY(hipMemcpyAsync(&nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                           c->stream));
+    HIP_TRY(c->h_nwin.resize(1));
+    HIP_TRY(hipMemcpyAsync(c->h_nwin.data(), c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    fill_result(c, n_seq, need_hits, (want & KGX_WANT_BEST) != 0, nwin, out);
+    tm.mark(" gather+d2h");
+    fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
     return KGX_OK;
 }
 

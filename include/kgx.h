@@ -42,7 +42,7 @@ extern "C" {
 /* ---- what kgx_process_* computes --------------------------------------- */
 #define KGX_WANT_HITS 1u  /* hit list (what hit_cb receives, kguts.cc:814-815) */
 #define KGX_WANT_CALLS 2u /* KmerCall runs (process_set_of_hits, kguts.cc:734-781) */
-#define KGX_WANT_OTU 4u   /* OTU tallies (KmerOtuStats, kguts.h:185-219) */
+#define KGX_WANT_OTU 4u   /* OTU tallies (KmerOtuStats, kguts.h:185-219), on the device */
 #define KGX_WANT_BEST 8u  /* find_best_call per sequence, on the device (kgx_best_call) */
 
 /* ---- on-disk / in-HBM record layouts (kmer_image.h:11-23) -------------- */
@@ -169,6 +169,10 @@ typedef struct kgx_device_result {
     const kgx_call *calls;       /* capacity window_base[n_seq] */
     const kgx_best_call *best;   /* n_seq, after a score stage with KGX_WANT_BEST, else NULL */
     uint32_t hit_format;         /* KGX_HIT_PACKED16 or KGX_HIT_PLANES */
+    /* with KGX_WANT_OTU (else NULL): sequence s's KmerOtuStats::otus_by_count
+     * pairs at otus[window_base[s] ..+ otu_count[s]) */
+    const uint32_t *otu_count;   /* n_seq */
+    const kgx_otu *otus;
 } kgx_device_result;
 #define KGX_HIT_PLANES 0u
 #define KGX_HIT_PACKED16 1u

@@ -729,3 +729,34 @@ def test_device_best_call_on_batches(small_world, oracle_lib, gpu):
         # BEST alone (no calls copied back), and in chunks
         only = ctx.process_batch(res, off, gpu.Params(*params), want=gpu.WANT_BEST)
         assert len(only.calls) == 0 and np.array_equal(only.best, got.best)
+
+
+@pytest.mark.parametrize("otu_range,layout", [(60, "packed"), (60, "aos"), (8, "packed"), (2000, "packed")])
+def test_device_otu_tallies_match_oracle(gpu, oracle_lib, otu_range, layout):
+    """OTU tallies on the device (otu_kernel): per-sequence otu_map in key
+    order, then libstdc++ std::sort by count (less_second, kguts.h:196-218).
+    60 OTUs over ~126 planted hits gives >16 distinct OTUs per sequence with
+    many tied counts (the introsort path of std::sort), 8 the insertion-sort
+    path; the AOS24 layout reads the OTU from the cold plane."""
+    import oracle
+    spec = synth.ImageSpec(30000)
+    k, f, o, a, w = spec.unique_entries()
+    rng = np.random.default_rng(otu_range)
+    o = rng.integers(-1, otu_range, len(k)).astype(np.int32)
+    table = oracle.build_table(spec.num_sigs, k, f, o, a, w)
+    res, off = synth.make_queries(spec, 600, x_permille=3)
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        if layout == "aos":
+            img.set_layout(gpu.Image.AOS24)
+        for params in [(5, 200, 0, 0), (2, 30, 0, 0)]:
+            want = oracle_lib.process_batch(table, res, off, params=params)
+            for w_ in (4, 7, 6):
+                got = ctx.process_batch(res, off, gpu.Params(*params), want=w_)
+                assert np.array_equal(got.otu_offsets, want.otu_offsets)
+                assert np.array_equal(got.otus["otu_index"], want.otus[:, 0])
+                assert np.array_equal(got.otus["count"], want.otus[:, 1])
+                if not w_ & 1:
+                    assert len(got.hits) == 0
+            n_otu = np.diff(want.otu_offsets)
+            if otu_range >= 60:
+                assert n_otu.max() > 16  # the introsort path ran
