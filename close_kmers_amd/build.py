@@ -23,7 +23,7 @@ ARCH = "gfx950"
 
 LIB_SOURCES = ["kgx_lookup.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
                "kguts_hip.cpp"]
-HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h"]
+HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-Wall", "-Wno-unused-function"]
 
