@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t base_class(uint8_t c)
     }
 }
 
-/* frame f's k-th residue of the read [b, b+len) */
+/* frame f's k-th residue of the read [b, b+len); b may point into LDS */
 struct FrameReader {
     const uint8_t *b;
     uint64_t len;
@@ -69,6 +69,46 @@ struct FrameReader {
     }
 };
 
+/* the same over a short read staged in LDS as base classes (0-3, 4 = not
+ * ACGTU), with the code table in LDS: every codon is LDS reads only */
+struct LdsFrameReader {
+    const uint8_t *cls_b; /* LDS: class of base i */
+    const char *code;     /* LDS copy of kCode11 */
+    uint64_t len;
+    int frame;
+    __device__ uint64_t n_codons() const
+    {
+        const uint64_t off = (uint64_t)(frame < 0 ? -frame : frame) - 1;
+        return len >= off ? (len - off) / 3 : 0;
+    }
+    __device__ uint32_t cls(uint64_t i) const
+    {
+        if (frame > 0)
+            return cls_b[i];
+        const uint32_t c = cls_b[len - 1 - i];
+        return c < 4 ? 3 - c : 4;
+    }
+    __device__ char aa(uint64_t k) const
+    {
+        const uint64_t i = (uint64_t)(frame < 0 ? -frame : frame) - 1 + 3 * k;
+        const uint32_t e1 = cls(i), e2 = cls(i + 1), e3 = cls(i + 2);
+        return code[(e1 | e2 | e3) < 4 ? e1 * 16 + e2 * 4 + e3 : 64];
+    }
+};
+
+/* per-workgroup LDS tables: base -> class, and the code-11 table */
+struct FqTables {
+    uint8_t cls[256];
+    char code[68];
+};
+__device__ __forceinline__ void fq_tables_init(FqTables &t)
+{
+    t.cls[threadIdx.x] = (uint8_t)base_class((uint8_t)threadIdx.x);
+    if (threadIdx.x < 65)
+        t.code[threadIdx.x] = kCode11[threadIdx.x];
+    __syncthreads();
+}
+
 __device__ __forceinline__ int frame_of(uint32_t f) { return f < 3 ? (int)f + 1 : -(int)(f - 2); }
 
 /*
@@ -88,7 +128,7 @@ struct FrameFragments { /* one frame's ballot view (lane k = codon k) */
     char aa;         /* this lane's residue */
 };
 
-__device__ __forceinline__ FrameFragments frame_fragments(const FrameReader &fr, uint32_t lane)
+template <class Reader> __device__ __forceinline__ FrameFragments frame_fragments(const Reader &fr, uint32_t lane)
 {
     const uint64_t nc = fr.n_codons();
     const bool valid = lane < nc;
@@ -142,22 +182,39 @@ __device__ void frame_serial(const FrameReader &fr, uint32_t r, uint32_t fi, uin
     }
 }
 
-__global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                       uint32_t n_reads, uint32_t *n_frag, uint64_t *n_res)
+/* a short read -> this wave's LDS slot as base classes, with one aligned
+ * dword load per lane (every dword holds a byte of the read, so none reaches
+ * past the read's own aligned words); returns the read's first class in LDS.
+ * The frames then take their codons from LDS instead of 18 scattered global
+ * byte loads and 6 constant-memory table loads per lane. */
+constexpr uint32_t LDS_READ_WORDS = (SHORT_READ + 3) / 4 + 1;
+__device__ __forceinline__ const uint8_t *stage_read(uint32_t *slot, const uint8_t *b, uint64_t len, uint32_t lane,
+                                                     const uint8_t *cls_tab)
 {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
-    if (r == n_reads && lane == 0) {
-        n_frag[r * 6] = 0;
-        n_res[r * 6] = 0;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(b), a0 = a & ~(uintptr_t)3;
+    const uint32_t mis = (uint32_t)(a - a0);
+    const uint32_t words = (uint32_t)((mis + len + 3) / 4);
+    __builtin_amdgcn_wave_barrier(); /* the previous read's LDS loads are done (grid-stride loop) */
+    if (lane < words) { /* 4 bases -> 4 class bytes */
+        const uint32_t w = reinterpret_cast<const uint32_t *>(a0)[lane];
+        slot[lane] = (uint32_t)cls_tab[w & 0xFF] | (uint32_t)cls_tab[(w >> 8) & 0xFF] << 8 |
+                     (uint32_t)cls_tab[(w >> 16) & 0xFF] << 16 | (uint32_t)cls_tab[w >> 24] << 24;
     }
-    if (r >= n_reads)
-        return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return reinterpret_cast<const uint8_t *>(slot) + mis;
+}
+
+__device__ __forceinline__ void count_read(const uint8_t *bases, const uint64_t *read_off, uint64_t r, uint32_t lane,
+                                           uint32_t *slot, const FqTables &tabs, uint32_t *n_frag, uint64_t *n_res)
+{
     const uint8_t *b = bases + read_off[r];
     const uint64_t len = read_off[r + 1] - read_off[r];
     if (len <= SHORT_READ) {
+        const uint8_t *lb = len ? stage_read(slot, b, len, lane, tabs.cls) : tabs.cls;
         for (uint32_t f = 0; f < 6; f++) {
-            const FrameFragments ff = frame_fragments(FrameReader{b, len, frame_of(f)}, lane);
+            const FrameFragments ff = frame_fragments(LdsFrameReader{lb, tabs.code, len, frame_of(f)}, lane);
             if (lane == 0) {
                 n_frag[r * 6 + f] = (uint32_t)__popcll(ff.starts);
                 n_res[r * 6 + f] = (uint64_t)__popcll(ff.kept);
@@ -173,21 +230,34 @@ __global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, con
     }
 }
 
-/* fragment records (offset, read, frame, first codon) and residues */
-__global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                      uint32_t n_reads, const uint32_t *frag_base,
-                                                      const uint64_t *res_base, uint8_t *out_res, uint64_t *out_off,
-                                                      uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
+__global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                       uint32_t n_reads, uint32_t *n_frag, uint64_t *n_res)
 {
+    __shared__ uint32_t lds_read[WAVES_PER_WG][LDS_READ_WORDS];
+    __shared__ FqTables tabs;
+    fq_tables_init(tabs);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
-    if (r >= n_reads)
-        return;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES_PER_WG;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { /* the scans' tail */
+        n_frag[(uint64_t)n_reads * 6] = 0;
+        n_res[(uint64_t)n_reads * 6] = 0;
+    }
+    for (uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6); r < n_reads; r += stride)
+        count_read(bases, read_off, r, lane, lds_read[threadIdx.x >> 6], tabs, n_frag, n_res);
+}
+
+__device__ __forceinline__ void emit_read(const uint8_t *bases, const uint64_t *read_off, uint64_t r, uint32_t lane,
+                                          uint32_t *slot, const FqTables &tabs, const uint32_t *frag_base,
+                                          const uint64_t *res_base,
+                                          uint8_t *out_res, uint64_t *out_off, uint32_t *out_read, int8_t *out_frame,
+                                          uint32_t *out_start)
+{
     const uint8_t *b = bases + read_off[r];
     const uint64_t len = read_off[r + 1] - read_off[r];
     if (len <= SHORT_READ) {
+        const uint8_t *lb = len ? stage_read(slot, b, len, lane, tabs.cls) : tabs.cls;
         for (uint32_t f = 0; f < 6; f++) {
-            const FrameReader fr{b, len, frame_of(f)};
+            const LdsFrameReader fr{lb, tabs.code, len, frame_of(f)};
             const FrameFragments ff = frame_fragments(fr, lane);
             const uint64_t g = r * 6 + f;
             const uint64_t ri = res_base[g] + popc_below(ff.kept, lane);
@@ -208,6 +278,22 @@ __global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, cons
         frame_serial(FrameReader{b, len, frame_of(lane)}, (uint32_t)r, frag_base[g], res_base[g], frags, res, out_res,
                      out_off, out_read, out_frame, out_start);
     }
+}
+
+/* fragment records (offset, read, frame, first codon) and residues */
+__global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                      uint32_t n_reads, const uint32_t *frag_base,
+                                                      const uint64_t *res_base, uint8_t *out_res, uint64_t *out_off,
+                                                      uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
+{
+    __shared__ uint32_t lds_read[WAVES_PER_WG][LDS_READ_WORDS];
+    __shared__ FqTables tabs;
+    fq_tables_init(tabs);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES_PER_WG;
+    for (uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6); r < n_reads; r += stride)
+        emit_read(bases, read_off, r, lane, lds_read[threadIdx.x >> 6], tabs, frag_base, res_base, out_res, out_off,
+                  out_read, out_frame, out_start);
 }
 
 __global__ void fq_close_kernel(const uint32_t *frag_base, const uint64_t *res_base, uint64_t n_rf,
@@ -232,7 +318,10 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     HIP_TRY(c->fq_nres.reserve((n_rf + 1) * 8));
     HIP_TRY(c->fq_fbase.reserve((n_rf + 1) * 4));
     HIP_TRY(c->fq_rbase.reserve((n_rf + 1) * 8));
-    const dim3 wgs((uint32_t)(n_reads / WAVES_PER_WG + 1)); /* one wave per read, +1 for the scan's tail */
+    /* one wave per read in a grid-stride loop: workgroups live for many
+     * reads, so the dispatcher is not the limit (a read is ~100 cycles of
+     * work; a launch per read spent longer starting waves than running them) */
+    const dim3 wgs((uint32_t)std::min<uint64_t>((uint64_t)n_reads / WAVES_PER_WG + 1, 256ull * 16));
     if (n_reads)
         hipLaunchKernelGGL(fq_count_kernel, wgs, dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint64_t>());
