@@ -17,6 +17,7 @@
 #include <fstream>
 #include <iostream>
 #include <sstream>
+#include <thread>
 
 namespace kgx {
 
@@ -981,93 +982,247 @@ void FqRequest::process(const std::string &block, bool finished, std::ostream &o
     process(block.data(), block.size(), finished, os);
 }
 
-void FqRequest::process(const char *text, size_t n, bool finished, std::ostream &os)
+namespace {
+
+enum { FQ_START, FQ_ID, FQ_DEF, FQ_DATA, FQ_PLUS_START, FQ_PLUS, FQ_QUAL };
+
+/* FastqParser::parse_char (fastq_parser.h:40-150), line-at-a-time, over
+ * [p, end): the id runs to the first blank, sequence lines keep isalpha()
+ * characters only (others are reported there and dropped), '+' and quality
+ * lines are skipped; a record is emitted at the quality line's newline.  The
+ * current record's residues are built in place at the end of `bases`;
+ * `state` and `id` carry the parser across calls. */
+void fq_parse(const char *p, const char *end, int &state, std::string &id, std::string &bases,
+              std::vector<uint64_t> &roff, std::string &id_chars, std::vector<uint64_t> &id_off)
 {
-    /* FastqParser::parse_char (fastq_parser.h:40-150), line-at-a-time: the
-     * id runs to the first blank, sequence lines keep isalpha() characters
-     * only (others are reported there and dropped), '+' and quality lines
-     * are skipped; a record is emitted at the quality line's newline and by
-     * parse_complete() (fastq_parser.cc:29-35) */
     static const auto alpha = [] {
         std::array<bool, 256> t{};
         for (int c = 'A'; c <= 'Z'; c++)
             t[c] = t[c + 32] = true;
         return t;
     }();
-    enum { S_START, S_ID, S_DEF, S_DATA, S_PLUS_START, S_PLUS, S_QUAL };
-    FqBlock blk;
-    blk.bases.reserve(n / 2 + seq_.size());
-    /* the current record's residues are built in place at the end of
-     * blk.bases (a record cut by the block end is carried in seq_) */
-    blk.bases += seq_;
-    seq_.clear();
     auto emit = [&]() {
-        blk.ids.push_back(id_);
-        blk.roff.push_back(blk.bases.size());
-        id_.clear();
+        id_chars += id;
+        id_off.push_back(id_chars.size());
+        roff.push_back(bases.size());
+        id.clear();
     };
-    const char *p = text, *end = text + n;
     while (p < end) {
-        switch (state_) {
-        case S_START:
+        switch (state) {
+        case FQ_START:
             if (*p++ == '@')
-                state_ = S_ID;
+                state = FQ_ID;
             break;
-        case S_ID: {
+        case FQ_ID: {
             const char c = *p++;
             if (c == ' ' || c == '\t')
-                state_ = S_DEF;
+                state = FQ_DEF;
             else if (c == '\n')
-                state_ = S_DATA;
+                state = FQ_DATA;
             else
-                id_.push_back(c);
+                id.push_back(c);
             break;
         }
-        case S_DEF:
-        case S_PLUS:
-        case S_QUAL: {
+        case FQ_DEF:
+        case FQ_PLUS:
+        case FQ_QUAL: {
             const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(end - p)));
             if (!nl) {
                 p = end;
                 break;
             }
             p = nl + 1;
-            if (state_ == S_QUAL) {
+            if (state == FQ_QUAL) {
                 emit();
-                state_ = S_START;
+                state = FQ_START;
             } else {
-                state_ = state_ == S_DEF ? S_DATA : S_QUAL;
+                state = state == FQ_DEF ? FQ_DATA : FQ_QUAL;
             }
             break;
         }
-        case S_DATA: {
+        case FQ_DATA: {
             const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(end - p)));
             const char *stop = nl ? nl : end;
             const char *q = p;
             while (q < stop && alpha[(unsigned char)*q])
                 q++;
-            blk.bases.append(p, (size_t)(q - p)); /* the all-letter prefix in one go */
+            bases.append(p, (size_t)(q - p)); /* the all-letter prefix in one go */
             for (p = q; p < stop; p++)
                 if (alpha[(unsigned char)*p])
-                    blk.bases.push_back(*p);
+                    bases.push_back(*p);
             if (nl) {
                 p = nl + 1;
-                state_ = S_PLUS_START;
+                state = FQ_PLUS_START;
             }
             break;
         }
-        case S_PLUS_START:
+        case FQ_PLUS_START:
             if (*p++ == '+')
-                state_ = S_PLUS;
+                state = FQ_PLUS;
             break;
         }
     }
-    if (finished) {
-        emit();
-    } else {
-        seq_.assign(blk.bases, blk.roff.back(), std::string::npos);
-        blk.bases.resize(blk.roff.back());
+}
+
+/* a place to cut a FASTQ block for a parallel parse: a line that starts
+ * with '@' and whose next-but-one line starts with '+' (a record start in
+ * any well-formed file), searched from p for up to 1 MiB; null if none */
+const char *fq_cut_after(const char *p, const char *end)
+{
+    const char *limit = std::min(end, p + (1 << 20));
+    while (p < limit) {
+        const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(limit - p)));
+        if (!nl || nl + 1 >= end)
+            return nullptr;
+        const char *l0 = nl + 1;
+        if (*l0 == '@') {
+            const char *n1 = static_cast<const char *>(std::memchr(l0, '\n', (size_t)(end - l0)));
+            const char *n2 = n1 ? static_cast<const char *>(std::memchr(n1 + 1, '\n', (size_t)(end - n1 - 1))) : nullptr;
+            if (!n2)
+                return nullptr;
+            if (n2 + 1 < end && n2[1] == '+')
+                return l0;
+        }
+        p = l0;
     }
+    return nullptr;
+}
+
+}  // namespace
+
+void FqRequest::process(const char *text, size_t n, bool finished, std::ostream &os)
+{
+    const bool timing = std::getenv("KGX_FQ_TIMING") != nullptr;
+    const auto t_parse = std::chrono::steady_clock::now();
+    FqBlock blk;
+    /* the current record's residues are built in place at the end of
+     * blk.bases (a record cut by the block end is carried in seq_) */
+    blk.bases += seq_;
+    seq_.clear();
+    const char *end = text + n;
+    /* Large blocks are parsed in parallel: cut at record starts
+     * (fq_cut_after), chunk 0 continues the carried parser state, the others
+     * start speculatively in the start state.  A chunk's parse is used only
+     * if the exact sequential parse reaches its first byte in that state with
+     * nothing pending (the previous record emitted); otherwise it is parsed
+     * again from the true state.  The result is the sequential parse's. */
+    std::vector<const char *> cuts{text};
+    const size_t T = std::min<size_t>(16, n / (4u << 20));
+    for (size_t i = 1; i < T; i++) {
+        const char *c = fq_cut_after(text + n * i / T, end);
+        if (c && c > cuts.back())
+            cuts.push_back(c);
+    }
+    cuts.push_back(end);
+    const size_t K = cuts.size() - 1;
+    if (K == 1) {
+        blk.bases.reserve(blk.bases.size() + n / 2);
+        fq_parse(text, end, state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
+    } else {
+        if (parts_.size() < K)
+            parts_.resize(K);
+        std::vector<std::thread> pool;
+        for (size_t k = 1; k < K; k++)
+            pool.emplace_back([&, k]() {
+                FqPart &pt = parts_[k];
+                pt.state = FQ_START;
+                pt.id.clear();
+                pt.bases.clear();
+                pt.id_chars.clear();
+                pt.roff.assign(1, 0);
+                pt.id_off.assign(1, 0);
+                fq_parse(cuts[k], cuts[k + 1], pt.state, pt.id, pt.bases, pt.roff, pt.id_chars, pt.id_off);
+            });
+        fq_parse(cuts[0], cuts[1], state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
+        for (auto &th : pool)
+            th.join();
+        pool.clear();
+        /* chunks 1 .. A-1 began where the sequential parse is at a record start */
+        size_t A = 1;
+        {
+            int st = state_;
+            bool idle = id_.empty() && blk.bases.size() == blk.roff.back();
+            while (A < K && st == FQ_START && idle) {
+                const FqPart &pt = parts_[A];
+                st = pt.state;
+                idle = pt.id.empty() && pt.bases.size() == pt.roff.back();
+                A++;
+            }
+        }
+        if (A == K) { /* every speculation held: assemble in parallel */
+            std::vector<uint64_t> boff(K + 1, 0), roff_at(K + 1, 0), ioff(K + 1, 0), iat(K + 1, 0);
+            boff[1] = blk.bases.size();
+            roff_at[1] = blk.roff.size();
+            ioff[1] = blk.id_chars.size();
+            iat[1] = blk.id_off.size();
+            for (size_t k = 1; k < K; k++) {
+                const FqPart &pt = parts_[k];
+                boff[k + 1] = boff[k] + pt.bases.size();
+                roff_at[k + 1] = roff_at[k] + pt.roff.size() - 1;
+                ioff[k + 1] = ioff[k] + pt.id_chars.size();
+                iat[k + 1] = iat[k] + pt.id_off.size() - 1;
+            }
+            if (joined_cap_ < boff[K]) {
+                joined_.reset(new char[boff[K]]);
+                joined_cap_ = boff[K];
+            }
+            char *jb = joined_.get();
+            blk.roff.resize(roff_at[K]);
+            blk.id_off.resize(iat[K]);
+            blk.id_chars.resize(ioff[K]);
+            std::memcpy(jb, blk.bases.data(), blk.bases.size());
+            for (size_t k = 1; k < K; k++)
+                pool.emplace_back([&, k]() {
+                    const FqPart &pt = parts_[k];
+                    std::memcpy(jb + boff[k], pt.bases.data(), pt.bases.size());
+                    std::memcpy(&blk.id_chars[ioff[k]], pt.id_chars.data(), pt.id_chars.size());
+                    for (size_t i = 1; i < pt.roff.size(); i++)
+                        blk.roff[roff_at[k] + i - 1] = boff[k] + pt.roff[i];
+                    for (size_t i = 1; i < pt.id_off.size(); i++)
+                        blk.id_off[iat[k] + i - 1] = ioff[k] + pt.id_off[i];
+                });
+            for (auto &th : pool)
+                th.join();
+            blk.joined = jb;
+            blk.joined_len = boff[K];
+            blk.bases.clear();
+            state_ = parts_[K - 1].state;
+            id_ = parts_[K - 1].id;
+        } else { /* a cut missed a record start: append the good chunks, parse the rest exactly */
+            for (size_t k = 1; k < K; k++) {
+                const FqPart &pt = parts_[k];
+                if (k >= A) {
+                    fq_parse(cuts[k], cuts[k + 1], state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
+                    continue;
+                }
+                const uint64_t base = blk.bases.size(), ibase = blk.id_chars.size();
+                blk.bases += pt.bases;
+                blk.id_chars += pt.id_chars;
+                for (size_t i = 1; i < pt.roff.size(); i++)
+                    blk.roff.push_back(base + pt.roff[i]);
+                for (size_t i = 1; i < pt.id_off.size(); i++)
+                    blk.id_off.push_back(ibase + pt.id_off[i]);
+                state_ = pt.state;
+                id_ = pt.id;
+            }
+        }
+    }
+    if (finished) { /* parse_complete() emits the last record */
+        blk.id_chars += id_;
+        blk.id_off.push_back(blk.id_chars.size());
+        blk.roff.push_back(blk.residues_len());
+        id_.clear();
+    } else { /* the cut record's residues wait for the next block */
+        seq_.assign(blk.residues() + blk.roff.back(), blk.residues_len() - blk.roff.back());
+        if (blk.joined)
+            blk.joined_len = blk.roff.back();
+        else
+            blk.bases.resize(blk.roff.back());
+    }
+    if (timing)
+        std::fprintf(stderr, "[fq] %-12s %8.3f ms (%zu chunks)\n", "parse",
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_parse).count(),
+                     K);
     process_block(blk, os);
 }
 
@@ -1075,7 +1230,8 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
 {
     FqBlock blk;
     for (auto &r : reads) {
-        blk.ids.push_back(r.first);
+        blk.id_chars += r.first;
+        blk.id_off.push_back(blk.id_chars.size());
         blk.bases += r.second;
         blk.roff.push_back(blk.bases.size());
     }
@@ -1084,7 +1240,7 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
 
 void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
 {
-    const uint32_t n_reads = (uint32_t)blk.ids.size();
+    const uint32_t n_reads = (uint32_t)blk.n_reads();
     if (n_reads == 0)
         return;
     /* KGX_FQ_TIMING=1: per-phase wall times on stderr */
@@ -1102,7 +1258,7 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     /* the block's reads -> fragments -> lookup, one GPU batch */
     kgx_ctx *ctx = kg_.ctx();
     kgx_fragments fr;
-    int rc = kgx_fq_fragments(ctx, blk.bases.data(), blk.roff.data(), n_reads, &fr);
+    int rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff.data(), n_reads, &fr);
     if (rc)
         throw_last(rc, "kgx_fq_fragments");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
@@ -1181,7 +1337,7 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
         const bool has_calls = next_called < called.size() && called[next_called] == r;
         if (has_calls)
             next_called++;
-        if (blk.ids[r].empty())
+        if (blk.id_len(r) == 0)
             continue;
         if (!families && !has_calls)
             continue; /* no calls in any frame: no output, no mapper state */
@@ -1226,7 +1382,8 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
                     throw_last(rc, "fragment offsets");
                 offs = slice.data() - f0;
             }
-            os << blk.ids[r] << "\t" << best_frame << "\t" << best_score << "\t";
+            os.write(blk.id(r), (std::streamsize)blk.id_len(r));
+            os << "\t" << best_frame << "\t" << best_score << "\t";
             for (size_t i = 0; i < best_matches.size(); i++) {
                 const uint64_t g2 = best_frag[i];
                 if (i)

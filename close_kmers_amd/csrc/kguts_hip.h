@@ -357,10 +357,26 @@ public:
     void process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os);
 
 private:
-    struct FqBlock { /* parsed reads: ids, bases concatenated, offsets */
-        std::vector<std::string> ids;
-        std::string bases;
+    /* parsed reads, flat: read r's id is id_chars[id_off[r], id_off[r+1]),
+     * its bases [roff[r], roff[r+1]) of the residues */
+    struct FqBlock {
+        std::string bases; /* the bases of a one-piece parse */
+        std::string id_chars;
+        std::vector<uint64_t> id_off{0};
         std::vector<uint64_t> roff{0};
+        const char *joined = nullptr; /* the bases of a parallel parse, assembled (FqRequest::joined_) */
+        uint64_t joined_len = 0;
+        const char *residues() const { return joined ? joined : bases.data(); }
+        uint64_t residues_len() const { return joined ? joined_len : bases.size(); }
+        size_t n_reads() const { return id_off.size() - 1; }
+        const char *id(size_t r) const { return id_chars.data() + id_off[r]; }
+        size_t id_len(size_t r) const { return (size_t)(id_off[r + 1] - id_off[r]); }
+    };
+    /* a parallel parse's chunk (kept across blocks, so its buffers are reused) */
+    struct FqPart {
+        int state = 0;
+        std::string id, bases, id_chars;
+        std::vector<uint64_t> roff{0}, id_off{0};
     };
     void process_block(const FqBlock &blk, std::ostream &os);
     KmerGuts &kg_;
@@ -368,6 +384,9 @@ private:
     /* FastqParser state (fastq_parser.h:40-150) */
     int state_ = 0;
     std::string id_, seq_;
+    std::vector<FqPart> parts_;
+    std::unique_ptr<char[]> joined_;
+    size_t joined_cap_ = 0;
 };
 
 /* one host-buffer batch through kg's context, device results only (no D2H):

@@ -399,8 +399,11 @@ int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets
     }
     HIP_TRY(c->fq_bases.reserve(nb + 16));
     HIP_TRY(c->fq_roff.reserve(((uint64_t)n_reads + 1) * 8));
-    if (nb)
-        HIP_TRY(hipMemcpyAsync(c->fq_bases.p, bases + r0, nb, hipMemcpyHostToDevice, c->stream));
+    if (nb) { /* through the context's pinned staging: DMA at link speed */
+        HIP_TRY(c->h_res.resize(nb));
+        parallel_memcpy(c->h_res.data(), bases + r0, nb);
+        HIP_TRY(hipMemcpyAsync(c->fq_bases.p, c->h_res.data(), nb, hipMemcpyHostToDevice, c->stream));
+    }
     HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
     return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, out);
 }

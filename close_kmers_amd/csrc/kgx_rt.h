@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kgx_internal.h"
@@ -122,6 +123,25 @@ template <class T> struct PinnedVec {
 };
 
 inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
+
+/* memcpy by up to 8 host threads for large copies (host staging into pinned
+ * buffers runs at several times one core's copy rate) */
+inline void parallel_memcpy(void *dst, const void *src, size_t n)
+{
+    const size_t T = std::min<size_t>(8, n >> 23); /* one thread per 8 MiB, up to 8 */
+    if (T <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < T; t++)
+        pool.emplace_back([=]() {
+            const size_t a = n * t / T, b = n * (t + 1) / T;
+            std::memcpy(static_cast<char *>(dst) + a, static_cast<const char *>(src) + a, b - a);
+        });
+    for (auto &th : pool)
+        th.join();
+}
 
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
                  kgx_fragments *out);

@@ -123,3 +123,53 @@ def test_fragments_of_long_and_empty_batches(gpu, oracle_lib):
         got.setdefault(int(h["read"][i]), []).append((int(h["frame"][i]), s))
     for r, dna in enumerate(reads):
         assert got.get(r, []) == oracle_lib.fq_fragments(dna), r
+
+
+_BACK = {"A": "GCT", "C": "TGT", "D": "GAT", "E": "GAA", "F": "TTT", "G": "GGT", "H": "CAT", "I": "ATT",
+         "K": "AAA", "L": "CTT", "M": "ATG", "N": "AAT", "P": "CCT", "Q": "CAA", "R": "CGT", "S": "TCT",
+         "T": "ACT", "V": "GTT", "W": "TGG", "Y": "TAT"}
+
+
+def test_fq_handler_parallel_parse_matches_oracle(gpu, oracle_lib, tmp_path):
+    """A 40 MB FASTQ block is parsed by several threads (cut at record starts,
+    each cut checked against the sequential parse): the handler's output must
+    equal the oracle's, with irregular records at and around the cuts
+    (quality lines starting with '@', blank lines, descriptions, non-letters
+    and lower case in sequence lines, reads without calls), and equal the
+    output of the same text fed as small blocks."""
+    from close_kmers_amd import synth
+    from helpers import data_dir_for
+    spec, table = synthetic_table(30000)
+    d = data_dir_for(str(tmp_path), table)
+    rng = np.random.default_rng(31)
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(spec.n_src))].reshape(spec.n_src, -1)
+    recs = []
+    for i in range(130000):
+        if i % 3:
+            p = bytes(src[int(rng.integers(0, spec.n_src))]).decode()
+            a = int(rng.integers(0, len(p) - 50))
+            seq = "".join(_BACK[c] for c in p[a:a + 50])
+        else:
+            seq = "".join("ACGT"[x] for x in rng.integers(0, 4, 150))
+        qual = "I" * len(seq)
+        head = f"r{i}"
+        if i % 997 == 0:
+            qual = "@" + qual[1:]          # a quality line that looks like a header
+        if i % 1009 == 0:
+            head += "\tsome description"
+        if i % 1013 == 0:
+            seq = seq[:40].lower() + "N1-" + seq[40:]
+        blank = "\n" if i % 1019 == 0 else ""
+        recs.append(f"{blank}@{head}\n{seq}\n+\n{qual}\n")
+    fastq = "".join(recs).encode()
+    assert len(fastq) > 32 << 20
+    path = tmp_path / "reads.fq"
+    path.write_bytes(fastq)
+    want = oracle_lib.query_text(d, str(path), "fq", {})
+    assert want.count(b"\n") > 50000
+    with gpu.Image.from_table(table) as img, gpu.FqHandler(img, d) as fq:
+        assert fq.process(fastq, True) == want
+    with gpu.Image.from_table(table) as img, gpu.FqHandler(img, d) as fq:
+        cuts = [0] + sorted(int(x) for x in rng.integers(1, len(fastq), 12)) + [len(fastq)]
+        out = b"".join(fq.process(fastq[a:b], b == len(fastq)) for a, b in zip(cuts, cuts[1:]))
+    assert out == want
