@@ -158,6 +158,7 @@ SIGNATURES = {
     "kgx_ctx_create": (_INT, [_P, _PP]),
     "kgx_ctx_destroy": (_INT, [_P]),
     "kgx_find_best_calls": (_INT, [_P, _P, _P, _U32, _P]),
+    "kgx_fq_called_reads": (_INT, [_P, _P, _P]),
     "kgx_ctx_stream": (_P, [_P]),
     "kgx_ctx_set_stream": (_INT, [_P, _P]),
     "kgx_ctx_set_option": (_INT, [_P, _CS, ctypes.c_int64]),

@@ -1278,6 +1278,63 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     if (rc)
         throw_last(rc, "kgx_run_device");
     mark("lookup");
+    if (!families) {
+        /* only the reads with a call in some fragment come back (sparse):
+         * the others produce no output and no mapper state */
+        kgx_fq_called cr;
+        if ((rc = kgx_fq_called_reads(ctx, &fr, &cr)))
+            throw_last(rc, "kgx_fq_called_reads");
+        mark("collect");
+        FamilyMapper mapper(kg_, mapping_);
+        const std::vector<std::pair<uint64_t, uint32_t>> no_hits;
+        std::vector<KmerCall> calls;
+        std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
+        std::vector<uint32_t> match_len, best_len;
+        for (uint32_t i = 0; i < cr.n; i++) {
+            const uint32_t r = cr.reads[i];
+            if (blk.id_len(r) == 0)
+                continue;
+            double best_score = 0.0;
+            int best_frame = 0;
+            best_matches.clear();
+            best_len.clear();
+            uint64_t g = cr.frag_offsets[i];
+            for (int fs = 0; fs < 6; fs++) {
+                const int frame = fs < 3 ? fs + 1 : -(fs - 2);
+                const uint64_t g_end = g + cr.frame_counts[(size_t)i * 6 + fs];
+                double score = 0.0;
+                matches.clear();
+                match_len.clear();
+                for (; g < g_end; g++) {
+                    calls.clear();
+                    for (uint64_t c = cr.call_offsets[g]; c < cr.call_offsets[g + 1]; c++)
+                        calls.emplace_back(cr.calls[c].start, cr.calls[c].end, cr.calls[c].count,
+                                           cr.calls[c].function_index, cr.calls[c].weighted_hits);
+                    matches.emplace_back(0, mapper.find_best_family_match(no_hits, nullptr, calls));
+                    match_len.push_back(cr.frag_len[g]);
+                    score += matches.back().second.score;
+                    if (score > best_score) {
+                        best_score = score;
+                        best_frame = frame;
+                        best_matches = matches;
+                        best_len = match_len;
+                    }
+                }
+            }
+            if (best_score > 0.0) {
+                os.write(blk.id(r), (std::streamsize)blk.id_len(r));
+                os << "\t" << best_frame << "\t" << best_score << "\t";
+                for (size_t k = 0; k < best_matches.size(); k++) {
+                    if (k)
+                        os << "\t";
+                    os << (size_t)best_len[k] << "\t" << best_matches[k].second;
+                }
+                os << std::endl;
+            }
+        }
+        mark("host loop");
+        return;
+    }
     /* fragments per (read, frame): fragment g of read r, frame slot k */
     std::vector<uint32_t> fcount((size_t)n_reads * 6);
     if ((rc = kgx_ctx_synchronize(ctx)) || (rc = kgx_memcpy_d2h(fcount.data(), fr.frame_counts, fcount.size() * 4)))

@@ -368,6 +368,152 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     return KGX_OK;
 }
 
+/* ---- reads with calls (kgx_fq_called_reads) ---- */
+
+/* flag[r] = read r has a fragment with a call (fbase = scanned per-(read,
+ * frame) fragment counts: read r's fragments are [fbase[6r], fbase[6r+6])) */
+__global__ void fq_flag_called_kernel(uint32_t n_reads, const uint32_t *fbase, const uint32_t *call_count,
+                                      uint32_t *flag)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_reads)
+        return;
+    uint32_t any = 0;
+    for (uint32_t g = fbase[6 * r]; g < fbase[6 * r + 6] && !any; g++)
+        any = call_count[g] != 0;
+    flag[r] = any;
+}
+
+/* per selected read: its fragment and call totals */
+__global__ void fq_called_sizes_kernel(uint32_t n, const uint32_t *reads, const uint32_t *fbase,
+                                       const uint32_t *call_count, uint64_t *nfrag, uint64_t *ncall)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n)
+        return;
+    if (i == n) { /* the scans' tails */
+        nfrag[n] = 0;
+        ncall[n] = 0;
+        return;
+    }
+    const uint64_t r = reads[i];
+    uint64_t c = 0;
+    for (uint32_t g = fbase[6 * r]; g < fbase[6 * r + 6]; g++)
+        c += call_count[g];
+    nfrag[i] = fbase[6 * r + 6] - fbase[6 * r];
+    ncall[i] = c;
+}
+
+/* per selected read: frame counts, fragment lengths, per-fragment call CSR and the calls */
+__global__ void fq_called_fill_kernel(uint32_t n, const uint32_t *reads, const uint32_t *fbase,
+                                      const uint32_t *frame_counts, const uint64_t *frag_off,
+                                      const uint32_t *call_count, const uint64_t *wbase, const kgx_call *calls,
+                                      const uint64_t *fo, const uint64_t *co, uint32_t *out_fc, uint32_t *out_len,
+                                      uint64_t *out_coff, kgx_call *out_calls)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t r = reads[i];
+    for (int f = 0; f < 6; f++)
+        out_fc[6 * i + f] = frame_counts[6 * r + f];
+    uint64_t at = fo[i], c = co[i];
+    for (uint32_t g = fbase[6 * r]; g < fbase[6 * r + 6]; g++, at++) {
+        out_len[at] = (uint32_t)(frag_off[g + 1] - frag_off[g]);
+        out_coff[at] = c;
+        const kgx_call *src = calls + wbase[g];
+        for (uint32_t k = 0; k < call_count[g]; k++)
+            out_calls[c++] = src[k];
+    }
+    if (i == n - 1)
+        out_coff[at] = c;
+}
+
+int fq_called_reads(kgx_ctx *c, const kgx_fragments *fr, kgx_fq_called *out)
+{
+    hipStream_t st = c->stream;
+    const uint32_t n_reads = fr->n_reads;
+    if (c->n_seq != fr->n_fragments || !c->have_hits)
+        return fail(KGX_EINVAL, "kgx_fq_called_reads: run kgx_run_device over these fragments first");
+    const uint32_t *fbase = c->fq_fbase.as<uint32_t>();
+    HIP_TRY(c->fqc_flag.reserve(((uint64_t)n_reads + 1) * 4));
+    HIP_TRY(c->fqc_reads.reserve(((uint64_t)n_reads + 1) * 4));
+    HIP_TRY(c->fqc_nsel.reserve(8));
+    if (n_reads)
+        hipLaunchKernelGGL(fq_flag_called_kernel, grid_for(n_reads), dim3(256), 0, st, n_reads, fbase,
+                           c->call_count.as<uint32_t>(), c->fqc_flag.as<uint32_t>());
+    size_t tb = 0;
+    hipcub::CountingInputIterator<uint32_t> ids(0);
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, ids, c->fqc_flag.as<uint32_t>(), c->fqc_reads.as<uint32_t>(),
+                                          c->fqc_nsel.as<uint32_t>(), (int)n_reads, st));
+    HIP_TRY(c->fq_tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(c->fq_tmp.p, tb, ids, c->fqc_flag.as<uint32_t>(),
+                                          c->fqc_reads.as<uint32_t>(), c->fqc_nsel.as<uint32_t>(), (int)n_reads, st));
+    HIP_TRY(c->h_fqc_n.resize(1));
+    HIP_TRY(hipMemcpyAsync(c->h_fqc_n.data(), c->fqc_nsel.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint32_t n = n_reads ? c->h_fqc_n[0] : 0;
+    HIP_TRY(c->fqc_nfrag.reserve(((uint64_t)n + 1) * 8));
+    HIP_TRY(c->fqc_ncall.reserve(((uint64_t)n + 1) * 8));
+    HIP_TRY(c->fqc_fo.reserve(((uint64_t)n + 1) * 8));
+    HIP_TRY(c->fqc_co.reserve(((uint64_t)n + 1) * 8));
+    hipLaunchKernelGGL(fq_called_sizes_kernel, grid_for(n + 1), dim3(256), 0, st, n, c->fqc_reads.as<uint32_t>(),
+                       fbase, c->call_count.as<uint32_t>(), c->fqc_nfrag.as<uint64_t>(), c->fqc_ncall.as<uint64_t>());
+    size_t t1 = 0, t2 = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, c->fqc_nfrag.as<uint64_t>(), c->fqc_fo.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, c->fqc_ncall.as<uint64_t>(), c->fqc_co.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(c->fq_tmp.reserve(std::max(t1, t2)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->fq_tmp.p, t1, c->fqc_nfrag.as<uint64_t>(), c->fqc_fo.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->fq_tmp.p, t2, c->fqc_ncall.as<uint64_t>(), c->fqc_co.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(c->h_fqc_tot.resize(2));
+    HIP_TRY(hipMemcpyAsync(c->h_fqc_tot.data(), c->fqc_fo.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_fqc_tot.data() + 1, c->fqc_co.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t nf = c->h_fqc_tot[0], nc = c->h_fqc_tot[1];
+    HIP_TRY(c->fqc_fc.reserve(((uint64_t)n * 6 + 1) * 4));
+    HIP_TRY(c->fqc_len.reserve((nf + 1) * 4));
+    HIP_TRY(c->fqc_coff.reserve((nf + 1) * 8));
+    HIP_TRY(c->fqc_calls.reserve((nc + 1) * sizeof(kgx_call)));
+    if (n)
+        hipLaunchKernelGGL(fq_called_fill_kernel, grid_for(n), dim3(256), 0, st, n, c->fqc_reads.as<uint32_t>(), fbase,
+                           fr->frame_counts, fr->offsets, c->call_count.as<uint32_t>(), c->wbase.as<uint64_t>(),
+                           c->calls.as<kgx_call>(), c->fqc_fo.as<uint64_t>(), c->fqc_co.as<uint64_t>(),
+                           c->fqc_fc.as<uint32_t>(), c->fqc_len.as<uint32_t>(), c->fqc_coff.as<uint64_t>(),
+                           c->fqc_calls.as<kgx_call>());
+    else
+        HIP_TRY(hipMemsetAsync(c->fqc_coff.p, 0, 8, st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(c->h_fqc_reads.resize(n + 1));
+    HIP_TRY(c->h_fqc_fc.resize((uint64_t)n * 6 + 1));
+    HIP_TRY(c->h_fqc_fo.resize(n + 1));
+    HIP_TRY(c->h_fqc_len.resize(nf + 1));
+    HIP_TRY(c->h_fqc_coff.resize(nf + 1));
+    HIP_TRY(c->h_fqc_calls.resize(nc + 1));
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(c->h_fqc_reads.data(), c->fqc_reads.p, (uint64_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_fqc_fc.data(), c->fqc_fc.p, (uint64_t)n * 24, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipMemcpyAsync(c->h_fqc_fo.data(), c->fqc_fo.p, ((uint64_t)n + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (nf)
+        HIP_TRY(hipMemcpyAsync(c->h_fqc_len.data(), c->fqc_len.p, nf * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(c->h_fqc_coff.data(), c->fqc_coff.p, (nf + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (nc)
+        HIP_TRY(hipMemcpyAsync(c->h_fqc_calls.data(), c->fqc_calls.p, nc * sizeof(kgx_call), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    out->n = n;
+    out->reads = c->h_fqc_reads.data();
+    out->frame_counts = c->h_fqc_fc.data();
+    out->frag_offsets = c->h_fqc_fo.data();
+    out->frag_len = c->h_fqc_len.data();
+    out->call_offsets = c->h_fqc_coff.data();
+    out->calls = c->h_fqc_calls.data();
+    return KGX_OK;
+}
+
 }  // namespace kgx
 
 extern "C" {
@@ -379,6 +525,14 @@ int kgx_fq_fragments_device(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *
         return fail(KGX_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(c->img->device));
     return fq_fragments(c, d_bases, d_read_offsets, n_reads, out);
+}
+
+int kgx_fq_called_reads(kgx_ctx *c, const kgx_fragments *fragments, kgx_fq_called *out)
+{
+    if (!c || !fragments || !out)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->img->device));
+    return fq_called_reads(c, fragments, out);
 }
 
 int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,

@@ -196,6 +196,12 @@ struct kgx_ctx {
     /* fq fragments (kgx_fq.hip) */
     kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_nres, fq_fbase, fq_rbase, fq_tmp, fq_res, fq_off, fq_read,
         fq_frame, fq_start;
+    /* kgx_fq_called_reads */
+    kgx::DevBuf fqc_flag, fqc_reads, fqc_nsel, fqc_nfrag, fqc_ncall, fqc_fo, fqc_co, fqc_fc, fqc_len, fqc_coff,
+        fqc_calls;
+    kgx::PinnedVec<uint32_t> h_fqc_n, h_fqc_reads, h_fqc_fc, h_fqc_len;
+    kgx::PinnedVec<uint64_t> h_fqc_tot, h_fqc_fo, h_fqc_coff;
+    kgx::PinnedVec<kgx_call> h_fqc_calls;
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;

@@ -370,6 +370,26 @@ int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offse
 int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint32_t n_reads, kgx_fragments *out);
 
+/* After kgx_run_device over a kgx_fragments batch (with KGX_WANT_CALLS): only
+ * the reads that have a call in some fragment, in read order, with what the
+ * fq handler's frame choice reads of them (fq_process_request.cc:298-365):
+ * per read its fragments per frame, per fragment its length and its calls.
+ * Host views owned by the context, valid until its next call:
+ *   reads[n]                       read indices
+ *   frame_counts[6 n]              fragments per (read, frame)
+ *   frag_offsets[n + 1]            read i's fragments [frag_offsets[i], frag_offsets[i+1])
+ *   frag_len[...], call_offsets[...+1], calls[...]   per fragment */
+typedef struct kgx_fq_called {
+    uint32_t n;
+    const uint32_t *reads;
+    const uint32_t *frame_counts;
+    const uint64_t *frag_offsets;
+    const uint32_t *frag_len;
+    const uint64_t *call_offsets;
+    const kgx_call *calls;
+} kgx_fq_called;
+int kgx_fq_called_reads(kgx_ctx *ctx, const kgx_fragments *fragments, kgx_fq_called *out);
+
 /* ---- the fq request handler (FqProcessRequest, fq_process_request.cc) ---
  * FASTQ text in, the handler's output lines out (per read: best frame,
  * score and the frame's family matches, fq_process_request.cc:298-365, over
