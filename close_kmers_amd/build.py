@@ -2,6 +2,7 @@
 
     libkgx.so   kernels (csrc/kgx_kernels.hip) + C ABI runtime + KmerGuts facade
     kgx_query   request-handler surface driver linked against libkgx.so
+    kgx_server  the kser HTTP request server (krequest2.cc routes) over libkgx.so
 
 hipcc cross-compiles for gfx950 without a GPU, so this runs in the CPU
 container as well as on the GPU box.
@@ -18,12 +19,13 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libkgx.so")
 QUERY = os.path.join(PKG, "kgx_query")
+SERVER = os.path.join(PKG, "kgx_server")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 LIB_SOURCES = ["kgx_lookup.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
-               "kguts_hip.cpp"]
-HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h"]
+               "kguts_hip.cpp", "kgx_handlers.cpp"]
+HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h", "kgx_handlers.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-Wall", "-Wno-unused-function"]
 
@@ -50,20 +52,25 @@ def build(force: bool = False, verbose: bool = False) -> None:
         for src in LIB_SOURCES:
             obj = os.path.join(CSRC, "_obj", src + ".o")
             os.makedirs(os.path.dirname(obj), exist_ok=True)
+            objs.append(obj)
+            # an object is rebuilt when its source, a header or this script changed
+            obj_deps = [os.path.join(CSRC, src)] + [d for d in deps if not d.endswith((".hip", ".cpp"))]
+            if not force and not _newer(obj, obj_deps):
+                continue
             cmd = [HIPCC] + COMMON + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
             if verbose:
                 print(" ".join(cmd))
             _run(cmd)
-            objs.append(obj)
         tmp = LIB + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
         os.replace(tmp, LIB)
-    qsrc = os.path.join(CSRC, "kgx_query.cpp")
-    if force or _newer(QUERY, [qsrc, LIB] + deps):
-        tmp = QUERY + ".tmp"
-        _run([HIPCC] + COMMON + ["-x", "hip", qsrc, "-o", tmp, f"-L{PKG}", "-lkgx",
-                                 "-Wl,-rpath,$ORIGIN"])
-        os.replace(tmp, QUERY)
+    for exe, src in ((QUERY, "kgx_query.cpp"), (SERVER, "kgx_server.cpp")):
+        esrc = os.path.join(CSRC, src)
+        if force or _newer(exe, [esrc, LIB] + deps):
+            tmp = exe + ".tmp"
+            _run([HIPCC] + COMMON + ["-x", "hip", esrc, "-o", tmp, f"-L{PKG}", "-lkgx",
+                                     "-Wl,-rpath,$ORIGIN", "-pthread"])
+            os.replace(tmp, exe)
 
 
 if __name__ == "__main__":

@@ -544,6 +544,16 @@ std::string KmerPegMapping::decode_id(encoded_id_t id) const
     return id < id_to_peg_.size() ? id_to_peg_[id] : std::string();
 }
 
+void KmerPegMapping::dump_sizes(std::ostream &os) const
+{
+    os << "kmer_to_id_: size=" << kgx_kmap_num_kmers(kmer_to_id_) << "\n";
+    os << "kmer_to_id_: content size=" << kgx_kmap_num_values(kmer_to_id_) << "\n";
+    os << "peg_to_id_: size=" << peg_to_id_.size() << "\n";
+    os << "id_to_peg_: size=" << id_to_peg_.size() << "\n";
+    os << "genome_to_id_: size=0\n";
+    os << "id_to_genome_: size=0\n";
+}
+
 void KmerPegMapping::add_batch_mappings(KmerGuts &kg, const std::vector<encoded_id_t> &ids)
 {
     int rc = kgx_kmap_add_hits(kmer_to_id_, kg.ctx(), ids.data());

@@ -203,6 +203,9 @@ public:
 
     encoded_id_t encode_id(const std::string &peg);
     std::string decode_id(encoded_id_t id) const; /* "" when unknown, kmer.cc:288-295 */
+    /* GET /dump_sizes body for this mapping (kmer.cc:510-524); the genome
+     * tables are never filled by the request path, so they print 0 */
+    void dump_sizes(std::ostream &os) const;
     /* add_mapping (kmer.cc:173-210) for every hit of kg's last batch, in
      * order: sequence s contributes ids[s] (add_request.cc:164-170) */
     void add_batch_mappings(KmerGuts &kg, const std::vector<encoded_id_t> &ids);

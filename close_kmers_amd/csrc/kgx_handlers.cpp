@@ -1,0 +1,364 @@
+/*
+ * kgx_handlers.cpp -- request handlers and the HTTP request router over the
+ * KmerGuts facade (see kgx_handlers.h).
+ */
+#include "kgx_handlers.h"
+
+#include <algorithm>
+#include <cctype>
+#include <regex>
+#include <sstream>
+
+namespace kgx {
+
+work_list_t parse_fasta_body(const char *body, size_t n)
+{
+    work_list_t work;
+    FastaParser parser;
+    parser.set_callback([&work](const std::string &id, const std::string &seq) {
+        work.emplace_back(id, seq);
+        return 0;
+    });
+    for (size_t i = 0; i < n; i++)
+        parser.parse_char(body[i]);
+    parser.parse_complete();
+    return work;
+}
+
+int param_int(const request_params_t &params, const std::string &name, int dflt)
+{
+    auto it = params.find(name);
+    if (it == params.end())
+        return dflt;
+    try {
+        return std::stoi(it->second);
+    } catch (...) {
+        return dflt;
+    }
+}
+
+static std::vector<KmerGuts::SeqJob> jobs_for(const work_list_t &work)
+{
+    std::vector<KmerGuts::SeqJob> jobs(work.size());
+    for (size_t i = 0; i < work.size(); i++) {
+        jobs[i].id = work[i].first;
+        jobs[i].seq = work[i].second;
+        jobs[i].calls = std::make_shared<std::vector<KmerCall>>();
+        jobs[i].otu_stats = std::make_shared<KmerOtuStats>();
+    }
+    return jobs;
+}
+
+void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_best_call,
+                   std::ostream &os)
+{
+    std::vector<KmerGuts::SeqJob> jobs = jobs_for(work);
+    std::vector<std::shared_ptr<std::vector<KmerGuts::hit_in_sequence_t>>> hit_lists(jobs.size());
+    if (details && !find_best_call) /* the HIT lines are printed only without find_best_call */
+        for (size_t i = 0; i < jobs.size(); i++) {
+            auto hl = std::make_shared<std::vector<KmerGuts::hit_in_sequence_t>>();
+            hit_lists[i] = hl;
+            jobs[i].hit_cb = [hl](KmerGuts::hit_in_sequence_t h) { hl->push_back(h); };
+        }
+    kg.process_aa_batch(jobs);
+    for (size_t i = 0; i < jobs.size(); i++) {
+        const std::string &id = jobs[i].id, &seq = jobs[i].seq;
+        auto &calls = *jobs[i].calls;
+        if (find_best_call) { /* query_request.cc:124-135 */
+            int fi;
+            std::string fn;
+            float score, wscore, off = 0.0f;
+            kg.find_best_call(calls, fi, fn, score, wscore, off);
+            if (!fn.empty())
+                os << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+            continue;
+        }
+        os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+        for (auto &c : calls)
+            os << kg.format_call(c);
+        if (hit_lists[i])
+            for (auto &h : *hit_lists[i])
+                os << kg.format_hit(h);
+        os << kg.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
+    }
+}
+
+void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work, int silent,
+                 std::ostream &os)
+{
+    std::vector<KmerGuts::SeqJob> jobs = jobs_for(work);
+    kg.process_aa_batch(jobs); /* the batch's hits stay on the device for the mapping */
+    if (!silent)
+        for (auto &j : jobs) { /* add_request.cc:134-161 */
+            os << "PROTEIN-ID\t" << j.id << "\t" << j.seq.size() << "\n";
+            for (auto &c : *j.calls)
+                os << kg.format_call(c);
+            os << kg.format_otu_stats(j.id, j.seq.size(), *j.otu_stats);
+            int fi;
+            std::string fn;
+            /* uninitialised in the reference when there are no calls
+             * (add_request.cc:143-150, kguts.cc:1015-1018); 0 here */
+            float score, wscore, off = 0.0f;
+            kg.find_best_call(*j.calls, fi, fn, score, wscore, off);
+            if (fn.empty() || fn.find(" ?? ") != std::string::npos)
+                fn = "hypothetical protein";
+            os << "BEST-CALL\t" << j.id << "\t" << fn << "\t" << score << "\t" << wscore << "\t" << off
+               << "\n";
+        }
+    /* add_request.cc:164-170: ids encoded in request order, every hit's
+     * k-mer mapped to its sequence's id */
+    std::vector<KmerPegMapping::encoded_id_t> ids;
+    ids.reserve(jobs.size());
+    for (auto &j : jobs)
+        ids.push_back(mapping.encode_id(j.id));
+    mapping.add_batch_mappings(kg, ids);
+}
+
+void matrix_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, const work_list_t &work,
+                    std::ostream &os)
+{
+    MatrixRequest mx(mapping);
+    mx.process_work(kg, work);
+    mx.write_results(os);
+}
+
+void lookup_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
+                    const request_params_t &params, const work_list_t &work, std::ostream &os)
+{
+    LookupRequest req(mapping, family_mode, params);
+    req.process_work(kg, work, os);
+}
+
+void fq_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, const char *body, size_t n,
+                std::ostream &os)
+{
+    FqRequest req(kg, mapping);
+    req.process(body, n, true, os);
+}
+
+/* ---- HTTP request framing (krequest2.cc) -------------------------------- */
+
+bool parse_request_line(const std::string &line, HttpRequest &req)
+{
+    /* krequest2.cc:24 */
+    static const std::regex request_regex("^([A-Z]+) ([^?#]*)(\\?([^#]*))?(#(.*))? HTTP/(\\d+\\.\\d+)");
+    std::smatch m;
+    if (!std::regex_match(line, m, request_regex))
+        return false;
+    req.method = m[1];
+    req.path = m[2];
+    req.parameters_raw = m[4];
+    req.fragment = m[6];
+    req.http_version = m[7];
+    /* krequest2.cc:113-125: split on ';' or '&', keep "k=v" parts */
+    size_t b = 0;
+    const std::string &raw = req.parameters_raw;
+    while (!raw.empty() && b <= raw.size()) {
+        size_t e = raw.find_first_of(";&", b);
+        if (e == std::string::npos)
+            e = raw.size();
+        const std::string part = raw.substr(b, e - b);
+        const size_t eq = part.find('=');
+        if (eq != std::string::npos)
+            req.parameters[part.substr(0, eq)] = part.substr(eq + 1);
+        b = e + 1;
+    }
+    return true;
+}
+
+void parse_header_line(const std::string &line, HttpRequest &req)
+{
+    /* krequest2.cc:176-186 */
+    size_t x = line.find(':');
+    std::string k = line.substr(0, x);
+    std::string v;
+    if (x != std::string::npos) {
+        x++;
+        while (x < line.size() && line[x] == ' ')
+            x++;
+        v = line.substr(x);
+    }
+    std::transform(k.begin(), k.end(), k.begin(), [](unsigned char c) { return std::tolower(c); });
+    req.headers[k] = v;
+}
+
+/* ---- router --------------------------------------------------------------- */
+
+class KmerRequestRouter::GutsLease {
+public:
+    explicit GutsLease(KmerRequestRouter &r) : r_(r), kg_(r.acquire()) {}
+    ~GutsLease() { r_.release(kg_); }
+    KmerGuts &operator*() { return *kg_; }
+
+private:
+    KmerRequestRouter &r_;
+    KmerGuts *kg_;
+};
+
+KmerRequestRouter::KmerRequestRouter(const Options &opt)
+    : opt_(opt), family_mode_(!opt.families_file.empty()) /* kser.cc:289 */
+{
+    image_ = std::make_shared<KmerImage>(opt_.kmer_data_dir, opt_.device);
+    const int n = std::max(1, opt_.n_kmer_threads);
+    for (int i = 0; i < n; i++) {
+        pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, image_));
+        idle_.push_back(pool_.back().get());
+    }
+    /* kserver.cc:40-130: the family DB goes into the root mapping */
+    auto root = std::make_shared<KmerPegMapping>(opt_.device);
+    mapping_map_[""] = root;
+    if (!opt_.genus_mapping.empty())
+        root->load_genus_map(opt_.genus_mapping);
+    if (!opt_.families_file.empty())
+        root->load_families(opt_.families_file);
+    if (family_mode_)
+        for (auto &nr : opt_.families_nr)
+            root->load_nr_families(*pool_[0], nr);
+}
+
+KmerRequestRouter::~KmerRequestRouter() = default;
+
+KmerGuts *KmerRequestRouter::acquire()
+{
+    std::unique_lock<std::mutex> lk(pool_mu_);
+    pool_cv_.wait(lk, [this] { return !idle_.empty(); });
+    KmerGuts *kg = idle_.back();
+    idle_.pop_back();
+    return kg;
+}
+
+void KmerRequestRouter::release(KmerGuts *kg)
+{
+    {
+        std::lock_guard<std::mutex> lk(pool_mu_);
+        idle_.push_back(kg);
+    }
+    pool_cv_.notify_one();
+}
+
+std::shared_ptr<KmerPegMapping> KmerRequestRouter::mapping_for(const std::string &key)
+{
+    /* caller holds mapping_mu_; krequest2.cc:416-425 creates unknown keys */
+    auto &m = mapping_map_[key];
+    if (!m)
+        m = std::make_shared<KmerPegMapping>(opt_.device);
+    return m;
+}
+
+std::string KmerRequestRouter::header(const std::string &http_version, int code, const std::string &status)
+{
+    std::ostringstream os;
+    os << "HTTP/" << http_version << " " << code << " " << status << "\n";
+    os << "Content-type: text/plain\n";
+    return os.str();
+}
+
+std::string KmerRequestRouter::respond(const std::string &http_version, int code,
+                                       const std::string &status, const std::string &body)
+{
+    std::ostringstream os;
+    os << header(http_version, code, status) << "Content-length: " << body.size() << "\n\n" << body;
+    return os.str();
+}
+
+std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
+{
+    const std::string &ver = req.http_version;
+    auto te = req.headers.find("transfer-encoding"); /* krequest2.cc:199-205 */
+    if (te != req.headers.end() && te->second == "chunked")
+        return respond(ver, 501, "Chunked encoding not implemented", "Chunked encoding not implemented\n");
+    try {
+        if (req.method == "GET") {
+            static const std::regex genus_re("^/genus_lookup/([^/]+)$");
+            std::smatch m;
+            if (req.path == "/quit") {
+                if (quit)
+                    *quit = true;
+                return respond(ver, 200, "OK", "OK, quitting\n");
+            }
+            if (req.path == "/version") {
+                std::ostringstream os;
+                if (!opt_.kmer_version.empty())
+                    os << "kmer\t" << opt_.kmer_version << "\n";
+                if (!opt_.families_version.empty())
+                    os << "families\t" << opt_.families_version << "\n";
+                os << "family-mode\t" << (family_mode_ ? "1" : "0") << "\n";
+                return respond(ver, 200, "OK", os.str());
+            }
+            if (std::regex_match(req.path, m, genus_re)) {
+                std::lock_guard<std::mutex> lk(mapping_mu_);
+                auto root = mapping_map_.find("");
+                auto hit = root->second->genus_map_.find(m[1].str());
+                if (hit == root->second->genus_map_.end())
+                    return respond(ver, 404, "Not Found", "genus not found\n");
+                return respond(ver, 200, "OK", hit->second + "\n");
+            }
+            if (req.path == "/dump_sizes") {
+                std::lock_guard<std::mutex> lk(mapping_mu_);
+                std::ostringstream os;
+                os << "memory dump\n";
+                for (auto &it : mapping_map_) {
+                    os << "Mapping '" << it.first << "':\n";
+                    it.second->dump_sizes(os);
+                }
+                return respond(ver, 200, "OK", os.str());
+            }
+            return respond(ver, 404, "Not found", "path not found\n");
+        }
+        if (req.method != "POST")
+            return std::string(); /* the reference sends nothing for other methods */
+        if (!req.headers.count("content-length"))
+            return respond(ver, 500, "Missing content length", "Missing content length header\n");
+
+        static const std::regex mapping_re("^/mapping/([^/]+)(/(add|matrix|lookup))$");
+        std::string key, action = req.path;
+        std::smatch m;
+        if (std::regex_match(req.path, m, mapping_re)) {
+            key = m[1];
+            action = m[2];
+        }
+        const char *body = req.body.data();
+        const size_t n = req.body.size();
+        std::ostringstream os;
+        if (action == "/query") {
+            GutsLease kg(*this);
+            (*kg).set_parameters(req.parameters);
+            const work_list_t work = parse_fasta_body(body, n);
+            os << header(ver, 200, "OK") << "\n";
+            query_request(*kg, work, param_int(req.parameters, "details", 0),
+                          param_int(req.parameters, "find_best_call", 0), os);
+            return os.str();
+        }
+        if (action != "/add" && action != "/matrix" && action != "/lookup" && action != "/fq_lookup")
+            return respond(ver, 404, "Not found", "path not found\n");
+        if (action == "/fq_lookup" && n == 0) /* fq_process_request.cc:42-46 */
+            return respond(ver, 200, "OK", "data done\n");
+
+        GutsLease kg(*this);
+        (*kg).set_parameters(req.parameters);
+        std::lock_guard<std::mutex> lk(mapping_mu_);
+        auto mapping = mapping_for(key);
+        if (action == "/fq_lookup") {
+            os << header(ver, 200, "OK") << "\n";
+            fq_request(*kg, mapping, body, n, os);
+            return os.str();
+        }
+        const work_list_t work = parse_fasta_body(body, n);
+        if (action == "/add") { /* krequest2.cc:429-436 */
+            os << header(ver, 200, "OK") << "\n";
+            add_request(*kg, *mapping, work, param_int(req.parameters, "silent", 0), os);
+        } else if (action == "/matrix") { /* matrix_request.cc:166-170 */
+            os << "HTTP/1.1 200 OK\nContent-type: text/plain\n\n";
+            matrix_request(*kg, mapping, work, os);
+        } else { /* lookup_request.cc:146-150 */
+            os << header(ver, 200, "OK") << "\n";
+            lookup_request(*kg, mapping, family_mode_, req.parameters, work, os);
+        }
+        return os.str();
+    } catch (const std::exception &e) { /* krequest2.cc:206-220 */
+        const std::string msg = std::string("Caught exception ") + e.what() + "\n";
+        return respond(ver, 500, "Failed", msg);
+    }
+}
+
+} // namespace kgx

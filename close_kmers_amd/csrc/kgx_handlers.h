@@ -1,0 +1,131 @@
+/*
+ * kgx_handlers.h -- the kserver request surface over the KmerGuts facade.
+ *
+ * Request handlers (the per-chunk worker loops of query_request.cc,
+ * add_request.cc, matrix_request.cc, lookup_request.cc and
+ * fq_process_request.cc) as functions of (KmerGuts, mapping, parameters,
+ * request body) writing the response body, and the HTTP request router of
+ * krequest2.cc:273-489 (KmerRequestRouter) that picks a handler and the
+ * keyed mapping for a request.  The router is transport-free: kgx_server
+ * feeds it requests read from a socket, an embedding server (the
+ * reference's boost.asio loop) can feed it its own.
+ *
+ * Each handler runs a request body as one work list: one GPU pass for the
+ * body's sequences, then the per-sequence output in request order.  The
+ * reference splits a body into 1-MiB chunks and writes each chunk's output
+ * as it completes; the concatenated output is the same, because every line
+ * depends only on its own sequence and on state updated in request order.
+ */
+#pragma once
+
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <ostream>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "kguts_hip.h"
+
+namespace kgx {
+
+typedef std::vector<std::pair<std::string, std::string>> work_list_t;
+typedef std::map<std::string, std::string> request_params_t;
+
+/* FastaParser over a whole body: (id, seq) pairs in input order */
+work_list_t parse_fasta_body(const char *body, size_t n);
+
+/* the reference reads integer flags with std::stoi and keeps the default
+ * when the value is absent or not a number (query_request.cc:92-100) */
+int param_int(const request_params_t &params, const std::string &name, int dflt);
+
+/* /query (query_request.cc:103-151): details=1 adds HIT lines,
+ * find_best_call=1 prints one best-call line per sequence with a call */
+void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_best_call,
+                   std::ostream &os);
+
+/* /add (add_request.cc:115-170): per sequence PROTEIN-ID / CALL / OTU-COUNTS /
+ * BEST-CALL unless silent, then every hit's k-mer is mapped to the
+ * sequence's id in mapping.kmer_to_id_ (ids encoded in request order) */
+void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work, int silent,
+                 std::ostream &os);
+
+/* /matrix (matrix_request.cc:83-190): pair counts against the proteins seen
+ * earlier in the same request and present in mapping.kmer_to_id_ */
+void matrix_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, const work_list_t &work,
+                    std::ostream &os);
+
+/* /lookup (lookup_request.cc:153-400) */
+void lookup_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
+                    const request_params_t &params, const work_list_t &work, std::ostream &os);
+
+/* /fq_lookup (fq_process_request.cc:230-365): FASTQ body */
+void fq_request(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping, const char *body, size_t n,
+                std::ostream &os);
+
+/* one parsed HTTP request (krequest2.cc:24-29, 92-213) */
+struct HttpRequest {
+    std::string method, path, parameters_raw, fragment, http_version;
+    request_params_t parameters;            /* split on ';' and '&', "k=v" parts only */
+    std::map<std::string, std::string> headers; /* keys lower-cased */
+    std::string body;
+};
+
+/* the request line "METHOD path[?params][#frag] HTTP/x.y" (krequest2.cc:24,
+ * 92-131); false when it does not match */
+bool parse_request_line(const std::string &line, HttpRequest &req);
+/* one header line "Key: value" ('\r' stripped by the caller) */
+void parse_header_line(const std::string &line, HttpRequest &req);
+
+/*
+ * KmerRequestRouter (krequest2.cc:273-489 + kserver.cc:40-130): owns the
+ * image, a pool of KmerGuts (one per worker, like threadpool.cc:33-36) and
+ * the keyed mappings ("" = the root mapping, which carries the family DB).
+ * handle() returns the full response bytes.  Thread-safe: handlers that
+ * touch a mapping run one at a time per server (the reference's TBB maps
+ * make concurrent /add safe; one lock keeps request-order id assignment
+ * deterministic here), /query runs concurrently up to the pool size.
+ */
+class KmerRequestRouter {
+public:
+    struct Options {
+        std::string kmer_data_dir;
+        int device = 0;
+        int n_kmer_threads = 1;
+        std::string kmer_version, families_version; /* "" = not given */
+        std::string genus_mapping, families_file;
+        std::vector<std::string> families_nr;
+    };
+    explicit KmerRequestRouter(const Options &opt);
+    ~KmerRequestRouter();
+
+    bool family_mode() const { return family_mode_; }
+    /* *quit is set for GET /quit (after the response is built) */
+    std::string handle(const HttpRequest &req, bool *quit);
+
+    /* "HTTP/ver code status\nContent-type: text/plain\n" (krequest2.cc:491-495) */
+    static std::string header(const std::string &http_version, int code, const std::string &status);
+    /* header + Content-length + body (krequest2.cc:497-503) */
+    static std::string respond(const std::string &http_version, int code, const std::string &status,
+                               const std::string &body);
+
+private:
+    class GutsLease;
+    KmerGuts *acquire();
+    void release(KmerGuts *kg);
+    std::shared_ptr<KmerPegMapping> mapping_for(const std::string &key);
+
+    Options opt_;
+    bool family_mode_;
+    std::shared_ptr<KmerImage> image_;
+    std::vector<std::unique_ptr<KmerGuts>> pool_;
+    std::vector<KmerGuts *> idle_;
+    std::mutex pool_mu_;
+    std::condition_variable pool_cv_;
+    std::mutex mapping_mu_; /* the mapping map and every handler that uses a mapping */
+    std::map<std::string, std::shared_ptr<KmerPegMapping>> mapping_map_;
+};
+
+} // namespace kgx

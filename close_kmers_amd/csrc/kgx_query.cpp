@@ -28,7 +28,7 @@
 #include <string>
 #include <vector>
 
-#include "kguts_hip.h"
+#include "kgx_handlers.h"
 
 using namespace kgx;
 
@@ -79,25 +79,16 @@ int main(int argc, char **argv)
             std::fwrite(s.data(), 1, s.size(), stdout);
             return 0;
         }
-        std::vector<KmerGuts::SeqJob> jobs;
-        FastaParser parser;
-        parser.set_callback([&jobs](const std::string &id, const std::string &seq) {
-            KmerGuts::SeqJob j;
-            j.id = id;
-            j.seq = seq;
-            jobs.push_back(std::move(j));
-            return 0;
-        });
         std::ifstream in(fasta, std::ios::binary);
         if (!in) {
             std::fprintf(stderr, "cannot open %s\n", fasta.c_str());
             return 1;
         }
-        char ch;
-        while (in.get(ch))
-            parser.parse_char(ch);
-        parser.parse_complete();
-
+        std::stringstream ss;
+        ss << in.rdbuf();
+        const std::string body = ss.str();
+        const work_list_t work = parse_fasta_body(body.data(), body.size());
+        std::ostringstream os;
         if (mode == "lookup") {
             auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
             if (!qp["genus"].empty())
@@ -107,96 +98,22 @@ int main(int argc, char **argv)
             const bool family_mode = qp["family_mode"] == "1";
             if (family_mode && !qp["nr"].empty())
                 mapping->load_nr_families(kguts, qp["nr"]);
-            std::vector<std::pair<std::string, std::string>> work;
-            std::vector<std::string> seqs;
-            for (auto &j : jobs) {
-                work.emplace_back(j.id, j.seq);
-                seqs.push_back(j.seq);
+            if (!family_mode) { /* a silent /add of the same FASTA first */
+                std::ostringstream discard;
+                add_request(kguts, *mapping, work, 1, discard);
             }
-            if (!family_mode) { /* /add first, ids encoded in order after the chunk */
-                run_batch_on_device(kguts, seqs);
-                std::vector<KmerPegMapping::encoded_id_t> ids;
-                for (auto &j : jobs)
-                    ids.push_back(mapping->encode_id(j.id));
-                mapping->add_batch_mappings(kguts, ids);
-            }
-            LookupRequest req(mapping, family_mode, qp);
-            std::ostringstream os;
-            req.process_work(kguts, work, os);
-            const std::string s = os.str();
-            std::fwrite(s.data(), 1, s.size(), stdout);
-            return 0;
-        }
-        if (mode == "matrix") {
+            lookup_request(kguts, mapping, family_mode, qp, work, os);
+        } else if (mode == "matrix") {
+            /* /add of the FASTA into an empty mapping, then one /matrix request */
             auto mapping = std::make_shared<KmerPegMapping>(kgx_image_device(image->handle()));
-            std::vector<std::string> seqs;
-            std::vector<std::pair<std::string, std::string>> work;
-            for (auto &j : jobs) {
-                seqs.push_back(j.seq);
-                work.emplace_back(j.id, j.seq);
-            }
-            /* /add (add_request.cc:164-170 / 196-206): ids encoded in order */
-            run_batch_on_device(kguts, seqs);
-            std::vector<KmerPegMapping::encoded_id_t> ids;
-            for (auto &j : jobs)
-                ids.push_back(mapping->encode_id(j.id));
-            mapping->add_batch_mappings(kguts, ids);
-            MatrixRequest mx(mapping);
-            mx.process_work(kguts, work);
-            std::ostringstream os;
-            mx.write_results(os);
-            const std::string s = os.str();
-            std::fwrite(s.data(), 1, s.size(), stdout);
-            return 0;
-        }
-        const bool details = mode == "query_details";
-        std::vector<std::shared_ptr<std::vector<KmerGuts::hit_in_sequence_t>>> hit_lists(jobs.size());
-        for (size_t i = 0; i < jobs.size(); i++) {
-            jobs[i].calls = std::make_shared<std::vector<KmerCall>>();
-            jobs[i].otu_stats = std::make_shared<KmerOtuStats>();
-            if (details || mode == "add") {
-                auto hl = std::make_shared<std::vector<KmerGuts::hit_in_sequence_t>>();
-                hit_lists[i] = hl;
-                jobs[i].hit_cb = [hl](KmerGuts::hit_in_sequence_t h) { hl->push_back(h); };
-            }
-        }
-        kguts.process_aa_batch(jobs);
-
-        std::ostringstream os;
-        for (size_t i = 0; i < jobs.size(); i++) {
-            const std::string &id = jobs[i].id, &seq = jobs[i].seq;
-            auto &calls = *jobs[i].calls;
-            if (mode == "query_best") {
-                int fi;
-                std::string fn;
-                float score, wscore, off = 0.0f;
-                kguts.find_best_call(calls, fi, fn, score, wscore, off);
-                if (!fn.empty())
-                    os << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
-            } else if (mode == "add") {
-                os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
-                for (auto &c : calls)
-                    os << kguts.format_call(c);
-                os << kguts.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
-                int fi;
-                std::string fn;
-                /* uninitialised in the reference when there are no calls
-                 * (add_request.cc:334); 0 here */
-                float score, wscore, off = 0.0f;
-                kguts.find_best_call(calls, fi, fn, score, wscore, off);
-                if (fn.empty() || fn.find(" ?? ") != std::string::npos)
-                    fn = "hypothetical protein";
-                os << "BEST-CALL\t" << id << "\t" << fn << "\t" << score << "\t" << wscore << "\t"
-                   << off << "\n";
-            } else {
-                os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
-                for (auto &c : calls)
-                    os << kguts.format_call(c);
-                if (details)
-                    for (auto &h : *hit_lists[i])
-                        os << kguts.format_hit(h);
-                os << kguts.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
-            }
+            std::ostringstream discard;
+            add_request(kguts, *mapping, work, 1, discard);
+            matrix_request(kguts, mapping, work, os);
+        } else if (mode == "add") {
+            KmerPegMapping mapping(kgx_image_device(image->handle()));
+            add_request(kguts, mapping, work, 0, os);
+        } else {
+            query_request(kguts, work, mode == "query_details", mode == "query_best", os);
         }
         const std::string s = os.str();
         std::fwrite(s.data(), 1, s.size(), stdout);

@@ -1,0 +1,281 @@
+/*
+ * kgx_server.cpp -- the kser request server over the HIP engine.
+ *
+ *   kgx_server [options] listen-port kmer-data-dir
+ *
+ * Options follow kser.cc:52-75 where they apply to the request path:
+ *   --listen-port-file F      write the bound port here (port 0 = any free port)
+ *   --n-kmer-threads N        KmerGuts workers (one GPU context each)
+ *   --kmer-version V, --families-version V       reported by GET /version
+ *   --families-genus-mapping F, --families-file F, --families-nr F [F ...]
+ *                             the family DB (family mode = --families-file given)
+ *   --bind ADDR               listen address (default 0.0.0.0, as kserver.cc:144-152)
+ *   --device N                GPU (default $KGX_DEVICE or 0)
+ *
+ * One connection = one request, as in krequest2.cc: the request line and
+ * headers are read, then Content-length bytes of body, the router builds the
+ * response, the connection is closed.  Each connection runs on its own
+ * thread; the router's KmerGuts pool bounds how many run on the GPU at once.
+ * GET /quit stops the listener after its response.
+ */
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cerrno>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kgx_handlers.h"
+
+using namespace kgx;
+
+namespace {
+
+std::atomic<bool> g_stop{false};
+int g_listen_fd = -1;
+std::atomic<int> g_active{0}; /* connection threads still running */
+
+bool write_all(int fd, const char *p, size_t n)
+{
+    while (n > 0) {
+        ssize_t w = ::send(fd, p, n, MSG_NOSIGNAL);
+        if (w < 0 && errno == EINTR)
+            continue;
+        if (w <= 0)
+            return false;
+        p += w;
+        n -= (size_t)w;
+    }
+    return true;
+}
+
+/* reads bytes into buf until it holds "\n" at or after `from`; returns the
+ * position of that '\n' or npos at EOF/error */
+size_t read_line(int fd, std::string &buf, size_t from)
+{
+    for (;;) {
+        size_t nl = buf.find('\n', from);
+        if (nl != std::string::npos)
+            return nl;
+        char tmp[65536];
+        ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+        if (r < 0 && errno == EINTR)
+            continue;
+        if (r <= 0)
+            return std::string::npos;
+        buf.append(tmp, (size_t)r);
+    }
+}
+
+void serve_connection(KmerRequestRouter &router, int fd)
+{
+    std::string buf;
+    HttpRequest req;
+    size_t nl = read_line(fd, buf, 0);
+    if (nl == std::string::npos) {
+        ::close(fd);
+        return;
+    }
+    std::string line = buf.substr(0, nl);
+    size_t cr = line.find('\r');
+    if (cr != std::string::npos)
+        line.erase(cr);
+    size_t pos = nl + 1;
+    if (!parse_request_line(line, req)) {
+        std::cerr << "Invalid request '" << line << "'\n";
+        ::close(fd);
+        return;
+    }
+    for (;;) { /* headers up to the empty line */
+        nl = read_line(fd, buf, pos);
+        if (nl == std::string::npos) {
+            ::close(fd);
+            return;
+        }
+        line = buf.substr(pos, nl - pos);
+        pos = nl + 1;
+        cr = line.find('\r');
+        if (cr != std::string::npos)
+            line.erase(cr);
+        if (line.empty())
+            break;
+        parse_header_line(line, req);
+    }
+    auto ex = req.headers.find("expect"); /* krequest2.cc:262-270 */
+    if (ex != req.headers.end() && ex->second == "100-continue") {
+        const std::string cont = "HTTP/" + req.http_version + " 100 Continue\n\n";
+        write_all(fd, cont.data(), cont.size());
+    }
+    auto cl = req.headers.find("content-length");
+    if (req.method == "POST" && cl != req.headers.end()) {
+        size_t len = 0;
+        try {
+            len = std::stoul(cl->second);
+        } catch (...) {
+            len = 0;
+        }
+        req.body = buf.substr(pos);
+        while (req.body.size() < len) {
+            char tmp[1 << 16];
+            ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+            if (r < 0 && errno == EINTR)
+                continue;
+            if (r <= 0)
+                break;
+            req.body.append(tmp, (size_t)r);
+        }
+        if (req.body.size() > len)
+            req.body.resize(len);
+    }
+    bool quit = false;
+    const std::string resp = router.handle(req, &quit);
+    write_all(fd, resp.data(), resp.size());
+    ::shutdown(fd, SHUT_WR);
+    ::close(fd);
+    if (quit) {
+        std::cerr << "stopping io service\n";
+        g_stop = true;
+        ::shutdown(g_listen_fd, SHUT_RDWR);
+    }
+}
+
+void on_signal(int)
+{
+    g_stop = true;
+    if (g_listen_fd >= 0)
+        ::shutdown(g_listen_fd, SHUT_RDWR);
+}
+
+int usage(const char *argv0)
+{
+    std::fprintf(stderr,
+                 "Usage: %s [options] listen-port kmer-data-dir\n"
+                 "  --listen-port-file F  --n-kmer-threads N  --kmer-version V  --families-version V\n"
+                 "  --families-genus-mapping F  --families-file F  --families-nr F [F ...]\n"
+                 "  --bind ADDR  --device N\n",
+                 argv0);
+    return 2;
+}
+
+} // namespace
+
+int main(int argc, char **argv)
+{
+    KmerRequestRouter::Options opt;
+    const char *dev = std::getenv("KGX_DEVICE");
+    opt.device = dev ? std::atoi(dev) : 0;
+    std::string port_file = "/dev/null", bind_addr = "0.0.0.0";
+    std::vector<std::string> positional;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto value = [&](std::string &dst) {
+            if (i + 1 >= argc)
+                return false;
+            dst = argv[++i];
+            return true;
+        };
+        std::string v;
+        if (a == "-h" || a == "--help")
+            return usage(argv[0]);
+        else if (a == "--listen-port-file") {
+            if (!value(port_file))
+                return usage(argv[0]);
+        } else if (a == "--n-kmer-threads") {
+            if (!value(v))
+                return usage(argv[0]);
+            opt.n_kmer_threads = std::atoi(v.c_str());
+        } else if (a == "--kmer-version") {
+            if (!value(opt.kmer_version))
+                return usage(argv[0]);
+        } else if (a == "--families-version") {
+            if (!value(opt.families_version))
+                return usage(argv[0]);
+        } else if (a == "--families-genus-mapping") {
+            if (!value(opt.genus_mapping))
+                return usage(argv[0]);
+        } else if (a == "--families-file") {
+            if (!value(opt.families_file))
+                return usage(argv[0]);
+        } else if (a == "--families-nr") { /* multitoken (kser.cc:65) */
+            while (i + 1 < argc && argv[i + 1][0] != '-')
+                opt.families_nr.push_back(argv[++i]);
+        } else if (a == "--bind") {
+            if (!value(bind_addr))
+                return usage(argv[0]);
+        } else if (a == "--device") {
+            if (!value(v))
+                return usage(argv[0]);
+            opt.device = std::atoi(v.c_str());
+        } else if (!a.empty() && a[0] == '-') {
+            std::fprintf(stderr, "unknown option %s\n", a.c_str());
+            return usage(argv[0]);
+        } else
+            positional.push_back(a);
+    }
+    if (positional.size() != 2)
+        return usage(argv[0]);
+    opt.kmer_data_dir = positional[1];
+    const int port = std::atoi(positional[0].c_str());
+
+    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in addr{};
+    addr.sin_family = AF_INET;
+    addr.sin_port = htons((uint16_t)port);
+    if (::inet_pton(AF_INET, bind_addr.c_str(), &addr.sin_addr) != 1) {
+        std::fprintf(stderr, "bad --bind address %s\n", bind_addr.c_str());
+        return 2;
+    }
+    if (::bind(fd, (sockaddr *)&addr, sizeof addr) < 0 || ::listen(fd, 128) < 0) {
+        std::fprintf(stderr, "cannot listen on %s:%d: %s\n", bind_addr.c_str(), port, std::strerror(errno));
+        return 1;
+    }
+    socklen_t alen = sizeof addr;
+    ::getsockname(fd, (sockaddr *)&addr, &alen);
+    g_listen_fd = fd;
+
+    std::unique_ptr<KmerRequestRouter> router;
+    try {
+        router.reset(new KmerRequestRouter(opt));
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "kgx_server: %s\n", e.what());
+        return 1;
+    }
+    { /* the port file is written once the data are loaded, as kserver.cc */
+        std::ofstream pf(port_file);
+        pf << ntohs(addr.sin_port) << "\n";
+    }
+    std::cerr << "Listening on port " << ntohs(addr.sin_port) << "\n";
+    std::signal(SIGINT, on_signal);
+    std::signal(SIGTERM, on_signal);
+
+    while (!g_stop) {
+        int c = ::accept(fd, nullptr, nullptr);
+        if (c < 0) {
+            if (errno == EINTR && !g_stop)
+                continue;
+            break;
+        }
+        g_active++;
+        std::thread([&router, c] {
+            serve_connection(*router, c);
+            g_active--;
+        }).detach();
+    }
+    while (g_active > 0) /* let running requests finish before the router goes */
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    ::close(fd);
+    return 0;
+}

@@ -1,0 +1,192 @@
+"""The kser request surface over HTTP (kgx_server, krequest2.cc:273-489 routes).
+
+GPU tests drive every golden handler case through a running server and
+compare the response body with the same golden text the kgx_query driver and
+the oracle reproduce; CPU tests cover the command line and the start-up
+errors, which need no device."""
+import os
+import socket
+import subprocess
+import tempfile
+import time
+
+import pytest
+
+from close_kmers_amd import build as kbuild
+from helpers import GOLDEN
+from test_oracle_golden import FQ_FILES, PARAMS, parse_case
+
+HEADER = b"HTTP/1.1 200 OK\nContent-type: text/plain\n\n"
+
+
+def _server_exe():
+    kbuild.build()
+    return kbuild.SERVER
+
+
+def test_server_usage_and_bad_data_dir():
+    exe = _server_exe()
+    r = subprocess.run([exe, "--help"], capture_output=True, timeout=60)
+    assert r.returncode == 2 and b"listen-port kmer-data-dir" in r.stderr
+    r = subprocess.run([exe, "--bind", "127.0.0.1", "0", "/nonexistent-kmer-dir"], capture_output=True,
+                       timeout=60)
+    assert r.returncode == 1 and b"kmer.table.mem_map" in r.stderr
+    r = subprocess.run([exe, "--bogus", "0", "x"], capture_output=True, timeout=60)
+    assert r.returncode == 2
+
+
+class Server:
+    """A kgx_server on 127.0.0.1 with an ephemeral port."""
+
+    def __init__(self, data_dir, family_db=False, threads=2):
+        self.tmp = tempfile.TemporaryDirectory()
+        port_file = os.path.join(self.tmp.name, "port")
+        args = [_server_exe(), "--bind", "127.0.0.1", "--listen-port-file", port_file,
+                "--n-kmer-threads", str(threads), "--kmer-version", "kv1"]
+        if family_db:
+            fq = os.path.join(GOLDEN, "fq")
+            args += ["--families-genus-mapping", os.path.join(fq, FQ_FILES["genus"]),
+                     "--families-file", os.path.join(fq, FQ_FILES["families"]),
+                     "--families-version", "fv1"]
+        args += ["0", data_dir]
+        if family_db:
+            args += ["--families-nr", os.path.join(GOLDEN, "fq", FQ_FILES["nr"])]
+        self.proc = subprocess.Popen(args, stderr=subprocess.PIPE)
+        deadline = time.time() + 120
+        self.port = None
+        while time.time() < deadline:
+            if self.proc.poll() is not None:
+                raise RuntimeError(self.proc.stderr.read().decode())
+            try:
+                txt = open(port_file).read().strip()
+                if txt:
+                    self.port = int(txt)
+                    break
+            except FileNotFoundError:
+                pass
+            time.sleep(0.05)
+        assert self.port, "server did not start"
+
+    def request(self, method, path, body=b""):
+        with socket.create_connection(("127.0.0.1", self.port), timeout=120) as s:
+            head = f"{method} {path} HTTP/1.1\r\nHost: x\r\n"
+            if method == "POST":
+                head += f"Content-Length: {len(body)}\r\n"
+            s.sendall(head.encode() + b"\r\n" + body)
+            out = b""
+            while True:
+                chunk = s.recv(1 << 16)
+                if not chunk:
+                    return out
+                out += chunk
+
+    def close(self):
+        if self.proc.poll() is None:
+            r = self.request("GET", "/quit")
+            assert b"OK, quitting" in r
+            self.proc.wait(timeout=60)
+        assert self.proc.returncode == 0
+        self.tmp.cleanup()
+
+
+def _query_string(pname):
+    p = {k: v for k, v in PARAMS[pname].items() if k != "family_mode"}
+    return "&".join(f"{k}={v}" for k, v in p.items())
+
+
+def _cases(ds):
+    d = os.path.join(GOLDEN, ds)
+    return sorted(f for f in os.listdir(d) if f.startswith("expected_") and f.endswith(".txt"))
+
+
+QUERY_FLAGS = {"query": "", "query_details": "details=1", "query_best": "find_best_call=1"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ds", ["scoring", "edge", "cap"])
+def test_query_and_add_routes_match_golden(gpu, ds):
+    d = os.path.join(GOLDEN, ds)
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(d, "data"))
+    try:
+        for fname in _cases(ds):
+            mode, pname = parse_case(fname)
+            qs = "&".join(x for x in (QUERY_FLAGS.get(mode, ""), _query_string(pname)) if x)
+            route = "/query" if mode in QUERY_FLAGS else "/mapping/m_%s/add" % pname
+            got = srv.request("POST", route + ("?" + qs if qs else ""), fasta)
+            assert got.startswith(HEADER), (fname, got[:80])
+            assert got[len(HEADER):] == open(os.path.join(d, fname), "rb").read(), fname
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
+def test_matrix_route_after_add_matches_golden(gpu):
+    d = os.path.join(GOLDEN, "matrix")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(d, "data"))
+    try:
+        r = srv.request("POST", "/mapping/mx/add?silent=1", fasta)
+        assert r == HEADER  # silent: header only
+        got = srv.request("POST", "/mapping/mx/matrix", fasta)
+        assert got == HEADER + open(os.path.join(d, "expected_matrix_default.txt"), "rb").read()
+        # a mapping key nobody /add-ed: no partners, empty matrix
+        assert srv.request("POST", "/mapping/other/matrix", fasta) == HEADER
+        sizes = srv.request("GET", "/dump_sizes")
+        assert b"Mapping 'mx':" in sizes and b"peg_to_id_: size=" in sizes
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
+def test_lookup_peg_mode_routes_match_oracle(gpu, oracle_lib):
+    """A server without --families-file is in peg mode (kser.cc:289) and its
+    mappings carry no family data, so the expected text is the oracle's
+    /add + /lookup without a family DB (the golden peg files were made with
+    one, which only kgx_query's file arguments can combine with peg mode)."""
+    d = os.path.join(GOLDEN, "lookup")
+    fasta_path = os.path.join(d, "input.fasta")
+    fasta = open(fasta_path, "rb").read()
+    srv = Server(os.path.join(d, "data"))
+    try:
+        assert srv.request("POST", "/add?silent=1", fasta) == HEADER
+        for pname in ("peg", "peg_all"):
+            qs = _query_string(pname)
+            got = srv.request("POST", "/lookup" + ("?" + qs if qs else ""), fasta)
+            want = oracle_lib.query_text(os.path.join(d, "data"), fasta_path, "lookup", PARAMS[pname])
+            assert want.count(b"//") > 5
+            assert got == HEADER + want, pname
+        v = srv.request("GET", "/version")
+        assert v.endswith(b"kmer\tkv1\nfamily-mode\t0\n")
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
+def test_family_mode_lookup_and_fq_routes_match_golden(gpu):
+    d = os.path.join(GOLDEN, "lookup")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(d, "data"), family_db=True)
+    try:
+        for fname in _cases("lookup"):
+            mode, pname = parse_case(fname)
+            if not pname.startswith("fam_"):
+                continue
+            got = srv.request("POST", "/lookup?" + _query_string(pname), fasta)
+            assert got == HEADER + open(os.path.join(d, fname), "rb").read(), fname
+        v = srv.request("GET", "/version")
+        assert v.endswith(b"kmer\tkv1\nfamilies\tfv1\nfamily-mode\t1\n")
+        assert srv.request("GET", "/genus_lookup/Escherichia").endswith(b"\n\n561\n")
+        assert srv.request("GET", "/genus_lookup/no_such_genus").startswith(b"HTTP/1.1 404 Not Found")
+        assert srv.request("GET", "/nowhere").startswith(b"HTTP/1.1 404 Not found")
+        assert srv.request("POST", "/nowhere", b"x").startswith(b"HTTP/1.1 404 Not found")
+        assert srv.request("POST", "/fq_lookup", b"").endswith(b"\n\ndata done\n")
+    finally:
+        srv.close()
+    fq = os.path.join(GOLDEN, "fq")
+    srv = Server(os.path.join(fq, "data"), family_db=True)
+    try:
+        got = srv.request("POST", "/fq_lookup", open(os.path.join(fq, "input.fasta"), "rb").read())
+        assert got == HEADER + open(os.path.join(fq, "expected_fq_default.txt"), "rb").read()
+    finally:
+        srv.close()
