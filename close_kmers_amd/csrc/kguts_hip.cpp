@@ -8,6 +8,7 @@
 #include "kguts_hip.h"
 
 #include <algorithm>
+#include <charconv>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -253,34 +254,103 @@ unsigned long long KmerGuts::encoded_aa_kmer(const char *p)
 
 /* format_call / format_hit / format_otu_stats: iostream defaults (6
  * significant digits for floats), kguts.cc:939-973 */
+/* iostream's default formatting of the numbers in the handler lines */
+static void append_u64(std::string &out, unsigned long long v)
+{
+    char b[24];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    out.append(b, r.ptr);
+}
+
+static void append_i64(std::string &out, long long v)
+{
+    char b[24];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    out.append(b, r.ptr);
+}
+
+static void append_f32(std::string &out, float v)
+{
+    /* operator<<(float) with precision 6 and no floatfield is "%.*g" of the
+     * value widened to double (libstdc++ num_put::_M_insert_float) */
+    char b[48];
+    int n = std::snprintf(b, sizeof b, "%.6g", (double)v);
+    out.append(b, (size_t)n);
+}
+
+void KmerGuts::append_call(std::string &out, const KmerCall &c) const
+{
+    out += "CALL\t";
+    append_u64(out, c.start);
+    out += '\t';
+    append_u64(out, c.end);
+    out += '\t';
+    append_i64(out, c.count);
+    out += '\t';
+    append_u64(out, c.function_index);
+    out += '\t';
+    out += function_at_index((int)c.function_index);
+    out += '\t';
+    append_f32(out, c.weighted_hits);
+    out += '\n';
+}
+
+void KmerGuts::append_hit(std::string &out, const hit_in_sequence_t &h) const
+{
+    char dc[9];
+    decoded_kmer(h.hit.which_kmer, dc);
+    out += "HIT\t";
+    append_u64(out, h.offset);
+    out += '\t';
+    out += dc;
+    out += '\t';
+    append_u64(out, h.hit.avg_from_end);
+    out += '\t';
+    out += function_at_index(h.hit.function_index);
+    out += '\t';
+    append_f32(out, h.hit.function_wt);
+    out += '\t';
+    append_i64(out, h.hit.otu_index);
+    out += '\n';
+}
+
+void KmerGuts::append_otu_stats(std::string &out, const std::string &id, size_t size,
+                                const KmerOtuStats &s) const
+{
+    out += "OTU-COUNTS\t";
+    out += id;
+    out += '[';
+    append_u64(out, size);
+    out += ']';
+    const size_t top = std::min<size_t>(s.otus_by_count.size(), 5);
+    for (size_t i = 0; i < top; i++) {
+        out += '\t';
+        append_i64(out, s.otus_by_count[i].second);
+        out += '-';
+        append_i64(out, s.otus_by_count[i].first);
+    }
+    out += '\n';
+}
+
 std::string KmerGuts::format_call(const KmerCall &c)
 {
-    std::ostringstream o;
-    o << "CALL\t" << c.start << "\t" << c.end << "\t" << c.count << "\t" << c.function_index << "\t"
-      << function_at_index((int)c.function_index) << "\t" << c.weighted_hits << "\n";
-    return o.str();
+    std::string o;
+    append_call(o, c);
+    return o;
 }
 
 std::string KmerGuts::format_hit(const hit_in_sequence_t &h)
 {
-    char dc[9];
-    decoded_kmer(h.hit.which_kmer, dc);
-    std::ostringstream o;
-    o << "HIT\t" << h.offset << "\t" << dc << "\t" << h.hit.avg_from_end << "\t"
-      << function_at_index(h.hit.function_index) << "\t" << h.hit.function_wt << "\t"
-      << h.hit.otu_index << "\n";
-    return o.str();
+    std::string o;
+    append_hit(o, h);
+    return o;
 }
 
 std::string KmerGuts::format_otu_stats(const std::string &id, size_t size, KmerOtuStats &s)
 {
-    std::ostringstream o;
-    o << "OTU-COUNTS\t" << id << "[" << size << "]";
-    const size_t top = std::min<size_t>(s.otus_by_count.size(), 5);
-    for (size_t i = 0; i < top; i++)
-        o << "\t" << s.otus_by_count[i].second << "-" << s.otus_by_count[i].first;
-    o << "\n";
-    return o.str();
+    std::string o;
+    append_otu_stats(o, id, size, s);
+    return o;
 }
 
 /* find_best_call, kguts.cc:1008-1199 -- a port of the SEED

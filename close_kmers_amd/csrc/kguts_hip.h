@@ -147,6 +147,13 @@ public:
     std::string format_call(const KmerCall &c);
     std::string format_hit(const hit_in_sequence_t &h);
     std::string format_otu_stats(const std::string &id, size_t size, KmerOtuStats &otu_stats);
+    /* the same lines appended to out, without a stream per line: the
+     * handlers' bulk output path (numbers as iostream prints them: decimal
+     * integers, floats as "%.6g") */
+    void append_call(std::string &out, const KmerCall &c) const;
+    void append_hit(std::string &out, const hit_in_sequence_t &h) const;
+    void append_otu_stats(std::string &out, const std::string &id, size_t size,
+                          const KmerOtuStats &otu_stats) const;
 
     const char *function_at_index(int i) const;
     int function_count() const { return (int)functions_.size(); }

@@ -6,12 +6,15 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstring>
 #include <regex>
 #include <sstream>
 
 namespace kgx {
 
-work_list_t parse_fasta_body(const char *body, size_t n)
+/* FastaParser's state machine (fasta_parser.h:45-133) one byte at a time:
+ * the exact path, also for bodies with '\r', bad characters or odd framing */
+static work_list_t parse_fasta_body_bytewise(const char *body, size_t n)
 {
     work_list_t work;
     FastaParser parser;
@@ -23,6 +26,59 @@ work_list_t parse_fasta_body(const char *body, size_t n)
         parser.parse_char(body[i]);
     parser.parse_complete();
     return work;
+}
+
+/* Line-at-a-time parse of well-formed bodies, the common case, with the same
+ * result as the state machine: every record starts with a header line
+ * ('>' id [blank defline] '\n'), and every sequence line holds only letters
+ * and '*' ('*' not first on a line other than the record's first line, where
+ * the machine is still in DATA).  Blank lines are skipped, as in
+ * ID_OR_DATA.  Anything else -- '\r', a bad character, a header right
+ * after a header, a body not starting with '>' or ending inside a header --
+ * returns false and the caller takes the bytewise path. */
+static bool parse_fasta_body_lines(const char *body, size_t n, work_list_t &work)
+{
+    if (n == 0 || body[0] != '>' || std::memchr(body, '\r', n))
+        return false;
+    const char *p = body, *end = body + n;
+    while (p < end) { /* p at a '>' */
+        const char *eol = (const char *)std::memchr(p, '\n', end - p);
+        if (!eol)
+            return false; /* ends inside a header: leave it to the machine */
+        const char *id_end = p + 1;
+        while (id_end < eol && *id_end != ' ' && *id_end != '\t')
+            id_end++;
+        work.emplace_back(std::string(p + 1, id_end), std::string());
+        std::string &seq = work.back().second;
+        p = eol + 1;
+        bool first_line = true;
+        while (p < end && *p != '>') {
+            eol = (const char *)std::memchr(p, '\n', end - p);
+            const char *le = eol ? eol : end;
+            /* letters (C locale isalpha) or '*'; no early exit, so it vectorises */
+            unsigned ok = 1;
+            for (const char *q = p; q < le; q++) {
+                const unsigned char c = (unsigned char)*q;
+                ok &= (unsigned)((unsigned char)((c | 0x20) - 'a') < 26) | (unsigned)(c == '*');
+            }
+            if (!ok || (le > p && *p == '*' && !first_line))
+                return false;
+            seq.append(p, le);
+            first_line = false;
+            p = eol ? eol + 1 : end;
+        }
+        if (p < end && first_line)
+            return false; /* '>' while the machine is in DATA: an error path */
+    }
+    return true;
+}
+
+work_list_t parse_fasta_body(const char *body, size_t n)
+{
+    work_list_t work;
+    if (parse_fasta_body_lines(body, n, work))
+        return work;
+    return parse_fasta_body_bytewise(body, n);
 }
 
 int param_int(const request_params_t &params, const std::string &name, int dflt)
@@ -61,6 +117,8 @@ void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_
             jobs[i].hit_cb = [hl](KmerGuts::hit_in_sequence_t h) { hl->push_back(h); };
         }
     kg.process_aa_batch(jobs);
+    std::string out;
+    out.reserve(jobs.size() * 96);
     for (size_t i = 0; i < jobs.size(); i++) {
         const std::string &id = jobs[i].id, &seq = jobs[i].seq;
         auto &calls = *jobs[i].calls;
@@ -69,18 +127,26 @@ void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_
             std::string fn;
             float score, wscore, off = 0.0f;
             kg.find_best_call(calls, fi, fn, score, wscore, off);
-            if (!fn.empty())
-                os << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+            if (!fn.empty()) {
+                std::ostringstream line; /* one line per call: the float format stays iostream's */
+                line << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+                out += line.str();
+            }
             continue;
         }
-        os << "PROTEIN-ID\t" << id << "\t" << seq.size() << "\n";
+        out += "PROTEIN-ID\t";
+        out += id;
+        out += '\t';
+        out += std::to_string(seq.size());
+        out += '\n';
         for (auto &c : calls)
-            os << kg.format_call(c);
+            kg.append_call(out, c);
         if (hit_lists[i])
             for (auto &h : *hit_lists[i])
-                os << kg.format_hit(h);
-        os << kg.format_otu_stats(id, seq.size(), *jobs[i].otu_stats);
+                kg.append_hit(out, h);
+        kg.append_otu_stats(out, id, seq.size(), *jobs[i].otu_stats);
     }
+    os.write(out.data(), (std::streamsize)out.size());
 }
 
 void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work, int silent,
@@ -88,12 +154,18 @@ void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work,
 {
     std::vector<KmerGuts::SeqJob> jobs = jobs_for(work);
     kg.process_aa_batch(jobs); /* the batch's hits stay on the device for the mapping */
-    if (!silent)
+    if (!silent) {
+        std::string out;
+        out.reserve(jobs.size() * 160);
         for (auto &j : jobs) { /* add_request.cc:134-161 */
-            os << "PROTEIN-ID\t" << j.id << "\t" << j.seq.size() << "\n";
+            out += "PROTEIN-ID\t";
+            out += j.id;
+            out += '\t';
+            out += std::to_string(j.seq.size());
+            out += '\n';
             for (auto &c : *j.calls)
-                os << kg.format_call(c);
-            os << kg.format_otu_stats(j.id, j.seq.size(), *j.otu_stats);
+                kg.append_call(out, c);
+            kg.append_otu_stats(out, j.id, j.seq.size(), *j.otu_stats);
             int fi;
             std::string fn;
             /* uninitialised in the reference when there are no calls
@@ -102,9 +174,13 @@ void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work,
             kg.find_best_call(*j.calls, fi, fn, score, wscore, off);
             if (fn.empty() || fn.find(" ?? ") != std::string::npos)
                 fn = "hypothetical protein";
-            os << "BEST-CALL\t" << j.id << "\t" << fn << "\t" << score << "\t" << wscore << "\t" << off
-               << "\n";
+            std::ostringstream line;
+            line << "BEST-CALL\t" << j.id << "\t" << fn << "\t" << score << "\t" << wscore << "\t" << off
+                 << "\n";
+            out += line.str();
         }
+        os.write(out.data(), (std::streamsize)out.size());
+    }
     /* add_request.cc:164-170: ids encoded in request order, every hit's
      * k-mer mapped to its sequence's id */
     std::vector<KmerPegMapping::encoded_id_t> ids;
@@ -198,7 +274,16 @@ private:
 KmerRequestRouter::KmerRequestRouter(const Options &opt)
     : opt_(opt), family_mode_(!opt.families_file.empty()) /* kser.cc:289 */
 {
-    image_ = std::make_shared<KmerImage>(opt_.kmer_data_dir, opt_.device);
+    if (opt_.synthetic_keys) {
+        kgx_image *img = nullptr;
+        uint64_t stored = 0;
+        int rc = kgx_image_build_synthetic(opt_.synthetic_keys, opt_.synthetic_sigs, opt_.device, &img, &stored);
+        if (rc)
+            throw Error(rc, std::string("kgx_image_build_synthetic: ") + kgx_last_error());
+        image_ = std::make_shared<KmerImage>(img);
+    } else {
+        image_ = std::make_shared<KmerImage>(opt_.kmer_data_dir, opt_.device);
+    }
     const int n = std::max(1, opt_.n_kmer_threads);
     for (int i = 0; i < n; i++) {
         pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, image_));

@@ -97,6 +97,11 @@ public:
         std::string kmer_version, families_version; /* "" = not given */
         std::string genus_mapping, families_file;
         std::vector<std::string> families_nr;
+        /* benchmark hook: when synthetic_keys > 0 the image is built in HBM
+         * by kgx_image_build_synthetic (synthetic_keys keys in synthetic_sigs
+         * buckets) instead of loading kmer_data_dir/kmer.table.mem_map; the
+         * directory still provides function.index and otu.index */
+        uint64_t synthetic_keys = 0, synthetic_sigs = 0;
     };
     explicit KmerRequestRouter(const Options &opt);
     ~KmerRequestRouter();

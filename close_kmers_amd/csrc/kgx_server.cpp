@@ -11,6 +11,9 @@
  *                             the family DB (family mode = --families-file given)
  *   --bind ADDR               listen address (default 0.0.0.0, as kserver.cc:144-152)
  *   --device N                GPU (default $KGX_DEVICE or 0)
+ *   --synthetic-image K:S     benchmark hook: a synthetic image of K keys in S
+ *                             buckets built in HBM (kmer-data-dir still holds
+ *                             function.index / otu.index)
  *
  * One connection = one request, as in krequest2.cc: the request line and
  * headers are read, then Content-length bytes of body, the router builds the
@@ -163,7 +166,7 @@ int usage(const char *argv0)
                  "Usage: %s [options] listen-port kmer-data-dir\n"
                  "  --listen-port-file F  --n-kmer-threads N  --kmer-version V  --families-version V\n"
                  "  --families-genus-mapping F  --families-file F  --families-nr F [F ...]\n"
-                 "  --bind ADDR  --device N\n",
+                 "  --bind ADDR  --device N  --synthetic-image KEYS:BUCKETS\n",
                  argv0);
     return 2;
 }
@@ -217,6 +220,12 @@ int main(int argc, char **argv)
             if (!value(v))
                 return usage(argv[0]);
             opt.device = std::atoi(v.c_str());
+        } else if (a == "--synthetic-image") {
+            size_t colon;
+            if (!value(v) || (colon = v.find(':')) == std::string::npos)
+                return usage(argv[0]);
+            opt.synthetic_keys = std::strtoull(v.c_str(), nullptr, 10);
+            opt.synthetic_sigs = std::strtoull(v.c_str() + colon + 1, nullptr, 10);
         } else if (!a.empty() && a[0] == '-') {
             std::fprintf(stderr, "unknown option %s\n", a.c_str());
             return usage(argv[0]);
