@@ -9,6 +9,7 @@
 #include <cstring>
 #include <regex>
 #include <sstream>
+#include <thread>
 
 namespace kgx {
 
@@ -71,6 +72,49 @@ static bool parse_fasta_body_lines(const char *body, size_t n, work_list_t &work
             return false; /* '>' while the machine is in DATA: an error path */
     }
     return true;
+}
+
+std::vector<std::pair<size_t, size_t>> split_fasta_body(const char *body, size_t n, size_t pieces)
+{
+    std::vector<std::pair<size_t, size_t>> out;
+    if (pieces < 2 || n == 0 || body[0] != '>')
+        return out;
+    size_t start = 0;
+    for (size_t k = 1; k < pieces; k++) {
+        size_t at = std::max(start + 1, k * (n / pieces));
+        size_t cut = 0;
+        while (at < n) {
+            const char *nl = (const char *)std::memchr(body + at, '\n', n - at);
+            if (!nl || nl + 1 >= body + n)
+                break;
+            const size_t c = (size_t)(nl - body) + 1;
+            if (body[c] == '>') {
+                /* the line before the cut must not be a header: a header right
+                 * before '>' is an error path of the whole-body machine */
+                size_t ls = c - 1;
+                while (ls > start && body[ls - 1] != '\n')
+                    ls--;
+                if (body[ls] != '>') {
+                    cut = c;
+                    break;
+                }
+            }
+            at = c;
+        }
+        if (!cut)
+            break;
+        out.emplace_back(start, cut);
+        start = cut;
+    }
+    if (out.empty())
+        return out;
+    out.emplace_back(start, n);
+    return out;
+}
+
+bool parse_fasta_piece(const char *piece, size_t n, work_list_t &work)
+{
+    return parse_fasta_body_lines(piece, n, work);
 }
 
 work_list_t parse_fasta_body(const char *body, size_t n)
@@ -406,13 +450,49 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
         const size_t n = req.body.size();
         std::ostringstream os;
         if (action == "/query") {
-            GutsLease kg(*this);
-            (*kg).set_parameters(req.parameters);
-            const work_list_t work = parse_fasta_body(body, n);
+            const int details = param_int(req.parameters, "details", 0);
+            const int fbc = param_int(req.parameters, "find_best_call", 0);
             os << header(ver, 200, "OK") << "\n";
-            query_request(*kg, work, param_int(req.parameters, "details", 0),
-                          param_int(req.parameters, "find_best_call", 0), os);
-            return os.str();
+            /* a large body is cut into pieces at record starts that run on
+             * several workers at once and are written in request order -- the
+             * reference's 1-MiB chunks on its thread pool (krequest2.cc:41,
+             * query_request.cc:62-160) -- when every piece parses line by line */
+            const size_t n_pieces = std::min(pool_.size(), n / kPieceBytes);
+            auto cuts = split_fasta_body(body, n, n_pieces);
+            std::vector<work_list_t> works(cuts.size());
+            bool ok = !cuts.empty();
+            for (size_t i = 0; ok && i < cuts.size(); i++)
+                ok = parse_fasta_piece(body + cuts[i].first, cuts[i].second - cuts[i].first, works[i]);
+            if (!ok) {
+                GutsLease kg(*this);
+                (*kg).set_parameters(req.parameters);
+                query_request(*kg, parse_fasta_body(body, n), details, fbc, os);
+                return os.str();
+            }
+            std::vector<std::string> outs(works.size());
+            std::vector<std::string> errs(works.size());
+            std::vector<std::thread> ths;
+            for (size_t i = 0; i < works.size(); i++)
+                ths.emplace_back([&, i] {
+                    try {
+                        GutsLease kg(*this);
+                        (*kg).set_parameters(req.parameters);
+                        std::ostringstream po;
+                        query_request(*kg, works[i], details, fbc, po);
+                        outs[i] = po.str();
+                    } catch (const std::exception &e) {
+                        errs[i] = e.what();
+                    }
+                });
+            for (auto &t : ths)
+                t.join();
+            for (auto &e : errs)
+                if (!e.empty())
+                    throw Error(KGX_EDEVICE, e);
+            std::string all = os.str();
+            for (auto &o : outs)
+                all += o;
+            return all;
         }
         if (action != "/add" && action != "/matrix" && action != "/lookup" && action != "/fq_lookup")
             return respond(ver, 404, "Not found", "path not found\n");

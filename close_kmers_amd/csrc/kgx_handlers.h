@@ -37,6 +37,14 @@ typedef std::map<std::string, std::string> request_params_t;
 /* FastaParser over a whole body: (id, seq) pairs in input order */
 work_list_t parse_fasta_body(const char *body, size_t n);
 
+/* cut points [begin, end) of at most `pieces` pieces of a FASTA body, each
+ * starting at a record's '>' that follows a sequence or blank line; empty
+ * when the body cannot be cut (too small, not starting with '>') */
+std::vector<std::pair<size_t, size_t>> split_fasta_body(const char *body, size_t n, size_t pieces);
+/* the line-at-a-time parse of one piece; false when the piece needs the
+ * byte machine (then the whole body must be parsed as one) */
+bool parse_fasta_piece(const char *piece, size_t n, work_list_t &work);
+
 /* the reference reads integer flags with std::stoi and keeps the default
  * when the value is absent or not a number (query_request.cc:92-100) */
 int param_int(const request_params_t &params, const std::string &name, int dflt);
@@ -117,6 +125,7 @@ public:
                                const std::string &body);
 
 private:
+    static constexpr size_t kPieceBytes = 1 << 20; /* krequest2.cc:41 */
     class GutsLease;
     KmerGuts *acquire();
     void release(KmerGuts *kg);

@@ -85,6 +85,43 @@ int main(int argc, char **argv)
             return 1;
         }
     }
+    /* pieces cut by split_fasta_body, each parsed line by line, concatenate
+     * to the whole-body parse whenever every piece parses */
+    int split_used = 0;
+    for (int t = 0; t < n; t++) {
+        std::string b = t % 3 ? well_formed(rng, 1 + (int)(rng() % 40)) : noisy(rng);
+        if (t % 7 == 0)
+            b += ">hdr_only\n>next\nACDE\n"; /* a header right before '>' */
+        const size_t pieces = 2 + rng() % 6;
+        auto cuts = split_fasta_body(b.data(), b.size(), pieces);
+        if (cuts.empty())
+            continue;
+        if (cuts.front().first != 0 || cuts.back().second != b.size()) {
+            std::printf("BAD CUTS case %d\n", t);
+            return 1;
+        }
+        work_list_t joined;
+        bool ok = true;
+        for (auto &c : cuts) {
+            if (c.second <= c.first || b[c.first] != '>') {
+                std::printf("BAD PIECE case %d\n", t);
+                return 1;
+            }
+            ok = ok && parse_fasta_piece(b.data() + c.first, c.second - c.first, joined);
+        }
+        if (!ok)
+            continue;
+        split_used++;
+        if (joined != machine(b)) {
+            std::printf("SPLIT MISMATCH case %d\n", t);
+            std::fwrite(b.data(), 1, b.size(), stdout);
+            return 1;
+        }
+    }
+    if (split_used < n / 20) {
+        std::printf("split path too rarely taken (%d)\n", split_used);
+        return 1;
+    }
     /* rates on a 30 MB body of 300-aa proteins (the C2 request shape) */
     std::string big;
     for (int r = 0; r < 100000; r++) {

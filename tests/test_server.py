@@ -121,6 +121,84 @@ def test_query_and_add_routes_match_golden(gpu, ds):
 
 
 @pytest.mark.gpu
+def test_concurrent_requests_match_golden(gpu):
+    """Requests on 8 connections at once (4 KmerGuts workers) get the same
+    bytes as one at a time; a client sending Expect: 100-continue gets the
+    interim response first (krequest2.cc:262-270)."""
+    import threading
+    d = os.path.join(GOLDEN, "edge")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    cases = [f for f in _cases("edge") if parse_case(f)[0] in QUERY_FLAGS]
+    srv = Server(os.path.join(d, "data"), threads=4)
+    errors = []
+
+    def run(fname):
+        mode, pname = parse_case(fname)
+        qs = "&".join(x for x in (QUERY_FLAGS[mode], _query_string(pname)) if x)
+        for _ in range(3):
+            got = srv.request("POST", "/query" + ("?" + qs if qs else ""), fasta)
+            if got != HEADER + open(os.path.join(d, fname), "rb").read():
+                errors.append(fname)
+
+    try:
+        ths = [threading.Thread(target=run, args=(f,)) for f in cases[:8]]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert not errors, errors
+        with socket.create_connection(("127.0.0.1", srv.port), timeout=120) as s:
+            s.sendall(b"POST /query HTTP/1.1\r\nExpect: 100-continue\r\nContent-Length: %d\r\n\r\n"
+                      % len(fasta))
+            assert s.recv(64).startswith(b"HTTP/1.1 100 Continue")
+            s.sendall(fasta)
+            out = b""
+            while True:
+                c = s.recv(1 << 16)
+                if not c:
+                    break
+                out += c
+        assert out.endswith(open(os.path.join(d, "expected_query_default.txt"), "rb").read())
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
+def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp_path):
+    """A 5-MiB /query body is cut at record starts and its pieces run on 4
+    workers at once; the response is the oracle's text for the whole body."""
+    import numpy as np
+    from helpers import random_protein
+    d = os.path.join(GOLDEN, "scoring")
+    base = open(os.path.join(d, "input.fasta"), "rb").read()
+    rng = np.random.default_rng(99)
+    recs = [base]
+    size = len(base)
+    i = 0
+    while size < 5 << 20:
+        r = b">p%d\n%s\n" % (i, random_protein(rng, int(rng.integers(5, 600))).encode())
+        recs.append(r)
+        size += len(r)
+        i += 1
+        if i % 50 == 0:
+            recs.append(base)
+            size += len(base)
+    body = b"".join(recs)
+    fasta = tmp_path / "big.fasta"
+    fasta.write_bytes(body)
+    want = oracle_lib.query_text(os.path.join(d, "data"), str(fasta), "query", {})
+    srv = Server(os.path.join(d, "data"), threads=4)
+    try:
+        got = srv.request("POST", "/query", body)
+        assert got == HEADER + want
+        got = srv.request("POST", "/query?details=1", body)
+        want_d = oracle_lib.query_text(os.path.join(d, "data"), str(fasta), "query_details", {})
+        assert got == HEADER + want_d
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
 def test_matrix_route_after_add_matches_golden(gpu):
     d = os.path.join(GOLDEN, "matrix")
     fasta = open(os.path.join(d, "input.fasta"), "rb").read()
