@@ -58,12 +58,21 @@ def main():
     ids = np.arange(n, dtype=np.uint32)
     lens = np.diff(off)
 
-    # /add: one request over all proteins
-    kmap = abi.Kmap(0, abi.KMAP_APPEND)
-    t0 = time.perf_counter()
-    ctx.process_batch(res, off, want=0)
-    kmap.add_hits(ctx, ids)
-    t_add = time.perf_counter() - t0
+    # /add: one request over all proteins into an empty mapping; the first
+    # one warms the path (code objects, context buffers), the median of the
+    # next three is reported, the last mapping serves the /matrix requests
+    add_times = []
+    kmap = None
+    for r in range(4):
+        if kmap is not None:
+            kmap.close()
+        kmap = abi.Kmap(0, abi.KMAP_APPEND)
+        t0 = time.perf_counter()
+        ctx.process_batch(res, off, want=0)
+        kmap.add_hits(ctx, ids)
+        if r:
+            add_times.append(time.perf_counter() - t0)
+    t_add = float(np.median(add_times))
 
     def matrix_request():
         mx = abi.Matrix(kmap)
