@@ -18,7 +18,8 @@
  * One connection = one request, as in krequest2.cc: the request line and
  * headers are read, then Content-length bytes of body, the router builds the
  * response, the connection is closed.  Each connection runs on its own
- * thread; the router's KmerGuts pool bounds how many run on the GPU at once.
+ * thread (at most 256 open at once); the router's KmerGuts pool bounds how
+ * many run on the GPU at once.
  * GET /quit stops the listener after its response.
  */
 #include <arpa/inet.h>
@@ -48,6 +49,7 @@ namespace {
 std::atomic<bool> g_stop{false};
 int g_listen_fd = -1;
 std::atomic<int> g_active{0}; /* connection threads still running */
+constexpr int kMaxConnections = 256; /* accept waits while this many are open */
 
 bool write_all(int fd, const char *p, size_t n)
 {
@@ -271,6 +273,8 @@ int main(int argc, char **argv)
     std::signal(SIGTERM, on_signal);
 
     while (!g_stop) {
+        while (g_active >= kMaxConnections && !g_stop)
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
         int c = ::accept(fd, nullptr, nullptr);
         if (c < 0) {
             if (errno == EINTR && !g_stop)
