@@ -69,19 +69,34 @@ __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__rest
         sums[blockIdx.x] = total;
 }
 
+/* exclusive scan of the workgroup sums in place, one workgroup.  (Each
+ * plan_scan workgroup used to add up all earlier sums itself: quadratic in
+ * the number of workgroups, 0.5 ms for the 9.9M fragments of a 1M-read fq
+ * chunk.) */
+__global__ __launch_bounds__(256) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups)
+{
+    __shared__ uint64_t lds4[4];
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < groups; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t v = i < groups ? sums[i] : 0;
+        uint64_t tot;
+        const uint64_t incl = block_scan(v, lds4, tot);
+        if (i < groups)
+            sums[i] = carry + incl - v;
+        carry += tot;
+        __syncthreads(); /* lds4 is rewritten by the next round */
+    }
+}
+
 __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restrict__ seq_off,
                                                         uint32_t n, const uint64_t *__restrict__ sums,
                                                         uint64_t *__restrict__ wbase,
                                                         uint32_t *__restrict__ tile_seq,
                                                         uint32_t tile_windows)
 {
-    __shared__ uint64_t lds_a[4], lds_b[4];
-    uint64_t p = 0; /* windows of all earlier workgroups */
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 256)
-        p += sums[b];
-    uint64_t before;
-    block_scan(p, lds_a, before);
-    __syncthreads();
+    __shared__ uint64_t lds_b[4];
+    const uint64_t before = sums[blockIdx.x]; /* windows of all earlier workgroups */
 
     const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
     const uint64_t mine = thread_windows(seq_off, n, s0);
@@ -111,6 +126,8 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase,
     const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
     hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<uint64_t *>(workspace));
+    hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(256), 0, stream, static_cast<uint64_t *>(workspace),
+                       groups);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
     return hipGetLastError();
