@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box pass (run through gpurun from the repo root):
 #   bash tools/gpu_check.sh TAG [quick]
-# 1. the -m gpu test suite   2. bench.py (C2)   3. C3 /matrix   4. C4 fq
+# 1. the -m gpu test suite   2. bench.py (C2)   3. C3 /matrix   4. C4 fq   5. HTTP serving
 # "quick" skips the CPU baselines.  Output in gpurun_out/TAG; every GPU step
 # has its own time limit and the script stops at the first failure.
 set -euo pipefail
@@ -17,4 +17,5 @@ timeout -k 10 1500 python3 -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 
 timeout -k 10 900 python3 bench.py $NOCPU > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 600 python3 tools/bench_matrix.py $NOCPU > "$OUT/bench_matrix.json" 2> "$OUT/bench_matrix.err"
 timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
+timeout -k 10 600 python3 tools/bench_server.py > "$OUT/bench_server.json" 2> "$OUT/bench_server.err"
 echo "[gpu_check] done" >&2
