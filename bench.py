@@ -5,20 +5,25 @@
 
 Workload (BASELINE.json configs[1], SURVEY §8(d) "C2"): per GPU, 100,000
 synthetic 300-aa proteins (half planted copies of image proteins with 10%
-substitutions, half uniform) against a synthetic 1,000,000,000-entry signature
-image in the reference's 24-byte bucket format (num_sigs 3,559,786,523 by the
-builder's sizing rule, 85.4 GB), built directly in HBM.  Every rank holds an
-image replica and its own query shard (weak scaling; no collective on the data
-path -- torch.distributed is used for the barrier and the max-time reduction).
+substitutions, half uniform) against a synthetic 1B-entry signature image:
+exactly 1,000,000,000 distinct keys (kgx_image_build_synthetic_distinct) in
+the reference's 24-byte bucket format (num_sigs 3,559,786,523 by the builder's
+sizing rule, 85.4 GB; alpha = 0.281), built directly in HBM.  Every rank holds
+an image replica and its own query shard (weak scaling; no collective on the
+data path -- torch.distributed is used for the barrier and the max-time
+reduction).  --strong runs C5 instead (BASELINE.json configs[4]): one batch of
+1,000,000 x 300 aa split across the ranks in residue-balanced shards
+(shard.balanced_shards, the kgx_pool split), strong scaling.
 
-A step = one pass over the rank's resident batch: plan -> probe -> score
-(kgx_run_device), inputs and outputs in HBM.  Steps rotate over --pipeline
-worker contexts (own stream + buffers each, as the reference's thread pool
-keeps one KmerGuts per worker), so one batch's scoring overlaps the next
-batch's probe.  The probe kernel is timed with
-HIP events on the stream it runs on; the roofline uses SURVEY §8(d)'s
-algorithmic bytes per window, (24 * P + 1), with P the mean buckets examined
-per probed window measured by the CPU oracle on the rank-0 sample.
+A step = one pass over one resident batch: plan -> probe -> score
+(kgx_run_device), inputs and outputs in HBM.  Steps rotate over --batches
+distinct batches (so no step re-probes the lines the previous one left in
+the 256 MiB Infinity Cache) and over --pipeline worker contexts (own stream +
+buffers each, as the reference's thread pool keeps one KmerGuts per worker),
+so one batch's scoring overlaps the next batch's probe.  The probe kernel is
+timed with HIP events on the stream it runs on; the roofline uses SURVEY
+§8(d)'s algorithmic bytes per window, (24 * P + 1), with P the mean buckets
+examined per probed window measured by the CPU oracle on the rank-0 sample.
 """
 from __future__ import annotations
 
@@ -43,7 +48,22 @@ def log(*a):
 
 
 
-def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, target_s):
+def host_cpus():
+    """(threads to use, CPUs in this process's affinity mask, cgroup CPU quota
+    or None): SURVEY §8(d) d4's T = nproc, where a cgroup quota (cpu.max)
+    caps what the affinity mask shows."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        quota = None
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, target_s, want):
     """The oracle (bit-exact CPU restatement) over a bounded sample of rank 0's
     batch, on this host's cores, against a host copy of the same image.  The
     sample is processed repeatedly until about target_s seconds of timed work
@@ -56,11 +76,11 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
     res, off = spec_queries(spec, n_seq_sample, length, x_permille)
     secs, passes, probes, windows = 0.0, 0, 0, 0
     while secs < target_s and passes < 200:
-        r = oracle.process_batch(table, res, off, want=7, n_threads=threads)
+        r = oracle.process_batch(table, res, off, want=want, n_threads=threads)
         secs += r.seconds
         passes += 1
         probes, windows = r.probes, r.windows
-    r1 = oracle.process_batch(table, res, off, want=7, n_threads=1)
+    r1 = oracle.process_batch(table, res, off, want=want, n_threads=1)
     del table
     cpu_model = ""
     try:
@@ -77,12 +97,17 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
         "cores": threads,
         "kind": "port",
         "sample": f"{passes} passes over the first {n_seq_sample} x {length}-aa queries of rank 0's "
-                  f"batch against a host copy of the same image (hits+calls+OTU), {threads} threads, "
-                  f"{secs:.1f} s timed",
+                  f"batch against a host copy of the same image ({WANT_NAMES.get(want, want)}, the GPU "
+                  f"step's outputs), {threads} threads, {secs:.1f} s timed",
+        "want": want,
         "single_thread_value": float(len(res) / r1.seconds),
         "pbar": probes / max(1, windows),
         "windows": int(windows),
     }
+
+
+WANT_NAMES = {3: "hits + calls", 7: "hits + calls + OTU", 11: "hits + calls + best call",
+              15: "hits + calls + OTU + best call"}
 
 
 def spec_queries(spec, n, length, x_permille):
@@ -95,13 +120,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n-keys", type=float, default=1e9)
+    ap.add_argument("--n-keys", type=float, default=1e9, help="distinct keys stored in the image")
     ap.add_argument("--num-sigs", type=int, default=0, help="0 = builder sizing rule")
-    ap.add_argument("--n-seq", type=int, default=100000, help="sequences per GPU")
+    ap.add_argument("--n-seq", type=int, default=100000, help="sequences per GPU (C2) / per batch (--strong)")
+    ap.add_argument("--strong", action="store_true",
+                    help="C5: one batch of --strong-seq proteins split across the ranks (strong scaling)")
+    ap.add_argument("--strong-seq", type=int, default=1000000)
+    ap.add_argument("--batches", type=int, default=8, help="distinct resident batches the steps rotate over")
     ap.add_argument("--length", type=int, default=300)
     ap.add_argument("--x-permille", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=100000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the CPUs this process may use (affinity mask, capped by a cgroup quota)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-microbench", action="store_true")
@@ -130,9 +160,12 @@ def main():
         raise SystemExit(f"rank {d.rank}: no gfx950 device {dev}")
 
     t0 = time.time()
-    img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs, device=dev)
-    log(f"[bench] rank {d.rank}: built {stored} keys in {spec.num_sigs} buckets "
-        f"({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
+    # n_keys distinct keys stored (the generator's stream
+    # runs past n_keys entries until that many distinct keys are in)
+    img, n_entries = abi.Image.synthetic_distinct(spec.n_keys, n_keys, spec.num_sigs, device=dev)
+    stored = n_keys
+    log(f"[bench] rank {d.rank}: built {stored} distinct keys ({n_entries} entries of the stream) in "
+        f"{spec.num_sigs} buckets ({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
     if args.image_layout == "aos":
         img.set_layout(abi.Image.AOS24)
     if args.filter_log2:
@@ -144,14 +177,32 @@ def main():
     probe_kernel = "probe_line_kernel" if layout == "PACKED16" and not args.filter_log2 else "probe_kernel"
     log(f"[bench] resident layout {layout}")
     ctx = abi.Context(img)
-    n, Ls = args.n_seq, args.length
+    Ls = args.length
+
+    # this rank's queries: weak (C2) = its own n_seq per batch; strong (C5) =
+    # its residue-balanced shard of each global batch (all lengths equal, so
+    # balanced_shards cuts equal counts)
+    if args.strong:
+        n_global = args.strong_seq
+        glob_off = np.arange(n_global + 1, dtype=np.uint64) * np.uint64(Ls)
+        s0, s1 = shard.balanced_shards(glob_off, d.world)[d.rank]
+        n = s1 - s0
+        q0s = [b * n_global + s0 for b in range(args.batches)]
+    else:
+        n_global = args.n_seq * d.world
+        n = args.n_seq
+        q0s = [(b * d.world + d.rank) * n for b in range(args.batches)]
+    if n < 1:
+        raise SystemExit(f"rank {d.rank}: empty shard")
     n_res = n * Ls
-    d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
-    abi.check(L.kgx_device_alloc(dev, n_res, ctypes.byref(d_res)), "alloc residues")
-    abi.check(L.kgx_device_alloc(dev, (n + 1) * 8, ctypes.byref(d_off)), "alloc offsets")
-    q0, _ = shard.weak_shard(d.rank, n)  # weak scaling: each rank its own shard
-    abi.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, args.x_permille, q0, d_res, d_off),
-              "synth queries")
+    batches = []
+    for q0 in q0s:
+        d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+        abi.check(L.kgx_device_alloc(dev, n_res, ctypes.byref(d_res)), "alloc residues")
+        abi.check(L.kgx_device_alloc(dev, (n + 1) * 8, ctypes.byref(d_off)), "alloc offsets")
+        abi.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, args.x_permille, q0, d_res, d_off),
+                  "synth queries")
+        batches.append((d_res, d_off))
     ctx.synchronize()
 
     params = abi.default_params()
@@ -168,7 +219,8 @@ def main():
     # probe.  Every step is still a full pass over a whole batch.
     ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
 
-    def step(timed_probe: list | None, c=ctx):
+    def step(timed_probe: list | None, c=ctx, b=0):
+        d_res, d_off = batches[b % len(batches)]
         abi.check(L.kgx_stage_plan(c.handle, d_off, n, n_res), "plan")
         if timed_probe is not None:
             abi.check(L.kgx_event_record(ev[0], c.handle), "event")
@@ -182,14 +234,15 @@ def main():
             timed_probe.append(ms.value)
 
     for i in range(args.warmup * len(ctxs)):
-        step(None, ctxs[i % len(ctxs)])
+        step(None, ctxs[i % len(ctxs)], i)
     for c in ctxs:
         c.synchronize()
 
-    # probe-kernel duration (HIP events on the context's stream), untimed pass
+    # probe-kernel duration (HIP events on the context's stream), untimed
+    # pass, rotating over the batches like the timed steps
     probe_ms: list = []
-    for _ in range(max(3, min(args.steps, 10))):
-        step(probe_ms)
+    for i in range(max(3, min(args.steps, 10))):
+        step(probe_ms, ctx, i)
     ctx.synchronize()
 
     probe_ab = None
@@ -201,11 +254,13 @@ def main():
         names = name.split(",")
         vals = vals.split(",")
         times = {v: [] for v in vals}
+        k = 0
         for _ in range(args.ab_rounds):
             for v in vals:
                 for nm, x in zip(names, v.split(":")):
                     ctx.set_option(nm, int(x))
-                step(times[v])
+                step(times[v], ctx, k)
+                k += 1
         ctx.set_option("probe_variant", -1)
         ctx.set_option("probe_j", 2)
         ctx.set_option("probe_filter", 1)
@@ -219,7 +274,7 @@ def main():
         c.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(None, ctxs[i % len(ctxs)])
+        step(None, ctxs[i % len(ctxs)], i)
     for c in ctxs:
         c.synchronize()
     d.barrier()
@@ -230,14 +285,15 @@ def main():
     # sanity: counts of the last step
     out = abi.DeviceResult()
     abi.check(L.kgx_device_result_get(last.handle, ctypes.byref(out)), "result")
+    last.check_plan()
     hc = np.empty(n, np.uint32)
     cc = np.empty(n, np.uint32)
     abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
     abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
     total_hits = int(d.sum(float(hc.sum())))
     log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
-        f"(planted mean {hc[::2].mean():.1f}, random mean {hc[1::2].mean():.2f}); "
-        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts), "
+        f"(even-q mean {hc[::2].mean():.1f}, odd-q mean {hc[1::2].mean():.2f}); "
+        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
         f"probe {np.mean(probe_ms):.3f} ms")
 
     # PCIe-inclusive rate of the host-buffer boundary (kgx_process_batch:
@@ -245,6 +301,7 @@ def main():
     # beside `value`, never as it
     host_path = None
     if d.rank == 0 and not args.no_host_path:
+        d_res, d_off = batches[0]
         res_h = np.empty(n_res, np.uint8)
         off_h = np.empty(n + 1, np.uint64)
         abi.check(L.kgx_memcpy_d2h(res_h.ctypes.data, d_res, res_h.nbytes), "d2h")
@@ -272,7 +329,7 @@ def main():
     ceiling = None
     if d.rank == 0 and not args.no_microbench:
         ceiling = {}
-        n_reads = int(n * max(0, Ls - 8) * 1.4)
+        n_reads = int(min(n, 100000) * max(0, Ls - 8) * 1.4)
         for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64),
                                    (3, "rec16", 16), (4, "line64", 64)):
             ms, reads = ctypes.c_float(), ctypes.c_uint64()
@@ -290,16 +347,20 @@ def main():
     # the CPU port is timed at N=1 only (one host, one baseline; at N>1 the
     # other ranks would wait on rank 0's host copy of the image)
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t_auto, aff, quota = host_cpus()
+        threads = args.cpu_threads or t_auto
         cpu = cpu_baseline(abi, img, spec, min(args.cpu_sample, n), Ls, threads, args.x_permille,
-                           args.cpu_seconds)
-        log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads, "
-            f"P = {cpu['pbar']:.4f}")
+                           args.cpu_seconds, want)
+        cpu["affinity_cpus"] = aff
+        cpu["cgroup_cpu_quota"] = quota
+        log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads "
+            f"(affinity {aff} CPUs, cgroup quota {quota}), P = {cpu['pbar']:.4f}")
 
     for e in ev:
         L.kgx_event_destroy(e)
-    L.kgx_device_free(d_res)
-    L.kgx_device_free(d_off)
+    for d_res, d_off in batches:
+        L.kgx_device_free(d_res)
+        L.kgx_device_free(d_off)
     for c in ctxs:
         c.close()
     img.close()
@@ -318,12 +379,20 @@ def main():
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if (tj.get("n_keys") == n_keys and tj.get("n_seq") == n and tj.get("length") == Ls
-                        and tj.get("image_layout", "AOS24") == layout):
+                if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
+                        and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout):
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        value = shard.job_throughput(d.world, n_res, args.steps, t_max)
+        residues_per_step_job = n_global * Ls  # every rank's shard of every step
+        value = residues_per_step_job * args.steps / t_max
+        if args.strong:
+            workload = (f"C5: {n_global} x {Ls}-aa synthetic proteins per step split across {d.world} GPU(s) "
+                        f"(residue-balanced shards) vs {n_keys:,}-entry signature image replicated per GPU")
+        else:
+            workload = (f"C2: {n} x {Ls}-aa synthetic proteins per GPU vs {n_keys:,}-entry signature image "
+                        f"({spec.num_sigs:,} buckets, {spec.num_sigs * 24 / 1e9:.1f} GB) resident in HBM")
+        line_ceiling = ceiling["line64"] if ceiling else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -333,18 +402,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
             "config": {
-                "workload": f"C2: {n} x {Ls}-aa synthetic proteins per GPU vs {n_keys:,}-entry "
-                            f"signature image ({spec.num_sigs:,} buckets, "
-                            f"{spec.num_sigs * 24 / 1e9:.1f} GB) resident in HBM",
-                "n_seq_per_gpu": n, "seq_len": Ls, "n_keys": n_keys, "keys_stored": stored,
+                "workload": workload,
+                "n_seq_per_gpu": n, "n_seq_per_step": n_global, "seq_len": Ls, "n_keys": n_keys,
+                "keys_stored": stored, "stream_entries": n_entries,
+                "load_factor": stored / spec.num_sigs,
                 "presence_filter_bits": (1 << args.filter_log2) if args.filter_log2 else 0,
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
-                "worker_contexts": len(ctxs),
+                "worker_contexts": len(ctxs), "distinct_batches": len(batches),
                 "hits_total": total_hits,
                 "outputs": {3: "hits + calls (lookup_request, find_best_match)",
                             7: "hits + calls + OTU (add_request)"}.get(want, f"want={want}"),
@@ -358,6 +427,7 @@ def main():
                 "traffic": traffic,
                 "kernel": probe_kernel,
                 "kernel_ms": probe_s * 1e3,
+                "windows_per_launch": windows_per_launch,
                 "alg_bytes_per_launch": alg_bytes,
                 "pbar": pbar,
                 "random_read_ceiling": ceiling,
@@ -367,15 +437,16 @@ def main():
                 "image_layout": layout,
                 "alg_bytes_per_launch_resident_layout": windows_per_launch * (
                     (16.0 if layout == "PACKED16" else 24.0) * pbar + 1.0),
-                "frac_of_random_bucket_ceiling": (
-                    windows_per_launch * pbar / probe_s /
-                    ceiling["rec16" if layout == "PACKED16" else "bucket24"]["reads_per_s"]
-                    if ceiling else None),
-                # the line probe reads >= 1 64-B line per window: windows/s
-                # over the cooperative random-line ceiling (a lower bound)
-                "frac_of_random_line_ceiling": (
-                    windows_per_launch / probe_s / ceiling["line64"]["reads_per_s"]
-                    if ceiling and probe_kernel == "probe_line_kernel" else None),
+                # north_star: algorithmic bytes/s (24 P + 1 per window) over the
+                # measured random-access bandwidth of the same buffer (useful
+                # bytes/s of the cooperative random 64-B line reads the probe does)
+                "frac_of_measured_random_access": (
+                    achieved / (line_ceiling["useful_GBps"] * 1e9) if line_ceiling else None),
+                # the line probe reads >= 1 64-B line per window: windows/s over
+                # the random-line rate (a lower bound of the line-rate fraction)
+                "frac_of_random_line_rate": (
+                    windows_per_launch / probe_s / line_ceiling["reads_per_s"]
+                    if line_ceiling and probe_kernel == "probe_line_kernel" else None),
             },
             "cpu_baseline": cpu,
             "host_path": host_path,

@@ -145,6 +145,7 @@ SIGNATURES = {
     "kgx_image_open": (_INT, [_CS, _INT, _PP]),
     "kgx_image_from_memory": (_INT, [_P, _U64, _INT, _PP]),
     "kgx_image_build_synthetic": (_INT, [_U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
+    "kgx_image_build_synthetic_distinct": (_INT, [_U64, _U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
     "kgx_image_build": (_INT, [_P, _P, _P, _P, _P, _U64, _U64, _INT, _PP, ctypes.POINTER(_U64)]),
     "kgx_image_save": (_INT, [_P, _CS]),
     "kgx_image_close": (_INT, [_P]),
@@ -201,6 +202,15 @@ SIGNATURES = {
     "kgx_memcpy_h2d": (_INT, [_P, _P, _U64]),
     "kgx_memcpy_d2h": (_INT, [_P, _P, _U64]),
     "kgx_ctx_synchronize": (_INT, [_P]),
+    "kgx_ctx_check": (_INT, [_P]),
+    "kgx_image_open_replicas": (_INT, [_CS, ctypes.POINTER(_INT), _U32, _PP]),
+    "kgx_image_replicate": (_INT, [_P, _INT, _PP]),
+    "kgx_pool_create": (_INT, [_PP, _U32, _U32, _PP]),
+    "kgx_pool_destroy": (_INT, [_P]),
+    "kgx_pool_size": (_U32, [_P]),
+    "kgx_pool_ctx": (_P, [_P, _U32]),
+    "kgx_pool_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
+    "kgx_shard_cuts": (_INT, [_P, _U32, _U32, _P]),
 }
 
 
@@ -279,6 +289,25 @@ class Image:
         return cls(h.value)
 
     @classmethod
+    def open_replicas(cls, data_dir: str, devices: list[int]) -> list["Image"]:
+        """One replica per listed device, the file read once (kgx_image_open_replicas)."""
+        n = len(devices)
+        devs = (_INT * max(1, n))(*devices)
+        hs = (ctypes.c_void_p * max(1, n))()
+        check(lib().kgx_image_open_replicas(data_dir.encode(), devs, n, hs), f"kgx_image_open_replicas({data_dir})")
+        return [cls(hs[i]) for i in range(n)]
+
+    def replicate(self, device: int) -> "Image":
+        """A device-to-device copy of this image on `device` (kgx_image_replicate)."""
+        h = ctypes.c_void_p()
+        check(lib().kgx_image_replicate(self.handle, device, ctypes.byref(h)), "kgx_image_replicate")
+        return Image(h.value)
+
+    @property
+    def device(self) -> int:
+        return lib().kgx_image_device(self.handle)
+
+    @classmethod
     def from_table(cls, table: np.ndarray, device: int = 0) -> "Image":
         table = np.ascontiguousarray(table)
         hdr = np.array([table.nbytes // 24, 24, 1], dtype=np.int64)
@@ -295,6 +324,17 @@ class Image:
         check(lib().kgx_image_build_synthetic(n_keys, num_sigs, device, ctypes.byref(h),
                                               ctypes.byref(stored)), "kgx_image_build_synthetic")
         return cls(h.value), stored.value
+
+    @classmethod
+    def synthetic_distinct(cls, n_keys: int, n_distinct: int, num_sigs: int,
+                           device: int = 0) -> tuple["Image", int]:
+        """The n_keys spec's stream cut where it holds n_distinct distinct keys;
+        returns (image, entries used)."""
+        h = ctypes.c_void_p()
+        m = ctypes.c_uint64()
+        check(lib().kgx_image_build_synthetic_distinct(n_keys, n_distinct, num_sigs, device, ctypes.byref(h),
+                                                       ctypes.byref(m)), "kgx_image_build_synthetic_distinct")
+        return cls(h.value), m.value
 
     @classmethod
     def build(cls, keys, function_index, otu_index, avg_from_end, function_wt, num_sigs: int,
@@ -444,6 +484,10 @@ class Context:
     def synchronize(self) -> None:
         check(lib().kgx_ctx_synchronize(self.handle), "kgx_ctx_synchronize")
 
+    def check_plan(self) -> None:
+        """kgx_ctx_check: raises when the last plan's offsets were bad."""
+        check(lib().kgx_ctx_check(self.handle), "kgx_ctx_check")
+
     def close(self) -> None:
         if self.handle:
             lib().kgx_ctx_destroy(self.handle)
@@ -573,6 +617,62 @@ class FqHandler:
     def close(self) -> None:
         if self.handle:
             lib().kgx_fq_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def shard_cuts(offsets, n_shards: int) -> np.ndarray:
+    """kgx_shard_cuts: cut points of n_shards residue-balanced contiguous shards."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    cuts = np.zeros(n_shards + 1, np.uint32)
+    check(lib().kgx_shard_cuts(off.ctypes.data, len(off) - 1, n_shards, cuts.ctypes.data), "kgx_shard_cuts")
+    return cuts
+
+
+class Pool:
+    """Contexts over image replicas; one batch split across them (kgx_pool)."""
+
+    def __init__(self, images: list[Image], n_ctx: int | None = None):
+        self.images = images
+        n_ctx = len(images) if n_ctx is None else n_ctx
+        hs = (ctypes.c_void_p * len(images))(*[im.handle for im in images])
+        h = ctypes.c_void_p()
+        check(lib().kgx_pool_create(hs, len(images), n_ctx, ctypes.byref(h)), "kgx_pool_create")
+        self.handle = h.value
+
+    @property
+    def size(self) -> int:
+        return lib().kgx_pool_size(self.handle)
+
+    def set_option(self, name: str, value: int) -> None:
+        """kgx_ctx_set_option on every context of the pool."""
+        for i in range(self.size):
+            check(lib().kgx_ctx_set_option(lib().kgx_pool_ctx(self.handle, i), name.encode(), value),
+                  f"set_option({name})")
+
+    def process_batch(self, residues, offsets, params: Params | dict | None = None,
+                      want: int = WANT_HITS | WANT_CALLS | WANT_OTU, copy: bool = True) -> BatchResult:
+        if params is None or isinstance(params, dict):
+            params = parse_params(params)
+        residues = np.ascontiguousarray(np.frombuffer(bytes(residues), np.uint8)
+                                        if isinstance(residues, (bytes, bytearray)) else residues,
+                                        dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        r = Result()
+        check(lib().kgx_pool_process_batch(self.handle, ctypes.byref(params),
+                                           residues.ctypes.data if residues.size else None,
+                                           offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
+              "kgx_pool_process_batch")
+        return BatchResult(r, want, copy)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().kgx_pool_destroy(self.handle)
             self.handle = None
 
     def __enter__(self):

@@ -609,6 +609,28 @@ KmerPegMapping::encoded_id_t KmerPegMapping::encode_id(const std::string &peg)
     return id;
 }
 
+std::string KmerPegMapping::lookup_genus(const std::string &genus)
+{
+    std::lock_guard<std::mutex> lk(genus_mu_);
+    return genus_map_[genus];
+}
+
+bool KmerPegMapping::find_genus(const std::string &genus, std::string *id) const
+{
+    std::lock_guard<std::mutex> lk(genus_mu_);
+    auto it = genus_map_.find(genus);
+    if (it == genus_map_.end())
+        return false;
+    *id = it->second;
+    return true;
+}
+
+KmerPegMapping::family_data_t KmerPegMapping::family_at(encoded_family_id_t id) const
+{
+    auto it = family_data_.find(id);
+    return it == family_data_.end() ? family_data_t{} : it->second;
+}
+
 std::string KmerPegMapping::decode_id(encoded_id_t id) const
 {
     return id < id_to_peg_.size() ? id_to_peg_[id] : std::string();
@@ -895,7 +917,7 @@ LookupRequest::LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool famil
     if (stoi_param(params, "allow_ambiguous_functions", v))
         allow_ambiguous_functions_ = v != 0;
     auto tg_it = params.find("target_genus");
-    const std::string tg = mapping_->genus_map_[tg_it == params.end() ? std::string() : tg_it->second];
+    const std::string tg = mapping_->lookup_genus(tg_it == params.end() ? std::string() : tg_it->second);
     try {
         if (!tg.empty())
             target_genus_id_ = std::stoul(tg);
@@ -1032,7 +1054,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
                 if (se.hit_total < kmer_hit_threshold_)
                     break;
                 if (family_mode_) {
-                    const KmerPegMapping::family_data_t fd = mapping_->family_data_[it.first];
+                    const KmerPegMapping::family_data_t fd = mapping_->family_at(it.first);
                     const float scaled = (float)se.hit_count / (float)fd.total_size;
                     os << se.hit_count << "\t" << se.hit_total << "\t" << se.weighted_total << "\t" << fd.pgf << "\t"
                        << fd.plf << "\t" << fd.total_size << "\t" << fd.count << "\t" << scaled << "\t"
@@ -1043,7 +1065,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
                     os << mapping_->decode_id(it.first) << "\t" << se.hit_count;
                     auto fh = mapping_->peg_to_family_.find(it.first);
                     if (fh != mapping_->peg_to_family_.end()) {
-                        const KmerPegMapping::family_data_t fd = mapping_->family_data_[fh->second];
+                        const KmerPegMapping::family_data_t fd = mapping_->family_at(fh->second);
                         os << "\t" << fd.pgf << "\t" << fd.plf << "\t" << fd.function << "\n";
                     } else {
                         os << "\n";

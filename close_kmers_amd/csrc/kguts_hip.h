@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <unordered_map>
 #include <ostream>
 #include <memory>
@@ -234,6 +235,16 @@ public:
     };
     std::map<std::string, std::string> genus_map_;
     std::unordered_map<encoded_family_id_t, family_data_t> family_data_;
+    /* genus_map_[genus] (kmer.h:136 lookup_genus: an unknown genus is
+     * inserted with an empty id, which later GET /genus_lookup requests
+     * see) and genus_map_.find (krequest2.cc:311-316), safe beside
+     * concurrent /lookup requests */
+    std::string lookup_genus(const std::string &genus);
+    bool find_genus(const std::string &genus, std::string *id) const;
+    /* family_data_[id] without inserting: the default record when unknown
+     * (the reference's operator[] inserts one into a TBB map, which no
+     * output shows), safe beside concurrent readers */
+    family_data_t family_at(encoded_family_id_t id) const;
     std::map<std::pair<std::string, std::string>, encoded_family_id_t> family_key_to_id_;
     std::unordered_map<encoded_id_t, encoded_family_id_t> peg_to_family_;
     encoded_id_t assign_new_peg_id(const std::string &peg); /* kmer.h:114-121 */
@@ -247,6 +258,7 @@ public:
     void load_nr_families(KmerGuts &kg, const std::string &nr_fasta, size_t batch = 100000);
 
 private:
+    mutable std::mutex genus_mu_;
     encoded_family_id_t next_family_id_ = 0;
     int device_;
     std::map<std::string, encoded_id_t> peg_to_id_;

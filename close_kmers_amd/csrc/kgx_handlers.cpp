@@ -306,7 +306,7 @@ void parse_header_line(const std::string &line, HttpRequest &req)
 
 class KmerRequestRouter::GutsLease {
 public:
-    explicit GutsLease(KmerRequestRouter &r) : r_(r), kg_(r.acquire()) {}
+    explicit GutsLease(KmerRequestRouter &r, long only_slot = -1) : r_(r), kg_(r.acquire(only_slot)) {}
     ~GutsLease() { r_.release(kg_); }
     KmerGuts &operator*() { return *kg_; }
 
@@ -315,62 +315,121 @@ private:
     KmerGuts *kg_;
 };
 
-KmerRequestRouter::KmerRequestRouter(const Options &opt)
-    : opt_(opt), family_mode_(!opt.families_file.empty()) /* kser.cc:289 */
+namespace {
+
+/* one replica per device slot: from the file (read once, copied to every
+ * device) or, for the synthetic hook, built on the first device and copied
+ * device to device to the others */
+std::vector<std::shared_ptr<KmerImage>> open_images(const KmerRequestRouter::Options &opt,
+                                                    const std::vector<int> &devs)
 {
-    if (opt_.synthetic_keys) {
-        kgx_image *img = nullptr;
+    std::vector<kgx_image *> raw(devs.size(), nullptr);
+    int rc;
+    if (opt.synthetic_keys) {
         uint64_t stored = 0;
-        int rc = kgx_image_build_synthetic(opt_.synthetic_keys, opt_.synthetic_sigs, opt_.device, &img, &stored);
+        rc = kgx_image_build_synthetic(opt.synthetic_keys, opt.synthetic_sigs, devs[0], &raw[0], &stored);
         if (rc)
             throw Error(rc, std::string("kgx_image_build_synthetic: ") + kgx_last_error());
-        image_ = std::make_shared<KmerImage>(img);
+        std::vector<int> rcs(devs.size(), KGX_OK);
+        std::vector<std::string> errs(devs.size());
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < devs.size(); i++)
+            th.emplace_back([&, i] {
+                rcs[i] = kgx_image_replicate(raw[0], devs[i], &raw[i]);
+                if (rcs[i])
+                    errs[i] = kgx_last_error();
+            });
+        for (auto &t : th)
+            t.join();
+        for (size_t i = 1; i < devs.size(); i++)
+            if (rcs[i]) {
+                for (auto *im : raw)
+                    kgx_image_close(im);
+                throw Error(rcs[i], "kgx_image_replicate to device " + std::to_string(devs[i]) + ": " + errs[i]);
+            }
     } else {
-        image_ = std::make_shared<KmerImage>(opt_.kmer_data_dir, opt_.device);
+        rc = kgx_image_open_replicas(opt.kmer_data_dir.c_str(), devs.data(), (uint32_t)devs.size(), raw.data());
+        if (rc)
+            throw Error(rc, "KmerImage(" + opt.kmer_data_dir + "): " + kgx_strerror(rc) + " (" + kgx_last_error() +
+                                ")");
     }
-    const int n = std::max(1, opt_.n_kmer_threads);
-    for (int i = 0; i < n; i++) {
-        pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, image_));
-        idle_.push_back(pool_.back().get());
-    }
-    /* kserver.cc:40-130: the family DB goes into the root mapping */
-    auto root = std::make_shared<KmerPegMapping>(opt_.device);
-    mapping_map_[""] = root;
+    std::vector<std::shared_ptr<KmerImage>> out;
+    for (auto *im : raw)
+        out.push_back(std::make_shared<KmerImage>(im));
+    return out;
+}
+
+std::vector<int> device_list(const KmerRequestRouter::Options &opt)
+{
+    return opt.devices.empty() ? std::vector<int>{opt.device} : opt.devices;
+}
+
+} // namespace
+
+KmerRequestRouter::KmerRequestRouter(const Options &opt)
+    : opt_(opt), family_mode_(!opt.families_file.empty()) /* kser.cc:289 */,
+      picker_(std::max<size_t>((size_t)std::max(1, opt.n_kmer_threads), device_list(opt).size()),
+              device_list(opt).size())
+{
+    const std::vector<int> devs = device_list(opt_);
+    images_ = open_images(opt_, devs);
+    /* every device gets at least one worker; worker w on slot w % n (kgx_dispatch.h) */
+    for (size_t w = 0; w < picker_.n_workers(); w++)
+        pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, images_[picker_.slot_of(w)]));
+    /* kserver.cc:40-130: the family DB goes into the root mapping, on the first device */
+    auto root = std::make_shared<KmerPegMapping>(devs[0]);
+    mapping_map_[""] = Mapping{root, std::make_shared<std::shared_mutex>()};
     if (!opt_.genus_mapping.empty())
         root->load_genus_map(opt_.genus_mapping);
     if (!opt_.families_file.empty())
         root->load_families(opt_.families_file);
     if (family_mode_)
         for (auto &nr : opt_.families_nr)
-            root->load_nr_families(*pool_[0], nr);
+            root->load_nr_families(*pool_[0], nr); /* worker 0 is on slot 0: the mapping's device */
 }
 
 KmerRequestRouter::~KmerRequestRouter() = default;
 
-KmerGuts *KmerRequestRouter::acquire()
+std::vector<int> KmerRequestRouter::worker_devices() const
+{
+    std::vector<int> out;
+    for (auto &kg : pool_)
+        out.push_back(kgx_image_device(kg->image_->handle()));
+    return out;
+}
+
+KmerGuts *KmerRequestRouter::acquire(long only_slot)
 {
     std::unique_lock<std::mutex> lk(pool_mu_);
-    pool_cv_.wait(lk, [this] { return !idle_.empty(); });
-    KmerGuts *kg = idle_.back();
-    idle_.pop_back();
-    return kg;
+    long w = -1;
+    pool_cv_.wait(lk, [&] { return (w = picker_.pick(only_slot)) >= 0; });
+    picker_.lease((size_t)w);
+    return pool_[(size_t)w].get();
 }
 
 void KmerRequestRouter::release(KmerGuts *kg)
 {
     {
         std::lock_guard<std::mutex> lk(pool_mu_);
-        idle_.push_back(kg);
+        for (size_t w = 0; w < pool_.size(); w++)
+            if (pool_[w].get() == kg) {
+                picker_.release(w);
+                break;
+            }
     }
-    pool_cv_.notify_one();
+    pool_cv_.notify_all(); /* a slot-restricted waiter may need this worker */
 }
 
-std::shared_ptr<KmerPegMapping> KmerRequestRouter::mapping_for(const std::string &key)
+KmerRequestRouter::Mapping KmerRequestRouter::mapping_for(const std::string &key)
 {
-    /* caller holds mapping_mu_; krequest2.cc:416-425 creates unknown keys */
+    /* krequest2.cc:416-425 creates unknown keys; the k-mer tables of every
+     * mapping live on the first device */
+    std::lock_guard<std::mutex> lk(mapping_mu_);
     auto &m = mapping_map_[key];
-    if (!m)
-        m = std::make_shared<KmerPegMapping>(opt_.device);
+    if (!m.map) {
+        m.map = std::make_shared<KmerPegMapping>(device_list(opt_)[0]);
+        m.mu = std::make_shared<std::shared_mutex>();
+    }
     return m;
 }
 
@@ -415,20 +474,23 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
                 return respond(ver, 200, "OK", os.str());
             }
             if (std::regex_match(req.path, m, genus_re)) {
-                std::lock_guard<std::mutex> lk(mapping_mu_);
-                auto root = mapping_map_.find("");
-                auto hit = root->second->genus_map_.find(m[1].str());
-                if (hit == root->second->genus_map_.end())
+                std::string id;
+                if (!mapping_for("").map->find_genus(m[1].str(), &id))
                     return respond(ver, 404, "Not Found", "genus not found\n");
-                return respond(ver, 200, "OK", hit->second + "\n");
+                return respond(ver, 200, "OK", id + "\n");
             }
             if (req.path == "/dump_sizes") {
-                std::lock_guard<std::mutex> lk(mapping_mu_);
+                std::vector<std::pair<std::string, Mapping>> all;
+                {
+                    std::lock_guard<std::mutex> lk(mapping_mu_);
+                    all.assign(mapping_map_.begin(), mapping_map_.end());
+                }
                 std::ostringstream os;
                 os << "memory dump\n";
-                for (auto &it : mapping_map_) {
+                for (auto &it : all) {
+                    std::shared_lock<std::shared_mutex> rl(*it.second.mu);
                     os << "Mapping '" << it.first << "':\n";
-                    it.second->dump_sizes(os);
+                    it.second.map->dump_sizes(os);
                 }
                 return respond(ver, 200, "OK", os.str());
             }
@@ -499,10 +561,20 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
         if (action == "/fq_lookup" && n == 0) /* fq_process_request.cc:42-46 */
             return respond(ver, 200, "OK", "data done\n");
 
-        GutsLease kg(*this);
+        Mapping mp = mapping_for(key);
+        /* /add and /matrix assign peg ids and read the device k-mer tables
+         * of the mapping (its device: slot 0) -- one at a time per mapping;
+         * /lookup and /fq_lookup only read the mapping, on any device */
+        const bool writes = action == "/add" || action == "/matrix";
+        std::unique_lock<std::shared_mutex> wl(*mp.mu, std::defer_lock);
+        std::shared_lock<std::shared_mutex> rl(*mp.mu, std::defer_lock);
+        if (writes)
+            wl.lock();
+        else
+            rl.lock();
+        GutsLease kg(*this, writes ? 0 : -1);
         (*kg).set_parameters(req.parameters);
-        std::lock_guard<std::mutex> lk(mapping_mu_);
-        auto mapping = mapping_for(key);
+        auto mapping = mp.map;
         if (action == "/fq_lookup") {
             os << header(ver, 200, "OK") << "\n";
             fq_request(*kg, mapping, body, n, os);

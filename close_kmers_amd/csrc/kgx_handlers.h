@@ -23,10 +23,12 @@
 #include <memory>
 #include <mutex>
 #include <ostream>
+#include <shared_mutex>
 #include <string>
 #include <utility>
 #include <vector>
 
+#include "kgx_dispatch.h"
 #include "kguts_hip.h"
 
 namespace kgx {
@@ -89,18 +91,27 @@ void parse_header_line(const std::string &line, HttpRequest &req);
 
 /*
  * KmerRequestRouter (krequest2.cc:273-489 + kserver.cc:40-130): owns the
- * image, a pool of KmerGuts (one per worker, like threadpool.cc:33-36) and
+ * image replicas (one per listed device), a pool of KmerGuts (one per
+ * worker, like threadpool.cc:33-36; worker w on replica w % n_devices) and
  * the keyed mappings ("" = the root mapping, which carries the family DB).
- * handle() returns the full response bytes.  Thread-safe: handlers that
- * touch a mapping run one at a time per server (the reference's TBB maps
- * make concurrent /add safe; one lock keeps request-order id assignment
- * deterministic here), /query runs concurrently up to the pool size.
+ * handle() returns the full response bytes.  Thread-safe: requests run
+ * concurrently up to the pool size; each mapping has a reader/writer lock --
+ * /add writes it (one at a time, so request-order id assignment stays
+ * deterministic; the reference's TBB maps make concurrent /add safe),
+ * /matrix, /lookup and /fq_lookup read it concurrently.  Workers are dealt
+ * by WorkerPicker (kgx_dispatch.h), so the pieces of a large /query and
+ * concurrent requests spread over the devices; /add and /matrix run on a
+ * worker of the mappings' device (their k-mer tables live there).
  */
 class KmerRequestRouter {
 public:
     struct Options {
         std::string kmer_data_dir;
         int device = 0;
+        /* one image replica per entry (the file read once, or the synthetic
+         * image built on the first and copied device to device); empty =
+         * {device}.  The mappings' device tables live on devices[0]. */
+        std::vector<int> devices;
         int n_kmer_threads = 1;
         std::string kmer_version, families_version; /* "" = not given */
         std::string genus_mapping, families_file;
@@ -124,22 +135,30 @@ public:
     static std::string respond(const std::string &http_version, int code, const std::string &status,
                                const std::string &body);
 
+    /* the device each worker runs on (for tests / logs) */
+    std::vector<int> worker_devices() const;
+
 private:
     static constexpr size_t kPieceBytes = 1 << 20; /* krequest2.cc:41 */
     class GutsLease;
-    KmerGuts *acquire();
+    struct Mapping {
+        std::shared_ptr<KmerPegMapping> map;
+        std::shared_ptr<std::shared_mutex> mu; /* /add: exclusive, other handlers: shared */
+    };
+    /* only_slot >= 0: a worker on that device slot */
+    KmerGuts *acquire(long only_slot = -1);
     void release(KmerGuts *kg);
-    std::shared_ptr<KmerPegMapping> mapping_for(const std::string &key);
+    Mapping mapping_for(const std::string &key);
 
     Options opt_;
     bool family_mode_;
-    std::shared_ptr<KmerImage> image_;
+    std::vector<std::shared_ptr<KmerImage>> images_; /* one per device slot */
     std::vector<std::unique_ptr<KmerGuts>> pool_;
-    std::vector<KmerGuts *> idle_;
+    WorkerPicker picker_;
     std::mutex pool_mu_;
     std::condition_variable pool_cv_;
-    std::mutex mapping_mu_; /* the mapping map and every handler that uses a mapping */
-    std::map<std::string, std::shared_ptr<KmerPegMapping>> mapping_map_;
+    std::mutex mapping_mu_; /* the mapping map itself */
+    std::map<std::string, Mapping> mapping_map_;
 };
 
 } // namespace kgx

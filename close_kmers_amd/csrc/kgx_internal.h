@@ -142,8 +142,11 @@ inline bool probe_j_supported(int j) { return (j >= 1 && j <= 5) || j == 8; }
 
 /* launchers; all asynchronous on `stream` */
 size_t plan_workspace_bytes(uint32_t n_seq);
-hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase, uint32_t *tile_seq,
-                       uint32_t tile_windows, void *workspace, hipStream_t stream);
+/* status[0] = 1 when the offsets are not monotone or span more than
+ * n_residues bytes (the batch is then planned as empty), else 0 */
+hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                       uint32_t *tile_seq, uint32_t tile_windows, void *workspace, uint32_t *status,
+                       hipStream_t stream);
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
@@ -179,8 +182,15 @@ hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64
 hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
                               uint32_t rounds, int mode, int ilp, uint64_t *sink, hipStream_t stream);
-hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
-                              unsigned long long *n_stored, hipStream_t stream);
+/* the synthetic spec of n_keys entries (its source proteins), the first
+ * n_entries of its entry stream inserted (entries past n_keys are random
+ * keys); payload = false leaves every stored bucket's owner id in word 2 */
+hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys, uint64_t n_entries,
+                              bool payload, unsigned long long *n_stored, hipStream_t stream);
+/* hist[256] = histogram of owner byte (shift/8) over stored buckets whose
+ * owner matches prefix under prefix_mask (after a payload-less insert) */
+hipError_t launch_owner_hist(const kgx_sig_kmer *table, uint64_t num_sigs, uint32_t prefix, uint32_t prefix_mask,
+                             uint32_t shift, unsigned long long *hist, hipStream_t stream);
 hipError_t launch_entries_image(kgx_sig_kmer *table, uint64_t num_sigs, const uint64_t *keys,
                                 const int32_t *fi, const int32_t *otu, const uint16_t *avg, const float *wt,
                                 uint64_t n_entries, unsigned long long *n_stored, hipStream_t stream);

@@ -36,6 +36,23 @@ __device__ __forceinline__ uint64_t thread_windows(const uint64_t *seq_off, uint
     return w;
 }
 
+/* the batch's offsets are usable iff they are monotone and span at most
+ * n_residues bytes (kgx.h, kgx_run_device); then every window count is
+ * bounded by its length and the plan's buffers (sized from n_residues) hold
+ * the batch.  Checked per thread over its PLAN_PER sequences. */
+__device__ __forceinline__ bool thread_offsets_bad(const uint64_t *seq_off, uint32_t n, uint32_t s0,
+                                                   uint64_t n_residues)
+{
+    const uint64_t first = seq_off[0];
+    bool bad = seq_off[n] < first || seq_off[n] - first > n_residues;
+    for (uint32_t k = 0; k < PLAN_PER; k++)
+        if (s0 + k < n)
+            bad |= seq_off[s0 + k + 1] < seq_off[s0 + k];
+    return bad;
+}
+
+constexpr uint64_t PLAN_BAD = 1ull << 63; /* marks a workgroup sum whose offsets are bad */
+
 /* inclusive scan over a 256-thread workgroup; `total` = sum of all */
 __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *lds4, uint64_t &total)
 {
@@ -59,33 +76,46 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *lds4, uint6
 }
 
 __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__restrict__ seq_off,
-                                                          uint32_t n, uint64_t *__restrict__ sums)
+                                                          uint32_t n, uint64_t n_residues,
+                                                          uint64_t *__restrict__ sums)
 {
     __shared__ uint64_t lds4[4];
     uint64_t total;
-    block_scan(thread_windows(seq_off, n, blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER), lds4,
-               total);
+    const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
+    const bool bad = __syncthreads_or(thread_offsets_bad(seq_off, n, s0, n_residues));
+    block_scan(bad ? 0 : thread_windows(seq_off, n, s0), lds4, total);
     if (threadIdx.x == 0)
-        sums[blockIdx.x] = total;
+        sums[blockIdx.x] = bad ? PLAN_BAD : total;
 }
 
 /* exclusive scan of the workgroup sums in place, one workgroup.  (Each
  * plan_scan workgroup used to add up all earlier sums itself: quadratic in
  * the number of workgroups, 0.5 ms for the 9.9M fragments of a 1M-read fq
  * chunk.) */
-__global__ __launch_bounds__(256) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups)
+__global__ __launch_bounds__(256) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups,
+                                                             uint32_t *__restrict__ status)
 {
     __shared__ uint64_t lds4[4];
+    /* any workgroup that saw bad offsets empties the whole batch (sums[groups]
+     * = 1 tells plan_scan) and raises the context's status word */
+    bool bad = false;
+    for (uint32_t i = threadIdx.x; i < groups; i += 256)
+        bad |= (sums[i] & PLAN_BAD) != 0;
+    bad = __syncthreads_or(bad);
     uint64_t carry = 0;
     for (uint32_t base = 0; base < groups; base += 256) {
         const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < groups ? sums[i] : 0;
+        const uint64_t v = i < groups && !bad ? sums[i] : 0;
         uint64_t tot;
         const uint64_t incl = block_scan(v, lds4, tot);
         if (i < groups)
             sums[i] = carry + incl - v;
         carry += tot;
         __syncthreads(); /* lds4 is rewritten by the next round */
+    }
+    if (threadIdx.x == 0) {
+        sums[groups] = bad ? 1 : 0;
+        status[0] = bad ? 1u : 0u;
     }
 }
 
@@ -97,9 +127,10 @@ __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restri
 {
     __shared__ uint64_t lds_b[4];
     const uint64_t before = sums[blockIdx.x]; /* windows of all earlier workgroups */
+    const bool bad = sums[gridDim.x] != 0;    /* bad offsets: an empty batch */
 
     const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
-    const uint64_t mine = thread_windows(seq_off, n, s0);
+    const uint64_t mine = bad ? 0 : thread_windows(seq_off, n, s0);
     uint64_t tot;
     const uint64_t incl = block_scan(mine, lds_b, tot);
     uint64_t wb = before + incl - mine;
@@ -107,7 +138,7 @@ __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restri
         const uint32_t s = s0 + k;
         if (s >= n)
             break;
-        const uint64_t we = wb + windows_of(seq_off[s + 1] - seq_off[s]);
+        const uint64_t we = wb + (bad ? 0 : windows_of(seq_off[s + 1] - seq_off[s]));
         wbase[s] = wb;
         /* tiles whose first window lies in [wb, we) start inside sequence s */
         for (uint64_t t = (wb + tile_windows - 1) / tile_windows; t * tile_windows < we; t++)
@@ -118,16 +149,18 @@ __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restri
         wbase[n] = before + tot;
 }
 
-size_t plan_workspace_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 1) * sizeof(uint64_t); }
+/* the workgroup sums + the bad-offsets word */
+size_t plan_workspace_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 2) * sizeof(uint64_t); }
 
-hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t *wbase, uint32_t *tile_seq,
-                       uint32_t tile_windows, void *workspace, hipStream_t stream)
+hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                       uint32_t *tile_seq, uint32_t tile_windows, void *workspace, uint32_t *status,
+                       hipStream_t stream)
 {
     const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
-    hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
+    hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq, n_residues,
                        static_cast<uint64_t *>(workspace));
     hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(256), 0, stream, static_cast<uint64_t *>(workspace),
-                       groups);
+                       groups, status);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
     return hipGetLastError();

@@ -181,6 +181,9 @@ struct kgx_ctx {
     /* device scratch */
     kgx::DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
         dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
+    /* plan status word (1 = the last plan's offsets were bad, batch emptied) */
+    kgx::DevBuf plan_status;
+    kgx::PinnedVec<uint32_t> h_plan_status;
     /* current plan */
     uint32_t n_seq = 0;
     uint64_t n_residues = 0;

@@ -253,17 +253,26 @@ static int validate_header(const kgx_image_header &h, uint64_t file_size)
     return KGX_OK;
 }
 
-/* file bytes [off, off + total) -> dev, by `threads` host threads: thread t
- * reads chunks t, t + threads, ... with pread into its own two pinned
- * buffers and copies each up on its own stream, so file reads (page cache or
- * disk) run in parallel and overlap the H2D copies.  The reference maps the
- * file with MAP_POPULATE instead (kmer_image.cc:66-77); the bytes are the same. */
-static int load_file_range(int fd, uint64_t off, uint64_t total, char *dev, int device, int threads,
+/* A device destination of a file load: `dev` on `device`. */
+struct LoadDst {
+    char *dev;
+    int device;
+};
+
+/* file bytes [off, off + total) -> every destination, by `threads` host
+ * threads: thread t reads chunks t, t + threads, ... with pread into its own
+ * two pinned buffers and copies each chunk up to every destination on that
+ * destination's stream, so file reads (page cache or disk) run in parallel and
+ * overlap the H2D copies, and a replicated image is read from the file once
+ * (each device's copy runs on its own PCIe link).  The reference maps the file
+ * with MAP_POPULATE instead (kmer_image.cc:66-77); the bytes are the same. */
+static int load_file_range(int fd, uint64_t off, uint64_t total, const std::vector<LoadDst> &dsts, int threads,
                            size_t chunk)
 {
     chunk = (size_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, total)); /* small files: small buffers */
     const uint64_t n_chunks = (total + chunk - 1) / chunk;
     threads = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n_chunks));
+    const size_t D = dsts.size();
     std::atomic<bool> ok(true);
     std::string err;
     std::mutex err_mu;
@@ -273,23 +282,29 @@ static int load_file_range(int fd, uint64_t off, uint64_t total, char *dev, int 
             err = e;
     };
     auto worker = [&](int t) {
-        if (hipSetDevice(device) != hipSuccess)
-            return set_err("hipSetDevice failed");
         void *buf[2] = {nullptr, nullptr};
-        hipStream_t st = nullptr;
-        hipEvent_t ev[2] = {nullptr, nullptr};
+        std::vector<hipStream_t> st(D, nullptr);
+        std::vector<hipEvent_t> ev(2 * D, nullptr); /* ev[k * D + d]: buffer k's copy to dst d */
         bool used[2] = {false, false};
-        if (hipHostMalloc(&buf[0], chunk) != hipSuccess || hipHostMalloc(&buf[1], chunk) != hipSuccess ||
-            hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ev[1], hipEventDisableTiming) != hipSuccess) {
+        bool setup = hipSetDevice(dsts[0].device) == hipSuccess && hipHostMalloc(&buf[0], chunk) == hipSuccess &&
+                     hipHostMalloc(&buf[1], chunk) == hipSuccess;
+        for (size_t d = 0; setup && d < D; d++) {
+            setup = hipSetDevice(dsts[d].device) == hipSuccess &&
+                    hipStreamCreateWithFlags(&st[d], hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&ev[d], hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&ev[D + d], hipEventDisableTiming) == hipSuccess;
+        }
+        if (!setup) {
             set_err("pinned staging allocation failed");
         } else {
             int k = 0;
             for (uint64_t c = (uint64_t)t; c < n_chunks && ok.load(); c += (uint64_t)threads, k ^= 1) {
                 const uint64_t at = c * chunk;
                 const size_t n = (size_t)std::min<uint64_t>(chunk, total - at);
-                if (used[k] && hipEventSynchronize(ev[k]) != hipSuccess) {
+                bool waited = true;
+                for (size_t d = 0; used[k] && d < D; d++)
+                    waited = waited && hipEventSynchronize(ev[k * D + d]) == hipSuccess;
+                if (!waited) {
                     set_err("staging copy failed");
                     break;
                 }
@@ -304,24 +319,32 @@ static int load_file_range(int fd, uint64_t off, uint64_t total, char *dev, int 
                     set_err("short read");
                     break;
                 }
-                if (hipMemcpyAsync(dev + at, buf[k], n, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipEventRecord(ev[k], st) != hipSuccess) {
+                bool copied = true;
+                for (size_t d = 0; copied && d < D; d++)
+                    copied = hipSetDevice(dsts[d].device) == hipSuccess &&
+                             hipMemcpyAsync(dsts[d].dev + at, buf[k], n, hipMemcpyHostToDevice, st[d]) == hipSuccess &&
+                             hipEventRecord(ev[k * D + d], st[d]) == hipSuccess;
+                if (!copied) {
                     set_err("H2D copy failed");
                     break;
                 }
                 used[k] = true;
             }
         }
-        if (st)
-            (void)hipStreamSynchronize(st);
-        for (int i = 0; i < 2; i++) {
-            if (ev[i])
-                (void)hipEventDestroy(ev[i]);
+        for (size_t d = 0; d < D; d++)
+            if (st[d]) {
+                (void)hipSetDevice(dsts[d].device);
+                (void)hipStreamSynchronize(st[d]);
+            }
+        for (auto e : ev)
+            if (e)
+                (void)hipEventDestroy(e);
+        for (int i = 0; i < 2; i++)
             if (buf[i])
                 (void)hipHostFree(buf[i]);
-        }
-        if (st)
-            (void)hipStreamDestroy(st);
+        for (size_t d = 0; d < D; d++)
+            if (st[d])
+                (void)hipStreamDestroy(st[d]);
     };
     std::vector<std::thread> pool;
     for (int t = 0; t < threads; t++)
@@ -342,11 +365,12 @@ static int load_threads(uint64_t bytes)
     return std::max(1, std::min(n, 64));
 }
 
-int kgx_image_open(const char *dir, int device, kgx_image **out)
+/* <dir>/kmer.table.mem_map: opened, stat'ed and its header validated
+ * (kmer_image.cc:128-147); *fd stays open on success */
+static int open_image_file(const char *dir, int *fd_out, kgx_image_header *h, std::string *path_out)
 {
-    if (!dir || !out)
-        return fail(KGX_EINVAL, "null argument");
     const std::string path = std::string(dir) + "/kmer.table.mem_map";
+    *path_out = path;
     const int fd = ::open(path.c_str(), O_RDONLY);
     if (fd < 0)
         return fail(KGX_EIO, "open " + path + ": " + std::strerror(errno));
@@ -355,30 +379,126 @@ int kgx_image_open(const char *dir, int device, kgx_image **out)
         ::close(fd);
         return fail(KGX_EIO, "stat " + path + " failed");
     }
-    kgx_image_header h;
-    if (pread(fd, &h, sizeof(h), 0) != (ssize_t)sizeof(h)) {
+    if (pread(fd, h, sizeof(*h), 0) != (ssize_t)sizeof(*h)) {
         ::close(fd);
         return fail(KGX_EFORMAT, "Version mismatch: file size does not match");
     }
-    int rc = validate_header(h, (uint64_t)st.st_size);
+    int rc = validate_header(*h, (uint64_t)st.st_size);
     if (rc) {
         ::close(fd);
         return rc;
     }
-    kgx_image *img = nullptr;
-    rc = image_alloc(device, h.num_sigs, &img);
-    if (rc) {
-        ::close(fd);
+    *fd_out = fd;
+    return KGX_OK;
+}
+
+int kgx_image_open(const char *dir, int device, kgx_image **out)
+{
+    if (!dir || !out)
+        return fail(KGX_EINVAL, "null argument");
+    return kgx_image_open_replicas(dir, &device, 1, out);
+}
+
+int kgx_image_open_replicas(const char *dir, const int *devices, uint32_t n, kgx_image **out)
+{
+    if (!dir || !out || !devices || n == 0)
+        return fail(KGX_EINVAL, "null argument or no devices");
+    for (uint32_t i = 0; i < n; i++)
+        out[i] = nullptr;
+    int fd = -1;
+    kgx_image_header h;
+    std::string path;
+    int rc = open_image_file(dir, &fd, &h, &path);
+    if (rc)
         return rc;
+    std::vector<kgx_image *> imgs(n, nullptr);
+    std::vector<LoadDst> dsts;
+    auto close_all = [&]() {
+        for (auto *im : imgs)
+            kgx_image_close(im);
+    };
+    for (uint32_t i = 0; i < n; i++) {
+        rc = image_alloc(devices[i], h.num_sigs, &imgs[i]);
+        if (rc) {
+            ::close(fd);
+            close_all();
+            return rc;
+        }
+        dsts.push_back({reinterpret_cast<char *>(imgs[i]->d_table), devices[i]});
     }
-    rc = load_file_range(fd, sizeof(h), h.num_sigs * sizeof(kgx_sig_kmer), reinterpret_cast<char *>(img->d_table),
-                         device, load_threads(h.num_sigs * sizeof(kgx_sig_kmer)), 32ull << 20);
+    rc = load_file_range(fd, sizeof(h), h.num_sigs * sizeof(kgx_sig_kmer), dsts,
+                         load_threads(h.num_sigs * sizeof(kgx_sig_kmer)), 32ull << 20);
     ::close(fd);
     if (rc) {
-        kgx_image_close(img);
+        close_all();
         return fail(rc, "loading " + path + ": " + kgx_last_error());
     }
-    return image_settle(img, out);
+    /* every replica is packed on its own device at once */
+    std::vector<int> rcs(n, KGX_OK);
+    std::vector<std::string> errs(n);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < n; i++)
+        th.emplace_back([&, i] {
+            kgx_image *settled = nullptr;
+            rcs[i] = image_settle(imgs[i], &settled); /* closes the image on failure */
+            if (rcs[i])
+                errs[i] = kgx_last_error();
+            imgs[i] = rcs[i] ? nullptr : settled;
+        });
+    for (auto &t : th)
+        t.join();
+    for (uint32_t i = 0; i < n; i++)
+        if (rcs[i]) {
+            close_all();
+            return fail(rcs[i], "replica on device " + std::to_string(devices[i]) + ": " + errs[i]);
+        }
+    for (uint32_t i = 0; i < n; i++)
+        out[i] = imgs[i];
+    return KGX_OK;
+}
+
+int kgx_image_replicate(const kgx_image *src, int device, kgx_image **out)
+{
+    if (!src || !out)
+        return fail(KGX_EINVAL, "null argument");
+    *out = nullptr;
+    kgx_image *img = nullptr;
+    int rc = image_alloc(device, src->num_sigs, &img);
+    if (rc)
+        return rc;
+    hipError_t e = hipSuccess;
+    if (src->layout == KGX_LAYOUT_PACKED16) {
+        /* the same resident layout: allocate the packed table instead */
+        (void)hipFree(img->d_table);
+        img->d_table = nullptr;
+        e = hipMalloc(&img->d_packed, src->num_sigs * sizeof(packed_bucket));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            kgx_image_close(img);
+            return fail(KGX_ENOMEM, "no room for the packed replica");
+        }
+        img->layout = KGX_LAYOUT_PACKED16;
+    }
+    /* device to device: xGMI between two GPUs (the runtime picks the path),
+     * a device-local copy when both are the same GPU */
+    e = hipMemcpyPeer(img->layout == KGX_LAYOUT_PACKED16 ? static_cast<void *>(img->d_packed) : img->d_table,
+                      device, src->resident(), src->device, src->resident_bytes());
+    if (e == hipSuccess && src->d_filter) {
+        const uint64_t fbytes = 8ull << src->filter_log2_words;
+        e = hipMalloc(&img->d_filter, fbytes);
+        if (e == hipSuccess)
+            e = hipMemcpyPeer(img->d_filter, device, src->d_filter, src->device, fbytes);
+        if (e == hipSuccess)
+            img->filter_log2_words = src->filter_log2_words;
+    }
+    if (e == hipSuccess)
+        e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        kgx_image_close(img);
+        return fail(KGX_EDEVICE, std::string("replicate: ") + hipGetErrorString(e));
+    }
+    *out = img;
+    return KGX_OK;
 }
 
 int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, kgx_image **out)
@@ -417,7 +537,7 @@ int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kg
         kgx_image_close(img);
         return fail(KGX_ENOMEM, "counter allocation failed");
     }
-    hipError_t e = launch_synth_image(img->d_table, num_sigs, n_keys, d_count, nullptr);
+    hipError_t e = launch_synth_image(img->d_table, num_sigs, n_keys, n_keys, true, d_count, nullptr);
     unsigned long long cnt = 0;
     if (e == hipSuccess)
         e = hipMemcpy(&cnt, d_count, sizeof(cnt), hipMemcpyDeviceToHost);
@@ -428,6 +548,70 @@ int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kg
     }
     if (n_stored)
         *n_stored = cnt;
+    return image_settle(img, out);
+}
+
+int kgx_image_build_synthetic_distinct(uint64_t n_keys, uint64_t n_distinct, uint64_t num_sigs, int device,
+                                       kgx_image **out, uint64_t *n_entries)
+{
+    if (!out)
+        return fail(KGX_EINVAL, "null output");
+    /* the stream is searched up to 1/8 past n_distinct (a synthetic 8-mer
+     * stream repeats keys ~2% of the time at 1e9 of 20^8); owners are 32-bit */
+    const uint64_t upper = n_distinct + n_distinct / 8 + 1024;
+    if (2 * upper >= num_sigs || upper >= (1ull << 32))
+        return fail(KGX_EFULL, "Your Kmer hash is half-full (kguts.cc:213-216)");
+    kgx_image *img = nullptr;
+    int rc = image_alloc(device, num_sigs, &img);
+    if (rc)
+        return rc;
+    DevBuf d_count, d_hist;
+    hipError_t e = d_count.reserve(sizeof(unsigned long long));
+    if (e == hipSuccess)
+        e = d_hist.reserve(256 * sizeof(unsigned long long));
+    unsigned long long cnt = 0;
+    if (e == hipSuccess)
+        e = launch_synth_image(img->d_table, num_sigs, n_keys, upper, false, d_count.as<unsigned long long>(),
+                               nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(&cnt, d_count.p, sizeof(cnt), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && cnt < n_distinct) {
+        kgx_image_close(img);
+        return fail(KGX_ERANGE, "the synthetic stream holds fewer distinct keys than asked for");
+    }
+    /* radix select of the n_distinct-th smallest owner, a byte per pass */
+    uint32_t prefix = 0, mask = 0;
+    uint64_t k = n_distinct; /* 1-based rank within the current prefix */
+    for (int shift = 24; e == hipSuccess && shift >= 0; shift -= 8) {
+        unsigned long long h[256];
+        e = launch_owner_hist(img->d_table, num_sigs, prefix, mask, (uint32_t)shift,
+                              d_hist.as<unsigned long long>(), nullptr);
+        if (e == hipSuccess)
+            e = hipMemcpy(h, d_hist.p, sizeof(h), hipMemcpyDeviceToHost);
+        if (e != hipSuccess)
+            break;
+        uint32_t b = 0;
+        while (b < 255 && k > h[b])
+            k -= h[b++];
+        prefix |= b << shift;
+        mask |= 255u << shift;
+    }
+    const uint64_t m = (uint64_t)prefix + 1; /* entries [0, m) hold exactly n_distinct keys */
+    if (e == hipSuccess)
+        e = launch_synth_image(img->d_table, num_sigs, n_keys, m, true, d_count.as<unsigned long long>(), nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(&cnt, d_count.p, sizeof(cnt), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        kgx_image_close(img);
+        return fail(KGX_EDEVICE, std::string("synthetic build: ") + hipGetErrorString(e));
+    }
+    if (cnt != n_distinct) {
+        kgx_image_close(img);
+        return fail(KGX_EDEVICE, "synthetic build stored " + std::to_string(cnt) + " keys, not " +
+                                     std::to_string(n_distinct));
+    }
+    if (n_entries)
+        *n_entries = m;
     return image_settle(img, out);
 }
 
@@ -732,6 +916,23 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
     return fail(KGX_EINVAL, "unknown option " + n);
 }
 
+int kgx_ctx_check(kgx_ctx *c)
+{
+    if (!c)
+        return fail(KGX_EINVAL, "null ctx");
+    HIP_TRY(hipSetDevice(c->img->device));
+    if (!c->plan_status.p)
+        return KGX_OK; /* nothing planned yet */
+    HIP_TRY(c->h_plan_status.resize(1));
+    HIP_TRY(hipMemcpyAsync(c->h_plan_status.data(), c->plan_status.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_plan_status[0])
+        return fail(KGX_EINVAL, "batch offsets not monotone or spanning more than n_residues bytes "
+                                "(the batch was processed as empty)");
+    return KGX_OK;
+}
+
 int kgx_ctx_synchronize(kgx_ctx *c)
 {
     if (!c)
@@ -764,8 +965,9 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
-    HIP_TRY(launch_plan(d_off, n_seq, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                        tile_windows, c->plan_ws.p, c->stream));
+    HIP_TRY(c->plan_status.reserve(sizeof(uint32_t)));
+    HIP_TRY(launch_plan(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                        tile_windows, c->plan_ws.p, c->plan_status.as<uint32_t>(), c->stream));
     c->n_seq = n_seq;
     c->n_residues = n_residues;
     c->max_tiles = max_tiles;
@@ -1232,6 +1434,9 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     if (want_best && !c->have_best)
         return fail(KGX_EINVAL, "no device best calls (score with KGX_WANT_BEST)");
     HIP_TRY(hipSetDevice(c->img->device));
+    int rc = kgx_ctx_check(c); /* bad device offsets: an error, not an empty result */
+    if (rc)
+        return rc;
     PhaseTimer tm(c);
     const uint32_t n_seq = c->n_seq;
     /* counts -> dense CSR offsets on the host, gather on the device */

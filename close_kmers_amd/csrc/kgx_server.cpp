@@ -11,6 +11,13 @@
  *                             the family DB (family mode = --families-file given)
  *   --bind ADDR               listen address (default 0.0.0.0, as kserver.cc:144-152)
  *   --device N                GPU (default $KGX_DEVICE or 0)
+ *   --devices LIST            several GPUs, e.g. 0-7 or 0,2,5 (a device may
+ *                             repeat): one image replica each (the file is
+ *                             read once and copied to every device), workers
+ *                             spread over them (worker w on LIST[w % n]; at
+ *                             least one per device), a large /query's pieces
+ *                             and concurrent requests dealt to the least busy
+ *                             device first (kgx_dispatch.h)
  *   --synthetic-image K:S     benchmark hook: a synthetic image of K keys in S
  *                             buckets built in HBM (kmer-data-dir still holds
  *                             function.index / otu.index)
@@ -36,6 +43,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -162,13 +170,49 @@ void on_signal(int)
         ::shutdown(g_listen_fd, SHUT_RDWR);
 }
 
+/* "0-7", "0,2,5", "0,0" -> device list; empty on a syntax error */
+std::vector<int> parse_devices(const std::string &spec)
+{
+    std::vector<int> out;
+    size_t a = 0;
+    while (a <= spec.size()) {
+        size_t b = spec.find(',', a);
+        if (b == std::string::npos)
+            b = spec.size();
+        const std::string part = spec.substr(a, b - a);
+        const size_t dash = part.find('-');
+        char *end = nullptr;
+        if (part.empty())
+            return {};
+        if (dash == std::string::npos) {
+            long v = std::strtol(part.c_str(), &end, 10);
+            if (*end || v < 0)
+                return {};
+            out.push_back((int)v);
+        } else {
+            if (dash == 0 || dash + 1 == part.size())
+                return {};
+            long lo = std::strtol(part.substr(0, dash).c_str(), &end, 10);
+            if (*end)
+                return {};
+            long hi = std::strtol(part.substr(dash + 1).c_str(), &end, 10);
+            if (*end || lo < 0 || hi < lo || hi - lo > 255)
+                return {};
+            for (long v = lo; v <= hi; v++)
+                out.push_back((int)v);
+        }
+        a = b + 1;
+    }
+    return out;
+}
+
 int usage(const char *argv0)
 {
     std::fprintf(stderr,
                  "Usage: %s [options] listen-port kmer-data-dir\n"
                  "  --listen-port-file F  --n-kmer-threads N  --kmer-version V  --families-version V\n"
                  "  --families-genus-mapping F  --families-file F  --families-nr F [F ...]\n"
-                 "  --bind ADDR  --device N  --synthetic-image KEYS:BUCKETS\n",
+                 "  --bind ADDR  --device N  --devices LIST  --synthetic-image KEYS:BUCKETS\n",
                  argv0);
     return 2;
 }
@@ -222,6 +266,11 @@ int main(int argc, char **argv)
             if (!value(v))
                 return usage(argv[0]);
             opt.device = std::atoi(v.c_str());
+        } else if (a == "--devices") {
+            if (!value(v) || (opt.devices = parse_devices(v)).empty()) {
+                std::fprintf(stderr, "bad --devices list\n");
+                return usage(argv[0]);
+            }
         } else if (a == "--synthetic-image") {
             size_t colon;
             if (!value(v) || (colon = v.find(':')) == std::string::npos)
@@ -267,6 +316,12 @@ int main(int argc, char **argv)
     { /* the port file is written once the data are loaded, as kserver.cc */
         std::ofstream pf(port_file);
         pf << ntohs(addr.sin_port) << "\n";
+    }
+    {
+        std::ostringstream ws;
+        for (int d : router->worker_devices())
+            ws << " " << d;
+        std::cerr << "workers on devices" << ws.str() << "\n";
     }
     std::cerr << "Listening on port " << ntohs(addr.sin_port) << "\n";
     std::signal(SIGINT, on_signal);

@@ -263,16 +263,52 @@ hipError_t launch_entries_image(kgx_sig_kmer *table, uint64_t num_sigs, const ui
     return hipGetLastError();
 }
 
-hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys,
-                              unsigned long long *n_stored, hipStream_t stream)
+hipError_t launch_synth_image(kgx_sig_kmer *table, uint64_t num_sigs, uint64_t n_keys, uint64_t n_entries,
+                              bool payload, unsigned long long *n_stored, hipStream_t stream)
 {
-    const uint64_t n_src = (n_keys / 4) / SRC_WIN;
+    const uint64_t n_src = (n_keys / 4) / SRC_WIN; /* the spec's source proteins */
     const dim3 grid(256 * 32), block(256);
     (void)hipMemsetAsync(n_stored, 0, sizeof(unsigned long long), stream);
     hipLaunchKernelGGL(synth_init_kernel, grid, block, 0, stream, table, num_sigs);
     hipLaunchKernelGGL(synth_insert_kernel, grid, block, 0, stream, table, num_sigs,
-                       mod_magic(num_sigs), n_keys, n_src, n_stored);
-    hipLaunchKernelGGL(synth_payload_kernel, grid, block, 0, stream, table, num_sigs, n_src);
+                       mod_magic(num_sigs), n_entries, n_src, n_stored);
+    if (payload)
+        hipLaunchKernelGGL(synth_payload_kernel, grid, block, 0, stream, table, num_sigs, n_src);
+    return hipGetLastError();
+}
+
+/* After an insert without payload every stored bucket holds its owner (the
+ * lowest entry id with its key) in word 2.  One radix-select pass: a
+ * histogram of owner byte (shift / 8) over the stored buckets whose owner
+ * matches `prefix` under `prefix_mask` -- four passes find the k-th smallest
+ * owner, hence how many entries of the stream hold k distinct keys. */
+__global__ __launch_bounds__(256) void owner_hist_kernel(const kgx_sig_kmer *t, uint64_t n, uint32_t prefix,
+                                                         uint32_t prefix_mask, uint32_t shift,
+                                                         unsigned long long *hist)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(t + i);
+        if (w[0] > MAX_ENCODED)
+            continue;
+        const uint32_t o = (uint32_t)w[2];
+        if ((o & prefix_mask) == prefix)
+            atomicAdd(&h[(o >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x])
+        atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+hipError_t launch_owner_hist(const kgx_sig_kmer *table, uint64_t num_sigs, uint32_t prefix, uint32_t prefix_mask,
+                             uint32_t shift, unsigned long long *hist, hipStream_t stream)
+{
+    (void)hipMemsetAsync(hist, 0, 256 * sizeof(unsigned long long), stream);
+    hipLaunchKernelGGL(owner_hist_kernel, dim3(256 * 16), dim3(256), 0, stream, table, num_sigs, prefix,
+                       prefix_mask, shift, hist);
     return hipGetLastError();
 }
 

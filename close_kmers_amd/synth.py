@@ -85,16 +85,31 @@ def encode_windows(codes: np.ndarray, n_win: int) -> np.ndarray:
 
 
 class ImageSpec:
-    def __init__(self, n_keys: int, num_sigs: int | None = None):
+    """n_keys fixes the generator (its source proteins); the image holds the
+    first n_entries entries of its stream (default n_keys; entries past n_keys
+    are random keys) -- kgx_image_build_synthetic_distinct picks n_entries so
+    that exactly n_distinct keys are stored."""
+
+    def __init__(self, n_keys: int, num_sigs: int | None = None, n_entries: int | None = None):
         self.n_keys = int(n_keys)
+        self.n_entries = int(n_entries) if n_entries is not None else self.n_keys
         self.num_sigs = int(num_sigs) if num_sigs else builder_num_sigs(self.n_keys)
         self.n_src = (self.n_keys // 4) // SRC_WIN
-        if 2 * self.n_keys >= self.num_sigs:
+        if 2 * self.n_entries >= self.num_sigs:
             raise ValueError("more keys than a half-full table allows (kguts.cc:213)")
+
+    def entries_for_distinct(self, n_distinct: int) -> int:
+        """The smallest n such that entries [0, n) hold n_distinct distinct keys."""
+        hi = n_distinct + n_distinct // 8 + 1024
+        keys = self.entries(0, hi)[0]
+        _, first = np.unique(keys, return_index=True)
+        if len(first) < n_distinct:
+            raise ValueError("stream too short")
+        return int(np.sort(first)[n_distinct - 1]) + 1
 
     def entries(self, lo: int = 0, hi: int | None = None):
         """Raw entries [lo, hi) before de-duplication: keys, fI, oI, avg, wt."""
-        hi = self.n_keys if hi is None else hi
+        hi = self.n_entries if hi is None else hi
         e = np.arange(lo, hi, dtype=np.uint64)
         keys = np.zeros(hi - lo, dtype=np.uint64)
         fI = np.zeros(hi - lo, dtype=np.int32)

@@ -196,6 +196,19 @@ int kgx_params_parse(kgx_params *p, const char *const *names, const char *const 
 /* Load <dir>/kmer.table.mem_map into HBM of `device`, validating size,
  * version and entry size exactly as kmer_image.cc:128-147. */
 int kgx_image_open(const char *dir, int device, kgx_image **out);
+/* One replica per entry of devices[0..n) (north_star: the read-only image
+ * replicated per GPU): the file is read ONCE -- each chunk is pread into
+ * pinned host memory and copied up to every device on that device's own
+ * link -- then every replica is packed on its device.  A device may be
+ * listed more than once (independent replicas on one GPU).  out[i] receives
+ * the replica on devices[i]; on failure every out[i] is NULL.  Replaces one
+ * KmerImage per process (threadpool.cc:18-20) when a process drives several
+ * GPUs. */
+int kgx_image_open_replicas(const char *dir, const int *devices, uint32_t n, kgx_image **out);
+/* A replica of src on `device`, copied device to device (hipMemcpyPeer: over
+ * xGMI between two GPUs, a local copy on the same GPU): same resident layout
+ * and presence filter, identical lookups. */
+int kgx_image_replicate(const kgx_image *src, int device, kgx_image **out);
 /* Same, from an in-memory file image (header followed by the table). */
 int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, kgx_image **out);
 /* Synthetic image built in HBM (close_kmers_amd/synth.py documents the
@@ -204,6 +217,12 @@ int kgx_image_from_memory(const void *file_bytes, uint64_t nbytes, int device, k
  * number of distinct keys stored. */
 int kgx_image_build_synthetic(uint64_t n_keys, uint64_t num_sigs, int device, kgx_image **out,
                               uint64_t *n_stored);
+/* The same generator (source proteins of the n_keys spec), its entry stream
+ * extended past n_keys with random keys, cut after the first *n_entries
+ * entries that hold exactly n_distinct distinct keys (the smallest such
+ * count): SURVEY §8(d)'s "1B-entry image" = 1e9 distinct keys stored. */
+int kgx_image_build_synthetic_distinct(uint64_t n_keys, uint64_t n_distinct, uint64_t num_sigs, int device,
+                                       kgx_image **out, uint64_t *n_entries);
 /* An image from caller entries (host arrays, n each), in num_sigs buckets:
  * KmerGuts::insert_kmer semantics (kguts.cc:166-228) -- keys above 20^8
  * are skipped, KGX_EFULL when the valid entries (duplicates included) reach
@@ -294,7 +313,12 @@ int kgx_process_batch(kgx_ctx *ctx, const kgx_params *params, const char *residu
 
 /* Device-buffer batch: same computation on residues / offsets already in HBM
  * (NUL-free sequences), enqueued on the context's stream without host
- * synchronisation.  The results stay in HBM (kgx_device_result). */
+ * synchronisation.  The results stay in HBM (kgx_device_result).
+ * Preconditions (checked on the device): d_seq_offsets[0..n_seq] are
+ * monotone, absolute indices into d_residues, and d_seq_offsets[n_seq] -
+ * d_seq_offsets[0] <= n_residues (the buffers are sized from n_residues).  A
+ * batch that breaks them is processed as empty (no out-of-bounds access);
+ * kgx_ctx_check and kgx_device_batch_collect then return KGX_EINVAL. */
 int kgx_run_device(kgx_ctx *ctx, const kgx_params *params, const uint8_t *d_residues,
                    const uint64_t *d_seq_offsets, uint32_t n_seq, uint64_t n_residues,
                    uint32_t want, kgx_device_result *out);
@@ -304,6 +328,9 @@ int kgx_run_device(kgx_ctx *ctx, const kgx_params *params, const uint8_t *d_resi
  *   kgx_stage_probe  encode + probe: the HBM random-access kernel
  *   kgx_stage_score  hit-run scorer (calls, OTU flags; find_best_call with KGX_WANT_BEST) */
 int kgx_stage_plan(kgx_ctx *ctx, const uint64_t *d_seq_offsets, uint32_t n_seq, uint64_t n_residues);
+/* waits for the context's stream; KGX_EINVAL when its last plan found bad
+ * offsets (see kgx_run_device), else KGX_OK */
+int kgx_ctx_check(kgx_ctx *ctx);
 int kgx_stage_probe(kgx_ctx *ctx, const uint8_t *d_residues, const uint64_t *d_seq_offsets);
 int kgx_stage_score(kgx_ctx *ctx, const kgx_params *params, uint32_t want);
 int kgx_device_result_get(kgx_ctx *ctx, kgx_device_result *out);
@@ -312,6 +339,33 @@ int kgx_device_result_get(kgx_ctx *ctx, kgx_device_result *out);
 int kgx_synth_queries(kgx_ctx *ctx, uint64_t image_n_keys, uint32_t n_seq, uint32_t length,
                       uint32_t x_permille, uint64_t q0, uint8_t *d_residues,
                       uint64_t *d_seq_offsets);
+
+/* ---- pools: one batch split across GPUs --------------------------------
+ * north_star: query batches are split across the GPUs of one node with no
+ * collective (sequences are independent, lookup_request.cc:153; KmerGuts
+ * state is per sequence, kguts.h:263-266).  A pool holds n_ctx contexts,
+ * context i on images[i % n_images] (typically one replica per GPU), each
+ * driven by its own host thread -- the reference's thread pool of KmerGuts
+ * over one image (threadpool.cc:18-44), spread over the node's GPUs. */
+typedef struct kgx_pool kgx_pool;
+int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx, kgx_pool **out);
+int kgx_pool_destroy(kgx_pool *pool);
+uint32_t kgx_pool_size(const kgx_pool *pool);
+/* context i of the pool (owned by the pool; options may be set on it) */
+kgx_ctx *kgx_pool_ctx(kgx_pool *pool, uint32_t i);
+/* kgx_process_batch over the pool: the batch is cut into min(n_ctx, n_seq)
+ * contiguous, residue-balanced shards of whole sequences (kgx_shard_cuts),
+ * shard i runs on context i -- all at once, on every GPU -- and the results
+ * are concatenated in input order: the same CSR, the same bytes (kgx_hit.seq
+ * included) as one context processing the whole batch.  The views are owned
+ * by the pool and valid until its next call. */
+int kgx_pool_process_batch(kgx_pool *pool, const kgx_params *params, const char *residues,
+                           const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out);
+/* cut points of n_shards contiguous residue-balanced shards: shard i is
+ * sequences [cuts[i], cuts[i+1]), cuts[0] = 0, cuts[n_shards] = n_seq; cut i
+ * is the first sequence starting at or after residue (total * i / n_shards)
+ * (close_kmers_amd/shard.py balanced_shards).  Shards may be empty. */
+int kgx_shard_cuts(const uint64_t *seq_offsets, uint32_t n_seq, uint32_t n_shards, uint32_t *cuts);
 
 /* ---- host-side rules on results (run on the CPU, no device needed) ------ */
 /* find_best_call (kguts.cc:1008-1199) over one sequence's calls.  names /

@@ -77,3 +77,34 @@ def test_find_best_call_random_vs_oracle(kgx, oracle_lib):
             np.float32(got[3]) == np.float32(want[3]) and \
             (got[4] is None) == (want[4] is None) and (got[4] is None or np.float32(got[4]) == np.float32(want[4])), \
             (trial, calls, got, want)
+
+
+def test_shard_cuts_match_balanced_shards(kgx):
+    """kgx_shard_cuts (the pool's split, C ABI) == shard.balanced_shards (the
+    bench's split): contiguous, residue-balanced, whole sequences."""
+    from close_kmers_amd import shard
+    rng = np.random.default_rng(11)
+    for trial in range(300):
+        n = int(rng.integers(0, 60))
+        lens = rng.integers(0, 400, n) if trial % 3 else np.full(n, 300)
+        off = np.zeros(n + 1, np.uint64)
+        off[1:] = np.cumsum(lens)
+        off += np.uint64(rng.integers(0, 50))  # absolute offsets need not start at 0
+        for k in (1, 2, 3, 8, 13):
+            cuts = kgx.shard_cuts(off, k)
+            want = shard.balanced_shards(off, k)
+            assert [(int(cuts[i]), int(cuts[i + 1])) for i in range(k)] == want, (trial, k)
+    with pytest.raises(kgx.KgxError):
+        kgx.shard_cuts(np.zeros(1, np.uint64), 0)
+
+
+def test_synthetic_stream_cut_for_distinct_keys():
+    """synth.ImageSpec's n_entries / entries_for_distinct (host side of
+    kgx_image_build_synthetic_distinct): the cut holds exactly the asked
+    number of distinct keys and one entry less holds one key fewer."""
+    from close_kmers_amd import synth
+    spec = synth.ImageSpec(5000, 101533)
+    for nd in (4000, 5000, 6500):
+        m = spec.entries_for_distinct(nd)
+        assert len(synth.ImageSpec(5000, 101533, n_entries=m).unique_entries()[0]) == nd
+        assert len(synth.ImageSpec(5000, 101533, n_entries=m - 1).unique_entries()[0]) == nd - 1

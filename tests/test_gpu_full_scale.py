@@ -57,6 +57,16 @@ def test_c2_full_scale(gpu, oracle_lib):
         hb = ctx.process_batch(res, off, params, want=3)  # host-buffer path
         _same(r1, {"hit_offsets": hb.hit_offsets, "hits": hb.hits, "call_offsets": hb.call_offsets,
                    "calls": hb.calls})
+        # C5's split on one device: the batch as 8 residue-balanced shards on 8
+        # contexts (kgx_pool), concatenated in input order == one pass, byte for byte
+        one = ctx.process_batch(res, off, params, want=15)
+        with gpu.Pool([img], n_ctx=8) as pool:
+            split = pool.process_batch(res, off, params, want=15)
+        for k in ("hit_offsets", "call_offsets", "otu_offsets"):
+            assert np.array_equal(getattr(split, k), getattr(one, k)), k
+        for k in ("hits", "calls", "otus", "best"):
+            assert np.array_equal(getattr(split, k).view(np.uint8), getattr(one, k).view(np.uint8)), k
+        del one, split
         # every 100th sequence against the oracle on a host copy of the image
         table = img.download()
         idx = np.arange(0, n, 100)

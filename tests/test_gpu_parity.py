@@ -449,6 +449,26 @@ def test_image_open_validation(gpu, tmp_path):
     L.kgx_image_close(h)
 
 
+@pytest.mark.parametrize("n_distinct", [39000, 41000])
+def test_device_synthetic_distinct_equals_host_build(gpu, oracle_lib, n_distinct):
+    """kgx_image_build_synthetic_distinct: the spec's stream cut at the
+    smallest entry count holding n_distinct distinct keys (bench.py's 1e9
+    distinct keys at C2), the same buckets as the host build of that cut."""
+    spec = synth.ImageSpec(40000, 101533)
+    m_host = spec.entries_for_distinct(n_distinct)
+    img, m = gpu.Image.synthetic_distinct(spec.n_keys, n_distinct, spec.num_sigs)
+    with img:
+        dev = img.download()
+    assert m == m_host
+    cut = synth.ImageSpec(40000, 101533, n_entries=m)
+    k, f, o, a, w = cut.unique_entries()
+    assert len(k) == n_distinct
+    occ_d = np.sort(dev[dev["which_kmer"] <= 20 ** 8], order="which_kmer")
+    host = oracle_lib.build_table(spec.num_sigs, k, f, o, a, w)
+    occ_h = np.sort(host[host["which_kmer"] <= 20 ** 8], order="which_kmer")
+    assert np.array_equal(occ_d.view(np.uint8), occ_h.view(np.uint8))
+
+
 def test_device_synthetic_image_equals_host_build(gpu, oracle_lib):
     spec = synth.ImageSpec(40000)
     img, stored = gpu.Image.synthetic(spec.n_keys, spec.num_sigs)

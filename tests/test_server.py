@@ -33,16 +33,21 @@ def test_server_usage_and_bad_data_dir():
     assert r.returncode == 1 and b"kmer.table.mem_map" in r.stderr
     r = subprocess.run([exe, "--bogus", "0", "x"], capture_output=True, timeout=60)
     assert r.returncode == 2
+    for bad in ("3-1", "", "a", "0,,1", "-2"):
+        r = subprocess.run([exe, "--devices", bad, "0", "x"], capture_output=True, timeout=60)
+        assert r.returncode == 2 and b"--devices" in r.stderr, bad
 
 
 class Server:
     """A kgx_server on 127.0.0.1 with an ephemeral port."""
 
-    def __init__(self, data_dir, family_db=False, threads=2):
+    def __init__(self, data_dir, family_db=False, threads=2, devices=None):
         self.tmp = tempfile.TemporaryDirectory()
         port_file = os.path.join(self.tmp.name, "port")
         args = [_server_exe(), "--bind", "127.0.0.1", "--listen-port-file", port_file,
                 "--n-kmer-threads", str(threads), "--kmer-version", "kv1"]
+        if devices:
+            args += ["--devices", devices]
         if family_db:
             fq = os.path.join(GOLDEN, "fq")
             args += ["--families-genus-mapping", os.path.join(fq, FQ_FILES["genus"]),
@@ -51,12 +56,14 @@ class Server:
         args += ["0", data_dir]
         if family_db:
             args += ["--families-nr", os.path.join(GOLDEN, "fq", FQ_FILES["nr"])]
-        self.proc = subprocess.Popen(args, stderr=subprocess.PIPE)
+        self.err_path = os.path.join(self.tmp.name, "stderr")
+        self.err = open(self.err_path, "wb")
+        self.proc = subprocess.Popen(args, stderr=self.err)
         deadline = time.time() + 120
         self.port = None
         while time.time() < deadline:
             if self.proc.poll() is not None:
-                raise RuntimeError(self.proc.stderr.read().decode())
+                raise RuntimeError(open(self.err_path, "rb").read().decode())
             try:
                 txt = open(port_file).read().strip()
                 if txt:
@@ -80,11 +87,16 @@ class Server:
                     return out
                 out += chunk
 
+    def log(self) -> bytes:
+        self.err.flush()
+        return open(self.err_path, "rb").read()
+
     def close(self):
         if self.proc.poll() is None:
             r = self.request("GET", "/quit")
             assert b"OK, quitting" in r
             self.proc.wait(timeout=60)
+        self.err.close()
         assert self.proc.returncode == 0
         self.tmp.cleanup()
 
@@ -256,6 +268,10 @@ def test_family_mode_lookup_and_fq_routes_match_golden(gpu):
         assert v.endswith(b"kmer\tkv1\nfamilies\tfv1\nfamily-mode\t1\n")
         assert srv.request("GET", "/genus_lookup/Escherichia").endswith(b"\n\n561\n")
         assert srv.request("GET", "/genus_lookup/no_such_genus").startswith(b"HTTP/1.1 404 Not Found")
+        # lookup_request.cc:74 resolves target_genus with genus_map_[...] (kmer.h:136), which
+        # inserts an unknown genus with an empty id: /genus_lookup finds it afterwards
+        srv.request("POST", "/lookup?target_genus=Nogenus", fasta)
+        assert srv.request("GET", "/genus_lookup/Nogenus").endswith(b"\n\n\n")
         assert srv.request("GET", "/nowhere").startswith(b"HTTP/1.1 404 Not found")
         assert srv.request("POST", "/nowhere", b"x").startswith(b"HTTP/1.1 404 Not found")
         assert srv.request("POST", "/fq_lookup", b"").endswith(b"\n\ndata done\n")
@@ -263,6 +279,91 @@ def test_family_mode_lookup_and_fq_routes_match_golden(gpu):
         srv.close()
     fq = os.path.join(GOLDEN, "fq")
     srv = Server(os.path.join(fq, "data"), family_db=True)
+    try:
+        got = srv.request("POST", "/fq_lookup", open(os.path.join(fq, "input.fasta"), "rb").read())
+        assert got == HEADER + open(os.path.join(fq, "expected_fq_default.txt"), "rb").read()
+    finally:
+        srv.close()
+
+
+def _big_body(seed=99, mib=5):
+    import numpy as np
+    from helpers import random_protein
+    base = open(os.path.join(GOLDEN, "scoring", "input.fasta"), "rb").read()
+    rng = np.random.default_rng(seed)
+    recs, size, i = [base], len(base), 0
+    while size < mib << 20:
+        r = b">p%d\n%s\n" % (i, random_protein(rng, int(rng.integers(5, 600))).encode())
+        recs.append(r)
+        size += len(r)
+        i += 1
+        if i % 50 == 0:
+            recs.append(base)
+            size += len(base)
+    return b"".join(recs)
+
+
+@pytest.mark.gpu
+def test_devices_replicas_serve_every_route(gpu, oracle_lib, tmp_path):
+    """kgx_server --devices: one image replica per listed device (here three
+    replicas on device 0 of a one-GPU box, the same code an 8-GPU node runs),
+    workers spread over them, a large /query cut into pieces that run on
+    several replicas at once, /add + /matrix on the mappings' device, family
+    /lookup and /fq_lookup on any replica: every response is the golden /
+    oracle text."""
+    import threading
+    d = os.path.join(GOLDEN, "scoring")
+    body = _big_body(7, 5)
+    fasta = tmp_path / "big.fasta"
+    fasta.write_bytes(body)
+    want = oracle_lib.query_text(os.path.join(d, "data"), str(fasta), "query", {})
+    srv = Server(os.path.join(d, "data"), threads=5, devices="0,0,0")
+    try:
+        assert b"workers on devices 0 0 0 0 0" in srv.log()
+        outs = [None] * 3
+
+        def run(i):
+            outs[i] = srv.request("POST", "/query", body)
+
+        ths = [threading.Thread(target=run, args=(i,)) for i in range(3)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(o == HEADER + want for o in outs)
+        md = os.path.join(GOLDEN, "matrix")
+        mfasta = open(os.path.join(md, "input.fasta"), "rb").read()
+    finally:
+        srv.close()
+    srv = Server(os.path.join(md, "data"), threads=3, devices="0,0")
+    try:
+        assert srv.request("POST", "/mapping/mx/add?silent=1", mfasta) == HEADER
+        got = srv.request("POST", "/mapping/mx/matrix", mfasta)
+        assert got == HEADER + open(os.path.join(md, "expected_matrix_default.txt"), "rb").read()
+    finally:
+        srv.close()
+    ld = os.path.join(GOLDEN, "lookup")
+    lfasta = open(os.path.join(ld, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(ld, "data"), family_db=True, threads=4, devices="0,0")
+    try:
+        cases = [f for f in _cases("lookup") if parse_case(f)[1].startswith("fam_")]
+        errors = []
+
+        def look(fname):
+            got = srv.request("POST", "/lookup?" + _query_string(parse_case(fname)[1]), lfasta)
+            if got != HEADER + open(os.path.join(ld, fname), "rb").read():
+                errors.append(fname)
+
+        ths = [threading.Thread(target=look, args=(f,)) for f in cases]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert cases and not errors, errors
+    finally:
+        srv.close()
+    fq = os.path.join(GOLDEN, "fq")
+    srv = Server(os.path.join(fq, "data"), family_db=True, threads=2, devices="0,0")
     try:
         got = srv.request("POST", "/fq_lookup", open(os.path.join(fq, "input.fasta"), "rb").read())
         assert got == HEADER + open(os.path.join(fq, "expected_fq_default.txt"), "rb").read()

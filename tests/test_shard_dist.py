@@ -84,3 +84,62 @@ def test_two_rank_gloo_shards_equal_single_rank():
     assert pos == whole.hits["pos"].tolist()
     assert keys == whole.hits["which_kmer"].tolist()
     assert calls == np.diff(whole.call_offsets).tolist()
+
+
+def _strong_worker(rank, world, port, q):
+    """bench.py --strong (C5) on CPU: every rank takes its residue-balanced
+    shard of one global batch of mixed lengths."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import oracle
+    from helpers import synthetic_table
+    d = shard.Dist("gloo")
+    spec, table = synthetic_table(20000)
+    res, off = _mixed_global(spec)
+    lo, hi = shard.balanced_shards(off, d.world)[d.rank]
+    r0, r1 = int(off[lo]), int(off[hi])
+    r = oracle.process_batch(table, res[r0:r1], off[lo:hi + 1] - off[lo])
+    parts = d.gather_objects((lo, hi, r1 - r0, r.hits["pos"].tolist(), r.hits["which_kmer"].tolist(),
+                              np.diff(r.call_offsets).tolist(), r.calls["weighted_hits"].tolist()))
+    if d.rank == 0:
+        q.put(parts)
+    d.close()
+
+
+def _mixed_global(spec):
+    rng = np.random.default_rng(3)
+    res, off = synth.make_queries(spec, 301, x_permille=5, q0=17)
+    lens = rng.integers(0, 300, 301)
+    seqs = [bytes(res[int(off[i]):int(off[i]) + int(lens[i])]) for i in range(301)]
+    o = np.zeros(302, np.uint64)
+    o[1:] = np.cumsum([len(x) for x in seqs])
+    return np.frombuffer(b"".join(seqs), np.uint8).copy(), o
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_split_ranks_concatenate_to_one_pass(world):
+    import torch.multiprocessing as mp
+    import oracle
+    from helpers import synthetic_table
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    spec, table = synthetic_table(20000)
+    res, off = _mixed_global(spec)
+    whole = oracle.process_batch(table, res, off)
+    assert [p[0] for p in parts][0] == 0 and parts[-1][1] == 301
+    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    sizes = [p[2] for p in parts]
+    assert max(sizes) - min(sizes) <= 2 * 300  # residue-balanced
+    assert sum((p[3] for p in parts), []) == whole.hits["pos"].tolist()
+    assert sum((p[4] for p in parts), []) == whole.hits["which_kmer"].tolist()
+    assert sum((p[5] for p in parts), []) == np.diff(whole.call_offsets).tolist()
+    got_w = np.array(sum((p[6] for p in parts), []), np.float32)
+    assert np.array_equal(got_w.view(np.uint32), whole.calls["weighted_hits"].view(np.uint32))
