@@ -11,9 +11,16 @@
  * batch of protein sequences, in (read, frame, position) order -- the order
  * the handler visits them -- with their read index and frame.
  *
- * Launches: count (one wave per read: fragments and residues per frame),
- * scans, emit (the same waves write each fragment's offset, read, frame and
- * first codon, and the residues, at the scanned bases).
+ * Launches: count (one wave per read: fragments and residues of the six
+ * frames; per workgroup of 64 reads their sums), a scan of the sums
+ * (hipcub), emit (the same waves translate again and write each fragment's
+ * offset, read, frame and first codon, and the residues, at the scanned
+ * bases).  The output buffers are sized by the bound of 2 residues per base,
+ * so nothing waits for the host in between.  A single pass -- translate once,
+ * keep the residues in LDS, place each tile by a decoupled look-back over
+ * the earlier tiles' totals -- measured slower (2.8-3.4 ms per 1M reads vs
+ * 1.2 ms): the tiles of a launch finish translating at about the same time
+ * and each then waits on a look-back chain of device-scope flag reads.
  */
 #include <hipcub/hipcub.hpp>
 
@@ -44,7 +51,8 @@ __device__ __forceinline__ uint32_t base_class(uint8_t c)
     }
 }
 
-/* frame f's k-th residue of the read [b, b+len); b may point into LDS */
+/* frame f's k-th residue of the read [b, b+len), from global memory: the
+ * serial path of reads whose frames exceed 64 codons */
 struct FrameReader {
     const uint8_t *b;
     uint64_t len;
@@ -69,90 +77,10 @@ struct FrameReader {
     }
 };
 
-/* the same over a short read staged in LDS as base classes (0-3, 4 = not
- * ACGTU), with the code table in LDS: every codon is LDS reads only */
-struct LdsFrameReader {
-    const uint8_t *cls_b; /* LDS: class of base i */
-    const char *code;     /* LDS copy of kCode11 */
-    uint64_t len;
-    int frame;
-    __device__ uint64_t n_codons() const
-    {
-        const uint64_t off = (uint64_t)(frame < 0 ? -frame : frame) - 1;
-        return len >= off ? (len - off) / 3 : 0;
-    }
-    __device__ uint32_t cls(uint64_t i) const
-    {
-        if (frame > 0)
-            return cls_b[i];
-        const uint32_t c = cls_b[len - 1 - i];
-        return c < 4 ? 3 - c : 4;
-    }
-    __device__ char aa(uint64_t k) const
-    {
-        const uint64_t i = (uint64_t)(frame < 0 ? -frame : frame) - 1 + 3 * k;
-        const uint32_t e1 = cls(i), e2 = cls(i + 1), e3 = cls(i + 2);
-        return code[(e1 | e2 | e3) < 4 ? e1 * 16 + e2 * 4 + e3 : 64];
-    }
-};
-
-/* per-workgroup LDS tables: base -> class, and the code-11 table */
-struct FqTables {
-    uint8_t cls[256];
-    char code[68];
-};
-__device__ __forceinline__ void fq_tables_init(FqTables &t)
-{
-    t.cls[threadIdx.x] = (uint8_t)base_class((uint8_t)threadIdx.x);
-    if (threadIdx.x < 65)
-        t.code[threadIdx.x] = kCode11[threadIdx.x];
-    __syncthreads();
-}
-
 __device__ __forceinline__ int frame_of(uint32_t f) { return f < 3 ? (int)f + 1 : -(int)(f - 2); }
 
-/*
- * One wave per read.  When every frame of the read has at most 64 codons
- * (reads up to 194 bases), lane k holds codon k of the frame: the stop mask
- * is a ballot, each lane finds its run's ends with bit scans, and kept
- * residues / run starts are counted and placed with popcounts, so the
- * residue stores of a frame are one contiguous, coalesced stretch.  Longer
- * reads take the serial path: lanes 0..5 walk one frame each.
- */
-constexpr uint32_t WAVES_PER_WG = 4;
-constexpr uint64_t SHORT_READ = 3 * 64 + 2;
-
-struct FrameFragments { /* one frame's ballot view (lane k = codon k) */
-    uint64_t kept;   /* lanes whose residue is in a fragment */
-    uint64_t starts; /* lanes that start a fragment */
-    char aa;         /* this lane's residue */
-};
-
-template <class Reader> __device__ __forceinline__ FrameFragments frame_fragments(const Reader &fr, uint32_t lane)
-{
-    const uint64_t nc = fr.n_codons();
-    const bool valid = lane < nc;
-    const char aa = valid ? fr.aa(lane) : '*';
-    const uint64_t stop = __ballot(aa == '*') | (nc >= 64 ? 0ull : ~0ull << nc);
-    const uint64_t below = lane ? stop & (~0ull >> (64 - lane)) : 0ull;
-    const uint32_t run_start = below ? 64u - (uint32_t)__builtin_clzll(below) : 0u; /* after the last stop below */
-    const uint64_t at_or_above = stop >> lane;
-    const uint32_t run_end = at_or_above ? lane + (uint32_t)__builtin_ctzll(at_or_above) : 64u; /* next stop */
-    const bool in_kept_run = valid && aa != '*' && run_end - run_start >= MIN_FRAGMENT;
-    FrameFragments r;
-    r.kept = __ballot(in_kept_run);
-    r.starts = __ballot(in_kept_run && lane == run_start);
-    r.aa = aa;
-    return r;
-}
-
-__device__ __forceinline__ uint32_t popc_below(uint64_t m, uint32_t lane)
-{
-    return lane ? (uint32_t)__popcll(m & (~0ull >> (64 - lane))) : 0u;
-}
-
 /* serial walk of one frame: (fragments, residues); emit when out_res != null */
-__device__ void frame_serial(const FrameReader &fr, uint32_t r, uint32_t fi, uint64_t ri, uint32_t &frags,
+__device__ void frame_serial(const FrameReader &fr, uint32_t r, uint64_t fi, uint64_t ri, uint32_t &frags,
                              uint64_t &res, uint8_t *out_res, uint64_t *out_off, uint32_t *out_read,
                              int8_t *out_frame, uint32_t *out_start)
 {
@@ -182,124 +110,356 @@ __device__ void frame_serial(const FrameReader &fr, uint32_t r, uint32_t fi, uin
     }
 }
 
-/* a short read -> this wave's LDS slot as base classes, with one aligned
- * dword load per lane (every dword holds a byte of the read, so none reaches
- * past the read's own aligned words); returns the read's first class in LDS.
- * The frames then take their codons from LDS instead of 18 scattered global
- * byte loads and 6 constant-memory table loads per lane. */
-constexpr uint32_t LDS_READ_WORDS = (SHORT_READ + 3) / 4 + 1;
-__device__ __forceinline__ const uint8_t *stage_read(uint32_t *slot, const uint8_t *b, uint64_t len, uint32_t lane,
-                                                     const uint8_t *cls_tab)
+/*
+ * Short reads (every frame <= 64 codons: up to 194 bases) take the wave path:
+ * one wave per read, lane k = codon k of a frame.
+ *
+ *  - staging: each lane loads one aligned dword of the read (4 bases) and
+ *    turns it into 4 nibbles, bits 0-1 = base class (A0 C1 G2 T/U3, by
+ *    arithmetic on the ASCII code), bit 2 = not in ACGTU; the wave's nibble
+ *    string sits in LDS (16 bits per lane, 8 bases per dword);
+ *  - a codon is 12 bits of that string (one funnel shift of two dwords);
+ *    its table index is a few shifts (the reverse strand complements with
+ *    xor 3 and reverses the three fields), the residue one LDS byte read;
+ *  - a frame's stops are one ballot; the residues kept (runs of >= 11 codons
+ *    between stops, fq_process_request.cc:333) and the fragment starts are
+ *    computed on that wave-uniform mask with scalar shifts and ands; each
+ *    lane places its residue with a masked bit count.
+ */
+constexpr uint32_t WAVES_PER_WG = 4;
+constexpr uint64_t SHORT_READ = 3 * 64 + 2;
+constexpr uint32_t FQ_READS_PER_WAVE = 16;
+constexpr uint32_t FQ_TILE = WAVES_PER_WG * FQ_READS_PER_WAVE; /* reads per workgroup */
+constexpr uint32_t NIB_WORDS = 34; /* 64 lanes x 4 nibbles + a funnel-shift pad (a short read needs <= 26) */
+
+/* 4 bases (the bytes of w) -> 4 nibbles, base j at bits 4j */
+__device__ __forceinline__ uint32_t nibbles4(uint32_t w)
 {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(b), a0 = a & ~(uintptr_t)3;
-    const uint32_t mis = (uint32_t)(a - a0);
+    uint32_t out = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t b = ((w >> (8 * j)) & 0xFFu) | 0x20u;
+        const uint32_t cls = ((b >> 1) ^ (b >> 2)) & 3u;     /* a 0, c 1, g 2, t/u 3 */
+        const uint32_t d = b - 0x60u;                        /* a=1 c=3 g=7 t=20 u=21 */
+        const uint32_t ok = d < 32u ? (0x30008Au >> d) & 1u : 0u;
+        out |= (cls | ((ok ^ 1u) << 2)) << (4 * j);
+    }
+    return out;
+}
+
+/* the read's bytes as the dword this lane stages (0 past the read), and the
+ * nibble position of base 0 (the read's offset in its first dword) */
+__device__ __forceinline__ uint32_t load_read_dword(const uint8_t *b, uint64_t len, uint32_t lane, uint32_t &mis)
+{
+    mis = (uint32_t)(reinterpret_cast<uintptr_t>(b) & 3);
     const uint32_t words = (uint32_t)((mis + len + 3) / 4);
-    __builtin_amdgcn_wave_barrier(); /* the previous read's LDS loads are done (grid-stride loop) */
-    if (lane < words) { /* 4 bases -> 4 class bytes */
-        const uint32_t w = reinterpret_cast<const uint32_t *>(a0)[lane];
-        slot[lane] = (uint32_t)cls_tab[w & 0xFF] | (uint32_t)cls_tab[(w >> 8) & 0xFF] << 8 |
-                     (uint32_t)cls_tab[(w >> 16) & 0xFF] << 16 | (uint32_t)cls_tab[w >> 24] << 24;
+    /* pointer arithmetic, not an integer round trip: the compiler keeps the
+     * global address space (a flat load would also count against the LDS
+     * wait counter and serialise the staging loads behind LDS operations) */
+    return lane < words && len ? reinterpret_cast<const uint32_t *>(b - mis)[lane] : 0u;
+}
+
+/* a wave-uniform value the compiler cannot prove uniform (a shuffle
+ * result), moved to scalar registers: what depends on it -- frame lengths,
+ * stop masks, run masks -- then runs on the scalar unit */
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
+{
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+}
+
+/* the wave's short reads -> their nibble strings in LDS (slot j = read j).
+ * my_off: lane i <= n holds read i's start offset.  Every read's dword load
+ * is issued before the first is converted: a wave keeps 16 loads in flight
+ * instead of waiting out one memory latency per read. */
+__device__ __forceinline__ void stage_wave_reads(uint32_t (*slots)[NIB_WORDS], const uint8_t *bases, uint64_t my_off,
+                                                 uint32_t n, uint32_t lane)
+{
+    uint32_t v[FQ_READS_PER_WAVE];
+#pragma unroll
+    for (uint32_t j = 0; j < FQ_READS_PER_WAVE; j++) {
+        const uint64_t ob = uniform_u64(__shfl(my_off, (int)j)), oe = uniform_u64(__shfl(my_off, (int)j + 1));
+        uint32_t mis;
+        v[j] = j < n && oe - ob <= SHORT_READ ? load_read_dword(bases + ob, oe - ob, lane, mis) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < FQ_READS_PER_WAVE; j++) {
+        uint16_t *s16 = reinterpret_cast<uint16_t *>(slots[j]);
+        s16[lane] = (uint16_t)nibbles4(v[j]);
+        if (lane < 2 * (NIB_WORDS - 32)) /* pad beyond 64 lanes' halves */
+            s16[64 + lane] = 0;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    return reinterpret_cast<const uint8_t *>(slot) + mis;
 }
 
-__device__ __forceinline__ void count_read(const uint8_t *bases, const uint64_t *read_off, uint64_t r, uint32_t lane,
-                                           uint32_t *slot, const FqTables &tabs, uint32_t *n_frag, uint64_t *n_res)
+/* nibble position of a read's base 0 in its staged string */
+__device__ __forceinline__ uint32_t read_mis(const uint8_t *b) { return (uint32_t)(reinterpret_cast<uintptr_t>(b) & 3); }
+
+/* all six frames (f 0-2: +1..+3, 3-5: -1..-3) of a staged short read: this
+ * lane's residue of each ('*' past the frame) and each frame's stop mask
+ * (codons past the frame count as stops).  Straight-line code: the twelve
+ * LDS dword reads of the six codons go out together, then the six table
+ * reads, so a read costs two LDS latencies instead of twelve. */
+__device__ __forceinline__ void translate6(const uint32_t *W, const char *code, uint32_t mis, uint32_t len,
+                                           uint32_t lane, char aa[6], uint64_t stops[6])
 {
-    const uint8_t *b = bases + read_off[r];
-    const uint64_t len = read_off[r + 1] - read_off[r];
-    if (len <= SHORT_READ) {
-        const uint8_t *lb = len ? stage_read(slot, b, len, lane, tabs.cls) : tabs.cls;
-        for (uint32_t f = 0; f < 6; f++) {
-            const FrameFragments ff = frame_fragments(LdsFrameReader{lb, tabs.code, len, frame_of(f)}, lane);
-            if (lane == 0) {
-                n_frag[r * 6 + f] = (uint32_t)__popcll(ff.starts);
-                n_res[r * 6 + f] = (uint64_t)__popcll(ff.kept);
-            }
-        }
-    } else if (lane < 6) {
-        uint32_t frags;
-        uint64_t res;
-        frame_serial(FrameReader{b, len, frame_of(lane)}, (uint32_t)r, 0, 0, frags, res, nullptr, nullptr, nullptr,
-                     nullptr, nullptr);
-        n_frag[r * 6 + lane] = frags;
-        n_res[r * 6 + lane] = res;
+    uint32_t p[6], nc[6], lo[6], hi[6], at[6];
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        const uint32_t off = f < 3 ? f : f - 3;
+        nc[f] = len >= off ? (len - off) / 3 : 0;
+        /* first nibble of the codon's three bases, in ascending base order
+         * (lanes past the frame read base 0: harmless, their residue is '*') */
+        p[f] = mis + (lane < nc[f] ? (f < 3 ? off + 3 * lane : len - 3 - off - 3 * lane) : 0u);
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        lo[f] = W[p[f] >> 3];
+        hi[f] = W[(p[f] >> 3) + 1];
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        const uint32_t x = __builtin_amdgcn_alignbit(hi[f], lo[f], (p[f] & 7u) * 4u);
+        const uint32_t idx = f < 3 ? (((x & 3u) << 4) | ((x >> 2) & 0xCu) | ((x >> 8) & 3u))
+                                   : ((((x >> 4) & 0x30u) | ((x >> 2) & 0xCu) | (x & 3u)) ^ 0x3Fu);
+        at[f] = (x & 0x444u) ? 64u : idx;
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++)
+        aa[f] = code[at[f]];
+    /* lanes past a frame read some codon: the beyond-frame mask covers them
+     * (their residue is never stored, it is not in a kept run) */
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++)
+        stops[f] = __ballot(aa[f] == '*') | (nc[f] >= 64 ? 0ull : ~0ull << nc[f]);
+}
+
+/* codons in runs of >= 11 between stops (S: the wave-uniform stop mask;
+ * bits past 63 are stops), on the mask itself: scalar shifts and ands.
+ * (Per-lane bit scans of S and a ballot moved the work to the vector units
+ * and measured no faster: 511 vs 493 us per 1M reads for the count pass.) */
+__device__ __forceinline__ uint64_t kept_runs(uint64_t S)
+{
+    const uint64_t Z = ~S;
+    const uint64_t a1 = Z & (Z >> 1);                 /* bit p: p..p+1 are codons */
+    const uint64_t a2 = a1 & (a1 >> 2);               /* p..p+3 */
+    const uint64_t a3 = a2 & (a2 >> 4);               /* p..p+7 */
+    const uint64_t w = a3 & (a1 >> 8) & (Z >> 10);    /* p..p+10: a run of 11 starts at p */
+    uint64_t d = w | (w << 1);
+    d |= d << 2;
+    d |= d << 4;                                      /* covered by a window starting p-7..p */
+    return d | (d << 3);                              /* p-10..p */
+}
+
+__device__ __forceinline__ uint32_t popc_below(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v)
+{
+    for (uint32_t o = 32; o; o >>= 1)
+        v += __shfl_xor(v, o);
+    return v;
+}
+
+/* per-workgroup LDS: the code table and the nibble strings of every read */
+struct FqLds {
+    char code[68];
+    uint32_t nib[WAVES_PER_WG][FQ_READS_PER_WAVE][NIB_WORDS];
+};
+
+__device__ __forceinline__ void fq_lds_init(FqLds &t)
+{
+    if (threadIdx.x < 65)
+        t.code[threadIdx.x] = kCode11[threadIdx.x];
+    __syncthreads();
+}
+
+/* one read's fragments and residues (all frames), uniform over the wave */
+__device__ __forceinline__ void count_short(const uint32_t *W, const char *code, uint32_t mis, uint32_t len,
+                                            uint32_t lane, uint32_t &nf, uint32_t &nr)
+{
+    nf = nr = 0;
+    char aa[6];
+    uint64_t stops[6];
+    translate6(W, code, mis, len, lane, aa, stops);
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        const uint64_t kept = kept_runs(stops[f]);
+        nf += (uint32_t)__popcll(kept & ~(kept << 1));
+        nr += (uint32_t)__popcll(kept);
     }
 }
 
+/* 1. per read: fragments and residues; per workgroup: their sums */
 __global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                       uint32_t n_reads, uint32_t *n_frag, uint64_t *n_res)
+                                                       uint32_t n_reads, uint2 *read_counts, ulonglong2 *tile_sum)
 {
-    __shared__ uint32_t lds_read[WAVES_PER_WG][LDS_READ_WORDS];
-    __shared__ FqTables tabs;
-    fq_tables_init(tabs);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES_PER_WG;
-    if (blockIdx.x == 0 && threadIdx.x == 0) { /* the scans' tail */
-        n_frag[(uint64_t)n_reads * 6] = 0;
-        n_res[(uint64_t)n_reads * 6] = 0;
-    }
-    for (uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6); r < n_reads; r += stride)
-        count_read(bases, read_off, r, lane, lds_read[threadIdx.x >> 6], tabs, n_frag, n_res);
-}
-
-__device__ __forceinline__ void emit_read(const uint8_t *bases, const uint64_t *read_off, uint64_t r, uint32_t lane,
-                                          uint32_t *slot, const FqTables &tabs, const uint32_t *frag_base,
-                                          const uint64_t *res_base,
-                                          uint8_t *out_res, uint64_t *out_off, uint32_t *out_read, int8_t *out_frame,
-                                          uint32_t *out_start)
-{
-    const uint8_t *b = bases + read_off[r];
-    const uint64_t len = read_off[r + 1] - read_off[r];
-    if (len <= SHORT_READ) {
-        const uint8_t *lb = len ? stage_read(slot, b, len, lane, tabs.cls) : tabs.cls;
-        for (uint32_t f = 0; f < 6; f++) {
-            const LdsFrameReader fr{lb, tabs.code, len, frame_of(f)};
-            const FrameFragments ff = frame_fragments(fr, lane);
-            const uint64_t g = r * 6 + f;
-            const uint64_t ri = res_base[g] + popc_below(ff.kept, lane);
-            if ((ff.kept >> lane) & 1)
-                out_res[ri] = (uint8_t)ff.aa;
-            if ((ff.starts >> lane) & 1) {
-                const uint64_t fi = frag_base[g] + popc_below(ff.starts, lane);
-                out_off[fi] = ri;
-                out_read[fi] = (uint32_t)r;
-                out_frame[fi] = (int8_t)fr.frame;
-                out_start[fi] = lane;
-            }
+    __shared__ FqLds t;
+    __shared__ uint64_t sums[2][WAVES_PER_WG];
+    fq_lds_init(t);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t r0 = (uint64_t)blockIdx.x * FQ_TILE + w * FQ_READS_PER_WAVE;
+    const uint32_t n = (uint32_t)(r0 < n_reads ? std::min<uint64_t>(FQ_READS_PER_WAVE, n_reads - r0) : 0);
+    const uint64_t my_off = n && lane <= n ? read_off[r0 + lane] : 0;
+    uint64_t wf = 0, wr = 0;
+    stage_wave_reads(t.nib[w], bases, my_off, n, lane);
+    for (uint32_t j = 0; j < n; j++) {
+        const uint64_t ob = uniform_u64(__shfl(my_off, (int)j)), oe = uniform_u64(__shfl(my_off, (int)j + 1));
+        const uint64_t len = oe - ob;
+        uint32_t nf, nr;
+        if (len <= SHORT_READ) {
+            count_short(t.nib[w][j], t.code, read_mis(bases + ob), (uint32_t)len, lane, nf, nr);
+        } else {
+            uint32_t frags = 0;
+            uint64_t res = 0;
+            if (lane < 6)
+                frame_serial(FrameReader{bases + ob, len, frame_of(lane)}, 0, 0, 0, frags, res, nullptr, nullptr,
+                             nullptr, nullptr, nullptr);
+            nf = (uint32_t)wave_sum(lane < 6 ? frags : 0);
+            nr = (uint32_t)wave_sum(lane < 6 ? res : 0);
         }
-    } else if (lane < 6) {
-        const uint64_t g = r * 6 + lane;
-        uint32_t frags;
-        uint64_t res;
-        frame_serial(FrameReader{b, len, frame_of(lane)}, (uint32_t)r, frag_base[g], res_base[g], frags, res, out_res,
-                     out_off, out_read, out_frame, out_start);
+        if (lane == 0)
+            read_counts[r0 + j] = make_uint2(nf, nr);
+        wf += nf;
+        wr += nr;
+    }
+    if (lane == 0) {
+        sums[0][w] = wf;
+        sums[1][w] = wr;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t F = 0, R = 0;
+        for (uint32_t i = 0; i < WAVES_PER_WG; i++) {
+            F += sums[0][i];
+            R += sums[1][i];
+        }
+        tile_sum[blockIdx.x] = make_ulonglong2(F, R);
+        if (blockIdx.x == gridDim.x - 1)
+            tile_sum[gridDim.x] = make_ulonglong2(0, 0); /* the scan's last element = the totals */
     }
 }
 
-/* fragment records (offset, read, frame, first codon) and residues */
-__global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                      uint32_t n_reads, const uint32_t *frag_base,
-                                                      const uint64_t *res_base, uint8_t *out_res, uint64_t *out_off,
-                                                      uint32_t *out_read, int8_t *out_frame, uint32_t *out_start)
+struct PairSum {
+    __host__ __device__ ulonglong2 operator()(const ulonglong2 &a, const ulonglong2 &b) const
+    {
+        return make_ulonglong2(a.x + b.x, a.y + b.y);
+    }
+};
+
+/* 2b. after the exclusive scan of the workgroup sums (hipcub): the batch
+ * totals and the CSR tails */
+__global__ void fq_tail_kernel(const ulonglong2 *tile_base, uint64_t n_tiles, uint32_t n_reads, uint64_t *totals,
+                               uint64_t *out_off, uint32_t *frag_base, uint32_t *n_frag)
 {
-    __shared__ uint32_t lds_read[WAVES_PER_WG][LDS_READ_WORDS];
-    __shared__ FqTables tabs;
-    fq_tables_init(tabs);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES_PER_WG;
-    for (uint64_t r = (uint64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6); r < n_reads; r += stride)
-        emit_read(bases, read_off, r, lane, lds_read[threadIdx.x >> 6], tabs, frag_base, res_base, out_res, out_off,
-                  out_read, out_frame, out_start);
+    const ulonglong2 tot = tile_base[n_tiles];
+    totals[0] = tot.x;
+    totals[1] = tot.y;
+    out_off[tot.x] = tot.y;
+    frag_base[(uint64_t)n_reads * 6] = (uint32_t)tot.x;
+    n_frag[(uint64_t)n_reads * 6] = 0;
 }
 
-__global__ void fq_close_kernel(const uint32_t *frag_base, const uint64_t *res_base, uint64_t n_rf,
-                                uint64_t *out_off)
+/* 3. fragment records (offset, read, frame, first codon), residues and the
+ * per-(read, frame) counts / first fragments, at the scanned bases */
+__global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                      uint32_t n_reads, const uint2 *read_counts,
+                                                      const ulonglong2 *tile_base,
+                                                      uint32_t *n_frag, uint32_t *frag_base, uint8_t *out_res,
+                                                      uint64_t *out_off, uint32_t *out_read, int8_t *out_frame,
+                                                      uint32_t *out_start)
 {
-    out_off[frag_base[n_rf]] = res_base[n_rf];
+    __shared__ FqLds t;
+    fq_lds_init(t);
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * FQ_TILE;
+    /* the tile's reads' counts, lane i = read tile0 + i: exclusive prefix */
+    const uint2 c = lane < FQ_TILE && tile0 + lane < n_reads ? read_counts[tile0 + lane] : make_uint2(0, 0);
+    uint64_t pf = c.x, pr = c.y;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t xf = __shfl_up(pf, o), xr = __shfl_up(pr, o);
+        if (lane >= o) {
+            pf += xf;
+            pr += xr;
+        }
+    }
+    pf -= c.x;
+    pr -= c.y;
+    const uint64_t r0 = tile0 + w * FQ_READS_PER_WAVE;
+    const uint32_t n = (uint32_t)(r0 < n_reads ? std::min<uint64_t>(FQ_READS_PER_WAVE, n_reads - r0) : 0);
+    const ulonglong2 tb = tile_base[blockIdx.x];
+    uint64_t F = tb.x + __shfl(pf, (int)(w * FQ_READS_PER_WAVE));
+    uint64_t R = tb.y + __shfl(pr, (int)(w * FQ_READS_PER_WAVE));
+    const uint64_t my_off = n && lane <= n ? read_off[r0 + lane] : 0;
+    stage_wave_reads(t.nib[w], bases, my_off, n, lane);
+    for (uint32_t j = 0; j < n; j++) {
+        const uint64_t r = r0 + j;
+        const uint64_t ob = uniform_u64(__shfl(my_off, (int)j)), oe = uniform_u64(__shfl(my_off, (int)j + 1));
+        const uint64_t len = oe - ob;
+        uint32_t my_nf = 0;
+        uint64_t my_fb = 0;
+        if (len <= SHORT_READ) {
+            char aas[6];
+            uint64_t stops[6];
+            translate6(t.nib[w][j], t.code, read_mis(bases + ob), (uint32_t)len, lane, aas, stops);
+#pragma unroll
+            for (uint32_t f = 0; f < 6; f++) {
+                const char aa = aas[f];
+                const uint64_t kept = kept_runs(stops[f]);
+                const uint64_t starts = kept & ~(kept << 1);
+                if (lane == f) {
+                    my_nf = (uint32_t)__popcll(starts);
+                    my_fb = F;
+                }
+                const uint64_t ri = R + popc_below(kept);
+                if ((kept >> lane) & 1)
+                    out_res[ri] = (uint8_t)aa;
+                if ((starts >> lane) & 1) {
+                    const uint64_t fi = F + popc_below(starts);
+                    out_off[fi] = ri;
+                    out_read[fi] = (uint32_t)r;
+                    out_frame[fi] = (int8_t)frame_of(f);
+                    out_start[fi] = lane;
+                }
+                F += (uint64_t)__popcll(starts);
+                R += (uint64_t)__popcll(kept);
+            }
+        } else {
+            /* lanes 0-5 = frames: count, place after the earlier frames, emit */
+            uint32_t frags = 0;
+            uint64_t res = 0;
+            const FrameReader fr{bases + ob, len, frame_of(lane < 6 ? lane : 0)};
+            if (lane < 6)
+                frame_serial(fr, 0, 0, 0, frags, res, nullptr, nullptr, nullptr, nullptr, nullptr);
+            uint64_t ef = lane < 6 ? frags : 0, er = lane < 6 ? res : 0;
+            for (uint32_t o = 1; o < 8; o <<= 1) {
+                const uint64_t xf = __shfl_up(ef, o), xr = __shfl_up(er, o);
+                if (lane >= o) {
+                    ef += xf;
+                    er += xr;
+                }
+            }
+            const uint64_t tf = __shfl(ef, 5), tr = __shfl(er, 5);
+            ef -= lane < 6 ? frags : 0;
+            er -= lane < 6 ? res : 0;
+            if (lane < 6) {
+                frame_serial(fr, (uint32_t)r, F + ef, R + er, frags, res, out_res, out_off, out_read, out_frame,
+                             out_start);
+                my_nf = frags;
+                my_fb = F + ef;
+            }
+            F += tf;
+            R += tr;
+        }
+        if (lane < 6) {
+            n_frag[r * 6 + lane] = my_nf;
+            frag_base[r * 6 + lane] = (uint32_t)my_fb;
+        }
+    }
 }
 
 inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
@@ -308,57 +468,61 @@ inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 namespace kgx {
 
-/* fragments of the reads in [d_bases, read_off) into the ctx's fq buffers */
+/* fragments of the reads in [d_bases, read_off) into the ctx's fq buffers.
+ * n_bases: the bytes the reads span (read_off[n] - read_off[0]), which bounds
+ * the output: six frames give at most 2 residues per base, a fragment has at
+ * least 11 residues.  Launches: count -> scan of the workgroup sums (hipcub)
+ * -> emit, with no host round trip between them; one readback of the totals. */
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
-                 kgx_fragments *out)
+                 uint64_t n_bases, kgx_fragments *out)
 {
     hipStream_t st = c->stream;
     const uint64_t n_rf = (uint64_t)n_reads * 6;
+    const uint64_t max_res = 2 * n_bases, max_frag = max_res / MIN_FRAGMENT + 1;
+    const uint64_t n_tiles = ((uint64_t)n_reads + FQ_TILE - 1) / FQ_TILE;
     HIP_TRY(c->fq_nfrag.reserve((n_rf + 1) * 4));
-    HIP_TRY(c->fq_nres.reserve((n_rf + 1) * 8));
     HIP_TRY(c->fq_fbase.reserve((n_rf + 1) * 4));
-    HIP_TRY(c->fq_rbase.reserve((n_rf + 1) * 8));
-    /* one wave per read in a grid-stride loop: workgroups live for many
-     * reads, so the dispatcher is not the limit (a read is ~100 cycles of
-     * work; a launch per read spent longer starting waves than running them) */
-    const dim3 wgs((uint32_t)std::min<uint64_t>((uint64_t)n_reads / WAVES_PER_WG + 1, 256ull * 16));
+    /* per-read counts, the workgroup sums, their scan, the totals, the scan's scratch */
+    const uint64_t rc_bytes = ((uint64_t)n_reads + 1) * sizeof(uint2), ts_bytes = (n_tiles + 1) * sizeof(ulonglong2);
+    size_t scan_bytes = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, scan_bytes, (ulonglong2 *)nullptr, (ulonglong2 *)nullptr,
+                                              PairSum(), make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
+    const uint64_t ws_bytes = rc_bytes + 2 * ts_bytes + 16 + 256 + scan_bytes + 16;
+    HIP_TRY(c->fq_tmp.reserve(ws_bytes));
+    HIP_TRY(c->fq_res.reserve(max_res + 16));
+    HIP_TRY(c->fq_off.reserve((max_frag + 1) * 8));
+    HIP_TRY(c->fq_read.reserve((max_frag + 1) * 4));
+    HIP_TRY(c->fq_frame.reserve(max_frag + 1));
+    HIP_TRY(c->fq_start.reserve((max_frag + 1) * 4));
+    HIP_TRY(c->h_fq_tot.resize(2));
+    char *ws = static_cast<char *>(c->fq_tmp.p);
+    uint2 *read_counts = reinterpret_cast<uint2 *>(ws);
+    ulonglong2 *tile_sum = reinterpret_cast<ulonglong2 *>(ws + ((rc_bytes + 15) & ~15ull));
+    ulonglong2 *tile_base = tile_sum + (n_tiles + 1);
+    uint64_t *totals = reinterpret_cast<uint64_t *>(tile_base + (n_tiles + 1));
+    void *scan_tmp = ws + ((((rc_bytes + 15) & ~15ull) + 2 * ts_bytes + 16 + 255) & ~255ull);
     if (n_reads)
-        hipLaunchKernelGGL(fq_count_kernel, wgs, dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                           c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint64_t>());
-    else {
-        HIP_TRY(hipMemsetAsync(c->fq_nfrag.p, 0, 4, st));
-        HIP_TRY(hipMemsetAsync(c->fq_nres.p, 0, 8, st));
-    }
-    size_t tb1 = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb1, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
-                                             (int)(n_rf + 1), st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, c->fq_nres.as<uint64_t>(), c->fq_rbase.as<uint64_t>(),
-                                             (int)(n_rf + 1), st));
-    HIP_TRY(c->fq_tmp.reserve(std::max(tb1, tb2)));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->fq_tmp.p, tb1, c->fq_nfrag.as<uint32_t>(),
-                                             c->fq_fbase.as<uint32_t>(), (int)(n_rf + 1), st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(c->fq_tmp.p, tb2, c->fq_nres.as<uint64_t>(),
-                                             c->fq_rbase.as<uint64_t>(), (int)(n_rf + 1), st));
-    uint32_t nf = 0;
-    uint64_t nr = 0;
-    HIP_TRY(hipMemcpyAsync(&nf, c->fq_fbase.as<uint32_t>() + n_rf, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&nr, c->fq_rbase.as<uint64_t>() + n_rf, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(c->fq_res.reserve(nr + 16));
-    HIP_TRY(c->fq_off.reserve(((uint64_t)nf + 1) * 8));
-    HIP_TRY(c->fq_read.reserve(((uint64_t)nf + 1) * 4));
-    HIP_TRY(c->fq_frame.reserve((uint64_t)nf + 1));
-    HIP_TRY(c->fq_start.reserve(((uint64_t)nf + 1) * 4));
+        hipLaunchKernelGGL(fq_count_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
+                           read_counts, tile_sum);
+    else
+        HIP_TRY(hipMemsetAsync(tile_sum, 0, sizeof(ulonglong2), st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveScan(scan_tmp, scan_bytes, tile_sum, tile_base, PairSum(),
+                                              make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
+    hipLaunchKernelGGL(fq_tail_kernel, dim3(1), dim3(1), 0, st, tile_base, n_tiles, n_reads, totals,
+                       c->fq_off.as<uint64_t>(), c->fq_fbase.as<uint32_t>(), c->fq_nfrag.as<uint32_t>());
     if (n_reads)
-        hipLaunchKernelGGL(fq_emit_kernel, wgs, dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                           c->fq_fbase.as<uint32_t>(), c->fq_rbase.as<uint64_t>(), c->fq_res.as<uint8_t>(),
-                           c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(),
-                           c->fq_start.as<uint32_t>());
-    hipLaunchKernelGGL(fq_close_kernel, dim3(1), dim3(1), 0, st, c->fq_fbase.as<uint32_t>(),
-                       c->fq_rbase.as<uint64_t>(), n_rf, c->fq_off.as<uint64_t>());
+        hipLaunchKernelGGL(fq_emit_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
+                           read_counts, tile_base, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
+                           c->fq_res.as<uint8_t>(), c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(),
+                           c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>());
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data(), totals, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t nf = c->h_fq_tot[0], nr = c->h_fq_tot[1];
+    if (nf > max_frag || nr > max_res)
+        return fail(KGX_EDEVICE, "fq fragments overflowed their bound");
     out->n_reads = n_reads;
-    out->n_fragments = nf;
+    out->n_fragments = (uint32_t)nf;
     out->n_residues = nr;
     out->residues = c->fq_res.as<uint8_t>();
     out->offsets = c->fq_off.as<uint64_t>();
@@ -524,7 +688,20 @@ int kgx_fq_fragments_device(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *
     if (!c || !out || (n_reads && (!d_bases || !d_read_offsets)))
         return fail(KGX_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(c->img->device));
-    return fq_fragments(c, d_bases, d_read_offsets, n_reads, out);
+    /* the span of the reads bounds the output buffers */
+    uint64_t ends[2] = {0, 0};
+    if (n_reads) {
+        HIP_TRY(c->h_fq_tot.resize(2));
+        HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data(), d_read_offsets, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data() + 1, d_read_offsets + n_reads, 8, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        ends[0] = c->h_fq_tot[0];
+        ends[1] = c->h_fq_tot[1];
+        if (ends[1] < ends[0])
+            return fail(KGX_EINVAL, "read offsets not monotone");
+    }
+    return fq_fragments(c, d_bases, d_read_offsets, n_reads, ends[1] - ends[0], out);
 }
 
 int kgx_fq_called_reads(kgx_ctx *c, const kgx_fragments *fragments, kgx_fq_called *out)
@@ -559,7 +736,7 @@ int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets
         HIP_TRY(hipMemcpyAsync(c->fq_bases.p, c->h_res.data(), nb, hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
-    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, out);
+    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, nb, out);
 }
 
 }  // extern "C"

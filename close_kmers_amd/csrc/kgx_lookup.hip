@@ -170,18 +170,16 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_resid
 /* probe                                                                     */
 /* ------------------------------------------------------------------------ */
 
-/* 12 residue bytes from byte address `a` rounded down to 4; bytes outside
- * [lo, hi) read as 0 (code 20) */
-__device__ __forceinline__ uint3 load_residues(uintptr_t ab, uintptr_t lo, uintptr_t hi)
+/* 12 residue bytes at offset `abo` (a multiple of 4) of the 4-aligned base
+ * residues - bm; bytes outside the batch [bm, bm + n) read as 0 (code 20).
+ * Offsets and pointer arithmetic, not integer addresses, so the loads stay
+ * global loads (a flat load also counts against the LDS wait counter). */
+__device__ __forceinline__ uint3 load_residues(const uint8_t *residues, uint64_t bm, uint64_t n, uint64_t abo)
 {
-    if (ab >= lo && ab + 16 <= hi) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(ab);
-        return make_uint3(v.x, v.y, v.z);
-    }
     uint32_t d[3] = {0, 0, 0};
     for (int b = 0; b < 12; b++)
-        if (ab + b >= lo && ab + b < hi)
-            d[b >> 2] |= (uint32_t)(*reinterpret_cast<const uint8_t *>(ab + b)) << (8 * (b & 3));
+        if (abo + b >= bm && abo + b < bm + n)
+            d[b >> 2] |= (uint32_t)residues[abo + b - bm] << (8 * (b & 3));
     return make_uint3(d[0], d[1], d[2]);
 }
 
@@ -226,10 +224,10 @@ __device__ __forceinline__ void encode_tile(const uint8_t *__restrict__ residues
                                             const uint8_t *code_tab, uint64_t *key, bool *ok,
                                             uint32_t *pos, uint32_t *sq)
 {
-    const uintptr_t arr_lo = reinterpret_cast<uintptr_t>(residues);
-    const uintptr_t arr_hi = arr_lo + n_residues;
+    /* byte offsets from residues - bm, which is 4-aligned */
+    const uint64_t bm = reinterpret_cast<uintptr_t>(residues) & 3;
     uint64_t wb_lo = wbase[s], wb_hi = wbase[s + 1], soff = seq_off[s];
-    uintptr_t ab[J];
+    uint64_t ab[J];
     uint32_t sh[J];
     uint4 v[J];
     bool fast[J];
@@ -251,20 +249,20 @@ __device__ __forceinline__ void encode_tile(const uint8_t *__restrict__ residues
         }
         pos[j] = (uint32_t)(gw - wb_lo);
         sq[j] = s;
-        const uintptr_t a = arr_lo + soff + (gw - wb_lo);
-        ab[j] = a & ~(uintptr_t)3;
+        const uint64_t a = bm + soff + (gw - wb_lo);
+        ab[j] = a & ~3ull;
         sh[j] = (uint32_t)(a - ab[j]);
         ok[j] = act;
-        fast[j] = ab[j] >= arr_lo && ab[j] + 16 <= arr_hi;
+        fast[j] = ab[j] >= bm && ab[j] + 16 <= bm + n_residues;
         if (fast[j])
-            v[j] = *reinterpret_cast<const uint4 *>(ab[j]);
+            v[j] = *reinterpret_cast<const uint4 *>(residues + (ab[j] - bm));
     }
     /* pass 2: codes and keys */
 #pragma unroll
     for (int j = 0; j < J; j++) {
         uint3 d = make_uint3(v[j].x, v[j].y, v[j].z);
         if (!fast[j])
-            d = load_residues(ab[j], arr_lo, arr_hi);
+            d = load_residues(residues, bm, n_residues, ab[j]);
         const uint32_t lo = __builtin_amdgcn_alignbyte(d.y, d.x, sh[j]);
         const uint32_t hi = __builtin_amdgcn_alignbyte(d.z, d.y, sh[j]);
         const uint32_t c0 = code_tab[lo & 0xFF], c1 = code_tab[(lo >> 8) & 0xFF],

@@ -144,7 +144,7 @@ inline void parallel_memcpy(void *dst, const void *src, size_t n)
 }
 
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
-                 kgx_fragments *out);
+                 uint64_t n_bases, kgx_fragments *out);
 
 }  // namespace kgx
 
@@ -197,8 +197,8 @@ struct kgx_ctx {
     kgx::DevBuf best, best_ws, bc_calls, bc_start, bc_count; /* KGX_WANT_BEST / kgx_find_best_calls */
     kgx::PinnedVec<kgx_best_call> h_best;
     /* fq fragments (kgx_fq.hip) */
-    kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_nres, fq_fbase, fq_rbase, fq_tmp, fq_res, fq_off, fq_read,
-        fq_frame, fq_start;
+    kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start;
+    kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
     /* kgx_fq_called_reads */
     kgx::DevBuf fqc_flag, fqc_reads, fqc_nsel, fqc_nfrag, fqc_ncall, fqc_fo, fqc_co, fqc_fc, fqc_len, fqc_coff,
         fqc_calls;

@@ -59,7 +59,8 @@ def main():
             calib[name] = {"fetch_bytes_per_read": b / reads, "dispatches": n}
     cfg = bench["config"]
     out = {
-        "n_keys": cfg["n_keys"], "n_seq": cfg["n_seq_per_gpu"], "length": cfg["seq_len"],
+        "n_keys": cfg["n_keys"], "keys_stored": cfg.get("keys_stored"), "n_seq": cfg["n_seq_per_gpu"],
+        "length": cfg["seq_len"],
         "image_layout": (bench.get("roofline") or {}).get("image_layout", "AOS24"),
         "fetch_bytes_per_launch": pf, "write_bytes_per_launch": pw,
         "hbm_bytes_per_launch": (pf or 0) + (pw or 0) if pf is not None else None,
