@@ -12,6 +12,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -48,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> None:
     deps = [os.path.join(CSRC, f) for f in LIB_SOURCES + HEADERS] + [os.path.join(INCLUDE, "kgx.h"),
                                                                      __file__]
     if force or _newer(LIB, deps):
-        objs = []
+        objs, cmds = [], []
         for src in LIB_SOURCES:
             obj = os.path.join(CSRC, "_obj", src + ".o")
             os.makedirs(os.path.dirname(obj), exist_ok=True)
@@ -57,10 +58,14 @@ def build(force: bool = False, verbose: bool = False) -> None:
             obj_deps = [os.path.join(CSRC, src)] + [d for d in deps if not d.endswith((".hip", ".cpp"))]
             if not force and not _newer(obj, obj_deps):
                 continue
-            cmd = [HIPCC] + COMMON + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
-            if verbose:
+            cmds.append([HIPCC] + COMMON + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj])
+        if verbose:
+            for cmd in cmds:
                 print(" ".join(cmd))
-            _run(cmd)
+        # objects compile independently: one hipcc per source, a few at a time
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or min(8, os.cpu_count() or 1)))
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_run, cmds))
         tmp = LIB + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
         os.replace(tmp, LIB)

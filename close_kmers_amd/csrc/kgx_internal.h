@@ -170,7 +170,9 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          const kgx_call *calls, const uint64_t *hit_dense_off,
                          const uint64_t *call_dense_off, kgx_hit *hits_out, kgx_call *calls_out,
                          uint32_t seq_base, uint32_t hit_format, const uint32_t *otu_count, const kgx_otu *otus,
-                         const uint64_t *otu_dense_off, kgx_otu *otus_out, hipStream_t stream);
+                         const uint64_t *otu_dense_off, kgx_otu *otus_out, hipStream_t stream,
+                         uint4 *hits16_out = nullptr, /* PACKED16: the 16-B records, dense, instead of kgx_hit */
+                         uint32_t *hits12_out = nullptr); /* PACKED16: 12-B records without the key */
 /* per-sequence OTU tallies in otus_by_count order at otus[window_base[s]] */
 hipError_t launch_otus(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
                        const uint4 *hot, const uint4 *cold, int32_t *ws, kgx_otu *otus, uint32_t *otu_count,
@@ -178,6 +180,15 @@ hipError_t launch_otus(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hi
 /* find_best_call per sequence: calls[start[s] ..+ count[s]), ws same extent */
 hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64_t *start, const uint32_t *count,
                              kgx_call *ws, kgx_best_call *out, hipStream_t stream);
+/* dense CSR offsets (n + 1 each) of up to three per-sequence count arrays
+ * (NULL count array: all-zero offsets) */
+size_t count_scan_workspace_bytes(uint32_t n);
+hipError_t launch_count_scan(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
+                             uint64_t *o1, uint64_t *o2, void *workspace, hipStream_t stream);
+/* min(*count, cap) elements of elem_bytes (a multiple of 4) from src to dst,
+ * both 16-byte aligned */
+hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count, uint64_t cap,
+                               uint32_t elem_bytes, int blocks, hipStream_t stream);
 /* device stores of bytes (4-aligned) from HBM into mapped pinned host memory */
 hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,

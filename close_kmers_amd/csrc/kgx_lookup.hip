@@ -1067,14 +1067,15 @@ __global__ __launch_bounds__(256) void gather_kernel(
     const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
     const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
     uint32_t seq_base, const uint32_t *__restrict__ otu_count, const kgx_otu *__restrict__ otus,
-    const uint64_t *__restrict__ ooff, kgx_otu *__restrict__ otus_out)
+    const uint64_t *__restrict__ ooff, kgx_otu *__restrict__ otus_out, uint4 *__restrict__ hits16_out,
+    uint32_t *__restrict__ hits12_out)
 {
     const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= n_seq)
         return;
     const uint32_t lane = lane_id();
     const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
-    if (hits_out && gw0 < gw1) {
+    if ((hits_out || (PK && (hits16_out || hits12_out))) && gw0 < gw1) {
         const uint32_t J = tile_windows / 64;
         const uint64_t gfirst = gw0 >> 6, glast = (gw1 - 1) >> 6;
         uint64_t done = 0; /* hits of s written so far */
@@ -1103,6 +1104,23 @@ __global__ __launch_bounds__(256) void gather_kernel(
                     incl += x;
             }
             const uint64_t dst0 = hoff[s] + done + (incl - cnt);
+            if (PK && hits16_out) { /* the records as stored: position = mask bit */
+                for (uint32_t i = 0; i < cnt; i++)
+                    hits16_out[dst0 + i] = hot[at + i];
+                done += __shfl(incl, 63);
+                continue;
+            }
+            if (PK && hits12_out) { /* the records less the key (the host re-encodes it) */
+                for (uint32_t i = 0; i < cnt; i++) {
+                    const uint4 h = hot[at + i];
+                    uint32_t *d = hits12_out + 3 * (dst0 + i);
+                    d[0] = h.z;      /* function_wt bits */
+                    d[1] = h.w;      /* avg_from_end | (otu+1) high 12 << 16 | flags << 28 */
+                    d[2] = h.y >> 3; /* (fI+1) | (otu+1) low 9 << 20: packed lo >> 35 */
+                }
+                done += __shfl(incl, 63);
+                continue;
+            }
             uint4 *dst = reinterpret_cast<uint4 *>(hits_out + dst0);
             const uint32_t pbase = (uint32_t)(64 * g - gw0);
             for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its record(s) */
@@ -1144,18 +1162,142 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
                          const kgx_call *calls, const uint64_t *hoff, const uint64_t *coff,
                          kgx_hit *hits_out, kgx_call *calls_out, uint32_t seq_base, uint32_t hit_format,
                          const uint32_t *otu_count, const kgx_otu *otus, const uint64_t *ooff, kgx_otu *otus_out,
-                         hipStream_t stream)
+                         hipStream_t stream, uint4 *hits16_out, uint32_t *hits12_out)
 {
     if (n_seq == 0)
         return hipSuccess;
     if (hit_format == HIT_PACKED16)
         hipLaunchKernelGGL(gather_kernel<true>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                            hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                           calls_out, seq_base, otu_count, otus, ooff, otus_out);
+                           calls_out, seq_base, otu_count, otus, ooff, otus_out, hits16_out, hits12_out);
     else
         hipLaunchKernelGGL(gather_kernel<false>, dim3((n_seq + 3) / 4), dim3(256), 0, stream, n_seq, wbase,
                            hit_mask, tile_windows, call_count, hot, cold, calls, hoff, coff, hits_out,
-                           calls_out, seq_base, otu_count, otus, ooff, otus_out);
+                           calls_out, seq_base, otu_count, otus, ooff, otus_out, hits16_out, hits12_out);
+    return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* count scan: a chunk's dense CSR offsets from its per-sequence counts, on  */
+/* the device (the streamed host path needs no host round trip between the  */
+/* scorer and the gather): off[a][i] = sum_{j<i} count[a][j], i in [0, n]   */
+/* ------------------------------------------------------------------------ */
+
+constexpr uint32_t CS_PER = 4, CS_TILE = 256 * CS_PER;
+
+struct Counts3 {
+    const uint32_t *c[3]; /* NULL: an all-zero array */
+};
+struct Offsets3 {
+    uint64_t *o[3];
+};
+
+__device__ __forceinline__ uint64_t thread_count(const uint32_t *c, uint32_t n, uint32_t i0)
+{
+    uint64_t v = 0;
+    if (c)
+        for (uint32_t k = 0; k < CS_PER; k++)
+            if (i0 + k < n)
+                v += c[i0 + k];
+    return v;
+}
+
+__global__ __launch_bounds__(256) void count_reduce_kernel(Counts3 cnt, uint32_t n, uint64_t *__restrict__ sums)
+{
+    __shared__ uint64_t lds4[3][4];
+    const uint32_t i0 = blockIdx.x * CS_TILE + threadIdx.x * CS_PER;
+    for (int a = 0; a < 3; a++) {
+        uint64_t total;
+        block_scan(thread_count(cnt.c[a], n, i0), lds4[a], total);
+        if (threadIdx.x == 0)
+            sums[3 * (uint64_t)blockIdx.x + a] = total;
+    }
+}
+
+/* exclusive scan of the 3 x groups workgroup sums in place, one workgroup */
+__global__ __launch_bounds__(256) void count_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups)
+{
+    __shared__ uint64_t lds4[3][4];
+    uint64_t carry[3] = {0, 0, 0};
+    for (uint32_t base = 0; base < groups; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        for (int a = 0; a < 3; a++) {
+            const uint64_t v = i < groups ? sums[3 * (uint64_t)i + a] : 0;
+            uint64_t tot;
+            const uint64_t incl = block_scan(v, lds4[a], tot);
+            if (i < groups)
+                sums[3 * (uint64_t)i + a] = carry[a] + incl - v;
+            carry[a] += tot;
+        }
+        __syncthreads(); /* lds4 is rewritten by the next round */
+    }
+}
+
+__global__ __launch_bounds__(256) void count_scan_kernel(Counts3 cnt, uint32_t n, const uint64_t *__restrict__ sums,
+                                                         Offsets3 off)
+{
+    __shared__ uint64_t lds4[3][4];
+    const uint32_t i0 = blockIdx.x * CS_TILE + threadIdx.x * CS_PER;
+    for (int a = 0; a < 3; a++) {
+        uint64_t tot;
+        const uint64_t mine = thread_count(cnt.c[a], n, i0);
+        uint64_t at = sums[3 * (uint64_t)blockIdx.x + a] + block_scan(mine, lds4[a], tot) - mine;
+        /* entries [i0, i0 + CS_PER) of the n + 1 offsets */
+        for (uint32_t k = 0; k < CS_PER && i0 + k <= n; k++) {
+            off.o[a][i0 + k] = at;
+            if (cnt.c[a] && i0 + k < n)
+                at += cnt.c[a][i0 + k];
+        }
+    }
+}
+
+size_t count_scan_workspace_bytes(uint32_t n)
+{
+    return (size_t)3 * ((n + 1 + CS_TILE - 1) / CS_TILE) * sizeof(uint64_t);
+}
+
+hipError_t launch_count_scan(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
+                             uint64_t *o1, uint64_t *o2, void *workspace, hipStream_t stream)
+{
+    const uint32_t groups = (n + 1 + CS_TILE - 1) / CS_TILE; /* n + 1 offsets */
+    Counts3 cnt = {{c0, c1, c2}};
+    Offsets3 off = {{o0, o1, o2}};
+    uint64_t *sums = static_cast<uint64_t *>(workspace);
+    hipLaunchKernelGGL(count_reduce_kernel, dim3(groups), dim3(256), 0, stream, cnt, n, sums);
+    hipLaunchKernelGGL(count_sums_scan_kernel, dim3(1), dim3(256), 0, stream, sums, groups);
+    hipLaunchKernelGGL(count_scan_kernel, dim3(groups), dim3(256), 0, stream, cnt, n,
+                       static_cast<const uint64_t *>(sums), off);
+    return hipGetLastError();
+}
+
+/* min(*count, cap) elements of elem_bytes each, src -> dst: the size comes
+ * from the device (a chunk's scanned total), the room from the host.  The
+ * bytes move as 16-B stores (one 1-KB run per wave instruction over PCIe),
+ * the last < 16 as 4-B stores; both ends 16-B aligned. */
+__global__ __launch_bounds__(256) void copy_counted_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src,
+                                                           const uint64_t *__restrict__ count, uint64_t cap,
+                                                           uint32_t elem_bytes)
+{
+    const uint64_t bytes = (*count < cap ? *count : cap) * elem_bytes;
+    const uint64_t n16 = bytes / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < n16; i += stride)
+        dst[i] = src[i];
+    const uint32_t tail = (uint32_t)(bytes - 16 * n16) / 4; /* elem_bytes is a multiple of 4 */
+    if (tid < tail)
+        reinterpret_cast<uint32_t *>(dst + n16)[tid] = reinterpret_cast<const uint32_t *>(src + n16)[tid];
+}
+
+hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count, uint64_t cap,
+                               uint32_t elem_bytes, int blocks, hipStream_t stream)
+{
+    if (cap == 0)
+        return hipSuccess;
+    if (elem_bytes % 4 != 0 || (uintptr_t)dst % 16 != 0 || (uintptr_t)src % 16 != 0)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_counted_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
+                       static_cast<const uint4 *>(src), count, cap, elem_bytes);
     return hipGetLastError();
 }
 

@@ -9,7 +9,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -143,6 +147,84 @@ inline void parallel_memcpy(void *dst, const void *src, size_t n)
         th.join();
 }
 
+/* A few persistent host threads for work that overlaps device streams (the
+ * compact host path's hit expansion).  submit() queues a task; wait() blocks
+ * until every queued task has finished and returns the first nonzero code a
+ * task returned (then clears it). */
+class HostPool {
+  public:
+    explicit HostPool(unsigned n)
+    {
+        for (unsigned i = 0; i < n; i++)
+            th_.emplace_back([this] { run(); });
+    }
+    HostPool(const HostPool &) = delete;
+    HostPool &operator=(const HostPool &) = delete;
+    ~HostPool()
+    {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_)
+            t.join();
+    }
+    unsigned size() const { return (unsigned)th_.size(); }
+    void submit(std::function<int()> f)
+    {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            q_.push_back(std::move(f));
+            pending_++;
+        }
+        cv_.notify_one();
+    }
+    int wait()
+    {
+        std::unique_lock<std::mutex> l(mu_);
+        idle_.wait(l, [this] { return pending_ == 0; });
+        const int rc = rc_;
+        rc_ = 0;
+        if (rc)
+            fail(rc, msg_); /* the task's error text on the waiting thread */
+        return rc;
+    }
+
+  private:
+    void run()
+    {
+        for (;;) {
+            std::function<int()> f;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty())
+                    return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            const int rc = f();
+            const char *why = rc ? kgx_last_error() : nullptr; /* the failing thread's text */
+            std::lock_guard<std::mutex> l(mu_);
+            if (rc && !rc_) {
+                rc_ = rc;
+                msg_ = why ? why : "";
+            }
+            if (--pending_ == 0)
+                idle_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::deque<std::function<int()>> q_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_;
+    size_t pending_ = 0;
+    int rc_ = 0;
+    std::string msg_;
+    bool stop_ = false;
+};
+
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
                  uint64_t n_bases, kgx_fragments *out);
 
@@ -226,11 +308,46 @@ struct kgx_ctx {
     /* host-buffer batches in chunks (option "host_chunks"): chunks alternate
      * between this context and a twin over the same image, so one chunk's
      * gather + D2H overlaps the next chunk's H2D + kernels */
-    int host_chunks = 3;
+    int host_chunks = 6;
     int host_copy = 1; /* chunk D2H: 0 = DMA (hipMemcpyAsync), 1 = device stores into mapped memory */
     int host_copy_blocks = 64; /* workgroups of the store copy (option "host_copy_blocks") */
     kgx_ctx *twin = nullptr;
     kgx::PinnedVec<uint64_t> h_off_stage, h_dense_hoff, h_dense_coff, h_dense_ooff, h_nwin;
+    /* compact chunk D2H (option "host_hits16", PACKED16 images): a chunk's
+     * hits cross PCIe as their 16-byte table records plus the chunk's hit
+     * mask, and host threads expand them into kgx_hit (position = mask bit)
+     * while the next chunk streams */
+    int host_hits16 = 1;
+    int host_threads = 12; /* expansion threads (option "host_threads") */
+    std::unique_ptr<kgx::HostPool> pool;
+    /* chunk staging (pageable caller buffer -> pinned) in parts on
+     * stage_threads threads (option "stage_threads", 1 = the calling thread) */
+    int stage_threads = 4;
+    std::unique_ptr<kgx::HostPool> stage_pool;
+    kgx::PinnedVec<uint4> h_hits16;
+    kgx::PinnedVec<uint64_t> h_mask;
+    std::vector<uint64_t> h_wstart;     /* chunk-relative first window of each sequence */
+    std::vector<hipEvent_t> chunk_done; /* per chunk: its records and mask are on the host */
+    std::vector<hipEvent_t> chunk_counts; /* per chunk: its counts are on the host */
+    std::vector<hipEvent_t> chunk_gathered; /* per chunk: its dense buffers are complete */
+    hipStream_t copy_stream = nullptr; /* bulk chunk D2H, apart from the contexts' kernels */
+    kgx::DevBuf dense_mask, dense_best; /* a chunk's mask / best calls for its bulk copy */
+    /* streamed schedule (option "host_stream", compact records only): device
+     * CSR offsets, bulk copies sized on the device into host regions sized
+     * from the rates below (records per window seen so far, x 1.25) */
+    int host_stream_chunks = 1;
+    int host_taper = 1; /* first and last chunk half-size (option "host_taper") */
+    double rate_hits = 0.35, rate_calls = 0.05, rate_otus = 0.05;
+    uint64_t stream_fallbacks = 0; /* batches rerun exact after a region overflowed */
+    std::vector<hipEvent_t> chunk_h2d; /* per chunk: its staged residues are on the device */
+    kgx::DevBuf dense_counts, cscan_ws;
+    kgx::PinnedVec<uint32_t> h_counts;
+    kgx::PinnedVec<uint32_t> h_hits12; /* 12-B records (3 words per hit, no key) */
+    int host_rec12 = 1; /* streamed: 12-B records, key re-encoded on the host (option "host_rec12") */
+    int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
+    kgx::PinnedVec<kgx_call> h_calls_region;
+    kgx::PinnedVec<kgx_otu> h_otus_region;
+    int counts_first = 1; /* chunk k's bulk D2H waits for chunk k+1's counts (option "counts_first") */
 };
 
 #endif

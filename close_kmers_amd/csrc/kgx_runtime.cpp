@@ -824,6 +824,20 @@ int kgx_ctx_destroy(kgx_ctx *c)
             c->img->last_probe = nullptr;
     }
     (void)hipEventDestroy(c->probe_done);
+    c->pool.reset();
+    c->stage_pool.reset();
+    for (hipEvent_t e : c->chunk_done)
+        (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->chunk_counts)
+        (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->chunk_gathered)
+        (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->chunk_h2d)
+        (void)hipEventDestroy(e);
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+    }
     if (c->own_stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -899,6 +913,54 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "host_copy must be 0 or 1");
         c->host_copy = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_hits16") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_hits16 must be 0 or 1");
+        c->host_hits16 = (int)value;
+        return KGX_OK;
+    }
+    if (n == "stage_threads") {
+        if (value < 1 || value > 64)
+            return fail(KGX_EINVAL, "stage_threads must be 1..64");
+        c->stage_threads = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_rec12") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_rec12 must be 0 or 1");
+        c->host_rec12 = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_nt") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_nt must be 0 or 1");
+        c->host_nt = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_taper") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_taper must be 0 or 1");
+        c->host_taper = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_stream") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_stream must be 0 or 1");
+        c->host_stream_chunks = (int)value;
+        return KGX_OK;
+    }
+    if (n == "counts_first") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "counts_first must be 0 or 1");
+        c->counts_first = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_threads") {
+        if (value < 1 || value > 64)
+            return fail(KGX_EINVAL, "host_threads must be 1..64");
+        c->host_threads = (int)value;
         return KGX_OK;
     }
     if (n == "host_chunks") {
@@ -1134,17 +1196,38 @@ void cut_at_nul(char *b, uint64_t len)
     }
 }
 
-/* sequences [s0, s1) of a host batch -> x's pinned staging (host work only) */
-int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1)
+/* sequences [s0, s1) of a host batch -> x's pinned staging (host work only;
+ * large ranges copied and NUL-scanned in parts on the stage pool sp) */
+int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1,
+                    HostPool *sp = nullptr)
 {
     const uint32_t n = s1 - s0;
     const uint64_t r0 = n ? seq_offsets[s0] : 0;
     const uint64_t n_res = n ? seq_offsets[s1] - r0 : 0;
     HIP_TRY(x->h_res.resize(n_res));
-    if (n_res)
+    bool has_nul = false;
+    if (sp && n_res >= (1u << 20)) {
+        const unsigned P = sp->size();
+        std::atomic<bool> nul{false};
+        char *dst = x->h_res.data();
+        const char *src = residues + r0;
+        for (unsigned p = 0; p < P; p++) {
+            const uint64_t a = n_res * p / P, b = n_res * (p + 1) / P;
+            sp->submit([dst, src, a, b, &nul]() -> int {
+                std::memcpy(dst + a, src + a, b - a);
+                if (std::memchr(dst + a, 0, b - a))
+                    nul.store(true, std::memory_order_relaxed);
+                return KGX_OK;
+            });
+        }
+        (void)sp->wait();
+        has_nul = nul.load();
+    } else if (n_res) {
         std::memcpy(x->h_res.data(), residues + r0, n_res);
-    /* one scan of the whole range first: NUL bytes are rare */
-    if (n_res && std::memchr(x->h_res.data(), 0, n_res))
+        /* one scan of the whole range first: NUL bytes are rare */
+        has_nul = std::memchr(x->h_res.data(), 0, n_res) != nullptr;
+    }
+    if (has_nul)
         for (uint32_t s = s0; s < s1; s++)
             cut_at_nul(x->h_res.data() + (seq_offsets[s] - r0), seq_offsets[s + 1] - seq_offsets[s]);
     HIP_TRY(x->h_off_stage.resize(n + 1));
@@ -1173,7 +1256,7 @@ int stage_host_seqs(kgx_ctx *x, const char *residues, const uint64_t *seq_offset
 }
 
 /* one staged chunk on x: H2D, plan/probe/score, counts + window total -> host */
-int enqueue_chunk(kgx_ctx *x, const kgx_params *params, uint32_t want)
+int enqueue_chunk(kgx_ctx *x, const kgx_params *params, uint32_t want, hipEvent_t counts_done)
 {
     int rc = stage_upload(x);
     if (rc)
@@ -1198,6 +1281,7 @@ int enqueue_chunk(kgx_ctx *x, const kgx_params *params, uint32_t want)
     }
     HIP_TRY(hipMemcpyAsync(x->h_nwin.data(), x->wbase.as<uint64_t>() + n, sizeof(uint64_t),
                            hipMemcpyDeviceToHost, x->stream));
+    HIP_TRY(hipEventRecord(counts_done, x->stream));
     return KGX_OK;
 }
 
@@ -1212,6 +1296,409 @@ void fill_result(kgx_ctx *c, uint32_t n_seq, bool need_hits, bool want_best, uin
     out->otu_offsets = c->h_ooff.data();
     out->otus = c->h_otus.data();
     out->n_windows = nwin;
+}
+
+/* residue byte -> code, to_amino_acid_off (kguts.cc:273-339): the 20
+ * standard upper-case residues in alphabetical order, anything else 20 */
+struct ResidueCodes {
+    uint8_t code[256];
+    ResidueCodes()
+    {
+        std::memset(code, 20, sizeof(code));
+        const char *aa = "ACDEFGHIKLMNPQRSTVWY";
+        for (int i = 0; i < 20; i++)
+            code[(uint8_t)aa[i]] = (uint8_t)i;
+    }
+};
+const ResidueCodes kResidueCodes;
+
+/* the 8-mer key of the window at p (encoded_kmer, kguts.cc:438-455) */
+inline uint64_t window_key(const uint8_t *p)
+{
+    const uint8_t *t = kResidueCodes.code;
+    const uint32_t ka = ((t[p[0]] * 20u + t[p[1]]) * 20u + t[p[2]]) * 20u + t[p[3]];
+    const uint32_t kb = ((t[p[4]] * 20u + t[p[5]]) * 20u + t[p[6]]) * 20u + t[p[7]];
+    return (uint64_t)ka * 160000u + kb;
+}
+
+/* Sequences [a, b) of a compact chunk: table records (dense, CSR order) +
+ * the chunk's hit mask -> kgx_hit, position = the hit's mask bit minus the
+ * sequence's first window (what gather_kernel computes on the device).
+ * R12: 12-byte records without the key (gather_kernel's hits12 form), the key
+ * re-encoded from the window's residues; else the 16-byte table records. */
+int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_offsets, uint32_t a, uint32_t b,
+                uint64_t mbase, int64_t rec_delta)
+{
+    const uint4 *rec16 = R12 ? nullptr : c->h_hits16.data() + rec_delta; /* record of output hit j */
+    const uint32_t *rec12 = R12 ? c->h_hits12.data() + 3 * rec_delta : nullptr;
+    const uint64_t *mask = c->h_mask.data() + mbase;
+    kgx_hit *out = c->h_hits.data();
+    const bool nt = c->host_nt != 0;
+    for (uint32_t s = a; s < b; s++) {
+        uint64_t j = c->h_hoff[s];
+        const uint64_t j1 = c->h_hoff[s + 1];
+        if (j == j1)
+            continue;
+        const uint64_t w0 = c->h_wstart[s], w1 = w0 + windows_of(seq_offsets[s + 1] - seq_offsets[s]);
+        const uint8_t *seq = reinterpret_cast<const uint8_t *>(residues + seq_offsets[s]);
+        for (uint64_t g = w0 >> 6; g <= (w1 - 1) >> 6; g++) {
+            uint64_t bits = mask[g];
+            if (g == w0 >> 6)
+                bits &= ~0ull << (w0 & 63);
+            if (g == (w1 - 1) >> 6 && (w1 & 63))
+                bits &= ~(~0ull << (w1 & 63));
+            if (j + (uint64_t)__builtin_popcountll(bits) > j1)
+                return fail(KGX_EDEVICE, "compact hits: more mask bits than hits for sequence " + std::to_string(s));
+            for (; bits; bits &= bits - 1, j++) {
+                const uint32_t pos = (uint32_t)(64 * g + (uint64_t)__builtin_ctzll(bits) - w0);
+                packed_bucket pb;
+                uint32_t flags;
+                if (R12) {
+                    const uint32_t *r = rec12 + 3 * j;
+                    pb.lo = window_key(seq + pos) | (uint64_t)r[2] << 35;
+                    pb.hi = (uint64_t)r[1] << 32 | r[0];
+                    flags = (r[1] >> 28) & 7u;
+                } else {
+                    const uint4 h = rec16[j];
+                    pb.lo = (uint64_t)h.y << 32 | h.x;
+                    pb.hi = (uint64_t)h.w << 32 | h.z;
+                    flags = (h.w >> 28) & 7u;
+                }
+                const kgx_sig_kmer e = unpack_bucket(pb);
+                kgx_hit o;
+                o.which_kmer = e.which_kmer;
+                o.otu_index = e.otu_index;
+                o.avg_from_end = e.avg_from_end;
+                o.flags = (uint16_t)flags;
+                o.function_index = e.function_index;
+                o.function_wt = e.function_wt;
+                o.pos = pos;
+                o.seq = s;
+                if (nt) {
+                    /* streaming stores: the 32-B records are written once and
+                     * not read back here (no read-for-ownership of the lines) */
+                    typedef long long v2i __attribute__((vector_size(16)));
+                    v2i q[2];
+                    std::memcpy(q, &o, sizeof(o));
+                    __builtin_nontemporal_store(q[0], reinterpret_cast<v2i *>(out + j));
+                    __builtin_nontemporal_store(q[1], reinterpret_cast<v2i *>(out + j) + 1);
+                } else {
+                    out[j] = o;
+                }
+            }
+        }
+        if (j != j1)
+            return fail(KGX_EDEVICE, "compact hits: mask and hit count disagree for sequence " + std::to_string(s));
+    }
+    __builtin_ia32_sfence(); /* the streaming stores are visible before the task reports done */
+    return KGX_OK;
+}
+
+
+/* Streamed host batch (compact records, PACKED16 images): no host round
+ * trip inside a chunk.  Each chunk runs on its context's stream as
+ *   H2D -> plan/probe/score -> count scan (device CSR offsets) -> gather
+ *   into dense buffers (+ mask, counts, best calls)
+ * and its bulk device-to-host copy runs on the copy stream, sized on the
+ * device (the scanned totals) into host regions whose room the host set from
+ * the chunk's window count and the hit / call / OTU rates seen so far.  The
+ * host enqueues every chunk up front (each context's staging buffer is
+ * reused once its H2D is done), then, chunk by chunk as the copies land,
+ * builds the CSR offsets from the counts, moves calls / OTUs into place and
+ * hands the records to the expansion threads.  A chunk whose results did not
+ * fit its region makes the call return STREAM_OVERFLOW after raising the rates;
+ * the caller reruns the batch on the exact (host round trip) path. */
+constexpr int STREAM_OVERFLOW = 1; /* internal: a region overflowed, rerun exact */
+
+int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                           uint32_t n_seq, uint32_t want, uint32_t K, const std::vector<uint32_t> &cut,
+                           kgx_result *out)
+{
+    kgx_ctx *t = c->twin;
+    kgx_ctx *xs[2] = {c, t};
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    const bool timing = std::getenv("KGX_TIMING") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto T0 = now();
+
+    /* per-chunk windows, regions and offsets */
+    std::vector<uint64_t> win(K, 0), cap_h(K), cap_c(K), cap_o(K), rb_h(K + 1, 0), rb_c(K + 1, 0), rb_o(K + 1, 0),
+        mb(K + 1, 0);
+    c->h_wstart.resize(n_seq);
+    for (uint32_t k = 0; k < K; k++) {
+        uint64_t w = 0;
+        for (uint32_t s = cut[k]; s < cut[k + 1]; s++) {
+            c->h_wstart[s] = w;
+            w += windows_of(seq_offsets[s + 1] - seq_offsets[s]);
+        }
+        win[k] = w;
+        /* region starts stay 16-B aligned: multiples of 4 records */
+        auto room = [w](double rate, uint64_t extra) {
+            return (std::min<uint64_t>(w, (uint64_t)(rate * (double)w) + extra) + 3) & ~3ull;
+        };
+        cap_h[k] = room(c->rate_hits, 256);
+        cap_c[k] = want_calls ? room(c->rate_calls, 64) : 0;
+        cap_o[k] = want_otu ? room(c->rate_otus, 64) : 0;
+        rb_h[k + 1] = rb_h[k] + cap_h[k];
+        rb_c[k + 1] = rb_c[k] + cap_c[k];
+        rb_o[k + 1] = rb_o[k] + cap_o[k];
+        mb[k + 1] = mb[k] + (((w + 63) / 64 + 1) & ~1ull); /* 16-B aligned mask regions */
+    }
+    /* pinned host regions: resized before any copy or expansion is in flight */
+    const bool r12 = c->host_rec12 != 0;
+    if (r12)
+        HIP_TRY(c->h_hits12.resize(3 * rb_h[K]));
+    else
+        HIP_TRY(c->h_hits16.resize(rb_h[K]));
+    HIP_TRY(c->h_mask.resize(mb[K]));
+    HIP_TRY(c->h_calls_region.resize(rb_c[K]));
+    HIP_TRY(c->h_otus_region.resize(rb_o[K]));
+    HIP_TRY(c->h_counts.resize(3 * (uint64_t)n_seq));
+    HIP_TRY(c->h_hits.resize(rb_h[K])); /* room for every region's records; trimmed below */
+    HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+    c->h_hoff.assign(n_seq + 1, 0);
+    c->h_coff.assign(n_seq + 1, 0);
+    c->h_ooff.assign(n_seq + 1, 0);
+
+    /* device buffers of both contexts at the largest chunk's size up front:
+     * no reallocation while earlier chunks still read them */
+    uint64_t max_res = 1, max_n = 1;
+    for (uint32_t k = 0; k < K; k++) {
+        max_res = std::max(max_res, seq_offsets[cut[k + 1]] - seq_offsets[cut[k]]);
+        max_n = std::max<uint64_t>(max_n, cut[k + 1] - cut[k]);
+    }
+    for (kgx_ctx *x : xs) {
+        HIP_TRY(x->residues.reserve(max_res + 16));
+        HIP_TRY(x->offsets.reserve((max_n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_hoff.reserve((max_n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_coff.reserve((max_n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_ooff.reserve((max_n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->cscan_ws.reserve(count_scan_workspace_bytes((uint32_t)max_n)));
+        HIP_TRY(x->dense_hits.reserve(max_res * 16));
+        if (want_calls)
+            HIP_TRY(x->dense_calls.reserve(max_res * sizeof(kgx_call)));
+        if (want_otu)
+            HIP_TRY(x->dense_otus.reserve(max_res * sizeof(kgx_otu)));
+        HIP_TRY(x->dense_mask.reserve((max_res / 64 + 2) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_counts.reserve(3 * max_n * sizeof(uint32_t)));
+        if (want_best)
+            HIP_TRY(x->dense_best.reserve(max_n * sizeof(kgx_best_call)));
+    }
+
+    hipStream_t cs = c->copy_stream;
+    const int cb = c->host_copy_blocks;
+    auto mapped = [](auto &v, uint64_t at, void **d) -> hipError_t { return v.device_ptr(at, d); };
+
+    /* enqueue chunk k on x: everything up to its bulk copy */
+    auto enqueue = [&](kgx_ctx *x, uint32_t k) -> int {
+        const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
+        const uint64_t n_res = x->h_res.size();
+        int rc = stage_upload(x);
+        if (rc)
+            return rc;
+        HIP_TRY(hipEventRecord(c->chunk_h2d[k], x->stream));
+        if ((rc = kgx_run_device(x, params, x->residues.as<uint8_t>(), x->offsets.as<uint64_t>(), n, n_res, want,
+                                 nullptr)))
+            return rc;
+        const uint64_t rn = std::max<uint64_t>(n_res, 1); /* dense buffers: at most one record per residue */
+        HIP_TRY(x->dense_hoff.reserve((n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->dense_ooff.reserve((n + 1) * sizeof(uint64_t)));
+        HIP_TRY(x->cscan_ws.reserve(count_scan_workspace_bytes(n)));
+        HIP_TRY(launch_count_scan(n, x->hit_count.as<uint32_t>(), want_calls ? x->call_count.as<uint32_t>() : nullptr,
+                                  want_otu ? x->otu_count.as<uint32_t>() : nullptr, x->dense_hoff.as<uint64_t>(),
+                                  x->dense_coff.as<uint64_t>(), x->dense_ooff.as<uint64_t>(), x->cscan_ws.p,
+                                  x->stream));
+        /* x's dense buffers still feed chunk k-2's bulk copy */
+        if (k >= 2)
+            HIP_TRY(hipStreamWaitEvent(x->stream, c->chunk_done[k - 2], 0));
+        HIP_TRY(x->dense_hits.reserve(rn * 16));
+        if (want_calls)
+            HIP_TRY(x->dense_calls.reserve(rn * sizeof(kgx_call)));
+        if (want_otu)
+            HIP_TRY(x->dense_otus.reserve(rn * sizeof(kgx_otu)));
+        HIP_TRY(launch_gather(n, x->wbase.as<uint64_t>(), x->hit_mask.as<uint64_t>(), x->tile_windows,
+                              x->call_count.as<uint32_t>(), x->hits.as<uint4>(), x->hits.as<uint4>() + x->hit_slots,
+                              x->calls.as<kgx_call>(), x->dense_hoff.as<uint64_t>(), x->dense_coff.as<uint64_t>(),
+                              nullptr, want_calls ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->hit_format,
+                              x->otu_count.as<uint32_t>(), x->otus.as<kgx_otu>(), x->dense_ooff.as<uint64_t>(),
+                              want_otu ? x->dense_otus.as<kgx_otu>() : nullptr, x->stream,
+                              r12 ? nullptr : x->dense_hits.as<uint4>(), r12 ? x->dense_hits.as<uint32_t>() : nullptr));
+        /* what chunk k+2's kernels overwrite: mask, counts, best calls */
+        const uint64_t nwords = (win[k] + 63) / 64;
+        if (nwords) {
+            HIP_TRY(x->dense_mask.reserve(nwords * sizeof(uint64_t)));
+            HIP_TRY(launch_copy_to_host(x->dense_mask.p, x->hit_mask.p, nwords * sizeof(uint64_t), 256, x->stream));
+        }
+        if (n) {
+            HIP_TRY(x->dense_counts.reserve(3 * (uint64_t)n * sizeof(uint32_t)));
+            uint32_t *dc = x->dense_counts.as<uint32_t>();
+            HIP_TRY(launch_copy_to_host(dc, x->hit_count.p, n * sizeof(uint32_t), 64, x->stream));
+            if (want_calls)
+                HIP_TRY(launch_copy_to_host(dc + n, x->call_count.p, n * sizeof(uint32_t), 64, x->stream));
+            if (want_otu)
+                HIP_TRY(launch_copy_to_host(dc + 2 * (uint64_t)n, x->otu_count.p, n * sizeof(uint32_t), 64, x->stream));
+        }
+        if (want_best && n) {
+            HIP_TRY(x->dense_best.reserve(n * sizeof(kgx_best_call)));
+            HIP_TRY(hipMemcpyAsync(x->dense_best.p, x->best.p, n * sizeof(kgx_best_call), hipMemcpyDeviceToDevice,
+                                   x->stream));
+        }
+        HIP_TRY(hipEventRecord(c->chunk_gathered[k], x->stream));
+        /* the bulk copy, on the copy stream */
+        HIP_TRY(hipStreamWaitEvent(cs, c->chunk_gathered[k], 0));
+        void *d = nullptr;
+        if (n) {
+            const uint32_t planes = want_otu ? 3 : want_calls ? 2 : 1;
+            HIP_TRY(mapped(c->h_counts, 3 * (uint64_t)s0, &d));
+            HIP_TRY(launch_copy_to_host(d, x->dense_counts.p, planes * (uint64_t)n * sizeof(uint32_t), cb, cs));
+        }
+        if (r12)
+            HIP_TRY(mapped(c->h_hits12, 3 * rb_h[k], &d));
+        else
+            HIP_TRY(mapped(c->h_hits16, rb_h[k], &d));
+        HIP_TRY(launch_copy_counted(d, x->dense_hits.p, x->dense_hoff.as<uint64_t>() + n, cap_h[k], r12 ? 12 : 16,
+                                    cb, cs));
+        if (nwords) {
+            HIP_TRY(mapped(c->h_mask, mb[k], &d));
+            HIP_TRY(launch_copy_to_host(d, x->dense_mask.p, nwords * sizeof(uint64_t), cb, cs));
+        }
+        if (want_calls && cap_c[k]) {
+            HIP_TRY(mapped(c->h_calls_region, rb_c[k], &d));
+            HIP_TRY(launch_copy_counted(d, x->dense_calls.p, x->dense_coff.as<uint64_t>() + n, cap_c[k],
+                                        sizeof(kgx_call), cb, cs));
+        }
+        if (want_otu && cap_o[k]) {
+            HIP_TRY(mapped(c->h_otus_region, rb_o[k], &d));
+            HIP_TRY(launch_copy_counted(d, x->dense_otus.p, x->dense_ooff.as<uint64_t>() + n, cap_o[k],
+                                        sizeof(kgx_otu), cb, cs));
+        }
+        if (want_best && n) {
+            HIP_TRY(mapped(c->h_best, s0, &d));
+            HIP_TRY(launch_copy_to_host(d, x->dense_best.p, n * sizeof(kgx_best_call), cb, cs));
+        }
+        HIP_TRY(hipEventRecord(c->chunk_done[k], cs));
+        return KGX_OK;
+    };
+
+    /* chunk k's results on the host -> CSR offsets, calls / OTUs in place,
+     * expansion tasks; false in *fits when a region overflowed */
+    uint64_t hbase = 0, cbase = 0, obase = 0, nwin = 0;
+    double max_rh = 0, max_rc = 0, max_ro = 0;
+    bool fits = true;
+    auto collect = [&](uint32_t k) -> int {
+        HIP_TRY(hipEventSynchronize(c->chunk_done[k]));
+        const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
+        const uint32_t *hc = c->h_counts.data() + 3 * (uint64_t)s0, *cc = hc + n, *oc = hc + 2 * (uint64_t)n;
+        uint64_t nh = 0, nc = 0, no = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            nh += hc[i];
+            nc += want_calls ? cc[i] : 0;
+            no += want_otu ? oc[i] : 0;
+            c->h_hoff[s0 + i + 1] = hbase + nh;
+            c->h_coff[s0 + i + 1] = cbase + nc;
+            c->h_ooff[s0 + i + 1] = obase + no;
+        }
+        nwin += win[k];
+        if (win[k]) {
+            max_rh = std::max(max_rh, (double)nh / (double)win[k]);
+            max_rc = std::max(max_rc, (double)nc / (double)win[k]);
+            max_ro = std::max(max_ro, (double)no / (double)win[k]);
+        }
+        if (nh > cap_h[k] || nc > cap_c[k] || no > cap_o[k])
+            fits = false;
+        if (fits) {
+            if (nc)
+                std::memmove(c->h_calls_region.data() + cbase, c->h_calls_region.data() + rb_c[k],
+                             nc * sizeof(kgx_call));
+            if (no)
+                std::memmove(c->h_otus_region.data() + obase, c->h_otus_region.data() + rb_o[k],
+                             no * sizeof(kgx_otu));
+            if (nh) {
+                const int64_t delta = (int64_t)rb_h[k] - (int64_t)hbase;
+                const uint32_t P = c->pool->size();
+                uint32_t a = s0;
+                for (uint32_t p = 1; p <= P && a < s0 + n; p++) {
+                    uint32_t b = s0 + n;
+                    if (p < P) {
+                        const uint64_t target = hbase + nh * p / P;
+                        b = (uint32_t)(std::lower_bound(c->h_hoff.begin() + a, c->h_hoff.begin() + s0 + n, target) -
+                                       c->h_hoff.begin());
+                        b = std::max(b, a + 1);
+                    }
+                    const uint64_t m0 = mb[k];
+                    c->pool->submit([c, r12, residues, seq_offsets, a, b, m0, delta, k, timing, now, ms]() -> int {
+                        const auto q0 = now();
+                        const int erc = expand_hits(r12, c, residues, seq_offsets, a, b, m0, delta);
+                        if (timing)
+                            std::fprintf(stderr, "[kgx] streamed chunk %u expand [%u,%u): %.3f ms\n", k, a, b,
+                                         ms(q0, now()));
+                        return erc;
+                    });
+                    a = b;
+                }
+            }
+        }
+        hbase += nh;
+        cbase += nc;
+        obase += no;
+        return KGX_OK;
+    };
+
+    if (c->stage_threads > 1 && (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads))
+        c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
+    HostPool *sp = c->stage_threads > 1 ? c->stage_pool.get() : nullptr;
+    int rc = KGX_OK;
+    uint32_t next = 0; /* next chunk to collect */
+    for (uint32_t k = 0; k < K && !rc; k++) {
+        kgx_ctx *x = xs[k & 1];
+        if (k >= 2)
+            HIP_TRY(hipEventSynchronize(c->chunk_h2d[k - 2])); /* x's staging buffer is free */
+        if ((rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp)) || (rc = enqueue(x, k)))
+            break;
+        /* collect what has landed meanwhile */
+        while (!rc && next < k && hipEventQuery(c->chunk_done[next]) == hipSuccess)
+            rc = collect(next++);
+    }
+    while (!rc && next < K)
+        rc = collect(next++);
+    /* drain everything, whatever happened above */
+    const hipError_t e0 = hipStreamSynchronize(xs[0]->stream), e1 = hipStreamSynchronize(xs[1]->stream);
+    const hipError_t e2 = hipStreamSynchronize(cs);
+    const int prc = c->pool->wait();
+    if (rc)
+        return rc;
+    HIP_TRY(e0);
+    HIP_TRY(e1);
+    HIP_TRY(e2);
+    if (prc)
+        return prc;
+    /* the rates the next batch's regions are sized by */
+    c->rate_hits = std::max(0.02, max_rh * 1.25);
+    c->rate_calls = std::max(0.01, max_rc * 1.25);
+    c->rate_otus = std::max(0.01, max_ro * 1.25);
+    if (!fits)
+        return STREAM_OVERFLOW;
+    HIP_TRY(c->h_hits.resize(hbase));
+    c->have_hits = false;
+    t->have_hits = false;
+    if (timing)
+        std::fprintf(stderr, "[kgx] streamed batch: %u chunks, %.3f ms\n", K, ms(T0, now()));
+    out->best = want_best ? c->h_best.data() : nullptr;
+    out->n_seq = n_seq;
+    out->hit_offsets = c->h_hoff.data();
+    out->hits = c->h_hits.data();
+    out->call_offsets = c->h_coff.data();
+    out->calls = c->h_calls_region.data();
+    out->otu_offsets = c->h_ooff.data();
+    out->otus = c->h_otus_region.data();
+    out->n_windows = nwin;
+    return KGX_OK;
 }
 
 /* The host batch in K residue-balanced chunks of whole sequences, alternating
@@ -1235,12 +1722,26 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     t->probe_filter = c->probe_filter;
     t->probe_serialize = c->probe_serialize;
     kgx_ctx *xs[2] = {c, t};
+    if (!c->copy_stream)
+        HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    for (auto *ev : {&c->chunk_counts, &c->chunk_gathered, &c->chunk_done, &c->chunk_h2d})
+        while (ev->size() < K) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ev->push_back(e);
+        }
 
     const uint64_t r0 = seq_offsets[0], n_res = seq_offsets[n_seq] - r0;
     std::vector<uint32_t> cut(K + 1, 0);
     cut[K] = n_seq;
+    /* chunk weights: with host_taper the first and last chunks are half the
+     * others (the first one's kernels and the last one's copy + expansion
+     * are the parts of the batch nothing overlaps) */
+    const bool taper = c->host_taper && K >= 3;
+    const double wsum = taper ? (double)K - 1.0 : (double)K;
     for (uint32_t k = 1; k < K; k++) {
-        const uint64_t target = r0 + n_res * k / K;
+        const double before = taper ? 0.5 + (double)(k - 1) : (double)k; /* weight of chunks < k */
+        const uint64_t target = r0 + (uint64_t)((double)n_res * before / wsum);
         uint32_t s = (uint32_t)(std::lower_bound(seq_offsets, seq_offsets + n_seq + 1, target) - seq_offsets);
         cut[k] = std::min(std::max(s, cut[k - 1]), n_seq);
     }
@@ -1258,44 +1759,100 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     HIP_TRY(c->h_calls.resize(0));
     HIP_TRY(c->h_otus.resize(0));
     HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+    /* compact D2H: records + mask, expanded on the host pool */
+    const bool compact = c->host_hits16 && need_hits && c->img->layout == KGX_LAYOUT_PACKED16;
+    uint64_t mbase = 0;
+    struct PoolDrain { /* no expansion outlives this call, whatever path returns */
+        HostPool *p = nullptr;
+        ~PoolDrain()
+        {
+            if (p)
+                (void)p->wait();
+        }
+    } drain;
+    while (c->chunk_counts.size() < K) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->chunk_counts.push_back(e);
+    }
+    if (compact) {
+        if (!c->pool || c->pool->size() != (unsigned)c->host_threads)
+            c->pool.reset(new HostPool((unsigned)c->host_threads));
+        drain.p = c->pool.get();
+        HIP_TRY(c->h_hits16.resize(0));
+        HIP_TRY(c->h_mask.resize(0));
+        if (c->host_stream_chunks) {
+            const int src = process_batch_streamed(c, params, residues, seq_offsets, n_seq, want, K, cut, out);
+            if (src != STREAM_OVERFLOW)
+                return src;
+            /* a region overflowed: the rates are raised; this batch runs exact */
+            c->h_hoff.assign(n_seq + 1, 0);
+            c->h_coff.assign(n_seq + 1, 0);
+            c->h_ooff.assign(n_seq + 1, 0);
+            HIP_TRY(c->h_hits16.resize(0));
+            HIP_TRY(c->h_mask.resize(0));
+            HIP_TRY(c->h_hits.resize(0));
+            HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+            c->stream_fallbacks++;
+        }
+        c->h_wstart.resize(n_seq);
+        for (uint32_t k = 0; k < K; k++) {
+            uint64_t w = 0;
+            for (uint32_t s = cut[k]; s < cut[k + 1]; s++) {
+                c->h_wstart[s] = w;
+                w += windows_of(seq_offsets[s + 1] - seq_offsets[s]);
+            }
+        }
+    }
 
-    /* device bytes -> the pinned result array at element `at`: device stores
-     * into the mapped memory (host_copy 1) or a DMA copy */
-    auto copy_out = [&](kgx_ctx *x, auto &dst, uint64_t at, const void *src, uint64_t n) -> int {
+    hipStream_t cs = c->copy_stream;
+
+    /* device bytes -> the pinned result array at element `at`, on the copy
+     * stream: device stores into the mapped memory (host_copy 1) or a DMA
+     * copy */
+    auto copy_out = [&](auto &dst, uint64_t at, const void *src, uint64_t n) -> int {
         if (!n)
             return KGX_OK;
         const uint64_t bytes = n * sizeof(dst[0]);
         if (c->host_copy) {
             void *d = nullptr;
             HIP_TRY(dst.device_ptr(at, &d));
-            HIP_TRY(launch_copy_to_host(d, src, bytes, c->host_copy_blocks, x->stream));
+            HIP_TRY(launch_copy_to_host(d, src, bytes, c->host_copy_blocks, cs));
         } else {
-            HIP_TRY(hipMemcpyAsync(dst.data() + at, src, bytes, hipMemcpyDeviceToHost, x->stream));
+            HIP_TRY(hipMemcpyAsync(dst.data() + at, src, bytes, hipMemcpyDeviceToHost, cs));
         }
         return KGX_OK;
     };
 
-    /* Copies of both streams share the DMA engine in submission order, so the
-     * order of submission is the schedule: chunk k+1's H2D goes in before
-     * chunk k's D2H, and chunk k+1's kernels run while that D2H streams.
-     * The host staging of chunk k+2 runs meanwhile. */
-    int rc = stage_host_copy(xs[0], residues, seq_offsets, cut[0], cut[1]);
-    if (!rc)
-        rc = enqueue_chunk(xs[0], params, want);
-    if (!rc && K > 1)
-        rc = stage_host_copy(xs[1], residues, seq_offsets, cut[1], cut[2]);
+    /* Schedule.  Each chunk runs H2D -> plan/probe/score -> counts D2H on its
+     * context's stream (contexts alternate), then, once the host has turned
+     * the counts into offsets, a gather into that context's dense buffers;
+     * the bulk device-to-host copy of those buffers runs on a separate copy
+     * stream, so chunk k+2's kernels on the same context are not held behind
+     * chunk k's bulk copy (only chunk k+2's gather waits for it).
+     * Device-to-host bytes cross PCIe in order, so chunk k+1's counts must
+     * leave before chunk k's bulk (option counts_first): otherwise they queue
+     * behind it and the host learns chunk k+1's sizes only once the link has
+     * gone idle.  Chunks are staged and enqueued as soon as their context's
+     * staging buffer is free, and host threads expand chunk k's compact
+     * records while later chunks stream. */
+    if (c->stage_threads > 1 && (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads))
+        c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
+    HostPool *sp = c->stage_threads > 1 ? c->stage_pool.get() : nullptr;
+    int rc = KGX_OK;
+    for (uint32_t k = 0; k < std::min<uint32_t>(K, 2) && !rc; k++)
+        if (!(rc = stage_host_copy(xs[k], residues, seq_offsets, cut[k], cut[k + 1], sp)))
+            rc = enqueue_chunk(xs[k], params, want, c->chunk_counts[k]);
     const bool timing = std::getenv("KGX_TIMING") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     for (uint32_t k = 0; k < K && !rc; k++) {
-        kgx_ctx *x = xs[k & 1], *y = xs[(k + 1) & 1];
+        kgx_ctx *x = xs[k & 1];
         const auto t0 = now();
-        HIP_TRY(hipStreamSynchronize(x->stream)); /* chunk k's counts are on the host */
+        HIP_TRY(hipEventSynchronize(c->chunk_counts[k])); /* chunk k's counts are on the host */
         const auto t1 = now();
-        if (k + 1 < K && (rc = enqueue_chunk(y, params, want))) /* staged in the previous round */
-            break;
         const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
         HIP_TRY(x->h_dense_hoff.resize(n + 1));
         HIP_TRY(x->h_dense_coff.resize(n + 1));
@@ -1320,14 +1877,25 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
         if (!need_hits)
             nh = 0;
         const uint64_t hrec = need_hits ? hbase : 0; /* where this chunk's records go */
-        if (hrec + nh > c->h_hits.cap || cbase + nc > c->h_calls.cap || obase + no > c->h_otus.cap) {
-            /* growth moves the pinned arrays: no copy into them may be in flight */
-            HIP_TRY(hipStreamSynchronize(xs[0]->stream));
-            HIP_TRY(hipStreamSynchronize(xs[1]->stream));
+        const uint64_t nwords = compact && nh ? (x->h_nwin[0] + 63) / 64 : 0;
+        if (hrec + nh > c->h_hits.cap || cbase + nc > c->h_calls.cap || obase + no > c->h_otus.cap ||
+            (compact && (hrec + nh > c->h_hits16.cap || mbase + nwords > c->h_mask.cap))) {
+            /* growth moves the pinned arrays: no copy into them may be in
+             * flight, and no expansion may be reading or writing them */
+            HIP_TRY(hipStreamSynchronize(cs));
+            if (compact && (rc = c->pool->wait()))
+                break;
+        }
+        if (compact) {
+            HIP_TRY(c->h_hits16.resize(hrec + nh));
+            HIP_TRY(c->h_mask.resize(mbase + nwords));
         }
         HIP_TRY(c->h_hits.resize(hrec + nh));
         HIP_TRY(c->h_calls.resize(cbase + nc));
         HIP_TRY(c->h_otus.resize(obase + no));
+        /* x's dense buffers still feed chunk k-2's bulk copy */
+        if (k >= 2)
+            HIP_TRY(hipStreamWaitEvent(x->stream, c->chunk_done[k - 2], 0));
         if (nh || nc || no) {
             HIP_TRY(x->dense_hoff.reserve((n + 1) * sizeof(uint64_t)));
             HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
@@ -1345,36 +1913,93 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
                                   x->call_count.as<uint32_t>(), x->hits.as<uint4>(),
                                   x->hits.as<uint4>() + x->hit_slots, x->calls.as<kgx_call>(),
                                   x->dense_hoff.as<uint64_t>(), x->dense_coff.as<uint64_t>(),
-                                  nh ? x->dense_hits.as<kgx_hit>() : nullptr,
+                                  nh && !compact ? x->dense_hits.as<kgx_hit>() : nullptr,
                                   nc ? x->dense_calls.as<kgx_call>() : nullptr, s0, x->hit_format,
                                   x->otu_count.as<uint32_t>(), x->otus.as<kgx_otu>(), x->dense_ooff.as<uint64_t>(),
-                                  no ? x->dense_otus.as<kgx_otu>() : nullptr, x->stream));
-            if ((rc = copy_out(x, c->h_hits, hrec, x->dense_hits.p, nh)) ||
-                (rc = copy_out(x, c->h_calls, cbase, x->dense_calls.p, nc)) ||
-                (rc = copy_out(x, c->h_otus, obase, x->dense_otus.p, no)))
-                break;
+                                  no ? x->dense_otus.as<kgx_otu>() : nullptr, x->stream,
+                                  nh && compact ? x->dense_hits.as<uint4>() : nullptr));
         }
-        if (want_best && (rc = copy_out(x, c->h_best, s0, x->best.p, n)))
+        /* the mask and best calls too: chunk k+2's kernels overwrite them */
+        if (nwords) {
+            HIP_TRY(x->dense_mask.reserve(nwords * sizeof(uint64_t)));
+            HIP_TRY(launch_copy_to_host(x->dense_mask.p, x->hit_mask.p, nwords * sizeof(uint64_t), 256,
+                                        x->stream));
+        }
+        if (want_best && n) {
+            HIP_TRY(x->dense_best.reserve(n * sizeof(kgx_best_call)));
+            HIP_TRY(hipMemcpyAsync(x->dense_best.p, x->best.p, n * sizeof(kgx_best_call),
+                                   hipMemcpyDeviceToDevice, x->stream));
+        }
+        HIP_TRY(hipEventRecord(c->chunk_gathered[k], x->stream));
+        HIP_TRY(hipStreamWaitEvent(cs, c->chunk_gathered[k], 0));
+        if (k + 1 < K && c->counts_first)
+            HIP_TRY(hipStreamWaitEvent(cs, c->chunk_counts[k + 1], 0));
+        if (compact) {
+            if ((rc = copy_out(c->h_hits16, hrec, x->dense_hits.p, nh)) ||
+                (rc = copy_out(c->h_mask, mbase, x->dense_mask.p, nwords)))
+                break;
+        } else if ((rc = copy_out(c->h_hits, hrec, x->dense_hits.p, nh))) {
             break;
+        }
+        if ((rc = copy_out(c->h_calls, cbase, x->dense_calls.p, nc)) ||
+            (rc = copy_out(c->h_otus, obase, x->dense_otus.p, no)) ||
+            (want_best && (rc = copy_out(c->h_best, s0, x->dense_best.p, n))))
+            break;
+        HIP_TRY(hipEventRecord(c->chunk_done[k], cs));
+        if (compact && nh) {
+            /* host threads expand this chunk once its bytes have landed, in
+             * hit-balanced sequence ranges, while the next chunks stream */
+            hipEvent_t ev = c->chunk_done[k];
+            const uint32_t P = c->pool->size();
+            uint32_t a = s0;
+            for (uint32_t p = 1; p <= P && a < s0 + n; p++) {
+                uint32_t b = s0 + n;
+                if (p < P) {
+                    const uint64_t target = c->h_hoff[s0] + (c->h_hoff[s0 + n] - c->h_hoff[s0]) * p / P;
+                    b = (uint32_t)(std::lower_bound(c->h_hoff.begin() + a, c->h_hoff.begin() + s0 + n, target) -
+                                   c->h_hoff.begin());
+                    b = std::max(b, a + 1);
+                }
+                const uint64_t mb = mbase;
+                c->pool->submit([c, ev, residues, seq_offsets, a, b, mb, k, timing, now, ms]() -> int {
+                    const auto q0 = now();
+                    const hipError_t e = hipEventSynchronize(ev);
+                    if (e != hipSuccess)
+                        return fail(KGX_EDEVICE, std::string("chunk event: ") + hipGetErrorString(e));
+                    const auto q1 = now();
+                    const int erc = expand_hits(false, c, residues, seq_offsets, a, b, mb, 0);
+                    if (timing)
+                        std::fprintf(stderr, "[kgx] chunk %u expand [%u,%u): wait %.3f ms, expand %.3f ms\n", k, a,
+                                     b, ms(q0, q1), ms(q1, now()));
+                    return erc;
+                });
+                a = b;
+            }
+        }
+        mbase += nwords;
         hbase += nh_all;
         cbase += nc;
         obase += no;
         const auto t2 = now();
-        /* chunk k+2 -> x's pinned staging while the DMA engine and the device work */
-        /* (x's H2D of chunk k finished before its counts arrived; its pending
-         * D2H reads device memory only) */
-        if (k + 2 < K)
-            rc = stage_host_copy(x, residues, seq_offsets, cut[k + 2], cut[k + 3]);
+        /* chunk k+2 -> x (its H2D of chunk k finished before chunk k's counts
+         * arrived), enqueued at once */
+        if (k + 2 < K && !(rc = stage_host_copy(x, residues, seq_offsets, cut[k + 2], cut[k + 3], sp)))
+            rc = enqueue_chunk(x, params, want, c->chunk_counts[k + 2]);
         if (timing)
-            std::fprintf(stderr, "[kgx] chunk %u: wait counts %.3f ms, enqueue %.3f ms, stage k+2 %.3f ms\n", k,
-                         ms(t0, t1), ms(t1, t2), ms(t2, now()));
+            std::fprintf(stderr, "[kgx] chunk %u: wait counts %.3f ms, enqueue %.3f ms, stage+enqueue k+2 %.3f ms\n",
+                         k, ms(t0, t1), ms(t1, t2), ms(t2, now()));
     }
     /* drain both streams, whatever happened above */
     const hipError_t e0 = hipStreamSynchronize(xs[0]->stream), e1 = hipStreamSynchronize(xs[1]->stream);
+    const hipError_t e2 = hipStreamSynchronize(cs);
+    const int prc = compact ? c->pool->wait() : KGX_OK;
     if (rc)
         return rc;
+    if (prc)
+        return prc;
     HIP_TRY(e0);
     HIP_TRY(e1);
+    HIP_TRY(e2);
     /* the batch's device results are split over two contexts */
     c->have_hits = false;
     t->have_hits = false;

@@ -287,16 +287,30 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
- * "host_chunks" (1..64, default 3): kgx_process_batch splits a batch of at
- * least 4M residues into up to this many residue-balanced chunks of whole
- * sequences, alternating between the context and a twin context it creates
- * on first use, so that one chunk's D2H overlaps the next chunk's H2D and
- * kernels; "host_copy" 1 (default) / 0: a chunk's hits and calls reach the
- * host by device stores into the mapped pinned result arrays ("host_copy_blocks"
- * workgroups, default 64) / by DMA (hipMemcpyAsync, which shares the copy
- * engine with the next chunk's H2D).  After a chunked batch the device results are split over the two
- * contexts: kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch
- * (host_chunks 1, or want 0, which never chunks) */
+ * "host_chunks" (1..64, default 6): kgx_process_batch splits a batch into up
+ * to this many residue-balanced chunks of whole sequences (at least 2M
+ * residues each; with "host_taper" 1, the default, the first and last are
+ * half the others), alternating between the context and a twin context it
+ * creates on first use, so that one chunk's D2H overlaps later chunks' H2D and
+ * kernels; "host_copy" 1 (default) / 0: a chunk's results reach the host by
+ * device stores into mapped pinned memory ("host_copy_blocks" workgroups,
+ * default 64) / by DMA (hipMemcpyAsync).  PACKED16 images with hits wanted
+ * ("host_hits16" 1, the default): hits cross PCIe as table records without
+ * position or sequence (12 bytes with "host_rec12" 1, the default, the key
+ * re-encoded on the host from the residues; else the 16-B records) plus the
+ * batch's hit mask, and "host_threads" (default 12) host threads expand them
+ * into kgx_hit ("host_nt" 1: streaming stores) while later chunks stream.
+ * "host_stream" 1 (default): chunks need no host round trip -- CSR offsets
+ * are scanned on the device and the bulk copies (on a separate copy stream)
+ * are sized on the device into host regions sized from the hit / call / OTU
+ * rates of earlier batches; a batch that overflows them reruns on the exact
+ * schedule (host_stream 0: counts to the host, then gather and copy, with
+ * "counts_first" 1 holding chunk k's bulk copy until chunk k+1's counts are
+ * out).  "stage_threads" (default 4): threads copying the caller's residues
+ * into pinned staging.  Results are identical under every setting.  After a
+ * chunked batch the device results are split over the two contexts:
+ * kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch (host_chunks
+ * 1, or want 0, which never chunks) */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);

@@ -644,9 +644,20 @@ def test_chunked_host_batch_matches_oracle(small_world, oracle_lib, gpu):
     res = np.concatenate([np.frombuffer(b"MK", np.uint8)] + seqs)
     want = oracle_lib.process_batch(table, res, off)
     best_one_pass = None
-    for k, hc in ((2, 1), (3, 0), (3, 1), (8, 1), (1, 1)):
+    ctx.set_option("host_chunks", 1)  # one pass, 32-B records gathered on the device
+    flags_ref = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=7).hits["flags"].copy()
+    assert flags_ref.any()
+    # (chunks, host_copy, host_hits16, host_threads, host_stream): host_hits16
+    # 1 sends the 16-B table records + the hit mask and expands kgx_hit on host
+    # threads; host_stream 1 sizes each chunk's copy on the device (no host
+    # round trip inside a chunk), 0 the exact round-trip schedule
+    for k, hc, h16, nt, hs in ((2, 1, 1, 8, 1), (3, 0, 1, 3, 1), (3, 1, 0, 8, 1), (3, 1, 1, 1, 0), (8, 1, 1, 8, 1),
+                               (8, 0, 0, 8, 0), (5, 1, 1, 8, 0), (1, 1, 1, 8, 1)):
         ctx.set_option("host_chunks", k)
         ctx.set_option("host_copy", hc)
+        ctx.set_option("host_hits16", h16)
+        ctx.set_option("host_threads", nt)
+        ctx.set_option("host_stream", hs)
         got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
         assert_same(got, want, len(off) - 1)
         assert np.array_equal(got.hits["seq"], want.hits["seq"])
@@ -663,8 +674,38 @@ def test_chunked_host_batch_matches_oracle(small_world, oracle_lib, gpu):
                 assert eq_fields(g.hits, want.hits)
             else:
                 assert np.array_equal(g.call_offsets, want.call_offsets)
+        # with OTU tallies the hit flags are set: the same bits either way
+        g7 = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=7)
+        assert eq_fields(g7.hits, want.hits)
+        assert np.array_equal(g7.hits["flags"], flags_ref)
     ctx.set_option("host_chunks", 3)
     ctx.set_option("host_copy", 1)
+    ctx.set_option("host_hits16", 1)
+    ctx.set_option("host_threads", 8)
+    ctx.set_option("host_stream", 1)
+
+
+def test_streamed_host_batch_region_overflow(small_world, oracle_lib, gpu):
+    """The streamed schedule sizes each chunk's host regions from the hit /
+    call rates of earlier batches.  A hitless batch drives the rates to their
+    floor; the next, hit-dense batch overflows its regions and must rerun on
+    the exact schedule with identical results (and raise the rates)."""
+    spec, table, img, ctx = small_world
+    rng = np.random.default_rng(5)
+    ctx.set_option("host_chunks", 4)
+    ctx.set_option("host_stream", 1)
+    noise = np.frombuffer("".join(random_protein(rng, 300) for _ in range(20000)).encode(), np.uint8)
+    noff = np.arange(20001, dtype=np.uint64) * np.uint64(300)
+    for _ in range(2):
+        r0 = ctx.process_batch(noise, noff, gpu.Params(5, 200, 0, 0))
+        assert np.array_equal(r0.hit_offsets, oracle_lib.process_batch(table, noise, noff).hit_offsets)
+    res, off = synth.make_queries(spec, 16000, x_permille=0)
+    want = oracle_lib.process_batch(table, res, off)
+    for _ in range(2):  # overflow + exact rerun, then the raised rates fit
+        got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+        assert_same(got, want, len(off) - 1)
+        assert np.array_equal(got.hits["seq"], want.hits["seq"])
+    ctx.set_option("host_chunks", 3)
 
 
 # ---------------------------------------------------------------------------

@@ -30,6 +30,15 @@ def main():
     ap.add_argument("--chunks", default="1,2,4,8")
     ap.add_argument("--copy", default="0,1", help="host_copy settings to try")
     ap.add_argument("--copy-blocks", default="64", help="host_copy_blocks settings to try (copy 1)")
+    ap.add_argument("--hits16", default="0,1", help="host_hits16 settings to try")
+    ap.add_argument("--threads", default="8", help="host_threads settings to try (hits16 1)")
+    ap.add_argument("--stage", default="4", help="stage_threads settings to try")
+    ap.add_argument("--counts-first", default="1", help="counts_first settings to try")
+    ap.add_argument("--stream", default="0,1", help="host_stream settings to try")
+    ap.add_argument("--taper", default="1", help="host_taper settings to try")
+    ap.add_argument("--rec12", default="0", help="host_rec12 settings to try")
+    ap.add_argument("--nt", default="1", help="host_nt settings to try")
+    ap.add_argument("--timing", action="store_true", help="one extra KGX_TIMING pass per setting (stderr)")
     args = ap.parse_args()
     from close_kmers_amd import abi, synth
     import torch
@@ -41,19 +50,38 @@ def main():
     params = abi.default_params()
     out = {"n_residues": int(len(res))}
     times = {}
-    combos = [(int(x), int(y), int(b)) for y in args.copy.split(",") for x in args.chunks.split(",")
-              for b in (args.copy_blocks.split(",") if y == "1" else ["64"])]
-    for k, hc, nb in combos:
+    combos = [(int(x), int(y), int(b), int(h), int(t)) for y in args.copy.split(",") for x in args.chunks.split(",")
+              for b in (args.copy_blocks.split(",") if y == "1" else ["64"])
+              for h in args.hits16.split(",") for t in (args.threads.split(",") if h == "1" else ["8"])]
+    combos = [c + (int(st), int(cf), int(hs), int(tp)) for c in combos for st in args.stage.split(",")
+              for cf in args.counts_first.split(",") for hs in args.stream.split(",")
+              for tp in args.taper.split(",")]
+    combos = [c + (int(r), int(t)) for c in combos for r in args.rec12.split(",") for t in args.nt.split(",")]
+    for k, hc, nb, h16, nt, st, cf, hs, tp, r12, ntst in combos:
+        ctx.set_option("host_rec12", r12)
+        ctx.set_option("host_nt", ntst)
+        ctx.set_option("host_taper", tp)
+        ctx.set_option("host_stream", hs)
+        ctx.set_option("stage_threads", st)
+        ctx.set_option("counts_first", cf)
         ctx.set_option("host_chunks", k)
         ctx.set_option("host_copy", hc)
         ctx.set_option("host_copy_blocks", nb)
+        ctx.set_option("host_hits16", h16)
+        ctx.set_option("host_threads", nt)
         r = ctx.process_batch(res, off, params, want=3, copy=False)
         th = []
         for _ in range(7):
             t0 = time.perf_counter()
             r = ctx.process_batch(res, off, params, want=3, copy=False)
             th.append(time.perf_counter() - t0)
-        times[f"chunks{k}_copy{hc}" + (f"_blocks{nb}" if hc else "")] = float(np.median(th)) * 1e3
+        key = f"chunks{k}_copy{hc}" + (f"_blocks{nb}" if hc else "") + f"_h16{h16}" + (f"_t{nt}" if h16 else "") + f"_st{st}_cf{cf}_hs{hs}_tp{tp}_r{r12}_nt{ntst}"
+        times[key] = float(np.median(th)) * 1e3
+        if args.timing:
+            print(f"--- {key}", file=sys.stderr, flush=True)
+            os.environ["KGX_TIMING"] = "1"
+            ctx.process_batch(res, off, params, want=3, copy=False)
+            del os.environ["KGX_TIMING"]
     out["ms_by_host_chunks"] = times
     n_hits = len(r.hits)
     out["hits"] = n_hits
