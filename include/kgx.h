@@ -299,7 +299,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * position or sequence (12 bytes with "host_rec12" 1, the default, the key
  * re-encoded on the host from the residues; else the 16-B records) plus the
  * batch's hit mask, and "host_threads" (default 12) host threads expand them
- * into kgx_hit ("host_nt" 1: streaming stores) while later chunks stream.
+ * into kgx_hit records while later chunks stream ("host_nt" 1: with streaming
+ * stores).
  * "host_stream" 1 (default): chunks need no host round trip -- CSR offsets
  * are scanned on the device and the bulk copies (on a separate copy stream)
  * are sized on the device into host regions sized from the hit / call / OTU
