@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
+    ap.add_argument("--score-variant", type=int, default=1, help="1 = wave-parallel run scorer, 0 = lane per sequence")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 
@@ -218,6 +219,9 @@ def main():
     # stream and buffers, so one worker's scoring overlaps the next worker's
     # probe.  Every step is still a full pass over a whole batch.
     ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
+    for c in ctxs:
+        c.set_option("score_variant", args.score_variant)
+    score_ms: list = []  # score stage (+ best/OTU kernels with --want), same untimed pass as probe_ms
 
     def step(timed_probe: list | None, c=ctx, b=0):
         d_res, d_off = batches[b % len(batches)]
@@ -229,9 +233,12 @@ def main():
             abi.check(L.kgx_event_record(ev[1], c.handle), "event")
         abi.check(L.kgx_stage_score(c.handle, ctypes.byref(params), want), "score")
         if timed_probe is not None:
-            ms = ctypes.c_float()
+            abi.check(L.kgx_event_record(ev[2], c.handle), "event")
+            ms, ms2 = ctypes.c_float(), ctypes.c_float()
             abi.check(L.kgx_event_elapsed_ms(ev[0], ev[1], ctypes.byref(ms)), "elapsed")
+            abi.check(L.kgx_event_elapsed_ms(ev[1], ev[2], ctypes.byref(ms2)), "elapsed")
             timed_probe.append(ms.value)
+            score_ms.append(ms2.value)
 
     for i in range(args.warmup * len(ctxs)):
         step(None, ctxs[i % len(ctxs)], i)
@@ -426,6 +433,10 @@ def main():
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
                 "worker_contexts": len(ctxs), "distinct_batches": len(batches),
                 "hits_total": total_hits,
+                "score_variant": args.score_variant,
+                # the score stage alone (HIP events on the context's stream, same
+                # untimed pass as the probe time): what a single-context caller pays
+                "score_stage_ms": float(np.mean(score_ms)) if score_ms else None,
                 "outputs": {3: "hits + calls (lookup_request, find_best_match)",
                             7: "hits + calls + OTU (add_request)"}.get(want, f"want={want}"),
             },

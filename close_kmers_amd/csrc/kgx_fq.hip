@@ -344,6 +344,161 @@ __global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, con
     }
 }
 
+/*
+ * 1'. The same counts, one LANE per read: a read's fragments follow from its
+ * stop codons alone, so the count pass does not translate.  Every base is
+ * turned into its class nibble (nibbles4: A0 C1 G2 T/U3, bit 2 = outside
+ * ACGTU) and the last three nibbles are compared with the stop codons:
+ *   forward strand  TAA TAG TGA                         (trans_table.cc:8-15)
+ *   reverse strand  their reverse complements TTA CTA TCA read forward
+ * giving two masks per 64 bases, bit q = a stop codon whose last forward
+ * base is q.  Frame +k's codons end at q = k+1 (mod 3), frame -k's at
+ * q = len-k (mod 3); a run between consecutive stops of a frame (or the
+ * frame's ends) spans (q' - q)/3 - 1 codons and is kept when >= 11
+ * (fq_process_request.cc:333).  Blocks of 64 bases: the block's 17 dword
+ * loads are in flight together; each frame carries its last stop across
+ * blocks, so any read length takes this path.
+ */
+constexpr uint64_t EVERY3 = 0x9249249249249249ull; /* bits 0, 3, ..., 63 */
+
+__device__ __forceinline__ void frame_runs(uint64_t m, int base, int &prev, uint32_t &nf, uint32_t &nr)
+{
+    while (m) {
+        const int q = base + __builtin_ctzll(m);
+        m &= m - 1;
+        const int L = (q - prev) / 3 - 1;
+        if (L >= (int)MIN_FRAGMENT) {
+            nf++;
+            nr += (uint32_t)L;
+        }
+        prev = q;
+    }
+}
+
+/* a read's fragments and residues from its bytes: dword i of the read's
+ * aligned span comes from dw(i) (global memory or the wave's LDS copy) */
+template <class DW>
+__device__ __forceinline__ void lane_read_counts(DW dw, uint32_t mis, uint32_t len, uint32_t &nf, uint32_t &nr)
+{
+    nf = nr = 0;
+    const uint32_t nw = (mis + len + 3) / 4; /* aligned dwords spanning the read */
+    int prev[6], hi[6];
+    uint32_t rho[6];
+    for (uint32_t f = 0; f < 3; f++) { /* frame +(f+1): codon k = bases f+3k .. f+3k+2 */
+        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
+        prev[f] = (int)f - 1;
+        hi[f] = (int)(f + 2 + 3 * nc);
+        rho[f] = (f + 2) % 3;
+    }
+    for (uint32_t f = 0; f < 3; f++) { /* frame -(f+1): codon k ends at forward base len-1-f-3k */
+        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
+        const int top = (int)len - (int)f - 1;
+        prev[3 + f] = top - 3 * (int)nc;
+        hi[3 + f] = top + 3;
+        rho[3 + f] = (uint32_t)((top % 3 + 3) % 3);
+    }
+    uint32_t hist = 0x444; /* nibbles of the last three bases, newest lowest; bit 2 = not a base yet */
+    for (uint32_t blk = 0; 64 * blk < len; blk++) {
+        /* bases 64 blk .. 64 blk + 63: dwords 16 blk .. 16 blk + 16 of the
+         * span, shifted by mis bytes (the read's offset in its first dword) */
+        uint32_t d[17];
+#pragma unroll
+        for (uint32_t i = 0; i < 17; i++)
+            d[i] = 16 * blk + i < nw ? dw(16 * blk + i) : 0u;
+        uint64_t ef = 0, er = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) {
+            const uint32_t x = __builtin_amdgcn_alignbit(d[i + 1], d[i], mis * 8u);
+            const uint32_t nib = nibbles4(x);
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                hist = ((hist << 4) | ((nib >> (4 * j)) & 0xFu)) & 0xFFFu;
+                const uint32_t fs = hist == 0x300u || hist == 0x302u || hist == 0x320u;
+                const uint32_t rs = hist == 0x330u || hist == 0x130u || hist == 0x310u;
+                ef |= (uint64_t)fs << (4 * i + j);
+                er |= (uint64_t)rs << (4 * i + j);
+            }
+        }
+        /* bases past the read: their bits are dropped */
+        const uint32_t left = len - 64 * blk;
+        const uint64_t in = left >= 64 ? ~0ull : ((1ull << left) - 1);
+        ef &= in;
+        er &= in;
+        const int base = 64 * (int)blk;
+#pragma unroll
+        for (uint32_t f = 0; f < 6; f++) {
+            /* bits b of this block with 64 blk + b = rho (mod 3); 64 = 1 (mod 3) */
+            const uint32_t sh = (rho[f] + 3 - blk % 3) % 3;
+            frame_runs((f < 3 ? ef : er) & (EVERY3 << sh), base, prev[f], nf, nr);
+        }
+    }
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        const int L = (hi[f] - prev[f]) / 3 - 1;
+        if (L >= (int)MIN_FRAGMENT) {
+            nf++;
+            nr += (uint32_t)L;
+        }
+    }
+}
+
+/* per read: (fragments, residues); per 64 reads (the emit kernel's tile):
+ * their sums.  The wave's reads are usually back to back: their byte span is
+ * copied into the wave's LDS with 16-B coalesced loads and each lane reads its
+ * read from there (lanes reading their own reads straight from memory touch
+ * 64 lines per load, 150 bytes apart, and the L1 thrashes).  A wave whose span
+ * does not fit reads from memory. */
+constexpr uint32_t COUNT_SPAN = 12288; /* LDS bytes per wave */
+
+__global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                            uint32_t n_reads, uint2 *read_counts, ulonglong2 *tile_sum,
+                                                            uint32_t n_tiles)
+{
+    __shared__ uint4 span[WAVES_PER_WG][COUNT_SPAN / 16];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x * WAVES_PER_WG + wv;
+    if (tile >= n_tiles)
+        return;
+    const uint64_t r0 = (uint64_t)tile * FQ_TILE;
+    const uint32_t n = (uint32_t)std::min<uint64_t>(FQ_TILE, n_reads - r0);
+    const uint64_t r = r0 + lane;
+    const uint64_t ob = lane < n ? read_off[r] : 0, oe = lane < n ? read_off[r + 1] : 0;
+    /* the wave's span [a, e): 16-aligned start */
+    const uint64_t first = uniform_u64(__shfl(ob, 0)), end = uniform_u64(__shfl(oe, (int)n - 1));
+    const uintptr_t a = reinterpret_cast<uintptr_t>(bases + first) & ~(uintptr_t)15;
+    const uint64_t bytes = reinterpret_cast<uintptr_t>(bases + end) - a;
+    const bool staged = end > first && bytes <= COUNT_SPAN; /* (an empty span reads nothing) */
+    uint32_t nf = 0, nr = 0;
+    if (staged) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(bases + first - (reinterpret_cast<uintptr_t>(bases + first) & 15));
+        const uint32_t nv = (uint32_t)((bytes + 15) / 16);
+        for (uint32_t i = lane; i < nv; i += 64)
+            span[wv][i] = src[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < n) {
+            const uint32_t loc = (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a);
+            const uint32_t *L = reinterpret_cast<const uint32_t *>(span[wv]) + loc / 4;
+            const uint32_t lim = (uint32_t)((bytes + 3) / 4) - loc / 4; /* dwords of the span from L */
+            lane_read_counts([&](uint32_t i) { return i < lim ? L[i] : 0u; }, loc & 3, (uint32_t)(oe - ob), nf, nr);
+        }
+    } else if (lane < n) {
+        const uint8_t *b = bases + ob;
+        const uint32_t mis = read_mis(b);
+        const uint32_t *W = reinterpret_cast<const uint32_t *>(b - mis);
+        lane_read_counts([&](uint32_t i) { return W[i]; }, mis, (uint32_t)(oe - ob), nf, nr);
+    }
+    if (lane < n)
+        read_counts[r] = make_uint2(nf, nr);
+    const uint64_t F = wave_sum(nf), R = wave_sum(nr);
+    if (lane == 0) {
+        tile_sum[tile] = make_ulonglong2(F, R);
+        if (tile == n_tiles - 1)
+            tile_sum[n_tiles] = make_ulonglong2(0, 0); /* the scan's last element = the totals */
+    }
+}
+
 struct PairSum {
     __host__ __device__ ulonglong2 operator()(const ulonglong2 &a, const ulonglong2 &b) const
     {
@@ -501,7 +656,10 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     ulonglong2 *tile_base = tile_sum + (n_tiles + 1);
     uint64_t *totals = reinterpret_cast<uint64_t *>(tile_base + (n_tiles + 1));
     void *scan_tmp = ws + ((((rc_bytes + 15) & ~15ull) + 2 * ts_bytes + 16 + 255) & ~255ull);
-    if (n_reads)
+    if (n_reads && c->fq_count)
+        hipLaunchKernelGGL(fq_count_lane_kernel, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
+                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_sum, (uint32_t)n_tiles);
+    else if (n_reads)
         hipLaunchKernelGGL(fq_count_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            read_counts, tile_sum);
     else

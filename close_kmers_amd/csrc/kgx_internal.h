@@ -161,10 +161,12 @@ hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_
                        uint32_t *not_packable, hipStream_t stream);
 hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_t n,
                          hipStream_t stream);
-hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                        uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
-                        uint32_t *hit_count, uint32_t *call_count, kgx_params params,
-                        uint32_t want, uint32_t hit_format, hipStream_t stream);
+/* the run scorer: variant 1 = wave-parallel (order_constraint 0; the lane
+ * machine otherwise), 0 = one lane per sequence */
+hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *tile_seq, uint64_t max_tiles,
+                        const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
+                        uint32_t *hit_count, uint32_t *call_count, kgx_params params, uint32_t want,
+                        uint32_t hit_format, int variant, hipStream_t stream);
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,

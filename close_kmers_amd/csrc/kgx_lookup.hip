@@ -785,15 +785,12 @@ struct RunTail {
 constexpr int SCORE_BATCH = 8;
 
 template <bool PK>
-__global__ __launch_bounds__(256) void score_kernel(
-    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+__device__ __forceinline__ void score_sequence(
+    uint32_t s, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
     uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
-    kgx_params prm, uint32_t want)
+    const kgx_params &prm, uint32_t want)
 {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_seq)
-        return;
     const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
     const bool want_calls = (want & KGX_WANT_CALLS) != 0;
     const bool want_otu = (want & KGX_WANT_OTU) != 0;
@@ -964,14 +961,441 @@ __global__ __launch_bounds__(256) void score_kernel(
     }
 }
 
-hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
-                        uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
-                        uint32_t *hit_count, uint32_t *call_count, kgx_params params,
-                        uint32_t want, uint32_t hit_format, hipStream_t stream)
+template <bool PK>
+__global__ __launch_bounds__(256) void score_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+    uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
+    uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
+    kgx_params prm, uint32_t want)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n_seq)
+        score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
+}
+
+/* ------------------------------------------------------------------------ */
+/* score, wave-parallel                                                      */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * The same run rules (gather_hits kguts.cc:808-876, process_set_of_hits
+ * kguts.cc:734-781) evaluated 64 hits at a time by one wave, for
+ * order_constraint == 0 and sequences of at most RUN_CAP windows (every hit is
+ * then buffered: the 40,000-entry cap never binds).  Under those conditions
+ * the state machine reduces to per-hit predicates over a hit and its
+ * predecessor in the same sequence:
+ *   brk[i]  = first hit of its sequence, or prev.pos + max_gap < pos
+ *             (unsigned, kguts.cc:821-831): a new run starts at i;
+ *   mark[i] = brk[i] or fI[i] == fI[i-1]: after hit i, current_fI = fI[i];
+ *   cur[i]  = fI of the last marked hit at or before i (a segmented scan:
+ *             one ballot and a highest-set-bit per lane);
+ *   switch  = fI[i] == fI[i-1] != cur[i-1] (kguts.cc:852-856): the run so far
+ *             is flushed and the carried pair i-1, i starts a new sub-run
+ *             (kguts.cc:771-779; a gap flush never carries: its last two hits
+ *             would have switched already).
+ * Sub-runs start at brk hits and one hit before switch hits; a sub-run's call
+ * counts its hits with fI == its current_fI (its first hit always does), from
+ * its first hit to the last such hit, and is emitted when count >= min_hits
+ * and the f32 sum of their weights, added in hit order from 0.0f, is >=
+ * min_weighted_hits -- the same condition at a gap, a switch and the final
+ * flush.  Everything but that sum is ballots, bit counts and shuffles; the
+ * sums run serially (v_readlane + v_add_f32 in hit order) only over sub-runs
+ * that reach min_hits.
+ *
+ * Work: wave w takes the sequences whose first window lies in windows
+ * [w R, (w+1) R) (R = SCORE_WAVE_TILES tiles; found from tile_seq), walks
+ * their hit-mask words (64 at a time in a register) and queues each hit's
+ * (position, sequence, first window, storage slot) in LDS; every 64 queued
+ * hits -- of one long sequence or of many short fragments -- are one chunk.
+ * The open sub-run, the last hit and the open sequence's call count carry
+ * from chunk to chunk.  A sub-run that spans chunks and is emitted gets its
+ * OTU flags by a walk over its windows.  Sequences longer than RUN_CAP
+ * windows run the serial machine (score_sequence) on one lane.
+ */
+constexpr uint32_t SCORE_WAVE_TILES = 16;
+constexpr uint32_t SQ = 128; /* queue entries per wave (a power of two >= 128) */
+
+struct ScoreQueue {
+    uint32_t pos[SQ];
+    uint32_t seq[SQ];
+    uint64_t gw0[SQ];
+    uint64_t at[SQ];
+};
+
+__device__ __forceinline__ uint64_t lanes_le(uint32_t k) { return k >= 63 ? ~0ull : ((2ull << k) - 1); }
+__device__ __forceinline__ int hibit(uint64_t m) { return m ? 63 - (int)__clzll((long long)m) : -1; }
+__device__ __forceinline__ uint32_t lowbit(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
+{
+    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, l) |
+           (uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32;
+}
+__device__ __forceinline__ float rlf(float v, uint32_t l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* first sequence whose first window is >= x (x a tile boundary below the
+ * batch's window count); tile_seq[x / T] owns window x */
+__device__ __forceinline__ uint32_t seq_lower_bound(const uint64_t *__restrict__ wbase,
+                                                    const uint32_t *__restrict__ tile_seq, uint32_t T, uint64_t x)
+{
+    uint32_t s = tile_seq[x / T];
+    if (wbase[s] < x)
+        return s + 1;
+    while (s > 0 && wbase[s - 1] == x) /* empty sequences right before it */
+        s--;
+    return s;
+}
+
+template <bool PK>
+__global__ __launch_bounds__(256) void score_wave_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq,
+    const uint64_t *__restrict__ hit_mask, uint32_t tile_windows, uint4 *__restrict__ hot,
+    kgx_call *__restrict__ calls, uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count,
+    uint32_t *__restrict__ call_count, kgx_params prm, uint32_t want)
+{
+    __shared__ ScoreQueue queues[4];
+    typedef HitFields<PK> HF;
+    constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << HF::FLAG_SHIFT, F_CNT = KGX_HIT_COUNTED << HF::FLAG_SHIFT,
+                       F_OTU = KGX_HIT_OTU << HF::FLAG_SHIFT;
+    constexpr int FD = HF::FLAG_DWORD;
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    ScoreQueue &Q = queues[threadIdx.x >> 6];
+    uint32_t *hw = reinterpret_cast<uint32_t *>(hot);
+    const uint32_t lane = lane_id();
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t R = (uint64_t)tile_windows * SCORE_WAVE_TILES;
+    const uint64_t W = wbase[n_seq];
+    const uint64_t x0 = (uint64_t)w * R;
+    if (w > 0 && x0 >= W)
+        return;
+    const uint32_t s_lo = w == 0 ? 0u : seq_lower_bound(wbase, tile_seq, tile_windows, x0);
+    const uint32_t s_hi = x0 + R >= W ? n_seq : seq_lower_bound(wbase, tile_seq, tile_windows, x0 + R);
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    const bool scoring = want_calls || want_otu;
+    const uint32_t J = tile_windows / 64;
+    const uint32_t gap = (uint32_t)prm.max_gap;
+    const float min_wh = (float)prm.min_weighted_hits;
+
+    /* ---- the open sub-run (O) and the last hit, carried across chunks ---- */
+    bool o_valid = false, o_span = false;
+    uint32_t o_seq = NONE, o_cur = 0, o_cnt = 0, o_first = 0, o_last = 0, o_ncalls = 0;
+    float o_wsum = 0.0f;
+    uint64_t o_gw0 = 0;
+    uint32_t p_pos = 0, p_fi = 0, p_fb = 0;
+    float p_wt = 0.0f;
+    uint64_t p_at = 0;
+
+    /* OTU flags of an emitted sub-run that spans chunks: its hits are the
+     * sequence's hits in windows [first, last]; the ones with fI == cur count */
+    auto otu_fixup = [&](uint64_t gw0, uint32_t first, uint32_t last, uint32_t cur) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); /* earlier flag stores are done */
+        const uint64_t a = gw0 + first, b = gw0 + last;
+        for (uint64_t g = a >> 6; g <= (b >> 6); g++) {
+            const uint64_t full = hit_mask[g];
+            const uint32_t lo = g == (a >> 6) ? (uint32_t)(a & 63) : 0u;
+            const uint32_t hi = g == (b >> 6) ? (uint32_t)(b & 63) + 1 : 64u;
+            const uint64_t bits = full & bit_range(lo, hi);
+            const uint64_t tile = g / J;
+            uint32_t pre = 0;
+            for (uint64_t q = tile * J; q < g; q++)
+                pre += (uint32_t)__popcll(hit_mask[q]);
+            if ((bits >> lane) & 1) {
+                const uint64_t at = tile * tile_windows + pre + lanes_below(full);
+                const uint4 r = hot[at];
+                if (HF::fi(r) == cur)
+                    hw[4 * at + FD] = HF::flag_base(r) | F_RUN | F_CNT | F_OTU;
+            }
+        }
+    };
+    /* flush of O: the call (kguts.cc:757-770) when count and weight reach the minimums */
+    auto close_open = [&]() -> bool {
+        const bool em = (int)o_cnt >= prm.min_hits && o_wsum >= min_wh;
+        if (em) {
+            if (want_calls && lane == 0) {
+                kgx_call cl;
+                cl.start = o_first;
+                cl.end = o_last + (KMER - 1);
+                cl.count = (int32_t)o_cnt;
+                cl.function_index = o_cur;
+                cl.weighted_hits = o_wsum;
+                calls[o_gw0 + o_ncalls] = cl;
+            }
+            o_ncalls++;
+            if (want_otu && o_span)
+                otu_fixup(o_gw0, o_first, o_last, o_cur);
+        }
+        return em;
+    };
+
+    uint32_t qhead = 0, qtail = 0;
+
+    /* one chunk: queue entries [qhead, qhead + n), n <= 64 */
+    auto process_chunk = [&](uint32_t n) {
+        const uint32_t k = lane;
+        const bool act = k < n;
+        const uint64_t ACT = n >= 64 ? ~0ull : ((1ull << n) - 1);
+        const uint32_t e = (qhead + k) & (SQ - 1);
+        const uint32_t pos = act ? Q.pos[e] : 0u;
+        const uint32_t seq = act ? Q.seq[e] : NONE;
+        const uint64_t gw0 = act ? Q.gw0[e] : 0ull;
+        const uint64_t at = act ? Q.at[e] : 0ull;
+        uint4 r = make_uint4(0, 0, 0, 0);
+        if (act)
+            r = hot[at];
+        const uint32_t fi = HF::fi(r);
+        const float wt = __uint_as_float(HF::wt(r));
+        const uint32_t fb = HF::flag_base(r);
+
+        /* the predecessor of each hit (lane 0: the carried last hit) */
+        uint32_t ppos = __shfl_up(pos, 1), pfi = __shfl_up(fi, 1), pseq = __shfl_up(seq, 1);
+        if (k == 0) {
+            ppos = p_pos;
+            pfi = p_fi;
+            pseq = o_valid ? o_seq : NONE;
+        }
+        const bool newseq = seq != pseq;
+        const bool brk = newseq || (ppos + gap < pos);
+        const bool eqp = !brk && fi == pfi;
+        const uint64_t M = __ballot(act && (brk || eqp));
+        const uint64_t mle = M & lanes_le(k);
+        const int jm = hibit(mle);
+        uint32_t cur = __shfl(fi, jm < 0 ? 0 : jm);
+        if (jm < 0)
+            cur = o_cur;
+        uint32_t pcur = __shfl_up(cur, 1);
+        if (k == 0)
+            pcur = o_cur;
+        const bool sw = act && eqp && fi != pcur;
+        const uint64_t SW = __ballot(sw), NS = __ballot(act && newseq);
+        const uint64_t S = (__ballot(act && brk) | (SW >> 1)) & ACT; /* sub-run starts */
+        const bool memb = act && (fi == cur || ((S >> k) & 1));
+        const uint64_t MEMB = __ballot(memb);
+
+        /* a switch at lane 0: O is flushed before this chunk and the pair
+         * (last hit, lane 0) starts the new O */
+        if (SW & 1) {
+            close_open();
+            if (want_otu && lane == 0)
+                hw[4 * p_at + FD] = p_fb | F_RUN | F_CNT;
+            o_cur = rl32(fi, 0);
+            o_cnt = 1;
+            o_wsum = 0.0f + p_wt;
+            o_first = p_pos;
+            o_last = p_pos;
+            o_span = true;
+        }
+        /* lanes before the first start continue O */
+        const uint32_t fs = S ? lowbit(S) : n;
+        if (fs > 0) {
+            uint64_t mm = MEMB & bit_range(0, fs);
+            o_cnt += (uint32_t)__popcll(mm);
+            if (mm)
+                o_last = rl32(pos, (uint32_t)hibit(mm));
+            while (mm) {
+                o_wsum = o_wsum + rlf(wt, lowbit(mm));
+                mm &= mm - 1;
+            }
+        }
+        bool o_emitted = false;
+        if (fs < n && o_valid) {
+            o_emitted = close_open();
+            if (fs == 0 && (NS & 1)) /* O's sequence ended in the previous chunk */
+                if (lane == 0)
+                    call_count[o_seq] = want_calls ? o_ncalls : 0u;
+        }
+
+        /* sub-runs that start in this chunk, one per start lane */
+        const bool is_start = (S >> k) & 1;
+        const uint64_t above = S & ~lanes_le(k);
+        const uint32_t e_k = above ? lowbit(above) : n;
+        const uint64_t msg = MEMB & bit_range(k, e_k);
+        const uint32_t c_seg = (uint32_t)__popcll(msg);
+        const int lm = hibit(msg);
+        const uint32_t last_pos = __shfl(pos, lm < 0 ? 0 : lm);
+        const bool closed = e_k < n;
+        const int b_open = hibit(S); /* the sub-run left open at the chunk's end */
+        /* the f32 sums, serially, for the sub-runs that can be emitted and the open one */
+        uint64_t SUM = __ballot(is_start && closed && (int)c_seg >= prm.min_hits);
+        if (b_open >= 0)
+            SUM |= 1ull << b_open;
+        float ws = 0.0f;
+        while (SUM) {
+            const uint32_t b = lowbit(SUM);
+            SUM &= SUM - 1;
+            const uint64_t ab = S & ~lanes_le(b);
+            uint64_t mm = MEMB & bit_range(b, ab ? lowbit(ab) : n);
+            float acc = 0.0f;
+            while (mm) {
+                acc = acc + rlf(wt, lowbit(mm));
+                mm &= mm - 1;
+            }
+            if (lane == b)
+                ws = acc;
+        }
+        const uint64_t EMIT = __ballot(is_start && closed && (int)c_seg >= prm.min_hits && ws >= min_wh);
+        /* call index: the calls of the lane's sequence before it (O's sequence
+         * continues through the lanes before the chunk's first new sequence) */
+        const int fsq = hibit(NS & lanes_le(k));
+        const uint32_t from = fsq < 0 ? 0u : (uint32_t)fsq;
+        const uint32_t idx = (fsq < 0 ? o_ncalls : 0u) + (uint32_t)__popcll(EMIT & bit_range(from, k));
+        if (want_calls && ((EMIT >> k) & 1)) {
+            kgx_call cl;
+            cl.start = pos;
+            cl.end = last_pos + (KMER - 1);
+            cl.count = (int32_t)c_seg;
+            cl.function_index = fi;
+            cl.weighted_hits = ws;
+            calls[gw0 + idx] = cl;
+        }
+        /* sequences whose last hit is in this chunk (not its last lane) */
+        if (act && k + 1 < n && ((NS >> (k + 1)) & 1)) {
+            const uint32_t cc = idx + (uint32_t)((EMIT >> k) & 1);
+            call_count[seq] = want_calls ? cc : 0u;
+        }
+        if (want_otu && act) {
+            const int bk = hibit(S & lanes_le(k));
+            const bool em = bk >= 0 ? ((EMIT >> bk) & 1) != 0 : o_emitted;
+            hw[4 * at + FD] = fb | F_RUN | (memb ? F_CNT : 0u) | (memb && em ? F_OTU : 0u);
+        }
+
+        /* carry */
+        if (b_open >= 0) {
+            const uint32_t b = (uint32_t)b_open;
+            o_valid = true;
+            o_seq = rl32(seq, b);
+            o_gw0 = rl64(gw0, b);
+            o_cur = rl32(fi, b);
+            o_cnt = rl32(c_seg, b);
+            o_wsum = rlf(ws, b);
+            o_first = rl32(pos, b);
+            o_last = rl32(last_pos, b);
+            o_ncalls = rl32(idx, b);
+        }
+        o_span = true;
+        const uint32_t l = n - 1;
+        p_pos = rl32(pos, l);
+        p_fi = rl32(fi, l);
+        p_wt = rlf(wt, l);
+        p_fb = rl32(fb, l);
+        p_at = rl64(at, l);
+        qhead += n;
+    };
+
+    /* ---- walk the wave's sequences and their hit-mask words ---- */
+    uint32_t sb = s_lo; /* lane j: hit count of sequence sb + j */
+    uint32_t vhc = 0;
+    uint64_t pg = ~0ull, pfull = 0;
+    uint32_t ppre = 0;
+    auto flush_counts = [&](uint32_t upto) { /* sequences [sb, upto) */
+        if (lane < upto - sb && vhc != NONE) {
+            hit_count[sb + lane] = vhc;
+            if (vhc == 0 || !scoring)
+                call_count[sb + lane] = 0;
+        }
+    };
+    for (uint32_t s = s_lo; s < s_hi; s++) {
+        if (s + 1 - sb > 63) {
+            flush_counts(s);
+            sb = s;
+            vhc = 0;
+        }
+        const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
+        if (gw1 - gw0 > (uint64_t)RUN_CAP) { /* the serial machine, on one lane */
+            if (lane == 0)
+                score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count,
+                                   prm, want);
+            if (lane == s - sb)
+                vhc = NONE;
+            continue;
+        }
+        uint32_t nh = 0;
+        if (gw0 < gw1) {
+            const uint64_t g0 = gw0 >> 6, g1 = (gw1 - 1) >> 6;
+            for (uint64_t g = g0; g <= g1; g++) {
+                const uint64_t full = hit_mask[g];
+                if (g != pg) { /* hits of g's tile before word g */
+                    if (pg != ~0ull && g == pg + 1)
+                        ppre = g % J == 0 ? 0u : ppre + (uint32_t)__popcll(pfull);
+                    else {
+                        ppre = 0;
+                        for (uint64_t q = (g / J) * J; q < g; q++)
+                            ppre += (uint32_t)__popcll(hit_mask[q]);
+                    }
+                    pg = g;
+                    pfull = full;
+                }
+                const uint32_t lo = g == g0 ? (uint32_t)(gw0 & 63) : 0u;
+                const uint32_t hi = g == g1 ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
+                const uint64_t bits = full & bit_range(lo, hi);
+                if (!bits)
+                    continue;
+                const uint32_t c = (uint32_t)__popcll(bits);
+                nh += c;
+                if (!scoring)
+                    continue;
+                if ((bits >> lane) & 1) {
+                    const uint32_t slot = (qtail + lanes_below(bits)) & (SQ - 1);
+                    Q.pos[slot] = (uint32_t)(64 * g + lane - gw0);
+                    Q.seq[slot] = s;
+                    Q.gw0[slot] = gw0;
+                    Q.at[slot] = (g / J) * tile_windows + ppre + lanes_below(full);
+                }
+                qtail += c;
+                if (qtail - qhead >= 64) {
+                    wave_lds_sync();
+                    process_chunk(64);
+                    wave_lds_sync();
+                }
+            }
+        }
+        if (lane == s - sb)
+            vhc = nh;
+    }
+    flush_counts(s_hi);
+    if (!scoring)
+        return;
+    wave_lds_sync();
+    while (qtail != qhead)
+        process_chunk(min(64u, qtail - qhead));
+    if (o_valid) {
+        close_open();
+        if (lane == 0)
+            call_count[o_seq] = want_calls ? o_ncalls : 0u;
+    }
+}
+
+hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *tile_seq, uint64_t max_tiles,
+                        const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
+                        uint32_t *hit_count, uint32_t *call_count, kgx_params params, uint32_t want,
+                        uint32_t hit_format, int variant, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
-    if (hit_format == HIT_PACKED16)
+    const bool pk = hit_format == HIT_PACKED16;
+    if (variant == 1 && !params.order_constraint) {
+        const uint64_t waves = std::max<uint64_t>(1, (max_tiles + SCORE_WAVE_TILES - 1) / SCORE_WAVE_TILES);
+        const dim3 grid((uint32_t)((waves + 3) / 4));
+        if (pk)
+            hipLaunchKernelGGL(score_wave_kernel<true>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
+                               tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
+                               want);
+        else
+            hipLaunchKernelGGL(score_wave_kernel<false>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
+                               tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
+                               want);
+        return hipGetLastError();
+    }
+    if (pk)
         hipLaunchKernelGGL(score_kernel<true>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
                            hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
                            call_count, params, want);

@@ -969,6 +969,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->host_chunks = (int)value;
         return KGX_OK;
     }
+    if (n == "fq_count") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "fq_count must be 0 or 1");
+        c->fq_count = (int)value;
+        return KGX_OK;
+    }
+    if (n == "score_variant") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "score_variant must be 0 or 1");
+        c->score_variant = (int)value;
+        return KGX_OK;
+    }
     if (n == "probe_j") {
         if (!probe_j_supported((int)value))
             return fail(KGX_EINVAL, "probe_j must be 1, 2, 3, 4, 5 or 8");
@@ -1083,10 +1095,10 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
         kgx_params_default(&p);
     HIP_TRY(hipSetDevice(c->img->device));
     const bool best = (want & KGX_WANT_BEST) != 0;
-    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(),
-                         c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
+    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(), c->max_tiles,
+                         c->hit_mask.as<uint64_t>(), c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
-                         want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->stream));
+                         want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->score_variant, c->stream));
     c->have_best = false;
     c->have_otus = false;
     if (want & KGX_WANT_OTU) {

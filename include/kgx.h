@@ -287,6 +287,10 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
+ * "score_variant" 1 (default) = the wave-parallel run scorer (ballots over a
+ * wave's hits, sequential f32 sums only), 0 = one lane per sequence;
+ * "fq_count" 1 (default) = the fq count pass scans stop codons one lane per
+ * read, 0 = it translates like the emit pass (one wave per read);
  * "host_chunks" (1..64, default 6): kgx_process_batch splits a batch into up
  * to this many residue-balanced chunks of whole sequences (at least 2M
  * residues each; with "host_taper" 1, the default, the first and last are

@@ -42,6 +42,37 @@ def test_fragments_match_oracle(gpu, oracle_lib):
     assert n == f.n_fragments and n > 500
 
 
+@pytest.mark.parametrize("fq_count", [0, 1])
+def test_fragments_long_reads_both_count_passes(gpu, oracle_lib, fq_count):
+    """Both count passes (lane-per-read stop scan / wave translation) give the
+    emit pass the same offsets: reads of 0-1000 bases (several 64-base blocks
+    of the stop scan, the emit's serial path past 194 bases), stop-rich and
+    IUPAC-laden, at every start alignment."""
+    spec, table = synthetic_table(20000)
+    rng = np.random.default_rng(11)
+    stoppy = np.frombuffer(b"TAAGTGATAGCTTATCAACGT", np.uint8)
+    reads = []
+    for i in range(600):
+        L = int(rng.integers(0, 1000)) if i % 5 else int(rng.integers(0, 70))
+        pool = stoppy if i % 4 == 0 else np.frombuffer(b"ACGTACGTACGTacgtNnUuRYKX", np.uint8)
+        reads.append(bytes(pool[rng.integers(0, len(pool), L)]))
+    res, off = pack([("r", r) for r in reads])
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        ctx.set_option("fq_count", fq_count)
+        f = ctx.fq_fragments(res, off)
+        h = ctx.fragments_to_host(f)
+    got = {}
+    for i in range(f.n_fragments):
+        s = bytes(h["residues"][int(h["offsets"][i]):int(h["offsets"][i + 1])]).decode()
+        got.setdefault(int(h["read"][i]), []).append((int(h["frame"][i]), s))
+    n = 0
+    for r, dna in enumerate(reads):
+        want = oracle_lib.fq_fragments(dna)
+        assert got.get(r, []) == want, (r, len(dna))
+        n += len(want)
+    assert n == f.n_fragments and n > 1000
+
+
 def test_fragment_lookup_matches_oracle(gpu, oracle_lib):
     """Fragments fed to the lookup give the oracle's hits and calls."""
     from close_kmers_amd import synth
