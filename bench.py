@@ -144,7 +144,7 @@ def main():
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
-    ap.add_argument("--score-variant", type=int, default=1, help="1 = wave-parallel run scorer, 0 = lane per sequence")
+    ap.add_argument("--score-variant", type=int, default=0, help="0 = lane per sequence (default), 1 = wave-parallel run scorer")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 
@@ -261,18 +261,21 @@ def main():
         names = name.split(",")
         vals = vals.split(",")
         times = {v: [] for v in vals}
+        stimes = {v: [] for v in vals}
         k = 0
         for _ in range(args.ab_rounds):
             for v in vals:
                 for nm, x in zip(names, v.split(":")):
                     ctx.set_option(nm, int(x))
                 step(times[v], ctx, k)
+                stimes[v].append(score_ms.pop())
                 k += 1
         ctx.set_option("probe_variant", -1)
         ctx.set_option("probe_j", 2)
         ctx.set_option("probe_filter", 1)
         probe_ab = {"option": name,
-                    **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))}
+                    **{str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                                "score_median_ms": float(np.median(stimes[v]))}
                        for v, t in times.items()}}
         log(f"[bench] probe A/B: {probe_ab}")
 

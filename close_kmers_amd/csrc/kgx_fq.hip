@@ -164,8 +164,10 @@ __device__ __forceinline__ uint32_t load_read_dword(const uint8_t *b, uint64_t l
  * stop masks, run masks -- then runs on the scalar unit */
 __device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
 {
-    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-           (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+    /* the builtin returns int: widen through uint32_t (a low half >= 2^31
+     * would otherwise sign-extend into the high half) */
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
 }
 
 /* the wave's short reads -> their nibble strings in LDS (slot j = read j).

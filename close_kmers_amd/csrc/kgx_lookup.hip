@@ -1012,28 +1012,31 @@ __global__ __launch_bounds__(256) void score_kernel(
  * OTU flags by a walk over its windows.  Sequences longer than RUN_CAP
  * windows run the serial machine (score_sequence) on one lane.
  */
-constexpr uint32_t SCORE_WAVE_TILES = 16;
-constexpr uint32_t SQ = 128; /* queue entries per wave (a power of two >= 128) */
+constexpr uint32_t SQ = 256; /* queue entries per wave: a chunk in flight, the next, a word's overflow */
 
 struct ScoreQueue {
     uint32_t pos[SQ];
     uint32_t seq[SQ];
-    uint64_t gw0[SQ];
-    uint64_t at[SQ];
+    uint32_t at[SQ];
+    uint64_t mw[64]; /* hit-mask words gb .. gb + 63 */
+    uint64_t wb[65]; /* window bases of sequences sb .. sb + 64 */
 };
 
 __device__ __forceinline__ uint64_t lanes_le(uint32_t k) { return k >= 63 ? ~0ull : ((2ull << k) - 1); }
 __device__ __forceinline__ int hibit(uint64_t m) { return m ? 63 - (int)__clzll((long long)m) : -1; }
 __device__ __forceinline__ uint32_t lowbit(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t l)
-{
-    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, l) |
-           (uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32;
-}
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ float rlf(float v, uint32_t l)
 {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+/* (the builtins return int: widen through uint32_t, or a low half >= 2^31
+ * sign-extends into the high half) */
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
 }
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -1058,9 +1061,9 @@ __device__ __forceinline__ uint32_t seq_lower_bound(const uint64_t *__restrict__
 template <bool PK>
 __global__ __launch_bounds__(256) void score_wave_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq,
-    const uint64_t *__restrict__ hit_mask, uint32_t tile_windows, uint4 *__restrict__ hot,
-    kgx_call *__restrict__ calls, uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count,
-    uint32_t *__restrict__ call_count, kgx_params prm, uint32_t want)
+    const uint64_t *__restrict__ hit_mask, uint32_t tile_windows, uint32_t wave_tiles, uint4 *__restrict__ hot,
+    kgx_call *__restrict__ calls, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
+    kgx_params prm, uint32_t want)
 {
     __shared__ ScoreQueue queues[4];
     typedef HitFields<PK> HF;
@@ -1072,7 +1075,7 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
     uint32_t *hw = reinterpret_cast<uint32_t *>(hot);
     const uint32_t lane = lane_id();
     const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t R = (uint64_t)tile_windows * SCORE_WAVE_TILES;
+    const uint64_t R = (uint64_t)tile_windows * wave_tiles;
     const uint64_t W = wbase[n_seq];
     const uint64_t x0 = (uint64_t)w * R;
     if (w > 0 && x0 >= W)
@@ -1090,10 +1093,8 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
     bool o_valid = false, o_span = false;
     uint32_t o_seq = NONE, o_cur = 0, o_cnt = 0, o_first = 0, o_last = 0, o_ncalls = 0;
     float o_wsum = 0.0f;
-    uint64_t o_gw0 = 0;
-    uint32_t p_pos = 0, p_fi = 0, p_fb = 0;
+    uint32_t p_pos = 0, p_fi = 0, p_fb = 0, p_at = 0;
     float p_wt = 0.0f;
-    uint64_t p_at = 0;
 
     /* OTU flags of an emitted sub-run that spans chunks: its hits are the
      * sequence's hits in windows [first, last]; the ones with fI == cur count */
@@ -1121,6 +1122,7 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
     auto close_open = [&]() -> bool {
         const bool em = (int)o_cnt >= prm.min_hits && o_wsum >= min_wh;
         if (em) {
+            const uint64_t gw0 = wbase[o_seq];
             if (want_calls && lane == 0) {
                 kgx_call cl;
                 cl.start = o_first;
@@ -1128,30 +1130,26 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
                 cl.count = (int32_t)o_cnt;
                 cl.function_index = o_cur;
                 cl.weighted_hits = o_wsum;
-                calls[o_gw0 + o_ncalls] = cl;
+                calls[gw0 + o_ncalls] = cl;
             }
             o_ncalls++;
             if (want_otu && o_span)
-                otu_fixup(o_gw0, o_first, o_last, o_cur);
+                otu_fixup(gw0, o_first, o_last, o_cur);
         }
         return em;
     };
 
-    uint32_t qhead = 0, qtail = 0;
+    uint32_t qhead = 0, qissue = 0, qtail = 0;
 
-    /* one chunk: queue entries [qhead, qhead + n), n <= 64 */
-    auto process_chunk = [&](uint32_t n) {
+    /* one chunk: queue entries [qhead, qhead + n), n <= 64, records in r */
+    auto process_chunk = [&](uint32_t n, const uint4 &r) {
         const uint32_t k = lane;
         const bool act = k < n;
         const uint64_t ACT = n >= 64 ? ~0ull : ((1ull << n) - 1);
         const uint32_t e = (qhead + k) & (SQ - 1);
         const uint32_t pos = act ? Q.pos[e] : 0u;
         const uint32_t seq = act ? Q.seq[e] : NONE;
-        const uint64_t gw0 = act ? Q.gw0[e] : 0ull;
-        const uint64_t at = act ? Q.at[e] : 0ull;
-        uint4 r = make_uint4(0, 0, 0, 0);
-        if (act)
-            r = hot[at];
+        const uint32_t at = act ? Q.at[e] : 0u;
         const uint32_t fi = HF::fi(r);
         const float wt = __uint_as_float(HF::wt(r));
         const uint32_t fb = HF::flag_base(r);
@@ -1167,8 +1165,7 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
         const bool brk = newseq || (ppos + gap < pos);
         const bool eqp = !brk && fi == pfi;
         const uint64_t M = __ballot(act && (brk || eqp));
-        const uint64_t mle = M & lanes_le(k);
-        const int jm = hibit(mle);
+        const int jm = hibit(M & lanes_le(k));
         uint32_t cur = __shfl(fi, jm < 0 ? 0 : jm);
         if (jm < 0)
             cur = o_cur;
@@ -1186,7 +1183,7 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
         if (SW & 1) {
             close_open();
             if (want_otu && lane == 0)
-                hw[4 * p_at + FD] = p_fb | F_RUN | F_CNT;
+                hw[4 * (uint64_t)p_at + FD] = p_fb | F_RUN | F_CNT;
             o_cur = rl32(fi, 0);
             o_cnt = 1;
             o_wsum = 0.0f + p_wt;
@@ -1255,17 +1252,15 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
             cl.count = (int32_t)c_seg;
             cl.function_index = fi;
             cl.weighted_hits = ws;
-            calls[gw0 + idx] = cl;
+            calls[wbase[seq] + idx] = cl;
         }
         /* sequences whose last hit is in this chunk (not its last lane) */
-        if (act && k + 1 < n && ((NS >> (k + 1)) & 1)) {
-            const uint32_t cc = idx + (uint32_t)((EMIT >> k) & 1);
-            call_count[seq] = want_calls ? cc : 0u;
-        }
+        if (act && k + 1 < n && ((NS >> (k + 1)) & 1))
+            call_count[seq] = want_calls ? idx + (uint32_t)((EMIT >> k) & 1) : 0u;
         if (want_otu && act) {
             const int bk = hibit(S & lanes_le(k));
             const bool em = bk >= 0 ? ((EMIT >> bk) & 1) != 0 : o_emitted;
-            hw[4 * at + FD] = fb | F_RUN | (memb ? F_CNT : 0u) | (memb && em ? F_OTU : 0u);
+            hw[4 * (uint64_t)at + FD] = fb | F_RUN | (memb ? F_CNT : 0u) | (memb && em ? F_OTU : 0u);
         }
 
         /* carry */
@@ -1273,7 +1268,6 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
             const uint32_t b = (uint32_t)b_open;
             o_valid = true;
             o_seq = rl32(seq, b);
-            o_gw0 = rl64(gw0, b);
             o_cur = rl32(fi, b);
             o_cnt = rl32(c_seg, b);
             o_wsum = rlf(ws, b);
@@ -1287,34 +1281,57 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
         p_fi = rl32(fi, l);
         p_wt = rlf(wt, l);
         p_fb = rl32(fb, l);
-        p_at = rl64(at, l);
+        p_at = rl32(at, l);
         qhead += n;
     };
 
+    /* records of the queued chunk in flight while the previous one is scored */
+    uint4 rpend = make_uint4(0, 0, 0, 0);
+    uint32_t npend = 0;
+    auto issue = [&](uint32_t n_new) { /* entries [qissue, qissue + n_new) */
+        wave_lds_sync();
+        uint4 r = make_uint4(0, 0, 0, 0);
+        if (lane < n_new)
+            r = hot[Q.at[(qissue + lane) & (SQ - 1)]];
+        if (npend)
+            process_chunk(npend, rpend);
+        rpend = r;
+        npend = n_new;
+        qissue += n_new;
+        wave_lds_sync();
+    };
+
     /* ---- walk the wave's sequences and their hit-mask words ---- */
-    uint32_t sb = s_lo; /* lane j: hit count of sequence sb + j */
+    uint32_t sb = NONE; /* Q.wb[j] = wbase[sb + j] */
+    uint32_t hb = s_lo; /* lane j: hit count of sequence hb + j */
     uint32_t vhc = 0;
+    uint64_t gb = ~0ull; /* Q.mw[j] = hit_mask[gb + j] */
     uint64_t pg = ~0ull, pfull = 0;
     uint32_t ppre = 0;
-    auto flush_counts = [&](uint32_t upto) { /* sequences [sb, upto) */
-        if (lane < upto - sb && vhc != NONE) {
-            hit_count[sb + lane] = vhc;
+    auto flush_counts = [&](uint32_t upto) { /* sequences [hb, upto) */
+        if (lane < upto - hb && vhc != NONE) {
+            hit_count[hb + lane] = vhc;
             if (vhc == 0 || !scoring)
-                call_count[sb + lane] = 0;
+                call_count[hb + lane] = 0;
         }
     };
     for (uint32_t s = s_lo; s < s_hi; s++) {
-        if (s + 1 - sb > 63) {
+        if (s - hb > 63) {
             flush_counts(s);
-            sb = s;
+            hb = s;
             vhc = 0;
         }
-        const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
-        if (gw1 - gw0 > (uint64_t)RUN_CAP) { /* the serial machine, on one lane */
+        if (sb == NONE || s + 1 - sb > 64) {
+            wave_lds_sync();
+            sb = s;
+            Q.wb[lane] = wbase[min(sb + lane, n_seq)];
             if (lane == 0)
-                score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count,
-                                   prm, want);
-            if (lane == s - sb)
+                Q.wb[64] = wbase[min(sb + 64, n_seq)];
+            wave_lds_sync();
+        }
+        const uint64_t gw0 = uni64(Q.wb[s - sb]), gw1 = uni64(Q.wb[s + 1 - sb]);
+        if (gw1 - gw0 > (uint64_t)RUN_CAP) { /* score_long_kernel's */
+            if (lane == s - hb)
                 vhc = NONE;
             continue;
         }
@@ -1322,7 +1339,13 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
         if (gw0 < gw1) {
             const uint64_t g0 = gw0 >> 6, g1 = (gw1 - 1) >> 6;
             for (uint64_t g = g0; g <= g1; g++) {
-                const uint64_t full = hit_mask[g];
+                if (gb == ~0ull || g - gb > 63) {
+                    wave_lds_sync();
+                    gb = g;
+                    Q.mw[lane] = (gb + lane) * 64 < W ? hit_mask[gb + lane] : 0ull;
+                    wave_lds_sync();
+                }
+                const uint64_t full = uni64(Q.mw[g - gb]);
                 if (g != pg) { /* hits of g's tile before word g */
                     if (pg != ~0ull && g == pg + 1)
                         ppre = g % J == 0 ? 0u : ppre + (uint32_t)__popcll(pfull);
@@ -1347,26 +1370,25 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
                     const uint32_t slot = (qtail + lanes_below(bits)) & (SQ - 1);
                     Q.pos[slot] = (uint32_t)(64 * g + lane - gw0);
                     Q.seq[slot] = s;
-                    Q.gw0[slot] = gw0;
-                    Q.at[slot] = (g / J) * tile_windows + ppre + lanes_below(full);
+                    Q.at[slot] = (uint32_t)((g / J) * tile_windows + ppre + lanes_below(full));
                 }
                 qtail += c;
-                if (qtail - qhead >= 64) {
-                    wave_lds_sync();
-                    process_chunk(64);
-                    wave_lds_sync();
-                }
+                if (qtail - qissue >= 64)
+                    issue(64);
             }
         }
-        if (lane == s - sb)
+        if (lane == s - hb)
             vhc = nh;
     }
     flush_counts(s_hi);
     if (!scoring)
         return;
-    wave_lds_sync();
-    while (qtail != qhead)
-        process_chunk(min(64u, qtail - qhead));
+    if (qtail != qissue)
+        issue(qtail - qissue);
+    if (npend) {
+        wave_lds_sync();
+        process_chunk(npend, rpend);
+    }
     if (o_valid) {
         close_open();
         if (lane == 0)
@@ -1374,35 +1396,55 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
     }
 }
 
+/* the sequences past RUN_CAP windows (the wave kernel leaves them): the
+ * lane machine, which keeps the reference's 40,000-hit cap */
+template <bool PK>
+__global__ __launch_bounds__(256) void score_long_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+    uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
+    uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
+    kgx_params prm, uint32_t want)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n_seq && wbase[s + 1] - wbase[s] > (uint64_t)RUN_CAP)
+        score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
+}
+
 hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *tile_seq, uint64_t max_tiles,
                         const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
                         uint32_t *hit_count, uint32_t *call_count, kgx_params params, uint32_t want,
-                        uint32_t hit_format, int variant, hipStream_t stream)
+                        uint32_t hit_format, int variant, uint32_t wave_tiles, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     const bool pk = hit_format == HIT_PACKED16;
-    if (variant == 1 && !params.order_constraint) {
-        const uint64_t waves = std::max<uint64_t>(1, (max_tiles + SCORE_WAVE_TILES - 1) / SCORE_WAVE_TILES);
+    const dim3 lanes((n_seq + 255) / 256);
+    /* the wave kernel keeps hit slots in 32 bits */
+    if (variant == 1 && !params.order_constraint && max_tiles * tile_windows < (1ull << 32)) {
+        wave_tiles = std::max<uint32_t>(1, wave_tiles);
+        const uint64_t waves = std::max<uint64_t>(1, (max_tiles + wave_tiles - 1) / wave_tiles);
         const dim3 grid((uint32_t)((waves + 3) / 4));
-        if (pk)
+        if (pk) {
             hipLaunchKernelGGL(score_wave_kernel<true>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
+                               tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want);
+            hipLaunchKernelGGL(score_long_kernel<true>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask,
                                tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
                                want);
-        else
+        } else {
             hipLaunchKernelGGL(score_wave_kernel<false>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
+                               tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want);
+            hipLaunchKernelGGL(score_long_kernel<false>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask,
                                tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
                                want);
+        }
         return hipGetLastError();
     }
     if (pk)
-        hipLaunchKernelGGL(score_kernel<true>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
-                           hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
-                           call_count, params, want);
+        hipLaunchKernelGGL(score_kernel<true>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot,
+                           calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want);
     else
-        hipLaunchKernelGGL(score_kernel<false>, dim3((n_seq + 255) / 256), dim3(256), 0, stream, n_seq, wbase,
-                           hit_mask, tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count,
-                           call_count, params, want);
+        hipLaunchKernelGGL(score_kernel<false>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows,
+                           hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want);
     return hipGetLastError();
 }
 

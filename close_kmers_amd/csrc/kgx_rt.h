@@ -291,7 +291,8 @@ struct kgx_ctx {
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
-    int score_variant = 1; /* 1 = wave-parallel scorer, 0 = one lane per sequence (option "score_variant") */
+    int score_variant = 0; /* 0 = one lane per sequence, 1 = wave-parallel scorer (option "score_variant") */
+    int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */
     uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */
     int microbench_ilp = 8;       /* independent reads in flight per lane */

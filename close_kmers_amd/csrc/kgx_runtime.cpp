@@ -981,6 +981,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->score_variant = (int)value;
         return KGX_OK;
     }
+    if (n == "score_wave_tiles") {
+        if (value < 1 || value > 256)
+            return fail(KGX_EINVAL, "score_wave_tiles must be 1..256");
+        c->score_wave_tiles = (int)value;
+        return KGX_OK;
+    }
     if (n == "probe_j") {
         if (!probe_j_supported((int)value))
             return fail(KGX_EINVAL, "probe_j must be 1, 2, 3, 4, 5 or 8");
@@ -1098,7 +1104,8 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(), c->max_tiles,
                          c->hit_mask.as<uint64_t>(), c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
-                         want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->score_variant, c->stream));
+                         want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->score_variant,
+                         (uint32_t)c->score_wave_tiles, c->stream));
     c->have_best = false;
     c->have_otus = false;
     if (want & KGX_WANT_OTU) {

@@ -287,8 +287,10 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
- * "score_variant" 1 (default) = the wave-parallel run scorer (ballots over a
- * wave's hits, sequential f32 sums only), 0 = one lane per sequence;
+ * "score_variant" 0 (default) = the run scorer with one lane per sequence,
+ * 1 = the wave-parallel scorer (ballots over 64 queued hits, serial f32 sums
+ * only; order_constraint 0, else variant 0; measured slower: DESIGN.md §4),
+ * "score_wave_tiles" (1..256, default 16) = probe tiles of windows per wave;
  * "fq_count" 1 (default) = the fq count pass scans stop codons one lane per
  * read, 0 = it translates like the emit pass (one wave per read);
  * "host_chunks" (1..64, default 6): kgx_process_batch splits a batch into up

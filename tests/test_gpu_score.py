@@ -1,5 +1,5 @@
-"""The wave-parallel run scorer (score_variant 1, the default) against the
-lane-per-sequence machine (score_variant 0) and the oracle: gather_hits /
+"""The wave-parallel run scorer (score_variant 1, an option; the default is
+the lane-per-sequence machine, score_variant 0) against the lane machine and the oracle: gather_hits /
 process_set_of_hits (kguts.cc:734-877) on hit-dense batches built to hit
 every rule -- gap breaks, pair switches with carry-over, runs that span many
 64-hit chunks, fragments whose hits share a chunk, empty and hitless
