@@ -425,6 +425,9 @@ KmerRequestRouter::Mapping KmerRequestRouter::mapping_for(const std::string &key
     /* krequest2.cc:416-425 creates unknown keys; the k-mer tables of every
      * mapping live on the first device */
     std::lock_guard<std::mutex> lk(mapping_mu_);
+    /* (the root mapping "" always exists and is not counted) */
+    if (mapping_map_.find(key) == mapping_map_.end() && mapping_map_.size() >= opt_.max_mappings + 1)
+        return Mapping{}; /* over the cap: no new mapping */
     auto &m = mapping_map_[key];
     if (!m.map) {
         m.map = std::make_shared<KmerPegMapping>(device_list(opt_)[0]);
@@ -475,7 +478,8 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             }
             if (std::regex_match(req.path, m, genus_re)) {
                 std::string id;
-                if (!mapping_for("").map->find_genus(m[1].str(), &id))
+                Mapping root = mapping_for("");
+                if (!root.map || !root.map->find_genus(m[1].str(), &id))
                     return respond(ver, 404, "Not Found", "genus not found\n");
                 return respond(ver, 200, "OK", id + "\n");
             }
@@ -562,6 +566,8 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             return respond(ver, 200, "OK", "data done\n");
 
         Mapping mp = mapping_for(key);
+        if (!mp.map)
+            return respond(ver, 503, "Service Unavailable", "too many mappings\n");
         /* /add and /matrix assign peg ids and read the device k-mer tables
          * of the mapping (its device: slot 0) -- one at a time per mapping;
          * /lookup and /fq_lookup only read the mapping, on any device */

@@ -121,6 +121,10 @@ public:
          * buckets) instead of loading kmer_data_dir/kmer.table.mem_map; the
          * directory still provides function.index and otu.index */
         uint64_t synthetic_keys = 0, synthetic_sigs = 0;
+        /* distinct /mapping/<key> keys that may be created besides the root
+         * mapping (each holds device k-mer tables); a request for a new key
+         * past the cap answers 503 */
+        size_t max_mappings = 1024;
     };
     explicit KmerRequestRouter(const Options &opt);
     ~KmerRequestRouter();

@@ -21,6 +21,15 @@
  *   --synthetic-image K:S     benchmark hook: a synthetic image of K keys in S
  *                             buckets built in HBM (kmer-data-dir still holds
  *                             function.index / otu.index)
+ *   --max-header-kb N         request line + headers cap (default 64 KiB;
+ *                             past it: 431 and the connection is closed)
+ *   --max-body-mb N           Content-length cap (default 4096; past it: 413)
+ *   --max-mappings N          /mapping/<key> keys that may be created (default
+ *                             1024; a new key past it: 503)
+ *
+ * The listener is unauthenticated and GET /quit stops it, as in the
+ * reference: bind it to a trusted interface (--bind 127.0.0.1) when the port
+ * is reachable from untrusted peers.
  *
  * One connection = one request, as in krequest2.cc: the request line and
  * headers are read, then Content-length bytes of body, the router builds the
@@ -73,14 +82,22 @@ bool write_all(int fd, const char *p, size_t n)
     return true;
 }
 
+/* request size limits (options --max-header-kb, --max-body-mb) */
+size_t g_max_header_bytes = 64 << 10;
+uint64_t g_max_body_bytes = 4ull << 30;
+constexpr size_t TOO_LONG = std::string::npos - 1;
+
 /* reads bytes into buf until it holds "\n" at or after `from`; returns the
- * position of that '\n' or npos at EOF/error */
+ * position of that '\n', npos at EOF/error, TOO_LONG once the request line
+ * and headers exceed g_max_header_bytes without one */
 size_t read_line(int fd, std::string &buf, size_t from)
 {
     for (;;) {
         size_t nl = buf.find('\n', from);
         if (nl != std::string::npos)
-            return nl;
+            return nl > g_max_header_bytes ? TOO_LONG : nl;
+        if (buf.size() > g_max_header_bytes)
+            return TOO_LONG;
         char tmp[65536];
         ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
         if (r < 0 && errno == EINTR)
@@ -95,7 +112,15 @@ void serve_connection(KmerRequestRouter &router, int fd)
 {
     std::string buf;
     HttpRequest req;
+    auto refuse = [&](int code, const char *status) {
+        const std::string resp = KmerRequestRouter::respond("1.1", code, status, std::string(status) + "\n");
+        write_all(fd, resp.data(), resp.size());
+        ::shutdown(fd, SHUT_WR);
+        ::close(fd);
+    };
     size_t nl = read_line(fd, buf, 0);
+    if (nl == TOO_LONG)
+        return refuse(431, "Request Header Fields Too Large");
     if (nl == std::string::npos) {
         ::close(fd);
         return;
@@ -112,6 +137,8 @@ void serve_connection(KmerRequestRouter &router, int fd)
     }
     for (;;) { /* headers up to the empty line */
         nl = read_line(fd, buf, pos);
+        if (nl == TOO_LONG)
+            return refuse(431, "Request Header Fields Too Large");
         if (nl == std::string::npos) {
             ::close(fd);
             return;
@@ -138,6 +165,8 @@ void serve_connection(KmerRequestRouter &router, int fd)
         } catch (...) {
             len = 0;
         }
+        if (len > g_max_body_bytes)
+            return refuse(413, "Payload Too Large");
         req.body = buf.substr(pos);
         while (req.body.size() < len) {
             char tmp[1 << 16];
@@ -212,7 +241,8 @@ int usage(const char *argv0)
                  "Usage: %s [options] listen-port kmer-data-dir\n"
                  "  --listen-port-file F  --n-kmer-threads N  --kmer-version V  --families-version V\n"
                  "  --families-genus-mapping F  --families-file F  --families-nr F [F ...]\n"
-                 "  --bind ADDR  --device N  --devices LIST  --synthetic-image KEYS:BUCKETS\n",
+                 "  --bind ADDR  --device N  --devices LIST  --synthetic-image KEYS:BUCKETS\n"
+                 "  --max-header-kb N  --max-body-mb N  --max-mappings N\n",
                  argv0);
     return 2;
 }
@@ -259,6 +289,18 @@ int main(int argc, char **argv)
         } else if (a == "--families-nr") { /* multitoken (kser.cc:65) */
             while (i + 1 < argc && argv[i + 1][0] != '-')
                 opt.families_nr.push_back(argv[++i]);
+        } else if (a == "--max-header-kb" || a == "--max-body-mb" || a == "--max-mappings") {
+            if (!value(v))
+                return usage(argv[0]);
+            const long long x = std::atoll(v.c_str());
+            if (x < 1)
+                return usage(argv[0]);
+            if (a == "--max-header-kb")
+                g_max_header_bytes = (size_t)x << 10;
+            else if (a == "--max-body-mb")
+                g_max_body_bytes = (uint64_t)x << 20;
+            else
+                opt.max_mappings = (size_t)x;
         } else if (a == "--bind") {
             if (!value(bind_addr))
                 return usage(argv[0]);

@@ -41,13 +41,14 @@ def test_server_usage_and_bad_data_dir():
 class Server:
     """A kgx_server on 127.0.0.1 with an ephemeral port."""
 
-    def __init__(self, data_dir, family_db=False, threads=2, devices=None):
+    def __init__(self, data_dir, family_db=False, threads=2, devices=None, extra=()):
         self.tmp = tempfile.TemporaryDirectory()
         port_file = os.path.join(self.tmp.name, "port")
         args = [_server_exe(), "--bind", "127.0.0.1", "--listen-port-file", port_file,
                 "--n-kmer-threads", str(threads), "--kmer-version", "kv1"]
         if devices:
             args += ["--devices", devices]
+        args += list(extra)
         if family_db:
             fq = os.path.join(GOLDEN, "fq")
             args += ["--families-genus-mapping", os.path.join(fq, FQ_FILES["genus"]),
@@ -74,12 +75,12 @@ class Server:
             time.sleep(0.05)
         assert self.port, "server did not start"
 
-    def request(self, method, path, body=b""):
+    def request(self, method, path, body=b"", headers=b"", length=None):
         with socket.create_connection(("127.0.0.1", self.port), timeout=120) as s:
             head = f"{method} {path} HTTP/1.1\r\nHost: x\r\n"
             if method == "POST":
-                head += f"Content-Length: {len(body)}\r\n"
-            s.sendall(head.encode() + b"\r\n" + body)
+                head += f"Content-Length: {len(body) if length is None else length}\r\n"
+            s.sendall(head.encode() + headers + b"\r\n" + body)
             out = b""
             while True:
                 chunk = s.recv(1 << 16)
@@ -367,5 +368,29 @@ def test_devices_replicas_serve_every_route(gpu, oracle_lib, tmp_path):
     try:
         got = srv.request("POST", "/fq_lookup", open(os.path.join(fq, "input.fasta"), "rb").read())
         assert got == HEADER + open(os.path.join(fq, "expected_fq_default.txt"), "rb").read()
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
+def test_request_size_and_mapping_caps(gpu):
+    """Oversized headers answer 431, an oversized Content-length 413 (before
+    any body is read), a new /mapping key past --max-mappings 503; the server
+    keeps serving afterwards."""
+    d = os.path.join(GOLDEN, "scoring")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(d, "data"), extra=["--max-header-kb", "4", "--max-body-mb", "1",
+                                                 "--max-mappings", "2"])
+    try:
+        r = srv.request("GET", "/version", headers=b"X-Big: " + b"a" * 8000 + b"\r\n")
+        assert r.startswith(b"HTTP/1.1 431 "), r[:80]
+        r = srv.request("POST", "/query", body=b"", length=2 << 20)
+        assert r.startswith(b"HTTP/1.1 413 "), r[:80]
+        ok = srv.request("POST", "/query", fasta)
+        assert ok.startswith(HEADER)
+        for key, code in (("a", b"200"), ("b", b"200"), ("a", b"200"), ("c", b"503")):
+            r = srv.request("POST", f"/mapping/{key}/add?silent=1", fasta)
+            assert r.startswith(b"HTTP/1.1 " + code), (key, r[:80])
+        assert srv.request("POST", "/query", fasta) == ok
     finally:
         srv.close()

@@ -12,6 +12,12 @@ krequest2.cc:41).  Each request is one connection, as in krequest2.cc.
 Reports per C the aggregate residues/s (residues in the bodies completed ÷
 wall time) and the request latency (median, p99).  Prints one JSON line.
 
+With --families N a synthetic family DB is loaded (families.tsv, genus.map
+and nr.fasta over source proteins 0..N-1 of the synthetic image; each family
+holds one protein) so that /lookup runs in family mode
+(lookup_request.cc:153-400), e.g.
+    python tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1"
+
 Everything on the path is timed: loopback TCP, the server's FASTA parse,
 the GPU pass (H2D, kernels, D2H of calls and OTU tallies), the text output.
 """
@@ -53,6 +59,31 @@ def fasta_bodies(res: np.ndarray, off: np.ndarray, body_bytes: int):
     return bodies, out
 
 
+GENERA = [("Escherichia", 561), ("Bacillus", 1386), ("Mycoplasma", 2093), ("Streptomyces", 1883)]
+
+
+def write_family_db(d: str, n: int) -> list:
+    """families.tsv / genus.map / nr.fasta (the golden fq data set's formats)
+    with family i = source protein i of the synthetic image."""
+    from close_kmers_amd import synth
+    with open(os.path.join(d, "genus.map"), "w") as f:
+        for g, t in GENERA:
+            f.write(f"{g}\t{t}\n")
+    with open(os.path.join(d, "families.tsv"), "w") as fam, open(os.path.join(d, "nr.fasta"), "wb") as nr:
+        for a in range(0, n, 20000):
+            ids = np.arange(a, min(n, a + 20000))
+            seqs = synth.ALPHA[synth.source_residue_codes(ids)]
+            for i, row in zip(ids, seqs):
+                g = GENERA[int(i) % len(GENERA)][0]
+                peg = f"fig|{1000 + int(i) % 97}.{int(i) % 7}.peg.{int(i)}"
+                fam.write(f"GF{int(i):08d}\t1\t1\t{peg}\t{len(row)}\tfunction {int(i) % 100000}\t100\t{g}\t100\n")
+                nr.write(b">" + peg.encode() + b"\n" + row.tobytes() + b"\n")
+    # (--families-nr takes every following non-option word: it goes after the positionals)
+    return (["--families-genus-mapping", os.path.join(d, "genus.map"),
+             "--families-file", os.path.join(d, "families.tsv")],
+            ["--families-nr", os.path.join(d, "nr.fasta")])
+
+
 def post(port: int, path: str, body: bytes) -> bytes:
     with socket.create_connection(("127.0.0.1", port), timeout=300) as s:
         s.sendall(b"POST %s HTTP/1.1\r\nContent-Length: %d\r\n\r\n" % (path.encode(), len(body)) + body)
@@ -74,6 +105,7 @@ def main():
     ap.add_argument("--body-bytes", type=int, default=1 << 20)
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--path", default="/query")
+    ap.add_argument("--families", type=int, default=0, help="synthetic family DB over this many source proteins")
     args = ap.parse_args()
     from close_kmers_amd import build as kbuild
     from close_kmers_amd import image_files, synth
@@ -86,10 +118,13 @@ def main():
     image_files.write_index(os.path.join(tmp.name, "function.index"), [f"function {i}" for i in range(100000)])
     image_files.write_index(os.path.join(tmp.name, "otu.index"), ["otu0"])
     port_file = os.path.join(tmp.name, "port")
+    fam_pre, fam_post = [], []
+    if args.families:
+        fam_pre, fam_post = write_family_db(tmp.name, min(args.families, spec.n_src))
     t0 = time.time()
     srv = subprocess.Popen([kbuild.SERVER, "--bind", "127.0.0.1", "--listen-port-file", port_file,
                             "--n-kmer-threads", str(args.threads),
-                            "--synthetic-image", f"{spec.n_keys}:{spec.num_sigs}", "0", tmp.name],
+                            "--synthetic-image", f"{spec.n_keys}:{spec.num_sigs}"] + fam_pre + ["0", tmp.name] + fam_post,
                            stderr=subprocess.PIPE)
     port = None
     while time.time() - t0 < 300:
@@ -142,6 +177,7 @@ def main():
             "metric": "HTTP serving residues/s through kgx_server (kser drop-in), C2 image",
             "value": best["residues_per_s"], "unit": "residues/s",
             "config": {"n_keys": spec.n_keys, "num_sigs": spec.num_sigs, "path": args.path,
+                       "families": args.families,
                        "body_bytes": args.body_bytes, "proteins_per_body": round(args.n_seq / len(bodies), 1),
                        "server_threads": args.threads, "startup_s": startup_s},
             "by_clients": rows,

@@ -1,0 +1,113 @@
+/*
+ * facade_bench -- what the unchanged per-sequence drop-in costs: the
+ * reference's handler loop calls KmerGuts::process_aa_seq once per sequence
+ * (lookup_request.cc:153-172, query_request.cc:103-151); through the facade
+ * each call is one GPU round trip.  Times that call on single 300-aa C2
+ * proteins (latency distribution) and the same sequences through
+ * process_aa_batch (one pass), with the lookup handler's outputs (calls + a
+ * hit callback, no OTU stats).
+ *
+ *   facade_bench KMER_DIR N_KEYS NUM_SIGS QUERIES.bin [N_CALLS]
+ *
+ * QUERIES.bin: uint64 n, uint64 offsets[n+1], residues.  Prints one JSON line.
+ */
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kguts_hip.h"
+
+using clk = std::chrono::steady_clock;
+
+static double pct(std::vector<double> v, double p)
+{
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(p / 100.0 * (double)v.size()))];
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 5) {
+        std::fprintf(stderr, "usage: facade_bench KMER_DIR N_KEYS NUM_SIGS QUERIES.bin [N_CALLS]\n");
+        return 2;
+    }
+    const std::string dir = argv[1];
+    const uint64_t n_keys = std::strtoull(argv[2], nullptr, 10), num_sigs = std::strtoull(argv[3], nullptr, 10);
+    const size_t n_calls = argc > 5 ? std::strtoull(argv[5], nullptr, 10) : 2000;
+    std::ifstream in(argv[4], std::ios::binary);
+    uint64_t n = 0;
+    in.read(reinterpret_cast<char *>(&n), 8);
+    std::vector<uint64_t> off(n + 1);
+    in.read(reinterpret_cast<char *>(off.data()), (std::streamsize)(8 * (n + 1)));
+    std::string res(off[n], '\0');
+    in.read(&res[0], (std::streamsize)res.size());
+    if (!in) {
+        std::fprintf(stderr, "facade_bench: short query file\n");
+        return 2;
+    }
+    kgx_image *img = nullptr;
+    uint64_t stored = 0;
+    if (kgx_image_build_synthetic(n_keys, num_sigs, 0, &img, &stored) != KGX_OK) {
+        std::fprintf(stderr, "facade_bench: %s\n", kgx_last_error());
+        return 1;
+    }
+    auto image = std::make_shared<kgx::KmerImage>(img);
+    kgx::KmerGuts kg(dir, image);
+    const size_t m = std::min<size_t>(n, n_calls);
+    std::vector<std::string> seqs(m);
+    for (size_t i = 0; i < m; i++)
+        seqs[i] = res.substr(off[i], off[i + 1] - off[i]);
+
+    /* unbatched: one process_aa_seq per sequence, as the reference's loop */
+    uint64_t hits = 0, calls = 0, residues = 0;
+    std::vector<double> lat;
+    lat.reserve(m);
+    for (int warm = 0; warm < 20; warm++) {
+        auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+        kg.process_aa_seq("w", seqs[warm % m], cv, [](kgx::KmerGuts::hit_in_sequence_t) {}, nullptr);
+    }
+    const auto t_all = clk::now();
+    for (size_t i = 0; i < m; i++) {
+        auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+        const auto t0 = clk::now();
+        kg.process_aa_seq("q", seqs[i], cv, [&](kgx::KmerGuts::hit_in_sequence_t) { hits++; }, nullptr);
+        lat.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+        calls += cv->size();
+        residues += seqs[i].size();
+    }
+    const double t_seq = std::chrono::duration<double>(clk::now() - t_all).count();
+
+    /* the same sequences, one process_aa_batch */
+    uint64_t bhits = 0, bcalls = 0;
+    std::vector<double> tb;
+    for (int rep = 0; rep < 6; rep++) {
+        std::vector<kgx::KmerGuts::SeqJob> jobs(m);
+        for (size_t i = 0; i < m; i++) {
+            jobs[i].id = "q";
+            jobs[i].seq = seqs[i];
+            jobs[i].calls = std::make_shared<std::vector<kgx::KmerCall>>();
+            jobs[i].hit_cb = [&](kgx::KmerGuts::hit_in_sequence_t) { bhits++; };
+        }
+        const auto t0 = clk::now();
+        kg.process_aa_batch(jobs);
+        tb.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+        if (rep == 0)
+            for (auto &j : jobs)
+                bcalls += j.calls->size();
+    }
+    const double t_batch = pct(tb, 50);
+    std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
+                "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
+                "\"unbatched_residues_per_s\": %.4g, \"batched\": {\"sequences\": %zu, \"ms\": %.3f, "
+                "\"residues_per_s\": %.4g}, \"hits\": %llu, \"calls_out\": %llu, \"batch_hits_per_rep\": %llu, "
+                "\"batch_calls\": %llu, \"keys_stored\": %llu}\n",
+                m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, (double)residues / t_seq, m,
+                t_batch * 1e3, (double)residues / t_batch, (unsigned long long)hits, (unsigned long long)calls,
+                (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored);
+    return hits * 6 == bhits && calls == bcalls ? 0 : 3;
+}
