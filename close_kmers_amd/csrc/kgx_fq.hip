@@ -501,270 +501,6 @@ __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases
     }
 }
 
-/*
- * 3'. Emit, one LANE per read.  The wave's reads are staged in LDS as for the
- * count pass; each lane turns its read (<= 256 bases) into a nibble string
- * (registers, then its own LDS row) and its forward / reverse stop masks,
- * walks each frame's stops in codon order (frame -k: descending forward
- * position), and for every kept run writes the fragment record and its
- * residues, translating each kept codon once from the nibble string
- * (NCBI table 11 in LDS).  A wave holding a longer read, or whose span does
- * not fit, runs the wave-per-read code (emit_group) over its 64 reads.
- */
-constexpr uint32_t LANE_READ_MAX = 256;
-
-/* the old emit body over reads [r0, r0 + n), n <= 16, at running bases F, R */
-__device__ __forceinline__ void emit_group(uint32_t (*slots)[NIB_WORDS], const char *code, const uint8_t *bases,
-                                           const uint64_t *read_off, uint64_t r0, uint32_t n, uint64_t &F,
-                                           uint64_t &R, uint32_t lane, uint32_t *n_frag, uint32_t *frag_base,
-                                           uint8_t *out_res, uint64_t *out_off, uint32_t *out_read,
-                                           int8_t *out_frame, uint32_t *out_start)
-{
-    const uint64_t my_off = n && lane <= n ? read_off[r0 + lane] : 0;
-    stage_wave_reads(slots, bases, my_off, n, lane);
-    for (uint32_t j = 0; j < n; j++) {
-        const uint64_t r = r0 + j;
-        const uint64_t ob = uniform_u64(__shfl(my_off, (int)j)), oe = uniform_u64(__shfl(my_off, (int)j + 1));
-        const uint64_t len = oe - ob;
-        uint32_t my_nf = 0;
-        uint64_t my_fb = 0;
-        if (len <= SHORT_READ) {
-            char aas[6];
-            uint64_t stops[6];
-            translate6(slots[j], code, read_mis(bases + ob), (uint32_t)len, lane, aas, stops);
-#pragma unroll
-            for (uint32_t f = 0; f < 6; f++) {
-                const char aa = aas[f];
-                const uint64_t kept = kept_runs(stops[f]);
-                const uint64_t starts = kept & ~(kept << 1);
-                if (lane == f) {
-                    my_nf = (uint32_t)__popcll(starts);
-                    my_fb = F;
-                }
-                const uint64_t ri = R + popc_below(kept);
-                if ((kept >> lane) & 1)
-                    out_res[ri] = (uint8_t)aa;
-                if ((starts >> lane) & 1) {
-                    const uint64_t fi = F + popc_below(starts);
-                    out_off[fi] = ri;
-                    out_read[fi] = (uint32_t)r;
-                    out_frame[fi] = (int8_t)frame_of(f);
-                    out_start[fi] = lane;
-                }
-                F += (uint64_t)__popcll(starts);
-                R += (uint64_t)__popcll(kept);
-            }
-        } else {
-            uint32_t frags = 0;
-            uint64_t res = 0;
-            const FrameReader fr{bases + ob, len, frame_of(lane < 6 ? lane : 0)};
-            if (lane < 6)
-                frame_serial(fr, 0, 0, 0, frags, res, nullptr, nullptr, nullptr, nullptr, nullptr);
-            uint64_t ef = lane < 6 ? frags : 0, er = lane < 6 ? res : 0;
-            for (uint32_t o = 1; o < 8; o <<= 1) {
-                const uint64_t xf = __shfl_up(ef, o), xr = __shfl_up(er, o);
-                if (lane >= o) {
-                    ef += xf;
-                    er += xr;
-                }
-            }
-            const uint64_t tf = __shfl(ef, 5), tr = __shfl(er, 5);
-            ef -= lane < 6 ? frags : 0;
-            er -= lane < 6 ? res : 0;
-            if (lane < 6) {
-                frame_serial(fr, (uint32_t)r, F + ef, R + er, frags, res, out_res, out_off, out_read, out_frame,
-                             out_start);
-                my_nf = frags;
-                my_fb = F + ef;
-            }
-            F += tf;
-            R += tr;
-        }
-        if (lane < 6) {
-            n_frag[r * 6 + lane] = my_nf;
-            frag_base[r * 6 + lane] = (uint32_t)my_fb;
-        }
-    }
-}
-
-/* a kept run of frame f: codons [a, b).  ns: the wave's nibble string (byte
- * o of the staged span at bits 4o); the read's base p is nibble loc + p */
-struct LaneEmit {
-    const uint32_t *ns;
-    const char *code;
-    uint32_t loc, len, r;
-    uint64_t F, R;
-    uint32_t *out_read, *out_start;
-    uint64_t *out_off;
-    int8_t *out_frame;
-    uint8_t *out_res;
-    /* codon k of frame f -> residue */
-    __device__ __forceinline__ uint8_t aa(uint32_t f, uint32_t k) const
-    {
-        /* lowest forward base of the codon */
-        const uint32_t P = loc + (f < 3 ? f + 3 * k : len - 3 - (f - 3) - 3 * k);
-        const uint32_t x = __builtin_amdgcn_alignbit(ns[(P >> 3) + 1], ns[P >> 3], (P & 7u) * 4u);
-        const uint32_t idx = f < 3 ? (((x & 3u) << 4) | ((x >> 2) & 0xCu) | ((x >> 8) & 3u))
-                                   : ((((x >> 4) & 0x30u) | ((x >> 2) & 0xCu) | (x & 3u)) ^ 0x3Fu);
-        return (uint8_t)code[(x & 0x444u) ? 64u : idx];
-    }
-    __device__ __forceinline__ void run(uint32_t f, uint32_t a, uint32_t b, uint32_t &nfr)
-    {
-        if (b < a + MIN_FRAGMENT)
-            return;
-        out_off[F] = R;
-        out_read[F] = r;
-        out_frame[F] = (int8_t)frame_of(f);
-        out_start[F] = a;
-        for (uint32_t k = a; k < b; k++)
-            out_res[R++] = aa(f, k);
-        F++;
-        nfr++;
-    }
-};
-
-constexpr uint32_t NS_WORDS = COUNT_SPAN / 8 + 16; /* the nibble string of a COUNT_SPAN-byte span + slack */
-
-__global__ __launch_bounds__(256) void fq_emit_lane_kernel(const uint8_t *bases, const uint64_t *read_off,
-                                                           uint32_t n_reads, const uint2 *read_counts,
-                                                           const ulonglong2 *tile_base, uint32_t n_tiles,
-                                                           uint32_t *n_frag, uint32_t *frag_base, uint8_t *out_res,
-                                                           uint64_t *out_off, uint32_t *out_read, int8_t *out_frame,
-                                                           uint32_t *out_start)
-{
-    __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
-    __shared__ char code[68];
-    if (threadIdx.x < 65)
-        code[threadIdx.x] = kCode11[threadIdx.x];
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x * WAVES_PER_WG + wv;
-    if (tile >= n_tiles)
-        return;
-    uint32_t *ns = nspan[wv];
-    const uint64_t r0 = (uint64_t)tile * FQ_TILE;
-    const uint32_t n = (uint32_t)std::min<uint64_t>(FQ_TILE, n_reads - r0);
-    const uint64_t r = r0 + lane;
-    const bool act = lane < n;
-    /* this read's fragment / residue bases: the tile's base + the earlier reads' counts */
-    const uint2 c = act ? read_counts[r] : make_uint2(0, 0);
-    uint64_t pf = c.x, pr = c.y;
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint64_t xf = __shfl_up(pf, o), xr = __shfl_up(pr, o);
-        if (lane >= o) {
-            pf += xf;
-            pr += xr;
-        }
-    }
-    const ulonglong2 tb = tile_base[tile];
-    pf = tb.x + pf - c.x;
-    pr = tb.y + pr - c.y;
-    const uint64_t ob = act ? read_off[r] : 0, oe = act ? read_off[r + 1] : 0;
-    const uint32_t len = (uint32_t)(oe - ob);
-    const uint64_t first = uniform_u64(__shfl(ob, 0)), end = uniform_u64(__shfl(oe, (int)n - 1));
-    const uintptr_t a = reinterpret_cast<uintptr_t>(bases + first) & ~(uintptr_t)15;
-    const uint64_t bytes = reinterpret_cast<uintptr_t>(bases + end) - a;
-    const bool staged = end > first && bytes <= COUNT_SPAN;
-    const bool lane_path = staged && __ballot(act && oe - ob > LANE_READ_MAX) == 0;
-    if (!lane_path) { /* the wave-per-read code, 16 reads at a time */
-        uint64_t F = uniform_u64(__shfl(pf, 0)), R = uniform_u64(__shfl(pr, 0));
-        for (uint32_t g = 0; g < n; g += FQ_READS_PER_WAVE)
-            emit_group(reinterpret_cast<uint32_t (*)[NIB_WORDS]>(ns), code, bases, read_off, r0 + g,
-                       std::min<uint32_t>(FQ_READS_PER_WAVE, n - g), F, R, lane, n_frag, frag_base, out_res,
-                       out_off, out_read, out_frame, out_start);
-        return;
-    }
-    /* the span as a nibble string: 16 bytes per lane per round, coalesced */
-    const uint4 *src = reinterpret_cast<const uint4 *>(a);
-    const uint32_t nv = (uint32_t)((bytes + 15) / 16);
-    for (uint32_t i = lane; i < nv + 1; i += 64) { /* (+1: a zero pad for the funnel shifts) */
-        const uint4 v = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
-        ns[2 * i] = nibbles4(v.x) | nibbles4(v.y) << 16;
-        ns[2 * i + 1] = nibbles4(v.z) | nibbles4(v.w) << 16;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!act)
-        return;
-    const uint32_t loc = (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a);
-    /* stop masks, 64 bases a block: bit q = a stop codon ending at base q */
-    uint64_t EF[4], ER[4];
-    uint32_t hist = 0x444;
-    const uint32_t sh = (loc & 7u) * 4u;
-#pragma unroll
-    for (uint32_t blk = 0; blk < 4; blk++) {
-        uint64_t ef = 0, er = 0;
-        if (64 * blk < len) {
-            const uint32_t w0 = (loc + 64 * blk) >> 3;
-            uint32_t d[9];
-#pragma unroll
-            for (uint32_t i = 0; i < 9; i++)
-                d[i] = ns[w0 + i];
-#pragma unroll
-            for (uint32_t i = 0; i < 8; i++) {
-                const uint32_t x = __builtin_amdgcn_alignbit(d[i + 1], d[i], sh); /* bases 64 blk + 8i .. +7 */
-#pragma unroll
-                for (uint32_t j = 0; j < 8; j++) {
-                    hist = ((hist << 4) | ((x >> (4 * j)) & 0xFu)) & 0xFFFu;
-                    const uint32_t fs = hist == 0x300u || hist == 0x302u || hist == 0x320u;
-                    const uint32_t rs = hist == 0x330u || hist == 0x130u || hist == 0x310u;
-                    ef |= (uint64_t)fs << (8 * i + j);
-                    er |= (uint64_t)rs << (8 * i + j);
-                }
-            }
-            const uint32_t left = len - 64 * blk;
-            const uint64_t in = left >= 64 ? ~0ull : ((1ull << left) - 1);
-            ef &= in;
-            er &= in;
-        }
-        EF[blk] = ef;
-        ER[blk] = er;
-    }
-    LaneEmit em{ns, code, loc, len, (uint32_t)r, pf, pr, out_read, out_start, out_off, out_frame, out_res};
-#pragma unroll
-    for (uint32_t f = 0; f < 6; f++) {
-        const uint64_t fb = em.F;
-        uint32_t nfr = 0;
-        const uint32_t off = f < 3 ? f : f - 3;
-        const uint32_t nc = len >= off ? (len - off) / 3 : 0;
-        uint32_t next = 0; /* first codon of the current run */
-        if (f < 3) {
-            /* codon k ends at base q = f + 2 + 3k: ascending q */
-            const uint32_t rho = (f + 2) % 3;
-#pragma unroll
-            for (uint32_t w = 0; w < 4; w++) {
-                uint64_t m = EF[w] & (EVERY3 << ((rho + 3 - w % 3) % 3));
-                while (m) {
-                    const uint32_t q = 64 * w + (uint32_t)__builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint32_t k = (q - f - 2) / 3;
-                    em.run(f, next, k, nfr);
-                    next = k + 1;
-                }
-            }
-        } else {
-            /* codon k ends at base q = len - 1 - off - 3k: descending q */
-            const int top = (int)len - 1 - (int)off;
-            const uint32_t rho = (uint32_t)((top % 3 + 3) % 3);
-#pragma unroll
-            for (int w = 3; w >= 0; w--) {
-                uint64_t m = ER[w] & (EVERY3 << ((rho + 3 - (uint32_t)w % 3) % 3));
-                while (m) {
-                    const uint32_t bt = 63u - (uint32_t)__clzll((long long)m);
-                    m &= ~(1ull << bt);
-                    const uint32_t k = (uint32_t)(top - (int)(64 * w + bt)) / 3;
-                    em.run(f, next, k, nfr);
-                    next = k + 1;
-                }
-            }
-        }
-        em.run(f, next, nc, nfr);
-        n_frag[r * 6 + f] = nfr;
-        frag_base[r * 6 + f] = (uint32_t)fb;
-    }
-}
-
 struct PairSum {
     __host__ __device__ ulonglong2 operator()(const ulonglong2 &a, const ulonglong2 &b) const
     {
@@ -934,13 +670,7 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
                                               make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
     hipLaunchKernelGGL(fq_tail_kernel, dim3(1), dim3(1), 0, st, tile_base, n_tiles, n_reads, totals,
                        c->fq_off.as<uint64_t>(), c->fq_fbase.as<uint32_t>(), c->fq_nfrag.as<uint32_t>());
-    if (n_reads && c->fq_emit)
-        hipLaunchKernelGGL(fq_emit_lane_kernel, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
-                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_base, (uint32_t)n_tiles,
-                           c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(), c->fq_res.as<uint8_t>(),
-                           c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(), c->fq_frame.as<int8_t>(),
-                           c->fq_start.as<uint32_t>());
-    else if (n_reads)
+    if (n_reads)
         hipLaunchKernelGGL(fq_emit_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            read_counts, tile_base, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
                            c->fq_res.as<uint8_t>(), c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(),

@@ -290,7 +290,6 @@ struct kgx_ctx {
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
-    int fq_emit = 0;       /* fq emit pass: 0 = wave per read, 1 = lane per read (measured slower: scattered byte stores) */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
     int score_variant = 0; /* 0 = one lane per sequence, 1 = wave-parallel scorer (option "score_variant") */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */

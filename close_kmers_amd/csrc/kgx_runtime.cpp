@@ -975,12 +975,6 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->fq_count = (int)value;
         return KGX_OK;
     }
-    if (n == "fq_emit") {
-        if (value != 0 && value != 1)
-            return fail(KGX_EINVAL, "fq_emit must be 0 or 1");
-        c->fq_emit = (int)value;
-        return KGX_OK;
-    }
     if (n == "score_variant") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "score_variant must be 0 or 1");

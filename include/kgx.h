@@ -293,9 +293,6 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "score_wave_tiles" (1..256, default 16) = probe tiles of windows per wave;
  * "fq_count" 1 (default) = the fq count pass scans stop codons one lane per
  * read, 0 = it translates like the emit pass (one wave per read);
- * "fq_emit" 0 (default) = the fq emit pass runs one wave per read, 1 = one
- * lane per read (reads up to 256 bases; a wave with a longer read runs the
- * wave-per-read code; measured slower: DESIGN.md §7b);
  * "host_chunks" (1..64, default 6): kgx_process_batch splits a batch into up
  * to this many residue-balanced chunks of whole sequences (at least 2M
  * residues each; with "host_taper" 1, the default, the first and last are

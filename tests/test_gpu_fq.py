@@ -42,12 +42,10 @@ def test_fragments_match_oracle(gpu, oracle_lib):
     assert n == f.n_fragments and n > 500
 
 
-@pytest.mark.parametrize("fq_count,fq_emit,max_len", [(0, 0, 1000), (1, 1, 1000), (1, 0, 1000), (0, 1, 1000),
-                                                        (1, 1, 257), (1, 1, 200)])
-def test_fragments_long_reads_both_count_passes(gpu, oracle_lib, fq_count, fq_emit, max_len):
-    """Both count passes (lane-per-read stop scan / wave translation) and both
-    emit passes (lane per read with the wave fallback / wave per read) give
-    the oracle's fragments: reads of 0-1000 bases (several 64-base blocks
+@pytest.mark.parametrize("fq_count,max_len", [(0, 1000), (1, 1000), (1, 257), (1, 200)])
+def test_fragments_long_reads_both_count_passes(gpu, oracle_lib, fq_count, max_len):
+    """Both count passes (lane-per-read stop scan / wave translation) give
+    the emit pass the offsets that reproduce the oracle's fragments: reads of 0-1000 bases (several 64-base blocks
     of the stop scan, the emit's serial path past 194 bases), stop-rich and
     IUPAC-laden, at every start alignment."""
     spec, table = synthetic_table(20000)
@@ -61,7 +59,6 @@ def test_fragments_long_reads_both_count_passes(gpu, oracle_lib, fq_count, fq_em
     res, off = pack([("r", r) for r in reads])
     with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
         ctx.set_option("fq_count", fq_count)
-        ctx.set_option("fq_emit", fq_emit)
         f = ctx.fq_fragments(res, off)
         h = ctx.fragments_to_host(f)
     got = {}
