@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
+    ap.add_argument("--probe-lds-kb", type=int, default=-1, help="LDS KB reserved per probe workgroup (-1 = default)")
     ap.add_argument("--score-variant", type=int, default=0, help="0 = lane per sequence (default), 1 = wave-parallel run scorer")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
@@ -221,6 +222,8 @@ def main():
     ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
     for c in ctxs:
         c.set_option("score_variant", args.score_variant)
+        if args.probe_lds_kb >= 0:
+            c.set_option("probe_lds_kb", args.probe_lds_kb)
     score_ms: list = []  # score stage (+ best/OTU kernels with --want), same untimed pass as probe_ms
 
     def step(timed_probe: list | None, c=ctx, b=0):
@@ -436,7 +439,7 @@ def main():
                 "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
                 "worker_contexts": len(ctxs), "distinct_batches": len(batches),
                 "hits_total": total_hits,
-                "score_variant": args.score_variant,
+                "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb,
                 # the score stage alone (HIP events on the context's stream, same
                 # untimed pass as the probe time): what a single-context caller pays
                 "score_stage_ms": float(np.mean(score_ms)) if score_ms else None,

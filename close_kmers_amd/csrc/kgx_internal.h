@@ -152,7 +152,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2_words,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        hipStream_t stream);
+                        uint32_t lds_kb, hipStream_t stream);
 /* set the filter bits of every stored key of the resident table */
 hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
                                uint32_t log2_words, hipStream_t stream);

@@ -549,9 +549,9 @@ template <int J, int G>
 static void launch_probe_line(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                               const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
                               uint32_t n_seq, const void *table, uint64_t num_sigs, uint4 *hot, uint4 *cold,
-                              uint64_t *hit_mask)
+                              uint64_t *hit_mask, uint32_t dyn_lds)
 {
-    hipLaunchKernelGGL((probe_line_kernel<J, G>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
+    hipLaunchKernelGGL((probe_line_kernel<J, G>), grid, dim3(64 * PROBE_WAVES), dyn_lds, stream, residues,
                        n_residues, seq_off, wbase, tile_seq, n_seq, static_cast<const uint4 *>(table),
                        num_sigs, mod_magic(num_sigs), hot, cold, hit_mask);
 }
@@ -599,17 +599,21 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        hipStream_t stream)
+                        uint32_t lds_kb, hipStream_t stream)
 {
     if (max_tiles == 0)
         return hipSuccess;
+    /* lds_kb > 0: each probe workgroup reserves that much LDS (unused beyond
+     * its own ~9 KB), capping the probe at 160 / lds_kb workgroups per CU so
+     * that other contexts' kernels find room beside it */
+    const uint32_t dyn_lds = lds_kb * 1024u > 9216u ? lds_kb * 1024u - 9216u : 0u;
     const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
     if (variant == PROBE_AUTO && layout == KGX_LAYOUT_PACKED16 && !filter)
         variant = PROBE_LINE;
     if ((variant == PROBE_LINE || variant == PROBE_LINE8) && layout == KGX_LAYOUT_PACKED16 && !filter) {
 #define KGX_LINE(JJ, GG)                                                                             \
     launch_probe_line<JJ, GG>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
-                              num_sigs, hot, cold, hit_mask);                                        \
+                              num_sigs, hot, cold, hit_mask, dyn_lds);                               \
     return hipGetLastError()
         const int key = probe_j * 10 + (variant == PROBE_LINE8 ? 8 : 4);
         switch (key) {

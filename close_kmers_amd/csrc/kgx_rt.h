@@ -290,6 +290,7 @@ struct kgx_ctx {
     /* tuning options */
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
+    int probe_lds_kb = 0;  /* LDS reserved per probe workgroup, caps its occupancy (option "probe_lds_kb") */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
     int score_variant = 0; /* 0 = one lane per sequence, 1 = wave-parallel scorer (option "score_variant") */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */

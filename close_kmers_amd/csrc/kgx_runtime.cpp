@@ -981,6 +981,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->score_variant = (int)value;
         return KGX_OK;
     }
+    if (n == "probe_lds_kb") {
+        if (value < 0 || value > 160)
+            return fail(KGX_EINVAL, "probe_lds_kb must be 0..160");
+        c->probe_lds_kb = (int)value;
+        return KGX_OK;
+    }
     if (n == "score_wave_tiles") {
         if (value < 1 || value > 256)
             return fail(KGX_EINVAL, "score_wave_tiles must be 1..256");
@@ -1079,7 +1085,7 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
                          c->img->layout, c->img->num_sigs,
                          c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                          c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
-                         (int)(c->tile_windows / 64), c->probe_variant, c->stream));
+                         (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb, c->stream));
     if (c->probe_serialize) {
         HIP_TRY(hipEventRecord(c->probe_done, c->stream));
         img->last_probe = c->probe_done;

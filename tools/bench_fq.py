@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts alternating over chunks")
     ap.add_argument("--score-variant", type=int, default=-1, help="-1 = the library default")
+    ap.add_argument("--probe-lds-kb", type=int, default=-1, help="-1 = the library default")
     args = ap.parse_args()
 
     from close_kmers_amd import abi, image_files, synth
@@ -61,9 +62,11 @@ def main():
     # worker contexts (own stream + buffers), as for bench.py: one chunk's
     # host-side sizing sync overlaps the other context's kernels
     ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
-    if args.score_variant >= 0:
-        for c in ctxs:
+    for c in ctxs:
+        if args.score_variant >= 0:
             c.set_option("score_variant", args.score_variant)
+        if args.probe_lds_kb >= 0:
+            c.set_option("probe_lds_kb", args.probe_lds_kb)
     n, Lr = args.n_reads, args.length
     rng = np.random.default_rng(0x5EED0004)
     bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
@@ -126,7 +129,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "score_variant": args.score_variant, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),
