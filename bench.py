@@ -392,13 +392,8 @@ def main():
     if d.rank == 0:
         windows_per_launch = n * max(0, Ls - 8)  # x_permille = 0: every window is probed
         pbar = cpu["pbar"] if cpu else None
+        pbar_source = "measured (CPU baseline leg, this run)" if pbar is not None else None
         probe_s = float(np.mean(probe_ms)) / 1e3
-        if pbar is None:
-            # alpha = stored / num_sigs; linear probing, unsuccessful search
-            a = stored / spec.num_sigs
-            pbar = 0.5 * (1 + 1 / (1 - a) ** 2)
-        alg_bytes = windows_per_launch * (24.0 * pbar + 1.0)
-        achieved = alg_bytes / probe_s
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
@@ -406,8 +401,18 @@ def main():
                 if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
                         and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    if pbar is None and tj.get("pbar_measured"):
+                        pbar = tj["pbar_measured"]  # the same workload's P measured by an earlier run
+                        pbar_source = f"measured earlier on this workload ({os.path.basename(args.traffic_json)})"
             except Exception:
                 traffic = None
+        if pbar is None:
+            # alpha = stored / num_sigs; linear probing, unsuccessful search (an upper bound)
+            a = stored / spec.num_sigs
+            pbar = 0.5 * (1 + 1 / (1 - a) ** 2)
+            pbar_source = "analytic: linear probing, unsuccessful search (upper bound)"
+        alg_bytes = windows_per_launch * (24.0 * pbar + 1.0)
+        achieved = alg_bytes / probe_s
         residues_per_step_job = n_global * Ls  # every rank's shard of every step
         value = residues_per_step_job * args.steps / t_max
         if args.strong:
@@ -458,6 +463,7 @@ def main():
                 "windows_per_launch": windows_per_launch,
                 "alg_bytes_per_launch": alg_bytes,
                 "pbar": pbar,
+                "pbar_source": pbar_source,
                 "random_read_ceiling": ceiling,
                 "probe_ab": probe_ab,
                 # SURVEY §8(d) prices a bucket at the file's 24 B; the PACKED16
