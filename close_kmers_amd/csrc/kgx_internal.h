@@ -163,10 +163,11 @@ hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_
                          hipStream_t stream);
 /* the run scorer: variant 1 = wave-parallel (order_constraint 0; the lane
  * machine otherwise), 0 = one lane per sequence */
-hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *tile_seq, uint64_t max_tiles,
-                        const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
-                        uint32_t *hit_count, uint32_t *call_count, kgx_params params, uint32_t want,
-                        uint32_t hit_format, int variant, uint32_t wave_tiles, hipStream_t stream);
+hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wbase, const uint32_t *tile_seq,
+                        uint64_t max_tiles, const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot,
+                        kgx_call *calls, void *ranges, uint32_t *hit_count, uint32_t *call_count,
+                        kgx_params params, uint32_t want, uint32_t hit_format, int variant, uint32_t wave_tiles,
+                        hipStream_t stream);
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,

@@ -786,9 +786,9 @@ struct RunTail {
     uint64_t at; /* storage index */
 };
 
-constexpr int SCORE_BATCH = 8;
+constexpr int SCORE_BATCH = 8; /* records per load batch (double-buffered); 2 for short sequences */
 
-template <bool PK>
+template <bool PK, int SB = SCORE_BATCH>
 __device__ __forceinline__ void score_sequence(
     uint32_t s, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
@@ -901,36 +901,36 @@ __device__ __forceinline__ void score_sequence(
         }
     };
 
-    /* hits are read SCORE_BATCH at a time and double-buffered: batch b+1's
+    /* hits are read SB at a time and double-buffered: batch b+1's
      * loads are in flight while batch b runs through the state machine (the
      * machine is serial, its inputs are not) */
     auto load_batch = [&](uint4 *rb, uint64_t at0, uint32_t b, uint32_t c) {
 #pragma unroll
-        for (int k = 0; k < SCORE_BATCH; k++)
+        for (int k = 0; k < SB; k++)
             if (b + k < c)
                 rb[k] = hot[at0 + b + k];
     };
     const uint32_t nh = for_each_run(hit_mask, tile_windows, gw0, gw1,
                                      [&](uint64_t at0, uint32_t c, uint32_t ord0, uint64_t bits, uint32_t pbase) {
-        uint4 ra[SCORE_BATCH], rb[SCORE_BATCH];
+        uint4 ra[SB], rb[SB];
         load_batch(ra, at0, 0, c);
-        for (uint32_t b = 0; b < c; b += 2 * SCORE_BATCH) {
-            if (b + SCORE_BATCH < c)
-                load_batch(rb, at0, b + SCORE_BATCH, c);
+        for (uint32_t b = 0; b < c; b += 2 * SB) {
+            if (b + SB < c)
+                load_batch(rb, at0, b + SB, c);
 #pragma unroll
-            for (int k = 0; k < SCORE_BATCH; k++)
+            for (int k = 0; k < SB; k++)
                 if (b + k < c) {
                     step(ra[k], ord0 + b + k, at0 + b + k, pbase + (uint32_t)__builtin_ctzll(bits));
                     bits &= bits - 1;
                 }
-            if (b + SCORE_BATCH >= c)
+            if (b + SB >= c)
                 break;
-            if (b + 2 * SCORE_BATCH < c)
-                load_batch(ra, at0, b + 2 * SCORE_BATCH, c);
+            if (b + 2 * SB < c)
+                load_batch(ra, at0, b + 2 * SB, c);
 #pragma unroll
-            for (int k = 0; k < SCORE_BATCH; k++)
-                if (b + SCORE_BATCH + k < c) {
-                    step(rb[k], ord0 + b + SCORE_BATCH + k, at0 + b + SCORE_BATCH + k,
+            for (int k = 0; k < SB; k++)
+                if (b + SB + k < c) {
+                    step(rb[k], ord0 + b + SB + k, at0 + b + SB + k,
                          pbase + (uint32_t)__builtin_ctzll(bits));
                     bits &= bits - 1;
                 }
@@ -965,7 +965,7 @@ __device__ __forceinline__ void score_sequence(
     }
 }
 
-template <bool PK>
+template <bool PK, int SB>
 __global__ __launch_bounds__(256) void score_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
@@ -974,7 +974,8 @@ __global__ __launch_bounds__(256) void score_kernel(
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < n_seq)
-        score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
+        score_sequence<PK, SB>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm,
+                               want);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1414,10 +1415,11 @@ __global__ __launch_bounds__(256) void score_long_kernel(
         score_sequence<PK>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
 }
 
-hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *tile_seq, uint64_t max_tiles,
-                        const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot, kgx_call *calls, void *ranges,
-                        uint32_t *hit_count, uint32_t *call_count, kgx_params params, uint32_t want,
-                        uint32_t hit_format, int variant, uint32_t wave_tiles, hipStream_t stream)
+hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wbase, const uint32_t *tile_seq,
+                        uint64_t max_tiles, const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot,
+                        kgx_call *calls, void *ranges, uint32_t *hit_count, uint32_t *call_count,
+                        kgx_params params, uint32_t want, uint32_t hit_format, int variant, uint32_t wave_tiles,
+                        hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
@@ -1443,12 +1445,22 @@ hipError_t launch_score(uint32_t n_seq, const uint64_t *wbase, const uint32_t *t
         }
         return hipGetLastError();
     }
-    if (pk)
-        hipLaunchKernelGGL(score_kernel<true>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot,
-                           calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want);
+    /* short sequences (fq fragments: ~16 windows, <1 hit each) take the
+     * 2-record batches: fewer registers, more waves to hide the loads of
+     * sequences that mostly have no hits */
+    const bool small = n_residues < 64ull * n_seq;
+#define KGX_SCORE(P, B)                                                                                          \
+    hipLaunchKernelGGL((score_kernel<P, B>), lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot, \
+                       calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want)
+    if (pk && small)
+        KGX_SCORE(true, 2);
+    else if (pk)
+        KGX_SCORE(true, SCORE_BATCH);
+    else if (small)
+        KGX_SCORE(false, 2);
     else
-        hipLaunchKernelGGL(score_kernel<false>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows,
-                           hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want);
+        KGX_SCORE(false, SCORE_BATCH);
+#undef KGX_SCORE
     return hipGetLastError();
 }
 

@@ -1107,7 +1107,7 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
         kgx_params_default(&p);
     HIP_TRY(hipSetDevice(c->img->device));
     const bool best = (want & KGX_WANT_BEST) != 0;
-    HIP_TRY(launch_score(c->n_seq, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(), c->max_tiles,
+    HIP_TRY(launch_score(c->n_seq, c->n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(), c->max_tiles,
                          c->hit_mask.as<uint64_t>(), c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
                          want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->score_variant,
@@ -2084,15 +2084,22 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     if (want_best && !c->have_best)
         return fail(KGX_EINVAL, "no device best calls (score with KGX_WANT_BEST)");
     HIP_TRY(hipSetDevice(c->img->device));
-    int rc = kgx_ctx_check(c); /* bad device offsets: an error, not an empty result */
-    if (rc)
-        return rc;
     PhaseTimer tm(c);
     const uint32_t n_seq = c->n_seq;
-    /* counts -> dense CSR offsets on the host, gather on the device */
+    /* counts -> dense CSR offsets on the host, gather on the device.  The
+     * plan's status word (bad device offsets: an error, not an empty result)
+     * and the window total come back with the counts, in one round trip. */
     HIP_TRY(c->h_hcount.resize(n_seq + 1));
     HIP_TRY(c->h_ccount.resize(n_seq + 1));
     HIP_TRY(c->h_ocount.resize(n_seq + 1));
+    HIP_TRY(c->h_plan_status.resize(1));
+    HIP_TRY(c->h_nwin.resize(1));
+    c->h_plan_status[0] = 0;
+    if (c->plan_status.p)
+        HIP_TRY(hipMemcpyAsync(c->h_plan_status.data(), c->plan_status.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_nwin.data(), c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, c->stream));
     if (n_seq) {
         HIP_TRY(hipMemcpyAsync(c->h_hcount.data(), c->hit_count.p, n_seq * sizeof(uint32_t),
                                hipMemcpyDeviceToHost, c->stream));
@@ -2103,6 +2110,9 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                                    hipMemcpyDeviceToHost, c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_plan_status[0])
+        return fail(KGX_EINVAL, "batch offsets not monotone or spanning more than n_residues bytes "
+                                "(the batch was processed as empty)");
     c->h_hoff.assign(n_seq + 1, 0);
     c->h_coff.assign(n_seq + 1, 0);
     c->h_ooff.assign(n_seq + 1, 0);
@@ -2116,6 +2126,9 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     HIP_TRY(c->h_hits.resize(need_hits ? nh : 0));
     HIP_TRY(c->h_calls.resize(nc));
     HIP_TRY(c->h_otus.resize(no));
+    /* small results: the gather stores the records straight into the mapped
+     * pinned result arrays (no D2H copies to queue behind it) */
+    const bool mapped = (need_hits ? nh : 0) + nc + no <= (1u << 16);
     if ((need_hits && nh) || nc || no) {
         HIP_TRY(c->dense_hoff.reserve((n_seq + 1) * sizeof(uint64_t)));
         HIP_TRY(c->dense_coff.reserve((n_seq + 1) * sizeof(uint64_t)));
@@ -2129,33 +2142,43 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                                hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->dense_ooff.p, c->h_ooff.data(), (n_seq + 1) * sizeof(uint64_t),
                                hipMemcpyHostToDevice, c->stream));
+        void *mh = nullptr, *mc = nullptr, *mo = nullptr;
+        if (mapped) {
+            if (need_hits && nh)
+                HIP_TRY(c->h_hits.device_ptr(0, &mh));
+            if (nc)
+                HIP_TRY(c->h_calls.device_ptr(0, &mc));
+            if (no)
+                HIP_TRY(c->h_otus.device_ptr(0, &mo));
+        }
+        kgx_hit *gh = need_hits && nh ? (mapped ? static_cast<kgx_hit *>(mh) : c->dense_hits.as<kgx_hit>()) : nullptr;
+        kgx_call *gc = want_calls ? (mapped && nc ? static_cast<kgx_call *>(mc) : c->dense_calls.as<kgx_call>())
+                                  : nullptr;
+        kgx_otu *go = no ? (mapped ? static_cast<kgx_otu *>(mo) : c->dense_otus.as<kgx_otu>()) : nullptr;
         HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
                               c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
                               c->hits.as<uint4>() + c->hit_slots,
                               c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(),
-                              c->dense_coff.as<uint64_t>(),
-                              need_hits ? c->dense_hits.as<kgx_hit>() : nullptr,
-                              want_calls ? c->dense_calls.as<kgx_call>() : nullptr, 0u, c->hit_format,
+                              c->dense_coff.as<uint64_t>(), gh, gc, 0u, c->hit_format,
                               c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
-                              no ? c->dense_otus.as<kgx_otu>() : nullptr, c->stream));
-        if (need_hits && nh)
-            HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
-                                   hipMemcpyDeviceToHost, c->stream));
-        if (nc)
-            HIP_TRY(hipMemcpyAsync(c->h_calls.data(), c->dense_calls.p, nc * sizeof(kgx_call),
-                                   hipMemcpyDeviceToHost, c->stream));
-        if (no)
-            HIP_TRY(hipMemcpyAsync(c->h_otus.data(), c->dense_otus.p, no * sizeof(kgx_otu),
-                                   hipMemcpyDeviceToHost, c->stream));
+                              go, c->stream));
+        if (!mapped) {
+            if (need_hits && nh)
+                HIP_TRY(hipMemcpyAsync(c->h_hits.data(), c->dense_hits.p, nh * sizeof(kgx_hit),
+                                       hipMemcpyDeviceToHost, c->stream));
+            if (nc)
+                HIP_TRY(hipMemcpyAsync(c->h_calls.data(), c->dense_calls.p, nc * sizeof(kgx_call),
+                                       hipMemcpyDeviceToHost, c->stream));
+            if (no)
+                HIP_TRY(hipMemcpyAsync(c->h_otus.data(), c->dense_otus.p, no * sizeof(kgx_otu),
+                                       hipMemcpyDeviceToHost, c->stream));
+        }
     }
     if (want_best && n_seq) {
         HIP_TRY(c->h_best.resize(n_seq));
         HIP_TRY(hipMemcpyAsync(c->h_best.data(), c->best.p, n_seq * sizeof(kgx_best_call), hipMemcpyDeviceToHost,
                                c->stream));
     }
-    HIP_TRY(c->h_nwin.resize(1));
-    HIP_TRY(hipMemcpyAsync(c->h_nwin.data(), c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     tm.mark(" gather+d2h");
     fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
