@@ -377,22 +377,21 @@ __device__ __forceinline__ void frame_runs(uint64_t m, int base, int &prev, uint
     }
 }
 
-/* a read's fragments and residues from its bytes: dword i of the read's
- * aligned span comes from dw(i) (global memory or the wave's LDS copy) */
-template <class DW>
-__device__ __forceinline__ void lane_read_counts(DW dw, uint32_t mis, uint32_t len, uint32_t &nf, uint32_t &nr)
+/* a read's fragments and residues straight from its bytes in memory, one
+ * base at a time: the path of waves whose reads do not fit the LDS span
+ * (few registers, so the staged path keeps its occupancy) */
+__device__ __forceinline__ void lane_read_counts_global(const uint8_t *b, uint32_t len, uint32_t &nf, uint32_t &nr)
 {
     nf = nr = 0;
-    const uint32_t nw = (mis + len + 3) / 4; /* aligned dwords spanning the read */
     int prev[6], hi[6];
     uint32_t rho[6];
-    for (uint32_t f = 0; f < 3; f++) { /* frame +(f+1): codon k = bases f+3k .. f+3k+2 */
+    for (uint32_t f = 0; f < 3; f++) {
         const uint32_t nc = len >= f ? (len - f) / 3 : 0;
         prev[f] = (int)f - 1;
         hi[f] = (int)(f + 2 + 3 * nc);
         rho[f] = (f + 2) % 3;
     }
-    for (uint32_t f = 0; f < 3; f++) { /* frame -(f+1): codon k ends at forward base len-1-f-3k */
+    for (uint32_t f = 0; f < 3; f++) {
         const uint32_t nc = len >= f ? (len - f) / 3 : 0;
         const int top = (int)len - (int)f - 1;
         prev[3 + f] = top - 3 * (int)nc;
@@ -400,28 +399,95 @@ __device__ __forceinline__ void lane_read_counts(DW dw, uint32_t mis, uint32_t l
         rho[3 + f] = (uint32_t)((top % 3 + 3) % 3);
     }
     uint32_t hist = 0x444; /* nibbles of the last three bases, newest lowest; bit 2 = not a base yet */
-    for (uint32_t blk = 0; 64 * blk < len; blk++) {
-        /* bases 64 blk .. 64 blk + 63: dwords 16 blk .. 16 blk + 16 of the
-         * span, shifted by mis bytes (the read's offset in its first dword) */
-        uint32_t d[17];
-#pragma unroll
-        for (uint32_t i = 0; i < 17; i++)
-            d[i] = 16 * blk + i < nw ? dw(16 * blk + i) : 0u;
-        uint64_t ef = 0, er = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 16; i++) {
-            const uint32_t x = __builtin_amdgcn_alignbit(d[i + 1], d[i], mis * 8u);
-            const uint32_t nib = nibbles4(x);
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++) {
-                hist = ((hist << 4) | ((nib >> (4 * j)) & 0xFu)) & 0xFFFu;
-                const uint32_t fs = hist == 0x300u || hist == 0x302u || hist == 0x320u;
-                const uint32_t rs = hist == 0x330u || hist == 0x130u || hist == 0x310u;
-                ef |= (uint64_t)fs << (4 * i + j);
-                er |= (uint64_t)rs << (4 * i + j);
+    uint64_t ef = 0, er = 0;
+    for (uint32_t q = 0; q < len; q++) {
+        hist = ((hist << 4) | (nibbles4(b[q]) & 0xFu)) & 0xFFFu;
+        const uint32_t fs = hist == 0x300u || hist == 0x302u || hist == 0x320u;
+        const uint32_t rs = hist == 0x330u || hist == 0x130u || hist == 0x310u;
+        ef |= (uint64_t)fs << (q & 63);
+        er |= (uint64_t)rs << (q & 63);
+        if ((q & 63) == 63 || q + 1 == len) { /* a block of 64 bases is complete */
+            const uint32_t blk = q >> 6;
+            for (uint32_t f = 0; f < 6; f++) {
+                const uint32_t sh = (rho[f] + 3 - blk % 3) % 3;
+                frame_runs((f < 3 ? ef : er) & (EVERY3 << sh), 64 * (int)blk, prev[f], nf, nr);
             }
+            ef = er = 0;
         }
-        /* bases past the read: their bits are dropped */
+    }
+    for (uint32_t f = 0; f < 6; f++) {
+        const int L = (hi[f] - prev[f]) / 3 - 1;
+        if (L >= (int)MIN_FRAGMENT) {
+            nf++;
+            nr += (uint32_t)L;
+        }
+    }
+}
+
+/* bit j of the result = bit 4j of m (m's bits outside 0x11111111 clear) */
+__device__ __forceinline__ uint32_t nib_compress(uint32_t m)
+{
+    m = (m | (m >> 3)) & 0x03030303u;
+    m = (m | (m >> 6)) & 0x000F000Fu;
+    return (m | (m >> 12)) & 0xFFu;
+}
+
+/* stop codons ending at the 8 bases of x (nibble string, base j at bits
+ * 4j; prev = the 8 bases before): forward TAA TAG TGA / reverse strand TTA
+ * CTA TCA read forward.  Bit j of fs / rs.  SWAR over the nibbles: the
+ * per-base class tests are 64-bit masks, the bases one and two back are the
+ * same masks shifted by one and two nibbles. */
+__device__ __forceinline__ void stops8(uint32_t x, uint32_t prev, uint32_t &fs, uint32_t &rs)
+{
+    constexpr uint64_t N1 = 0x1111111111111111ull;
+    const uint64_t y = (uint64_t)x << 32 | prev;
+    const uint64_t lo = y & N1, hi = (y >> 1) & N1, ok = ~(y >> 2) & N1;
+    const uint64_t A = ~lo & ~hi & ok, C = lo & ~hi & ok, G = ~lo & hi & ok, T = lo & hi & ok;
+    const uint64_t A1 = A << 4, C1 = C << 4, G1 = G << 4, T1 = T << 4, C2 = C << 8, T2 = T << 8;
+    const uint64_t f = T2 & ((A1 & (A | G)) | (G1 & A));
+    const uint64_t r = A & ((T1 & (T2 | C2)) | (C1 & T2));
+    fs = nib_compress((uint32_t)(f >> 32));
+    rs = nib_compress((uint32_t)(r >> 32));
+}
+
+/* lane_read_counts over the wave's nibble string (ns: byte o of the staged
+ * span at bits 4o; the read's base p is nibble loc + p) */
+__device__ __forceinline__ void lane_read_counts_ns(const uint32_t *ns, uint32_t loc, uint32_t len, uint32_t &nf,
+                                                    uint32_t &nr)
+{
+    nf = nr = 0;
+    int prev[6], hi[6];
+    uint32_t rho[6];
+    for (uint32_t f = 0; f < 3; f++) {
+        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
+        prev[f] = (int)f - 1;
+        hi[f] = (int)(f + 2 + 3 * nc);
+        rho[f] = (f + 2) % 3;
+    }
+    for (uint32_t f = 0; f < 3; f++) {
+        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
+        const int top = (int)len - (int)f - 1;
+        prev[3 + f] = top - 3 * (int)nc;
+        hi[3 + f] = top + 3;
+        rho[3 + f] = (uint32_t)((top % 3 + 3) % 3);
+    }
+    const uint32_t sh = (loc & 7u) * 4u;
+    uint32_t px = 0x44444444u; /* no bases before base 0 */
+    for (uint32_t blk = 0; 64 * blk < len; blk++) {
+        const uint32_t w0 = (loc + 64 * blk) >> 3;
+        uint64_t ef = 0, er = 0;
+        uint32_t lo = ns[w0];
+#pragma unroll 2
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t hi = ns[w0 + i + 1];
+            const uint32_t x = __builtin_amdgcn_alignbit(hi, lo, sh); /* bases 64 blk + 8i .. +7 */
+            lo = hi;
+            uint32_t fs, rs;
+            stops8(x, px, fs, rs);
+            ef |= (uint64_t)fs << (8 * i);
+            er |= (uint64_t)rs << (8 * i);
+            px = x;
+        }
         const uint32_t left = len - 64 * blk;
         const uint64_t in = left >= 64 ? ~0ull : ((1ull << left) - 1);
         ef &= in;
@@ -429,9 +495,8 @@ __device__ __forceinline__ void lane_read_counts(DW dw, uint32_t mis, uint32_t l
         const int base = 64 * (int)blk;
 #pragma unroll
         for (uint32_t f = 0; f < 6; f++) {
-            /* bits b of this block with 64 blk + b = rho (mod 3); 64 = 1 (mod 3) */
-            const uint32_t sh = (rho[f] + 3 - blk % 3) % 3;
-            frame_runs((f < 3 ? ef : er) & (EVERY3 << sh), base, prev[f], nf, nr);
+            const uint32_t shf = (rho[f] + 3 - blk % 3) % 3;
+            frame_runs((f < 3 ? ef : er) & (EVERY3 << shf), base, prev[f], nf, nr);
         }
     }
 #pragma unroll
@@ -450,17 +515,19 @@ __device__ __forceinline__ void lane_read_counts(DW dw, uint32_t mis, uint32_t l
  * read from there (lanes reading their own reads straight from memory touch
  * 64 lines per load, 150 bytes apart, and the L1 thrashes).  A wave whose span
  * does not fit reads from memory. */
-constexpr uint32_t COUNT_SPAN = 12288; /* LDS bytes per wave */
+constexpr uint32_t COUNT_SPAN = 12288;               /* span bytes a wave stages */
+constexpr uint32_t NS_WORDS = COUNT_SPAN / 8 + 16;     /* their nibble string + slack */
 
 __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases, const uint64_t *read_off,
                                                             uint32_t n_reads, uint2 *read_counts, ulonglong2 *tile_sum,
                                                             uint32_t n_tiles)
 {
-    __shared__ uint4 span[WAVES_PER_WG][COUNT_SPAN / 16];
+    __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x * WAVES_PER_WG + wv;
     if (tile >= n_tiles)
         return;
+    uint32_t *ns = nspan[wv];
     const uint64_t r0 = (uint64_t)tile * FQ_TILE;
     const uint32_t n = (uint32_t)std::min<uint64_t>(FQ_TILE, n_reads - r0);
     const uint64_t r = r0 + lane;
@@ -472,24 +539,23 @@ __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases
     const bool staged = end > first && bytes <= COUNT_SPAN; /* (an empty span reads nothing) */
     uint32_t nf = 0, nr = 0;
     if (staged) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(bases + first - (reinterpret_cast<uintptr_t>(bases + first) & 15));
+        /* the span as a nibble string, 16 bytes per lane per round, coalesced
+         * (+1 round of zeros: the funnel shifts' pad) */
+        const uint4 *src = reinterpret_cast<const uint4 *>(a);
         const uint32_t nv = (uint32_t)((bytes + 15) / 16);
-        for (uint32_t i = lane; i < nv; i += 64)
-            span[wv][i] = src[i];
+        for (uint32_t i = lane; i < nv + 1; i += 64) {
+            const uint4 v = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+            ns[2 * i] = nibbles4(v.x) | nibbles4(v.y) << 16;
+            ns[2 * i + 1] = nibbles4(v.z) | nibbles4(v.w) << 16;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < n) {
-            const uint32_t loc = (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a);
-            const uint32_t *L = reinterpret_cast<const uint32_t *>(span[wv]) + loc / 4;
-            const uint32_t lim = (uint32_t)((bytes + 3) / 4) - loc / 4; /* dwords of the span from L */
-            lane_read_counts([&](uint32_t i) { return i < lim ? L[i] : 0u; }, loc & 3, (uint32_t)(oe - ob), nf, nr);
-        }
+        if (lane < n)
+            lane_read_counts_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), (uint32_t)(oe - ob), nf,
+                                nr);
     } else if (lane < n) {
-        const uint8_t *b = bases + ob;
-        const uint32_t mis = read_mis(b);
-        const uint32_t *W = reinterpret_cast<const uint32_t *>(b - mis);
-        lane_read_counts([&](uint32_t i) { return W[i]; }, mis, (uint32_t)(oe - ob), nf, nr);
+        lane_read_counts_global(bases + ob, (uint32_t)(oe - ob), nf, nr);
     }
     if (lane < n)
         read_counts[r] = make_uint2(nf, nr);

@@ -88,30 +88,59 @@ __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__rest
         sums[blockIdx.x] = bad ? PLAN_BAD : total;
 }
 
-/* exclusive scan of the workgroup sums in place, one workgroup.  (Each
- * plan_scan workgroup used to add up all earlier sums itself: quadratic in
- * the number of workgroups, 0.5 ms for the 9.9M fragments of a 1M-read fq
- * chunk.) */
-__global__ __launch_bounds__(256) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups,
-                                                             uint32_t *__restrict__ status)
+/* exclusive scan of the workgroup sums in place, one workgroup of 1,024
+ * threads, each scanning 16 consecutive sums per round (a 9.9M-fragment fq
+ * chunk's 9.7k sums: one round).  (Each plan_scan workgroup used to add up
+ * all earlier sums itself: quadratic in the number of workgroups, 0.5 ms for
+ * the 9.9M fragments of a 1M-read fq chunk; then 256 threads in rounds of
+ * 256: 31 us.) */
+constexpr uint32_t SUMS_THREADS = 1024, SUMS_PER = 16;
+
+__global__ __launch_bounds__(SUMS_THREADS) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups,
+                                                                      uint32_t *__restrict__ status)
 {
-    __shared__ uint64_t lds4[4];
+    __shared__ uint64_t wsum[SUMS_THREADS / 64];
     /* any workgroup that saw bad offsets empties the whole batch (sums[groups]
      * = 1 tells plan_scan) and raises the context's status word */
     bool bad = false;
-    for (uint32_t i = threadIdx.x; i < groups; i += 256)
+    for (uint32_t i = threadIdx.x; i < groups; i += SUMS_THREADS)
         bad |= (sums[i] & PLAN_BAD) != 0;
     bad = __syncthreads_or(bad);
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint64_t carry = 0;
-    for (uint32_t base = 0; base < groups; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < groups && !bad ? sums[i] : 0;
-        uint64_t tot;
-        const uint64_t incl = block_scan(v, lds4, tot);
-        if (i < groups)
-            sums[i] = carry + incl - v;
+    for (uint32_t base = 0; base < groups; base += SUMS_THREADS * SUMS_PER) {
+        const uint32_t i0 = base + threadIdx.x * SUMS_PER;
+        uint64_t v[SUMS_PER], t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SUMS_PER; k++) {
+            v[k] = i0 + k < groups && !bad ? sums[i0 + k] : 0;
+            t += v[k];
+        }
+        /* exclusive prefix of the threads' totals: wave scan, then the waves' sums */
+        uint64_t x = t;
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint64_t y = __shfl_up(x, off);
+            if (lane >= off)
+                x += y;
+        }
+        if (lane == 63)
+            wsum[wave] = x;
+        __syncthreads();
+        uint64_t pre = carry, tot = 0;
+        for (uint32_t w = 0; w < SUMS_THREADS / 64; w++) {
+            if (w < wave)
+                pre += wsum[w];
+            tot += wsum[w];
+        }
+        pre += x - t;
+#pragma unroll
+        for (uint32_t k = 0; k < SUMS_PER; k++) {
+            if (i0 + k < groups)
+                sums[i0 + k] = pre;
+            pre += v[k];
+        }
         carry += tot;
-        __syncthreads(); /* lds4 is rewritten by the next round */
+        __syncthreads(); /* wsum is rewritten by the next round */
     }
     if (threadIdx.x == 0) {
         sums[groups] = bad ? 1 : 0;
@@ -159,8 +188,8 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_resid
     const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
     hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq, n_residues,
                        static_cast<uint64_t *>(workspace));
-    hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(256), 0, stream, static_cast<uint64_t *>(workspace),
-                       groups, status);
+    hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(SUMS_THREADS), 0, stream,
+                       static_cast<uint64_t *>(workspace), groups, status);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
     return hipGetLastError();
