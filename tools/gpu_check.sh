@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box pass (run through gpurun from the repo root):
 #   bash tools/gpu_check.sh TAG [quick]
-# 1. the -m gpu test suite   2. bench.py (C2)   3. C3 /matrix   4. C4 fq   5. HTTP serving
+# 1. the -m gpu test suite + smoke   2. bench.py (C2)   3. C3 /matrix   4. C4 fq
+# 5. HTTP serving (/query; /lookup in family mode)   6. unbatched facade latency
 # "quick" skips the CPU baselines.  Output in gpurun_out/TAG; every GPU step
 # has its own time limit and the script stops at the first failure.
 set -euo pipefail
@@ -13,9 +14,13 @@ mkdir -p "$OUT"
 cd "$R"
 NOCPU=""
 [ "$QUICK" = "quick" ] && NOCPU="--no-cpu-baseline"
-timeout -k 10 1500 python3 -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 timeout -k 10 900 python3 bench.py $NOCPU > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -k 10 600 python3 tools/bench_matrix.py $NOCPU > "$OUT/bench_matrix.json" 2> "$OUT/bench_matrix.err"
 timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
 timeout -k 10 600 python3 tools/bench_server.py > "$OUT/bench_server.json" 2> "$OUT/bench_server.err"
+timeout -k 10 900 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
+    --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
+timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
 echo "[gpu_check] done" >&2
