@@ -145,7 +145,7 @@ def main():
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="LDS KB reserved per probe workgroup (-1 = default)")
-    ap.add_argument("--score-variant", type=int, default=0, help="0 = lane per sequence (default), 1 = wave-parallel run scorer")
+    ap.add_argument("--score-variant", type=int, default=0, help="0 = hybrid (default: lanes, long sequences on the wave scorer), 1 = wave-parallel, 2 = lanes only")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 

@@ -161,13 +161,19 @@ hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_
                        uint32_t *not_packable, hipStream_t stream);
 hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_t n,
                          hipStream_t stream);
-/* the run scorer: variant 1 = wave-parallel (order_constraint 0; the lane
- * machine otherwise), 0 = one lane per sequence */
+/* the run scorer.  variant SCORE_HYBRID (0, the default): the lane machine
+ * (one lane per sequence), except sequences of (LONG_SEQ, RUN_CAP] windows,
+ * which the wave-parallel scorer takes; SCORE_WAVE (1): the wave scorer for
+ * every sequence up to RUN_CAP windows; SCORE_LANE (2): the lane machine
+ * only.  The wave scorer needs order_constraint 0 (else: the lane machine).
+ * plan_status[1] = the batch's longest sequence in windows (launch_plan). */
+enum { SCORE_HYBRID = 0, SCORE_WAVE = 1, SCORE_LANE = 2 };
+constexpr uint32_t LONG_SEQ = 2048;
 hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wbase, const uint32_t *tile_seq,
                         uint64_t max_tiles, const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot,
                         kgx_call *calls, void *ranges, uint32_t *hit_count, uint32_t *call_count,
                         kgx_params params, uint32_t want, uint32_t hit_format, int variant, uint32_t wave_tiles,
-                        hipStream_t stream);
+                        const uint32_t *plan_status, hipStream_t stream);
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
                          uint32_t tile_windows, const uint32_t *call_count, const uint4 *hot, const uint4 *cold,
                          const kgx_call *calls, const uint64_t *hit_dense_off,

@@ -75,17 +75,37 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *lds4, uint6
     return v + pre;
 }
 
+/* the longest sequence's windows (capped at 2^32 - 1) of this thread's PLAN_PER */
+__device__ __forceinline__ uint32_t thread_max_windows(const uint64_t *seq_off, uint32_t n, uint32_t s0)
+{
+    uint64_t m = 0;
+    for (uint32_t k = 0; k < PLAN_PER; k++)
+        if (s0 + k < n)
+            m = max(m, windows_of(seq_off[s0 + k + 1] - seq_off[s0 + k]));
+    return (uint32_t)min<uint64_t>(m, 0xFFFFFFFFull);
+}
+
 __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__restrict__ seq_off,
                                                           uint32_t n, uint64_t n_residues,
-                                                          uint64_t *__restrict__ sums)
+                                                          uint64_t *__restrict__ sums, uint32_t *__restrict__ maxw)
 {
     __shared__ uint64_t lds4[4];
+    __shared__ uint32_t lmax[4];
     uint64_t total;
     const uint32_t s0 = blockIdx.x * PLAN_TILE + threadIdx.x * PLAN_PER;
     const bool bad = __syncthreads_or(thread_offsets_bad(seq_off, n, s0, n_residues));
     block_scan(bad ? 0 : thread_windows(seq_off, n, s0), lds4, total);
-    if (threadIdx.x == 0)
+    /* the workgroup's longest sequence (scorer dispatch, plan_sums_scan) */
+    uint32_t m = bad ? 0u : thread_max_windows(seq_off, n, s0);
+    for (uint32_t off = 32; off; off >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, (int)off));
+    if ((threadIdx.x & 63u) == 0)
+        lmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
         sums[blockIdx.x] = bad ? PLAN_BAD : total;
+        maxw[blockIdx.x] = max(max(lmax[0], lmax[1]), max(lmax[2], lmax[3]));
+    }
 }
 
 /* exclusive scan of the workgroup sums in place, one workgroup of 1,024
@@ -97,15 +117,31 @@ __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__rest
 constexpr uint32_t SUMS_THREADS = 1024, SUMS_PER = 16;
 
 __global__ __launch_bounds__(SUMS_THREADS) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups,
+                                                                      const uint32_t *__restrict__ maxw,
                                                                       uint32_t *__restrict__ status)
 {
     __shared__ uint64_t wsum[SUMS_THREADS / 64];
+    __shared__ uint32_t wmax[SUMS_THREADS / 64];
     /* any workgroup that saw bad offsets empties the whole batch (sums[groups]
-     * = 1 tells plan_scan) and raises the context's status word */
+     * = 1 tells plan_scan) and raises the context's status word; status[1] =
+     * the batch's longest sequence in windows (the scorer's dispatch) */
     bool bad = false;
-    for (uint32_t i = threadIdx.x; i < groups; i += SUMS_THREADS)
+    uint32_t m = 0;
+    for (uint32_t i = threadIdx.x; i < groups; i += SUMS_THREADS) {
         bad |= (sums[i] & PLAN_BAD) != 0;
+        m = max(m, maxw[i]);
+    }
+    for (uint32_t off = 32; off; off >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, (int)off));
+    if ((threadIdx.x & 63u) == 0)
+        wmax[threadIdx.x >> 6] = m;
     bad = __syncthreads_or(bad);
+    if (threadIdx.x == 0) {
+        uint32_t mm = 0;
+        for (uint32_t w = 0; w < SUMS_THREADS / 64; w++)
+            mm = max(mm, wmax[w]);
+        status[1] = bad ? 0u : mm;
+    }
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint64_t carry = 0;
     for (uint32_t base = 0; base < groups; base += SUMS_THREADS * SUMS_PER) {
@@ -178,18 +214,22 @@ __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restri
         wbase[n] = before + tot;
 }
 
-/* the workgroup sums + the bad-offsets word */
-size_t plan_workspace_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 2) * sizeof(uint64_t); }
+/* the workgroup sums + the bad-offsets word, then the workgroups' longest sequences */
+size_t plan_workspace_bytes(uint32_t n_seq)
+{
+    return ((size_t)n_seq / PLAN_TILE + 2) * (sizeof(uint64_t) + sizeof(uint32_t));
+}
 
 hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
                        uint32_t *tile_seq, uint32_t tile_windows, void *workspace, uint32_t *status,
                        hipStream_t stream)
 {
     const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
+    uint32_t *maxw = reinterpret_cast<uint32_t *>(static_cast<uint64_t *>(workspace) + groups + 2);
     hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq, n_residues,
-                       static_cast<uint64_t *>(workspace));
+                       static_cast<uint64_t *>(workspace), maxw);
     hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(SUMS_THREADS), 0, stream,
-                       static_cast<uint64_t *>(workspace), groups, status);
+                       static_cast<uint64_t *>(workspace), groups, maxw, status);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
     return hipGetLastError();
@@ -994,17 +1034,22 @@ __device__ __forceinline__ void score_sequence(
     }
 }
 
+/* skip_above: sequences with windows in (skip_above, RUN_CAP] are the wave
+ * scorer's (hybrid dispatch); ~0u = none */
 template <bool PK, int SB>
 __global__ __launch_bounds__(256) void score_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, uint4 *__restrict__ hot, kgx_call *__restrict__ calls,
     uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
-    kgx_params prm, uint32_t want)
+    kgx_params prm, uint32_t want, uint32_t skip_above)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < n_seq)
-        score_sequence<PK, SB>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm,
-                               want);
+    if (s >= n_seq)
+        return;
+    const uint64_t w = wbase[s + 1] - wbase[s];
+    if (w > skip_above && w <= (uint64_t)RUN_CAP)
+        return;
+    score_sequence<PK, SB>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1097,8 +1142,12 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
     uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq,
     const uint64_t *__restrict__ hit_mask, uint32_t tile_windows, uint32_t wave_tiles, uint4 *__restrict__ hot,
     kgx_call *__restrict__ calls, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
-    kgx_params prm, uint32_t want)
+    kgx_params prm, uint32_t want, uint32_t only_above, const uint32_t *__restrict__ plan_status)
 {
+    /* hybrid dispatch: only sequences over only_above windows are this
+     * kernel's; the plan's longest-sequence word says whether there are any */
+    if (only_above && plan_status[1] <= only_above)
+        return;
     __shared__ ScoreQueue queues[4];
     typedef HitFields<PK> HF;
     constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << HF::FLAG_SHIFT, F_CNT = KGX_HIT_COUNTED << HF::FLAG_SHIFT,
@@ -1364,7 +1413,8 @@ __global__ __launch_bounds__(256) void score_wave_kernel(
             wave_lds_sync();
         }
         const uint64_t gw0 = uni64(Q.wb[s - sb]), gw1 = uni64(Q.wb[s + 1 - sb]);
-        if (gw1 - gw0 > (uint64_t)RUN_CAP) { /* score_long_kernel's */
+        if (gw1 - gw0 > (uint64_t)RUN_CAP || (only_above && gw1 - gw0 <= only_above)) {
+            /* score_long_kernel's / (hybrid) the lane scorer's */
             if (lane == s - hb)
                 vhc = NONE;
             continue;
@@ -1448,39 +1498,46 @@ hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wba
                         uint64_t max_tiles, const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot,
                         kgx_call *calls, void *ranges, uint32_t *hit_count, uint32_t *call_count,
                         kgx_params params, uint32_t want, uint32_t hit_format, int variant, uint32_t wave_tiles,
-                        hipStream_t stream)
+                        const uint32_t *plan_status, hipStream_t stream)
 {
     if (n_seq == 0)
         return hipSuccess;
     const bool pk = hit_format == HIT_PACKED16;
     const dim3 lanes((n_seq + 255) / 256);
-    /* the wave kernel keeps hit slots in 32 bits */
-    if (variant == 1 && !params.order_constraint && max_tiles * tile_windows < (1ull << 32)) {
-        wave_tiles = std::max<uint32_t>(1, wave_tiles);
-        const uint64_t waves = std::max<uint64_t>(1, (max_tiles + wave_tiles - 1) / wave_tiles);
-        const dim3 grid((uint32_t)((waves + 3) / 4));
+    /* the wave scorer: order_constraint 0, hit slots in 32 bits */
+    const bool wave_ok = !params.order_constraint && max_tiles * tile_windows < (1ull << 32);
+    wave_tiles = std::max<uint32_t>(1, wave_tiles);
+    const uint64_t waves = std::max<uint64_t>(1, (max_tiles + wave_tiles - 1) / wave_tiles);
+    const dim3 wgrid((uint32_t)((waves + 3) / 4));
+#define KGX_WAVE(P, ABOVE)                                                                                      \
+    hipLaunchKernelGGL(score_wave_kernel<P>, wgrid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,     \
+                       tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want, (ABOVE), plan_status)
+    if (variant == SCORE_WAVE && wave_ok) { /* every sequence up to RUN_CAP windows */
         if (pk) {
-            hipLaunchKernelGGL(score_wave_kernel<true>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
-                               tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want);
+            KGX_WAVE(true, 0u);
             hipLaunchKernelGGL(score_long_kernel<true>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask,
                                tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
                                want);
         } else {
-            hipLaunchKernelGGL(score_wave_kernel<false>, grid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,
-                               tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want);
+            KGX_WAVE(false, 0u);
             hipLaunchKernelGGL(score_long_kernel<false>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask,
                                tile_windows, hot, calls, static_cast<uint2 *>(ranges), hit_count, call_count, params,
                                want);
         }
         return hipGetLastError();
     }
+    /* the lane machine; in the hybrid (the default) sequences of (LONG_SEQ,
+     * RUN_CAP] windows go to the wave scorer instead: one lane walking a
+     * 30k-aa protein's hits would hold the whole stage for milliseconds */
+    const bool hybrid = variant == SCORE_HYBRID && wave_ok;
+    const uint32_t skip = hybrid ? LONG_SEQ : ~0u;
     /* short sequences (fq fragments: ~16 windows, <1 hit each) take the
      * 2-record batches: fewer registers, more waves to hide the loads of
      * sequences that mostly have no hits */
     const bool small = n_residues < 64ull * n_seq;
 #define KGX_SCORE(P, B)                                                                                          \
     hipLaunchKernelGGL((score_kernel<P, B>), lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot, \
-                       calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want)
+                       calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want, skip)
     if (pk && small)
         KGX_SCORE(true, 2);
     else if (pk)
@@ -1490,6 +1547,13 @@ hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wba
     else
         KGX_SCORE(false, SCORE_BATCH);
 #undef KGX_SCORE
+    if (hybrid) {
+        if (pk)
+            KGX_WAVE(true, LONG_SEQ);
+        else
+            KGX_WAVE(false, LONG_SEQ);
+    }
+#undef KGX_WAVE
     return hipGetLastError();
 }
 

@@ -292,7 +292,7 @@ struct kgx_ctx {
     int probe_j = kgx::PROBE_J_DEFAULT;
     int probe_lds_kb = 0;  /* LDS reserved per probe workgroup, caps its occupancy (option "probe_lds_kb") */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
-    int score_variant = 0; /* 0 = one lane per sequence, 1 = wave-parallel scorer (option "score_variant") */
+    int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */
     uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */

@@ -976,8 +976,8 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         return KGX_OK;
     }
     if (n == "score_variant") {
-        if (value != 0 && value != 1)
-            return fail(KGX_EINVAL, "score_variant must be 0 or 1");
+        if (value < 0 || value > 2)
+            return fail(KGX_EINVAL, "score_variant must be 0, 1 or 2");
         c->score_variant = (int)value;
         return KGX_OK;
     }
@@ -1051,7 +1051,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
-    HIP_TRY(c->plan_status.reserve(sizeof(uint32_t)));
+    HIP_TRY(c->plan_status.reserve(2 * sizeof(uint32_t))); /* [0] bad offsets, [1] longest sequence (windows) */
     HIP_TRY(launch_plan(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
                         tile_windows, c->plan_ws.p, c->plan_status.as<uint32_t>(), c->stream));
     c->n_seq = n_seq;
@@ -1111,7 +1111,7 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
                          c->hit_mask.as<uint64_t>(), c->tile_windows, c->hits.as<uint4>(), c->calls.as<kgx_call>(),
                          c->ranges.p, c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), p,
                          want | (best ? KGX_WANT_CALLS : 0u), c->hit_format, c->score_variant,
-                         (uint32_t)c->score_wave_tiles, c->stream));
+                         (uint32_t)c->score_wave_tiles, c->plan_status.as<uint32_t>(), c->stream));
     c->have_best = false;
     c->have_otus = false;
     if (want & KGX_WANT_OTU) {

@@ -287,9 +287,12 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
- * "score_variant" 0 (default) = the run scorer with one lane per sequence,
- * 1 = the wave-parallel scorer (ballots over 64 queued hits, serial f32 sums
- * only; order_constraint 0, else variant 0; measured slower: DESIGN.md §4),
+ * "score_variant" 0 (default) = hybrid run scorer: one lane per sequence,
+ * except sequences of 2,049..39,998 windows, which the wave-parallel scorer
+ * takes (a lane walking a 30k-aa protein would hold the stage for ms);
+ * 1 = the wave-parallel scorer for every sequence (ballots over 64 queued
+ * hits, serial f32 sums only); 2 = lanes only.  The wave scorer needs
+ * order_constraint 0 (else lanes).  Results are identical;
  * "score_wave_tiles" (1..256, default 16) = probe tiles of windows per wave;
  * "fq_count" 1 (default) = the fq count pass scans stop codons one lane per
  * read, 0 = it translates like the emit pass (one wave per read);

@@ -1,5 +1,6 @@
-"""The wave-parallel run scorer (score_variant 1, an option; the default is
-the lane-per-sequence machine, score_variant 0) against the lane machine and the oracle: gather_hits /
+"""The run scorers against each other and the oracle: the lane machine
+(score_variant 2), the wave-parallel scorer (1) and the default hybrid (0:
+lanes, with sequences over 2,048 windows on the wave scorer): gather_hits /
 process_set_of_hits (kguts.cc:734-877) on hit-dense batches built to hit
 every rule -- gap breaks, pair switches with carry-over, runs that span many
 64-hit chunks, fragments whose hits share a chunk, empty and hitless
@@ -106,7 +107,7 @@ def test_wave_scorer_matches_lane_scorer(run_world, gpu, params):
     ctx.set_option("host_chunks", 1)
     n_calls = 0
     for want in (1, 3, 5, 7, 2, 4):
-        ctx.set_option("score_variant", 0)
+        ctx.set_option("score_variant", 2)
         a = ctx.process_batch(res, off, gpu.Params(*params), want=want)
         ctx.set_option("score_variant", 1)
         b = ctx.process_batch(res, off, gpu.Params(*params), want=want)
@@ -133,19 +134,43 @@ def test_wave_scorer_matches_oracle(run_world, gpu, oracle_lib, params):
     assert np.array_equal(got.otus["count"], want.otus[:, 1])
 
 
-def test_wave_scorer_long_sequence_and_device_path(run_world, gpu):
-    """A sequence past RUN_CAP windows (serial fallback inside the wave
-    kernel) between short ones, through the device-buffer path too."""
+def test_scorers_on_long_sequences(run_world, gpu):
+    """Sequences past RUN_CAP windows (the lane machine inside every variant),
+    between 2,048 and RUN_CAP windows (the hybrid's wave range) and short ones,
+    with empties: lane (2), wave (1) and hybrid (0) agree bit for bit."""
     rng, sources, table, ctx = run_world
-    long_seq = "".join(sources[int(rng.integers(0, len(sources)))] for _ in range(100))
-    assert len(long_seq) > 40100
-    res0, off0 = _batch(rng, sources, 200)
-    recs = [(f"a{i}", bytes(res0[int(off0[i]):int(off0[i + 1])])) for i in range(100)]
-    recs += [("long", long_seq)] + [(f"b{i}", bytes(res0[int(off0[i]):int(off0[i + 1])])) for i in range(100, 200)]
+    def longp(n):
+        return "".join(sources[int(rng.integers(0, len(sources)))] for _ in range(n))
+    res0, off0 = _batch(rng, sources, 300)
+    short = [(f"s{i}", bytes(res0[int(off0[i]):int(off0[i + 1])])) for i in range(300)]
+    recs = short[:100] + [("huge", longp(100))] + short[100:150] + [("mid1", longp(8)), ("mid2", longp(40))] \
+        + short[150:250] + [("edge", "A" * 2056), ("mid3", longp(70)), ("", "")] + short[250:]
+    assert len(recs[100][1]) > 40100
     res, off = pack(recs)
-    for params in SCORE_PARAMS[:4]:
-        ctx.set_option("score_variant", 0)
-        a = ctx.process_batch(res, off, gpu.Params(*params), want=7)
-        ctx.set_option("score_variant", 1)
-        b = ctx.process_batch(res, off, gpu.Params(*params), want=7)
-        _same(a, b, 7)
+    for params in SCORE_PARAMS[:5]:
+        outs = []
+        for v in (2, 1, 0):
+            ctx.set_option("score_variant", v)
+            outs.append(ctx.process_batch(res, off, gpu.Params(*params), want=7))
+        _same(outs[0], outs[1], 7)
+        _same(outs[0], outs[2], 7)
+    ctx.set_option("score_variant", 0)
+
+
+@pytest.mark.parametrize("params", SCORE_PARAMS[:3])
+def test_hybrid_scorer_with_long_sequences_matches_oracle(run_world, gpu, oracle_lib, params):
+    rng, sources, table, ctx = run_world
+    res0, off0 = _batch(rng, sources, 400)
+    recs = [(f"s{i}", bytes(res0[int(off0[i]):int(off0[i + 1])])) for i in range(400)]
+    for k in range(3):
+        recs.insert(100 * (k + 1), (f"long{k}", "".join(sources[(7 * k + j) % len(sources)] for j in range(12))))
+    res, off = pack(recs)
+    ctx.set_option("score_variant", 0)
+    got = ctx.process_batch(res, off, gpu.Params(*params), want=7)
+    want = oracle_lib.process_batch(table, res, off, params=params)
+    assert np.array_equal(got.hit_offsets, want.hit_offsets)
+    assert np.array_equal(got.call_offsets, want.call_offsets)
+    for f in ("start", "end", "count", "function_index"):
+        assert np.array_equal(got.calls[f], want.calls[f]), f
+    assert np.array_equal(got.calls["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+    assert np.array_equal(got.otus["count"], want.otus[:, 1])
