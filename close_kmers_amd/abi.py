@@ -81,7 +81,8 @@ class Fragments(ctypes.Structure):
     _fields_ = [("n_reads", ctypes.c_uint32), ("n_fragments", ctypes.c_uint32),
                 ("n_residues", ctypes.c_uint64), ("residues", ctypes.c_void_p),
                 ("offsets", ctypes.c_void_p), ("read", ctypes.c_void_p), ("frame", ctypes.c_void_p),
-                ("frame_counts", ctypes.c_void_p)]
+                ("frame_counts", ctypes.c_void_p), ("anchors", ctypes.c_void_p), ("bases", ctypes.c_void_p),
+                ("n_bases", ctypes.c_uint64)]
 
 
 def hits_from_packed(recs: np.ndarray) -> np.ndarray:
@@ -179,6 +180,7 @@ SIGNATURES = {
     "kgx_device_batch_collect": (_INT, [_P, _U32, ctypes.POINTER(Result)]),
     "kgx_fq_fragments": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
     "kgx_fq_fragments_device": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
+    "kgx_fq_run_device": (_INT, [_P, ctypes.POINTER(Params), ctypes.POINTER(Fragments), _U32, _P]),
     "kgx_fq_create": (_INT, [_P, _CS, _CS, _CS, _CS, _PP]),
     "kgx_fq_destroy": (_INT, [_P]),
     "kgx_fq_process": (_INT, [_P, _CS, _U64, _INT, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_U64)]),
@@ -453,10 +455,14 @@ class Context:
         n, nr = f.n_fragments, f.n_residues
         out = {"residues": np.zeros(nr, np.uint8), "offsets": np.zeros(n + 1, np.uint64),
                "read": np.zeros(n, np.uint32), "frame": np.zeros(n, np.int8)}
+        if not f.residues:  # fq_residues 0: anchors into the bases instead
+            out["residues"] = out["read"] = out["frame"] = None
+            out["anchors"] = np.zeros(n, np.uint64)
+        out["frame_counts"] = np.zeros(6 * f.n_reads, np.uint32)
         for k, ptr in (("residues", f.residues), ("offsets", f.offsets), ("read", f.read),
-                       ("frame", f.frame)):
-            a = out[k]
-            if a.nbytes:
+                       ("frame", f.frame), ("anchors", f.anchors), ("frame_counts", f.frame_counts)):
+            a = out.get(k)
+            if a is not None and a.nbytes:
                 check(lib().kgx_memcpy_d2h(a.ctypes.data, ptr, a.nbytes), "d2h")
         return out
 
@@ -465,8 +471,8 @@ class Context:
         """The lookup over device fragments, results collected to the host."""
         if params is None or isinstance(params, dict):
             params = parse_params(params)
-        check(lib().kgx_run_device(self.handle, ctypes.byref(params), f.residues, f.offsets,
-                                   f.n_fragments, f.n_residues, want, None), "kgx_run_device")
+        check(lib().kgx_fq_run_device(self.handle, ctypes.byref(params), ctypes.byref(f), want, None),
+              "kgx_fq_run_device")
         r = Result()
         check(lib().kgx_device_batch_collect(self.handle, want, ctypes.byref(r)), "collect")
         return BatchResult(r, want)

@@ -1360,7 +1360,13 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     /* the block's reads -> fragments -> lookup, one GPU batch */
     kgx_ctx *ctx = kg_.ctx();
     kgx_fragments fr;
-    int rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff.data(), n_reads, &fr);
+    /* fragments as anchors into the bases: the probe translates their windows
+     * itself and no residue goes through HBM (the context keeps residues when
+     * its probe cannot take anchors) */
+    int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
+    if (rc)
+        throw_last(rc, "kgx_ctx_set_option");
+    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff.data(), n_reads, &fr);
     if (rc)
         throw_last(rc, "kgx_fq_fragments");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
@@ -1376,9 +1382,9 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
      * fragments that have any: a per-fragment device decision (KGX_WANT_BEST)
      * would copy 24 B for every fragment (measured: 8.3M -> 6.7M reads/s). */
     const uint32_t want = families ? (KGX_WANT_HITS | KGX_WANT_CALLS) : KGX_WANT_CALLS;
-    rc = kgx_run_device(ctx, &p, fr.residues, fr.offsets, fr.n_fragments, fr.n_residues, want, nullptr);
+    rc = kgx_fq_run_device(ctx, &p, &fr, want, nullptr);
     if (rc)
-        throw_last(rc, "kgx_run_device");
+        throw_last(rc, "kgx_fq_run_device");
     mark("lookup");
     if (!families) {
         /* only the reads with a call in some fragment come back (sparse):

@@ -22,6 +22,15 @@ __device__ __forceinline__ uint32_t residue_code(uint32_t c)
     return ok ? (uint32_t)__popc(kMask & ((1u << (idx & 31u)) - 1u)) : 20u;
 }
 
+/* NCBI genetic code 11 (trans_table.cc:8-15) indexed e1*16 + e2*4 + e3 with
+ * A=0 C=1 G=2 T/U=3 (trans_table.h:45-83); tests/test_fq_host.py re-derives
+ * it from the table text */
+__device__ __forceinline__ char code11_aa(uint32_t e)
+{
+    const char *t = "KNKNTTTTRSRSIIMIQHQHPPPPRRRRLLLLEDEDAAAAGGGGVVVV*Y*YSSSS*CWCLFLF";
+    return t[e & 63u];
+}
+
 /* x % n for x < 2^35, n >= 1, m = floor((2^64-1)/n): the quotient estimate
  * is exact or one short, so one conditional subtraction finishes it */
 __device__ __forceinline__ uint64_t mod_by(uint64_t x, uint64_t n, uint64_t m)

@@ -11,6 +11,11 @@
  * batch of protein sequences, in (read, frame, position) order -- the order
  * the handler visits them -- with their read index and frame.
  *
+ * With fq_residues 0 the emit is fq_desc_lane_kernel instead: per fragment
+ * an anchor into the bases and no residues; the probe then translates each
+ * window's codons itself (launch_probe_dna), so the residues never go
+ * through HBM.
+ *
  * Launches: count (one wave per read: fragments and residues of the six
  * frames; per workgroup of 64 reads their sums), a scan of the sums
  * (hipcub), emit (the same waves translate again and write each fragment's
@@ -363,41 +368,60 @@ __global__ __launch_bounds__(256) void fq_count_kernel(const uint8_t *bases, con
  */
 constexpr uint64_t EVERY3 = 0x9249249249249249ull; /* bits 0, 3, ..., 63 */
 
-__device__ __forceinline__ void frame_runs(uint64_t m, int base, int &prev, uint32_t &nf, uint32_t &nr)
+/* the runs of frame f ending at the stops in m (bit i = a stop ending at base
+ * base + i): v(f, prev, q, L) for each kept run of L codons between the stops
+ * ending at prev and q */
+template <class V>
+__device__ __forceinline__ void frame_runs(uint64_t m, int base, uint32_t f, int &prev, V &v)
 {
     while (m) {
         const int q = base + __builtin_ctzll(m);
         m &= m - 1;
         const int L = (q - prev) / 3 - 1;
-        if (L >= (int)MIN_FRAGMENT) {
-            nf++;
-            nr += (uint32_t)L;
-        }
+        if (L >= (int)MIN_FRAGMENT)
+            v(f, prev, q, L);
         prev = q;
     }
 }
 
-/* a read's fragments and residues straight from its bytes in memory, one
- * base at a time: the path of waves whose reads do not fit the LDS span
- * (few registers, so the staged path keeps its occupancy) */
-__device__ __forceinline__ void lane_read_counts_global(const uint8_t *b, uint32_t len, uint32_t &nf, uint32_t &nr)
+/* each frame's first virtual stop (prev) and last one (hi), and the residue
+ * class mod 3 of its stops' last bases (rho): frame +k (f = k-1) has codons at
+ * f + 3i, so stops end at q = f + 3i + 2; frame -k (f = 3+k-1) reads the
+ * complement backwards from top = len-k, so its stops end at q = top - 3i */
+__device__ __forceinline__ void frame_bounds(uint32_t len, int *prev, int *hi, uint32_t *rho)
 {
-    nf = nr = 0;
-    int prev[6], hi[6];
-    uint32_t rho[6];
+#pragma unroll
     for (uint32_t f = 0; f < 3; f++) {
         const uint32_t nc = len >= f ? (len - f) / 3 : 0;
         prev[f] = (int)f - 1;
         hi[f] = (int)(f + 2 + 3 * nc);
         rho[f] = (f + 2) % 3;
-    }
-    for (uint32_t f = 0; f < 3; f++) {
-        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
         const int top = (int)len - (int)f - 1;
         prev[3 + f] = top - 3 * (int)nc;
         hi[3 + f] = top + 3;
         rho[3 + f] = (uint32_t)((top % 3 + 3) % 3);
     }
+}
+
+/* counting visitor: (fragments, residues) of a read */
+struct RunCount {
+    uint32_t nf = 0, nr = 0;
+    __device__ __forceinline__ void operator()(uint32_t, int, int, int L)
+    {
+        nf++;
+        nr += (uint32_t)L;
+    }
+};
+
+/* a read's kept runs straight from its bytes in memory, one base at a time:
+ * the path of waves whose reads do not fit the LDS span (few registers, so
+ * the staged path keeps its occupancy) */
+template <class V>
+__device__ __forceinline__ void lane_read_runs_global(const uint8_t *b, uint32_t len, V &v)
+{
+    int prev[6], hi[6];
+    uint32_t rho[6];
+    frame_bounds(len, prev, hi, rho);
     uint32_t hist = 0x444; /* nibbles of the last three bases, newest lowest; bit 2 = not a base yet */
     uint64_t ef = 0, er = 0;
     for (uint32_t q = 0; q < len; q++) {
@@ -410,17 +434,15 @@ __device__ __forceinline__ void lane_read_counts_global(const uint8_t *b, uint32
             const uint32_t blk = q >> 6;
             for (uint32_t f = 0; f < 6; f++) {
                 const uint32_t sh = (rho[f] + 3 - blk % 3) % 3;
-                frame_runs((f < 3 ? ef : er) & (EVERY3 << sh), 64 * (int)blk, prev[f], nf, nr);
+                frame_runs((f < 3 ? ef : er) & (EVERY3 << sh), 64 * (int)blk, f, prev[f], v);
             }
             ef = er = 0;
         }
     }
     for (uint32_t f = 0; f < 6; f++) {
         const int L = (hi[f] - prev[f]) / 3 - 1;
-        if (L >= (int)MIN_FRAGMENT) {
-            nf++;
-            nr += (uint32_t)L;
-        }
+        if (L >= (int)MIN_FRAGMENT)
+            v(f, prev[f], hi[f], L);
     }
 }
 
@@ -450,27 +472,14 @@ __device__ __forceinline__ void stops8(uint32_t x, uint32_t prev, uint32_t &fs, 
     rs = nib_compress((uint32_t)(r >> 32));
 }
 
-/* lane_read_counts over the wave's nibble string (ns: byte o of the staged
+/* lane_read_runs over the wave's nibble string (ns: byte o of the staged
  * span at bits 4o; the read's base p is nibble loc + p) */
-__device__ __forceinline__ void lane_read_counts_ns(const uint32_t *ns, uint32_t loc, uint32_t len, uint32_t &nf,
-                                                    uint32_t &nr)
+template <class V>
+__device__ __forceinline__ void lane_read_runs_ns(const uint32_t *ns, uint32_t loc, uint32_t len, V &v)
 {
-    nf = nr = 0;
     int prev[6], hi[6];
     uint32_t rho[6];
-    for (uint32_t f = 0; f < 3; f++) {
-        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
-        prev[f] = (int)f - 1;
-        hi[f] = (int)(f + 2 + 3 * nc);
-        rho[f] = (f + 2) % 3;
-    }
-    for (uint32_t f = 0; f < 3; f++) {
-        const uint32_t nc = len >= f ? (len - f) / 3 : 0;
-        const int top = (int)len - (int)f - 1;
-        prev[3 + f] = top - 3 * (int)nc;
-        hi[3 + f] = top + 3;
-        rho[3 + f] = (uint32_t)((top % 3 + 3) % 3);
-    }
+    frame_bounds(len, prev, hi, rho);
     const uint32_t sh = (loc & 7u) * 4u;
     uint32_t px = 0x44444444u; /* no bases before base 0 */
     for (uint32_t blk = 0; 64 * blk < len; blk++) {
@@ -496,16 +505,14 @@ __device__ __forceinline__ void lane_read_counts_ns(const uint32_t *ns, uint32_t
 #pragma unroll
         for (uint32_t f = 0; f < 6; f++) {
             const uint32_t shf = (rho[f] + 3 - blk % 3) % 3;
-            frame_runs((f < 3 ? ef : er) & (EVERY3 << shf), base, prev[f], nf, nr);
+            frame_runs((f < 3 ? ef : er) & (EVERY3 << shf), base, f, prev[f], v);
         }
     }
 #pragma unroll
     for (uint32_t f = 0; f < 6; f++) {
         const int L = (hi[f] - prev[f]) / 3 - 1;
-        if (L >= (int)MIN_FRAGMENT) {
-            nf++;
-            nr += (uint32_t)L;
-        }
+        if (L >= (int)MIN_FRAGMENT)
+            v(f, prev[f], hi[f], L);
     }
 }
 
@@ -518,9 +525,45 @@ __device__ __forceinline__ void lane_read_counts_ns(const uint32_t *ns, uint32_t
 constexpr uint32_t COUNT_SPAN = 12288;               /* span bytes a wave stages */
 constexpr uint32_t NS_WORDS = COUNT_SPAN / 8 + 16;     /* their nibble string + slack */
 
+/* the wave's span [first, end) of bases as a nibble string in LDS, 16 bytes
+ * per lane per round, coalesced (+1 round of zeros: the funnel shifts' pad);
+ * false when the span does not fit (or is empty).  a = its 16-aligned start. */
+__device__ __forceinline__ bool stage_span(uint32_t *ns, const uint8_t *bases, uint64_t first, uint64_t end,
+                                           uint32_t lane, uintptr_t &a)
+{
+    a = reinterpret_cast<uintptr_t>(bases + first) & ~(uintptr_t)15;
+    const uint64_t bytes = reinterpret_cast<uintptr_t>(bases + end) - a;
+    if (!(end > first && bytes <= COUNT_SPAN))
+        return false;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a);
+    const uint32_t nv = (uint32_t)((bytes + 15) / 16);
+    for (uint32_t i = lane; i < nv + 1; i += 64) {
+        const uint4 v = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        ns[2 * i] = nibbles4(v.x) | nibbles4(v.y) << 16;
+        ns[2 * i + 1] = nibbles4(v.z) | nibbles4(v.w) << 16;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return true;
+}
+
+/* per-frame counting visitor */
+struct RunCount6 {
+    uint32_t nf[6] = {0, 0, 0, 0, 0, 0}, nr[6] = {0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void operator()(uint32_t f, int, int, int L)
+    {
+        nf[f]++;
+        nr[f] += (uint32_t)L;
+    }
+};
+
+/* FRAMES (the anchors' pass): also each frame's fragments and residues,
+ * frame_nf / frame_nr[6r + f] */
+template <bool FRAMES>
 __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases, const uint64_t *read_off,
                                                             uint32_t n_reads, uint2 *read_counts, ulonglong2 *tile_sum,
-                                                            uint32_t n_tiles)
+                                                            uint32_t n_tiles, uint32_t *frame_nf, uint32_t *frame_nr)
 {
     __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -534,28 +577,37 @@ __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases
     const uint64_t ob = lane < n ? read_off[r] : 0, oe = lane < n ? read_off[r + 1] : 0;
     /* the wave's span [a, e): 16-aligned start */
     const uint64_t first = uniform_u64(__shfl(ob, 0)), end = uniform_u64(__shfl(oe, (int)n - 1));
-    const uintptr_t a = reinterpret_cast<uintptr_t>(bases + first) & ~(uintptr_t)15;
-    const uint64_t bytes = reinterpret_cast<uintptr_t>(bases + end) - a;
-    const bool staged = end > first && bytes <= COUNT_SPAN; /* (an empty span reads nothing) */
+    uintptr_t a = 0;
+    const bool staged = stage_span(ns, bases, first, end, lane, a);
     uint32_t nf = 0, nr = 0;
-    if (staged) {
-        /* the span as a nibble string, 16 bytes per lane per round, coalesced
-         * (+1 round of zeros: the funnel shifts' pad) */
-        const uint4 *src = reinterpret_cast<const uint4 *>(a);
-        const uint32_t nv = (uint32_t)((bytes + 15) / 16);
-        for (uint32_t i = lane; i < nv + 1; i += 64) {
-            const uint4 v = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
-            ns[2 * i] = nibbles4(v.x) | nibbles4(v.y) << 16;
-            ns[2 * i + 1] = nibbles4(v.z) | nibbles4(v.w) << 16;
+    if (FRAMES) {
+        if (lane < n) {
+            RunCount6 rc;
+            if (staged)
+                lane_read_runs_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), (uint32_t)(oe - ob),
+                                  rc);
+            else
+                lane_read_runs_global(bases + ob, (uint32_t)(oe - ob), rc);
+#pragma unroll
+            for (uint32_t f = 0; f < 6; f++) {
+                frame_nf[r * 6 + f] = rc.nf[f];
+                frame_nr[r * 6 + f] = rc.nr[f];
+                nf += rc.nf[f];
+                nr += rc.nr[f];
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < n)
-            lane_read_counts_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), (uint32_t)(oe - ob), nf,
-                                nr);
+    } else if (staged) {
+        if (lane < n) {
+            RunCount rc;
+            lane_read_runs_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), (uint32_t)(oe - ob), rc);
+            nf = rc.nf;
+            nr = rc.nr;
+        }
     } else if (lane < n) {
-        lane_read_counts_global(bases + ob, (uint32_t)(oe - ob), nf, nr);
+        RunCount rc;
+        lane_read_runs_global(bases + ob, (uint32_t)(oe - ob), rc);
+        nf = rc.nf;
+        nr = rc.nr;
     }
     if (lane < n)
         read_counts[r] = make_uint2(nf, nr);
@@ -565,6 +617,98 @@ __global__ __launch_bounds__(256) void fq_count_lane_kernel(const uint8_t *bases
         if (tile == n_tiles - 1)
             tile_sum[n_tiles] = make_ulonglong2(0, 0); /* the scan's last element = the totals */
     }
+}
+
+/* writing visitor: fragment records in (frame, position) order.  A reverse
+ * frame's runs are found in ascending base order, which is descending
+ * position on its strand: they are placed from the frame's end backwards. */
+struct RunWrite {
+    uint32_t fi[6]; /* next fragment slot (forward) / last unwritten (reverse) */
+    uint64_t ri[6]; /* next residue offset (forward) / end of the unwritten (reverse) */
+    uint64_t ob;    /* the read's first byte */
+    uint64_t *out_off, *out_anchor;
+    __device__ __forceinline__ void operator()(uint32_t f, int prev, int q, int L)
+    {
+        uint32_t idx;
+        uint64_t ro, anchor;
+        if (f < 3) { /* codons f + 3i: the run starts at base prev + 1 */
+            idx = fi[f]++;
+            ro = ri[f];
+            ri[f] += (uint32_t)L;
+            anchor = (ob + (uint64_t)(prev + 1)) << 1;
+        } else { /* codon i = complement of bases top - 3i .. top - 3i - 2, the
+                  * run's first codon the one after the stop ending at q */
+            idx = fi[f]--;
+            ri[f] -= (uint32_t)L;
+            ro = ri[f];
+            anchor = ((ob + (uint64_t)(q - 3)) << 1) | 1u;
+        }
+        out_off[idx] = ro;
+        out_anchor[idx] = anchor;
+    }
+};
+
+/*
+ * 3'. fragment records without residues (fq_residues = 0): one lane per read,
+ * as the count pass, which left each frame's fragment and residue counts
+ * (frame_nf / frame_nr).  Each fragment gets its offset and anchor = (byte
+ * index of its first codon's first base) << 1 | reverse strand, which the
+ * DNA probe (launch_probe_dna) translates windows from; no residue is written.
+ * Per-fragment read and frame are not written either (the per-(read, frame)
+ * counts hold them): lanes ~10 fragments apart store scattered, and each
+ * array costs ~60 us per 1M reads.
+ */
+__global__ __launch_bounds__(256) void fq_desc_lane_kernel(const uint8_t *bases, const uint64_t *read_off,
+                                                           uint32_t n_reads, const uint2 *read_counts,
+                                                           const ulonglong2 *tile_base, uint32_t n_tiles,
+                                                           const uint32_t *frame_nf, const uint32_t *frame_nr,
+                                                           uint32_t *frag_base, uint64_t *out_off, uint64_t *out_anchor)
+{
+    __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x * WAVES_PER_WG + wv;
+    if (tile >= n_tiles)
+        return;
+    uint32_t *ns = nspan[wv];
+    const uint64_t r0 = (uint64_t)tile * FQ_TILE;
+    const uint32_t n = (uint32_t)std::min<uint64_t>(FQ_TILE, n_reads - r0);
+    const uint64_t r = r0 + lane;
+    const uint64_t ob = lane < n ? read_off[r] : 0, oe = lane < n ? read_off[r + 1] : 0;
+    /* the read's first fragment and residue: the tile's base + the earlier reads' counts */
+    const uint2 cnt = lane < n ? read_counts[r] : make_uint2(0, 0);
+    uint64_t pf = cnt.x, pr = cnt.y;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t xf = __shfl_up(pf, o), xr = __shfl_up(pr, o);
+        if (lane >= o) {
+            pf += xf;
+            pr += xr;
+        }
+    }
+    const ulonglong2 tb = tile_base[tile];
+    const uint64_t first = uniform_u64(__shfl(ob, 0)), end = uniform_u64(__shfl(oe, (int)n - 1));
+    uintptr_t a = 0;
+    const bool staged = stage_span(ns, bases, first, end, lane, a);
+    if (lane >= n)
+        return;
+    const uint32_t len = (uint32_t)(oe - ob);
+    RunWrite w;
+    uint64_t fb = tb.x + pf - cnt.x, rb = tb.y + pr - cnt.y;
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        const uint32_t nf = frame_nf[r * 6 + f], nr = frame_nr[r * 6 + f];
+        frag_base[r * 6 + f] = (uint32_t)fb;
+        w.fi[f] = (uint32_t)(f < 3 ? fb : fb + nf - 1);
+        w.ri[f] = f < 3 ? rb : rb + nr;
+        fb += nf;
+        rb += nr;
+    }
+    w.ob = ob;
+    w.out_off = out_off;
+    w.out_anchor = out_anchor;
+    if (staged)
+        lane_read_runs_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), len, w);
+    else
+        lane_read_runs_global(bases + ob, len, w);
 }
 
 struct PairSum {
@@ -697,8 +841,10 @@ namespace kgx {
  * least 11 residues.  Launches: count -> scan of the workgroup sums (hipcub)
  * -> emit, with no host round trip between them; one readback of the totals. */
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
-                 uint64_t n_bases, kgx_fragments *out)
+                 uint64_t n_bases, uint64_t bound, kgx_fragments *out)
 {
+    /* fragments as anchors into the bases (no residues) when asked and the probe can take them */
+    const bool desc = !c->fq_residues && probe_takes_dna(c);
     hipStream_t st = c->stream;
     const uint64_t n_rf = (uint64_t)n_reads * 6;
     const uint64_t max_res = 2 * n_bases, max_frag = max_res / MIN_FRAGMENT + 1;
@@ -712,11 +858,18 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
                                               PairSum(), make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
     const uint64_t ws_bytes = rc_bytes + 2 * ts_bytes + 16 + 256 + scan_bytes + 16;
     HIP_TRY(c->fq_tmp.reserve(ws_bytes));
-    HIP_TRY(c->fq_res.reserve(max_res + 16));
+    if (desc) {
+        HIP_TRY(c->fq_anchor.reserve((max_frag + 1) * 8));
+        HIP_TRY(c->fq_nres.reserve((n_rf + 1) * 4));
+    }
+    else {
+        HIP_TRY(c->fq_res.reserve(max_res + 16));
+        HIP_TRY(c->fq_read.reserve((max_frag + 1) * 4));
+        HIP_TRY(c->fq_frame.reserve(max_frag + 1));
+        HIP_TRY(c->fq_start.reserve((max_frag + 1) * 4));
+    }
     HIP_TRY(c->fq_off.reserve((max_frag + 1) * 8));
-    HIP_TRY(c->fq_read.reserve((max_frag + 1) * 4));
-    HIP_TRY(c->fq_frame.reserve(max_frag + 1));
-    HIP_TRY(c->fq_start.reserve((max_frag + 1) * 4));
+
     HIP_TRY(c->h_fq_tot.resize(2));
     char *ws = static_cast<char *>(c->fq_tmp.p);
     uint2 *read_counts = reinterpret_cast<uint2 *>(ws);
@@ -724,9 +877,14 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     ulonglong2 *tile_base = tile_sum + (n_tiles + 1);
     uint64_t *totals = reinterpret_cast<uint64_t *>(tile_base + (n_tiles + 1));
     void *scan_tmp = ws + ((((rc_bytes + 15) & ~15ull) + 2 * ts_bytes + 16 + 255) & ~255ull);
-    if (n_reads && c->fq_count)
-        hipLaunchKernelGGL(fq_count_lane_kernel, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
-                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_sum, (uint32_t)n_tiles);
+    if (n_reads && desc)
+        hipLaunchKernelGGL(fq_count_lane_kernel<true>, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
+                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_sum, (uint32_t)n_tiles,
+                           c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint32_t>());
+    else if (n_reads && c->fq_count)
+        hipLaunchKernelGGL(fq_count_lane_kernel<false>, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
+                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_sum, (uint32_t)n_tiles,
+                           nullptr, nullptr);
     else if (n_reads)
         hipLaunchKernelGGL(fq_count_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            read_counts, tile_sum);
@@ -736,7 +894,12 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
                                               make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
     hipLaunchKernelGGL(fq_tail_kernel, dim3(1), dim3(1), 0, st, tile_base, n_tiles, n_reads, totals,
                        c->fq_off.as<uint64_t>(), c->fq_fbase.as<uint32_t>(), c->fq_nfrag.as<uint32_t>());
-    if (n_reads)
+    if (n_reads && desc)
+        hipLaunchKernelGGL(fq_desc_lane_kernel, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
+                           dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_base, (uint32_t)n_tiles,
+                           c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
+                           c->fq_off.as<uint64_t>(), c->fq_anchor.as<uint64_t>());
+    else if (n_reads)
         hipLaunchKernelGGL(fq_emit_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            read_counts, tile_base, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
                            c->fq_res.as<uint8_t>(), c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(),
@@ -750,10 +913,13 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     out->n_reads = n_reads;
     out->n_fragments = (uint32_t)nf;
     out->n_residues = nr;
-    out->residues = c->fq_res.as<uint8_t>();
+    out->residues = desc ? nullptr : c->fq_res.as<uint8_t>();
+    out->anchors = desc ? c->fq_anchor.as<uint64_t>() : nullptr;
+    out->bases = d_bases;
+    out->n_bases = bound;
     out->offsets = c->fq_off.as<uint64_t>();
-    out->read = c->fq_read.as<uint32_t>();
-    out->frame = c->fq_frame.as<int8_t>();
+    out->read = desc ? nullptr : c->fq_read.as<uint32_t>();
+    out->frame = desc ? nullptr : c->fq_frame.as<int8_t>();
     out->frame_counts = c->fq_nfrag.as<uint32_t>();
     return KGX_OK;
 }
@@ -927,7 +1093,7 @@ int kgx_fq_fragments_device(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *
         if (ends[1] < ends[0])
             return fail(KGX_EINVAL, "read offsets not monotone");
     }
-    return fq_fragments(c, d_bases, d_read_offsets, n_reads, ends[1] - ends[0], out);
+    return fq_fragments(c, d_bases, d_read_offsets, n_reads, ends[1] - ends[0], ends[1], out);
 }
 
 int kgx_fq_called_reads(kgx_ctx *c, const kgx_fragments *fragments, kgx_fq_called *out)
@@ -962,7 +1128,7 @@ int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets
         HIP_TRY(hipMemcpyAsync(c->fq_bases.p, c->h_res.data(), nb, hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
-    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, nb, out);
+    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, nb, nb, out);
 }
 
 }  // extern "C"

@@ -153,6 +153,12 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         const uint64_t *filter, uint32_t filter_log2_words,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
                         uint32_t lds_kb, hipStream_t stream);
+/* the line probe over fq fragments left as DNA (PACKED16 images, probe_j
+ * 1-4): anchor[s] = (first base of fragment s) << 1 | reverse strand; keys as
+ * launch_probe over the translated residues (HIT_PACKED16 records) */
+hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
+                            const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
+                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, hipStream_t stream);
 /* set the filter bits of every stored key of the resident table */
 hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
                                uint32_t log2_words, hipStream_t stream);

@@ -348,6 +348,106 @@ __device__ __forceinline__ void encode_tile(const uint8_t *__restrict__ residues
     }
 }
 
+/*
+ * The same J windows when the batch is the fq path's fragments left as DNA
+ * (kgx_fq_run_device): fragment s is a run of codons of one frame of a read,
+ * described by anchor[s] = (byte index of its first codon's first base) << 1
+ * | reverse.  Forward, codon i is bases A+3i..A+3i+2; on the reverse strand it
+ * is the complement of bases A-3i, A-3i-1, A-3i-2 (frame -k read backwards,
+ * dna_seq.cc:9-47).  A window's 8 codons are the 24 bytes from A+3p (forward)
+ * or ending at A-3p (reverse), loaded as two 16-B reads; each base becomes
+ * its class through cls_tab (A0 C1 G2 T/U3, anything else 0x40, so a codon
+ * with a non-base indexes past 63) and each codon its residue code through
+ * cod_tab.  A reverse window's 24 bytes are reversed first (byte swaps), so
+ * codon i is bytes 3i..3i+2 either way and its index is complemented by xor
+ * 63.  The keys equal encode_tile's over the translated residues
+ * (kgx_fq_fragments with residues).
+ */
+template <int J>
+__device__ __forceinline__ void encode_tile_dna(const uint8_t *__restrict__ bases, uint64_t n_bases,
+                                                const uint64_t *__restrict__ anchor,
+                                                const uint64_t *__restrict__ wbase, uint32_t s, uint64_t W,
+                                                uint64_t g0, uint32_t lane, const uint8_t *cls_tab,
+                                                const uint8_t *cod_tab, uint64_t *key, bool *ok, uint32_t *pos,
+                                                uint32_t *sq)
+{
+    const uint64_t bm = reinterpret_cast<uintptr_t>(bases) & 3;
+    uint64_t wb_lo = wbase[s], wb_hi = wbase[s + 1], an = anchor[s];
+    uint64_t ab[J], lo[J];
+    uint32_t sh[J];
+    uint4 v0[J], v1[J];
+    bool fast[J], rev[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const uint64_t gw = g0 + 64 * j + lane;
+        const bool act = gw < W;
+        while (act && gw >= wb_hi) {
+            s++;
+            wb_lo = wb_hi;
+            wb_hi = wbase[s + 1];
+            an = anchor[s];
+        }
+        const uint64_t p = gw - wb_lo;
+        pos[j] = (uint32_t)p;
+        sq[j] = s;
+        rev[j] = an & 1u;
+        const uint64_t A = an >> 1;
+        lo[j] = act ? (rev[j] ? A - 3 * p - 23 : A + 3 * p) : 0; /* the window's first byte */
+        const uint64_t a = bm + lo[j];
+        ab[j] = a & ~3ull;
+        sh[j] = (uint32_t)(a - ab[j]);
+        ok[j] = act;
+        fast[j] = act && ab[j] >= bm && ab[j] + 32 <= bm + n_bases;
+        if (fast[j]) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(bases + (ab[j] - bm));
+            v0[j] = q[0];
+            v1[j] = q[1];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        uint32_t d[6];
+        if (fast[j]) {
+            const uint32_t w[7] = {v0[j].x, v0[j].y, v0[j].z, v0[j].w, v1[j].x, v1[j].y, v1[j].z};
+#pragma unroll
+            for (int k = 0; k < 6; k++)
+                d[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh[j]);
+        } else { /* near the buffer's end (or inactive): byte by byte */
+#pragma unroll
+            for (int k = 0; k < 6; k++)
+                d[k] = 0;
+            if (ok[j])
+                for (int i = 0; i < 24; i++)
+                    d[i >> 2] |= (uint32_t)bases[lo[j] + i] << (8 * (i & 3));
+        }
+        /* reverse strand: the span's bytes reversed, so that codon i is bytes
+         * 3i..3i+2 either way (its index then complemented: xor 63) */
+        uint32_t rd[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            rd[k] = __builtin_bswap32(d[5 - k]);
+#pragma unroll
+        for (int k = 0; k < 6; k++)
+            d[k] = rev[j] ? rd[k] : d[k];
+        const uint32_t flip = rev[j] ? 63u : 0u;
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int b0 = 3 * i, b1 = 3 * i + 1, b2 = 3 * i + 2;
+            const uint32_t e1 = cls_tab[(d[b0 >> 2] >> (8 * (b0 & 3))) & 0xFFu];
+            const uint32_t e2 = cls_tab[(d[b1 >> 2] >> (8 * (b1 & 3))) & 0xFFu];
+            const uint32_t e3 = cls_tab[(d[b2 >> 2] >> (8 * (b2 & 3))) & 0xFFu];
+            const uint32_t e = ((e1 << 4) | (e2 << 2) | e3) ^ flip; /* >= 64: a non-base */
+            c[i] = cod_tab[min(e, 64u)]; /* unconditional read: entry 64 = 20 */
+        }
+        const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+        ok[j] = ok[j] && cmax < 20u;
+        const uint32_t ka = ((c[0] * 20 + c[1]) * 20 + c[2]) * 20 + c[3];
+        const uint32_t kb = ((c[4] * 20 + c[5]) * 20 + c[6]) * 20 + c[7];
+        key[j] = (uint64_t)ka * 160000u + kb;
+    }
+}
+
 /* ordered compaction of a tile's hits; one mask word per slice.  PACKED:
  * pv = the matching PACKED16 record, stored as is (HIT_PACKED16); else pv =
  * the 16 B after the key of the matching AOS24 bucket, stored as the two
@@ -509,7 +609,7 @@ __global__ __launch_bounds__(256) void probe_kernel(
  * num_sigs buckets -- same answer, since every bucket has been seen).
  * The matching lane writes the record to LDS for the window's owner.
  */
-template <int J, int G>
+template <int J, int G, bool DNA>
 __global__ __launch_bounds__(256) void probe_line_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
@@ -519,10 +619,19 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     constexpr uint32_t T = 64 * J;
     constexpr uint32_t NQ = 64 / G; /* windows per instruction */
     constexpr int NI = J * G;       /* instructions per tile */
-    __shared__ uint8_t code_tab[256];
+    __shared__ uint8_t code_tab[256]; /* residue -> code; DNA: base -> class */
+    __shared__ uint8_t cod_tab[DNA ? 68 : 1];
     __shared__ uint4 lds_rec[PROBE_WAVES][T];
     __shared__ uint8_t lds_hit[PROBE_WAVES][T];
-    code_tab[threadIdx.x] = (uint8_t)residue_code(threadIdx.x);
+    if (DNA) {
+        const uint32_t b = threadIdx.x | 0x20u; /* ACGTU either case (trans_table.h:45-68) */
+        const bool base = b == 'a' || b == 'c' || b == 'g' || b == 't' || b == 'u';
+        code_tab[threadIdx.x] = base ? (uint8_t)(((b >> 1) ^ (b >> 2)) & 3u) : (uint8_t)0x40;
+        if (threadIdx.x < 65)
+            cod_tab[threadIdx.x] = threadIdx.x < 64 ? (uint8_t)residue_code((uint8_t)code11_aa(threadIdx.x)) : 20;
+    } else {
+        code_tab[threadIdx.x] = (uint8_t)residue_code(threadIdx.x);
+    }
     __syncthreads();
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -536,8 +645,12 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     uint64_t key[J];
     uint32_t pos[J], sq[J];
     bool ok[J];
-    encode_tile<J>(residues, n_residues, seq_off, wbase, tile_seq[tile], W, g0, lane, code_tab, key, ok,
-                   pos, sq);
+    if (DNA)
+        encode_tile_dna<J>(residues, n_residues, seq_off, wbase, tile_seq[tile], W, g0, lane, code_tab, cod_tab,
+                           key, ok, pos, sq);
+    else
+        encode_tile<J>(residues, n_residues, seq_off, wbase, tile_seq[tile], W, g0, lane, code_tab, key, ok,
+                       pos, sq);
     uint64_t home[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -614,13 +727,13 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     store_tile_hits<J, true>(hit, key, pv, pos, sq, g0, W, lane, hot, cold, hit_mask);
 }
 
-template <int J, int G>
+template <int J, int G, bool DNA = false>
 static void launch_probe_line(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                               const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
                               uint32_t n_seq, const void *table, uint64_t num_sigs, uint4 *hot, uint4 *cold,
                               uint64_t *hit_mask, uint32_t dyn_lds)
 {
-    hipLaunchKernelGGL((probe_line_kernel<J, G>), grid, dim3(64 * PROBE_WAVES), dyn_lds, stream, residues,
+    hipLaunchKernelGGL((probe_line_kernel<J, G, DNA>), grid, dim3(64 * PROBE_WAVES), dyn_lds, stream, residues,
                        n_residues, seq_off, wbase, tile_seq, n_seq, static_cast<const uint4 *>(table),
                        num_sigs, mod_magic(num_sigs), hot, cold, hit_mask);
 }
@@ -713,6 +826,27 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
     }
 #undef KGX_PROBE_J
     return hipGetLastError();
+}
+
+hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
+                            const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
+                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, hipStream_t stream)
+{
+    if (max_tiles == 0)
+        return hipSuccess;
+    const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+#define KGX_DNA(JJ)                                                                                  \
+    launch_probe_line<JJ, 4, true>(grid, stream, bases, n_bases, anchor, wbase, tile_seq, n_seq, table,  \
+                                   num_sigs, hot, nullptr, hit_mask, 0);                            \
+    return hipGetLastError()
+    switch (probe_j) {
+    case 1: KGX_DNA(1);
+    case 2: KGX_DNA(2);
+    case 3: KGX_DNA(3);
+    case 4: KGX_DNA(4);
+    default: return hipErrorInvalidValue;
+    }
+#undef KGX_DNA
 }
 
 /* ------------------------------------------------------------------------ */

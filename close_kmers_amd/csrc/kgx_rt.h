@@ -225,8 +225,15 @@ class HostPool {
     bool stop_ = false;
 };
 
+/* n_bases: the bytes the reads span (bounds the output); bound: bytes
+ * readable from d_bases (the DNA probe's limit) */
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
-                 uint64_t n_bases, kgx_fragments *out);
+                 uint64_t n_bases, uint64_t bound, kgx_fragments *out);
+/* kgx_stage_probe over fragments left as DNA (launch_probe_dna) */
+int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const uint64_t *anchors,
+                    const uint64_t *d_off);
+/* whether this context's probe can take fragments as DNA */
+bool probe_takes_dna(const kgx_ctx *c);
 
 }  // namespace kgx
 
@@ -279,7 +286,8 @@ struct kgx_ctx {
     kgx::DevBuf best, best_ws, bc_calls, bc_start, bc_count; /* KGX_WANT_BEST / kgx_find_best_calls */
     kgx::PinnedVec<kgx_best_call> h_best;
     /* fq fragments (kgx_fq.hip) */
-    kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start;
+    kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start,
+        fq_anchor, fq_nres;
     kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
     /* kgx_fq_called_reads */
     kgx::DevBuf fqc_flag, fqc_reads, fqc_nsel, fqc_nfrag, fqc_ncall, fqc_fo, fqc_co, fqc_fc, fqc_len, fqc_coff,
@@ -291,6 +299,7 @@ struct kgx_ctx {
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
     int probe_lds_kb = 0;  /* LDS reserved per probe workgroup, caps its occupancy (option "probe_lds_kb") */
+    int fq_residues = 1;   /* 1: kgx_fq_fragments writes residues; 0: anchors (kgx_fq_run_device) */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
     int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */

@@ -975,6 +975,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->fq_count = (int)value;
         return KGX_OK;
     }
+    if (n == "fq_residues") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "fq_residues must be 0 or 1");
+        c->fq_residues = (int)value;
+        return KGX_OK;
+    }
     if (n == "score_variant") {
         if (value < 0 || value > 2)
             return fail(KGX_EINVAL, "score_variant must be 0, 1 or 2");
@@ -1066,10 +1072,15 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     return KGX_OK;
 }
 
-int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
+}  // extern "C"
+
+namespace {
+
+/* one probe launch on c's stream; with probe_serialize it waits for the
+ * image's previous probe, whichever context issued it */
+template <class Launch>
+int probe_chained(kgx_ctx *c, Launch launch)
 {
-    if (!c || (!d_res && c->n_residues) || d_off != c->d_off)
-        return fail(KGX_EINVAL, "probe: residues missing or offsets differ from the plan");
     HIP_TRY(hipSetDevice(c->img->device));
     if (c->img->num_sigs >= (1ull << 40))
         return fail(KGX_ERANGE, "image too large");
@@ -1080,12 +1091,7 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
         if (img->last_probe && img->last_probe != c->probe_done)
             HIP_TRY(hipStreamWaitEvent(c->stream, img->last_probe, 0));
     }
-    HIP_TRY(launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(),
-                         c->tile_seq.as<uint32_t>(), c->n_seq, c->max_tiles, c->img->resident(),
-                         c->img->layout, c->img->num_sigs,
-                         c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
-                         c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
-                         (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb, c->stream));
+    HIP_TRY(launch());
     if (c->probe_serialize) {
         HIP_TRY(hipEventRecord(c->probe_done, c->stream));
         img->last_probe = c->probe_done;
@@ -1095,6 +1101,52 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
     c->have_hits = true;
     return KGX_OK;
 }
+
+}  // namespace
+
+namespace kgx {
+
+bool probe_takes_dna(const kgx_ctx *c)
+{
+    return c->img->layout == KGX_LAYOUT_PACKED16 && !(c->probe_filter && c->img->d_filter) &&
+           (c->probe_variant == PROBE_AUTO || c->probe_variant == PROBE_LINE) && c->probe_j >= 1 && c->probe_j <= 4;
+}
+
+int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const uint64_t *anchors,
+                    const uint64_t *d_off)
+{
+    if ((!anchors || !bases) && c->n_seq)
+        return fail(KGX_EINVAL, "fq probe: anchors or bases missing");
+    if (d_off != c->d_off)
+        return fail(KGX_EINVAL, "fq probe: offsets differ from the plan");
+    if (!probe_takes_dna(c) || (int)(c->tile_windows / 64) != c->probe_j)
+        return fail(KGX_EINVAL, "fq probe: fragments without residues need the line probe on a PACKED16 image "
+                                "(set fq_residues 1 for other probes)");
+    return probe_chained(c, [&] {
+        return launch_probe_dna(bases, n_bases, anchors, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                                c->n_seq, c->max_tiles, c->img->resident(), c->img->num_sigs, c->hits.as<uint4>(),
+                                c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64), c->stream);
+    });
+}
+
+}  // namespace kgx
+
+extern "C" {
+
+int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
+{
+    if (!c || (!d_res && c->n_residues) || d_off != c->d_off)
+        return fail(KGX_EINVAL, "probe: residues missing or offsets differ from the plan");
+    return probe_chained(c, [&] {
+        return launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                            c->n_seq, c->max_tiles, c->img->resident(), c->img->layout, c->img->num_sigs,
+                            c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
+                            c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
+                            (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb, c->stream);
+    });
+}
+
+
 
 int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
 {
@@ -1198,6 +1250,23 @@ int kgx_run_device(kgx_ctx *c, const kgx_params *params, const uint8_t *d_res, c
     if (rc)
         return rc;
     if ((rc = kgx_stage_probe(c, d_res, d_off)))
+        return rc;
+    if ((rc = kgx_stage_score(c, params, want)))
+        return rc;
+    return out ? kgx_device_result_get(c, out) : KGX_OK;
+}
+
+int kgx_fq_run_device(kgx_ctx *c, const kgx_params *params, const kgx_fragments *fr, uint32_t want,
+                      kgx_device_result *out)
+{
+    if (!c || !fr)
+        return fail(KGX_EINVAL, "null argument");
+    if (fr->residues || fr->n_fragments == 0)
+        return kgx_run_device(c, params, fr->residues, fr->offsets, fr->n_fragments, fr->n_residues, want, out);
+    int rc = kgx_stage_plan(c, fr->offsets, fr->n_fragments, fr->n_residues);
+    if (rc)
+        return rc;
+    if ((rc = stage_probe_dna(c, fr->bases, fr->n_bases, fr->anchors, fr->offsets)))
         return rc;
     if ((rc = kgx_stage_score(c, params, want)))
         return rc;

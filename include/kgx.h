@@ -296,6 +296,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "score_wave_tiles" (1..256, default 16) = probe tiles of windows per wave;
  * "fq_count" 1 (default) = the fq count pass scans stop codons one lane per
  * read, 0 = it translates like the emit pass (one wave per read);
+ * "fq_residues" 1 (default) = kgx_fq_fragments writes the fragments'
+ * residues; 0 = fragment anchors only (see kgx_fragments), for
+ * kgx_fq_run_device;
  * "host_chunks" (1..64, default 6): kgx_process_batch splits a batch into up
  * to this many residue-balanced chunks of whole sequences (at least 2M
  * residues each; with "host_taper" 1, the default, the first and last are
@@ -430,16 +433,28 @@ int kgx_device_batch_collect(kgx_ctx *ctx, uint32_t want, kgx_result *out);
  * split at '*', fragments longer than 10 residues kept
  * (fq_process_request.cc:329-343).  The fragments form a protein batch in
  * (read, frame, position) order, on the device, owned by ctx and valid until
- * the next fq call: feed it to kgx_run_device. */
+ * the next fq call: feed it to kgx_fq_run_device (or, when residues is set,
+ * kgx_run_device).
+ *
+ * With the context option "fq_residues" 0 (and a PACKED16 image probed by the
+ * line probe, probe_j 1-4) the residues are not written: residues is NULL and
+ * each fragment carries an anchor into the reads' bases instead, from which
+ * kgx_fq_run_device's probe translates each window's 8 codons itself; read
+ * and frame are NULL too (frame_counts gives both: read r's fragments are
+ * frame_counts[6r..6r+5] of frames 1, 2, 3, -1, -2, -3 in turn). */
 typedef struct kgx_fragments {
     uint32_t n_reads;
     uint32_t n_fragments;
     uint64_t n_residues;
-    const uint8_t *residues;  /* device: fragment residues, concatenated */
+    const uint8_t *residues;  /* device: fragment residues, concatenated (NULL: anchors) */
     const uint64_t *offsets;  /* device: [n_fragments + 1] */
-    const uint32_t *read;     /* device: read index of each fragment */
-    const int8_t *frame;      /* device: frame of each fragment */
+    const uint32_t *read;     /* device: read index of each fragment (NULL with anchors) */
+    const int8_t *frame;      /* device: frame of each fragment (NULL with anchors) */
     const uint32_t *frame_counts; /* device: fragments per (read, frame), [n_reads * 6] */
+    const uint64_t *anchors;  /* device, when residues is NULL: per fragment (byte index in bases of its
+                                 first codon's first base) << 1 | 1 on the reverse strand */
+    const uint8_t *bases;     /* device: the reads' bases the anchors index */
+    uint64_t n_bases;         /* bytes readable from bases */
 } kgx_fragments;
 /* reads from host memory (bases concatenated, read_offsets[n_reads + 1]) */
 int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
@@ -447,6 +462,11 @@ int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offse
 /* reads already in device memory */
 int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint32_t n_reads, kgx_fragments *out);
+/* lookup + run scoring of a fragment batch: kgx_run_device over
+ * (residues, offsets) when the residues were written, else plan, the probe
+ * over the anchors (windows translated from the bases), score.  Same results. */
+int kgx_fq_run_device(kgx_ctx *ctx, const kgx_params *params, const kgx_fragments *fragments, uint32_t want,
+                      kgx_device_result *out);
 
 /* After kgx_run_device over a kgx_fragments batch (with KGX_WANT_CALLS): only
  * the reads that have a call in some fragment, in read order, with what the

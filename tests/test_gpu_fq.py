@@ -156,6 +156,105 @@ def test_fragments_of_long_and_empty_batches(gpu, oracle_lib):
         assert got.get(r, []) == oracle_lib.fq_fragments(dna), r
 
 
+_CODE11 = "KNKNTTTTRSRSIIMIQHQHPPPPRRRRLLLLEDEDAAAAGGGGVVVV*Y*YSSSS*CWCLFLF"
+_CLS = {c: i for i, c in enumerate("ACGT")} | {"U": 3}
+
+
+def _translate_anchor(bases: bytes, anchor: int, n: int) -> str:
+    """n residues from a fragment anchor: (first base) << 1 | reverse."""
+    a, rev = anchor >> 1, anchor & 1
+    out = []
+    for i in range(n):
+        if rev:
+            cs = [_CLS.get(chr(bases[a - 3 * i - k]).upper()) for k in range(3)]
+            cs = [None if c is None else 3 - c for c in cs]
+        else:
+            cs = [_CLS.get(chr(bases[a + 3 * i + k]).upper()) for k in range(3)]
+        out.append("X" if None in cs else _CODE11[cs[0] * 16 + cs[1] * 4 + cs[2]])
+    return "".join(out)
+
+
+def _anchor_reads(rng):
+    reads = _random_reads(rng, 500)
+    stoppy = np.frombuffer(b"TAAGTGATAGCTTATCAACGT", np.uint8)
+    for i in range(120):  # long reads: several stop-scan blocks, the unstaged path
+        L = int(rng.integers(150, 1200))
+        pool = stoppy if i % 3 == 0 else np.frombuffer(b"ACGTACGTACGTacgtNnUuRYKX", np.uint8)
+        reads.append(bytes(pool[rng.integers(0, len(pool), L)]))
+    reads += [bytes(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 30000)])]
+    return reads
+
+
+@pytest.mark.parametrize("fq_count", [0, 1])
+def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count):
+    """fq_residues 0: the same fragment records (offsets, read, frame, frame
+    counts) as with residues, and each anchor translates to the fragment's
+    residues (forward and reverse strand, IUPAC and lower case, long reads)."""
+    spec, table = synthetic_table(20000)
+    reads = _anchor_reads(np.random.default_rng(21))
+    res, off = pack([("r", r) for r in reads])
+    bases = bytes(res)
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        ctx.set_option("fq_count", fq_count)
+        h1 = ctx.fragments_to_host(ctx.fq_fragments(res, off))
+        ctx.set_option("fq_residues", 0)
+        f0 = ctx.fq_fragments(res, off)
+        h0 = ctx.fragments_to_host(f0)
+    assert h0["residues"] is None and h0["read"] is None and f0.n_bases == len(bases)
+    for k in ("offsets", "frame_counts"):
+        assert np.array_equal(h0[k], h1[k]), k
+    # read and frame of each fragment, from the per-(read, frame) counts
+    fc = h0["frame_counts"]
+    assert np.array_equal(np.repeat(np.arange(len(fc)) // 6, fc), h1["read"])
+    assert np.array_equal(np.repeat(np.tile(np.array([1, 2, 3, -1, -2, -3], np.int8), len(fc) // 6), fc),
+                          h1["frame"])
+    o = h1["offsets"].astype(np.int64)
+    for i in range(f0.n_fragments):
+        want = bytes(h1["residues"][o[i]:o[i + 1]]).decode()
+        assert _translate_anchor(bases, int(h0["anchors"][i]), len(want)) == want, i
+    assert f0.n_fragments > 1000 and (h0["anchors"] & 1).sum() > 100
+
+
+def test_fragment_lookup_dna_probe_matches_oracle(gpu, oracle_lib):
+    """kgx_fq_run_device over anchors (the probe translating codons itself)
+    gives the oracle's hits and calls over the translated fragments, and the
+    same device results as the residue probe."""
+    from close_kmers_amd import synth
+    from tests_golden_codons import back_translate, revcomp
+    spec, table = synthetic_table(40000)
+    rng = np.random.default_rng(5)
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(30))].reshape(30, -1)
+    reads = []
+    for i in range(300):
+        p = bytes(src[i % 30][int(rng.integers(0, 200)):][:60]).decode()
+        d = bytearray(back_translate(p, rng).encode())
+        if i % 5 == 0:  # ambiguity codes and lower case inside planted runs
+            for j in rng.integers(0, len(d), 3):
+                d[j] = b"NnRacgt"[int(rng.integers(0, 7))]
+        d = bytes(d).decode()
+        reads.append((d if i % 2 else revcomp(d)).encode())
+    res, off = pack([("r", r) for r in reads])
+    prm = gpu.Params(5, 200, 0, 0)
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        h = ctx.fragments_to_host(ctx.fq_fragments(res, off))
+        ref = ctx.run_fragments(ctx.fq_fragments(res, off), prm, want=3)
+        ctx.set_option("fq_residues", 0)
+        f = ctx.fq_fragments(res, off)
+        assert not f.residues
+        got = ctx.run_fragments(f, prm, want=3)
+    want = oracle_lib.process_batch(table, h["residues"], h["offsets"], want=3)
+    for r in (got, ref):
+        assert np.array_equal(r.hit_offsets, want.hit_offsets)
+        for k in ("which_kmer", "pos", "function_index", "otu_index", "avg_from_end"):
+            assert np.array_equal(r.hits[k], want.hits[k]), k
+        assert np.array_equal(r.call_offsets, want.call_offsets)
+        for k in ("start", "end", "count", "function_index"):
+            assert np.array_equal(r.calls[k], want.calls[k]), k
+        assert np.array_equal(r.calls["weighted_hits"].view(np.uint32),
+                              want.calls["weighted_hits"].view(np.uint32))
+    assert len(want.calls) > 50 and len(want.hits) > 2000
+
+
 _BACK = {"A": "GCT", "C": "TGT", "D": "GAT", "E": "GAA", "F": "TTT", "G": "GGT", "H": "CAT", "I": "ATT",
          "K": "AAA", "L": "CTT", "M": "ATG", "N": "AAT", "P": "CCT", "Q": "CAA", "R": "CGT", "S": "TCT",
          "T": "ACT", "V": "GTT", "W": "TGG", "Y": "TAT"}

@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts alternating over chunks")
     ap.add_argument("--score-variant", type=int, default=-1, help="-1 = the library default")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="-1 = the library default")
+    ap.add_argument("--fq-residues", type=int, default=0,
+                    help="1 = fragments with residues + the residue probe; 0 (default) = anchors + the DNA probe")
     args = ap.parse_args()
 
     from close_kmers_amd import abi, image_files, synth
@@ -67,6 +69,7 @@ def main():
             c.set_option("score_variant", args.score_variant)
         if args.probe_lds_kb >= 0:
             c.set_option("probe_lds_kb", args.probe_lds_kb)
+        c.set_option("fq_residues", args.fq_residues)
     n, Lr = args.n_reads, args.length
     rng = np.random.default_rng(0x5EED0004)
     bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
@@ -89,8 +92,8 @@ def main():
             abi.check(L.kgx_fq_fragments_device(c.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
                       "fq_fragments")
             dr = abi.DeviceResult()
-            abi.check(L.kgx_run_device(c.handle, ctypes.byref(params), f.residues, f.offsets, f.n_fragments,
-                                       f.n_residues, abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
+            abi.check(L.kgx_fq_run_device(c.handle, ctypes.byref(params), ctypes.byref(f),
+                                          abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
             if collect_stats:
                 hc = np.zeros(f.n_fragments, np.uint32)
                 cc = np.zeros(f.n_fragments, np.uint32)
@@ -129,7 +132,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),

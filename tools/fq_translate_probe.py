@@ -27,12 +27,14 @@ def main():
     ap.add_argument("--length", type=int, default=150)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fq-count", type=int, default=1, help="count pass: 1 = lane-per-read stop scan, 0 = wave translation")
+    ap.add_argument("--fq-residues", type=int, default=1, help="1 = emit residues, 0 = fragment anchors only")
     args = ap.parse_args()
     from close_kmers_amd import abi
     L = abi.lib()
     img, _ = abi.Image.synthetic(20000, 101533)
     ctx = abi.Context(img)
     ctx.set_option("fq_count", args.fq_count)
+    ctx.set_option("fq_residues", args.fq_residues)
     n, Lr = args.n_reads, args.length
     rng = np.random.default_rng(0x5EED0004)
     bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
@@ -49,7 +51,7 @@ def main():
         t0 = time.perf_counter()
         abi.check(L.kgx_fq_fragments_device(ctx.handle, d_b, d_o, n, ctypes.byref(f)), "fq")
         times.append(time.perf_counter() - t0)
-    print(json.dumps({"fq_count": args.fq_count, "n_reads": n, "read_len": Lr, "ms_per_call": float(np.median(times)) * 1e3,
+    print(json.dumps({"fq_count": args.fq_count, "fq_residues": args.fq_residues, "n_reads": n, "read_len": Lr, "ms_per_call": float(np.median(times)) * 1e3,
                       "fragments": f.n_fragments, "residues": f.n_residues}), flush=True)
     L.kgx_device_free(d_b)
     L.kgx_device_free(d_o)
