@@ -200,6 +200,23 @@ hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64
 size_t count_scan_workspace_bytes(uint32_t n);
 hipError_t launch_count_scan(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
                              uint64_t *o1, uint64_t *o2, void *workspace, hipStream_t stream);
+/* small batches: up to SMALL_PIECES arrays of 16-B words copied from mapped
+ * pinned host memory to HBM in one launch (piece p covers words
+ * [end16[p-1], end16[p]) of the concatenation) */
+constexpr int SMALL_PIECES = 5;
+struct SmallPieces {
+    uint4 *dst[SMALL_PIECES];
+    const uint4 *src[SMALL_PIECES];
+    uint64_t end16[SMALL_PIECES];
+};
+hipError_t launch_small_upload(const SmallPieces &pc, hipStream_t stream);
+/* one workgroup: launch_count_scan's offsets into o* (HBM) and h* (mapped
+ * host), plus status[0], wbase[n] and (best_host non-NULL) best[0, n) */
+hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
+                                uint64_t *o1, uint64_t *o2, uint64_t *h0, uint64_t *h1, uint64_t *h2,
+                                const uint32_t *status, const uint64_t *wbase, const kgx_best_call *best,
+                                kgx_best_call *best_host, uint32_t *status_host, uint64_t *nwin_host,
+                                hipStream_t stream);
 /* min(*count, cap) elements of elem_bytes (a multiple of 4) from src to dst,
  * both 16-byte aligned */
 hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count, uint64_t cap,

@@ -1979,6 +1979,91 @@ hipError_t launch_count_scan(uint32_t n, const uint32_t *c0, const uint32_t *c1,
     return hipGetLastError();
 }
 
+/* ------------------------------------------------------------------------ */
+/* small batches (one or a few sequences, e.g. the facade's process_aa_seq): */
+/* the host plans the batch itself and the device reads it from mapped      */
+/* pinned memory, and the counts are scanned and the results land in mapped */
+/* memory too, so a batch costs one host wait and no DMA copies             */
+/* ------------------------------------------------------------------------ */
+
+/* pieces of mapped pinned host memory -> HBM: one 16-B load per thread over
+ * the pieces' concatenation (one PCIe round trip for a small batch) */
+__global__ __launch_bounds__(256) void small_upload_kernel(SmallPieces pc)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pc.end16[SMALL_PIECES - 1];
+         i += stride) {
+        int p = 0;
+#pragma unroll
+        for (int k = 0; k < SMALL_PIECES - 1; k++)
+            p += i >= pc.end16[k];
+        const uint64_t j = i - (p ? pc.end16[p - 1] : 0);
+        pc.dst[p][j] = pc.src[p][j];
+    }
+}
+
+hipError_t launch_small_upload(const SmallPieces &pc, hipStream_t stream)
+{
+    const uint64_t n16 = pc.end16[SMALL_PIECES - 1];
+    if (n16 == 0)
+        return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n16 + 255) / 256, 256);
+    hipLaunchKernelGGL(small_upload_kernel, dim3(blocks), dim3(256), 0, stream, pc);
+    return hipGetLastError();
+}
+
+/* one workgroup: the dense CSR offsets of up to three count arrays, stored in
+ * HBM (the gather's) and in mapped host memory (the caller's), plus the plan
+ * status word, the window total and the best calls */
+__global__ __launch_bounds__(256) void small_collect_kernel(Counts3 cnt, uint32_t n, Offsets3 off, Offsets3 off_host,
+                                                            const uint32_t *__restrict__ status,
+                                                            const uint64_t *__restrict__ wbase,
+                                                            const kgx_best_call *__restrict__ best,
+                                                            kgx_best_call *__restrict__ best_host,
+                                                            uint32_t *__restrict__ status_host,
+                                                            uint64_t *__restrict__ nwin_host)
+{
+    __shared__ uint64_t lds4[3][4];
+    uint64_t carry[3] = {0, 0, 0};
+    for (uint32_t base = 0; base <= n; base += CS_TILE) {
+        const uint32_t i0 = base + threadIdx.x * CS_PER;
+        for (int a = 0; a < 3; a++) {
+            uint64_t tot;
+            const uint64_t mine = thread_count(cnt.c[a], n, i0);
+            uint64_t at = carry[a] + block_scan(mine, lds4[a], tot) - mine;
+            for (uint32_t k = 0; k < CS_PER && i0 + k <= n; k++) {
+                off.o[a][i0 + k] = at;
+                off_host.o[a][i0 + k] = at;
+                if (cnt.c[a] && i0 + k < n)
+                    at += cnt.c[a][i0 + k];
+            }
+            carry[a] += tot;
+        }
+        __syncthreads(); /* lds4 is rewritten by the next round */
+    }
+    if (best_host)
+        for (uint32_t s = threadIdx.x; s < n; s += blockDim.x)
+            best_host[s] = best[s];
+    if (threadIdx.x == 0) {
+        status_host[0] = status[0];
+        nwin_host[0] = wbase[n];
+    }
+}
+
+hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
+                                uint64_t *o1, uint64_t *o2, uint64_t *h0, uint64_t *h1, uint64_t *h2,
+                                const uint32_t *status, const uint64_t *wbase, const kgx_best_call *best,
+                                kgx_best_call *best_host, uint32_t *status_host, uint64_t *nwin_host,
+                                hipStream_t stream)
+{
+    Counts3 cnt = {{c0, c1, c2}};
+    Offsets3 off = {{o0, o1, o2}};
+    Offsets3 off_host = {{h0, h1, h2}};
+    hipLaunchKernelGGL(small_collect_kernel, dim3(1), dim3(256), 0, stream, cnt, n, off, off_host, status, wbase,
+                       best, best_host, status_host, nwin_host);
+    return hipGetLastError();
+}
+
 /* min(*count, cap) elements of elem_bytes each, src -> dst: the size comes
  * from the device (a chunk's scanned total), the room from the host.  The
  * bytes move as 16-B stores (one 1-KB run per wave instruction over PCIe),

@@ -232,6 +232,8 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
 /* kgx_stage_probe over fragments left as DNA (launch_probe_dna) */
 int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const uint64_t *anchors,
                     const uint64_t *d_off);
+/* kgx_stage_plan's buffers and bookkeeping without the plan kernels */
+int plan_reserve(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_residues);
 /* whether this context's probe can take fragments as DNA */
 bool probe_takes_dna(const kgx_ctx *c);
 
@@ -357,6 +359,11 @@ struct kgx_ctx {
     kgx::PinnedVec<uint32_t> h_counts;
     kgx::PinnedVec<uint32_t> h_hits12; /* 12-B records (3 words per hit, no key) */
     int host_rec12 = 1; /* streamed: 12-B records, key re-encoded on the host (option "host_rec12") */
+    /* small host batches (<= small_batch residues, option "small_batch", 0 =
+     * off): planned on the host, read by the device from the mapped staging
+     * blob, results stored into mapped memory: one host wait per batch */
+    int64_t small_batch = 1 << 16;
+    kgx::PinnedVec<uint4> h_small; /* offsets | window bases | tile owners | status | residues */
     int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
     kgx::PinnedVec<kgx_call> h_calls_region;
     kgx::PinnedVec<kgx_otu> h_otus_region;

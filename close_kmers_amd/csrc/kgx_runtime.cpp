@@ -963,6 +963,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->host_threads = (int)value;
         return KGX_OK;
     }
+    if (n == "small_batch") {
+        if (value < 0 || value > (1 << 24))
+            return fail(KGX_EINVAL, "small_batch must be 0..16777216 residues");
+        c->small_batch = value;
+        return KGX_OK;
+    }
     if (n == "host_chunks") {
         if (value < 1 || value > 64)
             return fail(KGX_EINVAL, "host_chunks must be 1..64");
@@ -1042,6 +1048,23 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     if (n_residues > (1ull << 40))
         return fail(KGX_ERANGE, "batch too large");
     HIP_TRY(hipSetDevice(c->img->device));
+    int rc = kgx::plan_reserve(c, d_off, n_seq, n_residues);
+    if (rc)
+        return rc;
+    HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
+    HIP_TRY(launch_plan(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                        c->tile_windows, c->plan_ws.p, c->plan_status.as<uint32_t>(), c->stream));
+    return KGX_OK;
+}
+
+}  // extern "C"
+
+namespace kgx {
+
+/* the plan's buffers and bookkeeping (everything of kgx_stage_plan but the
+ * plan kernels; the small-batch path writes the plan from the host) */
+int plan_reserve(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_residues)
+{
     /* bounds: windows <= residues, so tiles <= residues / tile + 1 */
     const uint32_t tile_windows = 64u * (uint32_t)c->probe_j;
     const uint64_t max_tiles = n_residues / tile_windows + 1;
@@ -1056,10 +1079,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     HIP_TRY(c->ranges.reserve(cap_win * 2 * sizeof(uint32_t)));
     HIP_TRY(c->hit_count.reserve((n_seq + 1) * sizeof(uint32_t)));
     HIP_TRY(c->call_count.reserve((n_seq + 1) * sizeof(uint32_t)));
-    HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
-    HIP_TRY(c->plan_status.reserve(2 * sizeof(uint32_t))); /* [0] bad offsets, [1] longest sequence (windows) */
-    HIP_TRY(launch_plan(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                        tile_windows, c->plan_ws.p, c->plan_status.as<uint32_t>(), c->stream));
+    HIP_TRY(c->plan_status.reserve(4 * sizeof(uint32_t))); /* [0] bad offsets, [1] longest sequence (windows) */
     c->n_seq = n_seq;
     c->n_residues = n_residues;
     c->max_tiles = max_tiles;
@@ -1072,7 +1092,7 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     return KGX_OK;
 }
 
-}  // extern "C"
+}  // namespace kgx
 
 namespace {
 
@@ -2101,6 +2121,139 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     return KGX_OK;
 }
 
+inline uint64_t round16(uint64_t bytes) { return (bytes + 15) & ~15ull; }
+
+/* A small host batch (process_aa_seq's one sequence, a request's few) in one
+ * host wait: the host writes the plan (window bases, tile owners, longest
+ * sequence) beside the staged residues and offsets in one pinned blob, one
+ * kernel pulls the blob into the plan's buffers, the probe and scorer run as
+ * for any batch, and one workgroup scans the counts into the CSR offsets, which
+ * the gather uses to store the records straight into mapped result arrays
+ * sized for the worst case (every window a hit).  Same kernels, same records
+ * as kgx_run_device + kgx_device_batch_collect. */
+int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                        uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq);
+    if (rc)
+        return rc;
+    const uint64_t n_res = c->h_res.size();
+    const uint64_t *off = c->h_off_stage.data();
+    HIP_TRY(c->residues.reserve(round16(n_res + 16)));
+    HIP_TRY(c->offsets.reserve(round16((n_seq + 1) * sizeof(uint64_t))));
+    if ((rc = plan_reserve(c, c->offsets.as<uint64_t>(), n_seq, n_res)))
+        return rc;
+    HIP_TRY(c->wbase.reserve(round16((n_seq + 1) * sizeof(uint64_t))));
+    HIP_TRY(c->tile_seq.reserve(round16(c->max_tiles * sizeof(uint32_t))));
+    /* the blob: offsets | window bases | tile owners | status | residues */
+    const uint64_t b_off = round16((n_seq + 1) * sizeof(uint64_t)), b_wb = b_off,
+                   b_tile = round16(c->max_tiles * sizeof(uint32_t)), b_st = 16, b_res = round16(n_res);
+    const uint64_t words = (b_off + b_wb + b_tile + b_st + b_res) / 16;
+    HIP_TRY(c->h_small.resize(words));
+    char *blob = reinterpret_cast<char *>(c->h_small.data());
+    uint64_t *h_off = reinterpret_cast<uint64_t *>(blob);
+    uint64_t *h_wb = reinterpret_cast<uint64_t *>(blob + b_off);
+    uint32_t *h_tile = reinterpret_cast<uint32_t *>(blob + b_off + b_wb);
+    uint32_t *h_st = reinterpret_cast<uint32_t *>(blob + b_off + b_wb + b_tile);
+    std::memcpy(h_off, off, (n_seq + 1) * sizeof(uint64_t));
+    std::memcpy(blob + b_off + b_wb + b_tile + b_st, c->h_res.data(), n_res);
+    /* plan_reduce / plan_scan on the host: window bases, the sequence owning
+     * each tile's first window, the longest sequence */
+    const uint64_t T = c->tile_windows;
+    uint64_t wb = 0;
+    uint32_t longest = 0;
+    for (uint32_t s = 0; s < n_seq; s++) {
+        const uint64_t w = windows_of(off[s + 1] - off[s]);
+        h_wb[s] = wb;
+        for (uint64_t t = (wb + T - 1) / T; t * T < wb + w; t++)
+            h_tile[t] = s;
+        wb += w;
+        longest = (uint32_t)std::max<uint64_t>(longest, std::min<uint64_t>(w, 0xFFFFFFFFull));
+    }
+    h_wb[n_seq] = wb;
+    for (uint64_t t = (wb + T - 1) / T; t < c->max_tiles; t++)
+        h_tile[t] = n_seq ? n_seq - 1 : 0; /* tiles past the last window (never probed) */
+    h_st[0] = 0;
+    h_st[1] = longest;
+    h_st[2] = h_st[3] = 0;
+    void *d_blob = nullptr;
+    HIP_TRY(c->h_small.device_ptr(0, &d_blob));
+    const uint4 *src = static_cast<const uint4 *>(d_blob);
+    SmallPieces pc;
+    const uint64_t sizes[SMALL_PIECES] = {b_off, b_wb, b_tile, b_st, b_res};
+    void *dsts[SMALL_PIECES] = {c->offsets.p, c->wbase.p, c->tile_seq.p, c->plan_status.p, c->residues.p};
+    uint64_t at = 0;
+    for (int p = 0; p < SMALL_PIECES; p++) {
+        pc.dst[p] = static_cast<uint4 *>(dsts[p]);
+        pc.src[p] = src + at;
+        at += sizes[p] / 16;
+        pc.end16[p] = at;
+    }
+    HIP_TRY(launch_small_upload(pc, c->stream));
+    if ((rc = kgx_stage_probe(c, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>())))
+        return rc;
+    if ((rc = kgx_stage_score(c, params, want)))
+        return rc;
+    /* results: worst-case mapped arrays, offsets and totals in mapped memory */
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0, want_otu = (want & KGX_WANT_OTU) != 0,
+               need_hits = (want & KGX_WANT_HITS) != 0, want_best = (want & KGX_WANT_BEST) != 0;
+    const uint64_t cap = std::max<uint64_t>(wb, 1);
+    HIP_TRY(c->dense_hoff.reserve((n_seq + 1) * sizeof(uint64_t)));
+    HIP_TRY(c->dense_coff.reserve((n_seq + 1) * sizeof(uint64_t)));
+    HIP_TRY(c->dense_ooff.reserve((n_seq + 1) * sizeof(uint64_t)));
+    HIP_TRY(c->h_dense_hoff.resize(n_seq + 1));
+    HIP_TRY(c->h_dense_coff.resize(n_seq + 1));
+    HIP_TRY(c->h_dense_ooff.resize(n_seq + 1));
+    HIP_TRY(c->h_plan_status.resize(1));
+    HIP_TRY(c->h_nwin.resize(1));
+    HIP_TRY(c->h_hits.resize(need_hits ? cap : 0));
+    HIP_TRY(c->h_calls.resize(want_calls ? cap : 0));
+    HIP_TRY(c->h_otus.resize(want_otu ? cap : 0));
+    HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+    void *m_hoff, *m_coff, *m_ooff, *m_st, *m_nwin, *mh = nullptr, *mc = nullptr, *mo = nullptr, *mb = nullptr;
+    HIP_TRY(c->h_dense_hoff.device_ptr(0, &m_hoff));
+    HIP_TRY(c->h_dense_coff.device_ptr(0, &m_coff));
+    HIP_TRY(c->h_dense_ooff.device_ptr(0, &m_ooff));
+    HIP_TRY(c->h_plan_status.device_ptr(0, &m_st));
+    HIP_TRY(c->h_nwin.device_ptr(0, &m_nwin));
+    if (need_hits)
+        HIP_TRY(c->h_hits.device_ptr(0, &mh));
+    if (want_calls)
+        HIP_TRY(c->h_calls.device_ptr(0, &mc));
+    if (want_otu)
+        HIP_TRY(c->h_otus.device_ptr(0, &mo));
+    if (want_best && n_seq)
+        HIP_TRY(c->h_best.device_ptr(0, &mb));
+    HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(), want_calls ? c->call_count.as<uint32_t>() : nullptr,
+                                 want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
+                                 c->dense_coff.as<uint64_t>(), c->dense_ooff.as<uint64_t>(),
+                                 static_cast<uint64_t *>(m_hoff), static_cast<uint64_t *>(m_coff),
+                                 static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
+                                 c->wbase.as<uint64_t>(), want_best ? c->best.as<kgx_best_call>() : nullptr,
+                                 static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
+                                 static_cast<uint64_t *>(m_nwin), c->stream));
+    HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                          c->call_count.as<uint32_t>(), c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots,
+                          c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
+                          static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
+                          c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
+                          static_cast<kgx_otu *>(mo), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_plan_status[0])
+        return fail(KGX_EINVAL, "small batch: plan status raised");
+    c->h_hoff.assign(c->h_dense_hoff.data(), c->h_dense_hoff.data() + n_seq + 1);
+    c->h_coff.assign(c->h_dense_coff.data(), c->h_dense_coff.data() + n_seq + 1);
+    c->h_ooff.assign(c->h_dense_ooff.data(), c->h_dense_ooff.data() + n_seq + 1);
+    const uint64_t nh = c->h_hoff[n_seq], nc = c->h_coff[n_seq], no = c->h_ooff[n_seq];
+    if ((need_hits && nh > cap) || (want_calls && nc > cap) || (want_otu && no > cap))
+        return fail(KGX_EDEVICE, "small batch: more records than windows");
+    HIP_TRY(c->h_hits.resize(need_hits ? nh : 0));
+    HIP_TRY(c->h_calls.resize(nc));
+    HIP_TRY(c->h_otus.resize(no));
+    fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
+    return KGX_OK;
+}
+
 }  // namespace
 
 int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues,
@@ -2121,6 +2274,8 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     const uint32_t K = (uint32_t)std::min<uint64_t>({(uint64_t)c->host_chunks, k_res, (uint64_t)n_seq});
     if (K >= 2 && (want & (KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU | KGX_WANT_BEST)))
         return process_batch_chunked(c, params, residues, seq_offsets, n_seq, want, K, out);
+    if (n_seq && n_res <= (uint64_t)c->small_batch && n_seq <= (1u << 16))
+        return process_batch_small(c, params, residues, seq_offsets, n_seq, want, out);
     PhaseTimer tm(c);
     int rc = stage_host_seqs(c, residues, seq_offsets, 0, n_seq);
     if (rc)

@@ -821,3 +821,44 @@ def test_device_otu_tallies_match_oracle(gpu, oracle_lib, otu_range, layout):
             n_otu = np.diff(want.otu_offsets)
             if otu_range >= 60:
                 assert n_otu.max() > 16  # the introsort path ran
+
+
+@pytest.mark.parametrize("params", PARAM_SETS[:4])
+def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu, params):
+    """Batches of <= small_batch residues (the facade's process_aa_seq) take
+    the one-wait path: host plan in the pinned blob, results stored into
+    mapped memory.  Same records as the oracle, and the same best calls as the
+    ordinary path (small_batch 0), for one sequence, a few with empties,
+    sub-window and NUL-cut sequences, a mid-buffer start and one long sequence
+    (wave scorer), on both resident layouts."""
+    spec, table, img, ctx = small_world
+    rng = np.random.default_rng(23)
+    res, off = synth.make_queries(spec, 60, x_permille=5, q0=777)
+    seqs = [res[int(off[i]):int(off[i + 1])].copy() for i in range(60)]
+    seqs[3][40] = 0  # NUL cut
+    long_seq = np.frombuffer(random_protein(rng, 20_000).encode(), np.uint8)
+    batches = [seqs[:1], seqs[1:2] + [np.zeros(0, np.uint8)], [np.zeros(0, np.uint8)] + seqs[2:20],
+               [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], [long_seq] + seqs[:3]]
+    p = gpu.Params(*params)
+    for layout_ctx in (ctx, aos_world[1]):
+        for b in batches:
+            lens = np.array([0] + [len(x) for x in b], np.uint64)
+            boff = np.cumsum(lens).astype(np.uint64) + np.uint64(3)
+            bres = np.concatenate([np.frombuffer(b"MKV", np.uint8)] + list(b))
+            want = oracle_lib.process_batch(table, bres, boff, params=params)
+            layout_ctx.set_option("small_batch", 65536)
+            got = layout_ctx.process_batch(bres, boff, p, want=7)
+            assert_same(got, want, len(b))
+            assert got.n_windows == int(np.maximum(lens[1:].astype(np.int64) - 8, 0).sum())
+            small_best = layout_ctx.process_batch(bres, boff, p, want=gpu.WANT_BEST | gpu.WANT_HITS)
+            assert eq_fields(small_best.hits, want.hits)
+            for w in (1, 2):
+                g = layout_ctx.process_batch(bres, boff, p, want=w)
+                assert np.array_equal(g.hit_offsets, want.hit_offsets)
+                assert np.array_equal(g.call_offsets, want.call_offsets if w == 2 else np.zeros_like(g.call_offsets))
+            layout_ctx.set_option("small_batch", 0)
+            try:
+                ref_best = layout_ctx.process_batch(bres, boff, p, want=gpu.WANT_BEST).best
+            finally:
+                layout_ctx.set_option("small_batch", 65536)
+            assert np.array_equal(small_best.best, ref_best)

@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--cpu-reads", type=int, default=20_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts alternating over chunks")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host threads, one per worker context (the server's worker pool: a worker's sizing wait "
+                         "does not hold the other workers' launches); 0 = one thread alternating over the contexts")
     ap.add_argument("--score-variant", type=int, default=-1, help="-1 = the library default")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="-1 = the library default")
     ap.add_argument("--fq-residues", type=int, default=0,
@@ -63,6 +66,8 @@ def main():
     ctx = abi.Context(img)
     # worker contexts (own stream + buffers), as for bench.py: one chunk's
     # host-side sizing sync overlaps the other context's kernels
+    if args.threads:
+        args.pipeline = args.threads
     ctxs = [ctx] + [abi.Context(img) for _ in range(args.pipeline - 1)]
     for c in ctxs:
         if args.score_variant >= 0:
@@ -84,26 +89,51 @@ def main():
     params = abi.default_params()
     stats = {"fragments": 0, "residues": 0, "hits": 0, "calls": 0}
 
+    def run_chunk(c, c0, collect_stats):
+        m = min(chunk, n - c0)
+        f = abi.Fragments()
+        abi.check(L.kgx_fq_fragments_device(c.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
+                  "fq_fragments")
+        dr = abi.DeviceResult()
+        abi.check(L.kgx_fq_run_device(c.handle, ctypes.byref(params), ctypes.byref(f),
+                                      abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
+        if collect_stats:
+            hc = np.zeros(f.n_fragments, np.uint32)
+            cc = np.zeros(f.n_fragments, np.uint32)
+            c.synchronize()
+            abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, dr.hit_count, hc.nbytes), "d2h")
+            abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, dr.call_count, cc.nbytes), "d2h")
+            stats["fragments"] += f.n_fragments
+            stats["residues"] += f.n_residues
+            stats["hits"] += int(hc.sum())
+            stats["calls"] += int(cc.sum())
+
     def device_pass(collect_stats=False):
-        for i, c0 in enumerate(range(0, n, chunk)):
-            c = ctxs[i % len(ctxs)]
-            m = min(chunk, n - c0)
-            f = abi.Fragments()
-            abi.check(L.kgx_fq_fragments_device(c.handle, d_bases.value + c0 * Lr, d_off, m, ctypes.byref(f)),
-                      "fq_fragments")
-            dr = abi.DeviceResult()
-            abi.check(L.kgx_fq_run_device(c.handle, ctypes.byref(params), ctypes.byref(f),
-                                          abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
-            if collect_stats:
-                hc = np.zeros(f.n_fragments, np.uint32)
-                cc = np.zeros(f.n_fragments, np.uint32)
-                c.synchronize()
-                abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, dr.hit_count, hc.nbytes), "d2h")
-                abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, dr.call_count, cc.nbytes), "d2h")
-                stats["fragments"] += f.n_fragments
-                stats["residues"] += f.n_residues
-                stats["hits"] += int(hc.sum())
-                stats["calls"] += int(cc.sum())
+        starts = list(range(0, n, chunk))
+        if args.threads and not collect_stats:
+            # worker w takes chunks w, w + P, ... on its own context (ctypes
+            # calls release the GIL, so the workers' waits overlap)
+            import threading
+            P = len(ctxs)
+            errs = []
+
+            def worker(w):
+                try:
+                    for c0 in starts[w::P]:
+                        run_chunk(ctxs[w], c0, False)
+                    ctxs[w].synchronize()
+                except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+                    errs.append(e)
+            ts = [threading.Thread(target=worker, args=(w,)) for w in range(P)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            if errs:
+                raise errs[0]
+            return
+        for i, c0 in enumerate(starts):
+            run_chunk(ctxs[i % len(ctxs)], c0, collect_stats)
         for c in ctxs:
             c.synchronize()
 
@@ -132,7 +162,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),

@@ -63,24 +63,38 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < m; i++)
         seqs[i] = res.substr(off[i], off[i + 1] - off[i]);
 
-    /* unbatched: one process_aa_seq per sequence, as the reference's loop */
-    uint64_t hits = 0, calls = 0, residues = 0;
-    std::vector<double> lat;
-    lat.reserve(m);
-    for (int warm = 0; warm < 20; warm++) {
-        auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
-        kg.process_aa_seq("w", seqs[warm % m], cv, [](kgx::KmerGuts::hit_in_sequence_t) {}, nullptr);
+    /* unbatched: one process_aa_seq per sequence, as the reference's loop;
+     * first on the ordinary batch path (small_batch 0: device plan, counts
+     * round trip, gather round trip), then on the default one-wait path */
+    uint64_t hits = 0, calls = 0, residues = 0, hits0 = 0, calls0 = 0;
+    std::vector<double> lat, lat0;
+    double t_seq = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        if (kgx_ctx_set_option(kg.ctx(), "small_batch", pass == 0 ? 0 : 65536) != KGX_OK) {
+            std::fprintf(stderr, "facade_bench: %s\n", kgx_last_error());
+            return 1;
+        }
+        for (int warm = 0; warm < 20; warm++) {
+            auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+            kg.process_aa_seq("w", seqs[warm % m], cv, [](kgx::KmerGuts::hit_in_sequence_t) {}, nullptr);
+        }
+        hits0 = hits;
+        calls0 = calls;
+        hits = calls = residues = 0;
+        lat0.swap(lat);
+        lat.clear();
+        lat.reserve(m);
+        const auto t_all = clk::now();
+        for (size_t i = 0; i < m; i++) {
+            auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+            const auto t0 = clk::now();
+            kg.process_aa_seq("q", seqs[i], cv, [&](kgx::KmerGuts::hit_in_sequence_t) { hits++; }, nullptr);
+            lat.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+            calls += cv->size();
+            residues += seqs[i].size();
+        }
+        t_seq = std::chrono::duration<double>(clk::now() - t_all).count();
     }
-    const auto t_all = clk::now();
-    for (size_t i = 0; i < m; i++) {
-        auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
-        const auto t0 = clk::now();
-        kg.process_aa_seq("q", seqs[i], cv, [&](kgx::KmerGuts::hit_in_sequence_t) { hits++; }, nullptr);
-        lat.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
-        calls += cv->size();
-        residues += seqs[i].size();
-    }
-    const double t_seq = std::chrono::duration<double>(clk::now() - t_all).count();
 
     /* the same sequences, one process_aa_batch */
     uint64_t bhits = 0, bcalls = 0;
@@ -103,11 +117,13 @@ int main(int argc, char **argv)
     const double t_batch = pct(tb, 50);
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
+                "\"latency_us_ordinary_path\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f}, "
                 "\"unbatched_residues_per_s\": %.4g, \"batched\": {\"sequences\": %zu, \"ms\": %.3f, "
                 "\"residues_per_s\": %.4g}, \"hits\": %llu, \"calls_out\": %llu, \"batch_hits_per_rep\": %llu, "
                 "\"batch_calls\": %llu, \"keys_stored\": %llu}\n",
-                m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, (double)residues / t_seq, m,
+                m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, pct(lat0, 50), pct(lat0, 90),
+                pct(lat0, 99), (double)residues / t_seq, m,
                 t_batch * 1e3, (double)residues / t_batch, (unsigned long long)hits, (unsigned long long)calls,
                 (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored);
-    return hits * 6 == bhits && calls == bcalls ? 0 : 3;
+    return hits * 6 == bhits && calls == bcalls && hits == hits0 && calls == calls0 ? 0 : 3;
 }
