@@ -320,7 +320,11 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * schedule (host_stream 0: counts to the host, then gather and copy, with
  * "counts_first" 1 holding chunk k's bulk copy until chunk k+1's counts are
  * out).  "stage_threads" (default 4): threads copying the caller's residues
- * into pinned staging.  Results are identical under every setting.  After a
+ * into pinned staging.  "small_batch" (0..2^24 residues, default 65536; 0 =
+ * off): a one-chunk batch of at most this many residues is planned on the
+ * host, read by the device from mapped pinned staging and its results stored
+ * into mapped memory -- one host wait, no DMA copy (process_aa_seq's
+ * latency).  Results are identical under every setting.  After a
  * chunked batch the device results are split over the two contexts:
  * kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch (host_chunks
  * 1, or want 0, which never chunks) */
