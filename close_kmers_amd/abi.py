@@ -180,6 +180,8 @@ SIGNATURES = {
     "kgx_device_batch_collect": (_INT, [_P, _U32, ctypes.POINTER(Result)]),
     "kgx_fq_fragments": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
     "kgx_fq_fragments_device": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
+    "kgx_fq_fragments_device_start": (_INT, [_P, _P, _P, _U32, _U64]),
+    "kgx_fq_fragments_finish": (_INT, [_P, ctypes.POINTER(Fragments)]),
     "kgx_fq_run_device": (_INT, [_P, ctypes.POINTER(Params), ctypes.POINTER(Fragments), _U32, _P]),
     "kgx_fq_create": (_INT, [_P, _CS, _CS, _CS, _CS, _PP]),
     "kgx_fq_destroy": (_INT, [_P]),

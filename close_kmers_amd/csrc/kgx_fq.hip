@@ -662,12 +662,13 @@ __global__ __launch_bounds__(256) void fq_desc_lane_kernel(const uint8_t *bases,
                                                            uint32_t n_reads, const uint2 *read_counts,
                                                            const ulonglong2 *tile_base, uint32_t n_tiles,
                                                            const uint32_t *frame_nf, const uint32_t *frame_nr,
-                                                           uint32_t *frag_base, uint64_t *out_off, uint64_t *out_anchor)
+                                                           uint32_t *frag_base, uint64_t *out_off, uint64_t *out_anchor,
+                                                           const uint64_t *totals, uint64_t max_frag)
 {
     __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x * WAVES_PER_WG + wv;
-    if (tile >= n_tiles)
+    if (tile >= n_tiles || totals[0] > max_frag) /* more fragments than the buffers hold: fq_tail flagged it */
         return;
     uint32_t *ns = nspan[wv];
     const uint64_t r0 = (uint64_t)tile * FQ_TILE;
@@ -721,11 +722,18 @@ struct PairSum {
 /* 2b. after the exclusive scan of the workgroup sums (hipcub): the batch
  * totals and the CSR tails */
 __global__ void fq_tail_kernel(const ulonglong2 *tile_base, uint64_t n_tiles, uint32_t n_reads, uint64_t *totals,
-                               uint64_t *out_off, uint32_t *frag_base, uint32_t *n_frag)
+                               uint64_t *out_off, uint32_t *frag_base, uint32_t *n_frag, uint64_t max_frag,
+                               uint64_t max_res)
 {
     const ulonglong2 tot = tile_base[n_tiles];
-    totals[0] = tot.x;
+    /* a caller's span bound that is too small (kgx_fq_fragments_device_start)
+     * shows as totals past the buffers: the emit passes then write nothing and
+     * the finish reports it */
+    const bool over = tot.x > max_frag || tot.y > max_res;
+    totals[0] = over ? max_frag + 1 : tot.x;
     totals[1] = tot.y;
+    if (over)
+        return;
     out_off[tot.x] = tot.y;
     frag_base[(uint64_t)n_reads * 6] = (uint32_t)tot.x;
     n_frag[(uint64_t)n_reads * 6] = 0;
@@ -738,8 +746,10 @@ __global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, cons
                                                       const ulonglong2 *tile_base,
                                                       uint32_t *n_frag, uint32_t *frag_base, uint8_t *out_res,
                                                       uint64_t *out_off, uint32_t *out_read, int8_t *out_frame,
-                                                      uint32_t *out_start)
+                                                      uint32_t *out_start, const uint64_t *totals, uint64_t max_frag)
 {
+    if (totals[0] > max_frag) /* fq_tail flagged an overflow: write nothing */
+        return;
     __shared__ FqLds t;
     fq_lds_init(t);
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
@@ -840,8 +850,10 @@ namespace kgx {
  * the output: six frames give at most 2 residues per base, a fragment has at
  * least 11 residues.  Launches: count -> scan of the workgroup sums (hipcub)
  * -> emit, with no host round trip between them; one readback of the totals. */
-int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
-                 uint64_t n_bases, uint64_t bound, kgx_fragments *out)
+/* the fragment pass up to the totals' D2H, without waiting (fq_fragments_finish
+ * waits); n_bases bounds the output buffers, bound the bytes readable from d_bases */
+int fq_fragments_enqueue(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
+                         uint64_t n_bases, uint64_t bound)
 {
     /* fragments as anchors into the bases (no residues) when asked and the probe can take them */
     const bool desc = !c->fq_residues && probe_takes_dna(c);
@@ -893,23 +905,39 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     HIP_TRY(hipcub::DeviceScan::ExclusiveScan(scan_tmp, scan_bytes, tile_sum, tile_base, PairSum(),
                                               make_ulonglong2(0, 0), (int)(n_tiles + 1), st));
     hipLaunchKernelGGL(fq_tail_kernel, dim3(1), dim3(1), 0, st, tile_base, n_tiles, n_reads, totals,
-                       c->fq_off.as<uint64_t>(), c->fq_fbase.as<uint32_t>(), c->fq_nfrag.as<uint32_t>());
+                       c->fq_off.as<uint64_t>(), c->fq_fbase.as<uint32_t>(), c->fq_nfrag.as<uint32_t>(), max_frag,
+                       max_res);
     if (n_reads && desc)
         hipLaunchKernelGGL(fq_desc_lane_kernel, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
                            dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_base, (uint32_t)n_tiles,
                            c->fq_nfrag.as<uint32_t>(), c->fq_nres.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
-                           c->fq_off.as<uint64_t>(), c->fq_anchor.as<uint64_t>());
+                           c->fq_off.as<uint64_t>(), c->fq_anchor.as<uint64_t>(), totals, max_frag);
     else if (n_reads)
         hipLaunchKernelGGL(fq_emit_kernel, dim3((uint32_t)n_tiles), dim3(256), 0, st, d_bases, d_read_off, n_reads,
                            read_counts, tile_base, c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(),
                            c->fq_res.as<uint8_t>(), c->fq_off.as<uint64_t>(), c->fq_read.as<uint32_t>(),
-                           c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>());
+                           c->fq_frame.as<int8_t>(), c->fq_start.as<uint32_t>(), totals, max_frag);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data(), totals, 16, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    c->fq_pend = {true, desc, n_reads, max_frag, max_res, d_bases, bound};
+    return KGX_OK;
+}
+
+/* wait for the enqueued fragment pass and describe its output */
+int fq_fragments_finish(kgx_ctx *c, kgx_fragments *out)
+{
+    if (!c->fq_pend.active)
+        return fail(KGX_EINVAL, "no fragment pass started on this context");
+    const FqPending p = c->fq_pend;
+    c->fq_pend.active = false;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const bool desc = p.desc;
     const uint64_t nf = c->h_fq_tot[0], nr = c->h_fq_tot[1];
-    if (nf > max_frag || nr > max_res)
-        return fail(KGX_EDEVICE, "fq fragments overflowed their bound");
+    if (nf > p.max_frag || nr > p.max_res)
+        return fail(KGX_EINVAL, "fq fragments overflowed their bound (the reads span more than n_bases)");
+    const uint32_t n_reads = p.n_reads;
+    const uint8_t *d_bases = p.bases;
+    const uint64_t bound = p.bound;
     out->n_reads = n_reads;
     out->n_fragments = (uint32_t)nf;
     out->n_residues = nr;
@@ -922,6 +950,13 @@ int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off,
     out->frame = desc ? nullptr : c->fq_frame.as<int8_t>();
     out->frame_counts = c->fq_nfrag.as<uint32_t>();
     return KGX_OK;
+}
+
+int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
+                 uint64_t n_bases, uint64_t bound, kgx_fragments *out)
+{
+    const int rc = fq_fragments_enqueue(c, d_bases, d_read_off, n_reads, n_bases, bound);
+    return rc ? rc : fq_fragments_finish(c, out);
 }
 
 /* ---- reads with calls (kgx_fq_called_reads) ---- */
@@ -1094,6 +1129,23 @@ int kgx_fq_fragments_device(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *
             return fail(KGX_EINVAL, "read offsets not monotone");
     }
     return fq_fragments(c, d_bases, d_read_offsets, n_reads, ends[1] - ends[0], ends[1], out);
+}
+
+int kgx_fq_fragments_device_start(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_offsets,
+                                  uint32_t n_reads, uint64_t n_bases)
+{
+    if (!c || (n_reads && (!d_bases || !d_read_offsets)))
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->img->device));
+    return fq_fragments_enqueue(c, d_bases, d_read_offsets, n_reads, n_bases, n_bases);
+}
+
+int kgx_fq_fragments_finish(kgx_ctx *c, kgx_fragments *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(c->img->device));
+    return fq_fragments_finish(c, out);
 }
 
 int kgx_fq_called_reads(kgx_ctx *c, const kgx_fragments *fragments, kgx_fq_called *out)

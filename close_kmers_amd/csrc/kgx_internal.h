@@ -173,7 +173,7 @@ hipError_t launch_unpack(const packed_bucket *packed, kgx_sig_kmer *out, uint64_
  * every sequence up to RUN_CAP windows; SCORE_LANE (2): the lane machine
  * only.  The wave scorer needs order_constraint 0 (else: the lane machine).
  * plan_status[1] = the batch's longest sequence in windows (launch_plan). */
-enum { SCORE_HYBRID = 0, SCORE_WAVE = 1, SCORE_LANE = 2 };
+enum { SCORE_HYBRID = 0, SCORE_WAVE = 1, SCORE_LANE = 2, SCORE_WAVE_ONLY = 3 /* internal: no sequence > RUN_CAP */ };
 constexpr uint32_t LONG_SEQ = 2048;
 hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wbase, const uint32_t *tile_seq,
                         uint64_t max_tiles, const uint64_t *hit_mask, uint32_t tile_windows, uint4 *hot,

@@ -1646,7 +1646,14 @@ hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wba
 #define KGX_WAVE(P, ABOVE)                                                                                      \
     hipLaunchKernelGGL(score_wave_kernel<P>, wgrid, dim3(256), 0, stream, n_seq, wbase, tile_seq, hit_mask,     \
                        tile_windows, wave_tiles, hot, calls, hit_count, call_count, params, want, (ABOVE), plan_status)
-    if (variant == SCORE_WAVE && wave_ok) { /* every sequence up to RUN_CAP windows */
+    if (variant == SCORE_WAVE_ONLY && wave_ok) { /* the caller knows no sequence exceeds RUN_CAP windows */
+        if (pk)
+            KGX_WAVE(true, 0u);
+        else
+            KGX_WAVE(false, 0u);
+        return hipGetLastError();
+    }
+    if ((variant == SCORE_WAVE || variant == SCORE_WAVE_ONLY) && wave_ok) { /* every sequence up to RUN_CAP windows */
         if (pk) {
             KGX_WAVE(true, 0u);
             hipLaunchKernelGGL(score_long_kernel<true>, lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask,

@@ -225,6 +225,18 @@ class HostPool {
     bool stop_ = false;
 };
 
+/* a fragment pass enqueued by fq_fragments_enqueue, finished by fq_fragments_finish */
+struct FqPending {
+    bool active = false;
+    bool desc = false;
+    uint32_t n_reads = 0;
+    uint64_t max_frag = 0, max_res = 0;
+    const uint8_t *bases = nullptr;
+    uint64_t bound = 0;
+};
+int fq_fragments_enqueue(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
+                         uint64_t n_bases, uint64_t bound);
+int fq_fragments_finish(kgx_ctx *c, kgx_fragments *out);
 /* n_bases: the bytes the reads span (bounds the output); bound: bytes
  * readable from d_bases (the DNA probe's limit) */
 int fq_fragments(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_read_off, uint32_t n_reads,
@@ -291,6 +303,7 @@ struct kgx_ctx {
     kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start,
         fq_anchor, fq_nres;
     kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
+    kgx::FqPending fq_pend;             /* an enqueued fragment pass awaiting its finish */
     /* kgx_fq_called_reads */
     kgx::DevBuf fqc_flag, fqc_reads, fqc_nsel, fqc_nfrag, fqc_ncall, fqc_fo, fqc_co, fqc_fc, fqc_len, fqc_coff,
         fqc_calls;
@@ -363,6 +376,7 @@ struct kgx_ctx {
      * off): planned on the host, read by the device from the mapped staging
      * blob, results stored into mapped memory: one host wait per batch */
     int64_t small_batch = 1 << 16;
+    int small_wave = 1; /* small batches: the wave scorer instead of the hybrid (option "small_wave") */
     kgx::PinnedVec<uint4> h_small; /* offsets | window bases | tile owners | status | residues */
     int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
     kgx::PinnedVec<kgx_call> h_calls_region;

@@ -969,6 +969,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->small_batch = value;
         return KGX_OK;
     }
+    if (n == "small_wave") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "small_wave must be 0 or 1");
+        c->small_wave = (int)value;
+        return KGX_OK;
+    }
     if (n == "host_chunks") {
         if (value < 1 || value > 64)
             return fail(KGX_EINVAL, "host_chunks must be 1..64");
@@ -2192,7 +2198,16 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     HIP_TRY(launch_small_upload(pc, c->stream));
     if ((rc = kgx_stage_probe(c, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>())))
         return rc;
-    if ((rc = kgx_stage_score(c, params, want)))
+    /* the scorer: with few sequences the lane machine's one-lane chain per
+     * sequence is the whole stage's latency (31 us for one 300-aa protein);
+     * the wave scorer spreads each sequence's hits over a wave (option
+     * small_wave; the lane machine still takes order_constraint 1) */
+    const int variant = c->score_variant;
+    if (c->small_wave && variant == SCORE_HYBRID) /* the host plan knows the longest sequence */
+        c->score_variant = longest <= (uint32_t)RUN_CAP ? SCORE_WAVE_ONLY : SCORE_WAVE;
+    rc = kgx_stage_score(c, params, want);
+    c->score_variant = variant;
+    if (rc)
         return rc;
     /* results: worst-case mapped arrays, offsets and totals in mapped memory */
     const bool want_calls = (want & KGX_WANT_CALLS) != 0, want_otu = (want & KGX_WANT_OTU) != 0,

@@ -324,7 +324,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * off): a one-chunk batch of at most this many residues is planned on the
  * host, read by the device from mapped pinned staging and its results stored
  * into mapped memory -- one host wait, no DMA copy (process_aa_seq's
- * latency).  Results are identical under every setting.  After a
+ * latency), scored by the wave scorer unless "small_wave" is 0.  Results are
+ * identical under every setting.  After a
  * chunked batch the device results are split over the two contexts:
  * kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch (host_chunks
  * 1, or want 0, which never chunks) */
@@ -466,6 +467,18 @@ int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offse
 /* reads already in device memory */
 int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint32_t n_reads, kgx_fragments *out);
+/* kgx_fq_fragments_device in two halves, for chunked streams of reads: _start
+ * enqueues the fragment pass on ctx's stream and returns at once; _finish
+ * waits for it and fills out (the same fragments).  Between the two the host
+ * can enqueue other contexts' work -- the previous chunk's lookup -- so that
+ * sizing one chunk never holds the GPU between two probes.  n_bases: the
+ * caller's bound on the bytes the reads span and may read (d_read_offsets[0]
+ * >= 0, d_read_offsets[n_reads] <= n_bases); a span past it is an error from
+ * _finish, with nothing written past the buffers.  Nothing else may run on
+ * ctx between the two calls. */
+int kgx_fq_fragments_device_start(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
+                                  uint32_t n_reads, uint64_t n_bases);
+int kgx_fq_fragments_finish(kgx_ctx *ctx, kgx_fragments *out);
 /* lookup + run scoring of a fragment batch: kgx_run_device over
  * (residues, offsets) when the residues were written, else plan, the probe
  * over the anchors (windows translated from the bases), score.  Same results. */

@@ -1,5 +1,7 @@
 """fq path on the GPU: 6-frame code-11 fragments vs the oracle's
 get_possible_proteins + split (dna_seq.cc:9-47), and their lookup."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -303,3 +305,74 @@ def test_fq_handler_parallel_parse_matches_oracle(gpu, oracle_lib, tmp_path):
         cuts = [0] + sorted(int(x) for x in rng.integers(1, len(fastq), 12)) + [len(fastq)]
         out = b"".join(fq.process(fastq[a:b], b == len(fastq)) for a, b in zip(cuts, cuts[1:]))
     assert out == want
+
+
+def test_fragments_start_finish_ahead_schedule(gpu):
+    """kgx_fq_fragments_device_start / _finish: the same fragments as
+    kgx_fq_fragments_device (anchors and residues); chunks sized one ahead on
+    two contexts (bench_fq's schedule) give the same hits and calls as chunk
+    by chunk; a span bound smaller than the reads' span is an error with
+    nothing written past the buffers, and the context stays usable."""
+    from close_kmers_amd import abi
+    L = abi.lib()
+    spec, table = synthetic_table(20000)
+    rng = np.random.default_rng(8)
+    Lr, n, chunk = 150, 6000, 1500
+    bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)].copy()
+    off = np.arange(0, chunk * Lr + 1, Lr, dtype=np.uint64)
+    prm = gpu.Params(5, 200, 0, 0)
+    d_b, d_o = ctypes.c_void_p(), ctypes.c_void_p()
+    abi.check(L.kgx_device_alloc(0, bases.nbytes, ctypes.byref(d_b)), "alloc")
+    abi.check(L.kgx_device_alloc(0, off.nbytes, ctypes.byref(d_o)), "alloc")
+    try:
+        abi.check(L.kgx_memcpy_h2d(d_b, bases.ctypes.data, bases.nbytes), "h2d")
+        abi.check(L.kgx_memcpy_h2d(d_o, off.ctypes.data, off.nbytes), "h2d")
+        with gpu.Image.from_table(table) as img, gpu.Context(img) as c0, gpu.Context(img) as c1:
+            for fq_res in (1, 0):
+                for c in (c0, c1):
+                    c.set_option("fq_residues", fq_res)
+                # chunk by chunk (kgx_fq_fragments_device)
+                want_frag, want_res = [], []
+                for k in range(n // chunk):
+                    f = abi.Fragments()
+                    abi.check(L.kgx_fq_fragments_device(c0.handle, d_b.value + k * chunk * Lr, d_o, chunk,
+                                                        ctypes.byref(f)), "frag")
+                    want_frag.append(c0.fragments_to_host(f))
+                    want_res.append(c0.run_fragments(f, prm))
+                # sized one ahead over two contexts
+                ctxs = [c0, c1]
+
+                def start(k):
+                    abi.check(L.kgx_fq_fragments_device_start(ctxs[k % 2].handle, d_b.value + k * chunk * Lr, d_o,
+                                                              chunk, chunk * Lr), "start")
+
+                def finish(k):
+                    f = abi.Fragments()
+                    abi.check(L.kgx_fq_fragments_finish(ctxs[k % 2].handle, ctypes.byref(f)), "finish")
+                    return f
+                start(0)
+                f = finish(0)
+                for k in range(n // chunk):
+                    if k + 1 < n // chunk:
+                        start(k + 1)
+                    h = ctxs[k % 2].fragments_to_host(f)
+                    for key, a in want_frag[k].items():
+                        assert (a is None and h[key] is None) or np.array_equal(a, h[key]), (fq_res, k, key)
+                    got = ctxs[k % 2].run_fragments(f, prm)
+                    w = want_res[k]
+                    assert np.array_equal(got.hit_offsets, w.hit_offsets)
+                    assert np.array_equal(got.hits["which_kmer"], w.hits["which_kmer"])
+                    assert np.array_equal(got.call_offsets, w.call_offsets)
+                    if k + 1 < n // chunk:
+                        f = finish(k + 1)
+                assert sum(len(r.hits) for r in want_res) > 0
+            # a span bound past which the reads run: an error, then the context still works
+            abi.check(L.kgx_fq_fragments_device_start(c0.handle, d_b, d_o, chunk, 600), "start")
+            f = abi.Fragments()
+            assert L.kgx_fq_fragments_finish(c0.handle, ctypes.byref(f)) == -1
+            assert L.kgx_fq_fragments_finish(c0.handle, ctypes.byref(f)) == -1  # nothing pending
+            abi.check(L.kgx_fq_fragments_device(c0.handle, d_b, d_o, chunk, ctypes.byref(f)), "frag")
+            assert f.n_fragments == len(want_frag[0]["offsets"]) - 1
+    finally:
+        L.kgx_device_free(d_b)
+        L.kgx_device_free(d_o)

@@ -830,7 +830,8 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
     mapped memory.  Same records as the oracle, and the same best calls as the
     ordinary path (small_batch 0), for one sequence, a few with empties,
     sub-window and NUL-cut sequences, a mid-buffer start and one long sequence
-    (wave scorer), on both resident layouts."""
+    (wave scorer), on both resident layouts, with the small path's wave
+    scorer and with the hybrid."""
     spec, table, img, ctx = small_world
     rng = np.random.default_rng(23)
     res, off = synth.make_queries(spec, 60, x_permille=5, q0=777)
@@ -840,7 +841,8 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
     batches = [seqs[:1], seqs[1:2] + [np.zeros(0, np.uint8)], [np.zeros(0, np.uint8)] + seqs[2:20],
                [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], [long_seq] + seqs[:3]]
     p = gpu.Params(*params)
-    for layout_ctx in (ctx, aos_world[1]):
+    for layout_ctx, sw in ((ctx, 1), (ctx, 0), (aos_world[1], 1)):
+        layout_ctx.set_option("small_wave", sw)  # wave scorer (default) / the hybrid
         for b in batches:
             lens = np.array([0] + [len(x) for x in b], np.uint64)
             boff = np.cumsum(lens).astype(np.uint64) + np.uint64(3)
@@ -862,3 +864,4 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
             finally:
                 layout_ctx.set_option("small_batch", 65536)
             assert np.array_equal(small_best.best, ref_best)
+        layout_ctx.set_option("small_wave", 1)

@@ -49,6 +49,10 @@ def main():
     ap.add_argument("--cpu-reads", type=int, default=20_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts alternating over chunks")
+    ap.add_argument("--ahead", type=int, default=0,
+                    help="1 = size chunk k+1 (kgx_fq_fragments_device_start / _finish) while chunk k's lookup is "
+                         "queued, so the probes run back to back; 0 = kgx_fq_fragments_device then the lookup, "
+                         "chunk by chunk")
     ap.add_argument("--threads", type=int, default=0,
                     help="host threads, one per worker context (the server's worker pool: a worker's sizing wait "
                          "does not hold the other workers' launches); 0 = one thread alternating over the contexts")
@@ -132,6 +136,35 @@ def main():
             if errs:
                 raise errs[0]
             return
+        if args.ahead and len(ctxs) >= 2 and not collect_stats:  # chunk k+1 sized on the other context
+            # start chunk k+1's fragment pass, queue chunk k's lookup, then
+            # wait for k+1's sizes: the wait ends early in chunk k's probe
+            # (k+1's pass runs behind chunk k-1's score on its context), and
+            # chunk k+1's lookup is queued before chunk k's probe ends
+            P = len(ctxs)
+
+            def start(i):
+                m = min(chunk, n - starts[i])
+                abi.check(L.kgx_fq_fragments_device_start(ctxs[i % P].handle, d_bases.value + starts[i] * Lr,
+                                                          d_off, m, m * Lr), "fq_start")
+
+            def finish(i):
+                f = abi.Fragments()
+                abi.check(L.kgx_fq_fragments_finish(ctxs[i % P].handle, ctypes.byref(f)), "fq_finish")
+                return f
+            start(0)
+            f = finish(0)
+            for i in range(len(starts)):
+                if i + 1 < len(starts):
+                    start(i + 1)
+                dr = abi.DeviceResult()
+                abi.check(L.kgx_fq_run_device(ctxs[i % P].handle, ctypes.byref(params), ctypes.byref(f),
+                                              abi.WANT_HITS | abi.WANT_CALLS, ctypes.byref(dr)), "run")
+                if i + 1 < len(starts):
+                    f = finish(i + 1)
+            for c in ctxs:
+                c.synchronize()
+            return
         for i, c0 in enumerate(starts):
             run_chunk(ctxs[i % len(ctxs)], c0, collect_stats)
         for c in ctxs:
@@ -162,7 +195,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "size_ahead": int(bool(args.ahead) and len(ctxs) >= 2), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),
