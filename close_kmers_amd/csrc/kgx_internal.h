@@ -152,13 +152,16 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2_words,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, hipStream_t stream);
-/* the line probe over fq fragments left as DNA (PACKED16 images, probe_j
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream);
+/* max_blocks > 0 caps the line probe's grid (its waves then stride over the
+ * tiles; option probe_persist); 0 = one workgroup per 4 tiles.
+ * The line probe over fq fragments left as DNA (PACKED16 images, probe_j
  * 1-4): anchor[s] = (first base of fragment s) << 1 | reverse strand; keys as
  * launch_probe over the translated residues (HIT_PACKED16 records) */
 hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
                             const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
-                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, hipStream_t stream);
+                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, uint32_t max_blocks,
+                            hipStream_t stream);
 /* set the filter bits of every stored key of the resident table */
 hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
                                uint32_t log2_words, hipStream_t stream);
@@ -210,6 +213,17 @@ struct SmallPieces {
     uint64_t end16[SMALL_PIECES];
 };
 hipError_t launch_small_upload(const SmallPieces &pc, hipStream_t stream);
+/* small_collect + gather in one workgroup, for batches of up to
+ * SMALL_GATHER_SEQ sequences (offsets into mapped h0..h2, records into the
+ * mapped outputs; a NULL output is not gathered) */
+constexpr uint32_t SMALL_GATHER_SEQ = 256;
+hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
+                               const uint32_t *hit_count, const uint32_t *call_count, const uint4 *hot,
+                               const uint4 *cold, const kgx_call *calls, const uint32_t *otu_count,
+                               const kgx_otu *otus, kgx_hit *hits_out, kgx_call *calls_out, kgx_otu *otus_out,
+                               uint64_t *h0, uint64_t *h1, uint64_t *h2, const uint32_t *status,
+                               const kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
+                               uint64_t *nwin_host, uint32_t hit_format, hipStream_t stream);
 /* one workgroup: launch_count_scan's offsets into o* (HBM) and h* (mapped
  * host), plus status[0], wbase[n] and (best_host non-NULL) best[0, n) */
 hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,

@@ -637,10 +637,12 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = lane_id();
     const uint64_t W = wbase[n_seq];
-    const uint64_t tile = (uint64_t)blockIdx.x * PROBE_WAVES + wave;
+    /* one tile per wave, or (a grid smaller than the tiles, option
+     * probe_persist) the wave strides over tiles: every wave leaves once its
+     * next tile lies past the batch's last window */
+    for (uint64_t tile = (uint64_t)blockIdx.x * PROBE_WAVES + wave; tile * T < W;
+         tile += (uint64_t)gridDim.x * PROBE_WAVES) {
     const uint64_t g0 = tile * T;
-    if (g0 >= W)
-        return;
 
     uint64_t key[J];
     uint32_t pos[J], sq[J];
@@ -725,6 +727,7 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
         pv[j] = hit[j] ? lds_rec[wave][64 * j + lane] : make_uint4(0, 0, 0, 0);
     }
     store_tile_hits<J, true>(hit, key, pv, pos, sq, g0, W, lane, hot, cold, hit_mask);
+    } /* tiles */
 }
 
 template <int J, int G, bool DNA = false>
@@ -781,7 +784,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, hipStream_t stream)
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream)
 {
     if (max_tiles == 0)
         return hipSuccess;
@@ -790,11 +793,13 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
      * that other contexts' kernels find room beside it */
     const uint32_t dyn_lds = lds_kb * 1024u > 9216u ? lds_kb * 1024u - 9216u : 0u;
     const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+    /* the line probe strides over tiles when its grid is capped */
+    const dim3 lgrid(max_blocks ? std::min<uint32_t>(grid.x, max_blocks) : grid.x);
     if (variant == PROBE_AUTO && layout == KGX_LAYOUT_PACKED16 && !filter)
         variant = PROBE_LINE;
     if ((variant == PROBE_LINE || variant == PROBE_LINE8) && layout == KGX_LAYOUT_PACKED16 && !filter) {
 #define KGX_LINE(JJ, GG)                                                                             \
-    launch_probe_line<JJ, GG>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
+    launch_probe_line<JJ, GG>(lgrid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
                               num_sigs, hot, cold, hit_mask, dyn_lds);                               \
     return hipGetLastError()
         const int key = probe_j * 10 + (variant == PROBE_LINE8 ? 8 : 4);
@@ -830,11 +835,13 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
 
 hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
                             const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
-                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, hipStream_t stream)
+                            uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, uint32_t max_blocks,
+                            hipStream_t stream)
 {
     if (max_tiles == 0)
         return hipSuccess;
-    const dim3 grid((uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES));
+    const uint32_t tiles_grid = (uint32_t)((max_tiles + PROBE_WAVES - 1) / PROBE_WAVES);
+    const dim3 grid(max_blocks ? std::min<uint32_t>(tiles_grid, max_blocks) : tiles_grid);
 #define KGX_DNA(JJ)                                                                                  \
     launch_probe_line<JJ, 4, true>(grid, stream, bases, n_bases, anchor, wbase, tile_seq, n_seq, table,  \
                                    num_sigs, hot, nullptr, hit_mask, 0);                            \
@@ -1776,19 +1783,26 @@ hipError_t launch_otus(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hi
 /* gather: tiled hits / sparse calls -> dense CSR, one wave per sequence     */
 /* ------------------------------------------------------------------------ */
 
+constexpr uint32_t CS_PER = 4, CS_TILE = 256 * CS_PER;
+
+struct Counts3 {
+    const uint32_t *c[3]; /* NULL: an all-zero array */
+};
+struct Offsets3 {
+    uint64_t *o[3];
+};
+
+/* sequence s's records, by one wave, to its dense CSR slots (hits from hoff_s,
+ * calls from coff_s, OTUs from ooff_s; each read only for the outputs asked) */
 template <bool PK>
-__global__ __launch_bounds__(256) void gather_kernel(
-    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+__device__ __forceinline__ void gather_one(
+    uint32_t s, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
     uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
-    const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
-    const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
-    uint32_t seq_base, const uint32_t *__restrict__ otu_count, const kgx_otu *__restrict__ otus,
-    const uint64_t *__restrict__ ooff, kgx_otu *__restrict__ otus_out, uint4 *__restrict__ hits16_out,
-    uint32_t *__restrict__ hits12_out)
+    const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, uint64_t hoff_s, uint64_t coff_s,
+    kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out, uint32_t seq_base,
+    const uint32_t *__restrict__ otu_count, const kgx_otu *__restrict__ otus, uint64_t ooff_s,
+    kgx_otu *__restrict__ otus_out, uint4 *__restrict__ hits16_out, uint32_t *__restrict__ hits12_out)
 {
-    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (s >= n_seq)
-        return;
     const uint32_t lane = lane_id();
     const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
     if ((hits_out || (PK && (hits16_out || hits12_out))) && gw0 < gw1) {
@@ -1819,7 +1833,7 @@ __global__ __launch_bounds__(256) void gather_kernel(
                 if (lane >= off)
                     incl += x;
             }
-            const uint64_t dst0 = hoff[s] + done + (incl - cnt);
+            const uint64_t dst0 = hoff_s + done + (incl - cnt);
             if (PK && hits16_out) { /* the records as stored: position = mask bit */
                 for (uint32_t i = 0; i < cnt; i++)
                     hits16_out[dst0 + i] = hot[at + i];
@@ -1860,17 +1874,100 @@ __global__ __launch_bounds__(256) void gather_kernel(
     }
     if (calls_out) {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(calls + gw0);
-        uint32_t *dst = reinterpret_cast<uint32_t *>(calls_out + coff[s]);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(calls_out + coff_s);
         const uint32_t n = 5 * call_count[s];
         for (uint32_t i = lane; i < n; i += 64)
             dst[i] = src[i];
     }
     if (otus_out) {
         const kgx_otu *src = otus + gw0;
-        kgx_otu *dst = otus_out + ooff[s];
+        kgx_otu *dst = otus_out + ooff_s;
         for (uint32_t i = lane; i < otu_count[s]; i += 64)
             dst[i] = src[i];
     }
+}
+
+template <bool PK>
+__global__ __launch_bounds__(256) void gather_kernel(
+    uint32_t n_seq, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask,
+    uint32_t tile_windows, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
+    const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint64_t *__restrict__ hoff,
+    const uint64_t *__restrict__ coff, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
+    uint32_t seq_base, const uint32_t *__restrict__ otu_count, const kgx_otu *__restrict__ otus,
+    const uint64_t *__restrict__ ooff, kgx_otu *__restrict__ otus_out, uint4 *__restrict__ hits16_out,
+    uint32_t *__restrict__ hits12_out)
+{
+    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= n_seq)
+        return;
+    const bool want_hits = hits_out || (PK && (hits16_out || hits12_out));
+    gather_one<PK>(s, wbase, hit_mask, tile_windows, call_count, hot, cold, calls, want_hits ? hoff[s] : 0,
+                   calls_out ? coff[s] : 0, hits_out, calls_out, seq_base, otu_count, otus,
+                   otus_out ? ooff[s] : 0, otus_out, hits16_out, hits12_out);
+}
+
+/* small batches (<= SMALL_GATHER_SEQ sequences): small_collect and gather in
+ * one workgroup -- the counts scanned into LDS (and into the caller's mapped
+ * offsets), then four waves gather the sequences from those offsets */
+template <bool PK>
+__global__ __launch_bounds__(256) void small_gather_kernel(
+    uint32_t n, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask, uint32_t tile_windows,
+    const uint32_t *__restrict__ hit_count, const uint32_t *__restrict__ call_count, const uint4 *__restrict__ hot,
+    const uint4 *__restrict__ cold, const kgx_call *__restrict__ calls, const uint32_t *__restrict__ otu_count,
+    const kgx_otu *__restrict__ otus, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
+    kgx_otu *__restrict__ otus_out, Offsets3 off_host, const uint32_t *__restrict__ status,
+    const kgx_best_call *__restrict__ best, kgx_best_call *__restrict__ best_host, uint32_t *__restrict__ status_host,
+    uint64_t *__restrict__ nwin_host)
+{
+    __shared__ uint64_t lds4[3][4];
+    __shared__ uint64_t lo[3][SMALL_GATHER_SEQ + 1];
+    const uint32_t t = threadIdx.x;
+    const uint32_t *cnt[3] = {hit_count, calls_out ? call_count : nullptr, otus_out ? otu_count : nullptr};
+    for (int a = 0; a < 3; a++) {
+        const uint64_t v = t < n && cnt[a] ? cnt[a][t] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_scan(v, lds4[a], tot) - v;
+        if (t < n) {
+            lo[a][t] = ex;
+            off_host.o[a][t] = ex;
+        }
+        if (t == 0) {
+            lo[a][n] = tot;
+            off_host.o[a][n] = tot;
+        }
+    }
+    if (best_host && t < n)
+        best_host[t] = best[t];
+    if (t == 0) {
+        status_host[0] = status[0];
+        nwin_host[0] = wbase[n];
+    }
+    __syncthreads();
+    for (uint32_t s = t >> 6; s < n; s += 4)
+        gather_one<PK>(s, wbase, hit_mask, tile_windows, call_count, hot, cold, calls, lo[0][s], lo[1][s], hits_out,
+                       calls_out, 0u, otu_count, otus, lo[2][s], otus_out, nullptr, nullptr);
+}
+
+hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
+                               const uint32_t *hit_count, const uint32_t *call_count, const uint4 *hot,
+                               const uint4 *cold, const kgx_call *calls, const uint32_t *otu_count,
+                               const kgx_otu *otus, kgx_hit *hits_out, kgx_call *calls_out, kgx_otu *otus_out,
+                               uint64_t *h0, uint64_t *h1, uint64_t *h2, const uint32_t *status,
+                               const kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
+                               uint64_t *nwin_host, uint32_t hit_format, hipStream_t stream)
+{
+    if (n == 0 || n > SMALL_GATHER_SEQ)
+        return hipErrorInvalidValue;
+    const Offsets3 off_host = {{h0, h1, h2}};
+    if (hit_format == HIT_PACKED16)
+        hipLaunchKernelGGL(small_gather_kernel<true>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask, tile_windows,
+                           hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out, calls_out, otus_out,
+                           off_host, status, best, best_host, status_host, nwin_host);
+    else
+        hipLaunchKernelGGL(small_gather_kernel<false>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask,
+                           tile_windows, hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out,
+                           calls_out, otus_out, off_host, status, best, best_host, status_host, nwin_host);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *hit_mask,
@@ -1899,14 +1996,6 @@ hipError_t launch_gather(uint32_t n_seq, const uint64_t *wbase, const uint64_t *
 /* scorer and the gather): off[a][i] = sum_{j<i} count[a][j], i in [0, n]   */
 /* ------------------------------------------------------------------------ */
 
-constexpr uint32_t CS_PER = 4, CS_TILE = 256 * CS_PER;
-
-struct Counts3 {
-    const uint32_t *c[3]; /* NULL: an all-zero array */
-};
-struct Offsets3 {
-    uint64_t *o[3];
-};
 
 __device__ __forceinline__ uint64_t thread_count(const uint32_t *c, uint32_t n, uint32_t i0)
 {

@@ -314,6 +314,7 @@ struct kgx_ctx {
     int probe_variant = kgx::PROBE_AUTO;
     int probe_j = kgx::PROBE_J_DEFAULT;
     int probe_lds_kb = 0;  /* LDS reserved per probe workgroup, caps its occupancy (option "probe_lds_kb") */
+    int probe_persist = 0; /* line probe grid cap in workgroups per CU, waves stride over tiles (option "probe_persist") */
     int fq_residues = 1;   /* 1: kgx_fq_fragments writes residues; 0: anchors (kgx_fq_run_device) */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
     int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */

@@ -969,6 +969,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->small_batch = value;
         return KGX_OK;
     }
+    if (n == "probe_persist") {
+        if (value < 0 || value > 32)
+            return fail(KGX_EINVAL, "probe_persist must be 0..32 workgroups per CU");
+        c->probe_persist = (int)value;
+        return KGX_OK;
+    }
     if (n == "small_wave") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "small_wave must be 0 or 1");
@@ -1102,6 +1108,18 @@ int plan_reserve(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_r
 
 namespace {
 
+/* option probe_persist: the line probe's grid capped at that many
+ * workgroups per CU (0 = uncapped) */
+uint32_t probe_max_blocks(const kgx_ctx *c)
+{
+    if (!c->probe_persist)
+        return 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->img->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    return (uint32_t)c->probe_persist * (uint32_t)cus;
+}
+
 /* one probe launch on c's stream; with probe_serialize it waits for the
  * image's previous probe, whichever context issued it */
 template <class Launch>
@@ -1151,7 +1169,8 @@ int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const ui
     return probe_chained(c, [&] {
         return launch_probe_dna(bases, n_bases, anchors, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
                                 c->n_seq, c->max_tiles, c->img->resident(), c->img->num_sigs, c->hits.as<uint4>(),
-                                c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64), c->stream);
+                                c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64), probe_max_blocks(c),
+                                c->stream);
     });
 }
 
@@ -1168,7 +1187,8 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
                             c->n_seq, c->max_tiles, c->img->resident(), c->img->layout, c->img->num_sigs,
                             c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                             c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
-                            (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb, c->stream);
+                            (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb,
+                            probe_max_blocks(c), c->stream);
     });
 }
 
@@ -2239,20 +2259,33 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
         HIP_TRY(c->h_otus.device_ptr(0, &mo));
     if (want_best && n_seq)
         HIP_TRY(c->h_best.device_ptr(0, &mb));
-    HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(), want_calls ? c->call_count.as<uint32_t>() : nullptr,
-                                 want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
-                                 c->dense_coff.as<uint64_t>(), c->dense_ooff.as<uint64_t>(),
-                                 static_cast<uint64_t *>(m_hoff), static_cast<uint64_t *>(m_coff),
-                                 static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
-                                 c->wbase.as<uint64_t>(), want_best ? c->best.as<kgx_best_call>() : nullptr,
-                                 static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
-                                 static_cast<uint64_t *>(m_nwin), c->stream));
-    HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
-                          c->call_count.as<uint32_t>(), c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots,
-                          c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
-                          static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
-                          c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
-                          static_cast<kgx_otu *>(mo), c->stream));
+    if (n_seq <= SMALL_GATHER_SEQ) { /* scan + gather in one workgroup */
+        HIP_TRY(launch_small_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                                    c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
+                                    c->hits.as<uint4>() + c->hit_slots, c->calls.as<kgx_call>(),
+                                    c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), static_cast<kgx_hit *>(mh),
+                                    static_cast<kgx_call *>(mc), static_cast<kgx_otu *>(mo),
+                                    static_cast<uint64_t *>(m_hoff), static_cast<uint64_t *>(m_coff),
+                                    static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
+                                    want_best ? c->best.as<kgx_best_call>() : nullptr,
+                                    static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
+                                    static_cast<uint64_t *>(m_nwin), c->hit_format, c->stream));
+    } else {
+        HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(),
+                                     want_calls ? c->call_count.as<uint32_t>() : nullptr, want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
+                                     c->dense_coff.as<uint64_t>(), c->dense_ooff.as<uint64_t>(),
+                                     static_cast<uint64_t *>(m_hoff), static_cast<uint64_t *>(m_coff),
+                                     static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
+                                     c->wbase.as<uint64_t>(), want_best ? c->best.as<kgx_best_call>() : nullptr,
+                                     static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
+                                     static_cast<uint64_t *>(m_nwin), c->stream));
+        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                              c->call_count.as<uint32_t>(), c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots,
+                              c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
+                              static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
+                              c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
+                              static_cast<kgx_otu *>(mo), c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->h_plan_status[0])
         return fail(KGX_EINVAL, "small batch: plan status raised");

@@ -16,7 +16,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1
+# (libkgx.so is built beforehand in the container and travels with the tree)
 echo "[collect] kernel trace" >&2
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt \
     -- python3 "$R/bench.py" --no-cpu-baseline --no-host-path --pipeline 1 --steps 20 > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err"
@@ -41,3 +41,4 @@ if b.get("cpu_baseline") and b["cpu_baseline"].get("pbar"):
     t["pbar_note"] = "mean buckets examined per window, counted by the oracle on the C2 batch (bench.py CPU-baseline leg)"
 json.dump(t, open(sys.argv[2], "w"), indent=1)
 PY
+cp "$R/profiles/probe_traffic.json" "$OUT/probe_traffic_final.json"

@@ -838,8 +838,11 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
     seqs = [res[int(off[i]):int(off[i + 1])].copy() for i in range(60)]
     seqs[3][40] = 0  # NUL cut
     long_seq = np.frombuffer(random_protein(rng, 20_000).encode(), np.uint8)
+    # more than SMALL_GATHER_SEQ (256) sequences: scan and gather in separate launches
+    res2, off2 = synth.make_queries(spec, 400, x_permille=5, q0=5000)
+    many = [res2[int(off2[i]):int(off2[i]) + int(k)] for i, k in enumerate(rng.integers(0, 150, 400))]
     batches = [seqs[:1], seqs[1:2] + [np.zeros(0, np.uint8)], [np.zeros(0, np.uint8)] + seqs[2:20],
-               [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], [long_seq] + seqs[:3]]
+               [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], [long_seq] + seqs[:3], many]
     p = gpu.Params(*params)
     for layout_ctx, sw in ((ctx, 1), (ctx, 0), (aos_world[1], 1)):
         layout_ctx.set_option("small_wave", sw)  # wave scorer (default) / the hybrid
@@ -865,3 +868,19 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
                 layout_ctx.set_option("small_batch", 65536)
             assert np.array_equal(small_best.best, ref_best)
         layout_ctx.set_option("small_wave", 1)
+
+
+@pytest.mark.parametrize("persist", [1, 3])
+def test_probe_persist_matches_oracle(small_world, oracle_lib, gpu, persist):
+    """probe_persist caps the line probe's grid (waves stride over the tiles:
+    a 900k-residue batch gives each wave several tiles); same records as the
+    oracle."""
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 3000, x_permille=5, q0=9000)
+    want = oracle_lib.process_batch(table, res, off)
+    ctx.set_option("probe_persist", persist)
+    try:
+        got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0))
+    finally:
+        ctx.set_option("probe_persist", 0)
+    assert_same(got, want, 3000)
