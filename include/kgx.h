@@ -287,6 +287,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
+ * "probe_persist" (0..32, default 0) caps the line probe's grid at that many
+ * workgroups per CU, its waves then striding over the tiles (measured slower,
+ * DESIGN.md §5);
  * "score_variant" 0 (default) = hybrid run scorer: one lane per sequence,
  * except sequences of 2,049..39,998 windows, which the wave-parallel scorer
  * takes (a lane walking a 30k-aa protein would hold the stage for ms);
