@@ -1917,7 +1917,7 @@ __global__ __launch_bounds__(256) void small_gather_kernel(
     const kgx_otu *__restrict__ otus, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
     kgx_otu *__restrict__ otus_out, Offsets3 off_host, const uint32_t *__restrict__ status,
     const kgx_best_call *__restrict__ best, kgx_best_call *__restrict__ best_host, uint32_t *__restrict__ status_host,
-    uint64_t *__restrict__ nwin_host)
+    uint64_t *__restrict__ nwin_host, uint32_t *done_host, uint32_t token)
 {
     __shared__ uint64_t lds4[3][4];
     __shared__ uint64_t lo[3][SMALL_GATHER_SEQ + 1];
@@ -1946,6 +1946,16 @@ __global__ __launch_bounds__(256) void small_gather_kernel(
     for (uint32_t s = t >> 6; s < n; s += 4)
         gather_one<PK>(s, wbase, hit_mask, tile_windows, call_count, hot, cold, calls, lo[0][s], lo[1][s], hits_out,
                        calls_out, 0u, otu_count, otus, lo[2][s], otus_out, nullptr, nullptr);
+    /* the batch's last word: every store above is visible to the host before
+     * the host sees done_host == token (it polls instead of a stream sync) */
+    if (done_host) {
+        __threadfence_system();
+        __syncthreads();
+        if (t == 0) {
+            __threadfence_system();
+            *reinterpret_cast<volatile uint32_t *>(done_host) = token;
+        }
+    }
 }
 
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
@@ -1954,7 +1964,8 @@ hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t
                                const kgx_otu *otus, kgx_hit *hits_out, kgx_call *calls_out, kgx_otu *otus_out,
                                uint64_t *h0, uint64_t *h1, uint64_t *h2, const uint32_t *status,
                                const kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
-                               uint64_t *nwin_host, uint32_t hit_format, hipStream_t stream)
+                               uint64_t *nwin_host, uint32_t *done_host, uint32_t token, uint32_t hit_format,
+                               hipStream_t stream)
 {
     if (n == 0 || n > SMALL_GATHER_SEQ)
         return hipErrorInvalidValue;
@@ -1962,11 +1973,12 @@ hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t
     if (hit_format == HIT_PACKED16)
         hipLaunchKernelGGL(small_gather_kernel<true>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask, tile_windows,
                            hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out, calls_out, otus_out,
-                           off_host, status, best, best_host, status_host, nwin_host);
+                           off_host, status, best, best_host, status_host, nwin_host, done_host, token);
     else
         hipLaunchKernelGGL(small_gather_kernel<false>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask,
                            tile_windows, hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out,
-                           calls_out, otus_out, off_host, status, best, best_host, status_host, nwin_host);
+                           calls_out, otus_out, off_host, status, best, best_host, status_host, nwin_host,
+                           done_host, token);
     return hipGetLastError();
 }
 

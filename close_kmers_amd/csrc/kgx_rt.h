@@ -84,6 +84,7 @@ struct DevBuf {
 template <class T> struct PinnedVec {
     T *p = nullptr;
     size_t n = 0, cap = 0;
+    mutable void *dp = nullptr; /* p's device address, looked up once per allocation */
     PinnedVec() = default;
     PinnedVec(const PinnedVec &) = delete;
     PinnedVec &operator=(const PinnedVec &) = delete;
@@ -106,6 +107,7 @@ template <class T> struct PinnedVec {
             }
             p = q;
             cap = want;
+            dp = nullptr;
         }
         n = m;
         return hipSuccess;
@@ -115,11 +117,15 @@ template <class T> struct PinnedVec {
     /* the device's address of element i (pinned host memory is mapped) */
     hipError_t device_ptr(size_t i, void **out) const
     {
-        void *d = nullptr;
-        hipError_t e = hipHostGetDevicePointer(&d, p, 0);
-        if (e == hipSuccess)
-            *out = static_cast<char *>(d) + i * sizeof(T);
-        return e;
+        if (!dp) {
+            hipError_t e = hipHostGetDevicePointer(&dp, p, 0);
+            if (e != hipSuccess) {
+                dp = nullptr;
+                return e;
+            }
+        }
+        *out = static_cast<char *>(dp) + i * sizeof(T);
+        return hipSuccess;
     }
     size_t size() const { return n; }
     T &operator[](size_t i) { return p[i]; }
@@ -379,6 +385,8 @@ struct kgx_ctx {
     int64_t small_batch = 1 << 16;
     int small_wave = 1; /* small batches: the wave scorer instead of the hybrid (option "small_wave") */
     kgx::PinnedVec<uint4> h_small; /* offsets | window bases | tile owners | status | residues */
+    kgx::PinnedVec<uint32_t> h_done; /* the fused small gather's completion token */
+    uint32_t small_token = 0;
     int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
     kgx::PinnedVec<kgx_call> h_calls_region;
     kgx::PinnedVec<kgx_otu> h_otus_region;

@@ -2259,7 +2259,17 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
         HIP_TRY(c->h_otus.device_ptr(0, &mo));
     if (want_best && n_seq)
         HIP_TRY(c->h_best.device_ptr(0, &mb));
-    if (n_seq <= SMALL_GATHER_SEQ) { /* scan + gather in one workgroup */
+    /* the fused gather stores a fresh token last; the host polls it (a stream
+     * sync costs several us more than the kernel's own end) */
+    const bool fused = n_seq <= SMALL_GATHER_SEQ;
+    const uint32_t token = ++c->small_token ? c->small_token : ++c->small_token;
+    void *m_done = nullptr;
+    if (fused) {
+        HIP_TRY(c->h_done.resize(1));
+        c->h_done[0] = 0;
+        HIP_TRY(c->h_done.device_ptr(0, &m_done));
+    }
+    if (fused) { /* scan + gather in one workgroup */
         HIP_TRY(launch_small_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
                                     c->hit_count.as<uint32_t>(), c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
                                     c->hits.as<uint4>() + c->hit_slots, c->calls.as<kgx_call>(),
@@ -2269,7 +2279,8 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                                     static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
                                     want_best ? c->best.as<kgx_best_call>() : nullptr,
                                     static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
-                                    static_cast<uint64_t *>(m_nwin), c->hit_format, c->stream));
+                                    static_cast<uint64_t *>(m_nwin), static_cast<uint32_t *>(m_done), token,
+                                    c->hit_format, c->stream));
     } else {
         HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(),
                                      want_calls ? c->call_count.as<uint32_t>() : nullptr, want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
@@ -2286,7 +2297,24 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                               c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
                               static_cast<kgx_otu *>(mo), c->stream));
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (fused) {
+        const volatile uint32_t *done = c->h_done.data();
+        for (uint32_t spin = 1; *done != token; spin++) {
+            if ((spin & 255u) == 0) { /* a fault or a lost store still ends the wait */
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q == hipSuccess)
+                    break;
+                if (q != hipErrorNotReady)
+                    HIP_TRY(q);
+            }
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     if (c->h_plan_status[0])
         return fail(KGX_EINVAL, "small batch: plan status raised");
     c->h_hoff.assign(c->h_dense_hoff.data(), c->h_dense_hoff.data() + n_seq + 1);
