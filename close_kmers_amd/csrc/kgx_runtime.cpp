@@ -2216,7 +2216,14 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
         pc.end16[p] = at;
     }
     HIP_TRY(launch_small_upload(pc, c->stream));
-    if ((rc = kgx_stage_probe(c, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>())))
+    /* a small probe neither waits for nor holds back the image's other probes:
+     * chaining it (probe_serialize, for probes that fill the chip) would make
+     * the pool's per-sequence calls run one at a time across worker threads */
+    const int serialize = c->probe_serialize;
+    c->probe_serialize = 0;
+    rc = kgx_stage_probe(c, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>());
+    c->probe_serialize = serialize;
+    if (rc)
         return rc;
     /* the scorer: with few sequences the lane machine's one-lane chain per
      * sequence is the whole stage's latency (31 us for one 300-aa protein);

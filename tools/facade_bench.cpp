@@ -5,7 +5,9 @@
  * each call is one GPU round trip.  Times that call on single 300-aa C2
  * proteins (latency distribution) and the same sequences through
  * process_aa_batch (one pass), with the lookup handler's outputs (calls + a
- * hit callback, no OTU stats).
+ * hit callback, no OTU stats); then the reference's pool shape: T worker
+ * threads, one KmerGuts each over the shared image (threadpool.cc:18-44),
+ * each calling process_aa_seq per sequence (aggregate rate per T).
  *
  *   facade_bench KMER_DIR N_KEYS NUM_SIGS QUERIES.bin [N_CALLS]
  *
@@ -18,6 +20,7 @@
 #include <fstream>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kguts_hip.h"
@@ -115,15 +118,57 @@ int main(int argc, char **argv)
                 bcalls += j.calls->size();
     }
     const double t_batch = pct(tb, 50);
+
+    /* the worker pool: T threads, one KmerGuts (context) each, per-sequence calls */
+    std::string pool_json;
+    bool pool_ok = true;
+    for (int T : {1, 4, 8, 16}) {
+        std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
+        for (int t = 0; t < T; t++)
+            kgs.emplace_back(new kgx::KmerGuts(dir, image));
+        std::vector<uint64_t> th_hits(T, 0);
+        auto work = [&](int t, bool count) {
+            for (size_t i = (size_t)t; i < m; i += (size_t)T) {
+                auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+                uint64_t h = 0;
+                kgs[t]->process_aa_seq("q", seqs[i], cv, [&h](kgx::KmerGuts::hit_in_sequence_t) { h++; }, nullptr);
+                if (count)
+                    th_hits[t] += h;
+            }
+        };
+        { /* warm: buffer growth on every context */
+            std::vector<std::thread> ws;
+            for (int t = 0; t < T; t++)
+                ws.emplace_back(work, t, false);
+            for (auto &w : ws)
+                w.join();
+        }
+        const auto t0 = clk::now();
+        std::vector<std::thread> ws;
+        for (int t = 0; t < T; t++)
+            ws.emplace_back(work, t, true);
+        for (auto &w : ws)
+            w.join();
+        const double tp = std::chrono::duration<double>(clk::now() - t0).count();
+        uint64_t ph = 0;
+        for (uint64_t h : th_hits)
+            ph += h;
+        pool_ok = pool_ok && ph == hits;
+        char b[160];
+        std::snprintf(b, sizeof b, "%s\"%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g}", pool_json.empty() ? "" : ", ",
+                      T, (double)m / tp, (double)residues / tp);
+        pool_json += b;
+    }
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
                 "\"latency_us_ordinary_path\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f}, "
                 "\"unbatched_residues_per_s\": %.4g, \"batched\": {\"sequences\": %zu, \"ms\": %.3f, "
                 "\"residues_per_s\": %.4g}, \"hits\": %llu, \"calls_out\": %llu, \"batch_hits_per_rep\": %llu, "
-                "\"batch_calls\": %llu, \"keys_stored\": %llu}\n",
+                "\"batch_calls\": %llu, \"keys_stored\": %llu, \"worker_pool_by_threads\": {%s}}\n",
                 m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, pct(lat0, 50), pct(lat0, 90),
                 pct(lat0, 99), (double)residues / t_seq, m,
                 t_batch * 1e3, (double)residues / t_batch, (unsigned long long)hits, (unsigned long long)calls,
-                (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored);
-    return hits * 6 == bhits && calls == bcalls && hits == hits0 && calls == calls0 ? 0 : 3;
+                (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored,
+                pool_json.c_str());
+    return hits * 6 == bhits && calls == bcalls && hits == hits0 && calls == calls0 && pool_ok ? 0 : 3;
 }
