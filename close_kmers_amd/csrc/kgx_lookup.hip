@@ -114,8 +114,14 @@ __global__ __launch_bounds__(256) void plan_reduce_kernel(const uint64_t *__rest
  * all earlier sums itself: quadratic in the number of workgroups, 0.5 ms for
  * the 9.9M fragments of a 1M-read fq chunk; then 256 threads in rounds of
  * 256: 31 us.) */
-constexpr uint32_t SUMS_THREADS = 1024, SUMS_PER = 16;
+constexpr uint32_t SUMS_PER = 16;
 
+/* SUMS_THREADS 256 for up to 4,096 sums (C2: 98): a 4-wave workgroup finds a
+ * slot beside the other context's probe at once, where a 16-wave one waited
+ * for that probe to drain (550 us stretched, kernel trace r2zr; 9 us, r2zs).
+ * The 12-14 us between consecutive probes did not change: that is the
+ * cross-queue event wait, not the plan. */
+template <uint32_t SUMS_THREADS>
 __global__ __launch_bounds__(SUMS_THREADS) void plan_sums_scan_kernel(uint64_t *__restrict__ sums, uint32_t groups,
                                                                       const uint32_t *__restrict__ maxw,
                                                                       uint32_t *__restrict__ status)
@@ -228,8 +234,12 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_resid
     uint32_t *maxw = reinterpret_cast<uint32_t *>(static_cast<uint64_t *>(workspace) + groups + 2);
     hipLaunchKernelGGL(plan_reduce_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq, n_residues,
                        static_cast<uint64_t *>(workspace), maxw);
-    hipLaunchKernelGGL(plan_sums_scan_kernel, dim3(1), dim3(SUMS_THREADS), 0, stream,
-                       static_cast<uint64_t *>(workspace), groups, maxw, status);
+    if (groups <= 256 * SUMS_PER)
+        hipLaunchKernelGGL(plan_sums_scan_kernel<256>, dim3(1), dim3(256), 0, stream,
+                           static_cast<uint64_t *>(workspace), groups, maxw, status);
+    else
+        hipLaunchKernelGGL(plan_sums_scan_kernel<1024>, dim3(1), dim3(1024), 0, stream,
+                           static_cast<uint64_t *>(workspace), groups, maxw, status);
     hipLaunchKernelGGL(plan_scan_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq,
                        static_cast<const uint64_t *>(workspace), wbase, tile_seq, tile_windows);
     return hipGetLastError();
