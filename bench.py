@@ -145,6 +145,8 @@ def main():
                     help="HBM-resident bucket layout (packed when the payloads fit)")
     ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="LDS KB reserved per probe workgroup (-1 = default)")
+    ap.add_argument("--probe-stream", type=int, default=-1,
+                    help="1 = the contexts' chained probes on one image stream (-1 = default)")
     ap.add_argument("--probe-persist", type=int, default=-1,
                     help="line-probe grid cap in workgroups per CU, waves striding over tiles (-1 = default)")
     ap.add_argument("--score-variant", type=int, default=0, help="0 = hybrid (default: lanes, long sequences on the wave scorer), 1 = wave-parallel, 2 = lanes only")
@@ -228,6 +230,8 @@ def main():
             c.set_option("probe_lds_kb", args.probe_lds_kb)
         if args.probe_persist >= 0:
             c.set_option("probe_persist", args.probe_persist)
+        if args.probe_stream >= 0:
+            c.set_option("probe_stream", args.probe_stream)
     score_ms: list = []  # score stage (+ best/OTU kernels with --want), same untimed pass as probe_ms
 
     def step(timed_probe: list | None, c=ctx, b=0):
@@ -449,7 +453,7 @@ def main():
                 "worker_contexts": len(ctxs), "distinct_batches": len(batches),
                 "hits_total": total_hits,
                 "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb,
-                "probe_persist": args.probe_persist,
+                "probe_persist": args.probe_persist, "probe_stream": args.probe_stream,
                 # the score stage alone (HIP events on the context's stream, same
                 # untimed pass as the probe time): what a single-context caller pays
                 "score_stage_ms": float(np.mean(score_ms)) if score_ms else None,

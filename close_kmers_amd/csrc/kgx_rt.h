@@ -271,6 +271,7 @@ struct kgx_image {
      * translation) overlap the next context's probe */
     std::mutex probe_mu;
     hipEvent_t last_probe = nullptr; /* end of the latest probe enqueued */
+    hipStream_t probe_stream = nullptr; /* contexts' chained probes with option probe_stream */
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
@@ -287,6 +288,8 @@ struct kgx_ctx {
     bool own_stream = false;
     hipEvent_t probe_done = nullptr; /* recorded after each of this context's probes */
     int probe_serialize = 1;          /* option "probe_serialize" */
+    int probe_stream = 0;             /* chained probes on the image's probe stream (option "probe_stream") */
+    hipEvent_t probe_ready = nullptr; /* this context's inputs are ready for its probe */
     /* device scratch */
     kgx::DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
         dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;

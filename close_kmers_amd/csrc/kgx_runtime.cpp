@@ -677,6 +677,10 @@ int kgx_image_close(kgx_image *img)
         (void)hipFree(img->d_packed);
     if (img->d_filter)
         (void)hipFree(img->d_filter);
+    if (img->probe_stream) {
+        (void)hipStreamSynchronize(img->probe_stream);
+        (void)hipStreamDestroy(img->probe_stream);
+    }
     delete img;
     return KGX_OK;
 }
@@ -824,6 +828,8 @@ int kgx_ctx_destroy(kgx_ctx *c)
             c->img->last_probe = nullptr;
     }
     (void)hipEventDestroy(c->probe_done);
+    if (c->probe_ready)
+        (void)hipEventDestroy(c->probe_ready);
     c->pool.reset();
     c->stage_pool.reset();
     for (hipEvent_t e : c->chunk_done)
@@ -967,6 +973,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value < 0 || value > (1 << 24))
             return fail(KGX_EINVAL, "small_batch must be 0..16777216 residues");
         c->small_batch = value;
+        return KGX_OK;
+    }
+    if (n == "probe_stream") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "probe_stream must be 0 or 1");
+        c->probe_stream = (int)value;
         return KGX_OK;
     }
     if (n == "probe_persist") {
@@ -1130,15 +1142,36 @@ int probe_chained(kgx_ctx *c, Launch launch)
         return fail(KGX_ERANGE, "image too large");
     kgx_image *img = c->img;
     std::unique_lock<std::mutex> lock(img->probe_mu, std::defer_lock);
-    if (c->probe_serialize) {
+    if (c->probe_serialize && c->probe_stream) {
+        /* option probe_stream: every chained probe of the image on one stream
+         * (one hardware queue), entered when this context's inputs are ready
+         * and left back to this context's stream */
         lock.lock();
-        if (img->last_probe && img->last_probe != c->probe_done)
-            HIP_TRY(hipStreamWaitEvent(c->stream, img->last_probe, 0));
-    }
-    HIP_TRY(launch());
-    if (c->probe_serialize) {
-        HIP_TRY(hipEventRecord(c->probe_done, c->stream));
+        if (!img->probe_stream)
+            HIP_TRY(hipStreamCreateWithFlags(&img->probe_stream, hipStreamNonBlocking));
+        if (!c->probe_ready)
+            HIP_TRY(hipEventCreateWithFlags(&c->probe_ready, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->probe_ready, c->stream));
+        HIP_TRY(hipStreamWaitEvent(img->probe_stream, c->probe_ready, 0));
+        hipStream_t own = c->stream;
+        c->stream = img->probe_stream; /* the launch reads c->stream */
+        const hipError_t le = launch();
+        c->stream = own;
+        HIP_TRY(le);
+        HIP_TRY(hipEventRecord(c->probe_done, img->probe_stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->probe_done, 0));
         img->last_probe = c->probe_done;
+    } else {
+        if (c->probe_serialize) {
+            lock.lock();
+            if (img->last_probe && img->last_probe != c->probe_done)
+                HIP_TRY(hipStreamWaitEvent(c->stream, img->last_probe, 0));
+        }
+        HIP_TRY(launch());
+        if (c->probe_serialize) {
+            HIP_TRY(hipEventRecord(c->probe_done, c->stream));
+            img->last_probe = c->probe_done;
+        }
     }
     /* every PACKED16 probe stores the matching record itself */
     c->hit_format = c->img->layout == KGX_LAYOUT_PACKED16 ? HIT_PACKED16 : HIT_PLANES;

@@ -287,6 +287,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
+ * "probe_stream" 1 = the image's chained probes all on one image-wide stream
+ * (default 0: each on its context's stream, chained by events; same speed);
  * "probe_persist" (0..32, default 0) caps the line probe's grid at that many
  * workgroups per CU, its waves then striding over the tiles (measured slower,
  * DESIGN.md §5);

@@ -884,3 +884,21 @@ def test_probe_persist_matches_oracle(small_world, oracle_lib, gpu, persist):
     finally:
         ctx.set_option("probe_persist", 0)
     assert_same(got, want, 3000)
+
+
+def test_probe_stream_two_contexts_match_oracle(small_world, oracle_lib, gpu):
+    """probe_stream 1: two contexts' chained probes share the image's probe
+    stream (entered on an event from each context's stream, left back to it);
+    both contexts' alternating batches give the oracle's records."""
+    spec, table, img, ctx = small_world
+    other = gpu.Context(img)
+    try:
+        for c in (ctx, other):
+            c.set_option("probe_stream", 1)
+        for k in range(4):
+            res, off = synth.make_queries(spec, 1500, x_permille=5, q0=20000 + 1500 * k)
+            got = (ctx, other)[k % 2].process_batch(res, off, gpu.Params(5, 200, 0, 0))
+            assert_same(got, oracle_lib.process_batch(table, res, off), 1500)
+    finally:
+        ctx.set_option("probe_stream", 0)
+        other.close()
