@@ -1,6 +1,7 @@
 """Benchmark of the hot path: protein residues/s against a 1B-entry k-mer image.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n-keys 1e9] [--n-seq 100000]
+        (N > 1 without torchrun: bench.py starts the N ranks itself, one per GPU)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Workload (BASELINE.json configs[1], SURVEY §8(d) "C2"): per GPU, 100,000
@@ -153,17 +154,33 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "probe_traffic.json"))
     args = ap.parse_args()
 
-    from close_kmers_amd import abi, shard, synth
+    from close_kmers_amd import shard
+
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # --gpus N without torchrun: start the N ranks here, one process
+            # per GPU, before anything in this process touches the GPU; rank
+            # 0's JSON line is relayed, a failing rank fails the job
+            cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+            sys.exit(shard.launch_ranks(cmd, args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {os.environ['WORLD_SIZE']} ranks")
+
+    # one GPU per rank; KGX_BENCH_DEVICE pins every rank to one device (a
+    # rehearsal of the multi-rank control flow on a 1-GPU box, small images)
+    dev = int(os.environ.get("KGX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    from close_kmers_amd import abi, synth
+    L = abi.lib()
+    n_dev = abi.device_count()
+    if n_dev <= dev:
+        raise SystemExit(f"rank {os.environ.get('RANK', '0')}: no device {dev} "
+                         f"({n_dev} gfx950 device(s) visible)")
 
     d = shard.Dist()
     n_keys = int(args.n_keys)
     spec = synth.ImageSpec(n_keys, args.num_sigs or None)
-    # one GPU per rank; KGX_BENCH_DEVICE pins every rank to one device (a
-    # rehearsal of the multi-rank control flow on a 1-GPU box, small images)
-    dev = int(os.environ.get("KGX_BENCH_DEVICE", d.local_rank))
-    L = abi.lib()
-    if abi.device_count() <= dev:
-        raise SystemExit(f"rank {d.rank}: no gfx950 device {dev}")
 
     t0 = time.time()
     # n_keys distinct keys stored (the generator's stream
@@ -312,6 +329,8 @@ def main():
     abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
     abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
     total_hits = int(d.sum(float(hc.sum())))
+    per_rank = d.gather_objects({"rank": d.rank, "device": dev, "ms_per_step": t_wall * 1e3 / args.steps,
+                                 "probe_ms": float(np.mean(probe_ms)), "n_seq": n, "hits": int(hc.sum())})
     log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
         f"(even-q mean {hc[::2].mean():.1f}, odd-q mean {hc[1::2].mean():.2f}); "
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
@@ -449,7 +468,9 @@ def main():
                 "keys_stored": stored, "stream_entries": n_entries,
                 "load_factor": stored / spec.num_sigs,
                 "presence_filter_bits": (1 << args.filter_log2) if args.filter_log2 else 0,
-                "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}, query shards",
+                "num_sigs": spec.num_sigs, "parallelism": f"replicas{d.world}",
+                "sharding": "one image replica + one contiguous query shard per GPU, no data-path collective",
+                "per_rank": per_rank,
                 "worker_contexts": len(ctxs), "distinct_batches": len(batches),
                 "hits_total": total_hits,
                 "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb,

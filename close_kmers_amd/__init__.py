@@ -5,11 +5,22 @@ hand-written gfx950 HIP kernels behind a C ABI (include/kgx.h, libkgx.so),
 with a KmerGuts-compatible C++ facade (csrc/kguts_hip.h) and this thin Python
 binding for tests and benchmarks.  There is no CPU fallback: without the
 library or a gfx950 device the entry points raise.
-"""
-from . import abi, image_files, synth  # noqa: F401
-from .abi import (CALL_DTYPE, HIT_DTYPE, OTU_DTYPE, SIG_DTYPE, WANT_CALLS, WANT_HITS,  # noqa: F401
-                  WANT_OTU, Context, Image, KgxError, device_count, find_best_call, parse_params)
 
-__all__ = ["abi", "synth", "image_files", "Image", "Context", "KgxError", "device_count",
-           "find_best_call", "parse_params", "HIT_DTYPE", "CALL_DTYPE", "OTU_DTYPE", "SIG_DTYPE",
-           "WANT_HITS", "WANT_CALLS", "WANT_OTU"]
+Submodules load on first use, so `import close_kmers_amd.shard` (the rank
+launcher bench.py runs before any GPU call) pulls in nothing of the ABI.
+"""
+import importlib
+
+_SUBMODULES = ("abi", "image_files", "synth", "shard", "build")
+_ABI_NAMES = ("CALL_DTYPE", "HIT_DTYPE", "OTU_DTYPE", "SIG_DTYPE", "WANT_CALLS", "WANT_HITS", "WANT_OTU",
+              "Context", "Image", "KgxError", "device_count", "find_best_call", "parse_params")
+
+__all__ = ["abi", "synth", "image_files", "shard", *_ABI_NAMES]
+
+
+def __getattr__(name):
+    if name in _SUBMODULES:
+        return importlib.import_module(f".{name}", __name__)
+    if name in _ABI_NAMES:
+        return getattr(importlib.import_module(".abi", __name__), name)
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")

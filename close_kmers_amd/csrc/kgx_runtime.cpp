@@ -143,7 +143,10 @@ int kgx_params_parse(kgx_params *p, const char *const *names, const char *const 
 
 /* ---- images ------------------------------------------------------------ */
 
-static int image_alloc(int device, uint64_t num_sigs, kgx_image **out)
+/* an image on `device` with its resident table allocated in `layout`
+ * (AOS24: the file's 24-B buckets; PACKED16: 16-B records, a replica of a
+ * packed image, so no 24-B table is ever allocated for it) */
+static int image_alloc(int device, uint64_t num_sigs, kgx_image **out, int layout = KGX_LAYOUT_AOS24)
 {
     if (!out)
         return fail(KGX_EINVAL, "null output");
@@ -158,12 +161,15 @@ static int image_alloc(int device, uint64_t num_sigs, kgx_image **out)
     kgx_image *img = new kgx_image;
     img->device = device;
     img->num_sigs = num_sigs;
-    hipError_t e = hipMalloc(&img->d_table, num_sigs * sizeof(kgx_sig_kmer));
+    hipError_t e = layout == KGX_LAYOUT_PACKED16 ? hipMalloc(&img->d_packed, num_sigs * sizeof(packed_bucket))
+                                                  : hipMalloc(&img->d_table, num_sigs * sizeof(kgx_sig_kmer));
     if (e != hipSuccess) {
+        (void)hipGetLastError();
         delete img;
         return fail(KGX_ENOMEM, "hipMalloc of the image table failed: " +
                                     std::string(hipGetErrorString(e)));
     }
+    img->layout = layout;
     *out = img;
     return KGX_OK;
 }
@@ -286,8 +292,8 @@ static int load_file_range(int fd, uint64_t off, uint64_t total, const std::vect
         std::vector<hipStream_t> st(D, nullptr);
         std::vector<hipEvent_t> ev(2 * D, nullptr); /* ev[k * D + d]: buffer k's copy to dst d */
         bool used[2] = {false, false};
-        bool setup = hipSetDevice(dsts[0].device) == hipSuccess && hipHostMalloc(&buf[0], chunk) == hipSuccess &&
-                     hipHostMalloc(&buf[1], chunk) == hipSuccess;
+        bool setup = hipSetDevice(dsts[0].device) == hipSuccess && hipHostMalloc(&buf[0], chunk, hipHostMallocPortable) == hipSuccess &&
+                     hipHostMalloc(&buf[1], chunk, hipHostMallocPortable) == hipSuccess;
         for (size_t d = 0; setup && d < D; d++) {
             setup = hipSetDevice(dsts[d].device) == hipSuccess &&
                     hipStreamCreateWithFlags(&st[d], hipStreamNonBlocking) == hipSuccess &&
@@ -463,22 +469,12 @@ int kgx_image_replicate(const kgx_image *src, int device, kgx_image **out)
         return fail(KGX_EINVAL, "null argument");
     *out = nullptr;
     kgx_image *img = nullptr;
-    int rc = image_alloc(device, src->num_sigs, &img);
+    /* the source's resident layout only (a packed source never costs a 24-B
+     * table on the target, not even briefly) */
+    int rc = image_alloc(device, src->num_sigs, &img, src->layout);
     if (rc)
         return rc;
     hipError_t e = hipSuccess;
-    if (src->layout == KGX_LAYOUT_PACKED16) {
-        /* the same resident layout: allocate the packed table instead */
-        (void)hipFree(img->d_table);
-        img->d_table = nullptr;
-        e = hipMalloc(&img->d_packed, src->num_sigs * sizeof(packed_bucket));
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            kgx_image_close(img);
-            return fail(KGX_ENOMEM, "no room for the packed replica");
-        }
-        img->layout = KGX_LAYOUT_PACKED16;
-    }
     /* device to device: xGMI between two GPUs (the runtime picks the path),
      * a device-local copy when both are the same GPU */
     e = hipMemcpyPeer(img->layout == KGX_LAYOUT_PACKED16 ? static_cast<void *>(img->d_packed) : img->d_table,
@@ -1683,13 +1679,15 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
         HIP_TRY(x->dense_ooff.reserve((n + 1) * sizeof(uint64_t)));
         HIP_TRY(x->cscan_ws.reserve(count_scan_workspace_bytes(n)));
+        /* x's dense buffers still feed chunk k-2's bulk copy, and so do its
+         * scanned totals (dense_hoff/coff/ooff + n, read by the counted copies
+         * when they run): nothing of chunk k touches them before that is done */
+        if (k >= 2)
+            HIP_TRY(hipStreamWaitEvent(x->stream, c->chunk_done[k - 2], 0));
         HIP_TRY(launch_count_scan(n, x->hit_count.as<uint32_t>(), want_calls ? x->call_count.as<uint32_t>() : nullptr,
                                   want_otu ? x->otu_count.as<uint32_t>() : nullptr, x->dense_hoff.as<uint64_t>(),
                                   x->dense_coff.as<uint64_t>(), x->dense_ooff.as<uint64_t>(), x->cscan_ws.p,
                                   x->stream));
-        /* x's dense buffers still feed chunk k-2's bulk copy */
-        if (k >= 2)
-            HIP_TRY(hipStreamWaitEvent(x->stream, c->chunk_done[k - 2], 0));
         HIP_TRY(x->dense_hits.reserve(rn * 16));
         if (want_calls)
             HIP_TRY(x->dense_calls.reserve(rn * sizeof(kgx_call)));
@@ -2352,6 +2350,10 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
 #endif
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        /* the stream drained without the gather's last store: its results
+         * are not there (an early exit or a lost store), never hand them out */
+        if (*done != token)
+            return fail(KGX_EDEVICE, "small batch: the gather ended without its completion token");
     } else {
         HIP_TRY(hipStreamSynchronize(c->stream));
     }

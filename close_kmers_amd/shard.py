@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import socket
 import sys
 
 import numpy as np
@@ -102,3 +103,83 @@ class Dist:
 def job_throughput(world: int, residues_per_rank: int, steps: int, max_seconds: float) -> float:
     """Whole-job residues/s: all ranks' residues over the slowest rank's time."""
     return world * residues_per_rank * steps / max_seconds
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_env(rank: int, world: int, port: int, base: dict | None = None) -> dict:
+    """The environment torchrun gives rank `rank` of a one-node job of `world`
+    ranks (one rank per GPU: LOCAL_RANK = RANK = the device index)."""
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0",
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    return env
+
+
+def launch_ranks(cmd: list[str], world: int, out=None, grace_s: float = 10.0,
+                 poll_s: float = 0.05) -> int:
+    """Run `cmd` as `world` ranks of one node, the way torchrun would, from a
+    parent that never touches the GPU (the reference's analogue is one worker
+    per execution resource over a shared image, threadpool.cc:18-44).
+
+    Each rank's stderr goes straight to ours; rank 0's stdout is relayed line
+    by line to `out` (default sys.stdout), the other ranks' stdout goes to our
+    stderr.  When a rank fails, the others are terminated (then killed after
+    `grace_s`): a rank left waiting in a barrier for a dead peer would hang.
+    Returns 0 when every rank exits 0, else the first failing rank's code
+    (or 1 when a rank was killed by a signal)."""
+    import subprocess
+    import threading
+    import time
+
+    out = out or sys.stdout
+    port = free_port()
+    procs = []
+    for r in range(world):
+        procs.append(subprocess.Popen(cmd, env=rank_env(r, world, port), stdout=subprocess.PIPE,
+                                      stderr=None, text=True, bufsize=1))
+
+    def relay(p, sink):
+        for line in p.stdout:
+            sink.write(line)
+            sink.flush()
+
+    relays = [threading.Thread(target=relay, args=(p, out if r == 0 else sys.stderr), daemon=True)
+              for r, p in enumerate(procs)]
+    for t in relays:
+        t.start()
+    rc = 0
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed, code = bad[0]
+            rc = code if code > 0 else 1
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(poll_s)
+    if failed is not None:
+        sys.stderr.write(f"[launch] rank {failed} exited with {procs[failed].returncode}; "
+                         f"stopping the other ranks\n")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    for t in relays:
+        t.join(timeout=5)
+    return rc

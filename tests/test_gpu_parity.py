@@ -708,6 +708,40 @@ def test_streamed_host_batch_region_overflow(small_world, oracle_lib, gpu):
     ctx.set_option("host_chunks", 3)
 
 
+def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
+    """The streamed schedule with its copy stream far behind the compute: one
+    workgroup per bulk copy, many chunks of unequal sizes (so chunk k's scanned
+    totals differ from chunk k-2's), hit-dense queries, every want mask.  Chunk
+    k reuses chunk k-2's device buffers, including the scanned totals that
+    chunk k-2's counted copies read when they run; nothing of chunk k may touch
+    them before those copies are done."""
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 24000, x_permille=0)
+    seqs = [res[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    # unequal chunks: runs of long and short sequences
+    lens = np.where((np.arange(len(seqs)) // 1500) % 2 == 0, 300, 60)
+    seqs = [s[:l] for s, l in zip(seqs, lens)]
+    off = np.zeros(len(seqs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(s) for s in seqs])
+    res = np.concatenate(seqs)
+    want = oracle_lib.process_batch(table, res, off)
+    try:
+        ctx.set_option("host_stream", 1)
+        ctx.set_option("host_hits16", 1)
+        ctx.set_option("host_copy_blocks", 1)
+        for k in (16, 37, 64):
+            ctx.set_option("host_chunks", k)
+            for _ in range(2):  # the second pass runs with the rates the first one raised
+                got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=7)
+                assert_same(got, want, len(off) - 1)
+                assert np.array_equal(got.hits["seq"], want.hits["seq"])
+            g = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=gpu.WANT_HITS)
+            assert eq_fields(g.hits, want.hits)
+    finally:
+        ctx.set_option("host_copy_blocks", 64)
+        ctx.set_option("host_chunks", 3)
+
+
 # ---------------------------------------------------------------------------
 # find_best_call on the device (KGX_WANT_BEST, kgx_find_best_calls)
 

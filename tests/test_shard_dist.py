@@ -143,3 +143,93 @@ def test_strong_split_ranks_concatenate_to_one_pass(world):
     assert sum((p[5] for p in parts), []) == np.diff(whole.call_offsets).tolist()
     got_w = np.array(sum((p[6] for p in parts), []), np.float32)
     assert np.array_equal(got_w.view(np.uint32), whole.calls["weighted_hits"].view(np.uint32))
+
+
+# ---- bench.py --gpus N: the rank launcher (shard.launch_ranks) ----------
+
+_RANK_SCRIPT = r'''
+import json, os, sys
+sys.path.insert(0, {root!r})
+from close_kmers_amd import shard
+assert "close_kmers_amd.abi" not in sys.modules
+d = shard.Dist("gloo")
+env = {{k: os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}}
+envs = d.gather_objects(env)
+t = d.max(float(d.rank + 1))
+if d.rank == 0:
+    print(json.dumps({{"world": d.world, "max": t, "envs": envs}}), flush=True)
+else:
+    print("not relayed to stdout", flush=True)
+d.close()
+'''
+
+
+def _script(tmp_path, body):
+    p = tmp_path / "rank.py"
+    p.write_text(body)
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_launch_ranks_plumbs_torchrun_env(tmp_path, world):
+    import io
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = _script(tmp_path, _RANK_SCRIPT.format(root=root))
+    out = io.StringIO()
+    rc = shard.launch_ranks([sys.executable, str(p)], world, out=out)
+    assert rc == 0
+    lines = out.getvalue().splitlines()
+    assert len(lines) == 1  # rank 0's line alone
+    got = json.loads(lines[0])
+    assert got["world"] == world and got["max"] == float(world)
+    assert [e["RANK"] for e in got["envs"]] == [str(r) for r in range(world)]
+    assert [e["LOCAL_RANK"] for e in got["envs"]] == [str(r) for r in range(world)]
+    assert all(e["WORLD_SIZE"] == str(world) and e["MASTER_ADDR"] == "127.0.0.1" for e in got["envs"])
+
+
+def test_launch_ranks_failing_rank_stops_the_others(tmp_path):
+    import io
+    import sys
+    import time
+    p = _script(tmp_path, "import os, sys, time\n"
+                          "if os.environ['RANK'] == '1': sys.exit(3)\n"
+                          "time.sleep(120)\n")
+    t0 = time.time()
+    rc = shard.launch_ranks([sys.executable, str(p)], 2, out=io.StringIO(), grace_s=5)
+    assert rc == 3
+    assert time.time() - t0 < 30
+
+
+def test_rank_env():
+    env = shard.rank_env(2, 4, 1234, base={"PATH": "/bin"})
+    assert env == {"PATH": "/bin", "RANK": "2", "LOCAL_RANK": "2", "WORLD_SIZE": "4",
+                   "LOCAL_WORLD_SIZE": "4", "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                   "MASTER_PORT": "1234"}
+
+
+def _bench(args, env_extra=None):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=120)
+
+
+def test_bench_gpus_n_launches_n_ranks_and_fails_without_devices():
+    """No GPU in this container: `bench.py --gpus 2` must start two ranks
+    (each reporting its missing device), print no JSON line and fail."""
+    r = _bench(["--gpus", "2", "--no-cpu-baseline"])
+    assert r.returncode != 0
+    assert r.stdout == ""
+    assert "no device" in r.stderr
+    assert "rank 1" in r.stderr or "rank 0" in r.stderr
+
+
+def test_bench_gpus_must_match_torchrun_world():
+    r = _bench(["--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "--gpus 3 but the launcher started 2 ranks" in r.stderr
