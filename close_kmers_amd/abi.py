@@ -64,6 +64,25 @@ class DeviceResult(ctypes.Structure):
 HIT_PLANES, HIT_PACKED16 = 0, 1
 
 
+class HitChunk(ctypes.Structure):
+    _fields_ = [("seq_begin", ctypes.c_uint32), ("seq_end", ctypes.c_uint32), ("record_words", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("hit_begin", ctypes.c_uint64), ("records", ctypes.c_void_p),
+                ("mask", ctypes.c_void_p), ("window_start", ctypes.c_void_p)]
+
+
+class CompactResult(ctypes.Structure):
+    _fields_ = [("r", Result), ("n_chunks", ctypes.c_uint32), ("chunks", ctypes.POINTER(HitChunk))]
+
+
+class HostProfile(ctypes.Structure):
+    _fields_ = [("chunks", ctypes.c_uint32), ("streamed", ctypes.c_uint32)] + \
+        [(k, ctypes.c_double) for k in ("wall_ms", "stage_ms", "h2d_ms", "device_ms", "gather_ms", "d2h_ms",
+                                        "expand_ms")] + [("h2d_bytes", ctypes.c_uint64), ("d2h_bytes", ctypes.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 def hits_from_planes(hot: np.ndarray, cold: np.ndarray) -> np.ndarray:
     """kgx_hit records from kgx_device_result's two hit planes (uint32 [n, 4]
     each): hot = {avg | flags << 16, function_index, function_wt, pos},
@@ -215,6 +234,12 @@ SIGNATURES = {
     "kgx_pool_ctx": (_P, [_P, _U32]),
     "kgx_pool_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
     "kgx_shard_cuts": (_INT, [_P, _U32, _U32, _P]),
+    "kgx_process_batch_compact": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32,
+                                         ctypes.POINTER(CompactResult)]),
+    "kgx_pool_process_batch_compact": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32,
+                                              ctypes.POINTER(CompactResult)]),
+    "kgx_compact_expand": (_INT, [ctypes.POINTER(CompactResult), _P, _P, _U32, _U32, _U32, _P]),
+    "kgx_ctx_host_profile": (_INT, [_P, ctypes.POINTER(HostProfile)]),
 }
 
 
@@ -407,6 +432,44 @@ class BatchResult:
         self.best = _view(r.best, n, BEST_DTYPE, copy) if r.best else None
 
 
+class CompactBatch:
+    """kgx_compact_result: offsets / calls / OTUs / best as BatchResult views
+    (valid until the producer's next call), hits kept as compact records.
+    expand() builds kgx_hit records (HIT_DTYPE) for a range of sequences."""
+
+    def __init__(self, cr: CompactResult, residues: np.ndarray, offsets: np.ndarray, want: int):
+        self._cr = cr
+        self._res = residues  # the batch's buffers: the keys are re-encoded from them
+        self._off = offsets
+        r = Result()
+        ctypes.memmove(ctypes.byref(r), ctypes.byref(cr.r), ctypes.sizeof(Result))
+        hits_ptr = r.hits
+        r.hits = None
+        self.result = BatchResult(r, want, copy=False)
+        self.n_chunks = cr.n_chunks
+        self.materialized = bool(hits_ptr)
+        self.chunks = [cr.chunks[i] for i in range(cr.n_chunks)]
+
+    def expand(self, s_begin: int = 0, s_end: int | None = None, seq_base: int = 0) -> np.ndarray:
+        n = len(self.result.hit_offsets) - 1
+        s_end = n if s_end is None else s_end
+        ho = self.result.hit_offsets
+        out = np.empty(int(ho[s_end] - ho[s_begin]) if n >= 0 else 0, HIT_DTYPE)
+        check(lib().kgx_compact_expand(ctypes.byref(self._cr), self._res.ctypes.data if self._res.size else None,
+                                       self._off.ctypes.data, s_begin, s_end, seq_base,
+                                       out.ctypes.data if len(out) else None), "kgx_compact_expand")
+        return out
+
+
+def _batch_args(residues, offsets, params):
+    if params is None or isinstance(params, dict):
+        params = parse_params(params)
+    residues = np.ascontiguousarray(np.frombuffer(bytes(residues), np.uint8)
+                                    if isinstance(residues, (bytes, bytearray)) else residues, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    return residues, offsets, params
+
+
 class Context:
     """One per host thread (like one KmerGuts per pool thread)."""
 
@@ -430,6 +493,21 @@ class Context:
                                       offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
               "kgx_process_batch")
         return BatchResult(r, want, copy)
+
+    def process_batch_compact(self, residues, offsets, params: Params | dict | None = None,
+                              want: int = WANT_HITS | WANT_CALLS) -> CompactBatch:
+        residues, offsets, params = _batch_args(residues, offsets, params)
+        cr = CompactResult()
+        check(lib().kgx_process_batch_compact(self.handle, ctypes.byref(params),
+                                              residues.ctypes.data if residues.size else None,
+                                              offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(cr)),
+              "kgx_process_batch_compact")
+        return CompactBatch(cr, residues, offsets, want)
+
+    def host_profile(self) -> dict:
+        p = HostProfile()
+        check(lib().kgx_ctx_host_profile(self.handle, ctypes.byref(p)), "kgx_ctx_host_profile")
+        return p.as_dict()
 
     def find_best_calls(self, calls: np.ndarray, call_offsets) -> np.ndarray:
         """find_best_call of every sequence's calls, on the device."""
@@ -677,6 +755,16 @@ class Pool:
                                            offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(r)),
               "kgx_pool_process_batch")
         return BatchResult(r, want, copy)
+
+    def process_batch_compact(self, residues, offsets, params: Params | dict | None = None,
+                              want: int = WANT_HITS | WANT_CALLS) -> CompactBatch:
+        residues, offsets, params = _batch_args(residues, offsets, params)
+        cr = CompactResult()
+        check(lib().kgx_pool_process_batch_compact(self.handle, ctypes.byref(params),
+                                                   residues.ctypes.data if residues.size else None,
+                                                   offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(cr)),
+              "kgx_pool_process_batch_compact")
+        return CompactBatch(cr, residues, offsets, want)
 
     def close(self) -> None:
         if self.handle:

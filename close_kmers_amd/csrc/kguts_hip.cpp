@@ -165,15 +165,23 @@ void KmerGuts::process_aa_batch(std::vector<SeqJob> &jobs)
     for (auto &j : jobs)
         buf += j.seq;
     kgx_params p{min_hits, max_gap, order_constraint, min_weighted_hits};
-    kgx_result r;
-    int rc = kgx_process_batch(ctx_, &p, buf.data(), off.data(), n, want, &r);
+    /* compact hits: each sequence's hit_in_sequence_t are built as its
+     * callbacks replay (no 32-B record per hit for the whole batch) */
+    kgx_compact_result cr;
+    int rc = kgx_process_batch_compact(ctx_, &p, buf.data(), off.data(), n, want, &cr);
     if (rc)
-        throw_last(rc, "kgx_process_batch");
+        throw_last(rc, "kgx_process_batch_compact");
+    const kgx_result &r = cr.r;
+    std::vector<kgx_hit> seq_hits;
     for (uint32_t s = 0; s < n; s++) {
         SeqJob &j = jobs[s];
         if (j.hit_cb) {
-            for (uint64_t i = r.hit_offsets[s]; i < r.hit_offsets[s + 1]; i++) {
-                const kgx_hit &h = r.hits[i];
+            const uint64_t nh = r.hit_offsets[s + 1] - r.hit_offsets[s];
+            seq_hits.resize(nh);
+            if (nh && (rc = kgx_compact_expand(&cr, buf.data(), off.data(), s, s + 1, 0, seq_hits.data())))
+                throw_last(rc, "kgx_compact_expand");
+            for (uint64_t i = 0; i < nh; i++) {
+                const kgx_hit &h = seq_hits[i];
                 sig_kmer_t e;
                 e.which_kmer = h.which_kmer;
                 e.otu_index = h.otu_index;

@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -36,7 +37,9 @@ struct kgx_pool {
     uint32_t job_width = 0;
     /* the concatenated result */
     std::vector<uint64_t> hoff, coff, ooff;
-    std::vector<kgx_hit> hits;
+    std::unique_ptr<kgx_hit[]> hits; /* grow-only (no zeroing of GBs per batch) */
+    uint64_t hits_cap = 0;
+    std::vector<kgx_hit_chunk> chunks; /* kgx_pool_process_batch_compact */
     std::vector<kgx_call> calls;
     std::vector<kgx_otu> otus;
     std::vector<kgx_best_call> best;
@@ -145,87 +148,181 @@ uint32_t kgx_pool_size(const kgx_pool *p) { return p ? (uint32_t)p->ctxs.size() 
 
 kgx_ctx *kgx_pool_ctx(kgx_pool *p, uint32_t i) { return p && i < p->ctxs.size() ? p->ctxs[i] : nullptr; }
 
-int kgx_pool_process_batch(kgx_pool *p, const kgx_params *params, const char *residues,
-                           const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out)
+}  // extern "C"
+
+namespace {
+
+/* phase 1 of a pool batch: the shards, each on its context, all at once,
+ * results left compact in the contexts (kgx_process_batch_compact); then the
+ * concatenation's offsets (hoff/coff/ooff) and the per-shard bases */
+struct PoolRun {
+    uint32_t K = 0;
+    std::vector<uint32_t> cuts;
+    std::vector<kgx_compact_result> part;
+    std::vector<uint64_t> hb, cb, ob;
+    uint64_t nwin = 0;
+};
+
+int pool_shards(kgx_pool *p, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                uint32_t n_seq, uint32_t want, PoolRun &R)
 {
-    if (!p || !out || (!seq_offsets && n_seq))
+    if (!p || (!seq_offsets && n_seq))
         return fail(KGX_EINVAL, "null argument");
     for (uint32_t s = 0; s < n_seq; s++)
         if (seq_offsets[s + 1] < seq_offsets[s])
             return fail(KGX_EINVAL, "seq_offsets not monotone");
-    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)p->ctxs.size(), n_seq));
-    std::vector<uint32_t> cuts(K + 1);
-    int rc = kgx_shard_cuts(seq_offsets, n_seq, K, cuts.data());
+    R.K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)p->ctxs.size(), n_seq));
+    const uint32_t K = R.K;
+    R.cuts.assign(K + 1, 0);
+    int rc = kgx_shard_cuts(seq_offsets, n_seq, K, R.cuts.data());
     if (rc)
         return rc;
-
-    /* phase 1: every shard on its own context, all at once.  A shard's
-     * offsets stay absolute: kgx_process_batch reads residues from
+    /* A shard's offsets stay absolute: kgx_process_batch reads residues from
      * seq_offsets[first] on. */
-    std::vector<kgx_result> part(K);
+    R.part.assign(K, kgx_compact_result{});
     std::vector<int> rcs(K, KGX_OK);
     std::vector<std::string> errs(K);
     p->run(K, [&](uint32_t i) {
-        rcs[i] = kgx_process_batch(p->ctxs[i], params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i],
-                                   want, &part[i]);
+        rcs[i] = kgx_process_batch_compact(p->ctxs[i], params, residues, seq_offsets + R.cuts[i],
+                                           R.cuts[i + 1] - R.cuts[i], want, &R.part[i]);
         if (rcs[i])
             errs[i] = kgx_last_error();
     });
     for (uint32_t i = 0; i < K; i++)
         if (rcs[i])
             return fail(rcs[i], "pool shard " + std::to_string(i) + ": " + errs[i]);
-
-    /* phase 2: offsets of the concatenation, then every shard copies its part */
-    const bool need_hits = (want & KGX_WANT_HITS) != 0;
-    const bool want_best = (want & KGX_WANT_BEST) != 0;
-    std::vector<uint64_t> hb(K + 1, 0), cb(K + 1, 0), ob(K + 1, 0);
-    uint64_t nwin = 0;
+    R.hb.assign(K + 1, 0);
+    R.cb.assign(K + 1, 0);
+    R.ob.assign(K + 1, 0);
+    R.nwin = 0;
     for (uint32_t i = 0; i < K; i++) {
-        const uint32_t n = cuts[i + 1] - cuts[i];
-        hb[i + 1] = hb[i] + part[i].hit_offsets[n];
-        cb[i + 1] = cb[i] + part[i].call_offsets[n];
-        ob[i + 1] = ob[i] + part[i].otu_offsets[n];
-        nwin += part[i].n_windows;
+        const uint32_t n = R.cuts[i + 1] - R.cuts[i];
+        const kgx_result &r = R.part[i].r;
+        R.hb[i + 1] = R.hb[i] + r.hit_offsets[n];
+        R.cb[i + 1] = R.cb[i] + r.call_offsets[n];
+        R.ob[i + 1] = R.ob[i] + r.otu_offsets[n];
+        R.nwin += r.n_windows;
     }
     p->hoff.resize((size_t)n_seq + 1);
     p->coff.resize((size_t)n_seq + 1);
     p->ooff.resize((size_t)n_seq + 1);
-    p->hits.resize(need_hits ? hb[K] : 0);
-    p->calls.resize(cb[K]);
-    p->otus.resize(ob[K]);
-    p->best.resize(want_best ? n_seq : 0);
     p->hoff[0] = p->coff[0] = p->ooff[0] = 0;
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    p->calls.resize(R.cb[K]);
+    p->otus.resize(R.ob[K]);
+    p->best.resize(want_best ? n_seq : 0);
+    /* offsets, calls, OTUs and best calls into place (small: no hit records) */
     p->run(K, [&](uint32_t i) {
-        const kgx_result &r = part[i];
-        const uint32_t s0 = cuts[i], n = cuts[i + 1] - cuts[i];
+        const kgx_result &r = R.part[i].r;
+        const uint32_t s0 = R.cuts[i], n = R.cuts[i + 1] - R.cuts[i];
         for (uint32_t s = 1; s <= n; s++) {
-            p->hoff[s0 + s] = hb[i] + r.hit_offsets[s];
-            p->coff[s0 + s] = cb[i] + r.call_offsets[s];
-            p->ooff[s0 + s] = ob[i] + r.otu_offsets[s];
+            p->hoff[s0 + s] = R.hb[i] + r.hit_offsets[s];
+            p->coff[s0 + s] = R.cb[i] + r.call_offsets[s];
+            p->ooff[s0 + s] = R.ob[i] + r.otu_offsets[s];
         }
-        const uint64_t nh = hb[i + 1] - hb[i];
-        if (need_hits && nh) {
-            kgx_hit *dst = p->hits.data() + hb[i];
-            std::memcpy(dst, r.hits, nh * sizeof(kgx_hit));
-            for (uint64_t h = 0; h < nh; h++)
-                dst[h].seq += s0; /* batch index, not shard index */
-        }
-        if (cb[i + 1] > cb[i])
-            std::memcpy(p->calls.data() + cb[i], r.calls, (cb[i + 1] - cb[i]) * sizeof(kgx_call));
-        if (ob[i + 1] > ob[i])
-            std::memcpy(p->otus.data() + ob[i], r.otus, (ob[i + 1] - ob[i]) * sizeof(kgx_otu));
+        if (R.cb[i + 1] > R.cb[i])
+            std::memcpy(p->calls.data() + R.cb[i], r.calls, (R.cb[i + 1] - R.cb[i]) * sizeof(kgx_call));
+        if (R.ob[i + 1] > R.ob[i])
+            std::memcpy(p->otus.data() + R.ob[i], r.otus, (R.ob[i + 1] - R.ob[i]) * sizeof(kgx_otu));
         if (want_best && n)
             std::memcpy(p->best.data() + s0, r.best, n * sizeof(kgx_best_call));
     });
+    return KGX_OK;
+}
+
+void pool_fill(kgx_pool *p, const PoolRun &R, uint32_t n_seq, uint32_t want, kgx_result *out)
+{
     out->n_seq = n_seq;
     out->hit_offsets = p->hoff.data();
-    out->hits = need_hits ? p->hits.data() : nullptr;
+    out->hits = nullptr;
     out->call_offsets = p->coff.data();
     out->calls = p->calls.data();
     out->otu_offsets = p->ooff.data();
     out->otus = p->otus.data();
-    out->n_windows = nwin;
-    out->best = want_best ? p->best.data() : nullptr;
+    out->n_windows = R.nwin;
+    out->best = (want & KGX_WANT_BEST) ? p->best.data() : nullptr;
+}
+
+/* every shard's hits as kgx_hit, each record written once, straight into its
+ * place in the concatenation (kgx_hit.seq = batch index) */
+int pool_expand(kgx_pool *p, const PoolRun &R, const char *residues, const uint64_t *seq_offsets)
+{
+    const uint64_t nh = R.hb[R.K];
+    if (nh > p->hits_cap) {
+        p->hits.reset(new kgx_hit[nh + nh / 4]); /* grow-only, not initialised */
+        p->hits_cap = nh + nh / 4;
+    }
+    std::vector<int> rcs(R.K, KGX_OK);
+    std::vector<std::string> errs(R.K);
+    p->run(R.K, [&](uint32_t i) {
+        const uint32_t s0 = R.cuts[i], n = R.cuts[i + 1] - R.cuts[i];
+        rcs[i] = kgx_compact_expand(&R.part[i], residues, seq_offsets + s0, 0, n, s0, p->hits.get() + R.hb[i]);
+        if (rcs[i])
+            errs[i] = kgx_last_error();
+    });
+    for (uint32_t i = 0; i < R.K; i++)
+        if (rcs[i])
+            return fail(rcs[i], "pool shard " + std::to_string(i) + " expansion: " + errs[i]);
+    return KGX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kgx_pool_process_batch(kgx_pool *p, const kgx_params *params, const char *residues,
+                           const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    if (!p || !out)
+        return fail(KGX_EINVAL, "null argument");
+    PoolRun R;
+    int rc = pool_shards(p, params, residues, seq_offsets, n_seq, want, R);
+    if (rc)
+        return rc;
+    if ((want & KGX_WANT_HITS) && (rc = pool_expand(p, R, residues, seq_offsets)))
+        return rc;
+    pool_fill(p, R, n_seq, want, out);
+    out->hits = (want & KGX_WANT_HITS) ? p->hits.get() : nullptr;
+    return KGX_OK;
+}
+
+int kgx_pool_process_batch_compact(kgx_pool *p, const kgx_params *params, const char *residues,
+                                   const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                                   kgx_compact_result *out)
+{
+    if (!p || !out)
+        return fail(KGX_EINVAL, "null argument");
+    PoolRun R;
+    int rc = pool_shards(p, params, residues, seq_offsets, n_seq, want, R);
+    if (rc)
+        return rc;
+    pool_fill(p, R, n_seq, want, &out->r);
+    out->n_chunks = 0;
+    out->chunks = nullptr;
+    if (!(want & KGX_WANT_HITS))
+        return KGX_OK;
+    bool all_compact = true;
+    for (uint32_t i = 0; i < R.K; i++)
+        if (R.part[i].n_chunks == 0 && R.hb[i + 1] > R.hb[i])
+            all_compact = false;
+    if (!all_compact) {
+        if ((rc = pool_expand(p, R, residues, seq_offsets)))
+            return rc;
+        out->r.hits = p->hits.get();
+        return KGX_OK;
+    }
+    /* every shard's chunks, renumbered into the batch: no record moves */
+    p->chunks.clear();
+    for (uint32_t i = 0; i < R.K; i++)
+        for (uint32_t k = 0; k < R.part[i].n_chunks; k++) {
+            kgx_hit_chunk ch = R.part[i].chunks[k];
+            ch.seq_begin += R.cuts[i];
+            ch.seq_end += R.cuts[i];
+            ch.hit_begin += R.hb[i];
+            p->chunks.push_back(ch);
+        }
+    out->n_chunks = (uint32_t)p->chunks.size();
+    out->chunks = p->chunks.data();
     return KGX_OK;
 }
 

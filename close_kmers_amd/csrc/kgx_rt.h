@@ -394,6 +394,30 @@ struct kgx_ctx {
     kgx::PinnedVec<kgx_call> h_calls_region;
     kgx::PinnedVec<kgx_otu> h_otus_region;
     int counts_first = 1; /* chunk k's bulk D2H waits for chunk k+1's counts (option "counts_first") */
+    /* compact results (kgx_process_batch_compact): the call leaves the hits as
+     * records + mask; compact_segs say where each chunk's landed (element
+     * offsets into h_hits12 / h_hits16 and h_mask, resolved to pointers once
+     * the pinned arrays stop growing) */
+    int compact_out = 0;
+    struct CompactSeg {
+        uint32_t s0, s1, words;
+        uint64_t hit_begin, rec_at, mask_at;
+    };
+    std::vector<CompactSeg> compact_segs;
+    std::vector<kgx_hit_chunk> compact_chunks;
+    /* option "host_profile": per-chunk timing events and the last call's profile */
+    int host_profile = 0;
+    std::vector<hipEvent_t> prof_ev; /* 4 per chunk: H2D start, H2D end, device end, gathered */
+    std::vector<hipEvent_t> prof_done; /* per chunk: bulk copy done (timing events on the copy stream) */
+    kgx_host_profile last_profile{};
 };
+
+namespace kgx {
+/* one chunk of compact records -> kgx_hit for sequences [a, b) of it:
+ * out[j - out_base] for CSR hit j (hoff: the batch's hit offsets);
+ * kgx_hit.seq = s + seq_base; nt = streaming stores */
+int expand_chunk(const kgx_hit_chunk &ch, const uint64_t *hoff, const char *residues, const uint64_t *seq_offsets,
+                 uint32_t a, uint32_t b, kgx_hit *out, uint64_t out_base, uint32_t seq_base, bool nt);
+}  // namespace kgx
 
 #endif

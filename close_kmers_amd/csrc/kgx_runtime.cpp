@@ -836,6 +836,10 @@ int kgx_ctx_destroy(kgx_ctx *c)
         (void)hipEventDestroy(e);
     for (hipEvent_t e : c->chunk_h2d)
         (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->prof_ev)
+        (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->prof_done)
+        (void)hipEventDestroy(e);
     if (c->copy_stream) {
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
@@ -987,6 +991,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "small_wave must be 0 or 1");
         c->small_wave = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_profile") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_profile must be 0 or 1");
+        c->host_profile = (int)value;
         return KGX_OK;
     }
     if (n == "host_chunks") {
@@ -1490,25 +1500,32 @@ inline uint64_t window_key(const uint8_t *p)
     return (uint64_t)ka * 160000u + kb;
 }
 
+}  // namespace
+
+extern "C++" {
+namespace kgx {
+
 /* Sequences [a, b) of a compact chunk: table records (dense, CSR order) +
  * the chunk's hit mask -> kgx_hit, position = the hit's mask bit minus the
  * sequence's first window (what gather_kernel computes on the device).
- * R12: 12-byte records without the key (gather_kernel's hits12 form), the key
- * re-encoded from the window's residues; else the 16-byte table records. */
-int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_offsets, uint32_t a, uint32_t b,
-                uint64_t mbase, int64_t rec_delta)
+ * 3-word records: the 12-byte form without the key (gather_kernel's hits12),
+ * the key re-encoded from the window's residues; 4 words: the 16-byte table
+ * records. */
+
+template <bool R12>
+static int expand_chunk_t(const kgx_hit_chunk &ch, const uint64_t *hoff, const char *residues,
+                          const uint64_t *seq_offsets, uint32_t a, uint32_t b, kgx_hit *out, uint64_t out_base,
+                          uint32_t seq_base, bool nt)
 {
-    const uint4 *rec16 = R12 ? nullptr : c->h_hits16.data() + rec_delta; /* record of output hit j */
-    const uint32_t *rec12 = R12 ? c->h_hits12.data() + 3 * rec_delta : nullptr;
-    const uint64_t *mask = c->h_mask.data() + mbase;
-    kgx_hit *out = c->h_hits.data();
-    const bool nt = c->host_nt != 0;
+    const uint64_t *mask = ch.mask;
     for (uint32_t s = a; s < b; s++) {
-        uint64_t j = c->h_hoff[s];
-        const uint64_t j1 = c->h_hoff[s + 1];
+        uint64_t j = hoff[s];
+        const uint64_t j1 = hoff[s + 1];
         if (j == j1)
             continue;
-        const uint64_t w0 = c->h_wstart[s], w1 = w0 + windows_of(seq_offsets[s + 1] - seq_offsets[s]);
+        const uint64_t w0 = ch.window_start[s - ch.seq_begin], w1 = w0 + windows_of(seq_offsets[s + 1] - seq_offsets[s]);
+        if (w1 == w0)
+            return fail(KGX_EDEVICE, "compact hits: hits for a sequence without windows (" + std::to_string(s) + ")");
         const uint8_t *seq = reinterpret_cast<const uint8_t *>(residues + seq_offsets[s]);
         for (uint64_t g = w0 >> 6; g <= (w1 - 1) >> 6; g++) {
             uint64_t bits = mask[g];
@@ -1520,18 +1537,17 @@ int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_
                 return fail(KGX_EDEVICE, "compact hits: more mask bits than hits for sequence " + std::to_string(s));
             for (; bits; bits &= bits - 1, j++) {
                 const uint32_t pos = (uint32_t)(64 * g + (uint64_t)__builtin_ctzll(bits) - w0);
+                const uint32_t *r = ch.records + (R12 ? 3 : 4) * (j - ch.hit_begin);
                 packed_bucket pb;
                 uint32_t flags;
                 if (R12) {
-                    const uint32_t *r = rec12 + 3 * j;
                     pb.lo = window_key(seq + pos) | (uint64_t)r[2] << 35;
                     pb.hi = (uint64_t)r[1] << 32 | r[0];
                     flags = (r[1] >> 28) & 7u;
                 } else {
-                    const uint4 h = rec16[j];
-                    pb.lo = (uint64_t)h.y << 32 | h.x;
-                    pb.hi = (uint64_t)h.w << 32 | h.z;
-                    flags = (h.w >> 28) & 7u;
+                    pb.lo = (uint64_t)r[1] << 32 | r[0];
+                    pb.hi = (uint64_t)r[3] << 32 | r[2];
+                    flags = (r[3] >> 28) & 7u;
                 }
                 const kgx_sig_kmer e = unpack_bucket(pb);
                 kgx_hit o;
@@ -1542,25 +1558,59 @@ int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_
                 o.function_index = e.function_index;
                 o.function_wt = e.function_wt;
                 o.pos = pos;
-                o.seq = s;
+                o.seq = s + seq_base;
+                kgx_hit *dst = out + (j - out_base);
                 if (nt) {
                     /* streaming stores: the 32-B records are written once and
                      * not read back here (no read-for-ownership of the lines) */
                     typedef long long v2i __attribute__((vector_size(16)));
                     v2i q[2];
                     std::memcpy(q, &o, sizeof(o));
-                    __builtin_nontemporal_store(q[0], reinterpret_cast<v2i *>(out + j));
-                    __builtin_nontemporal_store(q[1], reinterpret_cast<v2i *>(out + j) + 1);
+                    __builtin_nontemporal_store(q[0], reinterpret_cast<v2i *>(dst));
+                    __builtin_nontemporal_store(q[1], reinterpret_cast<v2i *>(dst) + 1);
                 } else {
-                    out[j] = o;
+                    *dst = o;
                 }
             }
         }
         if (j != j1)
             return fail(KGX_EDEVICE, "compact hits: mask and hit count disagree for sequence " + std::to_string(s));
     }
-    __builtin_ia32_sfence(); /* the streaming stores are visible before the task reports done */
+    if (nt)
+        __builtin_ia32_sfence(); /* the streaming stores are visible before the task reports done */
     return KGX_OK;
+}
+
+int expand_chunk(const kgx_hit_chunk &ch, const uint64_t *hoff, const char *residues, const uint64_t *seq_offsets,
+                 uint32_t a, uint32_t b, kgx_hit *out, uint64_t out_base, uint32_t seq_base, bool nt)
+{
+    if (ch.record_words == 3)
+        return expand_chunk_t<true>(ch, hoff, residues, seq_offsets, a, b, out, out_base, seq_base, nt);
+    if (ch.record_words == 4)
+        return expand_chunk_t<false>(ch, hoff, residues, seq_offsets, a, b, out, out_base, seq_base, nt);
+    return fail(KGX_EINVAL, "compact hits: record_words must be 3 or 4");
+}
+
+}  // namespace kgx
+}  // extern "C++"
+
+namespace {
+
+/* the context's own expansion (into h_hits, CSR numbering): R12 records of
+ * hit j at h_hits12 + 3 (j + rec_delta), else h_hits16[j + rec_delta]; the
+ * chunk's mask from h_mask + mbase */
+int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_offsets, uint32_t a, uint32_t b,
+                uint64_t mbase, int64_t rec_delta)
+{
+    kgx_hit_chunk ch{};
+    ch.seq_begin = 0;
+    ch.record_words = R12 ? 3 : 4;
+    ch.hit_begin = 0;
+    ch.records = R12 ? c->h_hits12.data() + 3 * rec_delta
+                     : reinterpret_cast<const uint32_t *>(c->h_hits16.data() + rec_delta);
+    ch.mask = c->h_mask.data() + mbase;
+    ch.window_start = c->h_wstart.data();
+    return expand_chunk(ch, c->h_hoff.data(), residues, seq_offsets, a, b, c->h_hits.data(), 0, 0, c->host_nt != 0);
 }
 
 
@@ -1628,7 +1678,28 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     HIP_TRY(c->h_calls_region.resize(rb_c[K]));
     HIP_TRY(c->h_otus_region.resize(rb_o[K]));
     HIP_TRY(c->h_counts.resize(3 * (uint64_t)n_seq));
-    HIP_TRY(c->h_hits.resize(rb_h[K])); /* room for every region's records; trimmed below */
+    const bool expand = !c->compact_out;
+    if (expand)
+        HIP_TRY(c->h_hits.resize(rb_h[K])); /* room for every region's records; trimmed below */
+    /* host_profile: timing events per chunk (4 on the contexts' streams, 1 on the copy stream) */
+    const bool prof = c->host_profile != 0;
+    if (prof) {
+        auto grow = [](std::vector<hipEvent_t> &v, size_t n) -> hipError_t {
+            while (v.size() < n) {
+                hipEvent_t e;
+                hipError_t err = hipEventCreate(&e);
+                if (err != hipSuccess)
+                    return err;
+                v.push_back(e);
+            }
+            return hipSuccess;
+        };
+        HIP_TRY(grow(c->prof_ev, 4 * (size_t)K));
+        HIP_TRY(grow(c->prof_done, K));
+    }
+    double stage_ms = 0;
+    std::atomic<uint64_t> expand_ns{0};
+    c->compact_segs.clear();
     HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
     c->h_hoff.assign(n_seq + 1, 0);
     c->h_coff.assign(n_seq + 1, 0);
@@ -1667,13 +1738,19 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     auto enqueue = [&](kgx_ctx *x, uint32_t k) -> int {
         const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
         const uint64_t n_res = x->h_res.size();
+        if (prof)
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k], x->stream));
         int rc = stage_upload(x);
         if (rc)
             return rc;
         HIP_TRY(hipEventRecord(c->chunk_h2d[k], x->stream));
+        if (prof)
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 1], x->stream));
         if ((rc = kgx_run_device(x, params, x->residues.as<uint8_t>(), x->offsets.as<uint64_t>(), n, n_res, want,
                                  nullptr)))
             return rc;
+        if (prof)
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 2], x->stream));
         const uint64_t rn = std::max<uint64_t>(n_res, 1); /* dense buffers: at most one record per residue */
         HIP_TRY(x->dense_hoff.reserve((n + 1) * sizeof(uint64_t)));
         HIP_TRY(x->dense_coff.reserve((n + 1) * sizeof(uint64_t)));
@@ -1721,6 +1798,8 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
                                    x->stream));
         }
         HIP_TRY(hipEventRecord(c->chunk_gathered[k], x->stream));
+        if (prof)
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 3], x->stream));
         /* the bulk copy, on the copy stream */
         HIP_TRY(hipStreamWaitEvent(cs, c->chunk_gathered[k], 0));
         void *d = nullptr;
@@ -1754,6 +1833,8 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
             HIP_TRY(launch_copy_to_host(d, x->dense_best.p, n * sizeof(kgx_best_call), cb, cs));
         }
         HIP_TRY(hipEventRecord(c->chunk_done[k], cs));
+        if (prof)
+            HIP_TRY(hipEventRecord(c->prof_done[k], cs));
         return KGX_OK;
     };
 
@@ -1790,7 +1871,10 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
             if (no)
                 std::memmove(c->h_otus_region.data() + obase, c->h_otus_region.data() + rb_o[k],
                              no * sizeof(kgx_otu));
-            if (nh) {
+            if (nh && !expand) {
+                /* compact results: the records stay where they landed */
+                c->compact_segs.push_back({s0, s0 + n, r12 ? 3u : 4u, hbase, rb_h[k], mb[k]});
+            } else if (nh) {
                 const int64_t delta = (int64_t)rb_h[k] - (int64_t)hbase;
                 const uint32_t P = c->pool->size();
                 uint32_t a = s0;
@@ -1803,9 +1887,11 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
                         b = std::max(b, a + 1);
                     }
                     const uint64_t m0 = mb[k];
-                    c->pool->submit([c, r12, residues, seq_offsets, a, b, m0, delta, k, timing, now, ms]() -> int {
+                    c->pool->submit([c, r12, residues, seq_offsets, a, b, m0, delta, k, timing, now, ms,
+                                     &expand_ns]() -> int {
                         const auto q0 = now();
                         const int erc = expand_hits(r12, c, residues, seq_offsets, a, b, m0, delta);
+                        expand_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now() - q0).count();
                         if (timing)
                             std::fprintf(stderr, "[kgx] streamed chunk %u expand [%u,%u): %.3f ms\n", k, a, b,
                                          ms(q0, now()));
@@ -1830,7 +1916,10 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         kgx_ctx *x = xs[k & 1];
         if (k >= 2)
             HIP_TRY(hipEventSynchronize(c->chunk_h2d[k - 2])); /* x's staging buffer is free */
-        if ((rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp)) || (rc = enqueue(x, k)))
+        const auto ts = now();
+        rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp);
+        stage_ms += ms(ts, now());
+        if (rc || (rc = enqueue(x, k)))
             break;
         /* collect what has landed meanwhile */
         while (!rc && next < k && hipEventQuery(c->chunk_done[next]) == hipSuccess)
@@ -1855,15 +1944,41 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     c->rate_otus = std::max(0.01, max_ro * 1.25);
     if (!fits)
         return STREAM_OVERFLOW;
-    HIP_TRY(c->h_hits.resize(hbase));
+    if (expand)
+        HIP_TRY(c->h_hits.resize(hbase));
     c->have_hits = false;
     t->have_hits = false;
     if (timing)
         std::fprintf(stderr, "[kgx] streamed batch: %u chunks, %.3f ms\n", K, ms(T0, now()));
+    if (prof) {
+        kgx_host_profile &P = c->last_profile;
+        P = kgx_host_profile{};
+        P.chunks = K;
+        P.streamed = 1;
+        P.wall_ms = ms(T0, now());
+        P.stage_ms = stage_ms;
+        P.expand_ms = (double)expand_ns.load() * 1e-6;
+        P.h2d_bytes = seq_offsets[n_seq] - seq_offsets[0] + (uint64_t)(n_seq + K) * sizeof(uint64_t);
+        for (uint32_t k = 0; k < K; k++) {
+            float a = 0, b = 0, g = 0, d = 0;
+            HIP_TRY(hipEventElapsedTime(&a, c->prof_ev[4 * k], c->prof_ev[4 * k + 1]));
+            HIP_TRY(hipEventElapsedTime(&b, c->prof_ev[4 * k + 1], c->prof_ev[4 * k + 2]));
+            HIP_TRY(hipEventElapsedTime(&g, c->prof_ev[4 * k + 2], c->prof_ev[4 * k + 3]));
+            HIP_TRY(hipEventElapsedTime(&d, c->prof_ev[4 * k + 3], c->prof_done[k]));
+            P.h2d_ms += a;
+            P.device_ms += b;
+            P.gather_ms += g;
+            P.d2h_ms += d;
+        }
+        const uint64_t recb = r12 ? 12 : 16;
+        P.d2h_bytes = hbase * recb + cbase * sizeof(kgx_call) +
+                      obase * sizeof(kgx_otu) + mb[K] * sizeof(uint64_t) + 3ull * n_seq * sizeof(uint32_t) +
+                      (want_best ? (uint64_t)n_seq * sizeof(kgx_best_call) : 0);
+    }
     out->best = want_best ? c->h_best.data() : nullptr;
     out->n_seq = n_seq;
     out->hit_offsets = c->h_hoff.data();
-    out->hits = c->h_hits.data();
+    out->hits = expand ? c->h_hits.data() : nullptr;
     out->call_offsets = c->h_coff.data();
     out->calls = c->h_calls_region.data();
     out->otu_offsets = c->h_ooff.data();
@@ -1964,6 +2079,7 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
             HIP_TRY(c->h_mask.resize(0));
             HIP_TRY(c->h_hits.resize(0));
             HIP_TRY(c->h_best.resize(want_best ? n_seq : 0));
+            c->compact_segs.clear();
             c->stream_fallbacks++;
         }
         c->h_wstart.resize(n_seq);
@@ -2061,7 +2177,8 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
             HIP_TRY(c->h_hits16.resize(hrec + nh));
             HIP_TRY(c->h_mask.resize(mbase + nwords));
         }
-        HIP_TRY(c->h_hits.resize(hrec + nh));
+        if (!(compact && c->compact_out))
+            HIP_TRY(c->h_hits.resize(hrec + nh));
         HIP_TRY(c->h_calls.resize(cbase + nc));
         HIP_TRY(c->h_otus.resize(obase + no));
         /* x's dense buffers still feed chunk k-2's bulk copy */
@@ -2117,7 +2234,10 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
             (want_best && (rc = copy_out(c->h_best, s0, x->dense_best.p, n))))
             break;
         HIP_TRY(hipEventRecord(c->chunk_done[k], cs));
-        if (compact && nh) {
+        if (compact && nh && c->compact_out) {
+            /* compact results: the records stay where they land */
+            c->compact_segs.push_back({s0, s0 + n, 4u, hbase, hrec, mbase});
+        } else if (compact && nh) {
             /* host threads expand this chunk once its bytes have landed, in
              * hit-balanced sequence ranges, while the next chunks stream */
             hipEvent_t ev = c->chunk_done[k];
@@ -2407,6 +2527,98 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     rc = kgx_device_batch_collect(c, want, out);
     tm.mark("collect");
     return rc;
+}
+
+int kgx_process_batch_compact(kgx_ctx *c, const kgx_params *params, const char *residues,
+                              const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_compact_result *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    c->compact_segs.clear();
+    c->compact_chunks.clear();
+    c->compact_out = 1;
+    const int rc = kgx_process_batch(c, params, residues, seq_offsets, n_seq, want, &out->r);
+    c->compact_out = 0;
+    out->n_chunks = 0;
+    out->chunks = nullptr;
+    if (rc) {
+        c->compact_segs.clear();
+        return rc;
+    }
+    if (!c->compact_segs.empty()) {
+        /* the pinned arrays no longer move: offsets -> pointers */
+        for (const auto &g : c->compact_segs) {
+            kgx_hit_chunk ch{};
+            ch.seq_begin = g.s0;
+            ch.seq_end = g.s1;
+            ch.record_words = g.words;
+            ch.hit_begin = g.hit_begin;
+            ch.records = g.words == 3 ? c->h_hits12.data() + 3 * g.rec_at
+                                      : reinterpret_cast<const uint32_t *>(c->h_hits16.data() + g.rec_at);
+            ch.mask = c->h_mask.data() + g.mask_at;
+            ch.window_start = c->h_wstart.data() + g.s0;
+            c->compact_chunks.push_back(ch);
+        }
+        out->r.hits = nullptr;
+        out->n_chunks = (uint32_t)c->compact_chunks.size();
+        out->chunks = c->compact_chunks.data();
+    }
+    return KGX_OK;
+}
+
+int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets,
+                       uint32_t s_begin, uint32_t s_end, uint32_t seq_base, kgx_hit *out)
+{
+    if (!r || s_begin > s_end || s_end > r->r.n_seq || !r->r.hit_offsets)
+        return fail(KGX_EINVAL, "bad compact range");
+    const uint64_t *hoff = r->r.hit_offsets;
+    const uint64_t j0 = hoff[s_begin], j1 = hoff[s_end];
+    if (j0 == j1)
+        return KGX_OK;
+    if (!out)
+        return fail(KGX_EINVAL, "null output");
+    if (r->n_chunks == 0) {
+        if (!r->r.hits)
+            return fail(KGX_EINVAL, "the result holds no hits (want without KGX_WANT_HITS)");
+        std::memcpy(out, r->r.hits + j0, (j1 - j0) * sizeof(kgx_hit));
+        if (seq_base)
+            for (uint64_t j = 0; j < j1 - j0; j++)
+                out[j].seq += seq_base;
+        return KGX_OK;
+    }
+    if (!residues || !seq_offsets)
+        return fail(KGX_EINVAL, "compact hits need the batch's residues and offsets");
+    /* the chunks are in sequence order: the first one that ends past s_begin */
+    const kgx_hit_chunk *ch = r->chunks, *end = r->chunks + r->n_chunks;
+    ch = std::upper_bound(ch, end, s_begin, [](uint32_t s, const kgx_hit_chunk &x) { return s < x.seq_end; });
+    uint32_t s = s_begin;
+    for (; ch != end && s < s_end; ch++) {
+        if (ch->seq_begin > s) {
+            /* sequences between chunks have no hits (a chunk without hits has no records) */
+            for (; s < std::min(ch->seq_begin, s_end); s++)
+                if (hoff[s + 1] != hoff[s])
+                    return fail(KGX_EINVAL, "compact hits: a sequence with hits outside every chunk");
+            if (s >= s_end)
+                break;
+        }
+        const uint32_t b = std::min(ch->seq_end, s_end);
+        const int rc = expand_chunk(*ch, hoff, residues, seq_offsets, s, b, out, j0, seq_base, false);
+        if (rc)
+            return rc;
+        s = b;
+    }
+    for (; s < s_end; s++)
+        if (hoff[s + 1] != hoff[s])
+            return fail(KGX_EINVAL, "compact hits: a sequence with hits outside every chunk");
+    return KGX_OK;
+}
+
+int kgx_ctx_host_profile(kgx_ctx *c, kgx_host_profile *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    *out = c->last_profile;
+    return KGX_OK;
 }
 
 /* the current device batch's results -> host CSR (gather on the device, OTU

@@ -348,6 +348,74 @@ int kgx_process_batch(kgx_ctx *ctx, const kgx_params *params, const char *residu
                       const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
                       kgx_result *out);
 
+/* ---- compact host results ----------------------------------------------
+ * What crosses PCIe, handed over without building 32-byte kgx_hit records
+ * (239 MB per 30M-residue C2 batch): per hit a record of the matched table
+ * bucket without its key, plus one hit-mask bit per window.  A hit's window
+ * -- hence its sequence and position -- is its mask bit, and its key is the
+ * window's 8-mer, re-encoded from the caller's residues.  The hits come in
+ * chunks of consecutive sequences:
+ *   records        record_words (3 or 4) 32-bit words per hit, CSR order:
+ *                  hit j of the batch (hit_offsets numbering) is at
+ *                  records + record_words * (j - hit_begin); the words are
+ *                  the PACKED16 bucket minus the key bits and
+ *                  are opaque: kgx_compact_expand decodes them
+ *   mask           chunk window w hit <=> bit w % 64 of mask[w / 64]
+ *   window_start   sequence s's first chunk window is window_start[s -
+ *                  seq_begin]; it owns max(0, len - 8) windows
+ * hit_in_sequence_t (kguts.h:228-233) for any hit is thus built on the fly,
+ * which is how the KmerGuts facade replays hit_cb (kguts.cc:814-815). */
+typedef struct kgx_hit_chunk {
+    uint32_t seq_begin, seq_end; /* the chunk's sequences [seq_begin, seq_end) */
+    uint32_t record_words;
+    uint32_t reserved;
+    uint64_t hit_begin;
+    const uint32_t *records;
+    const uint64_t *mask;
+    const uint64_t *window_start;
+} kgx_hit_chunk;
+typedef struct kgx_compact_result {
+    /* offsets, calls, OTUs, best calls and n_windows as kgx_result; r.hits is
+     * NULL when the hits are compact (n_chunks > 0), else (a batch that took
+     * a path without compact records: small, one-pass or AOS24) the kgx_hit
+     * records themselves, with n_chunks 0 */
+    kgx_result r;
+    uint32_t n_chunks;
+    const kgx_hit_chunk *chunks;
+} kgx_compact_result;
+/* kgx_process_batch with compact hits: the same offsets, calls, OTUs and best
+ * calls; the hits stay as the compact records (no kgx_hit expansion on the
+ * host).  Views owned by ctx, valid until its next call. */
+int kgx_process_batch_compact(kgx_ctx *ctx, const kgx_params *params, const char *residues,
+                              const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                              kgx_compact_result *out);
+/* kgx_hit records of sequences [s_begin, s_end) of a compact result into out
+ * (out[0] = the first hit of s_begin; hit_offsets[s_end] - hit_offsets[s_begin]
+ * records), kgx_hit.seq = batch index + seq_base.  residues / seq_offsets are
+ * the batch's, as passed to the call that produced r.  Thread-safe (reads r
+ * only): ranges may be expanded on several threads at once. */
+int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets,
+                       uint32_t s_begin, uint32_t s_end, uint32_t seq_base, kgx_hit *out);
+
+/* Host-side profile of the context's last kgx_process_batch* call with option
+ * "host_profile" 1 (HIP events per chunk; otherwise zeros).  Device stages are
+ * sums over the batch's chunks of HIP-event intervals; host stages are wall
+ * times on the host (expand_ms summed over the expansion threads). */
+typedef struct kgx_host_profile {
+    uint32_t chunks;
+    uint32_t streamed;   /* 1: the streamed schedule (no host round trip per chunk) */
+    double wall_ms;      /* the whole call */
+    double stage_ms;     /* caller residues -> pinned staging (host copy) */
+    double h2d_ms;       /* staged residues -> HBM */
+    double device_ms;    /* plan + probe + score */
+    double gather_ms;    /* count scan + gather into dense buffers */
+    double d2h_ms;       /* the bulk copy to pinned host memory (from gather end, incl. queueing) */
+    double expand_ms;    /* kgx_hit records built on host threads (0 in compact mode) */
+    uint64_t h2d_bytes;
+    uint64_t d2h_bytes;
+} kgx_host_profile;
+int kgx_ctx_host_profile(kgx_ctx *ctx, kgx_host_profile *out);
+
 /* Device-buffer batch: same computation on residues / offsets already in HBM
  * (NUL-free sequences), enqueued on the context's stream without host
  * synchronisation.  The results stay in HBM (kgx_device_result).
@@ -398,6 +466,14 @@ kgx_ctx *kgx_pool_ctx(kgx_pool *pool, uint32_t i);
  * by the pool and valid until its next call. */
 int kgx_pool_process_batch(kgx_pool *pool, const kgx_params *params, const char *residues,
                            const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out);
+/* The same with compact hits (kgx_process_batch_compact): every shard's
+ * chunks, renumbered into the whole batch (seq_begin / seq_end / hit_begin),
+ * pointing into the shard contexts' pinned buffers -- no host copy of any
+ * hit.  When some shard's hits did not come back compact, every shard's hits
+ * are expanded into one kgx_hit array instead (r.hits, n_chunks 0). */
+int kgx_pool_process_batch_compact(kgx_pool *pool, const kgx_params *params, const char *residues,
+                                   const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                                   kgx_compact_result *out);
 /* cut points of n_shards contiguous residue-balanced shards: shard i is
  * sequences [cuts[i], cuts[i+1]), cuts[0] = 0, cuts[n_shards] = n_seq; cut i
  * is the first sequence starting at or after residue (total * i / n_shards)

@@ -1,5 +1,6 @@
 """Parity at BASELINE.json's full C2 size (100k x 300 aa vs the 1B-entry
-image, 85.4 GB file format / 57 GB packed in HBM) through properties that do
+image bench.py measures: exactly 1e9 distinct keys, 85.4 GB file format /
+57 GB packed in HBM) through properties that do
 not need a full CPU run: idempotence, device path == host-buffer path ==
 24-byte layout, and every 100th sequence against the oracle on a host copy
 of the same image."""
@@ -28,11 +29,94 @@ def _same(a, b):
     assert np.array_equal(a["calls"].view(np.uint8), b["calls"].view(np.uint8))
 
 
-def test_c2_full_scale(gpu, oracle_lib):
-    L = gpu.lib()
+@pytest.fixture(scope="module")
+def bench_image(gpu):
+    """The bench's exact image (bench.py C2 / C5): 1e9 distinct keys stored in
+    the builder's 3,559,786,523 buckets, alpha = 0.281."""
     spec = synth.ImageSpec(10 ** 9)
-    img, stored = gpu.Image.synthetic(spec.n_keys, spec.num_sigs)
-    assert img.layout == gpu.Image.PACKED16 and stored > 9.7e8
+    img, n_entries = gpu.Image.synthetic_distinct(spec.n_keys, 10 ** 9, spec.num_sigs)
+    assert img.layout == gpu.Image.PACKED16 and spec.num_sigs == 3_559_786_523 and n_entries >= 10 ** 9
+    yield spec, img
+    img.close()
+
+
+def _device_queries(gpu, ctx, spec, n, Ls, q0=0):
+    """bench.py's queries (kgx_synth_queries) copied to the host."""
+    L = gpu.lib()
+    d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+    gpu.check(L.kgx_device_alloc(0, n * Ls, ctypes.byref(d_res)), "alloc")
+    gpu.check(L.kgx_device_alloc(0, (n + 1) * 8, ctypes.byref(d_off)), "alloc")
+    try:
+        gpu.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, 0, q0, d_res, d_off), "queries")
+        res = np.empty(n * Ls, np.uint8)
+        off = np.empty(n + 1, np.uint64)
+        gpu.check(L.kgx_memcpy_d2h(res.ctypes.data, d_res, res.nbytes), "d2h")
+        gpu.check(L.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
+    finally:
+        L.kgx_device_free(d_res)
+        L.kgx_device_free(d_off)
+    return res, off
+
+
+def _oracle_sample(oracle_lib, table, res, off, idx):
+    sres = np.concatenate([res[int(off[i]):int(off[i + 1])] for i in idx])
+    soff = np.concatenate([[0], np.cumsum(np.diff(off)[idx])]).astype(np.uint64)
+    return oracle_lib.process_batch(table, sres, soff, want=3, n_threads=8)
+
+
+def _assert_sample(got_hits, got_hoff, got_calls, got_coff, want, idx):
+    got_h = np.concatenate([got_hits[int(got_hoff[i]):int(got_hoff[i + 1])] for i in idx])
+    got_c = np.concatenate([got_calls[int(got_coff[i]):int(got_coff[i + 1])] for i in idx])
+    for f in ("which_kmer", "otu_index", "avg_from_end", "function_index", "pos"):
+        assert np.array_equal(got_h[f], want.hits[f]), f
+    assert np.array_equal(got_h["function_wt"].view(np.uint32), want.hits["function_wt"].view(np.uint32))
+    for f in ("start", "end", "count", "function_index"):
+        assert np.array_equal(got_c[f], want.calls[f]), f
+    assert np.array_equal(got_c["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+
+
+def test_c5_pool_one_batch_of_1m(gpu, oracle_lib, bench_image):
+    """C5 (BASELINE.json configs[4]): bench.py --strong's 1M x 300-aa batch
+    through kgx_pool on 8 contexts (device 0 here; one per GPU on a node),
+    residue-balanced shards, concatenated in input order.  The whole output
+    is byte-identical to ten sequential 100k single-context passes, the
+    compact pool result expands to the same bytes, and every 1000th sequence
+    matches the oracle on a host copy of the image."""
+    spec, img = bench_image
+    n, Ls, step = 1_000_000, 300, 100_000
+    with gpu.Context(img) as ctx:
+        res, off = _device_queries(gpu, ctx, spec, n, Ls)
+        with gpu.Pool([img], n_ctx=8) as pool:
+            split = pool.process_batch(res, off, want=3)
+            assert len(split.hits) > 70_000_000
+            cb = pool.process_batch_compact(res, off, want=3)
+            assert cb.n_chunks >= 8 and not cb.materialized
+            for a in range(0, n, step):  # the compact chunks against the expanded concatenation
+                b = a + step
+                assert np.array_equal(cb.expand(a, b).view(np.uint8),
+                                      split.hits[int(split.hit_offsets[a]):int(split.hit_offsets[b])].view(np.uint8))
+            del cb
+            for a in range(0, n, step):
+                b = a + step
+                one = ctx.process_batch(res, off[a:b + 1], want=3)
+                h0, h1 = int(split.hit_offsets[a]), int(split.hit_offsets[b])
+                c0, c1 = int(split.call_offsets[a]), int(split.call_offsets[b])
+                assert np.array_equal(split.hit_offsets[a:b + 1] - np.uint64(h0), one.hit_offsets)
+                assert np.array_equal(split.call_offsets[a:b + 1] - np.uint64(c0), one.call_offsets)
+                ph = split.hits[h0:h1].copy()
+                ph["seq"] -= a
+                assert np.array_equal(ph.view(np.uint8), one.hits.view(np.uint8))
+                assert np.array_equal(split.calls[c0:c1].view(np.uint8), one.calls.view(np.uint8))
+    table = img.download()
+    idx = np.arange(0, n, 1000)
+    want = _oracle_sample(oracle_lib, table, res, off, idx)
+    del table
+    _assert_sample(split.hits, split.hit_offsets, split.calls, split.call_offsets, want, idx)
+
+
+def test_c2_full_scale(gpu, oracle_lib, bench_image):
+    L = gpu.lib()
+    spec, img = bench_image
     ctx = gpu.Context(img)
     n, Ls = 100000, 300
     d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
@@ -69,25 +153,17 @@ def test_c2_full_scale(gpu, oracle_lib):
         del one, split
         # every 100th sequence against the oracle on a host copy of the image
         table = img.download()
+        keys_stored = int(np.count_nonzero(table["which_kmer"] <= 20 ** 8))
+        assert keys_stored == 10 ** 9
         idx = np.arange(0, n, 100)
-        sres = np.concatenate([res[int(off[i]):int(off[i + 1])] for i in idx])
-        soff = np.concatenate([[0], np.cumsum(np.diff(off)[idx])]).astype(np.uint64)
-        want = oracle_lib.process_batch(table, sres, soff, want=3, n_threads=8)
+        want = _oracle_sample(oracle_lib, table, res, off, idx)
         del table
-        got_h = np.concatenate([r1["hits"][int(r1["hit_offsets"][i]):int(r1["hit_offsets"][i + 1])] for i in idx])
-        got_c = np.concatenate([r1["calls"][int(r1["call_offsets"][i]):int(r1["call_offsets"][i + 1])]
-                                for i in idx])
-        for f in ("which_kmer", "otu_index", "avg_from_end", "function_index", "pos"):
-            assert np.array_equal(got_h[f], want.hits[f]), f
-        assert np.array_equal(got_h["function_wt"].view(np.uint32), want.hits["function_wt"].view(np.uint32))
-        for f in ("start", "end", "count", "function_index"):
-            assert np.array_equal(got_c[f], want.calls[f]), f
-        assert np.array_equal(got_c["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+        _assert_sample(r1["hits"], r1["hit_offsets"], r1["calls"], r1["call_offsets"], want, idx)
         # the file's 24-byte layout gives the same results
         img.set_layout(gpu.Image.AOS24)
         _same(r1, run())
+        img.set_layout(gpu.Image.PACKED16)
     finally:
         L.kgx_device_free(d_res)
         L.kgx_device_free(d_off)
         ctx.close()
-        img.close()

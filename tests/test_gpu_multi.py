@@ -176,3 +176,49 @@ def test_bad_device_offsets_are_an_error_not_a_fault(world, gpu):
     finally:
         L.kgx_device_free(d_res)
         L.kgx_device_free(d_off)
+
+
+def _compact_equals(cb, one, res, off):
+    """A compact result carries the same offsets / calls / OTUs / best calls,
+    and its hits expand to the same kgx_hit bytes, as a whole range, per
+    sequence and with a seq_base."""
+    for k in ("hit_offsets", "call_offsets", "otu_offsets"):
+        assert np.array_equal(getattr(cb.result, k), getattr(one, k)), k
+    for k in ("calls", "otus"):
+        assert np.array_equal(getattr(cb.result, k).view(np.uint8), getattr(one, k).view(np.uint8)), k
+    if one.best is not None:
+        assert np.array_equal(cb.result.best.view(np.uint8), one.best.view(np.uint8))
+    assert cb.result.n_windows == one.n_windows
+    assert np.array_equal(cb.expand().view(np.uint8), one.hits.view(np.uint8))
+    n = len(off) - 1
+    if n:
+        rng = np.random.default_rng(n)
+        for _ in range(20):
+            a = int(rng.integers(0, n))
+            b = int(rng.integers(a, n + 1))
+            got = cb.expand(a, b, seq_base=1000)
+            want = one.hits[int(one.hit_offsets[a]):int(one.hit_offsets[b])].copy()
+            want["seq"] += 1000
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+
+
+@pytest.mark.parametrize("n_ctx,n_seq", [(8, 2000), (3, 80000), (8, 5), (4, 0)])
+def test_pool_compact_result_expands_to_one_pass(world, gpu, n_ctx, n_seq):
+    """kgx_pool_process_batch_compact: every shard's chunks renumbered into
+    the batch, no hit record copied; expanding them gives one pass's bytes."""
+    spec, table, img = world
+    res, off = _mixed_batch(spec, n_seq, 7 * n_ctx + n_seq) if n_seq != 80000 else \
+        synth.make_queries(spec, n_seq, x_permille=5, q0=11)
+    with gpu.Context(img) as ctx:
+        one = ctx.process_batch(res, off, want=ALL)
+    with gpu.Pool([img], n_ctx=n_ctx) as pool:
+        pool.set_option("host_chunks", 3)
+        for _ in range(2):
+            cb = pool.process_batch_compact(res, off, want=ALL)
+            _compact_equals(cb, one, res, off)
+        if n_seq == 80000:
+            assert cb.n_chunks >= n_ctx and not cb.materialized
+            seqs = [(c.seq_begin, c.seq_end) for c in cb.chunks]
+            assert seqs == sorted(seqs) and all(a[1] <= b[0] for a, b in zip(seqs, seqs[1:]))
+        got = pool.process_batch(res, off, want=ALL)  # expanded once into the concatenation
+        _bytes_equal(got, one)

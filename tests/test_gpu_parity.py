@@ -742,6 +742,73 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_chunks", 3)
 
 
+@pytest.mark.parametrize("schedule", ["streamed_rec12", "streamed_rec16", "exact", "small", "aos24",
+                                      "one_pass", "overflow"])
+def test_compact_results_match_oracle(small_world, aos_world, oracle_lib, gpu, schedule):
+    """kgx_process_batch_compact: whatever path a batch takes, the compact
+    result carries the oracle's offsets, calls and OTUs, and its hits expand
+    (whole batch, any sequence range, seq_base) to the oracle's hits."""
+    spec, table, img, ctx = small_world
+    n = 60 if schedule == "small" else 16000
+    res, off = synth.make_queries(spec, n, x_permille=3, q0=5)
+    want = oracle_lib.process_batch(table, res, off)
+    opts = {"streamed_rec12": {"host_chunks": 5}, "streamed_rec16": {"host_chunks": 5, "host_rec12": 0},
+            "exact": {"host_chunks": 4, "host_stream": 0}, "small": {}, "aos24": {"host_chunks": 3},
+            "one_pass": {"host_chunks": 1}, "overflow": {"host_chunks": 4}}[schedule]
+    c = aos_world[1] if schedule == "aos24" else ctx
+    try:
+        for k, v in opts.items():
+            c.set_option(k, v)
+        if schedule == "overflow":  # a hitless batch drives the region rates to their floor
+            rng = np.random.default_rng(8)
+            noise = np.frombuffer("".join(random_protein(rng, 300) for _ in range(20000)).encode(), np.uint8)
+            c.process_batch_compact(noise, np.arange(20001, dtype=np.uint64) * np.uint64(300))
+        cb = c.process_batch_compact(res, off, gpu.Params(5, 200, 0, 0), want=7)
+        compact_paths = ("streamed_rec12", "streamed_rec16", "exact", "overflow")
+        assert (cb.n_chunks > 0) == (schedule in compact_paths), cb.n_chunks
+        if schedule in compact_paths:
+            assert {ch.record_words for ch in cb.chunks} == ({4} if schedule in ("exact", "overflow",
+                                                                               "streamed_rec16") else {3})
+        r = cb.result
+        assert np.array_equal(r.hit_offsets, want.hit_offsets)
+        assert np.array_equal(r.call_offsets, want.call_offsets)
+        for f in ["start", "end", "count", "function_index"]:
+            assert np.array_equal(r.calls[f], want.calls[f]), f
+        assert np.array_equal(r.calls["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+        assert np.array_equal(r.otus["otu_index"], want.otus[:, 0])
+        hits = cb.expand()
+        assert eq_fields(hits, want.hits)
+        rng = np.random.default_rng(len(schedule))
+        for _ in range(10):
+            a = int(rng.integers(0, n))
+            b = int(rng.integers(a, n + 1))
+            part = cb.expand(a, b, seq_base=7)
+            sl = want.hits[int(want.hit_offsets[a]):int(want.hit_offsets[b])]
+            assert eq_fields(part, sl, [f for f in HIT_FIELDS if f != "seq"])
+            assert np.array_equal(part["seq"], sl["seq"] + 7)
+    finally:
+        for k in opts:
+            c.set_option(k, {"host_chunks": 3, "host_rec12": 1, "host_stream": 1}[k])
+
+
+def test_host_profile_reports_the_streamed_stages(small_world, gpu):
+    spec, table, img, ctx = small_world
+    res, off = synth.make_queries(spec, 16000, x_permille=0, q0=9)
+    ctx.set_option("host_profile", 1)
+    ctx.set_option("host_chunks", 4)
+    try:
+        ctx.process_batch(res, off, want=3)
+        p = ctx.host_profile()
+        assert p["streamed"] == 1 and p["chunks"] >= 2
+        assert p["h2d_ms"] > 0 and p["device_ms"] > 0 and p["d2h_ms"] > 0 and p["expand_ms"] > 0
+        assert p["h2d_bytes"] >= res.nbytes and p["d2h_bytes"] > 0 and p["wall_ms"] > 0
+        ctx.process_batch_compact(res, off, want=3)
+        assert ctx.host_profile()["expand_ms"] == 0
+    finally:
+        ctx.set_option("host_profile", 0)
+        ctx.set_option("host_chunks", 3)
+
+
 # ---------------------------------------------------------------------------
 # find_best_call on the device (KGX_WANT_BEST, kgx_find_best_calls)
 
