@@ -346,36 +346,54 @@ def main():
         off_h = np.empty(n + 1, np.uint64)
         abi.check(L.kgx_memcpy_d2h(res_h.ctypes.data, d_res, res_h.nbytes), "d2h")
         abi.check(L.kgx_memcpy_d2h(off_h.ctypes.data, d_off, off_h.nbytes), "d2h")
-        by_cfg = {}
-        # the default schedule last (its result is reported), beside the
-        # round-1 schedule (3 chunks, 32-B records, host round trip per chunk)
-        # and one pass; option tuples (host_chunks, host_hits16, host_stream)
-        cfgs = {"one_pass": (1, 1, 1), "r1_exact_32B": (3, 0, 0), "exact_16B": (6, 1, 0), "default": (6, 1, 1)}
-        for name, (k, h16, hs) in cfgs.items():
+        by_cfg, profiles = {}, {}
+        # option tuples (host_chunks, host_hits16, host_stream, compact): the
+        # round-1 schedule (3 chunks, 32-B records, host round trip per chunk),
+        # the streamed schedule with kgx_hit expanded on host threads, and the
+        # compact result (kgx_process_batch_compact: the records + mask the
+        # facade replays hit_cb from, no kgx_hit array) -- reported as value
+        cfgs = {"one_pass": (1, 1, 1, 0), "r1_exact_32B": (3, 0, 0, 0), "exact_16B": (6, 1, 0, 0),
+                "expanded": (6, 1, 1, 0), "compact": (6, 1, 1, 1)}
+        ctx.set_option("host_profile", 1)
+        for name, (k, h16, hs, cp) in cfgs.items():
             ctx.set_option("host_chunks", k)
             ctx.set_option("host_hits16", h16)
             ctx.set_option("host_stream", hs)
-            r = ctx.process_batch(res_h, off_h, params, want=want, copy=False)  # warm (buffer growth)
-            th = []
+            run = ((lambda: ctx.process_batch_compact(res_h, off_h, params, want=want)) if cp else
+                   (lambda: ctx.process_batch(res_h, off_h, params, want=want, copy=False)))
+            r = run()  # warm (buffer growth)
+            th, pr = [], []
             for _ in range(7):
                 t0 = time.perf_counter()
-                r = ctx.process_batch(res_h, off_h, params, want=want, copy=False)
+                r = run()
                 th.append(time.perf_counter() - t0)
+                pr.append(ctx.host_profile())
             by_cfg[name] = float(np.median(th))
-        t_h = by_cfg["default"]
+            if pr[0]["streamed"]:
+                profiles[name] = {k2: float(np.median([q[k2] for q in pr])) for k2 in pr[0]}
+        ctx.set_option("host_profile", 0)
+        t_h = by_cfg["compact"]
+        t_x = by_cfg["expanded"]
+        rr = r.result
+        n_hits, n_calls = int(rr.hit_offsets[-1]), int(rr.call_offsets[-1])
         mask_bytes = n_res // 8  # the hit mask: one bit per window
         host_path = {"value": n_res / t_h, "unit": "residues/s", "ms_per_batch": t_h * 1e3,
+                     "value_kgx_hit": n_res / t_x, "ms_per_batch_kgx_hit": t_x * 1e3,
                      "ms_per_batch_by_schedule": {k: v * 1e3 for k, v in by_cfg.items()},
-                     "schedules": {k: dict(zip(("host_chunks", "host_hits16", "host_stream"), v))
+                     "schedules": {k: dict(zip(("host_chunks", "host_hits16", "host_stream", "compact"), v))
                                    for k, v in cfgs.items()},
-                     "d2h_bytes": int(len(r.hits) * 12 + mask_bytes + len(r.calls) * 20),
-                     "d2h_bytes_32B_records": int(len(r.hits) * 32 + len(r.calls) * 20),
-                     "note": "kgx_process_batch from host buffers: H2D residues + kernels + D2H into pinned "
-                             "host memory, full 32-B kgx_hit records on the host (PCIe-inclusive).  default: 6 "
-                             "chunks over two contexts, device CSR offsets, bulk copies on a copy stream sized on "
-                             "the device, 12-B records (no key) + the hit mask over PCIe, kgx_hit expanded by "
-                             "host threads (key re-encoded from the residues) while later chunks stream"}
-        log(f"[bench] host-buffer path {n_res / t_h:.3e} residues/s ({t_h * 1e3:.1f} ms/batch)")
+                     "stage_profile_ms": profiles,
+                     "d2h_bytes": int(n_hits * 12 + mask_bytes + n_calls * 20),
+                     "d2h_bytes_32B_records": int(n_hits * 32 + n_calls * 20),
+                     "note": "host buffers in, host results out (PCIe-inclusive): H2D residues + kernels + D2H "
+                             "into pinned host memory.  6 chunks over two contexts, device CSR offsets, bulk "
+                             "copies on a copy stream sized on the device, 12-B records (no key) + the hit mask "
+                             "over PCIe.  value: kgx_process_batch_compact (records + mask, what the facade "
+                             "replays hit_cb from); value_kgx_hit: kgx_process_batch, 32-B kgx_hit records built "
+                             "by host threads while later chunks stream.  stage_profile_ms: HIP-event sums per "
+                             "stage over the chunks (they overlap) and host wall times"}
+        log(f"[bench] host-buffer path {n_res / t_h:.3e} residues/s compact ({t_h * 1e3:.2f} ms/batch), "
+            f"{n_res / t_x:.3e} with kgx_hit ({t_x * 1e3:.2f} ms); profiles {profiles}")
 
     ceiling = None
     if d.rank == 0 and not args.no_microbench:

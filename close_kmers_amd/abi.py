@@ -240,6 +240,7 @@ SIGNATURES = {
                                               ctypes.POINTER(CompactResult)]),
     "kgx_compact_expand": (_INT, [ctypes.POINTER(CompactResult), _P, _P, _U32, _U32, _U32, _P]),
     "kgx_ctx_host_profile": (_INT, [_P, ctypes.POINTER(HostProfile)]),
+    "kgx_ctx_stat": (_INT, [_P, _CS, ctypes.POINTER(ctypes.c_int64)]),
 }
 
 
@@ -503,6 +504,11 @@ class Context:
                                               offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(cr)),
               "kgx_process_batch_compact")
         return CompactBatch(cr, residues, offsets, want)
+
+    def stat(self, name: str) -> int:
+        v = ctypes.c_int64()
+        check(lib().kgx_ctx_stat(self.handle, name.encode(), ctypes.byref(v)), f"stat({name})")
+        return v.value
 
     def host_profile(self) -> dict:
         p = HostProfile()

@@ -21,10 +21,12 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libkgx.so")
 QUERY = os.path.join(PKG, "kgx_query")
 SERVER = os.path.join(PKG, "kgx_server")
+# the facade under T concurrent worker threads (tests/test_gpu_coalesce.py)
+COALESCE_CHECK = os.path.join(ROOT, "tests", "native", "coalesce_check")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-LIB_SOURCES = ["kgx_lookup.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
+LIB_SOURCES = ["kgx_lookup.hip", "kgx_fused.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
                "kgx_pool.cpp", "kguts_hip.cpp", "kgx_handlers.cpp"]
 HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h", "kgx_handlers.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
@@ -69,12 +71,15 @@ def build(force: bool = False, verbose: bool = False) -> None:
         tmp = LIB + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
         os.replace(tmp, LIB)
-    for exe, src in ((QUERY, "kgx_query.cpp"), (SERVER, "kgx_server.cpp")):
-        esrc = os.path.join(CSRC, src)
+    for exe, esrc in ((QUERY, os.path.join(CSRC, "kgx_query.cpp")), (SERVER, os.path.join(CSRC, "kgx_server.cpp")),
+                      (COALESCE_CHECK, os.path.join(ROOT, "tests", "native", "coalesce_check.cpp"))):
+        if not os.path.exists(esrc):
+            continue
         if force or _newer(exe, [esrc, LIB] + deps):
             tmp = exe + ".tmp"
-            _run([HIPCC] + COMMON + ["-x", "hip", esrc, "-o", tmp, f"-L{PKG}", "-lkgx",
-                                     "-Wl,-rpath,$ORIGIN", "-pthread"])
+            rpath = os.path.join("$ORIGIN", os.path.relpath(PKG, os.path.dirname(exe)))  # libkgx.so, in-tree
+            _run([HIPCC] + COMMON + ["-x", "hip", esrc, "-o", tmp, f"-L{PKG}", "-lkgx", f"-Wl,-rpath,{rpath}",
+                                     "-pthread"])
             os.replace(tmp, exe)
 
 

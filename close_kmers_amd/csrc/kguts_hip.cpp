@@ -208,11 +208,137 @@ void KmerGuts::process_aa_batch(std::vector<SeqJob> &jobs)
     }
 }
 
+/* ---- SeqCoalescer ------------------------------------------------------- */
+
+SeqCoalescer::SeqCoalescer()
+{
+    if (const char *e = std::getenv("KGX_COALESCE_INFLIGHT"))
+        max_inflight = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("KGX_COALESCE_RESIDUES"))
+        max_residues = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+}
+
+void SeqCoalescer::submit(kgx_ctx *ctx, Req &r)
+{
+    std::unique_lock<std::mutex> lk(mu_);
+    queue_.push_back(&r);
+    while (!r.done) {
+        if (inflight_ < max_inflight && !queue_.empty()) {
+            /* lead a pass: the queue's head and every queued call with the
+             * same parameters, in arrival order, up to max_residues */
+            std::vector<Req *> batch;
+            uint64_t res = 0;
+            const kgx_params p0 = queue_.front()->params;
+            for (auto it = queue_.begin(); it != queue_.end();) {
+                Req *q = *it;
+                const bool same = q->params.min_hits == p0.min_hits && q->params.max_gap == p0.max_gap &&
+                                  q->params.order_constraint == p0.order_constraint &&
+                                  q->params.min_weighted_hits == p0.min_weighted_hits;
+                if (same && (batch.empty() || res + q->seq->size() <= max_residues)) {
+                    batch.push_back(q);
+                    res += q->seq->size();
+                    it = queue_.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            inflight_++;
+            lk.unlock();
+            run_batch(ctx, batch);
+            lk.lock();
+            inflight_--;
+            passes++;
+            calls += batch.size();
+            for (Req *q : batch)
+                q->done = true;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk);
+        }
+    }
+}
+
+void SeqCoalescer::run_batch(kgx_ctx *ctx, std::vector<Req *> &batch)
+{
+    const uint32_t n = (uint32_t)batch.size();
+    std::vector<uint64_t> off(n + 1, 0);
+    uint32_t want = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        off[i + 1] = off[i] + batch[i]->seq->size();
+        want |= batch[i]->want;
+    }
+    std::string buf;
+    buf.reserve(off[n]);
+    for (Req *q : batch)
+        buf += *q->seq;
+    kgx_compact_result cr;
+    /* per-sequence callers: the one-launch path where it applies */
+    (void)kgx_ctx_set_option(ctx, "small_fused", 1);
+    int rc = kgx_process_batch_compact(ctx, &batch[0]->params, buf.data(), off.data(), n, want, &cr);
+    (void)kgx_ctx_set_option(ctx, "small_fused", 0);
+    const kgx_result &r = cr.r;
+    for (uint32_t i = 0; i < n && !rc; i++) {
+        Req &q = *batch[i];
+        if (q.want & KGX_WANT_HITS) {
+            q.out.hits.resize(r.hit_offsets[i + 1] - r.hit_offsets[i]);
+            if (!q.out.hits.empty())
+                rc = kgx_compact_expand(&cr, buf.data(), off.data(), i, i + 1, 0, q.out.hits.data());
+        }
+        if (q.want & KGX_WANT_CALLS)
+            q.out.calls.assign(r.calls + r.call_offsets[i], r.calls + r.call_offsets[i + 1]);
+        if (q.want & KGX_WANT_OTU)
+            q.out.otus.assign(r.otus + r.otu_offsets[i], r.otus + r.otu_offsets[i + 1]);
+    }
+    if (rc) {
+        const std::string err = kgx_last_error();
+        for (Req *q : batch) {
+            q->rc = rc;
+            q->err = err;
+        }
+    }
+}
+
 void KmerGuts::process_aa_seq(const std::string &id, const std::string &seq,
                               std::shared_ptr<std::vector<KmerCall>> calls,
                               std::function<void(hit_in_sequence_t)> hit_cb,
                               std::shared_ptr<KmerOtuStats> otu_stats)
 {
+    if (coalesce) {
+        SeqCoalescer::Req q;
+        q.seq = &seq;
+        q.params = kgx_params{min_hits, max_gap, order_constraint, min_weighted_hits};
+        q.want = (hit_cb ? KGX_WANT_HITS : 0u) | (calls ? KGX_WANT_CALLS : 0u) | (otu_stats ? KGX_WANT_OTU : 0u);
+        image_->coalescer().submit(ctx_, q);
+        if (q.rc)
+            throw Error(q.rc, "process_aa_seq: " + std::string(kgx_strerror(q.rc)) + " (" + q.err + ")");
+        /* replay on the calling thread, in position order (kguts.cc:814-815) */
+        if (hit_cb)
+            for (const kgx_hit &h : q.out.hits) {
+                sig_kmer_t e;
+                e.which_kmer = h.which_kmer;
+                e.otu_index = h.otu_index;
+                e.avg_from_end = h.avg_from_end;
+                e.pad = 0;
+                e.function_index = h.function_index;
+                e.function_wt = h.function_wt;
+                hit_cb(hit_in_sequence_t(e, h.pos));
+            }
+        if (calls)
+            for (const kgx_call &c : q.out.calls)
+                calls->push_back(KmerCall(c.start, c.end, c.count, c.function_index, c.weighted_hits));
+        if (otu_stats) {
+            for (const kgx_otu &o : q.out.otus)
+                otu_stats->otu_map[o.otu_index] += o.count;
+            otu_stats->finalize(); /* kguts.cc:906-907 */
+        }
+        return;
+    }
+    /* one pass of one sequence: the one-launch path where it applies */
+    struct Fused {
+        kgx_ctx *c;
+        explicit Fused(kgx_ctx *x) : c(x) { (void)kgx_ctx_set_option(c, "small_fused", 1); }
+        ~Fused() { (void)kgx_ctx_set_option(c, "small_fused", 0); }
+    } fused(ctx_);
     std::vector<SeqJob> jobs(1);
     jobs[0].id = id;
     jobs[0].seq = seq;

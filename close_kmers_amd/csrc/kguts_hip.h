@@ -15,7 +15,9 @@
 #ifndef KGUTS_HIP_H
 #define KGUTS_HIP_H
 
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -69,6 +71,54 @@ public:
     void finalize();
 };
 
+/*
+ * Coalescing of concurrent per-sequence calls.  The reference's pool keeps one
+ * KmerGuts per worker thread, each calling process_aa_seq once per sequence
+ * (threadpool.cc:33-60, lookup_request.cc:153-172).  On a GPU one sequence is
+ * far too little work for a pass, so calls that arrive on an image while
+ * another pass is in flight are queued and run together: a caller that finds
+ * fewer than max_inflight passes running becomes the leader, takes every
+ * queued call with its parameters (up to max_residues residues) and runs them
+ * as one batch on its own context; each caller blocks until its slice is
+ * done, then replays its hit_cb / calls / OTU stats on its own thread, in
+ * position order, before returning (kguts.cc:814-815, 888-908).
+ */
+class SeqCoalescer {
+public:
+    struct Slice {
+        std::vector<kgx_hit> hits;
+        std::vector<kgx_call> calls;
+        std::vector<kgx_otu> otus;
+    };
+    /* one pending call */
+    struct Req {
+        const std::string *seq = nullptr;
+        kgx_params params{};
+        uint32_t want = 0;
+        Slice out;
+        bool done = false;
+        int rc = KGX_OK;
+        std::string err;
+    };
+    /* max_inflight / max_residues from KGX_COALESCE_INFLIGHT /
+     * KGX_COALESCE_RESIDUES when set */
+    SeqCoalescer();
+    /* runs r on ctx, joining whatever is queued meanwhile; returns when r is
+     * done (its slice filled, or r.rc set) */
+    void submit(kgx_ctx *ctx, Req &r);
+    int max_inflight = 2;
+    uint64_t max_residues = 1 << 16;
+    /* statistics: passes run and calls served */
+    uint64_t passes = 0, calls = 0;
+
+private:
+    void run_batch(kgx_ctx *ctx, std::vector<Req *> &batch);
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Req *> queue_;
+    int inflight_ = 0;
+};
+
 /* KmerImage (kmer_image.h:25-39): the read-only signature table, resident in
  * the HBM of one device.  Validation as kmer_image.cc:128-147. */
 class KmerImage {
@@ -85,8 +135,11 @@ public:
     kgx_image *handle() const { return img_; }
     uint64_t num_sigs() const { return kgx_image_num_sigs(img_); }
     const std::string &data_dir() const { return data_dir_; }
+    /* the queue that coalesces the image's concurrent process_aa_seq calls */
+    SeqCoalescer &coalescer() { return coalescer_; }
 
 private:
+    SeqCoalescer coalescer_;
     kgx_image *img_ = nullptr;
     std::string data_dir_;
     bool owned_ = true;
@@ -138,6 +191,9 @@ public:
                              std::shared_ptr<KmerOtuStats> otu_stats);
     /* every job as process_aa_seq would, in order, with one GPU pass */
     void process_aa_batch(std::vector<SeqJob> &jobs);
+    /* process_aa_seq joins the image's queue of concurrent calls (default
+     * on; SeqCoalescer); off: one GPU pass per call on this object's context */
+    bool coalesce = true;
 
     void find_best_call(std::vector<KmerCall> &calls, int &function_index, std::string &function,
                         float &score, float &weighted_score, float &score_offset);

@@ -69,6 +69,30 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t lo, uint32_t hi)
     return upto_hi & ~below_lo;
 }
 
+/* wave-level helpers of the wave-parallel scorers */
+__device__ __forceinline__ uint64_t lanes_le(uint32_t k) { return k >= 63 ? ~0ull : ((2ull << k) - 1); }
+__device__ __forceinline__ int hibit(uint64_t m) { return m ? 63 - (int)__clzll((long long)m) : -1; }
+__device__ __forceinline__ uint32_t lowbit(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rlf(float v, uint32_t l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+/* (the builtins return int: widen through uint32_t, or a low half >= 2^31
+ * sign-extends into the high half) */
+__device__ __forceinline__ uint64_t uni64(uint64_t v)
+{
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+}
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 /* ---- hit records (kgx_internal.h: HIT_PLANES / HIT_PACKED16) ---- */
 
 /* the fields of one hit record (hot = plane 0 / the packed record,

@@ -1,0 +1,345 @@
+/*
+ * kgx_fused.hip -- process_aa_seq for a few sequences in ONE launch.
+ *
+ * The reference's handlers call KmerGuts::process_aa_seq once per sequence
+ * (lookup_request.cc:153-172, kguts.cc:888-908); the facade coalesces the
+ * concurrent calls of a worker pool into small batches.  For such a batch
+ * the general path's four launches (upload, probe, score, gather) and their
+ * hand-offs through HBM are the whole cost, so here one workgroup takes one
+ * sequence end to end:
+ *
+ *   1. its residues, read straight from the caller's pinned staging over
+ *      PCIe, mapped to codes in LDS (to_amino_acid_off, kguts.cc:273-339);
+ *   2. every window encoded from LDS (encoded_kmer, kguts.cc:438-455; a
+ *      window with a code-20 residue is skipped, advance_past_ambig
+ *      kguts.cc:682-732) and probed in the PACKED16 table, all of a thread's
+ *      windows in flight at once (lookup_hash_entry, kguts.cc:585-602);
+ *   3. the hits compacted in window order into LDS (ballots + a wave scan);
+ *   4. the kgx_hit records stored to the caller's mapped result region while
+ *      wave 0 scores the hits 64 at a time (gather_hits / process_set_of_hits,
+ *      kguts.cc:734-877, the wave-parallel formulation of score_wave_kernel
+ *      for one sequence: run breaks, current_fI as a segmented last-mark scan,
+ *      pair switches; f32 sums serial in hit order);
+ *   5. counts, then a system-scope fence and the sequence's completion token.
+ *
+ * Preconditions (checked by the host): PACKED16 image, order_constraint 0,
+ * min_hits >= 1, want within HITS | CALLS, every sequence at most
+ * FUSED_MAX_WINDOWS windows.
+ */
+#include "kgx_device.h"
+#include "kgx_internal.h"
+
+namespace kgx {
+
+struct FusedArgs {
+    const uint8_t *res;    /* mapped: the batch's residues (NUL-cut), concatenated */
+    const uint64_t *off;   /* mapped: n + 1 offsets into res */
+    const uint64_t *wbase; /* mapped: n + 1 exclusive scan of the window counts */
+    uint32_t n;
+    uint32_t want;
+    const uint4 *table; /* PACKED16 records in HBM */
+    uint64_t num_sigs, magic;
+    kgx_params prm;
+    kgx_hit *hits;    /* mapped: sequence s's hits from hits[wbase[s]] */
+    kgx_call *calls;  /* mapped: sequence s's calls from calls[wbase[s]] */
+    uint32_t *counts; /* mapped: hit count of s at [s], call count at [n + s] */
+    uint32_t *done;   /* mapped: done[s] = token once s's results are visible */
+    uint32_t token;
+};
+
+constexpr uint32_t FJ = FUSED_MAX_WINDOWS / 256; /* windows per thread, at most */
+
+__global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
+{
+    __shared__ uint8_t code_tab[256];
+    __shared__ uint8_t codes[FUSED_MAX_WINDOWS + 8];
+    __shared__ uint4 hrec[FUSED_MAX_WINDOWS];
+    __shared__ uint32_t hpos[FUSED_MAX_WINDOWS];
+    __shared__ uint32_t wave_cnt[4];
+    typedef HitFields<true> HF;
+
+    const uint32_t s = blockIdx.x;
+    const uint32_t t = threadIdx.x, lane = lane_id(), wave = t >> 6;
+    code_tab[t] = (uint8_t)residue_code(t);
+    const uint64_t r0 = a.off[s], len = a.off[s + 1] - r0;
+    const uint64_t wb = a.wbase[s];
+    const uint32_t W = (uint32_t)windows_of(len);
+    __syncthreads();
+    /* 1. residues -> codes (each wave reads 64 consecutive bytes per round) */
+    for (uint32_t i = t; i < W + 8 && i < len; i += 256)
+        codes[i] = code_tab[a.res[r0 + i]];
+    __syncthreads();
+
+    /* 2. encode + probe: thread t owns windows t + 256 j */
+    const uint32_t J = (W + 255) / 256;
+    uint64_t key[FJ], slot[FJ];
+    bool pend[FJ], hit[FJ];
+    uint4 rec[FJ];
+#pragma unroll
+    for (uint32_t j = 0; j < FJ; j++) {
+        const uint32_t w = t + 256 * j;
+        hit[j] = false;
+        pend[j] = false;
+        rec[j] = make_uint4(0, 0, 0, 0);
+        key[j] = 0;
+        slot[j] = 0;
+        if (j < J && w < W) {
+            const uint8_t *c = codes + w;
+            const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+            const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
+            const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
+            key[j] = (uint64_t)ka * 160000u + kb;
+            pend[j] = cmax < 20u;
+            slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
+        }
+    }
+    /* linear probe rounds, every pending window's bucket in flight at once;
+     * bounded by num_sigs buckets where the reference would spin forever */
+    for (uint64_t round = 0;; round++) {
+        uint4 pv[FJ];
+#pragma unroll
+        for (uint32_t j = 0; j < FJ; j++)
+            if (pend[j])
+                pv[j] = a.table[slot[j]];
+        bool more = false;
+#pragma unroll
+        for (uint32_t j = 0; j < FJ; j++) {
+            const uint64_t kv = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
+            const bool m = pend[j] && kv == key[j];
+            const bool stop = kv > MAX_ENCODED || round + 1 >= a.num_sigs;
+            rec[j].x = m ? pv[j].x : rec[j].x;
+            rec[j].y = m ? pv[j].y : rec[j].y;
+            rec[j].z = m ? pv[j].z : rec[j].z;
+            rec[j].w = m ? pv[j].w : rec[j].w;
+            hit[j] = hit[j] || m;
+            pend[j] = pend[j] && !m && !stop;
+            slot[j] = pend[j] ? (slot[j] + 1 == a.num_sigs ? 0 : slot[j] + 1) : slot[j];
+            more = more || pend[j];
+        }
+        if (!__syncthreads_or(more))
+            break;
+    }
+
+    /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
+    uint32_t nh = 0;
+    for (uint32_t j = 0; j < J; j++) {
+        bool h = false;
+        uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t q = 0; q < FJ; q++)
+            if (q == j) {
+                h = hit[q];
+                r = rec[q];
+            }
+        const uint64_t m = __ballot(h);
+        if (lane == 0)
+            wave_cnt[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t v = 0; v < 4; v++) {
+            before += v < wave ? wave_cnt[v] : 0u;
+            total += wave_cnt[v];
+        }
+        if (h) {
+            const uint32_t at = nh + before + lanes_below(m);
+            hrec[at] = r;
+            hpos[at] = t + 256 * j;
+        }
+        nh += total;
+        __syncthreads();
+    }
+
+    /* 4a. kgx_hit records into the caller's mapped region (kguts.h:228-233) */
+    if (a.want & KGX_WANT_HITS)
+        for (uint32_t i = t; i < nh; i += 256) {
+            const uint4 h = hrec[i];
+            const uint64_t k = HF::key(h, h);
+            uint4 *dst = reinterpret_cast<uint4 *>(a.hits + wb + i);
+            dst[0] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), HF::otu(h, h), HF::avg(h));
+            dst[1] = make_uint4(HF::fi(h), HF::wt(h), hpos[i], s);
+        }
+
+    /* 4b. the run scorer, wave 0, 64 hits per step (score_wave_kernel's
+     * chunk rules for a single sequence) */
+    uint32_t ncalls_out = 0;
+    if ((a.want & KGX_WANT_CALLS) && wave == 0 && nh) {
+        const kgx_params prm = a.prm;
+        const uint32_t gap = (uint32_t)prm.max_gap;
+        const float min_wh = (float)prm.min_weighted_hits;
+        kgx_call *calls = a.calls + wb;
+        bool o_valid = false;
+        uint32_t o_cur = 0, o_cnt = 0, o_first = 0, o_last = 0, o_ncalls = 0;
+        float o_wsum = 0.0f;
+        uint32_t p_pos = 0, p_fi = 0;
+        float p_wt = 0.0f;
+        /* flush of the open sub-run (kguts.cc:757-770) */
+        auto close_open = [&]() {
+            if ((int)o_cnt >= prm.min_hits && o_wsum >= min_wh) {
+                if (lane == 0) {
+                    kgx_call cl;
+                    cl.start = o_first;
+                    cl.end = o_last + (KMER - 1);
+                    cl.count = (int32_t)o_cnt;
+                    cl.function_index = o_cur;
+                    cl.weighted_hits = o_wsum;
+                    calls[o_ncalls] = cl;
+                }
+                o_ncalls++;
+            }
+        };
+        for (uint32_t h0 = 0; h0 < nh; h0 += 64) {
+            const uint32_t n = min(64u, nh - h0);
+            const uint32_t k = lane;
+            const bool act = k < n;
+            const uint64_t ACT = n >= 64 ? ~0ull : ((1ull << n) - 1);
+            const uint4 r = act ? hrec[h0 + k] : make_uint4(0, 0, 0, 0);
+            const uint32_t pos = act ? hpos[h0 + k] : 0u;
+            const uint32_t fi = HF::fi(r);
+            const float wt = __uint_as_float(HF::wt(r));
+            /* the predecessor of each hit (lane 0: the carried last hit) */
+            uint32_t ppos = __shfl_up(pos, 1), pfi = __shfl_up(fi, 1);
+            const bool first_hit = h0 == 0 && k == 0;
+            if (k == 0) {
+                ppos = p_pos;
+                pfi = p_fi;
+            }
+            /* a run breaks at the first hit and where prev.pos + max_gap <
+             * pos, unsigned (kguts.cc:821-831) */
+            const bool brk = first_hit || (ppos + gap < pos);
+            const bool eqp = !brk && fi == pfi;
+            const uint64_t M = __ballot(act && (brk || eqp));
+            const int jm = hibit(M & lanes_le(k));
+            uint32_t cur = __shfl(fi, jm < 0 ? 0 : jm);
+            if (jm < 0)
+                cur = o_cur;
+            uint32_t pcur = __shfl_up(cur, 1);
+            if (k == 0)
+                pcur = o_cur;
+            /* pair switch (kguts.cc:852-856) */
+            const bool sw = act && eqp && fi != pcur;
+            const uint64_t SW = __ballot(sw);
+            const uint64_t S = (__ballot(act && brk) | (SW >> 1)) & ACT; /* sub-run starts */
+            const bool memb = act && (fi == cur || ((S >> k) & 1));
+            const uint64_t MEMB = __ballot(memb);
+            if (SW & 1) { /* the open run flushes; the pair (last hit, lane 0) carries */
+                close_open();
+                o_cur = rl32(fi, 0);
+                o_cnt = 1;
+                o_wsum = 0.0f + p_wt;
+                o_first = p_pos;
+                o_last = p_pos;
+            }
+            /* lanes before the first start continue the open sub-run */
+            const uint32_t fs = S ? lowbit(S) : n;
+            if (fs > 0) {
+                uint64_t mm = MEMB & bit_range(0, fs);
+                o_cnt += (uint32_t)__popcll(mm);
+                if (mm)
+                    o_last = rl32(pos, (uint32_t)hibit(mm));
+                while (mm) {
+                    o_wsum = o_wsum + rlf(wt, lowbit(mm));
+                    mm &= mm - 1;
+                }
+            }
+            if (fs < n && o_valid)
+                close_open();
+            /* sub-runs that start in this chunk, one per start lane */
+            const bool is_start = (S >> k) & 1;
+            const uint64_t above = S & ~lanes_le(k);
+            const uint32_t e_k = above ? lowbit(above) : n;
+            const uint64_t msg = MEMB & bit_range(k, e_k);
+            const uint32_t c_seg = (uint32_t)__popcll(msg);
+            const int lm = hibit(msg);
+            const uint32_t last_pos = __shfl(pos, lm < 0 ? 0 : lm);
+            const bool closed = e_k < n;
+            const int b_open = hibit(S);
+            uint64_t SUM = __ballot(is_start && closed && (int)c_seg >= prm.min_hits);
+            if (b_open >= 0)
+                SUM |= 1ull << b_open;
+            float ws = 0.0f;
+            while (SUM) { /* f32 sums in hit order (kguts.cc:744-756) */
+                const uint32_t b = lowbit(SUM);
+                SUM &= SUM - 1;
+                const uint64_t ab = S & ~lanes_le(b);
+                uint64_t mm = MEMB & bit_range(b, ab ? lowbit(ab) : n);
+                float acc = 0.0f;
+                while (mm) {
+                    acc = acc + rlf(wt, lowbit(mm));
+                    mm &= mm - 1;
+                }
+                if (lane == b)
+                    ws = acc;
+            }
+            const uint64_t EMIT = __ballot(is_start && closed && (int)c_seg >= prm.min_hits && ws >= min_wh);
+            const uint32_t idx = o_ncalls + (uint32_t)__popcll(EMIT & bit_range(0, k));
+            if ((EMIT >> k) & 1) {
+                kgx_call cl;
+                cl.start = pos;
+                cl.end = last_pos + (KMER - 1);
+                cl.count = (int32_t)c_seg;
+                cl.function_index = fi;
+                cl.weighted_hits = ws;
+                calls[idx] = cl;
+            }
+            if (b_open >= 0) { /* carry the sub-run left open */
+                const uint32_t b = (uint32_t)b_open;
+                o_valid = true;
+                o_cur = rl32(fi, b);
+                o_cnt = rl32(c_seg, b);
+                o_wsum = rlf(ws, b);
+                o_first = rl32(pos, b);
+                o_last = rl32(last_pos, b);
+                o_ncalls = rl32(idx, b);
+            }
+            p_pos = rl32(pos, n - 1);
+            p_fi = rl32(fi, n - 1);
+            p_wt = rlf(wt, n - 1);
+        }
+        if (o_valid) /* the final flush (kguts.cc:873-876) */
+            close_open();
+        ncalls_out = o_ncalls;
+    }
+
+    /* 5. counts, then the token: every store above is visible to the host
+     * before it sees done[s] == token */
+    if (t == 0) {
+        a.counts[s] = nh;
+        a.counts[a.n + s] = ncalls_out;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile uint32_t *>(a.done + s) = a.token;
+    }
+}
+
+hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uint64_t *wbase, uint32_t n,
+                              uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
+                              kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
+                              hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    if (n > FUSED_MAX_SEQ || num_sigs == 0 || !packed_table)
+        return hipErrorInvalidValue;
+    FusedArgs a;
+    a.res = res;
+    a.off = off;
+    a.wbase = wbase;
+    a.n = n;
+    a.want = want;
+    a.table = static_cast<const uint4 *>(packed_table);
+    a.num_sigs = num_sigs;
+    a.magic = mod_magic(num_sigs);
+    a.prm = prm;
+    a.hits = hits;
+    a.calls = calls;
+    a.counts = counts;
+    a.done = done;
+    a.token = token;
+    hipLaunchKernelGGL(fused_small_kernel, dim3(n), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace kgx

@@ -216,16 +216,28 @@ hipError_t launch_small_upload(const SmallPieces &pc, hipStream_t stream);
 /* small_collect + gather in one workgroup, for batches of up to
  * SMALL_GATHER_SEQ sequences (offsets into mapped h0..h2, records into the
  * mapped outputs; a NULL output is not gathered); last, token is stored to
- * mapped *done_host (when not NULL) after a system-scope fence */
+ * mapped *done_host (when not NULL) after a system-scope fence, by the last
+ * workgroup to finish (blocks_done: a zeroed device word the kernel leaves
+ * zeroed; NULL = one workgroup) */
+/* one launch per small batch (kgx_fused.hip, context option "small_fused"):
+ * one workgroup per sequence of at most FUSED_MAX_WINDOWS windows, results
+ * stored straight into mapped host memory */
+constexpr uint32_t FUSED_MAX_WINDOWS = 2048;
+constexpr uint32_t FUSED_MAX_SEQ = 4096;
+hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uint64_t *wbase, uint32_t n,
+                              uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
+                              kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
+                              hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
+constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
                                const uint32_t *hit_count, const uint32_t *call_count, const uint4 *hot,
                                const uint4 *cold, const kgx_call *calls, const uint32_t *otu_count,
                                const kgx_otu *otus, kgx_hit *hits_out, kgx_call *calls_out, kgx_otu *otus_out,
                                uint64_t *h0, uint64_t *h1, uint64_t *h2, const uint32_t *status,
                                const kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
-                               uint64_t *nwin_host, uint32_t *done_host, uint32_t token, uint32_t hit_format,
-                               hipStream_t stream);
+                               uint64_t *nwin_host, uint32_t *done_host, uint32_t token, uint32_t *blocks_done,
+                               uint32_t hit_format, hipStream_t stream);
 /* one workgroup: launch_count_scan's offsets into o* (HBM) and h* (mapped
  * host), plus status[0], wbase[n] and (best_host non-NULL) best[0, n) */
 hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,

@@ -1252,28 +1252,6 @@ struct ScoreQueue {
     uint64_t wb[65]; /* window bases of sequences sb .. sb + 64 */
 };
 
-__device__ __forceinline__ uint64_t lanes_le(uint32_t k) { return k >= 63 ? ~0ull : ((2ull << k) - 1); }
-__device__ __forceinline__ int hibit(uint64_t m) { return m ? 63 - (int)__clzll((long long)m) : -1; }
-__device__ __forceinline__ uint32_t lowbit(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
-__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rlf(float v, uint32_t l)
-{
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
-/* (the builtins return int: widen through uint32_t, or a low half >= 2^31
- * sign-extends into the high half) */
-__device__ __forceinline__ uint64_t uni64(uint64_t v)
-{
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
-}
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 /* first sequence whose first window is >= x (x a tile boundary below the
  * batch's window count); tile_seq[x / T] owns window x */
@@ -1844,39 +1822,71 @@ __device__ __forceinline__ void gather_one(
                     incl += x;
             }
             const uint64_t dst0 = hoff_s + done + (incl - cnt);
+            /* a lane's run is read GB records at a time, all in flight before
+             * any is stored (a load-store loop would wait on every record) */
+            constexpr uint32_t GB = 4;
             if (PK && hits16_out) { /* the records as stored: position = mask bit */
-                for (uint32_t i = 0; i < cnt; i++)
-                    hits16_out[dst0 + i] = hot[at + i];
+                for (uint32_t i0 = 0; i0 < cnt; i0 += GB) {
+                    uint4 h[GB];
+#pragma unroll
+                    for (uint32_t k = 0; k < GB; k++)
+                        if (i0 + k < cnt)
+                            h[k] = hot[at + i0 + k];
+#pragma unroll
+                    for (uint32_t k = 0; k < GB; k++)
+                        if (i0 + k < cnt)
+                            hits16_out[dst0 + i0 + k] = h[k];
+                }
                 done += __shfl(incl, 63);
                 continue;
             }
             if (PK && hits12_out) { /* the records less the key (the host re-encodes it) */
-                for (uint32_t i = 0; i < cnt; i++) {
-                    const uint4 h = hot[at + i];
-                    uint32_t *d = hits12_out + 3 * (dst0 + i);
-                    d[0] = h.z;      /* function_wt bits */
-                    d[1] = h.w;      /* avg_from_end | (otu+1) high 12 << 16 | flags << 28 */
-                    d[2] = h.y >> 3; /* (fI+1) | (otu+1) low 9 << 20: packed lo >> 35 */
+                for (uint32_t i0 = 0; i0 < cnt; i0 += GB) {
+                    uint4 h[GB];
+#pragma unroll
+                    for (uint32_t k = 0; k < GB; k++)
+                        if (i0 + k < cnt)
+                            h[k] = hot[at + i0 + k];
+#pragma unroll
+                    for (uint32_t k = 0; k < GB; k++)
+                        if (i0 + k < cnt) {
+                            uint32_t *d = hits12_out + 3 * (dst0 + i0 + k);
+                            d[0] = h[k].z;      /* function_wt bits */
+                            d[1] = h[k].w;      /* avg_from_end | (otu+1) high 12 << 16 | flags << 28 */
+                            d[2] = h[k].y >> 3; /* (fI+1) | (otu+1) low 9 << 20: packed lo >> 35 */
+                        }
                 }
                 done += __shfl(incl, 63);
                 continue;
             }
             uint4 *dst = reinterpret_cast<uint4 *>(hits_out + dst0);
             const uint32_t pbase = (uint32_t)(64 * g - gw0);
-            for (uint32_t i = 0; i < cnt; i++) { /* kgx_hit from its record(s) */
-                const uint4 h = hot[at + i];
-                const uint32_t pos = pbase + (uint32_t)__builtin_ctzll(bits);
-                bits &= bits - 1;
-                if (PK) {
-                    typedef HitFields<true> HF;
-                    const uint64_t k = HF::key(h, h);
-                    dst[2 * i] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), HF::otu(h, h),
-                                            HF::avg(h) | HF::flags(h) << 16);
-                    dst[2 * i + 1] = make_uint4(HF::fi(h), HF::wt(h), pos, s + seq_base);
-                } else {
-                    const uint4 c = cold[at + i];
-                    dst[2 * i] = make_uint4(c.x, c.y, c.z, h.x);
-                    dst[2 * i + 1] = make_uint4(h.y, h.z, pos, s + seq_base);
+            for (uint32_t i0 = 0; i0 < cnt; i0 += GB) { /* kgx_hit from its record(s) */
+                uint4 h[GB], c[GB];
+#pragma unroll
+                for (uint32_t k = 0; k < GB; k++)
+                    if (i0 + k < cnt) {
+                        h[k] = hot[at + i0 + k];
+                        if (!PK)
+                            c[k] = cold[at + i0 + k];
+                    }
+#pragma unroll
+                for (uint32_t k = 0; k < GB; k++) {
+                    if (i0 + k >= cnt)
+                        break;
+                    const uint32_t i = i0 + k;
+                    const uint32_t pos = pbase + (uint32_t)__builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    if (PK) {
+                        typedef HitFields<true> HF;
+                        const uint64_t key = HF::key(h[k], h[k]);
+                        dst[2 * i] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), HF::otu(h[k], h[k]),
+                                                HF::avg(h[k]) | HF::flags(h[k]) << 16);
+                        dst[2 * i + 1] = make_uint4(HF::fi(h[k]), HF::wt(h[k]), pos, s + seq_base);
+                    } else {
+                        dst[2 * i] = make_uint4(c[k].x, c[k].y, c[k].z, h[k].x);
+                        dst[2 * i + 1] = make_uint4(h[k].y, h[k].z, pos, s + seq_base);
+                    }
                 }
             }
             done += __shfl(incl, 63);
@@ -1917,8 +1927,11 @@ __global__ __launch_bounds__(256) void gather_kernel(
 }
 
 /* small batches (<= SMALL_GATHER_SEQ sequences): small_collect and gather in
- * one workgroup -- the counts scanned into LDS (and into the caller's mapped
- * offsets), then four waves gather the sequences from those offsets */
+ * one launch -- every workgroup scans the counts into LDS (workgroup 0 also
+ * into the caller's mapped offsets), then its four waves gather sequences
+ * 4 b .. 4 b + 3 from those offsets (SMALL_GATHER_BLOCKS workgroups at most,
+ * striding); the workgroup that finishes last (a device counter, reset by
+ * it) stores the token */
 template <bool PK>
 __global__ __launch_bounds__(256) void small_gather_kernel(
     uint32_t n, const uint64_t *__restrict__ wbase, const uint64_t *__restrict__ hit_mask, uint32_t tile_windows,
@@ -1927,11 +1940,13 @@ __global__ __launch_bounds__(256) void small_gather_kernel(
     const kgx_otu *__restrict__ otus, kgx_hit *__restrict__ hits_out, kgx_call *__restrict__ calls_out,
     kgx_otu *__restrict__ otus_out, Offsets3 off_host, const uint32_t *__restrict__ status,
     const kgx_best_call *__restrict__ best, kgx_best_call *__restrict__ best_host, uint32_t *__restrict__ status_host,
-    uint64_t *__restrict__ nwin_host, uint32_t *done_host, uint32_t token)
+    uint64_t *__restrict__ nwin_host, uint32_t *done_host, uint32_t token, uint32_t *blocks_done)
 {
     __shared__ uint64_t lds4[3][4];
     __shared__ uint64_t lo[3][SMALL_GATHER_SEQ + 1];
+    __shared__ uint32_t last;
     const uint32_t t = threadIdx.x;
+    const bool first = blockIdx.x == 0;
     const uint32_t *cnt[3] = {hit_count, calls_out ? call_count : nullptr, otus_out ? otu_count : nullptr};
     for (int a = 0; a < 3; a++) {
         const uint64_t v = t < n && cnt[a] ? cnt[a][t] : 0;
@@ -1939,29 +1954,38 @@ __global__ __launch_bounds__(256) void small_gather_kernel(
         const uint64_t ex = block_scan(v, lds4[a], tot) - v;
         if (t < n) {
             lo[a][t] = ex;
-            off_host.o[a][t] = ex;
+            if (first)
+                off_host.o[a][t] = ex;
         }
         if (t == 0) {
             lo[a][n] = tot;
-            off_host.o[a][n] = tot;
+            if (first)
+                off_host.o[a][n] = tot;
         }
     }
-    if (best_host && t < n)
+    if (first && best_host && t < n)
         best_host[t] = best[t];
-    if (t == 0) {
+    if (first && t == 0) {
         status_host[0] = status[0];
         nwin_host[0] = wbase[n];
     }
     __syncthreads();
-    for (uint32_t s = t >> 6; s < n; s += 4)
+    for (uint32_t s = blockIdx.x * 4 + (t >> 6); s < n; s += 4 * gridDim.x)
         gather_one<PK>(s, wbase, hit_mask, tile_windows, call_count, hot, cold, calls, lo[0][s], lo[1][s], hits_out,
                        calls_out, 0u, otu_count, otus, lo[2][s], otus_out, nullptr, nullptr);
-    /* the batch's last word: every store above is visible to the host before
-     * the host sees done_host == token (it polls instead of a stream sync) */
+    /* the batch's last word: every store above, of every workgroup, is
+     * visible to the host before the host sees done_host == token (it polls
+     * instead of a stream sync) */
     if (done_host) {
         __threadfence_system();
         __syncthreads();
         if (t == 0) {
+            last = gridDim.x == 1 || atomicAdd(blocks_done, 1u) == gridDim.x - 1;
+            if (last && gridDim.x > 1)
+                *blocks_done = 0; /* for the next launch on this stream */
+        }
+        __syncthreads();
+        if (t == 0 && last) {
             __threadfence_system();
             *reinterpret_cast<volatile uint32_t *>(done_host) = token;
         }
@@ -1974,21 +1998,24 @@ hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t
                                const kgx_otu *otus, kgx_hit *hits_out, kgx_call *calls_out, kgx_otu *otus_out,
                                uint64_t *h0, uint64_t *h1, uint64_t *h2, const uint32_t *status,
                                const kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
-                               uint64_t *nwin_host, uint32_t *done_host, uint32_t token, uint32_t hit_format,
-                               hipStream_t stream)
+                               uint64_t *nwin_host, uint32_t *done_host, uint32_t token, uint32_t *blocks_done,
+                               uint32_t hit_format, hipStream_t stream)
 {
     if (n == 0 || n > SMALL_GATHER_SEQ)
         return hipErrorInvalidValue;
     const Offsets3 off_host = {{h0, h1, h2}};
+    /* one wave per sequence (blocks_done NULL: one workgroup) */
+    const uint32_t blocks = blocks_done ? std::min<uint32_t>((n + 3) / 4, SMALL_GATHER_BLOCKS) : 1u;
     if (hit_format == HIT_PACKED16)
-        hipLaunchKernelGGL(small_gather_kernel<true>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask, tile_windows,
-                           hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out, calls_out, otus_out,
-                           off_host, status, best, best_host, status_host, nwin_host, done_host, token);
+        hipLaunchKernelGGL(small_gather_kernel<true>, dim3(blocks), dim3(256), 0, stream, n, wbase, hit_mask,
+                           tile_windows, hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out, calls_out,
+                           otus_out, off_host, status, best, best_host, status_host, nwin_host, done_host, token,
+                           blocks_done);
     else
-        hipLaunchKernelGGL(small_gather_kernel<false>, dim3(1), dim3(256), 0, stream, n, wbase, hit_mask,
+        hipLaunchKernelGGL(small_gather_kernel<false>, dim3(blocks), dim3(256), 0, stream, n, wbase, hit_mask,
                            tile_windows, hit_count, call_count, hot, cold, calls, otu_count, otus, hits_out,
                            calls_out, otus_out, off_host, status, best, best_host, status_host, nwin_host,
-                           done_host, token);
+                           done_host, token, blocks_done);
     return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
  */
 #include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -40,6 +41,9 @@ struct kgx_pool {
     std::unique_ptr<kgx_hit[]> hits; /* grow-only (no zeroing of GBs per batch) */
     uint64_t hits_cap = 0;
     std::vector<kgx_hit_chunk> chunks; /* kgx_pool_process_batch_compact */
+    /* kgx_hit expansion of the shards' compact records (KGX_POOL_EXPAND_THREADS, default 16) */
+    std::unique_ptr<kgx::HostPool> xpool;
+    unsigned expand_threads = 16;
     std::vector<kgx_call> calls;
     std::vector<kgx_otu> otus;
     std::vector<kgx_best_call> best;
@@ -121,6 +125,8 @@ int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx,
         }
         p->ctxs.push_back(c);
     }
+    if (const char *e = std::getenv("KGX_POOL_EXPAND_THREADS"))
+        p->expand_threads = (unsigned)std::min(256L, std::max(1L, std::strtol(e, nullptr, 10)));
     for (uint32_t i = 0; i < n_ctx; i++)
         p->threads.emplace_back([p, i] { p->worker(i); });
     *out = p;
@@ -252,18 +258,32 @@ int pool_expand(kgx_pool *p, const PoolRun &R, const char *residues, const uint6
         p->hits.reset(new kgx_hit[nh + nh / 4]); /* grow-only, not initialised */
         p->hits_cap = nh + nh / 4;
     }
-    std::vector<int> rcs(R.K, KGX_OK);
-    std::vector<std::string> errs(R.K);
-    p->run(R.K, [&](uint32_t i) {
+    if (!nh)
+        return KGX_OK;
+    /* pieces of about nh / (4 T) hits, never across a shard, on the pool's
+     * expansion threads (the contexts' own threads are idle by now) */
+    if (!p->xpool)
+        p->xpool.reset(new HostPool(p->expand_threads));
+    const uint64_t piece = std::max<uint64_t>(4096, nh / (4ull * p->xpool->size()));
+    kgx_hit *base = p->hits.get();
+    for (uint32_t i = 0; i < R.K; i++) {
         const uint32_t s0 = R.cuts[i], n = R.cuts[i + 1] - R.cuts[i];
-        rcs[i] = kgx_compact_expand(&R.part[i], residues, seq_offsets + s0, 0, n, s0, p->hits.get() + R.hb[i]);
-        if (rcs[i])
-            errs[i] = kgx_last_error();
-    });
-    for (uint32_t i = 0; i < R.K; i++)
-        if (rcs[i])
-            return fail(rcs[i], "pool shard " + std::to_string(i) + " expansion: " + errs[i]);
-    return KGX_OK;
+        const uint64_t *ho = R.part[i].r.hit_offsets;
+        uint32_t a = 0;
+        while (a < n) {
+            const uint64_t target = ho[a] + piece;
+            uint32_t b = (uint32_t)(std::lower_bound(ho + a + 1, ho + n, target) - ho);
+            b = std::min(std::max(b, a + 1), n);
+            const kgx_compact_result *cr = &R.part[i];
+            kgx_hit *dst = base + R.hb[i] + ho[a];
+            p->xpool->submit([cr, residues, seq_offsets, s0, a, b, dst]() -> int {
+                return compact_expand(cr, residues, seq_offsets + s0, a, b, s0, dst, true);
+            });
+            a = b;
+        }
+    }
+    const int rc = p->xpool->wait();
+    return rc ? fail(rc, std::string("pool expansion: ") + kgx_last_error()) : KGX_OK;
 }
 
 }  // namespace

@@ -387,8 +387,18 @@ struct kgx_ctx {
      * blob, results stored into mapped memory: one host wait per batch */
     int64_t small_batch = 1 << 16;
     int small_wave = 1; /* small batches: the wave scorer instead of the hybrid (option "small_wave") */
+    int small_wave_tiles = 1; /* small batches: probe tiles per scorer wave (option "small_wave_tiles") */
     kgx::PinnedVec<uint4> h_small; /* offsets | window bases | tile owners | status | residues */
     kgx::PinnedVec<uint32_t> h_done; /* the fused small gather's completion token */
+    kgx::DevBuf small_blocks_done;    /* its workgroup counter (zero between launches) */
+    /* one-launch small batches (option "small_fused"; kgx_fused.hip): mapped
+     * window bases, per-sequence result regions, counts and tokens */
+    int small_fused = 0;
+    uint64_t fused_batches = 0, small_batches = 0; /* kgx_ctx_stat */
+    kgx::PinnedVec<uint64_t> h_fwb;
+    kgx::PinnedVec<kgx_hit> h_fhits;
+    kgx::PinnedVec<kgx_call> h_fcalls;
+    kgx::PinnedVec<uint32_t> h_fcounts, h_fdone;
     uint32_t small_token = 0;
     int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
     kgx::PinnedVec<kgx_call> h_calls_region;
@@ -418,6 +428,9 @@ namespace kgx {
  * kgx_hit.seq = s + seq_base; nt = streaming stores */
 int expand_chunk(const kgx_hit_chunk &ch, const uint64_t *hoff, const char *residues, const uint64_t *seq_offsets,
                  uint32_t a, uint32_t b, kgx_hit *out, uint64_t out_base, uint32_t seq_base, bool nt);
+/* kgx_compact_expand with a choice of streaming stores */
+int compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets, uint32_t s_begin,
+                   uint32_t s_end, uint32_t seq_base, kgx_hit *out, bool nt);
 }  // namespace kgx
 
 #endif

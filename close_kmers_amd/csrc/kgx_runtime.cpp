@@ -1029,6 +1029,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->probe_lds_kb = (int)value;
         return KGX_OK;
     }
+    if (n == "small_fused") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "small_fused must be 0 or 1");
+        c->small_fused = (int)value;
+        return KGX_OK;
+    }
+    if (n == "small_wave_tiles") {
+        if (value < 1 || value > 256)
+            return fail(KGX_EINVAL, "small_wave_tiles must be 1..256");
+        c->small_wave_tiles = (int)value;
+        return KGX_OK;
+    }
     if (n == "score_wave_tiles") {
         if (value < 1 || value > 256)
             return fail(KGX_EINVAL, "score_wave_tiles must be 1..256");
@@ -2300,6 +2312,112 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
 
 inline uint64_t round16(uint64_t bytes) { return (bytes + 15) & ~15ull; }
 
+/* whether a host batch can take the one-launch path (kgx_fused.hip) */
+bool fused_eligible(const kgx_ctx *c, const kgx_params &p, const uint64_t *seq_offsets, uint32_t n_seq,
+                    uint32_t want)
+{
+    if (!c->small_fused || c->img->layout != KGX_LAYOUT_PACKED16 || !c->img->d_packed || n_seq == 0 ||
+        n_seq > FUSED_MAX_SEQ || want == 0 || (want & ~(KGX_WANT_HITS | KGX_WANT_CALLS)) || p.order_constraint != 0 ||
+        p.min_hits < 1)
+        return false;
+    for (uint32_t s = 0; s < n_seq; s++)
+        if (windows_of(seq_offsets[s + 1] - seq_offsets[s]) > FUSED_MAX_WINDOWS)
+            return false;
+    return true;
+}
+
+/* A small host batch in ONE launch: one workgroup per sequence reads its
+ * residues from the pinned staging, probes, compacts, scores and stores its
+ * kgx_hit / kgx_call records into per-sequence regions of mapped memory
+ * (from the sequence's first window), then its count and a completion
+ * token; the host polls the tokens and packs the regions into the CSR
+ * result.  The device keeps no batch (kgx_kmap_add_hits needs another path:
+ * the option is for per-sequence callers, e.g. the facade's process_aa_seq). */
+int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, const uint64_t *seq_offsets,
+                        uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq);
+    if (rc)
+        return rc;
+    const uint64_t *off = c->h_off_stage.data();
+    HIP_TRY(c->h_fwb.resize(n_seq + 1));
+    uint64_t W = 0;
+    for (uint32_t s = 0; s < n_seq; s++) {
+        c->h_fwb[s] = W;
+        W += windows_of(off[s + 1] - off[s]);
+    }
+    c->h_fwb[n_seq] = W;
+    const bool need_hits = (want & KGX_WANT_HITS) != 0, want_calls = (want & KGX_WANT_CALLS) != 0;
+    HIP_TRY(c->h_fhits.resize(std::max<uint64_t>(W, 1)));
+    HIP_TRY(c->h_fcalls.resize(std::max<uint64_t>(W, 1)));
+    HIP_TRY(c->h_fcounts.resize(2 * (uint64_t)n_seq));
+    HIP_TRY(c->h_fdone.resize(n_seq));
+    HIP_TRY(c->h_res.resize(std::max<uint64_t>(c->h_res.size(), 1)));
+    void *d_res = nullptr, *d_off = nullptr, *d_wb = nullptr, *d_hits = nullptr, *d_calls = nullptr,
+         *d_counts = nullptr, *d_done = nullptr;
+    HIP_TRY(c->h_res.device_ptr(0, &d_res));
+    HIP_TRY(c->h_off_stage.device_ptr(0, &d_off));
+    HIP_TRY(c->h_fwb.device_ptr(0, &d_wb));
+    HIP_TRY(c->h_fhits.device_ptr(0, &d_hits));
+    HIP_TRY(c->h_fcalls.device_ptr(0, &d_calls));
+    HIP_TRY(c->h_fcounts.device_ptr(0, &d_counts));
+    HIP_TRY(c->h_fdone.device_ptr(0, &d_done));
+    const uint32_t token = ++c->small_token ? c->small_token : ++c->small_token;
+    HIP_TRY(launch_fused_small(static_cast<const uint8_t *>(d_res), static_cast<const uint64_t *>(d_off),
+                               static_cast<const uint64_t *>(d_wb), n_seq, want, c->img->d_packed, c->img->num_sigs, p,
+                               static_cast<kgx_hit *>(d_hits), static_cast<kgx_call *>(d_calls),
+                               static_cast<uint32_t *>(d_counts), static_cast<uint32_t *>(d_done), token, c->stream));
+    /* every sequence's token (stored after its results, behind a
+     * system-scope fence); a fault or a lost store still ends the wait */
+    const volatile uint32_t *done = c->h_fdone.data();
+    for (uint32_t s = 0; s < n_seq; s++)
+        for (uint32_t spin = 1; done[s] != token; spin++) {
+            if ((spin & 255u) == 0) {
+                const hipError_t q = hipStreamQuery(c->stream);
+                if (q == hipSuccess) {
+                    std::atomic_thread_fence(std::memory_order_acquire);
+                    if (done[s] != token)
+                        return fail(KGX_EDEVICE, "fused batch: sequence " + std::to_string(s) +
+                                                     " ended without its completion token");
+                    break;
+                }
+                if (q != hipErrorNotReady)
+                    HIP_TRY(q);
+            }
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    /* the regions -> the CSR result */
+    const uint32_t *cnt = c->h_fcounts.data();
+    c->h_hoff.assign(n_seq + 1, 0);
+    c->h_coff.assign(n_seq + 1, 0);
+    c->h_ooff.assign(n_seq + 1, 0);
+    for (uint32_t s = 0; s < n_seq; s++) {
+        const uint64_t w = c->h_fwb[s + 1] - c->h_fwb[s];
+        if (cnt[s] > w || cnt[n_seq + s] > w)
+            return fail(KGX_EDEVICE, "fused batch: more records than windows");
+        c->h_hoff[s + 1] = c->h_hoff[s] + cnt[s];
+        c->h_coff[s + 1] = c->h_coff[s] + (want_calls ? cnt[n_seq + s] : 0u);
+    }
+    HIP_TRY(c->h_hits.resize(need_hits ? c->h_hoff[n_seq] : 0));
+    HIP_TRY(c->h_calls.resize(c->h_coff[n_seq]));
+    HIP_TRY(c->h_otus.resize(0));
+    for (uint32_t s = 0; s < n_seq; s++) {
+        if (need_hits && cnt[s])
+            std::memcpy(c->h_hits.data() + c->h_hoff[s], c->h_fhits.data() + c->h_fwb[s], cnt[s] * sizeof(kgx_hit));
+        if (want_calls && cnt[n_seq + s])
+            std::memcpy(c->h_calls.data() + c->h_coff[s], c->h_fcalls.data() + c->h_fwb[s],
+                        cnt[n_seq + s] * sizeof(kgx_call));
+    }
+    c->have_hits = false; /* nothing of the batch stays on the device */
+    c->have_best = false;
+    c->have_otus = false;
+    fill_result(c, n_seq, need_hits, false, W, out);
+    return KGX_OK;
+}
+
 /* A small host batch (process_aa_seq's one sequence, a request's few) in one
  * host wait: the host writes the plan (window bases, tile owners, longest
  * sequence) beside the staged residues and offsets in one pinned blob, one
@@ -2380,11 +2498,16 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
      * sequence is the whole stage's latency (31 us for one 300-aa protein);
      * the wave scorer spreads each sequence's hits over a wave (option
      * small_wave; the lane machine still takes order_constraint 1) */
-    const int variant = c->score_variant;
+    const int variant = c->score_variant, wave_tiles = c->score_wave_tiles;
     if (c->small_wave && variant == SCORE_HYBRID) /* the host plan knows the longest sequence */
         c->score_variant = longest <= (uint32_t)RUN_CAP ? SCORE_WAVE_ONLY : SCORE_WAVE;
+    /* a wave walks the sequences that start in its tiles one after another:
+     * few tiles per wave (option small_wave_tiles) put a coalesced batch's
+     * sequences on different waves, scored at once */
+    c->score_wave_tiles = c->small_wave_tiles;
     rc = kgx_stage_score(c, params, want);
     c->score_variant = variant;
+    c->score_wave_tiles = wave_tiles;
     if (rc)
         return rc;
     /* results: worst-case mapped arrays, offsets and totals in mapped memory */
@@ -2426,6 +2549,10 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
         HIP_TRY(c->h_done.resize(1));
         c->h_done[0] = 0;
         HIP_TRY(c->h_done.device_ptr(0, &m_done));
+        if (!c->small_blocks_done.p) { /* the gather's workgroup counter, zero between launches */
+            HIP_TRY(c->small_blocks_done.reserve(sizeof(uint32_t)));
+            HIP_TRY(hipMemsetAsync(c->small_blocks_done.p, 0, sizeof(uint32_t), c->stream));
+        }
     }
     if (fused) { /* scan + gather in one workgroup */
         HIP_TRY(launch_small_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
@@ -2438,7 +2565,7 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                                     want_best ? c->best.as<kgx_best_call>() : nullptr,
                                     static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
                                     static_cast<uint64_t *>(m_nwin), static_cast<uint32_t *>(m_done), token,
-                                    c->hit_format, c->stream));
+                                    c->small_blocks_done.as<uint32_t>(), c->hit_format, c->stream));
     } else {
         HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(),
                                      want_calls ? c->call_count.as<uint32_t>() : nullptr, want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
@@ -2512,8 +2639,19 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     const uint32_t K = (uint32_t)std::min<uint64_t>({(uint64_t)c->host_chunks, k_res, (uint64_t)n_seq});
     if (K >= 2 && (want & (KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU | KGX_WANT_BEST)))
         return process_batch_chunked(c, params, residues, seq_offsets, n_seq, want, K, out);
-    if (n_seq && n_res <= (uint64_t)c->small_batch && n_seq <= (1u << 16))
+    if (n_seq && n_res <= (uint64_t)c->small_batch && n_seq <= (1u << 16)) {
+        kgx_params p;
+        if (params)
+            p = *params;
+        else
+            kgx_params_default(&p);
+        if (fused_eligible(c, p, seq_offsets, n_seq, want)) {
+            c->fused_batches++;
+            return process_batch_fused(c, p, residues, seq_offsets, n_seq, want, out);
+        }
+        c->small_batches++;
         return process_batch_small(c, params, residues, seq_offsets, n_seq, want, out);
+    }
     PhaseTimer tm(c);
     int rc = stage_host_seqs(c, residues, seq_offsets, 0, n_seq);
     if (rc)
@@ -2569,6 +2707,14 @@ int kgx_process_batch_compact(kgx_ctx *c, const kgx_params *params, const char *
 int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets,
                        uint32_t s_begin, uint32_t s_end, uint32_t seq_base, kgx_hit *out)
 {
+    return compact_expand(r, residues, seq_offsets, s_begin, s_end, seq_base, out, false);
+}
+
+}  // extern "C"
+
+int kgx::compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets,
+                        uint32_t s_begin, uint32_t s_end, uint32_t seq_base, kgx_hit *out, bool nt)
+{
     if (!r || s_begin > s_end || s_end > r->r.n_seq || !r->r.hit_offsets)
         return fail(KGX_EINVAL, "bad compact range");
     const uint64_t *hoff = r->r.hit_offsets;
@@ -2602,7 +2748,7 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
                 break;
         }
         const uint32_t b = std::min(ch->seq_end, s_end);
-        const int rc = expand_chunk(*ch, hoff, residues, seq_offsets, s, b, out, j0, seq_base, false);
+        const int rc = expand_chunk(*ch, hoff, residues, seq_offsets, s, b, out, j0, seq_base, nt);
         if (rc)
             return rc;
         s = b;
@@ -2610,6 +2756,24 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
     for (; s < s_end; s++)
         if (hoff[s + 1] != hoff[s])
             return fail(KGX_EINVAL, "compact hits: a sequence with hits outside every chunk");
+    return KGX_OK;
+}
+
+extern "C" {
+
+int kgx_ctx_stat(kgx_ctx *c, const char *name, int64_t *value)
+{
+    if (!c || !name || !value)
+        return fail(KGX_EINVAL, "null argument");
+    const std::string n = name;
+    if (n == "fused_batches")
+        *value = (int64_t)c->fused_batches;
+    else if (n == "small_batches")
+        *value = (int64_t)c->small_batches;
+    else if (n == "stream_fallbacks")
+        *value = (int64_t)c->stream_fallbacks;
+    else
+        return fail(KGX_EINVAL, "unknown statistic " + n);
     return KGX_OK;
 }
 

@@ -329,12 +329,24 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * off): a one-chunk batch of at most this many residues is planned on the
  * host, read by the device from mapped pinned staging and its results stored
  * into mapped memory -- one host wait, no DMA copy (process_aa_seq's
- * latency), scored by the wave scorer unless "small_wave" is 0.  Results are
+ * latency), scored by the wave scorer unless "small_wave" is 0, with "small_wave_tiles"
+ * (default 1) probe tiles per scorer wave.
+ * "small_fused" 1 (default 0): such a batch runs as ONE launch when the image
+ * is PACKED16, want is within HITS | CALLS, order_constraint is 0, min_hits
+ * >= 1 and no sequence has more than 2,048 windows -- one workgroup per
+ * sequence encodes, probes, scores and stores its records into mapped memory
+ * (kgx_fused.hip); nothing of the batch stays on the device, so it is for
+ * per-sequence callers (the facade's process_aa_seq), not for a batch that
+ * kgx_kmap_add_hits / kgx_matrix_add_hits reads.  Results are
  * identical under every setting.  After a
  * chunked batch the device results are split over the two contexts:
  * kgx_kmap_add_hits / kgx_matrix_add_hits need a one-pass batch (host_chunks
  * 1, or want 0, which never chunks) */
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
+/* counters of the context since its creation: "fused_batches" / "small_batches"
+ * (small host batches that took the one-launch path / the one-wait path),
+ * "stream_fallbacks" (streamed batches rerun exact after a region overflow) */
+int kgx_ctx_stat(kgx_ctx *ctx, const char *name, int64_t *value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
 

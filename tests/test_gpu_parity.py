@@ -924,6 +924,64 @@ def test_device_otu_tallies_match_oracle(gpu, oracle_lib, otu_range, layout):
                 assert n_otu.max() > 16  # the introsort path ran
 
 
+@pytest.mark.parametrize("params", PARAM_SETS)
+def test_fused_small_path_matches_oracle(small_world, oracle_lib, gpu, params):
+    """small_fused 1 (the facade's per-sequence calls): a small batch runs as
+    one launch, one workgroup per sequence (kgx_fused.hip), when its
+    parameters, outputs and lengths allow -- else the one-wait path.  Either
+    way the oracle's hits and calls, for one sequence, empties, sub-window,
+    X / * / lower case / NUL-cut sequences, a mid-buffer start, the
+    2,048-window boundary (2,056 aa fused, 2,057 aa not) and 300 sequences."""
+    spec, table, img, ctx = small_world
+    rng = np.random.default_rng(31)
+    res, off = synth.make_queries(spec, 60, x_permille=5, q0=4242)
+    seqs = [res[int(off[i]):int(off[i + 1])].copy() for i in range(60)]
+    seqs[3][40] = 0  # NUL cut
+    seqs[4][17] = ord("x")
+    seqs[5][100] = ord("*")
+    planted, poff = synth.make_queries(spec, 40, x_permille=0, q0=9000)
+    edge = [np.concatenate([planted[int(poff[i]):int(poff[i + 1])] for i in range(2 * k, 2 * k + 7)])[:n]
+            for k, n in enumerate((2056, 2057))]
+    res2, off2 = synth.make_queries(spec, 300, x_permille=5, q0=6000)
+    many = [res2[int(off2[i]):int(off2[i]) + int(k)] for i, k in enumerate(rng.integers(0, 400, 300))]
+    batches = [seqs[:1], seqs[1:2] + [np.zeros(0, np.uint8)], [np.zeros(0, np.uint8)] + seqs[2:20],
+               [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], edge[:1], edge[1:], edge + seqs[:4],
+               many]
+    p = gpu.Params(*params)
+    eligible = params[2] == 0 and params[0] >= 1
+    ctx.set_option("small_fused", 1)
+    try:
+        for b in batches:
+            lens = np.array([0] + [len(x) for x in b], np.uint64)
+            boff = np.cumsum(lens).astype(np.uint64) + np.uint64(3)
+            bres = np.concatenate([np.frombuffer(b"MKV", np.uint8)] + list(b))
+            want = oracle_lib.process_batch(table, bres, boff, params=params)
+            fits = eligible and all(max(0, len(x) - 8) <= 2048 for x in b)
+            for w in (3, 1, 2):
+                f0 = ctx.stat("fused_batches")
+                got = ctx.process_batch(bres, boff, p, want=w)
+                assert ctx.stat("fused_batches") - f0 == (1 if fits else 0), (w, [len(x) for x in b][:5])
+                assert got.n_windows == int(np.maximum(lens[1:].astype(np.int64) - 8, 0).sum())
+                assert np.array_equal(got.hit_offsets, want.hit_offsets)
+                if w & 1:
+                    assert eq_fields(got.hits, want.hits)
+                    assert not got.hits["flags"].any()
+                if w & 2:
+                    assert np.array_equal(got.call_offsets, want.call_offsets)
+                    for f in ["start", "end", "count", "function_index"]:
+                        assert np.array_equal(got.calls[f], want.calls[f]), f
+                    assert np.array_equal(got.calls["weighted_hits"].view(np.uint32),
+                                          want.calls["weighted_hits"].view(np.uint32))
+                else:
+                    assert not got.call_offsets.any()
+            # OTU / best calls are never fused; the results stay the oracle's
+            f0 = ctx.stat("fused_batches")
+            assert_same(ctx.process_batch(bres, boff, p, want=7), want, len(b))
+            assert ctx.stat("fused_batches") == f0
+    finally:
+        ctx.set_option("small_fused", 0)
+
+
 @pytest.mark.parametrize("params", PARAM_SETS[:4])
 def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu, params):
     """Batches of <= small_batch residues (the facade's process_aa_seq) take

@@ -32,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-keys", type=float, default=1e9)
     ap.add_argument("--n-calls", type=int, default=2000)
+    ap.add_argument("--prof", default="", help="run the tool under rocprofv3 --kernel-trace --stats, output dir")
     args = ap.parse_args()
     from close_kmers_amd import image_files, synth
     tool = build_tool()
@@ -43,8 +44,10 @@ def main():
         q = os.path.join(d, "queries.bin")
         with open(q, "wb") as f:
             f.write(np.uint64(len(off) - 1).tobytes() + off.astype(np.uint64).tobytes() + res.tobytes())
-        r = subprocess.run([tool, d, str(spec.n_keys), str(spec.num_sigs), q, str(args.n_calls)],
-                           capture_output=True, text=True)
+        cmd = [tool, d, str(spec.n_keys), str(spec.num_sigs), q, str(args.n_calls)]
+        if args.prof:  # the tool itself after --: the profiler's library initialises the GPU
+            cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", args.prof, "-o", "facade", "--"] + cmd
+        r = subprocess.run(cmd, capture_output=True, text=True)
         sys.stderr.write(r.stderr)
         if r.returncode != 0:
             raise SystemExit(f"facade_bench exited {r.returncode}: {r.stdout}")

@@ -53,14 +53,17 @@ int main(int argc, char **argv)
         std::fprintf(stderr, "facade_bench: short query file\n");
         return 2;
     }
+    /* the bench's image: n_keys distinct keys stored (bench.py C2) */
     kgx_image *img = nullptr;
-    uint64_t stored = 0;
-    if (kgx_image_build_synthetic(n_keys, num_sigs, 0, &img, &stored) != KGX_OK) {
+    uint64_t entries = 0;
+    const uint64_t stored = n_keys;
+    if (kgx_image_build_synthetic_distinct(n_keys, n_keys, num_sigs, 0, &img, &entries) != KGX_OK) {
         std::fprintf(stderr, "facade_bench: %s\n", kgx_last_error());
         return 1;
     }
     auto image = std::make_shared<kgx::KmerImage>(img);
     kgx::KmerGuts kg(dir, image);
+    kg.coalesce = false; /* the single-thread latencies: one pass per call */
     const size_t m = std::min<size_t>(n, n_calls);
     std::vector<std::string> seqs(m);
     for (size_t i = 0; i < m; i++)
@@ -119,56 +122,108 @@ int main(int argc, char **argv)
     }
     const double t_batch = pct(tb, 50);
 
-    /* the worker pool: T threads, one KmerGuts (context) each, per-sequence calls */
+    /* one pass's latency by batch size (process_aa_batch of k proteins, one
+     * thread): what a coalesced pass of k concurrent calls costs */
+    std::string bs_json;
+    /* KGX_FACADE_BATCH=k: only this pass size, and no thread sweep (kernel traces) */
+    const char *only = std::getenv("KGX_FACADE_BATCH");
+    std::vector<size_t> sizes = {1, 2, 4, 8, 16, 32, 64};
+    if (only)
+        sizes = {(size_t)std::strtoull(only, nullptr, 10)};
+    for (size_t k : sizes) {
+        std::vector<double> lt;
+        for (int rep = 0; rep < 200; rep++) {
+            std::vector<kgx::KmerGuts::SeqJob> jobs(k);
+            for (size_t i = 0; i < k; i++) {
+                jobs[i].id = "q";
+                jobs[i].seq = seqs[(rep * k + i) % m];
+                jobs[i].calls = std::make_shared<std::vector<kgx::KmerCall>>();
+                jobs[i].hit_cb = [](kgx::KmerGuts::hit_in_sequence_t) {};
+            }
+            const auto t0 = clk::now();
+            kg.process_aa_batch(jobs);
+            if (rep >= 20)
+                lt.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+        }
+        char b[120];
+        std::snprintf(b, sizeof b, "%s\"%zu\": {\"p50_us\": %.1f, \"p99_us\": %.1f}", bs_json.empty() ? "" : ", ", k,
+                      pct(lt, 50), pct(lt, 99));
+        bs_json += b;
+        std::fprintf(stderr, "[facade] pass of %zu proteins: p50 %.1f us, p99 %.1f us\n", k, pct(lt, 50), pct(lt, 99));
+    }
+
+    /* the worker pool: T threads, one KmerGuts (context) each, per-sequence
+     * calls; concurrent calls coalesced into shared passes (the default) or
+     * one pass per call */
     std::string pool_json;
     bool pool_ok = true;
-    for (int T : {1, 4, 8, 16}) {
-        std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
-        for (int t = 0; t < T; t++)
-            kgs.emplace_back(new kgx::KmerGuts(dir, image));
-        std::vector<uint64_t> th_hits(T, 0);
-        auto work = [&](int t, bool count) {
-            for (size_t i = (size_t)t; i < m; i += (size_t)T) {
-                auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
-                uint64_t h = 0;
-                kgs[t]->process_aa_seq("q", seqs[i], cv, [&h](kgx::KmerGuts::hit_in_sequence_t) { h++; }, nullptr);
-                if (count)
-                    th_hits[t] += h;
+    for (int co = 1; co >= 0 && !only; co--)
+        for (int T : {1, 4, 8, 16, 32}) {
+            std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
+            for (int t = 0; t < T; t++) {
+                kgs.emplace_back(new kgx::KmerGuts(dir, image));
+                kgs.back()->coalesce = co != 0;
             }
-        };
-        { /* warm: buffer growth on every context */
+            std::vector<uint64_t> th_hits(T, 0);
+            std::vector<std::vector<double>> th_lat(T);
+            auto work = [&](int t, bool count) {
+                for (size_t i = (size_t)t; i < m; i += (size_t)T) {
+                    auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+                    uint64_t h = 0;
+                    const auto q0 = clk::now();
+                    kgs[t]->process_aa_seq("q", seqs[i], cv, [&h](kgx::KmerGuts::hit_in_sequence_t) { h++; },
+                                           nullptr);
+                    if (count) {
+                        th_lat[t].push_back(std::chrono::duration<double, std::micro>(clk::now() - q0).count());
+                        th_hits[t] += h;
+                    }
+                }
+            };
+            { /* warm: buffer growth on every context */
+                std::vector<std::thread> ws;
+                for (int t = 0; t < T; t++)
+                    ws.emplace_back(work, t, false);
+                for (auto &w : ws)
+                    w.join();
+            }
+            const uint64_t passes0 = image->coalescer().passes, calls0 = image->coalescer().calls;
+            const auto t0 = clk::now();
             std::vector<std::thread> ws;
             for (int t = 0; t < T; t++)
-                ws.emplace_back(work, t, false);
+                ws.emplace_back(work, t, true);
             for (auto &w : ws)
                 w.join();
+            const double tp = std::chrono::duration<double>(clk::now() - t0).count();
+            uint64_t ph = 0;
+            std::vector<double> all;
+            for (int t = 0; t < T; t++) {
+                ph += th_hits[t];
+                all.insert(all.end(), th_lat[t].begin(), th_lat[t].end());
+            }
+            pool_ok = pool_ok && ph == hits;
+            const uint64_t np = image->coalescer().passes - passes0, nc = image->coalescer().calls - calls0;
+            char b[400];
+            std::snprintf(b, sizeof b,
+                          "%s\"%s%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g, \"p50_us\": %.1f, "
+                          "\"p99_us\": %.1f, \"calls_per_pass\": %.2f}",
+                          pool_json.empty() ? "" : ", ", co ? "coalesced_T" : "per_call_T", T, (double)m / tp,
+                          (double)residues / tp, pct(all, 50), pct(all, 99), np ? (double)nc / (double)np : 1.0);
+            pool_json += b;
+            std::fprintf(stderr, "[facade] %s T=%d: %.4g calls/s, %.4g residues/s, p50 %.1f us, p99 %.1f us\n",
+                         co ? "coalesced" : "per-call", T, (double)m / tp, (double)residues / tp, pct(all, 50),
+                         pct(all, 99));
         }
-        const auto t0 = clk::now();
-        std::vector<std::thread> ws;
-        for (int t = 0; t < T; t++)
-            ws.emplace_back(work, t, true);
-        for (auto &w : ws)
-            w.join();
-        const double tp = std::chrono::duration<double>(clk::now() - t0).count();
-        uint64_t ph = 0;
-        for (uint64_t h : th_hits)
-            ph += h;
-        pool_ok = pool_ok && ph == hits;
-        char b[160];
-        std::snprintf(b, sizeof b, "%s\"%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g}", pool_json.empty() ? "" : ", ",
-                      T, (double)m / tp, (double)residues / tp);
-        pool_json += b;
-    }
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
                 "\"latency_us_ordinary_path\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f}, "
                 "\"unbatched_residues_per_s\": %.4g, \"batched\": {\"sequences\": %zu, \"ms\": %.3f, "
                 "\"residues_per_s\": %.4g}, \"hits\": %llu, \"calls_out\": %llu, \"batch_hits_per_rep\": %llu, "
-                "\"batch_calls\": %llu, \"keys_stored\": %llu, \"worker_pool_by_threads\": {%s}}\n",
+                "\"batch_calls\": %llu, \"keys_stored\": %llu, \"pass_latency_by_batch\": {%s}, "
+                "\"worker_pool_by_threads\": {%s}}\n",
                 m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, pct(lat0, 50), pct(lat0, 90),
                 pct(lat0, 99), (double)residues / t_seq, m,
                 t_batch * 1e3, (double)residues / t_batch, (unsigned long long)hits, (unsigned long long)calls,
                 (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored,
-                pool_json.c_str());
+                bs_json.c_str(), pool_json.c_str());
     return hits * 6 == bhits && calls == bcalls && hits == hits0 && calls == calls0 && pool_ok ? 0 : 3;
 }
