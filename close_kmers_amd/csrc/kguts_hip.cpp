@@ -31,6 +31,47 @@ const char kResidues[21] = "ACDEFGHIKLMNPQRSTVWY";
 }
 }  // namespace
 
+/* ---- stage clocks -------------------------------------------------------------- */
+
+namespace {
+uint64_t now_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+}  // namespace
+
+StageStats &stage_stats()
+{
+    static StageStats s;
+    return s;
+}
+
+void StageStats::reset()
+{
+    for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &handle_ns, &send_ns})
+        a->store(0);
+}
+
+std::string StageStats::json() const
+{
+    char b[512];
+    const double r = (double)std::max<uint64_t>(1, requests.load());
+    std::snprintf(b, sizeof b,
+                  "{\"requests\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, \"gpu_passes\": %llu, "
+                  "\"ms_per_request\": {\"recv\": %.4f, \"parse\": %.4f, \"gpu\": %.4f, \"handle\": %.4f, "
+                  "\"send\": %.4f}}\n",
+                  (unsigned long long)requests.load(), (unsigned long long)bytes_in.load(),
+                  (unsigned long long)bytes_out.load(), (unsigned long long)gpu_passes.load(), recv_ns.load() / r * 1e-6,
+                  parse_ns.load() / r * 1e-6, gpu_ns.load() / r * 1e-6, handle_ns.load() / r * 1e-6,
+                  send_ns.load() / r * 1e-6);
+    return b;
+}
+
+StageClock::StageClock(std::atomic<uint64_t> &acc) : acc_(acc), t0_(now_ns()) {}
+StageClock::~StageClock() { acc_ += now_ns() - t0_; }
+
 /* ---- KmerOtuStats ----------------------------------------------------------- */
 
 void KmerOtuStats::write(FILE *fh) const
@@ -168,7 +209,12 @@ void KmerGuts::process_aa_batch(std::vector<SeqJob> &jobs)
     /* compact hits: each sequence's hit_in_sequence_t are built as its
      * callbacks replay (no 32-B record per hit for the whole batch) */
     kgx_compact_result cr;
-    int rc = kgx_process_batch_compact(ctx_, &p, buf.data(), off.data(), n, want, &cr);
+    int rc;
+    {
+        StageClock clk(stage_stats().gpu_ns);
+        rc = kgx_process_batch_compact(ctx_, &p, buf.data(), off.data(), n, want, &cr);
+    }
+    stage_stats().gpu_passes++;
     if (rc)
         throw_last(rc, "kgx_process_batch_compact");
     const kgx_result &r = cr.r;
@@ -216,14 +262,36 @@ SeqCoalescer::SeqCoalescer()
         max_inflight = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("KGX_COALESCE_RESIDUES"))
         max_residues = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+    if (const char *e = std::getenv("KGX_COALESCE_SPIN_US"))
+        spin_us = std::max(0, std::atoi(e));
 }
 
 void SeqCoalescer::submit(kgx_ctx *ctx, Req &r)
 {
-    std::unique_lock<std::mutex> lk(mu_);
-    queue_.push_back(&r);
-    while (!r.done) {
-        if (inflight_ < max_inflight && !queue_.empty()) {
+    using clock = std::chrono::steady_clock;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        queue_.push_back(&r);
+        queued_.store(queue_.size(), std::memory_order_relaxed);
+    }
+    /* a waiter spins (a pass takes tens of us; a futex wake-up costs several)
+     * and sleeps only after spin_us; it wakes for its own result or to lead */
+    const auto spin_end = clock::now() + std::chrono::microseconds(spin_us);
+    for (uint32_t spin = 0;; spin++) {
+        if (r.done.load(std::memory_order_acquire))
+            return;
+        const bool can_lead = inflight_.load(std::memory_order_relaxed) < max_inflight &&
+                              queued_.load(std::memory_order_relaxed) > 0;
+        if (!can_lead && ((spin & 63u) != 0 || clock::now() < spin_end)) {
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+            continue;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        if (r.done.load(std::memory_order_acquire))
+            return;
+        if (inflight_.load(std::memory_order_relaxed) < max_inflight && !queue_.empty()) {
             /* lead a pass: the queue's head and every queued call with the
              * same parameters, in arrival order, up to max_residues */
             std::vector<Req *> batch;
@@ -242,19 +310,33 @@ void SeqCoalescer::submit(kgx_ctx *ctx, Req &r)
                     ++it;
                 }
             }
-            inflight_++;
+            queued_.store(queue_.size(), std::memory_order_relaxed);
+            inflight_.fetch_add(1, std::memory_order_relaxed);
             lk.unlock();
             run_batch(ctx, batch);
             lk.lock();
-            inflight_--;
+            inflight_.fetch_sub(1, std::memory_order_relaxed);
             passes++;
             calls += batch.size();
-            for (Req *q : batch)
-                q->done = true;
-            cv_.notify_all();
-        } else {
-            cv_.wait(lk);
+            /* the callers served, and a sleeping queue head to lead the next
+             * pass (spinning callers see the flags themselves) */
+            for (Req *q : batch) {
+                q->done.store(true, std::memory_order_release);
+                if (q->sleeping)
+                    q->cv.notify_one();
+            }
+            if (!queue_.empty() && queue_.front()->sleeping)
+                queue_.front()->cv.notify_one();
+            continue;
         }
+        if (clock::now() < spin_end)
+            continue; /* someone else leads: keep spinning */
+        r.sleeping = true;
+        r.cv.wait(lk, [&] {
+            return r.done.load(std::memory_order_acquire) ||
+                   (inflight_.load(std::memory_order_relaxed) < max_inflight && !queue_.empty());
+        });
+        r.sleeping = false;
     }
 }
 
@@ -1076,8 +1158,10 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
     kgx_result r;
     /* find_best_call runs on the device (KGX_WANT_BEST): only its decision
      * per sequence comes back, not the calls */
+    const uint64_t g0 = now_ns(); /* gpu stage: the pass and the k-mer table lookups */
     int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n,
                                KGX_WANT_HITS | (want_calls ? KGX_WANT_BEST : 0), &r);
+    stage_stats().gpu_passes++;
     if (rc)
         throw_last(rc, "kgx_process_batch");
     /* the on_hit lists of every hit: kmer_to_family_id_ or kmer_to_id_ */
@@ -1097,6 +1181,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
         if (rc)
             throw_last(rc, "kgx_kmap_lookup");
     }
+    stage_stats().gpu_ns += now_ns() - g0;
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
     for (uint32_t s = 0; s < n; s++) {
         const std::string &id = work[s].first;

@@ -15,6 +15,7 @@
 #ifndef KGUTS_HIP_H
 #define KGUTS_HIP_H
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
@@ -32,6 +33,35 @@
 #include "kgx.h"
 
 namespace kgx {
+
+/*
+ * Request-path stage clocks (kgx_server's GET /server_stats): nanoseconds
+ * summed over every thread that spent them -- recv / send / handle by the
+ * connection threads, parse by the router, gpu by the facade around each GPU
+ * pass (host buffers in, results on the host: staging, H2D, kernels, D2H)
+ * and the k-mer table lookups; handle - parse - gpu is the host rollups and
+ * the text output.  A large /query's pieces run on several workers at once,
+ * so their gpu time can add up to more than the request's handle time.
+ */
+struct StageStats {
+    std::atomic<uint64_t> requests{0}, bytes_in{0}, bytes_out{0}, gpu_passes{0};
+    std::atomic<uint64_t> recv_ns{0}, parse_ns{0}, gpu_ns{0}, handle_ns{0}, send_ns{0};
+    void reset();
+    std::string json() const;
+};
+StageStats &stage_stats();
+/* adds the scope's wall time to one clock */
+class StageClock {
+public:
+    explicit StageClock(std::atomic<uint64_t> &acc);
+    ~StageClock();
+    StageClock(const StageClock &) = delete;
+    StageClock &operator=(const StageClock &) = delete;
+
+private:
+    std::atomic<uint64_t> &acc_;
+    uint64_t t0_;
+};
 
 class Error : public std::runtime_error {
 public:
@@ -79,9 +109,10 @@ public:
  * another pass is in flight are queued and run together: a caller that finds
  * fewer than max_inflight passes running becomes the leader, takes every
  * queued call with its parameters (up to max_residues residues) and runs them
- * as one batch on its own context; each caller blocks until its slice is
- * done, then replays its hit_cb / calls / OTU stats on its own thread, in
- * position order, before returning (kguts.cc:814-815, 888-908).
+ * as one batch on its own context; each caller waits until its slice is
+ * done (spinning first, then sleeping), then replays its hit_cb / calls /
+ * OTU stats on its own thread, in position order, before returning
+ * (kguts.cc:814-815, 888-908).
  */
 class SeqCoalescer {
 public:
@@ -96,9 +127,11 @@ public:
         kgx_params params{};
         uint32_t want = 0;
         Slice out;
-        bool done = false;
+        std::atomic<bool> done{false};
         int rc = KGX_OK;
         std::string err;
+        bool sleeping = false;      /* under the queue's mutex */
+        std::condition_variable cv; /* a sleeping caller's wake-up: done, or lead the next pass */
     };
     /* max_inflight / max_residues from KGX_COALESCE_INFLIGHT /
      * KGX_COALESCE_RESIDUES when set */
@@ -106,17 +139,18 @@ public:
     /* runs r on ctx, joining whatever is queued meanwhile; returns when r is
      * done (its slice filled, or r.rc set) */
     void submit(kgx_ctx *ctx, Req &r);
-    int max_inflight = 2;
+    int max_inflight = 8;
     uint64_t max_residues = 1 << 16;
+    int spin_us = 200; /* a waiting caller spins this long before it sleeps */
     /* statistics: passes run and calls served */
     uint64_t passes = 0, calls = 0;
 
 private:
     void run_batch(kgx_ctx *ctx, std::vector<Req *> &batch);
     std::mutex mu_;
-    std::condition_variable cv_;
     std::deque<Req *> queue_;
-    int inflight_ = 0;
+    std::atomic<size_t> queued_{0};   /* queue_.size(), for spinning callers */
+    std::atomic<int> inflight_{0};
 };
 
 /* KmerImage (kmer_image.h:25-39): the read-only signature table, resident in

@@ -45,30 +45,76 @@ struct FusedArgs {
     uint32_t *counts; /* mapped: hit count of s at [s], call count at [n + s] */
     uint32_t *done;   /* mapped: done[s] = token once s's results are visible */
     uint32_t token;
+    uint64_t *dbg; /* mapped, or NULL: wall-clock stamps of workgroup 0's phases */
 };
 
-constexpr uint32_t FJ = FUSED_MAX_WINDOWS / 256; /* windows per thread, at most */
+/* a batch small enough to travel in the kernel arguments themselves
+ * (offsets, window bases, residues): the kernel then reads nothing over PCIe
+ * before it probes */
+struct FusedInline {
+    uint32_t off[FUSED_INLINE_SEQ + 1];
+    uint32_t wb[FUSED_INLINE_SEQ + 1];
+    uint8_t res[FUSED_INLINE_RES];
+};
+struct FusedMapped { /* the mapped arrays instead (FusedArgs.res / off / wbase) */
+};
 
+/* FJ = windows per thread at most (the batch's longest sequence has at most
+ * 256 FJ windows): 2 for proteins up to 520 aa, 8 up to FUSED_MAX_WINDOWS */
+template <uint32_t FJ, class IN>
+__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k);
+
+template <uint32_t FJ>
 __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
 {
+    fused_small_body<FJ>(a, FusedMapped{});
+}
+
+template <uint32_t FJ>
+__global__ __launch_bounds__(256) void fused_small_inline_kernel(FusedArgs a, FusedInline k)
+{
+    fused_small_body<FJ>(a, k);
+}
+
+template <class IN> struct FusedInput;
+template <> struct FusedInput<FusedMapped> {
+    __device__ static uint64_t off(const FusedArgs &a, const FusedMapped &, uint32_t i) { return a.off[i]; }
+    __device__ static uint64_t wb(const FusedArgs &a, const FusedMapped &, uint32_t i) { return a.wbase[i]; }
+    __device__ static uint8_t res(const FusedArgs &a, const FusedMapped &, uint64_t i) { return a.res[i]; }
+};
+template <> struct FusedInput<FusedInline> {
+    __device__ static uint64_t off(const FusedArgs &, const FusedInline &k, uint32_t i) { return k.off[i]; }
+    __device__ static uint64_t wb(const FusedArgs &, const FusedInline &k, uint32_t i) { return k.wb[i]; }
+    __device__ static uint8_t res(const FusedArgs &, const FusedInline &k, uint64_t i) { return k.res[i]; }
+};
+
+template <uint32_t FJ, class IN>
+__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k)
+{
+    typedef FusedInput<IN> In;
+    const bool dbg = a.dbg && blockIdx.x == 0 && threadIdx.x == 0;
+    if (dbg)
+        a.dbg[0] = wall_clock64();
     __shared__ uint8_t code_tab[256];
-    __shared__ uint8_t codes[FUSED_MAX_WINDOWS + 8];
-    __shared__ uint4 hrec[FUSED_MAX_WINDOWS];
-    __shared__ uint32_t hpos[FUSED_MAX_WINDOWS];
+    __shared__ uint8_t codes[256 * FJ + 8];
+    __shared__ uint4 hrec[256 * FJ];
+    __shared__ uint32_t hpos[256 * FJ];
     __shared__ uint32_t wave_cnt[4];
     typedef HitFields<true> HF;
 
     const uint32_t s = blockIdx.x;
     const uint32_t t = threadIdx.x, lane = lane_id(), wave = t >> 6;
     code_tab[t] = (uint8_t)residue_code(t);
-    const uint64_t r0 = a.off[s], len = a.off[s + 1] - r0;
-    const uint64_t wb = a.wbase[s];
+    const uint64_t r0 = In::off(a, k, s), len = In::off(a, k, s + 1) - r0;
+    const uint64_t wb = In::wb(a, k, s);
     const uint32_t W = (uint32_t)windows_of(len);
     __syncthreads();
     /* 1. residues -> codes (each wave reads 64 consecutive bytes per round) */
     for (uint32_t i = t; i < W + 8 && i < len; i += 256)
-        codes[i] = code_tab[a.res[r0 + i]];
+        codes[i] = code_tab[In::res(a, k, r0 + i)];
     __syncthreads();
+    if (dbg)
+        a.dbg[1] = wall_clock64();
 
     /* 2. encode + probe: thread t owns windows t + 256 j */
     const uint32_t J = (W + 255) / 256;
@@ -93,32 +139,60 @@ __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
             slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
         }
     }
-    /* linear probe rounds, every pending window's bucket in flight at once;
-     * bounded by num_sigs buckets where the reference would spin forever */
-    for (uint64_t round = 0;; round++) {
-        uint4 pv[FJ];
+    /* linear probe by 64-B lines: a round reads the rest of the line holding
+     * each pending window's next bucket (the table is 256-B aligned, 4
+     * records per line), all of a thread's windows in flight at once, and
+     * examines those buckets in probe order -- a chain costs one round per
+     * line it touches instead of one per bucket (reading the next line too,
+     * speculatively, measured slower: 6.8 vs 4.6 us for one protein).
+     * Bounded by num_sigs buckets where the reference would spin forever. */
+    constexpr uint32_t R = 4; /* records per round: one line */
+    uint64_t examined[FJ];
 #pragma unroll
-        for (uint32_t j = 0; j < FJ; j++)
-            if (pend[j])
-                pv[j] = a.table[slot[j]];
+    for (uint32_t j = 0; j < FJ; j++)
+        examined[j] = 0;
+    const uint64_t NS = a.num_sigs;
+    for (;;) {
+        uint4 pv[FJ][R];
+#pragma unroll
+        for (uint32_t j = 0; j < FJ; j++) {
+            const uint64_t base = slot[j] & ~3ull;
+#pragma unroll
+            for (uint32_t q = 0; q < R; q++)
+                if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
+                    pv[j][q] = a.table[base + q];
+        }
         bool more = false;
 #pragma unroll
         for (uint32_t j = 0; j < FJ; j++) {
-            const uint64_t kv = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
-            const bool m = pend[j] && kv == key[j];
-            const bool stop = kv > MAX_ENCODED || round + 1 >= a.num_sigs;
-            rec[j].x = m ? pv[j].x : rec[j].x;
-            rec[j].y = m ? pv[j].y : rec[j].y;
-            rec[j].z = m ? pv[j].z : rec[j].z;
-            rec[j].w = m ? pv[j].w : rec[j].w;
-            hit[j] = hit[j] || m;
-            pend[j] = pend[j] && !m && !stop;
-            slot[j] = pend[j] ? (slot[j] + 1 == a.num_sigs ? 0 : slot[j] + 1) : slot[j];
-            more = more || pend[j];
+            const uint64_t base = slot[j] & ~3ull;
+            bool live = pend[j]; /* still searching within this line */
+#pragma unroll
+            for (uint32_t q = 0; q < R; q++) {
+                const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
+                const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
+                const bool m = in && kv == key[j];
+                const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
+                rec[j].x = m ? pv[j][q].x : rec[j].x;
+                rec[j].y = m ? pv[j][q].y : rec[j].y;
+                rec[j].z = m ? pv[j][q].z : rec[j].z;
+                rec[j].w = m ? pv[j][q].w : rec[j].w;
+                hit[j] = hit[j] || m;
+                examined[j] += in ? 1u : 0u;
+                live = live && !stop;
+            }
+            /* not resolved in this line: on at the next one (wrapping at
+             * the table's end, where the round's loads stopped) */
+            const uint64_t next = base + R >= NS ? 0 : base + R;
+            pend[j] = live;
+            slot[j] = live ? next : slot[j];
+            more = more || live;
         }
         if (!__syncthreads_or(more))
             break;
     }
+    if (dbg)
+        a.dbg[2] = wall_clock64();
 
     /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
     uint32_t nh = 0;
@@ -148,6 +222,8 @@ __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
         nh += total;
         __syncthreads();
     }
+    if (dbg)
+        a.dbg[3] = wall_clock64();
 
     /* 4a. kgx_hit records into the caller's mapped region (kguts.h:228-233) */
     if (a.want & KGX_WANT_HITS)
@@ -300,6 +376,8 @@ __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
         ncalls_out = o_ncalls;
     }
 
+    if (dbg)
+        a.dbg[4] = wall_clock64();
     /* 5. counts, then the token: every store above is visible to the host
      * before it sees done[s] == token */
     if (t == 0) {
@@ -310,6 +388,8 @@ __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
     __syncthreads();
     if (t == 0) {
         __threadfence_system();
+        if (dbg)
+            a.dbg[5] = wall_clock64();
         *reinterpret_cast<volatile uint32_t *>(a.done + s) = a.token;
     }
 }
@@ -317,7 +397,8 @@ __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
 hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uint64_t *wbase, uint32_t n,
                               uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
                               kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
-                              hipStream_t stream)
+                              uint32_t max_windows, uint64_t *dbg, const uint64_t *h_off, const uint64_t *h_wbase,
+                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream)
 {
     if (n == 0)
         return hipSuccess;
@@ -338,7 +419,28 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
     a.counts = counts;
     a.done = done;
     a.token = token;
-    hipLaunchKernelGGL(fused_small_kernel, dim3(n), dim3(256), 0, stream, a);
+    a.dbg = dbg;
+    if (max_windows > FUSED_MAX_WINDOWS)
+        return hipErrorInvalidValue;
+    const bool small = max_windows <= 2 * 256;
+    if (inline_res) { /* offsets, window bases and residues in the kernel arguments */
+        if (n > FUSED_INLINE_SEQ || inline_res > FUSED_INLINE_RES)
+            return hipErrorInvalidValue;
+        FusedInline k;
+        for (uint32_t i = 0; i <= n; i++) {
+            k.off[i] = (uint32_t)h_off[i];
+            k.wb[i] = (uint32_t)h_wbase[i];
+        }
+        __builtin_memcpy(k.res, h_res, inline_res);
+        if (small)
+            hipLaunchKernelGGL(fused_small_inline_kernel<2>, dim3(n), dim3(256), 0, stream, a, k);
+        else
+            hipLaunchKernelGGL(fused_small_inline_kernel<FUSED_MAX_WINDOWS / 256>, dim3(n), dim3(256), 0, stream, a, k);
+    } else if (small) {
+        hipLaunchKernelGGL(fused_small_kernel<2>, dim3(n), dim3(256), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL(fused_small_kernel<FUSED_MAX_WINDOWS / 256>, dim3(n), dim3(256), 0, stream, a);
+    }
     return hipGetLastError();
 }
 

@@ -483,6 +483,12 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
                     return respond(ver, 404, "Not Found", "genus not found\n");
                 return respond(ver, 200, "OK", id + "\n");
             }
+            if (req.path == "/server_stats") { /* stage clocks (StageStats); ?reset=1 zeroes them after */
+                const std::string body = stage_stats().json();
+                if (param_int(req.parameters, "reset", 0))
+                    stage_stats().reset();
+                return respond(ver, 200, "OK", body);
+            }
             if (req.path == "/dump_sizes") {
                 std::vector<std::pair<std::string, Mapping>> all;
                 {
@@ -524,15 +530,26 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
              * reference's 1-MiB chunks on its thread pool (krequest2.cc:41,
              * query_request.cc:62-160) -- when every piece parses line by line */
             const size_t n_pieces = std::min(pool_.size(), n / kPieceBytes);
-            auto cuts = split_fasta_body(body, n, n_pieces);
-            std::vector<work_list_t> works(cuts.size());
-            bool ok = !cuts.empty();
-            for (size_t i = 0; ok && i < cuts.size(); i++)
-                ok = parse_fasta_piece(body + cuts[i].first, cuts[i].second - cuts[i].first, works[i]);
+            std::vector<std::pair<size_t, size_t>> cuts;
+            std::vector<work_list_t> works;
+            bool ok;
+            {
+                StageClock clk(stage_stats().parse_ns);
+                cuts = split_fasta_body(body, n, n_pieces);
+                works.resize(cuts.size());
+                ok = !cuts.empty();
+                for (size_t i = 0; ok && i < cuts.size(); i++)
+                    ok = parse_fasta_piece(body + cuts[i].first, cuts[i].second - cuts[i].first, works[i]);
+            }
             if (!ok) {
                 GutsLease kg(*this);
                 (*kg).set_parameters(req.parameters);
-                query_request(*kg, parse_fasta_body(body, n), details, fbc, os);
+                work_list_t work;
+                {
+                    StageClock clk(stage_stats().parse_ns);
+                    work = parse_fasta_body(body, n);
+                }
+                query_request(*kg, work, details, fbc, os);
                 return os.str();
             }
             std::vector<std::string> outs(works.size());
@@ -586,7 +603,11 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             fq_request(*kg, mapping, body, n, os);
             return os.str();
         }
-        const work_list_t work = parse_fasta_body(body, n);
+        work_list_t work;
+        {
+            StageClock clk(stage_stats().parse_ns);
+            work = parse_fasta_body(body, n);
+        }
         if (action == "/add") { /* krequest2.cc:429-436 */
             os << header(ver, 200, "OK") << "\n";
             add_request(*kg, *mapping, work, param_int(req.parameters, "silent", 0), os);

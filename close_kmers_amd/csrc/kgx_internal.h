@@ -224,10 +224,17 @@ hipError_t launch_small_upload(const SmallPieces &pc, hipStream_t stream);
  * stored straight into mapped host memory */
 constexpr uint32_t FUSED_MAX_WINDOWS = 2048;
 constexpr uint32_t FUSED_MAX_SEQ = 4096;
+/* a batch of at most FUSED_INLINE_SEQ sequences and FUSED_INLINE_RES residues
+ * travels in the kernel arguments (host pointers h_off / h_wbase / h_res,
+ * inline_res = its residue bytes; 0 = read res / off / wbase from mapped
+ * memory) */
+constexpr uint32_t FUSED_INLINE_SEQ = 32;
+constexpr uint32_t FUSED_INLINE_RES = 2048;
 hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uint64_t *wbase, uint32_t n,
                               uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
                               kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
-                              hipStream_t stream);
+                              uint32_t max_windows, uint64_t *dbg, const uint64_t *h_off, const uint64_t *h_wbase,
+                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,

@@ -394,11 +394,13 @@ struct kgx_ctx {
     /* one-launch small batches (option "small_fused"; kgx_fused.hip): mapped
      * window bases, per-sequence result regions, counts and tokens */
     int small_fused = 0;
+    int fused_inline = 1; /* a tiny fused batch travels in the kernel arguments (option "fused_inline") */
     uint64_t fused_batches = 0, small_batches = 0; /* kgx_ctx_stat */
     kgx::PinnedVec<uint64_t> h_fwb;
     kgx::PinnedVec<kgx_hit> h_fhits;
     kgx::PinnedVec<kgx_call> h_fcalls;
     kgx::PinnedVec<uint32_t> h_fcounts, h_fdone;
+    kgx::PinnedVec<uint64_t> h_fdbg; /* KGX_FUSED_DEBUG phase stamps */
     uint32_t small_token = 0;
     int host_nt = 1;    /* expansion with streaming stores (option "host_nt") */
     kgx::PinnedVec<kgx_call> h_calls_region;

@@ -1029,6 +1029,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->probe_lds_kb = (int)value;
         return KGX_OK;
     }
+    if (n == "fused_inline") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "fused_inline must be 0 or 1");
+        c->fused_inline = (int)value;
+        return KGX_OK;
+    }
     if (n == "small_fused") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "small_fused must be 0 or 1");
@@ -2341,10 +2347,12 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
         return rc;
     const uint64_t *off = c->h_off_stage.data();
     HIP_TRY(c->h_fwb.resize(n_seq + 1));
-    uint64_t W = 0;
+    uint64_t W = 0, longest = 0;
     for (uint32_t s = 0; s < n_seq; s++) {
         c->h_fwb[s] = W;
-        W += windows_of(off[s + 1] - off[s]);
+        const uint64_t w = windows_of(off[s + 1] - off[s]);
+        W += w;
+        longest = std::max(longest, w);
     }
     c->h_fwb[n_seq] = W;
     const bool need_hits = (want & KGX_WANT_HITS) != 0, want_calls = (want & KGX_WANT_CALLS) != 0;
@@ -2363,10 +2371,24 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
     HIP_TRY(c->h_fcounts.device_ptr(0, &d_counts));
     HIP_TRY(c->h_fdone.device_ptr(0, &d_done));
     const uint32_t token = ++c->small_token ? c->small_token : ++c->small_token;
+    /* KGX_FUSED_DEBUG: wall-clock stamps of the first workgroup's phases, to stderr */
+    static const bool debug = std::getenv("KGX_FUSED_DEBUG") != nullptr;
+    void *d_dbg = nullptr;
+    if (debug) {
+        HIP_TRY(c->h_fdbg.resize(8));
+        std::memset(c->h_fdbg.data(), 0, 8 * sizeof(uint64_t));
+        HIP_TRY(c->h_fdbg.device_ptr(0, &d_dbg));
+    }
     HIP_TRY(launch_fused_small(static_cast<const uint8_t *>(d_res), static_cast<const uint64_t *>(d_off),
                                static_cast<const uint64_t *>(d_wb), n_seq, want, c->img->d_packed, c->img->num_sigs, p,
                                static_cast<kgx_hit *>(d_hits), static_cast<kgx_call *>(d_calls),
-                               static_cast<uint32_t *>(d_counts), static_cast<uint32_t *>(d_done), token, c->stream));
+                               static_cast<uint32_t *>(d_counts), static_cast<uint32_t *>(d_done), token,
+                               (uint32_t)longest, static_cast<uint64_t *>(d_dbg), c->h_off_stage.data(),
+                               c->h_fwb.data(), reinterpret_cast<const uint8_t *>(c->h_res.data()),
+                               c->fused_inline && n_seq <= FUSED_INLINE_SEQ && off[n_seq] <= FUSED_INLINE_RES
+                                   ? (uint32_t)std::max<uint64_t>(off[n_seq], 1)
+                                   : 0u,
+                               c->stream));
     /* every sequence's token (stored after its results, behind a
      * system-scope fence); a fault or a lost store still ends the wait */
     const volatile uint32_t *done = c->h_fdone.data();
@@ -2389,6 +2411,13 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
 #endif
         }
     std::atomic_thread_fence(std::memory_order_acquire);
+    if (debug) {
+        const uint64_t *d = c->h_fdbg.data();
+        std::fprintf(stderr, "[kgx] fused n=%u: load %llu, probe %llu, compact %llu, store+score %llu, fence %llu ticks\n",
+                     n_seq, (unsigned long long)(d[1] - d[0]), (unsigned long long)(d[2] - d[1]),
+                     (unsigned long long)(d[3] - d[2]), (unsigned long long)(d[4] - d[3]),
+                     (unsigned long long)(d[5] - d[4]));
+    }
     /* the regions -> the CSR result */
     const uint32_t *cnt = c->h_fcounts.data();
     c->h_hoff.assign(n_seq + 1, 0);

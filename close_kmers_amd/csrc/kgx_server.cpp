@@ -108,8 +108,16 @@ size_t read_line(int fd, std::string &buf, size_t from)
     }
 }
 
+uint64_t clock_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 void serve_connection(KmerRequestRouter &router, int fd)
 {
+    const uint64_t t_recv = clock_ns(); /* stage clocks: recv from the accept */
     std::string buf;
     HttpRequest req;
     auto refuse = [&](int code, const char *status) {
@@ -181,10 +189,22 @@ void serve_connection(KmerRequestRouter &router, int fd)
             req.body.resize(len);
     }
     bool quit = false;
+    StageStats &st = stage_stats();
+    const uint64_t t_handle = clock_ns();
     const std::string resp = router.handle(req, &quit);
+    const uint64_t t_send = clock_ns();
     write_all(fd, resp.data(), resp.size());
     ::shutdown(fd, SHUT_WR);
     ::close(fd);
+    if (req.path != "/server_stats") {
+        const uint64_t t_end = clock_ns();
+        st.requests++;
+        st.bytes_in += req.body.size();
+        st.bytes_out += resp.size();
+        st.recv_ns += t_handle - t_recv;
+        st.handle_ns += t_send - t_handle;
+        st.send_ns += t_end - t_send;
+    }
     if (quit) {
         std::cerr << "stopping io service\n";
         g_stop = true;

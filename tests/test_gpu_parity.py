@@ -946,12 +946,15 @@ def test_fused_small_path_matches_oracle(small_world, oracle_lib, gpu, params):
     many = [res2[int(off2[i]):int(off2[i]) + int(k)] for i, k in enumerate(rng.integers(0, 400, 300))]
     batches = [seqs[:1], seqs[1:2] + [np.zeros(0, np.uint8)], [np.zeros(0, np.uint8)] + seqs[2:20],
                [seqs[20][:5], seqs[21][:9], seqs[22][:8]] + seqs[23:60], edge[:1], edge[1:], edge + seqs[:4],
-               many]
+               many, seqs[30:36], [s[:60] for s in seqs[:32]]]
     p = gpu.Params(*params)
     eligible = params[2] == 0 and params[0] >= 1
     ctx.set_option("small_fused", 1)
     try:
-        for b in batches:
+        # fused_inline 1: batches of <= 32 sequences and 2,048 residues travel
+        # in the kernel arguments; 0: always from mapped memory
+        for b, inl in [(b, inl) for inl in (1, 0) for b in batches]:
+            ctx.set_option("fused_inline", inl)
             lens = np.array([0] + [len(x) for x in b], np.uint64)
             boff = np.cumsum(lens).astype(np.uint64) + np.uint64(3)
             bres = np.concatenate([np.frombuffer(b"MKV", np.uint8)] + list(b))
@@ -980,6 +983,7 @@ def test_fused_small_path_matches_oracle(small_world, oracle_lib, gpu, params):
             assert ctx.stat("fused_batches") == f0
     finally:
         ctx.set_option("small_fused", 0)
+        ctx.set_option("fused_inline", 1)
 
 
 @pytest.mark.parametrize("params", PARAM_SETS[:4])

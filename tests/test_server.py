@@ -134,6 +134,31 @@ def test_query_and_add_routes_match_golden(gpu, ds):
 
 
 @pytest.mark.gpu
+def test_server_stats_count_the_request_stages(gpu):
+    """GET /server_stats: the server's per-stage clocks (recv, parse, gpu,
+    handle, send) over the requests served since the last ?reset=1."""
+    import json
+    d = os.path.join(GOLDEN, "edge")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    srv = Server(os.path.join(d, "data"))
+    try:
+        srv.request("GET", "/server_stats?reset=1")
+        for _ in range(3):
+            assert srv.request("POST", "/query", fasta).startswith(HEADER)
+        r = srv.request("GET", "/server_stats")
+        st = json.loads(r.split(b"\n\n", 1)[1])
+        assert st["requests"] == 3 and st["bytes_in"] == 3 * len(fasta) and st["gpu_passes"] >= 3
+        ms = st["ms_per_request"]
+        assert all(ms[k] > 0 for k in ("recv", "parse", "gpu", "handle", "send"))
+        assert ms["handle"] >= ms["gpu"]
+        srv.request("GET", "/server_stats?reset=1")
+        st = json.loads(srv.request("GET", "/server_stats").split(b"\n\n", 1)[1])
+        assert st["requests"] == 0
+    finally:
+        srv.close()
+
+
+@pytest.mark.gpu
 def test_concurrent_requests_match_golden(gpu):
     """Requests on 8 connections at once (4 KmerGuts workers) get the same
     bytes as one at a time; a client sending Expect: 100-continue gets the

@@ -4,22 +4,23 @@
 
 Starts close_kmers_amd/kgx_server on 127.0.0.1 with the C2 synthetic image
 (--synthetic-image: 1B keys built in HBM, PACKED16) and --threads KmerGuts
-workers, then C client threads POST FASTA bodies of the C2 query set to
-/query (query_request.cc: PROTEIN-ID / CALL / OTU-COUNTS text back) and
-read the responses to the end.  Bodies are cut at record boundaries to at
-most --body-bytes (default 1 MiB, the reference's request buffer,
-krequest2.cc:41).  Each request is one connection, as in krequest2.cc.
-Reports per C the aggregate residues/s (residues in the bodies completed ÷
-wall time) and the request latency (median, p99).  Prints one JSON line.
+workers, then runs tools/load_gen (native C++, its own process: C client
+threads, one connection per request as in krequest2.cc) POSTing FASTA bodies
+of the C2 query set to /query (query_request.cc: PROTEIN-ID / CALL /
+OTU-COUNTS text back) and reading the responses to the end.  Bodies are cut
+at record boundaries to at most --body-bytes (default 1 MiB, the reference's
+request buffer, krequest2.cc:41).  Server and load generator share the
+box's CPU share (16 CPUs on the GPU box's cgroup).  Reports per C the
+aggregate residues/s (residues in the bodies completed / wall time), the
+request latency (median, p99) and the server's own per-stage clocks (GET
+/server_stats: recv, parse, gpu, handle, send per request).  Prints one JSON
+line.
 
 With --families N a synthetic family DB is loaded (families.tsv, genus.map
 and nr.fasta over source proteins 0..N-1 of the synthetic image; each family
 holds one protein) so that /lookup runs in family mode
 (lookup_request.cc:153-400), e.g.
     python tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1"
-
-Everything on the path is timed: loopback TCP, the server's FASTA parse,
-the GPU pass (H2D, kernels, D2H of calls and OTU tallies), the text output.
 """
 from __future__ import annotations
 
@@ -30,7 +31,6 @@ import socket
 import subprocess
 import sys
 import tempfile
-import threading
 import time
 
 import numpy as np
@@ -96,6 +96,33 @@ def post(port: int, path: str, body: bytes) -> bytes:
     return b"".join(chunks)
 
 
+LOAD_GEN_SRC = os.path.join(ROOT, "tools", "load_gen.cpp")
+LOAD_GEN = os.path.join(ROOT, "tools", "load_gen")
+
+
+def build_load_gen() -> str:
+    if not os.path.exists(LOAD_GEN) or os.path.getmtime(LOAD_GEN) < os.path.getmtime(LOAD_GEN_SRC):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", LOAD_GEN_SRC, "-o", LOAD_GEN], check=True)
+    return LOAD_GEN
+
+
+def get(port: int, path: str) -> bytes:
+    with socket.create_connection(("127.0.0.1", port), timeout=60) as s:
+        s.sendall(b"GET %s HTTP/1.1\r\n\r\n" % path.encode())
+        chunks = []
+        while True:
+            c = s.recv(1 << 16)
+            if not c:
+                break
+            chunks.append(c)
+    return b"".join(chunks)
+
+
+def server_stats(port: int, reset: bool = False) -> dict:
+    r = get(port, "/server_stats" + ("?reset=1" if reset else ""))
+    return json.loads(r.split(b"\n\n", 1)[1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-keys", type=float, default=1e9)
@@ -111,10 +138,16 @@ def main():
     from close_kmers_amd import image_files, synth
 
     kbuild.build()
+    load_gen = build_load_gen()
     spec = synth.ImageSpec(int(args.n_keys))
     res, off = synth.make_queries(spec, args.n_seq)
     bodies, body_res = fasta_bodies(res, off, args.body_bytes)
     tmp = tempfile.TemporaryDirectory()
+    bodies_file = os.path.join(tmp.name, "bodies.bin")
+    with open(bodies_file, "wb") as f:
+        f.write(np.uint64(len(bodies)).tobytes())
+        for b, r in zip(bodies, body_res):
+            f.write(np.array([r, len(b)], np.uint64).tobytes() + b)
     image_files.write_index(os.path.join(tmp.name, "function.index"), [f"function {i}" for i in range(100000)])
     image_files.write_index(os.path.join(tmp.name, "otu.index"), ["otu0"])
     port_file = os.path.join(tmp.name, "port")
@@ -144,44 +177,27 @@ def main():
         assert r.count(b"PROTEIN-ID") == bodies[0].count(b">") or args.path != "/query"
         rows = {}
         for c in [int(x) for x in args.clients.split(",")]:
-            lat, done_res, nxt = [], [0], [0]
-            lock = threading.Lock()
-            stop = time.perf_counter() + args.seconds
-
-            def worker():
-                while time.perf_counter() < stop:
-                    with lock:
-                        i = nxt[0] % len(bodies)
-                        nxt[0] += 1
-                    t = time.perf_counter()
-                    out = post(port, args.path, bodies[i])
-                    dt = time.perf_counter() - t
-                    assert out.startswith(b"HTTP/1.1 200 OK")
-                    with lock:
-                        lat.append(dt)
-                        done_res[0] += body_res[i]
-
-            ths = [threading.Thread(target=worker) for _ in range(c)]
-            t = time.perf_counter()
-            for th in ths:
-                th.start()
-            for th in ths:
-                th.join()
-            wall = time.perf_counter() - t
-            lat_ms = np.array(lat) * 1e3
-            rows[str(c)] = {"residues_per_s": done_res[0] / wall, "requests": len(lat),
-                            "ms_median": float(np.median(lat_ms)), "ms_p99": float(np.percentile(lat_ms, 99))}
+            server_stats(port, reset=True)
+            r = subprocess.run([load_gen, str(port), args.path, bodies_file, str(c), str(args.seconds)],
+                               capture_output=True, text=True, timeout=args.seconds + 600)
+            if r.returncode != 0:
+                raise RuntimeError(f"load_gen: {r.stdout} {r.stderr}")
+            row = json.loads(r.stdout)
+            row["server_stages"] = server_stats(port)
+            rows[str(c)] = row
             print(f"[bench_server] clients={c}: {rows[str(c)]}", file=sys.stderr)
         best = max(rows.values(), key=lambda r: r["residues_per_s"])
         print(json.dumps({
             "metric": "HTTP serving residues/s through kgx_server (kser drop-in), C2 image",
-            "value": best["residues_per_s"], "unit": "residues/s",
+            "value": best["residues_per_s"], "unit": "residues/s", "load_generator": "tools/load_gen.cpp",
             "config": {"n_keys": spec.n_keys, "num_sigs": spec.num_sigs, "path": args.path,
                        "families": args.families,
                        "body_bytes": args.body_bytes, "proteins_per_body": round(args.n_seq / len(bodies), 1),
                        "server_threads": args.threads, "startup_s": startup_s},
             "by_clients": rows,
-            "note": "loopback TCP; server parses FASTA, one GPU pass per body, writes query_request text"}))
+            "note": "loopback TCP, native load generator (tools/load_gen) as its own process in the same CPU "
+                    "share; server parses FASTA, one GPU pass per body piece, writes query_request text; "
+                    "server_stages: the server's clocks per request (ms), gpu summed over a body's pieces"}))
     finally:
         try:
             with socket.create_connection(("127.0.0.1", port), timeout=60) as s:

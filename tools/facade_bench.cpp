@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <memory>
 #include <string>
@@ -130,6 +131,9 @@ int main(int argc, char **argv)
     std::vector<size_t> sizes = {1, 2, 4, 8, 16, 32, 64};
     if (only)
         sizes = {(size_t)std::strtoull(only, nullptr, 10)};
+    /* with the one-launch path the facade's per-sequence calls take (small_fused) */
+    if (kgx_ctx_set_option(kg.ctx(), "small_fused", 1) != KGX_OK)
+        return 1;
     for (size_t k : sizes) {
         std::vector<double> lt;
         for (int rep = 0; rep < 200; rep++) {
@@ -151,14 +155,28 @@ int main(int argc, char **argv)
         bs_json += b;
         std::fprintf(stderr, "[facade] pass of %zu proteins: p50 %.1f us, p99 %.1f us\n", k, pct(lt, 50), pct(lt, 99));
     }
+    (void)kgx_ctx_set_option(kg.ctx(), "small_fused", 0);
 
     /* the worker pool: T threads, one KmerGuts (context) each, per-sequence
      * calls; concurrent calls coalesced into shared passes (the default) or
      * one pass per call */
     std::string pool_json;
     bool pool_ok = true;
-    for (int co = 1; co >= 0 && !only; co--)
-        for (int T : {1, 4, 8, 16, 32}) {
+    /* KGX_FACADE_THREADS="16" or "8,16": only these pool sizes; KGX_FACADE_MODES="1" coalesced only */
+    std::vector<int> threads = {1, 4, 8, 16, 32};
+    if (const char *e = std::getenv("KGX_FACADE_THREADS")) {
+        threads.clear();
+        for (const char *q = e; *q;) {
+            threads.push_back(std::atoi(q));
+            while (*q && *q != ',')
+                q++;
+            if (*q == ',')
+                q++;
+        }
+    }
+    const char *modes = std::getenv("KGX_FACADE_MODES");
+    for (int co = 1; co >= (modes && std::strcmp(modes, "1") == 0 ? 1 : 0) && !only; co--)
+        for (int T : threads) {
             std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
             for (int t = 0; t < T; t++) {
                 kgs.emplace_back(new kgx::KmerGuts(dir, image));
