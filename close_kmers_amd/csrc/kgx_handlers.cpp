@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <charconv>
 #include <cstring>
 #include <regex>
 #include <sstream>
@@ -72,6 +73,67 @@ static bool parse_fasta_body_lines(const char *body, size_t n, work_list_t &work
             return false; /* '>' while the machine is in DATA: an error path */
     }
     return true;
+}
+
+/* parse_fasta_body_lines into the flat form (the same rules, record for
+ * record); false: the byte machine's case */
+static bool parse_fasta_flat_lines(const char *body, size_t n, FastaFlat &out)
+{
+    if (n == 0 || body[0] != '>' || std::memchr(body, '\r', n))
+        return false;
+    out.res.reserve(out.res.size() + n);
+    const char *p = body, *end = body + n;
+    while (p < end) { /* p at a '>' */
+        const char *eol = (const char *)std::memchr(p, '\n', end - p);
+        if (!eol)
+            return false;
+        const char *id_end = p + 1;
+        while (id_end < eol && *id_end != ' ' && *id_end != '\t')
+            id_end++;
+        out.ids.append(p + 1, id_end);
+        out.id_off.push_back(out.ids.size());
+        p = eol + 1;
+        bool first_line = true;
+        while (p < end && *p != '>') {
+            eol = (const char *)std::memchr(p, '\n', end - p);
+            const char *le = eol ? eol : end;
+            unsigned ok = 1;
+            for (const char *q = p; q < le; q++) {
+                const unsigned char c = (unsigned char)*q;
+                ok &= (unsigned)((unsigned char)((c | 0x20) - 'a') < 26) | (unsigned)(c == '*');
+            }
+            if (!ok || (le > p && *p == '*' && !first_line))
+                return false;
+            out.res.append(p, le);
+            first_line = false;
+            p = eol ? eol + 1 : end;
+        }
+        out.off.push_back(out.res.size());
+        if (p < end && first_line)
+            return false;
+    }
+    return true;
+}
+
+bool parse_fasta_piece_flat(const char *piece, size_t n, FastaFlat &out)
+{
+    return parse_fasta_flat_lines(piece, n, out);
+}
+
+FastaFlat flat_of(const work_list_t &work)
+{
+    FastaFlat f;
+    for (const auto &w : work)
+        f.add(w.first.data(), w.first.size(), w.second.data(), w.second.size());
+    return f;
+}
+
+FastaFlat parse_fasta_body_flat(const char *body, size_t n)
+{
+    FastaFlat f;
+    if (parse_fasta_flat_lines(body, n, f))
+        return f;
+    return flat_of(parse_fasta_body_bytewise(body, n));
 }
 
 std::vector<std::pair<size_t, size_t>> split_fasta_body(const char *body, size_t n, size_t pieces)
@@ -152,43 +214,93 @@ static std::vector<KmerGuts::SeqJob> jobs_for(const work_list_t &work)
 void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_best_call,
                    std::ostream &os)
 {
-    std::vector<KmerGuts::SeqJob> jobs = jobs_for(work);
-    std::vector<std::shared_ptr<std::vector<KmerGuts::hit_in_sequence_t>>> hit_lists(jobs.size());
-    if (details && !find_best_call) /* the HIT lines are printed only without find_best_call */
-        for (size_t i = 0; i < jobs.size(); i++) {
-            auto hl = std::make_shared<std::vector<KmerGuts::hit_in_sequence_t>>();
-            hit_lists[i] = hl;
-            jobs[i].hit_cb = [hl](KmerGuts::hit_in_sequence_t h) { hl->push_back(h); };
-        }
-    kg.process_aa_batch(jobs);
+    query_request(kg, flat_of(work), details, find_best_call, os);
+}
+
+void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_best_call, std::ostream &os)
+{
+    const uint32_t n = (uint32_t)work.size();
+    if (n == 0)
+        return;
+    const bool want_hits = details && !find_best_call; /* HIT lines only without find_best_call */
+    const uint32_t want = find_best_call ? KGX_WANT_BEST
+                                         : (KGX_WANT_CALLS | KGX_WANT_OTU | (want_hits ? KGX_WANT_HITS : 0u));
+    kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
+    kgx_compact_result cr;
+    int rc;
+    {
+        StageClock clk(stage_stats().gpu_ns);
+        rc = kgx_process_batch_compact(kg.ctx(), &p, work.res.data(), work.off.data(), n, want, &cr);
+    }
+    stage_stats().gpu_passes++;
+    if (rc)
+        throw Error(rc, std::string("kgx_process_batch_compact: ") + kgx_strerror(rc) + " (" + kgx_last_error() + ")");
+    const kgx_result &r = cr.r;
     std::string out;
-    out.reserve(jobs.size() * 96);
-    for (size_t i = 0; i < jobs.size(); i++) {
-        const std::string &id = jobs[i].id, &seq = jobs[i].seq;
-        auto &calls = *jobs[i].calls;
-        if (find_best_call) { /* query_request.cc:124-135 */
+    out.reserve((size_t)n * 96 + 64);
+    std::vector<kgx_hit> seq_hits;
+    char num[24];
+    auto put_num = [&](long long v) {
+        auto e = std::to_chars(num, num + sizeof num, v);
+        out.append(num, e.ptr);
+    };
+    for (uint32_t s = 0; s < n; s++) {
+        const char *id = work.ids.data() + work.id_off[s];
+        const size_t id_len = work.id_off[s + 1] - work.id_off[s];
+        const uint64_t len = work.off[s + 1] - work.off[s];
+        if (find_best_call) { /* query_request.cc:124-135, the device's decision */
             int fi;
             std::string fn;
             float score, wscore, off = 0.0f;
-            kg.find_best_call(calls, fi, fn, score, wscore, off);
+            kg.find_best_call(r.best[s], fi, fn, score, wscore, off);
             if (!fn.empty()) {
                 std::ostringstream line; /* one line per call: the float format stays iostream's */
-                line << id << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
+                line.write(id, (std::streamsize)id_len);
+                line << "\t" << fn << "\t" << score << "\t" << wscore << "\n";
                 out += line.str();
             }
             continue;
         }
         out += "PROTEIN-ID\t";
-        out += id;
+        out.append(id, id_len);
         out += '\t';
-        out += std::to_string(seq.size());
+        put_num((long long)len);
         out += '\n';
-        for (auto &c : calls)
-            kg.append_call(out, c);
-        if (hit_lists[i])
-            for (auto &h : *hit_lists[i])
-                kg.append_hit(out, h);
-        kg.append_otu_stats(out, id, seq.size(), *jobs[i].otu_stats);
+        for (uint64_t c = r.call_offsets[s]; c < r.call_offsets[s + 1]; c++) {
+            const kgx_call &k = r.calls[c];
+            kg.append_call(out, KmerCall(k.start, k.end, k.count, k.function_index, k.weighted_hits));
+        }
+        if (want_hits) {
+            const uint64_t nh = r.hit_offsets[s + 1] - r.hit_offsets[s];
+            seq_hits.resize(nh);
+            if (nh && (rc = kgx_compact_expand(&cr, work.res.data(), work.off.data(), s, s + 1, 0, seq_hits.data())))
+                throw Error(rc, std::string("kgx_compact_expand: ") + kgx_last_error());
+            for (const kgx_hit &h : seq_hits) {
+                sig_kmer_t e;
+                e.which_kmer = h.which_kmer;
+                e.otu_index = h.otu_index;
+                e.avg_from_end = h.avg_from_end;
+                e.pad = 0;
+                e.function_index = h.function_index;
+                e.function_wt = h.function_wt;
+                kg.append_hit(out, KmerGuts::hit_in_sequence_t(e, h.pos));
+            }
+        }
+        /* KmerOtuStats::write's line (kguts.h:196-218): the device tallies
+         * come in otus_by_count order; the top 5 */
+        out += "OTU-COUNTS\t";
+        out.append(id, id_len);
+        out += '[';
+        put_num((long long)len);
+        out += ']';
+        const uint64_t o0 = r.otu_offsets[s], o1 = std::min<uint64_t>(r.otu_offsets[s + 1], o0 + 5);
+        for (uint64_t o = o0; o < o1; o++) {
+            out += '\t';
+            put_num(r.otus[o].count);
+            out += '-';
+            put_num(r.otus[o].otu_index);
+        }
+        out += '\n';
     }
     os.write(out.data(), (std::streamsize)out.size());
 }
@@ -531,7 +643,7 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
              * query_request.cc:62-160) -- when every piece parses line by line */
             const size_t n_pieces = std::min(pool_.size(), n / kPieceBytes);
             std::vector<std::pair<size_t, size_t>> cuts;
-            std::vector<work_list_t> works;
+            std::vector<FastaFlat> works;
             bool ok;
             {
                 StageClock clk(stage_stats().parse_ns);
@@ -539,15 +651,15 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
                 works.resize(cuts.size());
                 ok = !cuts.empty();
                 for (size_t i = 0; ok && i < cuts.size(); i++)
-                    ok = parse_fasta_piece(body + cuts[i].first, cuts[i].second - cuts[i].first, works[i]);
+                    ok = parse_fasta_piece_flat(body + cuts[i].first, cuts[i].second - cuts[i].first, works[i]);
             }
             if (!ok) {
                 GutsLease kg(*this);
                 (*kg).set_parameters(req.parameters);
-                work_list_t work;
+                FastaFlat work;
                 {
                     StageClock clk(stage_stats().parse_ns);
-                    work = parse_fasta_body(body, n);
+                    work = parse_fasta_body_flat(body, n);
                 }
                 query_request(*kg, work, details, fbc, os);
                 return os.str();

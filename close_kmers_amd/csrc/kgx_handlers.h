@@ -47,6 +47,27 @@ std::vector<std::pair<size_t, size_t>> split_fasta_body(const char *body, size_t
  * byte machine (then the whole body must be parsed as one) */
 bool parse_fasta_piece(const char *piece, size_t n, work_list_t &work);
 
+/* A parsed body, flat (no string per record): record i's id is
+ * ids[id_off[i], id_off[i+1]), its residues res[off[i], off[i+1]) -- the
+ * batch layout kgx_process_batch takes as is. */
+struct FastaFlat {
+    std::string ids, res;
+    std::vector<uint64_t> id_off{0}, off{0};
+    size_t size() const { return off.size() - 1; }
+    std::string id(size_t i) const { return ids.substr(id_off[i], id_off[i + 1] - id_off[i]); }
+    void add(const char *id, size_t id_len, const char *seq, size_t seq_len)
+    {
+        ids.append(id, id_len);
+        id_off.push_back(ids.size());
+        res.append(seq, seq_len);
+        off.push_back(res.size());
+    }
+};
+/* parse_fasta_piece / parse_fasta_body into the flat form (same records) */
+bool parse_fasta_piece_flat(const char *piece, size_t n, FastaFlat &out);
+FastaFlat parse_fasta_body_flat(const char *body, size_t n);
+FastaFlat flat_of(const work_list_t &work);
+
 /* the reference reads integer flags with std::stoi and keeps the default
  * when the value is absent or not a number (query_request.cc:92-100) */
 int param_int(const request_params_t &params, const std::string &name, int dflt);
@@ -55,6 +76,10 @@ int param_int(const request_params_t &params, const std::string &name, int dflt)
  * find_best_call=1 prints one best-call line per sequence with a call */
 void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_best_call,
                    std::ostream &os);
+/* the same over a flat batch: one GPU pass, the lines written straight from
+ * the result CSR (calls, device OTU tallies already in otus_by_count order,
+ * device find_best_call decisions) -- no per-sequence objects */
+void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_best_call, std::ostream &os);
 
 /* /add (add_request.cc:115-170): per sequence PROTEIN-ID / CALL / OTU-COUNTS /
  * BEST-CALL unless silent, then every hit's k-mer is mapped to the

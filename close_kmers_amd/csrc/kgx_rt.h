@@ -385,7 +385,7 @@ struct kgx_ctx {
     /* small host batches (<= small_batch residues, option "small_batch", 0 =
      * off): planned on the host, read by the device from the mapped staging
      * blob, results stored into mapped memory: one host wait per batch */
-    int64_t small_batch = 1 << 16;
+    int64_t small_batch = 1 << 21; /* 2M residues: a 1-MiB request body and then some */
     int small_wave = 1; /* small batches: the wave scorer instead of the hybrid (option "small_wave") */
     int small_wave_tiles = 1; /* small batches: probe tiles per scorer wave (option "small_wave_tiles") */
     kgx::PinnedVec<uint4> h_small; /* offsets | window bases | tile owners | status | residues */

@@ -796,6 +796,9 @@ int kgx_ctx_create(kgx_image *img, kgx_ctx **out)
         return fail(KGX_EDEVICE, std::string("stream: ") + hipGetErrorString(e));
     }
     c->own_stream = true;
+    /* KGX_SMALL_BATCH: the default of option "small_batch" for new contexts */
+    if (const char *sb = std::getenv("KGX_SMALL_BATCH"))
+        c->small_batch = std::min<int64_t>(1 << 24, std::max<int64_t>(0, std::atoll(sb)));
     e = hipEventCreateWithFlags(&c->probe_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         (void)hipStreamDestroy(c->stream);
@@ -2472,15 +2475,17 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     /* the blob: offsets | window bases | tile owners | status | residues */
     const uint64_t b_off = round16((n_seq + 1) * sizeof(uint64_t)), b_wb = b_off,
                    b_tile = round16(c->max_tiles * sizeof(uint32_t)), b_st = 16, b_res = round16(n_res);
-    const uint64_t words = (b_off + b_wb + b_tile + b_st + b_res) / 16;
+    /* the residues stay in the pinned staging (h_res): the upload reads them
+     * from there, no second host copy */
+    const uint64_t words = (b_off + b_wb + b_tile + b_st) / 16;
     HIP_TRY(c->h_small.resize(words));
+    HIP_TRY(c->h_res.resize(b_res ? b_res : 16)); /* 16-B words: the upload's last one may run past n_res */
     char *blob = reinterpret_cast<char *>(c->h_small.data());
     uint64_t *h_off = reinterpret_cast<uint64_t *>(blob);
     uint64_t *h_wb = reinterpret_cast<uint64_t *>(blob + b_off);
     uint32_t *h_tile = reinterpret_cast<uint32_t *>(blob + b_off + b_wb);
     uint32_t *h_st = reinterpret_cast<uint32_t *>(blob + b_off + b_wb + b_tile);
     std::memcpy(h_off, off, (n_seq + 1) * sizeof(uint64_t));
-    std::memcpy(blob + b_off + b_wb + b_tile + b_st, c->h_res.data(), n_res);
     /* plan_reduce / plan_scan on the host: window bases, the sequence owning
      * each tile's first window, the longest sequence */
     const uint64_t T = c->tile_windows;
@@ -2500,8 +2505,9 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     h_st[0] = 0;
     h_st[1] = longest;
     h_st[2] = h_st[3] = 0;
-    void *d_blob = nullptr;
+    void *d_blob = nullptr, *d_res = nullptr;
     HIP_TRY(c->h_small.device_ptr(0, &d_blob));
+    HIP_TRY(c->h_res.device_ptr(0, &d_res));
     const uint4 *src = static_cast<const uint4 *>(d_blob);
     SmallPieces pc;
     const uint64_t sizes[SMALL_PIECES] = {b_off, b_wb, b_tile, b_st, b_res};
@@ -2509,7 +2515,8 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     uint64_t at = 0;
     for (int p = 0; p < SMALL_PIECES; p++) {
         pc.dst[p] = static_cast<uint4 *>(dsts[p]);
-        pc.src[p] = src + at;
+        /* the last piece (residues) from the staging, the others from the blob */
+        pc.src[p] = p == SMALL_PIECES - 1 ? static_cast<const uint4 *>(d_res) : src + at;
         at += sizes[p] / 16;
         pc.end16[p] = at;
     }

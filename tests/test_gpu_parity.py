@@ -88,11 +88,17 @@ def small_world(gpu):
 
 
 @pytest.mark.parametrize("params", PARAM_SETS)
-def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params):
+@pytest.mark.parametrize("small_batch", [1 << 21, 0])
+def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params, small_batch):
+    """400 proteins: the one-wait small path (default) and the one-pass path."""
     spec, table, img, ctx = small_world
     res, off = synth.make_queries(spec, 400, x_permille=5)
     want = oracle_lib.process_batch(table, res, off, params=params)
-    got = ctx.process_batch(res, off, gpu.Params(*params))
+    ctx.set_option("small_batch", small_batch)
+    try:
+        got = ctx.process_batch(res, off, gpu.Params(*params))
+    finally:
+        ctx.set_option("small_batch", 1 << 21)
     assert_same(got, want, 400)
     lens = np.diff(off).astype(np.int64)
     assert got.n_windows == int(np.maximum(lens - 8, 0).sum())
@@ -1028,7 +1034,7 @@ def test_small_batch_path_matches_oracle(small_world, aos_world, oracle_lib, gpu
             try:
                 ref_best = layout_ctx.process_batch(bres, boff, p, want=gpu.WANT_BEST).best
             finally:
-                layout_ctx.set_option("small_batch", 65536)
+                layout_ctx.set_option("small_batch", 1 << 21)
             assert np.array_equal(small_best.best, ref_best)
         layout_ctx.set_option("small_wave", 1)
 
