@@ -50,7 +50,7 @@ StageStats &stage_stats()
 
 void StageStats::reset()
 {
-    for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &handle_ns, &send_ns})
+    for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &text_ns, &handle_ns, &send_ns})
         a->store(0);
 }
 
@@ -60,11 +60,12 @@ std::string StageStats::json() const
     const double r = (double)std::max<uint64_t>(1, requests.load());
     std::snprintf(b, sizeof b,
                   "{\"requests\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, \"gpu_passes\": %llu, "
-                  "\"ms_per_request\": {\"recv\": %.4f, \"parse\": %.4f, \"gpu\": %.4f, \"handle\": %.4f, "
+                  "\"ms_per_request\": {\"recv\": %.4f, \"parse\": %.4f, \"gpu\": %.4f, \"text\": %.4f, \"handle\": %.4f, "
                   "\"send\": %.4f}}\n",
                   (unsigned long long)requests.load(), (unsigned long long)bytes_in.load(),
                   (unsigned long long)bytes_out.load(), (unsigned long long)gpu_passes.load(), recv_ns.load() / r * 1e-6,
-                  parse_ns.load() / r * 1e-6, gpu_ns.load() / r * 1e-6, handle_ns.load() / r * 1e-6,
+                  parse_ns.load() / r * 1e-6, gpu_ns.load() / r * 1e-6, text_ns.load() / r * 1e-6,
+                  handle_ns.load() / r * 1e-6,
                   send_ns.load() / r * 1e-6);
     return b;
 }

@@ -45,7 +45,7 @@ namespace kgx {
  */
 struct StageStats {
     std::atomic<uint64_t> requests{0}, bytes_in{0}, bytes_out{0}, gpu_passes{0};
-    std::atomic<uint64_t> recv_ns{0}, parse_ns{0}, gpu_ns{0}, handle_ns{0}, send_ns{0};
+    std::atomic<uint64_t> recv_ns{0}, parse_ns{0}, gpu_ns{0}, text_ns{0}, handle_ns{0}, send_ns{0};
     void reset();
     std::string json() const;
 };

@@ -5,9 +5,12 @@
 #include "kgx_handlers.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
+#include <exception>
 #include <charconv>
 #include <cstring>
+#include <emmintrin.h>
 #include <regex>
 #include <sstream>
 #include <thread>
@@ -28,6 +31,28 @@ static work_list_t parse_fasta_body_bytewise(const char *body, size_t n)
         parser.parse_char(body[i]);
     parser.parse_complete();
     return work;
+}
+
+/* true when [p, le) holds only letters (C locale isalpha) and '*': 16 bytes
+ * at a time (SSE2, the x86-64 baseline), then the tail */
+static bool residue_line_ok(const char *p, const char *le)
+{
+    const __m128i lc = _mm_set1_epi8(0x20), a = _mm_set1_epi8('a'), z = _mm_set1_epi8(25),
+                  star = _mm_set1_epi8('*');
+    __m128i bad = _mm_setzero_si128();
+    for (; le - p >= 16; p += 16) {
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(p));
+        const __m128i t = _mm_sub_epi8(_mm_or_si128(c, lc), a);             /* letter: t in [0, 25] */
+        const __m128i letter = _mm_cmpeq_epi8(_mm_min_epu8(t, z), t);       /* unsigned t <= 25 */
+        const __m128i ok = _mm_or_si128(letter, _mm_cmpeq_epi8(c, star));
+        bad = _mm_or_si128(bad, _mm_andnot_si128(ok, _mm_set1_epi8(-1)));
+    }
+    unsigned ok = _mm_movemask_epi8(bad) == 0;
+    for (; p < le; p++) {
+        const unsigned char c = (unsigned char)*p;
+        ok &= (unsigned)((unsigned char)((c | 0x20) - 'a') < 26) | (unsigned)(c == '*');
+    }
+    return ok != 0;
 }
 
 /* Line-at-a-time parse of well-formed bodies, the common case, with the same
@@ -57,12 +82,7 @@ static bool parse_fasta_body_lines(const char *body, size_t n, work_list_t &work
         while (p < end && *p != '>') {
             eol = (const char *)std::memchr(p, '\n', end - p);
             const char *le = eol ? eol : end;
-            /* letters (C locale isalpha) or '*'; no early exit, so it vectorises */
-            unsigned ok = 1;
-            for (const char *q = p; q < le; q++) {
-                const unsigned char c = (unsigned char)*q;
-                ok &= (unsigned)((unsigned char)((c | 0x20) - 'a') < 26) | (unsigned)(c == '*');
-            }
+            const bool ok = residue_line_ok(p, le);
             if (!ok || (le > p && *p == '*' && !first_line))
                 return false;
             seq.append(p, le);
@@ -97,11 +117,7 @@ static bool parse_fasta_flat_lines(const char *body, size_t n, FastaFlat &out)
         while (p < end && *p != '>') {
             eol = (const char *)std::memchr(p, '\n', end - p);
             const char *le = eol ? eol : end;
-            unsigned ok = 1;
-            for (const char *q = p; q < le; q++) {
-                const unsigned char c = (unsigned char)*q;
-                ok &= (unsigned)((unsigned char)((c | 0x20) - 'a') < 26) | (unsigned)(c == '*');
-            }
+            const bool ok = residue_line_ok(p, le);
             if (!ok || (le > p && *p == '*' && !first_line))
                 return false;
             out.res.append(p, le);
@@ -217,37 +233,39 @@ void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_
     query_request(kg, flat_of(work), details, find_best_call, os);
 }
 
-void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_best_call, std::ostream &os)
+void query_pass(KmerGuts &kg, const FastaFlat &batch, int details, int find_best_call, kgx_compact_result *cr)
 {
-    const uint32_t n = (uint32_t)work.size();
-    if (n == 0)
-        return;
+    const uint32_t n = (uint32_t)batch.size();
     const bool want_hits = details && !find_best_call; /* HIT lines only without find_best_call */
     const uint32_t want = find_best_call ? KGX_WANT_BEST
                                          : (KGX_WANT_CALLS | KGX_WANT_OTU | (want_hits ? KGX_WANT_HITS : 0u));
     kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
-    kgx_compact_result cr;
     int rc;
     {
         StageClock clk(stage_stats().gpu_ns);
-        rc = kgx_process_batch_compact(kg.ctx(), &p, work.res.data(), work.off.data(), n, want, &cr);
+        rc = kgx_process_batch_compact(kg.ctx(), &p, batch.res.data(), batch.off.data(), n, want, cr);
     }
     stage_stats().gpu_passes++;
     if (rc)
         throw Error(rc, std::string("kgx_process_batch_compact: ") + kgx_strerror(rc) + " (" + kgx_last_error() + ")");
+}
+
+void query_text(KmerGuts &kg, const kgx_compact_result &cr, const FastaFlat &batch, uint32_t s0, uint32_t s1,
+                const FastaFlat &ids, int details, int find_best_call, std::string &out)
+{
+    const bool want_hits = details && !find_best_call;
     const kgx_result &r = cr.r;
-    std::string out;
-    out.reserve((size_t)n * 96 + 64);
+    out.reserve(out.size() + (size_t)(s1 - s0) * 96 + 64);
     std::vector<kgx_hit> seq_hits;
     char num[24];
     auto put_num = [&](long long v) {
         auto e = std::to_chars(num, num + sizeof num, v);
         out.append(num, e.ptr);
     };
-    for (uint32_t s = 0; s < n; s++) {
-        const char *id = work.ids.data() + work.id_off[s];
-        const size_t id_len = work.id_off[s + 1] - work.id_off[s];
-        const uint64_t len = work.off[s + 1] - work.off[s];
+    for (uint32_t s = s0; s < s1; s++) {
+        const char *id = ids.ids.data() + ids.id_off[s - s0];
+        const size_t id_len = ids.id_off[s - s0 + 1] - ids.id_off[s - s0];
+        const uint64_t len = batch.off[s + 1] - batch.off[s];
         if (find_best_call) { /* query_request.cc:124-135, the device's decision */
             int fi;
             std::string fn;
@@ -273,7 +291,8 @@ void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_be
         if (want_hits) {
             const uint64_t nh = r.hit_offsets[s + 1] - r.hit_offsets[s];
             seq_hits.resize(nh);
-            if (nh && (rc = kgx_compact_expand(&cr, work.res.data(), work.off.data(), s, s + 1, 0, seq_hits.data())))
+            int rc;
+            if (nh && (rc = kgx_compact_expand(&cr, batch.res.data(), batch.off.data(), s, s + 1, 0, seq_hits.data())))
                 throw Error(rc, std::string("kgx_compact_expand: ") + kgx_last_error());
             for (const kgx_hit &h : seq_hits) {
                 sig_kmer_t e;
@@ -302,7 +321,128 @@ void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_be
         }
         out += '\n';
     }
+}
+
+void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_best_call, std::ostream &os)
+{
+    const uint32_t n = (uint32_t)work.size();
+    if (n == 0)
+        return;
+    kgx_compact_result cr;
+    query_pass(kg, work, details, find_best_call, &cr);
+    std::string out;
+    {
+        StageClock clk(stage_stats().text_ns);
+        query_text(kg, cr, work, 0, n, work, details, find_best_call, out);
+    }
     os.write(out.data(), (std::streamsize)out.size());
+}
+
+/* ------------------------------------------------------------------------ */
+/* ForkJoin                                                                  */
+/* ------------------------------------------------------------------------ */
+
+struct ForkJoin::Batch {
+    const std::function<void(size_t)> *f;
+    size_t k;
+    std::atomic<size_t> next{0}, done{0};
+    std::atomic<int> users{0}; /* helpers holding a pointer to the batch */
+    std::mutex mu;
+    std::condition_variable cv;
+    std::mutex err_mu;
+    std::exception_ptr err;
+};
+
+ForkJoin::ForkJoin(unsigned helpers)
+{
+    for (unsigned i = 0; i < helpers; i++)
+        th_.emplace_back([this] { helper(); });
+}
+
+ForkJoin::~ForkJoin()
+{
+    {
+        std::lock_guard<std::mutex> l(mu_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_)
+        t.join();
+}
+
+void ForkJoin::work(Batch &b)
+{
+    for (size_t i; (i = b.next.fetch_add(1)) < b.k;) {
+        try {
+            (*b.f)(i);
+        } catch (...) {
+            std::lock_guard<std::mutex> l(b.err_mu);
+            if (!b.err)
+                b.err = std::current_exception();
+        }
+        if (b.done.fetch_add(1) + 1 == b.k) {
+            std::lock_guard<std::mutex> l(b.mu);
+            b.cv.notify_all();
+        }
+    }
+}
+
+void ForkJoin::helper()
+{
+    for (;;) {
+        Batch *b;
+        {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [this] { return stop_ || !open_.empty(); });
+            if (stop_)
+                return;
+            b = open_.front();
+            b->users++;
+        }
+        work(*b);
+        {
+            std::lock_guard<std::mutex> l(mu_); /* every index is claimed: no one else takes it */
+            auto it = std::find(open_.begin(), open_.end(), b);
+            if (it != open_.end())
+                open_.erase(it);
+        }
+        b->users--; /* the last touch: run() may return now */
+    }
+}
+
+void ForkJoin::run(size_t k, const std::function<void(size_t)> &f)
+{
+    if (k == 0)
+        return;
+    if (k == 1 || th_.empty()) {
+        for (size_t i = 0; i < k; i++)
+            f(i);
+        return;
+    }
+    Batch b;
+    b.f = &f;
+    b.k = k;
+    {
+        std::lock_guard<std::mutex> l(mu_);
+        open_.push_back(&b);
+    }
+    for (size_t i = 1; i < std::min<size_t>(k, th_.size() + 1); i++)
+        cv_.notify_one();
+    work(b);
+    {
+        std::lock_guard<std::mutex> l(mu_);
+        auto it = std::find(open_.begin(), open_.end(), &b);
+        if (it != open_.end())
+            open_.erase(it);
+    }
+    {
+        std::unique_lock<std::mutex> l(b.mu);
+        b.cv.wait(l, [&b] { return b.done.load() == b.k; });
+    }
+    while (b.users.load())
+        std::this_thread::yield();
+    if (b.err)
+        std::rethrow_exception(b.err);
 }
 
 void add_request(KmerGuts &kg, KmerPegMapping &mapping, const work_list_t &work, int silent,
@@ -645,9 +785,78 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             std::vector<std::pair<size_t, size_t>> cuts;
             std::vector<FastaFlat> works;
             bool ok;
+            /* only while few /query bodies are in flight: under load the
+             * requests themselves keep the cores busy, and a helper holding a
+             * sub-piece while descheduled would stretch its request's tail */
+            struct InFlight {
+                std::atomic<int> &c;
+                int now;
+                explicit InFlight(std::atomic<int> &c_) : c(c_), now(++c_) {}
+                ~InFlight() { --c; }
+            } in_flight(query_in_flight_);
+            const size_t n_sub = in_flight.now <= (int)fj_.helpers() ? std::min<size_t>(fj_.helpers() + 1, n / kSplitBytes)
+                                                                      : 0;
+            if (n_pieces < 2 && n_sub >= 2) {
+                /* one GPU pass for the body; its parse and its text in
+                 * sub-pieces on the ForkJoin helpers */
+                FastaFlat batch;
+                std::vector<uint64_t> seq_base, res_base;
+                {
+                    StageClock clk(stage_stats().parse_ns);
+                    cuts = split_fasta_body(body, n, n_sub);
+                    works.resize(cuts.size());
+                    std::vector<char> good(cuts.size(), 0);
+                    fj_.run(cuts.size(), [&](size_t i) {
+                        good[i] = parse_fasta_piece_flat(body + cuts[i].first, cuts[i].second - cuts[i].first,
+                                                         works[i]);
+                    });
+                    ok = !cuts.empty() && std::all_of(good.begin(), good.end(), [](char c) { return c != 0; });
+                    if (ok) {
+                        seq_base.assign(works.size() + 1, 0);
+                        res_base.assign(works.size() + 1, 0);
+                        for (size_t i = 0; i < works.size(); i++) {
+                            seq_base[i + 1] = seq_base[i] + works[i].size();
+                            res_base[i + 1] = res_base[i] + works[i].res.size();
+                        }
+                        batch.res.resize(res_base.back());
+                        batch.off.resize(seq_base.back() + 1);
+                        fj_.run(works.size(), [&](size_t i) {
+                            const FastaFlat &w = works[i];
+                            std::memcpy(&batch.res[res_base[i]], w.res.data(), w.res.size());
+                            for (size_t j = 1; j <= w.size(); j++)
+                                batch.off[seq_base[i] + j] = w.off[j] + res_base[i];
+                        });
+                    }
+                }
+                if (ok) {
+                    if (batch.size() == 0)
+                        return os.str();
+                    GutsLease kg(*this);
+                    (*kg).set_parameters(req.parameters);
+                    kgx_compact_result cr;
+                    query_pass(*kg, batch, details, fbc, &cr);
+                    std::vector<std::string> outs(works.size());
+                    {
+                        StageClock clk(stage_stats().text_ns);
+                        fj_.run(works.size(), [&](size_t i) {
+                            query_text(*kg, cr, batch, (uint32_t)seq_base[i], (uint32_t)seq_base[i + 1], works[i],
+                                       details, fbc, outs[i]);
+                        });
+                    }
+                    std::string all = os.str();
+                    size_t total = all.size();
+                    for (auto &o : outs)
+                        total += o.size();
+                    all.reserve(total);
+                    for (auto &o : outs)
+                        all += o;
+                    return all;
+                }
+                works.clear();
+            }
             {
                 StageClock clk(stage_stats().parse_ns);
-                cuts = split_fasta_body(body, n, n_pieces);
+                cuts = n_pieces >= 2 ? split_fasta_body(body, n, n_pieces) : decltype(cuts)();
                 works.resize(cuts.size());
                 ok = !cuts.empty();
                 for (size_t i = 0; ok && i < cuts.size(); i++)

@@ -18,13 +18,16 @@
  */
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <ostream>
 #include <shared_mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -80,6 +83,42 @@ void query_request(KmerGuts &kg, const work_list_t &work, int details, int find_
  * the result CSR (calls, device OTU tallies already in otus_by_count order,
  * device find_best_call decisions) -- no per-sequence objects */
 void query_request(KmerGuts &kg, const FastaFlat &work, int details, int find_best_call, std::ostream &os);
+
+/* query_request in its two halves: the GPU pass over the whole flat batch
+ * (res / off; ids unused) into *cr, valid until the next pass on kg -- then
+ * the text of sequences [s0, s1) appended to out, their ids taken from
+ * `ids` (a piece whose record 0 is sequence s0).  Text of disjoint ranges may
+ * be written on several threads at once. */
+void query_pass(KmerGuts &kg, const FastaFlat &batch, int details, int find_best_call, kgx_compact_result *cr);
+void query_text(KmerGuts &kg, const kgx_compact_result &cr, const FastaFlat &batch, uint32_t s0, uint32_t s1,
+                const FastaFlat &ids, int details, int find_best_call, std::string &out);
+
+/*
+ * ForkJoin -- a few host threads shared by all requests: run(k, f) calls
+ * f(0) ... f(k-1), the caller taking indices too, and returns when all have
+ * returned (the first exception is rethrown on the caller).  Concurrent
+ * run()s share the helpers; a run never waits on another's work, so nothing
+ * deadlocks when every helper is busy -- the caller then does it all.
+ */
+class ForkJoin {
+public:
+    explicit ForkJoin(unsigned helpers);
+    ~ForkJoin();
+    ForkJoin(const ForkJoin &) = delete;
+    ForkJoin &operator=(const ForkJoin &) = delete;
+    unsigned helpers() const { return (unsigned)th_.size(); }
+    void run(size_t k, const std::function<void(size_t)> &f);
+
+private:
+    struct Batch;
+    void helper();
+    static void work(Batch &b);
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Batch *> open_; /* batches with unclaimed indices */
+    bool stop_ = false;
+};
 
 /* /add (add_request.cc:115-170): per sequence PROTEIN-ID / CALL / OTU-COUNTS /
  * BEST-CALL unless silent, then every hit's k-mer is mapped to the
@@ -169,6 +208,10 @@ public:
 
 private:
     static constexpr size_t kPieceBytes = 1 << 20; /* krequest2.cc:41 */
+    /* a body under 2 pieces: parsed and written in sub-pieces of at least
+     * this size on the ForkJoin helpers, around one GPU pass */
+    static constexpr size_t kSplitBytes = 192 << 10;
+    static constexpr unsigned kHelpers = 3;
     class GutsLease;
     struct Mapping {
         std::shared_ptr<KmerPegMapping> map;
@@ -188,6 +231,8 @@ private:
     std::condition_variable pool_cv_;
     std::mutex mapping_mu_; /* the mapping map itself */
     std::map<std::string, Mapping> mapping_map_;
+    ForkJoin fj_{kHelpers};
+    std::atomic<int> query_in_flight_{0};
 };
 
 } // namespace kgx

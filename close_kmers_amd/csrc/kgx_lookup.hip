@@ -1727,6 +1727,8 @@ hipError_t launch_best_calls(uint32_t n_seq, const kgx_call *calls, const uint64
  * pairs in key order, std::sort by count, larger first (kguts.h:214-218).
  * Scratch: ws / otus of sequence s start at window_base[s] (a sequence has
  * no more flagged hits than windows). */
+constexpr int64_t OTU_LDS = 24; /* flagged hits per lane sorted in LDS (24 x 256 x 4 B = 24 KiB) */
+
 template <bool PK>
 __global__ __launch_bounds__(256) void otu_kernel(uint32_t n_seq, const uint64_t *__restrict__ wbase,
                                                   const uint64_t *__restrict__ hit_mask, uint32_t tile_windows,
@@ -1741,14 +1743,56 @@ __global__ __launch_bounds__(256) void otu_kernel(uint32_t n_seq, const uint64_t
     const uint64_t gw0 = wbase[s], gw1 = wbase[s + 1];
     int32_t *v = ws + gw0;
     int64_t n = 0;
+    int32_t vmin = INT32_MAX, vmax = INT32_MIN;
+    /* the lane's first OTU_LDS values also in LDS: sorting them there avoids
+     * a chain of dependent global loads and stores per compare */
+    __shared__ int32_t lv[OTU_LDS][256];
+    int32_t *mine = &lv[0][threadIdx.x];
     for_each_run(hit_mask, tile_windows, gw0, gw1, [&](uint64_t at0, uint32_t c, uint32_t, uint64_t, uint32_t) {
         for (uint32_t k = 0; k < c; k++) {
             const uint4 h = hot[at0 + k];
-            if (HF::flags(h) & KGX_HIT_OTU)
-                v[n++] = (int32_t)HF::otu(h, PK ? h : cold[at0 + k]);
+            if (HF::flags(h) & KGX_HIT_OTU) {
+                const int32_t x = (int32_t)HF::otu(h, PK ? h : cold[at0 + k]);
+                if (n < OTU_LDS)
+                    mine[256 * n] = x;
+                v[n++] = x;
+                vmin = min(vmin, x);
+                vmax = max(vmax, x);
+            }
         }
     });
-    const int64_t m = otu_finalize(v, n, otus + gw0);
+    int64_t m;
+    kgx_otu *o = otus + gw0;
+    if (n == 0) {
+        m = 0;
+    } else if (vmin == vmax) { /* one OTU: otu_map holds one pair, nothing to sort */
+        o[0] = kgx_otu{vmin, (int32_t)n};
+        m = 1;
+    } else if (n <= OTU_LDS) {
+        /* the map's keys in order: any sort of plain ints gives the same
+         * array (equal values are indistinguishable); insertion sort in LDS */
+        for (int64_t i = 1; i < n; i++) {
+            const int32_t x = mine[256 * i];
+            int64_t j = i - 1;
+            while (j >= 0 && mine[256 * j] > x) {
+                mine[256 * (j + 1)] = mine[256 * j];
+                j--;
+            }
+            mine[256 * (j + 1)] = x;
+        }
+        m = 0;
+        for (int64_t i = 0; i < n;) {
+            int64_t j = i + 1;
+            while (j < n && mine[256 * j] == mine[256 * i])
+                j++;
+            o[m++] = kgx_otu{mine[256 * i], (int32_t)(j - i)};
+            i = j;
+        }
+        /* finalize()'s std::sort of the pairs, replayed (tie order matters) */
+        lstd_sort(o, m, [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; });
+    } else {
+        m = otu_finalize(v, n, o);
+    }
     otu_count[s] = (uint32_t)m;
 }
 

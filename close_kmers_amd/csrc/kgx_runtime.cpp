@@ -2461,9 +2461,11 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
 int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
                         uint32_t n_seq, uint32_t want, kgx_result *out)
 {
+    PhaseTimer tm(c); /* KGX_TIMING: phase times (each mark waits for the stream) */
     int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq);
     if (rc)
         return rc;
+    tm.mark("s.stage");
     const uint64_t n_res = c->h_res.size();
     const uint64_t *off = c->h_off_stage.data();
     HIP_TRY(c->residues.reserve(round16(n_res + 16)));
@@ -2520,7 +2522,9 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
         at += sizes[p] / 16;
         pc.end16[p] = at;
     }
+    tm.mark("s.plan");
     HIP_TRY(launch_small_upload(pc, c->stream));
+    tm.mark("s.upload");
     /* a small probe neither waits for nor holds back the image's other probes:
      * chaining it (probe_serialize, for probes that fill the chip) would make
      * the pool's per-sequence calls run one at a time across worker threads */
@@ -2530,6 +2534,7 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     c->probe_serialize = serialize;
     if (rc)
         return rc;
+    tm.mark("s.probe");
     /* the scorer: with few sequences the lane machine's one-lane chain per
      * sequence is the whole stage's latency (31 us for one 300-aa protein);
      * the wave scorer spreads each sequence's hits over a wave (option
@@ -2544,6 +2549,7 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     rc = kgx_stage_score(c, params, want);
     c->score_variant = variant;
     c->score_wave_tiles = wave_tiles;
+    tm.mark("s.score");
     if (rc)
         return rc;
     /* results: worst-case mapped arrays, offsets and totals in mapped memory */
@@ -2651,6 +2657,7 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     HIP_TRY(c->h_hits.resize(need_hits ? nh : 0));
     HIP_TRY(c->h_calls.resize(nc));
     HIP_TRY(c->h_otus.resize(no));
+    tm.mark("s.gather");
     fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
     return KGX_OK;
 }

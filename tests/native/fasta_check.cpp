@@ -60,7 +60,9 @@ static std::string well_formed(std::mt19937_64 &rng, int n_rec)
 static std::string noisy(std::mt19937_64 &rng)
 {
     std::string b = well_formed(rng, 1 + (int)(rng() % 5));
-    static const char extra[] = ">\n\r *\t9-.xA";
+    /* also the bytes next to the letter ranges and high bytes, for the
+     * 16-byte validation: '@' '[' '`' '{' 0x80 0xC1 0xFA */
+    static const char extra[] = ">\n\r *\t9-.xA@[`{\x80\xc1\xfa";
     int k = 1 + (int)(rng() % 3);
     for (int i = 0; i < k; i++) {
         size_t at = b.empty() ? 0 : rng() % (b.size() + 1);
@@ -84,6 +86,12 @@ int main(int argc, char **argv)
             std::fwrite(b.data(), 1, b.size(), stdout);
             return 1;
         }
+        if (flat_of(want).res != parse_fasta_body_flat(b.data(), b.size()).res ||
+            flat_of(want).ids != parse_fasta_body_flat(b.data(), b.size()).ids ||
+            flat_of(want).off != parse_fasta_body_flat(b.data(), b.size()).off) {
+            std::printf("FLAT MISMATCH case %d\n", t);
+            return 1;
+        }
     }
     /* pieces cut by split_fasta_body, each parsed line by line, concatenate
      * to the whole-body parse whenever every piece parses */
@@ -101,6 +109,7 @@ int main(int argc, char **argv)
             return 1;
         }
         work_list_t joined;
+        FastaFlat joined_flat;
         bool ok = true;
         for (auto &c : cuts) {
             if (c.second <= c.first || b[c.first] != '>') {
@@ -108,10 +117,24 @@ int main(int argc, char **argv)
                 return 1;
             }
             ok = ok && parse_fasta_piece(b.data() + c.first, c.second - c.first, joined);
+            FastaFlat piece;
+            if (ok && !parse_fasta_piece_flat(b.data() + c.first, c.second - c.first, piece)) {
+                std::printf("FLAT PIECE REFUSED case %d\n", t);
+                return 1;
+            }
+            for (size_t i = 0; ok && i < piece.size(); i++)
+                joined_flat.add(piece.ids.data() + piece.id_off[i], piece.id_off[i + 1] - piece.id_off[i],
+                                piece.res.data() + piece.off[i], piece.off[i + 1] - piece.off[i]);
         }
         if (!ok)
             continue;
         split_used++;
+        const FastaFlat want_flat = flat_of(machine(b));
+        if (joined_flat.res != want_flat.res || joined_flat.ids != want_flat.ids || joined_flat.off != want_flat.off ||
+            joined_flat.id_off != want_flat.id_off) {
+            std::printf("SPLIT FLAT MISMATCH case %d\n", t);
+            return 1;
+        }
         if (joined != machine(b)) {
             std::printf("SPLIT MISMATCH case %d\n", t);
             std::fwrite(b.data(), 1, b.size(), stdout);

@@ -25,5 +25,5 @@ def _binary() -> str:
 
 
 def test_line_parser_matches_state_machine():
-    r = subprocess.run([_binary(), "20000"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([_binary(), "20000"], capture_output=True, text=True, errors="replace", timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok 20000"), r.stdout[:2000]

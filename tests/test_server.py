@@ -202,9 +202,12 @@ def test_concurrent_requests_match_golden(gpu):
 
 
 @pytest.mark.gpu
-def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp_path):
+@pytest.mark.parametrize("mib", [5, 1])
+def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp_path, mib):
     """A 5-MiB /query body is cut at record starts and its pieces run on 4
-    workers at once; the response is the oracle's text for the whole body."""
+    workers at once; a 1-MiB body is one GPU pass whose parse and text run in
+    sub-pieces on the router's helper threads.  Either way the response is
+    the oracle's text for the whole body."""
     import numpy as np
     from helpers import random_protein
     d = os.path.join(GOLDEN, "scoring")
@@ -213,7 +216,7 @@ def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp
     recs = [base]
     size = len(base)
     i = 0
-    while size < 5 << 20:
+    while size < mib << 20:
         r = b">p%d\n%s\n" % (i, random_protein(rng, int(rng.integers(5, 600))).encode())
         recs.append(r)
         size += len(r)
@@ -232,6 +235,10 @@ def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp
         got = srv.request("POST", "/query?details=1", body)
         want_d = oracle_lib.query_text(os.path.join(d, "data"), str(fasta), "query_details", {})
         assert got == HEADER + want_d
+        if mib == 1:
+            got = srv.request("POST", "/query?find_best_call=1", body)
+            want_b = oracle_lib.query_text(os.path.join(d, "data"), str(fasta), "query_best", {})
+            assert got == HEADER + want_b
     finally:
         srv.close()
 
