@@ -841,9 +841,75 @@ __global__ __launch_bounds__(256) void fq_emit_kernel(const uint8_t *bases, cons
 
 inline dim3 grid_for(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
+/* launch_fq_plan: fragment i's window base wbase[i] = (off[i] - off[0]) - 8 i
+ * (each fragment has len - 8 windows, len >= 9), the tiles whose first
+ * window lies in its windows get tile_seq = i, wbase[n] = the total;
+ * block_max[workgroup] = its longest fragment in windows */
+__global__ __launch_bounds__(256) void fq_plan_kernel(const uint64_t *__restrict__ off, uint32_t n,
+                                                      uint64_t *__restrict__ wbase, uint32_t *__restrict__ tile_seq,
+                                                      uint32_t tw, uint32_t tw_shift, uint32_t *__restrict__ block_max)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t o0 = off[0];
+    uint32_t w = 0;
+    if (i < n) {
+        const uint64_t a = off[i], b = off[i + 1];
+        const uint64_t wb = (a - o0) - 8 * i;
+        w = (uint32_t)(b - a - 8);
+        wbase[i] = wb;
+        const uint64_t t0 = tw_shift ? (wb + tw - 1) >> tw_shift : (wb + tw - 1) / tw;
+        for (uint64_t t = t0; t * tw < wb + w; t++)
+            tile_seq[t] = (uint32_t)i;
+    } else if (i == n) {
+        wbase[n] = (off[n] - o0) - 8 * (uint64_t)n;
+    }
+    /* the workgroup's longest fragment into block_max (one address for the
+     * whole grid would serialise its atomics: 1.5 ms per 155k waves) */
+    __shared__ uint32_t wmax[4];
+    for (uint32_t o = 32; o; o >>= 1) /* every lane shuffles (w = 0 past the batch) */
+        w = max(w, (uint32_t)__shfl_xor((int)w, (int)o));
+    if ((threadIdx.x & 63u) == 0)
+        wmax[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        block_max[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+}
+
+/* status[0] = 0 (no bad offsets), status[1] = the longest fragment */
+__global__ __launch_bounds__(1024) void fq_plan_max_kernel(const uint32_t *__restrict__ block_max, uint32_t n,
+                                                           uint32_t *__restrict__ status)
+{
+    __shared__ uint32_t wmax[16];
+    uint32_t m = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += 1024)
+        m = max(m, block_max[i]);
+    for (uint32_t o = 32; o; o >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, (int)o));
+    if ((threadIdx.x & 63u) == 0)
+        wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t k = 1; k < 16; k++)
+            m = max(m, wmax[k]);
+        status[0] = 0;
+        status[1] = m;
+    }
+}
+
 }  // namespace
 
 namespace kgx {
+
+hipError_t launch_fq_plan(const uint64_t *off, uint32_t n, uint64_t *wbase, uint32_t *tile_seq, uint32_t tile_windows,
+                          uint32_t *status, uint32_t *block_max, hipStream_t stream)
+{
+    const uint32_t shift = (tile_windows & (tile_windows - 1)) ? 0u : (uint32_t)__builtin_ctz(tile_windows);
+    const dim3 grid = grid_for((uint64_t)n + 1);
+    hipLaunchKernelGGL(fq_plan_kernel, grid, dim3(256), 0, stream, off, n, wbase, tile_seq, tile_windows, shift,
+                       block_max);
+    hipLaunchKernelGGL(fq_plan_max_kernel, dim3(1), dim3(1024), 0, stream, block_max, grid.x, status);
+    return hipGetLastError();
+}
 
 /* fragments of the reads in [d_bases, read_off) into the ctx's fq buffers.
  * n_bases: the bytes the reads span (read_off[n] - read_off[0]), which bounds

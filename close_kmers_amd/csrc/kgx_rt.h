@@ -254,6 +254,12 @@ int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const ui
 int plan_reserve(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_residues);
 /* whether this context's probe can take fragments as DNA */
 bool probe_takes_dna(const kgx_ctx *c);
+/* the lookup's plan over fragments of at least 9 residues each (every
+ * fragment a fragment pass emits has >= 11): window base = residue offset - 8
+ * per earlier fragment, no scan; tile owners and the longest fragment as
+ * launch_plan writes them (kgx_fq.hip) */
+hipError_t launch_fq_plan(const uint64_t *off, uint32_t n, uint64_t *wbase, uint32_t *tile_seq, uint32_t tile_windows,
+                          uint32_t *status, uint32_t *block_max, hipStream_t stream);
 
 }  // namespace kgx
 
@@ -326,6 +332,8 @@ struct kgx_ctx {
     int probe_persist = 0; /* line probe grid cap in workgroups per CU, waves stride over tiles (option "probe_persist") */
     int fq_residues = 1;   /* 1: kgx_fq_fragments writes residues; 0: anchors (kgx_fq_run_device) */
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
+    int fq_probe_j = 1;    /* tile of the DNA probe (fragments as anchors), 64 x J windows; 0 = probe_j */
+    int fq_plan = 1;       /* 1: this context's fragments are planned elementwise (fq_plan_kernel); 0: launch_plan */
     int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */

@@ -1056,6 +1056,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->score_wave_tiles = (int)value;
         return KGX_OK;
     }
+    if (n == "fq_plan") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "fq_plan must be 0 or 1");
+        c->fq_plan = (int)value;
+        return KGX_OK;
+    }
+    if (n == "fq_probe_j") {
+        if (value < 0 || value > 4)
+            return fail(KGX_EINVAL, "fq_probe_j must be 0 (= probe_j), 1, 2, 3 or 4");
+        c->fq_probe_j = (int)value;
+        return KGX_OK;
+    }
     if (n == "probe_j") {
         if (!probe_j_supported((int)value))
             return fail(KGX_EINVAL, "probe_j must be 1, 2, 3, 4, 5 or 8");
@@ -1369,10 +1381,33 @@ int kgx_fq_run_device(kgx_ctx *c, const kgx_params *params, const kgx_fragments 
         return fail(KGX_EINVAL, "null argument");
     if (fr->residues || fr->n_fragments == 0)
         return kgx_run_device(c, params, fr->residues, fr->offsets, fr->n_fragments, fr->n_residues, want, out);
-    int rc = kgx_stage_plan(c, fr->offsets, fr->n_fragments, fr->n_residues);
+    /* the DNA probe's own tile (option fq_probe_j): its encode reads 24
+     * bases and 32 table entries per window, and one slice per wave keeps
+     * more waves' line requests in flight (C4 probe 4.0-4.3 vs 4.4-4.9 ms per
+     * 1M reads at J = 1 vs 2, profiles/r3e_fq_probe_j_sweep.json).  The plan,
+     * probe and score of the pass use it; the result carries its tile size. */
+    HIP_TRY(hipSetDevice(c->img->device));
+    const int keep_j = c->probe_j;
+    if (c->fq_probe_j)
+        c->probe_j = c->fq_probe_j;
+    /* this context's own fragments (>= 11 residues each) are planned by one
+     * elementwise kernel instead of launch_plan's reduce / scan / scan */
+    const bool own = c->fq_plan && fr->offsets == c->fq_off.as<uint64_t>();
+    int rc = own ? kgx::plan_reserve(c, fr->offsets, fr->n_fragments, fr->n_residues)
+                 : kgx_stage_plan(c, fr->offsets, fr->n_fragments, fr->n_residues);
+    if (!rc && own) {
+        /* one longest-fragment word per 256-fragment workgroup */
+        hipError_t e = c->plan_ws.reserve(((size_t)fr->n_fragments / 256 + 2) * sizeof(uint32_t));
+        if (e == hipSuccess)
+            e = launch_fq_plan(fr->offsets, fr->n_fragments, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                               c->tile_windows, c->plan_status.as<uint32_t>(), c->plan_ws.as<uint32_t>(), c->stream);
+        if (e != hipSuccess)
+            rc = fail(KGX_EDEVICE, std::string("fq plan: ") + hipGetErrorString(e));
+    }
+    if (!rc)
+        rc = stage_probe_dna(c, fr->bases, fr->n_bases, fr->anchors, fr->offsets);
+    c->probe_j = keep_j;
     if (rc)
-        return rc;
-    if ((rc = stage_probe_dna(c, fr->bases, fr->n_bases, fr->anchors, fr->offsets)))
         return rc;
     if ((rc = kgx_stage_score(c, params, want)))
         return rc;

@@ -287,6 +287,12 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "microbench_wgs" (1..32) 256-thread workgroups per CU;
  * "probe_j" = windows per lane (1, 2, 3, 4, 5 or 8, default 2; a tile
  * is 64 * probe_j windows), read at the next plan;
+ * "fq_probe_j" (0..4, default 1) = windows per lane of kgx_fq_run_device's
+ * DNA probe (fragments as anchors), 0 = probe_j;
+ * "fq_plan" 1 (default) = kgx_fq_run_device plans the fragments of the
+ * context's own fragment pass with one elementwise kernel (each has >= 11
+ * residues, so a window base is its residue offset - 8 per earlier fragment),
+ * 0 = the general plan (reduce, scan, scan);
  * "probe_stream" 1 = the image's chained probes all on one image-wide stream
  * (default 0: each on its context's stream, chained by events; same speed);
  * "probe_persist" (0..32, default 0) caps the line probe's grid at that many

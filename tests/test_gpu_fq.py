@@ -217,10 +217,12 @@ def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count):
     assert f0.n_fragments > 1000 and (h0["anchors"] & 1).sum() > 100
 
 
-def test_fragment_lookup_dna_probe_matches_oracle(gpu, oracle_lib):
+@pytest.mark.parametrize("fq_probe_j,fq_plan", [(1, 1), (2, 1), (4, 1), (0, 1), (1, 0)])
+def test_fragment_lookup_dna_probe_matches_oracle(gpu, oracle_lib, fq_probe_j, fq_plan):
     """kgx_fq_run_device over anchors (the probe translating codons itself)
     gives the oracle's hits and calls over the translated fragments, and the
-    same device results as the residue probe."""
+    same device results as the residue probe -- at each DNA probe tile
+    (fq_probe_j; 0 = the context's probe_j, here 3)."""
     from close_kmers_amd import synth
     from tests_golden_codons import back_translate, revcomp
     spec, table = synthetic_table(40000)
@@ -241,11 +243,19 @@ def test_fragment_lookup_dna_probe_matches_oracle(gpu, oracle_lib):
         h = ctx.fragments_to_host(ctx.fq_fragments(res, off))
         ref = ctx.run_fragments(ctx.fq_fragments(res, off), prm, want=3)
         ctx.set_option("fq_residues", 0)
+        ctx.set_option("fq_probe_j", fq_probe_j)
+        ctx.set_option("fq_plan", fq_plan)
+        if fq_probe_j == 0:
+            ctx.set_option("probe_j", 3)
         f = ctx.fq_fragments(res, off)
         assert not f.residues
         got = ctx.run_fragments(f, prm, want=3)
+        # the fragment pass wrote the lookup's plan; another batch on the
+        # context replaces it, and the same fragments then plan again
+        ctx.process_batch(h["residues"][:5000], np.array([0, 2000, 5000], np.uint64), prm)
+        again = ctx.run_fragments(f, prm, want=3)
     want = oracle_lib.process_batch(table, h["residues"], h["offsets"], want=3)
-    for r in (got, ref):
+    for r in (got, ref, again):
         assert np.array_equal(r.hit_offsets, want.hit_offsets)
         for k in ("which_kmer", "pos", "function_index", "otu_index", "avg_from_end"):
             assert np.array_equal(r.hits[k], want.hits[k]), k

@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--probe-persist", type=int, default=-1, help="line-probe grid cap per CU; -1 = the library default")
     ap.add_argument("--fq-residues", type=int, default=0,
                     help="1 = fragments with residues + the residue probe; 0 (default) = anchors + the DNA probe")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a context option (kgx_ctx_set_option) on every worker context, e.g. probe_j=3")
     args = ap.parse_args()
 
     from close_kmers_amd import abi, image_files, synth
@@ -82,6 +84,9 @@ def main():
         if args.probe_persist >= 0:
             c.set_option("probe_persist", args.probe_persist)
         c.set_option("fq_residues", args.fq_residues)
+        for o in args.opt:
+            k, v = o.split("=", 1)
+            c.set_option(k, int(v))
     n, Lr = args.n_reads, args.length
     rng = np.random.default_rng(0x5EED0004)
     bases = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * Lr, dtype=np.uint8)]
@@ -198,7 +203,7 @@ def main():
     line = {
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
-        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "size_ahead": int(bool(args.ahead) and len(ctxs) >= 2), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "probe_persist": args.probe_persist, "fq_residues": args.fq_residues, "n_keys": spec.n_keys,
+        "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "size_ahead": int(bool(args.ahead) and len(ctxs) >= 2), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "probe_persist": args.probe_persist, "fq_residues": args.fq_residues, "options": args.opt, "n_keys": spec.n_keys,
                    "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "output_lines": out.count(b"\n"),
