@@ -633,11 +633,6 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     __shared__ uint8_t cod_tab[DNA ? 68 : 1];
     __shared__ uint4 lds_rec[PROBE_WAVES][T];
     __shared__ uint8_t lds_hit[PROBE_WAVES][T];
-    const uint64_t W = wbase[n_seq];
-    /* the grid is sized by the residues' bound on the windows: a workgroup
-     * whose first tile is past the batch leaves before its table setup */
-    if ((uint64_t)blockIdx.x * PROBE_WAVES * T >= W)
-        return;
     if (DNA) {
         const uint32_t b = threadIdx.x | 0x20u; /* ACGTU either case (trans_table.h:45-68) */
         const bool base = b == 'a' || b == 'c' || b == 'g' || b == 't' || b == 'u';
@@ -651,6 +646,7 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = lane_id();
+    const uint64_t W = wbase[n_seq];
     /* one tile per wave, or (a grid smaller than the tiles, option
      * probe_persist) the wave strides over tiles: every wave leaves once its
      * next tile lies past the batch's last window */
