@@ -1185,6 +1185,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
             throw_last(rc, "kgx_kmap_lookup");
     }
     stage_stats().gpu_ns += now_ns() - g0;
+    StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
     for (uint32_t s = 0; s < n; s++) {
         const std::string &id = work[s].first;
