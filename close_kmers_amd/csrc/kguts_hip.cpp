@@ -1187,6 +1187,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
     stage_stats().gpu_ns += now_ns() - g0;
     StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
+    std::string line;
     for (uint32_t s = 0; s < n; s++) {
         const std::string &id = work[s].first;
         seq_score_.clear();
@@ -1230,7 +1231,7 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
             float lf_score = 0.0f, gf_score = 0.0f;
             std::string lf_fam, lf_fn, gf_fam;
             std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
-            for (auto hit_ent : seq_score_) {
+            for (const auto &hit_ent : seq_score_) {
                 const acc_t &se = hit_ent.second;
                 if (se.hit_total < kmer_hit_threshold_)
                     continue;
@@ -1258,13 +1259,30 @@ void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::
                 }
             }
             auto *rollup = (do_ambig && lf_fn == ambig) ? &pgf_rollup_ambig : &pgf_rollup;
-            for (auto pgf_ent : *rollup)
+            for (const auto &pgf_ent : *rollup)
                 if (pgf_ent.second > gf_score) {
                     gf_score = pgf_ent.second;
                     gf_fam = pgf_ent.first;
                 }
-            os << id << "\t" << gf_fam << "\t" << gf_score << "\t" << lf_fam << "\t" << lf_score << "\t"
-               << (do_ambig ? lf_fn : fn) << "\t" << score << "\t" << wscore << "\n";
+            /* the iostream line (lookup_request.cc), floats as operator<< prints them (%.6g) */
+            line.clear();
+            line += id;
+            line += '\t';
+            line += gf_fam;
+            line += '\t';
+            append_f32(line, gf_score);
+            line += '\t';
+            line += lf_fam;
+            line += '\t';
+            append_f32(line, lf_score);
+            line += '\t';
+            line += do_ambig ? lf_fn : fn;
+            line += '\t';
+            append_f32(line, score);
+            line += '\t';
+            append_f32(line, wscore);
+            line += '\n';
+            os.write(line.data(), (std::streamsize)line.size());
         } else {
             typedef std::pair<KmerPegMapping::encoded_id_t, acc_t> data_t;
             std::vector<data_t> vec(seq_score_.begin(), seq_score_.end());

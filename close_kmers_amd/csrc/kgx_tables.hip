@@ -17,6 +17,8 @@
  */
 #include <hipcub/hipcub.hpp>
 
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "kgx_device.h"
@@ -405,12 +407,24 @@ struct CubTemp {
 
 /* ------------------------------------------------------------------------ */
 
+/* buffers and a stream of one kgx_kmap_lookup call: a map serves concurrent
+ * lookups (the router's workers hold the mapping's read lock), each on a
+ * scratch of its own taken from the map's free list -- no allocation and no
+ * shared stream per call (a hipFree per call serialised the workers) */
+struct KmapScratch {
+    hipStream_t st = nullptr;
+    DevBuf k, c, ids;
+    PinnedVec<uint64_t> cnt;
+};
+
 struct kgx_kmap {
     int device = 0;
     int mode = KGX_KMAP_APPEND;
     hipStream_t stream = nullptr;
     uint64_t n_rows = 0, n_vals = 0, hcap = 0;
     DevBuf keys, starts, vals, hkeys, hrow;
+    std::mutex scratch_mu;
+    std::vector<std::unique_ptr<KmapScratch>> scratch_free;
     KmapView view() const
     {
         KmapView v;
@@ -618,6 +632,11 @@ int kgx_kmap_destroy(kgx_kmap *m)
     (void)hipStreamSynchronize(m->stream);
     for (DevBuf *b : {&m->keys, &m->starts, &m->vals, &m->hkeys, &m->hrow})
         b->release();
+    for (auto &sc : m->scratch_free) {
+        for (DevBuf *b : {&sc->k, &sc->c, &sc->ids})
+            b->release();
+        (void)hipStreamDestroy(sc->st);
+    }
     (void)hipStreamDestroy(m->stream);
     delete m;
     return KGX_OK;
@@ -700,28 +719,48 @@ int kgx_kmap_lookup(kgx_kmap *m, const uint64_t *kmers, uint64_t n, uint64_t *of
     if (n == 0)
         return KGX_OK;
     HIP_TRY(hipSetDevice(m->device));
-    hipStream_t st = m->stream;
-    DevBuf d_k, d_c;
-    HIP_TRY(d_k.reserve(n * 8));
-    HIP_TRY(d_c.reserve((n + 1) * 8));
-    HIP_TRY(hipMemcpyAsync(d_k.p, kmers, n * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(lookup_count_kernel, grid_for(n), dim3(256), 0, st, m->view(), d_k.as<uint64_t>(), n,
-                       d_c.as<uint64_t>());
-    std::vector<uint64_t> cnt(n);
-    HIP_TRY(hipMemcpyAsync(cnt.data(), d_c.p, n * 8, hipMemcpyDeviceToHost, st));
+    std::unique_ptr<KmapScratch> sc;
+    {
+        std::lock_guard<std::mutex> lk(m->scratch_mu);
+        if (!m->scratch_free.empty()) {
+            sc = std::move(m->scratch_free.back());
+            m->scratch_free.pop_back();
+        }
+    }
+    if (!sc) {
+        sc.reset(new KmapScratch);
+        HIP_TRY(hipStreamCreateWithFlags(&sc->st, hipStreamNonBlocking));
+    }
+    struct Return { /* the scratch goes back to the free list, whatever happens */
+        kgx_kmap *m;
+        std::unique_ptr<KmapScratch> &sc;
+        ~Return()
+        {
+            std::lock_guard<std::mutex> lk(m->scratch_mu);
+            m->scratch_free.push_back(std::move(sc));
+        }
+    } give_back{m, sc};
+    hipStream_t st = sc->st;
+    HIP_TRY(sc->k.reserve(n * 8));
+    HIP_TRY(sc->c.reserve((n + 1) * 8));
+    HIP_TRY(sc->cnt.resize(n));
+    HIP_TRY(hipMemcpyAsync(sc->k.p, kmers, n * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lookup_count_kernel, grid_for(n), dim3(256), 0, st, m->view(), sc->k.as<uint64_t>(), n,
+                       sc->c.as<uint64_t>());
+    HIP_TRY(hipMemcpyAsync(sc->cnt.data(), sc->c.p, n * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t *cnt = sc->cnt.data();
     for (uint64_t i = 0; i < n; i++)
         offsets[i + 1] = offsets[i] + cnt[i];
     if (!ids)
         return KGX_OK;
     if (ids_cap < offsets[n])
         return fail(KGX_ERANGE, "ids buffer too small");
-    DevBuf d_ids;
-    HIP_TRY(d_ids.reserve(std::max<uint64_t>(offsets[n], 1) * 4));
-    HIP_TRY(hipMemcpyAsync(d_c.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(lookup_ids_kernel, grid_for(n), dim3(256), 0, st, m->view(), d_k.as<uint64_t>(), n,
-                       d_c.as<uint64_t>(), d_ids.as<uint32_t>());
-    HIP_TRY(hipMemcpyAsync(ids, d_ids.p, offsets[n] * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(sc->ids.reserve(std::max<uint64_t>(offsets[n], 1) * 4));
+    HIP_TRY(hipMemcpyAsync(sc->c.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(lookup_ids_kernel, grid_for(n), dim3(256), 0, st, m->view(), sc->k.as<uint64_t>(), n,
+                       sc->c.as<uint64_t>(), sc->ids.as<uint32_t>());
+    HIP_TRY(hipMemcpyAsync(ids, sc->ids.p, offsets[n] * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return KGX_OK;
 }
