@@ -16,7 +16,8 @@ from . import build as _build
 
 KGX_OK = 0
 ERRORS = {-1: "EINVAL", -2: "EIO", -3: "EFORMAT", -4: "ENOMEM", -5: "EDEVICE", -6: "ERANGE",
-          -7: "EFULL"}
+          -7: "EFULL", -8: "EBUSY"}
+KGX_EBUSY = -8
 WANT_HITS, WANT_CALLS, WANT_OTU, WANT_BEST = 1, 2, 4, 8
 HIT_IN_RUN, HIT_OTU = 1, 2
 
@@ -241,6 +242,11 @@ SIGNATURES = {
     "kgx_compact_expand": (_INT, [ctypes.POINTER(CompactResult), _P, _P, _U32, _U32, _U32, _P]),
     "kgx_ctx_host_profile": (_INT, [_P, ctypes.POINTER(HostProfile)]),
     "kgx_ctx_stat": (_INT, [_P, _CS, ctypes.POINTER(ctypes.c_int64)]),
+    "kgx_svc_call": (_INT, [_P, ctypes.POINTER(Params), _P, _U64, _U32, _P, _U64, ctypes.POINTER(_U64), _P, _U64,
+                            ctypes.POINTER(_U64)]),
+    "kgx_svc_config": (_INT, [_P, _U32, _U32, _U32]),
+    "kgx_svc_stop": (_INT, [_P]),
+    "kgx_svc_stat": (_INT, [_P, _CS, ctypes.POINTER(_U64)]),
 }
 
 
@@ -404,6 +410,31 @@ class Image:
         t = np.empty(self.num_sigs, dtype=SIG_DTYPE)
         check(lib().kgx_image_download(self.handle, t.ctypes.data, t.nbytes), "kgx_image_download")
         return t
+
+    def svc_call(self, seq: bytes, params=None, want: int = WANT_HITS | WANT_CALLS):
+        """One sequence through the resident call service (kgx_svc_call):
+        (hits, calls) arrays; raises KgxError (code KGX_EBUSY) for a call the
+        service does not take."""
+        p = params if isinstance(params, Params) else parse_params(params)
+        W = max(len(seq) - 8, 0)
+        hits = np.empty(max(W, 1), HIT_DTYPE)
+        calls = np.empty(max(W, 1), CALL_DTYPE)
+        nh, nc = _U64(), _U64()
+        buf = ctypes.create_string_buffer(bytes(seq), max(len(seq), 1))
+        check(lib().kgx_svc_call(self.handle, ctypes.byref(p), buf, len(seq), want, hits.ctypes.data, W,
+                                 ctypes.byref(nh), calls.ctypes.data, W, ctypes.byref(nc)), "kgx_svc_call")
+        return hits[:nh.value].copy(), calls[:nc.value].copy()
+
+    def svc_config(self, slots: int = 32, idle_us: int = 1000, life_us: int = 4000) -> None:
+        check(lib().kgx_svc_config(self.handle, slots, idle_us, life_us), "kgx_svc_config")
+
+    def svc_stop(self) -> None:
+        check(lib().kgx_svc_stop(self.handle), "kgx_svc_stop")
+
+    def svc_stat(self, name: str) -> int:
+        v = _U64()
+        check(lib().kgx_svc_stat(self.handle, name.encode(), ctypes.byref(v)), "kgx_svc_stat")
+        return v.value
 
     def close(self) -> None:
         if self.handle:

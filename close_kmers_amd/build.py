@@ -27,7 +27,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 LIB_SOURCES = ["kgx_lookup.hip", "kgx_fused.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
-               "kgx_pool.cpp", "kguts_hip.cpp", "kgx_handlers.cpp"]
+               "kgx_pool.cpp", "kgx_svc.cpp", "kguts_hip.cpp", "kgx_handlers.cpp"]
 HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h", "kgx_handlers.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-Wall", "-Wno-unused-function"]

@@ -161,6 +161,12 @@ KmerGuts::KmerGuts(const std::string &kmer_dir, std::shared_ptr<KmerImage> image
 
 KmerGuts::~KmerGuts() { kgx_ctx_destroy(ctx_); }
 
+bool KmerGuts::default_service()
+{
+    const char *e = std::getenv("KGX_SVC");
+    return !(e && std::atoi(e) == 0);
+}
+
 void KmerGuts::set_default_parameters()
 {
     kgx_params p;
@@ -386,11 +392,50 @@ void KmerGuts::process_aa_seq(const std::string &id, const std::string &seq,
                               std::function<void(hit_in_sequence_t)> hit_cb,
                               std::shared_ptr<KmerOtuStats> otu_stats)
 {
+    const uint32_t want = (hit_cb ? KGX_WANT_HITS : 0u) | (calls ? KGX_WANT_CALLS : 0u) | (otu_stats ? KGX_WANT_OTU : 0u);
+    if (coalesce && service && want && !(want & KGX_WANT_OTU)) {
+        /* the image's resident call service: no launch on this call's path
+         * (KGX_EBUSY: not a call it serves, or every slot taken -> below) */
+        thread_local std::vector<kgx_hit> hbuf;
+        thread_local std::vector<kgx_call> cbuf;
+        const uint64_t W = seq.size() >= 9 ? seq.size() - 8 : 0;
+        if (hbuf.size() < W)
+            hbuf.resize(W);
+        if (cbuf.size() < W)
+            cbuf.resize(W);
+        const kgx_params p{min_hits, max_gap, order_constraint, min_weighted_hits};
+        uint64_t nh = 0, nc = 0;
+        const int rc = kgx_svc_call(image_->handle(), &p, seq.data(), seq.size(), want, hbuf.data(), hbuf.size(), &nh,
+                                    cbuf.data(), cbuf.size(), &nc);
+        if (rc == KGX_OK) {
+            /* replay on the calling thread, in position order (kguts.cc:814-815) */
+            if (hit_cb)
+                for (uint64_t i = 0; i < nh; i++) {
+                    const kgx_hit &h = hbuf[i];
+                    sig_kmer_t e;
+                    e.which_kmer = h.which_kmer;
+                    e.otu_index = h.otu_index;
+                    e.avg_from_end = h.avg_from_end;
+                    e.pad = 0;
+                    e.function_index = h.function_index;
+                    e.function_wt = h.function_wt;
+                    hit_cb(hit_in_sequence_t(e, h.pos));
+                }
+            if (calls)
+                for (uint64_t i = 0; i < nc; i++) {
+                    const kgx_call &c = cbuf[i];
+                    calls->push_back(KmerCall(c.start, c.end, c.count, c.function_index, c.weighted_hits));
+                }
+            return;
+        }
+        if (rc != KGX_EBUSY)
+            throw_last(rc, "kgx_svc_call");
+    }
     if (coalesce) {
         SeqCoalescer::Req q;
         q.seq = &seq;
         q.params = kgx_params{min_hits, max_gap, order_constraint, min_weighted_hits};
-        q.want = (hit_cb ? KGX_WANT_HITS : 0u) | (calls ? KGX_WANT_CALLS : 0u) | (otu_stats ? KGX_WANT_OTU : 0u);
+        q.want = want;
         image_->coalescer().submit(ctx_, q);
         if (q.rc)
             throw Error(q.rc, "process_aa_seq: " + std::string(kgx_strerror(q.rc)) + " (" + q.err + ")");

@@ -228,6 +228,11 @@ public:
     /* process_aa_seq joins the image's queue of concurrent calls (default
      * on; SeqCoalescer); off: one GPU pass per call on this object's context */
     bool coalesce = true;
+    /* with coalesce: calls the image's resident call service serves
+     * (kgx_svc_call: one sequence, hits / calls, order_constraint 0) skip the
+     * queue and the launch; default on, KGX_SVC=0 turns it off */
+    bool service = default_service();
+    static bool default_service();
 
     void find_best_call(std::vector<KmerCall> &calls, int &function_index, std::string &function,
                         float &score, float &weighted_score, float &score_offset);

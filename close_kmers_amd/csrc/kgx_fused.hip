@@ -62,19 +62,26 @@ struct FusedMapped { /* the mapped arrays instead (FusedArgs.res / off / wbase) 
 /* FJ = windows per thread at most (the batch's longest sequence has at most
  * 256 FJ windows): 2 for proteins up to 520 aa, 8 up to FUSED_MAX_WINDOWS */
 template <uint32_t FJ, class IN>
-__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k);
+__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, uint32_t s);
 
 template <uint32_t FJ>
 __global__ __launch_bounds__(256) void fused_small_kernel(FusedArgs a)
 {
-    fused_small_body<FJ>(a, FusedMapped{});
+    fused_small_body<FJ>(a, FusedMapped{}, blockIdx.x);
 }
 
 template <uint32_t FJ>
 __global__ __launch_bounds__(256) void fused_small_inline_kernel(FusedArgs a, FusedInline k)
 {
-    fused_small_body<FJ>(a, k);
+    fused_small_body<FJ>(a, k, blockIdx.x);
 }
+
+/* one sequence in a service slot (svc_kernel): residues in the slot's mapped
+ * buffer, offsets {0, len}, window bases {0, W} */
+struct FusedSlot {
+    const uint8_t *res;
+    uint32_t len;
+};
 
 template <class IN> struct FusedInput;
 template <> struct FusedInput<FusedMapped> {
@@ -87,9 +94,14 @@ template <> struct FusedInput<FusedInline> {
     __device__ static uint64_t wb(const FusedArgs &, const FusedInline &k, uint32_t i) { return k.wb[i]; }
     __device__ static uint8_t res(const FusedArgs &, const FusedInline &k, uint64_t i) { return k.res[i]; }
 };
+template <> struct FusedInput<FusedSlot> {
+    __device__ static uint64_t off(const FusedArgs &, const FusedSlot &k, uint32_t i) { return i ? k.len : 0u; }
+    __device__ static uint64_t wb(const FusedArgs &, const FusedSlot &, uint32_t) { return 0; }
+    __device__ static uint8_t res(const FusedArgs &, const FusedSlot &k, uint64_t i) { return k.res[i]; }
+};
 
 template <uint32_t FJ, class IN>
-__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k)
+__device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, const uint32_t s)
 {
     typedef FusedInput<IN> In;
     const bool dbg = a.dbg && blockIdx.x == 0 && threadIdx.x == 0;
@@ -102,7 +114,6 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     __shared__ uint32_t wave_cnt[4];
     typedef HitFields<true> HF;
 
-    const uint32_t s = blockIdx.x;
     const uint32_t t = threadIdx.x, lane = lane_id(), wave = t >> 6;
     code_tab[t] = (uint8_t)residue_code(t);
     const uint64_t r0 = In::off(a, k, s), len = In::off(a, k, s + 1) - r0;
@@ -441,6 +452,111 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
     } else {
         hipLaunchKernelGGL(fused_small_kernel<FUSED_MAX_WINDOWS / 256>, dim3(n), dim3(256), 0, stream, a);
     }
+    return hipGetLastError();
+}
+
+/*
+ * The resident call service: the same per-sequence body, served from slots in
+ * mapped host memory by workgroups that stay resident, so a call costs no
+ * launch (the runtime's launch path serialises a worker pool's threads:
+ * ~6 us of host time per launch, 170K calls/s at T = 16 in r3g).  Workgroup
+ * i owns slot i: thread 0 polls the slot's {req, stop} word with a
+ * system-scope acquire load (the host wrote the residues, length, want and
+ * parameters before it stored req), the workgroup runs the sequence, and
+ * fused_small_body stores the records, the counts and done = req behind a
+ * system-scope fence.  Every workgroup leaves on stop, after idle_ticks
+ * without a request in any slot, or life_ticks after its start -- a bound on
+ * how long the instance holds its hardware queue; the host keeps the next
+ * instance queued behind it (kgx_svc.cpp).
+ */
+__global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res_base,
+                                                  kgx_hit *hits, kgx_call *calls, const uint4 *table,
+                                                  uint64_t num_sigs, uint64_t magic, uint64_t *activity,
+                                                  uint64_t idle_ticks, uint64_t life_ticks)
+{
+    __shared__ uint32_t cmd[8];
+    const uint32_t slot = blockIdx.x, t = threadIdx.x;
+    const uint64_t t0 = wall_clock64();
+    uint32_t last = 0;
+    if (t == 0)
+        last = __hip_atomic_load(&out[slot].done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t *word = reinterpret_cast<const uint64_t *>(&hdr[slot].req);
+    for (;;) {
+        if (t == 0) {
+            uint32_t go = 0;
+            for (;;) {
+                const uint64_t w = __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((uint32_t)(w >> 32)) /* stop */
+                    break;
+                if ((uint32_t)w != last) {
+                    go = 1;
+                    cmd[1] = (uint32_t)w;
+                    break;
+                }
+                const uint64_t now = wall_clock64();
+                const uint64_t act = __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (now - t0 > life_ticks || now - (act > t0 ? act : t0) > idle_ticks)
+                    break;
+                __builtin_amdgcn_s_sleep(8);
+            }
+            if (go) {
+                __hip_atomic_fetch_max(activity, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const SvcSlotHdr &h = hdr[slot];
+                cmd[2] = __hip_atomic_load(&h.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[3] = __hip_atomic_load(&h.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[4] = (uint32_t)__hip_atomic_load(&h.prm.min_hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[5] = (uint32_t)__hip_atomic_load(&h.prm.max_gap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[6] = (uint32_t)__hip_atomic_load(&h.prm.order_constraint, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[7] = (uint32_t)__hip_atomic_load(&h.prm.min_weighted_hits, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            cmd[0] = go;
+        }
+        __syncthreads();
+        if (!cmd[0])
+            break;
+        /* the residues the host wrote before req: no stale line in this CU's caches */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        FusedArgs a;
+        const uint32_t len = min(cmd[2], SVC_MAX_RES);
+        a.res = nullptr;
+        a.off = nullptr;
+        a.wbase = nullptr;
+        a.n = 1;
+        a.want = cmd[3];
+        a.table = table;
+        a.num_sigs = num_sigs;
+        a.magic = magic;
+        a.prm.min_hits = (int32_t)cmd[4];
+        a.prm.max_gap = (int32_t)cmd[5];
+        a.prm.order_constraint = (int32_t)cmd[6];
+        a.prm.min_weighted_hits = (int32_t)cmd[7];
+        a.hits = hits + (uint64_t)slot * FUSED_MAX_WINDOWS;
+        a.calls = calls + (uint64_t)slot * FUSED_MAX_WINDOWS;
+        a.counts = &out[slot].nh;
+        a.done = &out[slot].done;
+        a.token = cmd[1];
+        a.dbg = nullptr;
+        const FusedSlot in{res_base + (uint64_t)slot * SVC_RES_STRIDE, len};
+        if (len <= 2 * 256 + 8)
+            fused_small_body<2>(a, in, 0);
+        else
+            fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
+        last = cmd[1];
+        __syncthreads(); /* cmd is rewritten by the next poll */
+    }
+}
+
+hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res, kgx_hit *hits, kgx_call *calls,
+                      uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
+                      uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream)
+{
+    if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, res, hits, calls,
+                       static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), activity, idle_ticks,
+                       life_ticks);
     return hipGetLastError();
 }
 

@@ -235,6 +235,33 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
                               kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
                               uint32_t max_windows, uint64_t *dbg, const uint64_t *h_off, const uint64_t *h_wbase,
                               const uint8_t *h_res, uint32_t inline_res, hipStream_t stream);
+/* resident call service (kgx_svc.cpp, svc_kernel in kgx_fused.hip): one
+ * persistent workgroup per slot polls its slot's request word in mapped host
+ * memory and runs fused_small_body on the slot's sequence; no launch per call.
+ * A slot takes one sequence of at most SVC_MAX_RES residues. */
+constexpr uint32_t SVC_MAX_RES = FUSED_MAX_WINDOWS + 8;
+constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residues per slot */
+constexpr uint32_t SVC_MAX_SLOTS = 64;
+struct SvcSlotHdr { /* host-written, one 64-B line per slot */
+    uint32_t req;   /* request number: the device serves it when it differs from SvcSlotOut.done */
+    uint32_t stop;  /* nonzero: the service's workgroups leave */
+    uint32_t len;   /* residues */
+    uint32_t want;  /* KGX_WANT_HITS | KGX_WANT_CALLS */
+    kgx_params prm;
+    uint32_t pad[8];
+};
+struct SvcSlotOut { /* device-written, one 64-B line per slot */
+    uint32_t nh, nc; /* hit / call records stored */
+    uint32_t done;   /* = req once the records and counts are visible */
+    uint32_t pad[13];
+};
+static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64, "service slot lines");
+/* slots workgroups on stream; each leaves once no slot has had a request for
+ * idle_ticks, or life_ticks after its start, or on stop (device wall clock,
+ * 100 MHz); activity: a device word, the latest request pickup */
+hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res, kgx_hit *hits, kgx_call *calls,
+                      uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
+                      uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,

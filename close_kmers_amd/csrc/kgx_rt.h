@@ -261,6 +261,10 @@ bool probe_takes_dna(const kgx_ctx *c);
 hipError_t launch_fq_plan(const uint64_t *off, uint32_t n, uint64_t *wbase, uint32_t *tile_seq, uint32_t tile_windows,
                           uint32_t *status, uint32_t *block_max, hipStream_t stream);
 
+struct SvcState;
+/* stops and frees the image's call service (kgx_svc.cpp), if any */
+void svc_shutdown(kgx_image *img);
+
 }  // namespace kgx
 
 struct kgx_image {
@@ -278,6 +282,10 @@ struct kgx_image {
     std::mutex probe_mu;
     hipEvent_t last_probe = nullptr; /* end of the latest probe enqueued */
     hipStream_t probe_stream = nullptr; /* contexts' chained probes with option probe_stream */
+    /* the resident call service (kgx_svc.cpp), created on the first kgx_svc_call */
+    std::mutex svc_mu;
+    kgx::SvcState *svc = nullptr;
+    uint32_t svc_slots = 32, svc_idle_us = 1000, svc_life_us = 4000;
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;

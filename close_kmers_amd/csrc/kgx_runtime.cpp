@@ -83,6 +83,7 @@ const char *kgx_strerror(int code)
     case KGX_EDEVICE: return "device error";
     case KGX_ERANGE: return "out of supported range";
     case KGX_EFULL: return "hash table half full";
+    case KGX_EBUSY: return "call service busy or not applicable";
     default: return "unknown error";
     }
 }
@@ -666,6 +667,7 @@ int kgx_image_close(kgx_image *img)
 {
     if (!img)
         return KGX_OK;
+    svc_shutdown(img);
     (void)hipSetDevice(img->device);
     if (img->d_table)
         (void)hipFree(img->d_table);
@@ -690,6 +692,7 @@ int kgx_image_set_filter(kgx_image *img, int log2_bits)
 {
     if (!img || log2_bits < 0 || (log2_bits && (log2_bits < 12 || log2_bits > 40)))
         return fail(KGX_EINVAL, "filter size: 0 (none) or 2^12 .. 2^40 bits");
+    svc_shutdown(img); /* the device-wide synchronisation below would wait out its instances */
     HIP_TRY(hipSetDevice(img->device));
     HIP_TRY(hipDeviceSynchronize());
     if (img->d_filter)
@@ -716,6 +719,7 @@ int kgx_image_set_layout(kgx_image *img, int layout)
 {
     if (!img)
         return fail(KGX_EINVAL, "null image");
+    svc_shutdown(img); /* its workgroups hold the resident table's address */
     if (layout == KGX_LAYOUT_PACKED16)
         return image_pack(img);
     if (layout == KGX_LAYOUT_AOS24)

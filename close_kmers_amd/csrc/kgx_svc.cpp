@@ -1,0 +1,412 @@
+/*
+ * kgx_svc.cpp -- the resident call service: KmerGuts::process_aa_seq for one
+ * sequence without a kernel launch per call.
+ *
+ * The reference's worker pool calls process_aa_seq once per sequence from T
+ * threads, one KmerGuts each (threadpool.cc:18-44, lookup_request.cc:153-172,
+ * kguts.cc:888-908).  A launch per call costs ~6 us of host time inside the
+ * runtime and those launches serialise across the pool's threads, so the pool
+ * topped out at 170K calls/s whatever T (r3g).  Here workgroups of svc_kernel
+ * (kgx_fused.hip) stay resident, one per slot; a caller takes a free slot,
+ * writes its residues, length, want mask and parameters into the slot's
+ * mapped host memory, stores the slot's request number, and spins until the
+ * device stores the same number into the slot's done word, behind the hit
+ * and call records (fused_small_body: probe, ordered compaction, wave
+ * scorer).  No runtime call is on a call's path.
+ *
+ * Instances: the kernel leaves after idle_us without a request, or life_us
+ * after its start (a bound on how long it holds its hardware queue, which
+ * other streams may share), or on stop.  The host keeps two instances
+ * enqueued on the service's stream, so when one leaves the next is already
+ * dispatched; callers top the queue up (hipEventQuery on the oldest, at most
+ * every 200 us) and, should a request wait more than 100 us, at once.  A
+ * request written while an instance was leaving stays pending in its slot and
+ * the next instance serves it (a workgroup starts from the slot's done word).
+ * kgx_image_close / set_layout / set_filter stop the service first, and an
+ * atexit hook stops every live one, so no instance outlives the process.
+ */
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <set>
+#include <string>
+
+#include "kgx_rt.h"
+
+namespace kgx {
+
+struct SvcState {
+    int device = 0;
+    uint32_t slots = 32;
+    uint64_t idle_us = 1000, life_us = 4000;
+    hipStream_t stream = nullptr;
+    char *host = nullptr; /* one mapped, coherent block: hdr | out | res | hits | calls */
+    SvcSlotHdr *hdr = nullptr;
+    SvcSlotOut *out = nullptr;
+    uint8_t *res = nullptr;
+    kgx_hit *hits = nullptr;
+    kgx_call *calls = nullptr;
+    /* their device addresses */
+    SvcSlotHdr *d_hdr = nullptr;
+    SvcSlotOut *d_out = nullptr;
+    uint8_t *d_res = nullptr;
+    kgx_hit *d_hits = nullptr;
+    kgx_call *d_calls = nullptr;
+    uint64_t *d_activity = nullptr;
+    const void *table = nullptr;
+    uint64_t num_sigs = 0;
+    std::atomic<uint64_t> free_mask{0};
+    uint32_t seq[SVC_MAX_SLOTS] = {}; /* a slot's last request number (its holder's) */
+    std::mutex mu;                    /* instances */
+    std::deque<hipEvent_t> running;   /* end of each enqueued instance */
+    std::vector<hipEvent_t> spare;
+    std::atomic<int64_t> next_check{0};
+    std::atomic<uint64_t> n_calls{0}, n_launches{0}, n_busy{0};
+    bool broken = false; /* a launch failed: callers take other paths */
+};
+
+namespace {
+
+std::mutex g_live_mu;
+std::set<SvcState *> g_live;
+bool g_atexit = false;
+
+int64_t now_ns()
+{
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+constexpr size_t align64(size_t x) { return (x + 63) & ~size_t(63); }
+
+/* keep two instances enqueued (mu held) */
+int top_up(SvcState *s)
+{
+    while (!s->running.empty()) {
+        const hipError_t q = hipEventQuery(s->running.front());
+        if (q == hipErrorNotReady)
+            break;
+        if (q != hipSuccess) {
+            s->broken = true;
+            return fail(KGX_EDEVICE, std::string("call service: ") + hipGetErrorString(q));
+        }
+        s->spare.push_back(s->running.front());
+        s->running.pop_front();
+    }
+    while (s->running.size() < 2) {
+        hipEvent_t ev = nullptr;
+        if (!s->spare.empty()) {
+            ev = s->spare.back();
+            s->spare.pop_back();
+        } else {
+            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        }
+        /* wall clock at 100 MHz: 100 ticks per us */
+        hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_res, s->d_hits, s->d_calls, s->slots, s->table,
+                                  s->num_sigs, s->d_activity, s->idle_us * 100, s->life_us * 100, s->stream);
+        if (e == hipSuccess)
+            e = hipEventRecord(ev, s->stream);
+        if (e != hipSuccess) {
+            s->spare.push_back(ev);
+            s->broken = true;
+            return fail(KGX_EDEVICE, std::string("call service launch: ") + hipGetErrorString(e));
+        }
+        s->running.push_back(ev);
+        s->n_launches++;
+    }
+    return KGX_OK;
+}
+
+/* every workgroup of every enqueued instance leaves; the slots stay */
+void drain(SvcState *s)
+{
+    std::lock_guard<std::mutex> lk(s->mu);
+    for (uint32_t i = 0; i < s->slots; i++)
+        __atomic_store_n(&s->hdr[i].stop, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(s->stream);
+    for (hipEvent_t e : s->running)
+        s->spare.push_back(e);
+    s->running.clear();
+    for (uint32_t i = 0; i < s->slots; i++)
+        __atomic_store_n(&s->hdr[i].stop, 0u, __ATOMIC_RELEASE);
+}
+
+void destroy(SvcState *s)
+{
+    if (!s)
+        return;
+    {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        g_live.erase(s);
+    }
+    (void)hipSetDevice(s->device);
+    if (s->stream)
+        drain(s);
+    for (hipEvent_t e : s->spare)
+        (void)hipEventDestroy(e);
+    if (s->stream)
+        (void)hipStreamDestroy(s->stream);
+    if (s->d_activity)
+        (void)hipFree(s->d_activity);
+    if (s->host)
+        (void)hipHostFree(s->host);
+    delete s;
+}
+
+void stop_all_at_exit()
+{
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    for (SvcState *s : g_live) {
+        (void)hipSetDevice(s->device);
+        drain(s);
+    }
+}
+
+int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, SvcState **out)
+{
+    if (img->layout != KGX_LAYOUT_PACKED16 || !img->d_packed)
+        return fail(KGX_EBUSY, "call service: PACKED16 images only");
+    HIP_TRY(hipSetDevice(img->device));
+    SvcState *s = new SvcState;
+    s->device = img->device;
+    s->slots = slots;
+    s->idle_us = idle_us;
+    s->life_us = life_us;
+    s->table = img->d_packed;
+    s->num_sigs = img->num_sigs;
+    const size_t b_hdr = align64(slots * sizeof(SvcSlotHdr)), b_out = align64(slots * sizeof(SvcSlotOut)),
+                 b_res = align64((size_t)slots * SVC_RES_STRIDE),
+                 b_hits = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_hit)),
+                 b_calls = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_call));
+    const size_t total = b_hdr + b_out + b_res + b_hits + b_calls;
+    void *h = nullptr, *d = nullptr;
+    hipError_t e = hipHostMalloc(&h, total, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess)
+        e = hipHostGetDevicePointer(&d, h, 0);
+    if (e == hipSuccess)
+        e = hipMalloc(reinterpret_cast<void **>(&s->d_activity), sizeof(uint64_t));
+    if (e == hipSuccess)
+        e = hipMemset(s->d_activity, 0, sizeof(uint64_t));
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    s->host = static_cast<char *>(h);
+    if (e != hipSuccess) {
+        destroy(s);
+        return fail(KGX_EDEVICE, std::string("call service: ") + hipGetErrorString(e));
+    }
+    std::memset(h, 0, b_hdr + b_out);
+    char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);
+    s->hdr = reinterpret_cast<SvcSlotHdr *>(hp);
+    s->d_hdr = reinterpret_cast<SvcSlotHdr *>(dp);
+    s->out = reinterpret_cast<SvcSlotOut *>(hp + b_hdr);
+    s->d_out = reinterpret_cast<SvcSlotOut *>(dp + b_hdr);
+    s->res = reinterpret_cast<uint8_t *>(hp + b_hdr + b_out);
+    s->d_res = reinterpret_cast<uint8_t *>(dp + b_hdr + b_out);
+    s->hits = reinterpret_cast<kgx_hit *>(hp + b_hdr + b_out + b_res);
+    s->d_hits = reinterpret_cast<kgx_hit *>(dp + b_hdr + b_out + b_res);
+    s->calls = reinterpret_cast<kgx_call *>(hp + b_hdr + b_out + b_res + b_hits);
+    s->d_calls = reinterpret_cast<kgx_call *>(dp + b_hdr + b_out + b_res + b_hits);
+    s->free_mask.store(slots >= 64 ? ~0ull : ((1ull << slots) - 1), std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        g_live.insert(s);
+        if (!g_atexit) {
+            std::atexit(stop_all_at_exit);
+            g_atexit = true;
+        }
+    }
+    *out = s;
+    return KGX_OK;
+}
+
+/* the image's service, created on first use with its configuration */
+int get(kgx_image *img, SvcState **out)
+{
+    std::lock_guard<std::mutex> lk(img->svc_mu);
+    if (!img->svc) {
+        int rc = create(img, img->svc_slots, img->svc_idle_us, img->svc_life_us, &img->svc);
+        if (rc)
+            return rc;
+    }
+    *out = img->svc;
+    return KGX_OK;
+}
+
+bool take_slot(SvcState *s, uint32_t &slot)
+{
+    uint64_t m = s->free_mask.load(std::memory_order_relaxed);
+    while (m) {
+        const uint32_t i = (uint32_t)__builtin_ctzll(m);
+        if (s->free_mask.compare_exchange_weak(m, m & ~(1ull << i), std::memory_order_acquire,
+                                               std::memory_order_relaxed)) {
+            slot = i;
+            return true;
+        }
+    }
+    return false;
+}
+
+void give_slot(SvcState *s, uint32_t slot) { s->free_mask.fetch_or(1ull << slot, std::memory_order_release); }
+
+}  // namespace
+
+void svc_shutdown(kgx_image *img)
+{
+    std::lock_guard<std::mutex> lk(img->svc_mu);
+    destroy(img->svc);
+    img->svc = nullptr;
+}
+
+}  // namespace kgx
+
+using namespace kgx;
+
+extern "C" {
+
+int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t life_us)
+{
+    if (!img)
+        return fail(KGX_EINVAL, "null image");
+    if (slots < 1 || slots > SVC_MAX_SLOTS || idle_us < 10 || life_us < idle_us)
+        return fail(KGX_EINVAL, "call service: 1..64 slots, idle_us >= 10, life_us >= idle_us");
+    svc_shutdown(img);
+    std::lock_guard<std::mutex> lk(img->svc_mu);
+    img->svc_slots = slots;
+    img->svc_idle_us = idle_us;
+    img->svc_life_us = life_us;
+    return KGX_OK;
+}
+
+int kgx_svc_stop(kgx_image *img)
+{
+    if (!img)
+        return fail(KGX_EINVAL, "null image");
+    svc_shutdown(img);
+    return KGX_OK;
+}
+
+int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
+{
+    if (!img || !name || !value)
+        return fail(KGX_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(img->svc_mu);
+    const SvcState *s = img->svc;
+    const std::string n(name);
+    if (n == "slots")
+        *value = img->svc_slots;
+    else if (n == "calls")
+        *value = s ? s->n_calls.load() : 0;
+    else if (n == "launches")
+        *value = s ? s->n_launches.load() : 0;
+    else if (n == "busy")
+        *value = s ? s->n_busy.load() : 0;
+    else
+        return fail(KGX_EINVAL, "unknown service statistic " + n);
+    return KGX_OK;
+}
+
+int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
+                 kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
+                 uint64_t *n_calls)
+{
+    if (!img || (len && !seq) || !n_hits || !n_calls)
+        return fail(KGX_EINVAL, "null argument");
+    kgx_params p;
+    if (params)
+        p = *params;
+    else
+        kgx_params_default(&p);
+    /* what fused_small_body serves (the rest takes the batch paths) */
+    if (len > SVC_MAX_RES || want == 0 || (want & ~(KGX_WANT_HITS | KGX_WANT_CALLS)) || p.order_constraint != 0 ||
+        p.min_hits < 1)
+        return fail(KGX_EBUSY, "call service: not a call it serves (length, want mask or parameters)");
+    const uint64_t W = windows_of(len);
+    if (((want & KGX_WANT_HITS) && hits_cap < W) || ((want & KGX_WANT_CALLS) && calls_cap < W))
+        return fail(KGX_EINVAL, "call service: result capacity below the sequence's window count");
+    if ((want & KGX_WANT_HITS && W && !hits) || (want & KGX_WANT_CALLS && W && !calls))
+        return fail(KGX_EINVAL, "null result buffer");
+    SvcState *s = nullptr;
+    int rc = get(img, &s);
+    if (rc)
+        return rc;
+    if (s->broken)
+        return fail(KGX_EBUSY, "call service: unavailable after a launch failure");
+    uint32_t slot = 0;
+    if (!take_slot(s, slot)) {
+        s->n_busy++;
+        return fail(KGX_EBUSY, "call service: every slot is in use");
+    }
+    /* the request: residues (cut at the first NUL as the batch paths do,
+     * kguts.cc:792), then the header, then the request number */
+    uint8_t *r = s->res + (size_t)slot * SVC_RES_STRIDE;
+    if (len)
+        std::memcpy(r, seq, len);
+    if (const void *z = len ? std::memchr(r, 0, len) : nullptr) {
+        const uint64_t z0 = (uint64_t)(static_cast<const uint8_t *>(z) - r);
+        std::memset(r + (z0 ? z0 - 1 : 0), 'X', len - (z0 ? z0 - 1 : 0));
+    }
+    SvcSlotHdr &h = s->hdr[slot];
+    h.len = (uint32_t)len;
+    h.want = want;
+    h.prm = p;
+    uint32_t q = s->seq[slot] + 1;
+    if (q == 0 || q == __atomic_load_n(&s->out[slot].done, __ATOMIC_RELAXED))
+        q++;
+    s->seq[slot] = q;
+    __atomic_store_n(&h.req, q, __ATOMIC_RELEASE);
+    /* keep instances enqueued (cheap: one clock read unless 200 us passed) */
+    const int64_t t0 = now_ns();
+    if (t0 >= s->next_check.load(std::memory_order_relaxed)) {
+        std::unique_lock<std::mutex> lk(s->mu, std::try_to_lock);
+        if (lk.owns_lock()) {
+            s->next_check.store(t0 + 200000, std::memory_order_relaxed);
+            if ((rc = top_up(s))) {
+                give_slot(s, slot); /* nothing will serve it; the holder's next request overwrites it */
+                return rc;
+            }
+        }
+    }
+    const volatile uint32_t *done = &s->out[slot].done;
+    bool nudged = false;
+    for (uint32_t spin = 1; *done != q; spin++) {
+        if ((spin & 1023u) == 0) {
+            const int64_t dt = now_ns() - t0;
+            if (!nudged && dt > 100000) { /* 100 us: no instance is serving the slots */
+                std::lock_guard<std::mutex> lk(s->mu);
+                if ((rc = top_up(s))) {
+                    give_slot(s, slot);
+                    return rc;
+                }
+                nudged = true;
+            }
+            if (dt > 10000000000ll) /* 10 s: the slot is abandoned (never handed out again) */
+                return fail(KGX_EDEVICE, "call service: no answer within 10 s");
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const SvcSlotOut &o = s->out[slot];
+    const uint32_t nh = o.nh, nc = o.nc;
+    if (nh > W || nc > W) {
+        give_slot(s, slot);
+        return fail(KGX_EDEVICE, "call service: more records than windows");
+    }
+    *n_hits = (want & KGX_WANT_HITS) ? nh : 0;
+    *n_calls = (want & KGX_WANT_CALLS) ? nc : 0;
+    if (*n_hits)
+        std::memcpy(hits, s->hits + (size_t)slot * FUSED_MAX_WINDOWS, *n_hits * sizeof(kgx_hit));
+    if (*n_calls)
+        std::memcpy(calls, s->calls + (size_t)slot * FUSED_MAX_WINDOWS, *n_calls * sizeof(kgx_call));
+    give_slot(s, slot);
+    s->n_calls++;
+    return KGX_OK;
+}
+
+}  // extern "C"

@@ -38,6 +38,7 @@ extern "C" {
 #define KGX_EDEVICE (-5)  /* HIP runtime error or no gfx950 device */
 #define KGX_ERANGE (-6)   /* image or batch larger than supported */
 #define KGX_EFULL (-7)    /* image builder: table would reach half full */
+#define KGX_EBUSY (-8)    /* call service: no free slot, or not a call it serves (use a batch path) */
 
 /* ---- what kgx_process_* computes --------------------------------------- */
 #define KGX_WANT_HITS 1u  /* hit list (what hit_cb receives, kguts.cc:814-815) */
@@ -414,6 +415,33 @@ int kgx_process_batch_compact(kgx_ctx *ctx, const kgx_params *params, const char
  * only): ranges may be expanded on several threads at once. */
 int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const uint64_t *seq_offsets,
                        uint32_t s_begin, uint32_t s_end, uint32_t seq_base, kgx_hit *out);
+
+/* Resident call service: KmerGuts::process_aa_seq for ONE sequence
+ * (kguts.cc:888-908) without a kernel launch per call -- for worker pools
+ * that call per sequence (threadpool.cc:18-44, lookup_request.cc:153-172).
+ * Persistent workgroups on the image's device, one per slot, poll slots in
+ * mapped host memory; the call writes its sequence into a free slot and spins
+ * until the device has stored its records.  Thread-safe; started on the first
+ * call, and its workgroups leave after idle_us without requests (restarted on
+ * demand).  Serves PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS,
+ * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues;
+ * anything else, or every slot busy, returns KGX_EBUSY and the caller takes a
+ * batch path (kgx_process_batch*).  Results as kgx_process_batch gives them
+ * for a batch of this one sequence (kgx_hit.seq = 0, hits in position order);
+ * hits_cap / calls_cap must be at least the sequence's window count
+ * (len - 8). */
+int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
+                 kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
+                 uint64_t *n_calls);
+/* slots (1..64, default 32), idle_us (default 1000) and life_us (default
+ * 4000: an instance's longest stay before the next one, already enqueued,
+ * takes over); stops a running service */
+int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t life_us);
+/* stops the service (its workgroups leave; kgx_image_close does this too) */
+int kgx_svc_stop(kgx_image *img);
+/* "slots", "calls" (served), "launches" (instances enqueued), "busy" (calls
+ * turned away for want of a slot) */
+int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option
  * "host_profile" 1 (HIP events per chunk; otherwise zeros).  Device stages are

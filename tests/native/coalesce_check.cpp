@@ -44,6 +44,7 @@ int main(int argc, char **argv)
     const int T = std::atoi(argv[3]);
     const bool coalesce = argc > 5 ? std::atoi(argv[5]) != 0 : true;
     const bool with_otu = argc > 6 ? std::atoi(argv[6]) != 0 : true;
+    const int svc_slots = argc > 7 ? std::atoi(argv[7]) : 0; /* call service slots (0: its default) */
     std::ifstream in(argv[2], std::ios::binary);
     uint64_t n = 0;
     in.read(reinterpret_cast<char *>(&n), 8);
@@ -60,6 +61,8 @@ int main(int argc, char **argv)
         seqs[i] = res.substr(off[i], off[i + 1] - off[i]);
     try {
         auto image = std::make_shared<kgx::KmerImage>(dir, 0);
+        if (svc_slots && kgx_svc_config(image->handle(), (uint32_t)svc_slots, 1000, 4000) != KGX_OK)
+            throw std::runtime_error("kgx_svc_config");
         std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
         for (int t = 0; t < T; t++) {
             kgs.emplace_back(new kgx::KmerGuts(dir, image));
@@ -131,8 +134,10 @@ int main(int argc, char **argv)
         }
         std::fclose(f);
         const auto &co = image->coalescer();
-        std::printf("{\"passes\": %llu, \"calls\": %llu}\n", (unsigned long long)co.passes,
-                    (unsigned long long)co.calls);
+        uint64_t svc_calls = 0;
+        (void)kgx_svc_stat(image->handle(), "calls", &svc_calls);
+        std::printf("{\"passes\": %llu, \"calls\": %llu, \"svc_calls\": %llu}\n", (unsigned long long)co.passes,
+                    (unsigned long long)co.calls, (unsigned long long)svc_calls);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "coalesce_check: %s\n", e.what());
         return 1;

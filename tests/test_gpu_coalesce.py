@@ -64,11 +64,16 @@ def _parse(path, n):
     return out
 
 
-@pytest.mark.parametrize("threads,coalesce,otu", [(16, 1, 1), (5, 1, 1), (1, 1, 1), (16, 0, 1), (16, 1, 0),
-                                                  (1, 0, 0)])
-def test_threads_calling_process_aa_seq_match_oracle(gpu, oracle_lib, tmp_path, threads, coalesce, otu):
-    """otu 0: hit callbacks + calls only (the lookup handler's outputs), which
-    take the one-launch path (kgx_fused.hip) for the default parameters."""
+@pytest.mark.parametrize("threads,coalesce,otu,svc,slots", [(16, 1, 1, 1, 0), (5, 1, 1, 1, 0), (1, 1, 1, 1, 0),
+                                                            (16, 0, 1, 1, 0), (16, 1, 0, 1, 0), (16, 1, 0, 0, 0),
+                                                            (32, 1, 0, 1, 0), (16, 1, 0, 1, 3), (1, 0, 0, 1, 0)])
+def test_threads_calling_process_aa_seq_match_oracle(gpu, oracle_lib, tmp_path, threads, coalesce, otu, svc, slots):
+    """otu 0: hit callbacks + calls only (the lookup handler's outputs): with
+    the resident call service (svc 1, csrc/kgx_svc.cpp) calls under
+    order_constraint 0 of at most 2,056 residues run there, the rest through
+    the coalescer; svc 0 (KGX_SVC=0): the coalescer's one-launch path
+    (kgx_fused.hip).  slots 3: most calls find every slot taken (KGX_EBUSY)
+    and take the coalescer."""
     spec, table = synthetic_table(30000)
     d = image_files.write_data_dir(str(tmp_path), table, [f"function {i}" for i in range(100000)])
     n = 3000
@@ -76,12 +81,19 @@ def test_threads_calling_process_aa_seq_match_oracle(gpu, oracle_lib, tmp_path, 
     q = tmp_path / "queries.bin"
     q.write_bytes(np.uint64(n).tobytes() + off.tobytes() + res.tobytes())
     outp = tmp_path / "out.bin"
-    r = subprocess.run([kbuild.COALESCE_CHECK, d, str(q), str(threads), str(outp), str(coalesce), str(otu)],
-                       capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, KGX_SVC=str(svc))
+    r = subprocess.run([kbuild.COALESCE_CHECK, d, str(q), str(threads), str(outp), str(coalesce), str(otu),
+                        str(slots)],
+                       capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     stats = json.loads(r.stdout)
-    assert stats["calls"] == (n if coalesce else 0)
-    if coalesce and threads >= 5:
+    assert stats["calls"] + stats["svc_calls"] == (n if coalesce else 0)
+    if coalesce and svc and not otu:
+        # thread parameter sets 0 and 1, ordinary lengths (3 slots: some)
+        assert stats["svc_calls"] > (n // 2 if not slots else 0)
+    else:
+        assert stats["svc_calls"] == 0
+    if coalesce and threads >= 5 and not (svc and not otu and not slots):
         assert stats["passes"] < n  # calls did share passes
     got = _parse(outp, n)
     # every sequence against the oracle under its thread's parameter set

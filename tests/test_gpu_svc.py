@@ -1,0 +1,139 @@
+"""The resident call service (csrc/kgx_svc.cpp, svc_kernel in kgx_fused.hip):
+process_aa_seq for one sequence (kguts.cc:888-908) without a launch per call,
+served by persistent workgroups from mapped slots.  Every call is compared
+with the oracle on the same sequence and parameters (hits in position order,
+calls, bit-exact), from one thread and from many at once (the reference's
+pool shape, threadpool.cc:18-44), across instance restarts (idle exits) and
+the calls the service turns away (KGX_EBUSY)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from close_kmers_amd import abi, synth
+from helpers import random_protein, synthetic_table
+
+pytestmark = pytest.mark.gpu
+
+PARAMS = [None, {"min_hits": "3", "max_gap": "50"}, {"min_hits": "1", "max_gap": "0"},
+          {"min_weighted_hits": "2"}]
+
+
+@pytest.fixture(scope="module")
+def svc_image(gpu):
+    spec, table = synthetic_table(30000)
+    with abi.Image.from_table(table, device=0) as img:
+        assert img.layout == abi.Image.PACKED16
+        yield spec, table, img
+
+
+def _seqs(spec, n, seed):
+    """C2-like proteins, planted and random, plus ragged ones: empty, < 9
+    aa, X / * / lower case, NUL inside, up to the 2,056-residue limit."""
+    rng = np.random.default_rng(seed)
+    res, off = synth.make_queries(spec, n, x_permille=3, q0=seed)
+    seqs = [bytes(res[int(off[i]):int(off[i + 1])]) for i in range(n)]
+    for i in rng.choice(n, n // 10, replace=False):
+        seqs[i] = seqs[i][:int(rng.integers(0, 12))]
+    for i in rng.choice(n, n // 20, replace=False):
+        s = bytearray(seqs[i])
+        if s:
+            s[int(rng.integers(0, len(s)))] = int(rng.choice([ord(c) for c in "X*bz"] + [0]))
+        seqs[i] = bytes(s)
+    for i, L in zip(rng.choice(n, 4, replace=False), (513, 520, 1500, 2056)):
+        seqs[i] = (seqs[i] * 8 + random_protein(rng, L).encode())[:L]
+    return seqs
+
+
+def _check(oracle_lib, table, seq, params, hits, calls, tag):
+    want = oracle_lib.process_batch(table, np.frombuffer(seq, np.uint8).copy(),
+                                    np.array([0, len(seq)], np.uint64), params=params, want=3)
+    wh = want.hits
+    assert len(hits) == len(wh), tag
+    for f in ("which_kmer", "otu_index", "avg_from_end", "function_index", "pos"):
+        assert np.array_equal(hits[f], wh[f]), (tag, f)
+    assert np.array_equal(hits["function_wt"].view(np.uint32), wh["function_wt"].view(np.uint32)), tag
+    wc = want.calls
+    assert len(calls) == len(wc), tag
+    for f in ("start", "end", "count", "function_index"):
+        assert np.array_equal(calls[f], wc[f]), (tag, f)
+    assert np.array_equal(calls["weighted_hits"].view(np.uint32), wc["weighted_hits"].view(np.uint32)), tag
+
+
+def _tuple(p):
+    q = abi.parse_params(p)
+    return (q.min_hits, q.max_gap, q.order_constraint, q.min_weighted_hits)
+
+
+def test_svc_single_thread_matches_oracle(svc_image, oracle_lib):
+    spec, table, img = svc_image
+    seqs = _seqs(spec, 400, 7)
+    for k, s in enumerate(seqs):
+        p = PARAMS[k % len(PARAMS)]
+        hits, calls = img.svc_call(s, p)
+        _check(oracle_lib, table, s, _tuple(p), hits, calls, k)
+    assert img.svc_stat("calls") >= len(seqs)
+
+
+def test_svc_want_masks(svc_image, oracle_lib):
+    spec, table, img = svc_image
+    s = _seqs(spec, 3, 11)[0]
+    h, c = img.svc_call(s, None, abi.WANT_HITS)
+    assert len(c) == 0 and len(h) > 0
+    h2, c2 = img.svc_call(s, None, abi.WANT_CALLS)
+    assert len(h2) == 0
+    h3, c3 = img.svc_call(s, None, abi.WANT_HITS | abi.WANT_CALLS)
+    assert np.array_equal(h, h3) and np.array_equal(c2, c3)
+
+
+def test_svc_turns_away_what_it_does_not_serve(svc_image):
+    spec, table, img = svc_image
+    for seq, p, want in ((b"A" * 2057, None, 3), (b"ACDEFGHIKLMN", {"order_constraint": "1"}, 3),
+                         (b"ACDEFGHIKLMN", {"min_hits": "0"}, 3), (b"ACDEFGHIKLMN", None, abi.WANT_OTU),
+                         (b"ACDEFGHIKLMN", None, 0)):
+        with pytest.raises(abi.KgxError) as e:
+            img.svc_call(seq, p, want)
+        assert e.value.code == abi.KGX_EBUSY
+
+
+def test_svc_threads_and_restarts_match_oracle(svc_image, oracle_lib):
+    """16 threads at once over 32 slots, then 40 threads over 8 slots (calls
+    turned away for want of a slot are counted and retried), with idle
+    exits between rounds (the next call relaunches the service)."""
+    spec, table, img = svc_image
+    seqs = _seqs(spec, 1600, 23)
+    for threads, slots in ((16, 32), (40, 8)):
+        img.svc_config(slots, 200, 2000)
+        out = [None] * len(seqs)
+        errs = []
+
+        def work(t):
+            try:
+                for i in range(t, len(seqs), threads):
+                    while True:
+                        try:
+                            out[i] = img.svc_call(seqs[i], PARAMS[i % 2])
+                            break
+                        except abi.KgxError as e:
+                            if e.code != abi.KGX_EBUSY:
+                                raise
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        ws = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        for w in ws:
+            w.start()
+        for w in ws:
+            w.join()
+        assert not errs, errs[:3]
+        for i, s in enumerate(seqs):
+            _check(oracle_lib, table, s, _tuple(PARAMS[i % 2]), out[i][0], out[i][1], i)
+        assert img.svc_stat("slots") == slots
+        time.sleep(0.01)  # > idle_us: every instance leaves
+        h, c = img.svc_call(seqs[0], PARAMS[0])  # relaunched on demand
+        _check(oracle_lib, table, seqs[0], _tuple(PARAMS[0]), h, c, "restart")
+    assert img.svc_stat("launches") >= 4
+    img.svc_stop()
+    h, c = img.svc_call(seqs[1], PARAMS[1])  # a stopped service starts again
+    _check(oracle_lib, table, seqs[1], _tuple(PARAMS[1]), h, c, "after stop")

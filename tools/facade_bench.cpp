@@ -174,18 +174,35 @@ int main(int argc, char **argv)
                 q++;
         }
     }
-    const char *modes = std::getenv("KGX_FACADE_MODES");
-    for (int co = 1; co >= (modes && std::strcmp(modes, "1") == 0 ? 1 : 0) && !only; co--)
+    /* modes: 2 = the resident call service (kgx_svc_call, the default),
+     * 1 = the coalescer (service off), 0 = one pass per call;
+     * KGX_FACADE_MODES="2" or "2,1": only these */
+    std::vector<int> modes = {2, 1, 0};
+    if (const char *e = std::getenv("KGX_FACADE_MODES")) {
+        modes.clear();
+        for (const char *q = e; *q; q++)
+            if (*q >= '0' && *q <= '2')
+                modes.push_back(*q - '0');
+    }
+    /* each pool run makes R passes over the m sequences (enough calls to
+     * time a pool of 16 threads at ~1M calls/s) */
+    const size_t R = std::getenv("KGX_FACADE_REPS") ? std::strtoull(std::getenv("KGX_FACADE_REPS"), nullptr, 10) : 10;
+    static const char *mode_name[3] = {"per_call_T", "coalesced_T", "service_T"};
+    for (int co : modes)
         for (int T : threads) {
+            if (only)
+                break;
             std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
             for (int t = 0; t < T; t++) {
                 kgs.emplace_back(new kgx::KmerGuts(dir, image));
                 kgs.back()->coalesce = co != 0;
+                kgs.back()->service = co == 2;
             }
             std::vector<uint64_t> th_hits(T, 0);
             std::vector<std::vector<double>> th_lat(T);
             auto work = [&](int t, bool count) {
-                for (size_t i = (size_t)t; i < m; i += (size_t)T) {
+                for (size_t k = (size_t)t; k < (count ? m * R : m); k += (size_t)T) {
+                    const size_t i = k % m;
                     auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
                     uint64_t h = 0;
                     const auto q0 = clk::now();
@@ -205,6 +222,8 @@ int main(int argc, char **argv)
                     w.join();
             }
             const uint64_t passes0 = image->coalescer().passes, calls0 = image->coalescer().calls;
+            uint64_t svc0 = 0, svc1 = 0;
+            (void)kgx_svc_stat(image->handle(), "calls", &svc0);
             const auto t0 = clk::now();
             std::vector<std::thread> ws;
             for (int t = 0; t < T; t++)
@@ -218,18 +237,20 @@ int main(int argc, char **argv)
                 ph += th_hits[t];
                 all.insert(all.end(), th_lat[t].begin(), th_lat[t].end());
             }
-            pool_ok = pool_ok && ph == hits;
+            pool_ok = pool_ok && ph == hits * R;
             const uint64_t np = image->coalescer().passes - passes0, nc = image->coalescer().calls - calls0;
+            (void)kgx_svc_stat(image->handle(), "calls", &svc1);
+            const double nm = (double)(m * R);
             char b[400];
             std::snprintf(b, sizeof b,
                           "%s\"%s%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g, \"p50_us\": %.1f, "
-                          "\"p99_us\": %.1f, \"calls_per_pass\": %.2f}",
-                          pool_json.empty() ? "" : ", ", co ? "coalesced_T" : "per_call_T", T, (double)m / tp,
-                          (double)residues / tp, pct(all, 50), pct(all, 99), np ? (double)nc / (double)np : 1.0);
+                          "\"p99_us\": %.1f, \"calls_per_pass\": %.2f, \"service_calls\": %llu}",
+                          pool_json.empty() ? "" : ", ", mode_name[co], T, nm / tp, (double)(residues * R) / tp,
+                          pct(all, 50), pct(all, 99), np ? (double)nc / (double)np : 1.0,
+                          (unsigned long long)(svc1 - svc0));
             pool_json += b;
-            std::fprintf(stderr, "[facade] %s T=%d: %.4g calls/s, %.4g residues/s, p50 %.1f us, p99 %.1f us\n",
-                         co ? "coalesced" : "per-call", T, (double)m / tp, (double)residues / tp, pct(all, 50),
-                         pct(all, 99));
+            std::fprintf(stderr, "[facade] %s%d: %.4g calls/s, %.4g residues/s, p50 %.1f us, p99 %.1f us\n",
+                         mode_name[co], T, nm / tp, (double)(residues * R) / tp, pct(all, 50), pct(all, 99));
         }
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
