@@ -104,7 +104,7 @@ template <uint32_t FJ, class IN>
 __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, const uint32_t s)
 {
     typedef FusedInput<IN> In;
-    const bool dbg = a.dbg && blockIdx.x == 0 && threadIdx.x == 0;
+    const bool dbg = a.dbg && s == 0 && threadIdx.x == 0;
     if (dbg)
         a.dbg[0] = wall_clock64();
     __shared__ uint8_t code_tab[256];
@@ -469,28 +469,37 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * how long the instance holds its hardware queue; the host keeps the next
  * instance queued behind it (kgx_svc.cpp).
  */
-__global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res_base,
-                                                  kgx_hit *hits, kgx_call *calls, const uint4 *table,
-                                                  uint64_t num_sigs, uint64_t magic, uint64_t *activity,
-                                                  uint64_t idle_ticks, uint64_t life_ticks)
+__global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbgs,
+                                                  const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
+                                                  const uint4 *table, uint64_t num_sigs, uint64_t magic,
+                                                  uint64_t *activity, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    __shared__ uint32_t cmd[8];
-    const uint32_t slot = blockIdx.x, t = threadIdx.x;
+    __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
+    const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
     const uint64_t t0 = wall_clock64();
     uint32_t last = 0;
     if (t == 0)
         last = __hip_atomic_load(&out[slot].done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t *word = reinterpret_cast<const uint64_t *>(&hdr[slot].req);
+    last = __shfl(last, 0);
+    const uint32_t *line = reinterpret_cast<const uint32_t *>(&hdr[slot]);
     for (;;) {
-        if (t == 0) {
+        if (t < 64) {
+            /* wave 0 polls: lanes 0-15 read the header line's 16 dwords at
+             * once (one PCIe round trip for the request number and its
+             * fields); a line whose copy word lags its request number was
+             * read mid-write and is read again */
             uint32_t go = 0;
             for (;;) {
-                const uint64_t w = __hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((uint32_t)(w >> 32)) /* stop */
+                const uint32_t v = lane < 16 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_SYSTEM)
+                                             : 0u;
+                const uint32_t req = rl32(v, 0), stop = rl32(v, 1), copy = rl32(v, 15);
+                if (stop)
                     break;
-                if ((uint32_t)w != last) {
+                if (req != last && copy == req) {
                     go = 1;
-                    cmd[1] = (uint32_t)w;
+                    if (lane < 16)
+                        cmd[lane] = v;
                     break;
                 }
                 const uint64_t now = wall_clock64();
@@ -499,62 +508,52 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                     break;
                 __builtin_amdgcn_s_sleep(8);
             }
-            if (go) {
-                __hip_atomic_fetch_max(activity, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const SvcSlotHdr &h = hdr[slot];
-                cmd[2] = __hip_atomic_load(&h.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                cmd[3] = __hip_atomic_load(&h.want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                cmd[4] = (uint32_t)__hip_atomic_load(&h.prm.min_hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                cmd[5] = (uint32_t)__hip_atomic_load(&h.prm.max_gap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                cmd[6] = (uint32_t)__hip_atomic_load(&h.prm.order_constraint, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_SYSTEM);
-                cmd[7] = (uint32_t)__hip_atomic_load(&h.prm.min_weighted_hits, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) {
+                cmd[16] = go;
+                if (go)
+                    __hip_atomic_fetch_max(activity, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            cmd[0] = go;
         }
         __syncthreads();
-        if (!cmd[0])
+        if (!cmd[16])
             break;
         /* the residues the host wrote before req: no stale line in this CU's caches */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const SvcSlotHdr *h = reinterpret_cast<const SvcSlotHdr *>(cmd);
         FusedArgs a;
-        const uint32_t len = min(cmd[2], SVC_MAX_RES);
+        const uint32_t req = h->req, len = min(h->len, SVC_MAX_RES);
         a.res = nullptr;
         a.off = nullptr;
         a.wbase = nullptr;
         a.n = 1;
-        a.want = cmd[3];
+        a.want = h->want;
         a.table = table;
         a.num_sigs = num_sigs;
         a.magic = magic;
-        a.prm.min_hits = (int32_t)cmd[4];
-        a.prm.max_gap = (int32_t)cmd[5];
-        a.prm.order_constraint = (int32_t)cmd[6];
-        a.prm.min_weighted_hits = (int32_t)cmd[7];
+        a.prm = h->prm;
         a.hits = hits + (uint64_t)slot * FUSED_MAX_WINDOWS;
         a.calls = calls + (uint64_t)slot * FUSED_MAX_WINDOWS;
         a.counts = &out[slot].nh;
         a.done = &out[slot].done;
-        a.token = cmd[1];
-        a.dbg = nullptr;
+        a.token = req;
+        a.dbg = h->debug ? dbgs[slot].stamp : nullptr;
         const FusedSlot in{res_base + (uint64_t)slot * SVC_RES_STRIDE, len};
+        __syncthreads(); /* every thread has its copy of the request before cmd can change */
         if (len <= 2 * 256 + 8)
             fused_small_body<2>(a, in, 0);
         else
             fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
-        last = cmd[1];
-        __syncthreads(); /* cmd is rewritten by the next poll */
+        last = req;
     }
 }
 
-hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res, kgx_hit *hits, kgx_call *calls,
-                      uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
-                      uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream)
+hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
+                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs,
+                      uint64_t *activity, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream)
 {
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, res, hits, calls,
+    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
                        static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), activity, idle_ticks,
                        life_ticks);
     return hipGetLastError();

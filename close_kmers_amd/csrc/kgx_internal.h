@@ -242,25 +242,31 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
 constexpr uint32_t SVC_MAX_RES = FUSED_MAX_WINDOWS + 8;
 constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residues per slot */
 constexpr uint32_t SVC_MAX_SLOTS = 64;
-struct SvcSlotHdr { /* host-written, one 64-B line per slot */
+struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the polling wave */
     uint32_t req;   /* request number: the device serves it when it differs from SvcSlotOut.done */
     uint32_t stop;  /* nonzero: the service's workgroups leave */
     uint32_t len;   /* residues */
     uint32_t want;  /* KGX_WANT_HITS | KGX_WANT_CALLS */
     kgx_params prm;
-    uint32_t pad[8];
+    uint32_t debug; /* nonzero: phase stamps into the slot's SvcSlotDbg */
+    uint32_t pad[6];
+    uint32_t copy; /* = req, written before it: a line read with copy != req is incomplete */
+};
+struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
+    uint64_t stamp[8];  /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc; /* hit / call records stored */
     uint32_t done;   /* = req once the records and counts are visible */
     uint32_t pad[13];
 };
-static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64, "service slot lines");
+static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 64,
+              "service slot lines");
 /* slots workgroups on stream; each leaves once no slot has had a request for
  * idle_ticks, or life_ticks after its start, or on stop (device wall clock,
  * 100 MHz); activity: a device word, the latest request pickup */
-hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, const uint8_t *res, kgx_hit *hits, kgx_call *calls,
-                      uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
+hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
+                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
                       uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */

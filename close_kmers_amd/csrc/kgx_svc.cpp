@@ -45,15 +45,22 @@ struct SvcState {
     uint32_t slots = 32;
     uint64_t idle_us = 1000, life_us = 4000;
     hipStream_t stream = nullptr;
-    char *host = nullptr; /* one mapped, coherent block: hdr | out | res | hits | calls */
+    char *host = nullptr; /* one mapped, coherent block: hdr | out | dbg | res | hits | calls */
+    /* large-BAR devices: the request side (hdr | res) in fine-grained device
+     * memory instead, which the host writes through the BAR (posted stores)
+     * and the polling wave reads from HBM, not across PCIe; the replies stay
+     * in host memory, where the host polls them */
+    char *reqmem = nullptr;
     SvcSlotHdr *hdr = nullptr;
     SvcSlotOut *out = nullptr;
+    SvcSlotDbg *dbg = nullptr;
     uint8_t *res = nullptr;
     kgx_hit *hits = nullptr;
     kgx_call *calls = nullptr;
     /* their device addresses */
     SvcSlotHdr *d_hdr = nullptr;
     SvcSlotOut *d_out = nullptr;
+    SvcSlotDbg *d_dbg = nullptr;
     uint8_t *d_res = nullptr;
     kgx_hit *d_hits = nullptr;
     kgx_call *d_calls = nullptr;
@@ -67,6 +74,12 @@ struct SvcState {
     std::vector<hipEvent_t> spare;
     std::atomic<int64_t> next_check{0};
     std::atomic<uint64_t> n_calls{0}, n_launches{0}, n_busy{0};
+    /* KGX_SVC_DEBUG=1: the device's phase stamps per call, summed (ns):
+     * [0] request stored -> done seen on the host (wall), [1..5] the device
+     * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
+     * + scorer, 4->5 system fence) */
+    bool debug = false;
+    std::atomic<uint64_t> phase_ns[6] = {};
     bool broken = false; /* a launch failed: callers take other paths */
 };
 
@@ -107,7 +120,7 @@ int top_up(SvcState *s)
             HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         }
         /* wall clock at 100 MHz: 100 ticks per us */
-        hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_res, s->d_hits, s->d_calls, s->slots, s->table,
+        hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->slots, s->table,
                                   s->num_sigs, s->d_activity, s->idle_us * 100, s->life_us * 100, s->stream);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
@@ -128,12 +141,14 @@ void drain(SvcState *s)
     std::lock_guard<std::mutex> lk(s->mu);
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 1u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
     (void)hipStreamSynchronize(s->stream);
     for (hipEvent_t e : s->running)
         s->spare.push_back(e);
     s->running.clear();
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 0u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
 }
 
 void destroy(SvcState *s)
@@ -153,6 +168,8 @@ void destroy(SvcState *s)
         (void)hipStreamDestroy(s->stream);
     if (s->d_activity)
         (void)hipFree(s->d_activity);
+    if (s->reqmem)
+        (void)hipFree(s->reqmem);
     if (s->host)
         (void)hipHostFree(s->host);
     delete s;
@@ -180,10 +197,10 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     s->table = img->d_packed;
     s->num_sigs = img->num_sigs;
     const size_t b_hdr = align64(slots * sizeof(SvcSlotHdr)), b_out = align64(slots * sizeof(SvcSlotOut)),
-                 b_res = align64((size_t)slots * SVC_RES_STRIDE),
+                 b_dbg = align64(slots * sizeof(SvcSlotDbg)), b_res = align64((size_t)slots * SVC_RES_STRIDE),
                  b_hits = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_hit)),
                  b_calls = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_call));
-    const size_t total = b_hdr + b_out + b_res + b_hits + b_calls;
+    const size_t total = b_hdr + b_out + b_dbg + b_res + b_hits + b_calls;
     void *h = nullptr, *d = nullptr;
     hipError_t e = hipHostMalloc(&h, total, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess)
@@ -199,18 +216,39 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
         destroy(s);
         return fail(KGX_EDEVICE, std::string("call service: ") + hipGetErrorString(e));
     }
-    std::memset(h, 0, b_hdr + b_out);
+    std::memset(h, 0, b_hdr + b_out + b_dbg);
+    const char *dbg_env = std::getenv("KGX_SVC_DEBUG");
+    s->debug = dbg_env && std::atoi(dbg_env) != 0;
     char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);
     s->hdr = reinterpret_cast<SvcSlotHdr *>(hp);
     s->d_hdr = reinterpret_cast<SvcSlotHdr *>(dp);
     s->out = reinterpret_cast<SvcSlotOut *>(hp + b_hdr);
     s->d_out = reinterpret_cast<SvcSlotOut *>(dp + b_hdr);
-    s->res = reinterpret_cast<uint8_t *>(hp + b_hdr + b_out);
-    s->d_res = reinterpret_cast<uint8_t *>(dp + b_hdr + b_out);
-    s->hits = reinterpret_cast<kgx_hit *>(hp + b_hdr + b_out + b_res);
-    s->d_hits = reinterpret_cast<kgx_hit *>(dp + b_hdr + b_out + b_res);
-    s->calls = reinterpret_cast<kgx_call *>(hp + b_hdr + b_out + b_res + b_hits);
-    s->d_calls = reinterpret_cast<kgx_call *>(dp + b_hdr + b_out + b_res + b_hits);
+    s->dbg = reinterpret_cast<SvcSlotDbg *>(hp + b_hdr + b_out);
+    s->d_dbg = reinterpret_cast<SvcSlotDbg *>(dp + b_hdr + b_out);
+    const size_t o_res = b_hdr + b_out + b_dbg;
+    s->res = reinterpret_cast<uint8_t *>(hp + o_res);
+    s->d_res = reinterpret_cast<uint8_t *>(dp + o_res);
+    int large_bar = 0;
+    const char *dm = std::getenv("KGX_SVC_DEVMEM");
+    if ((!dm || std::atoi(dm) != 0) &&
+        hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, img->device) == hipSuccess && large_bar) {
+        void *r = nullptr;
+        if (hipExtMallocWithFlags(&r, b_hdr + b_res, hipDeviceMallocFinegrained) == hipSuccess &&
+            hipMemset(r, 0, b_hdr) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+            s->reqmem = static_cast<char *>(r); /* one address for the host and the device */
+            s->hdr = s->d_hdr = reinterpret_cast<SvcSlotHdr *>(s->reqmem);
+            s->res = s->d_res = reinterpret_cast<uint8_t *>(s->reqmem + b_hdr);
+        } else {
+            (void)hipGetLastError();
+            if (r)
+                (void)hipFree(r);
+        }
+    }
+    s->hits = reinterpret_cast<kgx_hit *>(hp + o_res + b_res);
+    s->d_hits = reinterpret_cast<kgx_hit *>(dp + o_res + b_res);
+    s->calls = reinterpret_cast<kgx_call *>(hp + o_res + b_res + b_hits);
+    s->d_calls = reinterpret_cast<kgx_call *>(dp + o_res + b_res + b_hits);
     s->free_mask.store(slots >= 64 ? ~0ull : ((1ull << slots) - 1), std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> lk(g_live_mu);
@@ -305,6 +343,10 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? s->n_launches.load() : 0;
     else if (n == "busy")
         *value = s ? s->n_busy.load() : 0;
+    else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
+        *value = s && s->reqmem ? 1 : 0;
+    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '5') /* "phase_n0".."phase_n5" */
+        *value = s ? s->phase_ns[n[7] - '0'].load() : 0;
     else
         return fail(KGX_EINVAL, "unknown service statistic " + n);
     return KGX_OK;
@@ -343,22 +385,31 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     }
     /* the request: residues (cut at the first NUL as the batch paths do,
      * kguts.cc:792), then the header, then the request number */
-    uint8_t *r = s->res + (size_t)slot * SVC_RES_STRIDE;
-    if (len)
-        std::memcpy(r, seq, len);
-    if (const void *z = len ? std::memchr(r, 0, len) : nullptr) {
-        const uint64_t z0 = (uint64_t)(static_cast<const uint8_t *>(z) - r);
-        std::memset(r + (z0 ? z0 - 1 : 0), 'X', len - (z0 ? z0 - 1 : 0));
-    }
+    uint8_t *r = s->res + (size_t)slot * SVC_RES_STRIDE; /* written, never read, by the host */
+    const void *z = len ? std::memchr(seq, 0, len) : nullptr;
+    const uint64_t keep = z ? (uint64_t)(static_cast<const char *>(z) - seq) : len;
+    const uint64_t cut = z && keep ? keep - 1 : keep;
+    if (cut)
+        std::memcpy(r, seq, cut);
+    if (cut < len)
+        std::memset(r + cut, 'X', len - cut);
     SvcSlotHdr &h = s->hdr[slot];
     h.len = (uint32_t)len;
     h.want = want;
     h.prm = p;
+    h.debug = s->debug ? 1u : 0u;
     uint32_t q = s->seq[slot] + 1;
     if (q == 0 || q == __atomic_load_n(&s->out[slot].done, __ATOMIC_RELAXED))
         q++;
     s->seq[slot] = q;
+    /* device memory is written through a write-combining BAR mapping: the
+     * fences order the request's bytes before its number and push it out */
+    if (s->reqmem)
+        __builtin_ia32_sfence();
+    __atomic_store_n(&h.copy, q, __ATOMIC_RELEASE);
     __atomic_store_n(&h.req, q, __ATOMIC_RELEASE);
+    if (s->reqmem)
+        __builtin_ia32_sfence();
     /* keep instances enqueued (cheap: one clock read unless 200 us passed) */
     const int64_t t0 = now_ns();
     if (t0 >= s->next_check.load(std::memory_order_relaxed)) {
@@ -392,6 +443,12 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
 #endif
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    if (s->debug) {
+        const uint64_t *st = s->dbg[slot].stamp;
+        s->phase_ns[0] += (uint64_t)(now_ns() - t0);
+        for (int k = 1; k <= 5; k++)
+            s->phase_ns[k] += (st[k] - st[k - 1]) * 10; /* 100 MHz ticks */
+    }
     const SvcSlotOut &o = s->out[slot];
     const uint32_t nh = o.nh, nc = o.nc;
     if (nh > W || nc > W) {

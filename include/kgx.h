@@ -440,7 +440,10 @@ int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t li
 /* stops the service (its workgroups leave; kgx_image_close does this too) */
 int kgx_svc_stop(kgx_image *img);
 /* "slots", "calls" (served), "launches" (instances enqueued), "busy" (calls
- * turned away for want of a slot) */
+ * turned away for want of a slot), "devmem" (1: requests are written into
+ * fine-grained device memory through a large BAR, else mapped host memory;
+ * KGX_SVC_DEVMEM=0 forces the latter), "phase_n0".."phase_n5" (with
+ * KGX_SVC_DEBUG=1: summed ns of the host wall per call and the device phases) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option

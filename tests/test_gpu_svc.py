@@ -78,7 +78,10 @@ def test_svc_single_thread_matches_oracle(svc_image, oracle_lib):
 
 def test_svc_want_masks(svc_image, oracle_lib):
     spec, table, img = svc_image
-    s = _seqs(spec, 3, 11)[0]
+    def n_calls(x):
+        return len(oracle_lib.process_batch(table, np.frombuffer(x, np.uint8).copy(), np.array([0, len(x)], np.uint64),
+                                            want=3).calls)
+    s = next(x for x in _seqs(spec, 40, 11) if n_calls(x) > 0)
     h, c = img.svc_call(s, None, abi.WANT_HITS)
     assert len(c) == 0 and len(h) > 0
     h2, c2 = img.svc_call(s, None, abi.WANT_CALLS)
@@ -95,6 +98,21 @@ def test_svc_turns_away_what_it_does_not_serve(svc_image):
         with pytest.raises(abi.KgxError) as e:
             img.svc_call(seq, p, want)
         assert e.value.code == abi.KGX_EBUSY
+
+
+def test_svc_request_memory_host_and_device(svc_image, oracle_lib, monkeypatch):
+    """Requests through mapped host memory (KGX_SVC_DEVMEM=0) and, on
+    large-BAR devices, through fine-grained device memory: same results."""
+    spec, table, img = svc_image
+    seqs = _seqs(spec, 200, 31)
+    for dm in ("0", "1"):
+        monkeypatch.setenv("KGX_SVC_DEVMEM", dm)
+        img.svc_stop()  # the next call creates the service under this setting
+        for k, s in enumerate(seqs):
+            hits, calls = img.svc_call(s, PARAMS[k % 2])
+            _check(oracle_lib, table, s, _tuple(PARAMS[k % 2]), hits, calls, (dm, k))
+        if dm == "0":
+            assert img.svc_stat("devmem") == 0
 
 
 def test_svc_threads_and_restarts_match_oracle(svc_image, oracle_lib):

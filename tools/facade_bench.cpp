@@ -22,6 +22,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <atomic>
 #include <vector>
 
 #include "kguts_hip.h"
@@ -32,6 +33,14 @@ static double pct(std::vector<double> v, double p)
 {
     std::sort(v.begin(), v.end());
     return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(p / 100.0 * (double)v.size()))];
+}
+
+static double mean(const std::vector<double> &v)
+{
+    double t = 0;
+    for (double x : v)
+        t += x;
+    return v.empty() ? 0.0 : t / (double)v.size();
 }
 
 int main(int argc, char **argv)
@@ -200,8 +209,12 @@ int main(int argc, char **argv)
             }
             std::vector<uint64_t> th_hits(T, 0);
             std::vector<std::vector<double>> th_lat(T);
+            /* the pool's queue: each worker takes the next sequence (threadpool.cc:33-60); a
+             * fixed stride would hand even threads only the planted (hit-rich) proteins */
+            std::atomic<size_t> next{0};
             auto work = [&](int t, bool count) {
-                for (size_t k = (size_t)t; k < (count ? m * R : m); k += (size_t)T) {
+                const size_t total = count ? m * R : m;
+                for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < total;) {
                     const size_t i = k % m;
                     auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
                     uint64_t h = 0;
@@ -214,6 +227,7 @@ int main(int argc, char **argv)
                     }
                 }
             };
+            next = 0;
             { /* warm: buffer growth on every context */
                 std::vector<std::thread> ws;
                 for (int t = 0; t < T; t++)
@@ -222,8 +236,13 @@ int main(int argc, char **argv)
                     w.join();
             }
             const uint64_t passes0 = image->coalescer().passes, calls0 = image->coalescer().calls;
-            uint64_t svc0 = 0, svc1 = 0;
+            uint64_t svc0 = 0, svc1 = 0, ph0[6] = {}, ph1[6] = {};
             (void)kgx_svc_stat(image->handle(), "calls", &svc0);
+            for (int k = 0; k < 6; k++) {
+                const std::string nm = "phase_n" + std::to_string(k);
+                (void)kgx_svc_stat(image->handle(), nm.c_str(), &ph0[k]);
+            }
+            next = 0;
             const auto t0 = clk::now();
             std::vector<std::thread> ws;
             for (int t = 0; t < T; t++)
@@ -241,16 +260,32 @@ int main(int argc, char **argv)
             const uint64_t np = image->coalescer().passes - passes0, nc = image->coalescer().calls - calls0;
             (void)kgx_svc_stat(image->handle(), "calls", &svc1);
             const double nm = (double)(m * R);
+            /* KGX_SVC_DEBUG=1: mean per call of the host wall and the device phases (us) */
+            std::string phases;
+            for (int k = 0; k < 6; k++) {
+                const std::string nm2 = "phase_n" + std::to_string(k);
+                (void)kgx_svc_stat(image->handle(), nm2.c_str(), &ph1[k]);
+                if (svc1 > svc0 && ph1[0] > ph0[0]) {
+                    char q[40];
+                    std::snprintf(q, sizeof q, "%s%.2f", phases.empty() ? "" : ", ",
+                                  (double)(ph1[k] - ph0[k]) / 1e3 / (double)(svc1 - svc0));
+                    phases += q;
+                }
+            }
+            if (!phases.empty())
+                std::fprintf(stderr, "[facade] %s%d service phases (us: wall, residues, probe, compact, store+score, "
+                             "fence): %s\n", mode_name[co], T, phases.c_str());
             char b[400];
             std::snprintf(b, sizeof b,
                           "%s\"%s%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g, \"p50_us\": %.1f, "
-                          "\"p99_us\": %.1f, \"calls_per_pass\": %.2f, \"service_calls\": %llu}",
+                          "\"p99_us\": %.1f, \"mean_us\": %.2f, \"calls_per_pass\": %.2f, \"service_calls\": %llu}",
                           pool_json.empty() ? "" : ", ", mode_name[co], T, nm / tp, (double)(residues * R) / tp,
-                          pct(all, 50), pct(all, 99), np ? (double)nc / (double)np : 1.0,
+                          pct(all, 50), pct(all, 99), mean(all), np ? (double)nc / (double)np : 1.0,
                           (unsigned long long)(svc1 - svc0));
             pool_json += b;
-            std::fprintf(stderr, "[facade] %s%d: %.4g calls/s, %.4g residues/s, p50 %.1f us, p99 %.1f us\n",
-                         mode_name[co], T, nm / tp, (double)(residues * R) / tp, pct(all, 50), pct(all, 99));
+            std::fprintf(stderr, "[facade] %s%d: %.4g calls/s, %.4g residues/s, p50 %.1f us, p99 %.1f us, mean %.2f us "
+                         "(a thread's call cycle %.2f us)\n", mode_name[co], T, nm / tp, (double)(residues * R) / tp,
+                         pct(all, 50), pct(all, 99), mean(all), tp * 1e6 * T / nm);
         }
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
