@@ -712,6 +712,149 @@ __global__ __launch_bounds__(256) void fq_desc_lane_kernel(const uint8_t *bases,
         lane_read_runs_global(bases + ob, len, w);
 }
 
+/*
+ * 3''. count + scan + anchors in ONE pass (option fq_fused, the default with
+ * anchors): the count kernel, the scan of its wave sums, the tail kernel and
+ * the anchor kernel above fused by a decoupled look-back.  A wave takes the
+ * next tile of 64 reads from a counter (so every tile it waits on belongs to a
+ * wave already running), counts its reads' runs per frame into registers,
+ * publishes the tile's sums, sums the published sums / prefixes of the tiles
+ * before it (64 predecessors per step, one per lane), publishes its inclusive
+ * prefix, and writes its reads' fragment offsets and anchors from the same
+ * staged nibble string -- the reads are read once, and the per-(read, frame)
+ * residue counts never leave the registers.  Tile states are epoch-tagged
+ * (flag = epoch << 2 | 1 sums, | 2 prefix), so nothing is cleared between
+ * launches; the wave that draws the last id resets the counter.  Same
+ * outputs as count -> scan -> tail -> desc, bit for bit.
+ */
+__global__ __launch_bounds__(256) void fq_anchor_fused_kernel(
+    const uint8_t *bases, const uint64_t *read_off, uint32_t n_reads, uint32_t n_tiles, uint32_t total_waves,
+    uint32_t *tile_ctr, uint32_t *tile_flag, ulonglong2 *tile_agg, ulonglong2 *tile_inc, uint32_t epoch,
+    uint32_t *frame_nf, uint32_t *frag_base, uint64_t *out_off, uint64_t *out_anchor, uint64_t *totals,
+    uint64_t max_frag, uint64_t max_res)
+{
+    __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t tile = 0;
+    if (lane == 0)
+        tile = atomicAdd(tile_ctr, 1u);
+    tile = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)tile, 0));
+    if (tile == total_waves - 1 && lane == 0)
+        __hip_atomic_store(tile_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); /* every id is drawn */
+    if (tile >= n_tiles)
+        return;
+    uint32_t *ns = nspan[wv];
+    const uint64_t r0 = (uint64_t)tile * FQ_TILE;
+    const uint32_t n = (uint32_t)std::min<uint64_t>(FQ_TILE, n_reads - r0);
+    const uint64_t r = r0 + lane;
+    const uint64_t ob = lane < n ? read_off[r] : 0, oe = lane < n ? read_off[r + 1] : 0;
+    const uint64_t first = uniform_u64(__shfl(ob, 0)), end = uniform_u64(__shfl(oe, (int)n - 1));
+    uintptr_t a = 0;
+    const bool staged = stage_span(ns, bases, first, end, lane, a);
+    const uint32_t len = (uint32_t)(oe - ob);
+    RunCount6 rc;
+    if (lane < n) {
+        if (staged)
+            lane_read_runs_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), len, rc);
+        else
+            lane_read_runs_global(bases + ob, len, rc);
+    }
+    uint64_t nf = 0, nr = 0;
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        nf += rc.nf[f];
+        nr += rc.nr[f];
+    }
+    const uint64_t F = wave_sum(nf), R = wave_sum(nr);
+    /* publish the tile's sums (tile 0: its prefix) */
+    const uint32_t E = epoch << 2;
+    if (lane == 0) {
+        if (tile == 0) {
+            tile_inc[0] = make_ulonglong2(F, R);
+            __hip_atomic_store(&tile_flag[0], E | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            tile_agg[tile] = make_ulonglong2(F, R);
+            __hip_atomic_store(&tile_flag[tile], E | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    /* look back: lane l examines tile j - l */
+    uint64_t xf = 0, xr = 0;
+    for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64) {
+        const int64_t idx = j - (int64_t)lane;
+        uint32_t st = 2;
+        uint64_t vf = 0, vr = 0;
+        if (idx >= 0) {
+            uint32_t fl;
+            do {
+                fl = __hip_atomic_load(&tile_flag[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((fl & ~3u) != E || (fl & 3u) == 0);
+            st = fl & 3u;
+            const ulonglong2 v = st == 2 ? tile_inc[idx] : tile_agg[idx];
+            vf = v.x;
+            vr = v.y;
+        }
+        const uint64_t pm = __ballot(st == 2);
+        const uint32_t upto = pm ? (uint32_t)__builtin_ctzll(pm) : 63u; /* lanes 0..upto count */
+        if (lane > upto) {
+            vf = 0;
+            vr = 0;
+        }
+        xf += wave_sum(vf);
+        xr += wave_sum(vr);
+        if (pm)
+            break;
+    }
+    xf = uniform_u64(xf);
+    xr = uniform_u64(xr);
+    const uint64_t tf = xf + F, tr = xr + R;
+    if (lane == 0 && tile != 0) {
+        tile_inc[tile] = make_ulonglong2(tf, tr);
+        __hip_atomic_store(&tile_flag[tile], E | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    /* the batch's totals and CSR tails (fq_tail_kernel's work) */
+    if (tile == n_tiles - 1 && lane == 0) {
+        const bool over = tf > max_frag || tr > max_res;
+        totals[0] = over ? max_frag + 1 : tf;
+        totals[1] = tr;
+        if (!over) {
+            out_off[tf] = tr;
+            frag_base[(uint64_t)n_reads * 6] = (uint32_t)tf;
+            frame_nf[(uint64_t)n_reads * 6] = 0;
+        }
+    }
+    /* a batch past the buffers writes nothing beyond them (the finish
+     * reports it from the totals) */
+    if (tf > max_frag || tr > max_res || lane >= n)
+        return;
+    /* the read's first fragment and residue: the tile's prefix + the earlier reads' counts */
+    uint64_t pf = nf, pr = nr;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t yf = __shfl_up(pf, o), yr = __shfl_up(pr, o);
+        if (lane >= o) {
+            pf += yf;
+            pr += yr;
+        }
+    }
+    RunWrite w;
+    uint64_t fb = xf + pf - nf, rb = xr + pr - nr;
+#pragma unroll
+    for (uint32_t f = 0; f < 6; f++) {
+        frame_nf[r * 6 + f] = rc.nf[f];
+        frag_base[r * 6 + f] = (uint32_t)fb;
+        w.fi[f] = (uint32_t)(f < 3 ? fb : fb + rc.nf[f] - 1);
+        w.ri[f] = f < 3 ? rb : rb + rc.nr[f];
+        fb += rc.nf[f];
+        rb += rc.nr[f];
+    }
+    w.ob = ob;
+    w.out_off = out_off;
+    w.out_anchor = out_anchor;
+    if (staged)
+        lane_read_runs_ns(ns, (uint32_t)(reinterpret_cast<uintptr_t>(bases + ob) - a), len, w);
+    else
+        lane_read_runs_global(bases + ob, len, w);
+}
+
 struct PairSum {
     __host__ __device__ ulonglong2 operator()(const ulonglong2 &a, const ulonglong2 &b) const
     {
@@ -955,6 +1098,31 @@ int fq_fragments_enqueue(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_r
     ulonglong2 *tile_base = tile_sum + (n_tiles + 1);
     uint64_t *totals = reinterpret_cast<uint64_t *>(tile_base + (n_tiles + 1));
     void *scan_tmp = ws + ((((rc_bytes + 15) & ~15ull) + 2 * ts_bytes + 16 + 255) & ~255ull);
+    if (n_reads && desc && c->fq_fused) {
+        /* one pass: count + look-back scan + anchors */
+        const uint32_t grid = (uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG);
+        const size_t look_bytes = 256 + n_tiles * (4 + 2 * sizeof(ulonglong2));
+        const size_t cap0 = c->fq_look.cap;
+        HIP_TRY(c->fq_look.reserve(look_bytes));
+        if (c->fq_look.cap != cap0) /* fresh memory: no tile state of any epoch, counter 0 */
+            HIP_TRY(hipMemsetAsync(c->fq_look.p, 0, c->fq_look.cap, st));
+        char *lb = static_cast<char *>(c->fq_look.p);
+        uint32_t *ctr = reinterpret_cast<uint32_t *>(lb);
+        ulonglong2 *agg = reinterpret_cast<ulonglong2 *>(lb + 256);
+        ulonglong2 *inc = agg + n_tiles;
+        uint32_t *flag = reinterpret_cast<uint32_t *>(inc + n_tiles);
+        c->fq_epoch = (c->fq_epoch + 1) & 0x3FFFFFFFu;
+        if (c->fq_epoch == 0)
+            c->fq_epoch = 1;
+        hipLaunchKernelGGL(fq_anchor_fused_kernel, dim3(grid), dim3(256), 0, st, d_bases, d_read_off, n_reads,
+                           (uint32_t)n_tiles, grid * WAVES_PER_WG, ctr, flag, agg, inc, c->fq_epoch,
+                           c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(), c->fq_off.as<uint64_t>(),
+                           c->fq_anchor.as<uint64_t>(), totals, max_frag, max_res);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data(), totals, 16, hipMemcpyDeviceToHost, st));
+        c->fq_pend = {true, desc, n_reads, max_frag, max_res, d_bases, bound};
+        return KGX_OK;
+    }
     if (n_reads && desc)
         hipLaunchKernelGGL(fq_count_lane_kernel<true>, dim3((uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG)),
                            dim3(256), 0, st, d_bases, d_read_off, n_reads, read_counts, tile_sum, (uint32_t)n_tiles,

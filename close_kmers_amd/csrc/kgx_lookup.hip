@@ -1025,6 +1025,23 @@ __device__ __forceinline__ void score_sequence(
         call_count[s] = 0;
         return;
     }
+    if (!want_otu && prm.min_hits > 0 && gw1 > gw0) {
+        /* fewer hits than min_hits: no run can reach a call (a call counts
+         * at most the sequence's hits, kguts.cc:757-770), and without OTU
+         * output the run flags are not kept -- count and leave without
+         * reading a record (fq fragments: ~16 windows, < 1 hit each) */
+        uint32_t nh = 0;
+        for (uint64_t g = gw0 >> 6; g <= (gw1 - 1) >> 6; g++) {
+            const uint32_t lo = g == (gw0 >> 6) ? (uint32_t)(gw0 & 63) : 0u;
+            const uint32_t hi = g == ((gw1 - 1) >> 6) ? (uint32_t)((gw1 - 1) & 63) + 1 : 64u;
+            nh += (uint32_t)__popcll(hit_mask[g] & bit_range(lo, hi));
+        }
+        if ((int)nh < prm.min_hits) {
+            hit_count[s] = nh;
+            call_count[s] = 0;
+            return;
+        }
+    }
 
     typedef HitFields<PK> HF;
     constexpr uint32_t F_RUN = KGX_HIT_IN_RUN << HF::FLAG_SHIFT, F_CNT = KGX_HIT_COUNTED << HF::FLAG_SHIFT,

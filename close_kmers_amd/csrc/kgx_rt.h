@@ -325,6 +325,8 @@ struct kgx_ctx {
     /* fq fragments (kgx_fq.hip) */
     kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start,
         fq_anchor, fq_nres;
+    kgx::DevBuf fq_look; /* fq_fused: tile counter | tile sums | tile prefixes | tile states */
+    uint32_t fq_epoch = 0;
     kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
     kgx::FqPending fq_pend;             /* an enqueued fragment pass awaiting its finish */
     /* kgx_fq_called_reads */
@@ -342,6 +344,7 @@ struct kgx_ctx {
     int fq_count = 1;      /* fq count pass: 1 = lane-per-read stop scan, 0 = wave-per-read translation */
     int fq_probe_j = 1;    /* tile of the DNA probe (fragments as anchors), 64 x J windows; 0 = probe_j */
     int fq_plan = 1;       /* 1: this context's fragments are planned elementwise (fq_plan_kernel); 0: launch_plan */
+    int fq_fused = 1;      /* anchors: count + scan + emit in one look-back pass (fq_anchor_fused_kernel); 0: four launches */
     int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */

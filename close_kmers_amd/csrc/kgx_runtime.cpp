@@ -1060,6 +1060,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->score_wave_tiles = (int)value;
         return KGX_OK;
     }
+    if (n == "fq_fused") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "fq_fused must be 0 or 1");
+        c->fq_fused = (int)value;
+        return KGX_OK;
+    }
     if (n == "fq_plan") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "fq_plan must be 0 or 1");

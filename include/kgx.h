@@ -290,6 +290,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * is 64 * probe_j windows), read at the next plan;
  * "fq_probe_j" (0..4, default 1) = windows per lane of kgx_fq_run_device's
  * DNA probe (fragments as anchors), 0 = probe_j;
+ * "fq_fused" 1 (default) = the anchor fragment pass (fq_residues 0) counts,
+ * scans and writes in one launch (decoupled look-back over tiles of 64
+ * reads), 0 = count, scan, tail and anchor kernels;
  * "fq_plan" 1 (default) = kgx_fq_run_device plans the fragments of the
  * context's own fragment pass with one elementwise kernel (each has >= 11
  * residues, so a window base is its residue offset - 8 per earlier fragment),

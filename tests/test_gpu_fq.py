@@ -187,8 +187,8 @@ def _anchor_reads(rng):
     return reads
 
 
-@pytest.mark.parametrize("fq_count", [0, 1])
-def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count):
+@pytest.mark.parametrize("fq_count,fq_fused", [(0, 1), (1, 1), (1, 0)])
+def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count, fq_fused):
     """fq_residues 0: the same fragment records (offsets, read, frame, frame
     counts) as with residues, and each anchor translates to the fragment's
     residues (forward and reverse strand, IUPAC and lower case, long reads)."""
@@ -200,6 +200,7 @@ def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count):
         ctx.set_option("fq_count", fq_count)
         h1 = ctx.fragments_to_host(ctx.fq_fragments(res, off))
         ctx.set_option("fq_residues", 0)
+        ctx.set_option("fq_fused", fq_fused)
         f0 = ctx.fq_fragments(res, off)
         h0 = ctx.fragments_to_host(f0)
     assert h0["residues"] is None and h0["read"] is None and f0.n_bases == len(bases)
@@ -215,6 +216,36 @@ def test_fragment_anchors_translate_to_residues(gpu, oracle_lib, fq_count):
         want = bytes(h1["residues"][o[i]:o[i + 1]]).decode()
         assert _translate_anchor(bases, int(h0["anchors"][i]), len(want)) == want, i
     assert f0.n_fragments > 1000 and (h0["anchors"] & 1).sum() > 100
+
+
+def test_fused_anchor_pass_equals_four_launches(gpu):
+    """fq_fused 1 (count + look-back scan + anchors in one launch) writes the
+    same offsets, anchors, per-(read, frame) counts and first fragments as
+    the count / scan / tail / anchor launches, over thousands of tiles (the
+    look-back walks many 64-tile steps), batch after batch on one context
+    (epoch-tagged tile states, a shrinking and a growing batch), with empty
+    and short reads (the overflow report: test_fragments_start_finish_ahead_schedule)."""
+    spec, table = synthetic_table(20000)
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 300, 200_000)
+    lens[rng.choice(len(lens), 2000, replace=False)] = 0
+    pool = np.frombuffer(b"ACGTACGTACGTNacgtRY", np.uint8)
+    reads = [bytes(pool[rng.integers(0, len(pool), int(L))]) for L in lens]
+    with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        ctx.set_option("fq_residues", 0)
+        for n in (200_000, 3_000, 150_000, 1, 0, 200_000):
+            res, off = pack([("r", r) for r in reads[:n]])
+            out = []
+            for fused in (0, 1):
+                ctx.set_option("fq_fused", fused)
+                f = ctx.fq_fragments(res, off)
+                h = ctx.fragments_to_host(f)
+                out.append((f.n_fragments, f.n_residues, h["offsets"], h["anchors"], h["frame_counts"]))
+            assert out[0][0] == out[1][0] and out[0][1] == out[1][1], n
+            for k in (2, 3, 4):
+                assert np.array_equal(out[0][k], out[1][k]), (n, k)
+            if n > 1000:
+                assert out[1][0] > n
 
 
 @pytest.mark.parametrize("fq_probe_j,fq_plan", [(1, 1), (2, 1), (4, 1), (0, 1), (1, 0)])
