@@ -722,16 +722,20 @@ __global__ __launch_bounds__(256) void fq_desc_lane_kernel(const uint8_t *bases,
  * before it (64 predecessors per step, one per lane), publishes its inclusive
  * prefix, and writes its reads' fragment offsets and anchors from the same
  * staged nibble string -- the reads are read once, and the per-(read, frame)
- * residue counts never leave the registers.  Tile states are epoch-tagged
- * (flag = epoch << 2 | 1 sums, | 2 prefix), so nothing is cleared between
- * launches; the wave that draws the last id resets the counter.  Same
- * outputs as count -> scan -> tail -> desc, bit for bit.
+ * residue counts never leave the registers.  A tile's state is ONE 64-bit
+ * word, state << 62 | fragments << 31 | residues (1 sums, 2 prefix; zeroed
+ * before the launch), stored and loaded with relaxed device-scope atomics:
+ * no release / acquire, whose cross-XCD L2 write-backs made a first version
+ * with separate flag and value words 1.6x slower end to end.  Needs fewer
+ * than 2^31 fragments and residues per batch (the host checks).  The wave
+ * that draws the last id resets the counter.  Same outputs as count -> scan
+ * -> tail -> desc, bit for bit.
  */
+constexpr uint64_t LB_MASK31 = (1ull << 31) - 1;
 __global__ __launch_bounds__(256) void fq_anchor_fused_kernel(
     const uint8_t *bases, const uint64_t *read_off, uint32_t n_reads, uint32_t n_tiles, uint32_t total_waves,
-    uint32_t *tile_ctr, uint32_t *tile_flag, ulonglong2 *tile_agg, ulonglong2 *tile_inc, uint32_t epoch,
-    uint32_t *frame_nf, uint32_t *frag_base, uint64_t *out_off, uint64_t *out_anchor, uint64_t *totals,
-    uint64_t max_frag, uint64_t max_res)
+    uint32_t *tile_ctr, uint64_t *tile_state, uint32_t *frame_nf, uint32_t *frag_base, uint64_t *out_off,
+    uint64_t *out_anchor, uint64_t *totals, uint64_t max_frag, uint64_t max_res)
 {
     __shared__ uint32_t nspan[WAVES_PER_WG][NS_WORDS];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -767,50 +771,32 @@ __global__ __launch_bounds__(256) void fq_anchor_fused_kernel(
     }
     const uint64_t F = wave_sum(nf), R = wave_sum(nr);
     /* publish the tile's sums (tile 0: its prefix) */
-    const uint32_t E = epoch << 2;
-    if (lane == 0) {
-        if (tile == 0) {
-            tile_inc[0] = make_ulonglong2(F, R);
-            __hip_atomic_store(&tile_flag[0], E | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            tile_agg[tile] = make_ulonglong2(F, R);
-            __hip_atomic_store(&tile_flag[tile], E | 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (lane == 0)
+        __hip_atomic_store(&tile_state[tile], (tile == 0 ? 2ull : 1ull) << 62 | F << 31 | R, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     /* look back: lane l examines tile j - l */
     uint64_t xf = 0, xr = 0;
     for (int64_t j = (int64_t)tile - 1; j >= 0; j -= 64) {
         const int64_t idx = j - (int64_t)lane;
-        uint32_t st = 2;
-        uint64_t vf = 0, vr = 0;
-        if (idx >= 0) {
-            uint32_t fl;
+        uint64_t v = 2ull << 62; /* before tile 0: a zero prefix */
+        if (idx >= 0)
             do {
-                fl = __hip_atomic_load(&tile_flag[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            } while ((fl & ~3u) != E || (fl & 3u) == 0);
-            st = fl & 3u;
-            const ulonglong2 v = st == 2 ? tile_inc[idx] : tile_agg[idx];
-            vf = v.x;
-            vr = v.y;
-        }
-        const uint64_t pm = __ballot(st == 2);
+                v = __hip_atomic_load(&tile_state[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } while ((v >> 62) == 0);
+        const uint64_t pm = __ballot((v >> 62) == 2);
         const uint32_t upto = pm ? (uint32_t)__builtin_ctzll(pm) : 63u; /* lanes 0..upto count */
-        if (lane > upto) {
-            vf = 0;
-            vr = 0;
-        }
-        xf += wave_sum(vf);
-        xr += wave_sum(vr);
+        const bool in = lane <= upto;
+        xf += wave_sum(in ? (v >> 31) & LB_MASK31 : 0);
+        xr += wave_sum(in ? v & LB_MASK31 : 0);
         if (pm)
             break;
     }
     xf = uniform_u64(xf);
     xr = uniform_u64(xr);
     const uint64_t tf = xf + F, tr = xr + R;
-    if (lane == 0 && tile != 0) {
-        tile_inc[tile] = make_ulonglong2(tf, tr);
-        __hip_atomic_store(&tile_flag[tile], E | 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0 && tile != 0)
+        __hip_atomic_store(&tile_state[tile], 2ull << 62 | (tf & LB_MASK31) << 31 | (tr & LB_MASK31),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     /* the batch's totals and CSR tails (fq_tail_kernel's work) */
     if (tile == n_tiles - 1 && lane == 0) {
         const bool over = tf > max_frag || tr > max_res;
@@ -1098,26 +1084,20 @@ int fq_fragments_enqueue(kgx_ctx *c, const uint8_t *d_bases, const uint64_t *d_r
     ulonglong2 *tile_base = tile_sum + (n_tiles + 1);
     uint64_t *totals = reinterpret_cast<uint64_t *>(tile_base + (n_tiles + 1));
     void *scan_tmp = ws + ((((rc_bytes + 15) & ~15ull) + 2 * ts_bytes + 16 + 255) & ~255ull);
-    if (n_reads && desc && c->fq_fused) {
+    if (n_reads && desc && c->fq_fused && max_res < (1ull << 31)) {
         /* one pass: count + look-back scan + anchors */
         const uint32_t grid = (uint32_t)((n_tiles + WAVES_PER_WG - 1) / WAVES_PER_WG);
-        const size_t look_bytes = 256 + n_tiles * (4 + 2 * sizeof(ulonglong2));
         const size_t cap0 = c->fq_look.cap;
-        HIP_TRY(c->fq_look.reserve(look_bytes));
-        if (c->fq_look.cap != cap0) /* fresh memory: no tile state of any epoch, counter 0 */
-            HIP_TRY(hipMemsetAsync(c->fq_look.p, 0, c->fq_look.cap, st));
+        HIP_TRY(c->fq_look.reserve(256 + n_tiles * sizeof(uint64_t)));
         char *lb = static_cast<char *>(c->fq_look.p);
-        uint32_t *ctr = reinterpret_cast<uint32_t *>(lb);
-        ulonglong2 *agg = reinterpret_cast<ulonglong2 *>(lb + 256);
-        ulonglong2 *inc = agg + n_tiles;
-        uint32_t *flag = reinterpret_cast<uint32_t *>(inc + n_tiles);
-        c->fq_epoch = (c->fq_epoch + 1) & 0x3FFFFFFFu;
-        if (c->fq_epoch == 0)
-            c->fq_epoch = 1;
+        if (c->fq_look.cap != cap0) /* fresh memory: the tile counter starts at 0 */
+            HIP_TRY(hipMemsetAsync(lb, 0, 4, st));
+        HIP_TRY(hipMemsetAsync(lb + 256, 0, n_tiles * sizeof(uint64_t), st)); /* no tile published */
         hipLaunchKernelGGL(fq_anchor_fused_kernel, dim3(grid), dim3(256), 0, st, d_bases, d_read_off, n_reads,
-                           (uint32_t)n_tiles, grid * WAVES_PER_WG, ctr, flag, agg, inc, c->fq_epoch,
-                           c->fq_nfrag.as<uint32_t>(), c->fq_fbase.as<uint32_t>(), c->fq_off.as<uint64_t>(),
-                           c->fq_anchor.as<uint64_t>(), totals, max_frag, max_res);
+                           (uint32_t)n_tiles, grid * WAVES_PER_WG, reinterpret_cast<uint32_t *>(lb),
+                           reinterpret_cast<uint64_t *>(lb + 256), c->fq_nfrag.as<uint32_t>(),
+                           c->fq_fbase.as<uint32_t>(), c->fq_off.as<uint64_t>(), c->fq_anchor.as<uint64_t>(), totals,
+                           max_frag, max_res);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_fq_tot.data(), totals, 16, hipMemcpyDeviceToHost, st));
         c->fq_pend = {true, desc, n_reads, max_frag, max_res, d_bases, bound};

@@ -325,8 +325,7 @@ struct kgx_ctx {
     /* fq fragments (kgx_fq.hip) */
     kgx::DevBuf fq_bases, fq_roff, fq_nfrag, fq_fbase, fq_tmp, fq_res, fq_off, fq_read, fq_frame, fq_start,
         fq_anchor, fq_nres;
-    kgx::DevBuf fq_look; /* fq_fused: tile counter | tile sums | tile prefixes | tile states */
-    uint32_t fq_epoch = 0;
+    kgx::DevBuf fq_look; /* fq_fused: tile counter | tile states */
     kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
     kgx::FqPending fq_pend;             /* an enqueued fragment pass awaiting its finish */
     /* kgx_fq_called_reads */
