@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--rec12", default="0", help="host_rec12 settings to try")
     ap.add_argument("--nt", default="1", help="host_nt settings to try")
     ap.add_argument("--timing", action="store_true", help="one extra KGX_TIMING pass per setting (stderr)")
+    ap.add_argument("--compact", action="store_true",
+                    help="kgx_process_batch_compact (records + mask, bench.py's host_path value) instead of kgx_hit")
+    ap.add_argument("--no-pieces", action="store_true", help="skip the raw memcpy / PCIe rates")
     args = ap.parse_args()
     from close_kmers_amd import abi, synth
     import torch
@@ -69,11 +72,15 @@ def main():
         ctx.set_option("host_copy_blocks", nb)
         ctx.set_option("host_hits16", h16)
         ctx.set_option("host_threads", nt)
-        r = ctx.process_batch(res, off, params, want=3, copy=False)
+        def run():
+            if args.compact:
+                return ctx.process_batch_compact(res, off, params, want=3)
+            return ctx.process_batch(res, off, params, want=3, copy=False)
+        r = run()
         th = []
-        for _ in range(7):
+        for _ in range(9):
             t0 = time.perf_counter()
-            r = ctx.process_batch(res, off, params, want=3, copy=False)
+            r = run()
             th.append(time.perf_counter() - t0)
         key = f"chunks{k}_copy{hc}" + (f"_blocks{nb}" if hc else "") + f"_h16{h16}" + (f"_t{nt}" if h16 else "") + f"_st{st}_cf{cf}_hs{hs}_tp{tp}_r{r12}_nt{ntst}"
         times[key] = float(np.median(th)) * 1e3
@@ -83,6 +90,10 @@ def main():
             ctx.process_batch(res, off, params, want=3, copy=False)
             del os.environ["KGX_TIMING"]
     out["ms_by_host_chunks"] = times
+    out["compact"] = bool(args.compact)
+    if args.no_pieces:
+        print(json.dumps(out), flush=True)
+        return
     n_hits = len(r.hits)
     out["hits"] = n_hits
     # pieces alone
