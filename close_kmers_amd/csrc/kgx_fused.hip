@@ -246,6 +246,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             dst[1] = make_uint4(HF::fi(h), HF::wt(h), hpos[i], s);
         }
 
+    if (dbg)
+        a.dbg[6] = wall_clock64(); /* thread 0's record stores issued */
     /* 4b. the run scorer, wave 0, 64 hits per step (score_wave_kernel's
      * chunk rules for a single sequence) */
     uint32_t ncalls_out = 0;
@@ -464,15 +466,20 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * system-scope acquire load (the host wrote the residues, length, want and
  * parameters before it stored req), the workgroup runs the sequence, and
  * fused_small_body stores the records, the counts and done = req behind a
- * system-scope fence.  Every workgroup leaves on stop, after idle_ticks
- * without a request in any slot, or life_ticks after its start -- a bound on
- * how long the instance holds its hardware queue; the host keeps the next
- * instance queued behind it (kgx_svc.cpp).
+ * system-scope fence.  Every workgroup leaves on stop or life_ticks after
+ * its start -- a bound on how long the instance holds its hardware queue; the
+ * host keeps the next instance queued behind it while calls arrive
+ * (kgx_svc.cpp).  There is no per-workgroup idle exit: a first version left
+ * after 1 ms without a request in any slot, read from a device word every
+ * pickup raised, but a workgroup on another XCD could read that word stale
+ * from its own L2, leave while its slot was merely quiet, and strand the
+ * slot's next request until the instance ended (0.5% of calls waited up to
+ * the instance's lifetime: +40% mean latency at 16 callers).
  */
 __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbgs,
                                                   const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
                                                   const uint4 *table, uint64_t num_sigs, uint64_t magic,
-                                                  uint64_t *activity, uint64_t idle_ticks, uint64_t life_ticks)
+                                                  uint64_t life_ticks)
 {
     __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
     const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
@@ -502,17 +509,12 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                         cmd[lane] = v;
                     break;
                 }
-                const uint64_t now = wall_clock64();
-                const uint64_t act = __hip_atomic_load(activity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (now - t0 > life_ticks || now - (act > t0 ? act : t0) > idle_ticks)
+                if (wall_clock64() - t0 > life_ticks)
                     break;
-                __builtin_amdgcn_s_sleep(8);
+                __builtin_amdgcn_s_sleep(2);
             }
-            if (lane == 0) {
+            if (lane == 0)
                 cmd[16] = go;
-                if (go)
-                    __hip_atomic_fetch_max(activity, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
         }
         __syncthreads();
         if (!cmd[16])
@@ -549,13 +551,12 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t *activity, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream)
+                      uint64_t life_ticks, hipStream_t stream)
 {
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
-                       static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), activity, idle_ticks,
-                       life_ticks);
+                       static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
     return hipGetLastError();
 }
 

@@ -262,12 +262,11 @@ struct SvcSlotOut { /* device-written, one 64-B line per slot */
 };
 static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 64,
               "service slot lines");
-/* slots workgroups on stream; each leaves once no slot has had a request for
- * idle_ticks, or life_ticks after its start, or on stop (device wall clock,
- * 100 MHz); activity: a device word, the latest request pickup */
+/* slots workgroups on stream; each leaves life_ticks after its start (device
+ * wall clock, 100 MHz) or on stop */
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
-                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs, uint64_t *activity,
-                      uint64_t idle_ticks, uint64_t life_ticks, hipStream_t stream);
+                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs,
+                      uint64_t life_ticks, hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,

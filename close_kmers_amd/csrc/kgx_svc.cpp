@@ -14,12 +14,13 @@
  * and call records (fused_small_body: probe, ordered compaction, wave
  * scorer).  No runtime call is on a call's path.
  *
- * Instances: the kernel leaves after idle_us without a request, or life_us
- * after its start (a bound on how long it holds its hardware queue, which
- * other streams may share), or on stop.  The host keeps two instances
- * enqueued on the service's stream, so when one leaves the next is already
- * dispatched; callers top the queue up (hipEventQuery on the oldest, at most
- * every 200 us) and, should a request wait more than 100 us, at once.  A
+ * Instances: the kernel leaves life_us after its start (a bound on how long
+ * it holds its hardware queue, which other streams may share) or on stop.
+ * The host keeps two instances enqueued on the service's stream while calls
+ * arrive, so when one leaves the next is already dispatched; callers top the
+ * queue up (hipEventQuery on the oldest, at most every 200 us) and, should a
+ * request wait more than 100 us, at once.  Without calls nothing is
+ * enqueued, so the service leaves the GPU within 2 x life_us of the last call.  A
  * request written while an instance was leaving stays pending in its slot and
  * the next instance serves it (a workgroup starts from the slot's done word).
  * kgx_image_close / set_layout / set_filter stop the service first, and an
@@ -35,6 +36,9 @@
 #include <mutex>
 #include <set>
 #include <string>
+
+#include <sys/prctl.h>
+#include <time.h>
 
 #include "kgx_rt.h"
 
@@ -64,7 +68,6 @@ struct SvcState {
     uint8_t *d_res = nullptr;
     kgx_hit *d_hits = nullptr;
     kgx_call *d_calls = nullptr;
-    uint64_t *d_activity = nullptr;
     const void *table = nullptr;
     uint64_t num_sigs = 0;
     std::atomic<uint64_t> free_mask{0};
@@ -77,9 +80,13 @@ struct SvcState {
     /* KGX_SVC_DEBUG=1: the device's phase stamps per call, summed (ns):
      * [0] request stored -> done seen on the host (wall), [1..5] the device
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
-     * + scorer, 4->5 system fence) */
+     * + scorer, and [5] 3->6 the record stores alone) */
     bool debug = false;
     std::atomic<uint64_t> phase_ns[6] = {};
+    /* KGX_SVC_SLEEP_US: a caller sleeps this long before it spins for its
+     * answer (the device needs >= ~10 us per call), so a pool of spinning
+     * callers holds fewer CPUs; 0 = spin only */
+    uint32_t sleep_us = 0;
     bool broken = false; /* a launch failed: callers take other paths */
 };
 
@@ -121,7 +128,7 @@ int top_up(SvcState *s)
         }
         /* wall clock at 100 MHz: 100 ticks per us */
         hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->slots, s->table,
-                                  s->num_sigs, s->d_activity, s->idle_us * 100, s->life_us * 100, s->stream);
+                                  s->num_sigs, s->life_us * 100, s->stream);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
         if (e != hipSuccess) {
@@ -166,8 +173,6 @@ void destroy(SvcState *s)
         (void)hipEventDestroy(e);
     if (s->stream)
         (void)hipStreamDestroy(s->stream);
-    if (s->d_activity)
-        (void)hipFree(s->d_activity);
     if (s->reqmem)
         (void)hipFree(s->reqmem);
     if (s->host)
@@ -206,10 +211,6 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     if (e == hipSuccess)
         e = hipHostGetDevicePointer(&d, h, 0);
     if (e == hipSuccess)
-        e = hipMalloc(reinterpret_cast<void **>(&s->d_activity), sizeof(uint64_t));
-    if (e == hipSuccess)
-        e = hipMemset(s->d_activity, 0, sizeof(uint64_t));
-    if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     s->host = static_cast<char *>(h);
     if (e != hipSuccess) {
@@ -219,6 +220,8 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     std::memset(h, 0, b_hdr + b_out + b_dbg);
     const char *dbg_env = std::getenv("KGX_SVC_DEBUG");
     s->debug = dbg_env && std::atoi(dbg_env) != 0;
+    if (const char *sl = std::getenv("KGX_SVC_SLEEP_US"))
+        s->sleep_us = (uint32_t)std::max(0, std::atoi(sl));
     char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);
     s->hdr = reinterpret_cast<SvcSlotHdr *>(hp);
     s->d_hdr = reinterpret_cast<SvcSlotHdr *>(dp);
@@ -267,7 +270,13 @@ int get(kgx_image *img, SvcState **out)
 {
     std::lock_guard<std::mutex> lk(img->svc_mu);
     if (!img->svc) {
-        int rc = create(img, img->svc_slots, img->svc_idle_us, img->svc_life_us, &img->svc);
+        /* KGX_SVC_LIFE_US: a default for experiments (kgx_svc_config sets it per image) */
+        uint64_t idle = img->svc_idle_us, life = img->svc_life_us;
+        if (const char *e = std::getenv("KGX_SVC_IDLE_US"))
+            idle = std::max<uint64_t>(10, std::strtoull(e, nullptr, 10));
+        if (const char *e = std::getenv("KGX_SVC_LIFE_US"))
+            life = std::max<uint64_t>(idle, std::strtoull(e, nullptr, 10));
+        int rc = create(img, img->svc_slots, idle, life, &img->svc);
         if (rc)
             return rc;
     }
@@ -423,6 +432,15 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         }
     }
     const volatile uint32_t *done = &s->out[slot].done;
+    if (s->sleep_us) {
+        thread_local bool slack = false;
+        if (!slack) { /* hrtimer sleeps of a few us need a small timer slack */
+            (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+            slack = true;
+        }
+        const struct timespec ts = {0, (long)s->sleep_us * 1000};
+        nanosleep(&ts, nullptr);
+    }
     bool nudged = false;
     for (uint32_t spin = 1; *done != q; spin++) {
         if ((spin & 1023u) == 0) {
@@ -446,8 +464,9 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     if (s->debug) {
         const uint64_t *st = s->dbg[slot].stamp;
         s->phase_ns[0] += (uint64_t)(now_ns() - t0);
-        for (int k = 1; k <= 5; k++)
+        for (int k = 1; k <= 4; k++)
             s->phase_ns[k] += (st[k] - st[k - 1]) * 10; /* 100 MHz ticks */
+        s->phase_ns[5] += (st[6] - st[3]) * 10; /* compaction end -> thread 0's record stores issued */
     }
     const SvcSlotOut &o = s->out[slot];
     const uint32_t nh = o.nh, nc = o.nc;

@@ -425,8 +425,9 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
  * Persistent workgroups on the image's device, one per slot, poll slots in
  * mapped host memory; the call writes its sequence into a free slot and spins
  * until the device has stored its records.  Thread-safe; started on the first
- * call, and its workgroups leave after idle_us without requests (restarted on
- * demand).  Serves PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS,
+ * call; instances of the workgroups last life_us each and the host keeps one
+ * queued behind the running one while calls arrive, so the service leaves the
+ * GPU within 2 x life_us of the last call (restarted on demand).  Serves PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS,
  * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues;
  * anything else, or every slot busy, returns KGX_EBUSY and the caller takes a
  * batch path (kgx_process_batch*).  Results as kgx_process_batch gives them
@@ -436,9 +437,11 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
 int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
                  kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
                  uint64_t *n_calls);
-/* slots (1..64, default 32), idle_us (default 1000) and life_us (default
- * 4000: an instance's longest stay before the next one, already enqueued,
- * takes over); stops a running service */
+/* slots (1..64, default 32) and life_us (default 4000: an instance's stay
+ * before the next one, already enqueued, takes over; bounds how long the
+ * service holds its hardware queue); stops a running service.  idle_us is
+ * checked (>= 10, <= life_us) but no longer used: a per-workgroup idle exit
+ * could strand a quiet slot's next request. */
 int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t life_us);
 /* stops the service (its workgroups leave; kgx_image_close does this too) */
 int kgx_svc_stop(kgx_image *img);

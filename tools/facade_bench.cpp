@@ -274,7 +274,7 @@ int main(int argc, char **argv)
             }
             if (!phases.empty())
                 std::fprintf(stderr, "[facade] %s%d service phases (us: wall, residues, probe, compact, store+score, "
-                             "fence): %s\n", mode_name[co], T, phases.c_str());
+                             "stores): %s\n", mode_name[co], T, phases.c_str());
             char b[400];
             std::snprintf(b, sizeof b,
                           "%s\"%s%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g, \"p50_us\": %.1f, "
