@@ -285,7 +285,7 @@ struct kgx_image {
     /* the resident call service (kgx_svc.cpp), created on the first kgx_svc_call */
     std::mutex svc_mu;
     kgx::SvcState *svc = nullptr;
-    uint32_t svc_slots = 32, svc_idle_us = 1000, svc_life_us = 4000;
+    uint32_t svc_slots = 32, svc_idle_us = 1000, svc_life_us = 1000;
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;

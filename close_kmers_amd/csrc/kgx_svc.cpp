@@ -47,7 +47,7 @@ namespace kgx {
 struct SvcState {
     int device = 0;
     uint32_t slots = 32;
-    uint64_t idle_us = 1000, life_us = 4000;
+    uint64_t idle_us = 1000, life_us = 1000;
     hipStream_t stream = nullptr;
     char *host = nullptr; /* one mapped, coherent block: hdr | out | dbg | res | hits | calls */
     /* large-BAR devices: the request side (hdr | res) in fine-grained device

@@ -437,7 +437,7 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
 int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
                  kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
                  uint64_t *n_calls);
-/* slots (1..64, default 32) and life_us (default 4000: an instance's stay
+/* slots (1..64, default 32) and life_us (default 1000: an instance's stay
  * before the next one, already enqueued, takes over; bounds how long the
  * service holds its hardware queue); stops a running service.  idle_us is
  * checked (>= 10, <= life_us) but no longer used: a per-workgroup idle exit

@@ -155,3 +155,58 @@ def test_svc_threads_and_restarts_match_oracle(svc_image, oracle_lib):
     img.svc_stop()
     h, c = img.svc_call(seqs[1], PARAMS[1])  # a stopped service starts again
     _check(oracle_lib, table, seqs[1], _tuple(PARAMS[1]), h, c, "after stop")
+
+
+def test_svc_beside_batches_on_the_same_image(svc_image, oracle_lib):
+    """A pool of per-sequence callers (service) and a batch caller (its own
+    context) on one image at once: both stay exact, and the batches keep
+    finishing while service instances come and go (their kernels may share a
+    hardware queue with the service's stream: each instance stays at most
+    life_us)."""
+    spec, table, img = svc_image
+    img.svc_config(32, 1000, 4000)
+    seqs = _seqs(spec, 800, 41)
+    res, off = synth.make_queries(spec, 2000, x_permille=3, q0=99)
+    want = oracle_lib.process_batch(table, res, off, want=3)
+    stop = False
+    errs, batch_ms = [], []
+
+    def batches():
+        import time as _t
+        try:
+            with abi.Context(img) as ctx:
+                while not stop:
+                    t0 = _t.perf_counter()
+                    got = ctx.process_batch(res, off, abi.parse_params(None), want=3)
+                    batch_ms.append((_t.perf_counter() - t0) * 1e3)
+                    assert np.array_equal(got.hit_offsets, want.hit_offsets)
+                    assert np.array_equal(got.hits["which_kmer"], want.hits["which_kmer"])
+                    assert np.array_equal(got.calls["weighted_hits"].view(np.uint32),
+                                          want.calls["weighted_hits"].view(np.uint32))
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    out = [None] * len(seqs)
+
+    def callers(t, T):
+        try:
+            for i in range(t, len(seqs), T):
+                out[i] = img.svc_call(seqs[i], PARAMS[0])
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    bt = threading.Thread(target=batches)
+    bt.start()
+    ws = [threading.Thread(target=callers, args=(t, 8)) for t in range(8)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    stop = True
+    bt.join()
+    assert not errs, errs[:3]
+    assert len(batch_ms) >= 1
+    for i, s in enumerate(seqs):
+        _check(oracle_lib, table, s, _tuple(PARAMS[0]), out[i][0], out[i][1], i)
+    print(f"batches beside the service: {len(batch_ms)}, median {np.median(batch_ms):.2f} ms, "
+          f"max {max(batch_ms):.2f} ms")
