@@ -164,7 +164,7 @@ def test_svc_beside_batches_on_the_same_image(svc_image, oracle_lib):
     hardware queue with the service's stream: each instance stays at most
     life_us)."""
     spec, table, img = svc_image
-    img.svc_config(32, 1000, 4000)
+    img.svc_config(32, 1000, 1000)  # the default lifetime
     seqs = _seqs(spec, 800, 41)
     res, off = synth.make_queries(spec, 2000, x_permille=3, q0=99)
     want = oracle_lib.process_batch(table, res, off, want=3)
