@@ -87,7 +87,7 @@ struct SvcState {
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
     uint32_t sleep_us = 0;
-    bool broken = false; /* a launch failed: callers take other paths */
+    std::atomic<bool> broken{false}; /* a launch failed: callers take other paths */
 };
 
 namespace {
