@@ -537,10 +537,27 @@ __device__ __forceinline__ bool stage_span(uint32_t *ns, const uint8_t *bases, u
         return false;
     const uint4 *src = reinterpret_cast<const uint4 *>(a);
     const uint32_t nv = (uint32_t)((bytes + 15) / 16);
-    for (uint32_t i = lane; i < nv + 1; i += 64) {
-        const uint4 v = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
-        ns[2 * i] = nibbles4(v.x) | nibbles4(v.y) << 16;
-        ns[2 * i + 1] = nibbles4(v.z) | nibbles4(v.w) << 16;
+    /* 4 loads in flight per lane before any is converted.  The loads are
+     * unconditional (past the span they re-read its last 16 bytes) and the
+     * zero pad is a select afterwards: a load under a branch whose value
+     * merges at the join is waited for right there, and one wait per 16 B
+     * made the staging ~10 dependent round trips per wave */
+    constexpr uint32_t U = 4;
+    for (uint32_t i0 = lane; i0 < nv + 1; i0 += 64 * U) {
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++)
+            v[k] = src[min(i0 + 64 * k, nv - 1)];
+#pragma unroll
+        for (uint32_t k = 0; k < U; k++) {
+            const uint32_t i = i0 + 64 * k;
+            const bool in = i < nv;
+            const uint4 w = make_uint4(in ? v[k].x : 0u, in ? v[k].y : 0u, in ? v[k].z : 0u, in ? v[k].w : 0u);
+            if (i < nv + 1) {
+                ns[2 * i] = nibbles4(w.x) | nibbles4(w.y) << 16;
+                ns[2 * i + 1] = nibbles4(w.z) | nibbles4(w.w) << 16;
+            }
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
