@@ -243,7 +243,7 @@ SIGNATURES = {
     "kgx_ctx_host_profile": (_INT, [_P, ctypes.POINTER(HostProfile)]),
     "kgx_ctx_stat": (_INT, [_P, _CS, ctypes.POINTER(ctypes.c_int64)]),
     "kgx_svc_call": (_INT, [_P, ctypes.POINTER(Params), _P, _U64, _U32, _P, _U64, ctypes.POINTER(_U64), _P, _U64,
-                            ctypes.POINTER(_U64)]),
+                            ctypes.POINTER(_U64), _P, _U64, ctypes.POINTER(_U64)]),
     "kgx_svc_config": (_INT, [_P, _U32, _U32, _U32]),
     "kgx_svc_stop": (_INT, [_P]),
     "kgx_svc_stat": (_INT, [_P, _CS, ctypes.POINTER(_U64)]),
@@ -411,18 +411,25 @@ class Image:
         check(lib().kgx_image_download(self.handle, t.ctypes.data, t.nbytes), "kgx_image_download")
         return t
 
-    def svc_call(self, seq: bytes, params=None, want: int = WANT_HITS | WANT_CALLS):
+    def svc_call(self, seq: bytes, params=None, want: int = WANT_HITS | WANT_CALLS, otus: bool = False):
         """One sequence through the resident call service (kgx_svc_call):
-        (hits, calls) arrays; raises KgxError (code KGX_EBUSY) for a call the
-        service does not take."""
+        (hits, calls) arrays, or (hits, calls, otus) with otus=True (want
+        then includes WANT_OTU); raises KgxError (code KGX_EBUSY) for a call
+        the service does not take."""
         p = params if isinstance(params, Params) else parse_params(params)
         W = max(len(seq) - 8, 0)
         hits = np.empty(max(W, 1), HIT_DTYPE)
         calls = np.empty(max(W, 1), CALL_DTYPE)
-        nh, nc = _U64(), _U64()
+        ot = np.empty(max(W, 1), OTU_DTYPE)
+        nh, nc, no = _U64(), _U64(), _U64()
+        if otus:
+            want |= WANT_OTU
         buf = ctypes.create_string_buffer(bytes(seq), max(len(seq), 1))
         check(lib().kgx_svc_call(self.handle, ctypes.byref(p), buf, len(seq), want, hits.ctypes.data, W,
-                                 ctypes.byref(nh), calls.ctypes.data, W, ctypes.byref(nc)), "kgx_svc_call")
+                                 ctypes.byref(nh), calls.ctypes.data, W, ctypes.byref(nc), ot.ctypes.data, W,
+                                 ctypes.byref(no)), "kgx_svc_call")
+        if otus:
+            return hits[:nh.value].copy(), calls[:nc.value].copy(), ot[:no.value].copy()
         return hits[:nh.value].copy(), calls[:nc.value].copy()
 
     def svc_config(self, slots: int = 32, idle_us: int = 1000, life_us: int = 4000) -> None:

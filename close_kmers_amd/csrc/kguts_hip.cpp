@@ -393,20 +393,23 @@ void KmerGuts::process_aa_seq(const std::string &id, const std::string &seq,
                               std::shared_ptr<KmerOtuStats> otu_stats)
 {
     const uint32_t want = (hit_cb ? KGX_WANT_HITS : 0u) | (calls ? KGX_WANT_CALLS : 0u) | (otu_stats ? KGX_WANT_OTU : 0u);
-    if (coalesce && service && want && !(want & KGX_WANT_OTU)) {
+    if (coalesce && service && want) {
         /* the image's resident call service: no launch on this call's path
          * (KGX_EBUSY: not a call it serves, or every slot taken -> below) */
         thread_local std::vector<kgx_hit> hbuf;
         thread_local std::vector<kgx_call> cbuf;
+        thread_local std::vector<kgx_otu> obuf;
         const uint64_t W = seq.size() >= 9 ? seq.size() - 8 : 0;
         if (hbuf.size() < W)
             hbuf.resize(W);
         if (cbuf.size() < W)
             cbuf.resize(W);
+        if (otu_stats && obuf.size() < W)
+            obuf.resize(W);
         const kgx_params p{min_hits, max_gap, order_constraint, min_weighted_hits};
-        uint64_t nh = 0, nc = 0;
+        uint64_t nh = 0, nc = 0, no = 0;
         const int rc = kgx_svc_call(image_->handle(), &p, seq.data(), seq.size(), want, hbuf.data(), hbuf.size(), &nh,
-                                    cbuf.data(), cbuf.size(), &nc);
+                                    cbuf.data(), cbuf.size(), &nc, obuf.data(), obuf.size(), &no);
         if (rc == KGX_OK) {
             /* replay on the calling thread, in position order (kguts.cc:814-815) */
             if (hit_cb)
@@ -426,6 +429,11 @@ void KmerGuts::process_aa_seq(const std::string &id, const std::string &seq,
                     const kgx_call &c = cbuf[i];
                     calls->push_back(KmerCall(c.start, c.end, c.count, c.function_index, c.weighted_hits));
                 }
+            if (otu_stats) {
+                for (uint64_t i = 0; i < no; i++)
+                    otu_stats->otu_map[obuf[i].otu_index] += obuf[i].count;
+                otu_stats->finalize(); /* kguts.cc:906-907 */
+            }
             return;
         }
         if (rc != KGX_EBUSY)

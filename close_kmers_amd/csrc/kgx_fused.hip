@@ -28,6 +28,7 @@
  */
 #include "kgx_device.h"
 #include "kgx_internal.h"
+#include "kgx_lstd.h"
 
 namespace kgx {
 
@@ -42,7 +43,8 @@ struct FusedArgs {
     kgx_params prm;
     kgx_hit *hits;    /* mapped: sequence s's hits from hits[wbase[s]] */
     kgx_call *calls;  /* mapped: sequence s's calls from calls[wbase[s]] */
-    uint32_t *counts; /* mapped: hit count of s at [s], call count at [n + s] */
+    kgx_otu *otus;    /* mapped, want OTU (the call service only): s's OTU pairs from otus[wbase[s]] */
+    uint32_t *counts; /* mapped: hit count of s at [s], call count at [n + s], OTU pairs at [2n + s] */
     uint32_t *done;   /* mapped: done[s] = token once s's results are visible */
     uint32_t token;
     uint64_t *dbg; /* mapped, or NULL: wall-clock stamps of workgroup 0's phases */
@@ -112,6 +114,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     __shared__ uint4 hrec[256 * FJ];
     __shared__ uint32_t hpos[256 * FJ];
     __shared__ uint32_t wave_cnt[4];
+    __shared__ uint8_t oflag[256 * FJ]; /* want OTU: hit i is a counted member of an emitted call */
+    __shared__ uint32_t n_otu;
     typedef HitFields<true> HF;
 
     const uint32_t t = threadIdx.x, lane = lane_id(), wave = t >> 6;
@@ -236,6 +240,12 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     if (dbg)
         a.dbg[3] = wall_clock64();
 
+    const bool want_otu = (a.want & KGX_WANT_OTU) != 0;
+    if (want_otu) {
+        for (uint32_t i = t; i < nh; i += 256)
+            oflag[i] = 0;
+        __syncthreads();
+    }
     /* 4a. kgx_hit records into the caller's mapped region (kguts.h:228-233) */
     if (a.want & KGX_WANT_HITS)
         for (uint32_t i = t; i < nh; i += 256) {
@@ -251,20 +261,28 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     /* 4b. the run scorer, wave 0, 64 hits per step (score_wave_kernel's
      * chunk rules for a single sequence) */
     uint32_t ncalls_out = 0;
-    if ((a.want & KGX_WANT_CALLS) && wave == 0 && nh) {
+    const bool want_calls = (a.want & KGX_WANT_CALLS) != 0;
+    if ((want_calls || want_otu) && wave == 0 && nh) {
         const kgx_params prm = a.prm;
         const uint32_t gap = (uint32_t)prm.max_gap;
         const float min_wh = (float)prm.min_weighted_hits;
         kgx_call *calls = a.calls + wb;
         bool o_valid = false;
         uint32_t o_cur = 0, o_cnt = 0, o_first = 0, o_last = 0, o_ncalls = 0;
+        /* the open sub-run's first and last counted hit (indices), for its OTU flags */
+        uint32_t o_first_idx = 0, o_last_idx = 0;
         float o_wsum = 0.0f;
         uint32_t p_pos = 0, p_fi = 0;
         float p_wt = 0.0f;
         /* flush of the open sub-run (kguts.cc:757-770) */
         auto close_open = [&]() {
             if ((int)o_cnt >= prm.min_hits && o_wsum >= min_wh) {
-                if (lane == 0) {
+                /* OTU tally (kguts.cc:757-770): the run's hits of its function, first to last */
+                if (want_otu)
+                    for (uint32_t i = o_first_idx + lane; i <= o_last_idx; i += 64)
+                        if (HF::fi(hrec[i]) == o_cur)
+                            oflag[i] = 1;
+                if (want_calls && lane == 0) {
                     kgx_call cl;
                     cl.start = o_first;
                     cl.end = o_last + (KMER - 1);
@@ -317,14 +335,18 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 o_wsum = 0.0f + p_wt;
                 o_first = p_pos;
                 o_last = p_pos;
+                o_first_idx = h0 - 1;
+                o_last_idx = h0 - 1;
             }
             /* lanes before the first start continue the open sub-run */
             const uint32_t fs = S ? lowbit(S) : n;
             if (fs > 0) {
                 uint64_t mm = MEMB & bit_range(0, fs);
                 o_cnt += (uint32_t)__popcll(mm);
-                if (mm)
+                if (mm) {
                     o_last = rl32(pos, (uint32_t)hibit(mm));
+                    o_last_idx = h0 + (uint32_t)hibit(mm);
+                }
                 while (mm) {
                     o_wsum = o_wsum + rlf(wt, lowbit(mm));
                     mm &= mm - 1;
@@ -361,7 +383,12 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             }
             const uint64_t EMIT = __ballot(is_start && closed && (int)c_seg >= prm.min_hits && ws >= min_wh);
             const uint32_t idx = o_ncalls + (uint32_t)__popcll(EMIT & bit_range(0, k));
-            if ((EMIT >> k) & 1) {
+            if (want_otu && act && ((MEMB >> k) & 1)) { /* a counted member of a sub-run emitted here */
+                const int st = hibit(S & lanes_le(k));
+                if (st >= 0 && ((EMIT >> st) & 1))
+                    oflag[h0 + k] = 1;
+            }
+            if (want_calls && ((EMIT >> k) & 1)) {
                 kgx_call cl;
                 cl.start = pos;
                 cl.end = last_pos + (KMER - 1);
@@ -379,6 +406,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 o_first = rl32(pos, b);
                 o_last = rl32(last_pos, b);
                 o_ncalls = rl32(idx, b);
+                o_first_idx = h0 + b;
+                o_last_idx = h0 + (uint32_t)rl32((uint32_t)(lm < 0 ? 0 : lm), b);
             }
             p_pos = rl32(pos, n - 1);
             p_fi = rl32(fi, n - 1);
@@ -386,7 +415,97 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
         if (o_valid) /* the final flush (kguts.cc:873-876) */
             close_open();
-        ncalls_out = o_ncalls;
+        ncalls_out = want_calls ? o_ncalls : 0u;
+    }
+    /* 4c. OTU tallies (KmerOtuStats::finalize, kguts.h:196-218), all
+     * threads, in LDS (hpos, hrec and codes are free once the records are
+     * stored and the scorer is done): the flagged hits' OTUs compacted in hit
+     * order (ballots), each value's count and first occurrence by a scan of
+     * the list, the distinct values placed in key order by rank (= the
+     * std::map's order), then the pairs std::sort'ed by count on one thread
+     * (lstd_sort replays libstdc++'s tie order; there are few pairs).  One
+     * thread doing it all (otu_finalize's heap sort) cost ~70 us per call:
+     * every step a dependent LDS access. */
+    if (want_otu) {
+        __shared__ int32_t vlo, vhi;
+        if (t == 0) {
+            vlo = INT32_MAX;
+            vhi = INT32_MIN;
+        }
+        __syncthreads();
+        int32_t *v = reinterpret_cast<int32_t *>(hpos);
+        uint32_t m = 0;
+        for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
+            const uint32_t i = t + 256 * j;
+            const bool f = i < nh && oflag[i];
+            const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+            const uint64_t bm = __ballot(f);
+            if (lane == 0)
+                wave_cnt[wave] = (uint32_t)__popcll(bm);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            for (uint32_t w = 0; w < 4; w++) {
+                before += w < wave ? wave_cnt[w] : 0u;
+                total += wave_cnt[w];
+            }
+            __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
+            if (f) {
+                v[m + before + lanes_below(bm)] = x;
+                atomicMin(&vlo, x);
+                atomicMax(&vhi, x);
+            }
+            m += total;
+            __syncthreads();
+        }
+        /* one OTU among the tallied hits (the usual case): one pair */
+        const bool one = m > 0 && vlo == vhi;
+        kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
+        uint32_t *cnt = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
+        uint8_t *first = codes;
+        for (uint32_t i = t; i < (one ? 0u : m); i += 256) {
+            const int32_t x = v[i];
+            uint32_t c = 0;
+            bool fst = true;
+            for (uint32_t j = 0; j < m; j++) {
+                const bool e = v[j] == x;
+                c += e ? 1u : 0u;
+                fst = fst && !(e && j < i);
+            }
+            cnt[i] = c;
+            first[i] = fst ? 1 : 0;
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < (one ? 0u : m); i += 256) {
+            if (!first[i])
+                continue;
+            const int32_t x = v[i];
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < m; j++)
+                r += (first[j] && v[j] < x) ? 1u : 0u;
+            o[r] = kgx_otu{x, (int32_t)cnt[i]};
+        }
+        if (t == 0) {
+            if (one) {
+                o[0] = kgx_otu{vlo, (int32_t)m};
+                n_otu = 1;
+            } else {
+                uint32_t d = 0;
+                for (uint32_t j = 0; j < m; j++)
+                    d += first[j];
+                n_otu = d;
+            }
+        }
+        __syncthreads();
+        /* std::sort of up to 16 elements is its final insertion sort alone
+         * (lstd_sort, __final_insertion_sort); more distinct OTUs than that
+         * are left to the batch paths (SVC_OTU_UNSERVED: the host turns the
+         * call away), which keeps the introsort's stack out of this kernel */
+        if (t == 0 && n_otu > 1 && n_otu <= 16)
+            lstd_insertion_sort(o, (int64_t)n_otu,
+                                [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; });
+        __syncthreads();
+        for (uint32_t i = t; i < (n_otu <= 16 ? n_otu : 0u); i += 256)
+            a.otus[wb + i] = o[i];
     }
 
     if (dbg)
@@ -396,6 +515,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     if (t == 0) {
         a.counts[s] = nh;
         a.counts[a.n + s] = ncalls_out;
+        if (want_otu)
+            a.counts[2 * a.n + s] = n_otu <= 16 ? n_otu : SVC_OTU_UNSERVED;
     }
     __threadfence_system();
     __syncthreads();
@@ -429,6 +550,7 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
     a.prm = prm;
     a.hits = hits;
     a.calls = calls;
+    a.otus = nullptr;
     a.counts = counts;
     a.done = done;
     a.token = token;
@@ -478,6 +600,7 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  */
 __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbgs,
                                                   const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
+                                                  kgx_otu *otus,
                                                   const uint4 *table, uint64_t num_sigs, uint64_t magic,
                                                   uint64_t life_ticks)
 {
@@ -535,7 +658,8 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         a.prm = h->prm;
         a.hits = hits + (uint64_t)slot * FUSED_MAX_WINDOWS;
         a.calls = calls + (uint64_t)slot * FUSED_MAX_WINDOWS;
-        a.counts = &out[slot].nh;
+        a.otus = otus + (uint64_t)slot * FUSED_MAX_WINDOWS;
+        a.counts = &out[slot].nh; /* nh, nc, no */
         a.done = &out[slot].done;
         a.token = req;
         a.dbg = h->debug ? dbgs[slot].stamp : nullptr;
@@ -550,12 +674,12 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
 }
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
-                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs,
+                      kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
                       uint64_t life_ticks, hipStream_t stream)
 {
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
+    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls, otus,
                        static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
     return hipGetLastError();
 }

@@ -242,11 +242,12 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
 constexpr uint32_t SVC_MAX_RES = FUSED_MAX_WINDOWS + 8;
 constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residues per slot */
 constexpr uint32_t SVC_MAX_SLOTS = 64;
+constexpr uint32_t SVC_OTU_UNSERVED = 0xFFFFFFFFu; /* SvcSlotOut.no: more than 16 distinct OTUs */
 struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the polling wave */
     uint32_t req;   /* request number: the device serves it when it differs from SvcSlotOut.done */
     uint32_t stop;  /* nonzero: the service's workgroups leave */
     uint32_t len;   /* residues */
-    uint32_t want;  /* KGX_WANT_HITS | KGX_WANT_CALLS */
+    uint32_t want;  /* KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU */
     kgx_params prm;
     uint32_t debug; /* nonzero: phase stamps into the slot's SvcSlotDbg */
     uint32_t pad[6];
@@ -256,16 +257,16 @@ struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last req
     uint64_t stamp[8];  /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
-    uint32_t nh, nc; /* hit / call records stored */
-    uint32_t done;   /* = req once the records and counts are visible */
-    uint32_t pad[13];
+    uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */
+    uint32_t done;       /* = req once the records and counts are visible */
+    uint32_t pad[12];
 };
 static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 64,
               "service slot lines");
 /* slots workgroups on stream; each leaves life_ticks after its start (device
  * wall clock, 100 MHz) or on stop */
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
-                      kgx_call *calls, uint32_t slots, const void *packed_table, uint64_t num_sigs,
+                      kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
                       uint64_t life_ticks, hipStream_t stream);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */

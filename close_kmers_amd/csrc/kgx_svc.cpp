@@ -61,6 +61,7 @@ struct SvcState {
     uint8_t *res = nullptr;
     kgx_hit *hits = nullptr;
     kgx_call *calls = nullptr;
+    kgx_otu *otus = nullptr;
     /* their device addresses */
     SvcSlotHdr *d_hdr = nullptr;
     SvcSlotOut *d_out = nullptr;
@@ -68,6 +69,7 @@ struct SvcState {
     uint8_t *d_res = nullptr;
     kgx_hit *d_hits = nullptr;
     kgx_call *d_calls = nullptr;
+    kgx_otu *d_otus = nullptr;
     const void *table = nullptr;
     uint64_t num_sigs = 0;
     std::atomic<uint64_t> free_mask{0};
@@ -127,7 +129,8 @@ int top_up(SvcState *s)
             HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         }
         /* wall clock at 100 MHz: 100 ticks per us */
-        hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->slots, s->table,
+        hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->d_otus, s->slots,
+                                  s->table,
                                   s->num_sigs, s->life_us * 100, s->stream);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
@@ -204,8 +207,9 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     const size_t b_hdr = align64(slots * sizeof(SvcSlotHdr)), b_out = align64(slots * sizeof(SvcSlotOut)),
                  b_dbg = align64(slots * sizeof(SvcSlotDbg)), b_res = align64((size_t)slots * SVC_RES_STRIDE),
                  b_hits = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_hit)),
-                 b_calls = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_call));
-    const size_t total = b_hdr + b_out + b_dbg + b_res + b_hits + b_calls;
+                 b_calls = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_call)),
+                 b_otus = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_otu));
+    const size_t total = b_hdr + b_out + b_dbg + b_res + b_hits + b_calls + b_otus;
     void *h = nullptr, *d = nullptr;
     hipError_t e = hipHostMalloc(&h, total, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess)
@@ -252,6 +256,8 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     s->d_hits = reinterpret_cast<kgx_hit *>(dp + o_res + b_res);
     s->calls = reinterpret_cast<kgx_call *>(hp + o_res + b_res + b_hits);
     s->d_calls = reinterpret_cast<kgx_call *>(dp + o_res + b_res + b_hits);
+    s->otus = reinterpret_cast<kgx_otu *>(hp + o_res + b_res + b_hits + b_calls);
+    s->d_otus = reinterpret_cast<kgx_otu *>(dp + o_res + b_res + b_hits + b_calls);
     s->free_mask.store(slots >= 64 ? ~0ull : ((1ull << slots) - 1), std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> lk(g_live_mu);
@@ -363,9 +369,9 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
 
 int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
                  kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
-                 uint64_t *n_calls)
+                 uint64_t *n_calls, kgx_otu *otus, uint64_t otus_cap, uint64_t *n_otus)
 {
-    if (!img || (len && !seq) || !n_hits || !n_calls)
+    if (!img || (len && !seq) || !n_hits || !n_calls || ((want & KGX_WANT_OTU) && !n_otus))
         return fail(KGX_EINVAL, "null argument");
     kgx_params p;
     if (params)
@@ -373,13 +379,15 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     else
         kgx_params_default(&p);
     /* what fused_small_body serves (the rest takes the batch paths) */
-    if (len > SVC_MAX_RES || want == 0 || (want & ~(KGX_WANT_HITS | KGX_WANT_CALLS)) || p.order_constraint != 0 ||
-        p.min_hits < 1)
+    if (len > SVC_MAX_RES || want == 0 || (want & ~(KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU)) ||
+        p.order_constraint != 0 || p.min_hits < 1)
         return fail(KGX_EBUSY, "call service: not a call it serves (length, want mask or parameters)");
     const uint64_t W = windows_of(len);
-    if (((want & KGX_WANT_HITS) && hits_cap < W) || ((want & KGX_WANT_CALLS) && calls_cap < W))
+    if (((want & KGX_WANT_HITS) && hits_cap < W) || ((want & KGX_WANT_CALLS) && calls_cap < W) ||
+        ((want & KGX_WANT_OTU) && otus_cap < W))
         return fail(KGX_EINVAL, "call service: result capacity below the sequence's window count");
-    if ((want & KGX_WANT_HITS && W && !hits) || (want & KGX_WANT_CALLS && W && !calls))
+    if ((want & KGX_WANT_HITS && W && !hits) || (want & KGX_WANT_CALLS && W && !calls) ||
+        (want & KGX_WANT_OTU && W && !otus))
         return fail(KGX_EINVAL, "null result buffer");
     SvcState *s = nullptr;
     int rc = get(img, &s);
@@ -469,8 +477,13 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         s->phase_ns[5] += (st[6] - st[3]) * 10; /* compaction end -> thread 0's record stores issued */
     }
     const SvcSlotOut &o = s->out[slot];
-    const uint32_t nh = o.nh, nc = o.nc;
-    if (nh > W || nc > W) {
+    const uint32_t nh = o.nh, nc = o.nc, no = (want & KGX_WANT_OTU) ? o.no : 0u;
+    if (no == SVC_OTU_UNSERVED) {
+        give_slot(s, slot);
+        s->n_busy++;
+        return fail(KGX_EBUSY, "call service: more than 16 distinct OTUs (take a batch path)");
+    }
+    if (nh > W || nc > W || no > W) {
         give_slot(s, slot);
         return fail(KGX_EDEVICE, "call service: more records than windows");
     }
@@ -480,6 +493,13 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         std::memcpy(hits, s->hits + (size_t)slot * FUSED_MAX_WINDOWS, *n_hits * sizeof(kgx_hit));
     if (*n_calls)
         std::memcpy(calls, s->calls + (size_t)slot * FUSED_MAX_WINDOWS, *n_calls * sizeof(kgx_call));
+    if (want & KGX_WANT_OTU) {
+        *n_otus = no;
+        if (no)
+            std::memcpy(otus, s->otus + (size_t)slot * FUSED_MAX_WINDOWS, no * sizeof(kgx_otu));
+    } else if (n_otus) {
+        *n_otus = 0;
+    }
     give_slot(s, slot);
     s->n_calls++;
     return KGX_OK;

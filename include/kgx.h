@@ -427,16 +427,18 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
  * until the device has stored its records.  Thread-safe; started on the first
  * call; instances of the workgroups last life_us each and the host keeps one
  * queued behind the running one while calls arrive, so the service leaves the
- * GPU within 2 x life_us of the last call (restarted on demand).  Serves PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS,
- * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues;
+ * GPU within 2 x life_us of the last call (restarted on demand).  Serves
+ * PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU,
+ * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues
+ * (and, with OTU stats, at most 16 distinct OTUs among a sequence's calls);
  * anything else, or every slot busy, returns KGX_EBUSY and the caller takes a
  * batch path (kgx_process_batch*).  Results as kgx_process_batch gives them
- * for a batch of this one sequence (kgx_hit.seq = 0, hits in position order);
- * hits_cap / calls_cap must be at least the sequence's window count
- * (len - 8). */
+ * for a batch of this one sequence (kgx_hit.seq = 0, hits in position order;
+ * OTU pairs in otus_by_count order); hits_cap / calls_cap / otus_cap must be
+ * at least the sequence's window count (len - 8) for what want asks. */
 int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint64_t len, uint32_t want,
                  kgx_hit *hits, uint64_t hits_cap, uint64_t *n_hits, kgx_call *calls, uint64_t calls_cap,
-                 uint64_t *n_calls);
+                 uint64_t *n_calls, kgx_otu *otus, uint64_t otus_cap, uint64_t *n_otus);
 /* slots (1..64, default 32) and life_us (default 1000: an instance's stay
  * before the next one, already enqueued, takes over; bounds how long the
  * service holds its hardware queue); stops a running service.  idle_us is

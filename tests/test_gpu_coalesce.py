@@ -68,10 +68,10 @@ def _parse(path, n):
                                                             (16, 0, 1, 1, 0), (16, 1, 0, 1, 0), (16, 1, 0, 0, 0),
                                                             (32, 1, 0, 1, 0), (16, 1, 0, 1, 3), (1, 0, 0, 1, 0)])
 def test_threads_calling_process_aa_seq_match_oracle(gpu, oracle_lib, tmp_path, threads, coalesce, otu, svc, slots):
-    """otu 0: hit callbacks + calls only (the lookup handler's outputs): with
-    the resident call service (svc 1, csrc/kgx_svc.cpp) calls under
-    order_constraint 0 of at most 2,056 residues run there, the rest through
-    the coalescer; svc 0 (KGX_SVC=0): the coalescer's one-launch path
+    """otu 1: hit callbacks, calls and OTU stats (the query handler's
+    outputs), otu 0: hits + calls (the lookup handler's): with the resident
+    call service (svc 1, csrc/kgx_svc.cpp) calls under order_constraint 0 of
+    at most 2,056 residues run there, the rest through the coalescer; svc 0 (KGX_SVC=0): the coalescer's one-launch path
     (kgx_fused.hip).  slots 3: most calls find every slot taken (KGX_EBUSY)
     and take the coalescer."""
     spec, table = synthetic_table(30000)
@@ -88,12 +88,12 @@ def test_threads_calling_process_aa_seq_match_oracle(gpu, oracle_lib, tmp_path, 
     assert r.returncode == 0, r.stderr
     stats = json.loads(r.stdout)
     assert stats["calls"] + stats["svc_calls"] == (n if coalesce else 0)
-    if coalesce and svc and not otu:
+    if coalesce and svc:
         # thread parameter sets 0 and 1, ordinary lengths (3 slots: some)
         assert stats["svc_calls"] > (n // 2 if not slots else 0)
     else:
         assert stats["svc_calls"] == 0
-    if coalesce and threads >= 5 and not (svc and not otu and not slots):
+    if coalesce and threads >= 5 and not (svc and not slots):
         assert stats["passes"] < n  # calls did share passes
     got = _parse(outp, n)
     # every sequence against the oracle under its thread's parameter set

@@ -76,6 +76,73 @@ def test_svc_single_thread_matches_oracle(svc_image, oracle_lib):
     assert img.svc_stat("calls") >= len(seqs)
 
 
+def test_svc_otu_tallies_match_oracle(gpu, oracle_lib):
+    """want OTU: the OTU pairs of each call (KmerOtuStats after finalize(),
+    kguts.h:196-218) -- the counted hits of every emitted call, std::sort'ed
+    by count with the reference's tie order -- against the oracle, with hits
+    and calls, and alone; sequences with runs that span 64-hit chunks, pair
+    switches and carries (min_hits 3 / max_gap 50 among the parameter sets)."""
+    import oracle
+    spec = synth.ImageSpec(30000)
+    k, f, o, av, w = spec.unique_entries()
+    o = (k % np.uint64(6)).astype(np.int32) - 1  # OTUs -1..4: many equal counts, so tie order shows
+    table = oracle.build_table(spec.num_sigs, k, f, o, av, w)
+    seqs = _seqs(spec, 400, 53)
+    n_otu = 0
+    img = abi.Image.from_table(table, device=0)
+    for k, s in enumerate(seqs):
+        p = PARAMS[k % len(PARAMS)]
+        want = oracle_lib.process_batch(table, np.frombuffer(s, np.uint8).copy(), np.array([0, len(s)], np.uint64),
+                                        params=_tuple(p), want=7)
+        for w in (abi.WANT_HITS | abi.WANT_CALLS, 0):
+            if w == 0 and len(s) < 9:
+                continue
+            got = img.svc_call(s, p, want=w, otus=True)
+            if w:
+                _check(oracle_lib, table, s, _tuple(p), got[0], got[1], k)
+            wo = want.otus.reshape(-1, 2)
+            assert np.array_equal(got[2]["otu_index"], wo[:, 0]), (k, w)
+            assert np.array_equal(got[2]["count"], wo[:, 1]), (k, w)
+        n_otu += len(want.otus.reshape(-1, 2))
+    img.close()
+    assert n_otu > 500
+
+
+def test_svc_otu_over_16_turned_away(gpu, oracle_lib):
+    """The service sorts at most 16 distinct OTUs per sequence (std::sort of
+    that many is its final insertion sort alone); a sequence whose calls
+    name more is turned away (KGX_EBUSY) for a batch path, one with 16 or
+    fewer is served and matches the oracle.  OTUs k % 97, fragments of
+    12..2,056 residues put the count either side of the cut."""
+    import oracle
+    spec = synth.ImageSpec(30000)
+    k, f, o, av, w = spec.unique_entries()
+    o = (k % np.uint64(97)).astype(np.int32)
+    table = oracle.build_table(spec.num_sigs, k, f, o, av, w)
+    res, off = synth.make_queries(spec, 64, x_permille=0, q0=5)
+    base = b"".join(bytes(res[int(off[i]):int(off[i + 1])]) for i in range(64))
+    rng = np.random.default_rng(3)
+    served = away = 0
+    with abi.Image.from_table(table, device=0) as img:
+        for L in list(rng.integers(12, 40, 40)) + [300, 2056]:
+            a = int(rng.integers(0, len(base) - L))
+            s = base[a:a + int(L)]
+            want = oracle_lib.process_batch(table, np.frombuffer(s, np.uint8).copy(),
+                                            np.array([0, len(s)], np.uint64), params=_tuple(None), want=7)
+            wo = want.otus.reshape(-1, 2)
+            if len(wo) > 16:
+                with pytest.raises(abi.KgxError) as e:
+                    img.svc_call(s, None, want=3, otus=True)
+                assert e.value.code == abi.KGX_EBUSY
+                away += 1
+            else:
+                got = img.svc_call(s, None, want=3, otus=True)
+                _check(oracle_lib, table, s, _tuple(None), got[0], got[1], L)
+                assert np.array_equal(got[2]["otu_index"], wo[:, 0]) and np.array_equal(got[2]["count"], wo[:, 1])
+                served += len(wo) > 0
+    assert served >= 5 and away >= 2
+
+
 def test_svc_want_masks(svc_image, oracle_lib):
     spec, table, img = svc_image
     def n_calls(x):
@@ -93,7 +160,7 @@ def test_svc_want_masks(svc_image, oracle_lib):
 def test_svc_turns_away_what_it_does_not_serve(svc_image):
     spec, table, img = svc_image
     for seq, p, want in ((b"A" * 2057, None, 3), (b"ACDEFGHIKLMN", {"order_constraint": "1"}, 3),
-                         (b"ACDEFGHIKLMN", {"min_hits": "0"}, 3), (b"ACDEFGHIKLMN", None, abi.WANT_OTU),
+                         (b"ACDEFGHIKLMN", {"min_hits": "0"}, 3), (b"ACDEFGHIKLMN", None, abi.WANT_BEST),
                          (b"ACDEFGHIKLMN", None, 0)):
         with pytest.raises(abi.KgxError) as e:
             img.svc_call(seq, p, want)

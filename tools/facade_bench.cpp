@@ -197,6 +197,7 @@ int main(int argc, char **argv)
      * time a pool of 16 threads at ~1M calls/s) */
     const size_t R = std::getenv("KGX_FACADE_REPS") ? std::strtoull(std::getenv("KGX_FACADE_REPS"), nullptr, 10) : 10;
     static const char *mode_name[3] = {"per_call_T", "coalesced_T", "service_T"};
+    const bool with_otu = std::getenv("KGX_FACADE_OTU") && std::atoi(std::getenv("KGX_FACADE_OTU")) != 0;
     for (int co : modes)
         for (int T : threads) {
             if (only)
@@ -219,8 +220,10 @@ int main(int argc, char **argv)
                     auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
                     uint64_t h = 0;
                     const auto q0 = clk::now();
+                    /* KGX_FACADE_OTU=1: OTU stats wanted too (query_request.cc's per-sequence shape) */
+                    auto os = with_otu ? std::make_shared<kgx::KmerOtuStats>() : nullptr;
                     kgs[t]->process_aa_seq("q", seqs[i], cv, [&h](kgx::KmerGuts::hit_in_sequence_t) { h++; },
-                                           nullptr);
+                                           os);
                     if (count) {
                         th_lat[t].push_back(std::chrono::duration<double, std::micro>(clk::now() - q0).count());
                         th_hits[t] += h;
