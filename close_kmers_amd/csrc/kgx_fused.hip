@@ -423,11 +423,12 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
      * order (ballots), each value's count and first occurrence by a scan of
      * the list, the distinct values placed in key order by rank (= the
      * std::map's order), then the pairs std::sort'ed by count on one thread
-     * (lstd_sort replays libstdc++'s tie order; there are few pairs).  One
+     * (lstd_sort_on replays libstdc++'s tie order; there are few pairs).  One
      * thread doing it all (otu_finalize's heap sort) cost ~70 us per call:
      * every step a dependent LDS access. */
     if (want_otu) {
         __shared__ int32_t vlo, vhi;
+        __shared__ LstdPart ostack[64];
         if (t == 0) {
             vlo = INT32_MAX;
             vhi = INT32_MIN;
@@ -496,15 +497,13 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             }
         }
         __syncthreads();
-        /* std::sort of up to 16 elements is its final insertion sort alone
-         * (lstd_sort, __final_insertion_sort); more distinct OTUs than that
-         * are left to the batch paths (SVC_OTU_UNSERVED: the host turns the
-         * call away), which keeps the introsort's stack out of this kernel */
-        if (t == 0 && n_otu > 1 && n_otu <= 16)
-            lstd_insertion_sort(o, (int64_t)n_otu,
-                                [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; });
+        /* std::sort by count (lstd_sort_on: libstdc++'s introsort, its
+         * partition stack in LDS) */
+        if (t == 0 && n_otu > 1)
+            lstd_sort_on(o, (int64_t)n_otu, [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; },
+                         ostack);
         __syncthreads();
-        for (uint32_t i = t; i < (n_otu <= 16 ? n_otu : 0u); i += 256)
+        for (uint32_t i = t; i < n_otu; i += 256)
             a.otus[wb + i] = o[i];
     }
 
@@ -516,7 +515,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         a.counts[s] = nh;
         a.counts[a.n + s] = ncalls_out;
         if (want_otu)
-            a.counts[2 * a.n + s] = n_otu <= 16 ? n_otu : SVC_OTU_UNSERVED;
+            a.counts[2 * a.n + s] = n_otu;
     }
     __threadfence_system();
     __syncthreads();

@@ -242,7 +242,6 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
 constexpr uint32_t SVC_MAX_RES = FUSED_MAX_WINDOWS + 8;
 constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residues per slot */
 constexpr uint32_t SVC_MAX_SLOTS = 64;
-constexpr uint32_t SVC_OTU_UNSERVED = 0xFFFFFFFFu; /* SvcSlotOut.no: more than 16 distinct OTUs */
 struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the polling wave */
     uint32_t req;   /* request number: the device serves it when it differs from SvcSlotOut.done */
     uint32_t stop;  /* nonzero: the service's workgroups leave */

@@ -121,15 +121,21 @@ template <class T, class C> __host__ __device__ void lstd_insertion_sort(T *a, i
     }
 }
 
-template <class T, class C> __host__ __device__ void lstd_sort(T *a, int64_t n, C comp)
+/* one pending __introsort_loop range */
+struct LstdPart {
+    int64_t first, last;
+    int depth;
+};
+
+/* std::sort with the partition stack supplied by the caller (64 entries; the
+ * depth limit 2 log2 n bounds the pushes): a device caller passes LDS, so a
+ * persistent kernel holds no scratch for it */
+template <class T, class C> __host__ __device__ void lstd_sort_on(T *a, int64_t n, C comp, LstdPart *stack)
 {
     if (n <= 1)
         return;
     constexpr int64_t THRESH = 16;
-    struct Part {
-        int64_t first, last;
-        int depth;
-    } stack[64];
+    using Part = LstdPart;
     int sp = 0;
     stack[sp++] = Part{0, n, 2 * (63 - __builtin_clzll((unsigned long long)n))};
     while (sp) {
@@ -182,6 +188,12 @@ template <class T, class C> __host__ __device__ void lstd_sort(T *a, int64_t n, 
     } else {
         lstd_insertion_sort(a, n, comp);
     }
+}
+
+template <class T, class C> __host__ __device__ void lstd_sort(T *a, int64_t n, C comp)
+{
+    LstdPart stack[64];
+    lstd_sort_on(a, n, comp, stack);
 }
 
 /* find_best_call's decision over calls c[0, n); m = workspace of n calls.

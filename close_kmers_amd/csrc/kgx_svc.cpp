@@ -478,11 +478,6 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     }
     const SvcSlotOut &o = s->out[slot];
     const uint32_t nh = o.nh, nc = o.nc, no = (want & KGX_WANT_OTU) ? o.no : 0u;
-    if (no == SVC_OTU_UNSERVED) {
-        give_slot(s, slot);
-        s->n_busy++;
-        return fail(KGX_EBUSY, "call service: more than 16 distinct OTUs (take a batch path)");
-    }
     if (nh > W || nc > W || no > W) {
         give_slot(s, slot);
         return fail(KGX_EDEVICE, "call service: more records than windows");

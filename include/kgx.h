@@ -429,8 +429,7 @@ int kgx_compact_expand(const kgx_compact_result *r, const char *residues, const 
  * queued behind the running one while calls arrive, so the service leaves the
  * GPU within 2 x life_us of the last call (restarted on demand).  Serves
  * PACKED16 images, want within KGX_WANT_HITS | KGX_WANT_CALLS | KGX_WANT_OTU,
- * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues
- * (and, with OTU stats, at most 16 distinct OTUs among a sequence's calls);
+ * order_constraint 0, min_hits >= 1, sequences of at most 2,056 residues;
  * anything else, or every slot busy, returns KGX_EBUSY and the caller takes a
  * batch path (kgx_process_batch*).  Results as kgx_process_batch gives them
  * for a batch of this one sequence (kgx_hit.seq = 0, hits in position order;

@@ -108,12 +108,11 @@ def test_svc_otu_tallies_match_oracle(gpu, oracle_lib):
     assert n_otu > 500
 
 
-def test_svc_otu_over_16_turned_away(gpu, oracle_lib):
-    """The service sorts at most 16 distinct OTUs per sequence (std::sort of
-    that many is its final insertion sort alone); a sequence whose calls
-    name more is turned away (KGX_EBUSY) for a batch path, one with 16 or
-    fewer is served and matches the oracle.  OTUs k % 97, fragments of
-    12..2,056 residues put the count either side of the cut."""
+def test_svc_otu_many_distinct_match_oracle(gpu, oracle_lib):
+    """Many distinct OTUs per sequence (OTUs k % 97): fragments of 12..40
+    residues name up to 16 (where std::sort is its final insertion sort
+    alone), 300 and 2,056 residues name 50..97 (the introsort proper, its
+    partition stack in LDS); every pair list against the oracle."""
     import oracle
     spec = synth.ImageSpec(30000)
     k, f, o, av, w = spec.unique_entries()
@@ -122,25 +121,22 @@ def test_svc_otu_over_16_turned_away(gpu, oracle_lib):
     res, off = synth.make_queries(spec, 64, x_permille=0, q0=5)
     base = b"".join(bytes(res[int(off[i]):int(off[i + 1])]) for i in range(64))
     rng = np.random.default_rng(3)
-    served = away = 0
+    few = many = 0
     with abi.Image.from_table(table, device=0) as img:
-        for L in list(rng.integers(12, 40, 40)) + [300, 2056]:
+        for L in list(rng.integers(12, 40, 40)) + [300, 300, 1000, 2056, 2056]:
             a = int(rng.integers(0, len(base) - L))
             s = base[a:a + int(L)]
-            want = oracle_lib.process_batch(table, np.frombuffer(s, np.uint8).copy(),
-                                            np.array([0, len(s)], np.uint64), params=_tuple(None), want=7)
-            wo = want.otus.reshape(-1, 2)
-            if len(wo) > 16:
-                with pytest.raises(abi.KgxError) as e:
-                    img.svc_call(s, None, want=3, otus=True)
-                assert e.value.code == abi.KGX_EBUSY
-                away += 1
-            else:
-                got = img.svc_call(s, None, want=3, otus=True)
-                _check(oracle_lib, table, s, _tuple(None), got[0], got[1], L)
-                assert np.array_equal(got[2]["otu_index"], wo[:, 0]) and np.array_equal(got[2]["count"], wo[:, 1])
-                served += len(wo) > 0
-    assert served >= 5 and away >= 2
+            for p in (None, {"min_hits": "1", "max_gap": "0"}):
+                want = oracle_lib.process_batch(table, np.frombuffer(s, np.uint8).copy(),
+                                                np.array([0, len(s)], np.uint64), params=_tuple(p), want=7)
+                wo = want.otus.reshape(-1, 2)
+                got = img.svc_call(s, p, want=3, otus=True)
+                _check(oracle_lib, table, s, _tuple(p), got[0], got[1], L)
+                assert np.array_equal(got[2]["otu_index"], wo[:, 0]), L
+                assert np.array_equal(got[2]["count"], wo[:, 1]), L
+                few += 0 < len(wo) <= 16
+                many += len(wo) > 16
+    assert few >= 5 and many >= 4
 
 
 def test_svc_want_masks(svc_image, oracle_lib):
