@@ -427,12 +427,10 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
      * thread doing it all (otu_finalize's heap sort) cost ~70 us per call:
      * every step a dependent LDS access. */
     if (want_otu) {
-        __shared__ int32_t vlo, vhi;
+        __shared__ uint32_t multi;
         __shared__ LstdPart ostack[64];
-        if (t == 0) {
-            vlo = INT32_MAX;
-            vhi = INT32_MIN;
-        }
+        if (t == 0)
+            multi = 0;
         __syncthreads();
         int32_t *v = reinterpret_cast<int32_t *>(hpos);
         uint32_t m = 0;
@@ -450,16 +448,20 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 total += wave_cnt[w];
             }
             __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
-            if (f) {
+            if (f)
                 v[m + before + lanes_below(bm)] = x;
-                atomicMin(&vlo, x);
-                atomicMax(&vhi, x);
-            }
             m += total;
             __syncthreads();
         }
-        /* one OTU among the tallied hits (the usual case): one pair */
-        const bool one = m > 0 && vlo == vhi;
+        /* one OTU among the tallied hits (the usual case): one pair.  Every
+         * thread compares its entries with the first (plain stores of 1, no
+         * atomics: same-address LDS atomics from every flagged lane serialize) */
+        const int32_t v0 = m ? v[0] : 0;
+        for (uint32_t i = t; i < m; i += 256)
+            if (v[i] != v0)
+                multi = 1;
+        __syncthreads();
+        const bool one = m > 0 && !multi;
         kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
         uint32_t *cnt = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
         uint8_t *first = codes;
@@ -487,7 +489,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
         if (t == 0) {
             if (one) {
-                o[0] = kgx_otu{vlo, (int32_t)m};
+                o[0] = kgx_otu{v0, (int32_t)m};
                 n_otu = 1;
             } else {
                 uint32_t d = 0;
