@@ -469,6 +469,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             const int32_t x = v[i];
             uint32_t c = 0;
             bool fst = true;
+#pragma unroll 8
             for (uint32_t j = 0; j < m; j++) {
                 const bool e = v[j] == x;
                 c += e ? 1u : 0u;
@@ -483,6 +484,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 continue;
             const int32_t x = v[i];
             uint32_t r = 0;
+#pragma unroll 8
             for (uint32_t j = 0; j < m; j++)
                 r += (first[j] && v[j] < x) ? 1u : 0u;
             o[r] = kgx_otu{x, (int32_t)cnt[i]};
