@@ -109,11 +109,132 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
 
 WANT_NAMES = {3: "hits + calls", 7: "hits + calls + OTU", 11: "hits + calls + best call",
               15: "hits + calls + OTU + best call"}
+# what each want mask is in the reference's handlers
+WANT_OUTPUTS = {3: "hits + calls (lookup_request without find_best_match)",
+                7: "hits + calls + OTU (add_request / query_request)",
+                11: "hits + calls + device find_best_call per sequence (lookup_request find_best_match, "
+                    "lookup_request.cc:166-210)",
+                15: "hits + calls + OTU + device find_best_call"}
+
+
+def canary_check(abi, synth, d, dev):
+    """Every rank: the canary pass (close_kmers_amd/canary.py) on its own
+    device, digested; the digests are gathered and compared with the CPU
+    oracle's committed digest.  Returns (per-rank canary records, ok).  With
+    more than one rank and no KGX_BENCH_DEVICE override, the ranks' devices
+    must differ (one rank per GPU)."""
+    from close_kmers_amd import canary
+    t0 = time.time()
+    mine = canary.run_on_device(abi, synth, dev)
+    mine["rank"] = d.rank
+    mine["seconds"] = round(time.time() - t0, 2)
+    want = canary.expected()["digest"]
+    mine["ok"] = mine["digest"] == want
+    recs = d.gather_objects(mine)
+    ok = all(r["ok"] for r in recs)
+    devs = [r["device"] for r in recs]
+    if d.world > 1 and "KGX_BENCH_DEVICE" not in os.environ and len(set(devs)) != len(devs):
+        log(f"[bench] canary: ranks share a device: {devs}")
+        ok = False
+    if d.rank == 0:
+        log(f"[bench] canary ({canary.CANARY_SEQ} x {canary.CANARY_LEN} aa vs {canary.CANARY_KEYS:,}-entry image, "
+            f"want {canary.CANARY_WANT}): " + ", ".join(
+                f"rank {r['rank']} dev {r['device']} {'ok' if r['ok'] else 'MISMATCH ' + r['digest'][:16]}"
+                for r in recs))
+    return recs, ok
 
 
 def spec_queries(spec, n, length, x_permille):
     from close_kmers_amd import synth
     return synth.make_queries(spec, n, length=length, x_permille=x_permille, q0=0)
+
+
+def pool_main(args) -> int:
+    """--pool-devices N: the in-process multi-device serving shape (the
+    reference's pool: one worker per execution resource over one image,
+    threadpool.cc:18-44).  One process holds N replicas of the image (built on
+    the first device, copied device to device by kgx_image_replicate onto
+    device i % visible), runs BASELINE.json configs[4]'s batch (C5: 1M x
+    300 aa, host buffers) through kgx_pool (residue-balanced shards, one
+    context per replica, results concatenated in input order), checks the
+    result byte for byte against one context's pass over the whole batch,
+    and times the pool (compact results, as bench_pool).  Prints its own JSON
+    line; exits non-zero on a mismatch."""
+    from close_kmers_amd import abi, synth
+    L = abi.lib()
+    n_dev = abi.device_count()
+    if n_dev < 1:
+        raise SystemExit("no gfx950 device visible")
+    N = args.pool_devices
+    devices = [i % n_dev for i in range(N)]
+    n_keys = int(args.n_keys)
+    spec = synth.ImageSpec(n_keys, args.num_sigs or None)
+    t0 = time.time()
+    img0, _ = abi.Image.synthetic_distinct(spec.n_keys, n_keys, spec.num_sigs, device=devices[0])
+    t_build = time.time() - t0
+    t0 = time.time()
+    images = [img0] + [img0.replicate(dv) for dv in devices[1:]]
+    t_rep = time.time() - t0
+    log(f"[pool] {n_keys:,}-key image on device {devices[0]} in {t_build:.1f}s, {N - 1} replica(s) on "
+        f"{devices[1:]} in {t_rep:.1f}s")
+    n, Ls = args.strong_seq, args.length
+    ctx0 = abi.Context(img0)
+    d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+    abi.check(L.kgx_device_alloc(devices[0], n * Ls, ctypes.byref(d_res)), "alloc")
+    abi.check(L.kgx_device_alloc(devices[0], (n + 1) * 8, ctypes.byref(d_off)), "alloc")
+    abi.check(L.kgx_synth_queries(ctx0.handle, spec.n_keys, n, Ls, args.x_permille, 0, d_res, d_off), "queries")
+    ctx0.synchronize()
+    res = np.empty(n * Ls, np.uint8)
+    off = np.empty(n + 1, np.uint64)
+    abi.check(L.kgx_memcpy_d2h(res.ctypes.data, d_res, res.nbytes), "d2h")
+    abi.check(L.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
+    L.kgx_device_free(d_res)
+    L.kgx_device_free(d_off)
+    params = abi.default_params()
+    want = args.want
+    t0 = time.time()
+    one = ctx0.process_batch(res, off, params, want=want)
+    t_one = time.time() - t0
+    ctx0.close()
+    checks = {}
+    with abi.Pool(images, n_ctx=N) as pool:
+        got = pool.process_batch(res, off, params, want=want, copy=False)
+        checks["hit_offsets"] = bool(np.array_equal(got.hit_offsets, one.hit_offsets))
+        checks["hits"] = bool(got.hits.tobytes() == one.hits.tobytes())
+        checks["call_offsets"] = bool(np.array_equal(got.call_offsets, one.call_offsets))
+        checks["calls"] = bool(got.calls.tobytes() == one.calls.tobytes())
+        if one.best is not None:
+            checks["best"] = bool(got.best is not None and got.best.tobytes() == one.best.tobytes())
+        del got
+        ts = []
+        r = pool.process_batch_compact(res, off, params, want=want)  # warm
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r = pool.process_batch_compact(res, off, params, want=want)
+            ts.append(time.perf_counter() - t0)
+        checks["compact_hit_offsets"] = bool(np.array_equal(r.result.hit_offsets, one.hit_offsets))
+    t = float(np.median(ts))
+    ok = all(checks.values())
+    line = {
+        "metric": "C5 protein residues/s through kgx_pool, one process over N image replicas",
+        "value": n * Ls / t, "unit": "residues/s", "ms_per_batch": t * 1e3, "n_devices": N, "devices": devices,
+        "distinct_devices": len(set(devices)), "higher_is_better": True, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": f"C5: {n} x {Ls}-aa synthetic proteins, one host batch, vs {n_keys:,}-key image "
+                               f"replicated on {N} device slot(s)", "want": want,
+                   "outputs": WANT_OUTPUTS.get(want, f"want={want}"), "result": "compact (records + mask)"},
+        "match_single_context": ok, "checks": checks, "hits": int(one.hit_offsets[-1]),
+        "calls": int(one.call_offsets[-1]), "single_context_s": t_one,
+        "image_build_s": t_build, "replicate_s": t_rep,
+        "note": "host buffers in and out (PCIe-inclusive); on one GPU the replicas share device 0, so this "
+                "exercises the multi-device code path, not N devices' bandwidth",
+    }
+    print(json.dumps(line), flush=True)
+    for im in images:
+        im.close()
+    if not ok:
+        log(f"[pool] MISMATCH against the single-context pass: {checks}")
+        return 1
+    return 0
 
 
 def main():
@@ -144,7 +265,12 @@ def main():
                     help="presence filter of 2^N bits (0 = none), kgx_image_set_filter")
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
-    ap.add_argument("--want", type=int, default=3, help="KGX_WANT_* mask (3 = hits+calls)")
+    ap.add_argument("--want", type=int, default=11,
+                    help="KGX_WANT_* mask (11 = hits + calls + device best call, lookup_request find_best_match)")
+    ap.add_argument("--no-canary", action="store_true", help="skip the per-device canary self-check")
+    ap.add_argument("--pool-devices", type=int, default=0,
+                    help="N > 0: one process, the C5 batch through kgx_pool over N image replicas (devices "
+                         "i %% visible), checked byte for byte against one context; prints its own line")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="LDS KB reserved per probe workgroup (-1 = default)")
     ap.add_argument("--probe-stream", type=int, default=-1,
                     help="1 = the contexts' chained probes on one image stream (-1 = default)")
@@ -156,6 +282,8 @@ def main():
 
     from close_kmers_amd import shard
 
+    if args.pool_devices:
+        sys.exit(pool_main(args))
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ:
@@ -179,6 +307,12 @@ def main():
                          f"({n_dev} gfx950 device(s) visible)")
 
     d = shard.Dist()
+    canary_recs = None
+    if not args.no_canary:
+        canary_recs, canary_ok = canary_check(abi, synth, d, dev)
+        if not canary_ok:
+            d.close()
+            raise SystemExit(f"rank {d.rank}: canary check failed (a device's results differ from the oracle's)")
     n_keys = int(args.n_keys)
     spec = synth.ImageSpec(n_keys, args.num_sigs or None)
 
@@ -329,8 +463,12 @@ def main():
     abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
     abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
     total_hits = int(d.sum(float(hc.sum())))
-    per_rank = d.gather_objects({"rank": d.rank, "device": dev, "ms_per_step": t_wall * 1e3 / args.steps,
-                                 "probe_ms": float(np.mean(probe_ms)), "n_seq": n, "hits": int(hc.sum())})
+    mine = {"rank": d.rank, "device": dev, "ms_per_step": t_wall * 1e3 / args.steps,
+            "probe_ms": float(np.mean(probe_ms)), "n_seq": n, "hits": int(hc.sum())}
+    if canary_recs:
+        c = canary_recs[d.rank]
+        mine["canary"] = {"ok": c["ok"], "digest": c["digest"][:16], "hits": c["hits"], "calls": c["calls"]}
+    per_rank = d.gather_objects(mine)
     log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
         f"(even-q mean {hc[::2].mean():.1f}, odd-q mean {hc[1::2].mean():.2f}); "
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
@@ -443,12 +581,16 @@ def main():
         pbar_source = "measured (CPU baseline leg, this run)" if pbar is not None else None
         probe_s = float(np.mean(probe_ms)) / 1e3
         traffic = None
+        traffic_source = None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
                 if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
                         and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_source = (f"not measured in this run: FETCH_SIZE + WRITE_SIZE per probe launch from "
+                                      f"profiles/{os.path.basename(args.traffic_json)} "
+                                      f"({tj.get('collected', 'an earlier rocprofv3 --pmc run')}), same workload")
                     if pbar is None and tj.get("pbar_measured"):
                         pbar = tj["pbar_measured"]  # the same workload's P measured by an earlier run
                         pbar_source = f"measured earlier on this workload ({os.path.basename(args.traffic_json)})"
@@ -499,8 +641,11 @@ def main():
                 # the score stage alone (HIP events on the context's stream, same
                 # untimed pass as the probe time): what a single-context caller pays
                 "score_stage_ms": float(np.mean(score_ms)) if score_ms else None,
-                "outputs": {3: "hits + calls (lookup_request, find_best_match)",
-                            7: "hits + calls + OTU (add_request)"}.get(want, f"want={want}"),
+                "want": want,
+                "outputs": WANT_OUTPUTS.get(want, f"want={want}"),
+                "canary": ({"ok": all(r["ok"] for r in canary_recs), "digest": canary_recs[0]["digest"][:16],
+                            "check": "every rank's canary digest == the CPU oracle's (tests/golden/canary)"}
+                           if canary_recs else None),
             },
             "roofline": {
                 "bound": "hbm",
@@ -509,6 +654,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel": probe_kernel,
                 "kernel_ms": probe_s * 1e3,
                 "windows_per_launch": windows_per_launch,

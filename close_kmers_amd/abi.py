@@ -65,6 +65,16 @@ class DeviceResult(ctypes.Structure):
 HIT_PLANES, HIT_PACKED16 = 0, 1
 
 
+class RollupResult(ctypes.Structure):
+    _fields_ = [("n_seq", ctypes.c_uint32), ("offsets", ctypes.c_void_p), ("rows", ctypes.c_void_p),
+                ("n_events", ctypes.c_uint64)]
+
+
+# kgx_rollup_row: LookupRequest's sequence_accumulated_score_t with its id
+ROLLUP_DTYPE = np.dtype([("id", "<u4"), ("hit_count", "<u4"), ("hit_total", "<u4"), ("weighted_total", "<f4")])
+ROLLUP_PEG, ROLLUP_FAMILY = 0, 1
+
+
 class HitChunk(ctypes.Structure):
     _fields_ = [("seq_begin", ctypes.c_uint32), ("seq_end", ctypes.c_uint32), ("record_words", ctypes.c_uint32),
                 ("reserved", ctypes.c_uint32), ("hit_begin", ctypes.c_uint64), ("records", ctypes.c_void_p),
@@ -213,6 +223,7 @@ SIGNATURES = {
     "kgx_kmap_num_kmers": (_U64, [_P]),
     "kgx_kmap_num_values": (_U64, [_P]),
     "kgx_kmap_lookup": (_INT, [_P, _P, _U64, _P, _P, _U64]),
+    "kgx_kmap_rollup": (_INT, [_P, _P, _INT, ctypes.POINTER(RollupResult)]),
     "kgx_matrix_create": (_INT, [_P, _PP]),
     "kgx_matrix_destroy": (_INT, [_P]),
     "kgx_matrix_add_hits": (_INT, [_P, _P, _P]),
@@ -685,6 +696,13 @@ class Kmap:
             check(lib().kgx_kmap_lookup(self.handle, k.ctypes.data, len(k), off.ctypes.data,
                                         ids.ctypes.data, len(ids)), "kgx_kmap_lookup")
         return off, ids
+
+    def rollup(self, ctx: "Context", mode: int = ROLLUP_FAMILY) -> tuple[np.ndarray, np.ndarray]:
+        """kgx_kmap_rollup over ctx's last batch: (offsets [n_seq + 1], rows)."""
+        r = RollupResult()
+        check(lib().kgx_kmap_rollup(self.handle, ctx.handle, mode, ctypes.byref(r)), "kgx_kmap_rollup")
+        off = _view(r.offsets, r.n_seq + 1, np.uint64)
+        return off, _view(r.rows, int(off[-1]), ROLLUP_DTYPE)
 
     def close(self) -> None:
         if self.handle:

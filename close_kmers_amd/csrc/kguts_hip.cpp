@@ -1085,42 +1085,38 @@ void KmerPegMapping::load_nr_families(KmerGuts &kg, const std::string &nr_fasta,
 
 FamilyMapper::FamilyMapper(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping) : kg_(kg), mapping_(mapping) {}
 
-FamilyMapper::best_match_t
-FamilyMapper::find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
-                                     const uint32_t *list_ids, std::vector<KmerCall> &calls)
+FamilyMapper::best_match_t FamilyMapper::find_best_family_match(const kgx_rollup_row *rows, size_t n_rows,
+                                                                 std::vector<KmerCall> &calls)
 {
     int fi;
     std::string fn;
     float score, wscore, off = 0.0f;
     kg_.find_best_call(calls, fi, fn, score, wscore, off);
-    return match_from(hit_lists, list_ids, fn, score);
+    return match_from(rows, n_rows, fn, score);
 }
 
-FamilyMapper::best_match_t
-FamilyMapper::find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
-                                     const uint32_t *list_ids, const kgx_best_call &best)
+FamilyMapper::best_match_t FamilyMapper::find_best_family_match(const kgx_rollup_row *rows, size_t n_rows,
+                                                                 const kgx_best_call &best)
 {
     int fi;
     std::string fn;
     float score, wscore, off = 0.0f;
     kg_.find_best_call(best, fi, fn, score, wscore, off);
-    return match_from(hit_lists, list_ids, fn, score);
+    return match_from(rows, n_rows, fn, score);
 }
 
-FamilyMapper::best_match_t FamilyMapper::match_from(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
-                                                    const uint32_t *list_ids, std::string fn, float score)
+FamilyMapper::best_match_t FamilyMapper::match_from(const kgx_rollup_row *rows, size_t n_rows, std::string fn,
+                                                    float score)
 {
-    seq_score_.clear(); /* ingest_protein, family_mapper.cc:48 */
-    for (auto &hl : hit_lists) { /* on_hit, family_mapper.cc:287-312 */
-        if (hl.second == 0)
-            continue;
-        const float weight = 1.0f / (float)hl.second;
-        for (uint32_t j = 0; j < hl.second; j++) {
-            sequence_accumulated_score_t &s = seq_score_[list_ids[hl.first + j]];
-            s.hit_count++;
-            s.hit_total++;
-            s.weighted_total += weight;
-        }
+    /* ingest_protein clears seq_score_ (family_mapper.cc:48); on_hit's
+     * operator[] calls (family_mapper.cc:287-312) leave the ids in
+     * first-touch order, which is the rows' order */
+    seq_score_.clear();
+    for (size_t j = 0; j < n_rows; j++) {
+        sequence_accumulated_score_t &s = seq_score_[rows[j].id];
+        s.hit_count = rows[j].hit_count;
+        s.hit_total = rows[j].hit_total;
+        s.weighted_total = rows[j].weighted_total;
     }
     if (fn.empty() || fn.find(" ?? ") != std::string::npos)
         fn = "hypothetical protein"; /* allow_ambiguous_functions_ = false */
@@ -1200,66 +1196,64 @@ LookupRequest::LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool famil
 void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
                                  std::ostream &os)
 {
-    const uint32_t n = (uint32_t)work.size();
+    /* pieces that keep the batch's hits on the device (one small-batch pass
+     * each: at most 2M residues, 65,536 sequences) */
+    const size_t n_work = work.size();
+    size_t a = 0;
+    while (a < n_work) {
+        size_t b = a, res = 0;
+        while (b < n_work && (b == a || (res + work[b].second.size() <= (size_t(1) << 21) && b - a < 65536)))
+            res += work[b++].second.size();
+        process_piece(kg, work, a, b, os);
+        a = b;
+    }
+}
+
+void LookupRequest::process_piece(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
+                                  size_t w0, size_t w1, std::ostream &os)
+{
+    const uint32_t n = (uint32_t)(w1 - w0);
     if (n == 0)
         return;
     std::string buf;
     std::vector<uint64_t> off(n + 1, 0);
     for (uint32_t i = 0; i < n; i++) {
-        buf += work[i].second;
+        buf += work[w0 + i].second;
         off[i + 1] = buf.size();
     }
     const bool want_calls = find_best_match_ && family_mode_;
     kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
     kgx_result r;
     /* find_best_call runs on the device (KGX_WANT_BEST): only its decision
-     * per sequence comes back, not the calls */
-    const uint64_t g0 = now_ns(); /* gpu stage: the pass and the k-mer table lookups */
-    int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n,
-                               KGX_WANT_HITS | (want_calls ? KGX_WANT_BEST : 0), &r);
+     * per sequence comes back, not the calls; the hits stay on the device,
+     * where on_hit's rollups run (kgx_kmap_rollup) */
+    const uint64_t g0 = now_ns(); /* gpu stage: the pass and the rollups */
+    int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n, want_calls ? KGX_WANT_BEST : 0u, &r);
     stage_stats().gpu_passes++;
     if (rc)
         throw_last(rc, "kgx_process_batch");
-    /* the on_hit lists of every hit: kmer_to_family_id_ or kmer_to_id_ */
+    /* on_hit (lookup_request.cc:446-482) over kmer_to_family_id_ or kmer_to_id_ */
     kgx_kmap *map = family_mode_ ? mapping_->kmer_to_family_id() : mapping_->kmer_to_id();
-    const uint64_t nh = r.hit_offsets[n];
-    std::vector<uint64_t> loff(nh + 1, 0);
-    std::vector<uint32_t> lids;
-    if (nh && kgx_kmap_num_kmers(map)) {
-        std::vector<uint64_t> kmers(nh);
-        for (uint64_t h = 0; h < nh; h++)
-            kmers[h] = r.hits[h].which_kmer;
-        rc = kgx_kmap_lookup(map, kmers.data(), nh, loff.data(), nullptr, 0);
-        if (!rc) {
-            lids.resize(loff[nh]);
-            rc = kgx_kmap_lookup(map, kmers.data(), nh, loff.data(), lids.data(), lids.size());
-        }
-        if (rc)
-            throw_last(rc, "kgx_kmap_lookup");
-    }
+    kgx_rollup_result ru;
+    rc = kgx_kmap_rollup(map, kg.ctx(), family_mode_ ? KGX_ROLLUP_FAMILY : KGX_ROLLUP_PEG, &ru);
+    if (rc)
+        throw_last(rc, "kgx_kmap_rollup");
     stage_stats().gpu_ns += now_ns() - g0;
     StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
     std::string line;
     for (uint32_t s = 0; s < n; s++) {
-        const std::string &id = work[s].first;
+        const std::string &id = work[w0 + s].first;
+        /* seq_score_ as the reference's operator[] calls leave it: the ids in
+         * first-touch order into the request's one map (cleared per sequence,
+         * its bucket count kept), so its iteration order is the reference's */
         seq_score_.clear();
-        for (uint64_t h = r.hit_offsets[s]; h < r.hit_offsets[s + 1]; h++) {
-            const uint64_t a = loff[h], b = loff[h + 1];
-            if (a == b)
-                continue;
-            if (family_mode_) {
-                const float weight = 1.0f / (float)(b - a);
-                for (uint64_t j = a; j < b; j++) {
-                    acc_t &e = seq_score_[lids[j]];
-                    e.hit_count++;
-                    e.hit_total++;
-                    e.weighted_total += weight;
-                }
-            } else {
-                for (uint64_t j = a; j < b; j++)
-                    seq_score_[lids[j]].hit_count++;
-            }
+        for (uint64_t j = ru.offsets[s]; j < ru.offsets[s + 1]; j++) {
+            const kgx_rollup_row &row = ru.rows[j];
+            acc_t &e = seq_score_[row.id];
+            e.hit_count = row.hit_count;
+            e.hit_total = row.hit_total;
+            e.weighted_total = row.weighted_total;
         }
         if (want_calls) {
             int fi;
@@ -1675,7 +1669,7 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
      * so the calls come back and find_best_call runs on the host for the
      * fragments that have any: a per-fragment device decision (KGX_WANT_BEST)
      * would copy 24 B for every fragment (measured: 8.3M -> 6.7M reads/s). */
-    const uint32_t want = families ? (KGX_WANT_HITS | KGX_WANT_CALLS) : KGX_WANT_CALLS;
+    const uint32_t want = KGX_WANT_CALLS; /* the hits stay on the device for the rollups */
     rc = kgx_fq_run_device(ctx, &p, &fr, want, nullptr);
     if (rc)
         throw_last(rc, "kgx_fq_run_device");
@@ -1688,7 +1682,6 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
             throw_last(rc, "kgx_fq_called_reads");
         mark("collect");
         FamilyMapper mapper(kg_, mapping_);
-        const std::vector<std::pair<uint64_t, uint32_t>> no_hits;
         std::vector<KmerCall> calls;
         std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
         std::vector<uint32_t> match_len, best_len;
@@ -1712,7 +1705,7 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
                     for (uint64_t c = cr.call_offsets[g]; c < cr.call_offsets[g + 1]; c++)
                         calls.emplace_back(cr.calls[c].start, cr.calls[c].end, cr.calls[c].count,
                                            cr.calls[c].function_index, cr.calls[c].weighted_hits);
-                    matches.emplace_back(0, mapper.find_best_family_match(no_hits, nullptr, calls));
+                    matches.emplace_back(0, mapper.find_best_family_match(nullptr, 0, calls));
                     match_len.push_back(cr.frag_len[g]);
                     score += matches.back().second.score;
                     if (score > best_score) {
@@ -1746,23 +1739,10 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     if (rc)
         throw_last(rc, "kgx_device_batch_collect");
     mark("collect");
-    /* kmer_to_family_id_ lists of every hit */
-    const uint64_t nh = fr.n_fragments && families ? res.hit_offsets[fr.n_fragments] : 0;
-    std::vector<uint64_t> list_off(nh + 1, 0);
-    std::vector<uint32_t> list_ids;
-    if (nh) {
-        std::vector<uint64_t> kmers(nh);
-        for (uint64_t i = 0; i < nh; i++)
-            kmers[i] = res.hits[i].which_kmer;
-        rc = kgx_kmap_lookup(mapping_->kmer_to_family_id(), kmers.data(), nh, list_off.data(), nullptr, 0);
-        if (!rc) {
-            list_ids.resize(list_off[nh]);
-            rc = kgx_kmap_lookup(mapping_->kmer_to_family_id(), kmers.data(), nh, list_off.data(),
-                                 list_ids.data(), list_ids.size());
-        }
-        if (rc)
-            throw_last(rc, "kgx_kmap_lookup");
-    }
+    /* on_hit's rollups of every fragment (family_mapper.cc:287-312) on the device */
+    kgx_rollup_result ru;
+    if ((rc = kgx_kmap_rollup(mapping_->kmer_to_family_id(), ctx, KGX_ROLLUP_FAMILY, &ru)))
+        throw_last(rc, "kgx_kmap_rollup");
     /* fragment lengths (printed for matches) are needed only for reads with
      * calls: fetch their offset slices, or all offsets when there are many */
     std::vector<uint64_t> rfirst(n_reads + 1, 0);
@@ -1787,7 +1767,6 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     mark("family lists");
     /* on_parsed_seq (fq_process_request.cc:298-365), reads in order */
     FamilyMapper mapper(kg_, mapping_);
-    std::vector<std::pair<uint64_t, uint32_t>> hit_lists;
     std::vector<KmerCall> calls;
     std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
     std::vector<uint64_t> match_frag, best_frag;
@@ -1812,15 +1791,11 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
             matches.clear();
             match_frag.clear();
             for (; g < g_end; g++) {
-                hit_lists.clear();
-                if (families)
-                    for (uint64_t h = res.hit_offsets[g]; h < res.hit_offsets[g + 1]; h++)
-                        hit_lists.emplace_back(list_off[h], (uint32_t)(list_off[h + 1] - list_off[h]));
                 calls.clear();
                 for (uint64_t c = res.call_offsets[g]; c < res.call_offsets[g + 1]; c++)
                     calls.emplace_back(res.calls[c].start, res.calls[c].end, res.calls[c].count,
                                        res.calls[c].function_index, res.calls[c].weighted_hits);
-                matches.emplace_back(0, mapper.find_best_family_match(hit_lists, list_ids.data(), calls));
+                matches.emplace_back(0, mapper.find_best_family_match(ru.rows + ru.offsets[g], ru.offsets[g + 1] - ru.offsets[g], calls));
                 match_frag.push_back(g);
                 score += matches.back().second.score;
                 if (score > best_score) {

@@ -387,8 +387,8 @@ private:
 /*
  * FamilyMapper (family_mapper.cc:46-205, 287-330) in family mode with
  * allow_ambiguous_functions_ = false, over results computed in batches: the
- * caller supplies a fragment's hits (k-mers, in position order) with their
- * kmer_to_family_id_ lists and its calls.  seq_score_ is one
+ * caller supplies a fragment's on_hit rollups (computed on the device from
+ * its hits and their kmer_to_family_id_ lists) and its calls.  seq_score_ is one
  * std::unordered_map kept across calls (cleared per protein), as in the
  * reference, so iteration -- and with it tie and summation order -- matches.
  */
@@ -408,19 +408,17 @@ public:
         float weighted_total = 0.0f;
     };
     FamilyMapper(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping);
-    /* hit_lists[h] = (first, count) into list_ids for hit h */
-    best_match_t find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
-                                        const uint32_t *list_ids, std::vector<KmerCall> &calls);
+    /* rows: the fragment's on_hit rollups (kgx_kmap_rollup over
+     * kmer_to_family_id_, KGX_ROLLUP_FAMILY), in first-touch order */
+    best_match_t find_best_family_match(const kgx_rollup_row *rows, size_t n_rows, std::vector<KmerCall> &calls);
     /* the same with find_best_call decided on the device (KGX_WANT_BEST) */
-    best_match_t find_best_family_match(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists,
-                                        const uint32_t *list_ids, const kgx_best_call &best);
+    best_match_t find_best_family_match(const kgx_rollup_row *rows, size_t n_rows, const kgx_best_call &best);
     unsigned int kmer_hit_threshold_ = 3;
 
 private:
-    /* seq_score_ from the hits' family lists, then the family rollup for the
+    /* seq_score_ from the fragment's rollups, then the family rollup for the
      * called function (family_mapper.cc:46-205) */
-    best_match_t match_from(const std::vector<std::pair<uint64_t, uint32_t>> &hit_lists, const uint32_t *list_ids,
-                            std::string fn, float score);
+    best_match_t match_from(const kgx_rollup_row *rows, size_t n_rows, std::string fn, float score);
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     std::unordered_map<KmerPegMapping::encoded_id_t, sequence_accumulated_score_t> seq_score_;
@@ -433,8 +431,9 @@ std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m);
  * (kmer_hit_threhsold -- sic --, find_best_match, find_reps,
  * allow_ambiguous_functions, target_genus).  process_work() is the worker
  * loop over a chunk (lookup_request.cc:153-400): the chunk's lookups run as
- * one GPU batch, the per-sequence rollups (on_hit 446-482) and output run
- * on the host in order with one seq_score_ map for the request.  No family
+ * one GPU batch and the per-sequence rollups (on_hit 446-482) on the device
+ * (kgx_kmap_rollup); the rows go into one seq_score_ map for the request in
+ * first-touch order, and the selection and output run on the host in order.  No family
  * reps DB is loaded, so find_reps prints only the "///" separators.
  */
 class LookupRequest {
@@ -445,6 +444,9 @@ public:
                       std::ostream &os);
 
 private:
+    /* work[w0, w1) as one GPU pass, its rollups on the device */
+    void process_piece(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work, size_t w0,
+                       size_t w1, std::ostream &os);
     std::shared_ptr<KmerPegMapping> mapping_;
     bool family_mode_;
     unsigned int kmer_hit_threshold_ = 3;

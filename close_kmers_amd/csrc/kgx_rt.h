@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -265,6 +266,16 @@ struct SvcState;
 /* stops and frees the image's call service (kgx_svc.cpp), if any */
 void svc_shutdown(kgx_image *img);
 
+/* kgx_kmap_rollup's device scratch and host results (kgx_tables.hip), per
+ * context: grow-only, no allocation per call once warm */
+struct RollupScratch {
+    DevBuf tcount, tbase, hseq, hstart, hlen, eoff, key, key2, idx, idx2, ew, flag, rowdata, rows, rowcnt, rowoff,
+        nsel, tmp;
+    PinnedVec<uint64_t> h_n; /* [0] hits, [1] events, [2] rows */
+    PinnedVec<uint64_t> h_off;
+    PinnedVec<kgx_rollup_row> h_rows;
+};
+
 }  // namespace kgx
 
 struct kgx_image {
@@ -286,6 +297,7 @@ struct kgx_image {
     std::mutex svc_mu;
     kgx::SvcState *svc = nullptr;
     uint32_t svc_slots = 32, svc_idle_us = 1000, svc_life_us = 1000;
+    bool svc_configured = false; /* kgx_svc_config was called (env defaults no longer apply) */
     const void *resident() const
     {
         return layout == KGX_LAYOUT_PACKED16 ? static_cast<const void *>(d_packed) : d_table;
@@ -440,6 +452,8 @@ struct kgx_ctx {
     std::vector<hipEvent_t> prof_ev; /* 4 per chunk: H2D start, H2D end, device end, gathered */
     std::vector<hipEvent_t> prof_done; /* per chunk: bulk copy done (timing events on the copy stream) */
     kgx_host_profile last_profile{};
+    /* kgx_kmap_rollup */
+    std::unique_ptr<kgx::RollupScratch> rollup;
 };
 
 namespace kgx {

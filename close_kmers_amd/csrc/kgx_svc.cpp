@@ -36,6 +36,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 
 #include <sys/prctl.h>
 #include <time.h>
@@ -89,7 +90,9 @@ struct SvcState {
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
     uint32_t sleep_us = 0;
-    std::atomic<bool> broken{false}; /* a launch failed: callers take other paths */
+    std::atomic<bool> broken{false}; /* a launch failed or a call timed out: callers take other paths */
+    std::atomic<uint32_t> users{0};  /* callers inside kgx_svc_call holding this state */
+    std::atomic<uint64_t> n_abandoned{0}; /* slots given up after a 10-s wait (never handed out again) */
 };
 
 namespace {
@@ -105,6 +108,30 @@ int64_t now_ns()
 }
 
 constexpr size_t align64(size_t x) { return (x + 63) & ~size_t(63); }
+
+/* orders the host's stores to the request lines before what follows and, for
+ * device memory written through the write-combining BAR, pushes them out */
+inline void wc_fence()
+{
+#if defined(__x86_64__)
+    __builtin_ia32_sfence();
+#else
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+#endif
+}
+
+/* a caller's hold on the service: shutdown waits until none is left */
+struct SvcUse {
+    SvcState *s = nullptr;
+    SvcUse() = default;
+    SvcUse(const SvcUse &) = delete;
+    SvcUse &operator=(const SvcUse &) = delete;
+    ~SvcUse()
+    {
+        if (s)
+            s->users.fetch_sub(1, std::memory_order_release);
+    }
+};
 
 /* keep two instances enqueued (mu held) */
 int top_up(SvcState *s)
@@ -151,14 +178,14 @@ void drain(SvcState *s)
     std::lock_guard<std::mutex> lk(s->mu);
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 1u, __ATOMIC_RELEASE);
-    __builtin_ia32_sfence();
+    wc_fence();
     (void)hipStreamSynchronize(s->stream);
     for (hipEvent_t e : s->running)
         s->spare.push_back(e);
     s->running.clear();
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 0u, __ATOMIC_RELEASE);
-    __builtin_ia32_sfence();
+    wc_fence();
 }
 
 void destroy(SvcState *s)
@@ -271,23 +298,39 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     return KGX_OK;
 }
 
-/* the image's service, created on first use with its configuration */
-int get(kgx_image *img, SvcState **out)
+/* the image's service, created on first use with its configuration, held
+ * by `use` until the caller returns (svc_shutdown waits for every hold) */
+int get(kgx_image *img, SvcUse &use)
 {
     std::lock_guard<std::mutex> lk(img->svc_mu);
     if (!img->svc) {
-        /* KGX_SVC_LIFE_US: a default for experiments (kgx_svc_config sets it per image) */
-        uint64_t idle = img->svc_idle_us, life = img->svc_life_us;
-        if (const char *e = std::getenv("KGX_SVC_IDLE_US"))
-            idle = std::max<uint64_t>(10, std::strtoull(e, nullptr, 10));
-        if (const char *e = std::getenv("KGX_SVC_LIFE_US"))
-            life = std::max<uint64_t>(idle, std::strtoull(e, nullptr, 10));
-        int rc = create(img, img->svc_slots, idle, life, &img->svc);
+        /* KGX_SVC_LIFE_US: a default for experiments, for images that
+         * kgx_svc_config never configured */
+        uint64_t life = img->svc_life_us;
+        if (const char *e = std::getenv("KGX_SVC_LIFE_US"); e && !img->svc_configured)
+            life = std::max<uint64_t>(10, std::strtoull(e, nullptr, 10));
+        int rc = create(img, img->svc_slots, img->svc_idle_us, life, &img->svc);
         if (rc)
             return rc;
     }
-    *out = img->svc;
+    img->svc->users.fetch_add(1, std::memory_order_acquire);
+    use.s = img->svc;
     return KGX_OK;
+}
+
+/* detach and free the image's service (svc_mu held): new callers create a
+ * fresh one after the lock is released; callers already inside keep the old
+ * one's instances serving them until they return, then it is drained and
+ * freed */
+void shutdown_locked(kgx_image *img)
+{
+    SvcState *s = img->svc;
+    if (!s)
+        return;
+    img->svc = nullptr;
+    while (s->users.load(std::memory_order_acquire) != 0)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    destroy(s);
 }
 
 bool take_slot(SvcState *s, uint32_t &slot)
@@ -311,8 +354,7 @@ void give_slot(SvcState *s, uint32_t slot) { s->free_mask.fetch_or(1ull << slot,
 void svc_shutdown(kgx_image *img)
 {
     std::lock_guard<std::mutex> lk(img->svc_mu);
-    destroy(img->svc);
-    img->svc = nullptr;
+    shutdown_locked(img);
 }
 
 }  // namespace kgx
@@ -327,8 +369,10 @@ int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t li
         return fail(KGX_EINVAL, "null image");
     if (slots < 1 || slots > SVC_MAX_SLOTS || idle_us < 10 || life_us < idle_us)
         return fail(KGX_EINVAL, "call service: 1..64 slots, idle_us >= 10, life_us >= idle_us");
-    svc_shutdown(img);
+    /* one critical section: no call in between starts a service with the old settings */
     std::lock_guard<std::mutex> lk(img->svc_mu);
+    shutdown_locked(img);
+    img->svc_configured = true;
     img->svc_slots = slots;
     img->svc_idle_us = idle_us;
     img->svc_life_us = life_us;
@@ -358,6 +402,10 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? s->n_launches.load() : 0;
     else if (n == "busy")
         *value = s ? s->n_busy.load() : 0;
+    else if (n == "abandoned") /* slots given up after a 10-s wait */
+        *value = s ? s->n_abandoned.load() : 0;
+    else if (n == "broken") /* 1: the service turns every call away until kgx_svc_stop */
+        *value = s && s->broken ? 1 : 0;
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
     else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '5') /* "phase_n0".."phase_n5" */
@@ -389,10 +437,11 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     if ((want & KGX_WANT_HITS && W && !hits) || (want & KGX_WANT_CALLS && W && !calls) ||
         (want & KGX_WANT_OTU && W && !otus))
         return fail(KGX_EINVAL, "null result buffer");
-    SvcState *s = nullptr;
-    int rc = get(img, &s);
+    SvcUse use;
+    int rc = get(img, use);
     if (rc)
         return rc;
+    SvcState *s = use.s;
     if (s->broken)
         return fail(KGX_EBUSY, "call service: unavailable after a launch failure");
     uint32_t slot = 0;
@@ -422,11 +471,11 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     /* device memory is written through a write-combining BAR mapping: the
      * fences order the request's bytes before its number and push it out */
     if (s->reqmem)
-        __builtin_ia32_sfence();
+        wc_fence();
     __atomic_store_n(&h.copy, q, __ATOMIC_RELEASE);
     __atomic_store_n(&h.req, q, __ATOMIC_RELEASE);
     if (s->reqmem)
-        __builtin_ia32_sfence();
+        wc_fence();
     /* keep instances enqueued (cheap: one clock read unless 200 us passed) */
     const int64_t t0 = now_ns();
     if (t0 >= s->next_check.load(std::memory_order_relaxed)) {
@@ -461,8 +510,15 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
                 }
                 nudged = true;
             }
-            if (dt > 10000000000ll) /* 10 s: the slot is abandoned (never handed out again) */
+            if (dt > 10000000000ll) {
+                /* 10 s: the slot is abandoned (a late answer could still land
+                 * in it, so it is never handed out again) and the service
+                 * turns every later call away, to the batch paths, until
+                 * kgx_svc_stop / kgx_svc_config replaces it */
+                s->n_abandoned++;
+                s->broken = true;
                 return fail(KGX_EDEVICE, "call service: no answer within 10 s");
+            }
         }
 #if defined(__x86_64__)
         __builtin_ia32_pause();

@@ -246,6 +246,88 @@ __global__ void lookup_ids_kernel(KmapView m, const uint64_t *kmers, uint64_t n,
             ids[off[i] + (j - a)] = m.vals[j];
 }
 
+/* --- /lookup rollups (kgx_kmap_rollup) ---
+ * Events are the (hit, list entry) pairs of LookupRequest::on_hit
+ * (lookup_request.cc:446-482), numbered in hit order, then list order: event
+ * e of hit h is eoff[h] + j for list entry j.  A stable sort by (sequence,
+ * id) groups each sequence's id's events with their numbers ascending, so a
+ * group's f32 sum taken in sorted order is the reference's sum in hit order,
+ * and its first event number is when the reference first touched the id. */
+
+/* per tiled hit slot (tile * T + i): its sequence, list start and length
+ * (0 for slots past the tile's hits and for unmapped k-mers); slot n_slots
+ * gets length 0, the scan's last element */
+__global__ void rollup_hits_kernel(Tiled t, uint64_t n_tiles, KmapView m, uint32_t *hseq, uint64_t *hstart,
+                                   uint64_t *hlen)
+{
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n_slots = n_tiles * t.T;
+    if (slot > n_slots)
+        return;
+    uint64_t len = 0;
+    if (slot < n_slots) {
+        const uint64_t tile = slot / t.T;
+        const uint32_t i = (uint32_t)(slot % t.T);
+        if (i < tile_count(t, tile)) {
+            uint64_t key, a = 0, b = 0;
+            uint32_t seq;
+            hit_key_seq(t, tile, i, key, seq);
+            if (kmap_row(m, key, a, b)) {
+                len = b - a;
+                hseq[slot] = seq;
+                hstart[slot] = a;
+            }
+        }
+    }
+    hlen[slot] = len;
+}
+
+/* the events of every slot with a list: key = sequence << ib | id, the event
+ * number, and the hit's weight 1.0f / (float)|list| (lookup_request.cc:459) */
+__global__ void rollup_expand_kernel(uint64_t n_slots, const uint32_t *hseq, const uint64_t *hstart,
+                                     const uint64_t *hlen, const uint64_t *eoff, const uint32_t *vals, uint32_t ib,
+                                     uint64_t *key, uint32_t *idx, float *ew)
+{
+    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= n_slots)
+        return;
+    const uint64_t len = hlen[slot];
+    if (len == 0)
+        return;
+    const uint64_t e0 = eoff[slot], a = hstart[slot], hi = (uint64_t)hseq[slot] << ib;
+    const float w = 1.0f / (float)len;
+    for (uint64_t j = 0; j < len; j++) {
+        key[e0 + j] = hi | vals[a + j];
+        idx[e0 + j] = (uint32_t)(e0 + j);
+        ew[e0 + j] = w;
+    }
+}
+
+/* one thread per (sequence, id) group, at its first sorted event: the
+ * group's counts and its weights summed in event order, stored at the first
+ * event's number (flagged), and one more row for its sequence */
+__global__ void rollup_groups_kernel(uint64_t n_ev, const uint64_t *key, const uint32_t *idx, const float *ew,
+                                     uint32_t ib, int family, uint8_t *flag, uint4 *rowdata, uint32_t *rowcnt)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_ev)
+        return;
+    const uint64_t k = key[p];
+    if (p > 0 && key[p - 1] == k)
+        return;
+    uint32_t cnt = 0;
+    float ws = 0.0f;
+    for (uint64_t q = p; q < n_ev && key[q] == k; q++) {
+        ws += ew[idx[q]]; /* s.weighted_total += weight, hit by hit */
+        cnt++;
+    }
+    const uint32_t first = idx[p];
+    const uint32_t id = (uint32_t)(k & ((1ull << ib) - 1));
+    flag[first] = 1;
+    rowdata[first] = family ? make_uint4(id, cnt, cnt, __float_as_uint(ws)) : make_uint4(id, cnt, 0u, 0u);
+    atomicAdd(rowcnt + (k >> ib), 1u);
+}
+
 /* --- /matrix --- */
 
 __global__ void seen_insert_kernel(const uint32_t *ids, uint32_t n, uint64_t base, uint64_t *skeys,
@@ -422,6 +504,7 @@ struct kgx_kmap {
     int mode = KGX_KMAP_APPEND;
     hipStream_t stream = nullptr;
     uint64_t n_rows = 0, n_vals = 0, hcap = 0;
+    uint32_t max_id = 0; /* the largest id added (kgx_kmap_rollup's key width) */
     DevBuf keys, starts, vals, hkeys, hrow;
     std::mutex scratch_mu;
     std::vector<std::unique_ptr<KmapScratch>> scratch_free;
@@ -657,9 +740,13 @@ int kgx_kmap_add(kgx_kmap *m, const uint64_t *kmers, const uint32_t *ids, uint64
     int rc = kmap_expand(m, d_k, d_v, n, st);
     if (rc)
         return rc;
-    for (uint64_t i = 0; i < n; i++)
+    uint32_t mx = m->max_id;
+    for (uint64_t i = 0; i < n; i++) {
         if (ids[i] == NO_ID)
             return fail(KGX_EINVAL, "id 0xFFFFFFFF is reserved");
+        mx = std::max(mx, ids[i]);
+    }
+    m->max_id = mx;
     HIP_TRY(hipMemcpyAsync(d_k.as<uint64_t>() + m->n_vals, kmers, n * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d_v.as<uint32_t>() + m->n_vals, ids, n * 4, hipMemcpyHostToDevice, st));
     return kmap_rebuild(m, d_k, d_v, m->n_vals + n, st);
@@ -684,6 +771,7 @@ int kgx_kmap_add_hits(kgx_kmap *m, kgx_ctx *c, const uint32_t *seq_ids)
     rc = upload_ids(d_ids, seq_ids, c->n_seq, st);
     if (rc)
         return rc;
+    const uint32_t batch_max = *std::max_element(seq_ids, seq_ids + c->n_seq);
     const Tiled t = tiled_of(c);
     const uint64_t nt = c->max_tiles;
     HIP_TRY(counts.reserve((nt + 1) * 4));
@@ -704,6 +792,7 @@ int kgx_kmap_add_hits(kgx_kmap *m, kgx_ctx *c, const uint32_t *seq_ids)
     rc = kmap_expand(m, d_k, d_v, total, st);
     if (rc)
         return rc;
+    m->max_id = std::max(m->max_id, batch_max);
     hipLaunchKernelGGL(hits_to_pairs_kernel, grid_for(nt * t.T), dim3(256), 0, st, t, nt, base.as<uint32_t>(),
                        d_ids.as<uint32_t>(), d_k.as<uint64_t>() + m->n_vals, d_v.as<uint32_t>() + m->n_vals);
     HIP_TRY(hipGetLastError());
@@ -762,6 +851,111 @@ int kgx_kmap_lookup(kgx_kmap *m, const uint64_t *kmers, uint64_t n, uint64_t *of
                        sc->c.as<uint64_t>(), sc->ids.as<uint32_t>());
     HIP_TRY(hipMemcpyAsync(ids, sc->ids.p, offsets[n] * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    return KGX_OK;
+}
+
+int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
+{
+    if (!m || !out || (mode != KGX_ROLLUP_PEG && mode != KGX_ROLLUP_FAMILY))
+        return fail(KGX_EINVAL, "bad kmap_rollup arguments");
+    int rc = check_ctx_hits(c);
+    if (rc)
+        return rc;
+    if (c->img->device != m->device)
+        return fail(KGX_EINVAL, "kmap and context are on different devices");
+    HIP_TRY(hipSetDevice(m->device));
+    if (!c->rollup)
+        c->rollup.reset(new RollupScratch);
+    RollupScratch &r = *c->rollup;
+    const uint32_t n = c->n_seq;
+    hipStream_t st = c->stream;
+    HIP_TRY(r.h_off.resize(n + 1));
+    HIP_TRY(r.h_n.resize(4));
+    out->n_seq = n;
+    out->offsets = r.h_off.data();
+    out->rows = r.h_rows.data();
+    out->n_events = 0;
+    if (n == 0 || m->n_rows == 0) {
+        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
+        return KGX_OK;
+    }
+    /* 1. per hit slot: sequence, list, length; the event offsets by a scan */
+    const Tiled t = tiled_of(c);
+    const uint64_t nt = c->max_tiles, n_slots = nt * t.T;
+    const KmapView view = m->view();
+    HIP_TRY(r.hseq.reserve(n_slots * 4));
+    HIP_TRY(r.hstart.reserve(n_slots * 8));
+    HIP_TRY(r.hlen.reserve((n_slots + 1) * 8));
+    HIP_TRY(r.eoff.reserve((n_slots + 1) * 8));
+    hipLaunchKernelGGL(rollup_hits_kernel, grid_for(n_slots + 1), dim3(256), 0, st, t, nt, view,
+                       r.hseq.as<uint32_t>(), r.hstart.as<uint64_t>(), r.hlen.as<uint64_t>());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(),
+                                             (int)(n_slots + 1), st));
+    HIP_TRY(r.tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(),
+                                             (int)(n_slots + 1), st));
+    HIP_TRY(hipMemcpyAsync(r.h_n.data(), r.eoff.as<uint64_t>() + n_slots, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t E = r.h_n[0];
+    out->n_events = E;
+    if (E == 0) {
+        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
+        return KGX_OK;
+    }
+    if (E >= (1ull << 31))
+        return fail(KGX_ERANGE, "rollup: more than 2^31 (hit, id) events in one batch");
+    /* 2. events keyed (sequence, id), stably sorted: hit order within a key */
+    const uint32_t ib = std::max(1, 32 - __builtin_clz(std::max(m->max_id, 1u)));
+    const uint32_t sb = n > 1 ? 32 - __builtin_clz(n - 1) : 1;
+    HIP_TRY(r.key.reserve(E * 8));
+    HIP_TRY(r.key2.reserve(E * 8));
+    HIP_TRY(r.idx.reserve(E * 4));
+    HIP_TRY(r.idx2.reserve(E * 4));
+    HIP_TRY(r.ew.reserve(E * 4));
+    HIP_TRY(r.flag.reserve(E));
+    HIP_TRY(r.rowdata.reserve(E * 16));
+    HIP_TRY(r.rowcnt.reserve((n + 1) * 4));
+    HIP_TRY(r.nsel.reserve(8));
+    hipLaunchKernelGGL(rollup_expand_kernel, grid_for(n_slots), dim3(256), 0, st, n_slots, r.hseq.as<uint32_t>(),
+                       r.hstart.as<uint64_t>(), r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(), view.vals, ib,
+                       r.key.as<uint64_t>(), r.idx.as<uint32_t>(), r.ew.as<float>());
+    tb = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, r.key.as<uint64_t>(), r.key2.as<uint64_t>(),
+                                               r.idx.as<uint32_t>(), r.idx2.as<uint32_t>(), (int)E, 0,
+                                               (int)(ib + sb), st));
+    HIP_TRY(r.tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(r.tmp.p, tb, r.key.as<uint64_t>(), r.key2.as<uint64_t>(),
+                                               r.idx.as<uint32_t>(), r.idx2.as<uint32_t>(), (int)E, 0,
+                                               (int)(ib + sb), st));
+    /* 3. one row per group at its first event; rows in event order = per
+     * sequence in first-touch order, straight into the mapped host arrays */
+    HIP_TRY(hipMemsetAsync(r.flag.p, 0, E, st));
+    HIP_TRY(hipMemsetAsync(r.rowcnt.p, 0, (n + 1) * 4, st));
+    hipLaunchKernelGGL(rollup_groups_kernel, grid_for(E), dim3(256), 0, st, E, r.key2.as<uint64_t>(),
+                       r.idx2.as<uint32_t>(), r.ew.as<float>(), ib, mode == KGX_ROLLUP_FAMILY ? 1 : 0,
+                       r.flag.as<uint8_t>(), r.rowdata.as<uint4>(), r.rowcnt.as<uint32_t>());
+    HIP_TRY(r.h_rows.resize(E));
+    out->rows = r.h_rows.data();
+    void *d_rows = nullptr, *d_off = nullptr, *d_n = nullptr;
+    HIP_TRY(r.h_rows.device_ptr(0, &d_rows));
+    HIP_TRY(r.h_off.device_ptr(0, &d_off));
+    HIP_TRY(r.h_n.device_ptr(1, &d_n));
+    size_t tb1 = 0, tb2 = 0;
+    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb1, r.rowdata.as<uint4>(), r.flag.as<uint8_t>(),
+                                          static_cast<uint4 *>(d_rows), static_cast<uint64_t *>(d_n), (int)E, st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, r.rowcnt.as<uint32_t>(), static_cast<uint64_t *>(d_off),
+                                             (int)(n + 1), st));
+    HIP_TRY(r.tmp.reserve(std::max(tb1, tb2)));
+    HIP_TRY(hipcub::DeviceSelect::Flagged(r.tmp.p, tb1, r.rowdata.as<uint4>(), r.flag.as<uint8_t>(),
+                                          static_cast<uint4 *>(d_rows), static_cast<uint64_t *>(d_n), (int)E, st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb2, r.rowcnt.as<uint32_t>(), static_cast<uint64_t *>(d_off),
+                                             (int)(n + 1), st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (r.h_n[1] != r.h_off[n] || r.h_off[n] > E)
+        return fail(KGX_EDEVICE, "rollup: row counts disagree");
     return KGX_OK;
 }
 

@@ -440,17 +440,29 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
                  uint64_t *n_calls, kgx_otu *otus, uint64_t otus_cap, uint64_t *n_otus);
 /* slots (1..64, default 32) and life_us (default 1000: an instance's stay
  * before the next one, already enqueued, takes over; bounds how long the
- * service holds its hardware queue); stops a running service.  idle_us is
- * checked (>= 10, <= life_us) but no longer used: a per-workgroup idle exit
- * could strand a quiet slot's next request. */
+ * service holds its hardware queue); stops a running service (as
+ * kgx_svc_stop) and applies the settings in one step, so the next call starts
+ * the service with them.  idle_us is checked (>= 10, <= life_us) and ignored:
+ * a per-workgroup idle exit could strand a quiet slot's next request
+ * (DESIGN.md §8.8).  The KGX_SVC_LIFE_US environment default applies only to
+ * images this was never called for. */
 int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t life_us);
-/* stops the service (its workgroups leave; kgx_image_close does this too) */
+/* Stops the service: its workgroups leave and its memory is freed (so do
+ * kgx_svc_config, kgx_image_set_layout / set_filter and kgx_image_close).
+ * Safe while other threads are inside kgx_svc_call: it waits until they have
+ * returned (their calls are served); a call that starts afterwards starts a
+ * new service.  A call that gets no answer within 10 s returns KGX_EDEVICE and
+ * leaves its slot for good (a late answer may still land in it) and the
+ * service "broken": every later call returns KGX_EBUSY (take a batch path)
+ * until kgx_svc_stop or kgx_svc_config replaces the service. */
 int kgx_svc_stop(kgx_image *img);
 /* "slots", "calls" (served), "launches" (instances enqueued), "busy" (calls
- * turned away for want of a slot), "devmem" (1: requests are written into
- * fine-grained device memory through a large BAR, else mapped host memory;
- * KGX_SVC_DEVMEM=0 forces the latter), "phase_n0".."phase_n5" (with
- * KGX_SVC_DEBUG=1: summed ns of the host wall per call and the device phases) */
+ * turned away for want of a slot), "abandoned" (slots given up after a 10-s
+ * wait), "broken" (1: calls are turned away until the service is replaced),
+ * "devmem" (1: requests are written into fine-grained device memory through a
+ * large BAR, else mapped host memory; KGX_SVC_DEVMEM=0 forces the latter),
+ * "phase_n0".."phase_n5" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
+ * call and the device phases) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option
@@ -683,6 +695,36 @@ uint64_t kgx_kmap_num_values(const kgx_kmap *map);
  * the ids (ids_cap >= offsets[n]); unmapped k-mers have empty lists */
 int kgx_kmap_lookup(kgx_kmap *map, const uint64_t *kmers, uint64_t n, uint64_t *offsets,
                     uint32_t *ids, uint64_t ids_cap);
+
+/* ---- /lookup per-sequence rollups (LookupRequest::on_hit, lookup_request.cc:
+ * 446-482; FamilyMapper::on_hit, family_mapper.cc:287-312) on the device ----
+ * For each sequence s of the context's last batch (its hits still on the
+ * device: kgx_process_batch / kgx_run_device / kgx_fq_run_device; any want),
+ * each hit in position order, with L = map[hit.which_kmer] (no row: skipped):
+ *   KGX_ROLLUP_FAMILY (kmer_to_family_id_): w = 1.0f / (float)|L|; for each
+ *     id in L: row[id].hit_count++, .hit_total++, .weighted_total += w
+ *   KGX_ROLLUP_PEG (kmer_to_id_): for each id in L: row[id].hit_count++
+ * weighted_total is the f32 sum in that (hit) order.  A sequence's rows come
+ * in the order its ids were first touched (hit order, then list order): a
+ * caller that inserts them in that order into the request's one
+ * std::unordered_map seq_score_ (cleared per sequence, as the reference does)
+ * gets the map the reference's operator[] calls build, bucket by bucket, so
+ * its iteration order too.  Buffers are owned by ctx and valid until its next
+ * rollup. */
+enum { KGX_ROLLUP_PEG = 0, KGX_ROLLUP_FAMILY = 1 };
+typedef struct kgx_rollup_row { /* sequence_accumulated_score_t (lookup_request.h:26-42) + its key */
+    uint32_t id;
+    uint32_t hit_count;
+    uint32_t hit_total;
+    float weighted_total;
+} kgx_rollup_row;
+typedef struct kgx_rollup_result {
+    uint32_t n_seq;
+    const uint64_t *offsets;    /* [n_seq + 1]: sequence s's rows are [offsets[s], offsets[s+1]) */
+    const kgx_rollup_row *rows; /* host */
+    uint64_t n_events;          /* (hit, list entry) pairs folded */
+} kgx_rollup_result;
+int kgx_kmap_rollup(kgx_kmap *map, kgx_ctx *ctx, int mode, kgx_rollup_result *out);
 
 /* ---- /matrix pair counting (matrix_request.cc:83-190) --------------------
  * One kgx_matrix per /matrix request (the request's matrix_proteins_ and

@@ -56,7 +56,7 @@ SIG_DTYPE = np.dtype(
 )
 assert SIG_DTYPE.itemsize == 24
 
-WANT_HITS, WANT_CALLS, WANT_OTU = 1, 2, 4
+WANT_HITS, WANT_CALLS, WANT_OTU, WANT_BEST = 1, 2, 4, 8
 
 
 class _Result(ctypes.Structure):
@@ -71,7 +71,13 @@ class _Result(ctypes.Structure):
         ("probes", ctypes.c_uint64),
         ("windows", ctypes.c_uint64),
         ("seconds", ctypes.c_double),
+        ("best", ctypes.c_void_p),
     ]
+
+
+# oracle_best: find_best_call per sequence (want WANT_BEST)
+BEST_DTYPE = np.dtype([("function_index", "<i4"), ("score", "<f4"), ("weighted_score", "<f4"),
+                       ("score_offset", "<f4"), ("offset_set", "<i4")])
 
 
 def build(ref: bool | None = None) -> None:
@@ -171,6 +177,7 @@ class BatchResult:
     probes: int
     windows: int
     seconds: float
+    best: np.ndarray | None = None  # BEST_DTYPE per sequence with WANT_BEST
 
 
 def _arr(ptr, n, dtype):
@@ -204,7 +211,8 @@ def process_batch(table: np.ndarray, residues: np.ndarray, offsets: np.ndarray,
         hits = _arr(r.hits, int(ho[-1]), HIT_DTYPE)
         calls = _arr(r.calls, int(co[-1]), CALL_DTYPE)
         otus = _arr(ctypes.cast(r.otus, ctypes.c_void_p).value, 2 * int(oo[-1]), np.int32).reshape(-1, 2)
-        return BatchResult(ho, hits, co, calls, oo, otus, r.probes, r.windows, r.seconds)
+        best = _arr(r.best, n, BEST_DTYPE) if r.best else None
+        return BatchResult(ho, hits, co, calls, oo, otus, r.probes, r.windows, r.seconds, best)
     finally:
         L.oracle_result_free(ctypes.byref(r))
 

@@ -11,9 +11,11 @@
 #include <algorithm>
 #include <cctype>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <sstream>
 #include <thread>
 
@@ -536,6 +538,14 @@ struct oracle_hit {
 static_assert(sizeof(oracle_hit) == 32, "hit record is 32 bytes");
 static_assert(sizeof(Call) == 20, "KmerCall is 20 bytes");
 
+/* find_best_call's outputs for one sequence (kguts.cc:1008-1199; function
+ * names are not loaded: every index reads as INVALID_OFFSET) */
+struct oracle_best {
+    int32_t function_index;
+    float score, weighted_score, score_offset;
+    int32_t offset_set; /* 0: score_offset left untouched (no calls, kguts.cc:1015-1018) */
+};
+
 struct oracle_result {
     uint64_t n_seq;
     uint64_t *hit_offsets; /* n_seq + 1 */
@@ -547,9 +557,10 @@ struct oracle_result {
     uint64_t probes;
     uint64_t windows;
     double seconds; /* processing loop only */
+    oracle_best *best; /* n_seq entries with WANT_BEST, else NULL */
 };
 
-enum { WANT_HITS = 1, WANT_CALLS = 2, WANT_OTU = 4 };
+enum { WANT_HITS = 1, WANT_CALLS = 2, WANT_OTU = 4, WANT_BEST = 8 };
 
 int oracle_process_batch(const void *table, uint64_t num_sigs, const int32_t *params4,
                          const char *residues, const uint64_t *offsets, uint64_t n_seq,
@@ -563,7 +574,10 @@ int oracle_process_batch(const void *table, uint64_t num_sigs, const int32_t *pa
         std::vector<SeqHit> hits;
         std::vector<Call> calls;
         OtuStats otu;
+        oracle_best best{};
     };
+    const bool want_best = (want & WANT_BEST) != 0;
+    const std::vector<std::string> no_names;
     std::vector<PerSeq> res(n_seq);
     std::vector<uint64_t> probes(n_threads, 0), windows(n_threads, 0);
     const SigKmer *tab = (const SigKmer *)table;
@@ -580,10 +594,22 @@ int oracle_process_batch(const void *table, uint64_t num_sigs, const int32_t *pa
         for (uint64_t i = lo; i < hi; i++) {
             PerSeq &r = res[i];
             s.process(residues + offsets[i], offsets[i + 1] - offsets[i],
-                      (want & WANT_CALLS) ? &r.calls : nullptr,
+                      (want & (WANT_CALLS | WANT_BEST)) ? &r.calls : nullptr,
                       (want & WANT_HITS) ? &r.hits : nullptr,
                       (want & WANT_OTU) ? &r.otu : nullptr,
-                      (want & (WANT_CALLS | WANT_OTU)) != 0);
+                      (want & (WANT_CALLS | WANT_OTU | WANT_BEST)) != 0);
+            if (want_best) { /* lookup_request.cc:203-210: per sequence, in the worker */
+                std::string fn;
+                float off = 0.0f;
+                r.best.score_offset = std::numeric_limits<float>::quiet_NaN();
+                off = r.best.score_offset;
+                find_best_call(r.calls, no_names, r.best.function_index, fn, r.best.score, r.best.weighted_score,
+                               off);
+                r.best.offset_set = !std::isnan(off);
+                r.best.score_offset = r.best.offset_set ? off : 0.0f;
+                if (!(want & WANT_CALLS))
+                    r.calls.clear();
+            }
         }
         probes[t] = s.probes;
         windows[t] = s.windows;
@@ -640,6 +666,11 @@ int oracle_process_batch(const void *table, uint64_t num_sigs, const int32_t *pa
     out->hit_offsets[n_seq] = ih;
     out->call_offsets[n_seq] = ic;
     out->otu_offsets[n_seq] = io;
+    if (want_best) {
+        out->best = (oracle_best *)std::calloc(n_seq + 1, sizeof(oracle_best));
+        for (uint64_t i = 0; i < n_seq; i++)
+            out->best[i] = res[i].best;
+    }
     return 0;
 }
 
@@ -651,6 +682,7 @@ void oracle_result_free(oracle_result *r)
     std::free(r->calls);
     std::free(r->otu_offsets);
     std::free(r->otus);
+    std::free(r->best);
     std::memset(r, 0, sizeof(*r));
 }
 

@@ -32,10 +32,11 @@ echo "[collect] bench" >&2
 timeout -k 10 900 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "[collect] done" >&2
 # the measured P (mean buckets per window, from the bench's CPU-baseline leg) goes with the traffic
-python3 - "$OUT/bench.json" "$R/profiles/probe_traffic.json" <<'PY'
+python3 - "$OUT/bench.json" "$R/profiles/probe_traffic.json" "$TAG" <<'PY'
 import json, sys
 b = json.load(open(sys.argv[1]))
 t = json.load(open(sys.argv[2]))
+t["collected"] = f"{sys.argv[3]}: profiles/collect.sh {sys.argv[3]}"
 if b.get("cpu_baseline") and b["cpu_baseline"].get("pbar"):
     t["pbar_measured"] = b["cpu_baseline"]["pbar"]
     t["pbar_note"] = "mean buckets examined per window, counted by the oracle on the C2 batch (bench.py CPU-baseline leg)"

@@ -273,3 +273,53 @@ def test_svc_beside_batches_on_the_same_image(svc_image, oracle_lib):
         _check(oracle_lib, table, s, _tuple(PARAMS[0]), out[i][0], out[i][1], i)
     print(f"batches beside the service: {len(batch_ms)}, median {np.median(batch_ms):.2f} ms, "
           f"max {max(batch_ms):.2f} ms")
+
+
+def test_svc_stop_and_config_while_calling(svc_image, oracle_lib):
+    """kgx_svc_stop / kgx_svc_config from another thread while 16 callers are
+    inside kgx_svc_call: the shutdown waits for the calls in flight (no freed
+    slot memory under a caller), the next calls start a new service with the
+    new settings, and every answer stays exact."""
+    spec, table, img = svc_image
+    seqs = _seqs(spec, 1200, 61)
+    out = [None] * len(seqs)
+    errs = []
+    done = threading.Event()
+
+    def work(t, T):
+        try:
+            for i in range(t, len(seqs), T):
+                while True:
+                    try:
+                        out[i] = img.svc_call(seqs[i], PARAMS[i % 2])
+                        break
+                    except abi.KgxError as e:
+                        if e.code != abi.KGX_EBUSY:
+                            raise
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    def control():
+        k = 0
+        while not done.is_set():
+            if k % 2:
+                img.svc_stop()
+            else:
+                img.svc_config(8 + 8 * (k % 4), 100, 1000)
+            k += 1
+            time.sleep(0.002)
+
+    ws = [threading.Thread(target=work, args=(t, 16)) for t in range(16)]
+    ct = threading.Thread(target=control)
+    ct.start()
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    done.set()
+    ct.join()
+    assert not errs, errs[:3]
+    for i, s in enumerate(seqs):
+        _check(oracle_lib, table, s, _tuple(PARAMS[i % 2]), out[i][0], out[i][1], i)
+    img.svc_config(32, 1000, 1000)
+    assert img.svc_stat("slots") == 32 and img.svc_stat("broken") == 0

@@ -130,3 +130,71 @@ def test_matrix_matches_oracle(table_world, gpu, oracle_lib):
         assert np.array_equal(got["id1"], id1)
         assert np.array_equal(got["id2"], id2)
         assert np.array_equal(got["count"], cnt)
+
+
+def _on_hit_rollup(hit_kmers, orc_kmap, family):
+    """LookupRequest::on_hit (lookup_request.cc:446-482) over one sequence's
+    hits in position order: {id: [hit_count, hit_total, weighted_total]} in
+    first-touch order (a dict keeps insertion order), f32 sums hit by hit."""
+    d = {}
+    for k in hit_kmers:
+        lst = orc_kmap.lookup(int(k))
+        if len(lst) == 0:
+            continue
+        w = np.float32(1.0) / np.float32(len(lst))
+        for i in lst.tolist():
+            e = d.setdefault(i, [0, 0, np.float32(0.0)])
+            e[0] += 1
+            if family:
+                e[1] += 1
+                e[2] = np.float32(e[2] + w)
+    return d
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kmap_rollup_matches_on_hit(table_world, gpu, oracle_lib, mode):
+    """Device rollups (kgx_kmap_rollup) == on_hit replayed over the oracle's
+    hits and lists: k-mers mapping to 1-9 ids out of a small pool (tied
+    weighted totals), repeated ids in peg lists, unmapped hits, empty and
+    hit-free sequences, ids with a high bit."""
+    spec, table, img, ctx = table_world
+    rng = np.random.default_rng(31 + mode)
+    seqs = _family_proteins(spec, rng, 14, 4) + [b"", b"ACDEFGH", bytes(synth.ALPHA[rng.integers(0, 20, 400)])]
+    order = rng.permutation(len(seqs))
+    seqs = [seqs[i] for i in order]
+    hoff, hk, res, off = _oracle_hit_kmers(oracle_lib, table, seqs)
+    uk = np.unique(hk)
+    mapped = uk[rng.random(len(uk)) < 0.8]
+    pool = np.array([3, 7, 11, 12, 40, 41, 1000, 77777, (1 << 31) + 5], np.uint32)
+    kms, ids = [], []
+    for k in mapped:
+        n = int(rng.integers(1, 10))
+        sel = pool[rng.integers(0, len(pool), n)]
+        kms.append(np.full(n, k, np.uint64))
+        ids.append(sel)
+    kms, ids = np.concatenate(kms), np.concatenate(ids)
+    orc = oracle_lib.Kmap(1 if mode == 1 else 0)
+    orc.add(kms, ids)
+    family = mode == gpu.ROLLUP_FAMILY
+    with gpu.Kmap(0, 1 if family else 0) as dev:
+        dev.add(kms, ids)
+        for want in (0, 1, 3):
+            ctx.process_batch(res, off, want=want)
+            roff, rows = dev.rollup(ctx, mode)
+            assert len(roff) == len(seqs) + 1
+            n_tied = 0
+            for s in range(len(seqs)):
+                exp = _on_hit_rollup(hk[int(hoff[s]):int(hoff[s + 1])], orc, family)
+                got = rows[int(roff[s]):int(roff[s + 1])]
+                assert got["id"].tolist() == list(exp.keys()), s
+                assert got["hit_count"].tolist() == [v[0] for v in exp.values()], s
+                assert got["hit_total"].tolist() == [v[1] for v in exp.values()], s
+                wexp = np.array([v[2] for v in exp.values()], np.float32)
+                assert np.array_equal(got["weighted_total"].view(np.uint32), wexp.view(np.uint32)), s
+                n_tied += len(wexp) - len(np.unique(wexp))
+            if family:
+                assert n_tied > 0  # the pool makes equal weighted totals within a sequence
+    # an empty mapping: every sequence without rows
+    with gpu.Kmap(0, 1) as empty:
+        roff, rows = empty.rollup(ctx, gpu.ROLLUP_FAMILY)
+        assert len(rows) == 0 and not roff.any()
