@@ -234,6 +234,8 @@ SIGNATURES = {
     "kgx_event_elapsed_ms": (_INT, [_P, _P, ctypes.POINTER(ctypes.c_float)]),
     "kgx_device_alloc": (_INT, [_INT, _U64, _PP]),
     "kgx_device_free": (_INT, [_P]),
+    "kgx_host_alloc": (_INT, [_U64, _PP]),
+    "kgx_host_free": (_INT, [_P]),
     "kgx_memcpy_h2d": (_INT, [_P, _P, _U64]),
     "kgx_memcpy_d2h": (_INT, [_P, _P, _U64]),
     "kgx_ctx_synchronize": (_INT, [_P]),

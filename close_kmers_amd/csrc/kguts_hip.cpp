@@ -1376,27 +1376,29 @@ namespace {
 
 enum { FQ_START, FQ_ID, FQ_DEF, FQ_DATA, FQ_PLUS_START, FQ_PLUS, FQ_QUAL };
 
+/* every byte a letter (isalpha in the C locale: A-Z, a-z): a branch-free
+ * reduction the compiler vectorises */
+inline bool all_letters(const char *s, size_t n)
+{
+    unsigned bad = 0;
+    for (size_t i = 0; i < n; i++)
+        bad |= (unsigned)((unsigned char)((unsigned char)s[i] | 0x20u) - (unsigned char)'a') >= 26u;
+    return bad == 0;
+}
+
+inline bool is_letter(char c) { return (unsigned char)((unsigned char)c | 0x20u) - (unsigned char)'a' < 26u; }
+
 /* FastqParser::parse_char (fastq_parser.h:40-150), line-at-a-time, over
  * [p, end): the id runs to the first blank, sequence lines keep isalpha()
  * characters only (others are reported there and dropped), '+' and quality
  * lines are skipped; a record is emitted at the quality line's newline.  The
- * current record's residues are built in place at the end of `bases`;
- * `state` and `id` carry the parser across calls. */
-void fq_parse(const char *p, const char *end, int &state, std::string &id, std::string &bases,
+ * current record's residues are built in place at the end of `bases` (the
+ * caller sizes it: at most one byte per byte parsed); `state` and `id` carry
+ * the parser across calls. */
+void fq_parse(const char *p, const char *end, int &state, std::string &id, char *bases, size_t &n_bases,
               std::vector<uint64_t> &roff, std::string &id_chars, std::vector<uint64_t> &id_off)
 {
-    static const auto alpha = [] {
-        std::array<bool, 256> t{};
-        for (int c = 'A'; c <= 'Z'; c++)
-            t[c] = t[c + 32] = true;
-        return t;
-    }();
-    auto emit = [&]() {
-        id_chars += id;
-        id_off.push_back(id_chars.size());
-        roff.push_back(bases.size());
-        id.clear();
-    };
+    size_t nb = n_bases;
     while (p < end) {
         switch (state) {
         case FQ_START:
@@ -1404,13 +1406,13 @@ void fq_parse(const char *p, const char *end, int &state, std::string &id, std::
                 state = FQ_ID;
             break;
         case FQ_ID: {
-            const char c = *p++;
-            if (c == ' ' || c == '\t')
-                state = FQ_DEF;
-            else if (c == '\n')
-                state = FQ_DATA;
-            else
-                id.push_back(c);
+            const char *q = p;
+            while (q < end && *q != ' ' && *q != '\t' && *q != '\n')
+                q++;
+            id.append(p, (size_t)(q - p));
+            if (q < end)
+                state = *q == '\n' ? FQ_DATA : FQ_DEF;
+            p = q < end ? q + 1 : end;
             break;
         }
         case FQ_DEF:
@@ -1422,8 +1424,11 @@ void fq_parse(const char *p, const char *end, int &state, std::string &id, std::
                 break;
             }
             p = nl + 1;
-            if (state == FQ_QUAL) {
-                emit();
+            if (state == FQ_QUAL) { /* emit */
+                id_chars += id;
+                id_off.push_back(id_chars.size());
+                roff.push_back(nb);
+                id.clear();
                 state = FQ_START;
             } else {
                 state = state == FQ_DEF ? FQ_DATA : FQ_QUAL;
@@ -1433,13 +1438,16 @@ void fq_parse(const char *p, const char *end, int &state, std::string &id, std::
         case FQ_DATA: {
             const char *nl = static_cast<const char *>(std::memchr(p, '\n', (size_t)(end - p)));
             const char *stop = nl ? nl : end;
-            const char *q = p;
-            while (q < stop && alpha[(unsigned char)*q])
-                q++;
-            bases.append(p, (size_t)(q - p)); /* the all-letter prefix in one go */
-            for (p = q; p < stop; p++)
-                if (alpha[(unsigned char)*p])
-                    bases.push_back(*p);
+            const size_t L = (size_t)(stop - p);
+            if (all_letters(p, L)) { /* the usual line: copied whole */
+                std::memcpy(bases + nb, p, L);
+                nb += L;
+            } else {
+                for (const char *q = p; q < stop; q++)
+                    if (is_letter(*q))
+                        bases[nb++] = *q;
+            }
+            p = stop;
             if (nl) {
                 p = nl + 1;
                 state = FQ_PLUS_START;
@@ -1452,6 +1460,7 @@ void fq_parse(const char *p, const char *end, int &state, std::string &id, std::
             break;
         }
     }
+    n_bases = nb;
 }
 
 /* a place to cut a FASTQ block for a parallel parse: a line that starts
@@ -1480,155 +1489,245 @@ const char *fq_cut_after(const char *p, const char *end)
 
 }  // namespace
 
+FqRequest::FqPart::~FqPart()
+{
+    if (bases)
+        kgx_host_free(bases);
+}
+
+void FqRequest::FqPart::begin(size_t need, int st, const std::string &carried_id, const std::string &carried_bases)
+{
+    if (need > cap) {
+        if (bases)
+            kgx_host_free(bases);
+        bases = nullptr;
+        cap = 0;
+        void *q = nullptr;
+        const size_t want = need + need / 8 + 4096;
+        int rc = kgx_host_alloc(want, &q);
+        if (rc)
+            throw_last(rc, "kgx_host_alloc");
+        bases = static_cast<char *>(q);
+        cap = want;
+    }
+    state = st;
+    id = carried_id;
+    std::memcpy(bases, carried_bases.data(), carried_bases.size());
+    len = carried_bases.size();
+    roff.assign(1, 0);
+    id_off.assign(1, 0);
+    id_chars.clear();
+}
+
+void FqRequest::FqPart::parse(const char *a, const char *b)
+{
+    fq_parse(a, b, state, id, bases, len, roff, id_chars, id_off);
+}
+
+FqRequest::FqBlock FqRequest::FqPart::view() const
+{
+    FqBlock v;
+    v.res = bases;
+    v.roff = roff.data();
+    v.ids = id_chars.data();
+    v.id_off = id_off.data();
+    v.n = id_off.size() - 1;
+    return v;
+}
+
+/* The block is cut into parts of about kPartBytes at record starts
+ * (fq_cut_after).  Worker threads parse the parts ahead, in order, into
+ * pinned buffers (a ring of a few per worker); this thread takes them in
+ * order and runs each through the GPU (its bases go to the device by DMA from
+ * the part's buffer) and the frame choice, so parsing overlaps the device
+ * work.  Part 0 continues the carried parser state; the others start
+ * speculatively in the start state, and a part is used only if the exact
+ * sequential parse reaches its first byte in that state with nothing pending
+ * (the previous record emitted).  Otherwise the rest of the block is parsed
+ * again here from the true state.  So the reads, and the output, are the
+ * sequential parse's.  One FamilyMapper serves the whole block, as the
+ * reference keeps one per block (fq_process_request.cc:241). */
 void FqRequest::process(const char *text, size_t n, bool finished, std::ostream &os)
 {
+    /* KGX_FQ_PART_KB: the part size, for tests of the parallel parse */
+    const size_t kPartBytes = [] {
+        const char *e = std::getenv("KGX_FQ_PART_KB");
+        return e ? std::max<size_t>(4, std::strtoull(e, nullptr, 10)) << 10 : size_t(32) << 20;
+    }();
     const bool timing = std::getenv("KGX_FQ_TIMING") != nullptr;
-    const auto t_parse = std::chrono::steady_clock::now();
-    FqBlock blk;
-    /* the current record's residues are built in place at the end of
-     * blk.bases (a record cut by the block end is carried in seq_) */
-    blk.bases += seq_;
-    seq_.clear();
+    const auto t0 = std::chrono::steady_clock::now();
     const char *end = text + n;
-    /* Large blocks are parsed in parallel: cut at record starts
-     * (fq_cut_after), chunk 0 continues the carried parser state, the others
-     * start speculatively in the start state.  A chunk's parse is used only
-     * if the exact sequential parse reaches its first byte in that state with
-     * nothing pending (the previous record emitted); otherwise it is parsed
-     * again from the true state.  The result is the sequential parse's. */
     std::vector<const char *> cuts{text};
-    const size_t T = std::min<size_t>(16, n / (4u << 20));
-    for (size_t i = 1; i < T; i++) {
-        const char *c = fq_cut_after(text + n * i / T, end);
+    const size_t want_parts = n / kPartBytes;
+    for (size_t i = 1; i < want_parts; i++) {
+        const char *c = fq_cut_after(text + n * i / want_parts, end);
         if (c && c > cuts.back())
             cuts.push_back(c);
     }
     cuts.push_back(end);
     const size_t K = cuts.size() - 1;
-    if (K == 1) {
-        blk.bases.reserve(blk.bases.size() + n / 2);
-        fq_parse(text, end, state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
-    } else {
-        if (parts_.size() < K)
-            parts_.resize(K);
-        std::vector<std::thread> pool;
-        for (size_t k = 1; k < K; k++)
-            pool.emplace_back([&, k]() {
-                FqPart &pt = parts_[k];
-                pt.state = FQ_START;
-                pt.id.clear();
-                pt.bases.clear();
-                pt.id_chars.clear();
-                pt.roff.assign(1, 0);
-                pt.id_off.assign(1, 0);
-                fq_parse(cuts[k], cuts[k + 1], pt.state, pt.id, pt.bases, pt.roff, pt.id_chars, pt.id_off);
-            });
-        fq_parse(cuts[0], cuts[1], state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
-        for (auto &th : pool)
-            th.join();
-        pool.clear();
-        /* chunks 1 .. A-1 began where the sequential parse is at a record start */
-        size_t A = 1;
-        {
-            int st = state_;
-            bool idle = id_.empty() && blk.bases.size() == blk.roff.back();
-            while (A < K && st == FQ_START && idle) {
-                const FqPart &pt = parts_[A];
-                st = pt.state;
-                idle = pt.id.empty() && pt.bases.size() == pt.roff.back();
-                A++;
-            }
+    FamilyMapper mapper(kg_, mapping_);
+    double parse_wait_ms = 0.0, device_ms = 0.0;
+    /* the final part: the block's end state goes back to the request */
+    auto finish_part = [&](FqPart &pt) {
+        if (finished) { /* parse_complete() emits the last record */
+            pt.id_chars += pt.id;
+            pt.id_off.push_back(pt.id_chars.size());
+            pt.roff.push_back(pt.len);
+            pt.id.clear();
+            state_ = FQ_START;
+            id_.clear();
+            seq_.clear();
+        } else { /* the cut record's residues wait for the next block */
+            state_ = pt.state;
+            id_ = pt.id;
+            seq_.assign(pt.bases + pt.roff.back(), pt.len - pt.roff.back());
         }
-        if (A == K) { /* every speculation held: assemble in parallel */
-            std::vector<uint64_t> boff(K + 1, 0), roff_at(K + 1, 0), ioff(K + 1, 0), iat(K + 1, 0);
-            boff[1] = blk.bases.size();
-            roff_at[1] = blk.roff.size();
-            ioff[1] = blk.id_chars.size();
-            iat[1] = blk.id_off.size();
-            for (size_t k = 1; k < K; k++) {
-                const FqPart &pt = parts_[k];
-                boff[k + 1] = boff[k] + pt.bases.size();
-                roff_at[k + 1] = roff_at[k] + pt.roff.size() - 1;
-                ioff[k + 1] = ioff[k] + pt.id_chars.size();
-                iat[k + 1] = iat[k] + pt.id_off.size() - 1;
+    };
+    auto run_part = [&](const FqPart &pt) {
+        const auto d0 = std::chrono::steady_clock::now();
+        process_block(pt.view(), mapper, os);
+        device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d0).count();
+    };
+    if (K == 1) {
+        if (parts_.empty())
+            parts_.emplace_back(new FqPart);
+        FqPart &pt = *parts_[0];
+        pt.begin(seq_.size() + n, state_, id_, seq_);
+        pt.parse(text, end);
+        finish_part(pt);
+        run_part(pt);
+    } else {
+        const size_t W = std::min<size_t>(K, std::max<size_t>(1, std::min<size_t>(15, std::thread::hardware_concurrency() - 1)));
+        const size_t R = std::min(K, 2 * W + 2); /* parts in flight */
+        while (parts_.size() < R)
+            parts_.emplace_back(new FqPart);
+        std::mutex mu;
+        std::condition_variable cv;
+        size_t next = 0, consumed = 0;
+        bool abort = false;
+        std::vector<size_t> ready(R, SIZE_MAX); /* ring slot -> the part it holds, parsed */
+        std::string err;
+        const int carried_state = state_;
+        const std::string carried_id = id_, carried_seq = seq_;
+        auto worker = [&]() {
+            for (;;) {
+                size_t k;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    if (abort || next >= K)
+                        return;
+                    k = next++;
+                    cv.wait(lk, [&] { return abort || k < consumed + R; });
+                    if (abort)
+                        return;
+                }
+                FqPart &pt = *parts_[k % R];
+                try {
+                    const size_t span = (size_t)(cuts[k + 1] - cuts[k]);
+                    if (k == 0)
+                        pt.begin(carried_seq.size() + span, carried_state, carried_id, carried_seq);
+                    else
+                        pt.begin(span, FQ_START, std::string(), std::string());
+                    pt.parse(cuts[k], cuts[k + 1]);
+                } catch (const std::exception &e) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    err = e.what();
+                    abort = true;
+                    cv.notify_all();
+                    return;
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                ready[k % R] = k;
+                cv.notify_all();
             }
-            if (joined_cap_ < boff[K]) {
-                joined_.reset(new char[boff[K]]);
-                joined_cap_ = boff[K];
+        };
+        std::vector<std::thread> pool;
+        for (size_t w = 0; w < W; w++)
+            pool.emplace_back(worker);
+        auto stop_workers = [&]() {
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                abort = true;
             }
-            char *jb = joined_.get();
-            blk.roff.resize(roff_at[K]);
-            blk.id_off.resize(iat[K]);
-            blk.id_chars.resize(ioff[K]);
-            std::memcpy(jb, blk.bases.data(), blk.bases.size());
-            for (size_t k = 1; k < K; k++)
-                pool.emplace_back([&, k]() {
-                    const FqPart &pt = parts_[k];
-                    std::memcpy(jb + boff[k], pt.bases.data(), pt.bases.size());
-                    std::memcpy(&blk.id_chars[ioff[k]], pt.id_chars.data(), pt.id_chars.size());
-                    for (size_t i = 1; i < pt.roff.size(); i++)
-                        blk.roff[roff_at[k] + i - 1] = boff[k] + pt.roff[i];
-                    for (size_t i = 1; i < pt.id_off.size(); i++)
-                        blk.id_off[iat[k] + i - 1] = ioff[k] + pt.id_off[i];
-                });
+            cv.notify_all();
             for (auto &th : pool)
                 th.join();
-            blk.joined = jb;
-            blk.joined_len = boff[K];
-            blk.bases.clear();
-            state_ = parts_[K - 1].state;
-            id_ = parts_[K - 1].id;
-        } else { /* a cut missed a record start: append the good chunks, parse the rest exactly */
-            for (size_t k = 1; k < K; k++) {
-                const FqPart &pt = parts_[k];
-                if (k >= A) {
-                    fq_parse(cuts[k], cuts[k + 1], state_, id_, blk.bases, blk.roff, blk.id_chars, blk.id_off);
-                    continue;
+            pool.clear();
+        };
+        try {
+            for (size_t k = 0; k < K; k++) {
+                const auto w0 = std::chrono::steady_clock::now();
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return ready[k % R] == k || !err.empty(); });
+                    if (!err.empty())
+                        throw std::runtime_error(err);
                 }
-                const uint64_t base = blk.bases.size(), ibase = blk.id_chars.size();
-                blk.bases += pt.bases;
-                blk.id_chars += pt.id_chars;
-                for (size_t i = 1; i < pt.roff.size(); i++)
-                    blk.roff.push_back(base + pt.roff[i]);
-                for (size_t i = 1; i < pt.id_off.size(); i++)
-                    blk.id_off.push_back(ibase + pt.id_off[i]);
-                state_ = pt.state;
-                id_ = pt.id;
+                parse_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+                FqPart &pt = *parts_[k % R];
+                if (k + 1 < K) {
+                    /* the speculation of part k + 1 holds iff part k ends at a
+                     * record start with nothing pending */
+                    const bool holds = pt.state == FQ_START && pt.id.empty() && pt.len == pt.roff.back();
+                    if (!holds) {
+                        stop_workers();
+                        /* the rest of the block, exactly, from part k's end state */
+                        FqPart tail;
+                        tail.begin((size_t)(end - cuts[k + 1]) + (pt.len - pt.roff.back()), pt.state, pt.id,
+                                   std::string(pt.bases + pt.roff.back(), pt.len - pt.roff.back()));
+                        pt.len = pt.roff.back();
+                        pt.state = FQ_START;
+                        pt.id.clear();
+                        run_part(pt);
+                        tail.parse(cuts[k + 1], end);
+                        finish_part(tail);
+                        run_part(tail);
+                        break;
+                    }
+                    run_part(pt);
+                } else {
+                    finish_part(pt);
+                    run_part(pt);
+                }
+                std::lock_guard<std::mutex> lk(mu);
+                ready[k % R] = SIZE_MAX;
+                consumed = k + 1;
+                cv.notify_all();
             }
+        } catch (...) {
+            stop_workers();
+            throw;
         }
-    }
-    if (finished) { /* parse_complete() emits the last record */
-        blk.id_chars += id_;
-        blk.id_off.push_back(blk.id_chars.size());
-        blk.roff.push_back(blk.residues_len());
-        id_.clear();
-    } else { /* the cut record's residues wait for the next block */
-        seq_.assign(blk.residues() + blk.roff.back(), blk.residues_len() - blk.roff.back());
-        if (blk.joined)
-            blk.joined_len = blk.roff.back();
-        else
-            blk.bases.resize(blk.roff.back());
+        stop_workers();
     }
     if (timing)
-        std::fprintf(stderr, "[fq] %-12s %8.3f ms (%zu chunks)\n", "parse",
-                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_parse).count(),
-                     K);
-    process_block(blk, os);
+        std::fprintf(stderr, "[fq] block %.1f MB in %zu part(s): %.3f ms, waiting for the parse %.3f ms, device + "
+                             "frame choice %.3f ms\n",
+                     n / 1e6, K,
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                     parse_wait_ms, device_ms);
 }
 
 void FqRequest::process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os)
 {
-    FqBlock blk;
+    size_t nb = 0;
+    for (auto &r : reads)
+        nb += r.second.size();
+    FqPart pt;
+    pt.begin(nb, FQ_START, std::string(), std::string());
     for (auto &r : reads) {
-        blk.id_chars += r.first;
-        blk.id_off.push_back(blk.id_chars.size());
-        blk.bases += r.second;
-        blk.roff.push_back(blk.bases.size());
+        pt.id_chars += r.first;
+        pt.id_off.push_back(pt.id_chars.size());
+        std::memcpy(pt.bases + pt.len, r.second.data(), r.second.size());
+        pt.len += r.second.size();
+        pt.roff.push_back(pt.len);
     }
-    process_block(blk, os);
+    FamilyMapper mapper(kg_, mapping_);
+    process_block(pt.view(), mapper, os);
 }
 
-void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
+void FqRequest::process_block(const FqBlock &blk, FamilyMapper &mapper, std::ostream &os)
 {
     const uint32_t n_reads = (uint32_t)blk.n_reads();
     if (n_reads == 0)
@@ -1654,7 +1753,7 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
     if (rc)
         throw_last(rc, "kgx_ctx_set_option");
-    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff.data(), n_reads, &fr);
+    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff, n_reads, &fr);
     if (rc)
         throw_last(rc, "kgx_fq_fragments");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
@@ -1681,7 +1780,6 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
         if ((rc = kgx_fq_called_reads(ctx, &fr, &cr)))
             throw_last(rc, "kgx_fq_called_reads");
         mark("collect");
-        FamilyMapper mapper(kg_, mapping_);
         std::vector<KmerCall> calls;
         std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
         std::vector<uint32_t> match_len, best_len;
@@ -1766,7 +1864,6 @@ void FqRequest::process_block(const FqBlock &blk, std::ostream &os)
     std::vector<uint64_t> slice;
     mark("family lists");
     /* on_parsed_seq (fq_process_request.cc:298-365), reads in order */
-    FamilyMapper mapper(kg_, mapping_);
     std::vector<KmerCall> calls;
     std::vector<std::pair<size_t, FamilyMapper::best_match_t>> best_matches, matches;
     std::vector<uint64_t> match_frag, best_frag;

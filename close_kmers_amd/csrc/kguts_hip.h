@@ -476,36 +476,45 @@ public:
     void process_reads(const std::vector<std::pair<std::string, std::string>> &reads, std::ostream &os);
 
 private:
-    /* parsed reads, flat: read r's id is id_chars[id_off[r], id_off[r+1]),
-     * its bases [roff[r], roff[r+1]) of the residues */
+    /* parsed reads, flat (a view): read r's id is ids[id_off[r], id_off[r+1]),
+     * its bases res[roff[r], roff[r+1]) */
     struct FqBlock {
-        std::string bases; /* the bases of a one-piece parse */
-        std::string id_chars;
-        std::vector<uint64_t> id_off{0};
-        std::vector<uint64_t> roff{0};
-        const char *joined = nullptr; /* the bases of a parallel parse, assembled (FqRequest::joined_) */
-        uint64_t joined_len = 0;
-        const char *residues() const { return joined ? joined : bases.data(); }
-        uint64_t residues_len() const { return joined ? joined_len : bases.size(); }
-        size_t n_reads() const { return id_off.size() - 1; }
-        const char *id(size_t r) const { return id_chars.data() + id_off[r]; }
+        const char *res = nullptr;
+        const uint64_t *roff = nullptr;
+        const char *ids = nullptr;
+        const uint64_t *id_off = nullptr;
+        size_t n = 0;
+        const char *residues() const { return res; }
+        size_t n_reads() const { return n; }
+        const char *id(size_t r) const { return ids + id_off[r]; }
         size_t id_len(size_t r) const { return (size_t)(id_off[r + 1] - id_off[r]); }
     };
-    /* a parallel parse's chunk (kept across blocks, so its buffers are reused) */
+    /* one part of a block, parsed: its reads' bases in pinned host memory
+     * (kgx_host_alloc; the device copies them from there), offsets, ids, and
+     * the parser state at its end.  Kept across blocks (buffers reused). */
     struct FqPart {
         int state = 0;
-        std::string id, bases, id_chars;
+        std::string id;
+        char *bases = nullptr;
+        size_t cap = 0, len = 0;
         std::vector<uint64_t> roff{0}, id_off{0};
+        std::string id_chars;
+        FqPart() = default;
+        FqPart(const FqPart &) = delete;
+        FqPart &operator=(const FqPart &) = delete;
+        ~FqPart();
+        /* empty, from a parser state, room for `need` bases */
+        void begin(size_t need, int state, const std::string &carried_id, const std::string &carried_bases);
+        void parse(const char *a, const char *b);
+        FqBlock view() const;
     };
-    void process_block(const FqBlock &blk, std::ostream &os);
+    void process_block(const FqBlock &blk, FamilyMapper &mapper, std::ostream &os);
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     /* FastqParser state (fastq_parser.h:40-150) */
     int state_ = 0;
     std::string id_, seq_;
-    std::vector<FqPart> parts_;
-    std::unique_ptr<char[]> joined_;
-    size_t joined_cap_ = 0;
+    std::vector<std::unique_ptr<FqPart>> parts_;
 };
 
 /* one host-buffer batch through kg's context, device results only (no D2H):

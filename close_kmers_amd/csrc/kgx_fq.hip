@@ -1405,10 +1405,21 @@ int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets
     }
     HIP_TRY(c->fq_bases.reserve(nb + 16));
     HIP_TRY(c->fq_roff.reserve(((uint64_t)n_reads + 1) * 8));
-    if (nb) { /* through the context's pinned staging: DMA at link speed */
-        HIP_TRY(c->h_res.resize(nb));
-        parallel_memcpy(c->h_res.data(), bases + r0, nb);
-        HIP_TRY(hipMemcpyAsync(c->fq_bases.p, c->h_res.data(), nb, hipMemcpyHostToDevice, c->stream));
+    if (nb) {
+        /* bases in pinned memory (kgx_host_alloc) go by DMA straight from
+         * there; others through the context's pinned staging.  Either way the
+         * copy is done before this call returns (fq_fragments waits for the
+         * batch's sizes behind it). */
+        hipPointerAttribute_t attr{};
+        const bool pinned = hipPointerGetAttributes(&attr, bases + r0) == hipSuccess &&
+                            attr.type == hipMemoryTypeHost;
+        if (!pinned) {
+            (void)hipGetLastError(); /* an unregistered pointer is not an error here */
+            HIP_TRY(c->h_res.resize(nb));
+            parallel_memcpy(c->h_res.data(), bases + r0, nb);
+        }
+        HIP_TRY(hipMemcpyAsync(c->fq_bases.p, pinned ? static_cast<const void *>(bases + r0) : c->h_res.data(), nb,
+                               hipMemcpyHostToDevice, c->stream));
     }
     HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
     return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, nb, nb, out);

@@ -3083,6 +3083,27 @@ int kgx_device_free(void *p)
     return KGX_OK;
 }
 
+int kgx_host_alloc(uint64_t nbytes, void **out)
+{
+    if (!out)
+        return fail(KGX_EINVAL, "null output");
+    *out = nullptr;
+    /* portable: usable by every device's copies (the pool's replicas) */
+    hipError_t e = hipHostMalloc(out, std::max<uint64_t>(nbytes, 1), hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(KGX_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    return KGX_OK;
+}
+
+int kgx_host_free(void *p)
+{
+    if (p)
+        HIP_TRY(hipHostFree(p));
+    return KGX_OK;
+}
+
 int kgx_memcpy_h2d(void *dst, const void *src, uint64_t n)
 {
     HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));

@@ -93,6 +93,7 @@ struct SvcState {
     std::atomic<bool> broken{false}; /* a launch failed or a call timed out: callers take other paths */
     std::atomic<uint32_t> users{0};  /* callers inside kgx_svc_call holding this state */
     std::atomic<uint64_t> n_abandoned{0}; /* slots given up after a 10-s wait (never handed out again) */
+    int priority = 0; /* the stream's priority (hipDeviceGetStreamPriorityRange: lower = higher) */
 };
 
 namespace {
@@ -241,8 +242,23 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     hipError_t e = hipHostMalloc(&h, total, hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess)
         e = hipHostGetDevicePointer(&d, h, 0);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        /* the service's stream gets a hardware queue of its own: a queue is a
+         * FIFO, so a batch kernel whose stream shared the service's queue
+         * waited behind the enqueued persistent instances (r3z: 2,000-protein
+         * batches beside 8 service callers, median 3.0 ms / max 28 ms vs 1.3 ms
+         * alone).  The runtime keeps a queue pool per stream priority, so the
+         * high-priority stream never shares with the contexts' (normal)
+         * streams; KGX_SVC_PRIORITY=normal restores the old placement. */
+        int least = 0, greatest = 0;
+        const char *pe = std::getenv("KGX_SVC_PRIORITY");
+        const bool normal = pe && std::string(pe) == "normal";
+        if (!normal && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
+            e = hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, greatest);
+        else
+            e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+        s->priority = normal ? 0 : greatest;
+    }
     s->host = static_cast<char *>(h);
     if (e != hipSuccess) {
         destroy(s);
@@ -406,6 +422,8 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? s->n_abandoned.load() : 0;
     else if (n == "broken") /* 1: the service turns every call away until kgx_svc_stop */
         *value = s && s->broken ? 1 : 0;
+    else if (n == "priority") /* the service stream's priority + 100 (lower = higher priority) */
+        *value = s ? (uint64_t)(s->priority + 100) : 0;
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
     else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '5') /* "phase_n0".."phase_n5" */

@@ -461,6 +461,10 @@ int kgx_svc_stop(kgx_image *img);
  * wait), "broken" (1: calls are turned away until the service is replaced),
  * "devmem" (1: requests are written into fine-grained device memory through a
  * large BAR, else mapped host memory; KGX_SVC_DEVMEM=0 forces the latter),
+ * "priority" (100 + the service stream's priority; the stream is created at
+ * the device's highest priority, so it has a hardware queue of its own and
+ * batch streams never queue behind the persistent instances;
+ * KGX_SVC_PRIORITY=normal gives it a normal stream),
  * "phase_n0".."phase_n5" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
  * call and the device phases) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
@@ -756,6 +760,11 @@ int kgx_event_elapsed_ms(void *start, void *end, float *ms);
 /* Device memory helpers for callers without their own allocator. */
 int kgx_device_alloc(int device, uint64_t nbytes, void **out);
 int kgx_device_free(void *p);
+/* Pinned (page-locked, portable) host memory.  Batch inputs that live in it
+ * reach the device by DMA straight from there (kgx_fq_fragments skips its
+ * staging copy for such bases). */
+int kgx_host_alloc(uint64_t nbytes, void **out);
+int kgx_host_free(void *p);
 int kgx_memcpy_h2d(void *dst, const void *src, uint64_t nbytes);
 int kgx_memcpy_d2h(void *dst, const void *src, uint64_t nbytes);
 int kgx_ctx_synchronize(kgx_ctx *ctx);

@@ -303,7 +303,7 @@ _BACK = {"A": "GCT", "C": "TGT", "D": "GAT", "E": "GAA", "F": "TTT", "G": "GGT",
          "T": "ACT", "V": "GTT", "W": "TGG", "Y": "TAT"}
 
 
-def test_fq_handler_parallel_parse_matches_oracle(gpu, oracle_lib, tmp_path):
+def test_fq_handler_parallel_parse_matches_oracle(gpu, oracle_lib, tmp_path, monkeypatch):
     """A 40 MB FASTQ block is parsed by several threads (cut at record starts,
     each cut checked against the sequential parse): the handler's output must
     equal the oracle's, with irregular records at and around the cuts
@@ -342,10 +342,44 @@ def test_fq_handler_parallel_parse_matches_oracle(gpu, oracle_lib, tmp_path):
     assert want.count(b"\n") > 50000
     with gpu.Image.from_table(table) as img, gpu.FqHandler(img, d) as fq:
         assert fq.process(fastq, True) == want
+        # parts of 1 MiB: ~40 parts parsed ahead by the worker threads
+        monkeypatch.setenv("KGX_FQ_PART_KB", "1024")
+        assert fq.process(fastq, True) == want
+        monkeypatch.delenv("KGX_FQ_PART_KB")
     with gpu.Image.from_table(table) as img, gpu.FqHandler(img, d) as fq:
         cuts = [0] + sorted(int(x) for x in rng.integers(1, len(fastq), 12)) + [len(fastq)]
         out = b"".join(fq.process(fastq[a:b], b == len(fastq)) for a, b in zip(cuts, cuts[1:]))
     assert out == want
+
+
+def test_fq_handler_fooled_cuts_match_oracle(gpu, oracle_lib, tmp_path, monkeypatch):
+    """Every quality line starts with '@' and every sequence line with '+'
+    (dropped by the parser as a non-letter), so a quality line followed two
+    lines on by a '+' line looks like a record start to the cut search: many
+    of a block's part boundaries are not record starts, the speculative parse
+    of such a part is refused, and the rest of the block is parsed exactly
+    from the true state.  The output must still be the oracle's."""
+    from close_kmers_amd import synth
+    from helpers import data_dir_for
+    spec, table = synthetic_table(30000)
+    d = data_dir_for(str(tmp_path), table)
+    rng = np.random.default_rng(77)
+    src = synth.ALPHA[synth.source_residue_codes(np.arange(spec.n_src))].reshape(spec.n_src, -1)
+    recs = []
+    for i in range(6000):
+        p = bytes(src[int(rng.integers(0, spec.n_src))]).decode()
+        a = int(rng.integers(0, len(p) - 50))
+        seq = "".join(_BACK[c] for c in p[a:a + 50])
+        recs.append(f"@q{i}\n+{seq}\n+\n@{'I' * len(seq)}\n")
+    fastq = "".join(recs).encode()
+    path = tmp_path / "fooled.fq"
+    path.write_bytes(fastq)
+    want = oracle_lib.query_text(d, str(path), "fq", {})
+    assert want.count(b"\n") > 1000
+    with gpu.Image.from_table(table) as img, gpu.FqHandler(img, d) as fq:
+        for kb in ("16", "40", "100000"):
+            monkeypatch.setenv("KGX_FQ_PART_KB", kb)
+            assert fq.process(fastq, True) == want, kb
 
 
 def test_fragments_start_finish_ahead_schedule(gpu):

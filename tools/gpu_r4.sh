@@ -11,9 +11,11 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 900 python3 -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python3 -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
 timeout -k 10 600 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
     --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
 timeout -k 10 600 python3 bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
+KGX_SVC_PRIORITY=normal timeout -k 10 300 python3 -u -m pytest tests/test_gpu_svc.py -m gpu -x -v -s -k beside --timeout 200 --timeout-method thread > "$OUT/svc_beside_normal.log" 2>&1
+timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
 timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool2.json" 2> "$OUT/bench_pool2.err"
 echo "[gpu_r4] done" >&2
