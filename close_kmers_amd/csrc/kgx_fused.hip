@@ -102,6 +102,108 @@ template <> struct FusedInput<FusedSlot> {
     __device__ static uint8_t res(const FusedArgs &, const FusedSlot &k, uint64_t i) { return k.res[i]; }
 };
 
+/* libstdc++'s std::sort (lstd_sort_on, kgx_lstd.h) of n <= 64 elements in
+ * LDS, replayed by one wave.  Each __unguarded_partition step is done at
+ * once: its left scan stops at the positions whose element is not less than
+ * the pivot (L_1 < L_2 < ...), its right scan at those the pivot is not less
+ * than (R_1 > R_2 > ...); the t-th swap exchanges L_t and R_t for as long as
+ * L_t < R_t, and the cut is min(L_{P+1}, R_P) after P swaps (a scan that
+ * runs past its last stop halts at the other's last swapped position).  So a
+ * lane that holds L_t swaps iff at least t R-stops lie above it, a lane that
+ * holds R_t iff at least t L-stops lie below it, and partners meet through
+ * two 64-entry buffers indexed by t.  The median-of-three and the range
+ * stack are uniform; a range whose depth budget runs out goes to the serial
+ * heap sort (lane 0), as std::sort's does.  The final insertion sort is a
+ * stable sort, so each lane places its element by counting.  comp must be a
+ * strict weak order.  buf: 192 elements of scratch; stack: 64 ranges. */
+template <class T, class C>
+__device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *stack)
+{
+    const uint32_t lane = lane_id();
+    T *bl = buf, *br = buf + 64, *bs = buf + 128;
+    if (n > 16) {
+        int sp = 0;
+        if (lane == 0)
+            stack[0] = LstdPart{0, (int64_t)n, 2 * (31 - (int)__builtin_clz(n))};
+        sp = 1;
+        wave_lds_sync();
+        while (sp) {
+            --sp;
+            LstdPart p = stack[sp];
+            wave_lds_sync();
+            int32_t f = (int32_t)p.first, l = (int32_t)p.last, depth = p.depth;
+            while (l - f > 16) {
+                if (depth == 0) {
+                    if (lane == 0)
+                        lstd_heap_sort(a + f, l - f, comp);
+                    wave_lds_sync();
+                    break;
+                }
+                --depth;
+                /* __move_median_to_first(first, first + 1, mid, last - 1) */
+                const int32_t mid = f + (l - f) / 2;
+                const T x = a[f + 1], y = a[mid], z = a[l - 1];
+                int32_t pick;
+                if (comp(x, y))
+                    pick = comp(y, z) ? mid : (comp(x, z) ? l - 1 : f + 1);
+                else
+                    pick = comp(x, z) ? f + 1 : (comp(y, z) ? l - 1 : mid);
+                const T first_v = a[f], pick_v = a[pick];
+                wave_lds_sync();
+                if (lane == 0) {
+                    a[f] = pick_v;
+                    a[pick] = first_v;
+                }
+                wave_lds_sync();
+                const T pivot = a[f];
+                const int32_t i = f + 1 + (int32_t)lane;
+                const bool in = i < l;
+                const T v = in ? a[i] : pivot;
+                const bool lf = in && !comp(v, pivot), rf = in && !comp(pivot, v);
+                const uint64_t LM = __ballot(lf), RM = __ballot(rf);
+                const uint32_t l_below = (uint32_t)__popcll(LM & lanes_le(lane) & ~(1ull << lane));
+                const uint32_t r_above = (uint32_t)__popcll(RM & ~lanes_le(lane));
+                const uint32_t rank_l = l_below + 1, rank_r = r_above + 1;
+                const bool swl = lf && rank_l <= r_above, swr = rf && rank_r <= l_below;
+                const uint32_t P = (uint32_t)__popcll(__ballot(swl));
+                if (swl)
+                    bl[rank_l - 1] = v;
+                if (swr)
+                    br[rank_r - 1] = v;
+                wave_lds_sync();
+                if (swl)
+                    a[i] = br[rank_l - 1];
+                else if (swr)
+                    a[i] = bl[rank_r - 1];
+                const uint64_t LN = __ballot(lf && rank_l == P + 1), RP = __ballot(P > 0 && rf && rank_r == P);
+                const int32_t lcut = LN ? f + 1 + (int32_t)lowbit(LN) : INT32_MAX;
+                const int32_t rcut = RP ? f + 1 + (int32_t)lowbit(RP) : INT32_MAX;
+                const int32_t cut = min(lcut, rcut);
+                wave_lds_sync();
+                if (lane == 0)
+                    stack[sp] = LstdPart{cut, l, depth}; /* __introsort_loop(cut, last) */
+                sp++;
+                l = cut;
+                wave_lds_sync();
+            }
+        }
+    }
+    /* __final_insertion_sort: stable, so by counting */
+    if (lane < n) {
+        const T v = a[lane];
+        uint32_t pos = 0;
+        for (uint32_t j = 0; j < n; j++) {
+            const T w = a[j];
+            pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
+        }
+        bs[pos] = v;
+    }
+    wave_lds_sync();
+    if (lane < n)
+        a[lane] = bs[lane];
+    wave_lds_sync();
+}
+
 template <uint32_t FJ, class IN>
 __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, const uint32_t s)
 {
@@ -429,6 +531,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     if (want_otu) {
         __shared__ uint32_t multi;
         __shared__ LstdPart ostack[64];
+        if (dbg)
+            a.dbg[7] = wall_clock64();
         if (t == 0)
             multi = 0;
         __syncthreads();
@@ -489,23 +593,25 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 r += (first[j] && v[j] < x) ? 1u : 0u;
             o[r] = kgx_otu{x, (int32_t)cnt[i]};
         }
-        if (t == 0) {
-            if (one) {
-                o[0] = kgx_otu{v0, (int32_t)m};
-                n_otu = 1;
-            } else {
-                uint32_t d = 0;
-                for (uint32_t j = 0; j < m; j++)
-                    d += first[j];
-                n_otu = d;
-            }
-        }
+        /* distinct values: a block-wide count of the firsts (no serial scan) */
+        uint32_t d = one ? 1u : 0u;
+        for (uint32_t j0 = 0; j0 < (one ? 0u : m); j0 += 256)
+            d += (uint32_t)__syncthreads_count(j0 + t < m && first[j0 + t]);
+        if (one && t == 0)
+            o[0] = kgx_otu{v0, (int32_t)m};
         __syncthreads();
-        /* std::sort by count (lstd_sort_on: libstdc++'s introsort, its
+        /* std::sort by count (less_second, kguts.h:214-218): one wave replays
+         * it for up to 64 pairs (lstd_sort_wave64), thread 0 beyond (its
          * partition stack in LDS) */
-        if (t == 0 && n_otu > 1)
-            lstd_sort_on(o, (int64_t)n_otu, [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; },
-                         ostack);
+        const auto by_count = [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; };
+        if (d > 1 && d <= 64) {
+            if (wave == 0)
+                lstd_sort_wave64(o, d, by_count, o + 384 * FJ, ostack);
+        } else if (d > 64 && t == 0) {
+            lstd_sort_on(o, (int64_t)d, by_count, ostack);
+        }
+        if (t == 0)
+            n_otu = d;
         __syncthreads();
         for (uint32_t i = t; i < n_otu; i += 256)
             a.otus[wb + i] = o[i];

@@ -465,8 +465,8 @@ int kgx_svc_stop(kgx_image *img);
  * the device's highest priority, so it has a hardware queue of its own and
  * batch streams never queue behind the persistent instances;
  * KGX_SVC_PRIORITY=normal gives it a normal stream),
- * "phase_n0".."phase_n5" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
- * call and the device phases) */
+ * "phase_n0".."phase_n6" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
+ * call, the device phases, and the OTU tally of calls that want it) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option

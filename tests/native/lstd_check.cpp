@@ -31,6 +31,86 @@ static int fail(const char *what, long c)
     return 1;
 }
 
+/* a host emulation of lstd_sort_wave64 (kgx_fused.hip), one "lane" per
+ * element of a partition range: the partition by stop ranks (the t-th
+ * left stop swaps with the t-th right stop while L_t < R_t, cut =
+ * min(L_{P+1}, R_P)) and the final insertion sort as a stable sort by
+ * counting.  Checks the formulation the device replays against std::sort. */
+template <class T, class C> static void stops_sort(T *a, int n, C comp)
+{
+    struct Part {
+        int f, l, depth;
+    };
+    if (n > 16) {
+        std::vector<Part> st{{0, n, 2 * (31 - __builtin_clz((unsigned)n))}};
+        while (!st.empty()) {
+            Part p = st.back();
+            st.pop_back();
+            int f = p.f, l = p.l, depth = p.depth;
+            while (l - f > 16) {
+                if (depth == 0) {
+                    kgx::lstd_heap_sort(a + f, l - f, comp);
+                    break;
+                }
+                --depth;
+                const int mid = f + (l - f) / 2;
+                const T x = a[f + 1], y = a[mid], z = a[l - 1];
+                int pick;
+                if (comp(x, y))
+                    pick = comp(y, z) ? mid : (comp(x, z) ? l - 1 : f + 1);
+                else
+                    pick = comp(x, z) ? f + 1 : (comp(y, z) ? l - 1 : mid);
+                std::swap(a[f], a[pick]);
+                const T pivot = a[f];
+                const int len = l - f - 1;
+                std::vector<T> v(a + f + 1, a + l), bl(len), br(len);
+                std::vector<int> lf(len), rf(len), lb(len), ra(len);
+                for (int k = 0; k < len; k++) {
+                    lf[k] = !comp(v[k], pivot);
+                    rf[k] = !comp(pivot, v[k]);
+                }
+                for (int k = 0, c = 0; k < len; k++) {
+                    lb[k] = c;
+                    c += lf[k];
+                }
+                for (int k = len - 1, c = 0; k >= 0; k--) {
+                    ra[k] = c;
+                    c += rf[k];
+                }
+                int P = 0;
+                for (int k = 0; k < len; k++) {
+                    if (lf[k] && lb[k] + 1 <= ra[k]) {
+                        bl[lb[k]] = v[k];
+                        P++;
+                    }
+                    if (rf[k] && ra[k] + 1 <= lb[k])
+                        br[ra[k]] = v[k];
+                }
+                int lcut = 1 << 30, rcut = 1 << 30;
+                for (int k = 0; k < len; k++) {
+                    const bool swl = lf[k] && lb[k] + 1 <= ra[k], swr = rf[k] && ra[k] + 1 <= lb[k];
+                    a[f + 1 + k] = swl ? br[lb[k]] : swr ? bl[ra[k]] : v[k];
+                    if (lf[k] && lb[k] + 1 == P + 1 && lcut == (1 << 30))
+                        lcut = f + 1 + k;
+                    if (P > 0 && rf[k] && ra[k] + 1 == P && rcut == (1 << 30))
+                        rcut = f + 1 + k;
+                }
+                const int cut = std::min(lcut, rcut);
+                st.push_back({cut, l, depth});
+                l = cut;
+            }
+        }
+    }
+    std::vector<T> out(n);
+    for (int i = 0; i < n; i++) {
+        int pos = 0;
+        for (int j = 0; j < n; j++)
+            pos += comp(a[j], a[i]) || (j < i && !comp(a[i], a[j]));
+        out[pos] = a[i];
+    }
+    std::copy(out.begin(), out.end(), a);
+}
+
 int main(int argc, char **argv)
 {
     const long cases = argc > 1 ? std::atol(argv[1]) : 20000;
@@ -51,6 +131,19 @@ int main(int argc, char **argv)
         for (long i = 0; i < n; i++)
             if (a[i].otu_index != b[i].otu_index || a[i].count != b[i].count)
                 return fail("lstd_sort", c);
+        /* 1b. the wave replay's formulation, up to 64 elements (many ties) */
+        {
+            const long n2 = c % 4 ? uni(17, 64) : uni(0, 16);
+            std::vector<kgx_otu> w(n2), ws;
+            for (long i = 0; i < n2; i++)
+                w[i] = kgx_otu{(int32_t)i, (int32_t)uni(0, c % 3 ? keys : 2)};
+            ws = w;
+            std::sort(ws.begin(), ws.end(), less_second);
+            stops_sort(w.data(), (int)n2, less_second);
+            for (long i = 0; i < n2; i++)
+                if (w[i].otu_index != ws[i].otu_index || w[i].count != ws[i].count)
+                    return fail("stops_sort (lstd_sort_wave64's formulation)", c);
+        }
 
         /* 2. partial_sort(first, last, last) = the depth-limit fallback */
         std::vector<kgx_otu> p(n), q;

@@ -6,7 +6,7 @@
 set -euo pipefail
 TAG=${1:-r4}
 shift || true
-TESTS=${*:-tests/test_gpu_tables.py tests/test_server.py tests/test_gpu_fq.py tests/test_gpu_svc.py tests/test_canary.py}
+TESTS=${*:-tests/test_gpu_tables.py tests/test_server.py tests/test_gpu_fq.py tests/test_gpu_svc.py tests/test_canary.py tests/test_gpu_coalesce.py}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -18,4 +18,5 @@ timeout -k 10 600 python3 bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OU
 KGX_SVC_PRIORITY=normal timeout -k 10 300 python3 -u -m pytest tests/test_gpu_svc.py -m gpu -x -v -s -k beside --timeout 200 --timeout-method thread > "$OUT/svc_beside_normal.log" 2>&1
 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
 timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool2.json" 2> "$OUT/bench_pool2.err"
+KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
 echo "[gpu_r4] done" >&2
