@@ -1196,31 +1196,38 @@ LookupRequest::LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool famil
 void LookupRequest::process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
                                  std::ostream &os)
 {
+    std::string ids, res;
+    std::vector<uint64_t> id_off{0}, off{0};
+    for (const auto &w : work) {
+        ids += w.first;
+        id_off.push_back(ids.size());
+        res += w.second;
+        off.push_back(res.size());
+    }
+    process_flat(kg, res.data(), off.data(), ids.data(), id_off.data(), work.size(), os);
+}
+
+void LookupRequest::process_flat(KmerGuts &kg, const char *res, const uint64_t *off, const char *ids,
+                                 const uint64_t *id_off, size_t n_work, std::ostream &os)
+{
     /* pieces that keep the batch's hits on the device (one small-batch pass
      * each: at most 2M residues, 65,536 sequences) */
-    const size_t n_work = work.size();
+    const FlatWork fw{res, off, ids, id_off};
     size_t a = 0;
     while (a < n_work) {
-        size_t b = a, res = 0;
-        while (b < n_work && (b == a || (res + work[b].second.size() <= (size_t(1) << 21) && b - a < 65536)))
-            res += work[b++].second.size();
-        process_piece(kg, work, a, b, os);
+        size_t b = a + 1;
+        while (b < n_work && off[b + 1] - off[a] <= (uint64_t(1) << 21) && b - a < 65536)
+            b++;
+        process_piece(kg, fw, a, b, os);
         a = b;
     }
 }
 
-void LookupRequest::process_piece(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
-                                  size_t w0, size_t w1, std::ostream &os)
+void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, size_t w1, std::ostream &os)
 {
     const uint32_t n = (uint32_t)(w1 - w0);
     if (n == 0)
         return;
-    std::string buf;
-    std::vector<uint64_t> off(n + 1, 0);
-    for (uint32_t i = 0; i < n; i++) {
-        buf += work[w0 + i].second;
-        off[i + 1] = buf.size();
-    }
     const bool want_calls = find_best_match_ && family_mode_;
     kgx_params p{kg.min_hits, kg.max_gap, kg.order_constraint, kg.min_weighted_hits};
     kgx_result r;
@@ -1228,7 +1235,7 @@ void LookupRequest::process_piece(KmerGuts &kg, const std::vector<std::pair<std:
      * per sequence comes back, not the calls; the hits stay on the device,
      * where on_hit's rollups run (kgx_kmap_rollup) */
     const uint64_t g0 = now_ns(); /* gpu stage: the pass and the rollups */
-    int rc = kgx_process_batch(kg.ctx(), &p, buf.data(), off.data(), n, want_calls ? KGX_WANT_BEST : 0u, &r);
+    int rc = kgx_process_batch(kg.ctx(), &p, fw.res, fw.off + w0, n, want_calls ? KGX_WANT_BEST : 0u, &r);
     stage_stats().gpu_passes++;
     if (rc)
         throw_last(rc, "kgx_process_batch");
@@ -1243,7 +1250,8 @@ void LookupRequest::process_piece(KmerGuts &kg, const std::vector<std::pair<std:
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
     std::string line;
     for (uint32_t s = 0; s < n; s++) {
-        const std::string &id = work[w0 + s].first;
+        const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
+        const std::string id(fw.ids + ia, ib - ia);
         /* seq_score_ as the reference's operator[] calls leave it: the ids in
          * first-touch order into the request's one map (cleared per sequence,
          * its bucket count kept), so its iteration order is the reference's */

@@ -443,10 +443,20 @@ public:
     void process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
                       std::ostream &os);
 
+    /* the same over a flat work list: sequence i's residues res[off[i],
+     * off[i+1]), its id ids[id_off[i], id_off[i+1]) */
+    void process_flat(KmerGuts &kg, const char *res, const uint64_t *off, const char *ids, const uint64_t *id_off,
+                      size_t n, std::ostream &os);
+
 private:
-    /* work[w0, w1) as one GPU pass, its rollups on the device */
-    void process_piece(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work, size_t w0,
-                       size_t w1, std::ostream &os);
+    struct FlatWork {
+        const char *res;
+        const uint64_t *off;
+        const char *ids;
+        const uint64_t *id_off;
+    };
+    /* sequences [w0, w1) as one GPU pass, their rollups on the device */
+    void process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, size_t w1, std::ostream &os);
     std::shared_ptr<KmerPegMapping> mapping_;
     bool family_mode_;
     unsigned int kmer_hit_threshold_ = 3;

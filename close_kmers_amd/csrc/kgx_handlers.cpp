@@ -924,6 +924,18 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             fq_request(*kg, mapping, body, n, os);
             return os.str();
         }
+        if (action == "/lookup") { /* lookup_request.cc:146-150 */
+            FastaFlat flat;
+            {
+                StageClock clk(stage_stats().parse_ns);
+                flat = parse_fasta_body_flat(body, n);
+            }
+            os << header(ver, 200, "OK") << "\n";
+            LookupRequest lr(mapping, family_mode_, req.parameters);
+            lr.process_flat(*kg, flat.res.data(), flat.off.data(), flat.ids.data(), flat.id_off.data(), flat.size(),
+                            os);
+            return os.str();
+        }
         work_list_t work;
         {
             StageClock clk(stage_stats().parse_ns);

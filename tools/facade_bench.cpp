@@ -290,17 +290,80 @@ int main(int argc, char **argv)
                          "(a thread's call cycle %.2f us)\n", mode_name[co], T, nm / tp, (double)(residues * R) / tp,
                          pct(all, 50), pct(all, 99), mean(all), tp * 1e6 * T / nm);
         }
+    /* KGX_FACADE_BESIDE=T: T service callers (one KmerGuts each) and, at the
+     * same time, one batch caller (its own KmerGuts: process_aa_batch of the m
+     * proteins, over and over) on the same image -- a server whose pool mixes
+     * per-sequence calls and chunk batches (threadpool.cc:33-60).  Native
+     * threads: a Python harness's GIL would time itself. */
+    std::string beside_json;
+    if (const char *e = std::getenv("KGX_FACADE_BESIDE")) {
+        const int T = std::max(1, std::atoi(e));
+        std::vector<std::unique_ptr<kgx::KmerGuts>> kgs;
+        for (int t = 0; t <= T; t++) {
+            kgs.emplace_back(new kgx::KmerGuts(dir, image));
+            kgs.back()->coalesce = t < T;
+            kgs.back()->service = t < T;
+        }
+        auto batch_once = [&](kgx::KmerGuts &g) {
+            std::vector<kgx::KmerGuts::SeqJob> jobs(m);
+            for (size_t i = 0; i < m; i++) {
+                jobs[i].id = "q";
+                jobs[i].seq = seqs[i];
+                jobs[i].calls = std::make_shared<std::vector<kgx::KmerCall>>();
+                jobs[i].hit_cb = [](kgx::KmerGuts::hit_in_sequence_t) {};
+            }
+            const auto t0 = clk::now();
+            g.process_aa_batch(jobs);
+            return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        };
+        std::vector<double> alone;
+        for (int rep = 0; rep < 30; rep++)
+            alone.push_back(batch_once(*kgs[T]));
+        std::atomic<bool> stop{false};
+        std::atomic<uint64_t> n_calls{0};
+        std::vector<double> beside;
+        std::thread bt([&]() {
+            while (!stop.load())
+                beside.push_back(batch_once(*kgs[T]));
+        });
+        std::vector<std::thread> ws;
+        const auto t0 = clk::now();
+        for (int t = 0; t < T; t++)
+            ws.emplace_back([&, t]() {
+                for (size_t k = t; k < m * R; k += T) {
+                    auto cv = std::make_shared<std::vector<kgx::KmerCall>>();
+                    kgs[t]->process_aa_seq("q", seqs[k % m], cv, [](kgx::KmerGuts::hit_in_sequence_t) {}, nullptr);
+                    n_calls++;
+                }
+            });
+        for (auto &w : ws)
+            w.join();
+        const double tp = std::chrono::duration<double>(clk::now() - t0).count();
+        stop = true;
+        bt.join();
+        char b[400];
+        std::snprintf(b, sizeof b,
+                      ", \"beside\": {\"service_threads\": %d, \"batch_proteins\": %zu, \"batch_alone_ms\": {\"p50\": %.3f, "
+                      "\"max\": %.3f}, \"batch_beside_ms\": {\"n\": %zu, \"p50\": %.3f, \"p90\": %.3f, \"max\": %.3f}, "
+                      "\"service_calls_per_s\": %.4g}",
+                      T, m, pct(alone, 50), pct(alone, 100), beside.size(), pct(beside, 50), pct(beside, 90),
+                      pct(beside, 100), (double)n_calls / tp);
+        beside_json = b;
+        std::fprintf(stderr, "[facade] beside %d service callers: batch of %zu alone p50 %.3f ms, beside p50 %.3f p90 %.3f "
+                     "max %.3f ms (%zu batches); service %.4g calls/s\n", T, m, pct(alone, 50), pct(beside, 50),
+                     pct(beside, 90), pct(beside, 100), beside.size(), (double)n_calls / tp);
+    }
     std::printf("{\"metric\": \"KmerGuts facade per-call latency (process_aa_seq, one 300-aa C2 protein per call)\", "
                 "\"calls\": %zu, \"latency_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"mean\": %.1f}, "
                 "\"latency_us_ordinary_path\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f}, "
                 "\"unbatched_residues_per_s\": %.4g, \"batched\": {\"sequences\": %zu, \"ms\": %.3f, "
                 "\"residues_per_s\": %.4g}, \"hits\": %llu, \"calls_out\": %llu, \"batch_hits_per_rep\": %llu, "
                 "\"batch_calls\": %llu, \"keys_stored\": %llu, \"pass_latency_by_batch\": {%s}, "
-                "\"worker_pool_by_threads\": {%s}}\n",
+                "\"worker_pool_by_threads\": {%s}%s}\n",
                 m, pct(lat, 50), pct(lat, 90), pct(lat, 99), t_seq * 1e6 / (double)m, pct(lat0, 50), pct(lat0, 90),
                 pct(lat0, 99), (double)residues / t_seq, m,
                 t_batch * 1e3, (double)residues / t_batch, (unsigned long long)hits, (unsigned long long)calls,
                 (unsigned long long)(bhits / 6), (unsigned long long)bcalls, (unsigned long long)stored,
-                bs_json.c_str(), pool_json.c_str());
+                bs_json.c_str(), pool_json.c_str(), beside_json.c_str());
     return hits * 6 == bhits && calls == bcalls && hits == hits0 && calls == calls0 && pool_ok ? 0 : 3;
 }
