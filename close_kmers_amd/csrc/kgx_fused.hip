@@ -63,7 +63,7 @@ struct FusedMapped { /* the mapped arrays instead (FusedArgs.res / off / wbase) 
 
 /* FJ = windows per thread at most (the batch's longest sequence has at most
  * 256 FJ windows): 2 for proteins up to 520 aa, 8 up to FUSED_MAX_WINDOWS */
-template <uint32_t FJ, class IN>
+template <uint32_t FJ, class IN, bool QUAD = false>
 __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, uint32_t s);
 
 template <uint32_t FJ>
@@ -158,7 +158,9 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
                 const T pivot = a[f];
                 const int32_t i = f + 1 + (int32_t)lane;
                 const bool in = i < l;
-                const T v = in ? a[i] : pivot;
+                T v = pivot; /* (a select of the two structs went through scratch) */
+                if (in)
+                    v = a[i];
                 const bool lf = in && !comp(v, pivot), rf = in && !comp(pivot, v);
                 const uint64_t LM = __ballot(lf), RM = __ballot(rf);
                 const uint32_t l_below = (uint32_t)__popcll(LM & lanes_le(lane) & ~(1ull << lane));
@@ -204,7 +206,7 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
     wave_lds_sync();
 }
 
-template <uint32_t FJ, class IN>
+template <uint32_t FJ, class IN, bool QUAD>
 __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, const uint32_t s)
 {
     typedef FusedInput<IN> In;
@@ -233,111 +235,213 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     if (dbg)
         a.dbg[1] = wall_clock64();
 
-    /* 2. encode + probe: thread t owns windows t + 256 j */
-    const uint32_t J = (W + 255) / 256;
-    uint64_t key[FJ], slot[FJ];
-    bool pend[FJ], hit[FJ];
-    uint4 rec[FJ];
-#pragma unroll
-    for (uint32_t j = 0; j < FJ; j++) {
-        const uint32_t w = t + 256 * j;
-        hit[j] = false;
-        pend[j] = false;
-        rec[j] = make_uint4(0, 0, 0, 0);
-        key[j] = 0;
-        slot[j] = 0;
-        if (j < J && w < W) {
-            const uint8_t *c = codes + w;
-            const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
-            const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
-            const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
-            key[j] = (uint64_t)ka * 160000u + kb;
-            pend[j] = cmax < 20u;
-            slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
-        }
-    }
-    /* linear probe by 64-B lines: a round reads the rest of the line holding
-     * each pending window's next bucket (the table is 256-B aligned, 4
-     * records per line), all of a thread's windows in flight at once, and
-     * examines those buckets in probe order -- a chain costs one round per
-     * line it touches instead of one per bucket (reading the next line too,
-     * speculatively, measured slower: 6.8 vs 4.6 us for one protein).
-     * Bounded by num_sigs buckets where the reference would spin forever. */
-    constexpr uint32_t R = 4; /* records per round: one line */
-    uint64_t examined[FJ];
-#pragma unroll
-    for (uint32_t j = 0; j < FJ; j++)
-        examined[j] = 0;
-    const uint64_t NS = a.num_sigs;
-    for (;;) {
-        uint4 pv[FJ][R];
-#pragma unroll
-        for (uint32_t j = 0; j < FJ; j++) {
-            const uint64_t base = slot[j] & ~3ull;
-#pragma unroll
-            for (uint32_t q = 0; q < R; q++)
-                if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
-                    pv[j][q] = a.table[base + q];
-        }
-        bool more = false;
-#pragma unroll
-        for (uint32_t j = 0; j < FJ; j++) {
-            const uint64_t base = slot[j] & ~3ull;
-            bool live = pend[j]; /* still searching within this line */
-#pragma unroll
-            for (uint32_t q = 0; q < R; q++) {
-                const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
-                const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
-                const bool m = in && kv == key[j];
-                const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
-                rec[j].x = m ? pv[j][q].x : rec[j].x;
-                rec[j].y = m ? pv[j][q].y : rec[j].y;
-                rec[j].z = m ? pv[j][q].z : rec[j].z;
-                rec[j].w = m ? pv[j][q].w : rec[j].w;
-                hit[j] = hit[j] || m;
-                examined[j] += in ? 1u : 0u;
-                live = live && !stop;
-            }
-            /* not resolved in this line: on at the next one (wrapping at
-             * the table's end, where the round's loads stopped) */
-            const uint64_t next = base + R >= NS ? 0 : base + R;
-            pend[j] = live;
-            slot[j] = live ? next : slot[j];
-            more = more || live;
-        }
-        if (!__syncthreads_or(more))
-            break;
-    }
-    if (dbg)
-        a.dbg[2] = wall_clock64();
-
-    /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
     uint32_t nh = 0;
-    for (uint32_t j = 0; j < J; j++) {
-        bool h = false;
-        uint4 r = make_uint4(0, 0, 0, 0);
+    const uint32_t J = (W + 255) / 256; /* 256-window slices */
+    if constexpr (QUAD) {
+        /* 2'. encode + probe by quads: the 4 lanes of quad g = t / 4 own
+         * windows g + 64 i; each round they read the aligned 64-B line that
+         * holds a pending window's next bucket in ONE instruction (16 B a
+         * lane), and the quad's ballots settle the window: the first bucket
+         * from the slot on that is the key or a stop (kguts.cc:585-602)
+         * decides it.  A line costs one request instead of one per bucket
+         * read, and a wave instruction carries 16 windows instead of 64
+         * scattered records.  The matching lane puts the record into LDS at
+         * the window (wrec / whit alias hrec / oflag, free until the
+         * compaction, which reads a slice before it writes it). */
+        constexpr uint32_t QJ = 4 * FJ;
+        const uint32_t sub = t & 3u, quad = t >> 2, qs = 4u * (lane >> 2);
+        uint4 *wrec = hrec;
+        uint8_t *whit = oflag;
+        for (uint32_t i = t; i < W; i += 256)
+            whit[i] = 0;
+        uint64_t key[QJ], slot[QJ], examined[QJ];
+        bool pend[QJ];
 #pragma unroll
-        for (uint32_t q = 0; q < FJ; q++)
-            if (q == j) {
-                h = hit[q];
-                r = rec[q];
+        for (uint32_t j = 0; j < QJ; j++) {
+            const uint32_t w = quad + 64 * j;
+            pend[j] = false;
+            key[j] = 0;
+            slot[j] = 0;
+            examined[j] = 0;
+            if (w < W) {
+                const uint8_t *c = codes + w;
+                const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+                const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
+                const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
+                key[j] = (uint64_t)ka * 160000u + kb;
+                pend[j] = cmax < 20u;
+                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
             }
-        const uint64_t m = __ballot(h);
-        if (lane == 0)
-            wave_cnt[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (uint32_t v = 0; v < 4; v++) {
-            before += v < wave ? wave_cnt[v] : 0u;
-            total += wave_cnt[v];
         }
-        if (h) {
-            const uint32_t at = nh + before + lanes_below(m);
-            hrec[at] = r;
-            hpos[at] = t + 256 * j;
+        __syncthreads(); /* whit cleared */
+        const uint64_t NS = a.num_sigs;
+        for (;;) {
+            uint4 pv[QJ];
+#pragma unroll
+            for (uint32_t j = 0; j < QJ; j++) {
+                const uint64_t base = slot[j] & ~3ull;
+                if (pend[j] && base + sub < NS)
+                    pv[j] = a.table[base + sub];
+            }
+            bool more = false;
+#pragma unroll
+            for (uint32_t j = 0; j < QJ; j++) {
+                const uint64_t base = slot[j] & ~3ull;
+                const bool in = pend[j] && sub >= (uint32_t)(slot[j] & 3) && base + sub < NS;
+                const uint32_t iq = (uint32_t)(__ballot(in) >> qs) & 0xFu;
+                /* this bucket's place in the probe: examined so far + the
+                 * quad's in-range buckets before it + itself */
+                const uint64_t nth = examined[j] + (uint32_t)__popc(iq & ((1u << sub) - 1u)) + 1u;
+                const uint64_t kv = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
+                const bool m = in && kv == key[j];
+                /* past num_sigs buckets the reference would spin forever: a miss here */
+                const bool stop = in && (m || kv > MAX_ENCODED || nth >= NS);
+                const uint32_t sq = (uint32_t)(__ballot(stop) >> qs) & 0xFu;
+                const uint32_t mq = (uint32_t)(__ballot(m) >> qs) & 0xFu;
+                const uint32_t first = sq ? (uint32_t)__builtin_ctz(sq) : 4u;
+                const uint32_t w = quad + 64 * j;
+                if (sq && ((mq >> first) & 1u) && sub == first) {
+                    wrec[w] = pv[j];
+                    whit[w] = 1;
+                }
+                examined[j] += (uint32_t)__popc(iq);
+                const bool live = pend[j] && !sq;
+                slot[j] = live ? (base + 4 >= NS ? 0 : base + 4) : slot[j];
+                pend[j] = live;
+                more = more || live;
+            }
+            if (!__syncthreads_or(more))
+                break;
         }
-        nh += total;
-        __syncthreads();
+        if (dbg)
+            a.dbg[2] = wall_clock64();
+        /* 3'. ordered compaction into LDS (the records from wrec by window) */
+        for (uint32_t j = 0; j < J; j++) {
+            const uint32_t w = t + 256 * j;
+            const bool h = w < W && whit[w];
+            const uint4 r = h ? wrec[w] : make_uint4(0, 0, 0, 0);
+            const uint64_t m = __ballot(h);
+            if (lane == 0)
+                wave_cnt[wave] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            for (uint32_t v = 0; v < 4; v++) {
+                before += v < wave ? wave_cnt[v] : 0u;
+                total += wave_cnt[v];
+            }
+            if (h) {
+                const uint32_t at = nh + before + lanes_below(m);
+                hrec[at] = r;
+                hpos[at] = w;
+            }
+            nh += total;
+            __syncthreads();
+        }
+    } else {
+        /* 2. encode + probe: thread t owns windows t + 256 j */
+        uint64_t key[FJ], slot[FJ];
+        bool pend[FJ], hit[FJ];
+        uint4 rec[FJ];
+#pragma unroll
+        for (uint32_t j = 0; j < FJ; j++) {
+            const uint32_t w = t + 256 * j;
+            hit[j] = false;
+            pend[j] = false;
+            rec[j] = make_uint4(0, 0, 0, 0);
+            key[j] = 0;
+            slot[j] = 0;
+            if (j < J && w < W) {
+                const uint8_t *c = codes + w;
+                const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+                const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
+                const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
+                key[j] = (uint64_t)ka * 160000u + kb;
+                pend[j] = cmax < 20u;
+                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
+            }
+        }
+        /* linear probe by 64-B lines: a round reads the rest of the line holding
+         * each pending window's next bucket (the table is 256-B aligned, 4
+         * records per line), all of a thread's windows in flight at once, and
+         * examines those buckets in probe order -- a chain costs one round per
+         * line it touches instead of one per bucket (reading the next line too,
+         * speculatively, measured slower: 6.8 vs 4.6 us for one protein).
+         * Bounded by num_sigs buckets where the reference would spin forever. */
+        constexpr uint32_t R = 4; /* records per round: one line */
+        uint64_t examined[FJ];
+#pragma unroll
+        for (uint32_t j = 0; j < FJ; j++)
+            examined[j] = 0;
+        const uint64_t NS = a.num_sigs;
+        for (;;) {
+            uint4 pv[FJ][R];
+#pragma unroll
+            for (uint32_t j = 0; j < FJ; j++) {
+                const uint64_t base = slot[j] & ~3ull;
+#pragma unroll
+                for (uint32_t q = 0; q < R; q++)
+                    if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
+                        pv[j][q] = a.table[base + q];
+            }
+            bool more = false;
+#pragma unroll
+            for (uint32_t j = 0; j < FJ; j++) {
+                const uint64_t base = slot[j] & ~3ull;
+                bool live = pend[j]; /* still searching within this line */
+#pragma unroll
+                for (uint32_t q = 0; q < R; q++) {
+                    const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
+                    const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
+                    const bool m = in && kv == key[j];
+                    const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
+                    rec[j].x = m ? pv[j][q].x : rec[j].x;
+                    rec[j].y = m ? pv[j][q].y : rec[j].y;
+                    rec[j].z = m ? pv[j][q].z : rec[j].z;
+                    rec[j].w = m ? pv[j][q].w : rec[j].w;
+                    hit[j] = hit[j] || m;
+                    examined[j] += in ? 1u : 0u;
+                    live = live && !stop;
+                }
+                /* not resolved in this line: on at the next one (wrapping at
+                 * the table's end, where the round's loads stopped) */
+                const uint64_t next = base + R >= NS ? 0 : base + R;
+                pend[j] = live;
+                slot[j] = live ? next : slot[j];
+                more = more || live;
+            }
+            if (!__syncthreads_or(more))
+                break;
+        }
+        if (dbg)
+            a.dbg[2] = wall_clock64();
+
+        /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
+        for (uint32_t j = 0; j < J; j++) {
+            bool h = false;
+            uint4 r = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t q = 0; q < FJ; q++)
+                if (q == j) {
+                    h = hit[q];
+                    r = rec[q];
+                }
+            const uint64_t m = __ballot(h);
+            if (lane == 0)
+                wave_cnt[wave] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            for (uint32_t v = 0; v < 4; v++) {
+                before += v < wave ? wave_cnt[v] : 0u;
+                total += wave_cnt[v];
+            }
+            if (h) {
+                const uint32_t at = nh + before + lanes_below(m);
+                hrec[at] = r;
+                hpos[at] = t + 256 * j;
+            }
+            nh += total;
+            __syncthreads();
+        }
     }
     if (dbg)
         a.dbg[3] = wall_clock64();
@@ -607,7 +711,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         if (d > 1 && d <= 64) {
             if (wave == 0)
                 lstd_sort_wave64(o, d, by_count, o + 384 * FJ, ostack);
-        } else if (d > 64 && t == 0) {
+        } else if (d > 1 && t == 0) {
             lstd_sort_on(o, (int64_t)d, by_count, ostack);
         }
         if (t == 0)
@@ -707,6 +811,7 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * slot's next request until the instance ended (0.5% of calls waited up to
  * the instance's lifetime: +40% mean latency at 16 callers).
  */
+template <bool QUAD>
 __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbgs,
                                                   const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
                                                   kgx_otu *otus,
@@ -775,7 +880,7 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         const FusedSlot in{res_base + (uint64_t)slot * SVC_RES_STRIDE, len};
         __syncthreads(); /* every thread has its copy of the request before cmd can change */
         if (len <= 2 * 256 + 8)
-            fused_small_body<2>(a, in, 0);
+            fused_small_body<2, FusedSlot, QUAD>(a, in, 0); /* quads: up to 512 windows (8 per quad) */
         else
             fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
         last = req;
@@ -784,12 +889,16 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t life_ticks, hipStream_t stream)
+                      uint64_t life_ticks, int quad_probe, hipStream_t stream)
 {
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(svc_kernel, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls, otus,
-                       static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
+    if (quad_probe)
+        hipLaunchKernelGGL(svc_kernel<true>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls, otus,
+                           static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
+    else
+        hipLaunchKernelGGL(svc_kernel<false>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
+                           otus, static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
     return hipGetLastError();
 }
 

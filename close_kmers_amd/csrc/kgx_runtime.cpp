@@ -2073,6 +2073,8 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     t->probe_j = c->probe_j;
     t->probe_filter = c->probe_filter;
     t->probe_serialize = c->probe_serialize;
+    t->score_variant = c->score_variant;
+    t->score_wave_tiles = c->score_wave_tiles;
     kgx_ctx *xs[2] = {c, t};
     if (!c->copy_stream)
         HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));

@@ -94,6 +94,8 @@ struct SvcState {
     std::atomic<uint32_t> users{0};  /* callers inside kgx_svc_call holding this state */
     std::atomic<uint64_t> n_abandoned{0}; /* slots given up after a 10-s wait (never handed out again) */
     int priority = 0; /* the stream's priority (hipDeviceGetStreamPriorityRange: lower = higher) */
+    int quad_probe = 1; /* proteins up to 520 aa probed by 4-lane quads per 64-B line (KGX_SVC_PROBE=thread: a
+                           thread per window) */
 };
 
 namespace {
@@ -159,7 +161,7 @@ int top_up(SvcState *s)
         /* wall clock at 100 MHz: 100 ticks per us */
         hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->d_otus, s->slots,
                                   s->table,
-                                  s->num_sigs, s->life_us * 100, s->stream);
+                                  s->num_sigs, s->life_us * 100, s->quad_probe, s->stream);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
         if (e != hipSuccess) {
@@ -267,6 +269,8 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     std::memset(h, 0, b_hdr + b_out + b_dbg);
     const char *dbg_env = std::getenv("KGX_SVC_DEBUG");
     s->debug = dbg_env && std::atoi(dbg_env) != 0;
+    if (const char *pr = std::getenv("KGX_SVC_PROBE"))
+        s->quad_probe = std::string(pr) != "thread";
     if (const char *sl = std::getenv("KGX_SVC_SLEEP_US"))
         s->sleep_us = (uint32_t)std::max(0, std::atoi(sl));
     char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);

@@ -1,17 +1,19 @@
 #!/bin/bash
-# Round-4 measurements: facade service A/B (stream priority), batches beside
-# the service (native threads), family /lookup serving, the fq handler over
-# all C4 reads.  bash tools/gpu_r4b.sh TAG
+# Round-4 measurements: the call service (quad vs thread probe; stream
+# priority), batches beside the service (native threads), family /lookup
+# serving, the fq handler over all C4 reads.  bash tools/gpu_r4b.sh TAG
 set -euo pipefail
 TAG=${1:-r4b}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 600 python3 -u -m pytest tests/test_server.py tests/test_gpu_fq.py tests/test_gpu_tables.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
-KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_high.json" 2> "$OUT/facade_high.err"
-KGX_SVC_PRIORITY=normal KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_normal.json" 2> "$OUT/facade_normal.err"
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_svc.py tests/test_gpu_coalesce.py tests/test_server.py tests/test_gpu_fq.py tests/test_gpu_tables.py -m gpu -x -q -s --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
+env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 KGX_SVC_DEBUG=1 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_quad.json" 2> "$OUT/facade_quad.err"
+env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 KGX_SVC_DEBUG=1 KGX_SVC_PROBE=thread timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_thread.json" 2> "$OUT/facade_thread.err"
+env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=16 KGX_FACADE_BESIDE=8 KGX_SVC_PRIORITY=normal timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_normal.json" 2> "$OUT/facade_normal.err"
 timeout -k 10 600 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
     --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
 KGX_FQ_TIMING=1 timeout -k 10 900 python3 tools/bench_fq.py --no-cpu-baseline --reps 2 > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
+KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
 echo "[gpu_r4b] done" >&2

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--taper", default="1", help="host_taper settings to try")
     ap.add_argument("--rec12", default="0", help="host_rec12 settings to try")
     ap.add_argument("--nt", default="1", help="host_nt settings to try")
+    ap.add_argument("--score", default="0", help="score_variant settings to try (0 hybrid, 1 wave)")
+    ap.add_argument("--want", type=int, default=3)
     ap.add_argument("--timing", action="store_true", help="one extra KGX_TIMING pass per setting (stderr)")
     ap.add_argument("--compact", action="store_true",
                     help="kgx_process_batch_compact (records + mask, bench.py's host_path value) instead of kgx_hit")
@@ -59,8 +61,10 @@ def main():
     combos = [c + (int(st), int(cf), int(hs), int(tp)) for c in combos for st in args.stage.split(",")
               for cf in args.counts_first.split(",") for hs in args.stream.split(",")
               for tp in args.taper.split(",")]
-    combos = [c + (int(r), int(t)) for c in combos for r in args.rec12.split(",") for t in args.nt.split(",")]
-    for k, hc, nb, h16, nt, st, cf, hs, tp, r12, ntst in combos:
+    combos = [c + (int(r), int(t), int(sv)) for c in combos for r in args.rec12.split(",") for t in args.nt.split(",")
+              for sv in args.score.split(",")]
+    for k, hc, nb, h16, nt, st, cf, hs, tp, r12, ntst, sv in combos:
+        ctx.set_option("score_variant", sv)
         ctx.set_option("host_rec12", r12)
         ctx.set_option("host_nt", ntst)
         ctx.set_option("host_taper", tp)
@@ -74,15 +78,15 @@ def main():
         ctx.set_option("host_threads", nt)
         def run():
             if args.compact:
-                return ctx.process_batch_compact(res, off, params, want=3)
-            return ctx.process_batch(res, off, params, want=3, copy=False)
+                return ctx.process_batch_compact(res, off, params, want=args.want)
+            return ctx.process_batch(res, off, params, want=args.want, copy=False)
         r = run()
         th = []
         for _ in range(9):
             t0 = time.perf_counter()
             r = run()
             th.append(time.perf_counter() - t0)
-        key = f"chunks{k}_copy{hc}" + (f"_blocks{nb}" if hc else "") + f"_h16{h16}" + (f"_t{nt}" if h16 else "") + f"_st{st}_cf{cf}_hs{hs}_tp{tp}_r{r12}_nt{ntst}"
+        key = f"chunks{k}_copy{hc}" + (f"_blocks{nb}" if hc else "") + f"_h16{h16}" + (f"_t{nt}" if h16 else "") + f"_st{st}_cf{cf}_hs{hs}_tp{tp}_r{r12}_nt{ntst}_sv{sv}"
         times[key] = float(np.median(th)) * 1e3
         if args.timing:
             print(f"--- {key}", file=sys.stderr, flush=True)
