@@ -1663,45 +1663,68 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
                 th.join();
             pool.clear();
         };
+        /* parts alternate between two contexts: part k + 1 is sized and its
+         * lookup enqueued before part k's results are collected, so the host's
+         * collection and output of one part overlap the next part's probe */
+        kgx_ctx *ctxs[2] = {kg_.ctx(), twin_ctx()};
+        auto wait_part = [&](size_t k) -> FqPart & {
+            const auto w0 = std::chrono::steady_clock::now();
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return ready[k % R] == k || !err.empty(); });
+            if (!err.empty())
+                throw std::runtime_error(err);
+            parse_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+            return *parts_[k % R];
+        };
+        auto release = [&](size_t k) {
+            std::lock_guard<std::mutex> lk(mu);
+            ready[k % R] = SIZE_MAX;
+            consumed = k + 1;
+            cv.notify_all();
+        };
         try {
+            FqPart *cur = &wait_part(0);
+            const auto l0 = std::chrono::steady_clock::now();
+            FqLaunched lc = launch_block(cur->view(), ctxs[0]);
+            device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - l0).count();
             for (size_t k = 0; k < K; k++) {
-                const auto w0 = std::chrono::steady_clock::now();
-                {
-                    std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return ready[k % R] == k || !err.empty(); });
-                    if (!err.empty())
-                        throw std::runtime_error(err);
-                }
-                parse_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
-                FqPart &pt = *parts_[k % R];
+                FqPart *nxt = nullptr;
+                FqLaunched ln;
+                std::unique_ptr<FqPart> tail;
                 if (k + 1 < K) {
                     /* the speculation of part k + 1 holds iff part k ends at a
                      * record start with nothing pending */
-                    const bool holds = pt.state == FQ_START && pt.id.empty() && pt.len == pt.roff.back();
-                    if (!holds) {
-                        stop_workers();
+                    const bool holds = cur->state == FQ_START && cur->id.empty() && cur->len == cur->roff.back();
+                    if (holds) {
+                        nxt = &wait_part(k + 1);
+                        if (k + 2 == K)
+                            finish_part(*nxt);
+                    } else {
                         /* the rest of the block, exactly, from part k's end state */
-                        FqPart tail;
-                        tail.begin((size_t)(end - cuts[k + 1]) + (pt.len - pt.roff.back()), pt.state, pt.id,
-                                   std::string(pt.bases + pt.roff.back(), pt.len - pt.roff.back()));
-                        pt.len = pt.roff.back();
-                        pt.state = FQ_START;
-                        pt.id.clear();
-                        run_part(pt);
-                        tail.parse(cuts[k + 1], end);
-                        finish_part(tail);
-                        run_part(tail);
-                        break;
+                        stop_workers();
+                        tail.reset(new FqPart);
+                        tail->begin((size_t)(end - cuts[k + 1]) + (cur->len - cur->roff.back()), cur->state, cur->id,
+                                    std::string(cur->bases + cur->roff.back(), cur->len - cur->roff.back()));
+                        tail->parse(cuts[k + 1], end);
+                        finish_part(*tail);
+                        nxt = tail.get();
                     }
-                    run_part(pt);
-                } else {
-                    finish_part(pt);
-                    run_part(pt);
+                    const auto l1 = std::chrono::steady_clock::now();
+                    ln = launch_block(nxt->view(), ctxs[(k + 1) % 2]);
+                    device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - l1).count();
                 }
-                std::lock_guard<std::mutex> lk(mu);
-                ready[k % R] = SIZE_MAX;
-                consumed = k + 1;
-                cv.notify_all();
+                const auto f0 = std::chrono::steady_clock::now();
+                finish_block(cur->view(), lc, mapper, os);
+                device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count();
+                if (tail) { /* the exact re-parse was the last part */
+                    const auto f1 = std::chrono::steady_clock::now();
+                    finish_block(nxt->view(), ln, mapper, os);
+                    device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f1).count();
+                    break;
+                }
+                release(k);
+                cur = nxt;
+                lc = ln;
             }
         } catch (...) {
             stop_workers();
@@ -1737,34 +1760,77 @@ void FqRequest::process_reads(const std::vector<std::pair<std::string, std::stri
 
 void FqRequest::process_block(const FqBlock &blk, FamilyMapper &mapper, std::ostream &os)
 {
-    const uint32_t n_reads = (uint32_t)blk.n_reads();
-    if (n_reads == 0)
-        return;
-    /* KGX_FQ_TIMING=1: per-phase wall times on stderr */
-    static const bool timing = std::getenv("KGX_FQ_TIMING") != nullptr;
-    auto t_last = std::chrono::steady_clock::now();
-    auto mark = [&](const char *what) {
-        if (!timing)
-            return;
-        kgx_ctx_synchronize(kg_.ctx());
-        auto now = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[fq] %-12s %8.3f ms\n", what,
-                     std::chrono::duration<double, std::milli>(now - t_last).count());
-        t_last = now;
-    };
-    /* the block's reads -> fragments -> lookup, one GPU batch */
-    kgx_ctx *ctx = kg_.ctx();
-    kgx_fragments fr;
+    FqLaunched l = launch_block(blk, kg_.ctx());
+    finish_block(blk, l, mapper, os);
+}
+
+kgx_ctx *FqRequest::twin_ctx()
+{
+    if (!twin_) {
+        int rc = kgx_ctx_create(kg_.image_->handle(), &twin_);
+        if (rc)
+            throw_last(rc, "kgx_ctx_create");
+    }
+    return twin_;
+}
+
+FqRequest::~FqRequest()
+{
+    if (twin_)
+        kgx_ctx_destroy(twin_);
+}
+
+/* the block's reads -> fragments -> lookup, one GPU batch on ctx: returns
+ * once the fragment pass has sized the batch and the lookup is enqueued */
+FqRequest::FqLaunched FqRequest::launch_block(const FqBlock &blk, kgx_ctx *ctx)
+{
+    FqLaunched l;
+    l.ctx = ctx;
+    l.n_reads = (uint32_t)blk.n_reads();
+    if (l.n_reads == 0)
+        return l;
     /* fragments as anchors into the bases: the probe translates their windows
      * itself and no residue goes through HBM (the context keeps residues when
      * its probe cannot take anchors) */
     int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
     if (rc)
         throw_last(rc, "kgx_ctx_set_option");
-    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff, n_reads, &fr);
+    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff, l.n_reads, &l.fr);
     if (rc)
         throw_last(rc, "kgx_fq_fragments");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
+    /* Calls are sparse over fragments (most fragments of a read are noise),
+     * so the calls come back and find_best_call runs on the host for the
+     * fragments that have any: a per-fragment device decision (KGX_WANT_BEST)
+     * would copy 24 B for every fragment (measured: 8.3M -> 6.7M reads/s).
+     * The hits stay on the device for the rollups. */
+    rc = kgx_fq_run_device(ctx, &p, &l.fr, KGX_WANT_CALLS, nullptr);
+    if (rc)
+        throw_last(rc, "kgx_fq_run_device");
+    return l;
+}
+
+void FqRequest::finish_block(const FqBlock &blk, FqLaunched &l, FamilyMapper &mapper, std::ostream &os)
+{
+    const uint32_t n_reads = l.n_reads;
+    if (n_reads == 0)
+        return;
+    /* KGX_FQ_TIMING=1: per-phase wall times on stderr */
+    static const bool timing = std::getenv("KGX_FQ_TIMING") != nullptr && std::getenv("KGX_FQ_TIMING")[0] == '2';
+    auto t_last = std::chrono::steady_clock::now();
+    kgx_ctx *ctx = l.ctx;
+    auto mark = [&](const char *what) {
+        if (!timing)
+            return;
+        kgx_ctx_synchronize(ctx);
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[fq] %-12s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t_last).count());
+        t_last = now;
+    };
+    kgx_fragments &fr = l.fr;
+    const uint32_t want = KGX_WANT_CALLS;
+    int rc;
     /* Without family lists a fragment's match depends on its calls alone,
      * and a read without calls scores 0 in every frame: no output and no
      * FamilyMapper state (seq_score_ stays empty).  Only then may reads
@@ -1772,14 +1838,6 @@ void FqRequest::process_block(const FqBlock &blk, FamilyMapper &mapper, std::ost
      * loaded every fragment is replayed, since each one grows seq_score_ and
      * so shapes the iteration order later reads see. */
     const bool families = kgx_kmap_num_kmers(mapping_->kmer_to_family_id()) > 0;
-    /* Calls are sparse over fragments (most fragments of a read are noise),
-     * so the calls come back and find_best_call runs on the host for the
-     * fragments that have any: a per-fragment device decision (KGX_WANT_BEST)
-     * would copy 24 B for every fragment (measured: 8.3M -> 6.7M reads/s). */
-    const uint32_t want = KGX_WANT_CALLS; /* the hits stay on the device for the rollups */
-    rc = kgx_fq_run_device(ctx, &p, &fr, want, nullptr);
-    if (rc)
-        throw_last(rc, "kgx_fq_run_device");
     mark("lookup");
     if (!families) {
         /* only the reads with a call in some fragment come back (sparse):

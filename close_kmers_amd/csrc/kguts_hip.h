@@ -478,6 +478,9 @@ private:
 class FqRequest {
 public:
     FqRequest(KmerGuts &kg, std::shared_ptr<KmerPegMapping> mapping);
+    ~FqRequest();
+    FqRequest(const FqRequest &) = delete;
+    FqRequest &operator=(const FqRequest &) = delete;
     /* one block of FASTQ text; `finished` = the request's last block
      * (parse_complete).  Output lines are appended to os. */
     void process(const std::string &fastq_block, bool finished, std::ostream &os);
@@ -519,6 +522,19 @@ private:
         FqBlock view() const;
     };
     void process_block(const FqBlock &blk, FamilyMapper &mapper, std::ostream &os);
+    /* process_block in two halves: launch sizes the block's fragments and
+     * enqueues their lookup on ctx; finish collects the results and writes the
+     * block's lines.  Between the two the host may launch the next block on
+     * another context. */
+    struct FqLaunched {
+        kgx_ctx *ctx = nullptr;
+        uint32_t n_reads = 0;
+        kgx_fragments fr{};
+    };
+    FqLaunched launch_block(const FqBlock &blk, kgx_ctx *ctx);
+    void finish_block(const FqBlock &blk, FqLaunched &l, FamilyMapper &mapper, std::ostream &os);
+    kgx_ctx *twin_ctx(); /* a second context on the image, created on first use */
+    kgx_ctx *twin_ = nullptr;
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     /* FastqParser state (fastq_parser.h:40-150) */
