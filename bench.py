@@ -131,11 +131,9 @@ def canary_check(abi, synth, d, dev):
     want = canary.expected()["digest"]
     mine["ok"] = mine["digest"] == want
     recs = d.gather_objects(mine)
-    ok = all(r["ok"] for r in recs)
-    devs = [r["device"] for r in recs]
-    if d.world > 1 and "KGX_BENCH_DEVICE" not in os.environ and len(set(devs)) != len(devs):
-        log(f"[bench] canary: ranks share a device: {devs}")
-        ok = False
+    ok, why = canary.verdict(recs, want, d.world > 1 and "KGX_BENCH_DEVICE" not in os.environ)
+    if not ok:
+        log(f"[bench] canary: {why}")
     if d.rank == 0:
         log(f"[bench] canary ({canary.CANARY_SEQ} x {canary.CANARY_LEN} aa vs {canary.CANARY_KEYS:,}-entry image, "
             f"want {canary.CANARY_WANT}): " + ", ".join(

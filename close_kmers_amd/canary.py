@@ -83,6 +83,20 @@ def best_from_device(best) -> np.ndarray:
     return out
 
 
+def verdict(recs: list, expected_digest: str, distinct_devices: bool) -> tuple:
+    """The whole job's verdict over every rank's canary record (rank order):
+    (ok, reason).  Every digest must be the oracle's; with distinct_devices
+    (one rank per GPU, no KGX_BENCH_DEVICE override) no two ranks may share a
+    device."""
+    bad = [r["rank"] for r in recs if r["digest"] != expected_digest]
+    if bad:
+        return False, f"rank(s) {bad}: the canary digest differs from the CPU oracle's"
+    devs = [r["device"] for r in recs]
+    if distinct_devices and len(set(devs)) != len(devs):
+        return False, f"ranks share a device: {devs}"
+    return True, "ok"
+
+
 def expected() -> dict:
     with open(DIGEST_JSON) as f:
         return json.load(f)

@@ -233,3 +233,35 @@ def test_bench_gpus_must_match_torchrun_world():
     r = _bench(["--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "--gpus 3 but the launcher started 2 ranks" in r.stderr
+
+
+def _canary_worker(rank, world, port, q, corrupt_rank, same_device):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    from close_kmers_amd import canary
+    d = shard.Dist("gloo")
+    want = canary.expected()["digest"]
+    mine = {"rank": d.rank, "device": 0 if same_device else d.rank,
+            "digest": ("0" * 64) if d.rank == corrupt_rank else want, "hits": 1, "calls": 1}
+    recs = d.gather_objects(mine)
+    q.put((d.rank, canary.verdict(recs, want, True)))
+    d.close()
+
+
+@pytest.mark.parametrize("corrupt_rank,same_device,ok", [(-1, False, True), (1, False, False), (-1, True, False)])
+def test_canary_verdict_over_gloo_ranks(corrupt_rank, same_device, ok):
+    """bench.py's canary plumbing at world size 2: every rank's digest is
+    gathered and every rank reaches the same verdict -- a rank whose digest
+    is not the oracle's, or two ranks on one device, fail the whole job."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_canary_worker, args=(r, 2, port, q, corrupt_rank, same_device)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v[0] == ok for _, v in got), got

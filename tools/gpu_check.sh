@@ -1,9 +1,10 @@
 #!/bin/bash
 # One GPU-box pass (run through gpurun from the repo root):
 #   bash tools/gpu_check.sh TAG [quick]
-# 1. the -m gpu test suite + smoke   2. bench.py (C2)   3. C3 /matrix   4. C4 fq
-# 5. HTTP serving (/query; /lookup in family mode)   6. per-sequence facade calls (and with OTU stats)
-# 7. kgx_pool (C5 batch)
+# 1. the -m gpu test suite + smoke   2. bench.py (C2, with its canary)   3. C3 /matrix
+# 4. C4 fq (device pass and the handler over all reads)   5. HTTP serving (/query; /lookup in family mode)
+# 6. per-sequence facade calls (and with OTU stats, and batches beside the service)
+# 7. kgx_pool (C5 batch): contexts of one device, and bench.py --pool-devices 2
 # "quick" skips the CPU baselines.  Output in gpurun_out/TAG; every GPU step
 # has its own time limit and the script stops at the first failure.
 set -euo pipefail
@@ -23,8 +24,9 @@ timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$O
 timeout -k 10 600 python3 tools/bench_server.py > "$OUT/bench_server.json" 2> "$OUT/bench_server.err"
 timeout -k 10 900 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
     --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
-timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
+KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
 KGX_FACADE_OTU=1 KGX_FACADE_MODES=2 timeout -k 10 300 python3 tools/bench_facade.py \
     > "$OUT/bench_facade_otu.json" 2> "$OUT/bench_facade_otu.err"
 timeout -k 10 600 python3 tools/bench_pool.py > "$OUT/bench_pool.json" 2> "$OUT/bench_pool.err"
+timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool_devices.json" 2> "$OUT/bench_pool_devices.err"
 echo "[gpu_check] done" >&2

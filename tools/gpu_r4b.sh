@@ -14,6 +14,8 @@ env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 KGX_SVC_DE
 env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=16 KGX_FACADE_BESIDE=8 KGX_SVC_PRIORITY=normal timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_normal.json" 2> "$OUT/facade_normal.err"
 timeout -k 10 600 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
     --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
+timeout -k 10 600 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
+    --clients 16 --threads 12 > "$OUT/bench_lookup_fam_t12.json" 2> "$OUT/bench_lookup_fam_t12.err"
 KGX_FQ_TIMING=1 timeout -k 10 900 python3 tools/bench_fq.py --no-cpu-baseline --reps 2 > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
 KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
 echo "[gpu_r4b] done" >&2
