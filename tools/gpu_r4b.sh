@@ -18,4 +18,9 @@ timeout -k 10 600 python3 tools/bench_server.py --families 100000 --path "/looku
     --clients 16 --threads 12 > "$OUT/bench_lookup_fam_t12.json" 2> "$OUT/bench_lookup_fam_t12.err"
 KGX_FQ_TIMING=1 timeout -k 10 900 python3 tools/bench_fq.py --no-cpu-baseline --reps 2 > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
 KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
+timeout -k 10 600 python3 tools/host_path_probe.py --compact --no-pieces --chunks 4,6,8 --copy 1 --hits16 1 --stream 1 \
+    --rec12 1 --score 0,1 --want 11 > "$OUT/host_path_sweep.json" 2> "$OUT/host_path_sweep.err"
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/hp_trace" -o hp \
+    -- python3 "$R/tools/host_path_probe.py" --compact --no-pieces --chunks 6 --copy 1 --hits16 1 --stream 1 --rec12 1 \
+    --want 11 > "$OUT/hp_trace.json" 2> "$OUT/hp_trace.err")
 echo "[gpu_r4b] done" >&2
