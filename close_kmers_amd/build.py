@@ -23,6 +23,8 @@ QUERY = os.path.join(PKG, "kgx_query")
 SERVER = os.path.join(PKG, "kgx_server")
 # the facade under T concurrent worker threads (tests/test_gpu_coalesce.py)
 COALESCE_CHECK = os.path.join(ROOT, "tests", "native", "coalesce_check")
+# per-sequence service callers beside a batch caller (tests/test_gpu_svc.py)
+BESIDE_CHECK = os.path.join(ROOT, "tests", "native", "beside_check")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
@@ -72,7 +74,8 @@ def build(force: bool = False, verbose: bool = False) -> None:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
         os.replace(tmp, LIB)
     for exe, esrc in ((QUERY, os.path.join(CSRC, "kgx_query.cpp")), (SERVER, os.path.join(CSRC, "kgx_server.cpp")),
-                      (COALESCE_CHECK, os.path.join(ROOT, "tests", "native", "coalesce_check.cpp"))):
+                      (COALESCE_CHECK, os.path.join(ROOT, "tests", "native", "coalesce_check.cpp")),
+                      (BESIDE_CHECK, os.path.join(ROOT, "tests", "native", "beside_check.cpp"))):
         if not os.path.exists(esrc):
             continue
         if force or _newer(exe, [esrc, LIB] + deps):

@@ -623,87 +623,119 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             close_open();
         ncalls_out = want_calls ? o_ncalls : 0u;
     }
-    /* 4c. OTU tallies (KmerOtuStats::finalize, kguts.h:196-218), all
-     * threads, in LDS (hpos, hrec and codes are free once the records are
-     * stored and the scorer is done): the flagged hits' OTUs compacted in hit
-     * order (ballots), each value's count and first occurrence by a scan of
-     * the list, the distinct values placed in key order by rank (= the
-     * std::map's order), then the pairs std::sort'ed by count on one thread
-     * (lstd_sort_on replays libstdc++'s tie order; there are few pairs).  One
-     * thread doing it all (otu_finalize's heap sort) cost ~70 us per call:
-     * every step a dependent LDS access. */
+    /* 4c. OTU tallies (KmerOtuStats::finalize, kguts.h:196-218), in LDS
+     * (hpos, hrec and codes are free once the records are stored and the
+     * scorer is done).  Wave 0 collects the flagged hits' distinct OTUs in its
+     * registers -- lane j holds the j-th value met and its count -- with one
+     * ballot round per distinct value among each 64 hits (a handful: the hits
+     * of a call share few OTUs), then places each value by its rank among the
+     * others (= the std::map's key order).  More than 64 distinct values take
+     * the general path below.  Then the pairs are std::sort'ed by count
+     * (lstd_sort_wave64 / lstd_sort_on replay libstdc++'s tie order). */
     if (want_otu) {
-        __shared__ uint32_t multi;
         __shared__ LstdPart ostack[64];
         if (dbg)
             a.dbg[7] = wall_clock64();
-        if (t == 0)
-            multi = 0;
-        __syncthreads();
-        int32_t *v = reinterpret_cast<int32_t *>(hpos);
-        uint32_t m = 0;
-        for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
-            const uint32_t i = t + 256 * j;
-            const bool f = i < nh && oflag[i];
-            const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
-            const uint64_t bm = __ballot(f);
-            if (lane == 0)
-                wave_cnt[wave] = (uint32_t)__popcll(bm);
-            __syncthreads();
-            uint32_t before = 0, total = 0;
-            for (uint32_t w = 0; w < 4; w++) {
-                before += w < wave ? wave_cnt[w] : 0u;
-                total += wave_cnt[w];
-            }
-            __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
-            if (f)
-                v[m + before + lanes_below(bm)] = x;
-            m += total;
-            __syncthreads();
-        }
-        /* one OTU among the tallied hits (the usual case): one pair.  Every
-         * thread compares its entries with the first (plain stores of 1, no
-         * atomics: same-address LDS atomics from every flagged lane serialize) */
-        const int32_t v0 = m ? v[0] : 0;
-        for (uint32_t i = t; i < m; i += 256)
-            if (v[i] != v0)
-                multi = 1;
-        __syncthreads();
-        const bool one = m > 0 && !multi;
         kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
-        uint32_t *cnt = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
-        uint8_t *first = codes;
-        for (uint32_t i = t; i < (one ? 0u : m); i += 256) {
-            const int32_t x = v[i];
-            uint32_t c = 0;
-            bool fst = true;
-#pragma unroll 8
-            for (uint32_t j = 0; j < m; j++) {
-                const bool e = v[j] == x;
-                c += e ? 1u : 0u;
-                fst = fst && !(e && j < i);
+        __syncthreads();
+        if (wave == 0) {
+            int32_t dv = 0;
+            uint32_t dc = 0, dn = 0;
+            bool over = false;
+            for (uint32_t h0 = 0; h0 < nh && !over; h0 += 64) {
+                const uint32_t i = h0 + lane;
+                const bool f = i < nh && oflag[i];
+                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+                uint64_t rem = __ballot(f);
+                while (rem) {
+                    const int32_t y = (int32_t)rl32((uint32_t)x, lowbit(rem));
+                    const uint64_t mk = __ballot(f && x == y);
+                    rem &= ~mk;
+                    const uint64_t at = __ballot(lane < dn && dv == y);
+                    if (at) {
+                        if (lane == lowbit(at))
+                            dc += (uint32_t)__popcll(mk);
+                    } else if (dn < 64) {
+                        if (lane == dn) {
+                            dv = y;
+                            dc = (uint32_t)__popcll(mk);
+                        }
+                        dn++;
+                    } else {
+                        over = true;
+                        break;
+                    }
+                }
             }
-            cnt[i] = c;
-            first[i] = fst ? 1 : 0;
+            if (!over) {
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < dn; j++)
+                    r += (int32_t)rl32((uint32_t)dv, j) < dv ? 1u : 0u;
+                if (lane < dn)
+                    o[r] = kgx_otu{dv, (int32_t)dc};
+            }
+            if (lane == 0)
+                n_otu = over ? ~0u : dn;
         }
         __syncthreads();
-        for (uint32_t i = t; i < (one ? 0u : m); i += 256) {
-            if (!first[i])
-                continue;
-            const int32_t x = v[i];
-            uint32_t r = 0;
+        uint32_t d = n_otu;
+        if (d == ~0u) {
+            /* the general path: the flagged hits' OTUs compacted in hit order
+             * (ballots), each value's count and first occurrence by a scan of
+             * the list, the distinct values placed in key order by rank */
+            int32_t *v = reinterpret_cast<int32_t *>(hpos);
+            uint32_t m = 0;
+            for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
+                const uint32_t i = t + 256 * j;
+                const bool f = i < nh && oflag[i];
+                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+                const uint64_t bm = __ballot(f);
+                if (lane == 0)
+                    wave_cnt[wave] = (uint32_t)__popcll(bm);
+                __syncthreads();
+                uint32_t before = 0, total = 0;
+                for (uint32_t w = 0; w < 4; w++) {
+                    before += w < wave ? wave_cnt[w] : 0u;
+                    total += wave_cnt[w];
+                }
+                __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
+                if (f)
+                    v[m + before + lanes_below(bm)] = x;
+                m += total;
+                __syncthreads();
+            }
+            uint32_t *cnt = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
+            uint8_t *first = codes;
+            for (uint32_t i = t; i < m; i += 256) {
+                const int32_t x = v[i];
+                uint32_t c = 0;
+                bool fst = true;
 #pragma unroll 8
-            for (uint32_t j = 0; j < m; j++)
-                r += (first[j] && v[j] < x) ? 1u : 0u;
-            o[r] = kgx_otu{x, (int32_t)cnt[i]};
+                for (uint32_t j = 0; j < m; j++) {
+                    const bool e = v[j] == x;
+                    c += e ? 1u : 0u;
+                    fst = fst && !(e && j < i);
+                }
+                cnt[i] = c;
+                first[i] = fst ? 1 : 0;
+            }
+            __syncthreads();
+            for (uint32_t i = t; i < m; i += 256) {
+                if (!first[i])
+                    continue;
+                const int32_t x = v[i];
+                uint32_t r = 0;
+#pragma unroll 8
+                for (uint32_t j = 0; j < m; j++)
+                    r += (first[j] && v[j] < x) ? 1u : 0u;
+                o[r] = kgx_otu{x, (int32_t)cnt[i]};
+            }
+            /* distinct values: a block-wide count of the firsts (no serial scan) */
+            d = 0;
+            for (uint32_t j0 = 0; j0 < m; j0 += 256)
+                d += (uint32_t)__syncthreads_count(j0 + t < m && first[j0 + t]);
+            __syncthreads();
         }
-        /* distinct values: a block-wide count of the firsts (no serial scan) */
-        uint32_t d = one ? 1u : 0u;
-        for (uint32_t j0 = 0; j0 < (one ? 0u : m); j0 += 256)
-            d += (uint32_t)__syncthreads_count(j0 + t < m && first[j0 + t]);
-        if (one && t == 0)
-            o[0] = kgx_otu{v0, (int32_t)m};
-        __syncthreads();
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
          * it for up to 64 pairs (lstd_sort_wave64), thread 0 beyond (its
          * partition stack in LDS) */
@@ -717,7 +749,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         if (t == 0)
             n_otu = d;
         __syncthreads();
-        for (uint32_t i = t; i < n_otu; i += 256)
+        for (uint32_t i = t; i < d; i += 256)
             a.otus[wb + i] = o[i];
     }
 

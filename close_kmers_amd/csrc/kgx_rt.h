@@ -294,8 +294,15 @@ struct kgx_image {
     hipEvent_t last_probe = nullptr; /* end of the latest probe enqueued */
     hipStream_t probe_stream = nullptr; /* contexts' chained probes with option probe_stream */
     /* the resident call service (kgx_svc.cpp), created on the first kgx_svc_call */
-    std::mutex svc_mu;
-    kgx::SvcState *svc = nullptr;
+    std::mutex svc_mu; /* creation, configuration and shutdown; a call takes no lock */
+    std::atomic<kgx::SvcState *> svc{nullptr};
+    /* callers inside kgx_svc_call, counted per thread shard, each shard on a
+     * line of its own: a call writes no line that other callers write
+     * (kgx_svc.cpp: enter / shutdown_locked) */
+    struct alignas(64) SvcUsers {
+        std::atomic<uint32_t> n{0};
+    };
+    SvcUsers svc_users[32];
     uint32_t svc_slots = 32, svc_idle_us = 1000, svc_life_us = 1000;
     bool svc_configured = false; /* kgx_svc_config was called (env defaults no longer apply) */
     const void *resident() const

@@ -1978,21 +1978,40 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     HostPool *sp = c->stage_threads > 1 ? c->stage_pool.get() : nullptr;
     int rc = KGX_OK;
     uint32_t next = 0; /* next chunk to collect */
+    /* KGX_TIMING: the host's own clock per chunk (ms from T0): staging
+     * entered / staged / enqueued, and each collect's end */
+    std::vector<double> ht;
     for (uint32_t k = 0; k < K && !rc; k++) {
         kgx_ctx *x = xs[k & 1];
         if (k >= 2)
             HIP_TRY(hipEventSynchronize(c->chunk_h2d[k - 2])); /* x's staging buffer is free */
         const auto ts = now();
         rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp);
-        stage_ms += ms(ts, now());
+        const auto te = now();
+        stage_ms += ms(ts, te);
         if (rc || (rc = enqueue(x, k)))
             break;
+        if (timing)
+            ht.insert(ht.end(), {(double)k, ms(T0, ts), ms(T0, te), ms(T0, now())});
         /* collect what has landed meanwhile */
-        while (!rc && next < k && hipEventQuery(c->chunk_done[next]) == hipSuccess)
+        while (!rc && next < k && hipEventQuery(c->chunk_done[next]) == hipSuccess) {
             rc = collect(next++);
+            if (timing)
+                ht.insert(ht.end(), {-1.0 - (double)(next - 1), ms(T0, now()), 0.0, 0.0});
+        }
     }
-    while (!rc && next < K)
+    while (!rc && next < K) {
         rc = collect(next++);
+        if (timing)
+            ht.insert(ht.end(), {-1.0 - (double)(next - 1), ms(T0, now()), 0.0, 0.0});
+    }
+    for (size_t i = 0; timing && i + 3 < ht.size(); i += 4) {
+        if (ht[i] >= 0)
+            std::fprintf(stderr, "[kgx] host chunk %d: stage %.3f-%.3f, enqueued %.3f ms\n", (int)ht[i], ht[i + 1],
+                         ht[i + 2], ht[i + 3]);
+        else
+            std::fprintf(stderr, "[kgx] host collect %d done %.3f ms\n", (int)(-ht[i] - 1), ht[i + 1]);
+    }
     /* drain everything, whatever happened above */
     const hipError_t e0 = hipStreamSynchronize(xs[0]->stream), e1 = hipStreamSynchronize(xs[1]->stream);
     const hipError_t e2 = hipStreamSynchronize(cs);
@@ -2035,6 +2054,12 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
             P.device_ms += b;
             P.gather_ms += g;
             P.d2h_ms += d;
+            if (timing) { /* the device's clock, from chunk 0's first event */
+                float t0 = 0;
+                HIP_TRY(hipEventElapsedTime(&t0, c->prof_ev[0], c->prof_ev[4 * k]));
+                std::fprintf(stderr, "[kgx] device chunk %u: h2d %.3f, kernels %.3f, gather %.3f, d2h %.3f, done %.3f ms\n",
+                             k, t0, t0 + a, t0 + a + b, t0 + a + b + g, t0 + a + b + g + d);
+            }
         }
         const uint64_t recb = r12 ? 12 : 16;
         P.d2h_bytes = hbase * recb + cbase * sizeof(kgx_call) +

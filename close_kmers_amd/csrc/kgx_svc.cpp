@@ -73,13 +73,20 @@ struct SvcState {
     kgx_otu *d_otus = nullptr;
     const void *table = nullptr;
     uint64_t num_sigs = 0;
-    std::atomic<uint64_t> free_mask{0};
-    uint32_t seq[SVC_MAX_SLOTS] = {}; /* a slot's last request number (its holder's) */
+    /* the host side of each slot, a line apiece: a call touches only its
+     * own slot's line (a pool's threads each settle on a slot of their own,
+     * take_slot), never one that every caller writes */
+    struct alignas(64) Slot {
+        std::atomic<uint32_t> busy{0};
+        uint32_t seq = 0;                /* the last request number (its holder's) */
+        std::atomic<uint64_t> n_calls{0}; /* calls served through the slot (its holder counts) */
+    };
+    Slot slot[SVC_MAX_SLOTS];
     std::mutex mu;                    /* instances */
     std::deque<hipEvent_t> running;   /* end of each enqueued instance */
     std::vector<hipEvent_t> spare;
     std::atomic<int64_t> next_check{0};
-    std::atomic<uint64_t> n_calls{0}, n_launches{0}, n_busy{0};
+    std::atomic<uint64_t> n_launches{0}, n_busy{0};
     /* KGX_SVC_DEBUG=1: the device's phase stamps per call, summed (ns):
      * [0] request stored -> done seen on the host (wall), [1..5] the device
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
@@ -91,11 +98,13 @@ struct SvcState {
      * callers holds fewer CPUs; 0 = spin only */
     uint32_t sleep_us = 0;
     std::atomic<bool> broken{false}; /* a launch failed or a call timed out: callers take other paths */
-    std::atomic<uint32_t> users{0};  /* callers inside kgx_svc_call holding this state */
     std::atomic<uint64_t> n_abandoned{0}; /* slots given up after a 10-s wait (never handed out again) */
     int priority = 0; /* the stream's priority (hipDeviceGetStreamPriorityRange: lower = higher) */
-    int quad_probe = 1; /* proteins up to 520 aa probed by 4-lane quads per 64-B line (KGX_SVC_PROBE=thread: a
-                           thread per window) */
+    /* KGX_SVC_PROBE=quad: proteins up to 520 aa probed by 4-lane quads per
+     * 64-B line instead of a thread per window -- measured slower in the
+     * resident kernel (r4b: probe phase 7.3 vs 5.0 us per call), kept as an
+     * option */
+    int quad_probe = 0;
 };
 
 namespace {
@@ -123,16 +132,29 @@ inline void wc_fence()
 #endif
 }
 
+std::atomic<uint32_t> g_threads{0};
+
+/* the calling thread's number, fixed at its first call: it picks the
+ * thread's user shard and its first-choice slot */
+uint32_t thread_index()
+{
+    thread_local uint32_t t = ~0u;
+    if (t == ~0u)
+        t = g_threads.fetch_add(1, std::memory_order_relaxed);
+    return t;
+}
+
 /* a caller's hold on the service: shutdown waits until none is left */
 struct SvcUse {
+    std::atomic<uint32_t> *n = nullptr;
     SvcState *s = nullptr;
     SvcUse() = default;
     SvcUse(const SvcUse &) = delete;
     SvcUse &operator=(const SvcUse &) = delete;
     ~SvcUse()
     {
-        if (s)
-            s->users.fetch_sub(1, std::memory_order_release);
+        if (n)
+            n->fetch_sub(1, std::memory_order_release);
     }
 };
 
@@ -305,7 +327,6 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     s->d_calls = reinterpret_cast<kgx_call *>(dp + o_res + b_res + b_hits);
     s->otus = reinterpret_cast<kgx_otu *>(hp + o_res + b_res + b_hits + b_calls);
     s->d_otus = reinterpret_cast<kgx_otu *>(dp + o_res + b_res + b_hits + b_calls);
-    s->free_mask.store(slots >= 64 ? ~0ull : ((1ull << slots) - 1), std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> lk(g_live_mu);
         g_live.insert(s);
@@ -318,24 +339,38 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     return KGX_OK;
 }
 
+constexpr uint32_t kShards = sizeof(kgx_image::svc_users) / sizeof(kgx_image::svc_users[0]);
+
 /* the image's service, created on first use with its configuration, held
- * by `use` until the caller returns (svc_shutdown waits for every hold) */
-int get(kgx_image *img, SvcUse &use)
+ * by `use` until the caller returns.  No lock on the way in: the caller
+ * counts itself in its shard, then reads the service pointer; shutdown
+ * clears the pointer, then waits for every shard to read 0.  Both pairs are
+ * sequentially consistent, so a caller either sees the pointer cleared (and
+ * takes the lock, behind the shutdown) or is counted before shutdown looks. */
+int enter(kgx_image *img, SvcUse &use)
 {
-    std::lock_guard<std::mutex> lk(img->svc_mu);
-    if (!img->svc) {
-        /* KGX_SVC_LIFE_US: a default for experiments, for images that
-         * kgx_svc_config never configured */
-        uint64_t life = img->svc_life_us;
-        if (const char *e = std::getenv("KGX_SVC_LIFE_US"); e && !img->svc_configured)
-            life = std::max<uint64_t>(10, std::strtoull(e, nullptr, 10));
-        int rc = create(img, img->svc_slots, img->svc_idle_us, life, &img->svc);
-        if (rc)
-            return rc;
+    std::atomic<uint32_t> &n = img->svc_users[thread_index() % kShards].n;
+    for (;;) {
+        n.fetch_add(1, std::memory_order_seq_cst);
+        if (SvcState *s = img->svc.load(std::memory_order_seq_cst)) {
+            use.n = &n;
+            use.s = s;
+            return KGX_OK;
+        }
+        n.fetch_sub(1, std::memory_order_release);
+        std::lock_guard<std::mutex> lk(img->svc_mu);
+        if (!img->svc.load(std::memory_order_relaxed)) {
+            /* KGX_SVC_LIFE_US: a default for experiments, for images that
+             * kgx_svc_config never configured */
+            uint64_t life = img->svc_life_us;
+            if (const char *e = std::getenv("KGX_SVC_LIFE_US"); e && !img->svc_configured)
+                life = std::max<uint64_t>(10, std::strtoull(e, nullptr, 10));
+            SvcState *s = nullptr;
+            if (int rc = create(img, img->svc_slots, img->svc_idle_us, life, &s))
+                return rc;
+            img->svc.store(s, std::memory_order_seq_cst);
+        }
     }
-    img->svc->users.fetch_add(1, std::memory_order_acquire);
-    use.s = img->svc;
-    return KGX_OK;
 }
 
 /* detach and free the image's service (svc_mu held): new callers create a
@@ -344,22 +379,29 @@ int get(kgx_image *img, SvcUse &use)
  * freed */
 void shutdown_locked(kgx_image *img)
 {
-    SvcState *s = img->svc;
+    SvcState *s = img->svc.exchange(nullptr, std::memory_order_seq_cst);
     if (!s)
         return;
-    img->svc = nullptr;
-    while (s->users.load(std::memory_order_acquire) != 0)
+    for (;;) {
+        uint32_t inside = 0;
+        for (uint32_t i = 0; i < kShards; i++)
+            inside += img->svc_users[i].n.load(std::memory_order_seq_cst);
+        if (!inside)
+            break;
         std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     destroy(s);
 }
 
+/* the thread's own slot when it is free (a pool of at most `slots` threads
+ * keeps one slot each), else the first free one after it */
 bool take_slot(SvcState *s, uint32_t &slot)
 {
-    uint64_t m = s->free_mask.load(std::memory_order_relaxed);
-    while (m) {
-        const uint32_t i = (uint32_t)__builtin_ctzll(m);
-        if (s->free_mask.compare_exchange_weak(m, m & ~(1ull << i), std::memory_order_acquire,
-                                               std::memory_order_relaxed)) {
+    const uint32_t first = thread_index() % s->slots;
+    for (uint32_t k = 0; k < s->slots; k++) {
+        const uint32_t i = (first + k) % s->slots;
+        std::atomic<uint32_t> &b = s->slot[i].busy;
+        if (b.load(std::memory_order_relaxed) == 0 && b.exchange(1, std::memory_order_acquire) == 0) {
             slot = i;
             return true;
         }
@@ -367,7 +409,7 @@ bool take_slot(SvcState *s, uint32_t &slot)
     return false;
 }
 
-void give_slot(SvcState *s, uint32_t slot) { s->free_mask.fetch_or(1ull << slot, std::memory_order_release); }
+void give_slot(SvcState *s, uint32_t slot) { s->slot[slot].busy.store(0, std::memory_order_release); }
 
 }  // namespace
 
@@ -412,12 +454,17 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
     if (!img || !name || !value)
         return fail(KGX_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(img->svc_mu);
-    const SvcState *s = img->svc;
+    const SvcState *s = img->svc.load(std::memory_order_acquire);
     const std::string n(name);
     if (n == "slots")
         *value = img->svc_slots;
     else if (n == "calls")
-        *value = s ? s->n_calls.load() : 0;
+    {
+        uint64_t c = 0;
+        for (uint32_t i = 0; s && i < s->slots; i++)
+            c += s->slot[i].n_calls.load(std::memory_order_relaxed);
+        *value = c;
+    }
     else if (n == "launches")
         *value = s ? s->n_launches.load() : 0;
     else if (n == "busy")
@@ -460,7 +507,7 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         (want & KGX_WANT_OTU && W && !otus))
         return fail(KGX_EINVAL, "null result buffer");
     SvcUse use;
-    int rc = get(img, use);
+    int rc = enter(img, use);
     if (rc)
         return rc;
     SvcState *s = use.s;
@@ -486,10 +533,10 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     h.want = want;
     h.prm = p;
     h.debug = s->debug ? 1u : 0u;
-    uint32_t q = s->seq[slot] + 1;
+    uint32_t q = s->slot[slot].seq + 1;
     if (q == 0 || q == __atomic_load_n(&s->out[slot].done, __ATOMIC_RELAXED))
         q++;
-    s->seq[slot] = q;
+    s->slot[slot].seq = q;
     /* device memory is written through a write-combining BAR mapping: the
      * fences order the request's bytes before its number and push it out */
     if (s->reqmem)
@@ -575,8 +622,9 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     } else if (n_otus) {
         *n_otus = 0;
     }
+    std::atomic<uint64_t> &nc_slot = s->slot[slot].n_calls;
+    nc_slot.store(nc_slot.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
     give_slot(s, slot);
-    s->n_calls++;
     return KGX_OK;
 }
 

@@ -1,0 +1,174 @@
+/*
+ * beside_check -- a server whose pool mixes per-sequence calls and chunk
+ * batches on one image (threadpool.cc:18-60: some workers run
+ * process_aa_seq per sequence, another a handler's whole chunk): T threads
+ * call the resident service (kgx_svc_call) while one thread runs
+ * kgx_process_batch on its own context, over and over.  Native threads, so
+ * the clocks time the GPU paths, not a Python harness's GIL
+ * (tests/test_gpu_svc.py::test_svc_beside_batches_native).
+ *
+ *   beside_check N_KEYS NUM_SIGS QUERIES.bin T SECONDS
+ *
+ * QUERIES.bin: uint64 n, uint64 offsets[n+1], residues.  The image is the
+ * bench's synthetic one (N_KEYS distinct keys, bench.py C2).  Every batch run
+ * beside the service must equal the batch run alone, byte for byte; every
+ * service answer must equal its sequence's slice of that batch.  Prints one
+ * JSON line; exit 1 on a mismatch or an ABI error.
+ */
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kgx.h"
+
+using clk = std::chrono::steady_clock;
+
+static double pct(std::vector<double> v, double p)
+{
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[std::min(v.size() - 1, (size_t)(p / 100.0 * (double)v.size()))];
+}
+
+struct Batch {
+    std::vector<uint64_t> hoff, coff;
+    std::vector<kgx_hit> hits;
+    std::vector<kgx_call> calls;
+    bool operator==(const Batch &o) const
+    {
+        return hoff == o.hoff && coff == o.coff && hits.size() == o.hits.size() && calls.size() == o.calls.size() &&
+               !std::memcmp(hits.data(), o.hits.data(), hits.size() * sizeof(kgx_hit)) &&
+               !std::memcmp(calls.data(), o.calls.data(), calls.size() * sizeof(kgx_call));
+    }
+};
+
+int main(int argc, char **argv)
+{
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: beside_check N_KEYS NUM_SIGS QUERIES.bin T SECONDS\n");
+        return 2;
+    }
+    const uint64_t n_keys = std::strtoull(argv[1], nullptr, 10), num_sigs = std::strtoull(argv[2], nullptr, 10);
+    const int T = std::max(1, std::atoi(argv[4]));
+    const double seconds = std::atof(argv[5]);
+    std::ifstream in(argv[3], std::ios::binary);
+    uint64_t n = 0;
+    in.read(reinterpret_cast<char *>(&n), 8);
+    std::vector<uint64_t> off(n + 1);
+    in.read(reinterpret_cast<char *>(off.data()), (std::streamsize)(8 * (n + 1)));
+    std::string res(off[n], '\0');
+    in.read(&res[0], (std::streamsize)res.size());
+    if (!in || n == 0) {
+        std::fprintf(stderr, "beside_check: short query file\n");
+        return 2;
+    }
+    kgx_image *img = nullptr;
+    uint64_t entries = 0;
+    kgx_ctx *ctx = nullptr;
+    if (kgx_image_build_synthetic_distinct(n_keys, n_keys, num_sigs, 0, &img, &entries) != KGX_OK ||
+        kgx_ctx_create(img, &ctx) != KGX_OK) {
+        std::fprintf(stderr, "beside_check: %s\n", kgx_last_error());
+        return 1;
+    }
+    kgx_params prm;
+    kgx_params_default(&prm);
+    const uint32_t want = KGX_WANT_HITS | KGX_WANT_CALLS;
+    auto run_batch = [&](Batch &b) {
+        kgx_result r;
+        if (kgx_process_batch(ctx, &prm, res.data(), off.data(), (uint32_t)n, want, &r) != KGX_OK)
+            return false;
+        b.hoff.assign(r.hit_offsets, r.hit_offsets + n + 1);
+        b.coff.assign(r.call_offsets, r.call_offsets + n + 1);
+        b.hits.assign(r.hits, r.hits + b.hoff[n]);
+        b.calls.assign(r.calls, r.calls + b.coff[n]);
+        return true;
+    };
+    Batch ref;
+    std::vector<double> alone;
+    for (int rep = 0; rep < 30; rep++) {
+        Batch b;
+        const auto t0 = clk::now();
+        if (!run_batch(b)) {
+            std::fprintf(stderr, "beside_check: %s\n", kgx_last_error());
+            return 1;
+        }
+        alone.push_back(std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+        if (rep == 0)
+            ref = std::move(b);
+        else if (!(b == ref)) {
+            std::fprintf(stderr, "beside_check: batches alone differ\n");
+            return 1;
+        }
+    }
+    std::atomic<bool> stop{false}, failed{false};
+    std::atomic<uint64_t> n_calls{0}, n_busy{0}, svc_bad{0};
+    std::vector<double> beside;
+    uint64_t batch_bad = 0;
+    std::thread bt([&]() {
+        while (!stop.load()) {
+            Batch b;
+            const auto t0 = clk::now();
+            if (!run_batch(b)) {
+                failed = true;
+                return;
+            }
+            beside.push_back(std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+            batch_bad += !(b == ref);
+        }
+    });
+    std::vector<std::thread> ws;
+    const auto t_end = clk::now() + std::chrono::duration<double>(seconds);
+    const auto t0 = clk::now();
+    for (int t = 0; t < T; t++)
+        ws.emplace_back([&, t]() {
+            std::vector<kgx_hit> h(4096);
+            std::vector<kgx_call> c(4096);
+            for (uint64_t k = (uint64_t)t; clk::now() < t_end; k += (uint64_t)T) {
+                const uint64_t s = k % n, len = off[s + 1] - off[s];
+                uint64_t nh = 0, nc = 0;
+                const int rc = kgx_svc_call(img, &prm, res.data() + off[s], len, want, h.data(), h.size(), &nh,
+                                            c.data(), c.size(), &nc, nullptr, 0, nullptr);
+                if (rc == KGX_EBUSY) {
+                    n_busy++;
+                    continue;
+                }
+                if (rc != KGX_OK) {
+                    failed = true;
+                    return;
+                }
+                n_calls++;
+                bool ok = nh == ref.hoff[s + 1] - ref.hoff[s] && nc == ref.coff[s + 1] - ref.coff[s];
+                for (uint64_t j = 0; ok && j < nh; j++) {
+                    kgx_hit x = h[j];
+                    x.seq = (uint32_t)s;
+                    ok = !std::memcmp(&x, &ref.hits[ref.hoff[s] + j], sizeof x);
+                }
+                ok = ok && !std::memcmp(c.data(), ref.calls.data() + ref.coff[s], nc * sizeof(kgx_call));
+                svc_bad += !ok;
+            }
+        });
+    for (auto &w : ws)
+        w.join();
+    const double tp = std::chrono::duration<double>(clk::now() - t0).count();
+    stop = true;
+    bt.join();
+    std::printf("{\"service_threads\": %d, \"batch_proteins\": %llu, \"batch_alone_ms\": {\"p50\": %.3f, \"max\": %.3f}, "
+                "\"batch_beside_ms\": {\"n\": %zu, \"p50\": %.3f, \"p90\": %.3f, \"max\": %.3f}, "
+                "\"service_calls\": %llu, \"service_calls_per_s\": %.4g, \"service_busy\": %llu, "
+                "\"batch_mismatches\": %llu, \"service_mismatches\": %llu, \"failed\": %d}\n",
+                T, (unsigned long long)n, pct(alone, 50), pct(alone, 100), beside.size(), pct(beside, 50),
+                pct(beside, 90), pct(beside, 100), (unsigned long long)n_calls.load(), (double)n_calls.load() / tp,
+                (unsigned long long)n_busy.load(), (unsigned long long)batch_bad,
+                (unsigned long long)svc_bad.load(), failed.load() ? 1 : 0);
+    if (failed)
+        std::fprintf(stderr, "beside_check: %s\n", kgx_last_error());
+    kgx_ctx_destroy(ctx);
+    kgx_image_close(img);
+    return failed || batch_bad || svc_bad ? 1 : 0;
+}

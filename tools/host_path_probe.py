@@ -91,7 +91,11 @@ def main():
         if args.timing:
             print(f"--- {key}", file=sys.stderr, flush=True)
             os.environ["KGX_TIMING"] = "1"
-            ctx.process_batch(res, off, params, want=3, copy=False)
+            for prof in (0, 1):  # the host's clock alone, then with the per-chunk device events
+                print(f"--- host_profile {prof}", file=sys.stderr, flush=True)
+                ctx.set_option("host_profile", prof)
+                run()
+            ctx.set_option("host_profile", 0)
             del os.environ["KGX_TIMING"]
     out["ms_by_host_chunks"] = times
     out["compact"] = bool(args.compact)
