@@ -625,70 +625,118 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     }
     /* 4c. OTU tallies (KmerOtuStats::finalize, kguts.h:196-218), in LDS
      * (hpos, hrec and codes are free once the records are stored and the
-     * scorer is done).  Wave 0 collects the flagged hits' distinct OTUs in its
-     * registers -- lane j holds the j-th value met and its count -- with one
-     * ballot round per distinct value among each 64 hits (a handful: the hits
-     * of a call share few OTUs), then places each value by its rank among the
-     * others (= the std::map's key order).  More than 64 distinct values take
-     * the general path below.  Then the pairs are std::sort'ed by count
-     * (lstd_sort_wave64 / lstd_sort_on replay libstdc++'s tie order). */
+     * scorer is done): the flagged hits' OTUs compacted in hit order
+     * (ballots).  One value among them (the usual case) is one pair.  Else
+     * the values are sorted -- a bitonic network over P = max(256,
+     * 2^ceil(log2 m)) entries, P / 256 per thread in registers: exchanges
+     * within a wave by lane shuffles, between waves through LDS, between a
+     * thread's own entries in place -- and each run of equal values is one
+     * pair, in ascending key order (the std::map's).  Then the pairs are
+     * std::sort'ed by count: lstd_sort_wave64 / lstd_sort_on replay
+     * libstdc++'s tie order.  (r4b: O(m^2) count and rank scans, 18.8 us at
+     * 36 OTUs per call; a wave's register list of distinct values, 22.6.) */
     if (want_otu) {
         __shared__ LstdPart ostack[64];
+        __shared__ uint32_t multi;
         if (dbg)
             a.dbg[7] = wall_clock64();
-        kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
+        if (t == 0)
+            multi = 0;
         __syncthreads();
-        if (wave == 0) {
-            int32_t dv = 0;
-            uint32_t dc = 0, dn = 0;
-            bool over = false;
-            for (uint32_t h0 = 0; h0 < nh && !over; h0 += 64) {
-                const uint32_t i = h0 + lane;
-                const bool f = i < nh && oflag[i];
-                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
-                uint64_t rem = __ballot(f);
-                while (rem) {
-                    const int32_t y = (int32_t)rl32((uint32_t)x, lowbit(rem));
-                    const uint64_t mk = __ballot(f && x == y);
-                    rem &= ~mk;
-                    const uint64_t at = __ballot(lane < dn && dv == y);
-                    if (at) {
-                        if (lane == lowbit(at))
-                            dc += (uint32_t)__popcll(mk);
-                    } else if (dn < 64) {
-                        if (lane == dn) {
-                            dv = y;
-                            dc = (uint32_t)__popcll(mk);
-                        }
-                        dn++;
+        int32_t *v = reinterpret_cast<int32_t *>(hpos);
+        uint32_t m = 0;
+        for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
+            const uint32_t i = t + 256 * j;
+            const bool f = i < nh && oflag[i];
+            const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+            const uint64_t bm = __ballot(f);
+            if (lane == 0)
+                wave_cnt[wave] = (uint32_t)__popcll(bm);
+            __syncthreads();
+            uint32_t before = 0, total = 0;
+            for (uint32_t w = 0; w < 4; w++) {
+                before += w < wave ? wave_cnt[w] : 0u;
+                total += wave_cnt[w];
+            }
+            __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
+            if (f)
+                v[m + before + lanes_below(bm)] = x;
+            m += total;
+            __syncthreads();
+        }
+        /* plain stores of 1, no atomics: same-address LDS atomics from every
+         * differing lane serialize */
+        const int32_t v0 = m ? v[0] : 0;
+        for (uint32_t i = t; i < m; i += 256)
+            if (v[i] != v0)
+                multi = 1;
+        __syncthreads();
+        kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
+        uint32_t d = 0;
+        if (m && !multi) {
+            d = 1;
+            if (t == 0)
+                o[0] = kgx_otu{v0, (int32_t)m};
+        } else if (m) {
+            uint32_t R = 1;
+            while (256u * R < m)
+                R <<= 1;
+            const uint32_t P = 256u * R;
+            int32_t val[FJ];
+#pragma unroll
+            for (uint32_t r = 0; r < FJ; r++) {
+                const uint32_t e = t + 256u * r;
+                val[r] = (r < R && e < m) ? v[e] : INT32_MAX; /* the padding sorts last */
+            }
+            __syncthreads(); /* every entry read before the exchanges write v */
+            for (uint32_t k = 2; k <= P; k <<= 1) {
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    if (j >= 256) { /* a thread's own entries r and r ^ (j / 256) */
+                        const uint32_t rj = j >> 8;
+#pragma unroll
+                        for (uint32_t r = 0; r < FJ; r++)
+#pragma unroll
+                            for (uint32_t r2 = r + 1; r2 < FJ; r2++)
+                                if (r2 == (r ^ rj) && r2 < R) {
+                                    const bool up = ((t + 256u * r) & k) == 0;
+                                    const int32_t lo = min(val[r], val[r2]), hi = max(val[r], val[r2]);
+                                    val[r] = up ? lo : hi;
+                                    val[r2] = up ? hi : lo;
+                                }
                     } else {
-                        over = true;
-                        break;
+                        if (j >= 64) { /* the partner is in another wave */
+#pragma unroll
+                            for (uint32_t r = 0; r < FJ; r++)
+                                if (r < R)
+                                    v[t + 256u * r] = val[r];
+                            __syncthreads();
+                        }
+#pragma unroll
+                        for (uint32_t r = 0; r < FJ; r++) {
+                            if (r < R) {
+                                const uint32_t e = t + 256u * r;
+                                const int32_t b = j >= 64 ? v[e ^ j] : __shfl_xor(val[r], (int)j);
+                                /* the pair's lower entry keeps the min when ascending */
+                                const bool keep_min = ((e & j) == 0) == ((e & k) == 0);
+                                val[r] = keep_min ? min(val[r], b) : max(val[r], b);
+                            }
+                        }
+                        if (j >= 64)
+                            __syncthreads();
                     }
                 }
             }
-            if (!over) {
-                uint32_t r = 0;
-                for (uint32_t j = 0; j < dn; j++)
-                    r += (int32_t)rl32((uint32_t)dv, j) < dv ? 1u : 0u;
-                if (lane < dn)
-                    o[r] = kgx_otu{dv, (int32_t)dc};
-            }
-            if (lane == 0)
-                n_otu = over ? ~0u : dn;
-        }
-        __syncthreads();
-        uint32_t d = n_otu;
-        if (d == ~0u) {
-            /* the general path: the flagged hits' OTUs compacted in hit order
-             * (ballots), each value's count and first occurrence by a scan of
-             * the list, the distinct values placed in key order by rank */
-            int32_t *v = reinterpret_cast<int32_t *>(hpos);
-            uint32_t m = 0;
-            for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
-                const uint32_t i = t + 256 * j;
-                const bool f = i < nh && oflag[i];
-                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+#pragma unroll
+            for (uint32_t r = 0; r < FJ; r++)
+                if (r < R)
+                    v[t + 256u * r] = val[r];
+            __syncthreads();
+            /* each run's first entry, compacted in order: its value, and the
+             * run's length to the next first */
+            uint32_t *first = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
+            for (uint32_t r = 0; r < R; r++) {
+                const uint32_t e = t + 256u * r;
+                const bool f = e < m && (e == 0 || v[e - 1] != v[e]);
                 const uint64_t bm = __ballot(f);
                 if (lane == 0)
                     wave_cnt[wave] = (uint32_t)__popcll(bm);
@@ -698,44 +746,19 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     before += w < wave ? wave_cnt[w] : 0u;
                     total += wave_cnt[w];
                 }
-                __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
                 if (f)
-                    v[m + before + lanes_below(bm)] = x;
-                m += total;
+                    first[d + before + lanes_below(bm)] = e;
+                d += total;
                 __syncthreads();
             }
-            uint32_t *cnt = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
-            uint8_t *first = codes;
-            for (uint32_t i = t; i < m; i += 256) {
-                const int32_t x = v[i];
-                uint32_t c = 0;
-                bool fst = true;
-#pragma unroll 8
-                for (uint32_t j = 0; j < m; j++) {
-                    const bool e = v[j] == x;
-                    c += e ? 1u : 0u;
-                    fst = fst && !(e && j < i);
-                }
-                cnt[i] = c;
-                first[i] = fst ? 1 : 0;
+            for (uint32_t i = t; i < d; i += 256) {
+                const uint32_t e = first[i], e2 = i + 1 < d ? first[i + 1] : m;
+                o[i] = kgx_otu{v[e], (int32_t)(e2 - e)};
             }
-            __syncthreads();
-            for (uint32_t i = t; i < m; i += 256) {
-                if (!first[i])
-                    continue;
-                const int32_t x = v[i];
-                uint32_t r = 0;
-#pragma unroll 8
-                for (uint32_t j = 0; j < m; j++)
-                    r += (first[j] && v[j] < x) ? 1u : 0u;
-                o[r] = kgx_otu{x, (int32_t)cnt[i]};
-            }
-            /* distinct values: a block-wide count of the firsts (no serial scan) */
-            d = 0;
-            for (uint32_t j0 = 0; j0 < m; j0 += 256)
-                d += (uint32_t)__syncthreads_count(j0 + t < m && first[j0 + t]);
             __syncthreads();
         }
+        if (dbg)
+            a.dbg[8] = wall_clock64();
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
          * it for up to 64 pairs (lstd_sort_wave64), thread 0 beyond (its
          * partition stack in LDS) */

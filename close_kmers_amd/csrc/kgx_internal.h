@@ -253,14 +253,15 @@ struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the p
     uint32_t copy; /* = req, written before it: a line read with copy != req is incomplete */
 };
 struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
-    uint64_t stamp[8];  /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced */
+    uint64_t stamp[16]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
+                           0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */
     uint32_t done;       /* = req once the records and counts are visible */
     uint32_t pad[12];
 };
-static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 64,
+static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 128,
               "service slot lines");
 /* slots workgroups on stream; each leaves life_ticks after its start (device
  * wall clock, 100 MHz) or on stop */

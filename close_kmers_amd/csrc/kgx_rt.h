@@ -419,6 +419,7 @@ struct kgx_ctx {
     kgx::PinnedVec<uint32_t> h_counts;
     kgx::PinnedVec<uint32_t> h_hits12; /* 12-B records (3 words per hit, no key) */
     int host_rec12 = 1; /* streamed: 12-B records, key re-encoded on the host (option "host_rec12") */
+    int host_h2d_first = 1; /* streamed: chunk k's D2H waits for chunk k+1's H2D (option "host_h2d_first") */
     /* small host batches (<= small_batch residues, option "small_batch", 0 =
      * off): planned on the host, read by the device from the mapped staging
      * blob, results stored into mapped memory: one host wait per batch */

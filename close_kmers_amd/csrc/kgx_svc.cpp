@@ -92,7 +92,7 @@ struct SvcState {
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
      * + scorer, and [5] 3->6 the record stores alone) */
     bool debug = false;
-    std::atomic<uint64_t> phase_ns[7] = {};
+    std::atomic<uint64_t> phase_ns[8] = {};
     /* KGX_SVC_SLEEP_US: a caller sleeps this long before it spins for its
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
@@ -310,8 +310,10 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     if ((!dm || std::atoi(dm) != 0) &&
         hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, img->device) == hipSuccess && large_bar) {
         void *r = nullptr;
+        /* on the service's stream: a device-wide synchronisation would wait
+         * for every batch in flight on the device */
         if (hipExtMallocWithFlags(&r, b_hdr + b_res, hipDeviceMallocFinegrained) == hipSuccess &&
-            hipMemset(r, 0, b_hdr) == hipSuccess && hipDeviceSynchronize() == hipSuccess) {
+            hipMemsetAsync(r, 0, b_hdr, s->stream) == hipSuccess && hipStreamSynchronize(s->stream) == hipSuccess) {
             s->reqmem = static_cast<char *>(r); /* one address for the host and the device */
             s->hdr = s->d_hdr = reinterpret_cast<SvcSlotHdr *>(s->reqmem);
             s->res = s->d_res = reinterpret_cast<uint8_t *>(s->reqmem + b_hdr);
@@ -477,7 +479,7 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? (uint64_t)(s->priority + 100) : 0;
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
-    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '6') /* "phase_n0".."phase_n6" */
+    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '7') /* "phase_n0".."phase_n7" */
         *value = s ? s->phase_ns[n[7] - '0'].load() : 0;
     else
         return fail(KGX_EINVAL, "unknown service statistic " + n);
@@ -600,8 +602,10 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         for (int k = 1; k <= 4; k++)
             s->phase_ns[k] += (st[k] - st[k - 1]) * 10; /* 100 MHz ticks */
         s->phase_ns[5] += (st[6] - st[3]) * 10; /* compaction end -> thread 0's record stores issued */
-        if (want & KGX_WANT_OTU)
+        if (want & KGX_WANT_OTU) {
             s->phase_ns[6] += (st[4] - st[7]) * 10; /* the OTU tally alone */
+            s->phase_ns[7] += (st[4] - st[8]) * 10; /* ... its sort by count */
+        }
     }
     const SvcSlotOut &o = s->out[slot];
     const uint32_t nh = o.nh, nc = o.nc, no = (want & KGX_WANT_OTU) ? o.no : 0u;

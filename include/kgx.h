@@ -327,7 +327,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * re-encoded on the host from the residues; else the 16-B records) plus the
  * batch's hit mask, and "host_threads" (default 12) host threads expand them
  * into kgx_hit records while later chunks stream ("host_nt" 1: with streaming
- * stores).
+ * stores).  "host_h2d_first" 1 (default): a chunk's D2H starts once the next
+ * chunk's residues are up (an H2D beside the D2H's stores is slowed 3-4x).
  * "host_stream" 1 (default): chunks need no host round trip -- CSR offsets
  * are scanned on the device and the bulk copies (on a separate copy stream)
  * are sized on the device into host regions sized from the hit / call / OTU
@@ -465,8 +466,9 @@ int kgx_svc_stop(kgx_image *img);
  * the device's highest priority, so it has a hardware queue of its own and
  * batch streams never queue behind the persistent instances;
  * KGX_SVC_PRIORITY=normal gives it a normal stream),
- * "phase_n0".."phase_n6" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
- * call, the device phases, and the OTU tally of calls that want it) */
+ * "phase_n0".."phase_n7" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
+ * call, the device phases, the OTU tally of calls that want it and the
+ * tally's final sort by count) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option

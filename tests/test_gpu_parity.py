@@ -735,8 +735,9 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_stream", 1)
         ctx.set_option("host_hits16", 1)
         ctx.set_option("host_copy_blocks", 1)
-        for k in (16, 37, 64):
+        for k, h2d_first in ((16, 1), (37, 0), (64, 1)):  # chunk k's D2H behind chunk k+1's H2D, or not
             ctx.set_option("host_chunks", k)
+            ctx.set_option("host_h2d_first", h2d_first)
             for _ in range(2):  # the second pass runs with the rates the first one raised
                 got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=7)
                 assert_same(got, want, len(off) - 1)
@@ -746,6 +747,7 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
     finally:
         ctx.set_option("host_copy_blocks", 64)
         ctx.set_option("host_chunks", 3)
+        ctx.set_option("host_h2d_first", 1)
 
 
 @pytest.mark.parametrize("schedule", ["streamed_rec12", "streamed_rec16", "exact", "small", "aos24",

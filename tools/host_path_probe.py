@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--nt", default="1", help="host_nt settings to try")
     ap.add_argument("--score", default="0", help="score_variant settings to try (0 hybrid, 1 wave)")
     ap.add_argument("--want", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], help="name=value context option for every setting")
     ap.add_argument("--timing", action="store_true", help="one extra KGX_TIMING pass per setting (stderr)")
     ap.add_argument("--compact", action="store_true",
                     help="kgx_process_batch_compact (records + mask, bench.py's host_path value) instead of kgx_hit")
@@ -63,6 +64,10 @@ def main():
               for tp in args.taper.split(",")]
     combos = [c + (int(r), int(t), int(sv)) for c in combos for r in args.rec12.split(",") for t in args.nt.split(",")
               for sv in args.score.split(",")]
+    for o in args.opt:
+        name, val = o.split("=")
+        ctx.set_option(name, int(val))
+        out.setdefault("options", {})[name] = int(val)
     for k, hc, nb, h16, nt, st, cf, hs, tp, r12, ntst, sv in combos:
         ctx.set_option("score_variant", sv)
         ctx.set_option("host_rec12", r12)
