@@ -25,12 +25,14 @@ SERVER = os.path.join(PKG, "kgx_server")
 COALESCE_CHECK = os.path.join(ROOT, "tests", "native", "coalesce_check")
 # per-sequence service callers beside a batch caller (tests/test_gpu_svc.py)
 BESIDE_CHECK = os.path.join(ROOT, "tests", "native", "beside_check")
+# the one-wave std::sort replay against the serial one (tests/test_gpu_svc.py)
+WAVE_SORT_CHECK = os.path.join(ROOT, "tests", "native", "wave_sort_check")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 LIB_SOURCES = ["kgx_lookup.hip", "kgx_fused.hip", "kgx_synth.hip", "kgx_tables.hip", "kgx_fq.hip", "kgx_runtime.cpp",
                "kgx_pool.cpp", "kgx_svc.cpp", "kguts_hip.cpp", "kgx_handlers.cpp"]
-HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h", "kgx_handlers.h"]
+HEADERS = ["kgx_internal.h", "kgx_device.h", "kguts_hip.h", "kgx_rt.h", "kgx_lstd.h", "kgx_handlers.h", "kgx_wave_sort.h"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-Wall", "-Wno-unused-function"]
 
@@ -75,7 +77,8 @@ def build(force: bool = False, verbose: bool = False) -> None:
         os.replace(tmp, LIB)
     for exe, esrc in ((QUERY, os.path.join(CSRC, "kgx_query.cpp")), (SERVER, os.path.join(CSRC, "kgx_server.cpp")),
                       (COALESCE_CHECK, os.path.join(ROOT, "tests", "native", "coalesce_check.cpp")),
-                      (BESIDE_CHECK, os.path.join(ROOT, "tests", "native", "beside_check.cpp"))):
+                      (BESIDE_CHECK, os.path.join(ROOT, "tests", "native", "beside_check.cpp")),
+                      (WAVE_SORT_CHECK, os.path.join(ROOT, "tests", "native", "wave_sort_check.cpp"))):
         if not os.path.exists(esrc):
             continue
         if force or _newer(exe, [esrc, LIB] + deps):

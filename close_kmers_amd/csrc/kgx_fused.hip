@@ -29,6 +29,7 @@
 #include "kgx_device.h"
 #include "kgx_internal.h"
 #include "kgx_lstd.h"
+#include "kgx_wave_sort.h"
 
 namespace kgx {
 
@@ -101,110 +102,6 @@ template <> struct FusedInput<FusedSlot> {
     __device__ static uint64_t wb(const FusedArgs &, const FusedSlot &, uint32_t) { return 0; }
     __device__ static uint8_t res(const FusedArgs &, const FusedSlot &k, uint64_t i) { return k.res[i]; }
 };
-
-/* libstdc++'s std::sort (lstd_sort_on, kgx_lstd.h) of n <= 64 elements in
- * LDS, replayed by one wave.  Each __unguarded_partition step is done at
- * once: its left scan stops at the positions whose element is not less than
- * the pivot (L_1 < L_2 < ...), its right scan at those the pivot is not less
- * than (R_1 > R_2 > ...); the t-th swap exchanges L_t and R_t for as long as
- * L_t < R_t, and the cut is min(L_{P+1}, R_P) after P swaps (a scan that
- * runs past its last stop halts at the other's last swapped position).  So a
- * lane that holds L_t swaps iff at least t R-stops lie above it, a lane that
- * holds R_t iff at least t L-stops lie below it, and partners meet through
- * two 64-entry buffers indexed by t.  The median-of-three and the range
- * stack are uniform; a range whose depth budget runs out goes to the serial
- * heap sort (lane 0), as std::sort's does.  The final insertion sort is a
- * stable sort, so each lane places its element by counting.  comp must be a
- * strict weak order.  buf: 192 elements of scratch; stack: 64 ranges. */
-template <class T, class C>
-__device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *stack)
-{
-    const uint32_t lane = lane_id();
-    T *bl = buf, *br = buf + 64, *bs = buf + 128;
-    if (n > 16) {
-        int sp = 0;
-        if (lane == 0)
-            stack[0] = LstdPart{0, (int64_t)n, 2 * (31 - (int)__builtin_clz(n))};
-        sp = 1;
-        wave_lds_sync();
-        while (sp) {
-            --sp;
-            LstdPart p = stack[sp];
-            wave_lds_sync();
-            int32_t f = (int32_t)p.first, l = (int32_t)p.last, depth = p.depth;
-            while (l - f > 16) {
-                if (depth == 0) {
-                    if (lane == 0)
-                        lstd_heap_sort(a + f, l - f, comp);
-                    wave_lds_sync();
-                    break;
-                }
-                --depth;
-                /* __move_median_to_first(first, first + 1, mid, last - 1) */
-                const int32_t mid = f + (l - f) / 2;
-                const T x = a[f + 1], y = a[mid], z = a[l - 1];
-                int32_t pick;
-                if (comp(x, y))
-                    pick = comp(y, z) ? mid : (comp(x, z) ? l - 1 : f + 1);
-                else
-                    pick = comp(x, z) ? f + 1 : (comp(y, z) ? l - 1 : mid);
-                const T first_v = a[f], pick_v = a[pick];
-                wave_lds_sync();
-                if (lane == 0) {
-                    a[f] = pick_v;
-                    a[pick] = first_v;
-                }
-                wave_lds_sync();
-                const T pivot = a[f];
-                const int32_t i = f + 1 + (int32_t)lane;
-                const bool in = i < l;
-                T v = pivot; /* (a select of the two structs went through scratch) */
-                if (in)
-                    v = a[i];
-                const bool lf = in && !comp(v, pivot), rf = in && !comp(pivot, v);
-                const uint64_t LM = __ballot(lf), RM = __ballot(rf);
-                const uint32_t l_below = (uint32_t)__popcll(LM & lanes_le(lane) & ~(1ull << lane));
-                const uint32_t r_above = (uint32_t)__popcll(RM & ~lanes_le(lane));
-                const uint32_t rank_l = l_below + 1, rank_r = r_above + 1;
-                const bool swl = lf && rank_l <= r_above, swr = rf && rank_r <= l_below;
-                const uint32_t P = (uint32_t)__popcll(__ballot(swl));
-                if (swl)
-                    bl[rank_l - 1] = v;
-                if (swr)
-                    br[rank_r - 1] = v;
-                wave_lds_sync();
-                if (swl)
-                    a[i] = br[rank_l - 1];
-                else if (swr)
-                    a[i] = bl[rank_r - 1];
-                const uint64_t LN = __ballot(lf && rank_l == P + 1), RP = __ballot(P > 0 && rf && rank_r == P);
-                const int32_t lcut = LN ? f + 1 + (int32_t)lowbit(LN) : INT32_MAX;
-                const int32_t rcut = RP ? f + 1 + (int32_t)lowbit(RP) : INT32_MAX;
-                const int32_t cut = min(lcut, rcut);
-                wave_lds_sync();
-                if (lane == 0)
-                    stack[sp] = LstdPart{cut, l, depth}; /* __introsort_loop(cut, last) */
-                sp++;
-                l = cut;
-                wave_lds_sync();
-            }
-        }
-    }
-    /* __final_insertion_sort: stable, so by counting */
-    if (lane < n) {
-        const T v = a[lane];
-        uint32_t pos = 0;
-        for (uint32_t j = 0; j < n; j++) {
-            const T w = a[j];
-            pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
-        }
-        bs[pos] = v;
-    }
-    wave_lds_sync();
-    if (lane < n)
-        a[lane] = bs[lane];
-    wave_lds_sync();
-}
 
 template <uint32_t FJ, class IN, bool QUAD>
 __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k, const uint32_t s)
@@ -625,59 +522,91 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     }
     /* 4c. OTU tallies (KmerOtuStats::finalize, kguts.h:196-218), in LDS
      * (hpos, hrec and codes are free once the records are stored and the
-     * scorer is done): the flagged hits' OTUs compacted in hit order
-     * (ballots).  One value among them (the usual case) is one pair.  Else
-     * the values are sorted -- a bitonic network over P = max(256,
-     * 2^ceil(log2 m)) entries, P / 256 per thread in registers: exchanges
-     * within a wave by lane shuffles, between waves through LDS, between a
-     * thread's own entries in place -- and each run of equal values is one
-     * pair, in ascending key order (the std::map's).  Then the pairs are
-     * std::sort'ed by count: lstd_sort_wave64 / lstd_sort_on replay
-     * libstdc++'s tie order.  (r4b: O(m^2) count and rank scans, 18.8 us at
-     * 36 OTUs per call; a wave's register list of distinct values, 22.6.) */
+     * scorer is done).  A call's hits share few OTUs, so first wave 0 collects
+     * the flagged hits' distinct OTUs in its registers -- lane j holds the
+     * j-th value met and its count, one ballot round per distinct value among
+     * each 64 hits -- and places each value by its rank among the others (=
+     * the std::map's key order).  Past 8 distinct values that costs more than
+     * sorting: the values are compacted in hit order (ballots) and sorted --
+     * a bitonic network over P = max(256, 2^ceil(log2 m)) entries, P / 256
+     * per thread in registers: exchanges within a wave by lane shuffles,
+     * between waves through LDS, between a thread's own entries in place --
+     * and each run of equal values is one pair, in ascending key order.  Then
+     * the pairs are std::sort'ed by count: lstd_sort_wave64 / lstd_sort_on
+     * replay libstdc++'s tie order.  (r4b: O(m^2) count and rank scans, 18.8
+     * us at 36 OTUs per call, 6.6 at 3; r4c: the register list alone, 22.6 /
+     * 1.8; r4d: the sort alone, 15.9 / 4.4.) */
     if (want_otu) {
+        constexpr uint32_t KREG = 8;
         __shared__ LstdPart ostack[64];
-        __shared__ uint32_t multi;
         if (dbg)
             a.dbg[7] = wall_clock64();
-        if (t == 0)
-            multi = 0;
-        __syncthreads();
-        int32_t *v = reinterpret_cast<int32_t *>(hpos);
-        uint32_t m = 0;
-        for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
-            const uint32_t i = t + 256 * j;
-            const bool f = i < nh && oflag[i];
-            const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
-            const uint64_t bm = __ballot(f);
-            if (lane == 0)
-                wave_cnt[wave] = (uint32_t)__popcll(bm);
-            __syncthreads();
-            uint32_t before = 0, total = 0;
-            for (uint32_t w = 0; w < 4; w++) {
-                before += w < wave ? wave_cnt[w] : 0u;
-                total += wave_cnt[w];
-            }
-            __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
-            if (f)
-                v[m + before + lanes_below(bm)] = x;
-            m += total;
-            __syncthreads();
-        }
-        /* plain stores of 1, no atomics: same-address LDS atomics from every
-         * differing lane serialize */
-        const int32_t v0 = m ? v[0] : 0;
-        for (uint32_t i = t; i < m; i += 256)
-            if (v[i] != v0)
-                multi = 1;
-        __syncthreads();
         kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
-        uint32_t d = 0;
-        if (m && !multi) {
-            d = 1;
-            if (t == 0)
-                o[0] = kgx_otu{v0, (int32_t)m};
-        } else if (m) {
+        __syncthreads();
+        if (wave == 0) {
+            int32_t dv = 0;
+            uint32_t dc = 0, dn = 0;
+            bool over = false;
+            for (uint32_t h0 = 0; h0 < nh && !over; h0 += 64) {
+                const uint32_t i = h0 + lane;
+                const bool f = i < nh && oflag[i];
+                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+                uint64_t rem = __ballot(f);
+                while (rem) {
+                    const int32_t y = (int32_t)rl32((uint32_t)x, lowbit(rem));
+                    const uint64_t mk = __ballot(f && x == y);
+                    rem &= ~mk;
+                    const uint64_t at = __ballot(lane < dn && dv == y);
+                    if (at) {
+                        if (lane == lowbit(at))
+                            dc += (uint32_t)__popcll(mk);
+                    } else if (dn < KREG) {
+                        if (lane == dn) {
+                            dv = y;
+                            dc = (uint32_t)__popcll(mk);
+                        }
+                        dn++;
+                    } else {
+                        over = true;
+                        break;
+                    }
+                }
+            }
+            if (!over) {
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < dn; j++)
+                    r += (int32_t)rl32((uint32_t)dv, j) < dv ? 1u : 0u;
+                if (lane < dn)
+                    o[r] = kgx_otu{dv, (int32_t)dc};
+            }
+            if (lane == 0)
+                n_otu = over ? ~0u : dn;
+        }
+        __syncthreads();
+        uint32_t d = n_otu;
+        if (d == ~0u) {
+            d = 0;
+            int32_t *v = reinterpret_cast<int32_t *>(hpos);
+            uint32_t m = 0;
+            for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
+                const uint32_t i = t + 256 * j;
+                const bool f = i < nh && oflag[i];
+                const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
+                const uint64_t bm = __ballot(f);
+                if (lane == 0)
+                    wave_cnt[wave] = (uint32_t)__popcll(bm);
+                __syncthreads();
+                uint32_t before = 0, total = 0;
+                for (uint32_t w = 0; w < 4; w++) {
+                    before += w < wave ? wave_cnt[w] : 0u;
+                    total += wave_cnt[w];
+                }
+                __syncthreads(); /* hpos[m + ...] may overlap hits not yet read by slower waves: read, then write */
+                if (f)
+                    v[m + before + lanes_below(bm)] = x;
+                m += total;
+                __syncthreads();
+            }
             uint32_t R = 1;
             while (256u * R < m)
                 R <<= 1;

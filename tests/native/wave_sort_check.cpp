@@ -1,0 +1,123 @@
+/*
+ * wave_sort_check -- lstd_sort_wave64 (kgx_wave_sort.h: libstdc++'s std::sort
+ * of at most 64 elements, replayed by one wave in LDS) against the serial
+ * replay lstd_sort (kgx_lstd.h, itself checked against libstdc++ by
+ * lstd_check.cpp) on OTU pairs sorted by count (less_second, kguts.h:214-218),
+ * the call service's use.  One workgroup of one wave runs the cases one after
+ * another and times each sort with the device wall clock.
+ *
+ *   wave_sort_check CASES SEED
+ *
+ * Prints "ok CASES" and one JSON line of mean ns per sort by size band; exit
+ * 1 on the first mismatch.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "kgx_internal.h"
+#include "kgx_wave_sort.h"
+
+using namespace kgx;
+
+struct ByCount {
+    __host__ __device__ bool operator()(const kgx_otu &l, const kgx_otu &r) const { return r.count < l.count; }
+};
+
+__global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const uint32_t *n_of, uint32_t cases,
+                                                       kgx_otu *out, uint64_t *ns)
+{
+    __shared__ kgx_otu a[64];
+    __shared__ kgx_otu buf[192];
+    __shared__ LstdPart st[64];
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t c = 0; c < cases; c++) {
+        const uint32_t n = n_of[c];
+        if (lane < n)
+            a[lane] = in[64 * c + lane];
+        wave_lds_sync();
+        const uint64_t t0 = wall_clock64();
+        lstd_sort_wave64(a, n, ByCount{}, buf, st);
+        const uint64_t t1 = wall_clock64();
+        if (lane < n)
+            out[64 * c + lane] = a[lane];
+        if (lane == 0)
+            ns[c] = (t1 - t0) * 10; /* 100 MHz */
+        wave_lds_sync();
+    }
+}
+
+#define CHECK(x)                                                                   \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));          \
+            return 2;                                                              \
+        }                                                                          \
+    } while (0)
+
+int main(int argc, char **argv)
+{
+    const uint32_t cases = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 2000;
+    std::mt19937_64 rng(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1);
+    std::vector<kgx_otu> in(64 * (size_t)cases), want(64 * (size_t)cases), got(64 * (size_t)cases);
+    std::vector<uint32_t> n_of(cases);
+    for (uint32_t c = 0; c < cases; c++) {
+        const uint32_t n = 2 + (uint32_t)(rng() % 63);
+        /* counts over a narrow range (ties everywhere, as a call's OTU tallies
+         * have) or a wide one; OTU ids ascending, as the map leaves them */
+        const uint32_t span = c % 3 == 0 ? 3 : c % 3 == 1 ? 8 : 1000;
+        n_of[c] = n;
+        for (uint32_t i = 0; i < n; i++)
+            in[64 * (size_t)c + i] = kgx_otu{(int32_t)i * 7 - 5, 1 + (int32_t)(rng() % span)};
+        for (uint32_t i = 0; i < n; i++)
+            want[64 * (size_t)c + i] = in[64 * (size_t)c + i];
+        lstd_sort(want.data() + 64 * (size_t)c, (int64_t)n, ByCount{});
+    }
+    kgx_otu *d_in = nullptr, *d_out = nullptr;
+    uint32_t *d_n = nullptr;
+    uint64_t *d_ns = nullptr;
+    CHECK(hipMalloc(&d_in, in.size() * sizeof(kgx_otu)));
+    CHECK(hipMalloc(&d_out, in.size() * sizeof(kgx_otu)));
+    CHECK(hipMalloc(&d_n, cases * sizeof(uint32_t)));
+    CHECK(hipMalloc(&d_ns, cases * sizeof(uint64_t)));
+    CHECK(hipMemcpy(d_in, in.data(), in.size() * sizeof(kgx_otu), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d_n, n_of.data(), cases * sizeof(uint32_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(wave_sort_kernel, dim3(1), dim3(64), 0, 0, d_in, d_n, cases, d_out, d_ns);
+    CHECK(hipGetLastError());
+    CHECK(hipDeviceSynchronize());
+    std::vector<uint64_t> ns(cases);
+    CHECK(hipMemcpy(got.data(), d_out, got.size() * sizeof(kgx_otu), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(ns.data(), d_ns, cases * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint32_t c = 0; c < cases; c++)
+        for (uint32_t i = 0; i < n_of[c]; i++) {
+            const kgx_otu &g = got[64 * (size_t)c + i], &w = want[64 * (size_t)c + i];
+            if (g.otu_index != w.otu_index || g.count != w.count) {
+                std::printf("mismatch case %u (n %u) at %u: (%d,%d) vs (%d,%d)\n", c, n_of[c], i, g.otu_index,
+                            g.count, w.otu_index, w.count);
+                return 1;
+            }
+        }
+    /* mean ns per sort by size band */
+    const uint32_t bands[] = {2, 9, 17, 33, 49, 65};
+    std::printf("ok %u\n{", cases);
+    for (int b = 0; b < 5; b++) {
+        double s = 0;
+        uint32_t k = 0;
+        for (uint32_t c = 0; c < cases; c++)
+            if (n_of[c] >= bands[b] && n_of[c] < bands[b + 1]) {
+                s += (double)ns[c];
+                k++;
+            }
+        std::printf("%s\"n%u-%u_ns\": %.0f", b ? ", " : "", bands[b], bands[b + 1] - 1, k ? s / k : 0.0);
+    }
+    std::printf("}\n");
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    (void)hipFree(d_n);
+    (void)hipFree(d_ns);
+    return 0;
+}

@@ -352,3 +352,16 @@ def test_svc_stop_and_config_while_calling(svc_image, oracle_lib):
         _check(oracle_lib, table, s, _tuple(PARAMS[i % 2]), out[i][0], out[i][1], i)
     img.svc_config(32, 1000, 1000)
     assert img.svc_stat("slots") == 32 and img.svc_stat("broken") == 0
+
+
+def test_wave_sort_matches_serial_replay():
+    """lstd_sort_wave64 -- libstdc++'s std::sort of up to 64 OTU pairs by
+    count, replayed by one wave (the call service's tally, kguts.h:214-218) --
+    equals the serial replay (kgx_lstd.h, checked against libstdc++ on the
+    CPU) on 3,000 lists with heavy ties (tests/native/wave_sort_check.cpp);
+    prints the mean time per sort by list size."""
+    import subprocess
+    from close_kmers_amd import build as kbuild
+    r = subprocess.run([kbuild.WAVE_SORT_CHECK, "3000", "7"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and r.stdout.startswith("ok 3000"), r.stdout + r.stderr
+    print(r.stdout.strip().splitlines()[-1])
