@@ -605,6 +605,7 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         if (want & KGX_WANT_OTU) {
             s->phase_ns[6] += (st[4] - st[7]) * 10; /* the OTU tally alone */
             s->phase_ns[7] += (st[4] - st[8]) * 10; /* ... its sort by count */
+
         }
     }
     const SvcSlotOut &o = s->out[slot];

@@ -1,6 +1,6 @@
 /*
- * wave_sort_check -- lstd_sort_wave64 (kgx_wave_sort.h: libstdc++'s std::sort
- * of at most 64 elements, replayed by one wave in LDS) against the serial
+ * wave_sort_check -- lstd_sort_wave<4> (kgx_wave_sort.h: libstdc++'s std::sort
+ * of at most 256 elements, replayed by one wave in LDS) against the serial
  * replay lstd_sort (kgx_lstd.h, itself checked against libstdc++ by
  * lstd_check.cpp) on OTU pairs sorted by count (less_second, kguts.h:214-218),
  * the call service's use.  One workgroup of one wave runs the cases one after
@@ -30,20 +30,21 @@ struct ByCount {
 __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const uint32_t *n_of, uint32_t cases,
                                                        kgx_otu *out, uint64_t *ns)
 {
-    __shared__ kgx_otu a[64];
-    __shared__ kgx_otu buf[192];
+    __shared__ kgx_otu a[256];
+    __shared__ kgx_otu bl[256], br[256];
+    __shared__ uint8_t seg[256];
     __shared__ LstdPart st[64];
     const uint32_t lane = threadIdx.x;
     for (uint32_t c = 0; c < cases; c++) {
         const uint32_t n = n_of[c];
-        if (lane < n)
-            a[lane] = in[64 * c + lane];
+        for (uint32_t i = lane; i < n; i += 64)
+            a[i] = in[256 * c + i];
         wave_lds_sync();
         const uint64_t t0 = wall_clock64();
-        lstd_sort_wave64(a, n, ByCount{}, buf, st);
+        lstd_sort_wave<4>(a, n, ByCount{}, bl, br, seg, st);
         const uint64_t t1 = wall_clock64();
-        if (lane < n)
-            out[64 * c + lane] = a[lane];
+        for (uint32_t i = lane; i < n; i += 64)
+            out[256 * c + i] = a[i];
         if (lane == 0)
             ns[c] = (t1 - t0) * 10; /* 100 MHz */
         wave_lds_sync();
@@ -63,19 +64,19 @@ int main(int argc, char **argv)
 {
     const uint32_t cases = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 2000;
     std::mt19937_64 rng(argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 1);
-    std::vector<kgx_otu> in(64 * (size_t)cases), want(64 * (size_t)cases), got(64 * (size_t)cases);
+    std::vector<kgx_otu> in(256 * (size_t)cases), want(256 * (size_t)cases), got(256 * (size_t)cases);
     std::vector<uint32_t> n_of(cases);
     for (uint32_t c = 0; c < cases; c++) {
-        const uint32_t n = 2 + (uint32_t)(rng() % 63);
+        const uint32_t n = c % 4 == 3 ? 65 + (uint32_t)(rng() % 192) : 2 + (uint32_t)(rng() % 63);
         /* counts over a narrow range (ties everywhere, as a call's OTU tallies
          * have) or a wide one; OTU ids ascending, as the map leaves them */
         const uint32_t span = c % 3 == 0 ? 3 : c % 3 == 1 ? 8 : 1000;
         n_of[c] = n;
         for (uint32_t i = 0; i < n; i++)
-            in[64 * (size_t)c + i] = kgx_otu{(int32_t)i * 7 - 5, 1 + (int32_t)(rng() % span)};
+            in[256 * (size_t)c + i] = kgx_otu{(int32_t)i * 7 - 5, 1 + (int32_t)(rng() % span)};
         for (uint32_t i = 0; i < n; i++)
-            want[64 * (size_t)c + i] = in[64 * (size_t)c + i];
-        lstd_sort(want.data() + 64 * (size_t)c, (int64_t)n, ByCount{});
+            want[256 * (size_t)c + i] = in[256 * (size_t)c + i];
+        lstd_sort(want.data() + 256 * (size_t)c, (int64_t)n, ByCount{});
     }
     kgx_otu *d_in = nullptr, *d_out = nullptr;
     uint32_t *d_n = nullptr;
@@ -94,7 +95,7 @@ int main(int argc, char **argv)
     CHECK(hipMemcpy(ns.data(), d_ns, cases * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (uint32_t c = 0; c < cases; c++)
         for (uint32_t i = 0; i < n_of[c]; i++) {
-            const kgx_otu &g = got[64 * (size_t)c + i], &w = want[64 * (size_t)c + i];
+            const kgx_otu &g = got[256 * (size_t)c + i], &w = want[256 * (size_t)c + i];
             if (g.otu_index != w.otu_index || g.count != w.count) {
                 std::printf("mismatch case %u (n %u) at %u: (%d,%d) vs (%d,%d)\n", c, n_of[c], i, g.otu_index,
                             g.count, w.otu_index, w.count);
@@ -102,9 +103,9 @@ int main(int argc, char **argv)
             }
         }
     /* mean ns per sort by size band */
-    const uint32_t bands[] = {2, 9, 17, 33, 49, 65};
+    const uint32_t bands[] = {2, 9, 17, 33, 65, 129, 257};
     std::printf("ok %u\n{", cases);
-    for (int b = 0; b < 5; b++) {
+    for (int b = 0; b < 6; b++) {
         double s = 0;
         uint32_t k = 0;
         for (uint32_t c = 0; c < cases; c++)
