@@ -77,6 +77,7 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
             }
             wave_lds_sync();
             const T pivot = a[f];
+            const uint32_t nst = (uint32_t)(l - f - 1 + 63) / 64; /* strips of the range (uniform) */
             T v[S];
             bool lf[S], rf[S];
             uint64_t LM[S], RM[S];
@@ -84,7 +85,7 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
 #pragma unroll
             for (uint32_t s = 0; s < S; s++) {
                 const int32_t i = f + 1 + (int32_t)(64 * s + lane);
-                const bool in = i < l;
+                const bool in = s < nst && i < l;
                 v[s] = pivot; /* (a select of the two structs went through scratch) */
                 if (in)
                     v[s] = a[i];
@@ -99,6 +100,11 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
             uint32_t Lb = 0, Rle = 0, P = 0;
 #pragma unroll
             for (uint32_t s = 0; s < S; s++) {
+                if (s >= nst) {
+                    swl[s] = swr[s] = false;
+                    rank_l[s] = rank_r[s] = 0;
+                    continue;
+                }
                 const uint32_t lb = Lb + (uint32_t)__popcll(LM[s] & below);
                 const uint32_t r_above = NR - (Rle + (uint32_t)__popcll(RM[s] & le));
                 rank_l[s] = lb + 1;
@@ -119,7 +125,7 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
             wave_lds_sync();
             int32_t cut = INT32_MAX;
 #pragma unroll
-            for (uint32_t s = 0; s < S; s++) {
+            for (uint32_t s = 0; s < S && s < nst; s++) {
                 const int32_t i = f + 1 + (int32_t)(64 * s + lane);
                 if (swl[s])
                     a[i] = br[rank_l[s] - 1];
@@ -143,18 +149,43 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
             seg[f] = 1; /* [f, l) is final */
         wave_lds_sync();
     }
-    /* __final_insertion_sort: stable within each final range, so by counting */
-    for (uint32_t i = lane; i < n; i += 64) {
-        const T v = a[i];
-        uint32_t s0 = i;
-        while (!seg[s0])
-            s0--;
-        uint32_t pos = s0;
-        for (uint32_t j = s0; j < n && (j == s0 || !seg[j]); j++) {
-            const T w = a[j];
-            pos += comp(w, v) || (j < i && !comp(v, w)) ? 1u : 0u;
+    /* __final_insertion_sort: stable within each final range, so by
+     * counting.  Each lane's range bounds from ballots of the range marks:
+     * its start the last mark at or below it, its end the next mark above. */
+    const uint32_t nst = (n + 63) / 64;
+    uint32_t lo[S], hi[S];
+    uint32_t carry = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < S; s++) {
+        const uint32_t i = 64 * s + lane;
+        const uint64_t SM = s < nst ? __ballot(i < n && seg[i]) : 0ull;
+        const int hb = hibit(SM & le);
+        lo[s] = hb >= 0 ? 64 * s + (uint32_t)hb : carry;
+        if (SM)
+            carry = 64 * s + (uint32_t)hibit(SM);
+    }
+    carry = n;
+#pragma unroll
+    for (int s = (int)S - 1; s >= 0; s--) {
+        const uint32_t i = 64 * (uint32_t)s + lane;
+        const uint64_t SM = (uint32_t)s < nst ? __ballot(i < n && seg[i]) : 0ull;
+        const uint64_t up = SM & ~le;
+        hi[s] = up ? 64 * (uint32_t)s + lowbit(up) : carry;
+        if (SM)
+            carry = 64 * (uint32_t)s + lowbit(SM);
+    }
+#pragma unroll
+    for (uint32_t s = 0; s < S && s < nst; s++) {
+        const uint32_t i = 64 * s + lane;
+        if (i < n) {
+            const T v = a[i];
+            uint32_t pos = lo[s];
+            for (uint32_t j = lo[s]; j < hi[s]; j++) {
+                const T w = a[j];
+                pos += comp(w, v) || (j < i && !comp(v, w)) ? 1u : 0u;
+            }
+            bl[pos] = v;
         }
-        bl[pos] = v;
     }
     wave_lds_sync();
     for (uint32_t i = lane; i < n; i += 64)
