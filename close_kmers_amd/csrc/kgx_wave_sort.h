@@ -174,18 +174,26 @@ __device__ void lstd_sort_wave(T *a, uint32_t n, C comp, T *bl, T *br, uint8_t *
         if (SM)
             carry = 64 * (uint32_t)s + lowbit(SM);
     }
+    /* one uniform loop per strip over the union of its lanes' ranges (both
+     * bounds grow with the lane), so the loads pipeline */
 #pragma unroll
     for (uint32_t s = 0; s < S && s < nst; s++) {
         const uint32_t i = 64 * s + lane;
-        if (i < n) {
-            const T v = a[i];
-            uint32_t pos = lo[s];
-            for (uint32_t j = lo[s]; j < hi[s]; j++) {
-                const T w = a[j];
-                pos += comp(w, v) || (j < i && !comp(v, w)) ? 1u : 0u;
-            }
-            bl[pos] = v;
+        const bool in = i < n;
+        const uint32_t last = min(63u, n - 1 - 64 * s);
+        const uint32_t j0 = (uint32_t)__builtin_amdgcn_readfirstlane(lo[s]);
+        const uint32_t j1 = (uint32_t)__builtin_amdgcn_readlane(hi[s], last);
+        T v = a[64 * s];
+        if (in)
+            v = a[i];
+        uint32_t pos = lo[s];
+        for (uint32_t j = j0; j < j1; j++) {
+            const T w = a[j];
+            const bool mine = j >= lo[s] && j < hi[s];
+            pos += mine && (comp(w, v) || (j < i && !comp(v, w))) ? 1u : 0u;
         }
+        if (in)
+            bl[pos] = v;
     }
     wave_lds_sync();
     for (uint32_t i = lane; i < n; i += 64)
