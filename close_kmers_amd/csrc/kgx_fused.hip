@@ -689,13 +689,17 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         if (dbg)
             a.dbg[8] = wall_clock64();
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
-         * it for up to 64 SW pairs (lstd_sort_wave; its scratch past the
-         * pairs in hrec, its range marks in codes), thread 0 beyond (r4f: a
-         * 36-OTU call's pairs sort in 0.33 us; the calls past the old 64-pair
-         * wave limit took the serial replay, 11 us per call on average) */
+         * it, lstd_sort_wave64 up to 64 pairs, lstd_sort_wave up to 64 SW
+         * (their scratch past the pairs in hrec, range marks in codes),
+         * thread 0 beyond.  (r4f: a 36-OTU call's pairs sort in 0.33 us; the
+         * calls past 64 pairs, on the serial replay then, cost 11 us per
+         * call on average.) */
         constexpr uint32_t SW = FJ * 2 < 8 ? FJ * 2 : 8;
         const auto by_count = [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; };
-        if (d > 1 && d <= 64 * SW) {
+        if (d > 1 && d <= 64) {
+            if (wave == 0)
+                lstd_sort_wave64(o, d, by_count, o + 64 * SW, ostack);
+        } else if (d > 64 && d <= 64 * SW) {
             if (wave == 0)
                 lstd_sort_wave<SW>(o, d, by_count, o + 64 * SW, o + 128 * SW, codes, ostack);
         } else if (d > 1 && t == 0) {

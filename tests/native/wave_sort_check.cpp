@@ -1,6 +1,7 @@
 /*
- * wave_sort_check -- lstd_sort_wave<4> (kgx_wave_sort.h: libstdc++'s std::sort
- * of at most 256 elements, replayed by one wave in LDS) against the serial
+ * wave_sort_check -- lstd_sort_wave64 / lstd_sort_wave<4> (kgx_wave_sort.h:
+ * libstdc++'s std::sort of at most 64 / 256 elements, replayed by one wave in
+ * LDS, as the call service picks them) against the serial
  * replay lstd_sort (kgx_lstd.h, itself checked against libstdc++ by
  * lstd_check.cpp) on OTU pairs sorted by count (less_second, kguts.h:214-218),
  * the call service's use.  One workgroup of one wave runs the cases one after
@@ -31,7 +32,7 @@ __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const 
                                                        kgx_otu *out, uint64_t *ns)
 {
     __shared__ kgx_otu a[256];
-    __shared__ kgx_otu bl[256], br[256];
+    __shared__ kgx_otu bl[256], br[256]; /* bl: also lstd_sort_wave64's 192 elements of scratch */
     __shared__ uint8_t seg[256];
     __shared__ LstdPart st[64];
     const uint32_t lane = threadIdx.x;
@@ -41,7 +42,10 @@ __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const 
             a[i] = in[256 * c + i];
         wave_lds_sync();
         const uint64_t t0 = wall_clock64();
-        lstd_sort_wave<4>(a, n, ByCount{}, bl, br, seg, st);
+        if (n <= 64)
+            lstd_sort_wave64(a, n, ByCount{}, bl, st); /* bl, br: its 192 elements of scratch */
+        else
+            lstd_sort_wave<4>(a, n, ByCount{}, bl, br, seg, st);
         const uint64_t t1 = wall_clock64();
         for (uint32_t i = lane; i < n; i += 64)
             out[256 * c + i] = a[i];
