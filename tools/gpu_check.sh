@@ -5,6 +5,7 @@
 # 4. C4 fq (device pass and the handler over all reads)   5. HTTP serving (/query; /lookup in family mode)
 # 6. per-sequence facade calls (and with OTU stats, and batches beside the service)
 # 7. kgx_pool (C5 batch): contexts of one device, and bench.py --pool-devices 2
+# 8. call-service OTU phases; the host path by staging threads and H2D order
 # "quick" skips the CPU baselines.  Output in gpurun_out/TAG; every GPU step
 # has its own time limit and the script stops at the first failure.
 set -euo pipefail
@@ -29,4 +30,7 @@ KGX_FACADE_OTU=1 KGX_FACADE_MODES=2 timeout -k 10 300 python3 tools/bench_facade
     > "$OUT/bench_facade_otu.json" 2> "$OUT/bench_facade_otu.err"
 timeout -k 10 600 python3 tools/bench_pool.py > "$OUT/bench_pool.json" 2> "$OUT/bench_pool.err"
 timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool_devices.json" 2> "$OUT/bench_pool_devices.err"
+KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
+timeout -k 10 600 python3 tools/host_path_probe.py --compact --no-pieces --chunks 4,6 --copy 1 --hits16 1 --stream 1 \
+    --rec12 1 --score 1 --stage 4,8,12 --want 11 > "$OUT/host_path_sweep.json" 2> "$OUT/host_path_sweep.err"
 echo "[gpu_check] done" >&2
