@@ -406,6 +406,13 @@ struct kgx_ctx {
     std::vector<hipEvent_t> chunk_counts; /* per chunk: its counts are on the host */
     std::vector<hipEvent_t> chunk_gathered; /* per chunk: its dense buffers are complete */
     hipStream_t copy_stream = nullptr; /* bulk chunk D2H, apart from the contexts' kernels */
+    /* streamed schedule, option "host_upload_stream" 1 (default): every chunk's
+     * residues and offsets go up on a stream of their own into a region of
+     * the batch's own (up_res / up_off), as soon as they are staged, instead
+     * of behind the previous chunk's kernels on the context's stream */
+    int host_upload_stream = 1;
+    hipStream_t up_stream = nullptr;
+    kgx::DevBuf up_res, up_off;
     kgx::DevBuf dense_mask, dense_best; /* a chunk's mask / best calls for its bulk copy */
     /* streamed schedule (option "host_stream", compact records only): device
      * CSR offsets, bulk copies sized on the device into host regions sized

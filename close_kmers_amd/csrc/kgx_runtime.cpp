@@ -851,6 +851,10 @@ int kgx_ctx_destroy(kgx_ctx *c)
         (void)hipStreamSynchronize(c->copy_stream);
         (void)hipStreamDestroy(c->copy_stream);
     }
+    if (c->up_stream) {
+        (void)hipStreamSynchronize(c->up_stream);
+        (void)hipStreamDestroy(c->up_stream);
+    }
     if (c->own_stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -938,6 +942,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         if (value < 1 || value > 64)
             return fail(KGX_EINVAL, "stage_threads must be 1..64");
         c->stage_threads = (int)value;
+        return KGX_OK;
+    }
+    if (n == "host_upload_stream") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_upload_stream must be 0 or 1");
+        c->host_upload_stream = (int)value;
         return KGX_OK;
     }
     if (n == "host_h2d_first") {
@@ -1805,21 +1815,47 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     hipStream_t cs = c->copy_stream;
     const int cb = c->host_copy_blocks;
     auto mapped = [](auto &v, uint64_t at, void **d) -> hipError_t { return v.device_ptr(at, d); };
+    /* host_upload_stream: each chunk's regions of up_res (256-B aligned, 16
+     * bytes of slack for the probe's 16-B residue loads) and up_off */
+    const bool up = c->host_upload_stream != 0;
+    std::vector<uint64_t> res_at(K + 1, 0), off_at(K + 1, 0);
+    for (uint32_t k = 0; k < K; k++) {
+        res_at[k + 1] = res_at[k] + ((seq_offsets[cut[k + 1]] - seq_offsets[cut[k]] + 16 + 255) & ~255ull);
+        off_at[k + 1] = off_at[k] + ((cut[k + 1] - cut[k] + 1 + 1) & ~1ull);
+    }
+    if (up) {
+        HIP_TRY(c->up_res.reserve(std::max<uint64_t>(res_at[K], 256)));
+        HIP_TRY(c->up_off.reserve(std::max<uint64_t>(off_at[K], 2) * sizeof(uint64_t)));
+    }
 
     /* enqueue chunk k on x: everything up to its bulk copy */
     auto enqueue = [&](kgx_ctx *x, uint32_t k) -> int {
         const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
         const uint64_t n_res = x->h_res.size();
+        hipStream_t us = up ? c->up_stream : x->stream;
         if (prof)
-            HIP_TRY(hipEventRecord(c->prof_ev[4 * k], x->stream));
-        int rc = stage_upload(x);
-        if (rc)
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k], us));
+        const uint8_t *d_res = x->residues.as<uint8_t>();
+        const uint64_t *d_off = x->offsets.as<uint64_t>();
+        int rc = KGX_OK;
+        if (up) {
+            uint8_t *rd = c->up_res.as<uint8_t>() + res_at[k];
+            uint64_t *od = c->up_off.as<uint64_t>() + off_at[k];
+            if (n_res)
+                HIP_TRY(hipMemcpyAsync(rd, x->h_res.data(), n_res, hipMemcpyHostToDevice, us));
+            HIP_TRY(hipMemcpyAsync(od, x->h_off_stage.data(), x->h_off_stage.size() * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, us));
+            d_res = rd;
+            d_off = od;
+        } else if ((rc = stage_upload(x))) {
             return rc;
-        HIP_TRY(hipEventRecord(c->chunk_h2d[k], x->stream));
+        }
+        HIP_TRY(hipEventRecord(c->chunk_h2d[k], us));
         if (prof)
-            HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 1], x->stream));
-        if ((rc = kgx_run_device(x, params, x->residues.as<uint8_t>(), x->offsets.as<uint64_t>(), n, n_res, want,
-                                 nullptr)))
+            HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 1], us));
+        if (up)
+            HIP_TRY(hipStreamWaitEvent(x->stream, c->chunk_h2d[k], 0));
+        if ((rc = kgx_run_device(x, params, d_res, d_off, n, n_res, want, nullptr)))
             return rc;
         if (prof)
             HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 2], x->stream));
@@ -2127,6 +2163,8 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     kgx_ctx *xs[2] = {c, t};
     if (!c->copy_stream)
         HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->up_stream)
+        HIP_TRY(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
     for (auto *ev : {&c->chunk_counts, &c->chunk_gathered, &c->chunk_done, &c->chunk_h2d})
         while (ev->size() < K) {
             hipEvent_t e;
