@@ -406,11 +406,15 @@ struct kgx_ctx {
     std::vector<hipEvent_t> chunk_counts; /* per chunk: its counts are on the host */
     std::vector<hipEvent_t> chunk_gathered; /* per chunk: its dense buffers are complete */
     hipStream_t copy_stream = nullptr; /* bulk chunk D2H, apart from the contexts' kernels */
-    /* streamed schedule, option "host_upload_stream" 1 (default): every chunk's
-     * residues and offsets go up on a stream of their own into a region of
-     * the batch's own (up_res / up_off), as soon as they are staged, instead
-     * of behind the previous chunk's kernels on the context's stream */
-    int host_upload_stream = 1;
+    /* streamed schedule, option "host_upload_stream" 1: every chunk's residues
+     * and offsets go up on a stream of their own into a region of the
+     * batch's own (up_res / up_off), as soon as they are staged, instead of
+     * behind the previous chunk's kernels on the context's stream.  Off by
+     * default: with the runtime's 4 hardware queues per process the upload
+     * stream shares one with a stream that waits on events, and measured no
+     * faster (r4l/r4m: 3.66-4.21 vs 3.76-4.09 ms per 30M-residue batch; with
+     * 16 queues the uploads do run early, 3.60-3.90 ms) */
+    int host_upload_stream = 0;
     hipStream_t up_stream = nullptr;
     kgx::DevBuf up_res, up_off;
     kgx::DevBuf dense_mask, dense_best; /* a chunk's mask / best calls for its bulk copy */

@@ -736,7 +736,7 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_hits16", 1)
         ctx.set_option("host_copy_blocks", 1)
         # chunk k's D2H behind chunk k+1's H2D, or not; uploads on their own stream, or not
-        for k, h2d_first, up in ((16, 1, 1), (37, 0, 1), (64, 1, 0)):
+        for k, h2d_first, up in ((16, 1, 0), (37, 0, 1), (64, 1, 1)):
             ctx.set_option("host_chunks", k)
             ctx.set_option("host_h2d_first", h2d_first)
             ctx.set_option("host_upload_stream", up)
@@ -750,7 +750,7 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_copy_blocks", 64)
         ctx.set_option("host_chunks", 3)
         ctx.set_option("host_h2d_first", 1)
-        ctx.set_option("host_upload_stream", 1)
+        ctx.set_option("host_upload_stream", 0)
 
 
 @pytest.mark.parametrize("schedule", ["streamed_rec12", "streamed_rec16", "exact", "small", "aos24",
