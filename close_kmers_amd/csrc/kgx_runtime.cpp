@@ -2138,6 +2138,26 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     return KGX_OK;
 }
 
+/* A stream for the host path's bulk copies / uploads.  The runtime spreads a
+ * process's streams over a few hardware queues (4 by default), each a FIFO
+ * that blocks behind an event wait at its head, so the copy stream's waits
+ * could hold up another context's kernels queued behind them.  With
+ * KGX_OWN_QUEUES=1 the stream is created with a full CU mask: a masked
+ * stream gets a hardware queue of its own. */
+hipError_t own_queue_stream(int device, hipStream_t *s)
+{
+    const char *e = std::getenv("KGX_OWN_QUEUES");
+    if (e && std::atoi(e) != 0) {
+        int cus = 0;
+        hipError_t r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (r == hipSuccess && cus > 0) {
+            std::vector<uint32_t> mask((size_t)(cus + 31) / 32, ~0u);
+            return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 /* The host batch in K residue-balanced chunks of whole sequences, alternating
  * between c and its twin context: while chunk k's hits are gathered and
  * copied to the host on one stream, chunk k+1 is staged, copied up, probed
@@ -2162,9 +2182,9 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     t->score_wave_tiles = c->score_wave_tiles;
     kgx_ctx *xs[2] = {c, t};
     if (!c->copy_stream)
-        HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        HIP_TRY(own_queue_stream(c->img->device, &c->copy_stream));
     if (!c->up_stream)
-        HIP_TRY(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
+        HIP_TRY(own_queue_stream(c->img->device, &c->up_stream));
     for (auto *ev : {&c->chunk_counts, &c->chunk_gathered, &c->chunk_done, &c->chunk_h2d})
         while (ev->size() < K) {
             hipEvent_t e;
