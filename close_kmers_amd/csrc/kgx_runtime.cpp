@@ -1212,8 +1212,17 @@ int probe_chained(kgx_ctx *c, Launch launch)
          * (one hardware queue), entered when this context's inputs are ready
          * and left back to this context's stream */
         lock.lock();
-        if (!img->probe_stream)
-            HIP_TRY(hipStreamCreateWithFlags(&img->probe_stream, hipStreamNonBlocking));
+        if (!img->probe_stream) {
+            /* KGX_PROBE_PRIORITY=1: the probes' stream at the device's highest
+             * priority, so their workgroups dispatch ahead of the other
+             * contexts' scorers (an experiment: the step vs the probe alone) */
+            int least = 0, greatest = 0;
+            const char *pp = std::getenv("KGX_PROBE_PRIORITY");
+            if (pp && std::atoi(pp) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+                HIP_TRY(hipStreamCreateWithPriority(&img->probe_stream, hipStreamNonBlocking, greatest));
+            else
+                HIP_TRY(hipStreamCreateWithFlags(&img->probe_stream, hipStreamNonBlocking));
+        }
         if (!c->probe_ready)
             HIP_TRY(hipEventCreateWithFlags(&c->probe_ready, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(c->probe_ready, c->stream));
