@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 (o): the bench's host path vs hardware-queue sharing: default, a
-# CU-masked (own-queue) copy stream, and 16 queues per process.
+# CU-masked (own-queue) copy stream, and 16 queues per process; the C2 step
+# with the probes on a high-priority image stream.
 set -euo pipefail
 TAG=${1:-r4o}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -15,4 +16,11 @@ done
 GPU_MAX_HW_QUEUES=16 timeout -k 10 300 $B > "$OUT/bench_q16.json" 2> "$OUT/bench_q16.err"
 KGX_OWN_QUEUES=1 timeout -k 10 300 python3 tools/host_path_probe.py --compact --no-pieces --chunks 4,6 --copy 1 --hits16 1 --stream 1 \
     --rec12 1 --score 0 --want 11 > "$OUT/hp_ownq.json" 2> "$OUT/hp_ownq.err"
+# the C2 step vs its probe: probes on one image stream at high priority or normal, and the default chain
+B2="python3 bench.py --no-cpu-baseline --no-host-path --no-microbench --no-canary --steps 40 --warmup 5"
+for rep in 1 2 3; do
+  timeout -k 10 300 $B2 > "$OUT/c2_default.$rep.json" 2> "$OUT/c2_default.$rep.err"
+  timeout -k 10 300 $B2 --probe-stream 1 > "$OUT/c2_pstream.$rep.json" 2> "$OUT/c2_pstream.$rep.err"
+  KGX_PROBE_PRIORITY=1 timeout -k 10 300 $B2 --probe-stream 1 > "$OUT/c2_pstream_hi.$rep.json" 2> "$OUT/c2_pstream_hi.$rep.err"
+done
 echo "[gpu_r4o] done" >&2
