@@ -235,109 +235,116 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             __syncthreads();
         }
     } else {
-        /* 2. encode + probe: thread t owns windows t + 256 j */
-        uint64_t key[FJ], slot[FJ];
-        bool pend[FJ], hit[FJ];
-        uint4 rec[FJ];
+        /* 2. encode + probe: thread t owns windows t + 256 j, probed RB
+         * slices at a time (the LDS holds FJ slices; the registers hold RB,
+         * so a long protein costs more probe rounds, not spilled registers:
+         * with all FJ = 8 slices in registers the long-protein body spilled
+         * 150+ SGPRs, and the service kernel that inlines it spilled in its
+         * short-protein path too) */
+        constexpr uint32_t RB = FJ < 2 ? FJ : 2;
+        for (uint32_t jb = 0; jb < J; jb += RB) {
+            uint64_t key[RB], slot[RB];
+            bool pend[RB], hit[RB];
+            uint4 rec[RB];
 #pragma unroll
-        for (uint32_t j = 0; j < FJ; j++) {
-            const uint32_t w = t + 256 * j;
-            hit[j] = false;
-            pend[j] = false;
-            rec[j] = make_uint4(0, 0, 0, 0);
-            key[j] = 0;
-            slot[j] = 0;
-            if (j < J && w < W) {
-                const uint8_t *c = codes + w;
-                const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
-                const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
-                const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
-                key[j] = (uint64_t)ka * 160000u + kb;
-                pend[j] = cmax < 20u;
-                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
-            }
-        }
-        /* linear probe by 64-B lines: a round reads the rest of the line holding
-         * each pending window's next bucket (the table is 256-B aligned, 4
-         * records per line), all of a thread's windows in flight at once, and
-         * examines those buckets in probe order -- a chain costs one round per
-         * line it touches instead of one per bucket (reading the next line too,
-         * speculatively, measured slower: 6.8 vs 4.6 us for one protein).
-         * Bounded by num_sigs buckets where the reference would spin forever. */
-        constexpr uint32_t R = 4; /* records per round: one line */
-        uint64_t examined[FJ];
-#pragma unroll
-        for (uint32_t j = 0; j < FJ; j++)
-            examined[j] = 0;
-        const uint64_t NS = a.num_sigs;
-        for (;;) {
-            uint4 pv[FJ][R];
-#pragma unroll
-            for (uint32_t j = 0; j < FJ; j++) {
-                const uint64_t base = slot[j] & ~3ull;
-#pragma unroll
-                for (uint32_t q = 0; q < R; q++)
-                    if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
-                        pv[j][q] = a.table[base + q];
-            }
-            bool more = false;
-#pragma unroll
-            for (uint32_t j = 0; j < FJ; j++) {
-                const uint64_t base = slot[j] & ~3ull;
-                bool live = pend[j]; /* still searching within this line */
-#pragma unroll
-                for (uint32_t q = 0; q < R; q++) {
-                    const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
-                    const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
-                    const bool m = in && kv == key[j];
-                    const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
-                    rec[j].x = m ? pv[j][q].x : rec[j].x;
-                    rec[j].y = m ? pv[j][q].y : rec[j].y;
-                    rec[j].z = m ? pv[j][q].z : rec[j].z;
-                    rec[j].w = m ? pv[j][q].w : rec[j].w;
-                    hit[j] = hit[j] || m;
-                    examined[j] += in ? 1u : 0u;
-                    live = live && !stop;
+            for (uint32_t j = 0; j < RB; j++) {
+                const uint32_t w = t + 256 * (jb + j);
+                hit[j] = false;
+                pend[j] = false;
+                rec[j] = make_uint4(0, 0, 0, 0);
+                key[j] = 0;
+                slot[j] = 0;
+                if (jb + j < J && w < W) {
+                    const uint8_t *c = codes + w;
+                    const uint32_t cmax =
+                        max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+                    const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
+                    const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
+                    key[j] = (uint64_t)ka * 160000u + kb;
+                    pend[j] = cmax < 20u;
+                    slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
                 }
-                /* not resolved in this line: on at the next one (wrapping at
-                 * the table's end, where the round's loads stopped) */
-                const uint64_t next = base + R >= NS ? 0 : base + R;
-                pend[j] = live;
-                slot[j] = live ? next : slot[j];
-                more = more || live;
             }
-            if (!__syncthreads_or(more))
-                break;
-        }
-        if (dbg)
-            a.dbg[2] = wall_clock64();
+            /* linear probe by 64-B lines: a round reads the rest of the line
+             * holding each pending window's next bucket (the table is 256-B
+             * aligned, 4 records per line), all of a thread's windows in
+             * flight at once, and examines those buckets in probe order -- a
+             * chain costs one round per line it touches instead of one per
+             * bucket (reading the next line too, speculatively, measured
+             * slower: 6.8 vs 4.6 us for one protein).  Bounded by num_sigs
+             * buckets where the reference would spin forever. */
+            constexpr uint32_t R = 4; /* records per round: one line */
+            uint64_t examined[RB];
+#pragma unroll
+            for (uint32_t j = 0; j < RB; j++)
+                examined[j] = 0;
+            const uint64_t NS = a.num_sigs;
+            for (;;) {
+                uint4 pv[RB][R];
+#pragma unroll
+                for (uint32_t j = 0; j < RB; j++) {
+                    const uint64_t base = slot[j] & ~3ull;
+#pragma unroll
+                    for (uint32_t q = 0; q < R; q++)
+                        if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
+                            pv[j][q] = a.table[base + q];
+                }
+                bool more = false;
+#pragma unroll
+                for (uint32_t j = 0; j < RB; j++) {
+                    const uint64_t base = slot[j] & ~3ull;
+                    bool live = pend[j]; /* still searching within this line */
+#pragma unroll
+                    for (uint32_t q = 0; q < R; q++) {
+                        const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
+                        const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
+                        const bool m = in && kv == key[j];
+                        const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
+                        rec[j].x = m ? pv[j][q].x : rec[j].x;
+                        rec[j].y = m ? pv[j][q].y : rec[j].y;
+                        rec[j].z = m ? pv[j][q].z : rec[j].z;
+                        rec[j].w = m ? pv[j][q].w : rec[j].w;
+                        hit[j] = hit[j] || m;
+                        examined[j] += in ? 1u : 0u;
+                        live = live && !stop;
+                    }
+                    /* not resolved in this line: on at the next one (wrapping
+                     * at the table's end, where the round's loads stopped) */
+                    const uint64_t next = base + R >= NS ? 0 : base + R;
+                    pend[j] = live;
+                    slot[j] = live ? next : slot[j];
+                    more = more || live;
+                }
+                if (!__syncthreads_or(more))
+                    break;
+            }
+            if (dbg && jb + RB >= J)
+                a.dbg[2] = wall_clock64();
 
-        /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
-        for (uint32_t j = 0; j < J; j++) {
-            bool h = false;
-            uint4 r = make_uint4(0, 0, 0, 0);
+            /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
 #pragma unroll
-            for (uint32_t q = 0; q < FJ; q++)
-                if (q == j) {
-                    h = hit[q];
-                    r = rec[q];
+            for (uint32_t q = 0; q < RB; q++) {
+                if (jb + q >= J)
+                    break;
+                const bool h = hit[q];
+                const uint4 r = rec[q];
+                const uint64_t m = __ballot(h);
+                if (lane == 0)
+                    wave_cnt[wave] = (uint32_t)__popcll(m);
+                __syncthreads();
+                uint32_t before = 0, total = 0;
+                for (uint32_t v = 0; v < 4; v++) {
+                    before += v < wave ? wave_cnt[v] : 0u;
+                    total += wave_cnt[v];
                 }
-            const uint64_t m = __ballot(h);
-            if (lane == 0)
-                wave_cnt[wave] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t before = 0, total = 0;
-            for (uint32_t v = 0; v < 4; v++) {
-                before += v < wave ? wave_cnt[v] : 0u;
-                total += wave_cnt[v];
+                if (h) {
+                    const uint32_t at = nh + before + lanes_below(m);
+                    hrec[at] = r;
+                    hpos[at] = t + 256 * (jb + q);
+                }
+                nh += total;
+                __syncthreads();
             }
-            if (h) {
-                const uint32_t at = nh + before + lanes_below(m);
-                hrec[at] = r;
-                hpos[at] = t + 256 * j;
-            }
-            nh += total;
-            __syncthreads();
         }
     }
     if (dbg)
@@ -694,7 +701,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
          * thread 0 beyond.  (r4f: a 36-OTU call's pairs sort in 0.33 us; the
          * calls past 64 pairs, on the serial replay then, cost 11 us per
          * call on average.) */
-        constexpr uint32_t SW = FJ * 2 < 8 ? FJ * 2 : 8;
+        constexpr uint32_t SW = FJ * 2 < 4 ? FJ * 2 : 4;
         const auto by_count = [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; };
         if (d > 1 && d <= 64) {
             if (wave == 0)
@@ -870,10 +877,18 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         a.dbg = h->debug ? dbgs[slot].stamp : nullptr;
         const FusedSlot in{res_base + (uint64_t)slot * SVC_RES_STRIDE, len};
         __syncthreads(); /* every thread has its copy of the request before cmd can change */
-        if (len <= 2 * 256 + 8)
-            fused_small_body<2, FusedSlot, QUAD>(a, in, 0); /* quads: up to 512 windows (8 per quad) */
-        else
+        /* one body for every length (its registers probe two 256-window
+         * slices at a time, its LDS holds all of them): a second, inlined
+         * body for short proteins made the kernel spill ~190 SGPRs into VGPR
+         * lanes, reloaded in the short path's loops too */
+        if constexpr (QUAD) {
+            if (len <= 2 * 256 + 8)
+                fused_small_body<2, FusedSlot, true>(a, in, 0); /* quads: up to 512 windows (8 per quad) */
+            else
+                fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
+        } else {
             fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
+        }
         last = req;
     }
 }

@@ -23,4 +23,9 @@ for rep in 1 2 3; do
   timeout -k 10 300 $B2 --probe-stream 1 > "$OUT/c2_pstream.$rep.json" 2> "$OUT/c2_pstream.$rep.err"
   KGX_PROBE_PRIORITY=1 timeout -k 10 300 $B2 --probe-stream 1 > "$OUT/c2_pstream_hi.$rep.json" 2> "$OUT/c2_pstream_hi.$rep.err"
 done
+# the fused body probing two slices at a time (one body in the service kernel)
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_svc.py tests/test_gpu_coalesce.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_svc.log" 2>&1
+env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16,32 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade.json" 2> "$OUT/facade.err"
+env KGX_FACADE_MODES=2 KGX_FACADE_THREADS=1,16 KGX_SVC_DEBUG=1 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/facade_dbg.json" 2> "$OUT/facade_dbg.err"
+KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
 echo "[gpu_r4o] done" >&2
