@@ -1212,17 +1212,8 @@ int probe_chained(kgx_ctx *c, Launch launch)
          * (one hardware queue), entered when this context's inputs are ready
          * and left back to this context's stream */
         lock.lock();
-        if (!img->probe_stream) {
-            /* KGX_PROBE_PRIORITY=1: the probes' stream at the device's highest
-             * priority, so their workgroups dispatch ahead of the other
-             * contexts' scorers (an experiment: the step vs the probe alone) */
-            int least = 0, greatest = 0;
-            const char *pp = std::getenv("KGX_PROBE_PRIORITY");
-            if (pp && std::atoi(pp) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
-                HIP_TRY(hipStreamCreateWithPriority(&img->probe_stream, hipStreamNonBlocking, greatest));
-            else
-                HIP_TRY(hipStreamCreateWithFlags(&img->probe_stream, hipStreamNonBlocking));
-        }
+        if (!img->probe_stream)
+            HIP_TRY(hipStreamCreateWithFlags(&img->probe_stream, hipStreamNonBlocking));
         if (!c->probe_ready)
             HIP_TRY(hipEventCreateWithFlags(&c->probe_ready, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(c->probe_ready, c->stream));
@@ -2150,13 +2141,14 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
 /* A stream for the host path's bulk copies / uploads.  The runtime spreads a
  * process's streams over a few hardware queues (4 by default), each a FIFO
  * that blocks behind an event wait at its head, so the copy stream's waits
- * could hold up another context's kernels queued behind them.  With
- * KGX_OWN_QUEUES=1 the stream is created with a full CU mask: a masked
- * stream gets a hardware queue of its own. */
+ * held up other streams' work queued behind them.  The stream is created
+ * with a full CU mask: a masked stream gets a hardware queue of its own
+ * (r4o, the bench process's host path: 3.83 vs 4.17 ms per 30M-residue
+ * batch; KGX_OWN_QUEUES=0 restores a plain stream). */
 hipError_t own_queue_stream(int device, hipStream_t *s)
 {
     const char *e = std::getenv("KGX_OWN_QUEUES");
-    if (e && std::atoi(e) != 0) {
+    if (!e || std::atoi(e) != 0) {
         int cus = 0;
         hipError_t r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (r == hipSuccess && cus > 0) {
