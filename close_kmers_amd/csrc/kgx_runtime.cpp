@@ -2153,7 +2153,9 @@ hipError_t own_queue_stream(int device, hipStream_t *s)
         hipError_t r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (r == hipSuccess && cus > 0) {
             std::vector<uint32_t> mask((size_t)(cus + 31) / 32, ~0u);
-            return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+            if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess)
+                return hipSuccess;
+            (void)hipGetLastError(); /* no queue left for it: a plain stream */
         }
     }
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
