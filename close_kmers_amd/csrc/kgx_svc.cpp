@@ -92,7 +92,7 @@ struct SvcState {
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
      * + scorer, and [5] 3->6 the record stores alone) */
     bool debug = false;
-    std::atomic<uint64_t> phase_ns[10] = {};
+    std::atomic<uint64_t> phase_ns[8] = {};
     /* KGX_SVC_SLEEP_US: a caller sleeps this long before it spins for its
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
@@ -479,7 +479,7 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? (uint64_t)(s->priority + 100) : 0;
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
-    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '9') /* "phase_n0".."phase_n9" */
+    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '7') /* "phase_n0".."phase_n7" */
         *value = s ? s->phase_ns[n[7] - '0'].load() : 0;
     else
         return fail(KGX_EINVAL, "unknown service statistic " + n);
@@ -602,8 +602,6 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         for (int k = 1; k <= 4; k++)
             s->phase_ns[k] += (st[k] - st[k - 1]) * 10; /* 100 MHz ticks */
         s->phase_ns[5] += (st[6] - st[3]) * 10; /* compaction end -> thread 0's record stores issued */
-        s->phase_ns[8] += (st[5] - st[4]) * 10; /* counts stored + the system-scope fence */
-        s->phase_ns[9] += (st[5] - st[0]) * 10; /* the device's whole part: request seen -> fenced */
         if (want & KGX_WANT_OTU) {
             s->phase_ns[6] += (st[4] - st[7]) * 10; /* the OTU tally alone */
             s->phase_ns[7] += (st[4] - st[8]) * 10; /* ... its sort by count */

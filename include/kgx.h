@@ -469,9 +469,9 @@ int kgx_svc_stop(kgx_image *img);
  * the device's highest priority, so it has a hardware queue of its own and
  * batch streams never queue behind the persistent instances;
  * KGX_SVC_PRIORITY=normal gives it a normal stream),
- * "phase_n0".."phase_n9" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
- * call, the device phases, the OTU tally of calls that want it, the tally's
- * final sort by count, the closing fence, and the device's whole part) */
+ * "phase_n0".."phase_n7" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
+ * call, the device phases, the OTU tally of calls that want it and the
+ * tally's final sort by count) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option
