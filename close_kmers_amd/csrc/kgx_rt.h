@@ -415,6 +415,7 @@ struct kgx_ctx {
      * faster (r4l/r4m: 3.66-4.21 vs 3.76-4.09 ms per 30M-residue batch; with
      * 16 queues the uploads do run early, 3.60-3.90 ms) */
     int host_upload_stream = 0;
+    int host_score_variant = 1; /* streamed chunks' scorer (option "host_score_variant"; -1: score_variant) */
     hipStream_t up_stream = nullptr;
     kgx::DevBuf up_res, up_off;
     kgx::DevBuf dense_mask, dense_best; /* a chunk's mask / best calls for its bulk copy */

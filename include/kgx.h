@@ -331,7 +331,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * chunk's residues are up (an H2D beside the D2H's stores is slowed 3-4x).
  * "host_upload_stream" 1: chunks go up on a stream of their own into
  * per-batch device regions as soon as they are staged (0, the default: on
- * the context's stream, behind the chunk before).
+ * the context's stream, behind the chunk before).  "host_score_variant" (default 1,
+ * the wave scorer; -1: the context's "score_variant"): the streamed chunks'
+ * scorer.
  * "host_stream" 1 (default): chunks need no host round trip -- CSR offsets
  * are scanned on the device and the bulk copies (on a separate copy stream)
  * are sized on the device into host regions sized from the hit / call / OTU
