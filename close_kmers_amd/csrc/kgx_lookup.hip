@@ -1691,18 +1691,8 @@ hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wba
 #define KGX_SCORE(P, B)                                                                                          \
     hipLaunchKernelGGL((score_kernel<P, B>), lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot, \
                        calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want, skip)
-    /* KGX_SCORE_BATCH=16: records per batch for PACKED16 (an experiment:
-     * fewer dependent load rounds per lane vs more registers) */
-    static const int sb_env = [] {
-        const char *e = std::getenv("KGX_SCORE_BATCH");
-        return e ? std::atoi(e) : 0;
-    }();
     if (pk && small)
         KGX_SCORE(true, 2);
-    else if (pk && sb_env == 16)
-        KGX_SCORE(true, 16);
-    else if (pk && sb_env == 4)
-        KGX_SCORE(true, 4);
     else if (pk)
         KGX_SCORE(true, SCORE_BATCH);
     else if (small)
