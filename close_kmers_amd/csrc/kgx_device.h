@@ -86,6 +86,22 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v)
     return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
 }
+/* v of lane (lane ^ j), j < 64, every lane active: one DPP move where one
+ * does it -- j 1 and 2 quad permutes, j 8 a rotation by 8 within the 16-lane
+ * row -- and ds_bpermute (an LDS round trip) otherwise */
+__device__ __forceinline__ int32_t xor_lane(int32_t v, uint32_t j)
+{
+    switch (j) {
+    case 1:
+        return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); /* quad_perm [1,0,3,2] */
+    case 2:
+        return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); /* quad_perm [2,3,0,1] */
+    case 8:
+        return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false); /* row_ror:8 */
+    default:
+        return __shfl_xor(v, (int)j);
+    }
+}
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -651,7 +651,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                         for (uint32_t r = 0; r < FJ; r++) {
                             if (r < R) {
                                 const uint32_t e = t + 256u * r;
-                                const int32_t b = j >= 64 ? v[e ^ j] : __shfl_xor(val[r], (int)j);
+                                const int32_t b = j >= 64 ? v[e ^ j] : xor_lane(val[r], j);
                                 /* the pair's lower entry keeps the min when ascending */
                                 const bool keep_min = ((e & j) == 0) == ((e & k) == 0);
                                 val[r] = keep_min ? min(val[r], b) : max(val[r], b);
