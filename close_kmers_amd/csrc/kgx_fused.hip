@@ -26,6 +26,8 @@
  * min_hits >= 1, want within HITS | CALLS, every sequence at most
  * FUSED_MAX_WINDOWS windows.
  */
+#include <type_traits>
+
 #include "kgx_device.h"
 #include "kgx_internal.h"
 #include "kgx_lstd.h"
@@ -125,9 +127,27 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     const uint64_t wb = In::wb(a, k, s);
     const uint32_t W = (uint32_t)windows_of(len);
     __syncthreads();
-    /* 1. residues -> codes (each wave reads 64 consecutive bytes per round) */
-    for (uint32_t i = t; i < W + 8 && i < len; i += 256)
-        codes[i] = code_tab[In::res(a, k, r0 + i)];
+    /* 1. residues -> codes */
+    if constexpr (std::is_same<IN, FusedSlot>::value) {
+        /* the service's slot (16-B aligned, 4 KB): 16 bytes per thread, so a
+         * protein of up to 4,096 residues costs one device-memory round trip
+         * (a byte per thread took two for a 300-aa protein) */
+        const uint32_t nb = (uint32_t)min<uint64_t>(W + 8, len);
+        for (uint32_t c = t; 16 * c < nb; c += 256) {
+            const uint4 q = reinterpret_cast<const uint4 *>(k.res)[c];
+            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (uint32_t b = 0; b < 16; b++) {
+                const uint32_t i = 16 * c + b;
+                if (i < nb)
+                    codes[i] = code_tab[(w4[b >> 2] >> (8 * (b & 3))) & 0xFFu];
+            }
+        }
+    } else {
+        /* each wave reads 64 consecutive bytes per round */
+        for (uint32_t i = t; i < W + 8 && i < len; i += 256)
+            codes[i] = code_tab[In::res(a, k, r0 + i)];
+    }
     __syncthreads();
     if (dbg)
         a.dbg[1] = wall_clock64();
