@@ -5,7 +5,7 @@
  * call the resident service (kgx_svc_call) while one thread runs
  * kgx_process_batch on its own context, over and over.  Native threads, so
  * the clocks time the GPU paths, not a Python harness's GIL
- * (tests/test_gpu_svc.py::test_svc_beside_batches_native).
+ * (tests/test_gpu_svc.py::test_svc_beside_batches_on_the_same_image).
  *
  *   beside_check N_KEYS NUM_SIGS QUERIES.bin T SECONDS
  *

@@ -223,7 +223,7 @@ def test_svc_threads_and_restarts_match_oracle(svc_image, oracle_lib):
     _check(oracle_lib, table, seqs[1], _tuple(PARAMS[1]), h, c, "after stop")
 
 
-def test_svc_beside_batches_on_the_same_image(svc_image, oracle_lib):
+def test_svc_beside_batches_python_threads_exact(svc_image, oracle_lib):
     """A pool of per-sequence callers (service) and a batch caller (its own
     context) on one image at once: both stay exact, and the batches keep
     finishing while service instances come and go (their kernels may share a
@@ -278,10 +278,11 @@ def test_svc_beside_batches_on_the_same_image(svc_image, oracle_lib):
           f"max {max(batch_ms):.2f} ms")
 
 
-def test_svc_beside_batches_native(tmp_path):
-    """The same mix timed from native threads (tests/native/beside_check.cpp;
-    the Python test above times its own GIL: r3z's "3.0 ms median / 28 ms max"
-    beside the service was the harness): 8 service callers and a batch caller
+def test_svc_beside_batches_on_the_same_image(tmp_path):
+    """The mix of the Python test above (its exactness part), timed from
+    native threads (tests/native/beside_check.cpp; Python threads time their
+    own GIL: round 3's "3.0 ms median / 28 ms max" beside the service was the
+    harness): 8 service callers and a batch caller
     of 2,000 C2 proteins on the bench's 1e9-key image for 3 s.  Every batch
     equals the batch run alone and every service answer its slice of it, and
     the service's high-priority stream keeps the batches at speed: median
