@@ -129,19 +129,17 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     __syncthreads();
     /* 1. residues -> codes */
     if constexpr (std::is_same<IN, FusedSlot>::value) {
-        /* the service's slot (16-B aligned, 4 KB): 16 bytes per thread, so a
-         * protein of up to 4,096 residues costs one device-memory round trip
-         * (a byte per thread took two for a 300-aa protein) */
+        /* the service's slot (16-B aligned, 4 KB): 4 bytes per thread, so a
+         * protein of up to 1,024 residues costs one device-memory round trip
+         * (a byte per thread took two for a 300-aa protein; 16 bytes per
+         * thread left 16 dependent table lookups on a few threads, r4aa) */
         const uint32_t nb = (uint32_t)min<uint64_t>(W + 8, len);
-        for (uint32_t c = t; 16 * c < nb; c += 256) {
-            const uint4 q = reinterpret_cast<const uint4 *>(k.res)[c];
-            const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+        for (uint32_t c = t; 4 * c < nb; c += 256) {
+            const uint32_t w = reinterpret_cast<const uint32_t *>(k.res)[c];
 #pragma unroll
-            for (uint32_t b = 0; b < 16; b++) {
-                const uint32_t i = 16 * c + b;
-                if (i < nb)
-                    codes[i] = code_tab[(w4[b >> 2] >> (8 * (b & 3))) & 0xFFu];
-            }
+            for (uint32_t b = 0; b < 4; b++)
+                if (4 * c + b < nb)
+                    codes[4 * c + b] = code_tab[(w >> (8 * b)) & 0xFFu];
         }
     } else {
         /* each wave reads 64 consecutive bytes per round */
