@@ -340,7 +340,7 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * rates of earlier batches; a batch that overflows them reruns on the exact
  * schedule (host_stream 0: counts to the host, then gather and copy, with
  * "counts_first" 1 holding chunk k's bulk copy until chunk k+1's counts are
- * out).  "stage_threads" (default 4): threads copying the caller's residues
+ * out).  "stage_threads" (default 8): threads copying the caller's residues
  * into pinned staging.  "small_batch" (0..2^24 residues, default 2^21; 0 =
  * off): a one-chunk batch of at most this many residues is planned on the
  * host, read by the device from mapped pinned staging and its results stored

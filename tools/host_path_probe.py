@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--copy-blocks", default="64", help="host_copy_blocks settings to try (copy 1)")
     ap.add_argument("--hits16", default="0,1", help="host_hits16 settings to try")
     ap.add_argument("--threads", default="8", help="host_threads settings to try (hits16 1)")
-    ap.add_argument("--stage", default="4", help="stage_threads settings to try")
+    ap.add_argument("--stage", default="8", help="stage_threads settings to try")
     ap.add_argument("--counts-first", default="1", help="counts_first settings to try")
     ap.add_argument("--stream", default="0,1", help="host_stream settings to try")
     ap.add_argument("--taper", default="1", help="host_taper settings to try")
