@@ -432,6 +432,12 @@ struct kgx_ctx {
     kgx::PinnedVec<uint32_t> h_hits12; /* 12-B records (3 words per hit, no key) */
     int host_rec12 = 1; /* streamed: 12-B records, key re-encoded on the host (option "host_rec12") */
     int host_h2d_first = 1; /* streamed: chunk k's D2H waits for chunk k+1's H2D (option "host_h2d_first") */
+    /* streamed: every chunk staged into its own region of h_res_all / h_off_all
+     * (option "host_stage_all"), not into the context's h_res behind the H2D of
+     * the chunk two before */
+    int host_stage_all = 1;
+    kgx::PinnedVec<char> h_res_all;
+    kgx::PinnedVec<uint64_t> h_off_all;
     /* small host batches (<= small_batch residues, option "small_batch", 0 =
      * off): planned on the host, read by the device from the mapped staging
      * blob, results stored into mapped memory: one host wait per batch */

@@ -956,6 +956,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->host_upload_stream = (int)value;
         return KGX_OK;
     }
+    if (n == "host_stage_all") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_stage_all must be 0 or 1");
+        c->host_stage_all = (int)value;
+        return KGX_OK;
+    }
     if (n == "host_h2d_first") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "host_h2d_first must be 0 or 1");
@@ -1463,20 +1469,19 @@ void cut_at_nul(char *b, uint64_t len)
     }
 }
 
-/* sequences [s0, s1) of a host batch -> x's pinned staging (host work only;
- * large ranges copied and NUL-scanned in parts on the stage pool sp) */
-int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1,
-                    HostPool *sp = nullptr)
+/* sequences [s0, s1) of a host batch -> pinned staging at dst (residues) and
+ * off (the n + 1 chunk-relative offsets); host work only, large ranges copied
+ * and NUL-scanned in parts on the stage pool sp */
+void stage_copy_into(char *dst, uint64_t *off, const char *residues, const uint64_t *seq_offsets, uint32_t s0,
+                     uint32_t s1, HostPool *sp)
 {
     const uint32_t n = s1 - s0;
     const uint64_t r0 = n ? seq_offsets[s0] : 0;
     const uint64_t n_res = n ? seq_offsets[s1] - r0 : 0;
-    HIP_TRY(x->h_res.resize(n_res));
     bool has_nul = false;
     if (sp && n_res >= (1u << 20)) {
         const unsigned P = sp->size();
         std::atomic<bool> nul{false};
-        char *dst = x->h_res.data();
         const char *src = residues + r0;
         for (unsigned p = 0; p < P; p++) {
             const uint64_t a = n_res * p / P, b = n_res * (p + 1) / P;
@@ -1490,16 +1495,25 @@ int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offset
         (void)sp->wait();
         has_nul = nul.load();
     } else if (n_res) {
-        std::memcpy(x->h_res.data(), residues + r0, n_res);
+        std::memcpy(dst, residues + r0, n_res);
         /* one scan of the whole range first: NUL bytes are rare */
-        has_nul = std::memchr(x->h_res.data(), 0, n_res) != nullptr;
+        has_nul = std::memchr(dst, 0, n_res) != nullptr;
     }
     if (has_nul)
         for (uint32_t s = s0; s < s1; s++)
-            cut_at_nul(x->h_res.data() + (seq_offsets[s] - r0), seq_offsets[s + 1] - seq_offsets[s]);
-    HIP_TRY(x->h_off_stage.resize(n + 1));
+            cut_at_nul(dst + (seq_offsets[s] - r0), seq_offsets[s + 1] - seq_offsets[s]);
     for (uint32_t i = 0; i <= n; i++)
-        x->h_off_stage[i] = n ? seq_offsets[s0 + i] - r0 : 0;
+        off[i] = n ? seq_offsets[s0 + i] - r0 : 0;
+}
+
+/* sequences [s0, s1) of a host batch -> x's pinned staging */
+int stage_host_copy(kgx_ctx *x, const char *residues, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1,
+                    HostPool *sp = nullptr)
+{
+    const uint32_t n = s1 - s0;
+    HIP_TRY(x->h_res.resize(n ? seq_offsets[s1] - seq_offsets[s0] : 0));
+    HIP_TRY(x->h_off_stage.resize(n + 1));
+    stage_copy_into(x->h_res.data(), x->h_off_stage.data(), residues, seq_offsets, s0, s1, sp);
     return KGX_OK;
 }
 
@@ -1833,11 +1847,27 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         HIP_TRY(c->up_res.reserve(std::max<uint64_t>(res_at[K], 256)));
         HIP_TRY(c->up_off.reserve(std::max<uint64_t>(off_at[K], 2) * sizeof(uint64_t)));
     }
+    /* host_stage_all: every chunk staged into a pinned region of its own (the
+     * same res_at / off_at layout), so no staging waits for the H2D of the
+     * chunk two before to free its context's staging buffer */
+    const bool sall = c->host_stage_all != 0;
+    if (sall) {
+        HIP_TRY(c->h_res_all.resize(std::max<uint64_t>(res_at[K], 256)));
+        HIP_TRY(c->h_off_all.resize(std::max<uint64_t>(off_at[K], 2)));
+    }
+    auto staged_res = [&](kgx_ctx *x, uint32_t k) -> const char * {
+        return sall ? c->h_res_all.data() + res_at[k] : x->h_res.data();
+    };
+    auto staged_off = [&](kgx_ctx *x, uint32_t k) -> const uint64_t * {
+        return sall ? c->h_off_all.data() + off_at[k] : x->h_off_stage.data();
+    };
 
     /* enqueue chunk k on x: everything up to its bulk copy */
     auto enqueue = [&](kgx_ctx *x, uint32_t k) -> int {
         const uint32_t s0 = cut[k], n = cut[k + 1] - cut[k];
-        const uint64_t n_res = x->h_res.size();
+        const uint64_t n_res = n ? seq_offsets[cut[k + 1]] - seq_offsets[s0] : 0;
+        const char *hres = staged_res(x, k);
+        const uint64_t *hoff = staged_off(x, k);
         hipStream_t us = up ? c->up_stream : x->stream;
         if (prof)
             HIP_TRY(hipEventRecord(c->prof_ev[4 * k], us));
@@ -1848,13 +1878,17 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
             uint8_t *rd = c->up_res.as<uint8_t>() + res_at[k];
             uint64_t *od = c->up_off.as<uint64_t>() + off_at[k];
             if (n_res)
-                HIP_TRY(hipMemcpyAsync(rd, x->h_res.data(), n_res, hipMemcpyHostToDevice, us));
-            HIP_TRY(hipMemcpyAsync(od, x->h_off_stage.data(), x->h_off_stage.size() * sizeof(uint64_t),
-                                   hipMemcpyHostToDevice, us));
+                HIP_TRY(hipMemcpyAsync(rd, hres, n_res, hipMemcpyHostToDevice, us));
+            HIP_TRY(hipMemcpyAsync(od, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
             d_res = rd;
             d_off = od;
-        } else if ((rc = stage_upload(x))) {
-            return rc;
+        } else {
+            /* reserved for the largest chunk above: no reallocation here */
+            HIP_TRY(x->residues.reserve(n_res + 16));
+            HIP_TRY(x->offsets.reserve((n + 1) * sizeof(uint64_t)));
+            if (n_res)
+                HIP_TRY(hipMemcpyAsync(x->residues.p, hres, n_res, hipMemcpyHostToDevice, us));
+            HIP_TRY(hipMemcpyAsync(x->offsets.p, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
         }
         HIP_TRY(hipEventRecord(c->chunk_h2d[k], us));
         if (prof)
@@ -2045,10 +2079,14 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     std::vector<double> ht;
     for (uint32_t k = 0; k < K && !rc; k++) {
         kgx_ctx *x = xs[k & 1];
-        if (k >= 2)
+        if (k >= 2 && !sall)
             HIP_TRY(hipEventSynchronize(c->chunk_h2d[k - 2])); /* x's staging buffer is free */
         const auto ts = now();
-        rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp);
+        if (sall)
+            stage_copy_into(c->h_res_all.data() + res_at[k], c->h_off_all.data() + off_at[k], residues, seq_offsets,
+                            cut[k], cut[k + 1], sp);
+        else
+            rc = stage_host_copy(x, residues, seq_offsets, cut[k], cut[k + 1], sp);
         const auto te = now();
         stage_ms += ms(ts, te);
         if (rc || (rc = enqueue(x, k)))
