@@ -435,7 +435,7 @@ struct kgx_ctx {
     /* streamed: every chunk staged into its own region of h_res_all / h_off_all
      * (option "host_stage_all"), not into the context's h_res behind the H2D of
      * the chunk two before */
-    int host_stage_all = 1;
+    int host_stage_all = 0; /* r4ak: 3.61-3.70 vs 3.49-3.73 ms per batch, no gain */
     kgx::PinnedVec<char> h_res_all;
     kgx::PinnedVec<uint64_t> h_off_all;
     /* small host batches (<= small_batch residues, option "small_batch", 0 =

@@ -329,9 +329,10 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * into kgx_hit records while later chunks stream ("host_nt" 1: with streaming
  * stores).  "host_h2d_first" 1 (default): a chunk's D2H starts once the next
  * chunk's residues are up (an H2D beside the D2H's stores is slowed 3-4x).
- * "host_stage_all" 1 (default): every chunk is staged into pinned memory of
- * its own, so staging never waits for an earlier chunk's H2D (0: the two
- * contexts' staging buffers, each reused once its last H2D is done).
+ * "host_stage_all" 1: every chunk is staged into pinned memory of its own, so
+ * staging never waits for an earlier chunk's H2D (0, the default: the two
+ * contexts' staging buffers, each reused once its last H2D is done; the same
+ * batch time).
  * "host_upload_stream" 1: chunks go up on a stream of their own into
  * per-batch device regions as soon as they are staged (0, the default: on
  * the context's stream, behind the chunk before).  "host_score_variant" (default 1,

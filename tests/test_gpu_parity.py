@@ -755,7 +755,7 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_h2d_first", 1)
         ctx.set_option("host_upload_stream", 0)
         ctx.set_option("host_score_variant", 1)
-        ctx.set_option("host_stage_all", 1)
+        ctx.set_option("host_stage_all", 0)
 
 
 @pytest.mark.parametrize("schedule", ["streamed_rec12", "streamed_rec16", "exact", "small", "aos24",
