@@ -437,6 +437,10 @@ struct kgx_ctx {
      * the chunk two before */
     int host_stage_all = 0; /* r4ak: 3.61-3.70 vs 3.49-3.73 ms per batch, no gain */
     kgx::PinnedVec<char> h_res_all;
+    /* streamed: chunk copies by DMA (hipMemcpyAsync of each region whole, at
+     * its host-sized room) instead of the counted device-store copy (option
+     * "host_stream_dma") */
+    int host_stream_dma = 0;
     kgx::PinnedVec<uint64_t> h_off_all;
     /* small host batches (<= small_batch residues, option "small_batch", 0 =
      * off): planned on the host, read by the device from the mapped staging

@@ -956,6 +956,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->host_upload_stream = (int)value;
         return KGX_OK;
     }
+    if (n == "host_stream_dma") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "host_stream_dma must be 0 or 1");
+        c->host_stream_dma = (int)value;
+        return KGX_OK;
+    }
     if (n == "host_stage_all") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "host_stage_all must be 0 or 1");
@@ -1965,6 +1971,29 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         if (c->host_h2d_first && k + 1 < K)
             HIP_TRY(hipStreamWaitEvent(cs, c->chunk_h2d[k + 1], 0));
         void *d = nullptr;
+        if (c->host_stream_dma) {
+            /* DMA engines, sized on the host: every region copied whole */
+            auto dma = [&](void *dst, const void *src, uint64_t bytes) -> hipError_t {
+                return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, cs) : hipSuccess;
+            };
+            const uint32_t planes = want_otu ? 3 : want_calls ? 2 : 1;
+            HIP_TRY(dma(c->h_counts.data() + 3 * (uint64_t)s0, x->dense_counts.p, planes * (uint64_t)n * sizeof(uint32_t)));
+            if (r12)
+                HIP_TRY(dma(c->h_hits12.data() + 3 * rb_h[k], x->dense_hits.p, cap_h[k] * 12));
+            else
+                HIP_TRY(dma(c->h_hits16.data() + rb_h[k], x->dense_hits.p, cap_h[k] * 16));
+            HIP_TRY(dma(c->h_mask.data() + mb[k], x->dense_mask.p, nwords * sizeof(uint64_t)));
+            if (want_calls)
+                HIP_TRY(dma(c->h_calls_region.data() + rb_c[k], x->dense_calls.p, cap_c[k] * sizeof(kgx_call)));
+            if (want_otu)
+                HIP_TRY(dma(c->h_otus_region.data() + rb_o[k], x->dense_otus.p, cap_o[k] * sizeof(kgx_otu)));
+            if (want_best)
+                HIP_TRY(dma(c->h_best.data() + s0, x->dense_best.p, n * sizeof(kgx_best_call)));
+            HIP_TRY(hipEventRecord(c->chunk_done[k], cs));
+            if (prof)
+                HIP_TRY(hipEventRecord(c->prof_done[k], cs));
+            return KGX_OK;
+        }
         if (n) {
             const uint32_t planes = want_otu ? 3 : want_calls ? 2 : 1;
             HIP_TRY(mapped(c->h_counts, 3 * (uint64_t)s0, &d));

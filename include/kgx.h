@@ -333,6 +333,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * staging never waits for an earlier chunk's H2D (0, the default: the two
  * contexts' staging buffers, each reused once its last H2D is done; the same
  * batch time).
+ * "host_stream_dma" 1: the streamed chunks' copies by DMA, each host region
+ * copied whole at its room (0, the default: device stores of the counted
+ * records into mapped memory).
  * "host_upload_stream" 1: chunks go up on a stream of their own into
  * per-batch device regions as soon as they are staged (0, the default: on
  * the context's stream, behind the chunk before).  "host_score_variant" (default 1,

@@ -736,13 +736,16 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_hits16", 1)
         ctx.set_option("host_copy_blocks", 1)
         # chunk k's D2H behind chunk k+1's H2D, or not; uploads on their own stream, or not;
-        # every chunk staged into its own pinned region, or into its context's buffer
-        for k, h2d_first, up, sv, sall in ((16, 1, 0, 1, 1), (37, 0, 1, -1, 0), (64, 1, 1, 0, 1), (9, 1, 0, 1, 0)):
+        # every chunk staged into its own pinned region, or into its context's buffer;
+        # chunk copies by device stores (sized on the device) or DMA (whole regions)
+        for k, h2d_first, up, sv, sall, dma in ((16, 1, 0, 1, 1, 0), (37, 0, 1, -1, 0, 1), (64, 1, 1, 0, 1, 0),
+                                                (9, 1, 0, 1, 0, 1)):
             ctx.set_option("host_chunks", k)
             ctx.set_option("host_h2d_first", h2d_first)
             ctx.set_option("host_upload_stream", up)
             ctx.set_option("host_score_variant", sv)
             ctx.set_option("host_stage_all", sall)
+            ctx.set_option("host_stream_dma", dma)
             for _ in range(2):  # the second pass runs with the rates the first one raised
                 got = ctx.process_batch(res, off, gpu.Params(5, 200, 0, 0), want=7)
                 assert_same(got, want, len(off) - 1)
@@ -756,6 +759,7 @@ def test_streamed_host_batch_copy_stream_lag(small_world, oracle_lib, gpu):
         ctx.set_option("host_upload_stream", 0)
         ctx.set_option("host_score_variant", 1)
         ctx.set_option("host_stage_all", 0)
+        ctx.set_option("host_stream_dma", 0)
 
 
 @pytest.mark.parametrize("schedule", ["streamed_rec12", "streamed_rec16", "exact", "small", "aos24",
