@@ -105,6 +105,8 @@ def main():
     out["ms_by_host_chunks"] = times
     out["compact"] = bool(args.compact)
     if args.no_pieces:
+        ctx.close()  # before exit: under rocprofv3 a context left open faulted in __cxa_finalize (r4al)
+        img.close()
         print(json.dumps(out), flush=True)
         return
     n_hits = len(r.hits)
