@@ -436,8 +436,18 @@ void KmerGuts::process_aa_seq(const std::string &id, const std::string &seq,
             }
             return;
         }
-        if (rc != KGX_EBUSY)
+        if (rc == KGX_EDEVICE) {
+            /* no answer within 10 s leaves the service "broken" (every later
+             * call KGX_EBUSY): replace it, so one stall does not turn the
+             * service off for the rest of the process; this call takes the
+             * batch path below */
+            uint64_t broken = 0;
+            if (kgx_svc_stat(image_->handle(), "broken", &broken) != KGX_OK || !broken)
+                throw_last(rc, "kgx_svc_call");
+            (void)kgx_svc_stop(image_->handle());
+        } else if (rc != KGX_EBUSY) {
             throw_last(rc, "kgx_svc_call");
+        }
     }
     if (coalesce) {
         SeqCoalescer::Req q;
@@ -1690,7 +1700,7 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
             for (size_t k = 0; k < K; k++) {
                 FqPart *nxt = nullptr;
                 FqLaunched ln;
-                std::unique_ptr<FqPart> tail;
+                FqPart *tail = nullptr;
                 if (k + 1 < K) {
                     /* the speculation of part k + 1 holds iff part k ends at a
                      * record start with nothing pending */
@@ -1702,12 +1712,14 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
                     } else {
                         /* the rest of the block, exactly, from part k's end state */
                         stop_workers();
-                        tail.reset(new FqPart);
+                        if (!tail_)
+                            tail_.reset(new FqPart);
+                        tail = tail_.get();
                         tail->begin((size_t)(end - cuts[k + 1]) + (cur->len - cur->roff.back()), cur->state, cur->id,
                                     std::string(cur->bases + cur->roff.back(), cur->len - cur->roff.back()));
                         tail->parse(cuts[k + 1], end);
                         finish_part(*tail);
-                        nxt = tail.get();
+                        nxt = tail;
                     }
                     const auto l1 = std::chrono::steady_clock::now();
                     ln = launch_block(nxt->view(), ctxs[(k + 1) % 2]);

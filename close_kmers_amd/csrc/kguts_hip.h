@@ -541,6 +541,9 @@ private:
     int state_ = 0;
     std::string id_, seq_;
     std::vector<std::unique_ptr<FqPart>> parts_;
+    /* the exact re-parse after a rejected speculative cut: kept, so its pinned
+     * buffer is allocated once, not per fallback */
+    std::unique_ptr<FqPart> tail_;
 };
 
 /* one host-buffer batch through kg's context, device results only (no D2H):

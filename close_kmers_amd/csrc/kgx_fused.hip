@@ -929,6 +929,10 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         }
         last = req;
     }
+    /* counted out: the host's exit hook waits for every launched instance's
+     * workgroups without a runtime call (kgx_svc.cpp, stop_all_at_exit) */
+    if (t == 0)
+        __hip_atomic_fetch_add(&out[slot].left, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,

@@ -259,7 +259,8 @@ struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last req
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */
     uint32_t done;       /* = req once the records and counts are visible */
-    uint32_t pad[12];
+    uint32_t left;       /* workgroups of this slot that have left (one per instance launched) */
+    uint32_t pad[11];
 };
 static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 128,
               "service slot lines");

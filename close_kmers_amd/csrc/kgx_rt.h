@@ -265,6 +265,10 @@ hipError_t launch_fq_plan(const uint64_t *off, uint32_t n, uint64_t *wbase, uint
 struct SvcState;
 /* stops and frees the image's call service (kgx_svc.cpp), if any */
 void svc_shutdown(kgx_image *img);
+/* the same, and keeps the image's service lock until the returned guard
+ * goes: a call arriving meanwhile waits for it before it starts a new
+ * service, so no instance is created over a table being replaced */
+std::unique_lock<std::mutex> svc_shutdown_hold(kgx_image *img);
 
 /* kgx_kmap_rollup's device scratch and host results (kgx_tables.hip), per
  * context: grow-only, no allocation per call once warm */

@@ -692,7 +692,9 @@ int kgx_image_set_filter(kgx_image *img, int log2_bits)
 {
     if (!img || log2_bits < 0 || (log2_bits && (log2_bits < 12 || log2_bits > 40)))
         return fail(KGX_EINVAL, "filter size: 0 (none) or 2^12 .. 2^40 bits");
-    svc_shutdown(img); /* the device-wide synchronisation below would wait out its instances */
+    /* the device-wide synchronisation below would wait out its instances,
+     * and the filter buffer is replaced under any service a call starts */
+    const auto hold = svc_shutdown_hold(img);
     HIP_TRY(hipSetDevice(img->device));
     HIP_TRY(hipDeviceSynchronize());
     if (img->d_filter)
@@ -719,7 +721,9 @@ int kgx_image_set_layout(kgx_image *img, int layout)
 {
     if (!img)
         return fail(KGX_EINVAL, "null image");
-    svc_shutdown(img); /* its workgroups hold the resident table's address */
+    /* its workgroups hold the resident table's address: no call starts a
+     * service until the table it would use is the new one */
+    const auto hold = svc_shutdown_hold(img);
     if (layout == KGX_LAYOUT_PACKED16)
         return image_pack(img);
     if (layout == KGX_LAYOUT_AOS24)
@@ -2147,7 +2151,12 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     }
     /* drain everything, whatever happened above */
     const hipError_t e0 = hipStreamSynchronize(xs[0]->stream), e1 = hipStreamSynchronize(xs[1]->stream);
-    const hipError_t e2 = hipStreamSynchronize(cs);
+    hipError_t e2 = hipStreamSynchronize(cs);
+    if (c->up_stream) { /* an upload issued before a failed enqueue may still read the staging memory */
+        const hipError_t e3 = hipStreamSynchronize(c->up_stream);
+        if (e2 == hipSuccess)
+            e2 = e3;
+    }
     const int prc = c->pool->wait();
     if (rc)
         return rc;
@@ -2214,14 +2223,27 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
 /* A stream for the host path's bulk copies / uploads.  The runtime spreads a
  * process's streams over a few hardware queues (4 by default), each a FIFO
  * that blocks behind an event wait at its head, so the copy stream's waits
- * held up other streams' work queued behind them.  The stream is created
- * with a full CU mask: a masked stream gets a hardware queue of its own
- * (r4o, the bench process's host path: 3.83 vs 4.17 ms per 30M-residue
- * batch; KGX_OWN_QUEUES=0 restores a plain stream). */
+ * held up other streams' work queued behind them.  The copy stream therefore
+ * gets a hardware queue the contexts' streams never share.  KGX_OWN_QUEUES:
+ *   2 (default) a stream at the device's lowest priority: the runtime keeps a
+ *     queue pool per priority, so it shares only with other copy streams;
+ *   1 a full-CU-mask stream, which gets a queue of its own (r4o: the bench's
+ *     host path 3.83 vs 4.17 ms per 30M-residue batch on a plain stream).  A
+ *     process that exits with such a stream alive faults inside rocprofv3's
+ *     finalisation (r5c: SIGSEGV in __cxa_finalize under --kernel-trace;
+ *     priority streams exit clean), so it is no longer the default;
+ *   0 a plain stream. */
 hipError_t own_queue_stream(int device, hipStream_t *s)
 {
     const char *e = std::getenv("KGX_OWN_QUEUES");
-    if (!e || std::atoi(e) != 0) {
+    const int mode = e ? std::atoi(e) : 2;
+    if (mode == 2) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest &&
+            hipStreamCreateWithPriority(s, hipStreamNonBlocking, least) == hipSuccess)
+            return hipSuccess;
+        (void)hipGetLastError();
+    } else if (mode == 1) {
         int cus = 0;
         hipError_t r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (r == hipSuccess && cus > 0) {
@@ -2259,7 +2281,9 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
     kgx_ctx *xs[2] = {c, t};
     if (!c->copy_stream)
         HIP_TRY(own_queue_stream(c->img->device, &c->copy_stream));
-    if (!c->up_stream)
+    /* the upload stream only when asked for: each own-queue stream holds a
+     * hardware queue of the process's few */
+    if (c->host_upload_stream && !c->up_stream)
         HIP_TRY(own_queue_stream(c->img->device, &c->up_stream));
     for (auto *ev : {&c->chunk_counts, &c->chunk_gathered, &c->chunk_done, &c->chunk_h2d})
         while (ev->size() < K) {

@@ -235,12 +235,29 @@ void destroy(SvcState *s)
     delete s;
 }
 
+/* Process exit with services alive (the reference's server ends from a
+ * signal with its workers live, kserver.cc:206-214).  No runtime call here:
+ * by the time exit handlers run, the calling thread's thread_local objects
+ * are gone, and a profiler's HIP wrappers keep theirs there (r5a: rocprofv3
+ * aborted in hipStreamSynchronize from this hook, "get_stream_stack() must be
+ * non nullptr", and the process hung).  Every slot's stop word is raised by a
+ * plain store, and the hook waits -- at most 1 s -- until each slot's
+ * workgroups of every instance launched have counted themselves out
+ * (SvcSlotOut.left, a system-scope add in svc_kernel), so no persistent grid
+ * outlives the process.  Streams and pinned memory go with the process. */
 void stop_all_at_exit()
 {
     std::lock_guard<std::mutex> lk(g_live_mu);
+    for (SvcState *s : g_live)
+        for (uint32_t i = 0; i < s->slots; i++)
+            __atomic_store_n(&s->hdr[i].stop, 1u, __ATOMIC_RELEASE);
+    wc_fence();
+    const int64_t t0 = now_ns();
     for (SvcState *s : g_live) {
-        (void)hipSetDevice(s->device);
-        drain(s);
+        const uint32_t launched = (uint32_t)s->n_launches.load();
+        for (uint32_t i = 0; i < s->slots; i++)
+            while (__atomic_load_n(&s->out[i].left, __ATOMIC_ACQUIRE) != launched && now_ns() - t0 < 1000000000ll)
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
@@ -419,6 +436,13 @@ void svc_shutdown(kgx_image *img)
 {
     std::lock_guard<std::mutex> lk(img->svc_mu);
     shutdown_locked(img);
+}
+
+std::unique_lock<std::mutex> svc_shutdown_hold(kgx_image *img)
+{
+    std::unique_lock<std::mutex> lk(img->svc_mu);
+    shutdown_locked(img);
+    return lk;
 }
 
 }  // namespace kgx
