@@ -235,6 +235,147 @@ def pool_main(args) -> int:
     return 0
 
 
+def family_kmap(abi, synth, spec, dev, n_fam):
+    """The synthetic family DB of tools/bench_server.py --families: family i =
+    source protein i of the image (its 292 windows' k-mers), as
+    kmer_to_family_id_ (KMAP_SET) on device dev."""
+    n_fam = min(n_fam, spec.n_src)
+    keys, ids = [], []
+    for a in range(0, n_fam, 20000):  # bounded host memory per step
+        src = np.arange(a, min(n_fam, a + 20000))
+        keys.append(synth.encode_windows(synth.source_residue_codes(src), synth.SRC_WIN).reshape(-1))
+        ids.append(np.repeat(src.astype(np.uint32), synth.SRC_WIN))
+    fam = abi.Kmap(dev, abi.KMAP_SET)
+    fam.add(np.concatenate(keys), np.concatenate(ids))
+    return fam, n_fam
+
+
+def host_path_lookup_leg(abi, synth, img, spec, dev, res_h, off_h, params, n_fam=100000):
+    """/lookup in family mode with find_best_match (lookup_request.cc:153-210,
+    446-482) from host buffers: kgx_pool_lookup -- residues up, probe + score
+    + device find_best_call + on_hit rollups on the device, only the rollup
+    rows, offsets and best calls back (nothing per hit crosses PCIe).  Timed
+    over pool sizes, pinned and pageable input; a 1,000-sequence slice is
+    checked against one context's pass + kgx_kmap_rollup."""
+    t0 = time.time()
+    fam, n_fam = family_kmap(abi, synth, spec, dev, n_fam)
+    t_fam = time.time() - t0
+    n = len(off_h) - 1
+    n_res = int(off_h[-1] - off_h[0])
+    want = abi.WANT_BEST
+    pin = abi.pinned_empty(len(res_h))
+    pin[:] = res_h
+    by, rows_n, ev_n = {}, 0, 0
+    best_cfg, best_t = None, None
+    for n_ctx in (2, 4, 8):
+        with abi.Pool([img], n_ctx) as pool:
+            for name, src in (("pinned", pin), ("pageable", res_h)):
+                r, roff, rows = pool.lookup([fam], src, off_h, params, want=want, copy=False)  # warm
+                ts = []
+                for _ in range(7):
+                    t1 = time.perf_counter()
+                    r, roff, rows = pool.lookup([fam], src, off_h, params, want=want, copy=False)
+                    ts.append(time.perf_counter() - t1)
+                t = float(np.median(ts))
+                by[f"{name}_ctx{n_ctx}"] = t * 1e3
+                if name == "pinned" and (best_t is None or t < best_t):
+                    best_t, best_cfg = t, n_ctx
+            S = min(1000, n)
+            sl_off, sl_rows = roff[:S + 1].copy(), rows[:int(roff[S])].copy()
+            sl_best = r.best[:S].copy()
+            rows_n, ev_n = int(roff[-1]), int(r.hit_offsets[-1])
+    with abi.Context(img) as c1:
+        one = c1.process_batch(res_h[:int(off_h[S] - off_h[0])], off_h[:S + 1] - off_h[0], params, want=want)
+        woff, wrows = fam.rollup(c1, abi.ROLLUP_FAMILY)
+    ok = (np.array_equal(sl_off, woff) and sl_rows.tobytes() == wrows.tobytes()
+          and sl_best.tobytes() == one.best.tobytes())
+    fam.close()
+    t_pg = min(v for k, v in by.items() if k.startswith("pageable")) / 1e3
+    out = {"value": n_res / best_t, "unit": "residues/s", "ms_per_batch": best_t * 1e3, "pool_contexts": best_cfg,
+           "value_pageable_input": n_res / t_pg, "ms_by_config": by,
+           "rollup_rows": rows_n, "hits_on_device": ev_n, "families": n_fam, "family_db_build_s": round(t_fam, 2),
+           "slice_check": {"sequences": S, "equal_to_one_context_pass_plus_kgx_kmap_rollup": bool(ok)},
+           "note": "lookup_request family mode + find_best_match over the C2 batch from host buffers "
+                   "(kgx_pool_lookup over one device): H2D residues, probe, score, device find_best_call and the "
+                   "on_hit rollups on the device; D2H only rollup rows (16 B each), their offsets and the best "
+                   "calls.  value: residues in pinned memory (kgx_host_alloc, read by DMA, no staging); "
+                   "value_pageable_input: the same from pageable memory (staged).  Parity of the rows against "
+                   "on_hit over the oracle's hits: tests/test_gpu_lookup_pool.py"}
+    log(f"[bench] host_path_lookup {out['value']:.3e} residues/s ({best_t * 1e3:.2f} ms, {best_cfg} contexts), "
+        f"pageable {out['value_pageable_input']:.3e}; slice check {'ok' if ok else 'MISMATCH'}; {by}")
+    return out
+
+
+def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_permille):
+    """C5 (BASELINE.json configs[4]) as the reference would run it: one host
+    batch of n x Ls aa through kgx_pool over one image replica per device
+    (device-to-device copies of img0), residue-balanced shards, compact
+    results concatenated in input order (threadpool.cc:18-44,
+    lookup_request.cc:153).  Timed over contexts per device, pinned and
+    pageable input; checked against one context's pass over the batch."""
+    t0 = time.time()
+    images = [img0] + [img0.replicate(dv) for dv in devices[1:]]
+    t_rep = time.time() - t0
+    c0 = abi.Context(img0)
+    d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
+    abi.check(L.kgx_device_alloc(devices[0], n * Ls, ctypes.byref(d_res)), "alloc")
+    abi.check(L.kgx_device_alloc(devices[0], (n + 1) * 8, ctypes.byref(d_off)), "alloc")
+    abi.check(L.kgx_synth_queries(c0.handle, spec.n_keys, n, Ls, x_permille, 1 << 40, d_res, d_off), "queries")
+    c0.synchronize()
+    pin = abi.pinned_empty(n * Ls)
+    off = np.empty(n + 1, np.uint64)
+    abi.check(L.kgx_memcpy_d2h(pin.ctypes.data, d_res, pin.nbytes), "d2h")
+    abi.check(L.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
+    L.kgx_device_free(d_res)
+    L.kgx_device_free(d_off)
+    pageable = np.array(pin)
+    one = c0.process_batch_compact(pageable, off, params, want=want)
+    one_off = (one.result.hit_offsets.copy(), one.result.call_offsets.copy(), one.result.calls.copy(),
+               one.result.best.copy() if one.result.best is not None else None)
+    rng = np.random.default_rng(5)
+    starts = sorted(set([0, n - 500] + rng.integers(0, n - 500, 12).tolist()))
+    one_hits = {a: one.expand(a, a + 500).tobytes() for a in starts}
+    c0.close()
+    by, checks = {}, {}
+    best_t, best_k = None, None
+    for per_dev in (1, 2, 4, 8):
+        n_ctx = per_dev * len(devices)
+        with abi.Pool(images, n_ctx) as pool:
+            for name, src in (("pinned", pin), ("pageable", pageable)):
+                r = pool.process_batch_compact(src, off, params, want=want)  # warm
+                ts = []
+                for _ in range(5):
+                    t1 = time.perf_counter()
+                    r = pool.process_batch_compact(src, off, params, want=want)
+                    ts.append(time.perf_counter() - t1)
+                t = float(np.median(ts))
+                by[f"{name}_ctx{n_ctx}"] = t * 1e3
+                if name == "pinned" and (best_t is None or t < best_t):
+                    best_t, best_k = t, n_ctx
+                rr = r.result
+                ok = (np.array_equal(rr.hit_offsets, one_off[0]) and np.array_equal(rr.call_offsets, one_off[1])
+                      and rr.calls.tobytes() == one_off[2].tobytes()
+                      and (one_off[3] is None or rr.best.tobytes() == one_off[3].tobytes())
+                      and all(r.expand(a, a + 500).tobytes() == one_hits[a] for a in starts))
+                checks[f"{name}_ctx{n_ctx}"] = bool(ok)
+    for im in images[1:]:
+        im.close()
+    t_pg = min(v for k, v in by.items() if k.startswith("pageable")) / 1e3
+    out = {"value": n * Ls / best_t, "unit": "residues/s", "ms_per_batch": best_t * 1e3, "contexts": best_k,
+           "devices": devices, "value_pageable_input": n * Ls / t_pg, "ms_by_config": by,
+           "match_single_context": all(checks.values()), "checks": checks,
+           "hits": int(one_off[0][-1]), "replicate_s": round(t_rep, 2),
+           "note": "C5: one host batch through kgx_pool_process_batch_compact over one image replica per device "
+                   "(hits as compact records + mask, calls, device best calls back over PCIe), contexts per device "
+                   "swept; value: residues in pinned memory (read by DMA, no staging copy); checked against one "
+                   "context's pass (offsets, calls, best calls, and the expanded hits of 14 slices of 500 "
+                   "sequences, shard cuts included)"}
+    log(f"[bench] pool_e2e {out['value']:.3e} residues/s over {len(devices)} device(s) ({best_k} contexts, "
+        f"{best_t * 1e3:.1f} ms), pageable {out['value_pageable_input']:.3e}; checks "
+        f"{'ok' if out['match_single_context'] else checks}; {by}")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,6 +397,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-microbench", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-lookup", action="store_true", help="skip the host_path_lookup leg")
+    ap.add_argument("--no-pool", action="store_true", help="skip the pool_e2e leg (C5 through kgx_pool)")
+    ap.add_argument("--families", type=int, default=100000, help="family DB size of the host_path_lookup leg")
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts (streams) in flight")
@@ -534,6 +678,22 @@ def main():
         log(f"[bench] host-buffer path {n_res / t_h:.3e} residues/s compact ({t_h * 1e3:.2f} ms/batch), "
             f"{n_res / t_x:.3e} with kgx_hit ({t_x * 1e3:.2f} ms); profiles {profiles}")
 
+    host_path_lookup = None
+    if d.rank == 0 and not args.no_lookup:
+        d_res, d_off = batches[0]
+        res_h = np.empty(n_res, np.uint8)
+        off_h = np.empty(n + 1, np.uint64)
+        abi.check(L.kgx_memcpy_d2h(res_h.ctypes.data, d_res, res_h.nbytes), "d2h")
+        abi.check(L.kgx_memcpy_d2h(off_h.ctypes.data, d_off, off_h.nbytes), "d2h")
+        host_path_lookup = host_path_lookup_leg(abi, synth, img, spec, dev, res_h, off_h, params, args.families)
+
+    pool_e2e = None
+    if d.rank == 0 and not args.no_pool:
+        # one replica per rank's device: the N-GPU run measures C5 over N devices
+        pdevs = [dev] + [i for i in range(n_dev) if i != dev][:d.world - 1]
+        pool_e2e = pool_e2e_leg(abi, L, synth, img, spec, pdevs, params, want, args.strong_seq, Ls,
+                                args.x_permille)
+
     ceiling = None
     if d.rank == 0 and not args.no_microbench:
         ceiling = {}
@@ -679,6 +839,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "host_path": host_path,
+            "host_path_lookup": host_path_lookup,
+            "pool_e2e": pool_e2e,
         }
         print(json.dumps(line), flush=True)
     d.close()

@@ -7,6 +7,7 @@ KGX_EDEVICE when no gfx950 device is visible, and the wrappers raise.
 from __future__ import annotations
 
 import ctypes
+import weakref
 import os
 import re
 
@@ -224,6 +225,9 @@ SIGNATURES = {
     "kgx_kmap_num_values": (_U64, [_P]),
     "kgx_kmap_lookup": (_INT, [_P, _P, _U64, _P, _P, _U64]),
     "kgx_kmap_rollup": (_INT, [_P, _P, _INT, ctypes.POINTER(RollupResult)]),
+    "kgx_kmap_device": (_INT, [_P]),
+    "kgx_pool_lookup": (_INT, [_P, _PP, _U32, _INT, ctypes.POINTER(Params), _P, _P, _U32, _U32,
+                               ctypes.POINTER(Result), ctypes.POINTER(RollupResult)]),
     "kgx_matrix_create": (_INT, [_P, _PP]),
     "kgx_matrix_destroy": (_INT, [_P]),
     "kgx_matrix_add_hits": (_INT, [_P, _P, _P]),
@@ -784,6 +788,20 @@ def shard_cuts(offsets, n_shards: int) -> np.ndarray:
     return cuts
 
 
+def pinned_empty(n: int, dtype=np.uint8) -> np.ndarray:
+    """An uninitialised array in pinned, device-mapped host memory
+    (kgx_host_alloc), freed with the last reference to it.  Residues passed
+    in such memory go to the device by DMA with no staging copy (context
+    option "pinned_input")."""
+    dt = np.dtype(dtype)
+    nbytes = max(1, int(n) * dt.itemsize)
+    p = ctypes.c_void_p()
+    check(lib().kgx_host_alloc(nbytes, ctypes.byref(p)), "kgx_host_alloc")
+    buf = (ctypes.c_char * nbytes).from_address(p.value)
+    weakref.finalize(buf, lib().kgx_host_free, p.value)
+    return np.frombuffer(buf, dtype=dt, count=int(n))
+
+
 class Pool:
     """Contexts over image replicas; one batch split across them (kgx_pool)."""
 
@@ -829,6 +847,18 @@ class Pool:
                                                    offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(cr)),
               "kgx_pool_process_batch_compact")
         return CompactBatch(cr, residues, offsets, want)
+
+    def lookup(self, maps: list, residues, offsets, params: Params | dict | None = None,
+               want: int = WANT_BEST, mode: int = ROLLUP_FAMILY, copy: bool = True):
+        """kgx_pool_lookup: (BatchResult without hits, rollup offsets, rollup rows)."""
+        residues, offsets, params = _batch_args(residues, offsets, params)
+        hs = (ctypes.c_void_p * len(maps))(*[m.handle for m in maps])
+        r, ru = Result(), RollupResult()
+        check(lib().kgx_pool_lookup(self.handle, hs, len(maps), mode, ctypes.byref(params),
+                                    residues.ctypes.data if residues.size else None, offsets.ctypes.data,
+                                    len(offsets) - 1, want, ctypes.byref(r), ctypes.byref(ru)), "kgx_pool_lookup")
+        off = _view(ru.offsets, ru.n_seq + 1, np.uint64, copy)
+        return BatchResult(r, want, copy), off, _view(ru.rows, int(off[-1]) if len(off) else 0, ROLLUP_DTYPE, copy)
 
     def close(self) -> None:
         if self.handle:

@@ -290,6 +290,8 @@ hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *
  * both 16-byte aligned */
 hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count, uint64_t cap,
                                uint32_t elem_bytes, int blocks, hipStream_t stream);
+/* *flag_mapped = 1 when a byte of d[0, n) is 0 (d 16-byte aligned) */
+hipError_t launch_nul_scan(const uint8_t *d, uint64_t n, uint32_t *flag_mapped, hipStream_t stream);
 /* device stores of bytes (4-aligned) from HBM into mapped pinned host memory */
 hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,

@@ -2301,6 +2301,40 @@ hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count
     return hipGetLastError();
 }
 
+/* any NUL among bytes [0, n) of d -> *flag = 1 (a store into mapped host
+ * memory).  Residues the device reads straight from the caller's pinned
+ * buffer are not NUL-cut on the host (gather_hits' strlen bound, kguts.cc:792),
+ * so the host path checks them here and reruns a batch that has one. */
+__global__ __launch_bounds__(256) void nul_scan_kernel(const uint4 *__restrict__ d, uint64_t n, uint32_t *flag)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n16 = n / 16;
+    bool nul = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        const uint4 v = d[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4; j++)
+            nul |= ((w[j] - 0x01010101u) & ~w[j] & 0x80808080u) != 0;
+    }
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid < n - 16 * n16)
+        nul |= reinterpret_cast<const uint8_t *>(d)[16 * n16 + tid] == 0;
+    if (__ballot(nul) && lane_id() == 0)
+        __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_nul_scan(const uint8_t *d, uint64_t n, uint32_t *flag_mapped, hipStream_t stream)
+{
+    if (n == 0)
+        return hipSuccess;
+    if ((uintptr_t)d % 16 != 0)
+        return hipErrorInvalidValue;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n / 16 + 255) / 256 + 1, 1024);
+    hipLaunchKernelGGL(nul_scan_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const uint4 *>(d), n,
+                       flag_mapped);
+    return hipGetLastError();
+}
+
 /* ------------------------------------------------------------------------ */
 /* copy to mapped pinned host memory: the device's own stores stream the     */
 /* results over PCIe (one contiguous 1-KB run per wave instruction), so the */

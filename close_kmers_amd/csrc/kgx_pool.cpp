@@ -21,9 +21,36 @@
 #include <thread>
 #include <vector>
 
+#include <cstdio>
+
+#include <sched.h>
+
 #include "kgx_rt.h"
 
 using namespace kgx;
+
+unsigned kgx::host_cpu_budget()
+{
+    static const unsigned budget = [] {
+        cpu_set_t set;
+        unsigned n = 0;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0)
+            n = (unsigned)CPU_COUNT(&set);
+        if (n == 0)
+            n = std::max(1u, std::thread::hardware_concurrency());
+        if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[64] = {0};
+            unsigned long long period = 0;
+            if (std::fscanf(f, "%63s %llu", q, &period) == 2 && std::string(q) != "max" && period) {
+                const unsigned long long quota = std::strtoull(q, nullptr, 10);
+                n = std::min<unsigned>(n, (unsigned)std::max<unsigned long long>(1, quota / period));
+            }
+            std::fclose(f);
+        }
+        return n;
+    }();
+    return budget;
+}
 
 struct kgx_pool {
     std::vector<kgx_ctx *> ctxs;
@@ -47,6 +74,8 @@ struct kgx_pool {
     std::vector<kgx_call> calls;
     std::vector<kgx_otu> otus;
     std::vector<kgx_best_call> best;
+    std::vector<uint64_t> roff; /* kgx_pool_lookup's rollup rows */
+    std::vector<kgx_rollup_row> rows;
 
     void worker(uint32_t i)
     {
@@ -125,6 +154,16 @@ int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx,
         }
         p->ctxs.push_back(c);
     }
+    /* the contexts' host threads share the process's CPUs: staging and
+     * expansion threads per context sized so the pool keeps about as many
+     * busy as there are CPUs (8 contexts x 8 stagers on a 16-CPU share ran
+     * slower than 2 contexts, r4x_bench_pool) */
+    const unsigned cpus = host_cpu_budget();
+    for (kgx_ctx *c : p->ctxs) {
+        c->stage_threads = (int)std::max(1u, std::min<unsigned>((unsigned)c->stage_threads, cpus / n_ctx));
+        c->host_threads = (int)std::max(1u, std::min<unsigned>((unsigned)c->host_threads, cpus / n_ctx));
+    }
+    p->expand_threads = std::max(1u, std::min(p->expand_threads, cpus));
     if (const char *e = std::getenv("KGX_POOL_EXPAND_THREADS"))
         p->expand_threads = (unsigned)std::min(256L, std::max(1L, std::strtol(e, nullptr, 10)));
     for (uint32_t i = 0; i < n_ctx; i++)
@@ -343,6 +382,107 @@ int kgx_pool_process_batch_compact(kgx_pool *p, const kgx_params *params, const 
         }
     out->n_chunks = (uint32_t)p->chunks.size();
     out->chunks = p->chunks.data();
+    return KGX_OK;
+}
+
+int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mode, const kgx_params *params,
+                    const char *residues, const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                    kgx_result *out, kgx_rollup_result *rollup)
+{
+    if (!p || !out || !rollup || !maps || n_maps == 0 || (!seq_offsets && n_seq))
+        return fail(KGX_EINVAL, "null argument");
+    if (want & (KGX_WANT_HITS | KGX_WANT_OTU))
+        return fail(KGX_EINVAL, "pool lookup: want within KGX_WANT_CALLS | KGX_WANT_BEST (the hits stay on the device)");
+    for (uint32_t s = 0; s < n_seq; s++)
+        if (seq_offsets[s + 1] < seq_offsets[s])
+            return fail(KGX_EINVAL, "seq_offsets not monotone");
+    /* each context's map: the one on its device */
+    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)p->ctxs.size(), n_seq));
+    std::vector<kgx_kmap *> mine(K, nullptr);
+    for (uint32_t i = 0; i < K; i++) {
+        for (uint32_t j = 0; j < n_maps && !mine[i]; j++)
+            if (maps[j] && kgx_kmap_device(maps[j]) == kgx_image_device(p->ctxs[i]->img))
+                mine[i] = maps[j];
+        if (!mine[i])
+            return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(kgx_image_device(p->ctxs[i]->img)));
+    }
+    std::vector<uint32_t> cuts(K + 1, 0);
+    int rc = kgx_shard_cuts(seq_offsets, n_seq, K, cuts.data());
+    if (rc)
+        return rc;
+    /* every shard is ONE pass on its context (its hits stay on the device
+     * for the rollup: host_chunks 1 for the call), then its rollups */
+    std::vector<kgx_result> part(K, kgx_result{});
+    std::vector<kgx_rollup_result> ru(K, kgx_rollup_result{});
+    std::vector<int> rcs(K, KGX_OK);
+    std::vector<std::string> errs(K);
+    p->run(K, [&](uint32_t i) {
+        kgx_ctx *c = p->ctxs[i];
+        const int chunks = c->host_chunks, sv = c->score_variant;
+        c->host_chunks = 1;
+        /* a shard's sequences on the host path's scorer (option
+         * host_score_variant: the wave scorer; the lane scorer's longest chain
+         * sets a shard's score time whatever its size) */
+        if (c->host_score_variant >= 0)
+            c->score_variant = c->host_score_variant;
+        rcs[i] = kgx_process_batch(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want, &part[i]);
+        c->host_chunks = chunks;
+        c->score_variant = sv;
+        if (!rcs[i])
+            rcs[i] = kgx_kmap_rollup(mine[i], c, mode, &ru[i]);
+        if (rcs[i])
+            errs[i] = kgx_last_error();
+    });
+    for (uint32_t i = 0; i < K; i++)
+        if (rcs[i])
+            return fail(rcs[i], "pool lookup shard " + std::to_string(i) + ": " + errs[i]);
+    /* concatenation in input order: offsets, calls, best calls, rows */
+    std::vector<uint64_t> hb(K + 1, 0), cb(K + 1, 0), rb(K + 1, 0);
+    uint64_t nwin = 0, nev = 0;
+    for (uint32_t i = 0; i < K; i++) {
+        const uint32_t n = cuts[i + 1] - cuts[i];
+        hb[i + 1] = hb[i] + part[i].hit_offsets[n];
+        cb[i + 1] = cb[i] + part[i].call_offsets[n];
+        rb[i + 1] = rb[i] + ru[i].offsets[n];
+        nwin += part[i].n_windows;
+        nev += ru[i].n_events;
+    }
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    p->hoff.resize((size_t)n_seq + 1);
+    p->coff.resize((size_t)n_seq + 1);
+    p->ooff.assign((size_t)n_seq + 1, 0);
+    p->roff.resize((size_t)n_seq + 1);
+    p->hoff[0] = p->coff[0] = p->roff[0] = 0;
+    p->calls.resize(cb[K]);
+    p->best.resize(want_best ? n_seq : 0);
+    p->rows.resize(rb[K]);
+    p->run(K, [&](uint32_t i) {
+        const uint32_t s0 = cuts[i], n = cuts[i + 1] - cuts[i];
+        for (uint32_t s = 1; s <= n; s++) {
+            p->hoff[s0 + s] = hb[i] + part[i].hit_offsets[s];
+            p->coff[s0 + s] = cb[i] + part[i].call_offsets[s];
+            p->roff[s0 + s] = rb[i] + ru[i].offsets[s];
+        }
+        if (cb[i + 1] > cb[i])
+            std::memcpy(p->calls.data() + cb[i], part[i].calls, (cb[i + 1] - cb[i]) * sizeof(kgx_call));
+        if (rb[i + 1] > rb[i])
+            std::memcpy(p->rows.data() + rb[i], ru[i].rows, (rb[i + 1] - rb[i]) * sizeof(kgx_rollup_row));
+        if (want_best && n)
+            std::memcpy(p->best.data() + s0, part[i].best, n * sizeof(kgx_best_call));
+    });
+    out->n_seq = n_seq;
+    out->hit_offsets = p->hoff.data();
+    out->hits = nullptr;
+    out->call_offsets = p->coff.data();
+    out->calls = p->calls.data();
+    out->otu_offsets = p->ooff.data();
+    out->otus = nullptr;
+    out->n_windows = nwin;
+    out->best = want_best ? p->best.data() : nullptr;
+    rollup->n_seq = n_seq;
+    rollup->offsets = p->roff.data();
+    rollup->rows = p->rows.data();
+    rollup->n_events = nev;
     return KGX_OK;
 }
 

@@ -135,6 +135,11 @@ template <class T> struct PinnedVec {
 
 inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 
+/* host CPUs this process may keep busy: the affinity mask, capped by a
+ * cgroup v2 quota (cpu.max) -- on the GPU box the mask shows the whole
+ * machine while the quota is 16 */
+unsigned host_cpu_budget();
+
 /* memcpy by up to 8 host threads for large copies (host staging into pinned
  * buffers runs at several times one core's copy rate) */
 inline void parallel_memcpy(void *dst, const void *src, size_t n)
@@ -430,6 +435,14 @@ struct kgx_ctx {
     int host_taper = 1; /* first and last chunk half-size (option "host_taper") */
     double rate_hits = 0.35, rate_calls = 0.05, rate_otus = 0.05;
     uint64_t stream_fallbacks = 0; /* batches rerun exact after a region overflowed */
+    /* option "pinned_input" (default 1): a streamed host batch whose residues
+     * already sit in pinned memory (kgx_host_alloc, hipHostMalloc /
+     * hipHostRegister) goes to the device by DMA straight from the caller's
+     * buffer, with no staging copy on the host; a device scan flags NUL bytes
+     * (the host-side strlen cut, kguts.cc:792) and such a batch reruns staged */
+    int pinned_input = 1;
+    uint64_t pinned_batches = 0, nul_reruns = 0;
+    kgx::PinnedVec<uint32_t> h_nul;
     std::vector<hipEvent_t> chunk_h2d; /* per chunk: its staged residues are on the device */
     kgx::DevBuf dense_counts, cscan_ws;
     kgx::PinnedVec<uint32_t> h_counts;

@@ -966,6 +966,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->host_stream_dma = (int)value;
         return KGX_OK;
     }
+    if (n == "pinned_input") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "pinned_input must be 0 or 1");
+        c->pinned_input = (int)value;
+        return KGX_OK;
+    }
     if (n == "host_stage_all") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "host_stage_all must be 0 or 1");
@@ -1479,6 +1485,31 @@ void cut_at_nul(char *b, uint64_t len)
     }
 }
 
+/* [p, p + n) lies in one pinned, device-mapped host allocation */
+bool host_pinned_range(const void *p, uint64_t n)
+{
+    if (!p || n == 0)
+        return false;
+    hipPointerAttribute_t a{}, b{};
+    const char *first = static_cast<const char *>(p), *last = first + n - 1;
+    if (hipPointerGetAttributes(&a, first) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer ||
+        hipPointerGetAttributes(&b, last) != hipSuccess || b.type != hipMemoryTypeHost || !b.devicePointer) {
+        (void)hipGetLastError(); /* an unregistered pointer is not an error here */
+        return false;
+    }
+    return static_cast<const char *>(b.devicePointer) - static_cast<const char *>(a.devicePointer) ==
+           (std::ptrdiff_t)(n - 1);
+}
+
+/* the n + 1 chunk-relative offsets of sequences [s0, s1) */
+void stage_offsets_into(uint64_t *off, const uint64_t *seq_offsets, uint32_t s0, uint32_t s1)
+{
+    const uint32_t n = s1 - s0;
+    const uint64_t r0 = n ? seq_offsets[s0] : 0;
+    for (uint32_t i = 0; i <= n; i++)
+        off[i] = n ? seq_offsets[s0 + i] - r0 : 0;
+}
+
 /* sequences [s0, s1) of a host batch -> pinned staging at dst (residues) and
  * off (the n + 1 chunk-relative offsets); host work only, large ranges copied
  * and NUL-scanned in parts on the stage pool sp */
@@ -1533,10 +1564,10 @@ int stage_upload(kgx_ctx *x)
     const uint64_t n_res = x->h_res.size(), n1 = x->h_off_stage.size();
     HIP_TRY(x->residues.reserve(n_res + 16));
     HIP_TRY(x->offsets.reserve(n1 * sizeof(uint64_t)));
-    if (n_res)
-        HIP_TRY(hipMemcpyAsync(x->residues.p, x->h_res.data(), n_res, hipMemcpyHostToDevice, x->stream));
     HIP_TRY(hipMemcpyAsync(x->offsets.p, x->h_off_stage.data(), n1 * sizeof(uint64_t), hipMemcpyHostToDevice,
                            x->stream));
+    if (n_res)
+        HIP_TRY(hipMemcpyAsync(x->residues.p, x->h_res.data(), n_res, hipMemcpyHostToDevice, x->stream));
     return KGX_OK;
 }
 
@@ -1740,6 +1771,7 @@ int expand_hits(bool R12, kgx_ctx *c, const char *residues, const uint64_t *seq_
  * fit its region makes the call return STREAM_OVERFLOW after raising the rates;
  * the caller reruns the batch on the exact (host round trip) path. */
 constexpr int STREAM_OVERFLOW = 1; /* internal: a region overflowed, rerun exact */
+constexpr int STREAM_NUL = 2;      /* internal: the caller's pinned residues hold a NUL, rerun staged */
 
 int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
                            uint32_t n_seq, uint32_t want, uint32_t K, const std::vector<uint32_t> &cut,
@@ -1865,7 +1897,21 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         HIP_TRY(c->h_res_all.resize(std::max<uint64_t>(res_at[K], 256)));
         HIP_TRY(c->h_off_all.resize(std::max<uint64_t>(off_at[K], 2)));
     }
+    /* caller-pinned residues: no staging copy, a device NUL scan instead */
+    const uint64_t all_res = n_seq ? seq_offsets[n_seq] - seq_offsets[0] : 0;
+    const bool pin = c->pinned_input && host_pinned_range(residues + (n_seq ? seq_offsets[0] : 0), all_res);
+    uint32_t *d_nul = nullptr;
+    if (pin) {
+        HIP_TRY(c->h_nul.resize(1));
+        c->h_nul[0] = 0;
+        void *dn = nullptr;
+        HIP_TRY(c->h_nul.device_ptr(0, &dn));
+        d_nul = static_cast<uint32_t *>(dn);
+        c->pinned_batches++;
+    }
     auto staged_res = [&](kgx_ctx *x, uint32_t k) -> const char * {
+        if (pin)
+            return residues + seq_offsets[cut[k]];
         return sall ? c->h_res_all.data() + res_at[k] : x->h_res.data();
     };
     auto staged_off = [&](kgx_ctx *x, uint32_t k) -> const uint64_t * {
@@ -1887,20 +1933,22 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         if (up) {
             uint8_t *rd = c->up_res.as<uint8_t>() + res_at[k];
             uint64_t *od = c->up_off.as<uint64_t>() + off_at[k];
+            HIP_TRY(hipMemcpyAsync(od, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
             if (n_res)
                 HIP_TRY(hipMemcpyAsync(rd, hres, n_res, hipMemcpyHostToDevice, us));
-            HIP_TRY(hipMemcpyAsync(od, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
             d_res = rd;
             d_off = od;
         } else {
             /* reserved for the largest chunk above: no reallocation here */
             HIP_TRY(x->residues.reserve(n_res + 16));
             HIP_TRY(x->offsets.reserve((n + 1) * sizeof(uint64_t)));
+            HIP_TRY(hipMemcpyAsync(x->offsets.p, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
             if (n_res)
                 HIP_TRY(hipMemcpyAsync(x->residues.p, hres, n_res, hipMemcpyHostToDevice, us));
-            HIP_TRY(hipMemcpyAsync(x->offsets.p, hoff, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, us));
         }
         HIP_TRY(hipEventRecord(c->chunk_h2d[k], us));
+        if (pin)
+            HIP_TRY(launch_nul_scan(d_res, n_res, d_nul, us));
         if (prof)
             HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 1], us));
         if (up)
@@ -2115,7 +2163,14 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         if (k >= 2 && !sall)
             HIP_TRY(hipEventSynchronize(c->chunk_h2d[k - 2])); /* x's staging buffer is free */
         const auto ts = now();
-        if (sall)
+        if (pin && sall)
+            stage_offsets_into(c->h_off_all.data() + off_at[k], seq_offsets, cut[k], cut[k + 1]);
+        else if (pin) {
+            if (x->h_off_stage.resize(cut[k + 1] - cut[k] + 1) != hipSuccess)
+                rc = fail(KGX_ENOMEM, "pinned staging");
+            else
+                stage_offsets_into(x->h_off_stage.data(), seq_offsets, cut[k], cut[k + 1]);
+        } else if (sall)
             stage_copy_into(c->h_res_all.data() + res_at[k], c->h_off_all.data() + off_at[k], residues, seq_offsets,
                             cut[k], cut[k + 1], sp);
         else
@@ -2165,6 +2220,8 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
     HIP_TRY(e2);
     if (prc)
         return prc;
+    if (pin && __atomic_load_n(&c->h_nul[0], __ATOMIC_ACQUIRE))
+        return STREAM_NUL;
     /* the rates the next batch's regions are sized by */
     c->rate_hits = std::max(0.02, max_rh * 1.25);
     c->rate_calls = std::max(0.01, max_rc * 1.25);
@@ -2352,9 +2409,12 @@ int process_batch_chunked(kgx_ctx *c, const kgx_params *params, const char *resi
             const int src = process_batch_streamed(c, params, residues, seq_offsets, n_seq, want, K, cut, out);
             c->score_variant = sv_c;
             t->score_variant = sv_t;
-            if (src != STREAM_OVERFLOW)
+            if (src != STREAM_OVERFLOW && src != STREAM_NUL)
                 return src;
-            /* a region overflowed: the rates are raised; this batch runs exact */
+            /* a region overflowed (the rates are raised), or the caller's
+             * pinned residues hold a NUL: this batch runs exact, staged */
+            if (src == STREAM_NUL)
+                c->nul_reruns++;
             c->h_hoff.assign(n_seq + 1, 0);
             c->h_coff.assign(n_seq + 1, 0);
             c->h_ooff.assign(n_seq + 1, 0);
@@ -2924,6 +2984,76 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     return KGX_OK;
 }
 
+/* One pass over the whole host batch (its results stay on the device for
+ * kgx_kmap_rollup / kgx_kmap_add_hits / kgx_matrix_add_hits).  Residues in
+ * the caller's pinned memory go up by DMA straight from there (option
+ * "pinned_input"; a NUL among them reruns the batch staged, cut at the NUL);
+ * others are staged into pinned memory on the stage pool's threads. */
+int process_batch_one_pass(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                           uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    const uint64_t r0 = n_seq ? seq_offsets[0] : 0, n_res = n_seq ? seq_offsets[n_seq] - r0 : 0;
+    const bool pin = c->pinned_input && host_pinned_range(residues + r0, n_res);
+    PhaseTimer tm(c);
+    if (pin) {
+        HIP_TRY(c->h_off_stage.resize(n_seq + 1));
+        stage_offsets_into(c->h_off_stage.data(), seq_offsets, 0, n_seq);
+        HIP_TRY(c->h_nul.resize(1));
+        c->h_nul[0] = 0;
+        void *dn = nullptr;
+        HIP_TRY(c->h_nul.device_ptr(0, &dn));
+        HIP_TRY(c->residues.reserve(n_res + 16));
+        HIP_TRY(c->offsets.reserve((n_seq + 1) * sizeof(uint64_t)));
+        /* the small copy first: copies from all streams share the DMA engine
+         * in order, and a context's kernels need both */
+        HIP_TRY(hipMemcpyAsync(c->offsets.p, c->h_off_stage.data(), (n_seq + 1) * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->residues.p, residues + r0, n_res, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(launch_nul_scan(c->residues.as<uint8_t>(), n_res, static_cast<uint32_t *>(dn), c->stream));
+        c->pinned_batches++;
+    } else {
+        HostPool *sp = nullptr;
+        if (c->stage_threads > 1 && n_res >= (1u << 20)) {
+            if (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads)
+                c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
+            sp = c->stage_pool.get();
+        }
+        int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq, sp);
+        if (rc || (rc = stage_upload(c)))
+            return rc;
+    }
+    tm.mark("stage");
+    /* on the wave scorer, the host knows whether any sequence needs the lane
+     * machine's long-sequence pass (score_long): usually none does */
+    struct VariantGuard {
+        kgx_ctx *c;
+        int v;
+        ~VariantGuard() { c->score_variant = v; }
+    } vg{c, c->score_variant};
+    if (c->score_variant == SCORE_WAVE) {
+        uint64_t longest = 0;
+        for (uint32_t s = 0; s < n_seq; s++)
+            longest = std::max(longest, seq_offsets[s + 1] - seq_offsets[s]);
+        if (windows_of(longest) <= (uint64_t)RUN_CAP)
+            c->score_variant = SCORE_WAVE_ONLY;
+    }
+    int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq, n_res, want,
+                            nullptr);
+    if (rc)
+        return rc;
+    tm.mark("device");
+    rc = kgx_device_batch_collect(c, want, out);
+    tm.mark("collect");
+    if (!rc && pin && __atomic_load_n(&c->h_nul[0], __ATOMIC_ACQUIRE)) {
+        /* a NUL in the caller's residues: again, staged and cut */
+        c->nul_reruns++;
+        c->pinned_input = 0;
+        rc = process_batch_one_pass(c, params, residues, seq_offsets, n_seq, want, out);
+        c->pinned_input = 1;
+    }
+    return rc;
+}
+
 }  // namespace
 
 int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues,
@@ -2957,19 +3087,7 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
         c->small_batches++;
         return process_batch_small(c, params, residues, seq_offsets, n_seq, want, out);
     }
-    PhaseTimer tm(c);
-    int rc = stage_host_seqs(c, residues, seq_offsets, 0, n_seq);
-    if (rc)
-        return rc;
-    tm.mark("stage");
-    rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq, n_res, want,
-                        nullptr);
-    if (rc)
-        return rc;
-    tm.mark("device");
-    rc = kgx_device_batch_collect(c, want, out);
-    tm.mark("collect");
-    return rc;
+    return process_batch_one_pass(c, params, residues, seq_offsets, n_seq, want, out);
 }
 
 int kgx_process_batch_compact(kgx_ctx *c, const kgx_params *params, const char *residues,
@@ -3077,6 +3195,10 @@ int kgx_ctx_stat(kgx_ctx *c, const char *name, int64_t *value)
         *value = (int64_t)c->small_batches;
     else if (n == "stream_fallbacks")
         *value = (int64_t)c->stream_fallbacks;
+    else if (n == "pinned_batches")
+        *value = (int64_t)c->pinned_batches;
+    else if (n == "nul_reruns")
+        *value = (int64_t)c->nul_reruns;
     else
         return fail(KGX_EINVAL, "unknown statistic " + n);
     return KGX_OK;

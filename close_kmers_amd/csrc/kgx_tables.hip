@@ -18,6 +18,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <memory>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -75,10 +76,29 @@ struct KmapView {
     uint64_t hmask = 0;
     const uint64_t *starts = nullptr; /* rows + 1 */
     const uint32_t *vals = nullptr;
+    /* the index again, one 16-B slot per bucket: {k-mer lo, hi, list start,
+     * list length} -- one random read per probe step instead of three
+     * dependent ones (key, row, starts); built when every start fits 32 bits */
+    const uint4 *slots = nullptr;
 };
 
 __device__ __forceinline__ bool kmap_row(const KmapView &m, uint64_t kmer, uint64_t &a, uint64_t &b)
 {
+    if (m.slots) {
+        uint64_t h = hslot(kmer, m.hmask);
+        for (;;) {
+            const uint4 e = m.slots[h];
+            const uint64_t k = (uint64_t)e.y << 32 | e.x;
+            if (k == kmer) {
+                a = e.z;
+                b = (uint64_t)e.z + e.w;
+                return true;
+            }
+            if (k == EMPTY64)
+                return false;
+            h = (h + 1) & m.hmask;
+        }
+    }
     if (!m.hkeys)
         return false;
     const int64_t s = find(m.hkeys, m.hmask, kmer);
@@ -214,6 +234,23 @@ __global__ void row_heads_kernel(const uint64_t *k, uint64_t n, uint8_t *head)
         head[i] = (i == 0 || k[i] != k[i - 1]);
 }
 
+/* the 16-B index slots from the built index (n_vals < 2^32) */
+__global__ void index_slots_kernel(const uint64_t *hkeys, const uint32_t *hrow, const uint64_t *starts, uint64_t cap,
+                                   uint4 *slots)
+{
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap)
+        return;
+    const uint64_t k = hkeys[s];
+    if (k == EMPTY64) {
+        slots[s] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+        return;
+    }
+    const uint32_t r = hrow[s];
+    const uint64_t a = starts[r], b = starts[r + 1];
+    slots[s] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)a, (uint32_t)(b - a));
+}
+
 __global__ void index_insert_kernel(const uint64_t *keys, uint64_t n, uint64_t *hkeys, uint32_t *hrow,
                                     uint64_t mask)
 {
@@ -254,78 +291,155 @@ __global__ void lookup_ids_kernel(KmapView m, const uint64_t *kmers, uint64_t n,
  * group's f32 sum taken in sorted order is the reference's sum in hit order,
  * and its first event number is when the reference first touched the id. */
 
-/* per tiled hit slot (tile * T + i): its sequence, list start and length
- * (0 for slots past the tile's hits and for unmapped k-mers); slot n_slots
- * gets length 0, the scan's last element */
-__global__ void rollup_hits_kernel(Tiled t, uint64_t n_tiles, KmapView m, uint32_t *hseq, uint64_t *hstart,
-                                   uint64_t *hlen)
+/* Pass 1, one wave per tile: for each of the tile's hits (slot tile * T + i,
+ * i its rank in the tile's mask words) its sequence, list start and length
+ * (0 for an unmapped k-mer); the tile's event total.  A lane takes the hit
+ * whose window is its bit of the mask word, so no lane walks the bits.
+ * Block tile n_tiles writes the scan's last element, 0. */
+__global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_tiles, KmapView m, uint32_t *hseq,
+                                                           uint64_t *hstart, uint32_t *hlen, uint64_t *tcount)
 {
-    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t n_slots = n_tiles * t.T;
-    if (slot > n_slots)
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = lane_id();
+    if (tile >= n_tiles) {
+        if (tile == n_tiles && lane == 0)
+            tcount[n_tiles] = 0;
         return;
-    uint64_t len = 0;
-    if (slot < n_slots) {
-        const uint64_t tile = slot / t.T;
-        const uint32_t i = (uint32_t)(slot % t.T);
-        if (i < tile_count(t, tile)) {
-            uint64_t key, a = 0, b = 0;
-            uint32_t seq;
-            hit_key_seq(t, tile, i, key, seq);
-            if (kmap_row(m, key, a, b)) {
-                len = b - a;
-                hseq[slot] = seq;
-                hstart[slot] = a;
-            }
-        }
     }
-    hlen[slot] = len;
+    const uint32_t J = t.T / 64;
+    const uint64_t W = t.wbase[t.n_seq];
+    uint32_t base = 0;
+    uint64_t ev = 0;
+    for (uint32_t j = 0; j < J; j++) {
+        const uint64_t w0 = 64 * (tile * J + j);
+        const uint64_t mw = w0 < W ? t.mask[tile * J + j] : 0ull;
+        if ((mw >> lane) & 1ull) {
+            const uint64_t slot = tile * t.T + base + lanes_below(mw);
+            uint64_t key;
+            uint32_t seq;
+            if (t.packed) {
+                key = HitFields<true>::key(t.hot[slot], t.hot[slot]);
+                seq = window_seq(t.wbase, t.tile_seq, tile, w0 + lane);
+            } else {
+                const uint4 h = t.cold[slot];
+                key = (uint64_t)h.y << 32 | h.x;
+                seq = h.w;
+            }
+            uint64_t a = 0, b = 0;
+            const uint64_t len = kmap_row(m, key, a, b) ? b - a : 0;
+            hseq[slot] = seq;
+            hstart[slot] = a;
+            hlen[slot] = (uint32_t)len;
+            ev += len;
+        }
+        base += (uint32_t)__popcll(mw);
+    }
+    for (int o = 32; o > 0; o >>= 1)
+        ev += __shfl_xor(ev, o);
+    if (lane == 0)
+        tcount[tile] = ev;
 }
 
-/* the events of every slot with a list: key = sequence << ib | id, the event
- * number, and the hit's weight 1.0f / (float)|list| (lookup_request.cc:459) */
-__global__ void rollup_expand_kernel(uint64_t n_slots, const uint32_t *hseq, const uint64_t *hstart,
-                                     const uint64_t *hlen, const uint64_t *eoff, const uint32_t *vals, uint32_t ib,
-                                     uint64_t *key, uint32_t *idx, float *ew)
+/* Pass 2, one wave per tile: the events of its hits, numbered from the
+ * tile's scanned base in hit order, then list order: key = sequence << ib |
+ * id, the event number, and the hit's weight 1.0f / (float)|list|
+ * (lookup_request.cc:459) */
+template <typename K>
+__global__ __launch_bounds__(256) void rollup_events_kernel(Tiled t, uint64_t n_tiles, const uint32_t *hseq,
+                                                            const uint64_t *hstart, const uint32_t *hlen,
+                                                            const uint64_t *tbase, const uint32_t *vals, uint32_t ib,
+                                                            K *key, uint32_t *idx, float *ew)
 {
-    const uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= n_slots)
+    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= n_tiles)
         return;
-    const uint64_t len = hlen[slot];
-    if (len == 0)
+    uint64_t e0 = tbase[tile];
+    if (tbase[tile + 1] == e0)
         return;
-    const uint64_t e0 = eoff[slot], a = hstart[slot], hi = (uint64_t)hseq[slot] << ib;
-    const float w = 1.0f / (float)len;
-    for (uint64_t j = 0; j < len; j++) {
-        key[e0 + j] = hi | vals[a + j];
-        idx[e0 + j] = (uint32_t)(e0 + j);
-        ew[e0 + j] = w;
+    const uint32_t lane = lane_id();
+    const uint32_t J = t.T / 64;
+    const uint64_t W = t.wbase[t.n_seq];
+    uint32_t base = 0;
+    for (uint32_t j = 0; j < J; j++) {
+        const uint64_t w0 = 64 * (tile * J + j);
+        const uint64_t mw = w0 < W ? t.mask[tile * J + j] : 0ull;
+        if (!mw)
+            continue;
+        uint64_t len = 0, a = 0;
+        uint32_t seq = 0;
+        if ((mw >> lane) & 1ull) {
+            const uint64_t slot = tile * t.T + base + lanes_below(mw);
+            len = hlen[slot];
+            a = hstart[slot];
+            seq = hseq[slot];
+        }
+        uint64_t incl = len;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t v = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o)
+                incl += v;
+        }
+        const uint64_t e = e0 + incl - len;
+        if (len) {
+            const float w = 1.0f / (float)len;
+            const K hi = (K)seq << ib;
+            for (uint64_t q = 0; q < len; q++) {
+                key[e + q] = hi | (K)vals[a + q];
+                idx[e + q] = (uint32_t)(e + q);
+                ew[e + q] = w;
+            }
+        }
+        e0 += __shfl(incl, 63);
+        base += (uint32_t)__popcll(mw);
     }
 }
 
 /* one thread per (sequence, id) group, at its first sorted event: the
- * group's counts and its weights summed in event order, stored at the first
- * event's number (flagged), and one more row for its sequence */
-__global__ void rollup_groups_kernel(uint64_t n_ev, const uint64_t *key, const uint32_t *idx, const float *ew,
-                                     uint32_t ib, int family, uint8_t *flag, uint4 *rowdata, uint32_t *rowcnt)
+ * group's counts and its weights summed in event order (8 events' loads in
+ * flight at a time, the adds strictly in order), stored at the first event's
+ * number (flagged), and one more row for its sequence */
+template <typename K>
+__global__ void rollup_groups_kernel(uint64_t n_ev, const K *key, const uint32_t *idx, const float *ew, uint32_t ib,
+                                     int family, uint8_t *flag, uint4 *rowdata, uint32_t *rowcnt)
 {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_ev)
         return;
-    const uint64_t k = key[p];
+    const K k = key[p];
     if (p > 0 && key[p - 1] == k)
         return;
     uint32_t cnt = 0;
     float ws = 0.0f;
-    for (uint64_t q = p; q < n_ev && key[q] == k; q++) {
-        ws += ew[idx[q]]; /* s.weighted_total += weight, hit by hit */
-        cnt++;
+    for (uint64_t q = p;; q += 8) {
+        K kk[8];
+        uint32_t ii[8];
+        float ww[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint64_t r = q + u < n_ev ? q + u : n_ev - 1; /* clamped: every load is issued */
+            kk[u] = key[r];
+            ii[u] = idx[r];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            ww[u] = ew[ii[u]];
+        bool more = true;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            more = more && q + u < n_ev && kk[u] == k;
+            if (more) {
+                ws += ww[u]; /* s.weighted_total += weight, hit by hit */
+                cnt++;
+            }
+        }
+        if (!more)
+            break;
     }
     const uint32_t first = idx[p];
-    const uint32_t id = (uint32_t)(k & ((1ull << ib) - 1));
+    const uint32_t id = (uint32_t)((uint64_t)k & ((1ull << ib) - 1));
     flag[first] = 1;
     rowdata[first] = family ? make_uint4(id, cnt, cnt, __float_as_uint(ws)) : make_uint4(id, cnt, 0u, 0u);
-    atomicAdd(rowcnt + (k >> ib), 1u);
+    atomicAdd(rowcnt + (uint32_t)((uint64_t)k >> ib), 1u);
 }
 
 /* --- /matrix --- */
@@ -505,7 +619,7 @@ struct kgx_kmap {
     hipStream_t stream = nullptr;
     uint64_t n_rows = 0, n_vals = 0, hcap = 0;
     uint32_t max_id = 0; /* the largest id added (kgx_kmap_rollup's key width) */
-    DevBuf keys, starts, vals, hkeys, hrow;
+    DevBuf keys, starts, vals, hkeys, hrow, slots;
     std::mutex scratch_mu;
     std::vector<std::unique_ptr<KmapScratch>> scratch_free;
     KmapView view() const
@@ -515,6 +629,7 @@ struct kgx_kmap {
             v.hkeys = hkeys.as<uint64_t>();
             v.hrow = hrow.as<uint32_t>();
             v.hmask = hcap - 1;
+            v.slots = slots.p ? slots.as<uint4>() : nullptr;
             v.starts = starts.as<uint64_t>();
             v.vals = vals.as<uint32_t>();
         }
@@ -627,6 +742,13 @@ int kmap_rebuild(kgx_kmap *m, DevBuf &d_k, DevBuf &d_v, uint64_t n, hipStream_t 
     HIP_TRY(hipMemsetAsync(m->hkeys.p, 0xFF, cap * 8, st));
     hipLaunchKernelGGL(index_insert_kernel, grid_for(rows), dim3(256), 0, st, m->keys.as<uint64_t>(), rows,
                        m->hkeys.as<uint64_t>(), m->hrow.as<uint32_t>(), cap - 1);
+    if (n < (1ull << 32)) {
+        HIP_TRY(m->slots.reserve(cap * 16));
+        hipLaunchKernelGGL(index_slots_kernel, grid_for(cap), dim3(256), 0, st, m->hkeys.as<uint64_t>(),
+                           m->hrow.as<uint32_t>(), m->starts.as<uint64_t>(), cap, m->slots.as<uint4>());
+    } else {
+        m->slots.release();
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
     m->n_rows = rows;
@@ -713,7 +835,7 @@ int kgx_kmap_destroy(kgx_kmap *m)
         return KGX_OK;
     (void)hipSetDevice(m->device);
     (void)hipStreamSynchronize(m->stream);
-    for (DevBuf *b : {&m->keys, &m->starts, &m->vals, &m->hkeys, &m->hrow})
+    for (DevBuf *b : {&m->keys, &m->starts, &m->vals, &m->hkeys, &m->hrow, &m->slots})
         b->release();
     for (auto &sc : m->scratch_free) {
         for (DevBuf *b : {&sc->k, &sc->c, &sc->ids})
@@ -724,6 +846,8 @@ int kgx_kmap_destroy(kgx_kmap *m)
     delete m;
     return KGX_OK;
 }
+
+int kgx_kmap_device(const kgx_kmap *m) { return m ? m->device : -1; }
 
 uint64_t kgx_kmap_num_kmers(const kgx_kmap *m) { return m ? m->n_rows : 0; }
 uint64_t kgx_kmap_num_values(const kgx_kmap *m) { return m ? m->n_vals : 0; }
@@ -879,23 +1003,26 @@ int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
         std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
         return KGX_OK;
     }
-    /* 1. per hit slot: sequence, list, length; the event offsets by a scan */
+    /* 1. per tile (one wave each): its hits' sequence, list start and
+     * length per slot, and its event total; the tiles' event bases by a scan */
     const Tiled t = tiled_of(c);
     const uint64_t nt = c->max_tiles, n_slots = nt * t.T;
     const KmapView view = m->view();
     HIP_TRY(r.hseq.reserve(n_slots * 4));
     HIP_TRY(r.hstart.reserve(n_slots * 8));
-    HIP_TRY(r.hlen.reserve((n_slots + 1) * 8));
-    HIP_TRY(r.eoff.reserve((n_slots + 1) * 8));
-    hipLaunchKernelGGL(rollup_hits_kernel, grid_for(n_slots + 1), dim3(256), 0, st, t, nt, view,
-                       r.hseq.as<uint32_t>(), r.hstart.as<uint64_t>(), r.hlen.as<uint64_t>());
+    HIP_TRY(r.hlen.reserve(n_slots * 4));
+    HIP_TRY(r.tcount.reserve((nt + 1) * 8));
+    HIP_TRY(r.tbase.reserve((nt + 1) * 8));
+    const dim3 tile_grid((uint32_t)((nt + 1 + 3) / 4));
+    hipLaunchKernelGGL(rollup_tiles_kernel, tile_grid, dim3(256), 0, st, t, nt, view, r.hseq.as<uint32_t>(),
+                       r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tcount.as<uint64_t>());
     size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(),
-                                             (int)(n_slots + 1), st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
+                                             (int)(nt + 1), st));
     HIP_TRY(r.tmp.reserve(tb));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(),
-                                             (int)(n_slots + 1), st));
-    HIP_TRY(hipMemcpyAsync(r.h_n.data(), r.eoff.as<uint64_t>() + n_slots, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
+                                             (int)(nt + 1), st));
+    HIP_TRY(hipMemcpyAsync(r.h_n.data(), r.tbase.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const uint64_t E = r.h_n[0];
     out->n_events = E;
@@ -905,11 +1032,14 @@ int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
     }
     if (E >= (1ull << 31))
         return fail(KGX_ERANGE, "rollup: more than 2^31 (hit, id) events in one batch");
-    /* 2. events keyed (sequence, id), stably sorted: hit order within a key */
+    /* 2. events keyed (sequence, id), stably sorted: hit order within a key;
+     * 32-bit keys when the two fields fit */
     const uint32_t ib = std::max(1, 32 - __builtin_clz(std::max(m->max_id, 1u)));
     const uint32_t sb = n > 1 ? 32 - __builtin_clz(n - 1) : 1;
-    HIP_TRY(r.key.reserve(E * 8));
-    HIP_TRY(r.key2.reserve(E * 8));
+    const bool k32 = ib + sb <= 32;
+    const size_t kb = k32 ? 4 : 8;
+    HIP_TRY(r.key.reserve(E * kb));
+    HIP_TRY(r.key2.reserve(E * kb));
     HIP_TRY(r.idx.reserve(E * 4));
     HIP_TRY(r.idx2.reserve(E * 4));
     HIP_TRY(r.ew.reserve(E * 4));
@@ -917,24 +1047,30 @@ int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
     HIP_TRY(r.rowdata.reserve(E * 16));
     HIP_TRY(r.rowcnt.reserve((n + 1) * 4));
     HIP_TRY(r.nsel.reserve(8));
-    hipLaunchKernelGGL(rollup_expand_kernel, grid_for(n_slots), dim3(256), 0, st, n_slots, r.hseq.as<uint32_t>(),
-                       r.hstart.as<uint64_t>(), r.hlen.as<uint64_t>(), r.eoff.as<uint64_t>(), view.vals, ib,
-                       r.key.as<uint64_t>(), r.idx.as<uint32_t>(), r.ew.as<float>());
-    tb = 0;
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, r.key.as<uint64_t>(), r.key2.as<uint64_t>(),
-                                               r.idx.as<uint32_t>(), r.idx2.as<uint32_t>(), (int)E, 0,
-                                               (int)(ib + sb), st));
-    HIP_TRY(r.tmp.reserve(tb));
-    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(r.tmp.p, tb, r.key.as<uint64_t>(), r.key2.as<uint64_t>(),
-                                               r.idx.as<uint32_t>(), r.idx2.as<uint32_t>(), (int)E, 0,
-                                               (int)(ib + sb), st));
-    /* 3. one row per group at its first event; rows in event order = per
-     * sequence in first-touch order, straight into the mapped host arrays */
     HIP_TRY(hipMemsetAsync(r.flag.p, 0, E, st));
     HIP_TRY(hipMemsetAsync(r.rowcnt.p, 0, (n + 1) * 4, st));
-    hipLaunchKernelGGL(rollup_groups_kernel, grid_for(E), dim3(256), 0, st, E, r.key2.as<uint64_t>(),
-                       r.idx2.as<uint32_t>(), r.ew.as<float>(), ib, mode == KGX_ROLLUP_FAMILY ? 1 : 0,
-                       r.flag.as<uint8_t>(), r.rowdata.as<uint4>(), r.rowcnt.as<uint32_t>());
+    auto sort_and_group = [&](auto *k1, auto *k2) -> int {
+        typedef std::remove_pointer_t<decltype(k1)> K;
+        hipLaunchKernelGGL(rollup_events_kernel<K>, tile_grid, dim3(256), 0, st, t, nt, r.hseq.as<uint32_t>(),
+                           r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tbase.as<uint64_t>(), view.vals, ib,
+                           k1, r.idx.as<uint32_t>(), r.ew.as<float>());
+        size_t sbytes = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sbytes, k1, k2, r.idx.as<uint32_t>(),
+                                                   r.idx2.as<uint32_t>(), (int)E, 0, (int)(ib + sb), st));
+        HIP_TRY(r.tmp.reserve(sbytes));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(r.tmp.p, sbytes, k1, k2, r.idx.as<uint32_t>(),
+                                                   r.idx2.as<uint32_t>(), (int)E, 0, (int)(ib + sb), st));
+        hipLaunchKernelGGL(rollup_groups_kernel<K>, grid_for(E), dim3(256), 0, st, E, (const K *)k2,
+                           r.idx2.as<uint32_t>(), r.ew.as<float>(), ib, mode == KGX_ROLLUP_FAMILY ? 1 : 0,
+                           r.flag.as<uint8_t>(), r.rowdata.as<uint4>(), r.rowcnt.as<uint32_t>());
+        return KGX_OK;
+    };
+    const int src = k32 ? sort_and_group(r.key.as<uint32_t>(), r.key2.as<uint32_t>())
+                        : sort_and_group(r.key.as<uint64_t>(), r.key2.as<uint64_t>());
+    if (src)
+        return src;
+    /* 3. one row per group at its first event; rows in event order = per
+     * sequence in first-touch order, straight into the mapped host arrays */
     HIP_TRY(r.h_rows.resize(E));
     out->rows = r.h_rows.data();
     void *d_rows = nullptr, *d_off = nullptr, *d_n = nullptr;

@@ -333,6 +333,12 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * staging never waits for an earlier chunk's H2D (0, the default: the two
  * contexts' staging buffers, each reused once its last H2D is done; the same
  * batch time).
+ * "pinned_input" 1 (default): a streamed batch whose residues already lie in
+ * pinned, device-mapped host memory (kgx_host_alloc, hipHostMalloc,
+ * hipHostRegister) is read by DMA straight from the caller's buffer -- no
+ * staging copy on the host; a device scan looks for NUL bytes, and a batch
+ * with one reruns staged, cut at the NUL as always (kgx_ctx_stat
+ * "pinned_batches", "nul_reruns").
  * "host_stream_dma" 1: the streamed chunks' copies by DMA, each host region
  * copied whole at its room (0, the default: device stores of the counted
  * records into mapped memory).
@@ -368,7 +374,9 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
 int kgx_ctx_set_option(kgx_ctx *ctx, const char *name, int64_t value);
 /* counters of the context since its creation: "fused_batches" / "small_batches"
  * (small host batches that took the one-launch path / the one-wait path),
- * "stream_fallbacks" (streamed batches rerun exact after a region overflow) */
+ * "stream_fallbacks" (streamed batches rerun exact after a region overflow or
+ * a NUL in pinned input), "pinned_batches" (streamed batches read straight from
+ * the caller's pinned residues), "nul_reruns" */
 int kgx_ctx_stat(kgx_ctx *ctx, const char *name, int64_t *value);
 /* launch on a caller-owned stream instead (hipStream_t; NULL = own stream) */
 int kgx_ctx_set_stream(kgx_ctx *ctx, void *stream);
@@ -743,6 +751,24 @@ typedef struct kgx_rollup_result {
     uint64_t n_events;          /* (hit, list entry) pairs folded */
 } kgx_rollup_result;
 int kgx_kmap_rollup(kgx_kmap *map, kgx_ctx *ctx, int mode, kgx_rollup_result *out);
+/* the device the map lives on */
+int kgx_kmap_device(const kgx_kmap *map);
+
+/* /lookup's GPU side for a whole host batch over a pool
+ * (LookupRequest::process_work + on_hit, lookup_request.cc:153-210,446-482):
+ * the batch is cut into residue-balanced shards as kgx_pool_process_batch
+ * does; shard i runs on context i as ONE pass (its hits stay on the device),
+ * with want within KGX_WANT_CALLS | KGX_WANT_BEST (KGX_WANT_BEST: the
+ * find_best_match decision), and then kgx_kmap_rollup over maps[j], the map on
+ * that context's device (one map per device the pool spans).  Nothing per hit
+ * crosses PCIe.  out: hit and call offsets, calls and best calls over the whole
+ * batch (out->hits NULL); rollup: every sequence's rows in input order
+ * (offsets over the batch), each sequence's rows in first-touch order as
+ * kgx_kmap_rollup gives them.  Views owned by the pool, valid until its next
+ * call. */
+int kgx_pool_lookup(kgx_pool *pool, kgx_kmap *const *maps, uint32_t n_maps, int mode, const kgx_params *params,
+                    const char *residues, const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
+                    kgx_result *out, kgx_rollup_result *rollup);
 
 /* ---- /matrix pair counting (matrix_request.cc:83-190) --------------------
  * One kgx_matrix per /matrix request (the request's matrix_proteins_ and
