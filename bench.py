@@ -306,6 +306,13 @@ def host_path_lookup_leg(abi, synth, img, spec, dev, res_h, off_h, params, n_fam
     return out
 
 
+def pool_devices(dev: int, n_dev: int, world: int) -> list:
+    """The pool_e2e leg's devices: this rank's first, then as many of the
+    other visible devices as the job has ranks (an N-GPU run measures C5 over
+    N devices; the one-GPU run over one)."""
+    return [dev] + [i for i in range(n_dev) if i != dev][:max(0, world - 1)]
+
+
 def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_permille):
     """C5 (BASELINE.json configs[4]) as the reference would run it: one host
     batch of n x Ls aa through kgx_pool over one image replica per device
@@ -690,7 +697,7 @@ def main():
     pool_e2e = None
     if d.rank == 0 and not args.no_pool:
         # one replica per rank's device: the N-GPU run measures C5 over N devices
-        pdevs = [dev] + [i for i in range(n_dev) if i != dev][:d.world - 1]
+        pdevs = pool_devices(dev, n_dev, d.world)
         pool_e2e = pool_e2e_leg(abi, L, synth, img, spec, pdevs, params, want, args.strong_seq, Ls,
                                 args.x_permille)
 

@@ -14,6 +14,13 @@
  * beside the service must equal the batch run alone, byte for byte; every
  * service answer must equal its sequence's slice of that batch.  Prints one
  * JSON line; exit 1 on a mismatch or an ABI error.
+ *
+ * Evidence for the tail: per batch the batch thread's
+ * involuntary / voluntary context switches (getrusage RUSAGE_THREAD) and the
+ * split of its time between kgx_process_batch and copying the result; for
+ * the slowest batches the service calls that overlapped them (count, the
+ * longest) -- so a slow batch can be told apart as host preemption, a
+ * service-side stall, or the device.
  */
 #include <algorithm>
 #include <atomic>
@@ -25,6 +32,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <sys/resource.h>
 
 #include "kgx.h"
 
@@ -121,19 +130,40 @@ int main(int argc, char **argv)
     std::atomic<bool> stop{false}, failed{false};
     std::atomic<uint64_t> n_calls{0}, n_busy{0}, svc_bad{0};
     std::vector<double> beside;
+    struct BatchRec {
+        double t0, t1, call_ms; /* ms from the run's start; kgx_process_batch alone */
+        long nivcsw, nvcsw;     /* the batch thread's context switches during the batch */
+    };
+    std::vector<BatchRec> brec;
     uint64_t batch_bad = 0;
+    const auto T0 = clk::now();
+    auto since = [&](clk::time_point t) { return std::chrono::duration<double, std::milli>(t - T0).count(); };
     std::thread bt([&]() {
         while (!stop.load()) {
             Batch b;
+            struct rusage ra, rb;
+            getrusage(RUSAGE_THREAD, &ra);
             const auto t0 = clk::now();
-            if (!run_batch(b)) {
+            kgx_result r;
+            if (kgx_process_batch(ctx, &prm, res.data(), off.data(), (uint32_t)n, want, &r) != KGX_OK) {
                 failed = true;
                 return;
             }
-            beside.push_back(std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+            const auto tc = clk::now();
+            b.hoff.assign(r.hit_offsets, r.hit_offsets + n + 1);
+            b.coff.assign(r.call_offsets, r.call_offsets + n + 1);
+            b.hits.assign(r.hits, r.hits + b.hoff[n]);
+            b.calls.assign(r.calls, r.calls + b.coff[n]);
+            const auto t1 = clk::now();
+            getrusage(RUSAGE_THREAD, &rb);
+            beside.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            brec.push_back({since(t0), since(t1), std::chrono::duration<double, std::milli>(tc - t0).count(),
+                            rb.ru_nivcsw - ra.ru_nivcsw, rb.ru_nvcsw - ra.ru_nvcsw});
             batch_bad += !(b == ref);
         }
     });
+    /* every service call's [start, end) in ms from T0, per thread */
+    std::vector<std::vector<std::pair<double, double>>> calls_t(T);
     std::vector<std::thread> ws;
     const auto t_end = clk::now() + std::chrono::duration<double>(seconds);
     const auto t0 = clk::now();
@@ -144,8 +174,10 @@ int main(int argc, char **argv)
             for (uint64_t k = (uint64_t)t; clk::now() < t_end; k += (uint64_t)T) {
                 const uint64_t s = k % n, len = off[s + 1] - off[s];
                 uint64_t nh = 0, nc = 0;
+                const auto c0 = clk::now();
                 const int rc = kgx_svc_call(img, &prm, res.data() + off[s], len, want, h.data(), h.size(), &nh,
                                             c.data(), c.size(), &nc, nullptr, 0, nullptr);
+                calls_t[t].emplace_back(since(c0), since(clk::now()));
                 if (rc == KGX_EBUSY) {
                     n_busy++;
                     continue;
@@ -170,6 +202,47 @@ int main(int argc, char **argv)
     const double tp = std::chrono::duration<double>(clk::now() - t0).count();
     stop = true;
     bt.join();
+    /* the tail's evidence: batches with / without an involuntary switch, and
+     * the five slowest batches with what overlapped them */
+    std::vector<double> with_sw, without_sw;
+    for (const BatchRec &b : brec)
+        (b.nivcsw > 0 ? with_sw : without_sw).push_back(b.t1 - b.t0);
+    std::vector<size_t> order(brec.size());
+    for (size_t i = 0; i < order.size(); i++)
+        order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return brec[a].t1 - brec[a].t0 > brec[b].t1 - brec[b].t0; });
+    std::string slow = "[";
+    for (size_t k = 0; k < std::min<size_t>(5, order.size()); k++) {
+        const BatchRec &b = brec[order[k]];
+        size_t overl = 0;
+        double longest = 0.0;
+        for (const auto &v : calls_t)
+            for (const auto &c : v)
+                if (c.second > b.t0 && c.first < b.t1) {
+                    overl++;
+                    longest = std::max(longest, c.second - c.first);
+                }
+        char buf[320];
+        std::snprintf(buf, sizeof buf,
+                      "%s{\"ms\": %.3f, \"in_process_batch_ms\": %.3f, \"nivcsw\": %ld, \"nvcsw\": %ld, "
+                      "\"service_calls_overlapping\": %zu, \"longest_overlapping_call_ms\": %.3f}",
+                      k ? ", " : "", b.t1 - b.t0, b.call_ms, b.nivcsw, b.nvcsw, overl, longest);
+        slow += buf;
+    }
+    slow += "]";
+    std::vector<double> call_ms;
+    for (const auto &v : calls_t)
+        for (const auto &c : v)
+            call_ms.push_back(c.second - c.first);
+    struct rusage self;
+    getrusage(RUSAGE_SELF, &self);
+    std::printf("{\"tail_evidence\": {\"batches_with_involuntary_switch\": %zu, \"p50_ms_with\": %.3f, "
+                "\"max_ms_with\": %.3f, \"batches_without\": %zu, \"p50_ms_without\": %.3f, \"p99_ms_without\": %.3f, "
+                "\"max_ms_without\": %.3f, \"service_call_ms\": {\"p50\": %.4f, \"p99\": %.4f, \"max\": %.3f}, "
+                "\"process_nivcsw\": %ld, \"slowest\": %s}}\n",
+                with_sw.size(), pct(with_sw, 50), pct(with_sw, 100), without_sw.size(), pct(without_sw, 50),
+                pct(without_sw, 99), pct(without_sw, 100), pct(call_ms, 50), pct(call_ms, 99), pct(call_ms, 100),
+                self.ru_nivcsw, slow.c_str());
     std::printf("{\"service_threads\": %d, \"batch_proteins\": %llu, \"batch_alone_ms\": {\"p50\": %.3f, \"max\": %.3f}, "
                 "\"batch_beside_ms\": {\"n\": %zu, \"p50\": %.3f, \"p90\": %.3f, \"p99\": %.3f, \"max\": %.3f, "
                 "\"over_5ms\": %zu, \"argmax\": %zu}, "

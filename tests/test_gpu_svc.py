@@ -298,8 +298,11 @@ def test_svc_beside_batches_on_the_same_image(tmp_path):
     r = subprocess.run([kbuild.BESIDE_CHECK, str(spec.n_keys), str(spec.num_sigs), str(q), "8", "3"],
                        capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
-    out = json.loads(r.stdout.strip().splitlines()[-1])
+    lines = r.stdout.strip().splitlines()
+    out = json.loads(lines[-1])
+    ev = json.loads(lines[-2])["tail_evidence"]
     print(out)
+    print(json.dumps(ev))
     assert out["batch_mismatches"] == 0 and out["service_mismatches"] == 0
     assert out["batch_beside_ms"]["n"] >= 20 and out["service_calls"] >= 10000
     b = out["batch_beside_ms"]
