@@ -1577,6 +1577,11 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
     const char *end = text + n;
     std::vector<const char *> cuts{text};
     const size_t want_parts = n / kPartBytes;
+    /* the first part is an eighth of the others: nothing overlaps its parse
+     * (r5k: 4.4-5.9 ms of a 66-ms block waiting for a 32-MB first part) */
+    if (want_parts > 1)
+        if (const char *c = fq_cut_after(text + kPartBytes / 8, end))
+            cuts.push_back(c);
     for (size_t i = 1; i < want_parts; i++) {
         const char *c = fq_cut_after(text + n * i / want_parts, end);
         if (c && c > cuts.back())
@@ -1673,10 +1678,13 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
                 th.join();
             pool.clear();
         };
-        /* parts alternate between two contexts: part k + 1 is sized and its
-         * lookup enqueued before part k's results are collected, so the host's
-         * collection and output of one part overlap the next part's probe */
-        kgx_ctx *ctxs[2] = {kg_.ctx(), twin_ctx()};
+        /* parts rotate over three contexts, two parts ahead of the one being
+         * collected: part k + 2's bases go up by DMA while part k + 1 is sized
+         * and its lookup enqueued and part k is collected, so the next probe
+         * never waits for an upload (with two contexts and the upload inside
+         * the launch, each part's 16-MB H2D ran with the GPU idle: 1.06 ms
+         * per part against a 0.46-ms probe, r5j) */
+        kgx_ctx *ctxs[3] = {kg_.ctx(), twin_ctx(), twin2_ctx()};
         auto wait_part = [&](size_t k) -> FqPart & {
             const auto w0 = std::chrono::steady_clock::now();
             std::unique_lock<std::mutex> lk(mu);
@@ -1692,51 +1700,80 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
             consumed = k + 1;
             cv.notify_all();
         };
-        try {
-            FqPart *cur = &wait_part(0);
+        struct Slot {
+            FqPart *pt = nullptr;
+            bool tail = false; /* the exact re-parse of the rest of the block: the last part */
+            FqLaunched l;
+        };
+        /* part j, given part j - 1 (prev): the speculative part when the
+         * exact parse of prev ends at a record start with nothing pending,
+         * else the rest of the block parsed again from prev's end state */
+        auto next_part = [&](const FqPart &prev, size_t j) -> Slot {
+            Slot sl;
+            const bool holds = prev.state == FQ_START && prev.id.empty() && prev.len == prev.roff.back();
+            if (holds) {
+                sl.pt = &wait_part(j);
+                if (j + 1 == K)
+                    finish_part(*sl.pt);
+                return sl;
+            }
+            stop_workers();
+            if (!tail_)
+                tail_.reset(new FqPart);
+            tail_->begin((size_t)(end - cuts[j]) + (prev.len - prev.roff.back()), prev.state, prev.id,
+                         std::string(prev.bases + prev.roff.back(), prev.len - prev.roff.back()));
+            tail_->parse(cuts[j], end);
+            finish_part(*tail_);
+            sl.pt = tail_.get();
+            sl.tail = true;
+            return sl;
+        };
+        auto upload = [&](Slot &sl, kgx_ctx *ctx) {
+            const FqBlock v = sl.pt->view();
+            sl.l = FqLaunched{};
+            sl.l.ctx = ctx;
+            sl.l.n_reads = (uint32_t)v.n_reads();
+            if (sl.l.n_reads)
+                if (int rc = kgx_fq_upload(ctx, v.residues(), v.roff, sl.l.n_reads))
+                    throw_last(rc, "kgx_fq_upload");
+        };
+        auto launch = [&](Slot &sl) {
             const auto l0 = std::chrono::steady_clock::now();
-            FqLaunched lc = launch_block(cur->view(), ctxs[0]);
+            launch_uploaded(sl.l);
             device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - l0).count();
-            for (size_t k = 0; k < K; k++) {
-                FqPart *nxt = nullptr;
-                FqLaunched ln;
-                FqPart *tail = nullptr;
-                if (k + 1 < K) {
-                    /* the speculation of part k + 1 holds iff part k ends at a
-                     * record start with nothing pending */
-                    const bool holds = cur->state == FQ_START && cur->id.empty() && cur->len == cur->roff.back();
-                    if (holds) {
-                        nxt = &wait_part(k + 1);
-                        if (k + 2 == K)
-                            finish_part(*nxt);
-                    } else {
-                        /* the rest of the block, exactly, from part k's end state */
-                        stop_workers();
-                        if (!tail_)
-                            tail_.reset(new FqPart);
-                        tail = tail_.get();
-                        tail->begin((size_t)(end - cuts[k + 1]) + (cur->len - cur->roff.back()), cur->state, cur->id,
-                                    std::string(cur->bases + cur->roff.back(), cur->len - cur->roff.back()));
-                        tail->parse(cuts[k + 1], end);
-                        finish_part(*tail);
-                        nxt = tail;
+        };
+        try {
+            Slot sl[3];
+            size_t have = 1; /* parts 0 .. have-1 are prepared (uploaded) */
+            bool last_known = false; /* the last prepared part is the block's last */
+            sl[0].pt = &wait_part(0);
+            upload(sl[0], ctxs[0]);
+            launch(sl[0]);
+            if (K > 1) {
+                sl[1] = next_part(*sl[0].pt, 1);
+                upload(sl[1], ctxs[1]);
+                have = 2;
+                last_known = sl[1].tail || K == 2;
+            } else {
+                last_known = true;
+            }
+            for (size_t k = 0; k < have; k++) {
+                Slot &cur = sl[k % 3];
+                if (k + 1 < have) {
+                    Slot &nxt = sl[(k + 1) % 3];
+                    if (!last_known && k + 2 < K) { /* part k + 2 up while k + 1 launches and k finishes */
+                        sl[(k + 2) % 3] = next_part(*nxt.pt, k + 2);
+                        upload(sl[(k + 2) % 3], ctxs[(k + 2) % 3]);
+                        have = k + 3;
+                        last_known = sl[(k + 2) % 3].tail || k + 3 == K;
                     }
-                    const auto l1 = std::chrono::steady_clock::now();
-                    ln = launch_block(nxt->view(), ctxs[(k + 1) % 2]);
-                    device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - l1).count();
+                    launch(nxt);
                 }
                 const auto f0 = std::chrono::steady_clock::now();
-                finish_block(cur->view(), lc, mapper, os);
+                finish_block(cur.pt->view(), cur.l, mapper, os);
                 device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count();
-                if (tail) { /* the exact re-parse was the last part */
-                    const auto f1 = std::chrono::steady_clock::now();
-                    finish_block(nxt->view(), ln, mapper, os);
-                    device_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f1).count();
-                    break;
-                }
-                release(k);
-                cur = nxt;
-                lc = ln;
+                if (!cur.tail)
+                    release(k);
             }
         } catch (...) {
             stop_workers();
@@ -1776,6 +1813,16 @@ void FqRequest::process_block(const FqBlock &blk, FamilyMapper &mapper, std::ost
     finish_block(blk, l, mapper, os);
 }
 
+kgx_ctx *FqRequest::twin2_ctx()
+{
+    if (!twin2_) {
+        int rc = kgx_ctx_create(kg_.image_->handle(), &twin2_);
+        if (rc)
+            throw_last(rc, "kgx_ctx_create");
+    }
+    return twin2_;
+}
+
 kgx_ctx *FqRequest::twin_ctx()
 {
     if (!twin_) {
@@ -1790,6 +1837,8 @@ FqRequest::~FqRequest()
 {
     if (twin_)
         kgx_ctx_destroy(twin_);
+    if (twin2_)
+        kgx_ctx_destroy(twin2_);
 }
 
 /* the block's reads -> fragments -> lookup, one GPU batch on ctx: returns
@@ -1801,15 +1850,26 @@ FqRequest::FqLaunched FqRequest::launch_block(const FqBlock &blk, kgx_ctx *ctx)
     l.n_reads = (uint32_t)blk.n_reads();
     if (l.n_reads == 0)
         return l;
+    if (int rc = kgx_fq_upload(ctx, blk.residues(), blk.roff, l.n_reads))
+        throw_last(rc, "kgx_fq_upload");
+    launch_uploaded(l);
+    return l;
+}
+
+void FqRequest::launch_uploaded(FqLaunched &l)
+{
+    if (l.n_reads == 0)
+        return;
+    kgx_ctx *ctx = l.ctx;
     /* fragments as anchors into the bases: the probe translates their windows
      * itself and no residue goes through HBM (the context keeps residues when
      * its probe cannot take anchors) */
     int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
     if (rc)
         throw_last(rc, "kgx_ctx_set_option");
-    rc = kgx_fq_fragments(ctx, blk.residues(), blk.roff, l.n_reads, &l.fr);
+    rc = kgx_fq_fragments_uploaded(ctx, &l.fr);
     if (rc)
-        throw_last(rc, "kgx_fq_fragments");
+        throw_last(rc, "kgx_fq_fragments_uploaded");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
     /* Calls are sparse over fragments (most fragments of a read are noise),
      * so the calls come back and find_best_call runs on the host for the
@@ -1819,7 +1879,6 @@ FqRequest::FqLaunched FqRequest::launch_block(const FqBlock &blk, kgx_ctx *ctx)
     rc = kgx_fq_run_device(ctx, &p, &l.fr, KGX_WANT_CALLS, nullptr);
     if (rc)
         throw_last(rc, "kgx_fq_run_device");
-    return l;
 }
 
 void FqRequest::finish_block(const FqBlock &blk, FqLaunched &l, FamilyMapper &mapper, std::ostream &os)

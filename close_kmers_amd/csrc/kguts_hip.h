@@ -532,9 +532,13 @@ private:
         kgx_fragments fr{};
     };
     FqLaunched launch_block(const FqBlock &blk, kgx_ctx *ctx);
+    /* launch_block's second half, after kgx_fq_upload of l's reads on l.ctx */
+    void launch_uploaded(FqLaunched &l);
     void finish_block(const FqBlock &blk, FqLaunched &l, FamilyMapper &mapper, std::ostream &os);
     kgx_ctx *twin_ctx(); /* a second context on the image, created on first use */
     kgx_ctx *twin_ = nullptr;
+    kgx_ctx *twin2_ctx(); /* a third, for the multi-part pipeline */
+    kgx_ctx *twin2_ = nullptr;
     KmerGuts &kg_;
     std::shared_ptr<KmerPegMapping> mapping_;
     /* FastqParser state (fastq_parser.h:40-150) */

@@ -1387,42 +1387,63 @@ int kgx_fq_called_reads(kgx_ctx *c, const kgx_fragments *fragments, kgx_fq_calle
     return fq_called_reads(c, fragments, out);
 }
 
-int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
-                     kgx_fragments *out)
+int kgx_fq_upload(kgx_ctx *c, const char *bases, const uint64_t *read_offsets, uint32_t n_reads)
 {
-    if (!c || !out || (n_reads && !read_offsets))
+    if (!c || (n_reads && !read_offsets))
         return fail(KGX_EINVAL, "null argument");
     HIP_TRY(hipSetDevice(c->img->device));
     const uint64_t r0 = n_reads ? read_offsets[0] : 0;
     const uint64_t nb = n_reads ? read_offsets[n_reads] - r0 : 0;
     if (nb && !bases)
         return fail(KGX_EINVAL, "null bases");
-    std::vector<uint64_t> off(n_reads + 1, 0);
-    for (uint32_t r = 0; r <= n_reads && n_reads; r++) {
-        if (r && read_offsets[r] < read_offsets[r - 1])
+    HIP_TRY(c->h_fq_roff.resize((uint64_t)n_reads + 1));
+    uint64_t *off = c->h_fq_roff.data();
+    off[0] = 0;
+    for (uint32_t r = 1; r <= n_reads; r++) {
+        if (read_offsets[r] < read_offsets[r - 1])
             return fail(KGX_EINVAL, "read_offsets not monotone");
         off[r] = read_offsets[r] - r0;
     }
     HIP_TRY(c->fq_bases.reserve(nb + 16));
     HIP_TRY(c->fq_roff.reserve(((uint64_t)n_reads + 1) * 8));
+    /* the small copy first: copies from all streams share the DMA engine in order */
+    HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off, ((uint64_t)n_reads + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if (nb) {
         /* bases in pinned memory (kgx_host_alloc) go by DMA straight from
-         * there; others through the context's pinned staging.  Either way the
-         * copy is done before this call returns (fq_fragments waits for the
-         * batch's sizes behind it). */
-        hipPointerAttribute_t attr{};
-        const bool pinned = hipPointerGetAttributes(&attr, bases + r0) == hipSuccess &&
-                            attr.type == hipMemoryTypeHost;
+         * there; others through the context's pinned staging */
+        const bool pinned = host_pinned_range(bases + r0, nb);
         if (!pinned) {
-            (void)hipGetLastError(); /* an unregistered pointer is not an error here */
             HIP_TRY(c->h_res.resize(nb));
             parallel_memcpy(c->h_res.data(), bases + r0, nb);
         }
         HIP_TRY(hipMemcpyAsync(c->fq_bases.p, pinned ? static_cast<const void *>(bases + r0) : c->h_res.data(), nb,
                                hipMemcpyHostToDevice, c->stream));
     }
-    HIP_TRY(hipMemcpyAsync(c->fq_roff.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, c->stream));
-    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), n_reads, nb, nb, out);
+    c->fq_up.active = true;
+    c->fq_up.n_reads = n_reads;
+    c->fq_up.n_bases = nb;
+    return KGX_OK;
+}
+
+int kgx_fq_fragments_uploaded(kgx_ctx *c, kgx_fragments *out)
+{
+    if (!c || !out)
+        return fail(KGX_EINVAL, "null argument");
+    if (!c->fq_up.active)
+        return fail(KGX_EINVAL, "no reads uploaded on this context (kgx_fq_upload)");
+    HIP_TRY(hipSetDevice(c->img->device));
+    c->fq_up.active = false;
+    const uint64_t nb = c->fq_up.n_bases;
+    return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), c->fq_up.n_reads, nb, nb, out);
+}
+
+int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
+                     kgx_fragments *out)
+{
+    if (!c || !out || (n_reads && !read_offsets))
+        return fail(KGX_EINVAL, "null argument");
+    const int rc = kgx_fq_upload(c, bases, read_offsets, n_reads);
+    return rc ? rc : kgx_fq_fragments_uploaded(c, out);
 }
 
 }  // extern "C"

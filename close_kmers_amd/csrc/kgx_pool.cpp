@@ -76,38 +76,29 @@ struct kgx_pool {
     std::vector<kgx_best_call> best;
     std::vector<uint64_t> roff; /* kgx_pool_lookup's rollup rows */
     std::vector<kgx_rollup_row> rows;
-    /* at most `active` shards run at once on one device (KGX_POOL_ACTIVE, default
-     * 2): each shard's host batch runs its chunks on a context and its twin,
-     * with copy and event waits across their streams, and a process's streams
-     * share a few hardware queues, so past two shards per device they queue
-     * behind each other's waits (r5e: 8 contexts on one device 40.7 ms per C5
-     * batch vs 31.5 with 2) */
-    uint32_t active = 2;
-    struct DevGate {
-        std::mutex mu;
-        std::condition_variable cv;
-        uint32_t running = 0;
-    };
-    std::vector<std::unique_ptr<DevGate>> gates; /* per device ordinal seen */
-    DevGate *gate_of(int device)
+    /* Shards per device: a host batch runs its chunks on a context and its
+     * twin, with copies and event waits across their streams, and a process's
+     * streams share a few hardware queues (4), so past two batches at once on
+     * one device they queue behind each other's waits: 8 contexts of one
+     * device took 38-41 ms per C5 batch against 31 with 2 (r5e, r5i), gated
+     * to two at a time or not.  So a batch is cut into at most `per_device`
+     * shards per device (KGX_POOL_PER_DEVICE, default 2), run on the first
+     * contexts of each device; /lookup's one-pass shards take twice that
+     * (no twins: 4 contexts measured best, r5e) */
+    uint32_t per_device = 2;
+    std::vector<uint32_t> runners(uint32_t per) const
     {
-        return gates[(size_t)device].get();
-    }
-    /* fn(i) with context i's device gate held */
-    template <class F> void gated(uint32_t i, F &&fn)
-    {
-        DevGate *g = gate_of(kgx_image_device(ctxs[i]->img));
-        {
-            std::unique_lock<std::mutex> lk(g->mu);
-            g->cv.wait(lk, [&] { return g->running < active; });
-            g->running++;
+        std::vector<uint32_t> out, used;
+        for (uint32_t i = 0; i < (uint32_t)ctxs.size(); i++) {
+            const int d = kgx_image_device(ctxs[i]->img);
+            if ((int)used.size() <= d)
+                used.resize((size_t)d + 1, 0);
+            if (used[(size_t)d] < per) {
+                used[(size_t)d]++;
+                out.push_back(i);
+            }
         }
-        fn();
-        {
-            std::lock_guard<std::mutex> lk(g->mu);
-            g->running--;
-        }
-        g->cv.notify_one();
+        return out;
     }
 
     void worker(uint32_t i)
@@ -197,13 +188,8 @@ int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx,
         c->host_threads = (int)std::max(1u, std::min<unsigned>((unsigned)c->host_threads, cpus / n_ctx));
     }
     p->expand_threads = std::max(1u, std::min(p->expand_threads, cpus));
-    int max_dev = 0;
-    for (kgx_ctx *c : p->ctxs)
-        max_dev = std::max(max_dev, kgx_image_device(c->img));
-    for (int d = 0; d <= max_dev; d++)
-        p->gates.emplace_back(new kgx_pool::DevGate);
-    if (const char *e = std::getenv("KGX_POOL_ACTIVE"))
-        p->active = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
+    if (const char *e = std::getenv("KGX_POOL_PER_DEVICE"))
+        p->per_device = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     if (const char *e = std::getenv("KGX_POOL_EXPAND_THREADS"))
         p->expand_threads = (unsigned)std::min(256L, std::max(1L, std::strtol(e, nullptr, 10)));
     for (uint32_t i = 0; i < n_ctx; i++)
@@ -241,6 +227,7 @@ namespace {
  * results left compact in the contexts (kgx_process_batch_compact); then the
  * concatenation's offsets (hoff/coff/ooff) and the per-shard bases */
 struct PoolRun {
+    std::vector<uint32_t> run; /* shard i runs on context run[i] */
     uint32_t K = 0;
     std::vector<uint32_t> cuts;
     std::vector<kgx_compact_result> part;
@@ -256,7 +243,8 @@ int pool_shards(kgx_pool *p, const kgx_params *params, const char *residues, con
     for (uint32_t s = 0; s < n_seq; s++)
         if (seq_offsets[s + 1] < seq_offsets[s])
             return fail(KGX_EINVAL, "seq_offsets not monotone");
-    R.K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)p->ctxs.size(), n_seq));
+    R.run = p->runners(p->per_device);
+    R.K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)R.run.size(), n_seq));
     const uint32_t K = R.K;
     R.cuts.assign(K + 1, 0);
     int rc = kgx_shard_cuts(seq_offsets, n_seq, K, R.cuts.data());
@@ -268,10 +256,8 @@ int pool_shards(kgx_pool *p, const kgx_params *params, const char *residues, con
     std::vector<int> rcs(K, KGX_OK);
     std::vector<std::string> errs(K);
     p->run(K, [&](uint32_t i) {
-        p->gated(i, [&] {
-            rcs[i] = kgx_process_batch_compact(p->ctxs[i], params, residues, seq_offsets + R.cuts[i],
-                                               R.cuts[i + 1] - R.cuts[i], want, &R.part[i]);
-        });
+        rcs[i] = kgx_process_batch_compact(p->ctxs[R.run[i]], params, residues, seq_offsets + R.cuts[i],
+                                           R.cuts[i + 1] - R.cuts[i], want, &R.part[i]);
         if (rcs[i])
             errs[i] = kgx_last_error();
     });
@@ -439,14 +425,16 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         if (seq_offsets[s + 1] < seq_offsets[s])
             return fail(KGX_EINVAL, "seq_offsets not monotone");
     /* each context's map: the one on its device */
-    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)p->ctxs.size(), n_seq));
+    const std::vector<uint32_t> run = p->runners(2 * p->per_device);
+    const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)run.size(), n_seq));
     std::vector<kgx_kmap *> mine(K, nullptr);
     for (uint32_t i = 0; i < K; i++) {
+        const int dev = kgx_image_device(p->ctxs[run[i]]->img);
         for (uint32_t j = 0; j < n_maps && !mine[i]; j++)
-            if (maps[j] && kgx_kmap_device(maps[j]) == kgx_image_device(p->ctxs[i]->img))
+            if (maps[j] && kgx_kmap_device(maps[j]) == dev)
                 mine[i] = maps[j];
         if (!mine[i])
-            return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(kgx_image_device(p->ctxs[i]->img)));
+            return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(dev));
     }
     std::vector<uint32_t> cuts(K + 1, 0);
     int rc = kgx_shard_cuts(seq_offsets, n_seq, K, cuts.data());
@@ -459,7 +447,7 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
     std::vector<int> rcs(K, KGX_OK);
     std::vector<std::string> errs(K);
     p->run(K, [&](uint32_t i) {
-        kgx_ctx *c = p->ctxs[i];
+        kgx_ctx *c = p->ctxs[run[i]];
         const int chunks = c->host_chunks, sv = c->score_variant;
         c->host_chunks = 1;
         /* a shard's sequences on the host path's scorer (option

@@ -135,6 +135,10 @@ template <class T> struct PinnedVec {
 
 inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 
+/* [p, p + n) lies in one pinned, device-mapped host allocation (kgx_host_alloc,
+ * hipHostMalloc, hipHostRegister): the device may read it by DMA directly */
+bool host_pinned_range(const void *p, uint64_t n);
+
 /* host CPUs this process may keep busy: the affinity mask, capped by a
  * cgroup v2 quota (cpu.max) -- on the GPU box the mask shows the whole
  * machine while the quota is 16 */
@@ -356,6 +360,13 @@ struct kgx_ctx {
     kgx::DevBuf fq_look; /* fq_fused: tile counter | tile states */
     kgx::PinnedVec<uint64_t> h_fq_tot; /* fragments, residues of the last fq batch */
     kgx::FqPending fq_pend;             /* an enqueued fragment pass awaiting its finish */
+    /* kgx_fq_upload: reads whose H2D is enqueued, awaiting kgx_fq_fragments_uploaded */
+    struct {
+        bool active = false;
+        uint32_t n_reads = 0;
+        uint64_t n_bases = 0;
+    } fq_up;
+    kgx::PinnedVec<uint64_t> h_fq_roff; /* the uploaded reads' relative offsets (pinned: the copy is async) */
     /* kgx_fq_called_reads */
     kgx::DevBuf fqc_flag, fqc_reads, fqc_nsel, fqc_nfrag, fqc_ncall, fqc_fo, fqc_co, fqc_fc, fqc_len, fqc_coff,
         fqc_calls;

@@ -66,6 +66,23 @@ struct PhaseTimer {
 
 }  // namespace kgx
 
+/* [p, p + n) lies in one pinned, device-mapped host allocation */
+bool kgx::host_pinned_range(const void *p, uint64_t n)
+{
+    if (!p || n == 0)
+        return false;
+    hipPointerAttribute_t a{}, b{};
+    const char *first = static_cast<const char *>(p), *last = first + n - 1;
+    if (hipPointerGetAttributes(&a, first) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer ||
+        hipPointerGetAttributes(&b, last) != hipSuccess || b.type != hipMemoryTypeHost || !b.devicePointer) {
+        (void)hipGetLastError(); /* an unregistered pointer is not an error here */
+        return false;
+    }
+    return static_cast<const char *>(b.devicePointer) - static_cast<const char *>(a.devicePointer) ==
+           (std::ptrdiff_t)(n - 1);
+}
+
+
 extern "C" {
 
 const char *kgx_version(void) { return "close_kmers_amd 0.1 (gfx950)"; }
@@ -1483,22 +1500,6 @@ void cut_at_nul(char *b, uint64_t len)
         for (uint64_t i = slen ? slen - 1 : 0; i < len; i++)
             b[i] = 'X';
     }
-}
-
-/* [p, p + n) lies in one pinned, device-mapped host allocation */
-bool host_pinned_range(const void *p, uint64_t n)
-{
-    if (!p || n == 0)
-        return false;
-    hipPointerAttribute_t a{}, b{};
-    const char *first = static_cast<const char *>(p), *last = first + n - 1;
-    if (hipPointerGetAttributes(&a, first) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer ||
-        hipPointerGetAttributes(&b, last) != hipSuccess || b.type != hipMemoryTypeHost || !b.devicePointer) {
-        (void)hipGetLastError(); /* an unregistered pointer is not an error here */
-        return false;
-    }
-    return static_cast<const char *>(b.devicePointer) - static_cast<const char *>(a.devicePointer) ==
-           (std::ptrdiff_t)(n - 1);
 }
 
 /* the n + 1 chunk-relative offsets of sequences [s0, s1) */

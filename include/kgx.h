@@ -552,12 +552,15 @@ int kgx_pool_destroy(kgx_pool *pool);
 uint32_t kgx_pool_size(const kgx_pool *pool);
 /* context i of the pool (owned by the pool; options may be set on it) */
 kgx_ctx *kgx_pool_ctx(kgx_pool *pool, uint32_t i);
-/* kgx_process_batch over the pool: the batch is cut into min(n_ctx, n_seq)
- * contiguous, residue-balanced shards of whole sequences (kgx_shard_cuts),
- * shard i runs on context i -- all at once, on every GPU -- and the results
- * are concatenated in input order: the same CSR, the same bytes (kgx_hit.seq
- * included) as one context processing the whole batch.  The views are owned
- * by the pool and valid until its next call. */
+/* kgx_process_batch over the pool: the batch is cut into contiguous,
+ * residue-balanced shards of whole sequences (kgx_shard_cuts), one per
+ * running context -- the first two contexts of each device (environment
+ * KGX_POOL_PER_DEVICE; a host batch on more contexts of one device only
+ * queues behind the others' waits in the process's few hardware queues) --
+ * all at once, on every GPU, and the results are concatenated in input order:
+ * the same CSR, the same bytes (kgx_hit.seq included) as one context
+ * processing the whole batch.  The views are owned by the pool and valid
+ * until its next call. */
 int kgx_pool_process_batch(kgx_pool *pool, const kgx_params *params, const char *residues,
                            const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out);
 /* The same with compact hits (kgx_process_batch_compact): every shard's
@@ -639,6 +642,14 @@ typedef struct kgx_fragments {
 /* reads from host memory (bases concatenated, read_offsets[n_reads + 1]) */
 int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
                      kgx_fragments *out);
+/* kgx_fq_fragments in two steps, so that one block's upload overlaps earlier
+ * blocks' work: _upload enqueues the H2D of the reads' bases and offsets on
+ * ctx's stream and returns at once (bases in pinned memory go by DMA straight
+ * from there and must stay unchanged until _uploaded returns; others are
+ * staged first); _uploaded runs the fragment pass over them, as
+ * kgx_fq_fragments does.  Nothing else may run on ctx between the two. */
+int kgx_fq_upload(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads);
+int kgx_fq_fragments_uploaded(kgx_ctx *ctx, kgx_fragments *out);
 /* reads already in device memory */
 int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint32_t n_reads, kgx_fragments *out);
@@ -757,7 +768,8 @@ int kgx_kmap_device(const kgx_kmap *map);
 /* /lookup's GPU side for a whole host batch over a pool
  * (LookupRequest::process_work + on_hit, lookup_request.cc:153-210,446-482):
  * the batch is cut into residue-balanced shards as kgx_pool_process_batch
- * does; shard i runs on context i as ONE pass (its hits stay on the device),
+ * does (up to twice as many per device: a shard here is one pass, no twin);
+ * each runs on its context as ONE pass (its hits stay on the device),
  * with want within KGX_WANT_CALLS | KGX_WANT_BEST (KGX_WANT_BEST: the
  * find_best_match decision), and then kgx_kmap_rollup over maps[j], the map on
  * that context's device (one map per device the pool spans).  Nothing per hit

@@ -48,7 +48,11 @@ def _mixed_batch(spec, n, seed):
 
 
 @pytest.mark.parametrize("n_ctx,n_seq", [(8, 2000), (3, 1001), (8, 5), (2, 1), (4, 0)])
-def test_pool_split_is_byte_identical_to_one_pass(world, gpu, oracle_lib, n_ctx, n_seq):
+def test_pool_split_is_byte_identical_to_one_pass(world, gpu, oracle_lib, n_ctx, n_seq, monkeypatch):
+    """n_ctx shards, one per context: on a node each replica is on its own
+    device; here every replica is on device 0, so the pool's per-device shard
+    limit (KGX_POOL_PER_DEVICE, default 2) is raised to keep n_ctx shards"""
+    monkeypatch.setenv("KGX_POOL_PER_DEVICE", str(n_ctx))
     spec, table, img = world
     res, off = _mixed_batch(spec, n_seq, n_ctx * 100 + n_seq)
     with gpu.Context(img) as ctx:

@@ -307,10 +307,14 @@ def test_svc_beside_batches_on_the_same_image(tmp_path):
     assert out["batch_beside_ms"]["n"] >= 20 and out["service_calls"] >= 10000
     b = out["batch_beside_ms"]
     assert b["p50"] <= 1.6, out
-    # the tail: at most one batch in a thousand over 5 ms and none over 25 ms.
-    # Nine busy host threads on the box's 16-CPU share meet an occasional
-    # preemption: one batch of 5,490 took 5.07 ms in one run, none in others
-    assert b["p99"] <= 5.0 and b["over_5ms"] <= b["n"] // 1000 and b["max"] <= 25.0, out
+    # the tail: no batch over 5 ms (round 3's bound).  Round 4 once saw a
+    # single 5.07-ms batch of 5,490 and loosened it; round 5 records per batch
+    # the batch thread's context switches and the service calls around it
+    # (profiles/r5i_beside_tail_evidence.txt): the slowest batches had no
+    # involuntary switch and overlapped no slow service call -- they were the
+    # host copy of the result (the first batch's fresh vectors) -- so the
+    # bound is the hard one again
+    assert b["p99"] <= 5.0 and b["max"] <= 5.0, (out, ev)
 
 
 def test_svc_stop_and_config_while_calling(svc_image, oracle_lib):
