@@ -1211,13 +1211,15 @@ __global__ __launch_bounds__(256) void score_kernel(
     uint2 *__restrict__ ranges, uint32_t *__restrict__ hit_count, uint32_t *__restrict__ call_count,
     kgx_params prm, uint32_t want, uint32_t skip_above)
 {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_seq)
-        return;
-    const uint64_t w = wbase[s + 1] - wbase[s];
-    if (w > skip_above && w <= (uint64_t)RUN_CAP)
-        return;
-    score_sequence<PK, SB>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm, want);
+    /* grid-stride: a capped grid (KGX_SCORE_GRID_CAP) walks several
+     * sequences per lane */
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_seq; s += gridDim.x * blockDim.x) {
+        const uint64_t w = wbase[s + 1] - wbase[s];
+        if (w > skip_above && w <= (uint64_t)RUN_CAP)
+            continue;
+        score_sequence<PK, SB>(s, wbase, hit_mask, tile_windows, hot, calls, ranges, hit_count, call_count, prm,
+                               want);
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1688,8 +1690,16 @@ hipError_t launch_score(uint32_t n_seq, uint64_t n_residues, const uint64_t *wba
      * 2-record batches: fewer registers, more waves to hide the loads of
      * sequences that mostly have no hits */
     const bool small = n_residues < 64ull * n_seq;
+    /* KGX_SCORE_GRID_CAP (experiments): at most this many workgroups, each
+     * lane walking several sequences, so the scorer holds fewer wave slots
+     * beside the next batch's probe */
+    static const uint32_t grid_cap = [] {
+        const char *e = std::getenv("KGX_SCORE_GRID_CAP");
+        return e ? (uint32_t)std::max(0L, std::strtol(e, nullptr, 10)) : 0u;
+    }();
+    const dim3 sgrid(grid_cap ? std::min<uint32_t>(lanes.x, grid_cap) : lanes.x);
 #define KGX_SCORE(P, B)                                                                                          \
-    hipLaunchKernelGGL((score_kernel<P, B>), lanes, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot, \
+    hipLaunchKernelGGL((score_kernel<P, B>), sgrid, dim3(256), 0, stream, n_seq, wbase, hit_mask, tile_windows, hot, \
                        calls, static_cast<uint2 *>(ranges), hit_count, call_count, params, want, skip)
     if (pk && small)
         KGX_SCORE(true, 2);

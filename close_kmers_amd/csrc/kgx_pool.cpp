@@ -11,6 +11,7 @@
  * concatenates the per-shard CSR results in input order.  No collective.
  */
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -444,6 +445,8 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
      * for the rollup: host_chunks 1 for the call), then its rollups */
     std::vector<kgx_result> part(K, kgx_result{});
     std::vector<kgx_rollup_result> ru(K, kgx_rollup_result{});
+    static const bool timing = std::getenv("KGX_POOL_TIMING") != nullptr;
+    const auto T0 = std::chrono::steady_clock::now();
     std::vector<int> rcs(K, KGX_OK);
     std::vector<std::string> errs(K);
     p->run(K, [&](uint32_t i) {
@@ -455,11 +458,21 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
          * sets a shard's score time whatever its size) */
         if (c->host_score_variant >= 0)
             c->score_variant = c->host_score_variant;
+        const auto t0 = std::chrono::steady_clock::now();
         rcs[i] = kgx_process_batch(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want, &part[i]);
         c->host_chunks = chunks;
         c->score_variant = sv;
+        const auto t1 = std::chrono::steady_clock::now();
         if (!rcs[i])
             rcs[i] = kgx_kmap_rollup(mine[i], c, mode, &ru[i]);
+        if (timing) {
+            const auto t2 = std::chrono::steady_clock::now();
+            auto us = [&](std::chrono::steady_clock::time_point a) {
+                return std::chrono::duration<double, std::micro>(a - T0).count();
+            };
+            std::fprintf(stderr, "[pool] lookup shard %u: batch %.1f-%.1f us, rollup -%.1f us\n", i, us(t0), us(t1),
+                         us(t2));
+        }
         if (rcs[i])
             errs[i] = kgx_last_error();
     });

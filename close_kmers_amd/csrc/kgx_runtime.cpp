@@ -3241,19 +3241,30 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     HIP_TRY(c->h_plan_status.resize(1));
     HIP_TRY(c->h_nwin.resize(1));
     c->h_plan_status[0] = 0;
+    /* the small results by device stores into the mapped pinned arrays, not
+     * by DMA: copies from every stream share the DMA engine in order, so a
+     * few KB of counts queued behind other contexts' MB uploads (r5m: four
+     * /lookup shards' collects all returned with the last shard's upload) */
+    auto d2h = [&](auto &vec, const void *src, size_t bytes) -> hipError_t {
+        void *d = nullptr;
+        const hipError_t e = vec.device_ptr(0, &d);
+        return e != hipSuccess ? e : launch_copy_to_host(d, src, bytes, 64, c->stream);
+    };
     if (c->plan_status.p)
-        HIP_TRY(hipMemcpyAsync(c->h_plan_status.data(), c->plan_status.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                               c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_nwin.data(), c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(d2h(c->h_plan_status, c->plan_status.p, sizeof(uint32_t)));
+    HIP_TRY(d2h(c->h_nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t)));
     if (n_seq) {
-        HIP_TRY(hipMemcpyAsync(c->h_hcount.data(), c->hit_count.p, n_seq * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->h_ccount.data(), c->call_count.p, n_seq * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(d2h(c->h_hcount, c->hit_count.p, n_seq * sizeof(uint32_t)));
+        HIP_TRY(d2h(c->h_ccount, c->call_count.p, n_seq * sizeof(uint32_t)));
         if (want_otu)
-            HIP_TRY(hipMemcpyAsync(c->h_ocount.data(), c->otu_count.p, n_seq * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(d2h(c->h_ocount, c->otu_count.p, n_seq * sizeof(uint32_t)));
+    }
+    /* nothing to gather (the /lookup shape: hits stay on the device): the
+     * best calls come in the same round trip */
+    const bool best_now = want_best && n_seq && !need_hits && !want_calls && !want_otu;
+    if (best_now) {
+        HIP_TRY(c->h_best.resize(n_seq));
+        HIP_TRY(d2h(c->h_best, c->best.p, n_seq * sizeof(kgx_best_call)));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->h_plan_status[0])
@@ -3320,12 +3331,13 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                                        hipMemcpyDeviceToHost, c->stream));
         }
     }
-    if (want_best && n_seq) {
+    if (want_best && n_seq && !best_now) {
         HIP_TRY(c->h_best.resize(n_seq));
         HIP_TRY(hipMemcpyAsync(c->h_best.data(), c->best.p, n_seq * sizeof(kgx_best_call), hipMemcpyDeviceToHost,
                                c->stream));
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!best_now)
+        HIP_TRY(hipStreamSynchronize(c->stream));
     tm.mark(" gather+d2h");
     fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
     return KGX_OK;

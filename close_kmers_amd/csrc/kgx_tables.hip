@@ -1022,7 +1022,12 @@ int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
     HIP_TRY(r.tmp.reserve(tb));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
                                              (int)(nt + 1), st));
-    HIP_TRY(hipMemcpyAsync(r.h_n.data(), r.tbase.as<uint64_t>() + nt, 8, hipMemcpyDeviceToHost, st));
+    {   /* the event total by a device store into mapped memory: a DMA copy
+         * would queue behind other contexts' uploads */
+        void *dn = nullptr;
+        HIP_TRY(r.h_n.device_ptr(0, &dn));
+        HIP_TRY(launch_copy_to_host(dn, r.tbase.as<uint64_t>() + nt, 8, 1, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
     const uint64_t E = r.h_n[0];
     out->n_events = E;
