@@ -290,9 +290,34 @@ hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *
  * both 16-byte aligned */
 hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count, uint64_t cap,
                                uint32_t elem_bytes, int blocks, hipStream_t stream);
-/* *flag_mapped = 1 when a byte of d[0, n) is 0 (d 16-byte aligned) */
-hipError_t launch_nul_scan(const uint8_t *d, uint64_t n, uint32_t *flag_mapped, hipStream_t stream);
+/* *flag_mapped = 1 when a byte of d[skip, n) is 0 (d 16-byte aligned) */
+hipError_t launch_nul_scan(const uint8_t *d, uint64_t skip, uint64_t n, uint32_t *flag_mapped, hipStream_t stream);
+
 /* device stores of bytes (4-aligned) from HBM into mapped pinned host memory */
+/* up to kMax copies device -> mapped host memory in one launch; add() takes
+ * byte counts (4-B aligned; 16-B aligned spans copy by 16 B) */
+struct CopySpans {
+    static constexpr int kMax = 8;
+    void *dst[kMax];
+    const void *src[kMax];
+    uint64_t n[kMax];
+    bool v16[kMax];
+    int count = 0;
+    void add(void *d, const void *s, uint64_t bytes)
+    {
+        if (bytes == 0)
+            return;
+        if (count == kMax) {
+            count = kMax + 1; /* refused by launch_copy_spans */
+            return;
+        }
+        dst[count] = d;
+        src[count] = s;
+        n[count] = bytes;
+        count++;
+    }
+};
+hipError_t launch_copy_spans(CopySpans spans, int copy_blocks, hipStream_t stream);
 hipError_t launch_copy_to_host(void *dst_mapped, const void *src, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_random_read(const void *buffer, uint64_t bytes, uint64_t threads,
                               uint32_t rounds, int mode, int ilp, uint64_t *sink, hipStream_t stream);

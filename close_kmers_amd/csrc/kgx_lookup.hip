@@ -2311,11 +2311,12 @@ hipError_t launch_copy_counted(void *dst, const void *src, const uint64_t *count
     return hipGetLastError();
 }
 
-/* any NUL among bytes [0, n) of d -> *flag = 1 (a store into mapped host
+/* any NUL among bytes [skip, n) of d -> *flag = 1 (a store into mapped host
  * memory).  Residues the device reads straight from the caller's pinned
  * buffer are not NUL-cut on the host (gather_hits' strlen bound, kguts.cc:792),
  * so the host path checks them here and reruns a batch that has one. */
-__global__ __launch_bounds__(256) void nul_scan_kernel(const uint4 *__restrict__ d, uint64_t n, uint32_t *flag)
+__global__ __launch_bounds__(256) void nul_scan_kernel(const uint4 *__restrict__ d, uint64_t skip, uint64_t n,
+                                                       uint32_t *flag)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t n16 = n / 16;
@@ -2323,25 +2324,30 @@ __global__ __launch_bounds__(256) void nul_scan_kernel(const uint4 *__restrict__
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
         const uint4 v = d[i];
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        for (int j = 0; j < 4; j++)
-            nul |= ((w[j] - 0x01010101u) & ~w[j] & 0x80808080u) != 0;
+        if (16 * i >= skip) {
+            for (int j = 0; j < 4; j++)
+                nul |= ((w[j] - 0x01010101u) & ~w[j] & 0x80808080u) != 0;
+        } else { /* the first word: bytes before skip are not the batch's */
+            for (int b = 0; b < 16; b++)
+                nul |= 16 * i + b >= skip && ((w[b / 4] >> (8 * (b % 4))) & 0xFFu) == 0;
+        }
     }
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid < n - 16 * n16)
+    if (tid < n - 16 * n16 && 16 * n16 + tid >= skip)
         nul |= reinterpret_cast<const uint8_t *>(d)[16 * n16 + tid] == 0;
     if (__ballot(nul) && lane_id() == 0)
         __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_nul_scan(const uint8_t *d, uint64_t n, uint32_t *flag_mapped, hipStream_t stream)
+hipError_t launch_nul_scan(const uint8_t *d, uint64_t skip, uint64_t n, uint32_t *flag_mapped, hipStream_t stream)
 {
-    if (n == 0)
+    if (n <= skip)
         return hipSuccess;
     if ((uintptr_t)d % 16 != 0)
         return hipErrorInvalidValue;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((n / 16 + 255) / 256 + 1, 1024);
-    hipLaunchKernelGGL(nul_scan_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const uint4 *>(d), n,
-                       flag_mapped);
+    hipLaunchKernelGGL(nul_scan_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const uint4 *>(d), skip,
+                       n, flag_mapped);
     return hipGetLastError();
 }
 
@@ -2385,6 +2391,47 @@ hipError_t launch_copy_to_host(void *dst, const void *src, uint64_t bytes, int c
     else
         hipLaunchKernelGGL(copy4_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint32_t *>(dst),
                            static_cast<const uint32_t *>(src), n);
+    return hipGetLastError();
+}
+
+/* several spans in one launch (blockIdx.y = span): a collect's counts, totals
+ * and best calls cost one kernel instead of five back-to-back ones */
+__global__ __launch_bounds__(256) void copy_spans_kernel(CopySpans sp)
+{
+    const uint32_t k = blockIdx.y;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sp.v16[k]) {
+        uint4 *d = static_cast<uint4 *>(sp.dst[k]);
+        const uint4 *s = static_cast<const uint4 *>(sp.src[k]);
+        for (uint64_t i = i0; i < sp.n[k]; i += stride)
+            d[i] = s[i];
+    } else {
+        uint32_t *d = static_cast<uint32_t *>(sp.dst[k]);
+        const uint32_t *s = static_cast<const uint32_t *>(sp.src[k]);
+        for (uint64_t i = i0; i < sp.n[k]; i += stride)
+            d[i] = s[i];
+    }
+}
+
+hipError_t launch_copy_spans(CopySpans sp, int copy_blocks, hipStream_t stream)
+{
+    if (sp.count == 0)
+        return hipSuccess;
+    if (sp.count > CopySpans::kMax)
+        return hipErrorInvalidValue;
+    uint64_t most = 1;
+    for (int k = 0; k < sp.count; k++) {
+        const uintptr_t d = reinterpret_cast<uintptr_t>(sp.dst[k]), s = reinterpret_cast<uintptr_t>(sp.src[k]);
+        const uint64_t bytes = sp.n[k];
+        sp.v16[k] = d % 16 == 0 && s % 16 == 0 && bytes % 16 == 0;
+        if (!sp.v16[k] && ((d | s | bytes) % 4 != 0))
+            return hipErrorInvalidValue;
+        sp.n[k] = sp.v16[k] ? bytes / 16 : bytes / 4;
+        most = std::max(most, sp.n[k]);
+    }
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((most + 255) / 256, (uint64_t)copy_blocks);
+    hipLaunchKernelGGL(copy_spans_kernel, dim3(blocks, (uint32_t)sp.count), dim3(256), 0, stream, sp);
     return hipGetLastError();
 }
 

@@ -10,6 +10,8 @@
  * shards, runs shard i on context i from its own host thread, and
  * concatenates the per-shard CSR results in input order.  No collective.
  */
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -87,6 +89,10 @@ struct kgx_pool {
      * contexts of each device; /lookup's one-pass shards take twice that
      * (no twins: 4 contexts measured best, r5e) */
     uint32_t per_device = 2;
+    /* kgx_pool_lookup: per device a stream for the shards' uploads (lowest
+     * priority: a queue of its own), and an event per shard */
+    std::vector<hipStream_t> up_stream;
+    std::vector<hipEvent_t> up_done;
     std::vector<uint32_t> runners(uint32_t per) const
     {
         std::vector<uint32_t> out, used;
@@ -212,6 +218,14 @@ int kgx_pool_destroy(kgx_pool *p)
         t.join();
     for (auto *c : p->ctxs)
         kgx_ctx_destroy(c);
+    for (size_t d = 0; d < p->up_stream.size(); d++)
+        if (p->up_stream[d]) {
+            (void)hipSetDevice((int)d);
+            (void)hipStreamSynchronize(p->up_stream[d]);
+            (void)hipStreamDestroy(p->up_stream[d]);
+        }
+    for (hipEvent_t e : p->up_done)
+        (void)hipEventDestroy(e);
     delete p;
     return KGX_OK;
 }
@@ -449,22 +463,67 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
     const auto T0 = std::chrono::steady_clock::now();
     std::vector<int> rcs(K, KGX_OK);
     std::vector<std::string> errs(K);
-    p->run(K, [&](uint32_t i) {
+    /* every shard's upload and pass enqueued from this thread, in shard
+     * order: the uploads one after another at the link's full rate on the
+     * device's upload stream, each shard's pass behind its own upload (an
+     * event), and a hardware queue shared by two shards' streams holds them
+     * in shard order, so no shard's kernels wait behind a later shard's
+     * upload (r5q: per-shard threads enqueueing at once left shard 0's probe
+     * behind shard 2's upload).  Each shard's rollup follows its pass on the
+     * context's stream (sized by the context's previous rollup); the collects
+     * and the rollups' checks then run on the pool's threads. */
+    while (p->up_done.size() < K) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->up_done.push_back(e);
+    }
+    for (uint32_t i = 0; i < K; i++) {
         kgx_ctx *c = p->ctxs[run[i]];
-        const int chunks = c->host_chunks, sv = c->score_variant;
-        c->host_chunks = 1;
+        const int dev = kgx_image_device(c->img);
+        HIP_TRY(hipSetDevice(dev));
+        if ((int)p->up_stream.size() <= dev)
+            p->up_stream.resize((size_t)dev + 1, nullptr);
+        if (!p->up_stream[(size_t)dev]) {
+            int least = 0, greatest = 0;
+            hipStream_t st = nullptr;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) {
+                (void)hipGetLastError();
+                HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            }
+            p->up_stream[(size_t)dev] = st;
+        }
         /* a shard's sequences on the host path's scorer (option
-         * host_score_variant: the wave scorer; the lane scorer's longest chain
-         * sets a shard's score time whatever its size) */
+         * host_score_variant: the wave scorer; the lane scorer's longest
+         * chain sets a shard's score time whatever its size) */
+        const int sv = c->score_variant;
         if (c->host_score_variant >= 0)
             c->score_variant = c->host_score_variant;
-        const auto t0 = std::chrono::steady_clock::now();
-        rcs[i] = kgx_process_batch(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want, &part[i]);
-        c->host_chunks = chunks;
+        rcs[i] = one_pass_enqueue(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want,
+                                  p->up_stream[(size_t)dev], p->up_done[i]);
         c->score_variant = sv;
-        const auto t1 = std::chrono::steady_clock::now();
         if (!rcs[i])
-            rcs[i] = kgx_kmap_rollup(mine[i], c, mode, &ru[i]);
+            rcs[i] = collect_counts_enqueue(c, want);
+        if (!rcs[i])
+            rcs[i] = rollup_enqueue(mine[i], c, mode);
+        if (rcs[i]) {
+            errs[i] = kgx_last_error();
+            /* the shards enqueued so far still run: drain them before returning */
+            for (uint32_t j = 0; j < i; j++)
+                (void)kgx_ctx_synchronize(p->ctxs[run[j]]);
+            return fail(rcs[i], "pool lookup shard " + std::to_string(i) + ": " + errs[i]);
+        }
+    }
+    p->run(K, [&](uint32_t i) {
+        kgx_ctx *c = p->ctxs[run[i]];
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t reruns = c->nul_reruns;
+        rcs[i] = one_pass_collect(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want, &part[i]);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (!rcs[i] && c->nul_reruns != reruns) /* the pass ran again, staged: so does its rollup */
+            rcs[i] = rollup_enqueue(mine[i], c, mode);
+        if (!rcs[i])
+            rcs[i] = rollup_finish(mine[i], c, mode, &ru[i]);
         if (timing) {
             const auto t2 = std::chrono::steady_clock::now();
             auto us = [&](std::chrono::steady_clock::time_point a) {

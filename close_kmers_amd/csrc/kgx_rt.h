@@ -137,7 +137,15 @@ inline uint64_t windows_of(uint64_t len) { return len >= 9 ? len - 8 : 0; }
 
 /* [p, p + n) lies in one pinned, device-mapped host allocation (kgx_host_alloc,
  * hipHostMalloc, hipHostRegister): the device may read it by DMA directly */
-bool host_pinned_range(const void *p, uint64_t n);
+bool host_pinned_range(const void *p, uint64_t n, const void **device_address = nullptr);
+
+/* one pass over a whole host batch, split into enqueue and collect
+ * (kgx_runtime.cpp): the upload by pull kernels on `up` (recording up_done)
+ * when given, else on the context's stream */
+int one_pass_enqueue(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done);
+int one_pass_collect(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                     uint32_t n_seq, uint32_t want, kgx_result *out);
 
 /* host CPUs this process may keep busy: the affinity mask, capped by a
  * cgroup v2 quota (cpu.max) -- on the GPU box the mask shows the whole
@@ -278,15 +286,26 @@ void svc_shutdown(kgx_image *img);
  * goes: a call arriving meanwhile waits for it before it starts a new
  * service, so no instance is created over a table being replaced */
 std::unique_lock<std::mutex> svc_shutdown_hold(kgx_image *img);
+/* kgx_kmap_rollup in two steps: the device work enqueued on c's stream (no
+ * host wait once an earlier rollup on c gave a size), then the wait, the size
+ * check (passes 2-3 again when short) and the result */
+int rollup_enqueue(kgx_kmap *m, kgx_ctx *c, int mode);
+/* kgx_device_batch_collect's counts (and best calls) round trip enqueued on
+ * c's stream ahead of the collect, which then only waits */
+int collect_counts_enqueue(kgx_ctx *c, uint32_t want);
+int rollup_finish(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out);
 
 /* kgx_kmap_rollup's device scratch and host results (kgx_tables.hip), per
  * context: grow-only, no allocation per call once warm */
 struct RollupScratch {
-    DevBuf tcount, tbase, hseq, hstart, hlen, eoff, key, key2, idx, idx2, ew, flag, rowdata, rows, rowcnt, rowoff,
-        nsel, tmp;
+    DevBuf tcount, tbase, hseq, hstart, hlen, sfirst, send, ev_id, ev_w, flag, rowdata, rows2, rowcnt, rowoff, tmp;
     PinnedVec<uint64_t> h_n; /* [0] hits, [1] events, [2] rows */
     PinnedVec<uint64_t> h_off;
     PinnedVec<kgx_rollup_row> h_rows;
+    uint64_t hint = 0;          /* the previous rollup's event count: the next one's size */
+    uint64_t cap = 0;           /* the enqueued rollup's event capacity (0: not yet sized) */
+    uint64_t presize_misses = 0;
+    bool enqueued = false;
 };
 
 }  // namespace kgx
@@ -452,7 +471,9 @@ struct kgx_ctx {
      * buffer, with no staging copy on the host; a device scan flags NUL bytes
      * (the host-side strlen cut, kguts.cc:792) and such a batch reruns staged */
     int pinned_input = 1;
+    bool one_pass_pinned = false; /* the enqueued one-pass batch reads caller-pinned residues */
     uint64_t pinned_batches = 0, nul_reruns = 0;
+    uint32_t counts_enqueued = 0; /* want + 1 of an enqueued collect_counts_enqueue, else 0 */
     kgx::PinnedVec<uint32_t> h_nul;
     std::vector<hipEvent_t> chunk_h2d; /* per chunk: its staged residues are on the device */
     kgx::DevBuf dense_counts, cscan_ws;

@@ -67,7 +67,7 @@ struct PhaseTimer {
 }  // namespace kgx
 
 /* [p, p + n) lies in one pinned, device-mapped host allocation */
-bool kgx::host_pinned_range(const void *p, uint64_t n)
+bool kgx::host_pinned_range(const void *p, uint64_t n, const void **device_address)
 {
     if (!p || n == 0)
         return false;
@@ -78,8 +78,11 @@ bool kgx::host_pinned_range(const void *p, uint64_t n)
         (void)hipGetLastError(); /* an unregistered pointer is not an error here */
         return false;
     }
-    return static_cast<const char *>(b.devicePointer) - static_cast<const char *>(a.devicePointer) ==
-           (std::ptrdiff_t)(n - 1);
+    const bool one = static_cast<const char *>(b.devicePointer) - static_cast<const char *>(a.devicePointer) ==
+                     (std::ptrdiff_t)(n - 1);
+    if (one && device_address)
+        *device_address = a.devicePointer;
+    return one;
 }
 
 
@@ -1220,6 +1223,7 @@ int plan_reserve(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n_r
     c->tile_windows = tile_windows;
     c->hit_slots = cap_win;
     c->d_off = d_off;
+    c->counts_enqueued = 0;
     c->have_hits = false;
     c->have_best = false;
     c->have_otus = false;
@@ -1738,6 +1742,149 @@ int expand_chunk(const kgx_hit_chunk &ch, const uint64_t *hoff, const char *resi
 }  // namespace kgx
 }  // extern "C++"
 
+extern "C++" {
+namespace kgx {
+
+/* kgx_device_batch_collect's first round trip, enqueued: the plan status,
+ * window total and per-sequence counts (and, when nothing needs gathering --
+ * the /lookup shape, hits staying on the device -- the best calls) by device
+ * stores into the mapped pinned arrays, not by DMA: copies from every stream
+ * share the DMA engine in order, so a few KB of counts queued behind other
+ * contexts' MB uploads (r5m).  A pool enqueues these right behind each
+ * shard's pass, so they do not wait in a shared hardware queue behind a later
+ * shard's work (r5s). */
+int collect_counts_enqueue(kgx_ctx *c, uint32_t want)
+{
+    const bool want_calls = (want & KGX_WANT_CALLS) != 0;
+    const bool want_otu = (want & KGX_WANT_OTU) != 0;
+    const bool need_hits = (want & KGX_WANT_HITS) != 0;
+    const bool want_best = (want & KGX_WANT_BEST) != 0;
+    const uint32_t n_seq = c->n_seq;
+    HIP_TRY(hipSetDevice(c->img->device));
+    HIP_TRY(c->h_hcount.resize(n_seq + 1));
+    HIP_TRY(c->h_ccount.resize(n_seq + 1));
+    HIP_TRY(c->h_ocount.resize(n_seq + 1));
+    HIP_TRY(c->h_plan_status.resize(1));
+    HIP_TRY(c->h_nwin.resize(1));
+    c->h_plan_status[0] = 0;
+    CopySpans sp; /* one launch for all of them */
+    auto d2h = [&](auto &vec, const void *src, size_t bytes) -> hipError_t {
+        void *d = nullptr;
+        const hipError_t e = vec.device_ptr(0, &d);
+        if (e == hipSuccess)
+            sp.add(d, src, bytes);
+        return e;
+    };
+    if (c->plan_status.p)
+        HIP_TRY(d2h(c->h_plan_status, c->plan_status.p, sizeof(uint32_t)));
+    HIP_TRY(d2h(c->h_nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t)));
+    if (n_seq) {
+        HIP_TRY(d2h(c->h_hcount, c->hit_count.p, n_seq * sizeof(uint32_t)));
+        HIP_TRY(d2h(c->h_ccount, c->call_count.p, n_seq * sizeof(uint32_t)));
+        if (want_otu)
+            HIP_TRY(d2h(c->h_ocount, c->otu_count.p, n_seq * sizeof(uint32_t)));
+    }
+    if (want_best && n_seq && !need_hits && !want_calls && !want_otu) {
+        HIP_TRY(c->h_best.resize(n_seq));
+        HIP_TRY(d2h(c->h_best, c->best.p, n_seq * sizeof(kgx_best_call)));
+    }
+    HIP_TRY(launch_copy_spans(sp, 64, c->stream));
+    c->counts_enqueued = want + 1;
+    return KGX_OK;
+}
+
+/* One pass over a whole host batch, split so that a pool can enqueue its
+ * shards in order from one thread and collect them on several: the staging
+ * (or, for residues in the caller's pinned memory, nothing) and the upload by
+ * pull kernels -- on `up` with `up_done` recorded, which the context's stream
+ * waits for, when given, else on the context's stream -- then the device pass
+ * (plan, probe, score).  A caller-pinned batch is NUL-scanned on the device. */
+int one_pass_enqueue(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done)
+{
+    const uint64_t r0 = n_seq ? seq_offsets[0] : 0, n_res = n_seq ? seq_offsets[n_seq] - r0 : 0;
+    /* the residues to copy: the caller's pinned buffer, or our staging */
+    const void *src = residues + r0;
+    const bool pin = c->pinned_input && host_pinned_range(residues + r0, n_res);
+    c->one_pass_pinned = pin;
+    if (pin) {
+        HIP_TRY(c->h_off_stage.resize(n_seq + 1));
+        stage_offsets_into(c->h_off_stage.data(), seq_offsets, 0, n_seq);
+        c->pinned_batches++;
+    } else {
+        HostPool *sp = nullptr;
+        if (c->stage_threads > 1 && n_res >= (1u << 20)) {
+            if (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads)
+                c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
+            sp = c->stage_pool.get();
+        }
+        if (int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq, sp))
+            return rc;
+        src = c->h_res.data();
+    }
+    /* up by DMA, the small copy first (the DMA engine serves every stream in
+     * order).  With `up` the copies go on that stream and the context's
+     * stream waits for an event: a pool enqueues its shards' uploads on one
+     * such stream and their passes in shard order, so a hardware queue shared
+     * by two shards' streams never holds a shard's kernels behind a later
+     * shard's upload (r5o: per-shard threads uploading on their own streams
+     * at once did).  Uploads by kernels reading the mapped memory instead
+     * measured worse: the device's PCIe reads held up the other shards'
+     * kernels (r5q/r5r: a 10-us plan kernel took 140 us beside them). */
+    HIP_TRY(c->residues.reserve(n_res + 16));
+    HIP_TRY(c->offsets.reserve((n_seq + 1) * sizeof(uint64_t)));
+    hipStream_t us = up ? up : c->stream;
+    HIP_TRY(hipMemcpyAsync(c->offsets.p, c->h_off_stage.data(), (n_seq + 1) * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, us));
+    if (n_res)
+        HIP_TRY(hipMemcpyAsync(c->residues.p, src, n_res, hipMemcpyHostToDevice, us));
+    if (up) {
+        HIP_TRY(hipEventRecord(up_done, up));
+        HIP_TRY(hipStreamWaitEvent(c->stream, up_done, 0));
+    }
+    if (pin) {
+        HIP_TRY(c->h_nul.resize(1));
+        c->h_nul[0] = 0;
+        void *dn = nullptr;
+        HIP_TRY(c->h_nul.device_ptr(0, &dn));
+        HIP_TRY(launch_nul_scan(c->residues.as<uint8_t>(), 0, n_res, static_cast<uint32_t *>(dn), c->stream));
+    }
+    /* on the wave scorer, the host knows whether any sequence needs the lane
+     * machine's long-sequence pass (score_long): usually none does */
+    const int variant = c->score_variant;
+    if (c->score_variant == SCORE_WAVE) {
+        uint64_t longest = 0;
+        for (uint32_t s = 0; s < n_seq; s++)
+            longest = std::max(longest, seq_offsets[s + 1] - seq_offsets[s]);
+        if (windows_of(longest) <= (uint64_t)RUN_CAP)
+            c->score_variant = SCORE_WAVE_ONLY;
+    }
+    const int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq, n_res,
+                                  want, nullptr);
+    c->score_variant = variant;
+    return rc;
+}
+
+/* the enqueued pass's results (kgx_device_batch_collect); a caller-pinned
+ * batch whose scan found a NUL runs again, staged and cut at the NUL */
+int one_pass_collect(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
+                     uint32_t n_seq, uint32_t want, kgx_result *out)
+{
+    int rc = kgx_device_batch_collect(c, want, out);
+    if (!rc && c->one_pass_pinned && __atomic_load_n(&c->h_nul[0], __ATOMIC_ACQUIRE)) {
+        c->nul_reruns++;
+        c->pinned_input = 0;
+        rc = one_pass_enqueue(c, params, residues, seq_offsets, n_seq, want, nullptr, nullptr);
+        if (!rc)
+            rc = kgx_device_batch_collect(c, want, out);
+        c->pinned_input = 1;
+    }
+    return rc;
+}
+
+}  // namespace kgx
+}  // extern "C++"
+
 namespace {
 
 /* the context's own expansion (into h_hits, CSR numbering): R12 records of
@@ -1949,7 +2096,7 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
         }
         HIP_TRY(hipEventRecord(c->chunk_h2d[k], us));
         if (pin)
-            HIP_TRY(launch_nul_scan(d_res, n_res, d_nul, us));
+            HIP_TRY(launch_nul_scan(d_res, 0, n_res, d_nul, us));
         if (prof)
             HIP_TRY(hipEventRecord(c->prof_ev[4 * k + 1], us));
         if (up)
@@ -2993,65 +3140,13 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
 int process_batch_one_pass(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
                            uint32_t n_seq, uint32_t want, kgx_result *out)
 {
-    const uint64_t r0 = n_seq ? seq_offsets[0] : 0, n_res = n_seq ? seq_offsets[n_seq] - r0 : 0;
-    const bool pin = c->pinned_input && host_pinned_range(residues + r0, n_res);
     PhaseTimer tm(c);
-    if (pin) {
-        HIP_TRY(c->h_off_stage.resize(n_seq + 1));
-        stage_offsets_into(c->h_off_stage.data(), seq_offsets, 0, n_seq);
-        HIP_TRY(c->h_nul.resize(1));
-        c->h_nul[0] = 0;
-        void *dn = nullptr;
-        HIP_TRY(c->h_nul.device_ptr(0, &dn));
-        HIP_TRY(c->residues.reserve(n_res + 16));
-        HIP_TRY(c->offsets.reserve((n_seq + 1) * sizeof(uint64_t)));
-        /* the small copy first: copies from all streams share the DMA engine
-         * in order, and a context's kernels need both */
-        HIP_TRY(hipMemcpyAsync(c->offsets.p, c->h_off_stage.data(), (n_seq + 1) * sizeof(uint64_t),
-                               hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->residues.p, residues + r0, n_res, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(launch_nul_scan(c->residues.as<uint8_t>(), n_res, static_cast<uint32_t *>(dn), c->stream));
-        c->pinned_batches++;
-    } else {
-        HostPool *sp = nullptr;
-        if (c->stage_threads > 1 && n_res >= (1u << 20)) {
-            if (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads)
-                c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
-            sp = c->stage_pool.get();
-        }
-        int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq, sp);
-        if (rc || (rc = stage_upload(c)))
-            return rc;
-    }
-    tm.mark("stage");
-    /* on the wave scorer, the host knows whether any sequence needs the lane
-     * machine's long-sequence pass (score_long): usually none does */
-    struct VariantGuard {
-        kgx_ctx *c;
-        int v;
-        ~VariantGuard() { c->score_variant = v; }
-    } vg{c, c->score_variant};
-    if (c->score_variant == SCORE_WAVE) {
-        uint64_t longest = 0;
-        for (uint32_t s = 0; s < n_seq; s++)
-            longest = std::max(longest, seq_offsets[s + 1] - seq_offsets[s]);
-        if (windows_of(longest) <= (uint64_t)RUN_CAP)
-            c->score_variant = SCORE_WAVE_ONLY;
-    }
-    int rc = kgx_run_device(c, params, c->residues.as<uint8_t>(), c->offsets.as<uint64_t>(), n_seq, n_res, want,
-                            nullptr);
+    int rc = one_pass_enqueue(c, params, residues, seq_offsets, n_seq, want, nullptr, nullptr);
     if (rc)
         return rc;
-    tm.mark("device");
-    rc = kgx_device_batch_collect(c, want, out);
+    tm.mark("enqueue");
+    rc = one_pass_collect(c, params, residues, seq_offsets, n_seq, want, out);
     tm.mark("collect");
-    if (!rc && pin && __atomic_load_n(&c->h_nul[0], __ATOMIC_ACQUIRE)) {
-        /* a NUL in the caller's residues: again, staged and cut */
-        c->nul_reruns++;
-        c->pinned_input = 0;
-        rc = process_batch_one_pass(c, params, residues, seq_offsets, n_seq, want, out);
-        c->pinned_input = 1;
-    }
     return rc;
 }
 
@@ -3234,38 +3329,14 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
     const uint32_t n_seq = c->n_seq;
     /* counts -> dense CSR offsets on the host, gather on the device.  The
      * plan's status word (bad device offsets: an error, not an empty result)
-     * and the window total come back with the counts, in one round trip. */
-    HIP_TRY(c->h_hcount.resize(n_seq + 1));
-    HIP_TRY(c->h_ccount.resize(n_seq + 1));
-    HIP_TRY(c->h_ocount.resize(n_seq + 1));
-    HIP_TRY(c->h_plan_status.resize(1));
-    HIP_TRY(c->h_nwin.resize(1));
-    c->h_plan_status[0] = 0;
-    /* the small results by device stores into the mapped pinned arrays, not
-     * by DMA: copies from every stream share the DMA engine in order, so a
-     * few KB of counts queued behind other contexts' MB uploads (r5m: four
-     * /lookup shards' collects all returned with the last shard's upload) */
-    auto d2h = [&](auto &vec, const void *src, size_t bytes) -> hipError_t {
-        void *d = nullptr;
-        const hipError_t e = vec.device_ptr(0, &d);
-        return e != hipSuccess ? e : launch_copy_to_host(d, src, bytes, 64, c->stream);
-    };
-    if (c->plan_status.p)
-        HIP_TRY(d2h(c->h_plan_status, c->plan_status.p, sizeof(uint32_t)));
-    HIP_TRY(d2h(c->h_nwin, c->wbase.as<uint64_t>() + n_seq, sizeof(uint64_t)));
-    if (n_seq) {
-        HIP_TRY(d2h(c->h_hcount, c->hit_count.p, n_seq * sizeof(uint32_t)));
-        HIP_TRY(d2h(c->h_ccount, c->call_count.p, n_seq * sizeof(uint32_t)));
-        if (want_otu)
-            HIP_TRY(d2h(c->h_ocount, c->otu_count.p, n_seq * sizeof(uint32_t)));
-    }
-    /* nothing to gather (the /lookup shape: hits stay on the device): the
-     * best calls come in the same round trip */
+     * and the window total come back with the counts, in one round trip
+     * (collect_counts_enqueue, unless already enqueued). */
     const bool best_now = want_best && n_seq && !need_hits && !want_calls && !want_otu;
-    if (best_now) {
-        HIP_TRY(c->h_best.resize(n_seq));
-        HIP_TRY(d2h(c->h_best, c->best.p, n_seq * sizeof(kgx_best_call)));
+    if (c->counts_enqueued != want + 1) {
+        if (int rc = kgx::collect_counts_enqueue(c, want))
+            return rc;
     }
+    c->counts_enqueued = 0;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->h_plan_status[0])
         return fail(KGX_EINVAL, "batch offsets not monotone or spanning more than n_residues bytes "

@@ -286,160 +286,294 @@ __global__ void lookup_ids_kernel(KmapView m, const uint64_t *kmers, uint64_t n,
 /* --- /lookup rollups (kgx_kmap_rollup) ---
  * Events are the (hit, list entry) pairs of LookupRequest::on_hit
  * (lookup_request.cc:446-482), numbered in hit order, then list order: event
- * e of hit h is eoff[h] + j for list entry j.  A stable sort by (sequence,
- * id) groups each sequence's id's events with their numbers ascending, so a
- * group's f32 sum taken in sorted order is the reference's sum in hit order,
- * and its first event number is when the reference first touched the id. */
+ * e of hit h is eoff[h] + j for list entry j.  Hits are in (sequence,
+ * position) order, so a sequence's events are one contiguous range; one wave
+ * per sequence groups its events by id in LDS, summing each id's f32 weights
+ * strictly in event order (the reference's sum, hit by hit), and emits one row
+ * per id in first-touch order. */
 
-/* Pass 1, one wave per tile: for each of the tile's hits (slot tile * T + i,
- * i its rank in the tile's mask words) its sequence, list start and length
- * (0 for an unmapped k-mer); the tile's event total.  A lane takes the hit
- * whose window is its bit of the mask word, so no lane walks the bits.
- * Block tile n_tiles writes the scan's last element, 0. */
-__global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_tiles, KmapView m, uint32_t *hseq,
-                                                           uint64_t *hstart, uint32_t *hlen, uint64_t *tcount)
+constexpr uint32_t kNoEvent = 0xFFFFFFFFu;
+
+/* the wave's index in the grid, wave-uniform (scalar loads for its word) */
+__device__ __forceinline__ uint64_t wave_index()
 {
-    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    return (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+/* mask word w of a tiled result (0 past the batch's windows) and the number
+ * of hits of its tile's earlier words: hit slot = tile * T + base + rank */
+__device__ __forceinline__ uint64_t word_mask(const Tiled &t, uint64_t w, uint64_t W, uint32_t &base)
+{
+    const uint32_t J = t.T / 64;
+    const uint64_t w0 = w - w % J;
+    base = 0;
+    for (uint64_t x = w0; x < w; x++)
+        base += (uint32_t)__popcll(t.mask[x]); /* earlier words are inside the batch */
+    return 64 * w < W ? t.mask[w] : 0ull;
+}
+
+/* Pass 1, one wave per mask word (64 windows): for each of its hits (a lane
+ * takes the hit whose window is its bit) the sequence, list start and length
+ * (0 for an unmapped k-mer); the word's event total.  Wave n_words writes the
+ * scan's last element, 0; the grid also resets the sequences' event ranges
+ * and row counts for the later passes.  A wave per word, not per tile: the
+ * kernel is latency-bound (mask, record, index slot: a chain of dependent
+ * reads per hit), so it wants many small waves (r5t: four words' chains per
+ * wave at 44 VGPRs ran 150 us per 7.5M-residue shard vs 111 us for one word
+ * at a time at 20). */
+__global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_words, KmapView m, uint32_t *hseq,
+                                                           uint64_t *hstart, uint32_t *hlen, uint64_t *wcount,
+                                                           uint32_t *sfirst, uint32_t *send, uint32_t *rowcnt)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.n_seq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        sfirst[i] = kNoEvent;
+        send[i] = 0;
+        rowcnt[i] = 0;
+    }
+    const uint64_t w = wave_index();
     const uint32_t lane = lane_id();
-    if (tile >= n_tiles) {
-        if (tile == n_tiles && lane == 0)
-            tcount[n_tiles] = 0;
+    if (w >= n_words) {
+        if (w == n_words && lane == 0)
+            wcount[n_words] = 0;
         return;
     }
-    const uint32_t J = t.T / 64;
     const uint64_t W = t.wbase[t.n_seq];
-    uint32_t base = 0;
+    uint32_t base;
+    const uint64_t mw = word_mask(t, w, W, base);
     uint64_t ev = 0;
-    for (uint32_t j = 0; j < J; j++) {
-        const uint64_t w0 = 64 * (tile * J + j);
-        const uint64_t mw = w0 < W ? t.mask[tile * J + j] : 0ull;
-        if ((mw >> lane) & 1ull) {
-            const uint64_t slot = tile * t.T + base + lanes_below(mw);
-            uint64_t key;
-            uint32_t seq;
-            if (t.packed) {
-                key = HitFields<true>::key(t.hot[slot], t.hot[slot]);
-                seq = window_seq(t.wbase, t.tile_seq, tile, w0 + lane);
-            } else {
-                const uint4 h = t.cold[slot];
-                key = (uint64_t)h.y << 32 | h.x;
-                seq = h.w;
-            }
-            uint64_t a = 0, b = 0;
-            const uint64_t len = kmap_row(m, key, a, b) ? b - a : 0;
-            hseq[slot] = seq;
-            hstart[slot] = a;
-            hlen[slot] = (uint32_t)len;
-            ev += len;
+    if ((mw >> lane) & 1ull) {
+        const uint64_t tile = w / (t.T / 64);
+        const uint64_t slot = tile * t.T + base + lanes_below(mw);
+        uint64_t key;
+        uint32_t seq;
+        if (t.packed) {
+            key = HitFields<true>::key(t.hot[slot], t.hot[slot]);
+            seq = window_seq(t.wbase, t.tile_seq, tile, 64 * w + lane);
+        } else {
+            const uint4 h = t.cold[slot];
+            key = (uint64_t)h.y << 32 | h.x;
+            seq = h.w;
         }
-        base += (uint32_t)__popcll(mw);
+        uint64_t a = 0, b = 0;
+        const uint64_t len = kmap_row(m, key, a, b) ? b - a : 0;
+        hseq[slot] = seq;
+        hstart[slot] = a;
+        hlen[slot] = (uint32_t)len;
+        ev = len;
     }
     for (int o = 32; o > 0; o >>= 1)
         ev += __shfl_xor(ev, o);
     if (lane == 0)
-        tcount[tile] = ev;
+        wcount[w] = ev;
 }
 
-/* Pass 2, one wave per tile: the events of its hits, numbered from the
- * tile's scanned base in hit order, then list order: key = sequence << ib |
- * id, the event number, and the hit's weight 1.0f / (float)|list|
- * (lookup_request.cc:459) */
-template <typename K>
-__global__ __launch_bounds__(256) void rollup_events_kernel(Tiled t, uint64_t n_tiles, const uint32_t *hseq,
+/* Pass 2, one wave per mask word: the events of its hits, numbered from the
+ * word's scanned base in hit order, then list order: the id and the hit's
+ * weight 1.0f / (float)|list| (lookup_request.cc:459); each sequence's event
+ * range [sfirst, send) by one atomic per (word, sequence) at its first and
+ * last lane.  Writes nothing when the batch has more than cap events (the
+ * host runs the passes again at the true size). */
+__global__ __launch_bounds__(256) void rollup_events_kernel(Tiled t, uint64_t n_words, const uint32_t *hseq,
                                                             const uint64_t *hstart, const uint32_t *hlen,
-                                                            const uint64_t *tbase, const uint32_t *vals, uint32_t ib,
-                                                            K *key, uint32_t *idx, float *ew)
+                                                            const uint64_t *wbase_ev, const uint32_t *vals,
+                                                            uint64_t cap, uint32_t *ev_id, float *ev_w,
+                                                            uint32_t *sfirst, uint32_t *send)
 {
-    const uint64_t tile = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= n_tiles)
+    const uint64_t w = wave_index();
+    if (w >= n_words || wbase_ev[n_words] > cap)
         return;
-    uint64_t e0 = tbase[tile];
-    if (tbase[tile + 1] == e0)
+    const uint64_t e0 = wbase_ev[w];
+    if (wbase_ev[w + 1] == e0)
         return;
     const uint32_t lane = lane_id();
-    const uint32_t J = t.T / 64;
     const uint64_t W = t.wbase[t.n_seq];
-    uint32_t base = 0;
-    for (uint32_t j = 0; j < J; j++) {
-        const uint64_t w0 = 64 * (tile * J + j);
-        const uint64_t mw = w0 < W ? t.mask[tile * J + j] : 0ull;
-        if (!mw)
-            continue;
-        uint64_t len = 0, a = 0;
-        uint32_t seq = 0;
-        if ((mw >> lane) & 1ull) {
-            const uint64_t slot = tile * t.T + base + lanes_below(mw);
-            len = hlen[slot];
-            a = hstart[slot];
-            seq = hseq[slot];
+    uint32_t base;
+    const uint64_t mw = word_mask(t, w, W, base);
+    uint64_t len = 0, a = 0;
+    uint32_t seq = 0;
+    if ((mw >> lane) & 1ull) {
+        const uint64_t slot = (w / (t.T / 64)) * t.T + base + lanes_below(mw);
+        len = hlen[slot];
+        a = hstart[slot];
+        seq = hseq[slot];
+    }
+    uint64_t incl = len;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t v = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o)
+            incl += v;
+    }
+    const uint64_t e = e0 + incl - len;
+    if (len) {
+        const float wt = 1.0f / (float)len;
+        for (uint64_t q = 0; q < len; q++) {
+            ev_id[e + q] = vals[a + q];
+            ev_w[e + q] = wt;
         }
-        uint64_t incl = len;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t v = __shfl_up(incl, o);
-            if (lane >= (uint32_t)o)
-                incl += v;
-        }
-        const uint64_t e = e0 + incl - len;
-        if (len) {
-            const float w = 1.0f / (float)len;
-            const K hi = (K)seq << ib;
-            for (uint64_t q = 0; q < len; q++) {
-                key[e + q] = hi | (K)vals[a + q];
-                idx[e + q] = (uint32_t)(e + q);
-                ew[e + q] = w;
-            }
-        }
-        e0 += __shfl(incl, 63);
-        base += (uint32_t)__popcll(mw);
+    }
+    /* the lanes with events: each one's neighbours among them */
+    const uint64_t act = __ballot(len != 0);
+    const uint64_t below = act & ((1ull << lane) - 1ull);
+    const uint64_t above = lane == 63 ? 0ull : act & ~((2ull << lane) - 1ull);
+    const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+    const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : lane;
+    const uint32_t pseq = __shfl(seq, (int)prev), nseq = __shfl(seq, (int)next);
+    if (len) {
+        if (!below || pseq != seq)
+            atomicMin(sfirst + seq, (uint32_t)e);
+        if (!above || nseq != seq)
+            atomicMax(send + seq, (uint32_t)(e + len));
     }
 }
 
-/* one thread per (sequence, id) group, at its first sorted event: the
- * group's counts and its weights summed in event order (8 events' loads in
- * flight at a time, the adds strictly in order), stored at the first event's
- * number (flagged), and one more row for its sequence */
-template <typename K>
-__global__ void rollup_groups_kernel(uint64_t n_ev, const K *key, const uint32_t *idx, const float *ew, uint32_t ib,
-                                     int family, uint8_t *flag, uint4 *rowdata, uint32_t *rowcnt)
+/* Pass 3, one wave per sequence: its events [sfirst, send) in chunks of 64.
+ * Per chunk, the distinct ids one at a time, lowest lane first (ballot): the
+ * id's table entry in LDS is found or added (first event = that lane's), and
+ * its lanes' weights are added to the entry's f32 sum in lane order -- so
+ * every sum is taken in event order, as the reference adds them hit by hit,
+ * and entries are added in first-touch order.  Rows go to rows2[sfirst + q]
+ * for the q-th entry.  A sequence with more distinct ids than one table pass
+ * holds is taken in P id classes, each class's rows placed at their first
+ * event's position (flag, rowdata) and compacted in event order after. */
+constexpr uint32_t kRollH = 256;    /* LDS table slots per wave */
+constexpr uint32_t kRollFill = 192; /* ids per table pass */
+
+__device__ __forceinline__ uint32_t roll_hash(uint32_t id) { return (id * 0x9E3779B1u) >> 24; }
+__device__ __forceinline__ uint32_t roll_class(uint32_t id, uint32_t P) { return ((id * 0x85EBCA6Bu) >> 13) & (P - 1); }
+
+__global__ __launch_bounds__(256) void rollup_group_kernel(uint32_t n_seq, const uint32_t *sfirst,
+                                                           const uint32_t *send, const uint32_t *ev_id,
+                                                           const float *ev_w, int family, const uint64_t *n_events,
+                                                           uint64_t cap, uint8_t *flag, uint4 *rowdata, uint4 *rows2,
+                                                           uint32_t *rowcnt)
 {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_ev)
+    __shared__ uint32_t hk[4][kRollH], hc[4][kRollH], hf[4][kRollH], hl[4][kRollFill];
+    __shared__ float hw[4][kRollH];
+    const uint32_t wv = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t s = blockIdx.x * 4 + wv;
+    if (s >= n_seq || *n_events > cap)
         return;
-    const K k = key[p];
-    if (p > 0 && key[p - 1] == k)
+    const uint32_t f = sfirst[s], l = send[s];
+    if (f == kNoEvent || l <= f) {
+        if (lane == 0)
+            rowcnt[s] = 0;
         return;
-    uint32_t cnt = 0;
-    float ws = 0.0f;
-    for (uint64_t q = p;; q += 8) {
-        K kk[8];
-        uint32_t ii[8];
-        float ww[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint64_t r = q + u < n_ev ? q + u : n_ev - 1; /* clamped: every load is issued */
-            kk[u] = key[r];
-            ii[u] = idx[r];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            ww[u] = ew[ii[u]];
-        bool more = true;
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            more = more && q + u < n_ev && kk[u] == k;
-            if (more) {
-                ws += ww[u]; /* s.weighted_total += weight, hit by hit */
-                cnt++;
-            }
-        }
-        if (!more)
-            break;
     }
-    const uint32_t first = idx[p];
-    const uint32_t id = (uint32_t)((uint64_t)k & ((1ull << ib) - 1));
-    flag[first] = 1;
-    rowdata[first] = family ? make_uint4(id, cnt, cnt, __float_as_uint(ws)) : make_uint4(id, cnt, 0u, 0u);
-    atomicAdd(rowcnt + (uint32_t)((uint64_t)k >> ib), 1u);
+    uint32_t *K = hk[wv], *C = hc[wv], *F = hf[wv], *L = hl[wv];
+    float *Wt = hw[wv];
+    auto row = [&](uint32_t h) {
+        return family ? make_uint4(K[h], C[h], C[h], __float_as_uint(Wt[h])) : make_uint4(K[h], C[h], 0u, 0u);
+    };
+    uint32_t P = 1, nrows = 0;
+    for (;;) {
+        bool ok = true;
+        for (uint32_t p = 0; p < P && ok; p++) {
+            for (uint32_t i = lane; i < kRollH; i += 64)
+                K[i] = NO_ID;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t used = 0;
+            for (uint32_t e = f; e < l && ok; e += 64) {
+                const uint32_t i = e + lane;
+                const bool valid = i < l;
+                const uint32_t id = valid ? ev_id[i] : NO_ID;
+                const float w = valid ? ev_w[i] : 0.0f;
+                const bool mine = valid && roll_class(id, P) == p;
+                uint64_t rem = __ballot(mine);
+                while (rem) {
+                    const uint32_t ld = (uint32_t)__builtin_ctzll(rem);
+                    const uint32_t lid = (uint32_t)__builtin_amdgcn_readlane((int)id, (int)ld);
+                    const uint64_t grp = __ballot(mine && id == lid);
+                    rem &= ~grp;
+                    uint32_t h = roll_hash(lid);
+                    uint32_t kh;
+                    while ((kh = K[h]) != NO_ID && kh != lid)
+                        h = (h + 1) & (kRollH - 1);
+                    const bool fresh = kh == NO_ID;
+                    if (fresh && used == kRollFill) {
+                        ok = false; /* too many ids for one pass: classes */
+                        break;
+                    }
+                    float sum = fresh ? 0.0f : Wt[h];
+                    const uint32_t cnt = (fresh ? 0u : C[h]) + (uint32_t)__popcll(grp);
+                    for (uint64_t g = grp; g; g &= g - 1) {
+                        const int b = (int)__builtin_ctzll(g);
+                        sum += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b)); /* hit by hit */
+                    }
+                    if (lane == 0) {
+                        if (fresh) {
+                            K[h] = lid;
+                            F[h] = e + ld - f;
+                            L[used] = h;
+                        }
+                        C[h] = cnt;
+                        Wt[h] = sum;
+                    }
+                    used += fresh;
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (!ok)
+                break;
+            if (P == 1) {
+                for (uint32_t q = lane; q < used; q += 64)
+                    rows2[f + q] = row(L[q]);
+                nrows = used;
+            } else {
+                for (uint32_t q = lane; q < used; q += 64) {
+                    const uint32_t h = L[q];
+                    flag[f + F[h]] = 1;
+                    rowdata[f + F[h]] = row(h);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (ok)
+            break;
+        P *= 2;
+        for (uint32_t i = f + lane; i < l; i += 64)
+            flag[i] = 0;
+    }
+    if (P > 1) {
+        /* the classes' rows in first-event order (this wave's own stores) */
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        uint32_t rank = 0;
+        for (uint32_t e = f; e < l; e += 64) {
+            const uint32_t i = e + lane;
+            const bool fl = i < l && flag[i];
+            const uint64_t bm = __ballot(fl);
+            if (fl)
+                rows2[f + rank + lanes_below(bm)] = rowdata[i];
+            rank += (uint32_t)__popcll(bm);
+        }
+        nrows = rank;
+    }
+    if (lane == 0)
+        rowcnt[s] = nrows;
+}
+
+/* Pass 4, one wave per sequence: its rows and offset into the mapped host
+ * arrays (rows at off[s]); the last wave adds off[n] */
+__global__ __launch_bounds__(256) void rollup_emit_kernel(uint32_t n_seq, const uint32_t *sfirst,
+                                                          const uint32_t *rowcnt, const uint64_t *off,
+                                                          const uint4 *rows2, const uint64_t *n_events, uint64_t cap,
+                                                          uint4 *h_rows, uint64_t *h_off, uint64_t *h_nrows)
+{
+    const uint32_t s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = lane_id();
+    if (s > n_seq || *n_events > cap)
+        return;
+    const uint64_t o = off[s];
+    if (lane == 0) {
+        h_off[s] = o;
+        if (s == n_seq)
+            *h_nrows = o;
+    }
+    if (s == n_seq)
+        return;
+    const uint32_t c = rowcnt[s], f = sfirst[s];
+    for (uint32_t r = lane; r < c; r += 64)
+        h_rows[o + r] = rows2[f + r];
 }
 
 /* --- /matrix --- */
@@ -806,6 +940,183 @@ int upload_ids(DevBuf &d, const uint32_t *ids, uint64_t n, hipStream_t st)
 
 }  // namespace
 
+namespace kgx {
+
+namespace {
+
+/* rollup pass 1 on c's stream: per mask word its hits' sequence, list start
+ * and length per slot and its event total; the words' event bases by a scan; the
+ * total E into h_n[0] by a device store (a DMA copy would queue behind other
+ * contexts' uploads) */
+/* pass 1's buffers for c's planned batch */
+int rollup_reserve(kgx_ctx *c, RollupScratch &r)
+{
+    const uint32_t n = c->n_seq;
+    const uint64_t nt = c->max_tiles, n_slots = nt * c->tile_windows, nw = nt * (c->tile_windows / 64);
+    HIP_TRY(r.hseq.reserve(n_slots * 4));
+    HIP_TRY(r.hstart.reserve(n_slots * 8));
+    HIP_TRY(r.hlen.reserve(n_slots * 4));
+    HIP_TRY(r.tcount.reserve((nw + 1) * 8));
+    HIP_TRY(r.tbase.reserve((nw + 1) * 8));
+    HIP_TRY(r.sfirst.reserve((n + 1) * 4));
+    HIP_TRY(r.send.reserve((n + 1) * 4));
+    HIP_TRY(r.rowcnt.reserve((n + 1) * 4));
+    HIP_TRY(r.rowoff.reserve((n + 1) * 8));
+    return KGX_OK;
+}
+
+int rollup_tiles(kgx_kmap *m, kgx_ctx *c, RollupScratch &r)
+{
+    hipStream_t st = c->stream;
+    const Tiled t = tiled_of(c);
+    const uint32_t n = c->n_seq;
+    const uint64_t nt = c->max_tiles, nw = nt * (t.T / 64);
+    const KmapView view = m->view();
+    if (int rc = rollup_reserve(c, r))
+        return rc;
+    const dim3 word_grid((uint32_t)((nw + 1 + 3) / 4));
+    hipLaunchKernelGGL(rollup_tiles_kernel, word_grid, dim3(256), 0, st, t, nw, view, r.hseq.as<uint32_t>(),
+                       r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tcount.as<uint64_t>(),
+                       r.sfirst.as<uint32_t>(), r.send.as<uint32_t>(), r.rowcnt.as<uint32_t>());
+    size_t tb = 0, tb2 = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
+                                             (int)(nw + 1), st));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(r.tmp.reserve(std::max(tb, tb2)));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
+                                             (int)(nw + 1), st));
+    void *dn = nullptr;
+    HIP_TRY(r.h_n.device_ptr(0, &dn));
+    HIP_TRY(launch_copy_to_host(dn, r.tbase.as<uint64_t>() + nw, 8, 1, st));
+    return KGX_OK;
+}
+
+/* rollup passes 2-4 on c's stream, sized for `cap` events (the device's total
+ * E <= cap, else the kernels write nothing and the host runs them again at
+ * E): the events in hit order with each sequence's range, one wave per
+ * sequence grouping them by id in LDS, the rows' offsets by a scan, and the
+ * rows and offsets stored straight into the mapped host arrays */
+int rollup_rows(kgx_kmap *m, kgx_ctx *c, RollupScratch &r, int mode, uint64_t cap)
+{
+    hipStream_t st = c->stream;
+    const uint32_t n = c->n_seq;
+    const Tiled t = tiled_of(c);
+    const uint64_t nw = c->max_tiles * (t.T / 64);
+    const KmapView view = m->view();
+    const dim3 word_grid((uint32_t)((nw + 1 + 3) / 4)), seq_grid((n + 1 + 3) / 4);
+    const uint64_t *d_E = r.tbase.as<uint64_t>() + nw;
+    HIP_TRY(r.ev_id.reserve(cap * 4));
+    HIP_TRY(r.ev_w.reserve(cap * 4));
+    HIP_TRY(r.flag.reserve(cap));
+    HIP_TRY(r.rowdata.reserve(cap * 16));
+    HIP_TRY(r.rows2.reserve(cap * 16));
+    HIP_TRY(r.h_rows.resize(cap));
+    hipLaunchKernelGGL(rollup_events_kernel, word_grid, dim3(256), 0, st, t, nw, r.hseq.as<uint32_t>(),
+                       r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tbase.as<uint64_t>(), view.vals, cap,
+                       r.ev_id.as<uint32_t>(), r.ev_w.as<float>(), r.sfirst.as<uint32_t>(), r.send.as<uint32_t>());
+    hipLaunchKernelGGL(rollup_group_kernel, seq_grid, dim3(256), 0, st, n, r.sfirst.as<uint32_t>(),
+                       r.send.as<uint32_t>(), r.ev_id.as<uint32_t>(), r.ev_w.as<float>(),
+                       mode == KGX_ROLLUP_FAMILY ? 1 : 0, d_E, cap, r.flag.as<uint8_t>(), r.rowdata.as<uint4>(),
+                       r.rows2.as<uint4>(), r.rowcnt.as<uint32_t>());
+    size_t tb = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    HIP_TRY(r.tmp.reserve(tb));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
+                                             (int)(n + 1), st));
+    void *d_rows = nullptr, *d_off = nullptr, *d_n = nullptr;
+    HIP_TRY(r.h_rows.device_ptr(0, &d_rows));
+    HIP_TRY(r.h_off.device_ptr(0, &d_off));
+    HIP_TRY(r.h_n.device_ptr(1, &d_n));
+    hipLaunchKernelGGL(rollup_emit_kernel, seq_grid, dim3(256), 0, st, n, r.sfirst.as<uint32_t>(),
+                       r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(), r.rows2.as<uint4>(), d_E, cap,
+                       static_cast<uint4 *>(d_rows), static_cast<uint64_t *>(d_off), static_cast<uint64_t *>(d_n));
+    HIP_TRY(hipGetLastError());
+    return KGX_OK;
+}
+
+}  // namespace
+
+/* The rollup enqueued behind the context's pass with no host wait when the
+ * context's previous rollup gave an event count to size it by (that count +
+ * 1/8); rollup_finish checks the size and runs passes 2-3 again when the
+ * batch had more events.  A pool enqueues each shard's rollup right after its
+ * pass, so no rollup waits in a hardware queue behind later shards' kernels
+ * for a host round trip (r5r: rollups at the end of the call, 0.5 ms). */
+int rollup_enqueue(kgx_kmap *m, kgx_ctx *c, int mode)
+{
+    if (!m || (mode != KGX_ROLLUP_PEG && mode != KGX_ROLLUP_FAMILY))
+        return fail(KGX_EINVAL, "bad kmap_rollup arguments");
+    int rc = check_ctx_hits(c);
+    if (rc)
+        return rc;
+    if (c->img->device != m->device)
+        return fail(KGX_EINVAL, "kmap and context are on different devices");
+    HIP_TRY(hipSetDevice(m->device));
+    if (!c->rollup)
+        c->rollup.reset(new RollupScratch);
+    RollupScratch &r = *c->rollup;
+    const uint32_t n = c->n_seq;
+    HIP_TRY(r.h_off.resize(n + 1));
+    HIP_TRY(r.h_n.resize(4));
+    r.cap = 0;
+    r.enqueued = true;
+    if (n == 0 || m->n_rows == 0)
+        return KGX_OK;
+    if ((rc = rollup_tiles(m, c, r)))
+        return rc;
+    if (r.hint) {
+        const uint64_t cap = std::min<uint64_t>(r.hint + r.hint / 8 + 4096, (1ull << 31) - 1);
+        if ((rc = rollup_rows(m, c, r, mode, cap)))
+            return rc;
+        r.cap = cap;
+    }
+    return KGX_OK;
+}
+
+int rollup_finish(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
+{
+    if (!m || !c || !out || !c->rollup || !c->rollup->enqueued)
+        return fail(KGX_EINVAL, "rollup_finish without rollup_enqueue");
+    RollupScratch &r = *c->rollup;
+    r.enqueued = false;
+    const uint32_t n = c->n_seq;
+    out->n_seq = n;
+    out->offsets = r.h_off.data();
+    out->rows = r.h_rows.data();
+    out->n_events = 0;
+    if (n == 0 || m->n_rows == 0) {
+        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
+        return KGX_OK;
+    }
+    HIP_TRY(hipSetDevice(m->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint64_t E = r.h_n[0];
+    out->n_events = E;
+    r.hint = E;
+    if (E == 0) {
+        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
+        return KGX_OK;
+    }
+    if (E >= (1ull << 31))
+        return fail(KGX_ERANGE, "rollup: more than 2^31 (hit, id) events in one batch");
+    if (E > r.cap) { /* not sized, or sized too small: passes 2-3 at E */
+        r.presize_misses += r.cap != 0;
+        if (int rc = rollup_rows(m, c, r, mode, E))
+            return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    out->rows = r.h_rows.data();
+    if (r.h_n[1] != r.h_off[n] || r.h_off[n] > E)
+        return fail(KGX_EDEVICE, "rollup: row counts disagree");
+    return KGX_OK;
+}
+
+}  // namespace kgx
+
 extern "C" {
 
 int kgx_kmap_create(int device, int mode, kgx_kmap **out)
@@ -980,124 +1291,8 @@ int kgx_kmap_lookup(kgx_kmap *m, const uint64_t *kmers, uint64_t n, uint64_t *of
 
 int kgx_kmap_rollup(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
 {
-    if (!m || !out || (mode != KGX_ROLLUP_PEG && mode != KGX_ROLLUP_FAMILY))
-        return fail(KGX_EINVAL, "bad kmap_rollup arguments");
-    int rc = check_ctx_hits(c);
-    if (rc)
-        return rc;
-    if (c->img->device != m->device)
-        return fail(KGX_EINVAL, "kmap and context are on different devices");
-    HIP_TRY(hipSetDevice(m->device));
-    if (!c->rollup)
-        c->rollup.reset(new RollupScratch);
-    RollupScratch &r = *c->rollup;
-    const uint32_t n = c->n_seq;
-    hipStream_t st = c->stream;
-    HIP_TRY(r.h_off.resize(n + 1));
-    HIP_TRY(r.h_n.resize(4));
-    out->n_seq = n;
-    out->offsets = r.h_off.data();
-    out->rows = r.h_rows.data();
-    out->n_events = 0;
-    if (n == 0 || m->n_rows == 0) {
-        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
-        return KGX_OK;
-    }
-    /* 1. per tile (one wave each): its hits' sequence, list start and
-     * length per slot, and its event total; the tiles' event bases by a scan */
-    const Tiled t = tiled_of(c);
-    const uint64_t nt = c->max_tiles, n_slots = nt * t.T;
-    const KmapView view = m->view();
-    HIP_TRY(r.hseq.reserve(n_slots * 4));
-    HIP_TRY(r.hstart.reserve(n_slots * 8));
-    HIP_TRY(r.hlen.reserve(n_slots * 4));
-    HIP_TRY(r.tcount.reserve((nt + 1) * 8));
-    HIP_TRY(r.tbase.reserve((nt + 1) * 8));
-    const dim3 tile_grid((uint32_t)((nt + 1 + 3) / 4));
-    hipLaunchKernelGGL(rollup_tiles_kernel, tile_grid, dim3(256), 0, st, t, nt, view, r.hseq.as<uint32_t>(),
-                       r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tcount.as<uint64_t>());
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
-                                             (int)(nt + 1), st));
-    HIP_TRY(r.tmp.reserve(tb));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
-                                             (int)(nt + 1), st));
-    {   /* the event total by a device store into mapped memory: a DMA copy
-         * would queue behind other contexts' uploads */
-        void *dn = nullptr;
-        HIP_TRY(r.h_n.device_ptr(0, &dn));
-        HIP_TRY(launch_copy_to_host(dn, r.tbase.as<uint64_t>() + nt, 8, 1, st));
-    }
-    HIP_TRY(hipStreamSynchronize(st));
-    const uint64_t E = r.h_n[0];
-    out->n_events = E;
-    if (E == 0) {
-        std::fill(r.h_off.data(), r.h_off.data() + n + 1, 0ull);
-        return KGX_OK;
-    }
-    if (E >= (1ull << 31))
-        return fail(KGX_ERANGE, "rollup: more than 2^31 (hit, id) events in one batch");
-    /* 2. events keyed (sequence, id), stably sorted: hit order within a key;
-     * 32-bit keys when the two fields fit */
-    const uint32_t ib = std::max(1, 32 - __builtin_clz(std::max(m->max_id, 1u)));
-    const uint32_t sb = n > 1 ? 32 - __builtin_clz(n - 1) : 1;
-    const bool k32 = ib + sb <= 32;
-    const size_t kb = k32 ? 4 : 8;
-    HIP_TRY(r.key.reserve(E * kb));
-    HIP_TRY(r.key2.reserve(E * kb));
-    HIP_TRY(r.idx.reserve(E * 4));
-    HIP_TRY(r.idx2.reserve(E * 4));
-    HIP_TRY(r.ew.reserve(E * 4));
-    HIP_TRY(r.flag.reserve(E));
-    HIP_TRY(r.rowdata.reserve(E * 16));
-    HIP_TRY(r.rowcnt.reserve((n + 1) * 4));
-    HIP_TRY(r.nsel.reserve(8));
-    HIP_TRY(hipMemsetAsync(r.flag.p, 0, E, st));
-    HIP_TRY(hipMemsetAsync(r.rowcnt.p, 0, (n + 1) * 4, st));
-    auto sort_and_group = [&](auto *k1, auto *k2) -> int {
-        typedef std::remove_pointer_t<decltype(k1)> K;
-        hipLaunchKernelGGL(rollup_events_kernel<K>, tile_grid, dim3(256), 0, st, t, nt, r.hseq.as<uint32_t>(),
-                           r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tbase.as<uint64_t>(), view.vals, ib,
-                           k1, r.idx.as<uint32_t>(), r.ew.as<float>());
-        size_t sbytes = 0;
-        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sbytes, k1, k2, r.idx.as<uint32_t>(),
-                                                   r.idx2.as<uint32_t>(), (int)E, 0, (int)(ib + sb), st));
-        HIP_TRY(r.tmp.reserve(sbytes));
-        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(r.tmp.p, sbytes, k1, k2, r.idx.as<uint32_t>(),
-                                                   r.idx2.as<uint32_t>(), (int)E, 0, (int)(ib + sb), st));
-        hipLaunchKernelGGL(rollup_groups_kernel<K>, grid_for(E), dim3(256), 0, st, E, (const K *)k2,
-                           r.idx2.as<uint32_t>(), r.ew.as<float>(), ib, mode == KGX_ROLLUP_FAMILY ? 1 : 0,
-                           r.flag.as<uint8_t>(), r.rowdata.as<uint4>(), r.rowcnt.as<uint32_t>());
-        return KGX_OK;
-    };
-    const int src = k32 ? sort_and_group(r.key.as<uint32_t>(), r.key2.as<uint32_t>())
-                        : sort_and_group(r.key.as<uint64_t>(), r.key2.as<uint64_t>());
-    if (src)
-        return src;
-    /* 3. one row per group at its first event; rows in event order = per
-     * sequence in first-touch order, straight into the mapped host arrays */
-    HIP_TRY(r.h_rows.resize(E));
-    out->rows = r.h_rows.data();
-    void *d_rows = nullptr, *d_off = nullptr, *d_n = nullptr;
-    HIP_TRY(r.h_rows.device_ptr(0, &d_rows));
-    HIP_TRY(r.h_off.device_ptr(0, &d_off));
-    HIP_TRY(r.h_n.device_ptr(1, &d_n));
-    size_t tb1 = 0, tb2 = 0;
-    HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb1, r.rowdata.as<uint4>(), r.flag.as<uint8_t>(),
-                                          static_cast<uint4 *>(d_rows), static_cast<uint64_t *>(d_n), (int)E, st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, r.rowcnt.as<uint32_t>(), static_cast<uint64_t *>(d_off),
-                                             (int)(n + 1), st));
-    HIP_TRY(r.tmp.reserve(std::max(tb1, tb2)));
-    HIP_TRY(hipcub::DeviceSelect::Flagged(r.tmp.p, tb1, r.rowdata.as<uint4>(), r.flag.as<uint8_t>(),
-                                          static_cast<uint4 *>(d_rows), static_cast<uint64_t *>(d_n), (int)E, st));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb2, r.rowcnt.as<uint32_t>(), static_cast<uint64_t *>(d_off),
-                                             (int)(n + 1), st));
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st));
-    std::atomic_thread_fence(std::memory_order_acquire);
-    if (r.h_n[1] != r.h_off[n] || r.h_off[n] > E)
-        return fail(KGX_EDEVICE, "rollup: row counts disagree");
-    return KGX_OK;
+    int rc = kgx::rollup_enqueue(m, c, mode);
+    return rc ? rc : kgx::rollup_finish(m, c, mode, out);
 }
 
 int kgx_matrix_create(kgx_kmap *map, kgx_matrix **out)

@@ -198,3 +198,47 @@ def test_kmap_rollup_matches_on_hit(table_world, gpu, oracle_lib, mode):
     with gpu.Kmap(0, 1) as empty:
         roff, rows = empty.rollup(ctx, gpu.ROLLUP_FAMILY)
         assert len(rows) == 0 and not roff.any()
+
+
+def test_kmap_rollup_many_ids_and_resizing(table_world, gpu, oracle_lib):
+    """Sequences with hundreds to thousands of distinct ids (more than one LDS
+    table pass holds: the id-class path) and a context whose batches grow and
+    shrink between rollups (a rollup sized by the previous event count, then
+    one too small for its batch, which runs again at the true size)."""
+    spec, table, img, ctx = table_world
+    rng = np.random.default_rng(77)
+    fam = _family_proteins(spec, rng, 8, 2)
+    long_seqs = [b"".join(fam[i:i + 4]) for i in range(0, 8, 4)]  # ~1,100-1,200 aa
+    seqs = fam + long_seqs
+    hoff, hk, res, off = _oracle_hit_kmers(oracle_lib, table, seqs)
+    uk = np.unique(hk)
+    kms, ids = [], []
+    for k in uk:
+        n = int(rng.integers(1, 10))
+        kms.append(np.full(n, k, np.uint64))
+        ids.append(rng.integers(0, 50000, n).astype(np.uint32))
+    kms, ids = np.concatenate(kms), np.concatenate(ids)
+    orc = oracle_lib.Kmap(1)
+    orc.add(kms, ids)
+
+    def check(lo, hi):
+        sub_res = res[int(off[lo]):int(off[hi])]
+        ctx.process_batch(sub_res, off[lo:hi + 1] - off[lo], want=0)
+        roff, rows = dev.rollup(ctx, gpu.ROLLUP_FAMILY)
+        most = 0
+        for s in range(lo, hi):
+            exp = _on_hit_rollup(hk[int(hoff[s]):int(hoff[s + 1])], orc, True)
+            got = rows[int(roff[s - lo]):int(roff[s - lo + 1])]
+            assert got["id"].tolist() == list(exp.keys()), s
+            assert got["hit_count"].tolist() == [v[0] for v in exp.values()], s
+            wexp = np.array([v[2] for v in exp.values()], np.float32)
+            assert np.array_equal(got["weighted_total"].view(np.uint32), wexp.view(np.uint32)), s
+            most = max(most, len(exp))
+        return most
+
+    with gpu.Kmap(0, 1) as dev:
+        dev.add(kms, ids)
+        assert check(0, 2) > 0              # small: the next rollup's size
+        assert check(0, len(seqs)) > 400    # too small a size: run again; class path
+        assert check(0, len(seqs)) > 400    # sized by the last count
+        check(3, 5)                         # smaller again
