@@ -93,6 +93,19 @@ struct kgx_pool {
      * priority: a queue of its own), and an event per shard */
     std::vector<hipStream_t> up_stream;
     std::vector<hipEvent_t> up_done;
+    /* per device three streams made in a row before the contexts: the
+     * shards' plans and probes one after another, their scores (behind each
+     * probe, an event), and their rollups (behind each probe too).  The
+     * runtime spreads a process's streams over a few hardware queues
+     * (GPU_MAX_HW_QUEUES, 4), so streams made in a row rarely share one, and a
+     * shard's score and rollup run beside the next shard's probe instead of
+     * holding it back in a shared queue.  The shards' contexts lend their
+     * buffers; their own streams stay idle.  (r5x: passes and rollups on the
+     * contexts' streams, 1.86-2.09 ms for the same batch by which of them the
+     * runtime put on one queue; r5z/r6b: 2.08-2.10 ms with these streams,
+     * deterministic; more hardware queues than 4 measured slower still.) */
+    std::vector<hipStream_t> pass_stream, score_stream, roll_stream;
+    std::vector<hipEvent_t> pass_done, roll_done;
     std::vector<uint32_t> runners(uint32_t per) const
     {
         std::vector<uint32_t> out, used;
@@ -174,12 +187,47 @@ int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx,
         return fail(KGX_EINVAL, "a pool needs images and contexts");
     *out = nullptr;
     kgx_pool *p = new kgx_pool;
+    for (uint32_t i = 0; i < n_images; i++) {
+        const int d = images[i] ? kgx_image_device(images[i]) : -1;
+        if (d < 0)
+            continue;
+        if ((int)p->pass_stream.size() <= d)
+            p->pass_stream.resize((size_t)d + 1, nullptr);
+        if ((int)p->roll_stream.size() <= d) {
+            p->roll_stream.resize((size_t)d + 1, nullptr);
+            p->score_stream.resize((size_t)d + 1, nullptr);
+        }
+        if (!p->pass_stream[(size_t)d]) {
+            hipStream_t st[3] = {nullptr, nullptr, nullptr};
+            bool ok = hipSetDevice(d) == hipSuccess;
+            for (int k = 0; k < 3 && ok; k++)
+                ok = hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) == hipSuccess;
+            if (!ok) {
+                for (hipStream_t x : st)
+                    if (x)
+                        (void)hipStreamDestroy(x);
+                for (auto *v : {&p->pass_stream, &p->score_stream, &p->roll_stream})
+                    for (hipStream_t x : *v)
+                        if (x)
+                            (void)hipStreamDestroy(x);
+                delete p;
+                return fail(KGX_EDEVICE, "pool: stream creation failed");
+            }
+            p->pass_stream[(size_t)d] = st[0];
+            p->score_stream[(size_t)d] = st[1];
+            p->roll_stream[(size_t)d] = st[2];
+        }
+    }
     for (uint32_t i = 0; i < n_ctx; i++) {
         kgx_ctx *c = nullptr;
         int rc = images[i % n_images] ? kgx_ctx_create(images[i % n_images], &c) : fail(KGX_EINVAL, "null image");
         if (rc) {
             for (auto *x : p->ctxs)
                 kgx_ctx_destroy(x);
+            for (auto *v : {&p->pass_stream, &p->score_stream, &p->roll_stream})
+                for (hipStream_t x : *v)
+                    if (x)
+                        (void)hipStreamDestroy(x);
             delete p;
             return rc;
         }
@@ -226,6 +274,16 @@ int kgx_pool_destroy(kgx_pool *p)
         }
     for (hipEvent_t e : p->up_done)
         (void)hipEventDestroy(e);
+    for (auto *v : {&p->pass_stream, &p->score_stream, &p->roll_stream})
+        for (size_t d = 0; d < v->size(); d++)
+            if ((*v)[d]) {
+                (void)hipSetDevice((int)d);
+                (void)hipStreamSynchronize((*v)[d]);
+                (void)hipStreamDestroy((*v)[d]);
+            }
+    for (auto *v : {&p->pass_done, &p->roll_done})
+        for (hipEvent_t e : *v)
+            (void)hipEventDestroy(e);
     delete p;
     return KGX_OK;
 }
@@ -451,10 +509,49 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         if (!mine[i])
             return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(dev));
     }
+    /* residue shares: a device's first and last shards half the others'.
+     * Its pipeline fills with the first shard's upload and drains with the
+     * last one's score and rollup, the GPU part idle meanwhile; the inner
+     * shards overlap both (r5z: even quarters, 175 us fill and 290 us drain
+     * of a 2.1-ms call) */
+    std::vector<double> share(K, 2.0);
+    {
+        static const double edge = [] {
+            const char *e = std::getenv("KGX_POOL_EDGE_SHARE");
+            return e ? std::max(0.05, std::min(8.0, std::atof(e))) : 1.0;
+        }();
+        std::vector<int> first(64, -1), last(64, -1);
+        for (uint32_t i = 0; i < K; i++) {
+            const int d = kgx_image_device(p->ctxs[run[i]]->img);
+            if (d >= 0 && d < 64) {
+                if (first[(size_t)d] < 0)
+                    first[(size_t)d] = (int)i;
+                last[(size_t)d] = (int)i;
+            }
+        }
+        for (int d = 0; d < 64; d++)
+            if (first[(size_t)d] >= 0 && first[(size_t)d] != last[(size_t)d]) {
+                share[(size_t)first[(size_t)d]] = edge;
+                share[(size_t)last[(size_t)d]] = edge;
+            }
+    }
     std::vector<uint32_t> cuts(K + 1, 0);
-    int rc = kgx_shard_cuts(seq_offsets, n_seq, K, cuts.data());
-    if (rc)
-        return rc;
+    {
+        const uint64_t r0 = n_seq ? seq_offsets[0] : 0, total = n_seq ? seq_offsets[n_seq] - r0 : 0;
+        double sum = 0, acc = 0;
+        for (double w : share)
+            sum += w;
+        cuts[K] = n_seq;
+        for (uint32_t i = 1; i < K; i++) {
+            acc += share[i - 1];
+            const uint64_t target = r0 + (uint64_t)((double)total * (acc / sum));
+            const uint32_t s = n_seq ? (uint32_t)(std::lower_bound(seq_offsets, seq_offsets + n_seq, target) -
+                                                  seq_offsets)
+                                     : 0;
+            cuts[i] = std::min(n_seq, std::max(cuts[i - 1], s));
+        }
+    }
+    int rc = KGX_OK;
     /* every shard is ONE pass on its context (its hits stay on the device
      * for the rollup: host_chunks 1 for the call), then its rollups */
     std::vector<kgx_result> part(K, kgx_result{});
@@ -477,6 +574,12 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         p->up_done.push_back(e);
     }
+    for (auto *v : {&p->pass_done, &p->roll_done})
+        while (v->size() < K) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            v->push_back(e);
+        }
     for (uint32_t i = 0; i < K; i++) {
         kgx_ctx *c = p->ctxs[run[i]];
         const int dev = kgx_image_device(c->img);
@@ -499,18 +602,36 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         const int sv = c->score_variant;
         if (c->host_score_variant >= 0)
             c->score_variant = c->host_score_variant;
+        /* the pass (and its counts' copy) on the device's pass stream, the
+         * rollup on its rollup stream behind it; the context's own stream
+         * gets nothing (a wait on it could sit in the pass stream's queue) */
+        hipStream_t own = c->stream, ps = p->pass_stream[(size_t)dev], ss = p->score_stream[(size_t)dev],
+                    rs = p->roll_stream[(size_t)dev];
+        c->stream = ps;
+        c->score_stream = ss;
         rcs[i] = one_pass_enqueue(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want,
                                   p->up_stream[(size_t)dev], p->up_done[i]);
         c->score_variant = sv;
+        c->score_stream = nullptr;
+        c->stream = ss; /* the counts and best calls behind the score */
         if (!rcs[i])
             rcs[i] = collect_counts_enqueue(c, want);
+        if (!rcs[i] && (hipEventRecord(p->pass_done[i], ss) != hipSuccess ||
+                        hipStreamWaitEvent(rs, c->score_gate, 0) != hipSuccess))
+            rcs[i] = fail(KGX_EDEVICE, "pool lookup: pass event");
+        c->stream = rs; /* the rollup behind the probe */
         if (!rcs[i])
             rcs[i] = rollup_enqueue(mine[i], c, mode);
+        if (!rcs[i] && hipEventRecord(p->roll_done[i], rs) != hipSuccess)
+            rcs[i] = fail(KGX_EDEVICE, "pool lookup: rollup event");
+        c->stream = own;
         if (rcs[i]) {
             errs[i] = kgx_last_error();
             /* the shards enqueued so far still run: drain them before returning */
-            for (uint32_t j = 0; j < i; j++)
-                (void)kgx_ctx_synchronize(p->ctxs[run[j]]);
+            for (auto *v : {&p->pass_stream, &p->score_stream, &p->roll_stream})
+                for (hipStream_t x : *v)
+                    if (x)
+                        (void)hipStreamSynchronize(x);
             return fail(rcs[i], "pool lookup shard " + std::to_string(i) + ": " + errs[i]);
         }
     }
@@ -518,6 +639,12 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         kgx_ctx *c = p->ctxs[run[i]];
         const auto t0 = std::chrono::steady_clock::now();
         const uint64_t reruns = c->nul_reruns;
+        if (hipEventSynchronize(p->pass_done[i]) != hipSuccess ||
+            hipEventSynchronize(p->roll_done[i]) != hipSuccess) { /* the shard's pass and rollup */
+            rcs[i] = fail(KGX_EDEVICE, "pool lookup: rollup wait");
+            errs[i] = kgx_last_error();
+            return;
+        }
         rcs[i] = one_pass_collect(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want, &part[i]);
         const auto t1 = std::chrono::steady_clock::now();
         if (!rcs[i] && c->nul_reruns != reruns) /* the pass ran again, staged: so does its rollup */

@@ -355,6 +355,10 @@ struct kgx_ctx {
     int probe_serialize = 1;          /* option "probe_serialize" */
     int probe_stream = 0;             /* chained probes on the image's probe stream (option "probe_stream") */
     hipEvent_t probe_ready = nullptr; /* this context's inputs are ready for its probe */
+    /* a pool's /lookup: the stream the pass's score runs on after its probe
+     * (null: the context's stream), behind score_gate recorded after the probe */
+    hipStream_t score_stream = nullptr;
+    hipEvent_t score_gate = nullptr;
     /* device scratch */
     kgx::DevBuf residues, offsets, wbase, tile_seq, hit_mask, hits, calls, hit_count, call_count,
         dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;

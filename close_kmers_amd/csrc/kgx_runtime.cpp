@@ -857,6 +857,8 @@ int kgx_ctx_destroy(kgx_ctx *c)
     (void)hipEventDestroy(c->probe_done);
     if (c->probe_ready)
         (void)hipEventDestroy(c->probe_ready);
+    if (c->score_gate)
+        (void)hipEventDestroy(c->score_gate);
     c->pool.reset();
     c->stage_pool.reset();
     for (hipEvent_t e : c->chunk_done)
@@ -1444,8 +1446,21 @@ int kgx_run_device(kgx_ctx *c, const kgx_params *params, const uint8_t *d_res, c
         return rc;
     if ((rc = kgx_stage_probe(c, d_res, d_off)))
         return rc;
-    if ((rc = kgx_stage_score(c, params, want)))
+    if (c->score_stream) {
+        /* the score on its own stream behind the probe (kgx_pool_lookup) */
+        if (!c->score_gate)
+            HIP_TRY(hipEventCreateWithFlags(&c->score_gate, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->score_gate, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->score_stream, c->score_gate, 0));
+        hipStream_t own = c->stream;
+        c->stream = c->score_stream;
+        rc = kgx_stage_score(c, params, want);
+        c->stream = own;
+        if (rc)
+            return rc;
+    } else if ((rc = kgx_stage_score(c, params, want))) {
         return rc;
+    }
     return out ? kgx_device_result_get(c, out) : KGX_OK;
 }
 

@@ -294,62 +294,82 @@ __global__ void lookup_ids_kernel(KmapView m, const uint64_t *kmers, uint64_t n,
 
 constexpr uint32_t kNoEvent = 0xFFFFFFFFu;
 
-/* the wave's index in the grid, wave-uniform (scalar loads for its word) */
+/* the wave's index in the grid, wave-uniform */
 __device__ __forceinline__ uint64_t wave_index()
 {
     return (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
-/* mask word w of a tiled result (0 past the batch's windows) and the number
- * of hits of its tile's earlier words: hit slot = tile * T + base + rank */
-__device__ __forceinline__ uint64_t word_mask(const Tiled &t, uint64_t w, uint64_t W, uint32_t &base)
+/* Passes 1 and 2 take kRollTiles tiles per wave and their hits densely, one
+ * hit per lane: about a quarter of a batch's windows hit, so a lane per
+ * window would leave three in four idle in a kernel bound by its dependent
+ * reads (r5u: 106 us per 7.5M-residue shard with a wave per mask word). */
+constexpr uint32_t kRollTiles = 2;
+constexpr uint32_t kRollMaxT = 512; /* windows per tile (probe_j <= 8) */
+
+/* the wave's hits in order (tile, then window): LDS entry r = the hit's slot
+ * and window offsets from the wave's first tile; returns the count */
+__device__ __forceinline__ uint32_t roll_list(const Tiled &t, uint64_t tile0, uint64_t n_tiles, uint64_t W,
+                                              uint16_t *slot_off, uint16_t *win_off)
 {
-    const uint32_t J = t.T / 64;
-    const uint64_t w0 = w - w % J;
-    base = 0;
-    for (uint64_t x = w0; x < w; x++)
-        base += (uint32_t)__popcll(t.mask[x]); /* earlier words are inside the batch */
-    return 64 * w < W ? t.mask[w] : 0ull;
+    const uint32_t J = t.T / 64, lane = lane_id();
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < kRollTiles && tile0 + k < n_tiles; k++) {
+        uint32_t in_tile = 0;
+        for (uint32_t j = 0; j < J; j++) {
+            const uint64_t w = (tile0 + k) * J + j;
+            const uint64_t m = 64 * w < W ? t.mask[w] : 0ull;
+            if ((m >> lane) & 1ull) {
+                const uint32_t r = n + lanes_below(m);
+                slot_off[r] = (uint16_t)(k * t.T + in_tile + lanes_below(m));
+                win_off[r] = (uint16_t)(k * t.T + 64 * j + lane);
+            }
+            const uint32_t pc = (uint32_t)__popcll(m);
+            n += pc;
+            in_tile += pc;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return n;
 }
 
-/* Pass 1, one wave per mask word (64 windows): for each of its hits (a lane
- * takes the hit whose window is its bit) the sequence, list start and length
- * (0 for an unmapped k-mer); the word's event total.  Wave n_words writes the
- * scan's last element, 0; the grid also resets the sequences' event ranges
- * and row counts for the later passes.  A wave per word, not per tile: the
- * kernel is latency-bound (mask, record, index slot: a chain of dependent
- * reads per hit), so it wants many small waves (r5t: four words' chains per
- * wave at 44 VGPRs ran 150 us per 7.5M-residue shard vs 111 us for one word
- * at a time at 20). */
-__global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_words, KmapView m, uint32_t *hseq,
-                                                           uint64_t *hstart, uint32_t *hlen, uint64_t *wcount,
-                                                           uint32_t *sfirst, uint32_t *send, uint32_t *rowcnt)
+/* Pass 1: for each hit of the wave's tiles its sequence, list start and
+ * length (0 for an unmapped k-mer) at its slot; the wave's event total.  Wave
+ * n_waves writes the scan's last element, 0; the grid also resets the
+ * sequences' event ranges and row counts for the later passes. */
+__global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_tiles, uint64_t n_waves, KmapView m,
+                                                           uint32_t *hseq, uint64_t *hstart, uint32_t *hlen,
+                                                           uint64_t *wcount, uint32_t *sfirst, uint32_t *send,
+                                                           uint32_t *rowcnt)
 {
+    extern __shared__ uint16_t roll_lds[]; /* 4 waves x (slot, window) x kRollTiles * T */
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.n_seq;
          i += (uint64_t)gridDim.x * blockDim.x) {
         sfirst[i] = kNoEvent;
         send[i] = 0;
         rowcnt[i] = 0;
     }
-    const uint64_t w = wave_index();
-    const uint32_t lane = lane_id();
-    if (w >= n_words) {
-        if (w == n_words && lane == 0)
-            wcount[n_words] = 0;
+    const uint64_t v = wave_index();
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    if (v >= n_waves) {
+        if (v == n_waves && lane == 0)
+            wcount[n_waves] = 0;
         return;
     }
-    const uint64_t W = t.wbase[t.n_seq];
-    uint32_t base;
-    const uint64_t mw = word_mask(t, w, W, base);
+    const uint64_t tile0 = v * kRollTiles, W = t.wbase[t.n_seq];
+    uint16_t *so = roll_lds + wv * 2 * kRollTiles * t.T, *wo = so + kRollTiles * t.T;
+    const uint32_t n = roll_list(t, tile0, n_tiles, W, so, wo);
     uint64_t ev = 0;
-    if ((mw >> lane) & 1ull) {
-        const uint64_t tile = w / (t.T / 64);
-        const uint64_t slot = tile * t.T + base + lanes_below(mw);
+    for (uint32_t r = lane; r < n; r += 64) {
+        const uint64_t slot = tile0 * t.T + so[r];
         uint64_t key;
         uint32_t seq;
         if (t.packed) {
+            const uint64_t g = tile0 * t.T + wo[r];
             key = HitFields<true>::key(t.hot[slot], t.hot[slot]);
-            seq = window_seq(t.wbase, t.tile_seq, tile, 64 * w + lane);
+            seq = window_seq(t.wbase, t.tile_seq, g / t.T, g);
         } else {
             const uint4 h = t.cold[slot];
             key = (uint64_t)h.y << 32 | h.x;
@@ -360,70 +380,75 @@ __global__ __launch_bounds__(256) void rollup_tiles_kernel(Tiled t, uint64_t n_w
         hseq[slot] = seq;
         hstart[slot] = a;
         hlen[slot] = (uint32_t)len;
-        ev = len;
+        ev += len;
     }
     for (int o = 32; o > 0; o >>= 1)
         ev += __shfl_xor(ev, o);
     if (lane == 0)
-        wcount[w] = ev;
+        wcount[v] = ev;
 }
 
-/* Pass 2, one wave per mask word: the events of its hits, numbered from the
- * word's scanned base in hit order, then list order: the id and the hit's
- * weight 1.0f / (float)|list| (lookup_request.cc:459); each sequence's event
- * range [sfirst, send) by one atomic per (word, sequence) at its first and
- * last lane.  Writes nothing when the batch has more than cap events (the
- * host runs the passes again at the true size). */
-__global__ __launch_bounds__(256) void rollup_events_kernel(Tiled t, uint64_t n_words, const uint32_t *hseq,
-                                                            const uint64_t *hstart, const uint32_t *hlen,
-                                                            const uint64_t *wbase_ev, const uint32_t *vals,
-                                                            uint64_t cap, uint32_t *ev_id, float *ev_w,
-                                                            uint32_t *sfirst, uint32_t *send)
+/* Pass 2, the same waves: the events of their hits, numbered from the wave's
+ * scanned base in hit order, then list order: the id and the hit's weight
+ * 1.0f / (float)|list| (lookup_request.cc:459); each sequence's event range
+ * [sfirst, send) by atomics at the first and last lane of each run of one
+ * sequence in a 64-hit chunk.  Writes nothing when the batch has more than
+ * cap events (the host runs the passes again at the true size). */
+__global__ __launch_bounds__(256) void rollup_events_kernel(Tiled t, uint64_t n_tiles, uint64_t n_waves,
+                                                            const uint32_t *hseq, const uint64_t *hstart,
+                                                            const uint32_t *hlen, const uint64_t *vbase,
+                                                            const uint32_t *vals, uint64_t cap, uint32_t *ev_id,
+                                                            float *ev_w, uint32_t *sfirst, uint32_t *send)
 {
-    const uint64_t w = wave_index();
-    if (w >= n_words || wbase_ev[n_words] > cap)
+    extern __shared__ uint16_t roll_lds[];
+    const uint64_t v = wave_index();
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+    if (v >= n_waves || vbase[n_waves] > cap)
         return;
-    const uint64_t e0 = wbase_ev[w];
-    if (wbase_ev[w + 1] == e0)
+    uint64_t e0 = vbase[v];
+    if (vbase[v + 1] == e0)
         return;
-    const uint32_t lane = lane_id();
-    const uint64_t W = t.wbase[t.n_seq];
-    uint32_t base;
-    const uint64_t mw = word_mask(t, w, W, base);
-    uint64_t len = 0, a = 0;
-    uint32_t seq = 0;
-    if ((mw >> lane) & 1ull) {
-        const uint64_t slot = (w / (t.T / 64)) * t.T + base + lanes_below(mw);
-        len = hlen[slot];
-        a = hstart[slot];
-        seq = hseq[slot];
-    }
-    uint64_t incl = len;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t v = __shfl_up(incl, o);
-        if (lane >= (uint32_t)o)
-            incl += v;
-    }
-    const uint64_t e = e0 + incl - len;
-    if (len) {
-        const float wt = 1.0f / (float)len;
-        for (uint64_t q = 0; q < len; q++) {
-            ev_id[e + q] = vals[a + q];
-            ev_w[e + q] = wt;
+    const uint64_t tile0 = v * kRollTiles, W = t.wbase[t.n_seq];
+    uint16_t *so = roll_lds + wv * 2 * kRollTiles * t.T, *wo = so + kRollTiles * t.T;
+    const uint32_t n = roll_list(t, tile0, n_tiles, W, so, wo);
+    for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        uint64_t len = 0, a = 0;
+        uint32_t seq = 0;
+        if (r < n) {
+            const uint64_t slot = tile0 * t.T + so[r];
+            len = hlen[slot];
+            a = hstart[slot];
+            seq = hseq[slot];
         }
-    }
-    /* the lanes with events: each one's neighbours among them */
-    const uint64_t act = __ballot(len != 0);
-    const uint64_t below = act & ((1ull << lane) - 1ull);
-    const uint64_t above = lane == 63 ? 0ull : act & ~((2ull << lane) - 1ull);
-    const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
-    const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : lane;
-    const uint32_t pseq = __shfl(seq, (int)prev), nseq = __shfl(seq, (int)next);
-    if (len) {
-        if (!below || pseq != seq)
-            atomicMin(sfirst + seq, (uint32_t)e);
-        if (!above || nseq != seq)
-            atomicMax(send + seq, (uint32_t)(e + len));
+        uint64_t incl = len;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t x = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o)
+                incl += x;
+        }
+        const uint64_t e = e0 + incl - len;
+        if (len) {
+            const float wt = 1.0f / (float)len;
+            for (uint64_t q = 0; q < len; q++) {
+                ev_id[e + q] = vals[a + q];
+                ev_w[e + q] = wt;
+            }
+        }
+        /* the lanes with events: each one's neighbours among them */
+        const uint64_t act = __ballot(len != 0);
+        const uint64_t below = act & ((1ull << lane) - 1ull);
+        const uint64_t above = lane == 63 ? 0ull : act & ~((2ull << lane) - 1ull);
+        const uint32_t prev = below ? 63u - (uint32_t)__builtin_clzll(below) : lane;
+        const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : lane;
+        const uint32_t pseq = __shfl(seq, (int)prev), nseq = __shfl(seq, (int)next);
+        if (len) {
+            if (!below || pseq != seq)
+                atomicMin(sfirst + seq, (uint32_t)e);
+            if (!above || nseq != seq)
+                atomicMax(send + seq, (uint32_t)(e + len));
+        }
+        e0 += __shfl(incl, 63);
     }
 }
 
@@ -952,7 +977,7 @@ namespace {
 int rollup_reserve(kgx_ctx *c, RollupScratch &r)
 {
     const uint32_t n = c->n_seq;
-    const uint64_t nt = c->max_tiles, n_slots = nt * c->tile_windows, nw = nt * (c->tile_windows / 64);
+    const uint64_t nt = c->max_tiles, n_slots = nt * c->tile_windows, nw = (nt + kRollTiles - 1) / kRollTiles;
     HIP_TRY(r.hseq.reserve(n_slots * 4));
     HIP_TRY(r.hstart.reserve(n_slots * 8));
     HIP_TRY(r.hlen.reserve(n_slots * 4));
@@ -969,13 +994,16 @@ int rollup_tiles(kgx_kmap *m, kgx_ctx *c, RollupScratch &r)
 {
     hipStream_t st = c->stream;
     const Tiled t = tiled_of(c);
+    if (t.T > kRollMaxT)
+        return fail(KGX_EINVAL, "rollup: tiles of more than 512 windows");
     const uint32_t n = c->n_seq;
-    const uint64_t nt = c->max_tiles, nw = nt * (t.T / 64);
+    const uint64_t nt = c->max_tiles, nw = (nt + kRollTiles - 1) / kRollTiles;
     const KmapView view = m->view();
     if (int rc = rollup_reserve(c, r))
         return rc;
-    const dim3 word_grid((uint32_t)((nw + 1 + 3) / 4));
-    hipLaunchKernelGGL(rollup_tiles_kernel, word_grid, dim3(256), 0, st, t, nw, view, r.hseq.as<uint32_t>(),
+    const dim3 wave_grid((uint32_t)((nw + 1 + 3) / 4));
+    const uint32_t lds = 4 * 2 * kRollTiles * t.T * sizeof(uint16_t);
+    hipLaunchKernelGGL(rollup_tiles_kernel, wave_grid, dim3(256), lds, st, t, nt, nw, view, r.hseq.as<uint32_t>(),
                        r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tcount.as<uint64_t>(),
                        r.sfirst.as<uint32_t>(), r.send.as<uint32_t>(), r.rowcnt.as<uint32_t>());
     size_t tb = 0, tb2 = 0;
@@ -1002,9 +1030,9 @@ int rollup_rows(kgx_kmap *m, kgx_ctx *c, RollupScratch &r, int mode, uint64_t ca
     hipStream_t st = c->stream;
     const uint32_t n = c->n_seq;
     const Tiled t = tiled_of(c);
-    const uint64_t nw = c->max_tiles * (t.T / 64);
+    const uint64_t nt = c->max_tiles, nw = (nt + kRollTiles - 1) / kRollTiles;
     const KmapView view = m->view();
-    const dim3 word_grid((uint32_t)((nw + 1 + 3) / 4)), seq_grid((n + 1 + 3) / 4);
+    const dim3 wave_grid((uint32_t)((nw + 1 + 3) / 4)), seq_grid((n + 1 + 3) / 4);
     const uint64_t *d_E = r.tbase.as<uint64_t>() + nw;
     HIP_TRY(r.ev_id.reserve(cap * 4));
     HIP_TRY(r.ev_w.reserve(cap * 4));
@@ -1012,7 +1040,8 @@ int rollup_rows(kgx_kmap *m, kgx_ctx *c, RollupScratch &r, int mode, uint64_t ca
     HIP_TRY(r.rowdata.reserve(cap * 16));
     HIP_TRY(r.rows2.reserve(cap * 16));
     HIP_TRY(r.h_rows.resize(cap));
-    hipLaunchKernelGGL(rollup_events_kernel, word_grid, dim3(256), 0, st, t, nw, r.hseq.as<uint32_t>(),
+    const uint32_t lds = 4 * 2 * kRollTiles * t.T * sizeof(uint16_t);
+    hipLaunchKernelGGL(rollup_events_kernel, wave_grid, dim3(256), lds, st, t, nt, nw, r.hseq.as<uint32_t>(),
                        r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tbase.as<uint64_t>(), view.vals, cap,
                        r.ev_id.as<uint32_t>(), r.ev_w.as<float>(), r.sfirst.as<uint32_t>(), r.send.as<uint32_t>());
     hipLaunchKernelGGL(rollup_group_kernel, seq_grid, dim3(256), 0, st, n, r.sfirst.as<uint32_t>(),

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--n-seq", type=int, default=100000)
     ap.add_argument("--ctx", type=int, default=4)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--option", action="append", default=[],
+                    help="name=value context option for every pool context (repeatable)")
     args = ap.parse_args()
     import bench
     from close_kmers_amd import abi, synth
@@ -37,6 +39,9 @@ def main():
     params = abi.default_params()
     ts = []
     with abi.Pool([img], args.ctx) as pool:
+        for o in args.option:
+            name, value = o.split("=")
+            pool.set_option(name, int(value))
         for i in range(args.reps + 1):
             print(f"--- call {i}", file=sys.stderr, flush=True)
             t0 = time.perf_counter()
