@@ -410,6 +410,8 @@ def main():
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
     ap.add_argument("--pipeline", type=int, default=2, help="worker contexts (streams) in flight")
+    ap.add_argument("--ctx-option", action="append", default=[],
+                    help="name=value context option for every worker context (repeatable; tuning A/Bs)")
     ap.add_argument("--filter-log2", type=int, default=0,
                     help="presence filter of 2^N bits (0 = none), kgx_image_set_filter")
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
@@ -532,6 +534,9 @@ def main():
             c.set_option("probe_persist", args.probe_persist)
         if args.probe_stream >= 0:
             c.set_option("probe_stream", args.probe_stream)
+        for o in args.ctx_option:
+            name, value = o.split("=")
+            c.set_option(name, int(value))
     score_ms: list = []  # score stage (+ best/OTU kernels with --want), same untimed pass as probe_ms
 
     def step(timed_probe: list | None, c=ctx, b=0):
@@ -706,7 +711,7 @@ def main():
         ceiling = {}
         n_reads = int(min(n, 100000) * max(0, Ls - 8) * 1.4)
         for mode, name, useful in ((0, "bucket24", 24), (1, "key8", 8), (2, "sector64", 64),
-                                   (3, "rec16", 16), (4, "line64", 64)):
+                                   (3, "rec16", 16), (4, "line64", 64), (5, "line128", 128)):
             ms, reads = ctypes.c_float(), ctypes.c_uint64()
             abi.check(L.kgx_microbench_random_read(ctx.handle, n_reads, mode, ctypes.byref(ms),
                                                    ctypes.byref(reads)), "microbench")  # warm

@@ -767,9 +767,12 @@ int kgx_kmap_device(const kgx_kmap *map);
 
 /* /lookup's GPU side for a whole host batch over a pool
  * (LookupRequest::process_work + on_hit, lookup_request.cc:153-210,446-482):
- * the batch is cut into residue-balanced shards as kgx_pool_process_batch
- * does (up to twice as many per device: a shard here is one pass, no twin);
- * each runs on its context as ONE pass (its hits stay on the device),
+ * the batch is cut into shards of whole sequences (up to twice as many per
+ * device as kgx_pool_process_batch: a shard here is one pass, no twin; a
+ * device's first and last shards half the others' residues), enqueued in
+ * order on the pool's per-device pass, score and rollup streams with no host
+ * wait; each runs on its context's buffers as ONE pass (its hits stay on the
+ * device),
  * with want within KGX_WANT_CALLS | KGX_WANT_BEST (KGX_WANT_BEST: the
  * find_best_match decision), and then kgx_kmap_rollup over maps[j], the map on
  * that context's device (one map per device the pool spans).  Nothing per hit
