@@ -416,6 +416,9 @@ def main():
                     help="presence filter of 2^N bits (0 = none), kgx_image_set_filter")
     ap.add_argument("--image-layout", choices=["packed", "aos"], default="packed",
                     help="HBM-resident bucket layout (packed when the payloads fit)")
+    ap.add_argument("--line-index", type=int, default=36,
+                    help="kgx_image_set_line_index load, keys per 64 lines (default 36: 9/16 of a key per "
+                         "64-B line, 114 GB beside the 57-GB packed table at C2; 0 = probe the reference slots)")
     ap.add_argument("--want", type=int, default=11,
                     help="KGX_WANT_* mask (11 = hits + calls + device best call, lookup_request find_best_match)")
     ap.add_argument("--no-canary", action="store_true", help="skip the per-device canary self-check")
@@ -476,6 +479,11 @@ def main():
         f"{spec.num_sigs} buckets ({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
     if args.image_layout == "aos":
         img.set_layout(abi.Image.AOS24)
+    if args.line_index and img.layout == abi.Image.PACKED16:
+        t0 = time.time()
+        img.set_line_index(args.line_index)
+        log(f"[bench] line index: {img.line_count:,} lines ({img.line_count * 64 / 1e9:.1f} GB) "
+            f"in {time.time() - t0:.1f}s")
     if args.filter_log2:
         t0 = time.time()
         img.set_filter(args.filter_log2)
@@ -756,7 +764,8 @@ def main():
             try:
                 tj = json.load(open(args.traffic_json))
                 if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
-                        and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout):
+                        and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout
+                        and tj.get("line_index", 0) == (args.line_index if img.line_count else 0)):
                     traffic = tj.get("hbm_bytes_per_launch")
                     traffic_source = (f"not measured in this run: FETCH_SIZE + WRITE_SIZE per probe launch from "
                                       f"profiles/{os.path.basename(args.traffic_json)} "
@@ -836,6 +845,9 @@ def main():
                 # SURVEY §8(d) prices a bucket at the file's 24 B; the PACKED16
                 # resident layout moves 16 B per bucket examined
                 "image_layout": layout,
+                # kgx_image_set_line_index load (0: probes over the reference slots)
+                "line_index": args.line_index if img.line_count else 0,
+                "line_index_lines": img.line_count,
                 "alg_bytes_per_launch_resident_layout": windows_per_launch * (
                     (16.0 if layout == "PACKED16" else 24.0) * pbar + 1.0),
                 # north_star: algorithmic bytes/s (24 P + 1 per window) over the

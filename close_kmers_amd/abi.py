@@ -186,6 +186,8 @@ SIGNATURES = {
     "kgx_image_table": (_P, [_P]),
     "kgx_image_layout": (_INT, [_P]),
     "kgx_image_set_layout": (_INT, [_P, _INT]),
+    "kgx_image_set_line_index": (_INT, [_P, _U32]),
+    "kgx_image_line_count": (_U64, [_P]),
     "kgx_image_set_filter": (_INT, [_P, _INT]),
     "kgx_image_download": (_INT, [_P, _P, _U64]),
     "kgx_ctx_create": (_INT, [_P, _PP]),
@@ -424,6 +426,15 @@ class Image:
 
     def set_layout(self, layout: int) -> None:
         check(lib().kgx_image_set_layout(self.handle, layout), "kgx_image_set_layout")
+
+    def set_line_index(self, keys_per_64_lines: int) -> None:
+        """kgx_image_set_line_index: probes read a copy of the records with
+        line-aligned homes (0 drops it); results are unchanged."""
+        check(lib().kgx_image_set_line_index(self.handle, keys_per_64_lines), "kgx_image_set_line_index")
+
+    @property
+    def line_count(self) -> int:
+        return lib().kgx_image_line_count(self.handle)
 
     def download(self) -> np.ndarray:
         t = np.empty(self.num_sigs, dtype=SIG_DTYPE)

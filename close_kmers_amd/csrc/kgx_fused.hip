@@ -42,7 +42,8 @@ struct FusedArgs {
     uint32_t n;
     uint32_t want;
     const uint4 *table; /* PACKED16 records in HBM */
-    uint64_t num_sigs, magic;
+    uint64_t num_sigs, magic; /* buckets; magic of num_sigs >> hs */
+    uint32_t hs;              /* home = (key mod (num_sigs >> hs)) << hs (kgx_image_set_line_index) */
     kgx_params prm;
     kgx_hit *hits;    /* mapped: sequence s's hits from hits[wbase[s]] */
     kgx_call *calls;  /* mapped: sequence s's calls from calls[wbase[s]] */
@@ -185,7 +186,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
                 key[j] = (uint64_t)ka * 160000u + kb;
                 pend[j] = cmax < 20u;
-                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
+                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs >> a.hs, a.magic) << a.hs : 0;
             }
         }
         __syncthreads(); /* whit cleared */
@@ -280,7 +281,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
                     key[j] = (uint64_t)ka * 160000u + kb;
                     pend[j] = cmax < 20u;
-                    slot[j] = pend[j] ? mod_by(key[j], a.num_sigs, a.magic) : 0;
+                    slot[j] = pend[j] ? mod_by(key[j], a.num_sigs >> a.hs, a.magic) << a.hs : 0;
                 }
             }
             /* linear probe by 64-B lines: a round reads the rest of the line
@@ -781,7 +782,7 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
                               uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
                               kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
                               uint32_t max_windows, uint64_t *dbg, const uint64_t *h_off, const uint64_t *h_wbase,
-                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream)
+                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream, uint32_t hs)
 {
     if (n == 0)
         return hipSuccess;
@@ -795,7 +796,8 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
     a.want = want;
     a.table = static_cast<const uint4 *>(packed_table);
     a.num_sigs = num_sigs;
-    a.magic = mod_magic(num_sigs);
+    a.magic = mod_magic(num_sigs >> hs);
+    a.hs = hs;
     a.prm = prm;
     a.hits = hits;
     a.calls = calls;
@@ -852,7 +854,7 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                                                   const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
                                                   kgx_otu *otus,
                                                   const uint4 *table, uint64_t num_sigs, uint64_t magic,
-                                                  uint64_t life_ticks)
+                                                  uint32_t hs, uint64_t life_ticks)
 {
     __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
     const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
@@ -905,6 +907,7 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         a.table = table;
         a.num_sigs = num_sigs;
         a.magic = magic;
+        a.hs = hs;
         a.prm = h->prm;
         a.hits = hits + (uint64_t)slot * FUSED_MAX_WINDOWS;
         a.calls = calls + (uint64_t)slot * FUSED_MAX_WINDOWS;
@@ -937,16 +940,18 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t life_ticks, int quad_probe, hipStream_t stream)
+                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t hs)
 {
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
     if (quad_probe)
         hipLaunchKernelGGL(svc_kernel<true>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls, otus,
-                           static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
+                           static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs >> hs), hs,
+                           life_ticks);
     else
         hipLaunchKernelGGL(svc_kernel<false>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
-                           otus, static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs), life_ticks);
+                           otus, static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs >> hs), hs,
+                           life_ticks);
     return hipGetLastError();
 }
 

@@ -147,12 +147,16 @@ size_t plan_workspace_bytes(uint32_t n_seq);
 hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
                        uint32_t *tile_seq, uint32_t tile_windows, void *workspace, uint32_t *status,
                        hipStream_t stream);
+/* Probes of PACKED16 records take home_shift: a key's home bucket is
+ * (key mod (num_sigs >> home_shift)) << home_shift and num_sigs counts the
+ * table's buckets.  0: the reference's slot (key mod num_sigs); 2: the line
+ * index of kgx_image_set_line_index (4-bucket lines, homes at line starts). */
 hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint64_t *seq_off,
                         const uint64_t *wbase, const uint32_t *tile_seq, uint32_t n_seq,
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2_words,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream);
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t home_shift = 0);
 /* max_blocks > 0 caps the line probe's grid (its waves then stride over the
  * tiles; option probe_persist); 0 = one workgroup per 4 tiles.
  * The line probe over fq fragments left as DNA (PACKED16 images, probe_j
@@ -161,10 +165,16 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
 hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
                             const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
                             uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, uint32_t max_blocks,
-                            hipStream_t stream);
+                            hipStream_t stream, uint32_t home_shift = 0);
 /* set the filter bits of every stored key of the resident table */
 hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs, uint64_t *filter,
                                uint32_t log2_words, hipStream_t stream);
+/* *count += the PACKED16 table's stored keys */
+hipError_t launch_count_keys(const packed_bucket *t, uint64_t n, unsigned long long *count, hipStream_t stream);
+/* the line index of a PACKED16 table (lines_build_kernel): 4 * n_lines
+ * buckets; *overflow |= 1 when some record found no bucket */
+hipError_t launch_lines_build(const packed_bucket *src, uint64_t num_sigs, packed_bucket *lines, uint64_t n_lines,
+                              uint32_t *overflow, hipStream_t stream);
 /* AoS -> packed; *not_packable |= 1 when some stored bucket does not fit */
 hipError_t launch_pack(const kgx_sig_kmer *table, packed_bucket *packed, uint64_t n,
                        uint32_t *not_packable, hipStream_t stream);
@@ -234,7 +244,7 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
                               uint32_t want, const void *packed_table, uint64_t num_sigs, kgx_params prm,
                               kgx_hit *hits, kgx_call *calls, uint32_t *counts, uint32_t *done, uint32_t token,
                               uint32_t max_windows, uint64_t *dbg, const uint64_t *h_off, const uint64_t *h_wbase,
-                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream);
+                              const uint8_t *h_res, uint32_t inline_res, hipStream_t stream, uint32_t home_shift = 0);
 /* resident call service (kgx_svc.cpp, svc_kernel in kgx_fused.hip): one
  * persistent workgroup per slot polls its slot's request word in mapped host
  * memory and runs fused_small_body on the slot's sequence; no launch per call.
@@ -268,7 +278,7 @@ static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(Svc
  * wall clock, 100 MHz) or on stop */
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t life_ticks, int quad_probe, hipStream_t stream);
+                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t home_shift = 0);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,

@@ -492,7 +492,7 @@ template <int J, int MODE, bool FILTER, bool NT = FILTER>
 __global__ __launch_bounds__(256) void probe_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
-    const void *__restrict__ table_v, uint64_t num_sigs, uint64_t magic,
+    const void *__restrict__ table_v, uint64_t num_sigs, uint64_t magic, uint32_t hs,
     const uint64_t *__restrict__ filter, uint32_t filter_log2,
     uint4 *__restrict__ hot, uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask)
 {
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void probe_kernel(
             const uint64_t m = filter_bits(filter_hash(key[j]));
             pend[j] = (fw[j] & m) == m; /* else stored nowhere: a miss */
         }
-        slot[j] = pend[j] ? mod_by(key[j], num_sigs, magic) : 0;
+        slot[j] = pend[j] ? mod_by(key[j], num_sigs >> hs, magic) << hs : 0; /* hs: kgx_image_set_line_index */
     }
 
     uint4 rec[J]; /* the matching bucket's payload */
@@ -623,7 +623,7 @@ template <int J, int G, bool DNA>
 __global__ __launch_bounds__(256) void probe_line_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
-    const uint4 *__restrict__ packed, uint64_t num_sigs, uint64_t magic, uint4 *__restrict__ hot,
+    const uint4 *__restrict__ packed, uint64_t num_sigs, uint64_t magic, uint32_t hs, uint4 *__restrict__ hot,
     uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask)
 {
     constexpr uint32_t T = 64 * J;
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     uint64_t home[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        home[j] = ok[j] ? mod_by(key[j], num_sigs, magic) : 0;
+        home[j] = ok[j] ? mod_by(key[j], num_sigs >> hs, magic) << hs : 0; /* hs 2: line-aligned homes */
         lds_hit[wave][64 * j + lane] = 0;
     }
 
@@ -743,28 +743,29 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
 template <int J, int G, bool DNA = false>
 static void launch_probe_line(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                               const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
-                              uint32_t n_seq, const void *table, uint64_t num_sigs, uint4 *hot, uint4 *cold,
-                              uint64_t *hit_mask, uint32_t dyn_lds)
+                              uint32_t n_seq, const void *table, uint64_t num_sigs, uint32_t hs, uint4 *hot,
+                              uint4 *cold, uint64_t *hit_mask, uint32_t dyn_lds)
 {
     hipLaunchKernelGGL((probe_line_kernel<J, G, DNA>), grid, dim3(64 * PROBE_WAVES), dyn_lds, stream, residues,
                        n_residues, seq_off, wbase, tile_seq, n_seq, static_cast<const uint4 *>(table),
-                       num_sigs, mod_magic(num_sigs), hot, cold, hit_mask);
+                       num_sigs, mod_magic(num_sigs >> hs), hs, hot, cold, hit_mask);
 }
 
 template <int J, int MODE>
 static void launch_probe_m(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                            const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
-                           uint32_t n_seq, const void *table, uint64_t num_sigs, const uint64_t *filter,
-                           uint32_t filter_log2, uint4 *hot, uint4 *cold, uint64_t *hit_mask)
+                           uint32_t n_seq, const void *table, uint64_t num_sigs, uint32_t hs,
+                           const uint64_t *filter, uint32_t filter_log2, uint4 *hot, uint4 *cold,
+                           uint64_t *hit_mask)
 {
-    const uint64_t magic = mod_magic(num_sigs);
+    const uint64_t magic = mod_magic(num_sigs >> hs);
     if (filter)
         hipLaunchKernelGGL((probe_kernel<J, MODE, true>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
-                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
+                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, hs, filter,
                            filter_log2, hot, cold, hit_mask);
     else
         hipLaunchKernelGGL((probe_kernel<J, MODE, false>), grid, dim3(64 * PROBE_WAVES), 0, stream, residues,
-                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, filter,
+                           n_residues, seq_off, wbase, tile_seq, n_seq, table, num_sigs, magic, hs, filter,
                            filter_log2, hot, cold, hit_mask);
 }
 
@@ -772,12 +773,12 @@ template <int J>
 static void launch_probe_j(dim3 grid, hipStream_t stream, int mode, const uint8_t *residues,
                            uint64_t n_residues, const uint64_t *seq_off, const uint64_t *wbase,
                            const uint32_t *tile_seq, uint32_t n_seq, const void *table,
-                           uint64_t num_sigs, const uint64_t *filter, uint32_t filter_log2, uint4 *hot,
-                           uint4 *cold, uint64_t *hit_mask)
+                           uint64_t num_sigs, uint32_t hs, const uint64_t *filter, uint32_t filter_log2,
+                           uint4 *hot, uint4 *cold, uint64_t *hit_mask)
 {
 #define KGX_PROBE_M(M)                                                                               \
     launch_probe_m<J, M>(grid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table,  \
-                         num_sigs, filter, filter_log2, hot, cold, hit_mask)
+                         num_sigs, hs, filter, filter_log2, hot, cold, hit_mask)
     if (mode == MODE_PACKED_KEY_FIRST)
         KGX_PROBE_M(MODE_PACKED_KEY_FIRST);
     else if (mode == MODE_PACKED)
@@ -794,10 +795,12 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream)
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t hs)
 {
     if (max_tiles == 0)
         return hipSuccess;
+    if (hs && layout != KGX_LAYOUT_PACKED16)
+        return hipErrorInvalidValue; /* line-aligned homes exist for PACKED16 records only */
     /* lds_kb > 0: each probe workgroup reserves that much LDS (unused beyond
      * its own ~9 KB), capping the probe at 160 / lds_kb workgroups per CU so
      * that other contexts' kernels find room beside it */
@@ -810,7 +813,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
     if ((variant == PROBE_LINE || variant == PROBE_LINE8) && layout == KGX_LAYOUT_PACKED16 && !filter) {
 #define KGX_LINE(JJ, GG)                                                                             \
     launch_probe_line<JJ, GG>(lgrid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
-                              num_sigs, hot, cold, hit_mask, dyn_lds);                               \
+                              num_sigs, hs, hot, cold, hit_mask, dyn_lds);                           \
     return hipGetLastError()
         const int key = probe_j * 10 + (variant == PROBE_LINE8 ? 8 : 4);
         switch (key) {
@@ -829,7 +832,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                                                    : (kf ? MODE_KEY_FIRST : MODE_BUCKET);
 #define KGX_PROBE_J(JJ)                                                                              \
     launch_probe_j<JJ>(grid, stream, mode, residues, n_residues, seq_off, wbase, tile_seq, n_seq,   \
-                       table, num_sigs, filter, filter_log2, hot, cold, hit_mask)
+                       table, num_sigs, hs, filter, filter_log2, hot, cold, hit_mask)
     switch (probe_j) {
     case 1: KGX_PROBE_J(1); break;
     case 2: KGX_PROBE_J(2); break;
@@ -846,7 +849,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
 hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64_t *anchor, const uint64_t *wbase,
                             const uint32_t *tile_seq, uint32_t n_seq, uint64_t max_tiles, const void *table,
                             uint64_t num_sigs, uint4 *hot, uint64_t *hit_mask, int probe_j, uint32_t max_blocks,
-                            hipStream_t stream)
+                            hipStream_t stream, uint32_t hs)
 {
     if (max_tiles == 0)
         return hipSuccess;
@@ -854,7 +857,7 @@ hipError_t launch_probe_dna(const uint8_t *bases, uint64_t n_bases, const uint64
     const dim3 grid(max_blocks ? std::min<uint32_t>(tiles_grid, max_blocks) : tiles_grid);
 #define KGX_DNA(JJ)                                                                                  \
     launch_probe_line<JJ, 4, true>(grid, stream, bases, n_bases, anchor, wbase, tile_seq, n_seq, table,  \
-                                   num_sigs, hot, nullptr, hit_mask, 0);                            \
+                                   num_sigs, hs, hot, nullptr, hit_mask, 0);                        \
     return hipGetLastError()
     switch (probe_j) {
     case 1: KGX_DNA(1);
@@ -914,6 +917,88 @@ hipError_t launch_filter_build(const void *table, int layout, uint64_t num_sigs,
 {
     hipLaunchKernelGGL(filter_build_kernel, dim3(8192), dim3(256), 0, stream, table, layout, num_sigs, filter,
                        log2_words);
+    return hipGetLastError();
+}
+
+/* stored keys of a PACKED16 table (grid-stride blocks, one atomic each) */
+__global__ __launch_bounds__(256) void count_keys_kernel(const packed_bucket *__restrict__ t, uint64_t n,
+                                                         unsigned long long *count)
+{
+    uint64_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += (t[i].lo & PACK_KEY_MASK) <= MAX_ENCODED;
+    for (int o = 32; o > 0; o >>= 1)
+        c += __shfl_xor(c, o);
+    if (lane_id() == 0 && c)
+        atomicAdd(count, (unsigned long long)c);
+}
+
+/* The line index (kgx_image_set_line_index): every bucket b of the reference
+ * table whose key the reference's probe of that key reaches first --
+ * lookup_hash_entry (kguts.cc:585-602) walks from key mod num_sigs and stops at
+ * the key or at a stop bucket, so a duplicate further on or an entry behind a
+ * stop is never found -- is inserted into the line table by linear probing
+ * from the start of line (key mod n_lines), 4 buckets a line, by a 64-bit CAS
+ * on the record's first word.  A probe of the line table from that home finds
+ * exactly the records the reference finds, so results are unchanged while
+ * almost every chain ends in its first 64-B line. */
+__global__ __launch_bounds__(256) void lines_build_kernel(const packed_bucket *__restrict__ src, uint64_t num_sigs,
+                                                          uint64_t src_magic, packed_bucket *lines, uint64_t n_lines,
+                                                          uint64_t line_magic, uint32_t *overflow)
+{
+    const uint64_t NB = 4 * n_lines;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < num_sigs;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const packed_bucket e = src[b];
+        const uint64_t key = e.lo & PACK_KEY_MASK;
+        if (key > MAX_ENCODED)
+            continue;
+        bool first = true;
+        for (uint64_t x = mod_by(key, num_sigs, src_magic); x != b; x = x + 1 == num_sigs ? 0 : x + 1) {
+            const uint64_t k2 = src[x].lo & PACK_KEY_MASK;
+            if (k2 == key || k2 > MAX_ENCODED) {
+                first = false;
+                break;
+            }
+        }
+        if (!first)
+            continue;
+        uint64_t x = mod_by(key, n_lines, line_magic) * 4;
+        bool placed = false;
+        for (uint64_t n = 0; n < NB && !placed; n++) {
+            const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long *>(&lines[x].lo),
+                                                      (unsigned long long)EMPTY_KEY, (unsigned long long)e.lo);
+            if (prev == (unsigned long long)EMPTY_KEY) {
+                lines[x].hi = e.hi;
+                placed = true;
+            }
+            x = x + 1 == NB ? 0 : x + 1;
+        }
+        if (!placed)
+            atomicOr(overflow, 1u);
+    }
+}
+
+__global__ __launch_bounds__(256) void fill_empty_kernel(packed_bucket *t, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        t[i].lo = EMPTY_KEY;
+        t[i].hi = 0;
+    }
+}
+
+hipError_t launch_count_keys(const packed_bucket *t, uint64_t n, unsigned long long *count, hipStream_t stream)
+{
+    hipLaunchKernelGGL(count_keys_kernel, dim3(4096), dim3(256), 0, stream, t, n, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_lines_build(const packed_bucket *src, uint64_t num_sigs, packed_bucket *lines, uint64_t n_lines,
+                              uint32_t *overflow, hipStream_t stream)
+{
+    hipLaunchKernelGGL(fill_empty_kernel, dim3(8192), dim3(256), 0, stream, lines, 4 * n_lines);
+    hipLaunchKernelGGL(lines_build_kernel, dim3(8192), dim3(256), 0, stream, src, num_sigs, mod_magic(num_sigs), lines,
+                       n_lines, mod_magic(n_lines), overflow);
     return hipGetLastError();
 }
 

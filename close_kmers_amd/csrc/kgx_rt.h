@@ -316,6 +316,12 @@ struct kgx_image {
     int layout = KGX_LAYOUT_AOS24;
     kgx_sig_kmer *d_table = nullptr;   /* AOS24: the file's buckets */
     kgx::packed_bucket *d_packed = nullptr; /* PACKED16 */
+    /* kgx_image_set_line_index: the PACKED16 records again, 4 buckets a line,
+     * each key's home at the start of line (key mod n_lines); the probes read
+     * it instead of d_packed, which stays for downloads, saves and filters */
+    kgx::packed_bucket *d_lines = nullptr;
+    uint64_t n_lines = 0;
+    uint32_t lines_load = 0; /* keys per 64 lines it was built for */
     uint64_t *d_filter = nullptr;           /* presence filter (kgx_image_set_filter) */
     uint32_t filter_log2_words = 0;
     /* probe order across the image's contexts: the probe is bound by random
@@ -345,6 +351,10 @@ struct kgx_image {
     {
         return num_sigs * (layout == KGX_LAYOUT_PACKED16 ? sizeof(kgx::packed_bucket) : sizeof(kgx_sig_kmer));
     }
+    /* what the probes read: the line index when there is one */
+    const void *probe_table() const { return d_lines ? static_cast<const void *>(d_lines) : resident(); }
+    uint64_t probe_buckets() const { return d_lines ? 4 * n_lines : num_sigs; }
+    uint32_t home_shift() const { return d_lines ? 2u : 0u; }
 };
 
 struct kgx_ctx {

@@ -255,11 +255,23 @@ static int image_unpack(kgx_image *img)
     return KGX_OK;
 }
 
-/* images are packed at load when they fit; otherwise they stay AOS24 */
+/* images are packed at load when they fit; otherwise they stay AOS24.
+ * KGX_LINE_INDEX=<keys per 64 lines> also builds the line index of every
+ * packed image at load (kgx_image_set_line_index; for programs that only
+ * see images through the facade or the server) */
 static int image_settle(kgx_image *img, kgx_image **out)
 {
-    const int rc = image_pack(img);
+    int rc = image_pack(img);
     if (rc == KGX_EDEVICE) {
+        kgx_image_close(img);
+        return rc;
+    }
+    static const long line_load = [] {
+        const char *e = std::getenv("KGX_LINE_INDEX");
+        return e ? std::strtol(e, nullptr, 10) : 0L;
+    }();
+    if (line_load > 0 && img->layout == KGX_LAYOUT_PACKED16 &&
+        (rc = kgx_image_set_line_index(img, (uint32_t)std::min(line_load, 255L)))) {
         kgx_image_close(img);
         return rc;
     }
@@ -514,6 +526,10 @@ int kgx_image_replicate(const kgx_image *src, int device, kgx_image **out)
         kgx_image_close(img);
         return fail(KGX_EDEVICE, std::string("replicate: ") + hipGetErrorString(e));
     }
+    if (src->d_lines && (rc = kgx_image_set_line_index(img, src->lines_load))) { /* built again there */
+        kgx_image_close(img);
+        return rc;
+    }
     *out = img;
     return KGX_OK;
 }
@@ -693,6 +709,8 @@ int kgx_image_close(kgx_image *img)
         (void)hipFree(img->d_table);
     if (img->d_packed)
         (void)hipFree(img->d_packed);
+    if (img->d_lines)
+        (void)hipFree(img->d_lines);
     if (img->d_filter)
         (void)hipFree(img->d_filter);
     if (img->probe_stream) {
@@ -746,10 +764,77 @@ int kgx_image_set_layout(kgx_image *img, int layout)
     const auto hold = svc_shutdown_hold(img);
     if (layout == KGX_LAYOUT_PACKED16)
         return image_pack(img);
-    if (layout == KGX_LAYOUT_AOS24)
+    if (layout == KGX_LAYOUT_AOS24) {
+        if (img->d_lines) { /* the line index holds PACKED16 records */
+            HIP_TRY(hipSetDevice(img->device));
+            HIP_TRY(hipDeviceSynchronize());
+            (void)hipFree(img->d_lines);
+            img->d_lines = nullptr;
+            img->n_lines = 0;
+        }
         return image_unpack(img);
+    }
     return fail(KGX_EINVAL, "unknown layout " + std::to_string(layout));
 }
+
+int kgx_image_set_line_index(kgx_image *img, uint32_t keys_per_64_lines)
+{
+    if (!img)
+        return fail(KGX_EINVAL, "null image");
+    if (keys_per_64_lines > 255)
+        return fail(KGX_EINVAL, "line index load: 0 (none) or 1 .. 255 keys per 64 lines");
+    /* the service's workgroups hold the probe table's address */
+    const auto hold = svc_shutdown_hold(img);
+    HIP_TRY(hipSetDevice(img->device));
+    HIP_TRY(hipDeviceSynchronize());
+    if (img->d_lines)
+        (void)hipFree(img->d_lines);
+    img->d_lines = nullptr;
+    img->n_lines = 0;
+    if (!keys_per_64_lines)
+        return KGX_OK;
+    if (img->layout != KGX_LAYOUT_PACKED16)
+        return fail(KGX_EINVAL, "a line index needs a PACKED16 image");
+    unsigned long long *d_count = nullptr;
+    uint32_t *d_over = nullptr;
+    HIP_TRY(hipMalloc(&d_count, 16));
+    d_over = reinterpret_cast<uint32_t *>(d_count + 1);
+    hipError_t e = hipMemset(d_count, 0, 16);
+    if (e == hipSuccess)
+        e = launch_count_keys(img->d_packed, img->num_sigs, d_count, nullptr);
+    unsigned long long n_keys = 0;
+    if (e == hipSuccess)
+        e = hipMemcpy(&n_keys, d_count, 8, hipMemcpyDeviceToHost);
+    /* lines: n_keys * 64 / load, odd and prime to 5 (keys are base-20 codes) */
+    uint64_t n_lines = std::max<uint64_t>(1, (uint64_t)(((unsigned __int128)n_keys * 64 + keys_per_64_lines - 1) /
+                                                        keys_per_64_lines));
+    while (n_lines % 2 == 0 || n_lines % 5 == 0)
+        n_lines++;
+    packed_bucket *lines = nullptr;
+    if (e == hipSuccess && (4 * n_lines >= (1ull << 40) || hipMalloc(&lines, 4 * n_lines * sizeof(packed_bucket)) != hipSuccess)) {
+        (void)hipGetLastError();
+        (void)hipFree(d_count);
+        return fail(KGX_ENOMEM, "no room for the line index (" + std::to_string(4 * n_lines * 16) + " B)");
+    }
+    uint32_t over = 0;
+    if (e == hipSuccess)
+        e = launch_lines_build(img->d_packed, img->num_sigs, lines, n_lines, d_over, nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(&over, d_over, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_count);
+    if (e != hipSuccess || over) {
+        if (lines)
+            (void)hipFree(lines);
+        return fail(KGX_EDEVICE, e != hipSuccess ? std::string("line index: ") + hipGetErrorString(e)
+                                                 : std::string("line index: a record found no bucket"));
+    }
+    img->d_lines = lines;
+    img->n_lines = n_lines;
+    img->lines_load = keys_per_64_lines;
+    return KGX_OK;
+}
+
+uint64_t kgx_image_line_count(const kgx_image *img) { return img ? img->n_lines : 0; }
 
 /* buckets [first, first + count) in the file's format into host memory */
 static int image_read(const kgx_image *img, uint64_t first, uint64_t count, kgx_sig_kmer *dst)
@@ -1317,9 +1402,9 @@ int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const ui
                                 "(set fq_residues 1 for other probes)");
     return probe_chained(c, [&] {
         return launch_probe_dna(bases, n_bases, anchors, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                                c->n_seq, c->max_tiles, c->img->resident(), c->img->num_sigs, c->hits.as<uint4>(),
-                                c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64), probe_max_blocks(c),
-                                c->stream);
+                                c->n_seq, c->max_tiles, c->img->probe_table(), c->img->probe_buckets(),
+                                c->hits.as<uint4>(), c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64),
+                                probe_max_blocks(c), c->stream, c->img->home_shift());
     });
 }
 
@@ -1333,11 +1418,11 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
         return fail(KGX_EINVAL, "probe: residues missing or offsets differ from the plan");
     return probe_chained(c, [&] {
         return launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                            c->n_seq, c->max_tiles, c->img->resident(), c->img->layout, c->img->num_sigs,
+                            c->n_seq, c->max_tiles, c->img->probe_table(), c->img->layout, c->img->probe_buckets(),
                             c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                             c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
                             (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb,
-                            probe_max_blocks(c), c->stream);
+                            probe_max_blocks(c), c->stream, c->img->home_shift());
     });
 }
 
@@ -2868,7 +2953,8 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
         HIP_TRY(c->h_fdbg.device_ptr(0, &d_dbg));
     }
     HIP_TRY(launch_fused_small(static_cast<const uint8_t *>(d_res), static_cast<const uint64_t *>(d_off),
-                               static_cast<const uint64_t *>(d_wb), n_seq, want, c->img->d_packed, c->img->num_sigs, p,
+                               static_cast<const uint64_t *>(d_wb), n_seq, want, c->img->probe_table(),
+                               c->img->probe_buckets(), p,
                                static_cast<kgx_hit *>(d_hits), static_cast<kgx_call *>(d_calls),
                                static_cast<uint32_t *>(d_counts), static_cast<uint32_t *>(d_done), token,
                                (uint32_t)longest, static_cast<uint64_t *>(d_dbg), c->h_off_stage.data(),
@@ -2876,7 +2962,7 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
                                c->fused_inline && n_seq <= FUSED_INLINE_SEQ && off[n_seq] <= FUSED_INLINE_RES
                                    ? (uint32_t)std::max<uint64_t>(off[n_seq], 1)
                                    : 0u,
-                               c->stream));
+                               c->stream, c->img->home_shift()));
     /* every sequence's token (stored after its results, behind a
      * system-scope fence); a fault or a lost store still ends the wait */
     const volatile uint32_t *done = c->h_fdone.data();

@@ -72,7 +72,8 @@ struct SvcState {
     kgx_call *d_calls = nullptr;
     kgx_otu *d_otus = nullptr;
     const void *table = nullptr;
-    uint64_t num_sigs = 0;
+    uint64_t num_sigs = 0; /* buckets of the probe table */
+    uint32_t home_shift = 0;
     /* the host side of each slot, a line apiece: a call touches only its
      * own slot's line (a pool's threads each settle on a slot of their own,
      * take_slot), never one that every caller writes */
@@ -183,7 +184,7 @@ int top_up(SvcState *s)
         /* wall clock at 100 MHz: 100 ticks per us */
         hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->d_otus, s->slots,
                                   s->table,
-                                  s->num_sigs, s->life_us * 100, s->quad_probe, s->stream);
+                                  s->num_sigs, s->life_us * 100, s->quad_probe, s->stream, s->home_shift);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
         if (e != hipSuccess) {
@@ -271,8 +272,9 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
     s->slots = slots;
     s->idle_us = idle_us;
     s->life_us = life_us;
-    s->table = img->d_packed;
-    s->num_sigs = img->num_sigs;
+    s->table = img->probe_table();
+    s->num_sigs = img->probe_buckets();
+    s->home_shift = img->home_shift();
     const size_t b_hdr = align64(slots * sizeof(SvcSlotHdr)), b_out = align64(slots * sizeof(SvcSlotOut)),
                  b_dbg = align64(slots * sizeof(SvcSlotDbg)), b_res = align64((size_t)slots * SVC_RES_STRIDE),
                  b_hits = align64((size_t)slots * FUSED_MAX_WINDOWS * sizeof(kgx_hit)),

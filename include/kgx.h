@@ -251,6 +251,20 @@ int kgx_image_layout(const kgx_image *img);
 /* convert the resident table in place; KGX_ERANGE if PACKED16 is asked for
  * an image whose payloads do not fit (the image is left unchanged) */
 int kgx_image_set_layout(kgx_image *img, int layout);
+/* Line index of a PACKED16 image: the same records again in 64-B lines of 4
+ * buckets, each key's home at the start of line (key mod n_lines), n_lines =
+ * stored keys * 64 / keys_per_64_lines (0 drops the index).  Built from every
+ * bucket the reference's probe (lookup_hash_entry, kguts.cc:585-602) reaches
+ * first for its key -- a duplicate further on, or an entry behind a stop
+ * bucket, is never found there and is left out -- so every probe (batches,
+ * fq, the call service) returns exactly what it returns over the reference
+ * slots, while a key's chain nearly always ends in its first line: one random
+ * 64-B request per window instead of ~1.05.  Costs 64 B * n_lines of HBM
+ * beside the PACKED16 table, which downloads, saves and filters keep using.
+ * Like set_layout, no call may run on the image meanwhile. */
+int kgx_image_set_line_index(kgx_image *img, uint32_t keys_per_64_lines);
+/* lines of the image's line index (0: none) */
+uint64_t kgx_image_line_count(const kgx_image *img);
 /* Presence filter: 2^log2_bits bits (0 removes it), two bits per stored key
  * in one 64-bit word (blocked Bloom filter).  A probe whose key misses the
  * filter skips the table -- exactly the miss it would have found -- so

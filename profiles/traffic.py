@@ -62,6 +62,7 @@ def main():
         "n_keys": cfg["n_keys"], "keys_stored": cfg.get("keys_stored"), "n_seq": cfg["n_seq_per_gpu"],
         "length": cfg["seq_len"],
         "image_layout": (bench.get("roofline") or {}).get("image_layout", "AOS24"),
+        "line_index": (bench.get("roofline") or {}).get("line_index", 0),
         "fetch_bytes_per_launch": pf, "write_bytes_per_launch": pw,
         "hbm_bytes_per_launch": (pf or 0) + (pw or 0) if pf is not None else None,
         "probe_dispatches": {"fetch": nf, "write": nw},
