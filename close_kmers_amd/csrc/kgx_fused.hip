@@ -541,6 +541,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             p_pos = rl32(pos, n - 1);
             p_fi = rl32(fi, n - 1);
             p_wt = rlf(wt, n - 1);
+            if (dbg && h0 == 0)
+                a.dbg[9] = wall_clock64(); /* the first 64-hit chunk scored */
         }
         if (o_valid) /* the final flush (kguts.cc:873-876) */
             close_open();

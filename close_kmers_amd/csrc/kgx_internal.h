@@ -264,7 +264,8 @@ struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the p
 };
 struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
     uint64_t stamp[16]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
-                           0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order */
+                           0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order, 9 the
+                           scorer's first chunk done */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */

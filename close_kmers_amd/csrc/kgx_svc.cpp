@@ -631,7 +631,9 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         if (want & KGX_WANT_OTU) {
             s->phase_ns[6] += (st[4] - st[7]) * 10; /* the OTU tally alone */
             s->phase_ns[7] += (st[4] - st[8]) * 10; /* ... its sort by count */
-
+        } else if (st[9] >= st[6] && st[9] <= st[4]) {
+            s->phase_ns[6] += (st[9] - st[6]) * 10; /* the scorer's first 64-hit chunk */
+            s->phase_ns[7] += (st[4] - st[9]) * 10; /* its other chunks and the final flush */
         }
     }
     const SvcSlotOut &o = s->out[slot];
