@@ -479,10 +479,12 @@ def main():
         f"{spec.num_sigs} buckets ({spec.num_sigs * 24 / 1e9:.1f} GB) on device {dev} in {time.time() - t0:.1f}s")
     if args.image_layout == "aos":
         img.set_layout(abi.Image.AOS24)
+    line_lines = 0
     if args.line_index and img.layout == abi.Image.PACKED16:
         t0 = time.time()
         img.set_line_index(args.line_index)
-        log(f"[bench] line index: {img.line_count:,} lines ({img.line_count * 64 / 1e9:.1f} GB) "
+        line_lines = img.line_count
+        log(f"[bench] line index: {line_lines:,} lines ({line_lines * 64 / 1e9:.1f} GB) "
             f"in {time.time() - t0:.1f}s")
     if args.filter_log2:
         t0 = time.time()
@@ -765,7 +767,7 @@ def main():
                 tj = json.load(open(args.traffic_json))
                 if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
                         and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout
-                        and tj.get("line_index", 0) == (args.line_index if img.line_count else 0)):
+                        and tj.get("line_index", 0) == (args.line_index if line_lines else 0)):
                     traffic = tj.get("hbm_bytes_per_launch")
                     traffic_source = (f"not measured in this run: FETCH_SIZE + WRITE_SIZE per probe launch from "
                                       f"profiles/{os.path.basename(args.traffic_json)} "
@@ -846,8 +848,8 @@ def main():
                 # resident layout moves 16 B per bucket examined
                 "image_layout": layout,
                 # kgx_image_set_line_index load (0: probes over the reference slots)
-                "line_index": args.line_index if img.line_count else 0,
-                "line_index_lines": img.line_count,
+                "line_index": args.line_index if line_lines else 0,
+                "line_index_lines": line_lines,
                 "alg_bytes_per_launch_resident_layout": windows_per_launch * (
                     (16.0 if layout == "PACKED16" else 24.0) * pbar + 1.0),
                 # north_star: algorithmic bytes/s (24 P + 1 per window) over the
