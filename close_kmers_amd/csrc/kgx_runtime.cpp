@@ -526,10 +526,8 @@ int kgx_image_replicate(const kgx_image *src, int device, kgx_image **out)
         kgx_image_close(img);
         return fail(KGX_EDEVICE, std::string("replicate: ") + hipGetErrorString(e));
     }
-    if (src->d_lines && (rc = kgx_image_set_line_index(img, src->lines_load))) { /* built again there */
-        kgx_image_close(img);
-        return rc;
-    }
+    /* the line index is the caller's choice per replica (kgx_image_set_line_index):
+     * it doubles the HBM an image takes, and a device may already hold one */
     *out = img;
     return KGX_OK;
 }

@@ -261,7 +261,8 @@ int kgx_image_set_layout(kgx_image *img, int layout);
  * slots, while a key's chain nearly always ends in its first line: one random
  * 64-B request per window instead of ~1.05.  Costs 64 B * n_lines of HBM
  * beside the PACKED16 table, which downloads, saves and filters keep using.
- * Like set_layout, no call may run on the image meanwhile. */
+ * Like set_layout, no call may run on the image meanwhile.  Replicas
+ * (kgx_image_replicate) do not inherit it: build it on each that should. */
 int kgx_image_set_line_index(kgx_image *img, uint32_t keys_per_64_lines);
 /* lines of the image's line index (0: none) */
 uint64_t kgx_image_line_count(const kgx_image *img);
