@@ -554,13 +554,9 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
      * the flagged hits' distinct OTUs in its registers -- lane j holds the
      * j-th value met and its count, one ballot round per distinct value among
      * each 64 hits -- and places each value by its rank among the others (=
-     * the std::map's key order).  Past 8 distinct values that costs more than
-     * sorting: the values are compacted in hit order (ballots) and sorted --
-     * a bitonic network over P = max(256, 2^ceil(log2 m)) entries, P / 256
-     * per thread in registers: exchanges within a wave by lane shuffles,
-     * between waves through LDS, between a thread's own entries in place --
-     * and each run of equal values is one pair, in ascending key order.  Then
-     * the pairs are std::sort'ed by count: lstd_sort_wave64 / lstd_sort_on
+     * the std::map's key order).  Past 8 distinct values an LDS hash counts
+     * them and the distinct pairs are sorted by value (below).  Then the
+     * pairs are std::sort'ed by count: lstd_sort_wave64 / lstd_sort_on
      * replay libstdc++'s tie order.  (r4b: O(m^2) count and rank scans, 18.8
      * us at 36 OTUs per call, 6.6 at 3; r4c: the register list alone, 22.6 /
      * 1.8; r4d: the sort alone, 15.9 / 4.4.) */
@@ -613,7 +609,15 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         __syncthreads();
         uint32_t d = n_otu;
         if (d == ~0u) {
-            d = 0;
+            /* past KREG distinct values: the flagged hits' OTUs counted in an
+             * LDS hash (256 FJ slots: one per window at least, so it never
+             * fills), the distinct (value, count) pairs compacted, then
+             * sorted by value -- one wave's register bitonic network up to 64
+             * pairs, a block network beyond.  (r4o: a bitonic sort of every
+             * flagged hit's value, then runs -- 6.1 us of the 36-OTU tally.) */
+            constexpr uint32_t H = 256 * FJ;
+            /* the flagged values first, compacted in hit order into hpos (the
+             * records in hrec are dead then), so the hash can use hrec */
             int32_t *v = reinterpret_cast<int32_t *>(hpos);
             uint32_t m = 0;
             for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
@@ -635,85 +639,32 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 m += total;
                 __syncthreads();
             }
-            uint32_t R = 1;
-            while (256u * R < m)
-                R <<= 1;
-            const uint32_t P = 256u * R;
-            /* BJ entries per thread in registers (up to 512 values); more go
-             * through LDS stage by stage (proteins past 520 aa with many
-             * flagged hits) -- registers for all FJ slices made the common
-             * path's code heavier (r4o-r4x: 36-OTU tally 8.8 -> 11.0 us) */
-            constexpr uint32_t BJ = FJ < 2 ? FJ : 2;
-            if (R <= BJ) {
-                int32_t val[BJ];
-#pragma unroll
-                for (uint32_t r = 0; r < BJ; r++) {
-                    const uint32_t e = t + 256u * r;
-                    val[r] = (r < R && e < m) ? v[e] : INT32_MAX; /* the padding sorts last */
-                }
-                __syncthreads(); /* every entry read before the exchanges write v */
-                for (uint32_t k = 2; k <= P; k <<= 1) {
-                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                        if (j >= 256) { /* a thread's own entries 0 and 1 */
-                            if constexpr (BJ > 1) {
-                                const bool up = (t & k) == 0;
-                                const int32_t lo = min(val[0], val[1]), hi = max(val[0], val[1]);
-                                val[0] = up ? lo : hi;
-                                val[1] = up ? hi : lo;
-                            }
-                        } else {
-                            if (j >= 64) { /* the partner is in another wave */
-#pragma unroll
-                                for (uint32_t r = 0; r < BJ; r++)
-                                    if (r < R)
-                                        v[t + 256u * r] = val[r];
-                                __syncthreads();
-                            }
-#pragma unroll
-                            for (uint32_t r = 0; r < BJ; r++) {
-                                if (r < R) {
-                                    const uint32_t e = t + 256u * r;
-                                    const int32_t b = j >= 64 ? v[e ^ j] : xor_lane(val[r], j);
-                                    /* the pair's lower entry keeps the min when ascending */
-                                    const bool keep_min = ((e & j) == 0) == ((e & k) == 0);
-                                    val[r] = keep_min ? min(val[r], b) : max(val[r], b);
-                                }
-                            }
-                            if (j >= 64)
-                                __syncthreads();
-                        }
-                    }
-                }
-#pragma unroll
-                for (uint32_t r = 0; r < BJ; r++)
-                    if (r < R)
-                        v[t + 256u * r] = val[r];
-            } else {
-                for (uint32_t e = m + t; e < P; e += 256)
-                    v[e] = INT32_MAX;
-                __syncthreads();
-                for (uint32_t k = 2; k <= P; k <<= 1)
-                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                        for (uint32_t i = t; i < P; i += 256) {
-                            const uint32_t ixj = i ^ j;
-                            if (ixj > i) {
-                                const int32_t x = v[i], y = v[ixj];
-                                if ((x > y) == ((i & k) == 0)) {
-                                    v[i] = y;
-                                    v[ixj] = x;
-                                }
-                            }
-                        }
-                        __syncthreads();
-                    }
+            int32_t *hk = reinterpret_cast<int32_t *>(hrec) + 2 * 256 * FJ; /* past the pairs */
+            uint32_t *hcnt = reinterpret_cast<uint32_t *>(hrec) + 3 * 256 * FJ;
+            for (uint32_t i = t; i < H; i += 256) {
+                hk[i] = INT32_MIN; /* OTUs are -1 .. 2^21 - 2 */
+                hcnt[i] = 0;
             }
             __syncthreads();
-            /* each run's first entry, compacted in order: its value, and the
-             * run's length to the next first */
-            uint32_t *first = reinterpret_cast<uint32_t *>(hrec) + 2 * 256 * FJ;
-            for (uint32_t r = 0; r < R; r++) {
-                const uint32_t e = t + 256u * r;
-                const bool f = e < m && (e == 0 || v[e - 1] != v[e]);
+            for (uint32_t i = t; i < m; i += 256) {
+                const int32_t x = v[i];
+                uint32_t h = ((uint32_t)x * 0x9E3779B1u) & (H - 1);
+                for (;;) {
+                    const int32_t old = atomicCAS(hk + h, INT32_MIN, x);
+                    if (old == INT32_MIN || old == x)
+                        break;
+                    h = (h + 1) & (H - 1);
+                }
+                atomicAdd(hcnt + h, 1u);
+            }
+            __syncthreads();
+            /* the pairs, packed (value with its sign bit flipped << 32 | count)
+             * so that unsigned order is the map's key order */
+            uint64_t *pk = reinterpret_cast<uint64_t *>(o);
+            d = 0;
+            for (uint32_t j = 0; j < H / 256; j++) {
+                const uint32_t i = t + 256 * j;
+                const bool f = hk[i] != INT32_MIN;
                 const uint64_t bm = __ballot(f);
                 if (lane == 0)
                     wave_cnt[wave] = (uint32_t)__popcll(bm);
@@ -724,13 +675,49 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     total += wave_cnt[w];
                 }
                 if (f)
-                    first[d + before + lanes_below(bm)] = e;
+                    pk[d + before + lanes_below(bm)] = (uint64_t)((uint32_t)hk[i] ^ 0x80000000u) << 32 | hcnt[i];
                 d += total;
                 __syncthreads();
             }
+            if (d <= 64) {
+                if (wave == 0) {
+                    uint64_t x = lane < d ? pk[lane] : ~0ull; /* the padding sorts last */
+                    for (uint32_t k = 2; k <= 64; k <<= 1)
+                        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                            const uint64_t y = (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)x, j) |
+                                               (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)(x >> 32), j) << 32;
+                            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+                            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+                        }
+                    if (lane < d)
+                        pk[lane] = x;
+                }
+            } else {
+                uint32_t P = 128;
+                while (P < d)
+                    P <<= 1;
+                for (uint32_t i = d + t; i < P; i += 256)
+                    pk[i] = ~0ull;
+                __syncthreads();
+                for (uint32_t k = 2; k <= P; k <<= 1)
+                    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                        for (uint32_t i = t; i < P; i += 256) {
+                            const uint32_t ixj = i ^ j;
+                            if (ixj > i) {
+                                const uint64_t x = pk[i], y = pk[ixj];
+                                if ((x > y) == ((i & k) == 0)) {
+                                    pk[i] = y;
+                                    pk[ixj] = x;
+                                }
+                            }
+                        }
+                        __syncthreads();
+                    }
+            }
+            __syncthreads();
             for (uint32_t i = t; i < d; i += 256) {
-                const uint32_t e = first[i], e2 = i + 1 < d ? first[i + 1] : m;
-                o[i] = kgx_otu{v[e], (int32_t)(e2 - e)};
+                const uint64_t x = pk[i];
+                o[i] = kgx_otu{(int32_t)((uint32_t)(x >> 32) ^ 0x80000000u), (int32_t)(uint32_t)x};
             }
             __syncthreads();
         }
