@@ -11,12 +11,14 @@
 set -euo pipefail
 TAG=${1:-check}
 QUICK=${2:-}
+PART=${3:-all} # 1: suite, bench, C3, C4, HTTP; 2: facade, pool, OTU phases, host-path sweep (each fits one gpurun call)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$R"
 NOCPU=""
 [ "$QUICK" = "quick" ] && NOCPU="--no-cpu-baseline"
+if [ "$PART" != 2 ]; then
 timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 timeout -k 10 900 python3 bench.py $NOCPU > "$OUT/bench.json" 2> "$OUT/bench.err"
@@ -25,6 +27,8 @@ timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$O
 timeout -k 10 600 python3 tools/bench_server.py > "$OUT/bench_server.json" 2> "$OUT/bench_server.err"
 timeout -k 10 900 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
     --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
+fi
+if [ "$PART" != 1 ]; then
 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
 KGX_FACADE_OTU=1 KGX_FACADE_MODES=2 timeout -k 10 300 python3 tools/bench_facade.py \
     > "$OUT/bench_facade_otu.json" 2> "$OUT/bench_facade_otu.err"
@@ -33,4 +37,5 @@ timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool_devices.j
 KGX_SVC_DEBUG=1 timeout -k 10 300 python3 tests/perf_svc_otu_phases.py > "$OUT/svc_otu_phases.json" 2> "$OUT/svc_otu_phases.err"
 timeout -k 10 600 python3 tools/host_path_probe.py --compact --no-pieces --chunks 4,6 --copy 1 --hits16 1 --stream 1 \
     --rec12 1 --score 1 --stage 4,8,12 --want 11 > "$OUT/host_path_sweep.json" 2> "$OUT/host_path_sweep.err"
+fi
 echo "[gpu_check] done" >&2
