@@ -121,3 +121,40 @@ def test_pinned_input_streamed_and_one_pass(world):
         assert ctx.stat("nul_reruns") == n0 + 2
         assert a.hits.tobytes() == b.hits.tobytes() and a.calls.tobytes() == b.calls.tobytes()
         assert a.best.tobytes() == b.best.tobytes()
+
+
+def test_pool_lookup_tiny_growing_batches_and_pinned_nul(world):
+    """Fewer sequences than shards (empty shards, uneven edge shares), batches
+    that grow and shrink between calls on one pool (each context's rollup is
+    sized by its previous event count: too small, then large enough), and a
+    NUL in pinned input (that shard's pass and rollup run again, staged)."""
+    spec, table, img = world
+    rng = np.random.default_rng(77)
+    keys, ids = family_pairs(spec, spec.n_src, rng)
+    res_all, off_all = synth.make_queries(spec, 4000, x_permille=3, q0=11)
+    want = abi.WANT_BEST | abi.WANT_CALLS
+    with abi.Kmap(0, abi.KMAP_SET) as fam, abi.Context(img) as ctx, abi.Pool([img], 4) as pool:
+        fam.add(keys, ids)
+
+        def check(n, res=None):
+            off = off_all[:n + 1] - off_all[0]
+            base = res_all[:int(off[-1])] if res is None else res
+            got, roff, rows = pool.lookup([fam], base, off, want=want)
+            if n == 0:
+                assert len(rows) == 0 and roff.tolist() == [0]
+                return 0
+            one = ctx.process_batch(res_all[:int(off[-1])] if res is None else np.array(base), off, want=want)
+            woff, wrows = fam.rollup(ctx, abi.ROLLUP_FAMILY)
+            _rows_equal(roff, rows, woff, wrows)
+            assert np.array_equal(got.call_offsets, one.call_offsets)
+            assert got.best.tobytes() == one.best.tobytes()
+            return len(rows)
+
+        for n in (0, 1, 3, 5, 2000, 40, 4000, 7):
+            check(n)
+        # a NUL in pinned residues: the staged rerun cuts that sequence there
+        n = 3000
+        pres = abi.pinned_empty(int(off_all[n] - off_all[0]))
+        pres[:] = res_all[:len(pres)]
+        pres[int(off_all[1500]) + 50] = 0
+        check(n, pres)
