@@ -105,6 +105,10 @@ struct kgx_pool {
      * runtime put on one queue; r5z/r6b: 2.08-2.10 ms with these streams,
      * deterministic; more hardware queues than 4 measured slower still.) */
     std::vector<hipStream_t> pass_stream, score_stream, roll_stream;
+    /* kgx_pool_lookup stages a pageable batch shard after shard from one
+     * thread, so each shard's copy into pinned memory gets all the process's
+     * CPUs (a context's own stage pool has its share: cpus / contexts) */
+    std::unique_ptr<HostPool> lookup_stage;
     std::vector<hipEvent_t> pass_done, roll_done;
     std::vector<uint32_t> runners(uint32_t per) const
     {
@@ -609,8 +613,10 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
                     rs = p->roll_stream[(size_t)dev];
         c->stream = ps;
         c->score_stream = ss;
+        if (!p->lookup_stage)
+            p->lookup_stage.reset(new HostPool(std::max(1u, host_cpu_budget())));
         rcs[i] = one_pass_enqueue(c, params, residues, seq_offsets + cuts[i], cuts[i + 1] - cuts[i], want,
-                                  p->up_stream[(size_t)dev], p->up_done[i]);
+                                  p->up_stream[(size_t)dev], p->up_done[i], p->lookup_stage.get());
         c->score_variant = sv;
         c->score_stream = nullptr;
         c->stream = ss; /* the counts and best calls behind the score */

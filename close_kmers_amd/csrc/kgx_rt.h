@@ -142,8 +142,11 @@ bool host_pinned_range(const void *p, uint64_t n, const void **device_address = 
 /* one pass over a whole host batch, split into enqueue and collect
  * (kgx_runtime.cpp): the upload by pull kernels on `up` (recording up_done)
  * when given, else on the context's stream */
+class HostPool;
+/* stage: the threads that copy pageable residues into the context's pinned
+ * staging (null: the context's own stage pool) */
 int one_pass_enqueue(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
-                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done);
+                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done, HostPool *stage = nullptr);
 int one_pass_collect(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
                      uint32_t n_seq, uint32_t want, kgx_result *out);
 

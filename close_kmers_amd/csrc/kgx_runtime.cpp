@@ -1898,7 +1898,7 @@ int collect_counts_enqueue(kgx_ctx *c, uint32_t want)
  * waits for, when given, else on the context's stream -- then the device pass
  * (plan, probe, score).  A caller-pinned batch is NUL-scanned on the device. */
 int one_pass_enqueue(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
-                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done)
+                     uint32_t n_seq, uint32_t want, hipStream_t up, hipEvent_t up_done, HostPool *stage)
 {
     const uint64_t r0 = n_seq ? seq_offsets[0] : 0, n_res = n_seq ? seq_offsets[n_seq] - r0 : 0;
     /* the residues to copy: the caller's pinned buffer, or our staging */
@@ -1910,8 +1910,8 @@ int one_pass_enqueue(kgx_ctx *c, const kgx_params *params, const char *residues,
         stage_offsets_into(c->h_off_stage.data(), seq_offsets, 0, n_seq);
         c->pinned_batches++;
     } else {
-        HostPool *sp = nullptr;
-        if (c->stage_threads > 1 && n_res >= (1u << 20)) {
+        HostPool *sp = stage;
+        if (!sp && c->stage_threads > 1 && n_res >= (1u << 20)) {
             if (!c->stage_pool || c->stage_pool->size() != (unsigned)c->stage_threads)
                 c->stage_pool.reset(new HostPool((unsigned)c->stage_threads));
             sp = c->stage_pool.get();
