@@ -159,6 +159,11 @@ def test_c2_full_scale(gpu, oracle_lib, bench_image):
         want = _oracle_sample(oracle_lib, table, res, off, idx)
         del table
         _assert_sample(r1["hits"], r1["hit_offsets"], r1["calls"], r1["call_offsets"], want, idx)
+        # the line index (the bench's default, load 36) gives the same results
+        img.set_line_index(36)
+        assert img.line_count > 10 ** 9
+        _same(r1, run())
+        img.set_line_index(0)
         # the file's 24-byte layout gives the same results
         img.set_layout(gpu.Image.AOS24)
         _same(r1, run())
