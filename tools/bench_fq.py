@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--score-variant", type=int, default=-1, help="-1 = the library default")
     ap.add_argument("--probe-lds-kb", type=int, default=-1, help="-1 = the library default")
     ap.add_argument("--probe-persist", type=int, default=-1, help="line-probe grid cap per CU; -1 = the library default")
+    ap.add_argument("--line-index", type=int, default=36,
+                    help="kgx_image_set_line_index load (keys per 64 lines; 0 = probe the reference slots)")
     ap.add_argument("--fq-residues", type=int, default=0,
                     help="1 = fragments with residues + the residue probe; 0 (default) = anchors + the DNA probe")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -93,6 +95,9 @@ def main():
     spec = synth.ImageSpec(int(args.n_keys))
     t0 = time.time()
     img, stored = abi.Image.synthetic(spec.n_keys, spec.num_sigs)
+    if args.line_index and img.layout == abi.Image.PACKED16:
+        img.set_line_index(args.line_index)
+    line_lines = img.line_count
     ctx = abi.Context(img)
     # worker contexts (own stream + buffers), as for bench.py: one chunk's
     # host-side sizing sync overlaps the other context's kernels
@@ -236,7 +241,8 @@ def main():
         "metric": "fq_process_request reads/s: 6-frame translate + lookup (C4)",
         "value": n / t_dev, "unit": "reads/s", "ms_per_10M": t_dev * 1e3 * 1e7 / n,
         "config": {"n_reads": n, "read_len": Lr, "chunk": chunk, "worker_contexts": len(ctxs), "host_threads": args.threads or 1, "size_ahead": int(bool(args.ahead) and len(ctxs) >= 2), "score_variant": args.score_variant, "probe_lds_kb": args.probe_lds_kb, "probe_persist": args.probe_persist, "fq_residues": args.fq_residues, "options": args.opt, "n_keys": spec.n_keys,
-                   "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout]},
+                   "num_sigs": spec.num_sigs, "image_layout": ["AOS24", "PACKED16"][img.layout],
+                   "line_index": args.line_index if line_lines else 0},
         "per_pass": stats,
         "handler": {"reads": hn, "reads_per_s": hn / t_h, "ms": t_h * 1e3, "output_lines": out.count(b"\n"),
                     "fastq_bytes": len(text), "blocks": -(-len(text) // blk), "block_bytes": blk,
