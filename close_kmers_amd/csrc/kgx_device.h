@@ -79,6 +79,25 @@ __device__ __forceinline__ float rlf(float v, uint32_t l)
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+/* acc + w of each lane in mm, lane order (an f32 sum taken hit by hit).  Past
+ * a few lanes, every lane is added with non-members as -0.0f (x + -0.0f == x
+ * bit for bit), so the 64 lane reads do not wait on the chain of adds */
+__device__ __forceinline__ float sum_lanes_in_order(float acc, float w, uint64_t mm)
+{
+    if (__popcll(mm) < 12) {
+        while (mm) {
+            acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), (int)__builtin_ctzll(mm)));
+            mm &= mm - 1;
+        }
+        return acc;
+    }
+#pragma unroll
+    for (int l = 0; l < 64; l++) {
+        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), l));
+        acc = acc + (((mm >> l) & 1ull) ? x : -0.0f);
+    }
+    return acc;
+}
 /* (the builtins return int: widen through uint32_t, or a low half >= 2^31
  * sign-extends into the high half) */
 __device__ __forceinline__ uint64_t uni64(uint64_t v)

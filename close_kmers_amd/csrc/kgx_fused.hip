@@ -476,10 +476,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     o_last = rl32(pos, (uint32_t)hibit(mm));
                     o_last_idx = h0 + (uint32_t)hibit(mm);
                 }
-                while (mm) {
-                    o_wsum = o_wsum + rlf(wt, lowbit(mm));
-                    mm &= mm - 1;
-                }
+                o_wsum = sum_lanes_in_order(o_wsum, wt, mm);
             }
             if (fs < n && o_valid)
                 close_open();
@@ -501,12 +498,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 const uint32_t b = lowbit(SUM);
                 SUM &= SUM - 1;
                 const uint64_t ab = S & ~lanes_le(b);
-                uint64_t mm = MEMB & bit_range(b, ab ? lowbit(ab) : n);
-                float acc = 0.0f;
-                while (mm) {
-                    acc = acc + rlf(wt, lowbit(mm));
-                    mm &= mm - 1;
-                }
+                const uint64_t mm = MEMB & bit_range(b, ab ? lowbit(ab) : n);
+                const float acc = sum_lanes_in_order(0.0f, wt, mm);
                 if (lane == b)
                     ws = acc;
             }
