@@ -117,7 +117,7 @@ WANT_OUTPUTS = {3: "hits + calls (lookup_request without find_best_match)",
                 15: "hits + calls + OTU + device find_best_call"}
 
 
-def canary_check(abi, synth, d, dev):
+def canary_check(abi, synth, d, dev, line_index=0):
     """Every rank: the canary pass (close_kmers_amd/canary.py) on its own
     device, digested; the digests are gathered and compared with the CPU
     oracle's committed digest.  Returns (per-rank canary records, ok).  With
@@ -125,7 +125,7 @@ def canary_check(abi, synth, d, dev):
     must differ (one rank per GPU)."""
     from close_kmers_amd import canary
     t0 = time.time()
-    mine = canary.run_on_device(abi, synth, dev)
+    mine = canary.run_on_device(abi, synth, dev, line_index)
     mine["rank"] = d.rank
     mine["seconds"] = round(time.time() - t0, 2)
     want = canary.expected()["digest"]
@@ -463,7 +463,8 @@ def main():
     d = shard.Dist()
     canary_recs = None
     if not args.no_canary:
-        canary_recs, canary_ok = canary_check(abi, synth, d, dev)
+        canary_recs, canary_ok = canary_check(abi, synth, d, dev,
+                                              args.line_index if args.image_layout == "packed" else 0)
         if not canary_ok:
             d.close()
             raise SystemExit(f"rank {d.rank}: canary check failed (a device's results differ from the oracle's)")

@@ -102,17 +102,24 @@ def expected() -> dict:
         return json.load(f)
 
 
-def run_on_device(abi, synth, device: int) -> dict:
+def run_on_device(abi, synth, device: int, line_index: int = 0) -> dict:
     """The canary pass on `device` through the C ABI: {"digest", "hits",
-    "calls", "device"}."""
+    "calls", "device", "line_index"}.  `line_index` > 0 builds the image's
+    line index at that load first (as bench.py does for its timed image), so
+    the canary probes through the same path the timed steps use."""
     spec = synth.ImageSpec(CANARY_KEYS)
     img, _ = abi.Image.synthetic(spec.n_keys, spec.num_sigs, device=device)
     try:
+        if line_index and img.layout == abi.Image.PACKED16:
+            img.set_line_index(line_index)
+        else:
+            line_index = 0
         res, off = synth.make_queries(spec, CANARY_SEQ, length=CANARY_LEN, x_permille=CANARY_X_PERMILLE,
                                       q0=CANARY_Q0)
         with abi.Context(img) as ctx:
             r = ctx.process_batch(res, off, abi.default_params(), want=CANARY_WANT)
             dg = digest(r.hit_offsets, r.hits, r.call_offsets, r.calls, best_from_device(r.best))
-            return {"device": device, "digest": dg, "hits": int(r.hit_offsets[-1]), "calls": int(r.call_offsets[-1])}
+            return {"device": device, "digest": dg, "hits": int(r.hit_offsets[-1]), "calls": int(r.call_offsets[-1]),
+                    "line_index": int(line_index)}
     finally:
         img.close()

@@ -59,8 +59,9 @@ def test_digest_plumbing():
 
 
 @pytest.mark.gpu
-def test_canary_on_device(gpu):
+@pytest.mark.parametrize("line_index", [0, 36])
+def test_canary_on_device(gpu, line_index):
     from close_kmers_amd import synth
-    got = canary.run_on_device(gpu, synth, 0)
+    got = canary.run_on_device(gpu, synth, 0, line_index)
     want = canary.expected()
     assert got["digest"] == want["digest"], got
