@@ -153,107 +153,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
 
     uint32_t nh = 0;
     const uint32_t J = (W + 255) / 256; /* 256-window slices */
-    if constexpr (QUAD) {
-        /* 2'. encode + probe by quads: the 4 lanes of quad g = t / 4 own
-         * windows g + 64 i; each round they read the aligned 64-B line that
-         * holds a pending window's next bucket in ONE instruction (16 B a
-         * lane), and the quad's ballots settle the window: the first bucket
-         * from the slot on that is the key or a stop (kguts.cc:585-602)
-         * decides it.  A line costs one request instead of one per bucket
-         * read, and a wave instruction carries 16 windows instead of 64
-         * scattered records.  The matching lane puts the record into LDS at
-         * the window (wrec / whit alias hrec / oflag, free until the
-         * compaction, which reads a slice before it writes it). */
-        constexpr uint32_t QJ = 4 * FJ;
-        const uint32_t sub = t & 3u, quad = t >> 2, qs = 4u * (lane >> 2);
-        uint4 *wrec = hrec;
-        uint8_t *whit = oflag;
-        for (uint32_t i = t; i < W; i += 256)
-            whit[i] = 0;
-        uint64_t key[QJ], slot[QJ], examined[QJ];
-        bool pend[QJ];
-#pragma unroll
-        for (uint32_t j = 0; j < QJ; j++) {
-            const uint32_t w = quad + 64 * j;
-            pend[j] = false;
-            key[j] = 0;
-            slot[j] = 0;
-            examined[j] = 0;
-            if (w < W) {
-                const uint8_t *c = codes + w;
-                const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
-                const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
-                const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
-                key[j] = (uint64_t)ka * 160000u + kb;
-                pend[j] = cmax < 20u;
-                slot[j] = pend[j] ? mod_by(key[j], a.num_sigs >> a.hs, a.magic) << a.hs : 0;
-            }
-        }
-        __syncthreads(); /* whit cleared */
-        const uint64_t NS = a.num_sigs;
-        for (;;) {
-            uint4 pv[QJ];
-#pragma unroll
-            for (uint32_t j = 0; j < QJ; j++) {
-                const uint64_t base = slot[j] & ~3ull;
-                if (pend[j] && base + sub < NS)
-                    pv[j] = a.table[base + sub];
-            }
-            bool more = false;
-#pragma unroll
-            for (uint32_t j = 0; j < QJ; j++) {
-                const uint64_t base = slot[j] & ~3ull;
-                const bool in = pend[j] && sub >= (uint32_t)(slot[j] & 3) && base + sub < NS;
-                const uint32_t iq = (uint32_t)(__ballot(in) >> qs) & 0xFu;
-                /* this bucket's place in the probe: examined so far + the
-                 * quad's in-range buckets before it + itself */
-                const uint64_t nth = examined[j] + (uint32_t)__popc(iq & ((1u << sub) - 1u)) + 1u;
-                const uint64_t kv = ((uint64_t)pv[j].y << 32 | pv[j].x) & PACK_KEY_MASK;
-                const bool m = in && kv == key[j];
-                /* past num_sigs buckets the reference would spin forever: a miss here */
-                const bool stop = in && (m || kv > MAX_ENCODED || nth >= NS);
-                const uint32_t sq = (uint32_t)(__ballot(stop) >> qs) & 0xFu;
-                const uint32_t mq = (uint32_t)(__ballot(m) >> qs) & 0xFu;
-                const uint32_t first = sq ? (uint32_t)__builtin_ctz(sq) : 4u;
-                const uint32_t w = quad + 64 * j;
-                if (sq && ((mq >> first) & 1u) && sub == first) {
-                    wrec[w] = pv[j];
-                    whit[w] = 1;
-                }
-                examined[j] += (uint32_t)__popc(iq);
-                const bool live = pend[j] && !sq;
-                slot[j] = live ? (base + 4 >= NS ? 0 : base + 4) : slot[j];
-                pend[j] = live;
-                more = more || live;
-            }
-            if (!__syncthreads_or(more))
-                break;
-        }
-        if (dbg)
-            a.dbg[2] = wall_clock64();
-        /* 3'. ordered compaction into LDS (the records from wrec by window) */
-        for (uint32_t j = 0; j < J; j++) {
-            const uint32_t w = t + 256 * j;
-            const bool h = w < W && whit[w];
-            const uint4 r = h ? wrec[w] : make_uint4(0, 0, 0, 0);
-            const uint64_t m = __ballot(h);
-            if (lane == 0)
-                wave_cnt[wave] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t before = 0, total = 0;
-            for (uint32_t v = 0; v < 4; v++) {
-                before += v < wave ? wave_cnt[v] : 0u;
-                total += wave_cnt[v];
-            }
-            if (h) {
-                const uint32_t at = nh + before + lanes_below(m);
-                hrec[at] = r;
-                hpos[at] = w;
-            }
-            nh += total;
-            __syncthreads();
-        }
-    } else {
+    {
         /* 2. encode + probe: thread t owns windows t + 256 j, probed RB
          * slices at a time (the LDS holds FJ slices; the registers hold RB,
          * so a long protein costs more probe rounds, not spilled registers:
@@ -293,52 +193,149 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
              * slower: 6.8 vs 4.6 us for one protein).  Bounded by num_sigs
              * buckets where the reference would spin forever. */
             constexpr uint32_t R = 4; /* records per round: one line */
-            uint64_t examined[RB];
-#pragma unroll
-            for (uint32_t j = 0; j < RB; j++)
-                examined[j] = 0;
             const uint64_t NS = a.num_sigs;
-            for (;;) {
-                uint4 pv[RB][R];
+            uint32_t rounds = 0;
+            if (dbg && jb == 0)
+                a.dbg[12] = wall_clock64(); /* keys and homes computed */
+            if constexpr (QUAD) {
+                /* the loads by quads (the call service): the windows' keys and
+                 * next buckets go through LDS and the 4 lanes of quad g read
+                 * window g + 64 i's line, 16 B each, one instruction for 16
+                 * windows.  A round's lines then cost one address translation
+                 * each where a thread's four 16-B loads of its own line cost
+                 * four, and over a table of many GB those translations bound
+                 * the round (tools/tlb_probe.cpp, 293 lines over 114 GB: 2.3
+                 * vs 3.2 us) */
+                __shared__ uint4 qst[256 * RB]; /* key lo, key hi | pend << 31, next bucket lo, hi */
+                __shared__ uint4 qrec[256 * RB];
+                __shared__ uint8_t qhit[256 * RB];
 #pragma unroll
                 for (uint32_t j = 0; j < RB; j++) {
-                    const uint64_t base = slot[j] & ~3ull;
-#pragma unroll
-                    for (uint32_t q = 0; q < R; q++)
-                        if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
-                            pv[j][q] = a.table[base + q];
+                    const uint32_t wi = t + 256 * j;
+                    qst[wi] = make_uint4((uint32_t)key[j], (uint32_t)(key[j] >> 32) | (pend[j] ? 0x80000000u : 0u),
+                                         (uint32_t)slot[j], (uint32_t)(slot[j] >> 32));
+                    qhit[wi] = 0;
                 }
-                bool more = false;
+                __syncthreads();
+                const uint32_t CW = min(256u * RB, W - 256u * jb); /* this pass's windows */
+                const uint32_t g = t >> 2, sub = t & 3u, qsh = 4u * (lane >> 2);
+                /* every bucket examined once a window has gone round the
+                 * table (its first line may be partial): a miss where the
+                 * reference would spin forever */
+                const uint64_t turn = (NS + 3) / 4 + 1;
+                for (;;) {
+                    uint4 st[4 * RB], pv[4 * RB];
 #pragma unroll
-                for (uint32_t j = 0; j < RB; j++) {
-                    const uint64_t base = slot[j] & ~3ull;
-                    bool live = pend[j]; /* still searching within this line */
-#pragma unroll
-                    for (uint32_t q = 0; q < R; q++) {
-                        const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
-                        const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
-                        const bool m = in && kv == key[j];
-                        const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
-                        rec[j].x = m ? pv[j][q].x : rec[j].x;
-                        rec[j].y = m ? pv[j][q].y : rec[j].y;
-                        rec[j].z = m ? pv[j][q].z : rec[j].z;
-                        rec[j].w = m ? pv[j][q].w : rec[j].w;
-                        hit[j] = hit[j] || m;
-                        examined[j] += in ? 1u : 0u;
-                        live = live && !stop;
+                    for (uint32_t i = 0; i < 4 * RB; i++) {
+                        const uint32_t wi = g + 64 * i;
+                        st[i] = wi < CW ? qst[wi] : make_uint4(0, 0, 0, 0);
+                        const uint64_t sl = (uint64_t)st[i].w << 32 | st[i].z, base = sl & ~3ull;
+                        if ((st[i].y >> 31) && sub >= (uint32_t)(sl & 3) && base + sub < NS)
+                            pv[i] = a.table[base + sub];
                     }
-                    /* not resolved in this line: on at the next one (wrapping
-                     * at the table's end, where the round's loads stopped) */
-                    const uint64_t next = base + R >= NS ? 0 : base + R;
-                    pend[j] = live;
-                    slot[j] = live ? next : slot[j];
-                    more = more || live;
+                    rounds++;
+                    if (dbg && rounds == 1 && jb == 0) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        a.dbg[13] = wall_clock64(); /* thread 0's own loads back */
+                    }
+                    const bool turned = rounds >= turn;
+                    bool more = false;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4 * RB; i++) {
+                        const uint32_t wi = g + 64 * i;
+                        const bool pd = (st[i].y >> 31) != 0;
+                        const uint64_t sl = (uint64_t)st[i].w << 32 | st[i].z, base = sl & ~3ull;
+                        const bool in = pd && sub >= (uint32_t)(sl & 3) && base + sub < NS;
+                        const uint64_t kq = (uint64_t)(st[i].y & 0x7FFFFFFFu) << 32 | st[i].x;
+                        const uint64_t kv = ((uint64_t)pv[i].y << 32 | pv[i].x) & PACK_KEY_MASK;
+                        const bool m = in && kv == kq;
+                        const bool stop = in && (m || kv > MAX_ENCODED);
+                        /* the quad's first bucket in probe order that is the
+                         * key or a stop decides the window */
+                        const uint32_t sq = (uint32_t)(__ballot(stop) >> qsh) & 0xFu;
+                        const uint32_t mq = (uint32_t)(__ballot(m) >> qsh) & 0xFu;
+                        const uint32_t first = sq ? (uint32_t)__builtin_ctz(sq) : 4u;
+                        if (sq && ((mq >> first) & 1u) && sub == first) {
+                            qrec[wi] = pv[i];
+                            qhit[wi] = 1;
+                        }
+                        const bool live = pd && !sq && !turned;
+                        if (pd && sub == 0) {
+                            const uint64_t next = base + R >= NS ? 0 : base + R;
+                            qst[wi] = live ? make_uint4(st[i].x, st[i].y, (uint32_t)next, (uint32_t)(next >> 32))
+                                           : make_uint4(st[i].x, st[i].y & 0x7FFFFFFFu, st[i].z, st[i].w);
+                        }
+                        more = more || live;
+                    }
+                    const bool again = __syncthreads_or(more);
+                    if (dbg && rounds == 1 && jb == 0)
+                        a.dbg[11] = wall_clock64(); /* the first round examined */
+                    if (!again)
+                        break;
                 }
-                if (!__syncthreads_or(more))
-                    break;
+#pragma unroll
+                for (uint32_t j = 0; j < RB; j++) {
+                    const uint32_t wi = t + 256 * j;
+                    hit[j] = qhit[wi] != 0;
+                    rec[j] = hit[j] ? qrec[wi] : make_uint4(0, 0, 0, 0);
+                }
+            } else {
+                uint64_t examined[RB];
+#pragma unroll
+                for (uint32_t j = 0; j < RB; j++)
+                    examined[j] = 0;
+                for (;;) {
+                    uint4 pv[RB][R];
+    #pragma unroll
+                    for (uint32_t j = 0; j < RB; j++) {
+                        const uint64_t base = slot[j] & ~3ull;
+    #pragma unroll
+                        for (uint32_t q = 0; q < R; q++)
+                            if (pend[j] && q >= (uint32_t)(slot[j] & 3) && base + q < NS)
+                                pv[j][q] = a.table[base + q];
+                    }
+                    bool more = false;
+    #pragma unroll
+                    for (uint32_t j = 0; j < RB; j++) {
+                        const uint64_t base = slot[j] & ~3ull;
+                        bool live = pend[j]; /* still searching within this line */
+    #pragma unroll
+                        for (uint32_t q = 0; q < R; q++) {
+                            const bool in = live && q >= (uint32_t)(slot[j] & 3) && base + q < NS;
+                            const uint64_t kv = ((uint64_t)pv[j][q].y << 32 | pv[j][q].x) & PACK_KEY_MASK;
+                            const bool m = in && kv == key[j];
+                            const bool stop = in && (m || kv > MAX_ENCODED || examined[j] + 1 >= NS);
+                            rec[j].x = m ? pv[j][q].x : rec[j].x;
+                            rec[j].y = m ? pv[j][q].y : rec[j].y;
+                            rec[j].z = m ? pv[j][q].z : rec[j].z;
+                            rec[j].w = m ? pv[j][q].w : rec[j].w;
+                            hit[j] = hit[j] || m;
+                            examined[j] += in ? 1u : 0u;
+                            live = live && !stop;
+                        }
+                        /* not resolved in this line: on at the next one (wrapping
+                         * at the table's end, where the round's loads stopped) */
+                        const uint64_t next = base + R >= NS ? 0 : base + R;
+                        pend[j] = live;
+                        slot[j] = live ? next : slot[j];
+                        more = more || live;
+                    }
+                    if (dbg && rounds == 0 && jb == 0) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        a.dbg[13] = wall_clock64(); /* thread 0's own loads back */
+                    }
+                    const bool again = __syncthreads_or(more);
+                    if (dbg && rounds++ == 0 && jb == 0)
+                        a.dbg[11] = wall_clock64(); /* the first round examined */
+                    if (!again)
+                        break;
+                }
             }
-            if (dbg && jb + RB >= J)
-                a.dbg[2] = wall_clock64();
+            if (dbg) {
+                a.dbg[10] = (jb == 0 ? 0 : a.dbg[10]) + rounds;
+                if (jb + RB >= J)
+                    a.dbg[2] = wall_clock64();
+            }
 
             /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
 #pragma unroll
@@ -457,6 +454,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             const uint64_t S = (__ballot(act && brk) | (SW >> 1)) & ACT; /* sub-run starts */
             const bool memb = act && (fi == cur || ((S >> k) & 1));
             const uint64_t MEMB = __ballot(memb);
+            if (dbg && h0 == 0)
+                a.dbg[14] = wall_clock64(); /* the first chunk's runs and members */
             if (SW & 1) { /* the open run flushes; the pair (last hit, lane 0) carries */
                 close_open();
                 o_cur = rl32(fi, 0);
@@ -503,6 +502,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                 if (lane == b)
                     ws = acc;
             }
+            if (dbg && h0 == 0)
+                a.dbg[15] = wall_clock64(); /* the first chunk's sums */
             const uint64_t EMIT = __ballot(is_start && closed && (int)c_seg >= prm.min_hits && ws >= min_wh);
             const uint32_t idx = o_ncalls + (uint32_t)__popcll(EMIT & bit_range(0, k));
             if (want_otu && act && ((MEMB >> k) & 1)) { /* a counted member of a sub-run emitted here */
@@ -831,39 +832,72 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * slot's next request until the instance ended (0.5% of calls waited up to
  * the instance's lifetime: +40% mean latency at 16 callers).
  */
+/* a 16-B load at system scope (past every cache: the host writes this memory) */
+__device__ __forceinline__ uint4 load_system16(const uint4 *p)
+{
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <bool QUAD>
 __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbgs,
                                                   const uint8_t *res_base, kgx_hit *hits, kgx_call *calls,
                                                   kgx_otu *otus,
                                                   const uint4 *table, uint64_t num_sigs, uint64_t magic,
-                                                  uint32_t hs, uint64_t life_ticks)
+                                                  uint32_t hs, uint64_t life_ticks, uint32_t poll_chunks)
 {
     __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
+    __shared__ uint32_t rbuf[SVC_RES_CHUNKS * 3]; /* the request's residues, 12 per chunk */
     const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
     const uint64_t t0 = wall_clock64();
     uint32_t last = 0;
     if (t == 0)
         last = __hip_atomic_load(&out[slot].done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     last = __shfl(last, 0);
-    const uint32_t *line = reinterpret_cast<const uint32_t *>(&hdr[slot]);
+    const uint4 *hline = reinterpret_cast<const uint4 *>(&hdr[slot]);
+    const uint4 *chunks = reinterpret_cast<const uint4 *>(res_base + (uint64_t)slot * SVC_RES_STRIDE);
     for (;;) {
         if (t < 64) {
-            /* wave 0 polls: lanes 0-15 read the header line's 16 dwords at
-             * once (one PCIe round trip for the request number and its
-             * fields); a line whose copy word lags its request number was
-             * read mid-write and is read again */
+            /* wave 0 polls with one 16-B load a lane: lanes 0-3 the header
+             * line (its request number and fields), lanes 4-63 the first
+             * SVC_POLL_CHUNKS residue chunks (12 residues and the request
+             * number they belong to) -- so a protein of up to 720 aa comes in
+             * with its header and costs no second round trip.  A header whose
+             * copy word lags its request number was read mid-write and is
+             * read again; a chunk read with its header may predate it (its
+             * tag says so) and is read again, now behind the header. */
             uint32_t go = 0;
+            const uint4 *src = lane < 4 ? hline + lane : chunks + (lane - 4);
+            const bool polls = lane < 4 + poll_chunks;
             for (;;) {
-                const uint32_t v = lane < 16 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_SYSTEM)
-                                             : 0u;
-                const uint32_t req = rl32(v, 0), stop = rl32(v, 1), copy = rl32(v, 15);
+                uint4 v = polls ? load_system16(src) : make_uint4(0, 0, 0, 0);
+                const uint32_t req = rl32(v.x, 0), stop = rl32(v.y, 0), copy = rl32(v.w, 3);
                 if (stop)
                     break;
                 if (req != last && copy == req) {
                     go = 1;
-                    if (lane < 16)
-                        cmd[lane] = v;
+                    const uint32_t n_chunks = (min(rl32(v.z, 0), SVC_MAX_RES) + 11) / 12;
+                    const uint32_t c = lane - 4;
+                    bool stale = lane >= 4 && polls && c < n_chunks && v.w != req;
+                    const uint64_t t1 = wall_clock64();
+                    while (__ballot(stale) && wall_clock64() - t1 < 100000000ull) { /* (1 s: a bound, not a wait) */
+                        if (stale) {
+                            v = load_system16(src);
+                            stale = v.w != req;
+                        }
+                    }
+                    if (lane < 4) {
+                        cmd[4 * lane] = v.x;
+                        cmd[4 * lane + 1] = v.y;
+                        cmd[4 * lane + 2] = v.z;
+                        cmd[4 * lane + 3] = v.w;
+                    } else if (polls && c < n_chunks) {
+                        rbuf[3 * c] = v.x;
+                        rbuf[3 * c + 1] = v.y;
+                        rbuf[3 * c + 2] = v.z;
+                    }
                     break;
                 }
                 if (wall_clock64() - t0 > life_ticks)
@@ -898,20 +932,21 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         a.done = &out[slot].done;
         a.token = req;
         a.dbg = h->debug ? dbgs[slot].stamp : nullptr;
-        const FusedSlot in{res_base + (uint64_t)slot * SVC_RES_STRIDE, len};
-        __syncthreads(); /* every thread has its copy of the request before cmd can change */
+        /* the chunks past the polled ones (proteins over 720 aa), read now
+         * that the header is seen */
+        for (uint32_t c = poll_chunks + t; c < (len + 11) / 12; c += 256) {
+            const uint4 v = load_system16(chunks + c);
+            rbuf[3 * c] = v.x;
+            rbuf[3 * c + 1] = v.y;
+            rbuf[3 * c + 2] = v.z;
+        }
+        const FusedSlot in{reinterpret_cast<const uint8_t *>(rbuf), len};
+        __syncthreads(); /* every thread has its copy of the request and the residues before cmd can change */
         /* one body for every length (its registers probe two 256-window
          * slices at a time, its LDS holds all of them): a second, inlined
          * body for short proteins made the kernel spill ~190 SGPRs into VGPR
          * lanes, reloaded in the short path's loops too */
-        if constexpr (QUAD) {
-            if (len <= 2 * 256 + 8)
-                fused_small_body<2, FusedSlot, true>(a, in, 0); /* quads: up to 512 windows (8 per quad) */
-            else
-                fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
-        } else {
-            fused_small_body<FUSED_MAX_WINDOWS / 256>(a, in, 0);
-        }
+        fused_small_body<FUSED_MAX_WINDOWS / 256, FusedSlot, QUAD>(a, in, 0);
         last = req;
     }
     /* counted out: the host's exit hook waits for every launched instance's
@@ -922,18 +957,19 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
 
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t hs)
+                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t hs, uint32_t poll_chunks)
 {
+    poll_chunks = std::min(poll_chunks, SVC_POLL_CHUNKS);
     if (slots == 0 || slots > SVC_MAX_SLOTS || num_sigs == 0 || !packed_table)
         return hipErrorInvalidValue;
     if (quad_probe)
         hipLaunchKernelGGL(svc_kernel<true>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls, otus,
                            static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs >> hs), hs,
-                           life_ticks);
+                           life_ticks, poll_chunks);
     else
         hipLaunchKernelGGL(svc_kernel<false>, dim3(slots), dim3(256), 0, stream, hdr, out, dbg, res, hits, calls,
                            otus, static_cast<const uint4 *>(packed_table), num_sigs, mod_magic(num_sigs >> hs), hs,
-                           life_ticks);
+                           life_ticks, poll_chunks);
     return hipGetLastError();
 }
 

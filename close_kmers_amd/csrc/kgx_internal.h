@@ -250,7 +250,14 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * memory and runs fused_small_body on the slot's sequence; no launch per call.
  * A slot takes one sequence of at most SVC_MAX_RES residues. */
 constexpr uint32_t SVC_MAX_RES = FUSED_MAX_WINDOWS + 8;
-constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residues per slot */
+constexpr uint32_t SVC_RES_STRIDE = 4096;  /* bytes of residue chunks per slot */
+/* a slot's residues travel in 16-B chunks: 12 residues, then the request
+ * number they belong to (one 16-B store on the host, one 16-B load on the
+ * device: a chunk is read whole or not at all); the service's polling wave
+ * reads the first SVC_POLL_CHUNKS with the header line */
+constexpr uint32_t SVC_RES_CHUNKS = (SVC_MAX_RES + 11) / 12;
+constexpr uint32_t SVC_POLL_CHUNKS = 60;
+static_assert(SVC_RES_CHUNKS * 16 <= SVC_RES_STRIDE, "residue chunks per slot");
 constexpr uint32_t SVC_MAX_SLOTS = 64;
 struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the polling wave */
     uint32_t req;   /* request number: the device serves it when it differs from SvcSlotOut.done */
@@ -265,7 +272,10 @@ struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the p
 struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
     uint64_t stamp[16]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
                            0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order, 9 the
-                           scorer's first chunk done */
+                           scorer's first chunk done, 10 probe rounds (a count), 11 the
+                           probe's first round examined, 12 keys and homes computed, 13
+                           thread 0's first-round loads back, 14 / 15 the scorer's first
+                           chunk's runs and members / sums */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */
@@ -279,7 +289,8 @@ static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(Svc
  * wall clock, 100 MHz) or on stop */
 hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, const uint8_t *res, kgx_hit *hits,
                       kgx_call *calls, kgx_otu *otus, uint32_t slots, const void *packed_table, uint64_t num_sigs,
-                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t home_shift = 0);
+                      uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t home_shift = 0,
+                      uint32_t poll_chunks = SVC_POLL_CHUNKS);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,

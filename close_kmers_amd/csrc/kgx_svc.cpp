@@ -8,8 +8,11 @@
  * runtime and those launches serialise across the pool's threads, so the pool
  * topped out at 170K calls/s whatever T (r3g).  Here workgroups of svc_kernel
  * (kgx_fused.hip) stay resident, one per slot; a caller takes a free slot,
- * writes its residues, length, want mask and parameters into the slot's
- * mapped host memory, stores the slot's request number, and spins until the
+ * writes its residues (16-B chunks of 12 residues tagged with the request
+ * number, so the polling wave can take the first ones with the header line),
+ * length, want mask and parameters into the slot (device memory through a
+ * large BAR, else mapped host memory), stores the slot's request number, and
+ * spins until the
  * device stores the same number into the slot's done word, behind the hit
  * and call records (fused_small_body: probe, ordered compaction, wave
  * scorer).  No runtime call is on a call's path.
@@ -29,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -38,6 +42,9 @@
 #include <string>
 #include <thread>
 
+#if defined(__x86_64__)
+#include <emmintrin.h>
+#endif
 #include <sys/prctl.h>
 #include <time.h>
 
@@ -93,7 +100,7 @@ struct SvcState {
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
      * + scorer, and [5] 3->6 the record stores alone) */
     bool debug = false;
-    std::atomic<uint64_t> phase_ns[8] = {};
+    std::atomic<uint64_t> phase_ns[14] = {};
     /* KGX_SVC_SLEEP_US: a caller sleeps this long before it spins for its
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
@@ -101,11 +108,18 @@ struct SvcState {
     std::atomic<bool> broken{false}; /* a launch failed or a call timed out: callers take other paths */
     std::atomic<uint64_t> n_abandoned{0}; /* slots given up after a 10-s wait (never handed out again) */
     int priority = 0; /* the stream's priority (hipDeviceGetStreamPriorityRange: lower = higher) */
-    /* KGX_SVC_PROBE=quad: proteins up to 520 aa probed by 4-lane quads per
-     * 64-B line instead of a thread per window -- measured slower in the
-     * resident kernel (r4b: probe phase 7.3 vs 5.0 us per call), kept as an
-     * option */
-    int quad_probe = 0;
+    /* the probe's loads by 4-lane quads, one 64-B line per window in one
+     * instruction for 16 windows (the default), or KGX_SVC_PROBE=thread: a
+     * thread's four 16-B loads of its own window's line -- four address
+     * translations per line instead of one: probe phase 4.1 vs 3.8 us per
+     * 300-aa call over the 114-GB line index (r7c) */
+    int quad_probe = 1;
+    /* residue chunks the polling wave reads with the header
+     * (KGX_SVC_POLL_CHUNKS, at most SVC_POLL_CHUNKS): 28 = 336 residues.
+     * Read with the header they save the residues' own round trip after it
+     * (host wall per 300-aa call 11.25 vs 11.9 us, r7f); more chunks per
+     * poll measured no better (60: 11.3-11.6) */
+    uint32_t poll_chunks = 28;
 };
 
 namespace {
@@ -121,6 +135,33 @@ int64_t now_ns()
 }
 
 constexpr size_t align64(size_t x) { return (x + 63) & ~size_t(63); }
+
+/* a request's residues as the device reads them (kgx_internal.h,
+ * SVC_RES_CHUNKS): chunk c = residues [12 c, 12 c + 12) and the request
+ * number, one 16-B store each (written, never read, by the host); the bytes
+ * from cut to len read 'X' */
+inline void put_chunks(uint8_t *dst, const char *seq, uint64_t cut, uint64_t len, uint32_t q)
+{
+    const uint64_t n = (len + 11) / 12;
+    for (uint64_t c = 0; c < n; c++) {
+        alignas(16) uint8_t b[16];
+        const uint64_t i0 = 12 * c;
+        if (i0 + 12 <= cut) {
+            std::memcpy(b, seq + i0, 12);
+        } else {
+            for (uint64_t j = 0; j < 12; j++) {
+                const uint64_t i = i0 + j;
+                b[j] = i < cut ? (uint8_t)seq[i] : i < len ? (uint8_t)'X' : (uint8_t)0;
+            }
+        }
+        std::memcpy(b + 12, &q, 4);
+#if defined(__x86_64__)
+        _mm_store_si128(reinterpret_cast<__m128i *>(dst + 16 * c), _mm_load_si128(reinterpret_cast<const __m128i *>(b)));
+#else
+        std::memcpy(dst + 16 * c, b, 16);
+#endif
+    }
+}
 
 /* orders the host's stores to the request lines before what follows and, for
  * device memory written through the write-combining BAR, pushes them out */
@@ -184,7 +225,8 @@ int top_up(SvcState *s)
         /* wall clock at 100 MHz: 100 ticks per us */
         hipError_t e = launch_svc(s->d_hdr, s->d_out, s->d_dbg, s->d_res, s->d_hits, s->d_calls, s->d_otus, s->slots,
                                   s->table,
-                                  s->num_sigs, s->life_us * 100, s->quad_probe, s->stream, s->home_shift);
+                                  s->num_sigs, s->life_us * 100, s->quad_probe, s->stream, s->home_shift,
+                                  s->poll_chunks);
         if (e == hipSuccess)
             e = hipEventRecord(ev, s->stream);
         if (e != hipSuccess) {
@@ -307,11 +349,16 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
         destroy(s);
         return fail(KGX_EDEVICE, std::string("call service: ") + hipGetErrorString(e));
     }
-    std::memset(h, 0, b_hdr + b_out + b_dbg);
+    /* the residue chunks too: a chunk's tag must never match a request of
+     * this service before the host wrote it, and a new service's request
+     * numbers start again at 1 (on memory an earlier service may have used) */
+    std::memset(h, 0, b_hdr + b_out + b_dbg + b_res);
     const char *dbg_env = std::getenv("KGX_SVC_DEBUG");
     s->debug = dbg_env && std::atoi(dbg_env) != 0;
     if (const char *pr = std::getenv("KGX_SVC_PROBE"))
         s->quad_probe = std::string(pr) != "thread";
+    if (const char *pc = std::getenv("KGX_SVC_POLL_CHUNKS"))
+        s->poll_chunks = (uint32_t)std::min<long>(SVC_POLL_CHUNKS, std::max(0L, std::atol(pc)));
     if (const char *sl = std::getenv("KGX_SVC_SLEEP_US"))
         s->sleep_us = (uint32_t)std::max(0, std::atoi(sl));
     char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);
@@ -332,7 +379,8 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
         /* on the service's stream: a device-wide synchronisation would wait
          * for every batch in flight on the device */
         if (hipExtMallocWithFlags(&r, b_hdr + b_res, hipDeviceMallocFinegrained) == hipSuccess &&
-            hipMemsetAsync(r, 0, b_hdr, s->stream) == hipSuccess && hipStreamSynchronize(s->stream) == hipSuccess) {
+            hipMemsetAsync(r, 0, b_hdr + b_res, s->stream) == hipSuccess &&
+            hipStreamSynchronize(s->stream) == hipSuccess) {
             s->reqmem = static_cast<char *>(r); /* one address for the host and the device */
             s->hdr = s->d_hdr = reinterpret_cast<SvcSlotHdr *>(s->reqmem);
             s->res = s->d_res = reinterpret_cast<uint8_t *>(s->reqmem + b_hdr);
@@ -505,8 +553,10 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s ? (uint64_t)(s->priority + 100) : 0;
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
-    else if (n.size() == 8 && n.compare(0, 7, "phase_n") == 0 && n[7] >= '0' && n[7] <= '7') /* "phase_n0".."phase_n7" */
-        *value = s ? s->phase_ns[n[7] - '0'].load() : 0;
+    else if ((n.size() == 8 || n.size() == 9) && n.compare(0, 7, "phase_n") == 0 &&
+             std::isdigit((unsigned char)n[7]) && (n.size() == 8 || std::isdigit((unsigned char)n[8])) &&
+             std::stoul(n.substr(7)) < 14) /* "phase_n0".."phase_n13" */
+        *value = s ? s->phase_ns[std::stoul(n.substr(7))].load() : 0;
     else
         return fail(KGX_EINVAL, "unknown service statistic " + n);
     return KGX_OK;
@@ -547,24 +597,21 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         return fail(KGX_EBUSY, "call service: every slot is in use");
     }
     /* the request: residues (cut at the first NUL as the batch paths do,
-     * kguts.cc:792), then the header, then the request number */
-    uint8_t *r = s->res + (size_t)slot * SVC_RES_STRIDE; /* written, never read, by the host */
+     * kguts.cc:792) in 16-B chunks tagged with the request number, then the
+     * header, then the request number */
+    uint32_t q = s->slot[slot].seq + 1;
+    if (q == 0 || q == __atomic_load_n(&s->out[slot].done, __ATOMIC_RELAXED))
+        q++;
+    s->slot[slot].seq = q;
     const void *z = len ? std::memchr(seq, 0, len) : nullptr;
     const uint64_t keep = z ? (uint64_t)(static_cast<const char *>(z) - seq) : len;
     const uint64_t cut = z && keep ? keep - 1 : keep;
-    if (cut)
-        std::memcpy(r, seq, cut);
-    if (cut < len)
-        std::memset(r + cut, 'X', len - cut);
+    put_chunks(s->res + (size_t)slot * SVC_RES_STRIDE, seq, cut, len, q);
     SvcSlotHdr &h = s->hdr[slot];
     h.len = (uint32_t)len;
     h.want = want;
     h.prm = p;
     h.debug = s->debug ? 1u : 0u;
-    uint32_t q = s->slot[slot].seq + 1;
-    if (q == 0 || q == __atomic_load_n(&s->out[slot].done, __ATOMIC_RELAXED))
-        q++;
-    s->slot[slot].seq = q;
     /* device memory is written through a write-combining BAR mapping: the
      * fences order the request's bytes before its number and push it out */
     if (s->reqmem)
@@ -634,6 +681,17 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         } else if (st[9] >= st[6] && st[9] <= st[4]) {
             s->phase_ns[6] += (st[9] - st[6]) * 10; /* the scorer's first 64-hit chunk */
             s->phase_ns[7] += (st[4] - st[9]) * 10; /* its other chunks and the final flush */
+        }
+        s->phase_ns[8] += st[10] * 1000; /* probe rounds (x1000: read back per call like the times) */
+        if (st[11] >= st[1] && st[11] <= st[2])
+            s->phase_ns[9] += (st[11] - st[1]) * 10; /* the probe's first round */
+        if (st[12] >= st[1] && st[13] >= st[12] && st[13] <= st[11]) {
+            s->phase_ns[10] += (st[12] - st[1]) * 10; /* keys and homes */
+            s->phase_ns[11] += (st[13] - st[12]) * 10; /* thread 0's first-round loads */
+        }
+        if (!(want & KGX_WANT_OTU) && st[14] >= st[6] && st[15] >= st[14] && st[9] >= st[15]) {
+            s->phase_ns[12] += (st[14] - st[6]) * 10; /* the first chunk's runs and members */
+            s->phase_ns[13] += (st[15] - st[14]) * 10; /* ... its sums */
         }
     }
     const SvcSlotOut &o = s->out[slot];

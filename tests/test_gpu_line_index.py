@@ -161,3 +161,37 @@ def test_line_index_service_small_batches_and_fq(gpu, oracle_lib, load):
     assert np.array_equal(got.hits["which_kmer"], want.hits["which_kmer"])
     assert np.array_equal(got.calls["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
     assert len(want.calls) > 20
+
+
+@pytest.mark.parametrize("probe", ["thread", "quad"])
+def test_svc_probe_modes_chain_shapes(gpu, oracle_lib, monkeypatch, probe):
+    """The call service's two probe loops (KGX_SVC_PROBE: a thread's own
+    four 16-B loads per line, or quads reading a window's line together) over
+    tables that wrap, hold duplicates and stray stop keys, or have no empty
+    bucket, over the reference slots and the line index: every call is the
+    oracle's."""
+    monkeypatch.setenv("KGX_SVC_PROBE", probe)
+    rng = np.random.default_rng(31)
+    prm = gpu.Params(2, 200, 0, 0)
+    for shape in ("wrap", "dups_strays", "full"):
+        if shape == "wrap":
+            table, keys = _chain_table(rng, 1001, 800, tail_frac=0.3)
+        elif shape == "dups_strays":
+            table, keys = _chain_table(rng, 997, 500, dup_every=3, stray_every=4, tail_frac=0.2)
+        else:
+            table, keys = _chain_table(rng, 203, 300, tail_frac=0.1)
+        recs = _batch_from(rng, keys, 12)
+        with gpu.Image.from_table(table) as img:
+            for load in (0,) + LOADS:
+                img.set_line_index(load)
+                for name, s in recs:
+                    hits, calls = img.svc_call(s.encode(), prm)
+                    r, o = pack([(name, s)])
+                    w = oracle_lib.process_batch(table, r, o, params=(2, 200, 0, 0))
+                    for f in ("which_kmer", "pos", "function_index", "otu_index"):
+                        assert np.array_equal(hits[f], w.hits[f]), (shape, load, name, f)
+                    assert np.array_equal(hits["function_wt"].view(np.uint32), w.hits["function_wt"].view(np.uint32))
+                    for f in ("start", "end", "count", "function_index"):
+                        assert np.array_equal(calls[f], w.calls[f]), (shape, load, name, f)
+                    assert np.array_equal(calls["weighted_hits"].view(np.uint32),
+                                          w.calls["weighted_hits"].view(np.uint32)), (shape, load, name)

@@ -239,9 +239,9 @@ int main(int argc, char **argv)
                     w.join();
             }
             const uint64_t passes0 = image->coalescer().passes, calls0 = image->coalescer().calls;
-            uint64_t svc0 = 0, svc1 = 0, ph0[8] = {}, ph1[8] = {};
+            uint64_t svc0 = 0, svc1 = 0, ph0[14] = {}, ph1[14] = {};
             (void)kgx_svc_stat(image->handle(), "calls", &svc0);
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < 14; k++) {
                 const std::string nm = "phase_n" + std::to_string(k);
                 (void)kgx_svc_stat(image->handle(), nm.c_str(), &ph0[k]);
             }
@@ -265,7 +265,7 @@ int main(int argc, char **argv)
             const double nm = (double)(m * R);
             /* KGX_SVC_DEBUG=1: mean per call of the host wall and the device phases (us) */
             std::string phases;
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < 14; k++) {
                 const std::string nm2 = "phase_n" + std::to_string(k);
                 (void)kgx_svc_stat(image->handle(), nm2.c_str(), &ph1[k]);
                 if (svc1 > svc0 && ph1[0] > ph0[0]) {
@@ -277,7 +277,7 @@ int main(int argc, char **argv)
             }
             if (!phases.empty())
                 std::fprintf(stderr, "[facade] %s%d service phases (us: wall, residues, probe, compact, store+score, "
-                             "stores, first chunk, rest): %s\n", mode_name[co], T, phases.c_str());
+                             "stores, first chunk, rest, probe rounds, first round, keys, own loads, chunk runs, chunk sums): %s\n", mode_name[co], T, phases.c_str());
             char b[400];
             std::snprintf(b, sizeof b,
                           "%s\"%s%d\": {\"calls_per_s\": %.4g, \"residues_per_s\": %.4g, \"p50_us\": %.1f, "
