@@ -214,6 +214,7 @@ SIGNATURES = {
     "kgx_fq_fragments": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
     "kgx_fq_upload": (_INT, [_P, _P, _P, _U32]),
     "kgx_fq_fragments_uploaded": (_INT, [_P, ctypes.POINTER(Fragments)]),
+    "kgx_fq_fragments_uploaded_start": (_INT, [_P]),
     "kgx_fq_fragments_device": (_INT, [_P, _P, _P, _U32, ctypes.POINTER(Fragments)]),
     "kgx_fq_fragments_device_start": (_INT, [_P, _P, _P, _U32, _U64]),
     "kgx_fq_fragments_finish": (_INT, [_P, ctypes.POINTER(Fragments)]),

@@ -1733,9 +1733,11 @@ void FqRequest::process(const char *text, size_t n, bool finished, std::ostream 
             sl.l = FqLaunched{};
             sl.l.ctx = ctx;
             sl.l.n_reads = (uint32_t)v.n_reads();
-            if (sl.l.n_reads)
+            if (sl.l.n_reads) {
                 if (int rc = kgx_fq_upload(ctx, v.residues(), v.roff, sl.l.n_reads))
                     throw_last(rc, "kgx_fq_upload");
+                start_fragments(ctx);
+            }
         };
         auto launch = [&](Slot &sl) {
             const auto l0 = std::chrono::steady_clock::now();
@@ -1852,8 +1854,23 @@ FqRequest::FqLaunched FqRequest::launch_block(const FqBlock &blk, kgx_ctx *ctx)
         return l;
     if (int rc = kgx_fq_upload(ctx, blk.residues(), blk.roff, l.n_reads))
         throw_last(rc, "kgx_fq_upload");
+    start_fragments(ctx);
     launch_uploaded(l);
     return l;
+}
+
+/* the fragment pass over the reads just uploaded to ctx, enqueued behind the
+ * upload: a part's pass runs while the GPU still probes the part before it */
+void FqRequest::start_fragments(kgx_ctx *ctx)
+{
+    /* fragments as anchors into the bases: the probe translates their windows
+     * itself and no residue goes through HBM (the context keeps residues when
+     * its probe cannot take anchors) */
+    int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
+    if (rc)
+        throw_last(rc, "kgx_ctx_set_option");
+    if ((rc = kgx_fq_fragments_uploaded_start(ctx)))
+        throw_last(rc, "kgx_fq_fragments_uploaded_start");
 }
 
 void FqRequest::launch_uploaded(FqLaunched &l)
@@ -1861,15 +1878,9 @@ void FqRequest::launch_uploaded(FqLaunched &l)
     if (l.n_reads == 0)
         return;
     kgx_ctx *ctx = l.ctx;
-    /* fragments as anchors into the bases: the probe translates their windows
-     * itself and no residue goes through HBM (the context keeps residues when
-     * its probe cannot take anchors) */
-    int rc = kgx_ctx_set_option(ctx, "fq_residues", 0);
+    int rc = kgx_fq_fragments_finish(ctx, &l.fr); /* the pass start_fragments enqueued */
     if (rc)
-        throw_last(rc, "kgx_ctx_set_option");
-    rc = kgx_fq_fragments_uploaded(ctx, &l.fr);
-    if (rc)
-        throw_last(rc, "kgx_fq_fragments_uploaded");
+        throw_last(rc, "kgx_fq_fragments_finish");
     kgx_params p{kg_.min_hits, kg_.max_gap, kg_.order_constraint, kg_.min_weighted_hits};
     /* Calls are sparse over fragments (most fragments of a read are noise),
      * so the calls come back and find_best_call runs on the host for the

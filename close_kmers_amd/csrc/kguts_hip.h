@@ -532,7 +532,10 @@ private:
         kgx_fragments fr{};
     };
     FqLaunched launch_block(const FqBlock &blk, kgx_ctx *ctx);
-    /* launch_block's second half, after kgx_fq_upload of l's reads on l.ctx */
+    /* after kgx_fq_upload on ctx: enqueue the fragment pass over those reads */
+    void start_fragments(kgx_ctx *ctx);
+    /* launch_block's second half, after kgx_fq_upload and start_fragments of
+     * l's reads on l.ctx: the pass's sizes, then the lookup enqueued */
     void launch_uploaded(FqLaunched &l);
     void finish_block(const FqBlock &blk, FqLaunched &l, FamilyMapper &mapper, std::ostream &os);
     kgx_ctx *twin_ctx(); /* a second context on the image, created on first use */

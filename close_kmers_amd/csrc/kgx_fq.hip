@@ -1437,6 +1437,18 @@ int kgx_fq_fragments_uploaded(kgx_ctx *c, kgx_fragments *out)
     return fq_fragments(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), c->fq_up.n_reads, nb, nb, out);
 }
 
+int kgx_fq_fragments_uploaded_start(kgx_ctx *c)
+{
+    if (!c)
+        return fail(KGX_EINVAL, "null argument");
+    if (!c->fq_up.active)
+        return fail(KGX_EINVAL, "no reads uploaded on this context (kgx_fq_upload)");
+    HIP_TRY(hipSetDevice(c->img->device));
+    c->fq_up.active = false;
+    const uint64_t nb = c->fq_up.n_bases;
+    return fq_fragments_enqueue(c, c->fq_bases.as<uint8_t>(), c->fq_roff.as<uint64_t>(), c->fq_up.n_reads, nb, nb);
+}
+
 int kgx_fq_fragments(kgx_ctx *c, const char *bases, const uint64_t *read_offsets, uint32_t n_reads,
                      kgx_fragments *out)
 {

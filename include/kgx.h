@@ -667,6 +667,14 @@ int kgx_fq_fragments(kgx_ctx *ctx, const char *bases, const uint64_t *read_offse
  * kgx_fq_fragments does.  Nothing else may run on ctx between the two. */
 int kgx_fq_upload(kgx_ctx *ctx, const char *bases, const uint64_t *read_offsets, uint32_t n_reads);
 int kgx_fq_fragments_uploaded(kgx_ctx *ctx, kgx_fragments *out);
+/* kgx_fq_fragments_uploaded in two halves: _start enqueues the fragment pass
+ * over the uploaded reads behind their upload and returns at once;
+ * kgx_fq_fragments_finish waits for it and fills out.  The fq handler starts
+ * a part's pass as soon as its upload is enqueued, a part ahead of its
+ * lookup, so the pass runs in the previous probe's tail and sizing the part
+ * never holds the GPU idle between two probes.  The bases stay in use until
+ * _finish returns; nothing else may run on ctx between the two calls. */
+int kgx_fq_fragments_uploaded_start(kgx_ctx *ctx);
 /* reads already in device memory */
 int kgx_fq_fragments_device(kgx_ctx *ctx, const uint8_t *d_bases, const uint64_t *d_read_offsets,
                             uint32_t n_reads, kgx_fragments *out);
