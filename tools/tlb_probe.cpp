@@ -17,10 +17,11 @@
  * Build: hipcc --offload-arch=gfx950 -O3 tools/tlb_probe.cpp -o tools/tlb_probe
  *        -Lclose_kmers_amd -lkgx -Wl,-rpath,'$ORIGIN/../close_kmers_amd'
  *
- * "frag" allocates the buffer after the image build's allocations instead;
+ * "frag" allocates the buffer after the image build's allocations instead,
+ * "first" before them;
  * "kgx" reads a synthetic image's AOS24 table built by libkgx.
  *
- *     tlb_probe GB [contig|frag|kgx]
+ *     tlb_probe GB [contig|frag|first|kgx]
  */
 #include <hip/hip_runtime.h>
 
@@ -164,6 +165,7 @@ int main(int argc, char **argv)
     const uint64_t gb = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 100;
     const bool contig = argc > 2 && std::strcmp(argv[2], "contig") == 0;
     const bool frag = argc > 2 && std::strcmp(argv[2], "frag") == 0;
+    const bool alloc_first = argc > 2 && std::strcmp(argv[2], "first") == 0; /* the buffer before the build's */
     const uint64_t bytes = gb << 30;
     uint4 *buf = nullptr;
     void *keep = nullptr;
@@ -204,6 +206,14 @@ int main(int argc, char **argv)
     } else {
         ae = contig ? hipExtMallocWithFlags((void **)&buf, bytes, hipDeviceMallocContiguous)
                     : hipMalloc((void **)&buf, bytes);
+        if (ae == hipSuccess && alloc_first) {
+            void *aos = nullptr;
+            CHECK(hipMalloc(&aos, 85ull << 30));
+            CHECK(hipMemset(aos, 0, 85ull << 30));
+            CHECK(hipMalloc(&keep, 57ull << 30));
+            CHECK(hipMemset(keep, 0, 57ull << 30));
+            CHECK(hipFree(aos));
+        }
     }
     if (ae != hipSuccess) {
         std::printf("{\"gb\": %llu, \"contig\": %d, \"alloc\": \"%s\"}\n", (unsigned long long)gb, contig,
