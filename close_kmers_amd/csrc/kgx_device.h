@@ -91,11 +91,12 @@ __device__ __forceinline__ float sum_lanes_in_order(float acc, float w, uint64_t
         }
         return acc;
     }
+    /* each lane masks its own weight first, so a step is one lane read and
+     * one add (no scalar select between them) */
+    const float wm = ((mm >> lane_id()) & 1ull) ? w : -0.0f;
 #pragma unroll
-    for (int l = 0; l < 64; l++) {
-        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), l));
-        acc = acc + (((mm >> l) & 1ull) ? x : -0.0f);
-    }
+    for (int l = 0; l < 64; l++)
+        acc = acc + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wm), l));
     return acc;
 }
 /* (the builtins return int: widen through uint32_t, or a low half >= 2^31
