@@ -122,6 +122,25 @@ __device__ __forceinline__ int32_t xor_lane(int32_t v, uint32_t j)
         return __shfl_xor(v, (int)j);
     }
 }
+/* v of lane s (0-3) of this lane's quad: one DPP quad_perm move (s a
+ * constant once unrolled) */
+__device__ __forceinline__ uint32_t quad_bcast32(uint32_t v, uint32_t s)
+{
+    switch (s & 3u) {
+    case 0:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x00, 0xF, 0xF, false); /* [0,0,0,0] */
+    case 1:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x55, 0xF, 0xF, false); /* [1,1,1,1] */
+    case 2:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xAA, 0xF, 0xF, false); /* [2,2,2,2] */
+    default:
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false); /* [3,3,3,3] */
+    }
+}
+__device__ __forceinline__ uint64_t quad_bcast64(uint64_t v, uint32_t s)
+{
+    return (uint64_t)quad_bcast32((uint32_t)(v >> 32), s) << 32 | quad_bcast32((uint32_t)v, s);
+}
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

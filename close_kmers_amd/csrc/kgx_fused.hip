@@ -165,23 +165,33 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             uint64_t key[RB], slot[RB];
             bool pend[RB], hit[RB];
             uint4 rec[RB];
+            /* window w's key (encoded_kmer) and home; pend: no code 20 in it */
+            auto encode = [&](uint32_t w, uint64_t &k, uint64_t &sl, bool &pd) {
+                const uint8_t *c = codes + w;
+                const uint32_t cmax = max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
+                const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
+                const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
+                k = (uint64_t)ka * 160000u + kb;
+                pd = cmax < 20u;
+                sl = pd ? mod_by(k, a.num_sigs >> a.hs, a.magic) << a.hs : 0;
+            };
 #pragma unroll
             for (uint32_t j = 0; j < RB; j++) {
-                const uint32_t w = t + 256 * (jb + j);
                 hit[j] = false;
                 pend[j] = false;
                 rec[j] = make_uint4(0, 0, 0, 0);
                 key[j] = 0;
                 slot[j] = 0;
-                if (jb + j < J && w < W) {
-                    const uint8_t *c = codes + w;
-                    const uint32_t cmax =
-                        max(max(max(c[0], c[1]), max(c[2], c[3])), max(max(c[4], c[5]), max(c[6], c[7])));
-                    const uint32_t ka = ((c[0] * 20u + c[1]) * 20u + c[2]) * 20u + c[3];
-                    const uint32_t kb = ((c[4] * 20u + c[5]) * 20u + c[6]) * 20u + c[7];
-                    key[j] = (uint64_t)ka * 160000u + kb;
-                    pend[j] = cmax < 20u;
-                    slot[j] = pend[j] ? mod_by(key[j], a.num_sigs >> a.hs, a.magic) << a.hs : 0;
+                if constexpr (QUAD) {
+                    /* lane sub of quad g takes the pass's windows g + 64 i
+                     * with i = sub + 4 j (the quads' own windows, below) */
+                    const uint32_t wi = (t >> 2) + 64 * ((t & 3u) + 4 * j);
+                    if (wi < min(256u * RB, W - 256u * jb))
+                        encode(256 * jb + wi, key[j], slot[j], pend[j]);
+                } else {
+                    const uint32_t w = t + 256 * (jb + j);
+                    if (jb + j < J && w < W)
+                        encode(w, key[j], slot[j], pend[j]);
                 }
             }
             /* linear probe by 64-B lines: a round reads the rest of the line
@@ -198,39 +208,37 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             if (dbg && jb == 0)
                 a.dbg[12] = wall_clock64(); /* keys and homes computed */
             if constexpr (QUAD) {
-                /* the loads by quads (the call service): the windows' keys and
-                 * next buckets go through LDS and the 4 lanes of quad g read
-                 * window g + 64 i's line, 16 B each, one instruction for 16
-                 * windows.  A round's lines then cost one address translation
-                 * each where a thread's four 16-B loads of its own line cost
-                 * four, and over a table of many GB those translations bound
-                 * the round (tools/tlb_probe.cpp, 293 lines over 114 GB: 2.3
-                 * vs 3.2 us) */
-                __shared__ uint4 qst[256 * RB]; /* key lo, key hi | pend << 31, next bucket lo, hi */
+                /* the loads by quads (the call service): the 4 lanes of quad g
+                 * read window g + 64 i's line, 16 B each, one instruction for
+                 * 16 windows; lane i & 3 of the quad holds that window's key
+                 * and next bucket (its register j = i >> 2) and a DPP quad
+                 * broadcast hands them to the other three.  A round's lines
+                 * cost one address translation each where a thread's four 16-B
+                 * loads of its own line cost four, and over a table of many GB
+                 * those translations bound the round (tools/tlb_probe.cpp, 293
+                 * lines over 114 GB: 2.3 vs 3.2 us) */
                 __shared__ uint4 qrec[256 * RB];
                 __shared__ uint8_t qhit[256 * RB];
-#pragma unroll
-                for (uint32_t j = 0; j < RB; j++) {
-                    const uint32_t wi = t + 256 * j;
-                    qst[wi] = make_uint4((uint32_t)key[j], (uint32_t)(key[j] >> 32) | (pend[j] ? 0x80000000u : 0u),
-                                         (uint32_t)slot[j], (uint32_t)(slot[j] >> 32));
-                    qhit[wi] = 0;
-                }
-                __syncthreads();
-                const uint32_t CW = min(256u * RB, W - 256u * jb); /* this pass's windows */
                 const uint32_t g = t >> 2, sub = t & 3u, qsh = 4u * (lane >> 2);
+#pragma unroll
+                for (uint32_t j = 0; j < RB; j++)
+                    qhit[g + 64 * (sub + 4 * j)] = 0;
                 /* every bucket examined once a window has gone round the
                  * table (its first line may be partial): a miss where the
                  * reference would spin forever */
                 const uint64_t turn = (NS + 3) / 4 + 1;
                 for (;;) {
-                    uint4 st[4 * RB], pv[4 * RB];
+                    uint64_t kq[4 * RB], sl[4 * RB];
+                    bool pd[4 * RB];
+                    uint4 pv[4 * RB];
 #pragma unroll
                     for (uint32_t i = 0; i < 4 * RB; i++) {
-                        const uint32_t wi = g + 64 * i;
-                        st[i] = wi < CW ? qst[wi] : make_uint4(0, 0, 0, 0);
-                        const uint64_t sl = (uint64_t)st[i].w << 32 | st[i].z, base = sl & ~3ull;
-                        if ((st[i].y >> 31) && sub >= (uint32_t)(sl & 3) && base + sub < NS)
+                        const uint32_t j = i >> 2;
+                        kq[i] = quad_bcast64(key[j], i & 3);
+                        sl[i] = quad_bcast64(slot[j], i & 3);
+                        pd[i] = quad_bcast32(pend[j] ? 1u : 0u, i & 3) != 0;
+                        const uint64_t base = sl[i] & ~3ull;
+                        if (pd[i] && sub >= (uint32_t)(sl[i] & 3) && base + sub < NS)
                             pv[i] = a.table[base + sub];
                     }
                     rounds++;
@@ -243,12 +251,10 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
 #pragma unroll
                     for (uint32_t i = 0; i < 4 * RB; i++) {
                         const uint32_t wi = g + 64 * i;
-                        const bool pd = (st[i].y >> 31) != 0;
-                        const uint64_t sl = (uint64_t)st[i].w << 32 | st[i].z, base = sl & ~3ull;
-                        const bool in = pd && sub >= (uint32_t)(sl & 3) && base + sub < NS;
-                        const uint64_t kq = (uint64_t)(st[i].y & 0x7FFFFFFFu) << 32 | st[i].x;
+                        const uint64_t base = sl[i] & ~3ull;
+                        const bool in = pd[i] && sub >= (uint32_t)(sl[i] & 3) && base + sub < NS;
                         const uint64_t kv = ((uint64_t)pv[i].y << 32 | pv[i].x) & PACK_KEY_MASK;
-                        const bool m = in && kv == kq;
+                        const bool m = in && kv == kq[i];
                         const bool stop = in && (m || kv > MAX_ENCODED);
                         /* the quad's first bucket in probe order that is the
                          * key or a stop decides the window */
@@ -259,11 +265,11 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                             qrec[wi] = pv[i];
                             qhit[wi] = 1;
                         }
-                        const bool live = pd && !sq && !turned;
-                        if (pd && sub == 0) {
+                        const bool live = pd[i] && !sq && !turned;
+                        if (sub == (i & 3)) { /* the window's own lane moves it on */
                             const uint64_t next = base + R >= NS ? 0 : base + R;
-                            qst[wi] = live ? make_uint4(st[i].x, st[i].y, (uint32_t)next, (uint32_t)(next >> 32))
-                                           : make_uint4(st[i].x, st[i].y & 0x7FFFFFFFu, st[i].z, st[i].w);
+                            slot[i >> 2] = live ? next : slot[i >> 2];
+                            pend[i >> 2] = live;
                         }
                         more = more || live;
                     }
