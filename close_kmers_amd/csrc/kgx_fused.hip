@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256) void fused_small_inline_kernel(FusedArgs a, Fu
 struct FusedSlot {
     const uint8_t *res;
     uint32_t len;
+    uint8_t *codes; /* LDS: the residues' codes, decoded by the polling wave */
 };
 
 template <class IN> struct FusedInput;
@@ -114,7 +115,11 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     if (dbg)
         a.dbg[0] = wall_clock64();
     __shared__ uint8_t code_tab[256];
-    __shared__ uint8_t codes[256 * FJ + 8];
+    __shared__ uint8_t codes_own[256 * FJ + 8];
+    constexpr bool SLOT = std::is_same<IN, FusedSlot>::value;
+    uint8_t *codes = codes_own;
+    if constexpr (SLOT)
+        codes = k.codes;
     __shared__ uint4 hrec[256 * FJ];
     __shared__ uint32_t hpos[256 * FJ];
     __shared__ uint32_t wave_cnt[4];
@@ -123,31 +128,18 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     typedef HitFields<true> HF;
 
     const uint32_t t = threadIdx.x, lane = lane_id(), wave = t >> 6;
-    code_tab[t] = (uint8_t)residue_code(t);
     const uint64_t r0 = In::off(a, k, s), len = In::off(a, k, s + 1) - r0;
     const uint64_t wb = In::wb(a, k, s);
     const uint32_t W = (uint32_t)windows_of(len);
-    __syncthreads();
-    /* 1. residues -> codes */
-    if constexpr (std::is_same<IN, FusedSlot>::value) {
-        /* the service's slot (16-B aligned, 4 KB): 4 bytes per thread, so a
-         * protein of up to 1,024 residues costs one device-memory round trip
-         * (a byte per thread took two for a 300-aa protein; 16 bytes per
-         * thread left 16 dependent table lookups on a few threads, r4aa) */
-        const uint32_t nb = (uint32_t)min<uint64_t>(W + 8, len);
-        for (uint32_t c = t; 4 * c < nb; c += 256) {
-            const uint32_t w = reinterpret_cast<const uint32_t *>(k.res)[c];
-#pragma unroll
-            for (uint32_t b = 0; b < 4; b++)
-                if (4 * c + b < nb)
-                    codes[4 * c + b] = code_tab[(w >> (8 * b)) & 0xFFu];
-        }
-    } else {
+    /* 1. residues -> codes (the service's polling wave has decoded them) */
+    if constexpr (!SLOT) {
+        code_tab[t] = (uint8_t)residue_code(t);
+        __syncthreads();
         /* each wave reads 64 consecutive bytes per round */
         for (uint32_t i = t; i < W + 8 && i < len; i += 256)
             codes[i] = code_tab[In::res(a, k, r0 + i)];
+        __syncthreads();
     }
-    __syncthreads();
     if (dbg)
         a.dbg[1] = wall_clock64();
 
@@ -855,7 +847,8 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                                                   uint32_t hs, uint64_t life_ticks, uint32_t poll_chunks)
 {
     __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
-    __shared__ uint32_t rbuf[SVC_RES_CHUNKS * 3]; /* the request's residues, 12 per chunk */
+    __shared__ uint32_t scodes[SVC_RES_CHUNKS * 3]; /* the request's residue codes, 12 per chunk */
+    __shared__ uint8_t tab[256]; /* residue -> code (to_amino_acid_off, kguts.cc:273-339) */
     const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
     const uint64_t t0 = wall_clock64();
     uint32_t last = 0;
@@ -864,6 +857,13 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
     last = __shfl(last, 0);
     const uint4 *hline = reinterpret_cast<const uint4 *>(&hdr[slot]);
     const uint4 *chunks = reinterpret_cast<const uint4 *>(res_base + (uint64_t)slot * SVC_RES_STRIDE);
+    tab[t] = (uint8_t)residue_code(t);
+    __syncthreads();
+    /* 4 residues -> their 4 codes */
+    auto code4 = [&](uint32_t w) -> uint32_t {
+        return (uint32_t)tab[w & 0xFFu] | (uint32_t)tab[(w >> 8) & 0xFFu] << 8 |
+               (uint32_t)tab[(w >> 16) & 0xFFu] << 16 | (uint32_t)tab[w >> 24] << 24;
+    };
     for (;;) {
         if (t < 64) {
             /* wave 0 polls with one 16-B load a lane: lanes 0-3 the header
@@ -900,9 +900,9 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                         cmd[4 * lane + 2] = v.z;
                         cmd[4 * lane + 3] = v.w;
                     } else if (polls && c < n_chunks) {
-                        rbuf[3 * c] = v.x;
-                        rbuf[3 * c + 1] = v.y;
-                        rbuf[3 * c + 2] = v.z;
+                        scodes[3 * c] = code4(v.x);
+                        scodes[3 * c + 1] = code4(v.y);
+                        scodes[3 * c + 2] = code4(v.z);
                     }
                     break;
                 }
@@ -942,11 +942,11 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
          * that the header is seen */
         for (uint32_t c = poll_chunks + t; c < (len + 11) / 12; c += 256) {
             const uint4 v = load_system16(chunks + c);
-            rbuf[3 * c] = v.x;
-            rbuf[3 * c + 1] = v.y;
-            rbuf[3 * c + 2] = v.z;
+            scodes[3 * c] = code4(v.x);
+            scodes[3 * c + 1] = code4(v.y);
+            scodes[3 * c + 2] = code4(v.z);
         }
-        const FusedSlot in{reinterpret_cast<const uint8_t *>(rbuf), len};
+        const FusedSlot in{nullptr, len, reinterpret_cast<uint8_t *>(scodes)};
         __syncthreads(); /* every thread has its copy of the request and the residues before cmd can change */
         /* one body for every length (its registers probe two 256-window
          * slices at a time, its LDS holds all of them): a second, inlined
