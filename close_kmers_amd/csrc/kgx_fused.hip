@@ -816,11 +816,12 @@ hipError_t launch_fused_small(const uint8_t *res, const uint64_t *off, const uin
  * mapped host memory by workgroups that stay resident, so a call costs no
  * launch (the runtime's launch path serialises a worker pool's threads:
  * ~6 us of host time per launch, 170K calls/s at T = 16 in r3g).  Workgroup
- * i owns slot i: thread 0 polls the slot's {req, stop} word with a
- * system-scope acquire load (the host wrote the residues, length, want and
- * parameters before it stored req), the workgroup runs the sequence, and
- * fused_small_body stores the records, the counts and done = req behind a
- * system-scope fence.  Every workgroup leaves on stop or life_ticks after
+ * i owns slot i: wave 0 polls the slot's header line and its first residue
+ * chunks with system-scope loads (the host wrote the residues, length, want
+ * and parameters before it stored req; a chunk carries the request number it
+ * belongs to) and decodes the chunks into codes, the workgroup runs the
+ * sequence, and fused_small_body stores the records, the counts and done =
+ * req behind a system-scope fence.  Every workgroup leaves on stop or life_ticks after
  * its start -- a bound on how long the instance holds its hardware queue; the
  * host keeps the next instance queued behind it while calls arrive
  * (kgx_svc.cpp).  There is no per-workgroup idle exit: a first version left
