@@ -335,30 +335,32 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     a.dbg[2] = wall_clock64();
             }
 
-            /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j + 256) */
+            /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j
+             * + 256), every slice of the pass behind one barrier */
+            __shared__ uint32_t slice_cnt[RB][4];
+            uint64_t m[RB];
 #pragma unroll
             for (uint32_t q = 0; q < RB; q++) {
-                if (jb + q >= J)
-                    break;
-                const bool h = hit[q];
-                const uint4 r = rec[q];
-                const uint64_t m = __ballot(h);
+                m[q] = __ballot(hit[q]); /* (no hit past the last slice) */
                 if (lane == 0)
-                    wave_cnt[wave] = (uint32_t)__popcll(m);
-                __syncthreads();
+                    slice_cnt[q][wave] = (uint32_t)__popcll(m[q]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < RB; q++) {
                 uint32_t before = 0, total = 0;
                 for (uint32_t v = 0; v < 4; v++) {
-                    before += v < wave ? wave_cnt[v] : 0u;
-                    total += wave_cnt[v];
+                    before += v < wave ? slice_cnt[q][v] : 0u;
+                    total += slice_cnt[q][v];
                 }
-                if (h) {
-                    const uint32_t at = nh + before + lanes_below(m);
-                    hrec[at] = r;
+                if (hit[q]) {
+                    const uint32_t at = nh + before + lanes_below(m[q]);
+                    hrec[at] = rec[q];
                     hpos[at] = t + 256 * (jb + q);
                 }
                 nh += total;
-                __syncthreads();
             }
+            __syncthreads();
         }
     }
     if (dbg)
