@@ -64,17 +64,12 @@ def host_cpus():
     return (min(aff, quota) if quota else aff), aff, quota
 
 
-def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, target_s, want):
+def cpu_baseline(oracle, table, res, off, threads, target_s, want):
     """The oracle (bit-exact CPU restatement) over a bounded sample of rank 0's
-    batch, on this host's cores, against a host copy of the same image.  The
-    sample is processed repeatedly until about target_s seconds of timed work
-    (the 85 GB table does not fit any CPU cache, so repeats still miss)."""
-    import oracle
-    oracle.build(ref=False)
-    t0 = time.time()
-    table = img.download()
-    log(f"[bench] image copied to host in {time.time() - t0:.1f}s ({table.nbytes / 1e9:.1f} GB)")
-    res, off = spec_queries(spec, n_seq_sample, length, x_permille)
+    batch (res/off: its first sequences, host copies of the device batch), on
+    this host's cores, against a host copy of the same image.  The sample is
+    processed repeatedly until about target_s seconds of timed work (the 85 GB
+    table does not fit any CPU cache, so repeats still miss)."""
     secs, passes, probes, windows = 0.0, 0, 0, 0
     while secs < target_s and passes < 200:
         r = oracle.process_batch(table, res, off, want=want, n_threads=threads)
@@ -82,7 +77,6 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
         passes += 1
         probes, windows = r.probes, r.windows
     r1 = oracle.process_batch(table, res, off, want=want, n_threads=1)
-    del table
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -91,20 +85,41 @@ def cpu_baseline(abi, img, spec, n_seq_sample, length, threads, x_permille, targ
                 break
     except OSError:
         pass
+    n_seq = len(off) - 1
     return {
         "cpu_model": cpu_model,
         "value": float(passes * len(res) / secs),
         "unit": "residues/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{passes} passes over the first {n_seq_sample} x {length}-aa queries of rank 0's "
-                  f"batch against a host copy of the same image ({WANT_NAMES.get(want, want)}, the GPU "
+        "sample": f"{passes} passes over the first {n_seq} x {int(off[1] - off[0]) if n_seq else 0}-aa queries of "
+                  f"rank 0's batch against a host copy of the same image ({WANT_NAMES.get(want, want)}, the GPU "
                   f"step's outputs), {threads} threads, {secs:.1f} s timed",
         "want": want,
         "single_thread_value": float(len(res) / r1.seconds),
         "pbar": probes / max(1, windows),
         "windows": int(windows),
     }
+
+
+def parity_check(oracle, table, got, res, off, want, threads, line_index):
+    """The timed configuration against the oracle over the whole batch: the
+    device's results of rank 0's batch 0 (the timed want, the timed line
+    index) and the oracle's over the same residues and image, every sequence,
+    compared as bits (oracle.diff_batch: hits, calls, find_best_call)."""
+    t0 = time.time()
+    ref = oracle.process_batch(table, res, off, want=want, n_threads=threads)
+    bad = oracle.diff_batch(got, ref, want)
+    n_bad = sorted(set(i for v in bad.values() for i in v))
+    out = {"sequences": len(off) - 1, "equal": not n_bad, "want": want,
+           "outputs": sorted(bad), "line_index": line_index,
+           "hits": int(ref.hit_offsets[-1]), "calls": int(ref.call_offsets[-1]),
+           "differing_sequences": len(n_bad), "first_differing": n_bad[:8],
+           "by_output": {k: len(v) for k, v in bad.items()},
+           "check": "device results of batch 0 at the timed want and line index vs the CPU oracle over the "
+                    "same 100% of sequences, compared as bits (oracle.diff_batch)",
+           "seconds": round(time.time() - t0, 2)}
+    return out, ref
 
 
 WANT_NAMES = {3: "hits + calls", 7: "hits + calls + OTU", 11: "hits + calls + best call",
@@ -140,11 +155,6 @@ def canary_check(abi, synth, d, dev, line_index=0):
                 f"rank {r['rank']} dev {r['device']} {'ok' if r['ok'] else 'MISMATCH ' + r['digest'][:16]}"
                 for r in recs))
     return recs, ok
-
-
-def spec_queries(spec, n, length, x_permille):
-    from close_kmers_amd import synth
-    return synth.make_queries(spec, n, length=length, x_permille=x_permille, q0=0)
 
 
 def pool_main(args) -> int:
@@ -422,6 +432,12 @@ def main():
     ap.add_argument("--want", type=int, default=11,
                     help="KGX_WANT_* mask (11 = hits + calls + device best call, lookup_request find_best_match)")
     ap.add_argument("--no-canary", action="store_true", help="skip the per-device canary self-check")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the full-batch check of the timed configuration against the oracle")
+    ap.add_argument("--line-index-ab", type=int, default=10,
+                    help="rounds of the in-process line-index A/B (option line_index 0 / 1 over the same "
+                         "batches, interleaved; 0 = skip)")
+    ap.add_argument("--ab-steps", type=int, default=40, help="steps per A/B sample")
     ap.add_argument("--pool-devices", type=int, default=0,
                     help="N > 0: one process, the C5 batch through kgx_pool over N image replicas (devices "
                          "i %% visible), checked byte for byte against one context; prints its own line")
@@ -639,6 +655,66 @@ def main():
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
         f"probe {np.mean(probe_ms):.3f} ms")
 
+    # the line index, settled in this process: the same batches and contexts,
+    # option line_index 0 (probes over the reference slots) and 1 (the index)
+    # alternating, each sample a run of --ab-steps steps as timed above, plus
+    # one event-timed probe; rounds interleaved so drift hits both alike
+    line_ab = None
+    if line_lines and args.line_index_ab > 0:
+        samples = {v: {"step": [], "probe": []} for v in (0, 1)}
+        k = 0
+        for r in range(args.line_index_ab):
+            for v in ((0, 1) if r % 2 == 0 else (1, 0)):
+                for c in ctxs:
+                    c.set_option("line_index", v)
+                for i in range(len(ctxs)):  # settle the rotation
+                    step(None, ctxs[i % len(ctxs)], k)
+                    k += 1
+                for c in ctxs:
+                    c.synchronize()
+                t1 = time.perf_counter()
+                for i in range(args.ab_steps):
+                    step(None, ctxs[i % len(ctxs)], k)
+                    k += 1
+                for c in ctxs:
+                    c.synchronize()
+                samples[v]["step"].append((time.perf_counter() - t1) * 1e3 / args.ab_steps)
+                pm: list = []
+                step(pm, ctx, k)
+                k += 1
+                ctx.synchronize()
+                score_ms.pop()
+                samples[v]["probe"].append(pm[0])
+        for c in ctxs:
+            c.set_option("line_index", 1)
+        med = {v: {"median_step_ms": float(np.median(samples[v]["step"])),
+                   "median_probe_ms": float(np.median(samples[v]["probe"])),
+                   "step_ms": [round(x, 4) for x in samples[v]["step"]],
+                   "probe_ms": [round(x, 4) for x in samples[v]["probe"]]} for v in (0, 1)}
+        gain = med[0]["median_step_ms"] / med[1]["median_step_ms"] - 1.0
+        line_ab = {"rounds": args.line_index_ab, "steps_per_sample": args.ab_steps, "load": args.line_index,
+                   "without_index": med[0], "with_index": med[1],
+                   "step_gain": gain,
+                   "note": "one process, same batches and worker contexts; context option line_index 0 = probes "
+                           "over the reference slots, 1 = over the line index; step_gain = without / with - 1"}
+        log(f"[bench] line index A/B ({args.line_index_ab} rounds): step {med[0]['median_step_ms']:.4f} ms without, "
+            f"{med[1]['median_step_ms']:.4f} with ({gain * 100:+.1f}%); probe {med[0]['median_probe_ms']:.4f} / "
+            f"{med[1]['median_probe_ms']:.4f} ms")
+
+    # the timed configuration's results of batch 0, for the full-batch check
+    # against the oracle below (rank 0)
+    got0 = res0 = off0 = None
+    if d.rank == 0 and not args.no_parity:
+        step(None, ctx, 0)
+        r = abi.Result()
+        abi.check(L.kgx_device_batch_collect(ctx.handle, want, ctypes.byref(r)), "collect")
+        got0 = abi.BatchResult(r, want)
+        d_res, d_off = batches[0]
+        res0 = np.empty(n_res, np.uint8)
+        off0 = np.empty(n + 1, np.uint64)
+        abi.check(L.kgx_memcpy_d2h(res0.ctypes.data, d_res, res0.nbytes), "d2h")
+        abi.check(L.kgx_memcpy_d2h(off0.ctypes.data, d_off, off0.nbytes), "d2h")
+
     # PCIe-inclusive rate of the host-buffer boundary (kgx_process_batch:
     # H2D residues, plan/probe/score, gather, D2H hits + calls) -- reported
     # beside `value`, never as it
@@ -735,17 +811,39 @@ def main():
                 f"{rate * useful / 1e9:.0f} GB/s useful")
 
     cpu = None
+    parity = None
     # the CPU port is timed at N=1 only (one host, one baseline; at N>1 the
-    # other ranks would wait on rank 0's host copy of the image)
-    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+    # other ranks would wait on rank 0's host copy of the image); the parity
+    # check of batch 0 runs on rank 0 at every N
+    want_cpu = d.rank == 0 and d.world == 1 and not args.no_cpu_baseline
+    if got0 is not None or want_cpu:
+        import oracle
+        oracle.build(ref=False)
         t_auto, aff, quota = host_cpus()
         threads = args.cpu_threads or t_auto
-        cpu = cpu_baseline(abi, img, spec, min(args.cpu_sample, n), Ls, threads, args.x_permille,
-                           args.cpu_seconds, want)
-        cpu["affinity_cpus"] = aff
-        cpu["cgroup_cpu_quota"] = quota
-        log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads "
-            f"(affinity {aff} CPUs, cgroup quota {quota}), P = {cpu['pbar']:.4f}")
+        t0 = time.time()
+        table = img.download()
+        log(f"[bench] image copied to host in {time.time() - t0:.1f}s ({table.nbytes / 1e9:.1f} GB)")
+        if got0 is not None:
+            parity, _ = parity_check(oracle, table, got0, res0, off0, want, threads,
+                                     args.line_index if line_lines else 0)
+            del got0
+            log(f"[bench] parity vs oracle over {parity['sequences']} sequences (want {want}, line index "
+                f"{parity['line_index']}): {'equal' if parity['equal'] else 'MISMATCH ' + str(parity['by_output'])}")
+        if want_cpu:
+            ns = min(args.cpu_sample, n)
+            if res0 is None:
+                d_res, d_off = batches[0]
+                res0 = np.empty(n_res, np.uint8)
+                off0 = np.empty(n + 1, np.uint64)
+                abi.check(L.kgx_memcpy_d2h(res0.ctypes.data, d_res, res0.nbytes), "d2h")
+                abi.check(L.kgx_memcpy_d2h(off0.ctypes.data, d_off, off0.nbytes), "d2h")
+            cpu = cpu_baseline(oracle, table, res0[:int(off0[ns])], off0[:ns + 1], threads, args.cpu_seconds, want)
+            cpu["affinity_cpus"] = aff
+            cpu["cgroup_cpu_quota"] = quota
+            log(f"[bench] cpu baseline {cpu['value']:.3e} residues/s on {threads} threads "
+                f"(affinity {aff} CPUs, cgroup quota {quota}), P = {cpu['pbar']:.4f}")
+        del table
 
     for e in ev:
         L.kgx_event_destroy(e)
@@ -865,12 +963,16 @@ def main():
                     if line_ceiling and probe_kernel == "probe_line_kernel" else None),
             },
             "cpu_baseline": cpu,
+            "parity": parity,
+            "line_index_ab": line_ab,
             "host_path": host_path,
             "host_path_lookup": host_path_lookup,
             "pool_e2e": pool_e2e,
         }
         print(json.dumps(line), flush=True)
     d.close()
+    if parity is not None and not parity["equal"]:
+        raise SystemExit("parity check failed: the timed configuration's results differ from the oracle's")
 
 
 if __name__ == "__main__":

@@ -849,7 +849,7 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                                                   const uint4 *table, uint64_t num_sigs, uint64_t magic,
                                                   uint32_t hs, uint64_t life_ticks, uint32_t poll_chunks)
 {
-    __shared__ uint32_t cmd[17]; /* the request's header line; [16] = go */
+    __shared__ uint32_t cmd[18]; /* the request's header line; [16] = go, [17] = chunks still stale */
     __shared__ uint32_t scodes[SVC_RES_CHUNKS * 3]; /* the request's residue codes, 12 per chunk */
     __shared__ uint8_t tab[256]; /* residue -> code (to_amino_acid_off, kguts.cc:273-339) */
     const uint32_t slot = blockIdx.x, t = threadIdx.x, lane = lane_id();
@@ -897,6 +897,13 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
                             stale = v.w != req;
                         }
                     }
+                    /* past the bound with chunks still stale: the request is
+                     * answered with an impossible count (the host rejects it,
+                     * KGX_EDEVICE, and takes the batch path), never computed
+                     * over residues of another request */
+                    const bool lost = __ballot(stale) != 0;
+                    if (lane == 0)
+                        cmd[17] = lost ? 1u : 0u;
                     if (lane < 4) {
                         cmd[4 * lane] = v.x;
                         cmd[4 * lane + 1] = v.y;
@@ -919,6 +926,19 @@ __global__ __launch_bounds__(256) void svc_kernel(const SvcSlotHdr *hdr, SvcSlot
         __syncthreads();
         if (!cmd[16])
             break;
+        if (cmd[17]) {
+            const uint32_t req = cmd[0];
+            if (t == 0) {
+                out[slot].nh = 0xFFFFFFFFu;
+                out[slot].nc = 0;
+                out[slot].no = 0;
+                __threadfence_system();
+                *reinterpret_cast<volatile uint32_t *>(&out[slot].done) = req;
+            }
+            last = req;
+            __syncthreads(); /* cmd is rewritten by the next poll */
+            continue;
+        }
         /* the residues the host wrote before req: no stale line in this CU's caches */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const SvcSlotHdr *h = reinterpret_cast<const SvcSlotHdr *>(cmd);

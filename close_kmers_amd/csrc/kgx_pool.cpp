@@ -633,8 +633,10 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
         c->stream = own;
         if (rcs[i]) {
             errs[i] = kgx_last_error();
-            /* the shards enqueued so far still run: drain them before returning */
-            for (auto *v : {&p->pass_stream, &p->score_stream, &p->roll_stream})
+            /* the shards enqueued so far still run: drain them before returning
+             * (their uploads too, which may still read the caller's pinned
+             * residues or the shared staging buffer) */
+            for (auto *v : {&p->up_stream, &p->pass_stream, &p->score_stream, &p->roll_stream})
                 for (hipStream_t x : *v)
                     if (x)
                         (void)hipStreamSynchronize(x);

@@ -422,6 +422,7 @@ struct kgx_ctx {
     int score_variant = 0; /* 0 = hybrid, 1 = wave-parallel, 2 = lane only (option "score_variant", kgx_internal.h) */
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */
+    int use_line_index = 1; /* option "line_index": 0 = probe the reference slots even when the image has a line index */
     uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */
     int microbench_ilp = 8;       /* independent reads in flight per lane */
     int microbench_wgs = 8;       /* 256-thread workgroups per CU */
@@ -553,6 +554,14 @@ struct kgx_ctx {
 };
 
 namespace kgx {
+/* what c's probes read: the image's line index unless option "line_index" is 0 */
+inline bool ctx_lines(const kgx_ctx *c) { return c->img->d_lines && c->use_line_index; }
+inline const void *ctx_probe_table(const kgx_ctx *c)
+{
+    return ctx_lines(c) ? static_cast<const void *>(c->img->d_lines) : c->img->resident();
+}
+inline uint64_t ctx_probe_buckets(const kgx_ctx *c) { return ctx_lines(c) ? 4 * c->img->n_lines : c->img->num_sigs; }
+inline uint32_t ctx_home_shift(const kgx_ctx *c) { return ctx_lines(c) ? 2u : 0u; }
 /* one chunk of compact records -> kgx_hit for sequences [a, b) of it:
  * out[j - out_base] for CSR hit j (hoff: the batch's hit offsets);
  * kgx_hit.seq = s + seq_base; nt = streaming stores */

@@ -1023,6 +1023,12 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->probe_variant = (int)value;
         return KGX_OK;
     }
+    if (n == "line_index") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "line_index must be 0 or 1");
+        c->use_line_index = (int)value;
+        return KGX_OK;
+    }
     if (n == "probe_serialize") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "probe_serialize must be 0 or 1");
@@ -1400,9 +1406,9 @@ int stage_probe_dna(kgx_ctx *c, const uint8_t *bases, uint64_t n_bases, const ui
                                 "(set fq_residues 1 for other probes)");
     return probe_chained(c, [&] {
         return launch_probe_dna(bases, n_bases, anchors, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                                c->n_seq, c->max_tiles, c->img->probe_table(), c->img->probe_buckets(),
+                                c->n_seq, c->max_tiles, ctx_probe_table(c), ctx_probe_buckets(c),
                                 c->hits.as<uint4>(), c->hit_mask.as<uint64_t>(), (int)(c->tile_windows / 64),
-                                probe_max_blocks(c), c->stream, c->img->home_shift());
+                                probe_max_blocks(c), c->stream, ctx_home_shift(c));
     });
 }
 
@@ -1416,11 +1422,11 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
         return fail(KGX_EINVAL, "probe: residues missing or offsets differ from the plan");
     return probe_chained(c, [&] {
         return launch_probe(d_res, c->n_residues, d_off, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
-                            c->n_seq, c->max_tiles, c->img->probe_table(), c->img->layout, c->img->probe_buckets(),
+                            c->n_seq, c->max_tiles, ctx_probe_table(c), c->img->layout, ctx_probe_buckets(c),
                             c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                             c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
                             (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb,
-                            probe_max_blocks(c), c->stream, c->img->home_shift());
+                            probe_max_blocks(c), c->stream, ctx_home_shift(c));
     });
 }
 
@@ -2526,35 +2532,22 @@ int process_batch_streamed(kgx_ctx *c, const kgx_params *params, const char *res
 /* A stream for the host path's bulk copies / uploads.  The runtime spreads a
  * process's streams over a few hardware queues (4 by default), each a FIFO
  * that blocks behind an event wait at its head, so the copy stream's waits
- * held up other streams' work queued behind them.  The copy stream therefore
- * gets a hardware queue the contexts' streams never share.  KGX_OWN_QUEUES:
- *   2 (default) a stream at the device's lowest priority: the runtime keeps a
- *     queue pool per priority, so it shares only with other copy streams;
- *   1 a full-CU-mask stream, which gets a queue of its own (r4o: the bench's
- *     host path 3.83 vs 4.17 ms per 30M-residue batch on a plain stream).  A
- *     process that exits with such a stream alive faults inside rocprofv3's
- *     finalisation (r5c: SIGSEGV in __cxa_finalize under --kernel-trace;
- *     priority streams exit clean), so it is no longer the default;
- *   0 a plain stream. */
+ * held up other streams' work queued behind them.  The copy stream is made at
+ * the device's lowest priority: the runtime keeps a queue pool per priority,
+ * so it shares a queue only with other copy streams.  (Round 4's full-CU-mask
+ * stream got a queue of its own but faulted inside rocprofv3's finalisation
+ * when a process exited with it alive, r5c; it is gone.)  KGX_OWN_QUEUES=0:
+ * a plain stream. */
 hipError_t own_queue_stream(int device, hipStream_t *s)
 {
+    (void)device;
     const char *e = std::getenv("KGX_OWN_QUEUES");
-    const int mode = e ? std::atoi(e) : 2;
-    if (mode == 2) {
+    if (!e || std::atoi(e) != 0) {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest &&
             hipStreamCreateWithPriority(s, hipStreamNonBlocking, least) == hipSuccess)
             return hipSuccess;
         (void)hipGetLastError();
-    } else if (mode == 1) {
-        int cus = 0;
-        hipError_t r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (r == hipSuccess && cus > 0) {
-            std::vector<uint32_t> mask((size_t)(cus + 31) / 32, ~0u);
-            if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess)
-                return hipSuccess;
-            (void)hipGetLastError(); /* no queue left for it: a plain stream */
-        }
     }
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
@@ -2951,8 +2944,8 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
         HIP_TRY(c->h_fdbg.device_ptr(0, &d_dbg));
     }
     HIP_TRY(launch_fused_small(static_cast<const uint8_t *>(d_res), static_cast<const uint64_t *>(d_off),
-                               static_cast<const uint64_t *>(d_wb), n_seq, want, c->img->probe_table(),
-                               c->img->probe_buckets(), p,
+                               static_cast<const uint64_t *>(d_wb), n_seq, want, ctx_probe_table(c),
+                               ctx_probe_buckets(c), p,
                                static_cast<kgx_hit *>(d_hits), static_cast<kgx_call *>(d_calls),
                                static_cast<uint32_t *>(d_counts), static_cast<uint32_t *>(d_done), token,
                                (uint32_t)longest, static_cast<uint64_t *>(d_dbg), c->h_off_stage.data(),
@@ -2960,7 +2953,7 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
                                c->fused_inline && n_seq <= FUSED_INLINE_SEQ && off[n_seq] <= FUSED_INLINE_RES
                                    ? (uint32_t)std::max<uint64_t>(off[n_seq], 1)
                                    : 0u,
-                               c->stream, c->img->home_shift()));
+                               c->stream, ctx_home_shift(c)));
     /* every sequence's token (stored after its results, behind a
      * system-scope fence); a fault or a lost store still ends the wait */
     const volatile uint32_t *done = c->h_fdone.data();

@@ -120,6 +120,13 @@ struct SvcState {
      * (host wall per 300-aa call 11.25 vs 11.9 us, r7f); more chunks per
      * poll measured no better (60: 11.3-11.6) */
     uint32_t poll_chunks = 28;
+    /* a call unanswered this long marks the service broken (KGX_SVC_TIMEOUT_MS,
+     * default 10 s) */
+    int64_t timeout_ns = 10000000000ll;
+    /* test injection (KGX_SVC_TEST_DROP=n): the next n requests are written
+     * but never posted, as if the device had stalled on them */
+    std::atomic<int> drop{0};
+    bool leaked = false; /* drain timed out: the state stays allocated */
 };
 
 namespace {
@@ -240,13 +247,26 @@ int top_up(SvcState *s)
     return KGX_OK;
 }
 
-/* every workgroup of every enqueued instance leaves; the slots stay */
-void drain(SvcState *s)
+/* every workgroup of every enqueued instance leaves; the slots stay.  No
+ * unbounded runtime wait: every slot's stop word is raised and the host waits
+ * -- at most 2 s -- until each slot's workgroups of every instance launched
+ * have counted themselves out (SvcSlotOut.left); only then is the stream
+ * synchronised, which returns at once.  false: some workgroup did not leave
+ * (a stalled instance), and the caller must not free what it may touch. */
+bool drain(SvcState *s)
 {
     std::lock_guard<std::mutex> lk(s->mu);
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 1u, __ATOMIC_RELEASE);
     wc_fence();
+    const uint32_t launched = (uint32_t)s->n_launches.load();
+    const int64_t t0 = now_ns();
+    for (uint32_t i = 0; i < s->slots; i++)
+        while (__atomic_load_n(&s->out[i].left, __ATOMIC_ACQUIRE) != launched) {
+            if (now_ns() - t0 > 2000000000ll)
+                return false;
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
     (void)hipStreamSynchronize(s->stream);
     for (hipEvent_t e : s->running)
         s->spare.push_back(e);
@@ -254,7 +274,10 @@ void drain(SvcState *s)
     for (uint32_t i = 0; i < s->slots; i++)
         __atomic_store_n(&s->hdr[i].stop, 0u, __ATOMIC_RELEASE);
     wc_fence();
+    return true;
 }
+
+std::atomic<uint64_t> g_leaked{0};
 
 void destroy(SvcState *s)
 {
@@ -265,8 +288,13 @@ void destroy(SvcState *s)
         g_live.erase(s);
     }
     (void)hipSetDevice(s->device);
-    if (s->stream)
-        drain(s);
+    if (s->stream && !drain(s)) {
+        /* an instance that never left may still read the slots and write
+         * the replies: keep its memory and stream (leaked, counted) */
+        s->leaked = true;
+        g_leaked++;
+        return;
+    }
     for (hipEvent_t e : s->spare)
         (void)hipEventDestroy(e);
     if (s->stream)
@@ -361,6 +389,10 @@ int create(kgx_image *img, uint32_t slots, uint64_t idle_us, uint64_t life_us, S
         s->poll_chunks = (uint32_t)std::min<long>(SVC_POLL_CHUNKS, std::max(0L, std::atol(pc)));
     if (const char *sl = std::getenv("KGX_SVC_SLEEP_US"))
         s->sleep_us = (uint32_t)std::max(0, std::atoi(sl));
+    if (const char *to = std::getenv("KGX_SVC_TIMEOUT_MS"))
+        s->timeout_ns = std::max<int64_t>(1, std::atoll(to)) * 1000000ll;
+    if (const char *dr = std::getenv("KGX_SVC_TEST_DROP"))
+        s->drop = std::max(0, std::atoi(dr));
     char *hp = static_cast<char *>(h), *dp = static_cast<char *>(d);
     s->hdr = reinterpret_cast<SvcSlotHdr *>(hp);
     s->d_hdr = reinterpret_cast<SvcSlotHdr *>(dp);
@@ -551,6 +583,8 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s && s->broken ? 1 : 0;
     else if (n == "priority") /* the service stream's priority + 100 (lower = higher priority) */
         *value = s ? (uint64_t)(s->priority + 100) : 0;
+    else if (n == "leaked") /* services whose drain timed out (their memory kept), process-wide */
+        *value = g_leaked.load();
     else if (n == "devmem") /* 1: requests travel through device memory (large BAR) */
         *value = s && s->reqmem ? 1 : 0;
     else if ((n.size() == 8 || n.size() == 9) && n.compare(0, 7, "phase_n") == 0 &&
@@ -616,8 +650,11 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
      * fences order the request's bytes before its number and push it out */
     if (s->reqmem)
         wc_fence();
-    __atomic_store_n(&h.copy, q, __ATOMIC_RELEASE);
-    __atomic_store_n(&h.req, q, __ATOMIC_RELEASE);
+    const bool post = s->drop.load(std::memory_order_relaxed) <= 0 || s->drop.fetch_sub(1) <= 0;
+    if (post) {
+        __atomic_store_n(&h.copy, q, __ATOMIC_RELEASE);
+        __atomic_store_n(&h.req, q, __ATOMIC_RELEASE);
+    }
     if (s->reqmem)
         wc_fence();
     /* keep instances enqueued (cheap: one clock read unless 200 us passed) */
@@ -654,14 +691,20 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
                 }
                 nudged = true;
             }
-            if (dt > 10000000000ll) {
+            if (dt > s->timeout_ns) {
                 /* 10 s: the slot is abandoned (a late answer could still land
                  * in it, so it is never handed out again) and the service
                  * turns every later call away, to the batch paths, until
                  * kgx_svc_stop / kgx_svc_config replaces it */
                 s->n_abandoned++;
                 s->broken = true;
-                return fail(KGX_EDEVICE, "call service: no answer within 10 s");
+                return fail(KGX_EDEVICE, "call service: no answer within the timeout (10 s)");
+            }
+            if (s->broken.load(std::memory_order_relaxed)) {
+                /* another call found the service broken: do not wait out the
+                 * timeout too (the slot is abandoned the same way) */
+                s->n_abandoned++;
+                return fail(KGX_EBUSY, "call service: broken while this call waited");
             }
         }
 #if defined(__x86_64__)
@@ -696,6 +739,12 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
     }
     const SvcSlotOut &o = s->out[slot];
     const uint32_t nh = o.nh, nc = o.nc, no = (want & KGX_WANT_OTU) ? o.no : 0u;
+    if (nh == 0xFFFFFFFFu) {
+        /* the device gave up on residue chunks that never arrived (svc_kernel's
+         * 1-s bound): not computed, take the batch path */
+        give_slot(s, slot);
+        return fail(KGX_EBUSY, "call service: the request's residues did not reach the device");
+    }
     if (nh > W || nc > W || no > W) {
         give_slot(s, slot);
         return fail(KGX_EDEVICE, "call service: more records than windows");

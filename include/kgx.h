@@ -262,7 +262,11 @@ int kgx_image_set_layout(kgx_image *img, int layout);
  * 64-B request per window instead of ~1.05.  Costs 64 B * n_lines of HBM
  * beside the PACKED16 table, which downloads, saves and filters keep using.
  * Like set_layout, no call may run on the image meanwhile.  Replicas
- * (kgx_image_replicate) do not inherit it: build it on each that should. */
+ * (kgx_image_replicate) do not inherit it: build it on each that should.
+ * Loads past ~48 (75% of the buckets) are accepted for tests of full lines,
+ * but linear probing there walks ~1/(1-a)^2 buckets per miss: the build's
+ * insert walks and the probes' chains grow steeply (results stay exact);
+ * 36 is the measured load. */
 int kgx_image_set_line_index(kgx_image *img, uint32_t keys_per_64_lines);
 /* lines of the image's line index (0: none) */
 uint64_t kgx_image_line_count(const kgx_image *img);
@@ -295,6 +299,8 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * aligned 64-B / 128-B table line per instruction (probe_j 1-4 / 1-2; other
  * combinations run variant 0);
  * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
+ * "line_index" 1 (default) / 0 = this context's probes read the image's line
+ * index when it has one / the reference slots (in-process A/Bs);
  * "probe_serialize" 1 (default) / 0: this context's probes wait for the
  * image's previous probe (any context), so that probes run back to back and
  * the other kernels of the contexts overlap them;
@@ -487,14 +493,21 @@ int kgx_svc_config(kgx_image *img, uint32_t slots, uint32_t idle_us, uint32_t li
  * kgx_svc_config, kgx_image_set_layout / set_filter and kgx_image_close).
  * Safe while other threads are inside kgx_svc_call: it waits until they have
  * returned (their calls are served); a call that starts afterwards starts a
- * new service.  A call that gets no answer within 10 s returns KGX_EDEVICE and
- * leaves its slot for good (a late answer may still land in it) and the
- * service "broken": every later call returns KGX_EBUSY (take a batch path)
- * until kgx_svc_stop or kgx_svc_config replaces the service. */
+ * new service.  A call that gets no answer within 10 s (KGX_SVC_TIMEOUT_MS)
+ * returns KGX_EDEVICE and leaves its slot for good (a late answer may still
+ * land in it) and the service "broken": every later call, and every call
+ * still waiting, returns KGX_EBUSY (take a batch path) until kgx_svc_stop or
+ * kgx_svc_config replaces the service.  Stopping never waits on the runtime
+ * without a bound: it waits at most 2 s for the workgroups to leave, and a
+ * service whose workgroups did not is left allocated ("leaked") rather than
+ * freed under them.  A request whose residues never reached the device
+ * returns KGX_EBUSY. */
 int kgx_svc_stop(kgx_image *img);
 /* "slots", "calls" (served), "launches" (instances enqueued), "busy" (calls
  * turned away for want of a slot), "abandoned" (slots given up after a 10-s
  * wait), "broken" (1: calls are turned away until the service is replaced),
+ * "leaked" (process-wide: stopped services whose workgroups did not leave
+ * within 2 s, their memory kept),
  * "devmem" (1: requests are written into fine-grained device memory through a
  * large BAR, else mapped host memory; KGX_SVC_DEVMEM=0 forces the latter),
  * "priority" (100 + the service stream's priority; the stream is created at

@@ -76,8 +76,11 @@ class _Result(ctypes.Structure):
 
 
 # oracle_best: find_best_call per sequence (want WANT_BEST)
+# kind / fi0 / fi1: which branch decided (0 no calls, 1 called, 2 ambiguous
+# pair, 3 no call) and the function indices behind it (-1 where none)
 BEST_DTYPE = np.dtype([("function_index", "<i4"), ("score", "<f4"), ("weighted_score", "<f4"),
-                       ("score_offset", "<f4"), ("offset_set", "<i4")])
+                       ("score_offset", "<f4"), ("offset_set", "<i4"), ("kind", "<i4"), ("fi0", "<i4"),
+                       ("fi1", "<i4")])
 
 
 def build(ref: bool | None = None) -> None:
@@ -215,6 +218,72 @@ def process_batch(table: np.ndarray, residues: np.ndarray, offsets: np.ndarray,
         return BatchResult(ho, hits, co, calls, oo, otus, r.probes, r.windows, r.seconds, best)
     finally:
         L.oracle_result_free(ctypes.byref(r))
+
+
+def _bad_seqs(got_off, want_off, rows_equal) -> np.ndarray:
+    """Sequences whose rows differ: by count first, else by the rows that do."""
+    gc, wc = np.diff(np.asarray(got_off, np.int64)), np.diff(np.asarray(want_off, np.int64))
+    if len(gc) != len(wc):
+        return np.arange(max(len(gc), len(wc)))
+    if (gc != wc).any():
+        return np.nonzero(gc != wc)[0]
+    bad = np.nonzero(~rows_equal)[0] if rows_equal is not None else np.zeros(0, np.int64)
+    return np.unique(np.searchsorted(np.asarray(want_off, np.int64), bad, side="right") - 1)
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def diff_batch(got, want: BatchResult, mask: int) -> dict:
+    """Per output the sequences whose device results differ from the
+    oracle's, compared as bits: got has the device's hit_offsets / hits
+    (kgx_hit), call_offsets / calls, otu_offsets / otus (kgx_otu) and best
+    (kgx_best_call) arrays; mask = the WANT_* bits both were run with.
+    Returns {"hits": [...], "calls": [...], ...} of differing sequence
+    indices (empty lists: equal)."""
+    out = {}
+    if mask & WANT_HITS:
+        gh, wh = got.hits, want.hits
+        eq = None
+        if len(gh) == len(wh):
+            eq = np.ones(len(wh), bool)
+            for f in ("which_kmer", "otu_index", "avg_from_end", "function_index", "pos", "seq"):
+                eq &= gh[f] == wh[f]
+            eq &= _bits(gh["function_wt"]) == _bits(wh["function_wt"])
+        out["hits"] = _bad_seqs(got.hit_offsets, want.hit_offsets, eq).tolist()
+    if mask & WANT_CALLS:
+        gc, wc = got.calls, want.calls
+        eq = None
+        if len(gc) == len(wc):
+            eq = np.ones(len(wc), bool)
+            for f in ("start", "end", "count", "function_index"):
+                eq &= gc[f] == wc[f]
+            eq &= _bits(gc["weighted_hits"]) == _bits(wc["weighted_hits"])
+        out["calls"] = _bad_seqs(got.call_offsets, want.call_offsets, eq).tolist()
+    if mask & WANT_OTU:
+        go, wo = got.otus, want.otus
+        eq = None
+        if len(go) == len(wo):
+            eq = (go["otu_index"] == wo[:, 0]) & (go["count"] == wo[:, 1])
+        out["otus"] = _bad_seqs(got.otu_offsets, want.otu_offsets, eq).tolist()
+    if mask & WANT_BEST:
+        gb, wb = got.best, want.best
+        if gb is None or wb is None or len(gb) != len(wb):
+            out["best"] = list(range(len(want.hit_offsets) - 1))
+        else:
+            # kgx_best_call (kind, fi0, fi1, score, weighted_score, score_offset)
+            # against find_best_call's outputs and decision (kguts.cc:1008-1199)
+            k = gb["kind"]
+            eq = (k == wb["kind"]) & (_bits(gb["score"]) == _bits(wb["score"]))
+            eq &= _bits(gb["weighted_score"]) == _bits(wb["weighted_score"])
+            eq &= (k == 0) | (_bits(gb["score_offset"]) == _bits(wb["score_offset"]))
+            eq &= (k == 0) == (wb["offset_set"] == 0)
+            eq &= ((k != 1) & (k != 2)) | (gb["fi0"] == wb["fi0"])
+            eq &= (k != 2) | (gb["fi1"] == wb["fi1"])
+            eq &= np.where(k == 1, gb["fi0"], -1) == wb["function_index"]
+            out["best"] = np.nonzero(~eq)[0].tolist()
+    return out
 
 
 def build_table(num_sigs: int, keys, fI, oI, avg, wt) -> np.ndarray:

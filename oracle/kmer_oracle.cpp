@@ -346,14 +346,19 @@ static const char *function_at(const std::vector<std::string> &f, int i)
 /* find_best_call, kguts.cc:1008-1199 */
 void find_best_call(const std::vector<Call> &calls, const std::vector<std::string> &functions,
                     int &function_index, std::string &function, float &score,
-                    float &weighted_score, float &score_offset)
+                    float &weighted_score, float &score_offset, int *decision)
 {
+    int dummy[3];
+    int *d = decision ? decision : dummy;
+    d[0] = 0;
+    d[1] = d[2] = -1;
     function_index = -1;
     function = "";
     score = 0.0f;
     weighted_score = 0.0f;
     if (calls.empty())
         return; /* score_offset untouched, kguts.cc:1015-1018 */
+    d[0] = 3;
 
     /* 1: collapse runs of adjacent calls with one function (:1023-1040) */
     std::vector<Call> collapsed;
@@ -412,6 +417,8 @@ void find_best_call(const std::vector<Call> &calls, const std::vector<std::strin
         score_offset = (float)(vec[0].second.count - vec[1].second.count);
 
     if (score_offset >= 5.0f) { /* code says >= 5 (SCORING.txt:77 says > 5) */
+        d[0] = 1;
+        d[1] = vec[0].first;
         function_index = vec[0].first;
         function = function_at(functions, function_index);
         score = (float)vec[0].second.count;
@@ -427,11 +434,17 @@ void find_best_call(const std::vector<Call> &calls, const std::vector<std::strin
         if (f2 > f1)
             std::swap(f1, f2);
         if (vec.size() == 2) {
+            d[0] = 2;
+            d[1] = vec[0].first;
+            d[2] = vec[1].first;
             function = f1 + " ?? " + f2;
             score = (float)vec[0].second.count;
         } else {
             float pair_offset = (float)(vec[1].second.count - vec[2].second.count);
             if (pair_offset > 5.0f) {
+                d[0] = 2;
+                d[1] = vec[0].first;
+                d[2] = vec[1].first;
                 function = f1 + " ?? " + f2;
                 score = (float)vec[0].second.count;
                 score_offset = pair_offset;
@@ -544,6 +557,7 @@ struct oracle_best {
     int32_t function_index;
     float score, weighted_score, score_offset;
     int32_t offset_set; /* 0: score_offset left untouched (no calls, kguts.cc:1015-1018) */
+    int32_t kind, fi0, fi1; /* find_best_call's decision argument */
 };
 
 struct oracle_result {
@@ -603,8 +617,12 @@ int oracle_process_batch(const void *table, uint64_t num_sigs, const int32_t *pa
                 float off = 0.0f;
                 r.best.score_offset = std::numeric_limits<float>::quiet_NaN();
                 off = r.best.score_offset;
+                int dec[3];
                 find_best_call(r.calls, no_names, r.best.function_index, fn, r.best.score, r.best.weighted_score,
-                               off);
+                               off, dec);
+                r.best.kind = dec[0];
+                r.best.fi0 = dec[1];
+                r.best.fi1 = dec[2];
                 r.best.offset_set = !std::isnan(off);
                 r.best.score_offset = r.best.offset_set ? off : 0.0f;
                 if (!(want & WANT_CALLS))

@@ -119,11 +119,15 @@ unsigned char residue_code(char c);
 uint64_t encode8(const unsigned char *codes);
 void decode8(uint64_t key, char out[9]);
 
-/* find_best_call (kguts.cc:1008-1199) */
+/* find_best_call (kguts.cc:1008-1199).  decision (optional): which branch
+ * set the outputs -- [0] 0 no calls, 1 called, 2 ambiguous pair, 3 no call;
+ * [1], [2] the function indices behind the call / the pair (vec[0], vec[1]
+ * of :1134-1139), -1 where none -- so a caller without function names can
+ * still tell the decisions apart */
 void find_best_call(const std::vector<Call> &calls,
                     const std::vector<std::string> &functions, int &function_index,
                     std::string &function, float &score, float &weighted_score,
-                    float &score_offset);
+                    float &score_offset, int *decision = nullptr);
 
 /* FastaParser framing (fasta_parser.h:38-144, fasta_parser.cc:30-36) */
 std::vector<std::pair<std::string, std::string>> parse_fasta(const std::string &text);

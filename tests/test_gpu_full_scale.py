@@ -1,10 +1,12 @@
-"""Parity at BASELINE.json's full C2 size (100k x 300 aa vs the 1B-entry
-image bench.py measures: exactly 1e9 distinct keys, 85.4 GB file format /
-57 GB packed in HBM) through properties that do
-not need a full CPU run: idempotence, device path == host-buffer path ==
-24-byte layout, and every 100th sequence against the oracle on a host copy
-of the same image."""
+"""Parity at BASELINE.json's full C2 and C5 sizes (100k / 1M x 300 aa vs the
+1B-entry image bench.py measures: exactly 1e9 distinct keys, 85.4 GB file
+format / 57 GB packed in HBM): EVERY sequence's hits, calls, OTU tallies and
+find_best_call against the oracle on a host copy of the same image (want 15,
+compared as bits by oracle.diff_batch), over the reference slots and over the
+line index bench.py times (load 36); plus idempotence, device path ==
+host-buffer path == pool split == 24-byte layout."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -13,20 +15,24 @@ from close_kmers_amd import synth
 
 pytestmark = pytest.mark.gpu
 
+ALL = 15  # hits + calls + OTU tallies + find_best_call
 
-def _collect(gpu, ctx, want=3):
+
+def _collect(gpu, ctx, want=ALL):
     r = gpu.Result()
     gpu.check(gpu.lib().kgx_device_batch_collect(ctx.handle, want, ctypes.byref(r)), "collect")
-    b = gpu.BatchResult(r, want)
-    return {"hit_offsets": b.hit_offsets.copy(), "hits": b.hits.copy(),
-            "call_offsets": b.call_offsets.copy(), "calls": b.calls.copy()}
+    return gpu.BatchResult(r, want)
 
 
 def _same(a, b):
-    for k in ("hit_offsets", "call_offsets"):
-        assert np.array_equal(a[k], b[k]), k
-    assert np.array_equal(a["hits"].view(np.uint8), b["hits"].view(np.uint8))
-    assert np.array_equal(a["calls"].view(np.uint8), b["calls"].view(np.uint8))
+    """Byte-identical results (every output both carry)."""
+    for k in ("hit_offsets", "call_offsets", "otu_offsets"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    for k in ("hits", "calls", "otus", "best"):
+        x, y = getattr(a, k), getattr(b, k)
+        assert (x is None) == (y is None), k
+        if x is not None:
+            assert np.array_equal(x.view(np.uint8), y.view(np.uint8)), k
 
 
 @pytest.fixture(scope="module")
@@ -58,36 +64,38 @@ def _device_queries(gpu, ctx, spec, n, Ls, q0=0):
     return res, off
 
 
-def _oracle_sample(oracle_lib, table, res, off, idx):
-    sres = np.concatenate([res[int(off[i]):int(off[i + 1])] for i in idx])
-    soff = np.concatenate([[0], np.cumsum(np.diff(off)[idx])]).astype(np.uint64)
-    return oracle_lib.process_batch(table, sres, soff, want=3, n_threads=8)
+def _threads():
+    """The host CPUs the oracle may use (the box's cgroup share, not nproc)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 32))
 
 
-def _assert_sample(got_hits, got_hoff, got_calls, got_coff, want, idx):
-    got_h = np.concatenate([got_hits[int(got_hoff[i]):int(got_hoff[i + 1])] for i in idx])
-    got_c = np.concatenate([got_calls[int(got_coff[i]):int(got_coff[i + 1])] for i in idx])
-    for f in ("which_kmer", "otu_index", "avg_from_end", "function_index", "pos"):
-        assert np.array_equal(got_h[f], want.hits[f]), f
-    assert np.array_equal(got_h["function_wt"].view(np.uint32), want.hits["function_wt"].view(np.uint32))
-    for f in ("start", "end", "count", "function_index"):
-        assert np.array_equal(got_c[f], want.calls[f]), f
-    assert np.array_equal(got_c["weighted_hits"].view(np.uint32), want.calls["weighted_hits"].view(np.uint32))
+def _assert_oracle(oracle_lib, got, ref, what):
+    """Every sequence of got (device results, want 15) equals the oracle's."""
+    bad = oracle_lib.diff_batch(got, ref, ALL)
+    assert all(not v for v in bad.values()), (what, {k: (len(v), v[:5]) for k, v in bad.items() if v})
 
 
 def test_c5_pool_one_batch_of_1m(gpu, oracle_lib, bench_image):
     """C5 (BASELINE.json configs[4]): bench.py --strong's 1M x 300-aa batch
     through kgx_pool on 8 contexts (device 0 here; one per GPU on a node),
-    residue-balanced shards, concatenated in input order.  The whole output
-    is byte-identical to ten sequential 100k single-context passes, the
-    compact pool result expands to the same bytes, and every 1000th sequence
-    matches the oracle on a host copy of the image."""
+    residue-balanced shards, concatenated in input order.  Every sequence's
+    hits, calls, OTU tallies and best call equal the oracle's over a host copy
+    of the image, over the reference slots and over the line index; the
+    compact pool result expands to the same bytes, and ten sequential 100k
+    single-context passes give the same bytes."""
     spec, img = bench_image
     n, Ls, step = 1_000_000, 300, 100_000
     with gpu.Context(img) as ctx:
         res, off = _device_queries(gpu, ctx, spec, n, Ls)
         with gpu.Pool([img], n_ctx=8) as pool:
-            split = pool.process_batch(res, off, want=3)
+            split = pool.process_batch(res, off, want=ALL)
             assert len(split.hits) > 70_000_000
             cb = pool.process_batch_compact(res, off, want=3)
             assert cb.n_chunks >= 8 and not cb.materialized
@@ -107,11 +115,19 @@ def test_c5_pool_one_batch_of_1m(gpu, oracle_lib, bench_image):
                 ph["seq"] -= a
                 assert np.array_equal(ph.view(np.uint8), one.hits.view(np.uint8))
                 assert np.array_equal(split.calls[c0:c1].view(np.uint8), one.calls.view(np.uint8))
+                del one
     table = img.download()
-    idx = np.arange(0, n, 1000)
-    want = _oracle_sample(oracle_lib, table, res, off, idx)
+    ref = oracle_lib.process_batch(table, res, off, want=ALL, n_threads=_threads())
     del table
-    _assert_sample(split.hits, split.hit_offsets, split.calls, split.call_offsets, want, idx)
+    _assert_oracle(oracle_lib, split, ref, "C5 pool, reference slots")
+    del split
+    img.set_line_index(36)
+    try:
+        with gpu.Pool([img], n_ctx=8) as pool:
+            lined = pool.process_batch(res, off, want=ALL)
+        _assert_oracle(oracle_lib, lined, ref, "C5 pool, line index 36")
+    finally:
+        img.set_line_index(0)
 
 
 def test_c2_full_scale(gpu, oracle_lib, bench_image):
@@ -126,43 +142,40 @@ def test_c2_full_scale(gpu, oracle_lib, bench_image):
         gpu.check(L.kgx_synth_queries(ctx.handle, spec.n_keys, n, Ls, 0, 0, d_res, d_off), "queries")
         params = gpu.default_params()
 
-        def run():
-            gpu.check(L.kgx_run_device(ctx.handle, ctypes.byref(params), d_res, d_off, n, n * Ls, 3, None),
+        def run(want=ALL):
+            gpu.check(L.kgx_run_device(ctx.handle, ctypes.byref(params), d_res, d_off, n, n * Ls, want, None),
                       "run_device")
-            return _collect(gpu, ctx)
+            return _collect(gpu, ctx, want)
 
         r1 = run()
-        assert len(r1["hits"]) > 7_000_000 and len(r1["calls"]) > 50_000
+        assert len(r1.hits) > 7_000_000 and len(r1.calls) > 50_000
         _same(r1, run())  # idempotent
         res = np.empty(n * Ls, np.uint8)
         off = np.empty(n + 1, np.uint64)
         gpu.check(L.kgx_memcpy_d2h(res.ctypes.data, d_res, res.nbytes), "d2h")
         gpu.check(L.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
-        hb = ctx.process_batch(res, off, params, want=3)  # host-buffer path
-        _same(r1, {"hit_offsets": hb.hit_offsets, "hits": hb.hits, "call_offsets": hb.call_offsets,
-                   "calls": hb.calls})
+        _same(r1, ctx.process_batch(res, off, params, want=ALL))  # host-buffer path
         # C5's split on one device: the batch as 8 residue-balanced shards on 8
         # contexts (kgx_pool), concatenated in input order == one pass, byte for byte
-        one = ctx.process_batch(res, off, params, want=15)
         with gpu.Pool([img], n_ctx=8) as pool:
-            split = pool.process_batch(res, off, params, want=15)
-        for k in ("hit_offsets", "call_offsets", "otu_offsets"):
-            assert np.array_equal(getattr(split, k), getattr(one, k)), k
-        for k in ("hits", "calls", "otus", "best"):
-            assert np.array_equal(getattr(split, k).view(np.uint8), getattr(one, k).view(np.uint8)), k
-        del one, split
-        # every 100th sequence against the oracle on a host copy of the image
+            _same(r1, pool.process_batch(res, off, params, want=ALL))
+        # every sequence against the oracle on a host copy of the image
         table = img.download()
         keys_stored = int(np.count_nonzero(table["which_kmer"] <= 20 ** 8))
         assert keys_stored == 10 ** 9
-        idx = np.arange(0, n, 100)
-        want = _oracle_sample(oracle_lib, table, res, off, idx)
+        ref = oracle_lib.process_batch(table, res, off, want=ALL, n_threads=_threads())
         del table
-        _assert_sample(r1["hits"], r1["hit_offsets"], r1["calls"], r1["call_offsets"], want, idx)
-        # the line index (the bench's default, load 36) gives the same results
+        _assert_oracle(oracle_lib, r1, ref, "C2, reference slots")
+        # the line index (the bench's default, load 36): every sequence again
         img.set_line_index(36)
         assert img.line_count > 10 ** 9
-        _same(r1, run())
+        r2 = run()
+        _assert_oracle(oracle_lib, r2, ref, "C2, line index 36")
+        _same(r1, r2)
+        # the bench's want (11: hits + calls + best call) over the index
+        r3 = run(11)
+        bad = oracle_lib.diff_batch(r3, ref, 11)
+        assert all(not v for v in bad.values()), bad
         img.set_line_index(0)
         # the file's 24-byte layout gives the same results
         img.set_layout(gpu.Image.AOS24)

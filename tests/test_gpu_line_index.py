@@ -30,8 +30,14 @@ def _batch_from(rng, keys, n=60):
     return recs
 
 
+@pytest.mark.parametrize("filt", [0, 12])
 @pytest.mark.parametrize("shape", ["wrap", "dups_strays", "full"])
-def test_line_index_chain_shapes_all_variants(gpu, oracle_lib, shape):
+def test_line_index_chain_shapes_all_variants(gpu, oracle_lib, shape, filt):
+    """Every probe variant and tile size over the index at both loads; with a
+    presence filter (filt: 2^12 bits) too, which sends the probes to the
+    filtered per-bucket kernel over the index (home shift 2), the filter
+    built from the reference slots; and context option line_index 0 (the
+    reference slots while the image keeps its index)."""
     rng = np.random.default_rng({"wrap": 11, "dups_strays": 12, "full": 13}[shape])
     if shape == "wrap":
         table, keys = _chain_table(rng, 1001, 800, tail_frac=0.3)
@@ -45,6 +51,8 @@ def test_line_index_chain_shapes_all_variants(gpu, oracle_lib, shape):
     want = oracle_lib.process_batch(table, res, off, params=(2, 200, 0, 0))
     assert int(want.hit_offsets[-1]) > 0
     with gpu.Image.from_table(table) as img, gpu.Context(img) as ctx:
+        if filt:
+            img.set_filter(filt)
         for load in LOADS:
             img.set_line_index(load)
             assert img.line_count > 0
@@ -54,6 +62,9 @@ def test_line_index_chain_shapes_all_variants(gpu, oracle_lib, shape):
                     ctx.set_option("probe_j", probe_j)
                     got = ctx.process_batch(res, off, gpu.Params(2, 200, 0, 0))
                     assert_same(got, want, len(recs))
+            ctx.set_option("line_index", 0)
+            assert_same(ctx.process_batch(res, off, gpu.Params(2, 200, 0, 0)), want, len(recs))
+            ctx.set_option("line_index", 1)
         img.set_line_index(0)
         assert img.line_count == 0
         ctx.set_option("probe_variant", -1)

@@ -181,6 +181,40 @@ def test_svc_request_memory_host_and_device(svc_image, oracle_lib, monkeypatch):
             assert img.svc_stat("devmem") == 0
 
 
+def test_svc_stall_is_replaced_without_blocking(gpu, oracle_lib, monkeypatch):
+    """A request the device never answers (KGX_SVC_TEST_DROP: written but never
+    posted) times out (KGX_SVC_TIMEOUT_MS), the service turns broken, and the
+    facade's recovery -- kgx_svc_stop, then the batch path for that call --
+    returns promptly: the stop drains the workgroups with a bounded wait (no
+    runtime synchronisation under the service lock), the next call starts a
+    new service, and every answer equals the oracle's."""
+    spec, table = synthetic_table(20000)
+    seqs = _seqs(spec, 40, 91)
+    with abi.Image.from_table(table, device=0) as img, abi.Context(img) as ctx:
+        monkeypatch.setenv("KGX_SVC_TEST_DROP", "1")
+        monkeypatch.setenv("KGX_SVC_TIMEOUT_MS", "300")
+        t0 = time.time()
+        with pytest.raises(abi.KgxError) as e:
+            img.svc_call(seqs[0])
+        assert e.value.code == abi.KGX_EDEVICE and time.time() - t0 < 5
+        assert img.svc_stat("broken") == 1 and img.svc_stat("abandoned") == 1
+        with pytest.raises(abi.KgxError) as e:  # broken: turned away at once
+            img.svc_call(seqs[1])
+        assert e.value.code == abi.KGX_EBUSY
+        monkeypatch.delenv("KGX_SVC_TEST_DROP")
+        leaked = img.svc_stat("leaked")
+        t0 = time.time()
+        img.svc_stop()  # the facade's replacement (kguts_hip.cpp, process_aa_seq)
+        assert time.time() - t0 < 3 and img.svc_stat("leaked") == leaked
+        got = ctx.process_batch(np.frombuffer(seqs[0], np.uint8).copy(), np.array([0, len(seqs[0])], np.uint64),
+                                want=3)  # the batch path for the stalled call
+        _check(oracle_lib, table, seqs[0], (5, 200, 0, 0), got.hits, got.calls, "batch path")
+        for k, s in enumerate(seqs):  # a new service serves the rest
+            hits, calls = img.svc_call(s)
+            _check(oracle_lib, table, s, (5, 200, 0, 0), hits, calls, k)
+        assert img.svc_stat("broken") == 0
+
+
 def test_svc_threads_and_restarts_match_oracle(svc_image, oracle_lib):
     """16 threads at once over 32 slots, then 40 threads over 8 slots (calls
     turned away for want of a slot are counted and retried), with idle
