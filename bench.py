@@ -323,20 +323,36 @@ def pool_devices(dev: int, n_dev: int, world: int) -> list:
     return [dev] + [i for i in range(n_dev) if i != dev][:max(0, world - 1)]
 
 
-def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_permille):
-    """C5 (BASELINE.json configs[4]) as the reference would run it: one host
-    batch of n x Ls aa through kgx_pool over one image replica per device
-    (device-to-device copies of img0), residue-balanced shards, compact
-    results concatenated in input order (threadpool.cc:18-44,
-    lookup_request.cc:153).  Timed over contexts per device, pinned and
-    pageable input; checked against one context's pass over the batch."""
-    t0 = time.time()
-    images = [img0] + [img0.replicate(dv) for dv in devices[1:]]
-    t_rep = time.time() - t0
+GB = 1e9
+RANK_HBM = 8e9   # a rank's batches and worker contexts (C2), with room to spare
+POOL_HBM = 24e9  # the C5 legs per device: pool contexts (1M x 300 aa), family map, one-pass reference
+
+
+def image_bytes(n_keys: int, num_sigs: int, line_load: int) -> dict:
+    """HBM an image of the bench takes: the file's 24-B buckets while it is
+    built, its PACKED16 records, and the line index (stored keys x 64 / load
+    lines of 64 B)."""
+    lines = (n_keys * 64 + line_load - 1) // line_load if line_load else 0
+    return {"aos24": num_sigs * 24, "packed16": num_sigs * 16, "line_index": lines * 64}
+
+
+def hbm_check(abi, devices, need: float, what: str) -> None:
+    """Fail with a clear message when a device has less free HBM than need."""
+    for dv in devices:
+        free, total = abi.device_memory(dv)
+        if free < need:
+            raise SystemExit(f"device {dv}: {free / GB:.1f} GB of {total / GB:.1f} GB HBM free, but {what} needs "
+                             f"{need / GB:.1f} GB")
+
+
+def c5_batch(abi, L, img0, spec, n, Ls, x_permille):
+    """BASELINE.json configs[4]'s batch (C5: n x Ls aa), generated on img0's
+    device and copied into pinned host memory: (residues, offsets)."""
     c0 = abi.Context(img0)
+    dev = img0.device
     d_res, d_off = ctypes.c_void_p(), ctypes.c_void_p()
-    abi.check(L.kgx_device_alloc(devices[0], n * Ls, ctypes.byref(d_res)), "alloc")
-    abi.check(L.kgx_device_alloc(devices[0], (n + 1) * 8, ctypes.byref(d_off)), "alloc")
+    abi.check(L.kgx_device_alloc(dev, n * Ls, ctypes.byref(d_res)), "alloc")
+    abi.check(L.kgx_device_alloc(dev, (n + 1) * 8, ctypes.byref(d_off)), "alloc")
     abi.check(L.kgx_synth_queries(c0.handle, spec.n_keys, n, Ls, x_permille, 1 << 40, d_res, d_off), "queries")
     c0.synchronize()
     pin = abi.pinned_empty(n * Ls)
@@ -345,7 +361,22 @@ def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_perm
     abi.check(L.kgx_memcpy_d2h(off.ctypes.data, d_off, off.nbytes), "d2h")
     L.kgx_device_free(d_res)
     L.kgx_device_free(d_off)
+    c0.close()
+    return pin, off
+
+
+def pool_e2e_leg(abi, images, pin, off, params, want):
+    """C5 (BASELINE.json configs[4]) as the reference would run it: one host
+    batch through kgx_pool over one image replica per device (images: rank
+    0's image, then device-to-device copies of it), residue-balanced shards,
+    compact results concatenated in input order (threadpool.cc:18-44,
+    lookup_request.cc:153).  Timed over contexts per device, pinned and
+    pageable input; checked against one context's pass over the batch."""
+    devices = [im.device for im in images]
+    n = len(off) - 1
+    n_res = int(off[-1] - off[0])
     pageable = np.array(pin)
+    c0 = abi.Context(images[0])
     one = c0.process_batch_compact(pageable, off, params, want=want)
     one_off = (one.result.hit_offsets.copy(), one.result.call_offsets.copy(), one.result.calls.copy(),
                one.result.best.copy() if one.result.best is not None else None)
@@ -353,11 +384,13 @@ def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_perm
     starts = sorted(set([0, n - 500] + rng.integers(0, n - 500, 12).tolist()))
     one_hits = {a: one.expand(a, a + 500).tobytes() for a in starts}
     c0.close()
-    by, checks = {}, {}
+    by, checks, numa = {}, {}, None
     best_t, best_k = None, None
     for per_dev in (1, 2, 4, 8):
         n_ctx = per_dev * len(devices)
         with abi.Pool(images, n_ctx) as pool:
+            if numa is None:
+                numa = pool.numa_nodes()[:len(devices)]
             for name, src in (("pinned", pin), ("pageable", pageable)):
                 r = pool.process_batch_compact(src, off, params, want=want)  # warm
                 ts = []
@@ -375,20 +408,77 @@ def pool_e2e_leg(abi, L, synth, img0, spec, devices, params, want, n, Ls, x_perm
                       and (one_off[3] is None or rr.best.tobytes() == one_off[3].tobytes())
                       and all(r.expand(a, a + 500).tobytes() == one_hits[a] for a in starts))
                 checks[f"{name}_ctx{n_ctx}"] = bool(ok)
-    for im in images[1:]:
-        im.close()
     t_pg = min(v for k, v in by.items() if k.startswith("pageable")) / 1e3
-    out = {"value": n * Ls / best_t, "unit": "residues/s", "ms_per_batch": best_t * 1e3, "contexts": best_k,
-           "devices": devices, "value_pageable_input": n * Ls / t_pg, "ms_by_config": by,
+    out = {"value": n_res / best_t, "unit": "residues/s", "ms_per_batch": best_t * 1e3, "contexts": best_k,
+           "devices": devices, "numa_nodes": numa, "value_pageable_input": n_res / t_pg, "ms_by_config": by,
            "match_single_context": all(checks.values()), "checks": checks,
-           "hits": int(one_off[0][-1]), "replicate_s": round(t_rep, 2),
+           "hits": int(one_off[0][-1]),
            "note": "C5: one host batch through kgx_pool_process_batch_compact over one image replica per device "
                    "(hits as compact records + mask, calls, device best calls back over PCIe), contexts per device "
                    "swept; value: residues in pinned memory (read by DMA, no staging copy); checked against one "
                    "context's pass (offsets, calls, best calls, and the expanded hits of 14 slices of 500 "
-                   "sequences, shard cuts included)"}
+                   "sequences, shard cuts included); numa_nodes: the node each device's first pool thread is "
+                   "bound to (-1 unbound)"}
     log(f"[bench] pool_e2e {out['value']:.3e} residues/s over {len(devices)} device(s) ({best_k} contexts, "
         f"{best_t * 1e3:.1f} ms), pageable {out['value_pageable_input']:.3e}; checks "
+        f"{'ok' if out['match_single_context'] else checks}; numa {numa}; {by}")
+    return out
+
+
+def pool_lookup_leg(abi, synth, images, spec, pin, off, params, n_fam=100000):
+    """/lookup in family mode with find_best_match (lookup_request.cc:153-210,
+    446-482, the north_star handler) over C5's batch and every device of the
+    pool: kgx_pool_lookup with one family map per device (kgx_kmap on each
+    replica's device), rows + offsets + best calls back.  Timed at 4 and 8
+    contexts per device, pinned and pageable input; the whole batch's rows,
+    offsets and best calls are checked byte for byte against one context's
+    one-pass run + kgx_kmap_rollup."""
+    devices = [im.device for im in images]
+    n = len(off) - 1
+    n_res = int(off[-1] - off[0])
+    want = abi.WANT_BEST
+    t0 = time.time()
+    fams = [family_kmap(abi, synth, spec, dv, n_fam)[0] for dv in devices]
+    t_fam = time.time() - t0
+    pageable = np.array(pin)
+    with abi.Context(images[0]) as c1:
+        c1.set_option("host_chunks", 1)  # the rollup reads the pass's hits on the device
+        one = c1.process_batch(pageable, off, params, want=want)
+        woff, wrows = fams[0].rollup(c1, abi.ROLLUP_FAMILY)
+        wbest = one.best.copy()
+        del one
+    by, checks = {}, {}
+    best_t, best_k = None, None
+    for per_dev in (4, 8):
+        n_ctx = per_dev * len(devices)
+        with abi.Pool(images, n_ctx) as pool:
+            for name, src in (("pinned", pin), ("pageable", pageable)):
+                r, roff, rows = pool.lookup(fams, src, off, params, want=want, copy=False)  # warm
+                ts = []
+                for _ in range(5):
+                    t1 = time.perf_counter()
+                    r, roff, rows = pool.lookup(fams, src, off, params, want=want, copy=False)
+                    ts.append(time.perf_counter() - t1)
+                t = float(np.median(ts))
+                by[f"{name}_ctx{n_ctx}"] = t * 1e3
+                if name == "pinned" and (best_t is None or t < best_t):
+                    best_t, best_k = t, n_ctx
+                checks[f"{name}_ctx{n_ctx}"] = bool(np.array_equal(roff, woff) and rows.tobytes() == wrows.tobytes()
+                                                    and r.best.tobytes() == wbest.tobytes())
+    for f in fams:
+        f.close()
+    t_pg = min(v for k, v in by.items() if k.startswith("pageable")) / 1e3
+    out = {"value": n_res / best_t, "unit": "residues/s", "ms_per_batch": best_t * 1e3, "contexts": best_k,
+           "devices": devices, "value_pageable_input": n_res / t_pg, "ms_by_config": by,
+           "rollup_rows": int(woff[-1]), "families": n_fam, "family_db_build_s": round(t_fam, 2),
+           "match_single_context": all(checks.values()), "checks": checks,
+           "check": f"all {n} sequences' rollup offsets, rows and best calls == one context's one-pass run + "
+                    "kgx_kmap_rollup",
+           "note": "C5 /lookup (family mode + find_best_match, the north_star handler) through kgx_pool_lookup "
+                   "over one image replica and one family map per device: residues up, probe, score, device "
+                   "find_best_call and on_hit rollups on each device, only rows, offsets and best calls back"}
+    log(f"[bench] pool_lookup {out['value']:.3e} residues/s over {len(devices)} device(s) ({best_k} contexts, "
+        f"{best_t * 1e3:.2f} ms), pageable {out['value_pageable_input']:.3e}; checks "
         f"{'ok' if out['match_single_context'] else checks}; {by}")
     return out
 
@@ -416,6 +506,8 @@ def main():
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-lookup", action="store_true", help="skip the host_path_lookup leg")
     ap.add_argument("--no-pool", action="store_true", help="skip the pool_e2e leg (C5 through kgx_pool)")
+    ap.add_argument("--no-pool-lookup", action="store_true",
+                    help="skip the pool_lookup leg (C5 /lookup through kgx_pool_lookup over the devices)")
     ap.add_argument("--families", type=int, default=100000, help="family DB size of the host_path_lookup leg")
     ap.add_argument("--ab", default="", help='interleaved A/B of a ctx option, e.g. "probe_j=4,5,8"')
     ap.add_argument("--ab-rounds", type=int, default=10)
@@ -487,6 +579,14 @@ def main():
     n_keys = int(args.n_keys)
     spec = synth.ImageSpec(n_keys, args.num_sigs or None)
 
+    # HBM budget of this rank's image before building it: the 24-B build, then
+    # PACKED16 and the line index beside it, plus the batches and contexts
+    img_bytes = image_bytes(n_keys, spec.num_sigs, args.line_index if args.image_layout == "packed" else 0)
+    peak = max(img_bytes["aos24"] + (img_bytes["packed16"] if args.image_layout == "packed" else 0),
+               img_bytes["packed16"] + img_bytes["line_index"]) + RANK_HBM
+    hbm_check(abi, [dev], peak, f"rank {d.rank}'s image (built as {img_bytes['aos24'] / GB:.1f} GB of 24-B "
+                                f"buckets, kept as {img_bytes['packed16'] / GB:.1f} GB PACKED16 + "
+                                f"{img_bytes['line_index'] / GB:.1f} GB line index) and its batches")
     t0 = time.time()
     # n_keys distinct keys stored (the generator's stream
     # runs past n_keys entries until that many distinct keys are in)
@@ -715,6 +815,29 @@ def main():
         abi.check(L.kgx_memcpy_d2h(res0.ctypes.data, d_res, res0.nbytes), "d2h")
         abi.check(L.kgx_memcpy_d2h(off0.ctypes.data, d_off, off0.nbytes), "d2h")
 
+    released = []
+
+    def release():
+        """This rank's HBM back: events, batches, worker contexts, image."""
+        if released:
+            return
+        released.append(True)
+        for e in ev:
+            L.kgx_event_destroy(e)
+        for d_res, d_off in batches:
+            L.kgx_device_free(d_res)
+            L.kgx_device_free(d_off)
+        for c in ctxs:
+            c.close()
+        img.close()
+
+    # the other ranks are done with the GPU: they free their HBM before rank
+    # 0's C5 legs put image replicas on their devices
+    if d.world > 1:
+        if d.rank != 0:
+            release()
+        d.barrier()
+
     # PCIe-inclusive rate of the host-buffer boundary (kgx_process_batch:
     # H2D residues, plan/probe/score, gather, D2H hits + calls) -- reported
     # beside `value`, never as it
@@ -786,12 +909,27 @@ def main():
         abi.check(L.kgx_memcpy_d2h(off_h.ctypes.data, d_off, off_h.nbytes), "d2h")
         host_path_lookup = host_path_lookup_leg(abi, synth, img, spec, dev, res_h, off_h, params, args.families)
 
-    pool_e2e = None
-    if d.rank == 0 and not args.no_pool:
-        # one replica per rank's device: the N-GPU run measures C5 over N devices
+    pool_e2e = pool_lookup = None
+    if d.rank == 0 and not (args.no_pool and args.no_pool_lookup):
+        # one replica per rank's device (the other ranks released theirs
+        # above): the N-GPU run measures C5 over N devices
         pdevs = pool_devices(dev, n_dev, d.world)
-        pool_e2e = pool_e2e_leg(abi, L, synth, img, spec, pdevs, params, want, args.strong_seq, Ls,
-                                args.x_permille)
+        rep = img_bytes["packed16"] if img.layout == abi.Image.PACKED16 else img_bytes["aos24"]
+        hbm_check(abi, pdevs[1:], rep + POOL_HBM, f"an image replica ({rep / GB:.1f} GB) and the C5 pool's "
+                                                  f"buffers ({POOL_HBM / GB:.0f} GB)")
+        hbm_check(abi, pdevs[:1], POOL_HBM, f"the C5 pool's buffers ({POOL_HBM / GB:.0f} GB)")
+        t0 = time.time()
+        images = [img] + [img.replicate(dv) for dv in pdevs[1:]]
+        t_rep = time.time() - t0
+        pin, poff = c5_batch(abi, L, img, spec, args.strong_seq, Ls, args.x_permille)
+        if not args.no_pool:
+            pool_e2e = pool_e2e_leg(abi, images, pin, poff, params, want)
+            pool_e2e["replicate_s"] = round(t_rep, 2)
+        if not args.no_pool_lookup:
+            pool_lookup = pool_lookup_leg(abi, synth, images, spec, pin, poff, params, args.families)
+        for im in images[1:]:
+            im.close()
+        del pin
 
     ceiling = None
     if d.rank == 0 and not args.no_microbench:
@@ -845,14 +983,7 @@ def main():
                 f"(affinity {aff} CPUs, cgroup quota {quota}), P = {cpu['pbar']:.4f}")
         del table
 
-    for e in ev:
-        L.kgx_event_destroy(e)
-    for d_res, d_off in batches:
-        L.kgx_device_free(d_res)
-        L.kgx_device_free(d_off)
-    for c in ctxs:
-        c.close()
-    img.close()
+    release()
 
     if d.rank == 0:
         windows_per_launch = n * max(0, Ls - 8)  # x_permille = 0: every window is probed
@@ -968,6 +1099,7 @@ def main():
             "host_path": host_path,
             "host_path_lookup": host_path_lookup,
             "pool_e2e": pool_e2e,
+            "pool_lookup": pool_lookup,
         }
         print(json.dumps(line), flush=True)
     d.close()

@@ -19,6 +19,7 @@ KGX_OK = 0
 ERRORS = {-1: "EINVAL", -2: "EIO", -3: "EFORMAT", -4: "ENOMEM", -5: "EDEVICE", -6: "ERANGE",
           -7: "EFULL", -8: "EBUSY"}
 KGX_EBUSY = -8
+KGX_EDEVICE = -5
 WANT_HITS, WANT_CALLS, WANT_OTU, WANT_BEST = 1, 2, 4, 8
 HIT_IN_RUN, HIT_OTU = 1, 2
 
@@ -257,6 +258,11 @@ SIGNATURES = {
     "kgx_pool_ctx": (_P, [_P, _U32]),
     "kgx_pool_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
     "kgx_shard_cuts": (_INT, [_P, _U32, _U32, _P]),
+    "kgx_pool_numa_node": (_INT, [_P, _U32]),
+    "kgx_pool_map_select": (_INT, [_P, _U32, _P, _U32, _P]),
+    "kgx_device_numa_node": (_INT, [_INT]),
+    "kgx_numa_node_cpus": (_INT, [_INT, _P, _U32]),
+    "kgx_device_memory": (_INT, [_INT, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "kgx_process_batch_compact": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32,
                                          ctypes.POINTER(CompactResult)]),
     "kgx_pool_process_batch_compact": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32,
@@ -802,6 +808,31 @@ def shard_cuts(offsets, n_shards: int) -> np.ndarray:
     return cuts
 
 
+def pool_map_select(ctx_devices, map_devices) -> np.ndarray:
+    """kgx_pool_map_select: for each context device the index of its map."""
+    c = np.ascontiguousarray(ctx_devices, np.int32)
+    m = np.ascontiguousarray(map_devices, np.int32)
+    out = np.zeros(max(len(c), 1), np.int32)
+    check(lib().kgx_pool_map_select(c.ctypes.data, len(c), m.ctypes.data, len(m), out.ctypes.data),
+          "kgx_pool_map_select")
+    return out[:len(c)]
+
+
+def numa_node_cpus(node: int) -> list[int]:
+    """The CPUs of NUMA node `node` this process may run on (no device needed)."""
+    n = lib().kgx_numa_node_cpus(node, None, 0)
+    out = np.zeros(max(n, 1), np.uint32)
+    n = lib().kgx_numa_node_cpus(node, out.ctypes.data, len(out))
+    return out[:n].tolist()
+
+
+def device_memory(device: int) -> tuple[int, int]:
+    """(free, total) HBM bytes of a device."""
+    f, t = _U64(), _U64()
+    check(lib().kgx_device_memory(device, ctypes.byref(f), ctypes.byref(t)), "kgx_device_memory")
+    return f.value, t.value
+
+
 def pinned_empty(n: int, dtype=np.uint8) -> np.ndarray:
     """An uninitialised array in pinned, device-mapped host memory
     (kgx_host_alloc), freed with the last reference to it.  Residues passed
@@ -830,6 +861,10 @@ class Pool:
     @property
     def size(self) -> int:
         return lib().kgx_pool_size(self.handle)
+
+    def numa_nodes(self) -> list[int]:
+        """The NUMA node each context's host thread is bound to (-1: unbound)."""
+        return [lib().kgx_pool_numa_node(self.handle, i) for i in range(self.size)]
 
     def set_option(self, name: str, value: int) -> None:
         """kgx_ctx_set_option on every context of the pool."""

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -26,6 +27,7 @@
 
 #include <cstdio>
 
+#include <pthread.h>
 #include <sched.h>
 
 #include "kgx_rt.h"
@@ -55,8 +57,65 @@ unsigned kgx::host_cpu_budget()
     return budget;
 }
 
+namespace {
+
+/* "0-31,128-159" -> the CPUs it names, in set (false: unreadable) */
+bool parse_cpulist(const char *text, cpu_set_t &set)
+{
+    CPU_ZERO(&set);
+    const char *p = text;
+    bool any = false;
+    while (*p) {
+        while (*p == ',' || *p == ' ' || *p == '\n')
+            p++;
+        if (!*p)
+            break;
+        char *end = nullptr;
+        const long a = std::strtol(p, &end, 10);
+        if (end == p || a < 0)
+            return false;
+        long b = a;
+        p = end;
+        if (*p == '-') {
+            b = std::strtol(p + 1, &end, 10);
+            if (end == p + 1 || b < a)
+                return false;
+            p = end;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; c++)
+            CPU_SET((int)c, &set);
+        any = true;
+    }
+    return any;
+}
+
+/* the CPUs of node that this process may use (empty: none, or no such node) */
+bool node_cpus(int node, cpu_set_t &out)
+{
+    CPU_ZERO(&out);
+    if (node < 0)
+        return false;
+    char path[96];
+    std::snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE *f = std::fopen(path, "r");
+    if (!f)
+        return false;
+    char buf[4096] = {0};
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    cpu_set_t nodeset, mine;
+    if (!parse_cpulist(buf, nodeset) || sched_getaffinity(0, sizeof mine, &mine) != 0)
+        return false;
+    CPU_AND(&out, &nodeset, &mine);
+    return CPU_COUNT(&out) > 0;
+}
+
+}  // namespace
+
 struct kgx_pool {
     std::vector<kgx_ctx *> ctxs;
+    std::vector<int> numa; /* per context: the node its thread is bound to, -1 unbound */
     /* one persistent host thread per context: job generation counter */
     std::vector<std::thread> threads;
     std::mutex mu;
@@ -127,6 +186,13 @@ struct kgx_pool {
 
     void worker(uint32_t i)
     {
+        /* numa.cc:13-42: the worker on its device's node, before it allocates
+         * (pinned staging lands on the node of the thread that first touches it) */
+        if (numa[i] >= 0) {
+            cpu_set_t set;
+            if (!node_cpus(numa[i], set) || pthread_setaffinity_np(pthread_self(), sizeof set, &set) != 0)
+                numa[i] = -1;
+        }
         uint64_t seen = 0;
         for (;;) {
             std::function<void(uint32_t)> fn;
@@ -251,9 +317,91 @@ int kgx_pool_create(kgx_image *const *images, uint32_t n_images, uint32_t n_ctx,
         p->per_device = (uint32_t)std::max(1L, std::strtol(e, nullptr, 10));
     if (const char *e = std::getenv("KGX_POOL_EXPAND_THREADS"))
         p->expand_threads = (unsigned)std::min(256L, std::max(1L, std::strtol(e, nullptr, 10)));
+    /* each context's NUMA node, worked out here (the HIP call) and bound
+     * by its thread */
+    const char *ne = std::getenv("KGX_POOL_NUMA");
+    const bool bind = !ne || std::atoi(ne) != 0;
+    p->numa.assign(n_ctx, -1);
+    for (uint32_t i = 0; i < n_ctx && bind; i++) {
+        cpu_set_t set;
+        const int node = kgx_device_numa_node(kgx_image_device(p->ctxs[i]->img));
+        if (node_cpus(node, set))
+            p->numa[i] = node;
+    }
     for (uint32_t i = 0; i < n_ctx; i++)
         p->threads.emplace_back([p, i] { p->worker(i); });
+    /* the binding is read back only after the threads have started */
+    p->run(n_ctx, [](uint32_t) {});
     *out = p;
+    return KGX_OK;
+}
+
+int kgx_pool_map_select(const int32_t *ctx_device, uint32_t n_ctx, const int32_t *map_device, uint32_t n_maps,
+                        int32_t *pick)
+{
+    if (n_ctx && (!ctx_device || !pick || (n_maps && !map_device)))
+        return fail(KGX_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n_ctx; i++) {
+        pick[i] = -1;
+        for (uint32_t j = 0; j < n_maps && pick[i] < 0; j++)
+            if (map_device[j] >= 0 && map_device[j] == ctx_device[i])
+                pick[i] = (int32_t)j;
+        if (pick[i] < 0)
+            return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(ctx_device[i]));
+    }
+    return KGX_OK;
+}
+
+int kgx_pool_numa_node(const kgx_pool *p, uint32_t i)
+{
+    return p && i < p->numa.size() ? p->numa[i] : -1;
+}
+
+int kgx_device_numa_node(int device)
+{
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (char *q = bus; *q; q++)
+        *q = (char)std::tolower((unsigned char)*q);
+    char path[160];
+    std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+    FILE *f = std::fopen(path, "r");
+    if (!f)
+        return -1;
+    int node = -1;
+    if (std::fscanf(f, "%d", &node) != 1)
+        node = -1;
+    std::fclose(f);
+    return node;
+}
+
+int kgx_numa_node_cpus(int node, uint32_t *cpus, uint32_t cap)
+{
+    cpu_set_t set;
+    if (!node_cpus(node, set))
+        return 0;
+    uint32_t k = 0;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &set)) {
+            if (cpus && k < cap)
+                cpus[k] = (uint32_t)c;
+            k++;
+        }
+    return (int)k;
+}
+
+int kgx_device_memory(int device, uint64_t *free_bytes, uint64_t *total_bytes)
+{
+    if (!free_bytes || !total_bytes)
+        return fail(KGX_EINVAL, "null argument");
+    HIP_TRY(hipSetDevice(device));
+    size_t f = 0, t = 0;
+    HIP_TRY(hipMemGetInfo(&f, &t));
+    *free_bytes = f;
+    *total_bytes = t;
     return KGX_OK;
 }
 
@@ -505,13 +653,17 @@ int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mod
     const std::vector<uint32_t> run = p->runners(2 * p->per_device);
     const uint32_t K = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)run.size(), n_seq));
     std::vector<kgx_kmap *> mine(K, nullptr);
-    for (uint32_t i = 0; i < K; i++) {
-        const int dev = kgx_image_device(p->ctxs[run[i]]->img);
-        for (uint32_t j = 0; j < n_maps && !mine[i]; j++)
-            if (maps[j] && kgx_kmap_device(maps[j]) == dev)
-                mine[i] = maps[j];
-        if (!mine[i])
-            return fail(KGX_EINVAL, "pool lookup: no map on device " + std::to_string(dev));
+    {
+        std::vector<int32_t> cdev(K), mdev(n_maps), pick(K);
+        for (uint32_t i = 0; i < K; i++)
+            cdev[i] = kgx_image_device(p->ctxs[run[i]]->img);
+        for (uint32_t j = 0; j < n_maps; j++)
+            mdev[j] = maps[j] ? kgx_kmap_device(maps[j]) : -1;
+        int rc = kgx_pool_map_select(cdev.data(), K, mdev.data(), n_maps, pick.data());
+        if (rc)
+            return rc;
+        for (uint32_t i = 0; i < K; i++)
+            mine[i] = maps[pick[i]];
     }
     /* residue shares: a device's first and last shards half the others'.
      * Its pipeline fills with the first shard's upload and drains with the

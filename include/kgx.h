@@ -601,6 +601,31 @@ int kgx_pool_process_batch(kgx_pool *pool, const kgx_params *params, const char 
 int kgx_pool_process_batch_compact(kgx_pool *pool, const kgx_params *params, const char *residues,
                                    const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
                                    kgx_compact_result *out);
+/* kgx_pool_lookup's map for each running context: the first of the maps
+ * whose device (kgx_kmap_device; -1 for a missing map) is the context's --
+ * pick[i] indexes map_device; KGX_EINVAL when a context's device has none.
+ * Host only (no device needed). */
+int kgx_pool_map_select(const int32_t *ctx_device, uint32_t n_ctx, const int32_t *map_device, uint32_t n_maps,
+                        int32_t *pick);
+/* NUMA placement (the reference binds each worker's thread and memory to a
+ * node, numa.cc:13-42): every pool context's host thread is bound at creation
+ * to the CPUs of its device's NUMA node that the process may use (its affinity
+ * mask), so that the pinned staging it grows and the copies into it stay on
+ * the device's socket (pinned host memory is placed by first touch of the
+ * allocating thread's node).  KGX_POOL_NUMA=0 leaves the threads unbound.
+ * kgx_pool_numa_node: the node context i's thread is bound to, -1 when it is
+ * not (unknown node, no usable CPU of it, or binding off). */
+int kgx_pool_numa_node(const kgx_pool *pool, uint32_t i);
+/* the NUMA node of a device: /sys/bus/pci/devices/<bus id>/numa_node of its
+ * PCI function (-1: unknown or no NUMA information) */
+int kgx_device_numa_node(int device);
+/* the CPUs of NUMA node `node` that this process may run on (its affinity
+ * mask and the node's cpulist, /sys/devices/system/node/node<N>/cpulist):
+ * their count, and the first cap of them in cpus (may be NULL).  Needs no
+ * device. */
+int kgx_numa_node_cpus(int node, uint32_t *cpus, uint32_t cap);
+/* free and total HBM of a device (hipMemGetInfo) */
+int kgx_device_memory(int device, uint64_t *free_bytes, uint64_t *total_bytes);
 /* cut points of n_shards contiguous residue-balanced shards: shard i is
  * sequences [cuts[i], cuts[i+1]), cuts[0] = 0, cuts[n_shards] = n_seq; cut i
  * is the first sequence starting at or after residue (total * i / n_shards)

@@ -108,3 +108,41 @@ def test_synthetic_stream_cut_for_distinct_keys():
         m = spec.entries_for_distinct(nd)
         assert len(synth.ImageSpec(5000, 101533, n_entries=m).unique_entries()[0]) == nd
         assert len(synth.ImageSpec(5000, 101533, n_entries=m - 1).unique_entries()[0]) == nd - 1
+
+
+def test_pool_map_select_more_than_one_map(kgx):
+    """kgx_pool_lookup's map per context (kgx_pool.cpp): with several maps,
+    each running context takes the first map on its own device, whatever the
+    maps' order; missing maps (-1) are skipped; a device with no map fails."""
+    ctx = [0, 0, 1, 1, 2, 2, 3, 3]
+    assert kgx.pool_map_select(ctx, [3, 2, 1, 0]).tolist() == [3, 3, 2, 2, 1, 1, 0, 0]
+    assert kgx.pool_map_select(ctx, [0, 1, 2, 3]).tolist() == [0, 0, 1, 1, 2, 2, 3, 3]
+    # duplicates: the first one on the device wins; unrelated devices are ignored
+    assert kgx.pool_map_select([1, 0], [5, 1, -1, 0, 1, 0]).tolist() == [1, 3]
+    assert kgx.pool_map_select([], [0]).tolist() == []
+    with pytest.raises(kgx.KgxError) as e:
+        kgx.pool_map_select([0, 4], [0, 1, 2, 3])
+    assert e.value.code == -1 and "device 4" in kgx.last_error()
+
+
+def test_numa_node_cpus(kgx):
+    """kgx_numa_node_cpus (the pool threads' NUMA binding, numa.cc:13-42):
+    a node's CPUs are the node's cpulist within this process's affinity."""
+    aff = os.sched_getaffinity(0)
+    assert kgx.numa_node_cpus(-1) == [] and kgx.numa_node_cpus(100000) == []
+    base = "/sys/devices/system/node"
+    nodes = sorted(int(d[4:]) for d in os.listdir(base) if d.startswith("node") and d[4:].isdigit()) \
+        if os.path.isdir(base) else []
+    seen = set()
+    for nd in nodes:
+        cpus = kgx.numa_node_cpus(nd)
+        text = open(f"{base}/node{nd}/cpulist").read().strip()
+        listed = set()
+        for part in filter(None, text.split(",")):
+            a, _, b = part.partition("-")
+            listed.update(range(int(a), int(b or a) + 1))
+        assert set(cpus) == listed & aff, nd
+        assert not (set(cpus) & seen)
+        seen.update(cpus)
+    if nodes:
+        assert seen == aff & set().union(*[set(kgx.numa_node_cpus(nd)) for nd in nodes])
