@@ -530,6 +530,9 @@ def main():
                     help="rounds of the in-process line-index A/B (option line_index 0 / 1 over the same "
                          "batches, interleaved; 0 = skip)")
     ap.add_argument("--ab-steps", type=int, default=40, help="steps per A/B sample")
+    ap.add_argument("--pipe-ab", default="",
+                    help='interleaved A/B of a context option over pipelined steps, e.g. "probe_nt=0,1" '
+                         '(the first value stays set afterwards)')
     ap.add_argument("--pool-devices", type=int, default=0,
                     help="N > 0: one process, the C5 batch through kgx_pool over N image replicas (devices "
                          "i %% visible), checked byte for byte against one context; prints its own line")
@@ -755,18 +758,17 @@ def main():
         f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
         f"probe {np.mean(probe_ms):.3f} ms")
 
-    # the line index, settled in this process: the same batches and contexts,
-    # option line_index 0 (probes over the reference slots) and 1 (the index)
-    # alternating, each sample a run of --ab-steps steps as timed above, plus
-    # one event-timed probe; rounds interleaved so drift hits both alike
-    line_ab = None
-    if line_lines and args.line_index_ab > 0:
-        samples = {v: {"step": [], "probe": []} for v in (0, 1)}
+    def pipelined_ab(name, values, rounds, restore):
+        """Interleaved A/B of a context option over the timed loop's shape:
+        the same batches and worker contexts, each sample a run of
+        --ab-steps pipelined steps (wall clock) plus one event-timed probe,
+        the values' order alternating by round so drift hits all alike."""
+        samples = {v: {"step": [], "probe": []} for v in values}
         k = 0
-        for r in range(args.line_index_ab):
-            for v in ((0, 1) if r % 2 == 0 else (1, 0)):
+        for r in range(rounds):
+            for v in (values if r % 2 == 0 else values[::-1]):
                 for c in ctxs:
-                    c.set_option("line_index", v)
+                    c.set_option(name, v)
                 for i in range(len(ctxs)):  # settle the rotation
                     step(None, ctxs[i % len(ctxs)], k)
                     k += 1
@@ -786,20 +788,34 @@ def main():
                 score_ms.pop()
                 samples[v]["probe"].append(pm[0])
         for c in ctxs:
-            c.set_option("line_index", 1)
-        med = {v: {"median_step_ms": float(np.median(samples[v]["step"])),
-                   "median_probe_ms": float(np.median(samples[v]["probe"])),
-                   "step_ms": [round(x, 4) for x in samples[v]["step"]],
-                   "probe_ms": [round(x, 4) for x in samples[v]["probe"]]} for v in (0, 1)}
-        gain = med[0]["median_step_ms"] / med[1]["median_step_ms"] - 1.0
+            c.set_option(name, restore)
+        return {str(v): {"median_step_ms": float(np.median(samples[v]["step"])),
+                         "median_probe_ms": float(np.median(samples[v]["probe"])),
+                         "step_ms": [round(x, 4) for x in samples[v]["step"]],
+                         "probe_ms": [round(x, 4) for x in samples[v]["probe"]]} for v in values}
+
+    # the line index, settled in this process: option line_index 0 (probes
+    # over the reference slots) and 1 (the index) on the same batches
+    line_ab = None
+    if line_lines and args.line_index_ab > 0:
+        med = pipelined_ab("line_index", [0, 1], args.line_index_ab, 1)
+        gain = med["0"]["median_step_ms"] / med["1"]["median_step_ms"] - 1.0
         line_ab = {"rounds": args.line_index_ab, "steps_per_sample": args.ab_steps, "load": args.line_index,
-                   "without_index": med[0], "with_index": med[1],
+                   "without_index": med["0"], "with_index": med["1"],
                    "step_gain": gain,
                    "note": "one process, same batches and worker contexts; context option line_index 0 = probes "
                            "over the reference slots, 1 = over the line index; step_gain = without / with - 1"}
-        log(f"[bench] line index A/B ({args.line_index_ab} rounds): step {med[0]['median_step_ms']:.4f} ms without, "
-            f"{med[1]['median_step_ms']:.4f} with ({gain * 100:+.1f}%); probe {med[0]['median_probe_ms']:.4f} / "
-            f"{med[1]['median_probe_ms']:.4f} ms")
+        log(f"[bench] line index A/B ({args.line_index_ab} rounds): step {med['0']['median_step_ms']:.4f} ms "
+            f"without, {med['1']['median_step_ms']:.4f} with ({gain * 100:+.1f}%); probe "
+            f"{med['0']['median_probe_ms']:.4f} / {med['1']['median_probe_ms']:.4f} ms")
+    pipe_ab = None
+    if args.pipe_ab:
+        name, vals = args.pipe_ab.split("=")
+        values = [int(x) for x in vals.split(",")]
+        pipe_ab = {"option": name, **pipelined_ab(name, values, args.ab_rounds, values[0])}
+        log(f"[bench] pipelined A/B of {name}: " + ", ".join(
+            f"{v}: step {pipe_ab[str(v)]['median_step_ms']:.4f} probe {pipe_ab[str(v)]['median_probe_ms']:.4f} ms"
+            for v in values))
 
     # the timed configuration's results of batch 0, for the full-batch check
     # against the oracle below (rank 0)
@@ -1096,6 +1112,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "line_index_ab": line_ab,
+            "pipe_ab": pipe_ab,
             "host_path": host_path,
             "host_path_lookup": host_path_lookup,
             "pool_e2e": pool_e2e,

@@ -232,6 +232,8 @@ SIGNATURES = {
     "kgx_kmap_lookup": (_INT, [_P, _P, _U64, _P, _P, _U64]),
     "kgx_kmap_rollup": (_INT, [_P, _P, _INT, ctypes.POINTER(RollupResult)]),
     "kgx_kmap_device": (_INT, [_P]),
+    "kgx_lookup": (_INT, [_P, _P, _INT, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result),
+                          ctypes.POINTER(RollupResult)]),
     "kgx_pool_lookup": (_INT, [_P, _PP, _U32, _INT, ctypes.POINTER(Params), _P, _P, _U32, _U32,
                                ctypes.POINTER(Result), ctypes.POINTER(RollupResult)]),
     "kgx_matrix_create": (_INT, [_P, _PP]),
@@ -579,6 +581,18 @@ class Context:
                                               offsets.ctypes.data, len(offsets) - 1, want, ctypes.byref(cr)),
               "kgx_process_batch_compact")
         return CompactBatch(cr, residues, offsets, want)
+
+    def lookup(self, kmap: "Kmap", residues, offsets, params: Params | dict | None = None, want: int = WANT_BEST,
+               mode: int = 1):
+        """kgx_lookup: the pass and the rollup over kmap with one host wait:
+        (BatchResult without hits, rollup offsets, rollup rows)."""
+        residues, offsets, params = _batch_args(residues, offsets, params)
+        r, ru = Result(), RollupResult()
+        check(lib().kgx_lookup(self.handle, kmap.handle, mode, ctypes.byref(params),
+                               residues.ctypes.data if residues.size else None, offsets.ctypes.data,
+                               len(offsets) - 1, want, ctypes.byref(r), ctypes.byref(ru)), "kgx_lookup")
+        off = _view(ru.offsets, ru.n_seq + 1, np.uint64)
+        return BatchResult(r, want), off, _view(ru.rows, int(off[-1]) if len(off) else 0, ROLLUP_DTYPE)
 
     def stat(self, name: str) -> int:
         v = ctypes.c_int64()

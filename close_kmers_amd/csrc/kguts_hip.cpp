@@ -1245,27 +1245,47 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
      * per sequence comes back, not the calls; the hits stay on the device,
      * where on_hit's rollups run (kgx_kmap_rollup) */
     const uint64_t g0 = now_ns(); /* gpu stage: the pass and the rollups */
-    int rc = kgx_process_batch(kg.ctx(), &p, fw.res, fw.off + w0, n, want_calls ? KGX_WANT_BEST : 0u, &r);
-    stage_stats().gpu_passes++;
-    if (rc)
-        throw_last(rc, "kgx_process_batch");
     /* on_hit (lookup_request.cc:446-482) over kmer_to_family_id_ or kmer_to_id_ */
     kgx_kmap *map = family_mode_ ? mapping_->kmer_to_family_id() : mapping_->kmer_to_id();
+    const int mode = family_mode_ ? KGX_ROLLUP_FAMILY : KGX_ROLLUP_PEG;
+    const uint32_t want = want_calls ? KGX_WANT_BEST : 0u;
     kgx_rollup_result ru;
-    rc = kgx_kmap_rollup(map, kg.ctx(), family_mode_ ? KGX_ROLLUP_FAMILY : KGX_ROLLUP_PEG, &ru);
-    if (rc)
-        throw_last(rc, "kgx_kmap_rollup");
+    /* the pass and the rollup enqueued together, one host wait (kgx_lookup),
+     * when the map is on the worker's device; KGX_LOOKUP_ONE_WAIT=0: the pass
+     * (the small-batch path) and then the rollup, a wait each */
+    static const bool one_wait = [] {
+        const char *e = std::getenv("KGX_LOOKUP_ONE_WAIT");
+        return !e || std::atoi(e) != 0;
+    }();
+    int rc;
+    if (one_wait && kgx_kmap_device(map) == kgx_image_device(kg.image_->handle())) {
+        rc = kgx_lookup(kg.ctx(), map, mode, &p, fw.res, fw.off + w0, n, want, &r, &ru);
+        stage_stats().gpu_passes++;
+        if (rc)
+            throw_last(rc, "kgx_lookup");
+    } else {
+        rc = kgx_process_batch(kg.ctx(), &p, fw.res, fw.off + w0, n, want, &r);
+        stage_stats().gpu_passes++;
+        if (rc)
+            throw_last(rc, "kgx_process_batch");
+        rc = kgx_kmap_rollup(map, kg.ctx(), mode, &ru);
+        if (rc)
+            throw_last(rc, "kgx_kmap_rollup");
+    }
     stage_stats().gpu_ns += now_ns() - g0;
     StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
-    std::string line;
+    /* the per-sequence strings and maps live across the piece's sequences:
+     * their buffers are reused, not allocated per line */
+    std::string line, id, fn, ambig, lf_fam, lf_fn, gf_fam;
     for (uint32_t s = 0; s < n; s++) {
         const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
-        const std::string id(fw.ids + ia, ib - ia);
+        id.assign(fw.ids + ia, ib - ia);
         /* seq_score_ as the reference's operator[] calls leave it: the ids in
          * first-touch order into the request's one map (cleared per sequence,
          * its bucket count kept), so its iteration order is the reference's */
-        seq_score_.clear();
+        if (!seq_score_.empty())
+            seq_score_.clear();
         for (uint64_t j = ru.offsets[s]; j < ru.offsets[s + 1]; j++) {
             const kgx_rollup_row &row = ru.rows[j];
             acc_t &e = seq_score_[row.id];
@@ -1275,12 +1295,12 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
         }
         if (want_calls) {
             int fi;
-            std::string fn, ambig;
             float score, wscore, offs = 0.0f;
+            ambig.clear();
             kg.find_best_call(r.best[s], fi, fn, score, wscore, offs);
             bool do_ambig = false;
             if (fn.empty()) {
-                fn = "hypothetical protein";
+                fn.assign("hypothetical protein");
             } else {
                 const size_t where = fn.find(" ?? ");
                 if (where != std::string::npos) {
@@ -1294,7 +1314,13 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
                 }
             }
             float lf_score = 0.0f, gf_score = 0.0f;
-            std::string lf_fam, lf_fn, gf_fam;
+            lf_fam.clear();
+            lf_fn.clear();
+            gf_fam.clear();
+            /* fresh maps per sequence, as the reference declares them
+             * (lookup_request.cc:259): their iteration order -- the tie
+             * order of the family pick below -- depends on it (an empty
+             * map allocates nothing) */
             std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
             for (const auto &hit_ent : seq_score_) {
                 const acc_t &se = hit_ent.second;

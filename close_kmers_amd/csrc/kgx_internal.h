@@ -147,6 +147,13 @@ size_t plan_workspace_bytes(uint32_t n_seq);
 hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
                        uint32_t *tile_seq, uint32_t tile_windows, void *workspace, uint32_t *status,
                        hipStream_t stream);
+/* the same plan in one launch (a decoupled look-back over workgroups); look:
+ * plan_look_bytes(n_seq) bytes, zero-filled when allocated and left zero by
+ * every launch; tile owners past max_tiles are never written */
+size_t plan_look_bytes(uint32_t n_seq);
+hipError_t launch_plan_fused(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                             uint32_t *tile_seq, uint32_t tile_windows, uint64_t max_tiles, void *look,
+                             uint32_t *status, hipStream_t stream);
 /* Probes of PACKED16 records take home_shift: a key's home bucket is
  * (key mod (num_sigs >> home_shift)) << home_shift and num_sigs counts the
  * table's buckets.  0: the reference's slot (key mod num_sigs); 2: the line
@@ -156,8 +163,11 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2_words,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t home_shift = 0);
-/* max_blocks > 0 caps the line probe's grid (its waves then stride over the
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t home_shift = 0,
+                        uint32_t nt_stores = 0);
+/* nt_stores 1: the line probe writes its hit records and mask words with
+ * non-temporal stores (context option "probe_nt", an A/B knob).
+ * max_blocks > 0 caps the line probe's grid (its waves then stride over the
  * tiles; option probe_persist); 0 = one workgroup per 4 tiles.
  * The line probe over fq fragments left as DNA (PACKED16 images, probe_j
  * 1-4): anchor[s] = (first base of fragment s) << 1 | reverse strand; keys as

@@ -220,6 +220,136 @@ __global__ __launch_bounds__(256) void plan_scan_kernel(const uint64_t *__restri
         wbase[n] = before + tot;
 }
 
+/*
+ * The plan in ONE launch (the default; KGX_PLAN_FUSED=0: the three kernels
+ * above): plan_reduce, plan_sums_scan and plan_scan fused by a decoupled
+ * look-back over the workgroups of PLAN_TILE sequences, as fq_anchor_fused
+ * does for fragments.  Workgroup g publishes its windows (state 1) and, once
+ * it has summed the states of the workgroups before it -- 64 at a time, one
+ * per lane of wave 0, until one holds an inclusive prefix (state 2) -- its own
+ * inclusive prefix; then it writes its sequences' window bases and tile
+ * owners exactly as plan_scan.  Workgroups start in index order, so every
+ * state waited on belongs to a workgroup already running.  State words are
+ * state << 62 | value, relaxed device-scope atomics; after them in `look`: the
+ * finished-workgroup ticket, the bad-offsets flag and the longest sequence.
+ * The workgroup that finishes last writes the status words, empties the
+ * batch when any workgroup saw bad offsets (every window base 0: what the
+ * three kernels give), and zeroes `look` for the next launch (zero-filled
+ * when allocated).  Tile owners are written only below max_tiles: with bad
+ * offsets a workgroup's prefix may pass the buffer before the batch is
+ * emptied.
+ */
+constexpr uint64_t LOOK_MASK = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(256) void plan_fused_kernel(const uint64_t *__restrict__ seq_off, uint32_t n,
+                                                         uint64_t n_residues, uint64_t *__restrict__ wbase,
+                                                         uint32_t *__restrict__ tile_seq, uint32_t tile_windows,
+                                                         uint64_t max_tiles, uint64_t *__restrict__ look,
+                                                         uint32_t groups, uint32_t *__restrict__ status)
+{
+    __shared__ uint64_t lds4[4];
+    __shared__ uint32_t lmax[4];
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_last;
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(look + groups); /* ticket, bad, longest */
+    const uint32_t g = blockIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t s0 = g * PLAN_TILE + threadIdx.x * PLAN_PER;
+    const bool bad = __syncthreads_or(thread_offsets_bad(seq_off, n, s0, n_residues));
+    const uint64_t mine = bad ? 0 : thread_windows(seq_off, n, s0);
+    uint64_t tot;
+    const uint64_t incl = block_scan(mine, lds4, tot);
+    uint32_t m = bad ? 0u : thread_max_windows(seq_off, n, s0);
+    for (uint32_t off = 32; off; off >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, (int)off));
+    if (lane == 0)
+        lmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        if (threadIdx.x == 0) {
+            if (bad)
+                __hip_atomic_fetch_or(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max(&ctl[2], max(max(lmax[0], lmax[1]), max(lmax[2], lmax[3])), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&look[g], (g == 0 ? 2ull : 1ull) << 62 | tot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        /* look back: lane l examines workgroup j - l */
+        uint64_t x = 0;
+        for (int64_t j = (int64_t)g - 1; j >= 0; j -= 64) {
+            const int64_t idx = j - (int64_t)lane;
+            uint64_t v = 2ull << 62; /* before workgroup 0: a zero prefix */
+            if (idx >= 0)
+                do {
+                    v = __hip_atomic_load(&look[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } while ((v >> 62) == 0);
+            const uint64_t pm = __ballot((v >> 62) == 2);
+            const uint32_t upto = pm ? (uint32_t)__builtin_ctzll(pm) : 63u; /* lanes 0..upto count */
+            uint64_t y = lane <= upto ? v & LOOK_MASK : 0;
+            for (uint32_t o = 32; o; o >>= 1)
+                y += __shfl_xor(y, (int)o);
+            x += y;
+            if (pm)
+                break;
+        }
+        if (threadIdx.x == 0) {
+            if (g)
+                __hip_atomic_store(&look[g], 2ull << 62 | ((x + tot) & LOOK_MASK), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            s_prefix = x;
+        }
+    }
+    __syncthreads();
+    const uint64_t before = s_prefix;
+    uint64_t wb = before + incl - mine;
+    for (uint32_t k = 0; k < PLAN_PER; k++) {
+        const uint32_t s = s0 + k;
+        if (s >= n)
+            break;
+        const uint64_t we = wb + (bad ? 0 : windows_of(seq_off[s + 1] - seq_off[s]));
+        wbase[s] = wb;
+        /* tiles whose first window lies in [wb, we) start inside sequence s */
+        for (uint64_t t = (wb + tile_windows - 1) / tile_windows; t * tile_windows < we && t < max_tiles; t++)
+            tile_seq[t] = s;
+        wb = we;
+    }
+    if (g == groups - 1 && threadIdx.x == 255)
+        wbase[n] = before + tot;
+    /* the last workgroup to finish: status, the bad-offsets fix-up, the reset */
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
+    __syncthreads();
+    if (!s_last)
+        return;
+    __threadfence();
+    const uint32_t any_bad = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (any_bad)
+        for (uint64_t s = threadIdx.x; s <= n; s += 256)
+            wbase[s] = 0;
+    if (threadIdx.x == 0) {
+        status[0] = any_bad ? 1u : 0u;
+        status[1] = any_bad ? 0u : __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (uint32_t j = threadIdx.x; j < groups; j += 256)
+        __hip_atomic_store(&look[j], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 3)
+        __hip_atomic_store(&ctl[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+size_t plan_look_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 1) * sizeof(uint64_t) + 16; }
+
+hipError_t launch_plan_fused(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                             uint32_t *tile_seq, uint32_t tile_windows, uint64_t max_tiles, void *look,
+                             uint32_t *status, hipStream_t stream)
+{
+    const uint32_t groups = n_seq / PLAN_TILE + 1; /* >= 1 so wbase[n] is written */
+    hipLaunchKernelGGL(plan_fused_kernel, dim3(groups), dim3(256), 0, stream, seq_off, n_seq, n_residues, wbase,
+                       tile_seq, tile_windows, max_tiles, static_cast<uint64_t *>(look), groups, status);
+    return hipGetLastError();
+}
+
 /* the workgroup sums + the bad-offsets word, then the workgroups' longest sequences */
 size_t plan_workspace_bytes(uint32_t n_seq)
 {
@@ -467,7 +597,7 @@ __device__ __forceinline__ void store_tile_hits(const bool *hit, const uint64_t 
                                                 const uint32_t *pos, const uint32_t *sq, uint64_t g0,
                                                 uint64_t W, uint32_t lane, uint4 *__restrict__ hot,
                                                 uint4 *__restrict__ cold,
-                                                uint64_t *__restrict__ hit_mask)
+                                                uint64_t *__restrict__ hit_mask, bool nt = false)
 {
     uint32_t count = 0;
 #pragma unroll
@@ -475,15 +605,23 @@ __device__ __forceinline__ void store_tile_hits(const bool *hit, const uint64_t 
         const uint64_t m = __ballot(hit[j]);
         if (hit[j]) {
             const uint64_t at = g0 + count + lanes_below(m);
-            if (PACKED) {
+            if (PACKED && nt) {
+                typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+                const u32x4_t v = {pv[j].x, pv[j].y, pv[j].z, pv[j].w};
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4_t *>(hot + at));
+            } else if (PACKED) {
                 hot[at] = pv[j]; /* HIT_PACKED16: the table record itself */
             } else {
                 hot[at] = make_uint4(pv[j].y & 0xFFFFu, pv[j].z, pv[j].w, pos[j]);
                 cold[at] = make_uint4((uint32_t)kv[j], (uint32_t)(kv[j] >> 32), pv[j].x, sq[j]);
             }
         }
-        if (lane == 0 && g0 + 64 * j < W)
-            hit_mask[(g0 >> 6) + j] = m;
+        if (lane == 0 && g0 + 64 * j < W) {
+            if (nt)
+                __builtin_nontemporal_store(m, hit_mask + (g0 >> 6) + j);
+            else
+                hit_mask[(g0 >> 6) + j] = m;
+        }
         count += (uint32_t)__popcll(m);
     }
 }
@@ -624,7 +762,7 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
     const uint8_t *__restrict__ residues, uint64_t n_residues, const uint64_t *__restrict__ seq_off,
     const uint64_t *__restrict__ wbase, const uint32_t *__restrict__ tile_seq, uint32_t n_seq,
     const uint4 *__restrict__ packed, uint64_t num_sigs, uint64_t magic, uint32_t hs, uint4 *__restrict__ hot,
-    uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask)
+    uint4 *__restrict__ cold, uint64_t *__restrict__ hit_mask, uint32_t nt)
 {
     constexpr uint32_t T = 64 * J;
     constexpr uint32_t NQ = 64 / G; /* windows per instruction */
@@ -736,7 +874,7 @@ __global__ __launch_bounds__(256) void probe_line_kernel(
         hit[j] = lds_hit[wave][64 * j + lane] != 0;
         pv[j] = hit[j] ? lds_rec[wave][64 * j + lane] : make_uint4(0, 0, 0, 0);
     }
-    store_tile_hits<J, true>(hit, key, pv, pos, sq, g0, W, lane, hot, cold, hit_mask);
+    store_tile_hits<J, true>(hit, key, pv, pos, sq, g0, W, lane, hot, cold, hit_mask, nt != 0);
     } /* tiles */
 }
 
@@ -744,11 +882,11 @@ template <int J, int G, bool DNA = false>
 static void launch_probe_line(dim3 grid, hipStream_t stream, const uint8_t *residues, uint64_t n_residues,
                               const uint64_t *seq_off, const uint64_t *wbase, const uint32_t *tile_seq,
                               uint32_t n_seq, const void *table, uint64_t num_sigs, uint32_t hs, uint4 *hot,
-                              uint4 *cold, uint64_t *hit_mask, uint32_t dyn_lds)
+                              uint4 *cold, uint64_t *hit_mask, uint32_t dyn_lds, uint32_t nt = 0)
 {
     hipLaunchKernelGGL((probe_line_kernel<J, G, DNA>), grid, dim3(64 * PROBE_WAVES), dyn_lds, stream, residues,
                        n_residues, seq_off, wbase, tile_seq, n_seq, static_cast<const uint4 *>(table),
-                       num_sigs, mod_magic(num_sigs >> hs), hs, hot, cold, hit_mask);
+                       num_sigs, mod_magic(num_sigs >> hs), hs, hot, cold, hit_mask, nt);
 }
 
 template <int J, int MODE>
@@ -795,7 +933,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
                         uint64_t max_tiles, const void *table, int layout, uint64_t num_sigs,
                         const uint64_t *filter, uint32_t filter_log2,
                         uint4 *hot, uint4 *cold, uint64_t *hit_mask, int probe_j, int variant,
-                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t hs)
+                        uint32_t lds_kb, uint32_t max_blocks, hipStream_t stream, uint32_t hs, uint32_t nt)
 {
     if (max_tiles == 0)
         return hipSuccess;
@@ -813,7 +951,7 @@ hipError_t launch_probe(const uint8_t *residues, uint64_t n_residues, const uint
     if ((variant == PROBE_LINE || variant == PROBE_LINE8) && layout == KGX_LAYOUT_PACKED16 && !filter) {
 #define KGX_LINE(JJ, GG)                                                                             \
     launch_probe_line<JJ, GG>(lgrid, stream, residues, n_residues, seq_off, wbase, tile_seq, n_seq, table, \
-                              num_sigs, hs, hot, cold, hit_mask, dyn_lds);                           \
+                              num_sigs, hs, hot, cold, hit_mask, dyn_lds, nt);                       \
     return hipGetLastError()
         const int key = probe_j * 10 + (variant == PROBE_LINE8 ? 8 : 4);
         switch (key) {

@@ -638,6 +638,36 @@ int kgx_pool_process_batch_compact(kgx_pool *p, const kgx_params *params, const 
     return KGX_OK;
 }
 
+int kgx_lookup(kgx_ctx *c, kgx_kmap *map, int mode, const kgx_params *params, const char *residues,
+               const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out, kgx_rollup_result *rollup)
+{
+    if (!c || !map || !out || !rollup || (!seq_offsets && n_seq))
+        return fail(KGX_EINVAL, "null argument");
+    if (want & (KGX_WANT_HITS | KGX_WANT_OTU))
+        return fail(KGX_EINVAL, "lookup: want within KGX_WANT_CALLS | KGX_WANT_BEST (the hits stay on the device)");
+    if (kgx_kmap_device(map) != kgx_image_device(c->img))
+        return fail(KGX_EINVAL, "lookup: the map is on another device than the context");
+    for (uint32_t s = 0; s < n_seq; s++)
+        if (seq_offsets[s + 1] < seq_offsets[s])
+            return fail(KGX_EINVAL, "seq_offsets not monotone");
+    int rc = one_pass_enqueue(c, params, residues, seq_offsets, n_seq, want, nullptr, nullptr);
+    if (!rc)
+        rc = collect_counts_enqueue(c, want);
+    if (!rc)
+        rc = rollup_enqueue(map, c, mode);
+    if (!rc) {
+        const uint64_t reruns = c->nul_reruns;
+        rc = one_pass_collect(c, params, residues, seq_offsets, n_seq, want, out);
+        if (!rc && c->nul_reruns != reruns) /* the pass ran again, staged: so does its rollup */
+            rc = rollup_enqueue(map, c, mode);
+    }
+    if (!rc)
+        rc = rollup_finish(map, c, mode, rollup);
+    if (rc)
+        (void)hipStreamSynchronize(c->stream); /* nothing of the call left running */
+    return rc;
+}
+
 int kgx_pool_lookup(kgx_pool *p, kgx_kmap *const *maps, uint32_t n_maps, int mode, const kgx_params *params,
                     const char *residues, const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want,
                     kgx_result *out, kgx_rollup_result *rollup)

@@ -377,6 +377,9 @@ struct kgx_ctx {
         dense_hoff, dense_coff, dense_hits, dense_calls, plan_ws, ranges;
     /* plan status word (1 = the last plan's offsets were bad, batch emptied) */
     kgx::DevBuf plan_status;
+    /* the one-launch plan's look-back states (zero between launches) */
+    kgx::DevBuf plan_look;
+    int plan_fused = 1; /* option "plan_fused": 0 = the three plan kernels */
     kgx::PinnedVec<uint32_t> h_plan_status;
     /* current plan */
     uint32_t n_seq = 0;
@@ -423,6 +426,7 @@ struct kgx_ctx {
     int score_wave_tiles = 16; /* probe tiles of windows per scorer wave (option "score_wave_tiles") */
     int probe_filter = 1; /* use the image's presence filter when it has one */
     int use_line_index = 1; /* option "line_index": 0 = probe the reference slots even when the image has a line index */
+    int probe_nt = 0;       /* option "probe_nt": 1 = the line probe's hit stores non-temporal */
     uint64_t microbench_span = 0; /* bytes of the table the random-read ceiling covers; 0 = all */
     int microbench_ilp = 8;       /* independent reads in flight per lane */
     int microbench_wgs = 8;       /* 256-thread workgroups per CU */

@@ -7,6 +7,7 @@
  * KmerGuts::process_aa_seq (kguts.cc:888-908) with batched HIP launches.
  */
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -1023,6 +1024,18 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         c->probe_variant = (int)value;
         return KGX_OK;
     }
+    if (n == "plan_fused") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "plan_fused must be 0 or 1");
+        c->plan_fused = (int)value;
+        return KGX_OK;
+    }
+    if (n == "probe_nt") {
+        if (value != 0 && value != 1)
+            return fail(KGX_EINVAL, "probe_nt must be 0 or 1");
+        c->probe_nt = (int)value;
+        return KGX_OK;
+    }
     if (n == "line_index") {
         if (value != 0 && value != 1)
             return fail(KGX_EINVAL, "line_index must be 0 or 1");
@@ -1279,6 +1292,16 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     int rc = kgx::plan_reserve(c, d_off, n_seq, n_residues);
     if (rc)
         return rc;
+    if (c->plan_fused) {
+        const void *had = c->plan_look.p;
+        HIP_TRY(c->plan_look.reserve(plan_look_bytes(n_seq)));
+        if (c->plan_look.p != had) /* new states start at zero; every launch leaves them so */
+            HIP_TRY(hipMemsetAsync(c->plan_look.p, 0, c->plan_look.cap, c->stream));
+        HIP_TRY(launch_plan_fused(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                                  c->tile_windows, c->max_tiles, c->plan_look.p, c->plan_status.as<uint32_t>(),
+                                  c->stream));
+        return KGX_OK;
+    }
     HIP_TRY(c->plan_ws.reserve(plan_workspace_bytes(n_seq)));
     HIP_TRY(launch_plan(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
                         c->tile_windows, c->plan_ws.p, c->plan_status.as<uint32_t>(), c->stream));
@@ -1426,7 +1449,7 @@ int kgx_stage_probe(kgx_ctx *c, const uint8_t *d_res, const uint64_t *d_off)
                             c->probe_filter ? c->img->d_filter : nullptr, c->img->filter_log2_words,
                             c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots, c->hit_mask.as<uint64_t>(),
                             (int)(c->tile_windows / 64), c->probe_variant, (uint32_t)c->probe_lds_kb,
-                            probe_max_blocks(c), c->stream, ctx_home_shift(c));
+                            probe_max_blocks(c), c->stream, ctx_home_shift(c), (uint32_t)c->probe_nt);
     });
 }
 
@@ -3188,6 +3211,7 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     }
     if (fused) {
         const volatile uint32_t *done = c->h_done.data();
+        const auto w0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 1; *done != token; spin++) {
             if ((spin & 255u) == 0) { /* a fault or a lost store still ends the wait */
                 const hipError_t q = hipStreamQuery(c->stream);
@@ -3195,6 +3219,10 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                     break;
                 if (q != hipErrorNotReady)
                     HIP_TRY(q);
+                /* past 50 us of spinning the CPU goes to whoever else is
+                 * runnable (a server's other workers, its socket threads) */
+                if (std::chrono::steady_clock::now() - w0 > std::chrono::microseconds(50))
+                    sched_yield();
             }
 #if defined(__x86_64__)
             __builtin_ia32_pause();

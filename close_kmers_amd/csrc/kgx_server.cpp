@@ -175,18 +175,20 @@ void serve_connection(KmerRequestRouter &router, int fd)
         }
         if (len > g_max_body_bytes)
             return refuse(413, "Payload Too Large");
-        req.body = buf.substr(pos);
-        while (req.body.size() < len) {
-            char tmp[1 << 16];
-            ssize_t r = ::recv(fd, tmp, sizeof tmp, 0);
+        /* the body straight into place: one copy out of the socket, not two */
+        const size_t have = std::min(len, buf.size() - pos);
+        req.body.resize(len);
+        std::memcpy(&req.body[0], buf.data() + pos, have);
+        size_t got = have;
+        while (got < len) {
+            ssize_t r = ::recv(fd, &req.body[got], len - got, 0);
             if (r < 0 && errno == EINTR)
                 continue;
             if (r <= 0)
                 break;
-            req.body.append(tmp, (size_t)r);
+            got += (size_t)r;
         }
-        if (req.body.size() > len)
-            req.body.resize(len);
+        req.body.resize(got);
     }
     bool quit = false;
     StageStats &st = stage_stats();

@@ -301,6 +301,10 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * "probe_filter" 1 (default) / 0 = use / ignore the image's presence filter;
  * "line_index" 1 (default) / 0 = this context's probes read the image's line
  * index when it has one / the reference slots (in-process A/Bs);
+ * "probe_nt" 0 (default) / 1 = the line probe writes its hit records and mask
+ * with non-temporal stores;
+ * "plan_fused" 1 (default) = the plan (window bases, tile owners) in one
+ * launch, a decoupled look-back; 0 = three launches (reduce, scan, fill);
  * "probe_serialize" 1 (default) / 0: this context's probes wait for the
  * image's previous probe (any context), so that probes run back to back and
  * the other kernels of the contexts overlap them;
@@ -828,6 +832,17 @@ int kgx_kmap_rollup(kgx_kmap *map, kgx_ctx *ctx, int mode, kgx_rollup_result *ou
 /* the device the map lives on */
 int kgx_kmap_device(const kgx_kmap *map);
 
+/* /lookup's GPU side for a host batch on ONE context (a server worker's
+ * request piece, lookup_request.cc:153-210,446-482): the pass and the rollup
+ * over `map` (on the context's device) enqueued together -- upload, plan,
+ * probe, score, the counts (and best calls) into mapped memory, the rollup
+ * sized by the context's previous one -- and one host wait for both, instead
+ * of kgx_process_batch's wait and then kgx_kmap_rollup's.  want within
+ * KGX_WANT_CALLS | KGX_WANT_BEST; results as those two calls give them (out:
+ * no hits; the views valid until the context's next call). */
+int kgx_lookup(kgx_ctx *ctx, kgx_kmap *map, int mode, const kgx_params *params, const char *residues,
+               const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out,
+               kgx_rollup_result *rollup);
 /* /lookup's GPU side for a whole host batch over a pool
  * (LookupRequest::process_work + on_hit, lookup_request.cc:153-210,446-482):
  * the batch is cut into shards of whole sequences (up to twice as many per

@@ -158,3 +158,33 @@ def test_pool_lookup_tiny_growing_batches_and_pinned_nul(world):
         pres[:] = res_all[:len(pres)]
         pres[int(off_all[1500]) + 50] = 0
         check(n, pres)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_ctx_lookup_one_wait_matches_pass_plus_rollup(world, pinned):
+    """kgx_lookup (a server worker's /lookup piece: the pass and the rollup
+    enqueued together, one host wait) == kgx_process_batch (one pass) +
+    kgx_kmap_rollup, for batches growing and shrinking between calls (the
+    rollup is sized by the previous one), family and peg mode, pinned or
+    pageable residues."""
+    spec, table, img = world
+    rng = np.random.default_rng(77)
+    keys, ids = family_pairs(spec, spec.n_src, rng)
+    with abi.Kmap(0, abi.KMAP_SET) as fam, abi.Kmap(0, abi.KMAP_APPEND) as peg, \
+            abi.Context(img) as ctx, abi.Context(img) as ref:
+        fam.add(keys, ids)
+        peg.add(keys, ids)
+        ref.set_option("host_chunks", 1)
+        for k, n in enumerate((2000, 30, 4000, 1, 700)):
+            res, off = synth.make_queries(spec, n, x_permille=3, q0=100 * k)
+            if pinned:
+                pres = abi.pinned_empty(len(res))
+                pres[:] = res
+                res = pres
+            for kmap, mode in ((fam, abi.ROLLUP_FAMILY), (peg, abi.ROLLUP_PEG)):
+                got, g_off, g_rows = ctx.lookup(kmap, res, off, want=abi.WANT_BEST, mode=mode)
+                one = ref.process_batch(np.array(res), off, want=abi.WANT_BEST)
+                w_off, w_rows = kmap.rollup(ref, mode)
+                _rows_equal(g_off, g_rows, w_off, w_rows)
+                assert np.array_equal(got.best.view(np.uint8), one.best.view(np.uint8))
+                assert len(got.hits) == 0
