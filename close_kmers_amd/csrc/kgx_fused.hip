@@ -602,6 +602,76 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
         __syncthreads();
         uint32_t d = n_otu;
+        if (d == ~0u && nh <= 128 * FJ) {
+            /* past KREG distinct values, wave 0 alone (no block barrier): the
+             * flagged hits' OTUs counted in an LDS hash of 2 nh slots or more
+             * beside the records (they fill at most the first half of hrec),
+             * the distinct pairs counted, and -- up to 64 of them -- packed
+             * into registers, sorted by value by the register bitonic network
+             * and placed.  More than 64: the block path below, the records
+             * untouched. */
+            if (wave == 0) {
+                int32_t *hk = reinterpret_cast<int32_t *>(hrec) + 2 * 256 * FJ;
+                uint32_t *hcnt = reinterpret_cast<uint32_t *>(hrec) + 3 * 256 * FJ;
+                uint32_t Hs = 64;
+                while (Hs < 2 * nh)
+                    Hs <<= 1;
+                for (uint32_t i = lane; i < Hs; i += 64) {
+                    hk[i] = INT32_MIN; /* OTUs are -1 .. 2^21 - 2 */
+                    hcnt[i] = 0;
+                }
+                wave_lds_sync();
+                for (uint32_t h0 = 0; h0 < nh; h0 += 64) {
+                    const uint32_t i = h0 + lane;
+                    if (i < nh && oflag[i]) {
+                        const int32_t x = (int32_t)HF::otu(hrec[i], hrec[i]);
+                        uint32_t h = ((uint32_t)x * 0x9E3779B1u) & (Hs - 1);
+                        for (;;) {
+                            const int32_t old = atomicCAS(hk + h, INT32_MIN, x);
+                            if (old == INT32_MIN || old == x)
+                                break;
+                            h = (h + 1) & (Hs - 1);
+                        }
+                        atomicAdd(hcnt + h, 1u);
+                    }
+                }
+                wave_lds_sync();
+                uint32_t dd = 0;
+                for (uint32_t j0 = 0; j0 < Hs; j0 += 64)
+                    dd += (uint32_t)__popcll(__ballot(hk[j0 + lane] != INT32_MIN));
+                if (dd <= 64) {
+                    /* the pairs, packed (value with its sign bit flipped << 32 |
+                     * count) so that unsigned order is the map's key order */
+                    uint64_t *pk = reinterpret_cast<uint64_t *>(o);
+                    uint32_t at = 0;
+                    for (uint32_t j0 = 0; j0 < Hs; j0 += 64) {
+                        const int32_t kk = hk[j0 + lane];
+                        const bool f = kk != INT32_MIN;
+                        const uint64_t bm = __ballot(f);
+                        if (f)
+                            pk[at + lanes_below(bm)] = (uint64_t)((uint32_t)kk ^ 0x80000000u) << 32 |
+                                                       hcnt[j0 + lane];
+                        at += (uint32_t)__popcll(bm);
+                    }
+                    wave_lds_sync();
+                    uint64_t x = lane < dd ? pk[lane] : ~0ull; /* the padding sorts last */
+                    for (uint32_t k = 2; k <= 64; k <<= 1)
+                        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                            const uint64_t y = (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)x, j) |
+                                               (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)(x >> 32), j) << 32;
+                            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+                            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
+                        }
+                    wave_lds_sync();
+                    if (lane < dd)
+                        o[lane] = kgx_otu{(int32_t)((uint32_t)(x >> 32) ^ 0x80000000u), (int32_t)(uint32_t)x};
+                }
+                if (lane == 0)
+                    n_otu = dd <= 64 ? dd : ~0u;
+            }
+            __syncthreads();
+            d = n_otu;
+        }
         if (d == ~0u) {
             /* past KREG distinct values: the flagged hits' OTUs counted in an
              * LDS hash (256 FJ slots: one per window at least, so it never
@@ -718,7 +788,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         if (dbg)
             a.dbg[8] = wall_clock64();
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
-         * it, lstd_sort_wave64 up to 64 pairs, lstd_sort_wave up to 64 SW
+         * it, lstd_sort_wave64_reg up to 64 pairs (the pairs in registers),
+         * lstd_sort_wave up to 64 SW
          * (their scratch past the pairs in hrec, range marks in codes),
          * thread 0 beyond.  (r4f: a 36-OTU call's pairs sort in 0.33 us; the
          * calls past 64 pairs, on the serial replay then, cost 11 us per
@@ -727,7 +798,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         const auto by_count = [](const kgx_otu &lhs, const kgx_otu &rhs) { return rhs.count < lhs.count; };
         if (d > 1 && d <= 64) {
             if (wave == 0)
-                lstd_sort_wave64(o, d, by_count, o + 64 * SW, ostack);
+                lstd_sort_wave64_reg(o, d, by_count, o + 64 * SW, o + 64 * SW + 64);
         } else if (d > 64 && d <= 64 * SW) {
             if (wave == 0)
                 lstd_sort_wave<SW>(o, d, by_count, o + 64 * SW, o + 128 * SW, codes, ostack);

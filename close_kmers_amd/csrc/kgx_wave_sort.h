@@ -116,6 +116,108 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
     wave_lds_sync();
 }
 
+/* lstd_sort_wave64 for kgx_otu pairs with the elements in registers: lane i
+ * holds a[i] for the whole replay, so a partition step costs one LDS round
+ * trip (its swaps meet through bl / br, indexed by rank, as above) instead of
+ * the reads and writes of `a` around every move; the median of three, the
+ * pivot and the range stack (lane k holds entry k) are lane reads; and the
+ * final insertion sort's counting reads the others' elements by readlane, not
+ * from LDS.  Same steps, so the same result as lstd_sort_wave64 and the
+ * serial replay.  a: the n <= 64 pairs in LDS (read at the start, written at
+ * the end); bl, br: 64 elements of scratch each. */
+__device__ __forceinline__ kgx_otu otu_lane(const kgx_otu &v, uint32_t j)
+{
+    return kgx_otu{(int32_t)__builtin_amdgcn_readlane(v.otu_index, (int)j),
+                   (int32_t)__builtin_amdgcn_readlane(v.count, (int)j)};
+}
+
+template <class C>
+__device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl, kgx_otu *br)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t le = lanes_le(lane), below = le & ~(1ull << lane);
+    kgx_otu v = lane < n ? a[lane] : kgx_otu{0, 0};
+    if (n > 16) {
+        /* the range stack, entry k in lane k */
+        int32_t sf = 0, sl = (int32_t)n, sd = 2 * (31 - (int)__builtin_clz(n));
+        uint32_t sp = 1;
+        while (sp) {
+            --sp;
+            int32_t f = __builtin_amdgcn_readlane(sf, (int)sp);
+            int32_t l = __builtin_amdgcn_readlane(sl, (int)sp);
+            int32_t depth = __builtin_amdgcn_readlane(sd, (int)sp);
+            while (l - f > 16) {
+                if (depth == 0) { /* std::sort's heap sort of the range, serial */
+                    if (lane < n)
+                        a[lane] = v;
+                    wave_lds_sync();
+                    if (lane == 0)
+                        lstd_heap_sort(a + f, l - f, comp);
+                    wave_lds_sync();
+                    if (lane < n)
+                        v = a[lane];
+                    wave_lds_sync();
+                    break;
+                }
+                --depth;
+                /* __move_median_to_first(first, first + 1, mid, last - 1) */
+                const int32_t mid = f + (l - f) / 2;
+                const kgx_otu x = otu_lane(v, (uint32_t)(f + 1)), y = otu_lane(v, (uint32_t)mid),
+                              z = otu_lane(v, (uint32_t)(l - 1));
+                int32_t pick;
+                if (comp(x, y))
+                    pick = comp(y, z) ? mid : (comp(x, z) ? l - 1 : f + 1);
+                else
+                    pick = comp(x, z) ? f + 1 : (comp(y, z) ? l - 1 : mid);
+                pick = __builtin_amdgcn_readfirstlane(pick);
+                const kgx_otu first_v = otu_lane(v, (uint32_t)f), pivot = otu_lane(v, (uint32_t)pick);
+                if ((int32_t)lane == f)
+                    v = pivot;
+                else if ((int32_t)lane == pick)
+                    v = first_v;
+                const bool in = (int32_t)lane > f && (int32_t)lane < l;
+                const bool lf = in && !comp(v, pivot), rf = in && !comp(pivot, v);
+                const uint64_t LM = __ballot(lf), RM = __ballot(rf);
+                const uint32_t l_below = (uint32_t)__popcll(LM & below);
+                const uint32_t r_above = (uint32_t)__popcll(RM & ~le);
+                const uint32_t rank_l = l_below + 1, rank_r = r_above + 1;
+                const bool swl = lf && rank_l <= r_above, swr = rf && rank_r <= l_below;
+                const uint32_t P = (uint32_t)__popcll(__ballot(swl));
+                if (swl)
+                    bl[rank_l - 1] = v;
+                if (swr)
+                    br[rank_r - 1] = v;
+                wave_lds_sync();
+                if (swl)
+                    v = br[rank_l - 1];
+                else if (swr)
+                    v = bl[rank_r - 1];
+                const uint64_t LN = __ballot(lf && rank_l == P + 1), RP = __ballot(P > 0 && rf && rank_r == P);
+                const int32_t lcut = LN ? (int32_t)lowbit(LN) : INT32_MAX;
+                const int32_t rcut = RP ? (int32_t)lowbit(RP) : INT32_MAX;
+                const int32_t cut = min(lcut, rcut);
+                wave_lds_sync(); /* bl / br are written again by the next step */
+                if (lane == sp) { /* __introsort_loop(cut, last) */
+                    sf = cut;
+                    sl = l;
+                    sd = depth;
+                }
+                sp++;
+                l = cut;
+            }
+        }
+    }
+    /* __final_insertion_sort: stable, so by counting */
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const kgx_otu w = otu_lane(v, j);
+        pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
+    }
+    if (lane < n)
+        a[pos] = v;
+    wave_lds_sync();
+}
+
 /* The same for n <= 64 S elements, 64 positions per strip (the service
  * takes it past 64 pairs; up to 64 lstd_sort_wave64 is faster: r4h, 5.2 vs
  * 3.0 us at 33-64 pairs, 0.8 vs 0.4 at 2-8).

@@ -9,8 +9,9 @@
  *
  *   wave_sort_check CASES SEED
  *
- * Prints "ok CASES" and one JSON line of mean ns per sort by size band; exit
- * 1 on the first mismatch.
+ * Runs lstd_sort_wave64 (pairs in LDS) and lstd_sort_wave64_reg (pairs in
+ * registers) in turn; prints "ok CASES <variant>" and one JSON line of mean ns
+ * per sort by size band for each; exit 1 on the first mismatch.
  */
 #include <hip/hip_runtime.h>
 
@@ -29,7 +30,7 @@ struct ByCount {
 };
 
 __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const uint32_t *n_of, uint32_t cases,
-                                                       kgx_otu *out, uint64_t *ns)
+                                                       kgx_otu *out, uint64_t *ns, int reg)
 {
     __shared__ kgx_otu a[256];
     __shared__ kgx_otu bl[256], br[256]; /* bl: also lstd_sort_wave64's 192 elements of scratch */
@@ -42,7 +43,9 @@ __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const 
             a[i] = in[256 * c + i];
         wave_lds_sync();
         const uint64_t t0 = wall_clock64();
-        if (n <= 64)
+        if (n <= 64 && reg)
+            lstd_sort_wave64_reg(a, n, ByCount{}, bl, br);
+        else if (n <= 64)
             lstd_sort_wave64(a, n, ByCount{}, bl, st); /* bl, br: its 192 elements of scratch */
         else
             lstd_sort_wave<4>(a, n, ByCount{}, bl, br, seg, st);
@@ -91,35 +94,39 @@ int main(int argc, char **argv)
     CHECK(hipMalloc(&d_ns, cases * sizeof(uint64_t)));
     CHECK(hipMemcpy(d_in, in.data(), in.size() * sizeof(kgx_otu), hipMemcpyHostToDevice));
     CHECK(hipMemcpy(d_n, n_of.data(), cases * sizeof(uint32_t), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(wave_sort_kernel, dim3(1), dim3(64), 0, 0, d_in, d_n, cases, d_out, d_ns);
-    CHECK(hipGetLastError());
-    CHECK(hipDeviceSynchronize());
-    std::vector<uint64_t> ns(cases);
-    CHECK(hipMemcpy(got.data(), d_out, got.size() * sizeof(kgx_otu), hipMemcpyDeviceToHost));
-    CHECK(hipMemcpy(ns.data(), d_ns, cases * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    for (uint32_t c = 0; c < cases; c++)
-        for (uint32_t i = 0; i < n_of[c]; i++) {
-            const kgx_otu &g = got[256 * (size_t)c + i], &w = want[256 * (size_t)c + i];
-            if (g.otu_index != w.otu_index || g.count != w.count) {
-                std::printf("mismatch case %u (n %u) at %u: (%d,%d) vs (%d,%d)\n", c, n_of[c], i, g.otu_index,
-                            g.count, w.otu_index, w.count);
-                return 1;
-            }
-        }
-    /* mean ns per sort by size band */
+    /* variant 0: lstd_sort_wave64 (elements in LDS), 1: lstd_sort_wave64_reg
+     * (elements in registers); past 64 both use lstd_sort_wave<4> */
     const uint32_t bands[] = {2, 9, 17, 33, 65, 129, 257};
-    std::printf("ok %u\n{", cases);
-    for (int b = 0; b < 6; b++) {
-        double s = 0;
-        uint32_t k = 0;
+    for (int reg = 0; reg < 2; reg++) {
+        hipLaunchKernelGGL(wave_sort_kernel, dim3(1), dim3(64), 0, 0, d_in, d_n, cases, d_out, d_ns, reg);
+        CHECK(hipGetLastError());
+        CHECK(hipDeviceSynchronize());
+        std::vector<uint64_t> ns(cases);
+        CHECK(hipMemcpy(got.data(), d_out, got.size() * sizeof(kgx_otu), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(ns.data(), d_ns, cases * sizeof(uint64_t), hipMemcpyDeviceToHost));
         for (uint32_t c = 0; c < cases; c++)
-            if (n_of[c] >= bands[b] && n_of[c] < bands[b + 1]) {
-                s += (double)ns[c];
-                k++;
+            for (uint32_t i = 0; i < n_of[c]; i++) {
+                const kgx_otu &g = got[256 * (size_t)c + i], &w = want[256 * (size_t)c + i];
+                if (g.otu_index != w.otu_index || g.count != w.count) {
+                    std::printf("mismatch (variant %d) case %u (n %u) at %u: (%d,%d) vs (%d,%d)\n", reg, c,
+                                n_of[c], i, g.otu_index, g.count, w.otu_index, w.count);
+                    return 1;
+                }
             }
-        std::printf("%s\"n%u-%u_ns\": %.0f", b ? ", " : "", bands[b], bands[b + 1] - 1, k ? s / k : 0.0);
+        /* mean ns per sort by size band */
+        std::printf("ok %u %s\n{", cases, reg ? "registers" : "lds");
+        for (int b = 0; b < 6; b++) {
+            double t = 0;
+            uint32_t k = 0;
+            for (uint32_t c = 0; c < cases; c++)
+                if (n_of[c] >= bands[b] && n_of[c] < bands[b + 1]) {
+                    t += (double)ns[c];
+                    k++;
+                }
+            std::printf("%s\"n%u-%u_ns\": %.0f", b ? ", " : "", bands[b], bands[b + 1] - 1, k ? t / k : 0.0);
+        }
+        std::printf("}\n");
     }
-    std::printf("}\n");
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     (void)hipFree(d_n);

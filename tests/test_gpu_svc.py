@@ -402,8 +402,10 @@ def test_svc_stop_and_config_while_calling(svc_image, oracle_lib):
 
 
 def test_wave_sort_matches_serial_replay():
-    """lstd_sort_wave -- libstdc++'s std::sort of up to 256 OTU pairs by
-    count, replayed by one wave (the call service's tally, kguts.h:214-218) --
+    """lstd_sort_wave64 / lstd_sort_wave64_reg / lstd_sort_wave --
+    libstdc++'s std::sort of up to 256 OTU pairs by count, replayed by one
+    wave (the call service's tally, kguts.h:214-218), the pairs in LDS or in
+    registers --
     equals the serial replay (kgx_lstd.h, checked against libstdc++ on the
     CPU) on 3,000 lists of 2..256 pairs with heavy ties
     (tests/native/wave_sort_check.cpp); prints the mean time per sort by list
@@ -411,5 +413,6 @@ def test_wave_sort_matches_serial_replay():
     import subprocess
     from close_kmers_amd import build as kbuild
     r = subprocess.run([kbuild.WAVE_SORT_CHECK, "3000", "7"], capture_output=True, text=True, timeout=100)
-    assert r.returncode == 0 and r.stdout.startswith("ok 3000"), r.stdout + r.stderr
-    print(r.stdout.strip().splitlines()[-1])
+    lines = r.stdout.strip().splitlines()
+    assert r.returncode == 0 and "ok 3000 lds" in lines and "ok 3000 registers" in lines, r.stdout + r.stderr
+    print(r.stdout.strip())
