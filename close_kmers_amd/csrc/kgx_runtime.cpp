@@ -1293,9 +1293,11 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     if (rc)
         return rc;
     if (c->plan_fused) {
-        const void *had = c->plan_look.p;
+        /* new states start at zero (every launch leaves them so); a grown
+         * buffer may come back at the old address, so its capacity says */
+        const size_t had = c->plan_look.cap;
         HIP_TRY(c->plan_look.reserve(plan_look_bytes(n_seq)));
-        if (c->plan_look.p != had) /* new states start at zero; every launch leaves them so */
+        if (c->plan_look.cap != had)
             HIP_TRY(hipMemsetAsync(c->plan_look.p, 0, c->plan_look.cap, c->stream));
         HIP_TRY(launch_plan_fused(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
                                   c->tile_windows, c->max_tiles, c->plan_look.p, c->plan_status.as<uint32_t>(),

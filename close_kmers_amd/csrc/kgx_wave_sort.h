@@ -116,15 +116,16 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
     wave_lds_sync();
 }
 
-/* lstd_sort_wave64 for kgx_otu pairs with the elements in registers: lane i
- * holds a[i] for the whole replay, so a partition step costs one LDS round
- * trip (its swaps meet through bl / br, indexed by rank, as above) instead of
- * the reads and writes of `a` around every move; the median of three, the
- * pivot and the range stack (lane k holds entry k) are lane reads; and the
- * final insertion sort's counting reads the others' elements by readlane, not
- * from LDS.  Same steps, so the same result as lstd_sort_wave64 and the
- * serial replay.  a: the n <= 64 pairs in LDS (read at the start, written at
- * the end); bl, br: 64 elements of scratch each. */
+/* lstd_sort_wave64 for kgx_otu pairs by count (less_second: comp(l, r) =
+ * r.count < l.count) with the elements in registers: lane i holds a[i] for
+ * the whole replay, so a partition step costs one LDS round trip (its swaps
+ * meet through bl / br, indexed by rank, as above) instead of the reads and
+ * writes of `a` around every move; the median of three, the pivot and the
+ * range stack (lane k holds entry k) are lane reads; and the final insertion
+ * sort -- stable -- is a bitonic sort by (count, position).  Same steps, so
+ * the same result as lstd_sort_wave64 and the serial replay.  a: the n <= 64
+ * pairs in LDS (read at the start, written at the end); bl, br: 64 elements
+ * of scratch each. */
 __device__ __forceinline__ kgx_otu otu_lane(const kgx_otu &v, uint32_t j)
 {
     return kgx_otu{(int32_t)__builtin_amdgcn_readlane(v.otu_index, (int)j),
@@ -207,14 +208,27 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
             }
         }
     }
-    /* __final_insertion_sort: stable, so by counting */
-    uint32_t pos = 0;
-    for (uint32_t j = 0; j < n; j++) {
-        const kgx_otu w = otu_lane(v, j);
-        pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
-    }
+    /* __final_insertion_sort: a stable sort of what the loop left, so a
+     * sort by (key, position) -- a total order, one answer -- which the
+     * register bitonic network gives in 21 lane exchanges instead of n
+     * serial lane reads per element.  key(v) orders as comp does: comp is
+     * by count, larger first (less_second, kguts.h:214-218). */
+    uint64_t x = lane < n ? (uint64_t)(0x7FFFFFFFu - (uint32_t)v.count) << 32 | lane : ~0ull; /* padding last */
+    int32_t pay = v.otu_index;
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t y = (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)x, j) |
+                               (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)(x >> 32), j) << 32;
+            const int32_t py = xor_lane(pay, j);
+            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+            const bool take = keep_min ? y < x : x < y;
+            if (take) {
+                x = y;
+                pay = py;
+            }
+        }
     if (lane < n)
-        a[pos] = v;
+        a[lane] = kgx_otu{pay, (int32_t)(0x7FFFFFFFu - (uint32_t)(x >> 32))};
     wave_lds_sync();
 }
 
