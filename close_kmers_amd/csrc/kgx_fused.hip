@@ -602,76 +602,6 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
         __syncthreads();
         uint32_t d = n_otu;
-        if (d == ~0u && nh <= 128 * FJ) {
-            /* past KREG distinct values, wave 0 alone (no block barrier): the
-             * flagged hits' OTUs counted in an LDS hash of at least twice as
-             * many slots as flagged hits, beside the records (they fill at
-             * most the first half of hrec); the distinct pairs (value with its
-             * sign bit flipped, count: unsigned order = the map's key order)
-             * into hpos (free by now) and -- up to 64 of them -- sorted by value
-             * by the register bitonic network and placed.  More than 64: the
-             * block path below, the records untouched. */
-            if (wave == 0) {
-                int32_t *hk = reinterpret_cast<int32_t *>(hrec) + 2 * 256 * FJ;
-                uint32_t *hcnt = reinterpret_cast<uint32_t *>(hrec) + 3 * 256 * FJ;
-                uint32_t m = 0;
-                for (uint32_t h0 = 0; h0 < nh; h0 += 64)
-                    m += (uint32_t)__popcll(__ballot(h0 + lane < nh && oflag[h0 + lane]));
-                uint32_t Hs = 64;
-                while (Hs < 2 * m)
-                    Hs <<= 1;
-                for (uint32_t i = lane; i < Hs; i += 64) {
-                    hk[i] = INT32_MIN; /* OTUs are -1 .. 2^21 - 2 */
-                    hcnt[i] = 0;
-                }
-                wave_lds_sync();
-                for (uint32_t h0 = 0; h0 < nh; h0 += 64) {
-                    const uint32_t i = h0 + lane;
-                    if (i < nh && oflag[i]) {
-                        const int32_t x = (int32_t)HF::otu(hrec[i], hrec[i]);
-                        uint32_t h = ((uint32_t)x * 0x9E3779B1u) & (Hs - 1);
-                        for (;;) {
-                            const int32_t old = atomicCAS(hk + h, INT32_MIN, x);
-                            if (old == INT32_MIN || old == x)
-                                break;
-                            h = (h + 1) & (Hs - 1);
-                        }
-                        atomicAdd(hcnt + h, 1u);
-                    }
-                }
-                wave_lds_sync();
-                uint32_t *pk_hi = hpos, *pk_lo = hpos + 64; /* (hpos is 4-byte aligned) */
-                uint32_t dd = 0;
-                for (uint32_t j0 = 0; j0 < Hs; j0 += 64) {
-                    const int32_t kk = hk[j0 + lane];
-                    const bool f = kk != INT32_MIN;
-                    const uint64_t bm = __ballot(f);
-                    const uint32_t at = dd + lanes_below(bm);
-                    if (f && at < 64) {
-                        pk_hi[at] = (uint32_t)kk ^ 0x80000000u;
-                        pk_lo[at] = hcnt[j0 + lane];
-                    }
-                    dd += (uint32_t)__popcll(bm);
-                }
-                if (dd <= 64) {
-                    wave_lds_sync();
-                    uint64_t x = lane < dd ? (uint64_t)pk_hi[lane] << 32 | pk_lo[lane] : ~0ull; /* padding last */
-                    for (uint32_t k = 2; k <= 64; k <<= 1)
-                        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                            const uint64_t y = (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)x, j) |
-                                               (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)(x >> 32), j) << 32;
-                            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-                            x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
-                        }
-                    if (lane < dd)
-                        o[lane] = kgx_otu{(int32_t)((uint32_t)(x >> 32) ^ 0x80000000u), (int32_t)(uint32_t)x};
-                }
-                if (lane == 0)
-                    n_otu = dd <= 64 ? dd : ~0u;
-            }
-            __syncthreads();
-            d = n_otu;
-        }
         if (d == ~0u) {
             /* past KREG distinct values: the flagged hits' OTUs counted in an
              * LDS hash (256 FJ slots: one per window at least, so it never

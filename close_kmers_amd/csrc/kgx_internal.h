@@ -151,6 +151,10 @@ hipError_t launch_plan(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_resid
  * plan_look_bytes(n_seq) bytes, zero-filled when allocated and left zero by
  * every launch; tile owners past max_tiles are never written */
 size_t plan_look_bytes(uint32_t n_seq);
+/* the plan by one workgroup, for batches of at most 2^18 sequences */
+hipError_t launch_plan_one(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                           uint32_t *tile_seq, uint32_t tile_windows, uint64_t max_tiles, uint32_t *status,
+                           hipStream_t stream);
 hipError_t launch_plan_fused(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
                              uint32_t *tile_seq, uint32_t tile_windows, uint64_t max_tiles, void *look,
                              uint32_t *status, hipStream_t stream);

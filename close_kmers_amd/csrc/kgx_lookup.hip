@@ -338,6 +338,83 @@ __global__ __launch_bounds__(256) void plan_fused_kernel(const uint64_t *__restr
         __hip_atomic_store(&ctl[threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* The plan of a batch of up to PLAN_ONE_MAX sequences in ONE workgroup of
+ * 1,024 threads (option plan_fused 2): thread t takes a contiguous run of
+ * sequences, the runs' window counts are scanned across the workgroup, and
+ * each thread writes its sequences' window bases and tile owners -- one
+ * launch, nothing to wait on, one CU beside the probe.  Bad offsets empty the
+ * batch as the three kernels do. */
+constexpr uint32_t PLAN_ONE_MAX = 1u << 18;
+
+__global__ __launch_bounds__(1024) void plan_one_kernel(const uint64_t *__restrict__ seq_off, uint32_t n,
+                                                        uint64_t n_residues, uint64_t *__restrict__ wbase,
+                                                        uint32_t *__restrict__ tile_seq, uint32_t tile_windows,
+                                                        uint64_t max_tiles, uint32_t *__restrict__ status)
+{
+    __shared__ uint64_t wsum[16];
+    __shared__ uint32_t wmax[16];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t s0 = min(n, t * per), s1 = min(n, s0 + per);
+    const uint64_t first = seq_off[0], last = seq_off[n];
+    bool bad = last < first || last - first > n_residues;
+    uint64_t w = 0;
+    uint32_t m = 0;
+    for (uint32_t s = s0; s < s1; s++) {
+        const uint64_t a = seq_off[s], b = seq_off[s + 1];
+        bad |= b < a;
+        const uint64_t ww = b >= a ? windows_of(b - a) : 0;
+        w += ww;
+        m = max(m, (uint32_t)min<uint64_t>(ww, 0xFFFFFFFFull));
+    }
+    bad = __syncthreads_or(bad);
+    /* exclusive scan of the threads' windows: waves, then the 16 wave sums */
+    uint64_t x = w;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint64_t y = __shfl_up(x, off);
+        if (lane >= off)
+            x += y;
+    }
+    for (uint32_t off = 32; off; off >>= 1)
+        m = max(m, (uint32_t)__shfl_xor((int)m, (int)off));
+    if (lane == 63)
+        wsum[wave] = x;
+    if (lane == 0)
+        wmax[wave] = m;
+    __syncthreads();
+    uint64_t before = 0, total = 0;
+    uint32_t mm = 0;
+    for (uint32_t i = 0; i < 16; i++) {
+        before += i < wave ? wsum[i] : 0;
+        total += wsum[i];
+        mm = max(mm, wmax[i]);
+    }
+    uint64_t wb = bad ? 0 : before + x - w;
+    for (uint32_t s = s0; s < s1; s++) {
+        const uint64_t we = wb + (bad ? 0 : windows_of(seq_off[s + 1] - seq_off[s]));
+        wbase[s] = wb;
+        for (uint64_t k = (wb + tile_windows - 1) / tile_windows; k * tile_windows < we && k < max_tiles; k++)
+            tile_seq[k] = s;
+        wb = we;
+    }
+    if (t == 0) {
+        wbase[n] = bad ? 0 : total;
+        status[0] = bad ? 1u : 0u;
+        status[1] = bad ? 0u : mm;
+    }
+}
+
+hipError_t launch_plan_one(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,
+                           uint32_t *tile_seq, uint32_t tile_windows, uint64_t max_tiles, uint32_t *status,
+                           hipStream_t stream)
+{
+    if (n_seq > PLAN_ONE_MAX)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(plan_one_kernel, dim3(1), dim3(1024), 0, stream, seq_off, n_seq, n_residues, wbase, tile_seq,
+                       tile_windows, max_tiles, status);
+    return hipGetLastError();
+}
+
 size_t plan_look_bytes(uint32_t n_seq) { return ((size_t)n_seq / PLAN_TILE + 1) * sizeof(uint64_t) + 16; }
 
 hipError_t launch_plan_fused(const uint64_t *seq_off, uint32_t n_seq, uint64_t n_residues, uint64_t *wbase,

@@ -379,7 +379,7 @@ struct kgx_ctx {
     kgx::DevBuf plan_status;
     /* the one-launch plan's look-back states (zero between launches) */
     kgx::DevBuf plan_look;
-    int plan_fused = 1; /* option "plan_fused": 0 = the three plan kernels */
+    int plan_fused = 0; /* option "plan_fused": 0 = three kernels, 1 = one look-back launch, 2 = one workgroup */
     kgx::PinnedVec<uint32_t> h_plan_status;
     /* current plan */
     uint32_t n_seq = 0;

@@ -1025,8 +1025,8 @@ int kgx_ctx_set_option(kgx_ctx *c, const char *name, int64_t value)
         return KGX_OK;
     }
     if (n == "plan_fused") {
-        if (value != 0 && value != 1)
-            return fail(KGX_EINVAL, "plan_fused must be 0 or 1");
+        if (value < 0 || value > 2)
+            return fail(KGX_EINVAL, "plan_fused must be 0, 1 or 2");
         c->plan_fused = (int)value;
         return KGX_OK;
     }
@@ -1292,7 +1292,12 @@ int kgx_stage_plan(kgx_ctx *c, const uint64_t *d_off, uint32_t n_seq, uint64_t n
     int rc = kgx::plan_reserve(c, d_off, n_seq, n_residues);
     if (rc)
         return rc;
-    if (c->plan_fused) {
+    if (c->plan_fused == 2 && n_seq <= (1u << 18)) {
+        HIP_TRY(launch_plan_one(d_off, n_seq, n_residues, c->wbase.as<uint64_t>(), c->tile_seq.as<uint32_t>(),
+                                c->tile_windows, c->max_tiles, c->plan_status.as<uint32_t>(), c->stream));
+        return KGX_OK;
+    }
+    if (c->plan_fused == 1) {
         /* new states start at zero (every launch leaves them so); a grown
          * buffer may come back at the old address, so its capacity says */
         const size_t had = c->plan_look.cap;

@@ -122,7 +122,7 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
  * meet through bl / br, indexed by rank, as above) instead of the reads and
  * writes of `a` around every move; the median of three, the pivot and the
  * range stack (lane k holds entry k) are lane reads; and the final insertion
- * sort -- stable -- is a bitonic sort by (count, position).  Same steps, so
+ * sort -- stable -- places each element by counting over lane reads.  Same steps, so
  * the same result as lstd_sort_wave64 and the serial replay.  a: the n <= 64
  * pairs in LDS (read at the start, written at the end); bl, br: 64 elements
  * of scratch each. */
@@ -208,27 +208,16 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
             }
         }
     }
-    /* __final_insertion_sort: a stable sort of what the loop left, so a
-     * sort by (key, position) -- a total order, one answer -- which the
-     * register bitonic network gives in 21 lane exchanges instead of n
-     * serial lane reads per element.  key(v) orders as comp does: comp is
-     * by count, larger first (less_second, kguts.h:214-218). */
-    uint64_t x = lane < n ? (uint64_t)(0x7FFFFFFFu - (uint32_t)v.count) << 32 | lane : ~0ull; /* padding last */
-    int32_t pay = v.otu_index;
-    for (uint32_t k = 2; k <= 64; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t y = (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)x, j) |
-                               (uint64_t)(uint32_t)xor_lane((int32_t)(uint32_t)(x >> 32), j) << 32;
-            const int32_t py = xor_lane(pay, j);
-            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-            const bool take = keep_min ? y < x : x < y;
-            if (take) {
-                x = y;
-                pay = py;
-            }
-        }
+    /* __final_insertion_sort: stable, so by counting (the others' elements
+     * by lane reads; a register bitonic sort by (count, position) measured
+     * slower, its 21 dependent lane exchanges 3 us even for 3 pairs) */
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < n; j++) {
+        const kgx_otu w = otu_lane(v, j);
+        pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
+    }
     if (lane < n)
-        a[lane] = kgx_otu{pay, (int32_t)(0x7FFFFFFFu - (uint32_t)(x >> 32))};
+        a[pos] = v;
     wave_lds_sync();
 }
 

@@ -303,8 +303,10 @@ void *kgx_ctx_stream(kgx_ctx *ctx);
  * index when it has one / the reference slots (in-process A/Bs);
  * "probe_nt" 0 (default) / 1 = the line probe writes its hit records and mask
  * with non-temporal stores;
- * "plan_fused" 1 (default) = the plan (window bases, tile owners) in one
- * launch, a decoupled look-back; 0 = three launches (reduce, scan, fill);
+ * "plan_fused" 0 (default) = the plan (window bases, tile owners) in three
+ * launches (reduce, scan, fill); 1 = one launch, a decoupled look-back over
+ * workgroups (measured slower beside a probe: its waiting workgroups);
+ * 2 = one workgroup of 1,024 threads (batches of up to 2^18 sequences);
  * "probe_serialize" 1 (default) / 0: this context's probes wait for the
  * image's previous probe (any context), so that probes run back to back and
  * the other kernels of the contexts overlap them;

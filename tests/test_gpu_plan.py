@@ -1,6 +1,7 @@
 """The plan (window bases + tile owners, kgx_stage_plan) in one launch
-(plan_fused_kernel: a decoupled look-back over workgroups of 1,024
-sequences) against the three-kernel plan (option plan_fused 0), on batches
+(option plan_fused 1: a decoupled look-back over workgroups of 1,024
+sequences; 2: one workgroup, up to 2^18 sequences, past that the three
+kernels) against the three-kernel plan (option plan_fused 0), on batches
 of 1 .. 3M sequences with empty, short and long sequences, run back to back
 on one context so that every launch starts from the states the previous one
 left: the same window bases, and the same hits and calls through the whole
@@ -41,14 +42,16 @@ def _device_pass(L, ctx, d_res, d_off, n, n_res, want=3):
     return wb, abi.BatchResult(r, want)
 
 
-def test_fused_plan_matches_three_kernels(gpu):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_fused_plan_matches_three_kernels(gpu, variant):
     spec, table = synthetic_table(40000)
     L = abi.lib()
     rng = np.random.default_rng(8)
     with abi.Image.from_table(table, device=0) as img, abi.Context(img) as fused, abi.Context(img) as three:
         three.set_option("plan_fused", 0)
+        fused.set_option("plan_fused", variant)
         shapes = [(1, 300), (1023, 40), (1024, 40), (1025, 40), (5000, 9), (70000, 60), (3_000_000, 24),
-                  (200, 3000), (4097, 300), (1, 0), (2048, 0), (900_000, 30)]
+                  (200, 3000), (4097, 300), (1, 0), (2048, 0), (900_000, 30), (250_000, 20)]
         for n, max_len in shapes:
             res, off = _batch(rng, spec, n, max_len)
             n_res = int(off[-1])
