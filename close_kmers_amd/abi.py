@@ -261,6 +261,7 @@ SIGNATURES = {
     "kgx_pool_process_batch": (_INT, [_P, ctypes.POINTER(Params), _P, _P, _U32, _U32, ctypes.POINTER(Result)]),
     "kgx_shard_cuts": (_INT, [_P, _U32, _U32, _P]),
     "kgx_pool_numa_node": (_INT, [_P, _U32]),
+    "kgx_format_g6": (_SZ, [ctypes.c_float, ctypes.c_char_p, _SZ]),
     "kgx_pool_map_select": (_INT, [_P, _U32, _P, _U32, _P]),
     "kgx_device_numa_node": (_INT, [_INT]),
     "kgx_numa_node_cpus": (_INT, [_INT, _P, _U32]),

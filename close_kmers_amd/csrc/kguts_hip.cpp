@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <charconv>
+#include <cmath>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -549,15 +550,47 @@ static void append_i64(std::string &out, long long v)
     out.append(b, r.ptr);
 }
 
+/* operator<<(float) with precision 6 and no floatfield is "%.*g" of the
+ * value widened to double (libstdc++ num_put::_M_insert_float); to_chars in
+ * general format with a precision is specified as printf's %.6g, at a quarter
+ * of snprintf's cost.  Integral values below 1e6 in magnitude -- the scores
+ * (counts) and the zeros of most output lines -- print as %.6g prints them,
+ * their digits (and "-0" for negative zero), without the float formatter.
+ * kgx_format_g6 exports it; tests/test_abi_host.py checks it against
+ * printf's %.6g. */
+static size_t format_g6(char *b, size_t cap, float v)
+{
+    const double d = (double)v;
+    if (d == 0.0) {
+        if (std::signbit(d)) {
+            b[0] = '-';
+            b[1] = '0';
+            return 2;
+        }
+        b[0] = '0';
+        return 1;
+    }
+    if (d > -1e6 && d < 1e6 && d == (double)(long long)d)
+        return (size_t)(std::to_chars(b, b + cap, (long long)d).ptr - b);
+    return (size_t)(std::to_chars(b, b + cap, d, std::chars_format::general, 6).ptr - b);
+}
+
 static void append_f32(std::string &out, float v)
 {
-    /* operator<<(float) with precision 6 and no floatfield is "%.*g" of the
-     * value widened to double (libstdc++ num_put::_M_insert_float); to_chars
-     * in general format with a precision is specified as printf's %.6g (and
-     * checked against it on 2M values), at a quarter of snprintf's cost */
     char b[48];
-    const auto r = std::to_chars(b, b + sizeof b, (double)v, std::chars_format::general, 6);
-    out.append(b, r.ptr);
+    out.append(b, format_g6(b, sizeof b, v));
+}
+
+extern "C" size_t kgx_format_g6(float v, char *out, size_t cap)
+{
+    char b[48];
+    const size_t n = format_g6(b, sizeof b, v);
+    if (out && cap) {
+        const size_t k = std::min(n, cap - 1);
+        std::memcpy(out, b, k);
+        out[k] = 0;
+    }
+    return n;
 }
 
 void KmerGuts::append_call(std::string &out, const KmerCall &c) const

@@ -649,6 +649,11 @@ int kgx_find_best_call(const kgx_call *calls, size_t n_calls, const char *const 
                        float *score, float *weighted_score, float *score_offset,
                        int *score_offset_set);
 
+/* a float as the reference's iostreams print it (operator<< at the default
+ * precision: printf's %.6g of the value widened to double), NUL-terminated
+ * into out (cap bytes); returns the full length.  Host only. */
+size_t kgx_format_g6(float v, char *out, size_t cap);
+
 /* find_best_call for many sequences at once, on the context's device:
  * sequence s owns calls[call_offsets[s] .. call_offsets[s+1]) (host arrays);
  * out[n_seq] receives each decision (kgx_best_call).  Synchronous. */

@@ -146,3 +146,24 @@ def test_numa_node_cpus(kgx):
         seen.update(cpus)
     if nodes:
         assert seen == aff & set().union(*[set(kgx.numa_node_cpus(nd)) for nd in nodes])
+
+
+def test_format_g6_matches_printf(kgx):
+    """kgx_format_g6 -- how the handlers print floats (operator<< at the
+    default precision = printf's %.6g of the value widened to double), with
+    its fast path for integral values below 1e6 -- against Python's %-format
+    (C printf semantics) on edge values and 300k random floats."""
+    import ctypes
+    rng = np.random.default_rng(6)
+    vals = [0.0, -0.0, 1.0, -1.0, 999999.0, -999999.0, 1e6, -1e6, 1234567.0, 0.5, 1e-5, 123456.5,
+            3.4028235e38, 1.17549435e-38, 1e-45, float("inf"), float("-inf"), 2.0 ** 24, 16777217.0]
+    vals += rng.integers(-2_000_000, 2_000_000, 100_000).astype(np.float32).tolist()
+    vals += (rng.standard_normal(100_000) * 10.0 ** rng.integers(-8, 9, 100_000)).astype(np.float32).tolist()
+    vals += rng.integers(0, 300, 100_000).astype(np.float32).tolist()
+    buf = ctypes.create_string_buffer(64)
+    L = kgx.lib()
+    for v in vals:
+        f = float(np.float32(v))
+        n = L.kgx_format_g6(f, buf, len(buf))
+        want = "%.6g" % f
+        assert buf.value.decode() == want and n == len(want), (v, buf.value, want)
