@@ -122,7 +122,8 @@ __device__ void lstd_sort_wave64(T *a, uint32_t n, C comp, T *buf, LstdPart *sta
  * meet through bl / br, indexed by rank, as above) instead of the reads and
  * writes of `a` around every move; the median of three, the pivot and the
  * range stack (lane k holds entry k) are lane reads; and the final insertion
- * sort -- stable -- places each element by counting over lane reads.  Same steps, so
+ * sort -- stable -- places each element by counting over lane reads within
+ * its final range of at most 16.  Same steps, so
  * the same result as lstd_sort_wave64 and the serial replay.  a: the n <= 64
  * pairs in LDS (read at the start, written at the end); bl, br: 64 elements
  * of scratch each. */
@@ -138,6 +139,8 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
     const uint32_t lane = lane_id();
     const uint64_t le = lanes_le(lane), below = le & ~(1ull << lane);
     kgx_otu v = lane < n ? a[lane] : kgx_otu{0, 0};
+    uint64_t marks = 1; /* bit f: [f, next mark) is a range the loop left (<= 16 elements) */
+    bool heaped = false;
     if (n > 16) {
         /* the range stack, entry k in lane k */
         int32_t sf = 0, sl = (int32_t)n, sd = 2 * (31 - (int)__builtin_clz(n));
@@ -158,6 +161,7 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
                     if (lane < n)
                         v = a[lane];
                     wave_lds_sync();
+                    heaped = true;
                     break;
                 }
                 --depth;
@@ -206,15 +210,34 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
                 sp++;
                 l = cut;
             }
+            marks |= 1ull << f; /* [f, l) is final */
         }
     }
-    /* __final_insertion_sort: stable, so by counting (the others' elements
-     * by lane reads; a register bitonic sort by (count, position) measured
-     * slower, its 21 dependent lane exchanges 3 us even for 3 pairs) */
+    /* __final_insertion_sort: stable, so by counting.  No element moves
+     * across the boundary of a range the loop left (every element of an
+     * earlier range is not greater than every element of a later one), so
+     * each counts only within its own range of at most 16: 16 independent
+     * lane reads (a register bitonic sort by (count, position) measured
+     * slower, its 21 dependent exchanges 3 us even for 3 pairs).  After a
+     * heap sort (a range past 16 elements, rare) every element counts over
+     * all n. */
     uint32_t pos = 0;
-    for (uint32_t j = 0; j < n; j++) {
-        const kgx_otu w = otu_lane(v, j);
-        pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
+    if (heaped) {
+        for (uint32_t j = 0; j < n; j++) {
+            const kgx_otu w = otu_lane(v, j);
+            pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
+        }
+    } else {
+        const uint32_t lo = (uint32_t)hibit(marks & le);
+        const uint64_t up = marks & ~le;
+        const uint32_t hi = up ? min(n, lowbit(up)) : n;
+        pos = lo;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t j = lo + k;
+            const kgx_otu w{__shfl(v.otu_index, (int)min(j, 63u)), __shfl(v.count, (int)min(j, 63u))};
+            pos += j < hi && (comp(w, v) || (j < lane && !comp(v, w))) ? 1u : 0u;
+        }
     }
     if (lane < n)
         a[pos] = v;
