@@ -1283,12 +1283,15 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
     const int mode = family_mode_ ? KGX_ROLLUP_FAMILY : KGX_ROLLUP_PEG;
     const uint32_t want = want_calls ? KGX_WANT_BEST : 0u;
     kgx_rollup_result ru;
-    /* the pass and the rollup enqueued together, one host wait (kgx_lookup),
-     * when the map is on the worker's device; KGX_LOOKUP_ONE_WAIT=0: the pass
-     * (the small-batch path) and then the rollup, a wait each */
+    /* the pass (the small-batch path for a piece of up to 2M residues) and
+     * then the rollup, a wait each; KGX_LOOKUP_ONE_WAIT=1: both enqueued
+     * together with one host wait (kgx_lookup) when the map is on the
+     * worker's device -- measured slower for 1-MiB bodies (HTTP family
+     * /lookup at 16 clients 6.0e9 vs 6.8e9 residues/s, r8: its general pass
+     * costs more device time than the small-batch path saves in waits) */
     static const bool one_wait = [] {
         const char *e = std::getenv("KGX_LOOKUP_ONE_WAIT");
-        return !e || std::atoi(e) != 0;
+        return e && std::atoi(e) != 0;
     }();
     int rc;
     if (one_wait && kgx_kmap_device(map) == kgx_image_device(kg.image_->handle())) {

@@ -604,17 +604,26 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         uint32_t d = n_otu;
         if (d == ~0u) {
             /* past KREG distinct values: the flagged hits' OTUs counted in an
-             * LDS hash (256 FJ slots: one per window at least, so it never
-             * fills), the distinct (value, count) pairs compacted, then
+             * LDS hash (at most 256 FJ slots: one per window at least, so it
+             * never fills), the distinct (value, count) pairs compacted, then
              * sorted by value -- one wave's register bitonic network up to 64
              * pairs, a block network beyond.  (r4o: a bitonic sort of every
              * flagged hit's value, then runs -- 6.1 us of the 36-OTU tally.) */
             constexpr uint32_t H = 256 * FJ;
-            /* the flagged values first, compacted in hit order into hpos (the
-             * records in hrec are dead then), so the hash can use hrec */
+            /* the hash's slots: at least twice the hits (so it stays sparse),
+             * at most H; its scans below cost a barrier per 256 slots */
+            uint32_t Hs = 256;
+            while (Hs < 2 * nh && Hs < H)
+                Hs <<= 1;
+            /* the records end before the hash (the second half of hrec) when
+             * they fill at most half of it: the hash counts straight from
+             * them.  Else the flagged values first, compacted in hit order
+             * into hpos (the records in hrec are dead then), so the hash can
+             * use hrec */
+            const bool direct = nh <= 128 * FJ;
             int32_t *v = reinterpret_cast<int32_t *>(hpos);
             uint32_t m = 0;
-            for (uint32_t j = 0; j < (nh + 255) / 256; j++) {
+            for (uint32_t j = 0; !direct && j < (nh + 255) / 256; j++) {
                 const uint32_t i = t + 256 * j;
                 const bool f = i < nh && oflag[i];
                 const int32_t x = f ? (int32_t)HF::otu(hrec[i], hrec[i]) : 0;
@@ -635,19 +644,21 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             }
             int32_t *hk = reinterpret_cast<int32_t *>(hrec) + 2 * 256 * FJ; /* past the pairs */
             uint32_t *hcnt = reinterpret_cast<uint32_t *>(hrec) + 3 * 256 * FJ;
-            for (uint32_t i = t; i < H; i += 256) {
+            for (uint32_t i = t; i < Hs; i += 256) {
                 hk[i] = INT32_MIN; /* OTUs are -1 .. 2^21 - 2 */
                 hcnt[i] = 0;
             }
             __syncthreads();
-            for (uint32_t i = t; i < m; i += 256) {
-                const int32_t x = v[i];
-                uint32_t h = ((uint32_t)x * 0x9E3779B1u) & (H - 1);
+            for (uint32_t i = t; i < (direct ? nh : m); i += 256) {
+                if (direct && !oflag[i])
+                    continue;
+                const int32_t x = direct ? (int32_t)HF::otu(hrec[i], hrec[i]) : v[i];
+                uint32_t h = ((uint32_t)x * 0x9E3779B1u) & (Hs - 1);
                 for (;;) {
                     const int32_t old = atomicCAS(hk + h, INT32_MIN, x);
                     if (old == INT32_MIN || old == x)
                         break;
-                    h = (h + 1) & (H - 1);
+                    h = (h + 1) & (Hs - 1);
                 }
                 atomicAdd(hcnt + h, 1u);
             }
@@ -656,7 +667,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
              * so that unsigned order is the map's key order */
             uint64_t *pk = reinterpret_cast<uint64_t *>(o);
             d = 0;
-            for (uint32_t j = 0; j < H / 256; j++) {
+            for (uint32_t j = 0; j < Hs / 256; j++) {
                 const uint32_t i = t + 256 * j;
                 const bool f = hk[i] != INT32_MIN;
                 const uint64_t bm = __ballot(f);

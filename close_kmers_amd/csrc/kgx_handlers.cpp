@@ -628,6 +628,13 @@ KmerRequestRouter::KmerRequestRouter(const Options &opt)
     /* every device gets at least one worker; worker w on slot w % n (kgx_dispatch.h) */
     for (size_t w = 0; w < picker_.n_workers(); w++)
         pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, images_[picker_.slot_of(w)]));
+    /* KGX_SERVER_PROBE_SERIALIZE=0: the workers' probes are not chained
+     * behind one another (context option probe_serialize): a request piece's
+     * probe may then overlap another's instead of waiting for it */
+    if (const char *e = std::getenv("KGX_SERVER_PROBE_SERIALIZE"))
+        for (auto &kg : pool_)
+            if (int rc = kgx_ctx_set_option(kg->ctx(), "probe_serialize", std::atoi(e) != 0 ? 1 : 0))
+                throw Error(rc, std::string("probe_serialize: ") + kgx_last_error());
     /* kserver.cc:40-130: the family DB goes into the root mapping, on the first device */
     auto root = std::make_shared<KmerPegMapping>(devs[0]);
     mapping_map_[""] = Mapping{root, std::make_shared<std::shared_mutex>()};

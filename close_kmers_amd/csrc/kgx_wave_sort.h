@@ -222,7 +222,7 @@ __device__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl
      * heap sort (a range past 16 elements, rare) every element counts over
      * all n. */
     uint32_t pos = 0;
-    if (heaped) {
+    if (heaped || n <= 16) { /* (up to 16: n uniform lane reads beat 16 lane exchanges) */
         for (uint32_t j = 0; j < n; j++) {
             const kgx_otu w = otu_lane(v, j);
             pos += comp(w, v) || (j < lane && !comp(v, w)) ? 1u : 0u;
