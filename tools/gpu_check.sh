@@ -26,7 +26,7 @@ timeout -k 10 600 python3 tools/bench_matrix.py $NOCPU > "$OUT/bench_matrix.json
 timeout -k 10 900 python3 tools/bench_fq.py $NOCPU > "$OUT/bench_fq.json" 2> "$OUT/bench_fq.err"
 timeout -k 10 600 python3 tools/bench_server.py > "$OUT/bench_server.json" 2> "$OUT/bench_server.err"
 timeout -k 10 900 python3 tools/bench_server.py --families 100000 --path "/lookup?family_mode=1&find_best_match=1" \
-    --clients 1,8,16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
+    --clients 1,8,16 --threads 16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
 fi
 if [ "$PART" != 1 ]; then
 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
