@@ -51,7 +51,8 @@ StageStats &stage_stats()
 
 void StageStats::reset()
 {
-    for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &text_ns, &handle_ns, &send_ns})
+    for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &text_ns, &handle_ns,
+                    &send_ns, &batched_pieces, &batched_passes})
         a->store(0);
 }
 
@@ -61,10 +62,13 @@ std::string StageStats::json() const
     const double r = (double)std::max<uint64_t>(1, requests.load());
     std::snprintf(b, sizeof b,
                   "{\"requests\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, \"gpu_passes\": %llu, "
+                  "\"batched_pieces\": %llu, \"batched_passes\": %llu, "
                   "\"ms_per_request\": {\"recv\": %.4f, \"parse\": %.4f, \"gpu\": %.4f, \"text\": %.4f, \"handle\": %.4f, "
                   "\"send\": %.4f}}\n",
                   (unsigned long long)requests.load(), (unsigned long long)bytes_in.load(),
-                  (unsigned long long)bytes_out.load(), (unsigned long long)gpu_passes.load(), recv_ns.load() / r * 1e-6,
+                  (unsigned long long)bytes_out.load(), (unsigned long long)gpu_passes.load(),
+                  (unsigned long long)batched_pieces.load(), (unsigned long long)batched_passes.load(),
+                  recv_ns.load() / r * 1e-6,
                   parse_ns.load() / r * 1e-6, gpu_ns.load() / r * 1e-6, text_ns.load() / r * 1e-6,
                   handle_ns.load() / r * 1e-6,
                   send_ns.load() / r * 1e-6);
@@ -1198,6 +1202,191 @@ std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m)
     return os;
 }
 
+/* ---- LookupBatcher ------------------------------------------------------- */
+
+struct LookupBatcher::Piece {
+    uint32_t seq0 = 0, n = 0;
+    uint64_t res0 = 0;
+    Out *out = nullptr;
+    int rc = KGX_OK;
+    std::string err;
+    bool done = false;
+};
+
+/* a staging area: pieces' residues and rebased offsets, contiguous, in
+ * pinned host memory (the pass reads them by DMA, no staging copy) */
+struct LookupBatcher::Area {
+    char *res = nullptr;
+    uint64_t *off = nullptr;
+    uint64_t res_used = 0;
+    uint32_t seq_used = 0, copying = 0;
+    std::vector<Piece *> pieces;
+    kgx_kmap *map = nullptr;
+    int mode = 0;
+    kgx_params p{};
+    uint32_t want = 0;
+    ~Area()
+    {
+        if (res)
+            kgx_host_free(res);
+        if (off)
+            kgx_host_free(off);
+    }
+    bool fits(kgx_kmap *m, int md, const kgx_params &q, uint32_t w, uint64_t nres, uint32_t n, uint64_t max_res,
+              uint32_t max_seq) const
+    {
+        if (pieces.empty())
+            return true;
+        return m == map && md == mode && w == want && q.min_hits == p.min_hits && q.max_gap == p.max_gap &&
+               q.order_constraint == p.order_constraint && q.min_weighted_hits == p.min_weighted_hits &&
+               res_used + nres <= max_res && seq_used + n <= max_seq;
+    }
+};
+
+LookupBatcher::LookupBatcher(uint64_t max_residues, uint32_t max_seqs) : max_res_(max_residues), max_seq_(max_seqs)
+{
+    for (auto &a : area_)
+        a.reset(new Area);
+}
+
+LookupBatcher::~LookupBatcher() = default;
+
+void LookupBatcher::run_alone(KmerGuts &kg, kgx_kmap *map, int mode, const kgx_params &p, uint32_t want,
+                              const char *res, const uint64_t *off, uint32_t n, Out &out)
+{
+    kgx_result r;
+    int rc = kgx_process_batch(kg.ctx(), &p, res, off, n, want, &r);
+    if (rc)
+        throw_last(rc, "kgx_process_batch");
+    kgx_rollup_result ru;
+    if ((rc = kgx_kmap_rollup(map, kg.ctx(), mode, &ru)))
+        throw_last(rc, "kgx_kmap_rollup");
+    if (want & KGX_WANT_BEST)
+        out.best.assign(r.best, r.best + n);
+    out.roff.assign(ru.offsets, ru.offsets + n + 1);
+    out.rows.assign(ru.rows, ru.rows + ru.offsets[n]);
+}
+
+void LookupBatcher::run(KmerGuts &kg, kgx_kmap *map, int mode, const kgx_params &p, uint32_t want,
+                        const char *res, const uint64_t *off, uint32_t n, Out &out)
+{
+    const uint64_t nres = n ? off[n] - off[0] : 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    /* alone (no other request inside), too large for an area, or a map the
+     * worker's device cannot roll up in its own pass: the piece's own pass */
+    const bool alone = active_ == 0 && !busy_ && area_[open_]->pieces.empty();
+    if (alone || n == 0 || nres > max_res_ || n > max_seq_ ||
+        kgx_kmap_device(map) != kgx_image_device(kg.image_->handle())) {
+        active_++;
+        lk.unlock();
+        alone_++;
+        try {
+            run_alone(kg, map, mode, p, want, res, off, n, out);
+        } catch (...) {
+            lk.lock();
+            active_--;
+            throw;
+        }
+        lk.lock();
+        active_--;
+        return;
+    }
+    active_++;
+    /* a place in the open area (wait while it holds other parameters or is full) */
+    while (!area_[open_]->fits(map, mode, p, want, nres, n, max_res_, max_seq_))
+        cv_.wait(lk);
+    Area &A = *area_[open_];
+    if (!A.res) { /* first use: both areas' pinned buffers */
+        for (auto &a : area_) {
+            void *r = nullptr, *o = nullptr;
+            if (kgx_host_alloc(max_res_ + 64, &r) || kgx_host_alloc(((uint64_t)max_seq_ + 1) * 8, &o)) {
+                if (r)
+                    kgx_host_free(r);
+                active_--;
+                throw_last(KGX_ENOMEM, "lookup batcher: pinned staging");
+            }
+            a->res = static_cast<char *>(r);
+            a->off = static_cast<uint64_t *>(o);
+        }
+    }
+    Piece pc;
+    pc.seq0 = A.seq_used;
+    pc.res0 = A.res_used;
+    pc.n = n;
+    pc.out = &out;
+    if (A.pieces.empty()) {
+        A.map = map;
+        A.mode = mode;
+        A.p = p;
+        A.want = want;
+    }
+    A.pieces.push_back(&pc);
+    A.seq_used += n;
+    A.res_used += nres;
+    A.copying++;
+    lk.unlock();
+    /* the piece into place (each request copies its own, at once) */
+    std::memcpy(A.res + pc.res0, res + off[0], nres);
+    for (uint32_t i = 0; i < n; i++)
+        A.off[pc.seq0 + i] = pc.res0 + (off[i] - off[0]);
+    lk.lock();
+    A.copying--;
+    cv_.notify_all();
+    Area *mine = &A;
+    while (!pc.done) {
+        /* no pass running and our area complete: lead it, the other area
+         * (empty: its pass is over) opening for the next pieces */
+        if (!busy_ && mine == area_[open_].get() && mine->copying == 0) {
+            busy_ = true;
+            open_ ^= 1;
+            lk.unlock();
+            lead(kg, *mine);
+            lk.lock();
+            for (Piece *q : mine->pieces)
+                q->done = true;
+            mine->pieces.clear();
+            mine->seq_used = 0;
+            mine->res_used = 0;
+            busy_ = false;
+            cv_.notify_all();
+        } else {
+            cv_.wait(lk);
+        }
+    }
+    active_--;
+    if (pc.rc)
+        throw Error(pc.rc, "lookup batcher: " + pc.err);
+}
+
+void LookupBatcher::lead(KmerGuts &kg, Area &a)
+{
+    const uint32_t N = a.seq_used;
+    a.off[N] = a.res_used;
+    kgx_result r;
+    kgx_rollup_result ru;
+    const int rc = kgx_lookup(kg.ctx(), a.map, a.mode, &a.p, a.res, a.off, N, a.want, &r, &ru);
+    passes_++;
+    batched_ += a.pieces.size();
+    stage_stats().batched_passes++;
+    stage_stats().batched_pieces += a.pieces.size();
+    const std::string err = rc ? kgx_last_error() : "";
+    for (Piece *q : a.pieces) {
+        q->rc = rc;
+        if (rc) {
+            q->err = err;
+            continue;
+        }
+        Out &o = *q->out;
+        if (a.want & KGX_WANT_BEST)
+            o.best.assign(r.best + q->seq0, r.best + q->seq0 + q->n);
+        const uint64_t r0 = ru.offsets[q->seq0], r1 = ru.offsets[q->seq0 + q->n];
+        o.roff.resize((size_t)q->n + 1);
+        for (uint32_t i = 0; i <= q->n; i++)
+            o.roff[i] = ru.offsets[q->seq0 + i] - r0;
+        o.rows.assign(ru.rows + r0, ru.rows + r1);
+    }
+}
+
 /* ---- LookupRequest ------------------------------------------------------- */
 
 static bool stoi_param(const std::map<std::string, std::string> &p, const char *k, int &out)
@@ -1294,11 +1483,24 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
         return e && std::atoi(e) != 0;
     }();
     int rc;
-    if (one_wait && kgx_kmap_device(map) == kgx_image_device(kg.image_->handle())) {
+    const kgx_best_call *best = nullptr;
+    const uint64_t *roff = nullptr;
+    const kgx_rollup_row *rows = nullptr;
+    LookupBatcher::Out out;
+    if (batcher_) { /* a pass shared with concurrent requests' pieces */
+        batcher_->run(kg, map, mode, p, want, fw.res, fw.off + w0, n, out);
+        stage_stats().gpu_passes++;
+        best = out.best.data();
+        roff = out.roff.data();
+        rows = out.rows.data();
+    } else if (one_wait && kgx_kmap_device(map) == kgx_image_device(kg.image_->handle())) {
         rc = kgx_lookup(kg.ctx(), map, mode, &p, fw.res, fw.off + w0, n, want, &r, &ru);
         stage_stats().gpu_passes++;
         if (rc)
             throw_last(rc, "kgx_lookup");
+        best = r.best;
+        roff = ru.offsets;
+        rows = ru.rows;
     } else {
         rc = kgx_process_batch(kg.ctx(), &p, fw.res, fw.off + w0, n, want, &r);
         stage_stats().gpu_passes++;
@@ -1307,6 +1509,9 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
         rc = kgx_kmap_rollup(map, kg.ctx(), mode, &ru);
         if (rc)
             throw_last(rc, "kgx_kmap_rollup");
+        best = r.best;
+        roff = ru.offsets;
+        rows = ru.rows;
     }
     stage_stats().gpu_ns += now_ns() - g0;
     StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
@@ -1322,8 +1527,8 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
          * its bucket count kept), so its iteration order is the reference's */
         if (!seq_score_.empty())
             seq_score_.clear();
-        for (uint64_t j = ru.offsets[s]; j < ru.offsets[s + 1]; j++) {
-            const kgx_rollup_row &row = ru.rows[j];
+        for (uint64_t j = roff[s]; j < roff[s + 1]; j++) {
+            const kgx_rollup_row &row = rows[j];
             acc_t &e = seq_score_[row.id];
             e.hit_count = row.hit_count;
             e.hit_total = row.hit_total;
@@ -1333,7 +1538,7 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
             int fi;
             float score, wscore, offs = 0.0f;
             ambig.clear();
-            kg.find_best_call(r.best[s], fi, fn, score, wscore, offs);
+            kg.find_best_call(best[s], fi, fn, score, wscore, offs);
             bool do_ambig = false;
             if (fn.empty()) {
                 fn.assign("hypothetical protein");

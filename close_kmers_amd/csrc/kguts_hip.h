@@ -46,6 +46,8 @@ namespace kgx {
 struct StageStats {
     std::atomic<uint64_t> requests{0}, bytes_in{0}, bytes_out{0}, gpu_passes{0};
     std::atomic<uint64_t> recv_ns{0}, parse_ns{0}, gpu_ns{0}, text_ns{0}, handle_ns{0}, send_ns{0};
+    /* /lookup pieces that shared a pass (LookupBatcher) and those passes */
+    std::atomic<uint64_t> batched_pieces{0}, batched_passes{0};
     void reset();
     std::string json() const;
 };
@@ -436,10 +438,66 @@ std::ostream &operator<<(std::ostream &os, const FamilyMapper::best_match_t &m);
  * first-touch order, and the selection and output run on the host in order.  No family
  * reps DB is loaded, so find_reps prints only the "///" separators.
  */
+/*
+ * LookupBatcher: the device side of concurrent /lookup requests' pieces in
+ * shared passes -- the reference's pool runs one chunk per worker
+ * (lookup_request.cc:153-172); here, while other requests are in flight, a
+ * piece is copied into the open staging area (pinned, two areas: one
+ * filling while the other's pass runs) and the first waiting request whose
+ * area is complete leads ONE pass + rollup (kgx_lookup) for every piece in
+ * it on its own worker's context; each piece then gets its own best calls
+ * and rollup rows back.  A request alone (nothing in flight), a piece too
+ * large for an area, or a map on another device than the worker runs its
+ * own pass (the small-batch path + kgx_kmap_rollup).  Sequences are
+ * independent, so the results are the same bytes either way.
+ */
+class LookupBatcher {
+public:
+    /* pieces of a pass: at most max_residues residues and max_seqs sequences */
+    explicit LookupBatcher(uint64_t max_residues = 16u << 20, uint32_t max_seqs = 1u << 20);
+    ~LookupBatcher();
+    LookupBatcher(const LookupBatcher &) = delete;
+    LookupBatcher &operator=(const LookupBatcher &) = delete;
+    /* a piece's device results: best calls (want KGX_WANT_BEST), rollup
+     * offsets (n + 1, from 0) and rows */
+    struct Out {
+        std::vector<kgx_best_call> best;
+        std::vector<uint64_t> roff;
+        std::vector<kgx_rollup_row> rows;
+    };
+    /* the n sequences res[off[i], off[i+1]) through a pass (throws kgx::Error) */
+    void run(KmerGuts &kg, kgx_kmap *map, int mode, const kgx_params &p, uint32_t want, const char *res,
+             const uint64_t *off, uint32_t n, Out &out);
+    /* passes run, pieces they carried, pieces run alone */
+    uint64_t passes() const { return passes_; }
+    uint64_t batched() const { return batched_; }
+    uint64_t alone() const { return alone_; }
+    /* a piece's own pass (the small-batch path, then kgx_kmap_rollup) */
+    static void run_alone(KmerGuts &kg, kgx_kmap *map, int mode, const kgx_params &p, uint32_t want,
+                          const char *res, const uint64_t *off, uint32_t n, Out &out);
+
+private:
+    struct Piece;
+    struct Area;
+    void lead(KmerGuts &kg, Area &a);
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::unique_ptr<Area> area_[2];
+    int open_ = 0;
+    bool busy_ = false;
+    int active_ = 0; /* requests inside run() */
+    uint64_t max_res_;
+    uint32_t max_seq_;
+    std::atomic<uint64_t> passes_{0}, batched_{0}, alone_{0};
+};
+
 class LookupRequest {
 public:
     LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
                   const std::map<std::string, std::string> &params);
+    /* the device side through a batcher shared with concurrent requests
+     * (null: every piece its own pass) */
+    void set_batcher(LookupBatcher *b) { batcher_ = b; }
     void process_work(KmerGuts &kg, const std::vector<std::pair<std::string, std::string>> &work,
                       std::ostream &os);
 
@@ -465,6 +523,7 @@ private:
     bool find_reps_ = false;
     unsigned long target_genus_id_ = 0;
     std::unordered_map<KmerPegMapping::encoded_id_t, FamilyMapper::sequence_accumulated_score_t> seq_score_;
+    LookupBatcher *batcher_ = nullptr;
 };
 
 /*

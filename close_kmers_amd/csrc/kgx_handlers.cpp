@@ -628,6 +628,10 @@ KmerRequestRouter::KmerRequestRouter(const Options &opt)
     /* every device gets at least one worker; worker w on slot w % n (kgx_dispatch.h) */
     for (size_t w = 0; w < picker_.n_workers(); w++)
         pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, images_[picker_.slot_of(w)]));
+    /* concurrent /lookup pieces share device passes (LookupBatcher);
+     * KGX_LOOKUP_BATCH=0: every piece its own pass */
+    if (const char *e = std::getenv("KGX_LOOKUP_BATCH"); !e || std::atoi(e) != 0)
+        lookup_batcher_.reset(new LookupBatcher());
     /* KGX_SERVER_PROBE_SERIALIZE=0: the workers' probes are not chained
      * behind one another (context option probe_serialize): a request piece's
      * probe may then overlap another's instead of waiting for it */
@@ -939,6 +943,7 @@ std::string KmerRequestRouter::handle(const HttpRequest &req, bool *quit)
             }
             os << header(ver, 200, "OK") << "\n";
             LookupRequest lr(mapping, family_mode_, req.parameters);
+            lr.set_batcher(lookup_batcher_.get());
             lr.process_flat(*kg, flat.res.data(), flat.off.data(), flat.ids.data(), flat.id_off.data(), flat.size(),
                             os);
             return os.str();

@@ -232,6 +232,7 @@ private:
     std::mutex mapping_mu_; /* the mapping map itself */
     std::map<std::string, Mapping> mapping_map_;
     ForkJoin fj_{kHelpers};
+    std::unique_ptr<LookupBatcher> lookup_batcher_; /* /lookup pieces of concurrent requests, shared passes */
     std::atomic<int> query_in_flight_{0};
 };
 

@@ -319,6 +319,57 @@ def test_family_mode_lookup_and_fq_routes_match_golden(gpu):
         srv.close()
 
 
+@pytest.mark.gpu
+def test_concurrent_family_lookups_share_passes_and_match_golden(gpu):
+    """Family /lookup requests on 12 connections at once (6 workers): the
+    pieces of requests in flight share device passes (LookupBatcher: one
+    staging area fills while the other's pass runs) and every response is the
+    golden text byte for byte, whatever it shared a pass with; /server_stats
+    shows pieces carried by shared passes.  KGX_LOOKUP_BATCH=0 gives the same
+    bytes with every piece alone."""
+    import json
+    import threading
+    d = os.path.join(GOLDEN, "lookup")
+    fasta = open(os.path.join(d, "input.fasta"), "rb").read()
+    cases = [f for f in _cases("lookup") if parse_case(f)[1].startswith("fam_")]
+    assert len(cases) >= 3
+    for batch in ("1", "0"):
+        before = os.environ.get("KGX_LOOKUP_BATCH")
+        os.environ["KGX_LOOKUP_BATCH"] = batch
+        try:
+            srv = Server(os.path.join(d, "data"), family_db=True, threads=6)
+        finally:
+            if before is None:
+                del os.environ["KGX_LOOKUP_BATCH"]
+            else:
+                os.environ["KGX_LOOKUP_BATCH"] = before
+        errors = []
+
+        def run(k):
+            for i in range(6):
+                fname = cases[(k + i) % len(cases)]
+                got = srv.request("POST", "/lookup?" + _query_string(parse_case(fname)[1]), fasta)
+                if got != HEADER + open(os.path.join(d, fname), "rb").read():
+                    errors.append(fname)
+
+        try:
+            srv.request("GET", "/server_stats?reset=1")
+            ths = [threading.Thread(target=run, args=(k,)) for k in range(12)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            assert not errors, (batch, errors[:4])
+            st = json.loads(srv.request("GET", "/server_stats").split(b"\n\n", 1)[1])
+            print(batch, st)
+            if batch == "1":
+                assert st["batched_pieces"] >= st["batched_passes"] > 0, st
+            else:
+                assert st["batched_pieces"] == 0, st
+        finally:
+            srv.close()
+
+
 def _big_body(seed=99, mib=5):
     import numpy as np
     from helpers import random_protein
