@@ -628,9 +628,12 @@ KmerRequestRouter::KmerRequestRouter(const Options &opt)
     /* every device gets at least one worker; worker w on slot w % n (kgx_dispatch.h) */
     for (size_t w = 0; w < picker_.n_workers(); w++)
         pool_.emplace_back(new KmerGuts(opt_.kmer_data_dir, images_[picker_.slot_of(w)]));
-    /* concurrent /lookup pieces share device passes (LookupBatcher);
-     * KGX_LOOKUP_BATCH=0: every piece its own pass */
-    if (const char *e = std::getenv("KGX_LOOKUP_BATCH"); !e || std::atoi(e) != 0)
+    /* KGX_LOOKUP_BATCH=1: concurrent /lookup pieces share device passes
+     * (LookupBatcher).  Off by default: at 16 clients 6.3e9 vs 7.5e9
+     * residues/s with every piece its own pass (r8: ~5 pieces per shared pass,
+     * but one pass at a time and its general path serialise what 16 workers'
+     * small passes overlap) */
+    if (const char *e = std::getenv("KGX_LOOKUP_BATCH"); e && std::atoi(e) != 0)
         lookup_batcher_.reset(new LookupBatcher());
     /* KGX_SERVER_PROBE_SERIALIZE=0: the workers' probes are not chained
      * behind one another (context option probe_serialize): a request piece's

@@ -325,8 +325,8 @@ def test_concurrent_family_lookups_share_passes_and_match_golden(gpu):
     pieces of requests in flight share device passes (LookupBatcher: one
     staging area fills while the other's pass runs) and every response is the
     golden text byte for byte, whatever it shared a pass with; /server_stats
-    shows pieces carried by shared passes.  KGX_LOOKUP_BATCH=0 gives the same
-    bytes with every piece alone."""
+    shows pieces carried by shared passes.  KGX_LOOKUP_BATCH=0 (the default)
+    gives the same bytes with every piece alone."""
     import json
     import threading
     d = os.path.join(GOLDEN, "lookup")
