@@ -132,6 +132,7 @@ def main():
     ap.add_argument("--body-bytes", type=int, default=1 << 20)
     ap.add_argument("--seconds", type=float, default=4.0)
     ap.add_argument("--path", default="/query")
+    ap.add_argument("--server-prefix", default="", help="command words put before the server (a profiler)")
     ap.add_argument("--families", type=int, default=0, help="synthetic family DB over this many source proteins")
     args = ap.parse_args()
     from close_kmers_amd import build as kbuild
@@ -155,7 +156,7 @@ def main():
     if args.families:
         fam_pre, fam_post = write_family_db(tmp.name, min(args.families, spec.n_src))
     t0 = time.time()
-    srv = subprocess.Popen([kbuild.SERVER, "--bind", "127.0.0.1", "--listen-port-file", port_file,
+    srv = subprocess.Popen(args.server_prefix.split() + [kbuild.SERVER, "--bind", "127.0.0.1", "--listen-port-file", port_file,
                             "--n-kmer-threads", str(args.threads),
                             "--synthetic-image", f"{spec.n_keys}:{spec.num_sigs}"] + fam_pre + ["0", tmp.name] + fam_post,
                            stderr=subprocess.PIPE)
