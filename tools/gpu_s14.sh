@@ -12,4 +12,6 @@ P="/lookup?family_mode=1&find_best_match=1"
 export TMPDIR=/tmp
 step timeout -k 10 500 python3 tools/bench_server.py --families 100000 --path "$P" --clients 16 --threads 16 --seconds 3 \
    --server-prefix "rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/srv -o srv --" > "$OUT/lk_trace.json" 2> "$OUT/lk_trace.err"
+step timeout -k 10 120 python3 tools/server_trace.py "$OUT/srv" 1 > "$OUT/srv_trace.json"
+find "$OUT/srv" -name "*kernel_trace.csv" -delete
 echo "[gpu_s14] done" >&2
