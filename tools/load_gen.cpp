@@ -22,6 +22,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cerrno>
 #include <cstring>
 #include <fstream>
 #include <mutex>
@@ -104,6 +105,7 @@ int main(int argc, char **argv)
         heads[i] = "POST " + path + " HTTP/1.1\r\nContent-Length: " + std::to_string(bodies[i].bytes.size()) + "\r\n\r\n";
     std::atomic<uint64_t> next{0}, residues{0}, failures{0};
     std::mutex mu;
+    std::string first_failure;
     std::vector<double> lat;
     const auto t0 = clk::now();
     const auto stop = t0 + std::chrono::duration<double>(seconds);
@@ -116,7 +118,11 @@ int main(int argc, char **argv)
                 const uint64_t i = next++ % n;
                 const auto q0 = clk::now();
                 if (!post(port, heads[i], bodies[i].bytes, resp)) {
-                    failures++;
+                    if (failures++ == 0) {
+                        std::lock_guard<std::mutex> g(mu);
+                        first_failure = resp.empty() ? "no response (errno " + std::to_string(errno) + ")"
+                                                     : resp.substr(0, std::min<size_t>(resp.find('\r'), 80));
+                    }
                     continue;
                 }
                 my.push_back(std::chrono::duration<double, std::milli>(clk::now() - q0).count());
@@ -131,8 +137,8 @@ int main(int argc, char **argv)
     std::sort(lat.begin(), lat.end());
     auto pct = [&](double p) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, (size_t)(p / 100.0 * lat.size()))]; };
     std::printf("{\"clients\": %d, \"requests\": %zu, \"failures\": %llu, \"residues_per_s\": %.5g, "
-                "\"ms_median\": %.3f, \"ms_p99\": %.3f, \"wall_s\": %.3f}\n",
+                "\"ms_median\": %.3f, \"ms_p99\": %.3f, \"wall_s\": %.3f, \"first_failure\": \"%s\"}\n",
                 C, lat.size(), (unsigned long long)failures.load(), (double)residues.load() / wall, pct(50), pct(99),
-                wall);
+                wall, first_failure.c_str());
     return failures.load() ? 1 : 0;
 }
