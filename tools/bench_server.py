@@ -25,6 +25,7 @@ holds one protein) so that /lookup runs in family mode
 from __future__ import annotations
 
 import argparse
+import resource
 import json
 import os
 import socket
@@ -123,6 +124,50 @@ def server_stats(port: int, reset: bool = False) -> dict:
     return json.loads(r.split(b"\n\n", 1)[1])
 
 
+def cpu_snapshot(pid):
+    """CPU seconds of the server process, the children waited for so far (the
+    load generator) and the cgroup's usage/throttling where it shows them:
+    the box runs in a CPU share, and a server and its load generator that
+    together need more than that share are bound by it, not by the GPU"""
+    snap = {"t": time.time()}
+    try:
+        f = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()
+        tck = os.sysconf("SC_CLK_TCK")
+        snap["server_cpu_s"] = (int(f[11]) + int(f[12])) / tck
+    except OSError:
+        pass
+    ru = resource.getrusage(resource.RUSAGE_CHILDREN)
+    snap["children_cpu_s"] = ru.ru_utime + ru.ru_stime
+    for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpuacct/cpuacct.usage"):
+        try:
+            for ln in open(path).read().split("\n"):
+                kv = ln.split()
+                if len(kv) == 2:
+                    snap[path.rsplit("/", 1)[1] + ":" + kv[0]] = int(kv[1])
+                elif len(kv) == 1:
+                    snap[path.rsplit("/", 1)[1]] = int(kv[0])
+        except (OSError, ValueError):
+            pass
+    return snap
+
+
+def cpu_delta(a, b):
+    dt = b["t"] - a["t"]
+    out = {k: round((b[k] - a[k]) / dt, 3) for k in b if k != "t" and k in a}
+    out["wall_s"] = round(dt, 3)
+    return out
+
+
+def cpu_limits():
+    lim = {"affinity_cpus": len(os.sched_getaffinity(0))}
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "/sys/fs/cgroup/cpu/cpu.cfs_period_us"):
+        try:
+            lim[path] = open(path).read().strip()
+        except OSError:
+            pass
+    return lim
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n-keys", type=float, default=1e9)
@@ -180,11 +225,13 @@ def main():
         rows = {}
         for c in [int(x) for x in args.clients.split(",")]:
             server_stats(port, reset=True)
+            c0 = cpu_snapshot(srv.pid)
             r = subprocess.run([load_gen, str(port), args.path, bodies_file, str(c), str(args.seconds)],
                                capture_output=True, text=True, timeout=args.seconds + 600)
             if r.returncode != 0 and not (args.allow_failures and r.stdout.strip()):
                 raise RuntimeError(f"load_gen: {r.stdout} {r.stderr}")
             row = json.loads(r.stdout)
+            row["cpu_per_s"] = cpu_delta(c0, cpu_snapshot(srv.pid))
             row["server_stages"] = server_stats(port)
             rows[str(c)] = row
             print(f"[bench_server] clients={c}: {rows[str(c)]}", file=sys.stderr)
@@ -195,7 +242,7 @@ def main():
             "config": {"n_keys": spec.n_keys, "num_sigs": spec.num_sigs, "path": args.path,
                        "families": args.families,
                        "body_bytes": args.body_bytes, "proteins_per_body": round(args.n_seq / len(bodies), 1),
-                       "server_threads": args.threads, "startup_s": startup_s},
+                       "server_threads": args.threads, "startup_s": startup_s, "cpu_limits": cpu_limits()},
             "by_clients": rows,
             "note": "loopback TCP, native load generator (tools/load_gen) as its own process in the same CPU "
                     "share; server parses FASTA, one GPU pass per body piece, writes query_request text; "
