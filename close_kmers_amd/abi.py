@@ -20,6 +20,8 @@ ERRORS = {-1: "EINVAL", -2: "EIO", -3: "EFORMAT", -4: "ENOMEM", -5: "EDEVICE", -
           -7: "EFULL", -8: "EBUSY"}
 KGX_EBUSY = -8
 KGX_EDEVICE = -5
+KGX_EINVAL = -1
+KGX_WAIT_SPIN, KGX_WAIT_SLEEP, KGX_WAIT_BLOCK = 0, 1, 2
 WANT_HITS, WANT_CALLS, WANT_OTU, WANT_BEST = 1, 2, 4, 8
 HIT_IN_RUN, HIT_OTU = 1, 2
 
@@ -174,6 +176,8 @@ SIGNATURES = {
     "kgx_strerror": (_CS, [_INT]),
     "kgx_device_count": (_INT, []),
     "kgx_params_default": (_INT, [ctypes.POINTER(Params)]),
+    "kgx_set_host_wait": (_INT, [ctypes.c_int, ctypes.c_uint32]),
+    "kgx_get_host_wait": (_INT, [ctypes.POINTER(ctypes.c_uint32)]),
     "kgx_params_parse": (_INT, [ctypes.POINTER(Params), ctypes.POINTER(_CS), ctypes.POINTER(_CS), _SZ]),
     "kgx_image_open": (_INT, [_CS, _INT, _PP]),
     "kgx_image_from_memory": (_INT, [_P, _U64, _INT, _PP]),

@@ -35,6 +35,21 @@ bool is_gfx950(int dev);
             return ::kgx::fail(KGX_EDEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+/* How a thread waits for its own stream (kgx_set_host_wait): KGX_WAIT_SPIN
+ * (hipStreamSynchronize: the runtime polls), KGX_WAIT_SLEEP (hipStreamQuery
+ * every poll_us, the thread asleep in between) or KGX_WAIT_BLOCK (a
+ * blocking-sync event: the thread sleeps until the device signals).  A
+ * server of many workers under a CPU share (the box's 16 CPUs) spends that
+ * share spinning in the default; the two others hand it to the text and
+ * socket work.  Process-wide; KGX_HOST_WAIT=spin|sleep[:us]|block sets the
+ * starting mode. */
+extern std::atomic<int> g_host_wait_mode;
+extern std::atomic<uint32_t> g_host_wait_us;
+hipError_t host_wait(hipStream_t s);
+/* the host spins on a completion word the device stores (small batches):
+ * the same modes, polling `done` instead of the stream */
+hipError_t host_wait_word(const volatile uint32_t *done, uint32_t token, hipStream_t s);
+
 /* grow-only device buffer, freed with its owner */
 struct DevBuf {
     void *p = nullptr;

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <ctime>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -65,6 +66,103 @@ struct PhaseTimer {
     }
 };
 
+namespace {
+
+int wait_mode_from_env(uint32_t *us)
+{
+    *us = 20;
+    const char *e = std::getenv("KGX_HOST_WAIT");
+    if (!e)
+        return KGX_WAIT_SPIN;
+    const std::string v(e);
+    if (v.rfind("sleep", 0) == 0) {
+        if (v.size() > 6 && v[5] == ':')
+            *us = (uint32_t)std::max(1, std::atoi(v.c_str() + 6));
+        return KGX_WAIT_SLEEP;
+    }
+    return v == "block" ? KGX_WAIT_BLOCK : KGX_WAIT_SPIN;
+}
+
+uint32_t g_env_wait_us = 20;
+
+void sleep_us(uint32_t us)
+{
+    timespec ts{0, (long)us * 1000};
+    nanosleep(&ts, nullptr);
+}
+
+}  // namespace
+
+std::atomic<int> g_host_wait_mode{wait_mode_from_env(&g_env_wait_us)};
+std::atomic<uint32_t> g_host_wait_us{g_env_wait_us};
+
+hipError_t host_wait(hipStream_t s)
+{
+    const int mode = g_host_wait_mode.load(std::memory_order_relaxed);
+    if (mode == KGX_WAIT_SLEEP) {
+        const uint32_t us = g_host_wait_us.load(std::memory_order_relaxed);
+        for (;;) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipErrorNotReady)
+                return q;
+            sleep_us(us);
+        }
+    }
+    if (mode == KGX_WAIT_BLOCK) {
+        /* one blocking-sync event per thread and device, never destroyed (a
+         * thread_local destructor must not call the runtime at exit, §10) */
+        thread_local hipEvent_t ev[64] = {};
+        int dev = 0;
+        hipError_t e = hipStreamGetDevice(s, &dev);
+        if (e != hipSuccess || dev < 0 || dev >= 64)
+            return e != hipSuccess ? e : hipStreamSynchronize(s);
+        if (!ev[dev]) {
+            int cur = 0;
+            if ((e = hipGetDevice(&cur)) != hipSuccess || (cur != dev && (e = hipSetDevice(dev)) != hipSuccess))
+                return e;
+            e = hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming | hipEventBlockingSync);
+            if (cur != dev)
+                (void)hipSetDevice(cur);
+            if (e != hipSuccess) {
+                ev[dev] = nullptr;
+                return e;
+            }
+        }
+        if ((e = hipEventRecord(ev[dev], s)) != hipSuccess)
+            return e;
+        return hipEventSynchronize(ev[dev]);
+    }
+    return hipStreamSynchronize(s);
+}
+
+hipError_t host_wait_word(const volatile uint32_t *done, uint32_t token, hipStream_t s)
+{
+    const int mode = g_host_wait_mode.load(std::memory_order_relaxed);
+    if (mode == KGX_WAIT_BLOCK)
+        return host_wait(s); /* the stream drains after the word's store */
+    const uint32_t us = g_host_wait_us.load(std::memory_order_relaxed);
+    const auto w0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1; *done != token; spin++) {
+        if (mode == KGX_WAIT_SLEEP || (spin & 255u) == 0) { /* a fault or a lost store still ends the wait */
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess)
+                break;
+            if (q != hipErrorNotReady)
+                return q;
+            if (mode == KGX_WAIT_SLEEP)
+                sleep_us(us);
+            /* past 50 us of spinning the CPU goes to whoever else is
+             * runnable (a server's other workers, its socket threads) */
+            else if (std::chrono::steady_clock::now() - w0 > std::chrono::microseconds(50))
+                sched_yield();
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    return hipSuccess;
+}
+
 }  // namespace kgx
 
 /* [p, p + n) lies in one pinned, device-mapped host allocation */
@@ -118,6 +216,22 @@ int kgx_device_count(void)
     for (int d = 0; d < n; d++)
         good += is_gfx950(d) ? 1 : 0;
     return good;
+}
+
+int kgx_set_host_wait(int mode, uint32_t poll_us)
+{
+    if (mode != KGX_WAIT_SPIN && mode != KGX_WAIT_SLEEP && mode != KGX_WAIT_BLOCK)
+        return fail(KGX_EINVAL, "host wait mode: KGX_WAIT_SPIN, KGX_WAIT_SLEEP or KGX_WAIT_BLOCK");
+    g_host_wait_us.store(poll_us ? std::min<uint32_t>(poll_us, 100000) : 20u);
+    g_host_wait_mode.store(mode);
+    return KGX_OK;
+}
+
+int kgx_get_host_wait(uint32_t *poll_us)
+{
+    if (poll_us)
+        *poll_us = g_host_wait_us.load();
+    return g_host_wait_mode.load();
 }
 
 int kgx_params_default(kgx_params *p)
@@ -3218,30 +3332,14 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
     }
     if (fused) {
         const volatile uint32_t *done = c->h_done.data();
-        const auto w0 = std::chrono::steady_clock::now();
-        for (uint32_t spin = 1; *done != token; spin++) {
-            if ((spin & 255u) == 0) { /* a fault or a lost store still ends the wait */
-                const hipError_t q = hipStreamQuery(c->stream);
-                if (q == hipSuccess)
-                    break;
-                if (q != hipErrorNotReady)
-                    HIP_TRY(q);
-                /* past 50 us of spinning the CPU goes to whoever else is
-                 * runnable (a server's other workers, its socket threads) */
-                if (std::chrono::steady_clock::now() - w0 > std::chrono::microseconds(50))
-                    sched_yield();
-            }
-#if defined(__x86_64__)
-            __builtin_ia32_pause();
-#endif
-        }
+        HIP_TRY(host_wait_word(done, token, c->stream));
         std::atomic_thread_fence(std::memory_order_acquire);
         /* the stream drained without the gather's last store: its results
          * are not there (an early exit or a lost store), never hand them out */
         if (*done != token)
             return fail(KGX_EDEVICE, "small batch: the gather ended without its completion token");
     } else {
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(host_wait(c->stream));
     }
     if (c->h_plan_status[0])
         return fail(KGX_EINVAL, "small batch: plan status raised");

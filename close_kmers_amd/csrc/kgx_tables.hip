@@ -1120,7 +1120,7 @@ int rollup_finish(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
         return KGX_OK;
     }
     HIP_TRY(hipSetDevice(m->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(host_wait(c->stream));
     std::atomic_thread_fence(std::memory_order_acquire);
     const uint64_t E = r.h_n[0];
     out->n_events = E;
@@ -1135,7 +1135,7 @@ int rollup_finish(kgx_kmap *m, kgx_ctx *c, int mode, kgx_rollup_result *out)
         r.presize_misses += r.cap != 0;
         if (int rc = rollup_rows(m, c, r, mode, E))
             return rc;
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(host_wait(c->stream));
         std::atomic_thread_fence(std::memory_order_acquire);
     }
     out->rows = r.h_rows.data();

@@ -188,6 +188,18 @@ const char *kgx_strerror(int code);
 /* number of visible gfx950 devices (0 in a GPU-less container) */
 int kgx_device_count(void);
 int kgx_params_default(kgx_params *p);
+/* How the library's host threads wait for their own device work (the small-
+ * batch path, rollups, collects): KGX_WAIT_SPIN (the default: the HIP
+ * runtime's own wait, which polls), KGX_WAIT_SLEEP (poll every poll_us, the
+ * thread asleep in between; poll_us 0 = 20) or KGX_WAIT_BLOCK (blocking-sync
+ * events).  Process-wide; the environment variable KGX_HOST_WAIT
+ * (spin|sleep[:us]|block) sets the starting mode.  A server whose workers
+ * share a CPU quota gives the spinning time back to its other threads. */
+#define KGX_WAIT_SPIN 0
+#define KGX_WAIT_SLEEP 1
+#define KGX_WAIT_BLOCK 2
+int kgx_set_host_wait(int mode, uint32_t poll_us);
+int kgx_get_host_wait(uint32_t *poll_us);
 /* set_parameters (kguts.cc:244-268) over parallel name/value string arrays:
  * resets to the defaults, then applies std::stoi to the four known names;
  * an unparsable value leaves the default (the reference only warns). */

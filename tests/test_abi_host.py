@@ -148,6 +148,26 @@ def test_numa_node_cpus(kgx):
         assert seen == aff & set().union(*[set(kgx.numa_node_cpus(nd)) for nd in nodes])
 
 
+def test_host_wait_modes(kgx):
+    """kgx_set_host_wait: the three modes round-trip (poll 0 = 20 us, capped at
+    0.1 s), anything else is KGX_EINVAL and leaves the mode alone."""
+    import ctypes
+    L = kgx.lib()
+    us = ctypes.c_uint32()
+    mode0 = L.kgx_get_host_wait(ctypes.byref(us))
+    us0 = us.value
+    try:
+        for mode, poll, want in ((kgx.KGX_WAIT_SLEEP, 0, 20), (kgx.KGX_WAIT_SLEEP, 7, 7),
+                                 (kgx.KGX_WAIT_SLEEP, 10**6, 100000), (kgx.KGX_WAIT_BLOCK, 5, 5),
+                                 (kgx.KGX_WAIT_SPIN, 20, 20)):
+            assert L.kgx_set_host_wait(mode, poll) == 0
+            assert L.kgx_get_host_wait(ctypes.byref(us)) == mode and us.value == want
+        assert L.kgx_set_host_wait(3, 1) == kgx.KGX_EINVAL
+        assert L.kgx_get_host_wait(None) == kgx.KGX_WAIT_SPIN
+    finally:
+        L.kgx_set_host_wait(mode0, us0)
+
+
 def test_format_g6_matches_printf(kgx):
     """kgx_format_g6 -- how the handlers print floats (operator<< at the
     default precision = printf's %.6g of the value widened to double), with
