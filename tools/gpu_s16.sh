@@ -4,6 +4,7 @@ OUT=$R/gpurun_out/${1:-s16}
 mkdir -p "$OUT"
 cd "$R"
 step() { "$@"; rc=$?; if [ $rc -ne 0 ]; then echo "[gpu_s16] stop: rc $rc from $*" >&2; exit $rc; fi; }
+step timeout -k 10 120 tests/native/wave_sort_check 3000 7 > "$OUT/wave_sort.txt" 2>&1
 P="/lookup?family_mode=1&find_best_match=1"
 export TMPDIR=/tmp
 for m in block sleep:20 spin sleep:50 block; do
