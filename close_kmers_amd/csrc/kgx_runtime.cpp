@@ -3562,7 +3562,7 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
             return rc;
     }
     c->counts_enqueued = 0;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(host_wait(c->stream));
     if (c->h_plan_status[0])
         return fail(KGX_EINVAL, "batch offsets not monotone or spanning more than n_residues bytes "
                                 "(the batch was processed as empty)");
@@ -3633,7 +3633,7 @@ int kgx_device_batch_collect(kgx_ctx *c, uint32_t want, kgx_result *out)
                                c->stream));
     }
     if (!best_now)
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(host_wait(c->stream));
     tm.mark(" gather+d2h");
     fill_result(c, n_seq, need_hits, want_best, c->h_nwin[0], out);
     return KGX_OK;
