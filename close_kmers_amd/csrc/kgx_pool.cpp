@@ -650,7 +650,17 @@ int kgx_lookup(kgx_ctx *c, kgx_kmap *map, int mode, const kgx_params *params, co
     for (uint32_t s = 0; s < n_seq; s++)
         if (seq_offsets[s + 1] < seq_offsets[s])
             return fail(KGX_EINVAL, "seq_offsets not monotone");
-    int rc = one_pass_enqueue(c, params, residues, seq_offsets, n_seq, want, nullptr, nullptr);
+    bool small = false;
+    int rc = lookup_small(c, map, mode, params, residues, seq_offsets, n_seq, want, out, &small);
+    if (small) {
+        if (!rc)
+            rc = rollup_finish(map, c, mode, rollup);
+        if (rc)
+            (void)hipStreamSynchronize(c->stream);
+        return rc;
+    }
+    if (!rc)
+        rc = one_pass_enqueue(c, params, residues, seq_offsets, n_seq, want, nullptr, nullptr);
     if (!rc)
         rc = collect_counts_enqueue(c, want);
     if (!rc)

@@ -308,6 +308,8 @@ std::unique_lock<std::mutex> svc_shutdown_hold(kgx_image *img);
  * host wait once an earlier rollup on c gave a size), then the wait, the size
  * check (passes 2-3 again when short) and the result */
 int rollup_enqueue(kgx_kmap *m, kgx_ctx *c, int mode);
+int lookup_small(kgx_ctx *c, kgx_kmap *m, int mode, const kgx_params *params, const char *residues,
+                 const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out, bool *taken);
 /* kgx_device_batch_collect's counts (and best calls) round trip enqueued on
  * c's stream ahead of the collect, which then only waits */
 int collect_counts_enqueue(kgx_ctx *c, uint32_t want);

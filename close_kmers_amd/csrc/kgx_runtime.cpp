@@ -3165,7 +3165,8 @@ int process_batch_fused(kgx_ctx *c, const kgx_params &p, const char *residues, c
  * sized for the worst case (every window a hit).  Same kernels, same records
  * as kgx_run_device + kgx_device_batch_collect. */
 int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residues, const uint64_t *seq_offsets,
-                        uint32_t n_seq, uint32_t want, kgx_result *out)
+                        uint32_t n_seq, uint32_t want, kgx_result *out, kgx_kmap *roll_map = nullptr,
+                        int roll_mode = 0)
 {
     PhaseTimer tm(c); /* KGX_TIMING: phase times (each mark waits for the stream) */
     int rc = stage_host_copy(c, residues, seq_offsets, 0, n_seq);
@@ -3323,12 +3324,20 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                                      c->wbase.as<uint64_t>(), want_best ? c->best.as<kgx_best_call>() : nullptr,
                                      static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
                                      static_cast<uint64_t *>(m_nwin), c->stream));
-        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
-                              c->call_count.as<uint32_t>(), c->hits.as<uint4>(), c->hits.as<uint4>() + c->hit_slots,
-                              c->calls.as<kgx_call>(), c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
-                              static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
-                              c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
-                              static_cast<kgx_otu *>(mo), c->stream));
+        if (mh || mc || mo) /* a counts-and-best-calls batch (/lookup's) gathers nothing */
+            HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                                  c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
+                                  c->hits.as<uint4>() + c->hit_slots, c->calls.as<kgx_call>(),
+                                  c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
+                                  static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
+                                  c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
+                                  static_cast<kgx_otu *>(mo), c->stream));
+    }
+    /* kgx_lookup: the rollup queued behind the pass, one host wait for both */
+    if (roll_map) {
+        if ((rc = rollup_enqueue(roll_map, c, roll_mode)))
+            return rc;
+        HIP_TRY(host_wait(c->stream));
     }
     if (fused) {
         const volatile uint32_t *done = c->h_done.data();
@@ -3410,6 +3419,38 @@ int kgx_process_batch(kgx_ctx *c, const kgx_params *params, const char *residues
     }
     return process_batch_one_pass(c, params, residues, seq_offsets, n_seq, want, out);
 }
+
+extern "C++" {
+namespace kgx {
+
+/* kgx_lookup over a batch kgx_process_batch would take down the small-batch
+ * path: that path with the rollup queued behind the pass and one host wait
+ * for both (*taken = true); other batches are left to the caller */
+int lookup_small(kgx_ctx *c, kgx_kmap *m, int mode, const kgx_params *params, const char *residues,
+                 const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_result *out, bool *taken)
+{
+    *taken = false;
+    const uint64_t n_res = n_seq ? seq_offsets[n_seq] - seq_offsets[0] : 0;
+    if (!n_seq || n_res > (uint64_t)c->small_batch || n_seq > (1u << 16) || (n_res && !residues))
+        return KGX_OK;
+    const uint64_t k_res = std::max<uint64_t>(1, n_res >> 21);
+    if (std::min<uint64_t>({(uint64_t)c->host_chunks, k_res, (uint64_t)n_seq}) >= 2)
+        return KGX_OK;
+    kgx_params p;
+    if (params)
+        p = *params;
+    else
+        kgx_params_default(&p);
+    if (fused_eligible(c, p, seq_offsets, n_seq, want))
+        return KGX_OK; /* the fused kernel keeps nothing on the device to roll up */
+    HIP_TRY(hipSetDevice(c->img->device));
+    *taken = true;
+    c->small_batches++;
+    return process_batch_small(c, params, residues, seq_offsets, n_seq, want, out, m, mode);
+}
+
+}  // namespace kgx
+}  // extern "C++"
 
 int kgx_process_batch_compact(kgx_ctx *c, const kgx_params *params, const char *residues,
                               const uint64_t *seq_offsets, uint32_t n_seq, uint32_t want, kgx_compact_result *out)

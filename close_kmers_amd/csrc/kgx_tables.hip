@@ -601,6 +601,45 @@ __global__ __launch_bounds__(256) void rollup_emit_kernel(uint32_t n_seq, const 
         h_rows[o + r] = rows2[f + r];
 }
 
+/* Exclusive sum of in[0..n) into out[0..n) by one workgroup, and out[n-1]
+ * into *last_mapped (host-mapped) when given: the rollup's two scans for a
+ * small batch in one launch each instead of hipcub's two (look-back init +
+ * scan) and the copy of the event total (r8: a 1-MiB /lookup piece ran 15
+ * kernels, and at 16 concurrent pieces the chip's capacity was set by
+ * launches, not by their work) */
+constexpr uint64_t kScanOneMax = 1u << 16;
+
+template <typename T>
+__global__ __launch_bounds__(1024) void scan_one_kernel(const T *__restrict__ in, uint64_t n,
+                                                        uint64_t *__restrict__ out, uint64_t *last_mapped)
+{
+    __shared__ uint64_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t per = (n + 1023) / 1024;
+    const uint64_t a = min(n, (uint64_t)t * per), b = min(n, a + per);
+    uint64_t own = 0;
+    for (uint64_t i = a; i < b; i++)
+        own += (uint64_t)in[i];
+    uint64_t x = own; /* inclusive scan over the wave */
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= d)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wave] = x;
+    __syncthreads();
+    uint64_t run = x - own;
+    for (uint32_t w = 0; w < wave; w++)
+        run += wsum[w];
+    for (uint64_t i = a; i < b; i++) {
+        out[i] = run;
+        if (i == n - 1 && last_mapped)
+            *last_mapped = run;
+        run += (uint64_t)in[i];
+    }
+}
+
 /* --- /matrix --- */
 
 __global__ void seen_insert_kernel(const uint32_t *ids, uint32_t n, uint64_t base, uint64_t *skeys,
@@ -1006,6 +1045,14 @@ int rollup_tiles(kgx_kmap *m, kgx_ctx *c, RollupScratch &r)
     hipLaunchKernelGGL(rollup_tiles_kernel, wave_grid, dim3(256), lds, st, t, nt, nw, view, r.hseq.as<uint32_t>(),
                        r.hstart.as<uint64_t>(), r.hlen.as<uint32_t>(), r.tcount.as<uint64_t>(),
                        r.sfirst.as<uint32_t>(), r.send.as<uint32_t>(), r.rowcnt.as<uint32_t>());
+    void *dn = nullptr;
+    HIP_TRY(r.h_n.device_ptr(0, &dn));
+    if (nw + 1 <= kScanOneMax) { /* one launch: the scan and E into h_n[0] */
+        hipLaunchKernelGGL(scan_one_kernel<uint64_t>, dim3(1), dim3(1024), 0, st, r.tcount.as<uint64_t>(), nw + 1,
+                           r.tbase.as<uint64_t>(), static_cast<uint64_t *>(dn));
+        HIP_TRY(hipGetLastError());
+        return KGX_OK;
+    }
     size_t tb = 0, tb2 = 0;
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
                                              (int)(nw + 1), st));
@@ -1014,8 +1061,6 @@ int rollup_tiles(kgx_kmap *m, kgx_ctx *c, RollupScratch &r)
     HIP_TRY(r.tmp.reserve(std::max(tb, tb2)));
     HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.tcount.as<uint64_t>(), r.tbase.as<uint64_t>(),
                                              (int)(nw + 1), st));
-    void *dn = nullptr;
-    HIP_TRY(r.h_n.device_ptr(0, &dn));
     HIP_TRY(launch_copy_to_host(dn, r.tbase.as<uint64_t>() + nw, 8, 1, st));
     return KGX_OK;
 }
@@ -1048,12 +1093,17 @@ int rollup_rows(kgx_kmap *m, kgx_ctx *c, RollupScratch &r, int mode, uint64_t ca
                        r.send.as<uint32_t>(), r.ev_id.as<uint32_t>(), r.ev_w.as<float>(),
                        mode == KGX_ROLLUP_FAMILY ? 1 : 0, d_E, cap, r.flag.as<uint8_t>(), r.rowdata.as<uint4>(),
                        r.rows2.as<uint4>(), r.rowcnt.as<uint32_t>());
-    size_t tb = 0;
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
-                                             (int)(n + 1), st));
-    HIP_TRY(r.tmp.reserve(tb));
-    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
-                                             (int)(n + 1), st));
+    if (n + 1 <= kScanOneMax) {
+        hipLaunchKernelGGL(scan_one_kernel<uint32_t>, dim3(1), dim3(1024), 0, st, r.rowcnt.as<uint32_t>(),
+                           (uint64_t)n + 1, r.rowoff.as<uint64_t>(), nullptr);
+    } else {
+        size_t tb = 0;
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
+                                                 (int)(n + 1), st));
+        HIP_TRY(r.tmp.reserve(tb));
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(r.tmp.p, tb, r.rowcnt.as<uint32_t>(), r.rowoff.as<uint64_t>(),
+                                                 (int)(n + 1), st));
+    }
     void *d_rows = nullptr, *d_off = nullptr, *d_n = nullptr;
     HIP_TRY(r.h_rows.device_ptr(0, &d_rows));
     HIP_TRY(r.h_off.device_ptr(0, &d_off));

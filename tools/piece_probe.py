@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--per-piece", type=int, default=3333)
     ap.add_argument("--wait", default="")
     ap.add_argument("--line-index", type=int, default=0)
+    ap.add_argument("--one-wait", action="store_true", help="kgx_lookup (pass + rollup, one host wait)")
     args = ap.parse_args()
     import bench
     from close_kmers_amd import abi, synth
@@ -51,7 +52,7 @@ def main():
     fam, n_fam = bench.family_kmap(abi, synth, spec, 0, 100000)
     params = abi.default_params()
     out = {"per_piece_proteins": args.per_piece, "residues_per_piece": pieces[0][2], "wait": args.wait or "default",
-           "line_index": args.line_index,
+           "line_index": args.line_index, "one_wait": args.one_wait,
            "by_threads": {}}
     for T in [int(x) for x in args.threads.split(",")]:
         ctxs = [abi.Context(img) for _ in range(T)]
@@ -71,10 +72,16 @@ def main():
                     pr, po, nr = pieces[k % len(pieces)]
                     k += 1
                     t0 = time.perf_counter()
-                    abi.check(L.kgx_process_batch(c.handle, ctypes.byref(params), pr.ctypes.data, po.ctypes.data,
-                                                  len(po) - 1, abi.WANT_BEST, ctypes.byref(r)), "process_batch")
-                    abi.check(L.kgx_kmap_rollup(fam.handle, c.handle, abi.ROLLUP_FAMILY, ctypes.byref(ru)),
-                              "rollup")
+                    if args.one_wait:
+                        abi.check(L.kgx_lookup(c.handle, fam.handle, abi.ROLLUP_FAMILY, ctypes.byref(params),
+                                               pr.ctypes.data, po.ctypes.data, len(po) - 1, abi.WANT_BEST,
+                                               ctypes.byref(r), ctypes.byref(ru)), "lookup")
+                    else:
+                        abi.check(L.kgx_process_batch(c.handle, ctypes.byref(params), pr.ctypes.data,
+                                                      po.ctypes.data, len(po) - 1, abi.WANT_BEST, ctypes.byref(r)),
+                                  "process_batch")
+                        abi.check(L.kgx_kmap_rollup(fam.handle, c.handle, abi.ROLLUP_FAMILY, ctypes.byref(ru)),
+                                  "rollup")
                     busy[i] += time.perf_counter() - t0
                     counts[i] += 1
                     resid[i] += nr
