@@ -1472,15 +1472,14 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
     const int mode = family_mode_ ? KGX_ROLLUP_FAMILY : KGX_ROLLUP_PEG;
     const uint32_t want = want_calls ? KGX_WANT_BEST : 0u;
     kgx_rollup_result ru;
-    /* the pass (the small-batch path for a piece of up to 2M residues) and
-     * then the rollup, a wait each; KGX_LOOKUP_ONE_WAIT=1: both enqueued
-     * together with one host wait (kgx_lookup) when the map is on the
-     * worker's device -- measured slower for 1-MiB bodies (HTTP family
-     * /lookup at 16 clients 6.0e9 vs 6.8e9 residues/s, r8: its general pass
-     * costs more device time than the small-batch path saves in waits) */
+    /* the pass and the rollup enqueued together with one host wait
+     * (kgx_lookup: the small-batch path with the rollup queued behind it)
+     * when the map is on the worker's device; KGX_LOOKUP_ONE_WAIT=0: the
+     * pass, then the rollup, a wait each (HTTP family /lookup at 16 clients
+     * 9.05e9 vs 8.35e9 residues/s, r8 s20) */
     static const bool one_wait = [] {
         const char *e = std::getenv("KGX_LOOKUP_ONE_WAIT");
-        return e && std::atoi(e) != 0;
+        return !e || std::atoi(e) != 0;
     }();
     int rc;
     const kgx_best_call *best = nullptr;

@@ -306,6 +306,7 @@ hipError_t launch_svc(const SvcSlotHdr *hdr, SvcSlotOut *out, SvcSlotDbg *dbg, c
                       uint64_t life_ticks, int quad_probe, hipStream_t stream, uint32_t home_shift = 0,
                       uint32_t poll_chunks = SVC_POLL_CHUNKS);
 constexpr uint32_t SMALL_GATHER_SEQ = 256;
+constexpr uint32_t SMALL_COLLECT_BEST_SEQ = 8192;
 constexpr uint32_t SMALL_GATHER_BLOCKS = 64; /* workgroups of the small gather (one wave per sequence) */
 hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t *hit_mask, uint32_t tile_windows,
                                const uint32_t *hit_count, const uint32_t *call_count, const uint4 *hot,
@@ -317,6 +318,12 @@ hipError_t launch_small_gather(uint32_t n, const uint64_t *wbase, const uint64_t
                                uint32_t hit_format, hipStream_t stream);
 /* one workgroup: launch_count_scan's offsets into o* (HBM) and h* (mapped
  * host), plus status[0], wbase[n] and (best_host non-NULL) best[0, n) */
+hipError_t launch_small_collect_best(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2,
+                                     uint64_t *o0, uint64_t *o1, uint64_t *o2, uint64_t *h0, uint64_t *h1,
+                                     uint64_t *h2, const uint32_t *status, const uint64_t *wbase,
+                                     const kgx_call *calls, const uint32_t *call_count, kgx_call *ws,
+                                     kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
+                                     uint64_t *nwin_host, hipStream_t stream);
 hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2, uint64_t *o0,
                                 uint64_t *o1, uint64_t *o2, uint64_t *h0, uint64_t *h1, uint64_t *h2,
                                 const uint32_t *status, const uint64_t *wbase, const kgx_best_call *best,

@@ -2580,6 +2580,63 @@ hipError_t launch_small_collect(uint32_t n, const uint32_t *c0, const uint32_t *
     return hipGetLastError();
 }
 
+/* small_collect + best_call_kernel in one launch for batches of up to
+ * SMALL_COLLECT_BEST_SEQ sequences: block b owns offsets [256 b, 256 b + 256)
+ * (the last one offset n too), sums the counts before its range itself (at
+ * most 3 x 8,192 values from L2), scans its own, and decides its sequences'
+ * best calls (best_call_decide, into the device array and the mapped host
+ * one).  One launch instead of two, and no one-workgroup serial scan. */
+__global__ __launch_bounds__(256) void small_collect_best_kernel(
+    Counts3 cnt, uint32_t n, Offsets3 off, Offsets3 off_host, const uint32_t *__restrict__ status,
+    const uint64_t *__restrict__ wbase, const kgx_call *__restrict__ calls, const uint32_t *__restrict__ call_count,
+    kgx_call *__restrict__ ws, kgx_best_call *__restrict__ best, kgx_best_call *__restrict__ best_host,
+    uint32_t *__restrict__ status_host, uint64_t *__restrict__ nwin_host)
+{
+    __shared__ uint64_t lds_pre[3][4], lds_own[3][4];
+    const uint32_t t = threadIdx.x, s0 = blockIdx.x * 256u, i = s0 + t;
+    for (int a = 0; a < 3; a++) {
+        uint64_t v = 0, before = 0, tot = 0;
+        if (cnt.c[a])
+            for (uint32_t j = t; j < s0; j += 256)
+                v += cnt.c[a][j];
+        (void)block_scan(v, lds_pre[a], before);
+        const uint64_t mine = cnt.c[a] && i < n ? cnt.c[a][i] : 0;
+        const uint64_t at = before + block_scan(mine, lds_own[a], tot) - mine;
+        if (i <= n) {
+            off.o[a][i] = at;
+            off_host.o[a][i] = at;
+        }
+    }
+    if (i < n) {
+        const uint64_t w = wbase[i];
+        const kgx_best_call b = best_call_decide(calls + w, call_count[i], ws + w);
+        best[i] = b;
+        if (best_host)
+            best_host[i] = b;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+        status_host[0] = status[0];
+        nwin_host[0] = wbase[n];
+    }
+}
+
+hipError_t launch_small_collect_best(uint32_t n, const uint32_t *c0, const uint32_t *c1, const uint32_t *c2,
+                                     uint64_t *o0, uint64_t *o1, uint64_t *o2, uint64_t *h0, uint64_t *h1,
+                                     uint64_t *h2, const uint32_t *status, const uint64_t *wbase,
+                                     const kgx_call *calls, const uint32_t *call_count, kgx_call *ws,
+                                     kgx_best_call *best, kgx_best_call *best_host, uint32_t *status_host,
+                                     uint64_t *nwin_host, hipStream_t stream)
+{
+    if (n > SMALL_COLLECT_BEST_SEQ)
+        return hipErrorInvalidValue;
+    Counts3 cnt = {{c0, c1, c2}};
+    Offsets3 off = {{o0, o1, o2}};
+    Offsets3 off_host = {{h0, h1, h2}};
+    hipLaunchKernelGGL(small_collect_best_kernel, dim3(n / 256 + 1), dim3(256), 0, stream, cnt, n, off, off_host,
+                       status, wbase, calls, call_count, ws, best, best_host, status_host, nwin_host);
+    return hipGetLastError();
+}
+
 /* min(*count, cap) elements of elem_bytes each, src -> dst: the size comes
  * from the device (a chunk's scanned total), the room from the host.  The
  * bytes move as 16-B stores (one 1-KB run per wave instruction over PCIe),

@@ -408,6 +408,7 @@ struct kgx_ctx {
     bool have_hits = false; /* the tiled hits of the current plan are on the device */
     uint32_t hit_format = kgx::HIT_PLANES; /* of the current plan's hits (set by the probe) */
     bool have_best = false; /* best[] holds find_best_call of the current plan */
+    bool defer_best = false; /* kgx_stage_score leaves best[] to the small path's collect */
     kgx::DevBuf best, best_ws, bc_calls, bc_start, bc_count; /* KGX_WANT_BEST / kgx_find_best_calls */
     kgx::PinnedVec<kgx_best_call> h_best;
     /* fq fragments (kgx_fq.hip) */

@@ -1606,9 +1606,10 @@ int kgx_stage_score(kgx_ctx *c, const kgx_params *params, uint32_t want)
     if (best) {
         HIP_TRY(c->best.reserve(std::max<uint64_t>(c->n_seq, 1) * sizeof(kgx_best_call)));
         HIP_TRY(c->best_ws.reserve(c->hit_slots * sizeof(kgx_call)));
-        HIP_TRY(launch_best_calls(c->n_seq, c->calls.as<kgx_call>(), c->wbase.as<uint64_t>(),
-                                  c->call_count.as<uint32_t>(), c->best_ws.as<kgx_call>(),
-                                  c->best.as<kgx_best_call>(), c->stream));
+        if (!c->defer_best)
+            HIP_TRY(launch_best_calls(c->n_seq, c->calls.as<kgx_call>(), c->wbase.as<uint64_t>(),
+                                      c->call_count.as<uint32_t>(), c->best_ws.as<kgx_call>(),
+                                      c->best.as<kgx_best_call>(), c->stream));
         c->have_best = true;
     }
     return KGX_OK;
@@ -3253,7 +3254,11 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
      * few tiles per wave (option small_wave_tiles) put a coalesced batch's
      * sequences on different waves, scored at once */
     c->score_wave_tiles = c->small_wave_tiles;
+    /* past SMALL_GATHER_SEQ sequences the collect decides the best calls */
+    const bool collect_best = (want & KGX_WANT_BEST) && n_seq > SMALL_GATHER_SEQ && n_seq <= SMALL_COLLECT_BEST_SEQ;
+    c->defer_best = collect_best;
     rc = kgx_stage_score(c, params, want);
+    c->defer_best = false;
     c->score_variant = variant;
     c->score_wave_tiles = wave_tiles;
     tm.mark("s.score");
@@ -3315,6 +3320,15 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                                     static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
                                     static_cast<uint64_t *>(m_nwin), static_cast<uint32_t *>(m_done), token,
                                     c->small_blocks_done.as<uint32_t>(), c->hit_format, c->stream));
+    } else if (collect_best) {
+        HIP_TRY(launch_small_collect_best(
+            n_seq, c->hit_count.as<uint32_t>(), want_calls ? c->call_count.as<uint32_t>() : nullptr,
+            want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
+            c->dense_coff.as<uint64_t>(), c->dense_ooff.as<uint64_t>(), static_cast<uint64_t *>(m_hoff),
+            static_cast<uint64_t *>(m_coff), static_cast<uint64_t *>(m_ooff), c->plan_status.as<uint32_t>(),
+            c->wbase.as<uint64_t>(), c->calls.as<kgx_call>(), c->call_count.as<uint32_t>(),
+            c->best_ws.as<kgx_call>(), c->best.as<kgx_best_call>(), static_cast<kgx_best_call *>(mb),
+            static_cast<uint32_t *>(m_st), static_cast<uint64_t *>(m_nwin), c->stream));
     } else {
         HIP_TRY(launch_small_collect(n_seq, c->hit_count.as<uint32_t>(),
                                      want_calls ? c->call_count.as<uint32_t>() : nullptr, want_otu ? c->otu_count.as<uint32_t>() : nullptr, c->dense_hoff.as<uint64_t>(),
@@ -3324,15 +3338,15 @@ int process_batch_small(kgx_ctx *c, const kgx_params *params, const char *residu
                                      c->wbase.as<uint64_t>(), want_best ? c->best.as<kgx_best_call>() : nullptr,
                                      static_cast<kgx_best_call *>(mb), static_cast<uint32_t *>(m_st),
                                      static_cast<uint64_t *>(m_nwin), c->stream));
-        if (mh || mc || mo) /* a counts-and-best-calls batch (/lookup's) gathers nothing */
-            HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
-                                  c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
-                                  c->hits.as<uint4>() + c->hit_slots, c->calls.as<kgx_call>(),
-                                  c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
-                                  static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
-                                  c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
-                                  static_cast<kgx_otu *>(mo), c->stream));
     }
+    if (!fused && (mh || mc || mo)) /* a counts-and-best-calls batch (/lookup's) gathers nothing */
+        HIP_TRY(launch_gather(n_seq, c->wbase.as<uint64_t>(), c->hit_mask.as<uint64_t>(), c->tile_windows,
+                              c->call_count.as<uint32_t>(), c->hits.as<uint4>(),
+                              c->hits.as<uint4>() + c->hit_slots, c->calls.as<kgx_call>(),
+                              c->dense_hoff.as<uint64_t>(), c->dense_coff.as<uint64_t>(),
+                              static_cast<kgx_hit *>(mh), static_cast<kgx_call *>(mc), 0u, c->hit_format,
+                              c->otu_count.as<uint32_t>(), c->otus.as<kgx_otu>(), c->dense_ooff.as<uint64_t>(),
+                              static_cast<kgx_otu *>(mo), c->stream));
     /* kgx_lookup: the rollup queued behind the pass, one host wait for both */
     if (roll_map) {
         if ((rc = rollup_enqueue(roll_map, c, roll_mode)))

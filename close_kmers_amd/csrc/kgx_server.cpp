@@ -274,6 +274,12 @@ int usage(const char *argv0)
 int main(int argc, char **argv)
 {
     KmerRequestRouter::Options opt;
+    /* the workers wait for their device work asleep (polling every 20 us),
+     * not spinning: a server runs in a CPU share, and with 16 workers the
+     * spinning took it from the socket and text threads (r8: the 16-CPU
+     * cgroup throttled in 96% of its periods).  KGX_HOST_WAIT overrides. */
+    if (!std::getenv("KGX_HOST_WAIT"))
+        kgx_set_host_wait(KGX_WAIT_SLEEP, 20);
     const char *dev = std::getenv("KGX_DEVICE");
     opt.device = dev ? std::atoi(dev) : 0;
     std::string port_file = "/dev/null", bind_addr = "0.0.0.0";
