@@ -6,6 +6,7 @@
  * (fasta_parser.h:38-165, fasta_parser.cc:21-36).
  */
 #include "kguts_hip.h"
+#include "kgx_score_map.h"
 
 #include <algorithm>
 #include <charconv>
@@ -1403,6 +1404,92 @@ static bool stoi_param(const std::map<std::string, std::string> &p, const char *
     }
 }
 
+namespace {
+
+/* Helper threads for a request's text stage: run(parts, fn) calls fn(0 ..
+ * parts-1) once each, on the caller and on whichever helpers are idle (with
+ * none idle the caller runs every part itself).  KGX_TEXT_HELPERS threads
+ * (default 8, 0 = none), started on first use and never joined (a process
+ * may exit with them waiting). */
+class TextHelpers {
+public:
+    static TextHelpers &get()
+    {
+        static TextHelpers *h = new TextHelpers();
+        return *h;
+    }
+    uint32_t size() const { return n_; }
+    void run(uint32_t parts, const std::function<void(uint32_t)> &fn)
+    {
+        Job job{&fn, parts};
+        const bool shared = n_ && parts > 1;
+        if (shared) {
+            std::lock_guard<std::mutex> g(mu_);
+            jobs_.push_back(&job);
+        }
+        if (shared)
+            cv_.notify_all();
+        for (;;) {
+            uint32_t p;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                p = job.next < parts ? job.next++ : parts;
+                if (job.next == parts && shared)
+                    drop(&job);
+            }
+            if (p == parts)
+                break;
+            fn(p);
+            std::lock_guard<std::mutex> g(mu_);
+            job.done++;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return job.done == parts; });
+    }
+
+private:
+    struct Job {
+        const std::function<void(uint32_t)> *fn;
+        uint32_t parts;
+        uint32_t next = 0, done = 0;
+    };
+    TextHelpers()
+    {
+        const char *e = std::getenv("KGX_TEXT_HELPERS");
+        n_ = (uint32_t)std::max(0, std::min(64, e ? std::atoi(e) : 8));
+        for (uint32_t i = 0; i < n_; i++)
+            std::thread([this] { loop(); }).detach();
+    }
+    void drop(Job *j)
+    {
+        auto it = std::find(jobs_.begin(), jobs_.end(), j);
+        if (it != jobs_.end())
+            jobs_.erase(it);
+    }
+    void loop()
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return !jobs_.empty(); });
+            Job *j = jobs_.front(); /* a queued job has parts left */
+            const uint32_t p = j->next++;
+            if (j->next == j->parts)
+                jobs_.pop_front();
+            lk.unlock();
+            (*j->fn)(p);
+            lk.lock();
+            if (++j->done == j->parts)
+                done_cv_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job *> jobs_;
+    uint32_t n_ = 0;
+};
+
+}  // namespace
+
 LookupRequest::LookupRequest(std::shared_ptr<KmerPegMapping> mapping, bool family_mode,
                              const std::map<std::string, std::string> &params)
     : mapping_(mapping), family_mode_(family_mode)
@@ -1452,6 +1539,112 @@ void LookupRequest::process_flat(KmerGuts &kg, const char *res, const uint64_t *
             b++;
         process_piece(kg, fw, a, b, os);
         a = b;
+    }
+}
+
+void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0, uint32_t a, uint32_t b,
+                                     const kgx_best_call *best, const uint64_t *roff, const kgx_rollup_row *rows,
+                                     ScoreMap &smap, std::string &out) const
+{
+    typedef FamilyMapper::sequence_accumulated_score_t acc_t;
+    /* the per-sequence strings live across the part's sequences: their
+     * buffers are reused, not allocated per line */
+    std::string id, fn, ambig, lf_fam, lf_fn, gf_fam;
+    for (uint32_t s = a; s < b; s++) {
+        const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
+        id.assign(fw.ids + ia, ib - ia);
+        /* smap as the reference's operator[] calls leave it: the ids in
+         * first-touch order into the request's one map (cleared per sequence,
+         * its bucket count kept), so its iteration order is the reference's */
+        if (!smap.empty())
+            smap.clear();
+        for (uint64_t j = roff[s]; j < roff[s + 1]; j++) {
+            const kgx_rollup_row &row = rows[j];
+            acc_t &e = smap[row.id];
+            e.hit_count = row.hit_count;
+            e.hit_total = row.hit_total;
+            e.weighted_total = row.weighted_total;
+        }
+        {
+            int fi;
+            float score, wscore, offs = 0.0f;
+            ambig.clear();
+            kg.find_best_call(best[s], fi, fn, score, wscore, offs);
+            bool do_ambig = false;
+            if (fn.empty()) {
+                fn.assign("hypothetical protein");
+            } else {
+                const size_t where = fn.find(" ?? ");
+                if (where != std::string::npos) {
+                    if (allow_ambiguous_functions_) {
+                        ambig = fn.substr(where + 4);
+                        fn = fn.substr(0, where);
+                        do_ambig = true;
+                    } else {
+                        fn = "hypothetical protein";
+                    }
+                }
+            }
+            float lf_score = 0.0f, gf_score = 0.0f;
+            lf_fam.clear();
+            lf_fn.clear();
+            gf_fam.clear();
+            /* fresh maps per sequence, as the reference declares them
+             * (lookup_request.cc:259): their iteration order -- the tie
+             * order of the family pick below -- depends on it (an empty
+             * map allocates nothing) */
+            std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
+            for (const auto &hit_ent : smap) {
+                const acc_t &se = hit_ent.second;
+                if (se.hit_total < kmer_hit_threshold_)
+                    continue;
+                auto fent = mapping_->family_data_.find(hit_ent.first);
+                if (fent == mapping_->family_data_.end())
+                    continue;
+                const KmerPegMapping::family_data_t &fd = fent->second;
+                if (do_ambig) {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else if (fd.function == ambig)
+                        pgf_rollup_ambig[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                } else {
+                    if (fd.function == fn)
+                        pgf_rollup[fd.pgf] += se.weighted_total;
+                    else
+                        continue;
+                }
+                if (se.weighted_total > lf_score && fd.genus_id == target_genus_id_) {
+                    lf_score = se.weighted_total;
+                    lf_fam = fd.plf;
+                    lf_fn = fd.function;
+                }
+            }
+            auto *rollup = (do_ambig && lf_fn == ambig) ? &pgf_rollup_ambig : &pgf_rollup;
+            for (const auto &pgf_ent : *rollup)
+                if (pgf_ent.second > gf_score) {
+                    gf_score = pgf_ent.second;
+                    gf_fam = pgf_ent.first;
+                }
+            /* the iostream line (lookup_request.cc), floats as operator<< prints them (%.6g) */
+            out += id;
+            out += '\t';
+            out += gf_fam;
+            out += '\t';
+            append_f32(out, gf_score);
+            out += '\t';
+            out += lf_fam;
+            out += '\t';
+            append_f32(out, lf_score);
+            out += '\t';
+            out += do_ambig ? lf_fn : fn;
+            out += '\t';
+            append_f32(out, score);
+            out += '\t';
+            append_f32(out, wscore);
+            out += '\n';
+        }
     }
 }
 
@@ -1515,9 +1708,43 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
     stage_stats().gpu_ns += now_ns() - g0;
     StageClock text_clock(stage_stats().text_ns); /* the scoring and the output lines, to the end */
     typedef FamilyMapper::sequence_accumulated_score_t acc_t;
-    /* the per-sequence strings and maps live across the piece's sequences:
-     * their buffers are reused, not allocated per line */
-    std::string line, id, fn, ambig, lf_fam, lf_fn, gf_fam;
+    if (want_calls) {
+        /* the lines in parts on the text helpers (KGX_TEXT_HELPERS): part k
+         * starts from a map grown as the request's seq_score_ would be at
+         * its first sequence, so every map iterates as the reference's one
+         * does; the parts' text is written in order */
+        TextHelpers &th = TextHelpers::get();
+        const uint32_t P = std::max<uint32_t>(1u, std::min<uint32_t>(th.size() + 1, n / 768));
+        std::vector<uint32_t> cut(P + 1);
+        for (uint32_t k = 0; k <= P; k++)
+            cut[k] = (uint32_t)((uint64_t)n * k / P);
+        std::vector<size_t> most(P);
+        size_t m = seq_score_most_;
+        for (uint32_t k = 0, q = 0; k < P; k++) {
+            most[k] = m;
+            for (; q < cut[k + 1]; q++)
+                m = std::max<size_t>(m, (size_t)(roff[q + 1] - roff[q]));
+        }
+        std::vector<std::string> outs(P);
+        th.run(P, [&](uint32_t k) {
+            if (k == 0) {
+                best_match_lines(kg, fw, w0, cut[0], cut[1], best, roff, rows, seq_score_, outs[0]);
+                return;
+            }
+            ScoreMap score;
+            grow_to(score, most[k]);
+            best_match_lines(kg, fw, w0, cut[k], cut[k + 1], best, roff, rows, score, outs[k]);
+        });
+        for (const std::string &o : outs)
+            os.write(o.data(), (std::streamsize)o.size());
+        if (P > 1) {
+            seq_score_.clear();
+            grow_to(seq_score_, m);
+        }
+        seq_score_most_ = m;
+        return;
+    }
+    std::string id;
     for (uint32_t s = 0; s < n; s++) {
         const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
         id.assign(fw.ids + ia, ib - ia);
@@ -1533,88 +1760,7 @@ void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, s
             e.hit_total = row.hit_total;
             e.weighted_total = row.weighted_total;
         }
-        if (want_calls) {
-            int fi;
-            float score, wscore, offs = 0.0f;
-            ambig.clear();
-            kg.find_best_call(best[s], fi, fn, score, wscore, offs);
-            bool do_ambig = false;
-            if (fn.empty()) {
-                fn.assign("hypothetical protein");
-            } else {
-                const size_t where = fn.find(" ?? ");
-                if (where != std::string::npos) {
-                    if (allow_ambiguous_functions_) {
-                        ambig = fn.substr(where + 4);
-                        fn = fn.substr(0, where);
-                        do_ambig = true;
-                    } else {
-                        fn = "hypothetical protein";
-                    }
-                }
-            }
-            float lf_score = 0.0f, gf_score = 0.0f;
-            lf_fam.clear();
-            lf_fn.clear();
-            gf_fam.clear();
-            /* fresh maps per sequence, as the reference declares them
-             * (lookup_request.cc:259): their iteration order -- the tie
-             * order of the family pick below -- depends on it (an empty
-             * map allocates nothing) */
-            std::unordered_map<std::string, float> pgf_rollup, pgf_rollup_ambig;
-            for (const auto &hit_ent : seq_score_) {
-                const acc_t &se = hit_ent.second;
-                if (se.hit_total < kmer_hit_threshold_)
-                    continue;
-                auto fent = mapping_->family_data_.find(hit_ent.first);
-                if (fent == mapping_->family_data_.end())
-                    continue;
-                const KmerPegMapping::family_data_t &fd = fent->second;
-                if (do_ambig) {
-                    if (fd.function == fn)
-                        pgf_rollup[fd.pgf] += se.weighted_total;
-                    else if (fd.function == ambig)
-                        pgf_rollup_ambig[fd.pgf] += se.weighted_total;
-                    else
-                        continue;
-                } else {
-                    if (fd.function == fn)
-                        pgf_rollup[fd.pgf] += se.weighted_total;
-                    else
-                        continue;
-                }
-                if (se.weighted_total > lf_score && fd.genus_id == target_genus_id_) {
-                    lf_score = se.weighted_total;
-                    lf_fam = fd.plf;
-                    lf_fn = fd.function;
-                }
-            }
-            auto *rollup = (do_ambig && lf_fn == ambig) ? &pgf_rollup_ambig : &pgf_rollup;
-            for (const auto &pgf_ent : *rollup)
-                if (pgf_ent.second > gf_score) {
-                    gf_score = pgf_ent.second;
-                    gf_fam = pgf_ent.first;
-                }
-            /* the iostream line (lookup_request.cc), floats as operator<< prints them (%.6g) */
-            line.clear();
-            line += id;
-            line += '\t';
-            line += gf_fam;
-            line += '\t';
-            append_f32(line, gf_score);
-            line += '\t';
-            line += lf_fam;
-            line += '\t';
-            append_f32(line, lf_score);
-            line += '\t';
-            line += do_ambig ? lf_fn : fn;
-            line += '\t';
-            append_f32(line, score);
-            line += '\t';
-            append_f32(line, wscore);
-            line += '\n';
-            os.write(line.data(), (std::streamsize)line.size());
-        } else {
+        {
             typedef std::pair<KmerPegMapping::encoded_id_t, acc_t> data_t;
             std::vector<data_t> vec(seq_score_.begin(), seq_score_.end());
             std::sort(vec.begin(), vec.end(), [](const data_t &l, const data_t &rr) {

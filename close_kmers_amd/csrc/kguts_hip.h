@@ -516,8 +516,14 @@ private:
         const char *ids;
         const uint64_t *id_off;
     };
+    typedef std::unordered_map<KmerPegMapping::encoded_id_t, FamilyMapper::sequence_accumulated_score_t> ScoreMap;
     /* sequences [w0, w1) as one GPU pass, their rollups on the device */
     void process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, size_t w1, std::ostream &os);
+    /* the find_best_match lines of the piece's sequences [a, b) into out,
+     * `smap` in the state seq_score_ would be in at sequence a */
+    void best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0, uint32_t a, uint32_t b,
+                          const kgx_best_call *best, const uint64_t *roff, const kgx_rollup_row *rows,
+                          ScoreMap &smap, std::string &out) const;
     std::shared_ptr<KmerPegMapping> mapping_;
     bool family_mode_;
     unsigned int kmer_hit_threshold_ = 3;
@@ -525,7 +531,8 @@ private:
     bool allow_ambiguous_functions_ = false;
     bool find_reps_ = false;
     unsigned long target_genus_id_ = 0;
-    std::unordered_map<KmerPegMapping::encoded_id_t, FamilyMapper::sequence_accumulated_score_t> seq_score_;
+    ScoreMap seq_score_;
+    size_t seq_score_most_ = 0; /* the most rows seq_score_ has held (its bucket count follows from it) */
     LookupBatcher *batcher_ = nullptr;
 };
 

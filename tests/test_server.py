@@ -221,7 +221,7 @@ def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp
         recs.append(r)
         size += len(r)
         i += 1
-        if i % 50 == 0:
+        if i % every == 0:
             recs.append(base)
             size += len(base)
     body = b"".join(recs)
@@ -370,10 +370,41 @@ def test_concurrent_family_lookups_share_passes_and_match_golden(gpu):
             srv.close()
 
 
-def _big_body(seed=99, mib=5):
+@pytest.mark.gpu
+def test_family_lookup_text_parts_equal_serial_text(gpu):
+    """A family /lookup with find_best_match over a 3-MiB body (the golden
+    proteins again and again between random ones: pieces of thousands of
+    sequences, some with many rollup rows): the text written in parts on the
+    text helpers (each part's map grown as the request's map would be at the
+    part's first sequence, kgx_score_map.h) is the text of one thread
+    (KGX_TEXT_HELPERS=0) byte for byte, for every golden family parameter set."""
+    d = os.path.join(GOLDEN, "lookup")
+    cases = [f for f in _cases("lookup") if parse_case(f)[1].startswith("fam_")]
+    body = _big_body(seed=5, mib=3, base_name=os.path.join("lookup", "input.fasta"), every=3)
+    outs = {}
+    for helpers in ("0", "8"):
+        before = os.environ.get("KGX_TEXT_HELPERS")
+        os.environ["KGX_TEXT_HELPERS"] = helpers
+        try:
+            srv = Server(os.path.join(d, "data"), family_db=True, threads=2)
+        finally:
+            if before is None:
+                del os.environ["KGX_TEXT_HELPERS"]
+            else:
+                os.environ["KGX_TEXT_HELPERS"] = before
+        try:
+            outs[helpers] = [srv.request("POST", "/lookup?" + _query_string(parse_case(f)[1]), body) for f in cases]
+        finally:
+            srv.close()
+    for f, a, b in zip(cases, outs["0"], outs["8"]):
+        assert a.startswith(HEADER) and a.count(b"\n") > 3000, f
+        assert a == b, f
+
+
+def _big_body(seed=99, mib=5, base_name=os.path.join("scoring", "input.fasta"), every=50):
     import numpy as np
     from helpers import random_protein
-    base = open(os.path.join(GOLDEN, "scoring", "input.fasta"), "rb").read()
+    base = open(os.path.join(GOLDEN, base_name), "rb").read()
     rng = np.random.default_rng(seed)
     recs, size, i = [base], len(base), 0
     while size < mib << 20:
