@@ -221,7 +221,7 @@ def test_large_query_body_runs_in_pieces_and_matches_oracle(gpu, oracle_lib, tmp
         recs.append(r)
         size += len(r)
         i += 1
-        if i % every == 0:
+        if i % 50 == 0:
             recs.append(base)
             size += len(base)
     body = b"".join(recs)
@@ -412,7 +412,7 @@ def _big_body(seed=99, mib=5, base_name=os.path.join("scoring", "input.fasta"), 
         recs.append(r)
         size += len(r)
         i += 1
-        if i % 50 == 0:
+        if i % every == 0:
             recs.append(base)
             size += len(base)
     return b"".join(recs)
