@@ -9,6 +9,7 @@
 #include "kgx_score_map.h"
 
 #include <algorithm>
+#include <x86intrin.h>
 #include <charconv>
 #include <cmath>
 #include <array>
@@ -55,24 +56,28 @@ void StageStats::reset()
     for (auto *a : {&requests, &bytes_in, &bytes_out, &gpu_passes, &recv_ns, &parse_ns, &gpu_ns, &text_ns, &handle_ns,
                     &send_ns, &batched_pieces, &batched_passes})
         a->store(0);
+    for (auto &a : text_cycles)
+        a.store(0);
 }
 
 std::string StageStats::json() const
 {
-    char b[512];
+    char b[768];
     const double r = (double)std::max<uint64_t>(1, requests.load());
     std::snprintf(b, sizeof b,
                   "{\"requests\": %llu, \"bytes_in\": %llu, \"bytes_out\": %llu, \"gpu_passes\": %llu, "
                   "\"batched_pieces\": %llu, \"batched_passes\": %llu, "
                   "\"ms_per_request\": {\"recv\": %.4f, \"parse\": %.4f, \"gpu\": %.4f, \"text\": %.4f, \"handle\": %.4f, "
-                  "\"send\": %.4f}}\n",
+                  "\"send\": %.4f}, \"text_cycles\": [%llu, %llu, %llu, %llu, %llu]}\n",
                   (unsigned long long)requests.load(), (unsigned long long)bytes_in.load(),
                   (unsigned long long)bytes_out.load(), (unsigned long long)gpu_passes.load(),
                   (unsigned long long)batched_pieces.load(), (unsigned long long)batched_passes.load(),
                   recv_ns.load() / r * 1e-6,
                   parse_ns.load() / r * 1e-6, gpu_ns.load() / r * 1e-6, text_ns.load() / r * 1e-6,
                   handle_ns.load() / r * 1e-6,
-                  send_ns.load() / r * 1e-6);
+                  send_ns.load() / r * 1e-6, (unsigned long long)text_cycles[0].load(),
+                  (unsigned long long)text_cycles[1].load(), (unsigned long long)text_cycles[2].load(),
+                  (unsigned long long)text_cycles[3].load(), (unsigned long long)text_cycles[4].load());
     return b;
 }
 
@@ -1409,8 +1414,10 @@ namespace {
 /* Helper threads for a request's text stage: run(parts, fn) calls fn(0 ..
  * parts-1) once each, on the caller and on whichever helpers are idle (with
  * none idle the caller runs every part itself).  KGX_TEXT_HELPERS threads
- * (default 8, 0 = none), started on first use and never joined (a process
- * may exit with them waiting). */
+ * (default 0: none; r8 at 16 clients on the box's 16-CPU share: 8.59e9
+ * residues/s with none, 7.76e9 with 4, 7.34e9 with 8 -- the parts cost more
+ * CPU than the share has spare), started on first use and never joined (a
+ * process may exit with them waiting). */
 class TextHelpers {
 public:
     static TextHelpers &get()
@@ -1456,7 +1463,7 @@ private:
     TextHelpers()
     {
         const char *e = std::getenv("KGX_TEXT_HELPERS");
-        n_ = (uint32_t)std::max(0, std::min(64, e ? std::atoi(e) : 8));
+        n_ = (uint32_t)std::max(0, std::min(64, e ? std::atoi(e) : 0));
         for (uint32_t i = 0; i < n_; i++)
             std::thread([this] { loop(); }).detach();
     }
@@ -1550,6 +1557,15 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
     /* the per-sequence strings live across the part's sequences: their
      * buffers are reused, not allocated per line */
     std::string id, fn, ambig, lf_fam, lf_fn, gf_fam;
+    static const bool clocks = std::getenv("KGX_TEXT_CLOCKS") != nullptr;
+    uint64_t cyc[5] = {0, 0, 0, 0, 0}, t_last = clocks ? __rdtsc() : 0;
+    auto tick = [&](int k) {
+        if (clocks) {
+            const uint64_t t = __rdtsc();
+            cyc[k] += t - t_last;
+            t_last = t;
+        }
+    };
     for (uint32_t s = a; s < b; s++) {
         const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
         id.assign(fw.ids + ia, ib - ia);
@@ -1565,6 +1581,7 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
             e.hit_total = row.hit_total;
             e.weighted_total = row.weighted_total;
         }
+        tick(0);
         {
             int fi;
             float score, wscore, offs = 0.0f;
@@ -1585,6 +1602,7 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
                     }
                 }
             }
+            tick(1);
             float lf_score = 0.0f, gf_score = 0.0f;
             lf_fam.clear();
             lf_fn.clear();
@@ -1621,12 +1639,14 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
                     lf_fn = fd.function;
                 }
             }
+            tick(2);
             auto *rollup = (do_ambig && lf_fn == ambig) ? &pgf_rollup_ambig : &pgf_rollup;
             for (const auto &pgf_ent : *rollup)
                 if (pgf_ent.second > gf_score) {
                     gf_score = pgf_ent.second;
                     gf_fam = pgf_ent.first;
                 }
+            tick(3);
             /* the iostream line (lookup_request.cc), floats as operator<< prints them (%.6g) */
             out += id;
             out += '\t';
@@ -1645,7 +1665,11 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
             append_f32(out, wscore);
             out += '\n';
         }
+        tick(4);
     }
+    if (clocks)
+        for (int k = 0; k < 5; k++)
+            stage_stats().text_cycles[k] += cyc[k];
 }
 
 void LookupRequest::process_piece(KmerGuts &kg, const FlatWork &fw, size_t w0, size_t w1, std::ostream &os)

@@ -48,6 +48,9 @@ struct StageStats {
     std::atomic<uint64_t> recv_ns{0}, parse_ns{0}, gpu_ns{0}, text_ns{0}, handle_ns{0}, send_ns{0};
     /* /lookup pieces that shared a pass (LookupBatcher) and those passes */
     std::atomic<uint64_t> batched_pieces{0}, batched_passes{0};
+    /* KGX_TEXT_CLOCKS=1: TSC cycles of the family /lookup text's steps (rows
+     * into the map, best call, family loop, family pick, line) */
+    std::atomic<uint64_t> text_cycles[5] = {};
     void reset();
     std::string json() const;
 };
