@@ -1566,7 +1566,23 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
             t_last = t;
         }
     };
+    /* a block's family lookups and name fetches first: independent of each
+     * other, so their cache misses overlap instead of stalling one by one */
+    constexpr uint32_t BLK = 16;
+    std::vector<const KmerPegMapping::family_data_t *> fdv;
+    uint64_t fd0 = 0;
     for (uint32_t s = a; s < b; s++) {
+        if ((s - a) % BLK == 0) {
+            const uint32_t e = std::min(b, s + BLK);
+            fd0 = roff[s];
+            fdv.resize(roff[e] - fd0);
+            for (uint64_t j = fd0; j < roff[e]; j++) {
+                auto it = mapping_->family_data_.find(rows[j].id);
+                fdv[j - fd0] = it == mapping_->family_data_.end() ? nullptr : &it->second;
+            }
+            for (uint32_t q = s; q < e; q++)
+                kg.prefetch_call_names(best[q]);
+        }
         const size_t ia = fw.id_off[w0 + s], ib = fw.id_off[w0 + s + 1];
         id.assign(fw.ids + ia, ib - ia);
         /* smap as the reference's operator[] calls leave it: the ids in
@@ -1616,10 +1632,22 @@ void LookupRequest::best_match_lines(KmerGuts &kg, const FlatWork &fw, size_t w0
                 const acc_t &se = hit_ent.second;
                 if (se.hit_total < kmer_hit_threshold_)
                     continue;
-                auto fent = mapping_->family_data_.find(hit_ent.first);
-                if (fent == mapping_->family_data_.end())
+                /* the entry's family, looked up with the block (a search of
+                 * the sequence's rows; past 32 rows the map again) */
+                const KmerPegMapping::family_data_t *fdp = nullptr;
+                if (roff[s + 1] - roff[s] <= 32) {
+                    for (uint64_t j = roff[s]; j < roff[s + 1]; j++)
+                        if (rows[j].id == hit_ent.first) {
+                            fdp = fdv[j - fd0];
+                            break;
+                        }
+                } else {
+                    auto fent = mapping_->family_data_.find(hit_ent.first);
+                    fdp = fent == mapping_->family_data_.end() ? nullptr : &fent->second;
+                }
+                if (!fdp)
                     continue;
-                const KmerPegMapping::family_data_t &fd = fent->second;
+                const KmerPegMapping::family_data_t &fd = *fdp;
                 if (do_ambig) {
                     if (fd.function == fn)
                         pgf_rollup[fd.pgf] += se.weighted_total;

@@ -257,6 +257,16 @@ public:
                           const KmerOtuStats &otu_stats) const;
 
     const char *function_at_index(int i) const;
+    /* the name(s) a best call will print, toward the cache (the text stage
+     * asks a block of sequences ahead) */
+    void prefetch_call_names(const kgx_best_call &b) const
+    {
+        for (int k = 0; k < (b.kind == 2 ? 2 : b.kind == 1 ? 1 : 0); k++) {
+            const int i = k ? b.fi1 : b.fi0;
+            if (i >= 0 && (size_t)i < functions_.size())
+                __builtin_prefetch(functions_[i].data());
+        }
+    }
     int function_count() const { return (int)functions_.size(); }
     static void decoded_kmer(unsigned long long encodedK, char *decoded);
     static unsigned long long encoded_aa_kmer(const char *p);
