@@ -582,6 +582,50 @@ static size_t format_g6(char *b, size_t cap, float v)
     }
     if (d > -1e6 && d < 1e6 && d == (double)(long long)d)
         return (size_t)(std::to_chars(b, b + cap, (long long)d).ptr - b);
+    /* 1e-4 <= |v| < 1e6 (the scores): with 10^e <= |v| < 10^(e+1), |v| *
+     * 10^(5-e) is exact in a double (24 + at most 21 bits), so rounding it
+     * to an integer (nearbyint: to nearest, ties to even) gives printf's six
+     * significant digits; fixed notation, trailing zeros dropped */
+    static const double p10[] = {1e-4, 1e-3, 1e-2, 1e-1, 1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9};
+    const double a = std::fabs(d);
+    if (cap >= 16 && a >= 1e-4 && a < 1e6) {
+        int e = 5;
+        while (a < p10[e + 4])
+            e--;
+        long long r = (long long)std::nearbyint(a * p10[5 - e + 4]);
+        if (r == 1000000) { /* rounded up to 10^(e+1) */
+            if (e == 5)
+                return (size_t)(std::to_chars(b, b + cap, d, std::chars_format::general, 6).ptr - b);
+            r = 100000;
+            e++;
+        }
+        char dig[6];
+        for (int i = 5; i >= 0; i--, r /= 10)
+            dig[i] = (char)('0' + r % 10);
+        size_t n = 0;
+        if (d < 0)
+            b[n++] = '-';
+        int last = 5; /* the last significant digit kept */
+        while (last > 0 && last > e && dig[last] == '0')
+            last--;
+        if (e >= 0) {
+            for (int i = 0; i <= e; i++)
+                b[n++] = dig[i];
+            if (last > e) {
+                b[n++] = '.';
+                for (int i = e + 1; i <= last; i++)
+                    b[n++] = dig[i];
+            }
+        } else {
+            b[n++] = '0';
+            b[n++] = '.';
+            for (int i = 0; i < -e - 1; i++)
+                b[n++] = '0';
+            for (int i = 0; i <= last; i++)
+                b[n++] = dig[i];
+        }
+        return n;
+    }
     return (size_t)(std::to_chars(b, b + cap, d, std::chars_format::general, 6).ptr - b);
 }
 

@@ -171,8 +171,9 @@ def test_host_wait_modes(kgx):
 def test_format_g6_matches_printf(kgx):
     """kgx_format_g6 -- how the handlers print floats (operator<< at the
     default precision = printf's %.6g of the value widened to double), with
-    its fast path for integral values below 1e6 -- against Python's %-format
-    (C printf semantics) on edge values and 300k random floats."""
+    its fast paths for integral values below 1e6 and for 1e-4 <= |v| < 1e6 --
+    against Python's %-format (C printf semantics) on edge values, ties at
+    the sixth digit and 520k random floats."""
     import ctypes
     rng = np.random.default_rng(6)
     vals = [0.0, -0.0, 1.0, -1.0, 999999.0, -999999.0, 1e6, -1e6, 1234567.0, 0.5, 1e-5, 123456.5,
@@ -180,6 +181,15 @@ def test_format_g6_matches_printf(kgx):
     vals += rng.integers(-2_000_000, 2_000_000, 100_000).astype(np.float32).tolist()
     vals += (rng.standard_normal(100_000) * 10.0 ** rng.integers(-8, 9, 100_000)).astype(np.float32).tolist()
     vals += rng.integers(0, 300, 100_000).astype(np.float32).tolist()
+    # exact decimal ties at the sixth digit (ties to even) and their neighbours,
+    # across the fast path's decades, and values that round up to a power of ten
+    ints = rng.integers(100_000, 1_000_000, 20_000)
+    for scale in (1.0, 2.0, 4.0, 8.0, 16.0, 0.5):
+        vals += ((ints + 0.5) / scale).astype(np.float32).tolist()
+    for p in range(-4, 6):
+        for x in (9.999995, 9.999994, 9.999996, 1.0000005, 9.9999995):
+            vals += [x * 10.0 ** p, -x * 10.0 ** p]
+    vals += (rng.random(100_000) * 10.0 ** rng.integers(-5, 7, 100_000)).astype(np.float32).tolist()
     buf = ctypes.create_string_buffer(64)
     L = kgx.lib()
     for v in vals:
