@@ -856,7 +856,10 @@ int kgx_kmap_device(const kgx_kmap *map);
  * over `map` (on the context's device) enqueued together -- upload, plan,
  * probe, score, the counts (and best calls) into mapped memory, the rollup
  * sized by the context's previous one -- and one host wait for both, instead
- * of kgx_process_batch's wait and then kgx_kmap_rollup's.  want within
+ * of kgx_process_batch's wait and then kgx_kmap_rollup's.  A batch
+ * kgx_process_batch would run down its small-batch path (up to the context's
+ * small_batch residues, 65,536 sequences, one chunk) runs down that path with
+ * the rollup queued behind it; others take the one-pass path.  want within
  * KGX_WANT_CALLS | KGX_WANT_BEST; results as those two calls give them (out:
  * no hits; the views valid until the context's next call). */
 int kgx_lookup(kgx_ctx *ctx, kgx_kmap *map, int mode, const kgx_params *params, const char *residues,
