@@ -29,8 +29,8 @@ timeout -k 10 900 python3 tools/bench_server.py --families 100000 --path "/looku
     --clients 1,8,16 --threads 16 > "$OUT/bench_lookup_fam.json" 2> "$OUT/bench_lookup_fam.err"
 fi
 if [ "$PART" != 1 ]; then
-KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
-KGX_FACADE_OTU=1 KGX_FACADE_MODES=2 timeout -k 10 300 python3 tools/bench_facade.py \
+KGX_LINE_INDEX=36 KGX_FACADE_BESIDE=8 timeout -k 10 600 python3 tools/bench_facade.py > "$OUT/bench_facade.json" 2> "$OUT/bench_facade.err"
+KGX_LINE_INDEX=36 KGX_FACADE_OTU=1 KGX_FACADE_MODES=2 timeout -k 10 300 python3 tools/bench_facade.py \
     > "$OUT/bench_facade_otu.json" 2> "$OUT/bench_facade_otu.err"
 timeout -k 10 600 python3 tools/bench_pool.py > "$OUT/bench_pool.json" 2> "$OUT/bench_pool.err"
 timeout -k 10 600 python3 bench.py --pool-devices 2 > "$OUT/bench_pool_devices.json" 2> "$OUT/bench_pool_devices.err"
