@@ -2596,9 +2596,11 @@ __global__ __launch_bounds__(256) void small_collect_best_kernel(
     const uint32_t t = threadIdx.x, s0 = blockIdx.x * 256u, i = s0 + t;
     for (int a = 0; a < 3; a++) {
         uint64_t v = 0, before = 0, tot = 0;
-        if (cnt.c[a])
+        if (cnt.c[a]) {
+#pragma unroll 8
             for (uint32_t j = t; j < s0; j += 256)
                 v += cnt.c[a][j];
+        }
         (void)block_scan(v, lds_pre[a], before);
         const uint64_t mine = cnt.c[a] && i < n ? cnt.c[a][i] : 0;
         const uint64_t at = before + block_scan(mine, lds_own[a], tot) - mine;
