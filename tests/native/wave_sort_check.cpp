@@ -17,6 +17,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -146,6 +147,44 @@ int main(int argc, char **argv)
             k++;
         }
         std::printf("{\"cold_n33-64_ns\": %.0f, \"cold_sorts\": %u}\n", k ? t / k : 0.0, k);
+    }
+    /* lists shaped like the service's 36-OTU calls (tests/perf_svc_otu_phases.py,
+     * mod 97): 36 pairs whose counts are ~150 hits dealt over them at random */
+    {
+        const uint32_t K = std::min<uint32_t>(cases, 500);
+        std::vector<kgx_otu> in36(256 * (size_t)K), want36(256 * (size_t)K);
+        std::vector<uint32_t> n36(K, 36);
+        for (uint32_t c = 0; c < K; c++) {
+            int cnt[36] = {0};
+            for (int h = 0; h < 150; h++)
+                cnt[rng() % 36]++;
+            for (uint32_t i = 0; i < 36; i++)
+                in36[256 * (size_t)c + i] = kgx_otu{(int32_t)i * 97 + 3, cnt[i]};
+            std::copy(in36.begin() + 256 * (size_t)c, in36.begin() + 256 * (size_t)c + 36,
+                      want36.begin() + 256 * (size_t)c);
+            lstd_sort(want36.data() + 256 * (size_t)c, (int64_t)36, ByCount{});
+        }
+        CHECK(hipMemcpy(d_in, in36.data(), in36.size() * sizeof(kgx_otu), hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(d_n, n36.data(), K * sizeof(uint32_t), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(wave_sort_kernel, dim3(1), dim3(64), 0, 0, d_in, d_n, K, d_out, d_ns, 1);
+        CHECK(hipGetLastError());
+        CHECK(hipDeviceSynchronize());
+        std::vector<uint64_t> ns(K);
+        std::vector<kgx_otu> got36(in36.size());
+        CHECK(hipMemcpy(got36.data(), d_out, got36.size() * sizeof(kgx_otu), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(ns.data(), d_ns, K * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        double t = 0;
+        for (uint32_t c = 0; c < K; c++) {
+            t += (double)ns[c];
+            for (uint32_t i = 0; i < 36; i++) {
+                const kgx_otu &g = got36[256 * (size_t)c + i], &w = want36[256 * (size_t)c + i];
+                if (g.otu_index != w.otu_index || g.count != w.count) {
+                    std::printf("mismatch (36-OTU lists) case %u at %u\n", c, i);
+                    return 1;
+                }
+            }
+        }
+        std::printf("{\"svc36_ns\": %.0f, \"svc36_sorts\": %u}\n", t / K, K);
     }
     (void)hipFree(d_in);
     (void)hipFree(d_out);
