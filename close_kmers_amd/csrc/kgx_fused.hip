@@ -112,8 +112,14 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
 {
     typedef FusedInput<IN> In;
     const bool dbg = a.dbg && s == 0 && threadIdx.x == 0;
+    /* the stamps go to LDS and out to the mapped a.dbg only before the done
+     * token: a store to host memory in the middle of a phase made the next
+     * wait on stores (any s_waitcnt vmcnt) wait for PCIe, inflating the
+     * phase it sat in (the OTU by-count sort: 4.0 us in the service against
+     * 2.3 us for the same lists alone, tests/native/wave_sort_check.cpp) */
+    __shared__ uint64_t dstamp[16];
     if (dbg)
-        a.dbg[0] = wall_clock64();
+        dstamp[0] = wall_clock64();
     __shared__ uint8_t code_tab[256];
     __shared__ uint8_t codes_own[256 * FJ + 8];
     constexpr bool SLOT = std::is_same<IN, FusedSlot>::value;
@@ -141,7 +147,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         __syncthreads();
     }
     if (dbg)
-        a.dbg[1] = wall_clock64();
+        dstamp[1] = wall_clock64();
 
     uint32_t nh = 0;
     const uint32_t J = (W + 255) / 256; /* 256-window slices */
@@ -198,7 +204,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             const uint64_t NS = a.num_sigs;
             uint32_t rounds = 0;
             if (dbg && jb == 0)
-                a.dbg[12] = wall_clock64(); /* keys and homes computed */
+                dstamp[12] = wall_clock64(); /* keys and homes computed */
             if constexpr (QUAD) {
                 /* the loads by quads (the call service): the 4 lanes of quad g
                  * read window g + 64 i's line, 16 B each, one instruction for
@@ -236,7 +242,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     rounds++;
                     if (dbg && rounds == 1 && jb == 0) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        a.dbg[13] = wall_clock64(); /* thread 0's own loads back */
+                        dstamp[13] = wall_clock64(); /* thread 0's own loads back */
                     }
                     const bool turned = rounds >= turn;
                     bool more = false;
@@ -267,7 +273,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     }
                     const bool again = __syncthreads_or(more);
                     if (dbg && rounds == 1 && jb == 0)
-                        a.dbg[11] = wall_clock64(); /* the first round examined */
+                        dstamp[11] = wall_clock64(); /* the first round examined */
                     if (!again)
                         break;
                 }
@@ -320,19 +326,19 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     }
                     if (dbg && rounds == 0 && jb == 0) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        a.dbg[13] = wall_clock64(); /* thread 0's own loads back */
+                        dstamp[13] = wall_clock64(); /* thread 0's own loads back */
                     }
                     const bool again = __syncthreads_or(more);
                     if (dbg && rounds++ == 0 && jb == 0)
-                        a.dbg[11] = wall_clock64(); /* the first round examined */
+                        dstamp[11] = wall_clock64(); /* the first round examined */
                     if (!again)
                         break;
                 }
             }
             if (dbg) {
-                a.dbg[10] = (jb == 0 ? 0 : a.dbg[10]) + rounds;
+                dstamp[10] = (jb == 0 ? 0 : dstamp[10]) + rounds;
                 if (jb + RB >= J)
-                    a.dbg[2] = wall_clock64();
+                    dstamp[2] = wall_clock64();
             }
 
             /* 3. ordered compaction into LDS: slice j = windows [256 j, 256 j
@@ -364,7 +370,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
     }
     if (dbg)
-        a.dbg[3] = wall_clock64();
+        dstamp[3] = wall_clock64();
 
     const bool want_otu = (a.want & KGX_WANT_OTU) != 0;
     if (want_otu) {
@@ -383,7 +389,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         }
 
     if (dbg)
-        a.dbg[6] = wall_clock64(); /* thread 0's record stores issued */
+        dstamp[6] = wall_clock64(); /* thread 0's record stores issued */
     /* 4b. the run scorer, wave 0, 64 hits per step (score_wave_kernel's
      * chunk rules for a single sequence) */
     uint32_t ncalls_out = 0;
@@ -455,7 +461,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             const bool memb = act && (fi == cur || ((S >> k) & 1));
             const uint64_t MEMB = __ballot(memb);
             if (dbg && h0 == 0)
-                a.dbg[14] = wall_clock64(); /* the first chunk's runs and members */
+                dstamp[14] = wall_clock64(); /* the first chunk's runs and members */
             if (SW & 1) { /* the open run flushes; the pair (last hit, lane 0) carries */
                 close_open();
                 o_cur = rl32(fi, 0);
@@ -503,7 +509,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
                     ws = acc;
             }
             if (dbg && h0 == 0)
-                a.dbg[15] = wall_clock64(); /* the first chunk's sums */
+                dstamp[15] = wall_clock64(); /* the first chunk's sums */
             const uint64_t EMIT = __ballot(is_start && closed && (int)c_seg >= prm.min_hits && ws >= min_wh);
             const uint32_t idx = o_ncalls + (uint32_t)__popcll(EMIT & bit_range(0, k));
             if (want_otu && act && ((MEMB >> k) & 1)) { /* a counted member of a sub-run emitted here */
@@ -536,7 +542,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             p_fi = rl32(fi, n - 1);
             p_wt = rlf(wt, n - 1);
             if (dbg && h0 == 0)
-                a.dbg[9] = wall_clock64(); /* the first 64-hit chunk scored */
+                dstamp[9] = wall_clock64(); /* the first 64-hit chunk scored */
         }
         if (o_valid) /* the final flush (kguts.cc:873-876) */
             close_open();
@@ -558,7 +564,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         constexpr uint32_t KREG = 8;
         __shared__ LstdPart ostack[64];
         if (dbg)
-            a.dbg[7] = wall_clock64();
+            dstamp[7] = wall_clock64();
         kgx_otu *o = reinterpret_cast<kgx_otu *>(hrec);
         __syncthreads();
         if (wave == 0) {
@@ -727,7 +733,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             __syncthreads();
         }
         if (dbg)
-            a.dbg[8] = wall_clock64();
+            dstamp[8] = wall_clock64();
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
          * it, lstd_sort_wave64_reg up to 64 pairs (the pairs in registers),
          * lstd_sort_wave up to 64 SW
@@ -754,7 +760,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     }
 
     if (dbg)
-        a.dbg[4] = wall_clock64();
+        dstamp[4] = wall_clock64();
     /* 5. counts, then the token: every store above is visible to the host
      * before it sees done[s] == token */
     if (t == 0) {
@@ -767,8 +773,12 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
     __syncthreads();
     if (t == 0) {
         __threadfence_system();
-        if (dbg)
-            a.dbg[5] = wall_clock64();
+        if (dbg) {
+            dstamp[5] = wall_clock64();
+            for (int k = 0; k < 16; k++)
+                a.dbg[k] = dstamp[k];
+            __threadfence_system();
+        }
         *reinterpret_cast<volatile uint32_t *>(a.done + s) = a.token;
     }
 }
