@@ -134,7 +134,7 @@ __device__ __forceinline__ kgx_otu otu_lane(const kgx_otu &v, uint32_t j)
 }
 
 template <class C>
-__device__ __attribute__((noinline)) void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl, kgx_otu *br)
+__device__ __forceinline__ void lstd_sort_wave64_reg(kgx_otu *a, uint32_t n, C comp, kgx_otu *bl, kgx_otu *br)
 {
     const uint32_t lane = lane_id();
     const uint64_t le = lanes_le(lane), below = le & ~(1ull << lane);
