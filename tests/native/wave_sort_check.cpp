@@ -59,6 +59,36 @@ __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const 
     }
 }
 
+/* the register sort as the call service runs it: wave 0 of a 256-thread
+ * workgroup sorts while waves 1-3 wait at the barrier, with most of the LDS
+ * allocated (`big`: 96 KiB more) */
+__global__ __launch_bounds__(256) void wave_sort_wg_kernel(const kgx_otu *in, const uint32_t *n_of, uint32_t cases,
+                                                           kgx_otu *out, uint64_t *ns, int big)
+{
+    extern __shared__ uint8_t dyn[];
+    __shared__ kgx_otu a[256], bl[256], br[256];
+    const uint32_t t = threadIdx.x;
+    if (big && t == 0)
+        dyn[0] = 0;
+    for (uint32_t c = 0; c < cases; c++) {
+        const uint32_t n = n_of[c];
+        for (uint32_t i = t; i < n; i += 256)
+            a[i] = in[256 * c + i];
+        __syncthreads();
+        if (t < 64) {
+            const uint64_t t0 = wall_clock64();
+            lstd_sort_wave64_reg(a, n, ByCount{}, bl, br);
+            const uint64_t t1 = wall_clock64();
+            if (t == 0)
+                ns[c] = (t1 - t0) * 10;
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < n; i += 256)
+            out[256 * c + i] = a[i];
+        __syncthreads();
+    }
+}
+
 #define CHECK(x)                                                                   \
     do {                                                                           \
         hipError_t e_ = (x);                                                       \
@@ -185,6 +215,17 @@ int main(int argc, char **argv)
             }
         }
         std::printf("{\"svc36_ns\": %.0f, \"svc36_sorts\": %u}\n", t / K, K);
+        for (int big = 0; big < 2; big++) {
+            hipLaunchKernelGGL(wave_sort_wg_kernel, dim3(1), dim3(256), big ? 96 * 1024 : 0, 0, d_in, d_n, K, d_out,
+                               d_ns, big);
+            CHECK(hipGetLastError());
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipMemcpy(ns.data(), d_ns, K * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            double tw = 0;
+            for (uint32_t c = 0; c < K; c++)
+                tw += (double)ns[c];
+            std::printf("{\"svc36_wg256_%s_ns\": %.0f}\n", big ? "lds96k" : "lds", tw / K);
+        }
     }
     (void)hipFree(d_in);
     (void)hipFree(d_out);
