@@ -725,39 +725,6 @@ def main():
                        for v, t in times.items()}}
         log(f"[bench] probe A/B: {probe_ab}")
 
-    d.barrier()
-    for c in ctxs:
-        c.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(None, ctxs[i % len(ctxs)], i)
-    for c in ctxs:
-        c.synchronize()
-    d.barrier()
-    t_wall = time.perf_counter() - t_start
-    t_max = d.max(t_wall)
-    last = ctxs[(args.steps - 1) % len(ctxs)]
-
-    # sanity: counts of the last step
-    out = abi.DeviceResult()
-    abi.check(L.kgx_device_result_get(last.handle, ctypes.byref(out)), "result")
-    last.check_plan()
-    hc = np.empty(n, np.uint32)
-    cc = np.empty(n, np.uint32)
-    abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
-    abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
-    total_hits = int(d.sum(float(hc.sum())))
-    mine = {"rank": d.rank, "device": dev, "ms_per_step": t_wall * 1e3 / args.steps,
-            "probe_ms": float(np.mean(probe_ms)), "n_seq": n, "hits": int(hc.sum())}
-    if canary_recs:
-        c = canary_recs[d.rank]
-        mine["canary"] = {"ok": c["ok"], "digest": c["digest"][:16], "hits": c["hits"], "calls": c["calls"]}
-    per_rank = d.gather_objects(mine)
-    log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
-        f"(even-q mean {hc[::2].mean():.1f}, odd-q mean {hc[1::2].mean():.2f}); "
-        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
-        f"probe {np.mean(probe_ms):.3f} ms")
-
     def pipelined_ab(name, values, rounds, restore):
         """Interleaved A/B of a context option over the timed loop's shape:
         the same batches and worker contexts, each sample a run of
@@ -794,20 +761,34 @@ def main():
                          "step_ms": [round(x, 4) for x in samples[v]["step"]],
                          "probe_ms": [round(x, 4) for x in samples[v]["probe"]]} for v in values}
 
-    # the line index, settled in this process: option line_index 0 (probes
-    # over the reference slots) and 1 (the index) on the same batches
+    # the line index, settled in this process before the timed steps: option
+    # line_index 0 (probes over the reference slots) and 1 (the index) on the
+    # same batches; the timed steps then run the faster of the two on this
+    # box (round 6 measured +11.6% .. -0.3% across seven boxes)
     line_ab = None
+    use_index = 1 if line_lines else 0
     if line_lines and args.line_index_ab > 0:
         med = pipelined_ab("line_index", [0, 1], args.line_index_ab, 1)
         gain = med["0"]["median_step_ms"] / med["1"]["median_step_ms"] - 1.0
+        use_index = 1 if gain >= 0 else 0
+        for c in ctxs:
+            c.set_option("line_index", use_index)
         line_ab = {"rounds": args.line_index_ab, "steps_per_sample": args.ab_steps, "load": args.line_index,
                    "without_index": med["0"], "with_index": med["1"],
-                   "step_gain": gain,
-                   "note": "one process, same batches and worker contexts; context option line_index 0 = probes "
-                           "over the reference slots, 1 = over the line index; step_gain = without / with - 1"}
+                   "step_gain": gain, "timed_with_index": bool(use_index),
+                   "note": "one process, same batches and worker contexts, before the timed steps; context option "
+                           "line_index 0 = probes over the reference slots, 1 = over the line index; step_gain = "
+                           "without / with - 1; the timed steps, the probe time and the parity check use the faster"}
         log(f"[bench] line index A/B ({args.line_index_ab} rounds): step {med['0']['median_step_ms']:.4f} ms "
             f"without, {med['1']['median_step_ms']:.4f} with ({gain * 100:+.1f}%); probe "
-            f"{med['0']['median_probe_ms']:.4f} / {med['1']['median_probe_ms']:.4f} ms")
+            f"{med['0']['median_probe_ms']:.4f} / {med['1']['median_probe_ms']:.4f} ms; timed "
+            f"{'with' if use_index else 'without'} the index")
+        if not use_index:  # the probe time under the timed configuration
+            probe_ms.clear()
+            for i in range(max(3, min(args.steps, 10))):
+                step(probe_ms, ctx, i)
+            ctx.synchronize()
+    timed_load = args.line_index if (line_lines and use_index) else 0
     pipe_ab = None
     if args.pipe_ab:
         name, vals = args.pipe_ab.split("=")
@@ -816,6 +797,39 @@ def main():
         log(f"[bench] pipelined A/B of {name}: " + ", ".join(
             f"{v}: step {pipe_ab[str(v)]['median_step_ms']:.4f} probe {pipe_ab[str(v)]['median_probe_ms']:.4f} ms"
             for v in values))
+
+    d.barrier()
+    for c in ctxs:
+        c.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(None, ctxs[i % len(ctxs)], i)
+    for c in ctxs:
+        c.synchronize()
+    d.barrier()
+    t_wall = time.perf_counter() - t_start
+    t_max = d.max(t_wall)
+    last = ctxs[(args.steps - 1) % len(ctxs)]
+
+    # sanity: counts of the last step
+    out = abi.DeviceResult()
+    abi.check(L.kgx_device_result_get(last.handle, ctypes.byref(out)), "result")
+    last.check_plan()
+    hc = np.empty(n, np.uint32)
+    cc = np.empty(n, np.uint32)
+    abi.check(L.kgx_memcpy_d2h(hc.ctypes.data, out.hit_count, hc.nbytes), "d2h")
+    abi.check(L.kgx_memcpy_d2h(cc.ctypes.data, out.call_count, cc.nbytes), "d2h")
+    total_hits = int(d.sum(float(hc.sum())))
+    mine = {"rank": d.rank, "device": dev, "ms_per_step": t_wall * 1e3 / args.steps,
+            "probe_ms": float(np.mean(probe_ms)), "n_seq": n, "hits": int(hc.sum())}
+    if canary_recs:
+        c = canary_recs[d.rank]
+        mine["canary"] = {"ok": c["ok"], "digest": c["digest"][:16], "hits": c["hits"], "calls": c["calls"]}
+    per_rank = d.gather_objects(mine)
+    log(f"[bench] rank {d.rank}: hits {int(hc.sum())} calls {int(cc.sum())} "
+        f"(even-q mean {hc[::2].mean():.1f}, odd-q mean {hc[1::2].mean():.2f}); "
+        f"wall {t_wall * 1e3 / args.steps:.3f} ms/step ({len(ctxs)} worker contexts, {len(batches)} batches), "
+        f"probe {np.mean(probe_ms):.3f} ms")
 
     # the timed configuration's results of batch 0, for the full-batch check
     # against the oracle below (rank 0)
@@ -979,8 +993,7 @@ def main():
         table = img.download()
         log(f"[bench] image copied to host in {time.time() - t0:.1f}s ({table.nbytes / 1e9:.1f} GB)")
         if got0 is not None:
-            parity, _ = parity_check(oracle, table, got0, res0, off0, want, threads,
-                                     args.line_index if line_lines else 0)
+            parity, _ = parity_check(oracle, table, got0, res0, off0, want, threads, timed_load)
             del got0
             log(f"[bench] parity vs oracle over {parity['sequences']} sequences (want {want}, line index "
                 f"{parity['line_index']}): {'equal' if parity['equal'] else 'MISMATCH ' + str(parity['by_output'])}")
@@ -1013,7 +1026,7 @@ def main():
                 tj = json.load(open(args.traffic_json))
                 if (tj.get("n_keys") == n_keys and tj.get("keys_stored") == stored and tj.get("n_seq") == n
                         and tj.get("length") == Ls and tj.get("image_layout", "AOS24") == layout
-                        and tj.get("line_index", 0) == (args.line_index if line_lines else 0)):
+                        and tj.get("line_index", 0) == timed_load):
                     traffic = tj.get("hbm_bytes_per_launch")
                     traffic_source = (f"not measured in this run: FETCH_SIZE + WRITE_SIZE per probe launch from "
                                       f"profiles/{os.path.basename(args.traffic_json)} "
@@ -1094,7 +1107,7 @@ def main():
                 # resident layout moves 16 B per bucket examined
                 "image_layout": layout,
                 # kgx_image_set_line_index load (0: probes over the reference slots)
-                "line_index": args.line_index if line_lines else 0,
+                "line_index": timed_load,
                 "line_index_lines": line_lines,
                 "alg_bytes_per_launch_resident_layout": windows_per_launch * (
                     (16.0 if layout == "PACKED16" else 24.0) * pbar + 1.0),
