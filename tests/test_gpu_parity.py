@@ -106,6 +106,41 @@ def test_random_batch_matches_oracle(small_world, oracle_lib, gpu, params, small
 
 
 @pytest.fixture(scope="module")
+def few_functions_world(gpu, oracle_lib):
+    """A table whose k-mers carry 6 functions, so best calls take every
+    branch (one function, ambiguous pair, no call)."""
+    spec = synth.ImageSpec(30000)
+    k, f, o, a, w = spec.unique_entries()
+    f = np.random.default_rng(3).integers(0, 6, len(k)).astype(np.int32)
+    table = oracle_lib.build_table(spec.num_sigs, k, f, o, a, w)
+    img = gpu.Image.from_table(table)
+    ctx = gpu.Context(img)
+    yield spec, table, img, ctx
+    ctx.close()
+    img.close()
+
+
+@pytest.mark.parametrize("n", [200, 257, 1000, 5000, 8192, 8193])
+def test_small_batch_best_calls_in_the_collect(few_functions_world, oracle_lib, gpu, n):
+    """Small batches of 257..8,192 sequences decide their best calls inside
+    the multi-block collect (small_collect_best_kernel: each block sums the
+    counts before its range itself) instead of best_call_kernel + the
+    one-workgroup collect; below and above that the old kernels.  Every
+    sequence's hits, calls, OTU tallies and best calls equal the oracle's at
+    want 15, and the offsets and best calls at want BEST and CALLS | BEST."""
+    spec, table, img, ctx = few_functions_world
+    res, off = synth.make_queries(spec, n, length=200, x_permille=5, q0=n)
+    assert int(off[-1]) <= 1 << 21  # the small-batch path
+    ref = oracle_lib.process_batch(table, res, off, want=15, n_threads=4)
+    for want in (15, gpu.WANT_BEST, gpu.WANT_CALLS | gpu.WANT_BEST):
+        got = ctx.process_batch(res, off, want=want)
+        assert oracle_lib.diff_batch(got, ref, want) == {k: [] for k in oracle_lib.diff_batch(got, ref, want)}, \
+            (n, want)
+        assert np.array_equal(got.hit_offsets, ref.hit_offsets), (n, want)
+    assert set(np.unique(ref.best["kind"])) >= {0, 1}
+
+
+@pytest.fixture(scope="module")
 def aos_world(small_world, gpu):
     """The same table kept in the file's 24-byte layout."""
     spec, table, _, _ = small_world
