@@ -117,7 +117,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
      * wait on stores (any s_waitcnt vmcnt) wait for PCIe, inflating the
      * phase it sat in (the OTU by-count sort: 4.0 us in the service against
      * 2.3 us for the same lists alone, tests/native/wave_sort_check.cpp) */
-    __shared__ uint64_t dstamp[16];
+    __shared__ uint64_t dstamp[18];
     if (dbg)
         dstamp[0] = wall_clock64();
     __shared__ uint8_t code_tab[256];
@@ -732,8 +732,10 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
             }
             __syncthreads();
         }
-        if (dbg)
+        if (dbg) {
             dstamp[8] = wall_clock64();
+            dstamp[16] = __builtin_amdgcn_s_memtime();
+        }
         /* std::sort by count (less_second, kguts.h:214-218): one wave replays
          * it, lstd_sort_wave64_reg up to 64 pairs (the pairs in registers),
          * lstd_sort_wave up to 64 SW
@@ -752,6 +754,8 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         } else if (d > 1 && t == 0) {
             lstd_sort_on(o, (int64_t)d, by_count, ostack);
         }
+        if (dbg)
+            dstamp[17] = __builtin_amdgcn_s_memtime();
         if (t == 0)
             n_otu = d;
         __syncthreads();
@@ -775,7 +779,7 @@ __device__ __forceinline__ void fused_small_body(const FusedArgs &a, const IN &k
         __threadfence_system();
         if (dbg) {
             dstamp[5] = wall_clock64();
-            for (int k = 0; k < 16; k++)
+            for (int k = 0; k < 18; k++)
                 a.dbg[k] = dstamp[k];
             __threadfence_system();
         }

@@ -284,12 +284,12 @@ struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the p
     uint32_t copy; /* = req, written before it: a line read with copy != req is incomplete */
 };
 struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
-    uint64_t stamp[16]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
+    uint64_t stamp[18]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
                            0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order, 9 the
                            scorer's first chunk done, 10 probe rounds (a count), 11 the
                            probe's first round examined, 12 keys and homes computed, 13
                            thread 0's first-round loads back, 14 / 15 the scorer's first
-                           chunk's runs and members / sums */
+                           chunk's runs and members / sums, 16 / 17 the shader clock (s_memtime) at the OTU sort's start / end */
 };
 struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t nh, nc, no; /* hit / call records and OTU pairs stored */

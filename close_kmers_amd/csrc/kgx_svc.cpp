@@ -100,7 +100,7 @@ struct SvcState {
      * phases (stamps 0->1 residues, 1->2 probe, 2->3 compaction, 3->4 stores
      * + scorer, and [5] 3->6 the record stores alone) */
     bool debug = false;
-    std::atomic<uint64_t> phase_ns[15] = {};
+    std::atomic<uint64_t> phase_ns[16] = {};
     /* KGX_SVC_SLEEP_US: a caller sleeps this long before it spins for its
      * answer (the device needs >= ~10 us per call), so a pool of spinning
      * callers holds fewer CPUs; 0 = spin only */
@@ -589,7 +589,7 @@ int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value)
         *value = s && s->reqmem ? 1 : 0;
     else if ((n.size() == 8 || n.size() == 9) && n.compare(0, 7, "phase_n") == 0 &&
              std::isdigit((unsigned char)n[7]) && (n.size() == 8 || std::isdigit((unsigned char)n[8])) &&
-             std::stoul(n.substr(7)) < 15) /* "phase_n0".."phase_n14" */
+             std::stoul(n.substr(7)) < 16) /* "phase_n0".."phase_n15" */
         *value = s ? s->phase_ns[std::stoul(n.substr(7))].load() : 0;
     else
         return fail(KGX_EINVAL, "unknown service statistic " + n);
@@ -722,6 +722,7 @@ int kgx_svc_call(kgx_image *img, const kgx_params *params, const char *seq, uint
         if (want & KGX_WANT_OTU) {
             s->phase_ns[6] += (st[4] - st[7]) * 10; /* the OTU tally alone */
             s->phase_ns[7] += (st[4] - st[8]) * 10; /* ... its sort by count */
+            s->phase_ns[15] += st[17] - st[16]; /* the sort's shader clock cycles */
         } else if (st[9] >= st[6] && st[9] <= st[4]) {
             s->phase_ns[6] += (st[9] - st[6]) * 10; /* the scorer's first 64-hit chunk */
             s->phase_ns[7] += (st[4] - st[9]) * 10; /* its other chunks and the final flush */

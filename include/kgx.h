@@ -532,12 +532,13 @@ int kgx_svc_stop(kgx_image *img);
  * the device's highest priority, so it has a hardware queue of its own and
  * batch streams never queue behind the persistent instances;
  * KGX_SVC_PRIORITY=normal gives it a normal stream),
- * "phase_n0".."phase_n14" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
+ * "phase_n0".."phase_n15" (with KGX_SVC_DEBUG=1: summed ns of the host wall per
  * call, the device phases, the OTU tally of calls that want it and the
  * tally's final sort by count; n8 the probe rounds x 1000, n9 the probe's
  * first round, n10 its keys and homes, n11 thread 0's first-round loads,
  * n12 / n13 the scorer's first chunk's runs / sums, n14 the final system
- * fence: what is left of the results' stores to host memory) */
+ * fence: what is left of the results' stores to host memory, n15 the OTU
+ * sort's shader clock cycles: n15 / n7 its clock) */
 int kgx_svc_stat(kgx_image *img, const char *name, uint64_t *value);
 
 /* Host-side profile of the context's last kgx_process_batch* call with option

@@ -63,7 +63,7 @@ __global__ __launch_bounds__(64) void wave_sort_kernel(const kgx_otu *in, const 
  * workgroup sorts while waves 1-3 wait at the barrier, with most of the LDS
  * allocated (`big`: 96 KiB more) */
 __global__ __launch_bounds__(256) void wave_sort_wg_kernel(const kgx_otu *in, const uint32_t *n_of, uint32_t cases,
-                                                           kgx_otu *out, uint64_t *ns, int big)
+                                                           kgx_otu *out, uint64_t *ns, int big, uint64_t *clk)
 {
     extern __shared__ uint8_t dyn[];
     __shared__ kgx_otu a[256], bl[256], br[256];
@@ -76,11 +76,13 @@ __global__ __launch_bounds__(256) void wave_sort_wg_kernel(const kgx_otu *in, co
             a[i] = in[256 * c + i];
         __syncthreads();
         if (t < 64) {
-            const uint64_t t0 = wall_clock64();
+            const uint64_t t0 = wall_clock64(), k0 = __builtin_amdgcn_s_memtime();
             lstd_sort_wave64_reg(a, n, ByCount{}, bl, br);
-            const uint64_t t1 = wall_clock64();
-            if (t == 0)
+            const uint64_t t1 = wall_clock64(), k1 = __builtin_amdgcn_s_memtime();
+            if (t == 0) {
                 ns[c] = (t1 - t0) * 10;
+                clk[c] = k1 - k0;
+            }
         }
         __syncthreads();
         for (uint32_t i = t; i < n; i += 256)
@@ -216,15 +218,23 @@ int main(int argc, char **argv)
         }
         std::printf("{\"svc36_ns\": %.0f, \"svc36_sorts\": %u}\n", t / K, K);
         for (int big = 0; big < 2; big++) {
+            uint64_t *d_clk = nullptr;
+            CHECK(hipMalloc(&d_clk, K * sizeof(uint64_t)));
             hipLaunchKernelGGL(wave_sort_wg_kernel, dim3(1), dim3(256), big ? 96 * 1024 : 0, 0, d_in, d_n, K, d_out,
-                               d_ns, big);
+                               d_ns, big, d_clk);
             CHECK(hipGetLastError());
             CHECK(hipDeviceSynchronize());
+            std::vector<uint64_t> clk(K);
             CHECK(hipMemcpy(ns.data(), d_ns, K * sizeof(uint64_t), hipMemcpyDeviceToHost));
-            double tw = 0;
-            for (uint32_t c = 0; c < K; c++)
+            CHECK(hipMemcpy(clk.data(), d_clk, K * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            (void)hipFree(d_clk);
+            double tw = 0, cw = 0;
+            for (uint32_t c = 0; c < K; c++) {
                 tw += (double)ns[c];
-            std::printf("{\"svc36_wg256_%s_ns\": %.0f}\n", big ? "lds96k" : "lds", tw / K);
+                cw += (double)clk[c];
+            }
+            std::printf("{\"svc36_wg256_%s_ns\": %.0f, \"clock_mhz\": %.0f}\n", big ? "lds96k" : "lds", tw / K,
+                        cw / tw * 1e3);
         }
     }
     (void)hipFree(d_in);

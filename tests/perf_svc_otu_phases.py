@@ -34,18 +34,19 @@ def main():
                 for s in seqs[:50]:  # warm up
                     img.svc_call(s, None, want=3, otus=otus)
                 c0 = img.svc_stat("calls")
-                p0 = [img.svc_stat(f"phase_n{i}") for i in range(15)]
+                p0 = [img.svc_stat(f"phase_n{i}") for i in range(16)]
                 n_otu = 0
                 for s in seqs:
                     r = img.svc_call(s, None, want=3, otus=otus)
                     n_otu += len(r[2]) if otus else 0
                 n = img.svc_stat("calls") - c0
-                ph = [(img.svc_stat(f"phase_n{i}") - p0[i]) / n / 1e3 for i in range(15)]
+                ph = [(img.svc_stat(f"phase_n{i}") - p0[i]) / n / 1e3 for i in range(16)]
                 out[f"mod{mod}_otu{int(otus)}"] = {"calls": n, "wall_us": round(ph[0], 2),
                                                    "store_score_tally_us": round(ph[4], 2),
                                                    "tally_us": round(ph[6], 2),
                                                    "count_sort_us": round(ph[7], 2),
                                                    "fence_us": round(ph[14], 2),
+                                                   "sort_clock_mhz": round(ph[15] * 1e3 / max(ph[7], 1e-9), 0),
                                                    "otus_per_call": round(n_otu / n, 2)}
     print(json.dumps(out))
 
