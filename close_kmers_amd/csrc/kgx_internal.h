@@ -284,7 +284,7 @@ struct SvcSlotHdr { /* host-written, one 64-B line per slot, read whole by the p
     uint32_t copy; /* = req, written before it: a line read with copy != req is incomplete */
 };
 struct SvcSlotDbg { /* device wall clock (100 MHz) at the phases of the last request */
-    uint64_t stamp[18]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
+    uint64_t stamp[32]; /* 0 seen, 1 residues, 2 probed, 3 compacted, 4 stored + scored, 5 fenced, 6 thread
                            0's record stores issued, 7 OTU tally entered, 8 OTU pairs in key order, 9 the
                            scorer's first chunk done, 10 probe rounds (a count), 11 the
                            probe's first round examined, 12 keys and homes computed, 13
@@ -297,7 +297,7 @@ struct SvcSlotOut { /* device-written, one 64-B line per slot */
     uint32_t left;       /* workgroups of this slot that have left (one per instance launched) */
     uint32_t pad[11];
 };
-static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 128,
+static_assert(sizeof(SvcSlotHdr) == 64 && sizeof(SvcSlotOut) == 64 && sizeof(SvcSlotDbg) == 256,
               "service slot lines");
 /* slots workgroups on stream; each leaves life_ticks after its start (device
  * wall clock, 100 MHz) or on stop */
