@@ -217,7 +217,7 @@ int main(int argc, char **argv)
         std::vector<uint32_t> n36(K, 36);
         for (uint32_t c = 0; c < K; c++) {
             int cnt[36] = {0};
-            for (int h = 0; h < 150; h++)
+            for (int h = 0; h < (c & 1 ? 292 : 150); h++)
                 cnt[rng() % 36]++;
             for (uint32_t i = 0; i < 36; i++)
                 in36[256 * (size_t)c + i] = kgx_otu{(int32_t)i * 97 + 3, cnt[i]};
@@ -270,9 +270,10 @@ int main(int argc, char **argv)
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(ns.data(), d_ns, K * sizeof(uint64_t), hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(got36.data(), d_out, got36.size() * sizeof(kgx_otu), hipMemcpyDeviceToHost));
-        double tl = 0;
+        double tl = 0, to = 0;
         for (uint32_t c = 0; c < K; c++) {
             tl += (double)ns[c];
+            to += (c & 1) ? (double)ns[c] : 0.0;
             for (uint32_t i = 0; i < 36; i++)
                 if (got36[256 * (size_t)c + i].otu_index != want36[256 * (size_t)c + i].otu_index ||
                     got36[256 * (size_t)c + i].count != want36[256 * (size_t)c + i].count) {
@@ -280,7 +281,8 @@ int main(int argc, char **argv)
                     return 1;
                 }
         }
-        std::printf("{\"svc36_svc_layout_ns\": %.0f}\n", tl / K);
+        std::printf("{\"svc36_svc_layout_ns\": %.0f, \"hits292_ns\": %.0f, \"hits150_ns\": %.0f}\n", tl / K,
+                    to / (K / 2), (tl - to) / (K - K / 2));
     }
     (void)hipFree(d_in);
     (void)hipFree(d_out);
